@@ -1,0 +1,157 @@
+/* tmdnet.h -- C ABI of the MI355X-native TorchMD-NET hot path (libtmdnet_hip.so, gfx950).
+ *
+ * Plain pointers, sizes and an opaque hipStream_t (passed as void*); no torch types, no C++
+ * exceptions across the boundary.  Every entry point returns 0 (TMDNET_OK) or a status code and
+ * only ENQUEUES work on `stream` (no host synchronisation, no allocation: callers pass workspaces),
+ * so every call is HIP-graph capturable.
+ *
+ * Device buffers are row-major and contiguous unless a leading dimension (ld*) is given.
+ * `dtype` selects the floating type of every floating buffer of the call (TMDNET_F32/F64).
+ * Edge lists are destination-grouped CSR:  row t = edges e in [row_ptr[t], row_ptr[t+1]) whose
+ * destination (reference edge_index[1]) is t; src[e] (reference edge_index[0]) is its source.
+ * Indices at or beyond `max_pairs` are ignored (capacity overflow, reference common.cuh:106-116).
+ */
+#ifndef TMDNET_H
+#define TMDNET_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { TMDNET_OK = 0, TMDNET_BAD_ARGUMENT = 1, TMDNET_UNSUPPORTED = 2, TMDNET_LAUNCH_FAILED = 3,
+       TMDNET_WORKSPACE_TOO_SMALL = 4 };
+enum { TMDNET_F32 = 0, TMDNET_F64 = 1 };
+enum { TMDNET_NL_BRUTE = 0, TMDNET_NL_SHARED = 1, TMDNET_NL_CELL = 2 };
+enum { TMDNET_RBF_EXPNORM = 0, TMDNET_RBF_GAUSS = 1 };
+
+/* ------------------------------------------------------------------------------------------
+ * Neighbour list.  Replaces torchmdnet_neighbors::get_neighbor_pairs
+ *   (reference torchmdnet/neighbors/neighbors.cpp:3-5; CUDA forward_brute/_shared/_cell,
+ *    neighbors_cuda_brute.cuh:269-309, neighbors_cuda_shared.cuh:71-106,
+ *    neighbors_cuda_cell.cuh:338-378; output contract common.cuh:64-116).
+ * Outputs (reference layout): neighbors int32 [2][max_pairs] (row 0 = source, row 1 = destination),
+ * deltas [max_pairs][3] (= pos[src]-pos[dst], minimum image), distances [max_pairs],
+ * num_pairs int32[1] = number of pairs FOUND (may exceed max_pairs; extra pairs are dropped).
+ * pad_output=1 fills unused slots with -1 / 0 exactly like the reference; 0 leaves them untouched.
+ * row_ptr (int32[n_atoms+1], nullable) receives the CSR offsets (not clamped to max_pairs).
+ * transpose_map (int32[max_pairs], nullable) receives T[e] = index of the reversed edge (or -1);
+ * only meaningful when include_transpose=1.
+ * box9: row-major 3x3 box vectors on the HOST (reduced triclinic form), may be NULL if not periodic.
+ * The cell strategy needs a diagonal box (the caller supplies 3*cutoff when not periodic, as
+ * reference utils.py:199-202 does).
+ */
+size_t tmdnet_nl_workspace_bytes(int n_atoms, int strategy, const double* box9, double cutoff_upper);
+int tmdnet_nl_build(int dtype, int strategy, const void* pos, const int64_t* batch, int n_atoms,
+                    const double* box9, int use_periodic, double cutoff_lower, double cutoff_upper,
+                    int max_pairs, int loop, int include_transpose, int32_t* neighbors, void* deltas,
+                    void* distances, int32_t* num_pairs, int32_t* row_ptr, int32_t* transpose_map,
+                    int pad_output, void* workspace, size_t workspace_bytes, void* stream);
+
+/* Backward of the neighbour op w.r.t. positions (reference NeighborAutograd::backward,
+ * neighbors_cuda.cu:43-71) as a segmented CSR reduction (no atomics, deterministic):
+ *   g[e] = r[e]==0 ? 0 : gdelta[e] + delta[e]/r[e]*gr[e];  dpos[n] = sum_{e in row n} g[T[e]] - g[e].
+ * Requires a symmetric list (include_transpose=1) and its transpose_map.  grad_deltas or
+ * grad_distances may be NULL (treated as zero).  grad_pos [n_atoms][3] is overwritten. */
+int tmdnet_nl_backward(int dtype, int n_atoms, const int32_t* row_ptr, const int32_t* transpose_map,
+                       int max_pairs, const void* grad_deltas, const void* grad_distances,
+                       const void* deltas, const void* distances, void* grad_pos, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Edge geometry: radial basis + cosine cutoff + unit vectors, fused.  Replaces
+ *   ExpNormalSmearing.forward / GaussianSmearing.forward (reference models/utils.py:339-344,
+ *   298-300), CosineCutoff.forward (utils.py:368-390), and the d_ij normalisation of
+ *   TorchMD_ET.forward (torchmd_et.py:173-174) / TensorNet.forward (tensornet.py:223-226).
+ * rbf_type EXPNORM: f[e][k] = C0(r) exp(-beta_k (exp(alpha (cl - r)) - mu_k)^2), C0 = cosine
+ *   cutoff (0, cu), alpha = 5/(cu-cl);  GAUSS: f[e][k] = exp(coeff * (r - mu_k)^2) (coeff = beta_0).
+ * C[e] = CosineCutoff(cl, cu)(r);  unit[e] = self edge (src==dst) ? delta : delta / |delta|.
+ * Any output pointer may be NULL (not computed). */
+int tmdnet_edge_geom_fwd(int dtype, int n_edges, int num_rbf, int rbf_type, const int32_t* src,
+                         const int32_t* dst, const void* deltas, const void* dist, const void* mu,
+                         const void* beta, double cutoff_lower, double cutoff_upper, void* rbf,
+                         void* cutoff, void* unit, void* stream);
+/* Backward: given grad_rbf [E][R], grad_cutoff [E], grad_unit [E][3] (each nullable) produce
+ * grad_dist [E] and grad_deltas [E][3] (both overwritten). */
+int tmdnet_edge_geom_bwd(int dtype, int n_edges, int num_rbf, int rbf_type, const int32_t* src,
+                         const int32_t* dst, const void* deltas, const void* dist, const void* mu,
+                         const void* beta, double cutoff_lower, double cutoff_upper,
+                         const void* grad_rbf, const void* grad_cutoff, const void* grad_unit,
+                         void* grad_dist, void* grad_deltas, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Equivariant-Transformer edge message + aggregation (reference
+ *   EquivariantMultiHeadAttention.message/aggregate, models/torchmd_et.py:314-347, with the SiLU of
+ *   the dk/dv projections, torchmd_et.py:282-291, folded in).  For every edge e (s=src, t=dst),
+ *   head h, channel c of the head (d = H/heads):
+ *     a[e,h]   = silu( sum_c q[t,h,c] k[s,h,c] silu(pk[e,h,c]) ) * C[e]
+ *     x[t,h,c]       += v[s,h,c] silu(pv[e,h,c]) a[e,h]
+ *     vec[t,a,h,c]   += vec_in[s,a,h,c] v[s,h,d+c] silu(pv[e,h,d+c]) + v[s,h,2d+c] silu(pv[e,h,2d+c]) unit[e,a]
+ *   q,k: [N][H] (ld_q, ld_k); v: [N][3H] head-interleaved [x|v1|v2] (ld_v); vec_in, vec: [N][3][H];
+ *   pk: [E][H] (ld_pk), pv: [E][3H] (ld_pv): PRE-activation dk/dv projections (NULL = factor 1, i.e.
+ *   distance_influence without keys / values).  x: [N][H].  `order` (nullable) permutes the
+ *   destinations processed (locality only; results identical).
+ * One wave64 per destination; outputs written once; no atomics; deterministic.
+ */
+int tmdnet_et_message_fwd(int dtype, int n_nodes, int hidden, int heads, const int32_t* row_ptr,
+                          const int32_t* src, int max_pairs, const void* q, int ld_q, const void* k,
+                          int ld_k, const void* v, int ld_v, const void* vec_in, const void* pk,
+                          int ld_pk, const void* pv, int ld_pv, const void* cutoff, const void* unit,
+                          void* x_out, void* vec_out, const int32_t* order, void* stream);
+/* Backward (two CSR passes, no atomics): destination pass -> gq, gpk, gpv, gcut, gunit; source
+ * pass (requires a symmetric edge list, dk/dv/cutoff functions of |r| only) -> gk, gv, gvec_in.
+ * grad buffers are overwritten; gpk/gpv are gradients of the PRE-activation projections. */
+int tmdnet_et_message_bwd(int dtype, int n_nodes, int hidden, int heads, const int32_t* row_ptr,
+                          const int32_t* src, int max_pairs, const void* q, int ld_q, const void* k,
+                          int ld_k, const void* v, int ld_v, const void* vec_in, const void* pk,
+                          int ld_pk, const void* pv, int ld_pv, const void* cutoff, const void* unit,
+                          const void* grad_x, const void* grad_vec, void* gq, void* gk, void* gv,
+                          void* gvec_in, void* gpk, void* gpv, void* gcut, void* gunit,
+                          const int32_t* order, void* stream);
+
+/* Neighbour embedding aggregation (reference NeighborEmbedding.forward/message,
+ *   models/utils.py:73-108):  out[t] = sum_{e in row t, src!=dst} X[src[e]] * W[e] * C[e]
+ *   X: [N][H] (ld_x), W: [E][H] (ld_w) = distance_proj(rbf) pre-cutoff, C: [E], out [N][H]. */
+int tmdnet_nbr_embed_fwd(int dtype, int n_nodes, int hidden, const int32_t* row_ptr,
+                         const int32_t* src, int max_pairs, const void* x, int ld_x, const void* w,
+                         int ld_w, const void* cutoff, void* out, void* stream);
+/* Backward: gx[s] (source pass, symmetric list), gw[e], gcut[e] (destination pass); overwritten. */
+int tmdnet_nbr_embed_bwd(int dtype, int n_nodes, int hidden, const int32_t* row_ptr,
+                         const int32_t* src, int max_pairs, const void* x, int ld_x, const void* w,
+                         int ld_w, const void* cutoff, const void* grad_out, void* gx, void* gw,
+                         void* gcut, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * TensorNet edge kernels (reference models/tensornet.py:287-332).  Tensors are [N][H][3][3].
+ * self0_mult >= 1: multiplicity of atom 0's self loop (static_shapes padding emulation,
+ * tensornet.py:215-221; 1 = no padding).  Both require the symmetric CSR list.
+ * Embedding:  I/A/S[n] = sum_{edges e with reference edge_index[0]==n} (P[n] + Q[dst]) * W_k[e] * C[e]
+ *             * {Id, skew(u[e]), sym(u[e])},  W = [E][3H] = distance_proj1|2|3(rbf) (pre-cutoff),
+ *             P = emb(z) Wa^T + b, Q = emb(z) Wb^T  (emb2 split into its two input halves). */
+int tmdnet_tn_embed_fwd(int dtype, int n_nodes, int hidden, const int32_t* row_ptr,
+                        const int32_t* src, int max_pairs, double self0_mult, const void* P,
+                        const void* Q, const void* W, int ld_w, const void* cutoff, const void* unit,
+                        void* I, void* A, void* S, void* stream);
+int tmdnet_tn_embed_bwd(int dtype, int n_nodes, int hidden, const int32_t* row_ptr,
+                        const int32_t* src, int max_pairs, double self0_mult, const void* P,
+                        const void* Q, const void* W, int ld_w, const void* cutoff, const void* unit,
+                        const void* gI, const void* gA, const void* gS, void* gP, void* gQ, void* gW,
+                        void* gcut, void* gunit, void* stream);
+/* Message: msg[n] = sum_{edges e with edge_index[0]==n} ea[e,h,0] I[m] + ea[e,h,1] A[m] + ea[e,h,2] S[m],
+ * m = edge_index[1][e]; edge_attr [E][3H] interleaved (h, component) as reshape(E, H, 3). */
+int tmdnet_tn_message_fwd(int dtype, int n_nodes, int hidden, const int32_t* row_ptr,
+                          const int32_t* src, int max_pairs, double self0_mult, const void* edge_attr,
+                          int ld_ea, const void* I, const void* A, const void* S, void* msg,
+                          void* stream);
+int tmdnet_tn_message_bwd(int dtype, int n_nodes, int hidden, const int32_t* row_ptr,
+                          const int32_t* src, int max_pairs, double self0_mult, const void* edge_attr,
+                          int ld_ea, const void* I, const void* A, const void* S, const void* grad_msg,
+                          void* g_edge_attr, void* gI, void* gA, void* gS, void* stream);
+
+/* Library identification (for load checks). */
+const char* tmdnet_build_info(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TMDNET_H */

@@ -1,0 +1,376 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the oracle and the reference's fixtures.
+
+Tolerances: neighbour indices exact as sets; float64 outputs 1e-9 relative; float32 energies /
+forces 1e-4 relative (north_star); pairs within 1e-6 of the cutoff are excluded from exact
+neighbour-set comparisons (CPU reference compares |d| < cu, GPU reference d^2 < cu^2).
+"""
+import os
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN, golden, state_dict_from, yaml_args
+from oracle import model_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _seed(s=1234):
+    random.seed(s)
+    np.random.seed(s)
+    torch.manual_seed(s)
+
+
+def _rel(a, b):
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    return np.abs(a - b).max() / max(np.abs(b).max(), 1e-12)
+
+
+def _lib_loaded():
+    from torchmdnet import _native
+    lib = _native.load()
+    maps = open("/proc/self/maps").read()
+    assert "libtmdnet_hip.so" in maps
+    return lib
+
+
+# ----------------------------------------------------------------------------- neighbour op
+def _sets_equal_excluding_boundary(nb, dist, ref_nb, ref_dist, cutoff, eps=1e-6):
+    def keep(nbx, dx):
+        m = np.abs(dx - cutoff) > eps * max(cutoff, 1.0)
+        return nbx[:, m]
+    a = keep(nb, dist)
+    b = keep(ref_nb, ref_dist)
+    a = a[:, np.lexsort(a)]
+    b = b[:, np.lexsort(b)]
+    return a.shape == b.shape and np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("strategy", ["brute", "shared", "cell"])
+def test_neighbor_op_matches_reference_fixtures(strategy):
+    from torchmdnet.neighbors import get_neighbor_pairs_kernel
+    _lib_loaded()
+    d = golden("neighbors_ref.npz")
+    n_checked = 0
+    for k in range(int(d["ncases"][0])):
+        cutoff, loop, tr, periodic = d[f"c{k}/params"]
+        box = d[f"c{k}/box"]
+        if strategy == "cell" and periodic and np.count_nonzero(box - np.diag(np.diag(box))):
+            continue  # triclinic not supported by the cell list (reference _cell.cuh:349-352)
+        pos = torch.tensor(d[f"c{k}/pos"], device=DEV)
+        batch = torch.tensor(d[f"c{k}/batch"], device=DEV)
+        ref_nb = d[f"c{k}/neighbors"].astype(np.int64)
+        cap = ref_nb.shape[1] + 64
+        if periodic:
+            boxt = torch.tensor(box, dtype=pos.dtype)
+        elif strategy == "cell":
+            boxt = torch.tensor(np.eye(3) * 3 * cutoff, dtype=pos.dtype)
+            if 3 * cutoff < 2 * cutoff:
+                continue
+        else:
+            boxt = torch.empty((0, 0), dtype=pos.dtype)
+        if strategy == "cell" and not periodic:
+            # the reference cell list without a box wraps positions into a 3*cutoff box
+            # (utils.py:199-202), which only matches the plain list when every molecule fits it
+            continue
+        nb, dl, dist, num = get_neighbor_pairs_kernel(strategy, pos, batch, boxt, bool(periodic), 0.0, float(cutoff),
+                                                      cap, bool(loop), bool(tr))
+        P = int(num[0].item())
+        assert P == ref_nb.shape[1] or abs(P - ref_nb.shape[1]) <= 2, (k, P, ref_nb.shape)
+        nbh = nb[:, :P].cpu().numpy().astype(np.int64)
+        assert (nb[:, P:] == -1).all() and (dist[P:] == 0).all() and (dl[P:] == 0).all()
+        dh = dist[:P].cpu().numpy()
+        assert _sets_equal_excluding_boundary(nbh, dh, ref_nb, d[f"c{k}/distances"], cutoff), k
+        # deltas / distances of matched pairs
+        nbs, dls, ds = O.sort_pairs(nbh, dl[:P].cpu().numpy(), dh)
+        rnb, rdl, rds = ref_nb, d[f"c{k}/deltas"], d[f"c{k}/distances"]
+        if nbs.shape == rnb.shape and np.array_equal(nbs, rnb):
+            tol = 1e-5 if pos.dtype == torch.float32 else 1e-12
+            assert np.allclose(ds, rds, rtol=tol, atol=tol), k
+            assert np.allclose(dls, rdl, rtol=tol, atol=tol), k
+        n_checked += 1
+    assert n_checked > 0
+
+
+def test_neighbor_op_capacity_and_errors():
+    from torchmdnet.models.utils import OptimizedDistance
+    torch.manual_seed(0)
+    pos = torch.randn(50, 3, device=DEV) * 2
+    batch = torch.zeros(50, dtype=torch.long, device=DEV)
+    nl = OptimizedDistance(cutoff_upper=5.0, max_num_pairs=10, check_errors=True, loop=True)
+    with pytest.raises(RuntimeError, match="max_num_pairs"):
+        nl(pos, batch)
+    nl = OptimizedDistance(cutoff_upper=5.0, max_num_pairs=10, check_errors=False, resize_to_fit=False)
+    ei, ew, _ = nl(pos, batch)
+    assert ei.shape == (2, 10)
+    with pytest.raises(RuntimeError):
+        OptimizedDistance(strategy="nonsense")(pos, batch)
+    with pytest.raises(RuntimeError):
+        OptimizedDistance(box=torch.eye(3) * 1.0, cutoff_upper=5.0)(pos, batch)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+@pytest.mark.parametrize("box", [None, "rect", "tric"])
+def test_neighbor_grads_match_oracle(dtype, box):
+    from torchmdnet.models.utils import OptimizedDistance
+    torch.manual_seed(4321)
+    n = 120
+    lbox = 8.0
+    pos = (torch.rand(n, 3, dtype=dtype) * lbox).to(DEV).requires_grad_(True)
+    batch = torch.repeat_interleave(torch.arange(3), torch.tensor([30, 50, 40])).to(DEV)
+    boxt = None
+    if box == "rect":
+        boxt = torch.eye(3, dtype=dtype) * lbox
+    elif box == "tric":
+        boxt = torch.tensor([[lbox, 0, 0], [0.1, lbox, 0], [0.3, 0.2, lbox]], dtype=dtype)
+    nl = OptimizedDistance(cutoff_upper=3.0, max_num_pairs=-64, loop=True, return_vecs=True, box=boxt)
+    ei, ew, ev = nl(pos, batch)
+    w = torch.randn(ew.shape[0], dtype=dtype, device=DEV)
+    wv = torch.randn(ev.shape[0], 3, dtype=dtype, device=DEV)
+    (gp,) = torch.autograd.grad((ew * w).sum() + (ev * wv).sum(), pos)
+    # oracle: same pairs from the C list, differentiable deltas
+    p64 = pos.detach().cpu().double().requires_grad_(True)
+    nb = ei.cpu()
+    shift = (ev.detach().cpu().double() - (p64[nb[0]] - p64[nb[1]])).detach()
+    dl = p64[nb[0]] - p64[nb[1]] + shift
+    selfe = nb[0] == nb[1]
+    r = torch.where(selfe, torch.zeros(len(selfe), dtype=torch.float64),
+                    torch.where(selfe, torch.ones(len(selfe), dtype=torch.float64), (dl * dl).sum(1)).sqrt())
+    (gref,) = torch.autograd.grad((r * w.cpu().double()).sum() + (dl * wv.cpu().double()).sum(), p64)
+    tol = 1e-4 if dtype == torch.float32 else 1e-10
+    assert _rel(gp.cpu(), gref) < tol
+
+
+def test_csr_graph_invariants():
+    from torchmdnet import kernels
+    z, pos, batch = O.qm9_like(8)
+    pos = pos.float().to(DEV)
+    batch = batch.to(DEV)
+    g = kernels.build_graph(pos, batch, 0.0, 5.0, 64 * pos.shape[0], loop=True)
+    rp = g.row_ptr.cpu().numpy()
+    src, dst, T = g.src.cpu().numpy(), g.dst.cpu().numpy(), g.transpose.cpu().numpy()
+    E = len(src)
+    assert rp[-1] == E == g.num_pairs
+    for t in range(pos.shape[0]):
+        assert (dst[rp[t]:rp[t + 1]] == t).all()
+        assert np.all(np.diff(src[rp[t]:rp[t + 1]]) > 0)  # sorted, unique sources
+    assert (T >= 0).all()
+    assert np.array_equal(src[T], dst) and np.array_equal(dst[T], src)
+    dl = g.deltas.detach().cpu().numpy()
+    assert np.array_equal(dl[T], -dl)
+    ref_nb, _, _ = O.neighbors(pos.cpu().numpy(), batch.cpu().numpy(), 0.0, 5.0, loop=True, sq_compare=True)
+    mine = np.stack([src, dst]).astype(np.int64)
+    assert np.array_equal(mine[:, np.lexsort(mine)], ref_nb[:, np.lexsort(ref_nb)])
+
+
+def test_cell_list_matches_brute_water_box():
+    from torchmdnet import kernels
+    torch.manual_seed(0)
+    n = 3000
+    L = (n / 0.1003) ** (1 / 3)
+    pos = (torch.rand(n, 3, dtype=torch.float64) * L).to(DEV)
+    batch = torch.zeros(n, dtype=torch.long, device=DEV)
+    box = torch.eye(3, dtype=torch.float64) * L
+    a = kernels.build_graph(pos, batch, 0.0, 5.0, 128 * n, box=box, strategy="cell")
+    b = kernels.build_graph(pos, batch, 0.0, 5.0, 128 * n, box=box, strategy="brute")
+    ea = torch.stack([a.src, a.dst]).cpu().numpy().astype(np.int64)
+    eb = torch.stack([b.src, b.dst]).cpu().numpy().astype(np.int64)
+    assert ea.shape == eb.shape
+    assert np.array_equal(ea[:, np.lexsort(ea)], eb[:, np.lexsort(eb)])
+    assert (a.transpose >= 0).all()
+
+
+# ----------------------------------------------------------------------------- ET model
+def _et_cfg_args(H, L, R, heads, maxnb=32, precision=32):
+    return yaml_args("equivariant-transformer", embedding_dimension=H, num_layers=L, num_rbf=R, num_heads=heads,
+                     max_num_neighbors=maxnb, derivative=True, output_model="Scalar", precision=precision)
+
+
+def _model_from_fixture(args, d):
+    from torchmdnet.models.model import create_model
+    m = create_model(args)
+    sd = {k: torch.tensor(v) for k, v in state_dict_from(d).items()}
+    m.load_state_dict(sd)
+    return m.to(DEV)
+
+
+@pytest.mark.parametrize("tag,tol", [("f64", 1e-9), ("f32", 1e-4)])
+def test_et_tiny_matches_reference_fixture(tag, tol):
+    _lib_loaded()
+    d = golden(f"et_tiny_{tag}.npz")
+    args = _et_cfg_args(32, 2, 16, 4, precision=64 if tag == "f64" else 32)
+    m = _model_from_fixture(args, d)
+    pos = torch.tensor(d["pos"], device=DEV)
+    y, neg_dy = m(torch.tensor(d["z"], device=DEV), pos, torch.tensor(d["batch"], device=DEV))
+    assert _rel(y.detach().cpu(), d["y"]) < tol
+    assert _rel(neg_dy.detach().cpu(), d["neg_dy"]) < tol
+
+
+def test_et_double_backward_matches_reference_fixture():
+    d = golden("et_tiny_f64.npz")
+    args = _et_cfg_args(32, 2, 16, 4, precision=64)
+    m = _model_from_fixture(args, d)
+    pos = torch.tensor(d["pos"], device=DEV)
+    y, neg_dy = m(torch.tensor(d["z"], device=DEV), pos, torch.tensor(d["batch"], device=DEV))
+    loss = (y ** 2).sum() + (neg_dy ** 2).sum()
+    names = [n for n, p in m.named_parameters() if p.requires_grad]
+    grads = torch.autograd.grad(loss, [p for _, p in m.named_parameters() if p.requires_grad], allow_unused=True)
+    for n, g in zip(names, grads):
+        ref = d["g2/" + n]
+        got = np.zeros_like(ref) if g is None else g.detach().cpu().numpy()
+        assert np.allclose(got, ref, rtol=1e-7, atol=1e-9), n
+
+
+@pytest.mark.parametrize("tag,tol", [("f32", 1e-4), ("f64", 1e-9)])
+def test_et_c2_seeded_matches_reference_fixture(tag, tol):
+    from torchmdnet.models.model import create_model
+    d = golden(f"et_c2_{tag}.npz")
+    _seed()
+    args = yaml_args("equivariant-transformer", embedding_dimension=128, derivative=True, output_model="Scalar",
+                     precision=64 if tag == "f64" else 32)
+    m = create_model(args).to(DEV)
+    y, neg_dy = m(torch.tensor(d["z"], device=DEV), torch.tensor(d["pos"], device=DEV),
+                  torch.tensor(d["batch"], device=DEV))
+    assert _rel(y.detach().cpu(), d["y"]) < tol
+    assert _rel(neg_dy.detach().cpu(), d["neg_dy"]) < tol
+
+
+def test_expected_pkl_on_gpu():
+    import json
+    from torchmdnet.models.model import create_model
+    exp = json.load(open(os.path.join(GOLDEN, "expected_outputs.json")))
+    for model_name in ("equivariant-transformer", "tensornet"):
+        _seed()
+        m = create_model(yaml_args(model_name, output_model="Scalar", derivative=True))
+        zs = torch.tensor([1, 6, 7, 8, 9], dtype=torch.long)
+        z = zs[torch.randint(0, len(zs), (5,))]
+        pos = torch.randn(len(z), 3)
+        batch = torch.zeros(len(z), dtype=torch.long)
+        batch[len(batch) // 2:] = 1
+        if model_name == "tensornet":
+            # expected.pkl was produced by the CPU op (no padding); compare the unpadded semantics
+            m.representation_model.static_shapes = False
+        m = m.to(DEV)
+        y, neg_dy = m(z.to(DEV), pos.to(DEV), batch.to(DEV))
+        e = exp[model_name]["Scalar"]
+        assert np.allclose(y.detach().cpu().numpy().ravel(), e["pred"]["values"], rtol=1e-4, atol=1e-5), model_name
+        assert np.allclose(neg_dy.detach().cpu().numpy().ravel(), e["deriv"]["values"], rtol=1e-4, atol=1e-4)
+
+
+def test_et_c2_batch32_matches_oracle():
+    """The BASELINE workload (ET-QM9 128 ch, 8 layers, 32 QM9-like molecules) vs the fp64 oracle."""
+    from torchmdnet.models.model import create_model
+    _seed()
+    args = yaml_args("equivariant-transformer", embedding_dimension=128, derivative=True, output_model="Scalar")
+    m = create_model(args)
+    z, pos, batch = O.qm9_like(32)
+    y_ref, f_ref = O.energy_forces(m.state_dict(), dict(args), z, pos, batch)
+    m = m.to(DEV)
+    y, f = m(z.to(DEV), pos.float().to(DEV), batch.to(DEV))
+    assert _rel(y.detach().cpu(), y_ref.detach()) < 1e-4
+    assert _rel(f.detach().cpu(), f_ref) < 1e-4
+
+
+def test_et_rotation_equivariance():
+    from torchmdnet.models.model import create_model
+    torch.manual_seed(1234)
+    rot = torch.tensor([[0.9886788, -0.1102370, 0.1017945], [0.1363630, 0.9431761, -0.3030248],
+                        [-0.0626055, 0.3134752, 0.9475304]])
+    m = create_model(yaml_args("equivariant-transformer", derivative=True, output_model="Scalar")).to(DEV)
+    z = torch.ones(100, dtype=torch.long, device=DEV)
+    pos = torch.randn(100, 3, device=DEV)
+    batch = torch.arange(50, dtype=torch.long, device=DEV).repeat_interleave(2)
+    y, f = m(z, pos.clone(), batch)
+    y2, f2 = m(z, (pos @ rot.to(DEV)).contiguous(), batch)
+    assert torch.allclose(y, y2, atol=1e-5, rtol=1e-4)
+    assert torch.allclose(f @ rot.to(DEV), f2, atol=1e-4, rtol=1e-3)
+
+
+def test_et_edge_kernel_gradcheck():
+    from torchmdnet import kernels
+    torch.manual_seed(0)
+    z, pos, batch = O.qm9_like(2)
+    pos = pos.to(DEV)
+    g = kernels.build_graph(pos, batch.to(DEV), 0.0, 5.0, 64 * pos.shape[0], loop=True)
+    N, H, heads, E = pos.shape[0], 16, 2, g.n_edges
+    o = dict(dtype=torch.float64, device=DEV, requires_grad=True)
+    q, k = torch.randn(N, H, **o), torch.randn(N, H, **o)
+    v = torch.randn(N, 3 * H, **o)
+    vec = torch.randn(N, 3, H, **o)
+    pk = torch.randn(E, H, **o)
+    pv = torch.randn(E, 3 * H, **o)
+    # symmetric per-edge inputs (functions of |r|) as the source pass requires
+    T = g.transpose.long()
+    C = torch.rand(E, dtype=torch.float64, device=DEV)
+    C = ((C + C[T]) / 2).requires_grad_(True)
+    u = g.deltas.detach() / torch.where(g.distances.detach() > 0, g.distances.detach(),
+                                        torch.ones_like(g.distances.detach())).unsqueeze(1)
+    u = u.requires_grad_(True)
+    pk = ((pk + pk[T]) / 2).detach().requires_grad_(True)
+    pv = ((pv + pv[T]) / 2).detach().requires_grad_(True)
+    fn = lambda *a: kernels.et_message(*a, g, heads)
+    xo, vo = fn(q, k, v, vec, pk, pv, C, u)
+    xr, vr = kernels.et_message_composite(q, k, v, vec, pk, pv, C, u, g.src.long(), g.dst.long(), N, heads)
+    assert torch.allclose(xo, xr, atol=1e-11) and torch.allclose(vo, vr, atol=1e-11)
+    gx, gv = torch.randn_like(xo), torch.randn_like(vo)
+    ins = (q, k, v, vec, pk, pv, C, u)
+    a = torch.autograd.grad((xo, vo), ins, (gx, gv))
+    b = torch.autograd.grad((xr, vr), ins, (gx, gv))
+    # the kernel attributes per-edge gradients of symmetric inputs (pk, pv, C) to the row edge and
+    # antisymmetric u to its reverse; compare the symmetrised sums
+    for name, ga, gb in zip("q k v vec pk pv C u".split(), a, b):
+        if name in ("pk", "pv", "C"):
+            ga, gb = ga + ga[T], gb + gb[T]
+        if name == "u":
+            ga, gb = ga - ga[T], gb - gb[T]
+        assert torch.allclose(ga, gb, atol=1e-10, rtol=1e-9), name
+
+
+# ----------------------------------------------------------------------------- TensorNet
+@pytest.mark.parametrize("name", ["tn_tiny_o3_static_f64", "tn_tiny_so3_static_f64", "tn_tiny_o3_dyn_f64",
+                                  "tn_tiny_so3_dyn_f64", "tn_tiny_o3_static_f32"])
+def test_tensornet_tiny_matches_reference_fixture(name):
+    from torchmdnet.models.model import create_model
+    d = golden(name + ".npz")
+    group = "SO(3)" if "so3" in name else "O(3)"
+    f64 = name.endswith("f64")
+    args = yaml_args("tensornet", embedding_dimension=32, num_layers=2, num_rbf=16, max_num_neighbors=32,
+                     cutoff_upper=4.5, derivative=True, output_model="Scalar", precision=64 if f64 else 32,
+                     equivariance_invariance_group=group)
+    m = create_model(args)
+    m.load_state_dict({k: torch.tensor(v) for k, v in state_dict_from(d).items()})
+    m.representation_model.static_shapes = "static" in name
+    m = m.to(DEV)
+    y, neg_dy = m(torch.tensor(d["z"], device=DEV), torch.tensor(d["pos"], device=DEV),
+                  torch.tensor(d["batch"], device=DEV))
+    tol = 1e-9 if f64 else 1e-4
+    assert _rel(y.detach().cpu(), d["y"]) < tol
+    assert _rel(neg_dy.detach().cpu(), d["neg_dy"]) < tol
+    if f64:
+        loss = (y ** 2).sum() + (neg_dy ** 2).sum()
+        names = [n for n, p in m.named_parameters() if p.requires_grad]
+        grads = torch.autograd.grad(loss, [p for _, p in m.named_parameters() if p.requires_grad], allow_unused=True)
+        for n, g in zip(names, grads):
+            ref = d["g2/" + n]
+            got = np.zeros_like(ref) if g is None else g.detach().cpu().numpy()
+            assert np.allclose(got, ref, rtol=1e-6, atol=1e-8), n
+
+
+def test_tensornet_c3_padded_matches_fixture():
+    import yaml
+    from torchmdnet.models.model import create_model
+    d = golden("tn_c3_f32.npz")
+    args = yaml.safe_load(open(os.path.join(GOLDEN, "configs", "tensornet_rmd17.yaml")))
+    args["prior_model"] = None
+    args["precision"] = 32
+    _seed()
+    m = create_model(args).to(DEV)
+    y, neg_dy = m(torch.tensor(d["z"], device=DEV), torch.tensor(d["pos"], device=DEV),
+                  torch.tensor(d["batch"], device=DEV))
+    assert _rel(y.detach().cpu(), d["y"]) < 1e-4
+    assert _rel(neg_dy.detach().cpu(), d["neg_dy"]) < 1e-4

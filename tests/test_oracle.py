@@ -1,0 +1,160 @@
+"""CPU tests: the oracle (oracle/) pinned against the reference's own golden data.
+
+Fixtures: tests/golden/*.npz were produced by running the reference package
+(gen_reference_fixtures.py); expected_outputs.json is the reference's tests/expected.pkl
+(extract_expected_pkl.py, no unpickling).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN, golden, state_dict_from, yaml_args
+from oracle import model_oracle as O
+
+
+def _cases(npz):
+    return range(int(npz["ncases"][0]))
+
+
+def test_neighbor_oracle_matches_reference_op():
+    d = golden("neighbors_ref.npz")
+    checked = 0
+    for k in _cases(d):
+        pos, batch, box = d[f"c{k}/pos"], d[f"c{k}/batch"], d[f"c{k}/box"]
+        cutoff, loop, tr, periodic = d[f"c{k}/params"]
+        nb, dl, ds = O.neighbors(pos, batch, 0.0, cutoff, loop=bool(loop), include_transpose=bool(tr),
+                                 box=box if periodic else None)
+        nb, dl, ds = O.sort_pairs(nb, dl, ds)
+        ref_nb = d[f"c{k}/neighbors"]
+        assert nb.shape == ref_nb.shape, k
+        assert np.array_equal(nb, ref_nb), k
+        tol = 1e-5 if pos.dtype == np.float32 else 1e-12
+        assert np.allclose(ds, d[f"c{k}/distances"], rtol=tol, atol=tol), k
+        assert np.allclose(dl, d[f"c{k}/deltas"], rtol=tol, atol=tol), k
+        assert int(d[f"c{k}/num_pairs"][0]) == nb.shape[1]
+        checked += 1
+    assert checked >= 60
+
+
+def _et_cfg(H, L, R, heads, maxnb=32):
+    return dict(model="equivariant-transformer", embedding_dimension=H, num_layers=L, num_rbf=R,
+                num_heads=heads, cutoff_lower=0.0, cutoff_upper=5.0, max_num_neighbors=maxnb,
+                neighbor_embedding=True, distance_influence="both", rbf_type="expnorm")
+
+
+@pytest.mark.parametrize("tag,tol", [("f64", 1e-10), ("f32", 2e-5)])
+def test_et_oracle_matches_reference_tiny(tag, tol):
+    d = golden(f"et_tiny_{tag}.npz")
+    sd = state_dict_from(d)
+    hooks = {}
+    y, neg_dy = O.energy_forces(sd, _et_cfg(32, 2, 16, 4), d["z"], d["pos"], d["batch"], hooks=hooks)
+    assert np.allclose(y.detach().numpy(), d["y"], rtol=tol, atol=tol)
+    assert np.allclose(neg_dy.numpy(), d["neg_dy"], rtol=tol, atol=tol * 10)
+    for li in range(2):
+        assert np.allclose(hooks[f"layer{li}/dx"].detach().numpy(), d[f"layer{li}/dx"], rtol=tol, atol=tol * 10)
+        assert np.allclose(hooks[f"layer{li}/dvec"].detach().numpy(), d[f"layer{li}/dvec"], rtol=tol, atol=tol * 10)
+
+
+def test_et_oracle_double_backward_matches_reference():
+    d = golden("et_tiny_f64.npz")
+    sd = {k: torch.tensor(v, requires_grad=v.dtype.kind == "f") for k, v in state_dict_from(d).items()}
+    y, neg_dy = O.energy_forces(sd, _et_cfg(32, 2, 16, 4), d["z"], d["pos"], d["batch"], create_graph=True)
+    loss = (y ** 2).sum() + (neg_dy ** 2).sum()
+    names = [k for k in d.files if k.startswith("g2/")]
+    params = [sd[k[3:]] for k in names]
+    grads = torch.autograd.grad(loss, params, allow_unused=True)
+    for k, g in zip(names, grads):
+        ref = d[k]
+        if g is None:
+            assert np.allclose(ref, 0)
+            continue
+        assert np.allclose(g.detach().numpy(), ref, rtol=1e-8, atol=1e-10), k
+
+
+@pytest.mark.parametrize("name", ["tn_tiny_o3_static_f64", "tn_tiny_so3_static_f64", "tn_tiny_o3_dyn_f64",
+                                  "tn_tiny_so3_dyn_f64", "tn_tiny_o3_static_f32"])
+def test_tensornet_oracle_matches_reference_tiny(name):
+    d = golden(name + ".npz")
+    sd = state_dict_from(d)
+    group = "SO(3)" if "so3" in name else "O(3)"
+    cfg = dict(model="tensornet", embedding_dimension=32, num_layers=2, num_rbf=16, cutoff_lower=0.0,
+               cutoff_upper=4.5, max_num_neighbors=32, equivariance_invariance_group=group)
+    tol = 1e-10 if name.endswith("f64") else 2e-5
+    y, neg_dy = O.energy_forces(sd, cfg, d["z"], d["pos"], d["batch"], static_shapes="static" in name)
+    assert np.allclose(y.detach().numpy(), d["y"], rtol=tol, atol=tol)
+    assert np.allclose(neg_dy.numpy(), d["neg_dy"], rtol=tol, atol=tol * 10)
+
+
+def test_expected_pkl_reproduced_by_oracle_and_seeded_create_model():
+    """Reference tests/test_model.py:143-189 (ET and TensorNet, Scalar head): our create_model seeded
+    with 1234 must reproduce the reference weights, and the oracle the reference outputs."""
+    import random
+    from torchmdnet.models.model import create_model
+    exp = json.load(open(os.path.join(GOLDEN, "expected_outputs.json")))
+    for model_name in ("equivariant-transformer", "tensornet"):
+        random.seed(1234)
+        np.random.seed(1234)
+        torch.manual_seed(1234)
+        args = yaml_args(model_name, output_model="Scalar", derivative=True)
+        model = create_model(args)
+        zs = torch.tensor([1, 6, 7, 8, 9], dtype=torch.long)
+        z = zs[torch.randint(0, len(zs), (5,))]
+        pos = torch.randn(len(z), 3)
+        batch = torch.zeros(len(z), dtype=torch.long)
+        batch[len(batch) // 2:] = 1
+        cfg = dict(args)
+        y, neg_dy = O.energy_forces(model.state_dict(), cfg, z, pos, batch, dtype=torch.float64,
+                                    static_shapes=False)
+        e = exp[model_name]["Scalar"]
+        assert np.allclose(y.detach().numpy().ravel(), e["pred"]["values"], rtol=1e-5, atol=1e-6), model_name
+        assert np.allclose(neg_dy.numpy().ravel(), e["deriv"]["values"], rtol=1e-4, atol=1e-5), model_name
+
+
+@pytest.mark.parametrize("fixture,model,cfg_kw", [
+    ("et_c2_f32.npz", "equivariant-transformer", dict(embedding_dimension=128)),
+    ("et_c2_f64.npz", "equivariant-transformer", dict(embedding_dimension=128, precision=64)),
+])
+def test_c2_weights_and_outputs(fixture, model, cfg_kw):
+    import random
+    from torchmdnet.models.model import create_model
+    d = golden(fixture)
+    random.seed(1234)
+    np.random.seed(1234)
+    torch.manual_seed(1234)
+    args = yaml_args(model, output_model="Scalar", derivative=True, **cfg_kw)
+    m = create_model(args)
+    sd = m.state_dict()
+    for k, v in sd.items():
+        ck = d["ck/" + k]
+        a = v.double()
+        assert abs(a.sum().item() - ck[0]) <= 1e-9 * max(1.0, abs(ck[0])), k
+        assert abs((a * a).sum().item() - ck[1]) <= 1e-9 * max(1.0, ck[1]), k
+    y, neg_dy = O.energy_forces(sd, dict(args), d["z"], d["pos"], d["batch"])
+    tol = 1e-5 if fixture.endswith("f32.npz") else 1e-10
+    assert np.allclose(y.detach().numpy(), d["y"], rtol=tol * 10, atol=tol)
+    assert np.allclose(neg_dy.numpy(), d["neg_dy"], rtol=tol * 10, atol=tol * 10)
+
+
+def test_tensornet_c3_padded_fixture():
+    import random
+    import yaml
+    from torchmdnet.models.model import create_model
+    d = golden("tn_c3_f32.npz")
+    args = yaml.safe_load(open(os.path.join(GOLDEN, "configs", "tensornet_rmd17.yaml")))
+    args["prior_model"] = None
+    args["precision"] = 32
+    random.seed(1234)
+    np.random.seed(1234)
+    torch.manual_seed(1234)
+    m = create_model(args)
+    sd = m.state_dict()
+    for k, v in sd.items():
+        ck = d["ck/" + k]
+        a = v.double()
+        assert abs(a.sum().item() - ck[0]) <= 1e-9 * max(1.0, abs(ck[0])), k
+    y, neg_dy = O.energy_forces(sd, dict(args), d["z"], d["pos"], d["batch"], static_shapes=True)
+    assert np.allclose(y.detach().numpy(), d["y"], rtol=1e-4, atol=1e-5)
+    assert np.allclose(neg_dy.numpy(), d["neg_dy"], rtol=1e-4, atol=1e-4)

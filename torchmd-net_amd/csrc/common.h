@@ -1,0 +1,54 @@
+// Shared device helpers for the torchmd-net_amd HIP library (gfx950 / CDNA4, wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define TMD_WAVE 64
+
+namespace tmd {
+
+// ---- status codes returned across the C ABI (never throw across it) ----
+enum Status : int {
+  kOk = 0,
+  kBadArgument = 1,
+  kUnsupported = 2,
+  kLaunchFailed = 3,
+  kWorkspaceTooSmall = 4,
+};
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & (TMD_WAVE - 1); }
+
+// Number of set bits of `mask` strictly below this lane (exclusive lane prefix of a ballot).
+__device__ __forceinline__ int lane_prefix(unsigned long long mask) {
+  unsigned lo = __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u);
+  return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32), lo);
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// Sum over aligned groups of `width` lanes (width a power of two <= 64).
+template <typename T>
+__device__ __forceinline__ T group_sum(T v, int width) {
+  for (int o = width >> 1; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+template <typename T> __device__ __forceinline__ T sigmoid(T x) { return T(1) / (T(1) + exp(-x)); }
+template <> __device__ __forceinline__ float sigmoid<float>(float x) { return 1.0f / (1.0f + __expf(-x)); }
+
+// silu and its derivative, sharing the sigmoid
+template <typename T> struct Silu {
+  T s, sig;
+  __device__ __forceinline__ explicit Silu(T x) {
+    sig = sigmoid<T>(x);
+    s = x * sig;
+  }
+  __device__ __forceinline__ T d(T x) const { return sig * (T(1) + x * (T(1) - sig)); }
+};
+
+}  // namespace tmd

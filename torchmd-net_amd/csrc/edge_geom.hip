@@ -1,0 +1,197 @@
+// Fused per-edge geometry: RBF expansion (expnorm / gauss) + cosine cutoff + unit vectors.
+// Reference: ExpNormalSmearing (models/utils.py:303-344), GaussianSmearing (utils.py:272-300),
+// CosineCutoff (utils.py:362-390), d_ij normalisation (torchmd_et.py:173-174, tensornet.py:223-226).
+// HBM-bound streaming kernels: forward reads delta/r (16 B/edge) and writes R+4 values per edge;
+// backward reads the R+4 incoming gradients and writes 16 B/edge.
+#include "common.h"
+#include "tmdnet.h"
+
+namespace tmd {
+namespace geom {
+
+template <typename T> struct Cfg {
+  int E, R, type;
+  const int32_t* src;
+  const int32_t* dst;
+  const T* dl;
+  const T* r;
+  const T* mu;
+  const T* beta;
+  T cl, cu, alpha;
+};
+
+template <typename T> __device__ __forceinline__ T pi() { return T(3.14159265358979323846); }
+
+// CosineCutoff(cl, cu) and its derivative w.r.t. r (utils.py:368-390)
+template <typename T> __device__ __forceinline__ void cosine_cutoff(T r, T cl, T cu, T& c, T& dc) {
+  if (cl > T(0)) {
+    const T w = T(2) * pi<T>() / (cu - cl);
+    const T arg = pi<T>() * (T(2) * (r - cl) / (cu - cl) + T(1));
+    const bool in = (r < cu) && (r > cl);
+    c = in ? T(0.5) * (cos(arg) + T(1)) : T(0);
+    dc = in ? T(-0.5) * sin(arg) * w : T(0);
+  } else {
+    const bool in = r < cu;
+    const T arg = r * pi<T>() / cu;
+    c = in ? T(0.5) * (cos(arg) + T(1)) : T(0);
+    dc = in ? T(-0.5) * sin(arg) * pi<T>() / cu : T(0);
+  }
+}
+
+// basis value and d/dr
+template <typename T>
+__device__ __forceinline__ void basis(const Cfg<T>& P, T r, int k, T& f, T& df) {
+  if (P.type == TMDNET_RBF_EXPNORM) {
+    T c0, dc0;
+    cosine_cutoff<T>(r, T(0), P.cu, c0, dc0);
+    const T u = exp(P.alpha * (P.cl - r));
+    const T du = -P.alpha * u;
+    const T z = u - P.mu[k];
+    const T g = exp(-P.beta[k] * z * z);
+    const T dg = g * (T(-2) * P.beta[k] * z * du);
+    f = c0 * g;
+    df = dc0 * g + c0 * dg;
+  } else {
+    const T z = r - P.mu[k];
+    const T coeff = P.beta[0];
+    f = exp(coeff * z * z);
+    df = f * T(2) * coeff * z;
+  }
+}
+
+template <typename T>
+__global__ void k_fwd(Cfg<T> P, T* __restrict__ f, T* __restrict__ C, T* __restrict__ u) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long nf = f ? (long long)P.E * P.R : 0;
+  if (i < nf) {
+    const int e = (int)(i / P.R), k = (int)(i % P.R);
+    T v, dv;
+    basis(P, P.r[e], k, v, dv);
+    f[i] = v;
+  }
+  if (i < P.E) {
+    const int e = (int)i;
+    if (C) {
+      T c, dc;
+      cosine_cutoff<T>(P.r[e], P.cl, P.cu, c, dc);
+      C[e] = c;
+    }
+    if (u) {
+      const T x = P.dl[3 * e], y = P.dl[3 * e + 1], z = P.dl[3 * e + 2];
+      if (P.src[e] == P.dst[e]) {
+        u[3 * e] = x; u[3 * e + 1] = y; u[3 * e + 2] = z;
+      } else {
+        const T n = sqrt(x * x + y * y + z * z);
+        u[3 * e] = x / n; u[3 * e + 1] = y / n; u[3 * e + 2] = z / n;
+      }
+    }
+  }
+}
+
+// One wave per edge (grid-stride); lanes over the basis index.
+template <typename T>
+__global__ __launch_bounds__(256) void k_bwd(Cfg<T> P, const T* __restrict__ gf, const T* __restrict__ gC,
+                                             const T* __restrict__ gu, T* __restrict__ gr,
+                                             T* __restrict__ gdl) {
+  const int lane = lane_id();
+  const int nw = gridDim.x * (blockDim.x / TMD_WAVE);
+  for (int e = blockIdx.x * (blockDim.x / TMD_WAVE) + threadIdx.x / TMD_WAVE; e < P.E; e += nw) {
+    const T r = P.r[e];
+    T acc = T(0);
+    if (gf) {
+      for (int k = lane; k < P.R; k += TMD_WAVE) {
+        T v, dv;
+        basis(P, r, k, v, dv);
+        acc += gf[(long long)e * P.R + k] * dv;
+      }
+      acc = wave_sum(acc);
+    }
+    if (lane == 0) {
+      if (gC) {
+        T c, dc;
+        cosine_cutoff<T>(r, P.cl, P.cu, c, dc);
+        acc += gC[e] * dc;
+      }
+      gr[e] = acc;
+      T gx = T(0), gy = T(0), gz = T(0);
+      if (gu) {
+        const T x = P.dl[3 * e], y = P.dl[3 * e + 1], z = P.dl[3 * e + 2];
+        const T a = gu[3 * e], b = gu[3 * e + 1], c = gu[3 * e + 2];
+        if (P.src[e] == P.dst[e]) {
+          gx = a; gy = b; gz = c;
+        } else {
+          const T n = sqrt(x * x + y * y + z * z);
+          const T ux = x / n, uy = y / n, uz = z / n;
+          const T dot = ux * a + uy * b + uz * c;
+          gx = (a - ux * dot) / n;
+          gy = (b - uy * dot) / n;
+          gz = (c - uz * dot) / n;
+        }
+      }
+      gdl[3 * e] = gx;
+      gdl[3 * e + 1] = gy;
+      gdl[3 * e + 2] = gz;
+    }
+  }
+}
+
+template <typename T>
+static Cfg<T> make(int E, int R, int type, const int32_t* src, const int32_t* dst, const void* dl,
+                   const void* r, const void* mu, const void* beta, double cl, double cu) {
+  Cfg<T> P;
+  P.E = E; P.R = R; P.type = type; P.src = src; P.dst = dst;
+  P.dl = (const T*)dl; P.r = (const T*)r; P.mu = (const T*)mu; P.beta = (const T*)beta;
+  P.cl = (T)cl; P.cu = (T)cu; P.alpha = (T)(5.0 / (cu - cl));
+  return P;
+}
+
+}  // namespace geom
+}  // namespace tmd
+
+using namespace tmd;
+
+extern "C" int tmdnet_edge_geom_fwd(int dtype, int n_edges, int num_rbf, int rbf_type,
+                                    const int32_t* src, const int32_t* dst, const void* deltas,
+                                    const void* dist, const void* mu, const void* beta,
+                                    double cutoff_lower, double cutoff_upper, void* rbf, void* cutoff,
+                                    void* unit, void* stream) {
+  if (n_edges <= 0) return kOk;
+  hipStream_t st = (hipStream_t)stream;
+  const long long work = rbf ? (long long)n_edges * num_rbf : n_edges;
+  const int tb = 256;
+  dim3 g((unsigned)((work + tb - 1) / tb));
+  if (dtype == TMDNET_F32) {
+    auto P = geom::make<float>(n_edges, num_rbf, rbf_type, src, dst, deltas, dist, mu, beta, cutoff_lower, cutoff_upper);
+    hipLaunchKernelGGL(geom::k_fwd<float>, g, dim3(tb), 0, st, P, (float*)rbf, (float*)cutoff, (float*)unit);
+  } else if (dtype == TMDNET_F64) {
+    auto P = geom::make<double>(n_edges, num_rbf, rbf_type, src, dst, deltas, dist, mu, beta, cutoff_lower, cutoff_upper);
+    hipLaunchKernelGGL(geom::k_fwd<double>, g, dim3(tb), 0, st, P, (double*)rbf, (double*)cutoff, (double*)unit);
+  } else {
+    return kUnsupported;
+  }
+  return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
+}
+
+extern "C" int tmdnet_edge_geom_bwd(int dtype, int n_edges, int num_rbf, int rbf_type,
+                                    const int32_t* src, const int32_t* dst, const void* deltas,
+                                    const void* dist, const void* mu, const void* beta,
+                                    double cutoff_lower, double cutoff_upper, const void* grad_rbf,
+                                    const void* grad_cutoff, const void* grad_unit, void* grad_dist,
+                                    void* grad_deltas, void* stream) {
+  if (n_edges <= 0) return kOk;
+  hipStream_t st = (hipStream_t)stream;
+  const int tb = 256;
+  const int blocks = (int)std::min<long long>(((long long)n_edges + 3) / 4, 256LL * 64);
+  if (dtype == TMDNET_F32) {
+    auto P = geom::make<float>(n_edges, num_rbf, rbf_type, src, dst, deltas, dist, mu, beta, cutoff_lower, cutoff_upper);
+    hipLaunchKernelGGL(geom::k_bwd<float>, dim3(blocks), dim3(tb), 0, st, P, (const float*)grad_rbf,
+                       (const float*)grad_cutoff, (const float*)grad_unit, (float*)grad_dist, (float*)grad_deltas);
+  } else if (dtype == TMDNET_F64) {
+    auto P = geom::make<double>(n_edges, num_rbf, rbf_type, src, dst, deltas, dist, mu, beta, cutoff_lower, cutoff_upper);
+    hipLaunchKernelGGL(geom::k_bwd<double>, dim3(blocks), dim3(tb), 0, st, P, (const double*)grad_rbf,
+                       (const double*)grad_cutoff, (const double*)grad_unit, (double*)grad_dist, (double*)grad_deltas);
+  } else {
+    return kUnsupported;
+  }
+  return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
+}

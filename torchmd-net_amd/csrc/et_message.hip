@@ -1,0 +1,612 @@
+// Equivariant-Transformer edge message + aggregation, and the neighbour-embedding aggregation.
+//
+// Reference: EquivariantMultiHeadAttention.forward/message/aggregate (models/torchmd_et.py:272-347),
+// NeighborEmbedding.forward/message (models/utils.py:73-108).  The reference gathers q_i, k_j, v_j,
+// vec_j into E x (heads, d) and E x (3, heads, d) tensors, multiplies them elementwise and
+// scatter-adds with atomics (torch_scatter).  Here:
+//   * one wave64 owns one destination atom t; its q[t] (and, backward, dL/dx[t], dL/dvec[t]) sit in
+//     registers; the wave streams t's CSR row of edges (pre-activation dk/dv rows are read
+//     coalesced, 4*H values per edge) and gathers k/v/vec rows of the sources (L2 / Infinity-Cache
+//     resident for spatially ordered atoms);
+//   * heads are aligned lane groups: the q.k.dk dot product is a group_sum over d/VEC lanes;
+//   * x (H) and vec (3H) accumulate in registers and are written ONCE: no atomics, deterministic;
+//   * the backward is two such passes: a destination pass (gq, per-edge grads) and a source pass
+//     that walks the same CSR rows as reversed edges (valid for the symmetric lists the model
+//     builds: dk, dv, cutoff are functions of |r| only and unit vectors flip sign), giving
+//     gk, gv, gvec without a transpose scatter or atomics.
+#include "common.h"
+#include "tmdnet.h"
+
+namespace tmd {
+namespace et {
+
+template <typename T, int V> struct Vec;
+template <> struct Vec<float, 1> { using t = float; };
+template <> struct Vec<float, 2> { using t = float2; };
+template <> struct Vec<float, 4> { using t = float4; };
+template <> struct Vec<double, 1> { using t = double; };
+template <> struct Vec<double, 2> { using t = double2; };
+template <> struct Vec<double, 4> { using t = double4; };
+
+template <typename T, int V> __device__ __forceinline__ void ldv(T (&o)[V], const T* p) {
+  using VT = typename Vec<T, V>::t;
+  const VT x = *reinterpret_cast<const VT*>(p);
+  if constexpr (V == 1) { o[0] = x; }
+  else if constexpr (V == 2) { o[0] = x.x; o[1] = x.y; }
+  else { o[0] = x.x; o[1] = x.y; o[2] = x.z; o[3] = x.w; }
+}
+template <typename T, int V> __device__ __forceinline__ void stv(T* p, const T (&o)[V]) {
+  using VT = typename Vec<T, V>::t;
+  VT x;
+  if constexpr (V == 1) { x = o[0]; }
+  else if constexpr (V == 2) { x.x = o[0]; x.y = o[1]; }
+  else { x.x = o[0]; x.y = o[1]; x.z = o[2]; x.w = o[3]; }
+  *reinterpret_cast<VT*>(p) = x;
+}
+template <typename T, int V> __device__ __forceinline__ void zero(T (&o)[V]) {
+#pragma unroll
+  for (int i = 0; i < V; ++i) o[i] = T(0);
+}
+
+template <typename T> struct Args {
+  int n, H, d, L, lph, cap;
+  const int32_t* row_ptr;
+  const int32_t* src;
+  const int32_t* order;
+  const T* q; int ldq;
+  const T* k; int ldk;
+  const T* v; int ldv;
+  const T* vec;
+  const T* pk; int ldpk;
+  const T* pv; int ldpv;
+  const T* C;
+  const T* u;
+  // forward outputs
+  T* xo; T* veco;
+  // backward inputs / outputs
+  const T* gx; const T* gvec;
+  T* gq; T* gk; T* gv; T* gveci; T* gpk; T* gpv; T* gC; T* gu;
+};
+
+// silu of the pre-activation, or 1 when the projection is absent
+template <typename T, int V>
+__device__ __forceinline__ void act(const T* base, bool has, T (&x)[V], T (&s)[V], T (&ds)[V]) {
+  if (has) {
+    ldv<T, V>(x, base);
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+      Silu<T> f(x[i]);
+      s[i] = f.s;
+      ds[i] = f.d(x[i]);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < V; ++i) { x[i] = T(0); s[i] = T(1); ds[i] = T(0); }
+  }
+}
+
+// ------------------------------------------------------------------ forward
+template <typename T, int V>
+__global__ __launch_bounds__(256) void k_fwd(Args<T> A) {
+  const int w = blockIdx.x * (blockDim.x / TMD_WAVE) + threadIdx.x / TMD_WAVE;
+  if (w >= A.n) return;
+  const int t = A.order ? A.order[w] : w;
+  const int lane = lane_id();
+  const bool on = lane < A.L;
+  const int c0 = on ? lane * V : 0;
+  const int hh = c0 / A.d, cc = c0 % A.d;
+  const int vo = hh * 3 * A.d + cc;
+  const bool hk = A.pk != nullptr, hv = A.pv != nullptr;
+  T q[V];
+  ldv<T, V>(q, A.q + (size_t)t * A.ldq + c0);
+  T ax[V], a0[V], a1[V], a2[V];
+  zero(ax); zero(a0); zero(a1); zero(a2);
+  const int b = min(A.row_ptr[t], A.cap), e = min(A.row_ptr[t + 1], A.cap);
+  for (int k = b; k < e; ++k) {
+    const int s = A.src[k];
+    const T Ce = A.C[k];
+    const T u0 = A.u[3 * k], u1 = A.u[3 * k + 1], u2 = A.u[3 * k + 2];
+    T kk[V], px[V], dk[V], dd[V];
+    ldv<T, V>(kk, A.k + (size_t)s * A.ldk + c0);
+    act<T, V>(A.pk + (size_t)k * A.ldpk + c0, hk, px, dk, dd);
+    T part = T(0);
+#pragma unroll
+    for (int i = 0; i < V; ++i) part += q[i] * kk[i] * dk[i];
+    part = group_sum(part, A.lph);
+    const Silu<T> sa(part);
+    const T a = sa.s * Ce;
+    const T* vs = A.v + (size_t)s * A.ldv + vo;
+    const T* pvs = A.pv + (size_t)k * A.ldpv + vo;
+    T vx[V], v1[V], v2[V], dvx[V], dv1[V], dv2[V];
+    ldv<T, V>(vx, vs);
+    ldv<T, V>(v1, vs + A.d);
+    ldv<T, V>(v2, vs + 2 * A.d);
+    act<T, V>(pvs, hv, px, dvx, dd);
+    act<T, V>(pvs + A.d, hv, px, dv1, dd);
+    act<T, V>(pvs + 2 * A.d, hv, px, dv2, dd);
+    const T* vecs = A.vec + (size_t)s * 3 * A.H + c0;
+    T w0[V], w1[V], w2[V];
+    ldv<T, V>(w0, vecs);
+    ldv<T, V>(w1, vecs + A.H);
+    ldv<T, V>(w2, vecs + 2 * A.H);
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+      ax[i] += vx[i] * dvx[i] * a;
+      const T v1e = v1[i] * dv1[i], v2e = v2[i] * dv2[i];
+      a0[i] += w0[i] * v1e + v2e * u0;
+      a1[i] += w1[i] * v1e + v2e * u1;
+      a2[i] += w2[i] * v1e + v2e * u2;
+    }
+  }
+  if (on) {
+    stv<T, V>(A.xo + (size_t)t * A.H + c0, ax);
+    T* vo_ = A.veco + (size_t)t * 3 * A.H + c0;
+    stv<T, V>(vo_, a0);
+    stv<T, V>(vo_ + A.H, a1);
+    stv<T, V>(vo_ + 2 * A.H, a2);
+  }
+}
+
+// ------------------------------------------------------------------ backward, destination pass
+template <typename T, int V>
+__global__ __launch_bounds__(256) void k_bwd_dst(Args<T> A) {
+  const int w = blockIdx.x * (blockDim.x / TMD_WAVE) + threadIdx.x / TMD_WAVE;
+  if (w >= A.n) return;
+  const int t = A.order ? A.order[w] : w;
+  const int lane = lane_id();
+  const bool on = lane < A.L;
+  const int c0 = on ? lane * V : 0;
+  const int hh = c0 / A.d, cc = c0 % A.d;
+  const int vo = hh * 3 * A.d + cc;
+  const bool hk = A.pk != nullptr, hv = A.pv != nullptr;
+  const bool head_leader = on && (lane % A.lph) == 0;
+  T q[V], gx[V], g0[V], g1[V], g2[V];
+  ldv<T, V>(q, A.q + (size_t)t * A.ldq + c0);
+  ldv<T, V>(gx, A.gx + (size_t)t * A.H + c0);
+  const T* gvt = A.gvec + (size_t)t * 3 * A.H + c0;
+  ldv<T, V>(g0, gvt);
+  ldv<T, V>(g1, gvt + A.H);
+  ldv<T, V>(g2, gvt + 2 * A.H);
+  T gq[V];
+  zero(gq);
+  const int b = min(A.row_ptr[t], A.cap), e = min(A.row_ptr[t + 1], A.cap);
+  for (int k = b; k < e; ++k) {
+    const int s = A.src[k];
+    const T Ce = A.C[k];
+    const T u0 = A.u[3 * k], u1 = A.u[3 * k + 1], u2 = A.u[3 * k + 2];
+    T kk[V], pk[V], dk[V], ddk[V];
+    ldv<T, V>(kk, A.k + (size_t)s * A.ldk + c0);
+    act<T, V>(A.pk + (size_t)k * A.ldpk + c0, hk, pk, dk, ddk);
+    T part = T(0);
+#pragma unroll
+    for (int i = 0; i < V; ++i) part += q[i] * kk[i] * dk[i];
+    part = group_sum(part, A.lph);
+    const Silu<T> sa(part);
+    const T a = sa.s * Ce;
+    const T* vs = A.v + (size_t)s * A.ldv + vo;
+    const T* pvs = A.pv + (size_t)k * A.ldpv + vo;
+    T vx[V], v1[V], v2[V], px[V], p1[V], p2[V], dvx[V], dv1[V], dv2[V], ddx[V], dd1[V], dd2[V];
+    ldv<T, V>(vx, vs);
+    ldv<T, V>(v1, vs + A.d);
+    ldv<T, V>(v2, vs + 2 * A.d);
+    act<T, V>(pvs, hv, px, dvx, ddx);
+    act<T, V>(pvs + A.d, hv, p1, dv1, dd1);
+    act<T, V>(pvs + 2 * A.d, hv, p2, dv2, dd2);
+    const T* vecs = A.vec + (size_t)s * 3 * A.H + c0;
+    T w0[V], w1[V], w2[V];
+    ldv<T, V>(w0, vecs);
+    ldv<T, V>(w1, vecs + A.H);
+    ldv<T, V>(w2, vecs + 2 * A.H);
+    T ga = T(0), gu0 = T(0), gu1 = T(0), gu2 = T(0);
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+      ga += gx[i] * vx[i] * dvx[i];
+      const T v2e = v2[i] * dv2[i];
+      gu0 += g0[i] * v2e;
+      gu1 += g1[i] * v2e;
+      gu2 += g2[i] * v2e;
+    }
+    ga = group_sum(ga, A.lph);
+    const T gs = ga * Ce * sa.d(part);
+    T gpk[V], gpx[V], gp1[V], gp2[V];
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+      gq[i] += gs * kk[i] * dk[i];
+      gpk[i] = gs * q[i] * kk[i] * ddk[i];
+      gpx[i] = gx[i] * a * vx[i] * ddx[i];
+      const T gv1e = g0[i] * w0[i] + g1[i] * w1[i] + g2[i] * w2[i];
+      gp1[i] = gv1e * v1[i] * dd1[i];
+      const T gv2e = g0[i] * u0 + g1[i] * u1 + g2[i] * u2;
+      gp2[i] = gv2e * v2[i] * dd2[i];
+    }
+    T gc = head_leader ? ga * sa.s : T(0);
+    gc = wave_sum(gc);
+    gu0 = wave_sum(on ? gu0 : T(0));
+    gu1 = wave_sum(on ? gu1 : T(0));
+    gu2 = wave_sum(on ? gu2 : T(0));
+    if (on) {
+      if (hk) stv<T, V>(A.gpk + (size_t)k * A.H + c0, gpk);
+      if (hv) {
+        T* gp = A.gpv + (size_t)k * 3 * A.H + vo;
+        stv<T, V>(gp, gpx);
+        stv<T, V>(gp + A.d, gp1);
+        stv<T, V>(gp + 2 * A.d, gp2);
+      }
+    }
+    if (lane == 0) {
+      A.gC[k] = gc;
+      A.gu[3 * k] = gu0;
+      A.gu[3 * k + 1] = gu1;
+      A.gu[3 * k + 2] = gu2;
+    }
+  }
+  if (on) stv<T, V>(A.gq + (size_t)t * A.H + c0, gq);
+}
+
+// ------------------------------------------------------------------ backward, source pass
+// Wave owns node j as SOURCE.  Row j lists edges m->j; each is read as its reverse j->m
+// (same dk/dv/cutoff, unit vector negated), m being the destination whose q/gx/gvec are gathered.
+template <typename T, int V>
+__global__ __launch_bounds__(256) void k_bwd_src(Args<T> A) {
+  const int w = blockIdx.x * (blockDim.x / TMD_WAVE) + threadIdx.x / TMD_WAVE;
+  if (w >= A.n) return;
+  const int j = A.order ? A.order[w] : w;
+  const int lane = lane_id();
+  const bool on = lane < A.L;
+  const int c0 = on ? lane * V : 0;
+  const int hh = c0 / A.d, cc = c0 % A.d;
+  const int vo = hh * 3 * A.d + cc;
+  const bool hk = A.pk != nullptr, hv = A.pv != nullptr;
+  T kk[V], vx[V], v1[V], v2[V], w0[V], w1[V], w2[V];
+  ldv<T, V>(kk, A.k + (size_t)j * A.ldk + c0);
+  const T* vj = A.v + (size_t)j * A.ldv + vo;
+  ldv<T, V>(vx, vj);
+  ldv<T, V>(v1, vj + A.d);
+  ldv<T, V>(v2, vj + 2 * A.d);
+  const T* vecj = A.vec + (size_t)j * 3 * A.H + c0;
+  ldv<T, V>(w0, vecj);
+  ldv<T, V>(w1, vecj + A.H);
+  ldv<T, V>(w2, vecj + 2 * A.H);
+  T gk[V], gvx[V], gv1[V], gv2[V], gw0[V], gw1[V], gw2[V];
+  zero(gk); zero(gvx); zero(gv1); zero(gv2); zero(gw0); zero(gw1); zero(gw2);
+  const int b = min(A.row_ptr[j], A.cap), e = min(A.row_ptr[j + 1], A.cap);
+  for (int k = b; k < e; ++k) {
+    const int m = A.src[k];
+    const T Ce = A.C[k];
+    const T u0 = -A.u[3 * k], u1 = -A.u[3 * k + 1], u2 = -A.u[3 * k + 2];
+    T qm[V], gxm[V], g0[V], g1[V], g2[V], pk[V], dk[V], ddk[V];
+    ldv<T, V>(qm, A.q + (size_t)m * A.ldq + c0);
+    ldv<T, V>(gxm, A.gx + (size_t)m * A.H + c0);
+    const T* gvm = A.gvec + (size_t)m * 3 * A.H + c0;
+    ldv<T, V>(g0, gvm);
+    ldv<T, V>(g1, gvm + A.H);
+    ldv<T, V>(g2, gvm + 2 * A.H);
+    act<T, V>(A.pk + (size_t)k * A.ldpk + c0, hk, pk, dk, ddk);
+    const T* pvs = A.pv + (size_t)k * A.ldpv + vo;
+    T px[V], dvx[V], dv1[V], dv2[V], dd[V];
+    act<T, V>(pvs, hv, px, dvx, dd);
+    act<T, V>(pvs + A.d, hv, px, dv1, dd);
+    act<T, V>(pvs + 2 * A.d, hv, px, dv2, dd);
+    T part = T(0), ga = T(0);
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+      part += qm[i] * kk[i] * dk[i];
+      ga += gxm[i] * vx[i] * dvx[i];
+    }
+    part = group_sum(part, A.lph);
+    ga = group_sum(ga, A.lph);
+    const Silu<T> sa(part);
+    const T a = sa.s * Ce;
+    const T gs = ga * Ce * sa.d(part);
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+      gk[i] += gs * qm[i] * dk[i];
+      gvx[i] += gxm[i] * a * dvx[i];
+      const T gv1e = g0[i] * w0[i] + g1[i] * w1[i] + g2[i] * w2[i];
+      gv1[i] += gv1e * dv1[i];
+      const T gv2e = g0[i] * u0 + g1[i] * u1 + g2[i] * u2;
+      gv2[i] += gv2e * dv2[i];
+      const T v1e = v1[i] * dv1[i];
+      gw0[i] += g0[i] * v1e;
+      gw1[i] += g1[i] * v1e;
+      gw2[i] += g2[i] * v1e;
+    }
+  }
+  if (on) {
+    stv<T, V>(A.gk + (size_t)j * A.H + c0, gk);
+    T* gvj = A.gv + (size_t)j * 3 * A.H + vo;
+    stv<T, V>(gvj, gvx);
+    stv<T, V>(gvj + A.d, gv1);
+    stv<T, V>(gvj + 2 * A.d, gv2);
+    T* gwj = A.gveci + (size_t)j * 3 * A.H + c0;
+    stv<T, V>(gwj, gw0);
+    stv<T, V>(gwj + A.H, gw1);
+    stv<T, V>(gwj + 2 * A.H, gw2);
+  }
+}
+
+// ------------------------------------------------------------------ neighbour embedding
+template <typename T> struct NbArgs {
+  int n, H, L, cap;
+  const int32_t* row_ptr;
+  const int32_t* src;
+  const T* x; int ldx;
+  const T* w; int ldw;
+  const T* C;
+  T* out;
+  const T* gout;
+  T* gx; T* gw; T* gC;
+};
+
+template <typename T, int V>
+__global__ __launch_bounds__(256) void k_nb_fwd(NbArgs<T> A) {
+  const int t = blockIdx.x * (blockDim.x / TMD_WAVE) + threadIdx.x / TMD_WAVE;
+  if (t >= A.n) return;
+  const int lane = lane_id();
+  const bool on = lane < A.L;
+  const int c0 = on ? lane * V : 0;
+  T acc[V];
+  zero(acc);
+  const int b = min(A.row_ptr[t], A.cap), e = min(A.row_ptr[t + 1], A.cap);
+  for (int k = b; k < e; ++k) {
+    const int s = A.src[k];
+    if (s == t) continue;
+    const T Ce = A.C[k];
+    T xs[V], wk[V];
+    ldv<T, V>(xs, A.x + (size_t)s * A.ldx + c0);
+    ldv<T, V>(wk, A.w + (size_t)k * A.ldw + c0);
+#pragma unroll
+    for (int i = 0; i < V; ++i) acc[i] += xs[i] * (wk[i] * Ce);
+  }
+  if (on) stv<T, V>(A.out + (size_t)t * A.H + c0, acc);
+}
+
+// destination pass: gw[e] = gout[t] * x[s] * C[e], gC[e] = sum_c gout[t] x[s] w[e]
+template <typename T, int V>
+__global__ __launch_bounds__(256) void k_nb_bwd_dst(NbArgs<T> A) {
+  const int t = blockIdx.x * (blockDim.x / TMD_WAVE) + threadIdx.x / TMD_WAVE;
+  if (t >= A.n) return;
+  const int lane = lane_id();
+  const bool on = lane < A.L;
+  const int c0 = on ? lane * V : 0;
+  T go[V];
+  ldv<T, V>(go, A.gout + (size_t)t * A.H + c0);
+  const int b = min(A.row_ptr[t], A.cap), e = min(A.row_ptr[t + 1], A.cap);
+  for (int k = b; k < e; ++k) {
+    const int s = A.src[k];
+    T gw[V];
+    T gc = T(0);
+    if (s == t) {
+      zero(gw);
+    } else {
+      const T Ce = A.C[k];
+      T xs[V], wk[V];
+      ldv<T, V>(xs, A.x + (size_t)s * A.ldx + c0);
+      ldv<T, V>(wk, A.w + (size_t)k * A.ldw + c0);
+#pragma unroll
+      for (int i = 0; i < V; ++i) {
+        gw[i] = go[i] * xs[i] * Ce;
+        gc += go[i] * xs[i] * wk[i];
+      }
+    }
+    gc = wave_sum(on ? gc : T(0));
+    if (on) stv<T, V>(A.gw + (size_t)k * A.H + c0, gw);
+    if (lane == 0) A.gC[k] = gc;
+  }
+}
+
+// source pass: gx[j] = sum_{reverse edges j->m} gout[m] * w[e] * C[e]
+template <typename T, int V>
+__global__ __launch_bounds__(256) void k_nb_bwd_src(NbArgs<T> A) {
+  const int j = blockIdx.x * (blockDim.x / TMD_WAVE) + threadIdx.x / TMD_WAVE;
+  if (j >= A.n) return;
+  const int lane = lane_id();
+  const bool on = lane < A.L;
+  const int c0 = on ? lane * V : 0;
+  T acc[V];
+  zero(acc);
+  const int b = min(A.row_ptr[j], A.cap), e = min(A.row_ptr[j + 1], A.cap);
+  for (int k = b; k < e; ++k) {
+    const int m = A.src[k];
+    if (m == j) continue;
+    const T Ce = A.C[k];
+    T gm[V], wk[V];
+    ldv<T, V>(gm, A.gout + (size_t)m * A.H + c0);
+    ldv<T, V>(wk, A.w + (size_t)k * A.ldw + c0);
+#pragma unroll
+    for (int i = 0; i < V; ++i) acc[i] += gm[i] * (wk[i] * Ce);
+  }
+  if (on) stv<T, V>(A.gx + (size_t)j * A.H + c0, acc);
+}
+
+// ------------------------------------------------------------------ host helpers
+static inline int pick_vec(int H) {
+  if (H % 256 == 0) return 4;
+  if (H % 128 == 0) return 2;
+  return 1;
+}
+
+template <typename T>
+static bool aligned(const void* p, int ld, int V) {
+  if (!p) return true;
+  return ((uintptr_t)p % (sizeof(T) * V)) == 0 && (ld % V) == 0;
+}
+
+template <typename T, template <typename, int> class K, typename AT>
+static int launch_v(int V, int n, AT A, hipStream_t st) {
+  const int tb = 256, wpb = tb / TMD_WAVE;
+  dim3 g((n + wpb - 1) / wpb);
+  if (n <= 0) return kOk;
+  if (V == 1) hipLaunchKernelGGL((K<T, 1>::fn), g, dim3(tb), 0, st, A);
+  else if (V == 2) hipLaunchKernelGGL((K<T, 2>::fn), g, dim3(tb), 0, st, A);
+  else hipLaunchKernelGGL((K<T, 4>::fn), g, dim3(tb), 0, st, A);
+  return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
+}
+
+template <typename T, int V> struct KFwd { static constexpr auto fn = k_fwd<T, V>; };
+template <typename T, int V> struct KBwdDst { static constexpr auto fn = k_bwd_dst<T, V>; };
+template <typename T, int V> struct KBwdSrc { static constexpr auto fn = k_bwd_src<T, V>; };
+template <typename T, int V> struct KNbFwd { static constexpr auto fn = k_nb_fwd<T, V>; };
+template <typename T, int V> struct KNbDst { static constexpr auto fn = k_nb_bwd_dst<T, V>; };
+template <typename T, int V> struct KNbSrc { static constexpr auto fn = k_nb_bwd_src<T, V>; };
+
+template <typename T>
+static int setup(Args<T>& A, int n, int H, int heads, const int32_t* row_ptr, const int32_t* src,
+                 int cap, const void* q, int ldq, const void* k, int ldk, const void* v, int ldv_,
+                 const void* vec, const void* pk, int ldpk, const void* pv, int ldpv, const void* C,
+                 const void* u, const int32_t* order, int& V) {
+  if (H <= 0 || heads <= 0 || H % heads) return kBadArgument;
+  V = pick_vec(H);
+  const int d = H / heads;
+  while (V > 1 && (d % V)) V >>= 1;
+  if (H / V > TMD_WAVE) return kUnsupported;
+  const int lph = d / V;
+  if (lph & (lph - 1)) return kUnsupported;  // head must be a power-of-two lane group
+  if (!aligned<T>(q, ldq, V) || !aligned<T>(k, ldk, V) || !aligned<T>(v, ldv_, V) ||
+      !aligned<T>(pk, ldpk, V) || !aligned<T>(pv, ldpv, V) || !aligned<T>(vec, H, V))
+    return kBadArgument;
+  A = Args<T>{};
+  A.n = n; A.H = H; A.d = d; A.L = H / V; A.lph = lph; A.cap = cap;
+  A.row_ptr = row_ptr; A.src = src; A.order = order;
+  A.q = (const T*)q; A.ldq = ldq; A.k = (const T*)k; A.ldk = ldk; A.v = (const T*)v; A.ldv = ldv_;
+  A.vec = (const T*)vec; A.pk = (const T*)pk; A.ldpk = ldpk; A.pv = (const T*)pv; A.ldpv = ldpv;
+  A.C = (const T*)C; A.u = (const T*)u;
+  return kOk;
+}
+
+template <typename T>
+static int fwd(int n, int H, int heads, const int32_t* row_ptr, const int32_t* src, int cap,
+               const void* q, int ldq, const void* k, int ldk, const void* v, int ldv_,
+               const void* vec, const void* pk, int ldpk, const void* pv, int ldpv, const void* C,
+               const void* u, void* xo, void* veco, const int32_t* order, hipStream_t st) {
+  Args<T> A;
+  int V;
+  int rc = setup<T>(A, n, H, heads, row_ptr, src, cap, q, ldq, k, ldk, v, ldv_, vec, pk, ldpk, pv,
+                    ldpv, C, u, order, V);
+  if (rc) return rc;
+  A.xo = (T*)xo;
+  A.veco = (T*)veco;
+  return launch_v<T, KFwd>(V, n, A, st);
+}
+
+template <typename T>
+static int bwd(int n, int H, int heads, const int32_t* row_ptr, const int32_t* src, int cap,
+               const void* q, int ldq, const void* k, int ldk, const void* v, int ldv_,
+               const void* vec, const void* pk, int ldpk, const void* pv, int ldpv, const void* C,
+               const void* u, const void* gx, const void* gvec, void* gq, void* gk, void* gv,
+               void* gveci, void* gpk, void* gpv, void* gC, void* gu, const int32_t* order,
+               hipStream_t st) {
+  Args<T> A;
+  int V;
+  int rc = setup<T>(A, n, H, heads, row_ptr, src, cap, q, ldq, k, ldk, v, ldv_, vec, pk, ldpk, pv,
+                    ldpv, C, u, order, V);
+  if (rc) return rc;
+  A.gx = (const T*)gx; A.gvec = (const T*)gvec;
+  A.gq = (T*)gq; A.gk = (T*)gk; A.gv = (T*)gv; A.gveci = (T*)gveci;
+  A.gpk = (T*)gpk; A.gpv = (T*)gpv; A.gC = (T*)gC; A.gu = (T*)gu;
+  rc = launch_v<T, KBwdDst>(V, n, A, st);
+  if (rc) return rc;
+  return launch_v<T, KBwdSrc>(V, n, A, st);
+}
+
+template <typename T>
+static int nb_setup(NbArgs<T>& A, int n, int H, const int32_t* row_ptr, const int32_t* src, int cap,
+                    const void* x, int ldx, const void* w, int ldw, const void* C, int& V) {
+  V = pick_vec(H);
+  if (H / V > TMD_WAVE || H % V) return kUnsupported;
+  if (!aligned<T>(x, ldx, V) || !aligned<T>(w, ldw, V)) return kBadArgument;
+  A = NbArgs<T>{};
+  A.n = n; A.H = H; A.L = H / V; A.cap = cap; A.row_ptr = row_ptr; A.src = src;
+  A.x = (const T*)x; A.ldx = ldx; A.w = (const T*)w; A.ldw = ldw; A.C = (const T*)C;
+  return kOk;
+}
+
+}  // namespace et
+}  // namespace tmd
+
+using namespace tmd;
+
+extern "C" int tmdnet_et_message_fwd(int dtype, int n_nodes, int hidden, int heads,
+                                     const int32_t* row_ptr, const int32_t* src, int max_pairs,
+                                     const void* q, int ld_q, const void* k, int ld_k, const void* v,
+                                     int ld_v, const void* vec_in, const void* pk, int ld_pk,
+                                     const void* pv, int ld_pv, const void* cutoff, const void* unit,
+                                     void* x_out, void* vec_out, const int32_t* order, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == TMDNET_F32)
+    return et::fwd<float>(n_nodes, hidden, heads, row_ptr, src, max_pairs, q, ld_q, k, ld_k, v, ld_v,
+                          vec_in, pk, ld_pk, pv, ld_pv, cutoff, unit, x_out, vec_out, order, st);
+  if (dtype == TMDNET_F64)
+    return et::fwd<double>(n_nodes, hidden, heads, row_ptr, src, max_pairs, q, ld_q, k, ld_k, v, ld_v,
+                           vec_in, pk, ld_pk, pv, ld_pv, cutoff, unit, x_out, vec_out, order, st);
+  return kUnsupported;
+}
+
+extern "C" int tmdnet_et_message_bwd(int dtype, int n_nodes, int hidden, int heads,
+                                     const int32_t* row_ptr, const int32_t* src, int max_pairs,
+                                     const void* q, int ld_q, const void* k, int ld_k, const void* v,
+                                     int ld_v, const void* vec_in, const void* pk, int ld_pk,
+                                     const void* pv, int ld_pv, const void* cutoff, const void* unit,
+                                     const void* grad_x, const void* grad_vec, void* gq, void* gk,
+                                     void* gv, void* gvec_in, void* gpk, void* gpv, void* gcut,
+                                     void* gunit, const int32_t* order, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == TMDNET_F32)
+    return et::bwd<float>(n_nodes, hidden, heads, row_ptr, src, max_pairs, q, ld_q, k, ld_k, v, ld_v,
+                          vec_in, pk, ld_pk, pv, ld_pv, cutoff, unit, grad_x, grad_vec, gq, gk, gv,
+                          gvec_in, gpk, gpv, gcut, gunit, order, st);
+  if (dtype == TMDNET_F64)
+    return et::bwd<double>(n_nodes, hidden, heads, row_ptr, src, max_pairs, q, ld_q, k, ld_k, v, ld_v,
+                           vec_in, pk, ld_pk, pv, ld_pv, cutoff, unit, grad_x, grad_vec, gq, gk, gv,
+                           gvec_in, gpk, gpv, gcut, gunit, order, st);
+  return kUnsupported;
+}
+
+template <typename T>
+static int nb_fwd_t(int n, int H, const int32_t* row_ptr, const int32_t* src, int cap, const void* x,
+                    int ldx, const void* w, int ldw, const void* C, void* out, hipStream_t st) {
+  et::NbArgs<T> A;
+  int V;
+  int rc = et::nb_setup<T>(A, n, H, row_ptr, src, cap, x, ldx, w, ldw, C, V);
+  if (rc) return rc;
+  A.out = (T*)out;
+  return et::launch_v<T, et::KNbFwd>(V, n, A, st);
+}
+
+template <typename T>
+static int nb_bwd_t(int n, int H, const int32_t* row_ptr, const int32_t* src, int cap, const void* x,
+                    int ldx, const void* w, int ldw, const void* C, const void* gout, void* gx,
+                    void* gw, void* gC, hipStream_t st) {
+  et::NbArgs<T> A;
+  int V;
+  int rc = et::nb_setup<T>(A, n, H, row_ptr, src, cap, x, ldx, w, ldw, C, V);
+  if (rc) return rc;
+  A.gout = (const T*)gout;
+  A.gx = (T*)gx; A.gw = (T*)gw; A.gC = (T*)gC;
+  rc = et::launch_v<T, et::KNbDst>(V, n, A, st);
+  if (rc) return rc;
+  return et::launch_v<T, et::KNbSrc>(V, n, A, st);
+}
+
+extern "C" int tmdnet_nbr_embed_fwd(int dtype, int n_nodes, int hidden, const int32_t* row_ptr,
+                                    const int32_t* src, int max_pairs, const void* x, int ld_x,
+                                    const void* w, int ld_w, const void* cutoff, void* out, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == TMDNET_F32) return nb_fwd_t<float>(n_nodes, hidden, row_ptr, src, max_pairs, x, ld_x, w, ld_w, cutoff, out, st);
+  if (dtype == TMDNET_F64) return nb_fwd_t<double>(n_nodes, hidden, row_ptr, src, max_pairs, x, ld_x, w, ld_w, cutoff, out, st);
+  return kUnsupported;
+}
+
+extern "C" int tmdnet_nbr_embed_bwd(int dtype, int n_nodes, int hidden, const int32_t* row_ptr,
+                                    const int32_t* src, int max_pairs, const void* x, int ld_x,
+                                    const void* w, int ld_w, const void* cutoff, const void* grad_out,
+                                    void* gx, void* gw, void* gcut, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == TMDNET_F32) return nb_bwd_t<float>(n_nodes, hidden, row_ptr, src, max_pairs, x, ld_x, w, ld_w, cutoff, grad_out, gx, gw, gcut, st);
+  if (dtype == TMDNET_F64) return nb_bwd_t<double>(n_nodes, hidden, row_ptr, src, max_pairs, x, ld_x, w, ld_w, cutoff, grad_out, gx, gw, gcut, st);
+  return kUnsupported;
+}
+
+extern "C" const char* tmdnet_build_info(void) {
+  return "torchmd-net_amd libtmdnet_hip (gfx950, wave64 CSR edge kernels)";
+}

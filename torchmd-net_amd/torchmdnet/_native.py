@@ -1,0 +1,98 @@
+"""Loader for the C-ABI HIP library ``lib/libtmdnet_hip.so`` (declared in ``include/tmdnet.h``).
+
+The library is bound with ctypes AFTER torch is imported, so its ``libamdhip64.so.7`` dependency
+resolves to the HIP runtime torch already loaded (one runtime, one set of streams).  Every hot-path
+entry point of this package goes through here; if the library is missing or the device is not a ROCm
+GPU the call raises -- there is no CPU or eager-PyTorch fallback on the product path.
+"""
+import ctypes
+import os
+
+import torch
+
+_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libtmdnet_hip.so")
+
+F32, F64 = 0, 1
+NL_BRUTE, NL_SHARED, NL_CELL = 0, 1, 2
+RBF_EXPNORM, RBF_GAUSS = 0, 1
+
+_STATUS = {1: "bad argument", 2: "unsupported configuration", 3: "kernel launch failed",
+           4: "workspace too small"}
+
+P = ctypes.c_void_p
+I = ctypes.c_int
+D = ctypes.c_double
+SZ = ctypes.c_size_t
+
+# name -> (restype, argtypes); must match include/tmdnet.h exactly (tests check the exports)
+SIGNATURES = {
+    "tmdnet_nl_workspace_bytes": (SZ, [I, I, P, D]),
+    "tmdnet_nl_build": (I, [I, I, P, P, I, P, I, D, D, I, I, I, P, P, P, P, P, P, I, P, SZ, P]),
+    "tmdnet_nl_backward": (I, [I, I, P, P, I, P, P, P, P, P, P]),
+    "tmdnet_edge_geom_fwd": (I, [I, I, I, I, P, P, P, P, P, P, D, D, P, P, P, P]),
+    "tmdnet_edge_geom_bwd": (I, [I, I, I, I, P, P, P, P, P, P, D, D, P, P, P, P, P, P]),
+    "tmdnet_et_message_fwd": (I, [I, I, I, I, P, P, I, P, I, P, I, P, I, P, P, I, P, I, P, P, P, P, P, P]),
+    "tmdnet_et_message_bwd": (I, [I, I, I, I, P, P, I, P, I, P, I, P, I, P, P, I, P, I, P, P, P, P,
+                                  P, P, P, P, P, P, P, P, P, P]),
+    "tmdnet_nbr_embed_fwd": (I, [I, I, I, P, P, I, P, I, P, I, P, P, P]),
+    "tmdnet_nbr_embed_bwd": (I, [I, I, I, P, P, I, P, I, P, I, P, P, P, P, P, P]),
+    "tmdnet_tn_embed_fwd": (I, [I, I, I, P, P, I, D, P, P, P, I, P, P, P, P, P, P]),
+    "tmdnet_tn_embed_bwd": (I, [I, I, I, P, P, I, D, P, P, P, I, P, P, P, P, P, P, P, P, P, P, P]),
+    "tmdnet_tn_message_fwd": (I, [I, I, I, P, P, I, D, P, I, P, P, P, P, P]),
+    "tmdnet_tn_message_bwd": (I, [I, I, I, P, P, I, D, P, I, P, P, P, P, P, P, P, P, P]),
+    "tmdnet_build_info": (ctypes.c_char_p, []),
+}
+
+_lib = None
+
+
+def library_path():
+    return _LIB_PATH
+
+
+def load(required=True):
+    """Load and return the ctypes handle (raises if the library is absent and ``required``)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(_LIB_PATH):
+        if required:
+            raise RuntimeError(
+                f"torchmd-net_amd: HIP library not found at {_LIB_PATH}; run `make` (or "
+                "__graft_entry__.build()) -- there is no CPU fallback for the hot path")
+        return None
+    lib = ctypes.CDLL(_LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc, what):
+    if rc != 0:
+        raise RuntimeError(f"torchmd-net_amd: {what} failed: {_STATUS.get(rc, rc)}")
+
+
+def require_gpu(t, what):
+    if not t.is_cuda:
+        raise RuntimeError(
+            f"torchmd-net_amd: {what} runs only on a ROCm GPU (got a {t.device} tensor); this "
+            "package has no CPU implementation of the hot path")
+
+
+def dtype_code(dtype):
+    if dtype == torch.float32:
+        return F32
+    if dtype == torch.float64:
+        return F64
+    raise RuntimeError(f"torchmd-net_amd: unsupported floating type {dtype} (float32/float64)")
+
+
+def ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def stream(device=None):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)

@@ -1,0 +1,714 @@
+"""Autograd bindings of the HIP hot path (``include/tmdnet.h``).
+
+Every Function below runs its forward AND its first backward as HIP kernels of
+``libtmdnet_hip.so``.  The backward is itself a differentiable Function, so forces obtained with
+``create_graph=True`` (reference ``models/model.py:286-298``) can be differentiated again for
+force-loss training; that second-order step is expressed with composite PyTorch ops on the GPU
+(recompute + autograd), see DESIGN.md "Double backward".
+"""
+import ctypes
+import math
+
+import torch
+import torch.nn.functional as F
+from torch.autograd import Function
+
+from . import _native as nat
+
+
+# ----------------------------------------------------------------------------- neighbour graph
+class EdgeGraph:
+    """Destination-grouped CSR edge list built by ``tmdnet_nl_build``.
+
+    ``src``/``dst`` play the roles of the reference ``edge_index[0]``/``edge_index[1]``; row ``t`` of
+    the CSR (``row_ptr[t]:row_ptr[t+1]``) holds every edge whose destination is ``t``.  ``deltas``
+    (``pos[src]-pos[dst]``, minimum image) and ``distances`` carry autograd to the positions.
+    ``transpose[e]`` is the index of the reversed edge (symmetric lists only).
+    """
+
+    def __init__(self, n_nodes, row_ptr, src, dst, transpose, deltas, distances, num_pairs,
+                 symmetric):
+        self.n_nodes = n_nodes
+        self.row_ptr = row_ptr
+        self.src = src
+        self.dst = dst
+        self.transpose = transpose
+        self.deltas = deltas
+        self.distances = distances
+        self.num_pairs = num_pairs
+        self.symmetric = symmetric
+        self.cutoff = None  # per-edge CosineCutoff, filled by the model (same for every layer)
+        self._edge_index = None
+
+    @property
+    def n_edges(self):
+        return self.src.shape[0]
+
+    @property
+    def edge_index(self):
+        if self._edge_index is None:
+            self._edge_index = torch.stack([self.src, self.dst]).to(torch.long)
+        return self._edge_index
+
+    @staticmethod
+    def from_edge_index(edge_index, n_nodes):
+        """CSR view of an arbitrary (2, E) edge list.  Returns (graph, perm) with
+        ``graph`` edges = ``edge_index[:, perm]``; per-edge tensors must be permuted the same way."""
+        dev = edge_index.device
+        src = edge_index[0].to(torch.int64)
+        dst = edge_index[1].to(torch.int64)
+        key = dst * (n_nodes + 1) + src
+        perm = torch.argsort(key, stable=True)
+        src_s, dst_s = src[perm], dst[perm]
+        counts = torch.bincount(dst_s, minlength=n_nodes)
+        row_ptr = torch.zeros(n_nodes + 1, dtype=torch.int64, device=dev)
+        row_ptr[1:] = torch.cumsum(counts, 0)
+        # transpose: position of (dst, src) in the sorted key list
+        skey = key[perm]
+        rkey = src_s * (n_nodes + 1) + dst_s
+        pos = torch.searchsorted(skey, rkey).clamp(max=max(skey.numel() - 1, 0))
+        found = skey[pos] == rkey if skey.numel() else torch.zeros(0, dtype=torch.bool, device=dev)
+        tr = torch.where(found, pos, torch.full_like(pos, -1))
+        g = EdgeGraph(n_nodes, row_ptr.to(torch.int32), src_s.to(torch.int32), dst_s.to(torch.int32),
+                      tr.to(torch.int32), None, None, int(src.numel()),
+                      bool(found.all().item()) if found.numel() else True)
+        return g, perm
+
+
+def _box9(box):
+    if box is None or box.numel() == 0:
+        return None
+    vals = [float(v) for v in box.detach().cpu().reshape(-1).tolist()]
+    return (ctypes.c_double * 9)(*vals)
+
+
+_STRATEGY = {"brute": nat.NL_BRUTE, "shared": nat.NL_SHARED, "cell": nat.NL_CELL}
+
+
+def neighbor_pairs_raw(strategy, pos, batch, box, use_periodic, cutoff_lower, cutoff_upper,
+                       max_pairs, loop, include_transpose, pad_output=True, want_csr=False):
+    """Launch ``tmdnet_nl_build``.  Returns (neighbors, deltas, distances, num_pairs, row_ptr, T)."""
+    lib = nat.load()
+    nat.require_gpu(pos, "get_neighbor_pairs")
+    if strategy not in _STRATEGY:
+        raise RuntimeError("Unknown kernel name")
+    if pos.dim() != 2 or pos.shape[1] != 3:
+        raise RuntimeError('Expected "positions" to have two dimensions with size 3')
+    if pos.shape[0] == 0:
+        raise RuntimeError('Expected the 1nd dimension size of "positions" to be more than 0')
+    if not pos.is_contiguous():
+        raise RuntimeError('Expected "positions" to be contiguous')
+    if batch.dim() != 1 or batch.shape[0] != pos.shape[0] or batch.dtype != torch.int64 \
+            or not batch.is_contiguous():
+        raise RuntimeError('Expected "batch" to be a contiguous int64 vector matching "positions"')
+    if int(max_pairs) <= 0:
+        raise RuntimeError('Expected "max_num_neighbors" to be positive')
+    if not float(cutoff_upper) > 0:
+        raise RuntimeError('Expected "cutoff" to be positive')
+    n = pos.shape[0]
+    cap = int(max_pairs)
+    dev = pos.device
+    st = _STRATEGY[strategy]
+    box9 = _box9(box) if (use_periodic or st == nat.NL_CELL) else None
+    if st == nat.NL_CELL:
+        if box9 is None:
+            raise RuntimeError('Expected "box_size" to have shape (3, 3)')
+        b = list(box9)
+        if any(b[i] != 0 for i in (1, 2, 3, 5, 6, 7)):
+            raise RuntimeError('Expected "box_size" to be diagonal')
+    ws_bytes = lib.tmdnet_nl_workspace_bytes(n, st, box9, float(cutoff_upper))
+    ws = torch.empty(max(int(ws_bytes), 16), dtype=torch.uint8, device=dev)
+    nb = torch.empty((2, cap), dtype=torch.int32, device=dev)
+    dl = torch.empty((cap, 3), dtype=pos.dtype, device=dev)
+    dist = torch.empty((cap,), dtype=pos.dtype, device=dev)
+    num = torch.empty((1,), dtype=torch.int32, device=dev)
+    row_ptr = torch.empty((n + 1,), dtype=torch.int32, device=dev) if want_csr else None
+    tr = torch.empty((cap,), dtype=torch.int32, device=dev) if (want_csr and include_transpose) else None
+    rc = lib.tmdnet_nl_build(nat.dtype_code(pos.dtype), st, nat.ptr(pos), nat.ptr(batch), n, box9,
+                             int(bool(use_periodic)), float(cutoff_lower), float(cutoff_upper), cap,
+                             int(bool(loop)), int(bool(include_transpose)), nat.ptr(nb), nat.ptr(dl),
+                             nat.ptr(dist), nat.ptr(num), nat.ptr(row_ptr), nat.ptr(tr),
+                             int(bool(pad_output)), nat.ptr(ws), int(ws.numel()), nat.stream(dev))
+    nat.check(rc, "tmdnet_nl_build")
+    return nb, dl, dist, num, row_ptr, tr
+
+
+def validate_box(box, cutoff_upper):
+    """Reference box checks (neighbors_cpu.cpp:35-56)."""
+    if box.dim() != 2 or box.shape != (3, 3):
+        raise RuntimeError('Expected "box_vectors" to have shape (3, 3)')
+    v = box.detach().cpu().double().tolist()
+    c = float(cutoff_upper)
+    checks = [(v[0][1] == 0, "box_vectors[0][1] != 0"), (v[0][2] == 0, "box_vectors[0][2] != 0"),
+              (v[1][2] == 0, "box_vectors[1][2] != 0"), (v[0][0] >= 2 * c, "box_vectors[0][0] < 2*cutoff"),
+              (v[1][1] >= 2 * c, "box_vectors[1][1] < 2*cutoff"), (v[2][2] >= 2 * c, "box_vectors[2][2] < 2*cutoff"),
+              (v[0][0] >= 2 * v[1][0], "box_vectors[0][0] < 2*box_vectors[1][0]"),
+              (v[0][0] >= 2 * v[2][0], "box_vectors[0][0] < 2*box_vectors[1][0]"),
+              (v[1][1] >= 2 * v[2][1], "box_vectors[1][1] < 2*box_vectors[2][1]")]
+    for ok, msg in checks:
+        if not ok:
+            raise RuntimeError("Invalid box vectors: " + msg)
+
+
+class _NeighborGeom(Function):
+    """(pos) -> (deltas, distances) of a prebuilt graph; backward = tmdnet_nl_backward."""
+
+    @staticmethod
+    def forward(ctx, pos, graph, deltas, distances):
+        ctx.graph = graph
+        ctx.save_for_backward(pos, deltas, distances)
+        return deltas, distances
+
+    @staticmethod
+    def backward(ctx, g_deltas, g_dist):
+        pos, deltas, distances = ctx.saved_tensors
+        gpos = _NeighborGeomBwd.apply(pos, g_deltas, g_dist, deltas, distances, ctx.graph)
+        return gpos, None, None, None
+
+
+class _NeighborGeomBwd(Function):
+    @staticmethod
+    def forward(ctx, pos, g_deltas, g_dist, deltas, distances, graph):
+        lib = nat.load()
+        n = pos.shape[0]
+        gpos = torch.empty_like(pos)
+        gd = None if g_deltas is None else g_deltas.contiguous()
+        gr = None if g_dist is None else g_dist.contiguous()
+        rc = lib.tmdnet_nl_backward(nat.dtype_code(pos.dtype), n, nat.ptr(graph.row_ptr),
+                                    nat.ptr(graph.transpose), graph.n_edges, nat.ptr(gd), nat.ptr(gr),
+                                    nat.ptr(deltas), nat.ptr(distances), nat.ptr(gpos),
+                                    nat.stream(pos.device))
+        nat.check(rc, "tmdnet_nl_backward")
+        ctx.graph = graph
+        ctx.save_for_backward(pos, gd, gr, deltas, distances)
+        return gpos
+
+    @staticmethod
+    def backward(ctx, ggpos):
+        pos, gd, gr, deltas, distances = ctx.saved_tensors
+        graph = ctx.graph
+        src, dst = graph.src.long(), graph.dst.long()
+        with torch.enable_grad():
+            p = pos.detach().requires_grad_(True)
+            gd_ = (torch.zeros_like(deltas) if gd is None else gd.detach()).requires_grad_(True)
+            gr_ = (torch.zeros_like(distances) if gr is None else gr.detach()).requires_grad_(True)
+            shift = (deltas - (pos[src] - pos[dst])).detach()
+            dl = p[src] - p[dst] + shift
+            zero = (distances == 0).unsqueeze(1)
+            r = torch.where(zero.squeeze(1), torch.ones_like(distances), (dl * dl).sum(1).sqrt())
+            g = torch.where(zero, torch.zeros_like(dl), gd_ + dl / r.unsqueeze(1) * gr_.unsqueeze(1))
+            out = torch.zeros_like(p).index_add(0, src, g).index_add(0, dst, -g)
+            grads = torch.autograd.grad(out, (p, gd_, gr_), ggpos, create_graph=True, allow_unused=True)
+        return grads[0], (grads[1] if gd is not None else None), (grads[2] if gr is not None else None), \
+            None, None, None
+
+
+def build_graph(pos, batch, cutoff_lower, cutoff_upper, max_num_pairs, loop=True, strategy="brute",
+                box=None, check_errors=True):
+    """Symmetric (include_transpose) neighbour graph with CSR rows, transpose map and autograd
+    deltas/distances.  Mirrors OptimizedDistance(return_vecs=True, resize_to_fit=True) semantics
+    (reference models/utils.py:207-269): one host sync reads num_pairs for the overflow check."""
+    use_periodic = box is not None and box.numel() > 0
+    if use_periodic:
+        validate_box(box, cutoff_upper)
+    if strategy == "cell" and not use_periodic:
+        lbox = float(cutoff_upper) * 3.0
+        box = torch.tensor([[lbox, 0, 0], [0, lbox, 0], [0, 0, lbox]], dtype=torch.float64)
+    if strategy == "brute" and pos.shape[0] >= 32768:
+        strategy = "shared"
+    nb, dl, dist, num, row_ptr, tr = neighbor_pairs_raw(
+        strategy, pos, batch, box, use_periodic, cutoff_lower, cutoff_upper, max_num_pairs, loop,
+        True, pad_output=False, want_csr=True)
+    num_pairs = int(num.item())
+    cap = int(max_num_pairs)
+    if check_errors and num_pairs > cap:
+        raise RuntimeError("Found num_pairs({}) > max_num_pairs({})".format(num_pairs, cap))
+    E = min(num_pairs, cap)
+    graph = EdgeGraph(pos.shape[0], row_ptr, nb[0, :E], nb[1, :E], tr[:E], None, None, num_pairs,
+                      symmetric=num_pairs <= cap)
+    deltas, distances = _NeighborGeom.apply(pos, graph, dl[:E], dist[:E])
+    graph.deltas = deltas
+    graph.distances = distances
+    return graph
+
+
+# ----------------------------------------------------------------------------- edge geometry
+def _cosine_cutoff_torch(r, cl, cu):
+    if cl > 0:
+        c = 0.5 * (torch.cos(math.pi * (2 * (r - cl) / (cu - cl) + 1.0)) + 1.0)
+        return c * (r < cu) * (r > cl)
+    return 0.5 * (torch.cos(r * math.pi / cu) + 1.0) * (r < cu)
+
+
+def _edge_geom_composite(deltas, dist, selfmask, mu, beta, cl, cu, rbf_type, want):
+    outs = []
+    if want[0]:
+        r = dist.unsqueeze(-1)
+        if rbf_type == nat.RBF_EXPNORM:
+            alpha = 5.0 / (cu - cl)
+            f = _cosine_cutoff_torch(r, 0.0, cu) * torch.exp(-beta * (torch.exp(alpha * (-r + cl)) - mu) ** 2)
+        else:
+            f = torch.exp(beta[0] * (r - mu) ** 2)
+        outs.append(f)
+    else:
+        outs.append(None)
+    outs.append(_cosine_cutoff_torch(dist, cl, cu) if want[1] else None)
+    if want[2]:
+        sq = (deltas * deltas).sum(1)
+        n = torch.where(selfmask, torch.ones_like(sq), sq).sqrt().unsqueeze(1)
+        outs.append(torch.where(selfmask.unsqueeze(1), deltas, deltas / n))
+    else:
+        outs.append(None)
+    return outs
+
+
+class _EdgeGeom(Function):
+    @staticmethod
+    def forward(ctx, deltas, dist, graph, mu, beta, cl, cu, rbf_type, want):
+        lib = nat.load()
+        E = dist.shape[0]
+        R = mu.shape[0]
+        f = torch.empty((E, R), dtype=dist.dtype, device=dist.device) if want[0] else None
+        C = torch.empty((E,), dtype=dist.dtype, device=dist.device) if want[1] else None
+        u = torch.empty((E, 3), dtype=dist.dtype, device=dist.device) if want[2] else None
+        rc = lib.tmdnet_edge_geom_fwd(nat.dtype_code(dist.dtype), E, R, rbf_type, nat.ptr(graph.src),
+                                      nat.ptr(graph.dst), nat.ptr(deltas), nat.ptr(dist), nat.ptr(mu),
+                                      nat.ptr(beta), float(cl), float(cu), nat.ptr(f), nat.ptr(C),
+                                      nat.ptr(u), nat.stream(dist.device))
+        nat.check(rc, "tmdnet_edge_geom_fwd")
+        ctx.graph = graph
+        ctx.cfg = (cl, cu, rbf_type, want)
+        ctx.save_for_backward(deltas, dist, mu, beta)
+        return f, C, u
+
+    @staticmethod
+    def backward(ctx, gf, gC, gu):
+        deltas, dist, mu, beta = ctx.saved_tensors
+        cl, cu, rbf_type, want = ctx.cfg
+        g_dl, g_r = _EdgeGeomBwd.apply(deltas, dist, gf, gC, gu, ctx.graph, mu, beta, cl, cu, rbf_type)
+        return g_dl, g_r, None, None, None, None, None, None, None
+
+
+class _EdgeGeomBwd(Function):
+    @staticmethod
+    def forward(ctx, deltas, dist, gf, gC, gu, graph, mu, beta, cl, cu, rbf_type):
+        lib = nat.load()
+        E = dist.shape[0]
+        R = mu.shape[0]
+        g_r = torch.empty_like(dist)
+        g_dl = torch.empty_like(deltas)
+        gf_ = None if gf is None else gf.contiguous()
+        gC_ = None if gC is None else gC.contiguous()
+        gu_ = None if gu is None else gu.contiguous()
+        rc = lib.tmdnet_edge_geom_bwd(nat.dtype_code(dist.dtype), E, R, rbf_type, nat.ptr(graph.src),
+                                      nat.ptr(graph.dst), nat.ptr(deltas), nat.ptr(dist), nat.ptr(mu),
+                                      nat.ptr(beta), float(cl), float(cu), nat.ptr(gf_), nat.ptr(gC_),
+                                      nat.ptr(gu_), nat.ptr(g_r), nat.ptr(g_dl), nat.stream(dist.device))
+        nat.check(rc, "tmdnet_edge_geom_bwd")
+        ctx.graph = graph
+        ctx.cfg = (cl, cu, rbf_type)
+        ctx.save_for_backward(deltas, dist, gf_, gC_, gu_, mu, beta)
+        return g_dl, g_r
+
+    @staticmethod
+    def backward(ctx, gg_dl, gg_r):
+        deltas, dist, gf, gC, gu, mu, beta = ctx.saved_tensors
+        cl, cu, rbf_type = ctx.cfg
+        graph = ctx.graph
+        selfmask = graph.src == graph.dst
+        with torch.enable_grad():
+            dl = deltas.detach().requires_grad_(True)
+            r = dist.detach().requires_grad_(True)
+            ups = [None if t is None else t.detach().requires_grad_(True) for t in (gf, gC, gu)]
+            want = tuple(t is not None for t in ups)
+            outs = _edge_geom_composite(dl, r, selfmask, mu, beta, cl, cu, rbf_type, want)
+            pairs = [(o, g) for o, g in zip(outs, ups) if g is not None]
+            first = torch.autograd.grad([o for o, _ in pairs], (dl, r), [g for _, g in pairs],
+                                        create_graph=True, allow_unused=True)
+            inputs = [dl, r] + [u for u in ups if u is not None]
+            sel = [(f, g) for f, g in zip(first, (gg_dl, gg_r)) if f is not None and g is not None]
+            if not sel:
+                return (None,) * 11
+            second = torch.autograd.grad([f for f, _ in sel], inputs, [g for _, g in sel],
+                                         create_graph=True, allow_unused=True)
+        it = iter(second[2:])
+        gups = [next(it) if u is not None else None for u in ups]
+        return (second[0], second[1], gups[0], gups[1], gups[2], None, None, None, None, None, None)
+
+
+def edge_geometry(graph, mu, beta, cutoff_lower, cutoff_upper, rbf_type, want=(True, True, True)):
+    """(rbf [E,R], cutoff [E], unit vectors [E,3]) of the graph's edges, fused (one HIP kernel)."""
+    return _EdgeGeom.apply(graph.deltas, graph.distances, graph, mu.detach(), beta.detach(),
+                           float(cutoff_lower), float(cutoff_upper), rbf_type, tuple(want))
+
+
+# ----------------------------------------------------------------------------- ET message
+def _ld(t):
+    return 0 if t is None else t.stride(0)
+
+
+def _rowmajor(t):
+    """Rows may be strided (e.g. views into a fused projection) but elements must be contiguous."""
+    if t is None:
+        return None
+    if t.stride(-1) != 1:
+        t = t.contiguous()
+    return t
+
+
+def et_message_composite(q, k, v, vec, pk, pv, C, u, src, dst, n_nodes, heads):
+    """PyTorch restatement of torchmd_et.py:314-347 (used for the second-order backward only)."""
+    H = q.shape[1]
+    d = H // heads
+    qi = q.index_select(0, dst).view(-1, heads, d)
+    kj = k.index_select(0, src).view(-1, heads, d)
+    s = qi * kj
+    if pk is not None:
+        s = s * F.silu(pk).view(-1, heads, d)
+    attn = F.silu(s.sum(-1)) * C.unsqueeze(1)
+    vj = v.index_select(0, src).view(-1, heads, 3 * d)
+    if pv is not None:
+        vj = vj * F.silu(pv).view(-1, heads, 3 * d)
+    x, v1, v2 = torch.split(vj, d, dim=2)
+    xm = x * attn.unsqueeze(2)
+    vecj = vec.index_select(0, src).view(-1, 3, heads, d)
+    vm = vecj * v1.unsqueeze(1) + v2.unsqueeze(1) * u.view(-1, 3, 1, 1)
+    xo = torch.zeros((n_nodes, heads, d), dtype=q.dtype, device=q.device).index_add(0, dst, xm)
+    vo = torch.zeros((n_nodes, 3, heads, d), dtype=q.dtype, device=q.device).index_add(0, dst, vm)
+    return xo.view(n_nodes, H), vo.view(n_nodes, 3, H)
+
+
+class _ETMessage(Function):
+    @staticmethod
+    def forward(ctx, q, k, v, vec, pk, pv, C, u, graph, heads):
+        lib = nat.load()
+        N, H = q.shape
+        xo = torch.empty((N, H), dtype=q.dtype, device=q.device)
+        vo = torch.empty((N, 3, H), dtype=q.dtype, device=q.device)
+        rc = lib.tmdnet_et_message_fwd(nat.dtype_code(q.dtype), N, H, heads, nat.ptr(graph.row_ptr),
+                                       nat.ptr(graph.src), graph.n_edges, nat.ptr(q), _ld(q), nat.ptr(k),
+                                       _ld(k), nat.ptr(v), _ld(v), nat.ptr(vec), nat.ptr(pk), _ld(pk),
+                                       nat.ptr(pv), _ld(pv), nat.ptr(C), nat.ptr(u), nat.ptr(xo),
+                                       nat.ptr(vo), None, nat.stream(q.device))
+        nat.check(rc, "tmdnet_et_message_fwd")
+        ctx.graph = graph
+        ctx.heads = heads
+        ctx.save_for_backward(q, k, v, vec, pk, pv, C, u)
+        return xo, vo
+
+    @staticmethod
+    def backward(ctx, gx, gvec):
+        q, k, v, vec, pk, pv, C, u = ctx.saved_tensors
+        if gx is None:
+            gx = torch.zeros((q.shape[0], q.shape[1]), dtype=q.dtype, device=q.device)
+        if gvec is None:
+            gvec = torch.zeros((q.shape[0], 3, q.shape[1]), dtype=q.dtype, device=q.device)
+        outs = _ETMessageBwd.apply(gx.contiguous(), gvec.contiguous(), q, k, v, vec, pk, pv, C, u,
+                                   ctx.graph, ctx.heads)
+        gq, gk, gv, gw, gpk, gpv, gC, gu = outs
+        return gq, gk, gv, gw, (gpk if pk is not None else None), (gpv if pv is not None else None), \
+            gC, gu, None, None
+
+
+class _ETMessageBwd(Function):
+    @staticmethod
+    def forward(ctx, gx, gvec, q, k, v, vec, pk, pv, C, u, graph, heads):
+        if not graph.symmetric:
+            raise RuntimeError("torchmd-net_amd: the ET backward source pass needs a symmetric edge "
+                               "list (include_transpose=True, no capacity overflow)")
+        lib = nat.load()
+        N, H = q.shape
+        E = graph.n_edges
+        o = dict(dtype=q.dtype, device=q.device)
+        gq = torch.empty((N, H), **o)
+        gk = torch.empty((N, H), **o)
+        gv = torch.empty((N, 3 * H), **o)
+        gw = torch.empty((N, 3, H), **o)
+        gpk = torch.empty((E, H), **o) if pk is not None else torch.zeros(0, **o)
+        gpv = torch.empty((E, 3 * H), **o) if pv is not None else torch.zeros(0, **o)
+        gC = torch.empty((E,), **o)
+        gu = torch.empty((E, 3), **o)
+        rc = lib.tmdnet_et_message_bwd(
+            nat.dtype_code(q.dtype), N, H, heads, nat.ptr(graph.row_ptr), nat.ptr(graph.src), E,
+            nat.ptr(q), _ld(q), nat.ptr(k), _ld(k), nat.ptr(v), _ld(v), nat.ptr(vec), nat.ptr(pk),
+            _ld(pk), nat.ptr(pv), _ld(pv), nat.ptr(C), nat.ptr(u), nat.ptr(gx), nat.ptr(gvec),
+            nat.ptr(gq), nat.ptr(gk), nat.ptr(gv), nat.ptr(gw),
+            nat.ptr(gpk) if pk is not None else None, nat.ptr(gpv) if pv is not None else None,
+            nat.ptr(gC), nat.ptr(gu), None, nat.stream(q.device))
+        nat.check(rc, "tmdnet_et_message_bwd")
+        ctx.graph = graph
+        ctx.heads = heads
+        ctx.save_for_backward(gx, gvec, q, k, v, vec, pk, pv, C, u)
+        return gq, gk, gv, gw, gpk, gpv, gC, gu
+
+    @staticmethod
+    def backward(ctx, *ggs):
+        saved = ctx.saved_tensors
+        graph = ctx.graph
+        src, dst = graph.src.long(), graph.dst.long()
+        with torch.enable_grad():
+            leaves = [None if t is None else t.detach().requires_grad_(True) for t in saved]
+            gx, gvec, q, k, v, vec, pk, pv, C, u = leaves
+            xo, vo = et_message_composite(q, k, v, vec, pk, pv, C, u, src, dst, graph.n_nodes, ctx.heads)
+            wrt = [t for t in (q, k, v, vec, pk, pv, C, u)]
+            live = [t for t in wrt if t is not None]
+            first = torch.autograd.grad((xo, vo), live, (gx, gvec), create_graph=True, allow_unused=True)
+            it = iter(first)
+            first_full = [next(it) if t is not None else None for t in wrt]
+            sel = [(f, g) for f, g in zip(first_full, ggs) if f is not None and g is not None and g.numel()]
+            ins = [t for t in leaves if t is not None]
+            if not sel:
+                return (None,) * 12
+            second = torch.autograd.grad([f for f, _ in sel], ins, [g for _, g in sel],
+                                         create_graph=True, allow_unused=True)
+        it = iter(second)
+        res = [next(it) if t is not None else None for t in leaves]
+        return tuple(res) + (None, None)
+
+
+def et_message(q, k, v, vec, pk, pv, C, u, graph, heads):
+    q, k, v, pk, pv = (_rowmajor(t) for t in (q, k, v, pk, pv))
+    return _ETMessage.apply(q, k, v, vec.contiguous(), pk, pv, C.contiguous(), u.contiguous(), graph, heads)
+
+
+# ----------------------------------------------------------------------------- neighbour embedding
+def nbr_embed_composite(x, w, C, src, dst, n_nodes):
+    keep = (src != dst).to(x.dtype).unsqueeze(1)
+    m = x.index_select(0, src) * (w * C.unsqueeze(1)) * keep
+    return torch.zeros((n_nodes, x.shape[1]), dtype=x.dtype, device=x.device).index_add(0, dst, m)
+
+
+class _NbrEmbed(Function):
+    @staticmethod
+    def forward(ctx, x, w, C, graph):
+        lib = nat.load()
+        N, H = x.shape
+        out = torch.empty((N, H), dtype=x.dtype, device=x.device)
+        rc = lib.tmdnet_nbr_embed_fwd(nat.dtype_code(x.dtype), N, H, nat.ptr(graph.row_ptr),
+                                      nat.ptr(graph.src), graph.n_edges, nat.ptr(x), _ld(x), nat.ptr(w),
+                                      _ld(w), nat.ptr(C), nat.ptr(out), nat.stream(x.device))
+        nat.check(rc, "tmdnet_nbr_embed_fwd")
+        ctx.graph = graph
+        ctx.save_for_backward(x, w, C)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        x, w, C = ctx.saved_tensors
+        gx, gw, gC = _NbrEmbedBwd.apply(gout.contiguous(), x, w, C, ctx.graph)
+        return gx, gw, gC, None
+
+
+class _NbrEmbedBwd(Function):
+    @staticmethod
+    def forward(ctx, gout, x, w, C, graph):
+        if not graph.symmetric:
+            raise RuntimeError("torchmd-net_amd: neighbour-embedding backward needs a symmetric edge list")
+        lib = nat.load()
+        N, H = x.shape
+        E = graph.n_edges
+        gx = torch.empty_like(x, memory_format=torch.contiguous_format)
+        gw = torch.empty((E, H), dtype=x.dtype, device=x.device)
+        gC = torch.empty((E,), dtype=x.dtype, device=x.device)
+        rc = lib.tmdnet_nbr_embed_bwd(nat.dtype_code(x.dtype), N, H, nat.ptr(graph.row_ptr),
+                                      nat.ptr(graph.src), E, nat.ptr(x), _ld(x), nat.ptr(w), _ld(w),
+                                      nat.ptr(C), nat.ptr(gout), nat.ptr(gx), nat.ptr(gw), nat.ptr(gC),
+                                      nat.stream(x.device))
+        nat.check(rc, "tmdnet_nbr_embed_bwd")
+        ctx.graph = graph
+        ctx.save_for_backward(gout, x, w, C)
+        return gx, gw, gC
+
+    @staticmethod
+    def backward(ctx, ggx, ggw, ggC):
+        gout, x, w, C = ctx.saved_tensors
+        graph = ctx.graph
+        src, dst = graph.src.long(), graph.dst.long()
+        with torch.enable_grad():
+            leaves = [t.detach().requires_grad_(True) for t in (gout, x, w, C)]
+            go, x_, w_, C_ = leaves
+            out = nbr_embed_composite(x_, w_, C_, src, dst, graph.n_nodes)
+            first = torch.autograd.grad(out, (x_, w_, C_), go, create_graph=True)
+            sel = [(f, g) for f, g in zip(first, (ggx, ggw, ggC)) if g is not None]
+            if not sel:
+                return (None,) * 5
+            second = torch.autograd.grad([f for f, _ in sel], leaves, [g for _, g in sel],
+                                         create_graph=True, allow_unused=True)
+        return tuple(second) + (None,)
+
+
+def nbr_embed(x, w, C, graph):
+    return _NbrEmbed.apply(_rowmajor(x), _rowmajor(w), C.contiguous(), graph)
+
+
+# ----------------------------------------------------------------------------- TensorNet
+def _self0_weight(graph, like):
+    w = torch.ones(graph.n_edges, dtype=like.dtype, device=like.device)
+    m = getattr(graph, "self0_mult", 1.0)
+    if m != 1.0:
+        w = torch.where((graph.src == 0) & (graph.dst == 0), torch.full_like(w, m), w)
+    return w
+
+
+def _skew(v):
+    z = torch.zeros_like(v[:, 0])
+    return torch.stack((z, -v[:, 2], v[:, 1], v[:, 2], z, -v[:, 0], -v[:, 1], v[:, 0], z), dim=1).view(-1, 3, 3)
+
+
+def _sym(v):
+    t = v.unsqueeze(-1) * v.unsqueeze(-2)
+    eye = torch.eye(3, dtype=v.dtype, device=v.device)
+    return 0.5 * (t + t.transpose(-2, -1)) - t.diagonal(dim1=-2, dim2=-1).mean(-1)[..., None, None] * eye
+
+
+def tn_embed_composite(P, Q, W, C, u, graph):
+    """tensornet.py:295-315 in reference orientation (scatter to edge_index[0])."""
+    src, dst = graph.src.long(), graph.dst.long()
+    H = P.shape[1]
+    N = graph.n_nodes
+    wt = (_self0_weight(graph, C) * C).unsqueeze(1)
+    z = (P.index_select(0, src) + Q.index_select(0, dst)) * wt
+    W1, W2, W3 = W[:, :H], W[:, H:2 * H], W[:, 2 * H:]
+    eye = torch.eye(3, dtype=P.dtype, device=P.device)
+    zero = torch.zeros((N, H, 3, 3), dtype=P.dtype, device=P.device)
+    I = zero.index_add(0, src, (z * W1)[..., None, None] * eye)
+    A = zero.index_add(0, src, (z * W2)[..., None, None] * _skew(u)[:, None])
+    S = zero.index_add(0, src, (z * W3)[..., None, None] * _sym(u)[:, None])
+    return I, A, S
+
+
+def tn_message_composite(ea, I, A, S, graph):
+    """tensornet.py:329-332 (gather edge_index[1], scatter edge_index[0]) for the three components."""
+    src, dst = graph.src.long(), graph.dst.long()
+    N, H = I.shape[0], I.shape[1]
+    f = (ea.view(-1, H, 3) * _self0_weight(graph, ea).view(-1, 1, 1))
+    m = f[..., 0, None, None] * I.index_select(0, dst) + f[..., 1, None, None] * A.index_select(0, dst) \
+        + f[..., 2, None, None] * S.index_select(0, dst)
+    return torch.zeros((N, H, 3, 3), dtype=I.dtype, device=I.device).index_add(0, src, m)
+
+
+class _TNEmbed(Function):
+    @staticmethod
+    def forward(ctx, P, Q, W, C, u, graph):
+        lib = nat.load()
+        N, H = P.shape
+        o = dict(dtype=P.dtype, device=P.device)
+        I, A, S = (torch.empty((N, H, 3, 3), **o) for _ in range(3))
+        rc = lib.tmdnet_tn_embed_fwd(nat.dtype_code(P.dtype), N, H, nat.ptr(graph.row_ptr), nat.ptr(graph.src),
+                                     graph.n_edges, float(getattr(graph, "self0_mult", 1.0)), nat.ptr(P),
+                                     nat.ptr(Q), nat.ptr(W), _ld(W), nat.ptr(C), nat.ptr(u), nat.ptr(I),
+                                     nat.ptr(A), nat.ptr(S), nat.stream(P.device))
+        nat.check(rc, "tmdnet_tn_embed_fwd")
+        ctx.graph = graph
+        ctx.save_for_backward(P, Q, W, C, u)
+        return I, A, S
+
+    @staticmethod
+    def backward(ctx, gI, gA, gS):
+        P, Q, W, C, u = ctx.saved_tensors
+        z = lambda g: torch.zeros((P.shape[0], P.shape[1], 3, 3), dtype=P.dtype, device=P.device) if g is None else g.contiguous()
+        outs = _TNEmbedBwd.apply(z(gI), z(gA), z(gS), P, Q, W, C, u, ctx.graph)
+        return tuple(outs) + (None,)
+
+
+class _TNEmbedBwd(Function):
+    @staticmethod
+    def forward(ctx, gI, gA, gS, P, Q, W, C, u, graph):
+        if not graph.symmetric:
+            raise RuntimeError("torchmd-net_amd: TensorNet backward needs a symmetric edge list")
+        lib = nat.load()
+        N, H = P.shape
+        E = graph.n_edges
+        o = dict(dtype=P.dtype, device=P.device)
+        gP, gQ = torch.empty((N, H), **o), torch.empty((N, H), **o)
+        gW = torch.empty((E, 3 * H), **o)
+        gC, gu = torch.empty((E,), **o), torch.empty((E, 3), **o)
+        rc = lib.tmdnet_tn_embed_bwd(nat.dtype_code(P.dtype), N, H, nat.ptr(graph.row_ptr), nat.ptr(graph.src), E,
+                                     float(getattr(graph, "self0_mult", 1.0)), nat.ptr(P), nat.ptr(Q), nat.ptr(W),
+                                     _ld(W), nat.ptr(C), nat.ptr(u), nat.ptr(gI), nat.ptr(gA), nat.ptr(gS),
+                                     nat.ptr(gP), nat.ptr(gQ), nat.ptr(gW), nat.ptr(gC), nat.ptr(gu),
+                                     nat.stream(P.device))
+        nat.check(rc, "tmdnet_tn_embed_bwd")
+        ctx.graph = graph
+        ctx.save_for_backward(gI, gA, gS, P, Q, W, C, u)
+        return gP, gQ, gW, gC, gu
+
+    @staticmethod
+    def backward(ctx, *ggs):
+        saved = ctx.saved_tensors
+        with torch.enable_grad():
+            leaves = [t.detach().requires_grad_(True) for t in saved]
+            gI, gA, gS, P, Q, W, C, u = leaves
+            I, A, S = tn_embed_composite(P, Q, W, C, u, ctx.graph)
+            first = torch.autograd.grad((I, A, S), (P, Q, W, C, u), (gI, gA, gS), create_graph=True)
+            sel = [(f, g) for f, g in zip(first, ggs) if g is not None]
+            if not sel:
+                return (None,) * 9
+            second = torch.autograd.grad([f for f, _ in sel], leaves, [g for _, g in sel],
+                                         create_graph=True, allow_unused=True)
+        return tuple(second) + (None,)
+
+
+class _TNMessage(Function):
+    @staticmethod
+    def forward(ctx, ea, I, A, S, graph):
+        lib = nat.load()
+        N, H = I.shape[0], I.shape[1]
+        msg = torch.empty((N, H, 3, 3), dtype=I.dtype, device=I.device)
+        rc = lib.tmdnet_tn_message_fwd(nat.dtype_code(I.dtype), N, H, nat.ptr(graph.row_ptr), nat.ptr(graph.src),
+                                       graph.n_edges, float(getattr(graph, "self0_mult", 1.0)), nat.ptr(ea),
+                                       _ld(ea), nat.ptr(I), nat.ptr(A), nat.ptr(S), nat.ptr(msg),
+                                       nat.stream(I.device))
+        nat.check(rc, "tmdnet_tn_message_fwd")
+        ctx.graph = graph
+        ctx.save_for_backward(ea, I, A, S)
+        return msg
+
+    @staticmethod
+    def backward(ctx, gmsg):
+        ea, I, A, S = ctx.saved_tensors
+        outs = _TNMessageBwd.apply(gmsg.contiguous(), ea, I, A, S, ctx.graph)
+        return tuple(outs) + (None,)
+
+
+class _TNMessageBwd(Function):
+    @staticmethod
+    def forward(ctx, gmsg, ea, I, A, S, graph):
+        if not graph.symmetric:
+            raise RuntimeError("torchmd-net_amd: TensorNet backward needs a symmetric edge list")
+        lib = nat.load()
+        N, H = I.shape[0], I.shape[1]
+        E = graph.n_edges
+        gea = torch.empty((E, 3 * H), dtype=I.dtype, device=I.device)
+        gI, gA, gS = (torch.empty_like(I) for _ in range(3))
+        rc = lib.tmdnet_tn_message_bwd(nat.dtype_code(I.dtype), N, H, nat.ptr(graph.row_ptr), nat.ptr(graph.src), E,
+                                       float(getattr(graph, "self0_mult", 1.0)), nat.ptr(ea), _ld(ea), nat.ptr(I),
+                                       nat.ptr(A), nat.ptr(S), nat.ptr(gmsg), nat.ptr(gea), nat.ptr(gI),
+                                       nat.ptr(gA), nat.ptr(gS), nat.stream(I.device))
+        nat.check(rc, "tmdnet_tn_message_bwd")
+        ctx.graph = graph
+        ctx.save_for_backward(gmsg, ea, I, A, S)
+        return gea, gI, gA, gS
+
+    @staticmethod
+    def backward(ctx, *ggs):
+        saved = ctx.saved_tensors
+        with torch.enable_grad():
+            leaves = [t.detach().requires_grad_(True) for t in saved]
+            gmsg, ea, I, A, S = leaves
+            msg = tn_message_composite(ea, I, A, S, ctx.graph)
+            first = torch.autograd.grad(msg, (ea, I, A, S), gmsg, create_graph=True)
+            sel = [(f, g) for f, g in zip(first, ggs) if g is not None]
+            if not sel:
+                return (None,) * 6
+            second = torch.autograd.grad([f for f, _ in sel], leaves, [g for _, g in sel],
+                                         create_graph=True, allow_unused=True)
+        return tuple(second) + (None,)
+
+
+def tn_embed(P, Q, W, C, u, graph):
+    return _TNEmbed.apply(P.contiguous(), Q.contiguous(), _rowmajor(W), C.contiguous(), u.contiguous(), graph)
+
+
+def tn_message(ea, I, A, S, graph):
+    return _TNMessage.apply(_rowmajor(ea), I.contiguous(), A.contiguous(), S.contiguous(), graph)

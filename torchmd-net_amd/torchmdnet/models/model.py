@@ -1,0 +1,180 @@
+"""Model assembly (mirror of reference ``torchmdnet/models/model.py``).
+
+``create_model(args)`` accepts the reference's argument dict (examples/*.yaml keys) and builds the
+same module tree in the same order (so seeded initialisation and checkpoints match);
+``TorchMD_Net.forward`` returns (y, -dy/dpos) with forces from autograd on ``pos`` exactly as the
+reference does (model.py:232-300, ``create_graph=True`` so force losses can be trained).
+"""
+import re
+import warnings
+from typing import Dict, List, Optional, Tuple
+
+import torch
+from torch import Tensor, nn
+from torch.autograd import grad
+
+from . import output_modules
+from .utils import dtype_mapping
+from .. import priors
+
+
+def create_model(args, prior_model=None, mean=None, std=None):
+    dtype = dtype_mapping[args["precision"]]
+    if dtype not in (torch.float32, torch.float64):
+        raise NotImplementedError("torchmd-net_amd computes in float32 or float64 (precision 32/64)")
+    shared_args = dict(
+        hidden_channels=args["embedding_dimension"],
+        num_layers=args["num_layers"],
+        num_rbf=args["num_rbf"],
+        rbf_type=args["rbf_type"],
+        trainable_rbf=args["trainable_rbf"],
+        activation=args["activation"],
+        cutoff_lower=args["cutoff_lower"],
+        cutoff_upper=args["cutoff_upper"],
+        max_z=args["max_z"],
+        max_num_neighbors=args["max_num_neighbors"],
+        dtype=dtype,
+    )
+    if args["model"] == "equivariant-transformer":
+        from .torchmd_et import TorchMD_ET
+
+        is_equivariant = True
+        representation_model = TorchMD_ET(
+            attn_activation=args["attn_activation"],
+            num_heads=args["num_heads"],
+            distance_influence=args["distance_influence"],
+            neighbor_embedding=args["neighbor_embedding"],
+            **shared_args,
+        )
+    elif args["model"] == "tensornet":
+        from .tensornet import TensorNet
+
+        is_equivariant = False
+        representation_model = TensorNet(
+            equivariance_invariance_group=args["equivariance_invariance_group"],
+            **shared_args,
+        )
+    elif args["model"] in ("graph-network", "transformer"):
+        raise NotImplementedError(f'{args["model"]} is outside the MI355X hot path (ET, TensorNet)')
+    else:
+        raise ValueError(f'Unknown architecture: {args["model"]}')
+
+    if args.get("atom_filter", -1) > -1:
+        raise NotImplementedError("AtomFilter wrapper is outside the hot path")
+
+    if args.get("prior_model") and prior_model is None:
+        prior_model = create_prior_models(args)
+
+    output_prefix = "Equivariant" if is_equivariant else ""
+    output_model = getattr(output_modules, output_prefix + args["output_model"])(
+        args["embedding_dimension"],
+        activation=args["activation"],
+        reduce_op=args["reduce_op"],
+        dtype=dtype,
+    )
+    return TorchMD_Net(representation_model, output_model, prior_model=prior_model, mean=mean, std=std,
+                       derivative=args["derivative"], dtype=dtype)
+
+
+def load_model(filepath, args=None, device="cpu", **kwargs):
+    """Reference model.py:121-143.  Checkpoints are read with ``weights_only=True``."""
+    ckpt = torch.load(filepath, map_location="cpu", weights_only=True)
+    if args is None:
+        args = ckpt["hyper_parameters"]
+    for key, value in kwargs.items():
+        if key not in args:
+            warnings.warn(f"Unknown hyperparameter: {key}={value}")
+        args[key] = value
+    model = create_model(args)
+    state_dict = {re.sub(r"^model\.", "", k): v for k, v in ckpt["state_dict"].items()}
+    if "prior_model.initial_atomref" in state_dict:
+        state_dict["prior_model.0.initial_atomref"] = state_dict.pop("prior_model.initial_atomref")
+    if "prior_model.atomref.weight" in state_dict:
+        state_dict["prior_model.0.atomref.weight"] = state_dict.pop("prior_model.atomref.weight")
+    model.load_state_dict(state_dict)
+    return model.to(device)
+
+
+def create_prior_models(args, dataset=None):
+    prior_models = []
+    if args["prior_model"]:
+        prior_model = args["prior_model"]
+        prior_names, prior_args = [], []
+        if not isinstance(prior_model, list):
+            prior_model = [prior_model]
+        for prior in prior_model:
+            if isinstance(prior, dict):
+                for key, value in prior.items():
+                    prior_names.append(key)
+                    prior_args.append({} if value is None else value)
+            else:
+                prior_names.append(prior)
+                prior_args.append({})
+        if "prior_args" in args:
+            prior_args = args["prior_args"]
+            if not isinstance(prior_args, list):
+                prior_args = [prior_args]
+        for name, arg in zip(prior_names, prior_args):
+            assert hasattr(priors, name), (f"Unknown prior model {name}. "
+                                           f"Available models are {', '.join(priors.__all__)}")
+            prior_models.append(getattr(priors, name)(dataset=dataset, **arg))
+    return prior_models
+
+
+class TorchMD_Net(nn.Module):
+    """Representation model + output head + priors; forces = -d(sum y)/d pos (reference model.py:180-300)."""
+
+    def __init__(self, representation_model, output_model, prior_model=None, mean=None, std=None,
+                 derivative=False, dtype=torch.float32):
+        super().__init__()
+        self.representation_model = representation_model.to(dtype=dtype)
+        self.output_model = output_model.to(dtype=dtype)
+        if not output_model.allow_prior_model and prior_model is not None:
+            prior_model = None
+            warnings.warn("Prior model was given but the output model does not allow prior models. "
+                          "Dropping the prior model.")
+        if isinstance(prior_model, priors.base.BasePrior):
+            prior_model = [prior_model]
+        self.prior_model = None if prior_model is None else torch.nn.ModuleList(prior_model).to(dtype=dtype)
+        self.derivative = derivative
+        mean = torch.scalar_tensor(0) if mean is None else mean
+        self.register_buffer("mean", mean.to(dtype=dtype))
+        std = torch.scalar_tensor(1) if std is None else std
+        self.register_buffer("std", std.to(dtype=dtype))
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        self.representation_model.reset_parameters()
+        self.output_model.reset_parameters()
+        if self.prior_model is not None:
+            for prior in self.prior_model:
+                prior.reset_parameters()
+
+    def forward(self, z: Tensor, pos: Tensor, batch: Optional[Tensor] = None, q: Optional[Tensor] = None,
+                s: Optional[Tensor] = None, extra_args: Optional[Dict[str, Tensor]] = None
+                ) -> Tuple[Tensor, Optional[Tensor]]:
+        assert z.dim() == 1 and z.dtype == torch.long
+        batch = torch.zeros_like(z) if batch is None else batch
+        if self.derivative:
+            pos.requires_grad_(True)
+        x, v, z, pos, batch = self.representation_model(z, pos, batch, q=q, s=s)
+        x = self.output_model.pre_reduce(x, v, z, pos, batch)
+        if self.std is not None:
+            x = x * self.std
+        if self.prior_model is not None:
+            for prior in self.prior_model:
+                x = prior.pre_reduce(x, z, pos, batch, extra_args)
+        x = self.output_model.reduce(x, batch)
+        if self.mean is not None:
+            x = x + self.mean
+        y = self.output_model.post_reduce(x)
+        if self.prior_model is not None:
+            for prior in self.prior_model:
+                y = prior.post_reduce(y, z, pos, batch, extra_args)
+        if self.derivative:
+            grad_outputs: List[Optional[torch.Tensor]] = [torch.ones_like(y)]
+            dy = grad([y], [pos], grad_outputs=grad_outputs, create_graph=True, retain_graph=True)[0]
+            if dy is None:
+                raise RuntimeError("Autograd returned None for the force prediction.")
+            return y, -dy
+        return y, None

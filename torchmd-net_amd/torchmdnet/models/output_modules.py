@@ -1,0 +1,170 @@
+"""Output heads (mirror of reference ``torchmdnet/models/output_modules.py``).
+
+Node-level and tiny (H -> H/2 -> 1 per atom); they run as PyTorch GPU ops.  ``reduce`` sums atoms
+into molecules with ``index_add`` (the reference uses torch_scatter, output_modules.py:27-43).
+"""
+from abc import ABCMeta, abstractmethod
+from typing import Optional
+
+import torch
+from torch import nn
+
+from .utils import GatedEquivariantBlock, act_class_mapping, check_stream_capturing
+from ..utils import atomic_masses
+
+__all__ = ["Scalar", "DipoleMoment", "ElectronicSpatialExtent"]
+
+
+def scatter(src, index, dim=0, dim_size=None, reduce="sum"):
+    """Segment reduction over dim 0 (sum/add/mean), torch_scatter 2.1.1 semantics for this use."""
+    if dim_size is None:
+        dim_size = int(index.max().item()) + 1
+    out = torch.zeros((dim_size,) + tuple(src.shape[1:]), dtype=src.dtype, device=src.device)
+    out = out.index_add(0, index, src)
+    if reduce in ("sum", "add"):
+        return out
+    if reduce == "mean":
+        cnt = torch.zeros(dim_size, dtype=src.dtype, device=src.device).index_add(
+            0, index, torch.ones_like(index, dtype=src.dtype))
+        return out / cnt.clamp(min=1).view(-1, *([1] * (src.dim() - 1)))
+    raise NotImplementedError(f"reduce_op {reduce}")
+
+
+class OutputModel(nn.Module, metaclass=ABCMeta):
+    def __init__(self, allow_prior_model, reduce_op):
+        super().__init__()
+        self.allow_prior_model = allow_prior_model
+        self.reduce_op = reduce_op
+        self.dim_size = 0
+
+    def reset_parameters(self):
+        pass
+
+    @abstractmethod
+    def pre_reduce(self, x, v, z, pos, batch):
+        return
+
+    def reduce(self, x, batch):
+        is_capturing = x.is_cuda and check_stream_capturing()
+        if not x.is_cuda or not is_capturing:
+            self.dim_size = int(batch.max().item() + 1)
+        if is_capturing:
+            assert self.dim_size > 0, "Warming up is needed before capturing the model into a CUDA graph"
+        return scatter(x, batch, dim=0, dim_size=self.dim_size, reduce=self.reduce_op)
+
+    def post_reduce(self, x):
+        return x
+
+
+class Scalar(OutputModel):
+    def __init__(self, hidden_channels, activation="silu", allow_prior_model=True, reduce_op="sum",
+                 dtype=torch.float):
+        super().__init__(allow_prior_model=allow_prior_model, reduce_op=reduce_op)
+        act_class = act_class_mapping[activation]
+        self.output_network = nn.Sequential(
+            nn.Linear(hidden_channels, hidden_channels // 2, dtype=dtype),
+            act_class(),
+            nn.Linear(hidden_channels // 2, 1, dtype=dtype),
+        )
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        nn.init.xavier_uniform_(self.output_network[0].weight)
+        self.output_network[0].bias.data.fill_(0)
+        nn.init.xavier_uniform_(self.output_network[2].weight)
+        self.output_network[2].bias.data.fill_(0)
+
+    def pre_reduce(self, x, v: Optional[torch.Tensor], z, pos, batch):
+        return self.output_network(x)
+
+
+class EquivariantScalar(OutputModel):
+    def __init__(self, hidden_channels, activation="silu", allow_prior_model=True, reduce_op="sum",
+                 dtype=torch.float):
+        super().__init__(allow_prior_model=allow_prior_model, reduce_op=reduce_op)
+        self.output_network = nn.ModuleList([
+            GatedEquivariantBlock(hidden_channels, hidden_channels // 2, activation=activation,
+                                  scalar_activation=True, dtype=dtype),
+            GatedEquivariantBlock(hidden_channels // 2, 1, activation=activation, dtype=dtype),
+        ])
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        for layer in self.output_network:
+            layer.reset_parameters()
+
+    def pre_reduce(self, x, v, z, pos, batch):
+        for layer in self.output_network:
+            x, v = layer(x, v)
+        return x + v.sum() * 0
+
+
+class DipoleMoment(Scalar):
+    def __init__(self, hidden_channels, activation="silu", reduce_op="sum", dtype=torch.float):
+        super().__init__(hidden_channels, activation, allow_prior_model=False, reduce_op=reduce_op, dtype=dtype)
+        self.register_buffer("atomic_mass", torch.from_numpy(atomic_masses).to(dtype))
+
+    def pre_reduce(self, x, v: Optional[torch.Tensor], z, pos, batch):
+        x = self.output_network(x)
+        mass = self.atomic_mass[z].view(-1, 1)
+        c = scatter(mass * pos, batch, dim=0) / scatter(mass, batch, dim=0)
+        return x * (pos - c[batch])
+
+    def post_reduce(self, x):
+        return torch.norm(x, dim=-1, keepdim=True)
+
+
+class EquivariantDipoleMoment(EquivariantScalar):
+    def __init__(self, hidden_channels, activation="silu", reduce_op="sum", dtype=torch.float):
+        super().__init__(hidden_channels, activation, allow_prior_model=False, reduce_op=reduce_op, dtype=dtype)
+        self.register_buffer("atomic_mass", torch.from_numpy(atomic_masses).to(dtype))
+
+    def pre_reduce(self, x, v, z, pos, batch):
+        for layer in self.output_network:
+            x, v = layer(x, v)
+        mass = self.atomic_mass[z].view(-1, 1)
+        c = scatter(mass * pos, batch, dim=0) / scatter(mass, batch, dim=0)
+        x = x * (pos - c[batch])
+        return x + v.squeeze()
+
+    def post_reduce(self, x):
+        return torch.norm(x, dim=-1, keepdim=True)
+
+
+class ElectronicSpatialExtent(OutputModel):
+    def __init__(self, hidden_channels, activation="silu", reduce_op="sum", dtype=torch.float):
+        super().__init__(allow_prior_model=False, reduce_op=reduce_op)
+        act_class = act_class_mapping[activation]
+        self.output_network = nn.Sequential(
+            nn.Linear(hidden_channels, hidden_channels // 2, dtype=dtype),
+            act_class(),
+            nn.Linear(hidden_channels // 2, 1, dtype=dtype),
+        )
+        self.register_buffer("atomic_mass", torch.from_numpy(atomic_masses).to(dtype))
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        nn.init.xavier_uniform_(self.output_network[0].weight)
+        self.output_network[0].bias.data.fill_(0)
+        nn.init.xavier_uniform_(self.output_network[2].weight)
+        self.output_network[2].bias.data.fill_(0)
+
+    def pre_reduce(self, x, v: Optional[torch.Tensor], z, pos, batch):
+        x = self.output_network(x)
+        mass = self.atomic_mass[z].view(-1, 1)
+        c = scatter(mass * pos, batch, dim=0) / scatter(mass, batch, dim=0)
+        return torch.norm(pos - c[batch], dim=1, keepdim=True) ** 2 * x
+
+
+class EquivariantElectronicSpatialExtent(ElectronicSpatialExtent):
+    pass
+
+
+class EquivariantVectorOutput(EquivariantScalar):
+    def __init__(self, hidden_channels, activation="silu", reduce_op="sum", dtype=torch.float):
+        super().__init__(hidden_channels, activation, allow_prior_model=False, reduce_op="sum", dtype=dtype)
+
+    def pre_reduce(self, x, v, z, pos, batch):
+        for layer in self.output_network:
+            x, v = layer(x, v)
+        return v.squeeze()

@@ -1,0 +1,233 @@
+"""TensorNet (mirror of reference ``torchmdnet/models/tensornet.py``; Simeon & De Fabritiis 2023).
+
+Module tree, parameter names and initialisation order follow the reference (tensornet.py:70-410).
+Edge work runs in HIP kernels (``tmdnet_tn_embed_*``, ``tmdnet_tn_message_*``): the per-edge
+``emb2(cat(Z_i, Z_j))`` of TensorEmbedding is split into two per-node GEMM halves and the
+scatter over ``edge_index[0]`` becomes a CSR walk of the reversed rows (no atomics).
+``static_shapes=True`` (the reference default) reproduces the reference CUDA semantics: padded
+neighbour slots become extra (0, 0) edges with r = 0 (tensornet.py:215-221), applied here as a
+multiplicity on atom 0's self loop.
+"""
+from typing import Optional, Tuple
+
+import torch
+from torch import Tensor, nn
+
+from .. import kernels
+from .utils import CosineCutoff, OptimizedDistance, act_class_mapping, as_graph, rbf_class_mapping
+
+# reference tensornet.py:13-14 sets TF32 matmul globally; gfx950 has no TF32/xf32 path, so fp32
+# GEMMs stay exact fp32 here.
+
+
+def vector_to_skewtensor(vector):
+    return kernels._skew(vector).squeeze(0)
+
+
+def vector_to_symtensor(vector):
+    return kernels._sym(vector)
+
+
+def decompose_tensor(tensor):
+    I = (tensor.diagonal(offset=0, dim1=-1, dim2=-2)).mean(-1)[..., None, None] * torch.eye(
+        3, 3, device=tensor.device, dtype=tensor.dtype)
+    A = 0.5 * (tensor - tensor.transpose(-2, -1))
+    S = 0.5 * (tensor + tensor.transpose(-2, -1)) - I
+    return I, A, S
+
+
+def new_radial_tensor(I, A, S, f_I, f_A, f_S):
+    return f_I[..., None, None] * I, f_A[..., None, None] * A, f_S[..., None, None] * S
+
+
+def tensor_norm(tensor):
+    return (tensor ** 2).sum((-2, -1))
+
+
+class TensorNet(nn.Module):
+    def __init__(self, hidden_channels=128, num_layers=2, num_rbf=32, rbf_type="expnorm",
+                 trainable_rbf=False, activation="silu", cutoff_lower=0, cutoff_upper=4.5,
+                 max_num_neighbors=64, max_z=128, equivariance_invariance_group="O(3)",
+                 static_shapes=True, dtype=torch.float32):
+        super().__init__()
+        assert rbf_type in rbf_class_mapping, (
+            f'Unknown RBF type "{rbf_type}". Choose from {", ".join(rbf_class_mapping.keys())}.')
+        assert activation in act_class_mapping, (
+            f'Unknown activation function "{activation}". Choose from {", ".join(act_class_mapping.keys())}.')
+        assert equivariance_invariance_group in ["O(3)", "SO(3)"], (
+            f'Unknown group "{equivariance_invariance_group}". Choose O(3) or SO(3).')
+        self.hidden_channels = hidden_channels
+        self.equivariance_invariance_group = equivariance_invariance_group
+        self.num_layers = num_layers
+        self.num_rbf = num_rbf
+        self.rbf_type = rbf_type
+        self.activation = activation
+        self.cutoff_lower = cutoff_lower
+        self.cutoff_upper = cutoff_upper
+        self.trainable_rbf = trainable_rbf
+        act_class = act_class_mapping[activation]
+        self.distance_expansion = rbf_class_mapping[rbf_type](cutoff_lower, cutoff_upper, num_rbf, trainable_rbf)
+        self.tensor_embedding = TensorEmbedding(hidden_channels, num_rbf, act_class, cutoff_lower,
+                                                cutoff_upper, trainable_rbf, max_z, dtype)
+        self.layers = nn.ModuleList()
+        if num_layers != 0:
+            for _ in range(num_layers):
+                self.layers.append(Interaction(num_rbf, hidden_channels, act_class, cutoff_lower, cutoff_upper,
+                                               equivariance_invariance_group, dtype))
+        self.linear = nn.Linear(3 * hidden_channels, hidden_channels, dtype=dtype)
+        self.out_norm = nn.LayerNorm(3 * hidden_channels, dtype=dtype)
+        self.act = act_class()
+        self.static_shapes = static_shapes
+        self.distance = OptimizedDistance(cutoff_lower, cutoff_upper, max_num_pairs=-max_num_neighbors,
+                                          return_vecs=True, loop=True, check_errors=False,
+                                          resize_to_fit=not self.static_shapes, long_edge_index=True)
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        self.tensor_embedding.reset_parameters()
+        for layer in self.layers:
+            layer.reset_parameters()
+        self.linear.reset_parameters()
+        self.out_norm.reset_parameters()
+
+    def forward(self, z: Tensor, pos: Tensor, batch: Tensor, q: Optional[Tensor] = None,
+                s: Optional[Tensor] = None) -> Tuple[Tensor, Optional[Tensor], Tensor, Tensor, Tensor]:
+        graph = self.distance.graph(pos, batch)
+        cap = self.distance._max_pairs(pos.shape[0])
+        graph.self0_mult = float(1 + max(0, cap - graph.num_pairs)) if self.static_shapes else 1.0
+        de = self.distance_expansion
+        if self.trainable_rbf and torch.is_grad_enabled():
+            edge_attr = de(graph.distances)
+            _, C, edge_vec = kernels.edge_geometry(graph, *de.kernel_params(), self.cutoff_lower,
+                                                   self.cutoff_upper, de.rbf_type, want=(False, True, True))
+        else:
+            edge_attr, C, edge_vec = kernels.edge_geometry(graph, *de.kernel_params(), self.cutoff_lower,
+                                                           self.cutoff_upper, de.rbf_type)
+        graph.cutoff = C
+        X = self.tensor_embedding(z, graph, graph.distances, edge_vec, edge_attr)
+        for layer in self.layers:
+            X = layer(X, graph, graph.distances, edge_attr)
+        I, A, S = decompose_tensor(X)
+        x = torch.cat((tensor_norm(I), tensor_norm(A), tensor_norm(S)), dim=-1)
+        x = self.out_norm(x)
+        x = self.act(self.linear(x))
+        return x, None, z, pos, batch
+
+
+def _check_symmetric_graph(edge_index, n):
+    graph, perm = as_graph(edge_index, n)
+    return graph, perm
+
+
+class TensorEmbedding(nn.Module):
+    def __init__(self, hidden_channels, num_rbf, activation, cutoff_lower, cutoff_upper, trainable_rbf=False,
+                 max_z=128, dtype=torch.float32):
+        super().__init__()
+        self.hidden_channels = hidden_channels
+        self.distance_proj1 = nn.Linear(num_rbf, hidden_channels, dtype=dtype)
+        self.distance_proj2 = nn.Linear(num_rbf, hidden_channels, dtype=dtype)
+        self.distance_proj3 = nn.Linear(num_rbf, hidden_channels, dtype=dtype)
+        self.cutoff = CosineCutoff(cutoff_lower, cutoff_upper)
+        self.max_z = max_z
+        self.emb = nn.Embedding(max_z, hidden_channels, dtype=dtype)
+        self.emb2 = nn.Linear(2 * hidden_channels, hidden_channels, dtype=dtype)
+        self.act = activation()
+        self.linears_tensor = nn.ModuleList()
+        for _ in range(3):
+            self.linears_tensor.append(nn.Linear(hidden_channels, hidden_channels, bias=False))
+        self.linears_scalar = nn.ModuleList()
+        self.linears_scalar.append(nn.Linear(hidden_channels, 2 * hidden_channels, bias=True, dtype=dtype))
+        self.linears_scalar.append(nn.Linear(2 * hidden_channels, 3 * hidden_channels, bias=True, dtype=dtype))
+        self.init_norm = nn.LayerNorm(hidden_channels, dtype=dtype)
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        self.distance_proj1.reset_parameters()
+        self.distance_proj2.reset_parameters()
+        self.distance_proj3.reset_parameters()
+        self.emb.reset_parameters()
+        self.emb2.reset_parameters()
+        for linear in self.linears_tensor:
+            linear.reset_parameters()
+        for linear in self.linears_scalar:
+            linear.reset_parameters()
+        self.init_norm.reset_parameters()
+
+    def forward(self, z: Tensor, edge_index, edge_weight: Tensor, edge_vec_norm: Tensor,
+                edge_attr: Tensor) -> Tensor:
+        graph, perm = _check_symmetric_graph(edge_index, z.shape[0])
+        if perm is not None:
+            edge_weight, edge_vec_norm, edge_attr = edge_weight[perm], edge_vec_norm[perm], edge_attr[perm]
+        C = graph.cutoff if (perm is None and graph.cutoff is not None) else self.cutoff(edge_weight)
+        H = self.hidden_channels
+        W = torch.nn.functional.linear(
+            edge_attr, torch.cat([self.distance_proj1.weight, self.distance_proj2.weight, self.distance_proj3.weight]),
+            torch.cat([self.distance_proj1.bias, self.distance_proj2.bias, self.distance_proj3.bias]))
+        Z = self.emb(z)
+        P = torch.nn.functional.linear(Z, self.emb2.weight[:, :H], self.emb2.bias)
+        Q = torch.nn.functional.linear(Z, self.emb2.weight[:, H:])
+        I, A, S = kernels.tn_embed(P, Q, W, C, edge_vec_norm, graph)
+        norm = self.init_norm(tensor_norm(I + A + S))
+        I = self.linears_tensor[0](I.permute(0, 2, 3, 1)).permute(0, 3, 1, 2)
+        A = self.linears_tensor[1](A.permute(0, 2, 3, 1)).permute(0, 3, 1, 2)
+        S = self.linears_tensor[2](S.permute(0, 2, 3, 1)).permute(0, 3, 1, 2)
+        for linear_scalar in self.linears_scalar:
+            norm = self.act(linear_scalar(norm))
+        norm = norm.reshape(norm.shape[0], self.hidden_channels, 3)
+        I, A, S = new_radial_tensor(I, A, S, norm[..., 0], norm[..., 1], norm[..., 2])
+        return I + A + S
+
+
+class Interaction(nn.Module):
+    def __init__(self, num_rbf, hidden_channels, activation, cutoff_lower, cutoff_upper,
+                 equivariance_invariance_group, dtype=torch.float32):
+        super().__init__()
+        self.num_rbf = num_rbf
+        self.hidden_channels = hidden_channels
+        self.cutoff = CosineCutoff(cutoff_lower, cutoff_upper)
+        self.linears_scalar = nn.ModuleList()
+        self.linears_scalar.append(nn.Linear(num_rbf, hidden_channels, bias=True, dtype=dtype))
+        self.linears_scalar.append(nn.Linear(hidden_channels, 2 * hidden_channels, bias=True, dtype=dtype))
+        self.linears_scalar.append(nn.Linear(2 * hidden_channels, 3 * hidden_channels, bias=True, dtype=dtype))
+        self.linears_tensor = nn.ModuleList()
+        for _ in range(6):
+            self.linears_tensor.append(nn.Linear(hidden_channels, hidden_channels, bias=False))
+        self.act = activation()
+        self.equivariance_invariance_group = equivariance_invariance_group
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        for linear in self.linears_scalar:
+            linear.reset_parameters()
+        for linear in self.linears_tensor:
+            linear.reset_parameters()
+
+    def forward(self, X: Tensor, edge_index, edge_weight: Tensor, edge_attr: Tensor) -> Tensor:
+        graph, perm = _check_symmetric_graph(edge_index, X.shape[0])
+        if perm is not None:
+            edge_weight, edge_attr = edge_weight[perm], edge_attr[perm]
+        C = graph.cutoff if (perm is None and graph.cutoff is not None) else self.cutoff(edge_weight)
+        for linear_scalar in self.linears_scalar:
+            edge_attr = self.act(linear_scalar(edge_attr))
+        edge_attr = edge_attr * C.view(-1, 1)
+        X = X / (tensor_norm(X) + 1)[..., None, None]
+        I, A, S = decompose_tensor(X)
+        I = self.linears_tensor[0](I.permute(0, 2, 3, 1)).permute(0, 3, 1, 2)
+        A = self.linears_tensor[1](A.permute(0, 2, 3, 1)).permute(0, 3, 1, 2)
+        S = self.linears_tensor[2](S.permute(0, 2, 3, 1)).permute(0, 3, 1, 2)
+        Y = I + A + S
+        msg = kernels.tn_message(edge_attr, I, A, S, graph)
+        if self.equivariance_invariance_group == "O(3)":
+            A = torch.matmul(msg, Y)
+            B = torch.matmul(Y, msg)
+            I, A, S = decompose_tensor(A + B)
+        if self.equivariance_invariance_group == "SO(3)":
+            B = torch.matmul(Y, msg)
+            I, A, S = decompose_tensor(2 * B)
+        normp1 = (tensor_norm(I + A + S) + 1)[..., None, None]
+        I, A, S = I / normp1, A / normp1, S / normp1
+        I = self.linears_tensor[3](I.permute(0, 2, 3, 1)).permute(0, 3, 1, 2)
+        A = self.linears_tensor[4](A.permute(0, 2, 3, 1)).permute(0, 3, 1, 2)
+        S = self.linears_tensor[5](S.permute(0, 2, 3, 1)).permute(0, 3, 1, 2)
+        dX = I + A + S
+        return X + dX + torch.matrix_power(dX, 2)
