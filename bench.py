@@ -1,0 +1,277 @@
+#!/usr/bin/env python
+"""Benchmark: ET-QM9 (128 channels, 8 layers, 64 RBF, cutoff 5) energy + forces, molecules/s.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--mode infer|train]
+  (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
+
+One step = TorchMD_Net.forward with derivative=True (y and -dy/dpos, create_graph=True exactly as
+reference models/model.py:286-298) on a batch of 32 synthetic QM9-like molecules resident in HBM
+(SURVEY.md §8(d) generator; weights random-init with the reference architecture).  --mode train
+adds the force-matching loss, double backward, the fused RCCL gradient all-reduce and AdamW.
+Weak scaling: every rank processes its own batch; value = molecules of all ranks / max-rank time.
+
+Also reported (rank 0):
+  roofline     -- the ET edge-aggregation kernel (tmdnet_et_message_fwd) on a C5-scale periodic
+                  water box (50,001 atoms, ~2.7 M edges), HIP events on the launching stream;
+                  algorithmic bytes per launch = E*(20 + 16H) + N*(48H + 4)  (SURVEY.md §8(d)).
+  roofline_c2  -- the same kernel live inside the timed region of the metric workload.
+  cpu_baseline -- oracle/model_oracle.py (plain PyTorch-CPU restatement of the reference) on the
+                  same 32 molecules and weights, host cores of this box, bounded sample (N=1 only).
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for p in (os.path.join(ROOT, "torchmd-net_amd"), ROOT):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--mode", choices=["infer", "train"], default="infer")
+    ap.add_argument("--batch", type=int, default=32, help="molecules per GPU")
+    ap.add_argument("--channels", type=int, default=128)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--roofline-atoms", type=int, default=50001)
+    ap.add_argument("--roofline-reps", type=int, default=20)
+    return ap.parse_args()
+
+
+def qm9_like(n_mol, gen_seed):
+    """n = randint(9, 30) atoms, floor(n/2) heavy atoms in {C,N,O,F}, rest H,
+    pos = randn * 1.6 A; molecules concatenated, batch = molecule id."""
+    g = torch.Generator().manual_seed(gen_seed)
+    zs, ps, bs = [], [], []
+    for m in range(n_mol):
+        n = int(torch.randint(9, 30, (1,), generator=g))
+        heavy = n // 2
+        z = torch.ones(n, dtype=torch.long)
+        z[:heavy] = torch.tensor([6, 7, 8, 9])[torch.randint(0, 4, (heavy,), generator=g)]
+        zs.append(z)
+        ps.append(torch.randn(n, 3, generator=g, dtype=torch.float64) * 1.6)
+        bs.append(torch.full((n,), m, dtype=torch.long))
+    return torch.cat(zs), torch.cat(ps), torch.cat(bs)
+
+
+def et_args(channels):
+    import yaml
+    with open(os.path.join(ROOT, "tests", "golden", "configs", "et_qm9.yaml")) as f:
+        args = yaml.safe_load(f)
+    args.update(prior_model=None, embedding_dimension=channels, derivative=True, output_model="Scalar",
+                precision=32)
+    return args
+
+
+def setup_dist():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if ws > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    return ws, rank, torch.device("cuda", local if ws > 1 else 0)
+
+
+def barrier(ws):
+    if ws > 1:
+        dist.barrier()
+
+
+def max_over_ranks(x, ws, dev):
+    if ws == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def et_algorithmic_bytes(E, N, H, s=4):
+    return E * (4 + 4 + 12 + 4 * H * s) + N * (12 * H * s + 4)
+
+
+def roofline_probe(n_atoms, reps, H, dev):
+    """ET edge-aggregation forward on a C5-scale water box."""
+    from torchmdnet import kernels
+    g = torch.Generator().manual_seed(7)
+    L = (n_atoms / 0.1003) ** (1.0 / 3.0)
+    pos = (torch.rand(n_atoms, 3, generator=g, dtype=torch.float64) * L).float().to(dev)
+    batch = torch.zeros(n_atoms, dtype=torch.long, device=dev)
+    box = torch.eye(3, dtype=torch.float32) * L
+    graph = kernels.build_graph(pos, batch, 0.0, 5.0, 128 * n_atoms, loop=True, strategy="cell", box=box)
+    E = graph.n_edges
+    # destinations in cell order: the waves in flight gather from a compact window of source rows
+    nc = max(3, int(L / 5.0))
+    cell = torch.clamp((pos / (L / nc)).long(), 0, nc - 1)
+    key = (cell[:, 2] * nc + cell[:, 1]) * nc + cell[:, 0]
+    order = torch.argsort(key).to(torch.int32)
+    dl, r = graph.deltas.detach(), graph.distances.detach()
+    C = 0.5 * (torch.cos(r * math.pi / 5.0) + 1.0)
+    u = dl / torch.where(r > 0, r, torch.ones_like(r)).unsqueeze(1)
+    gen = torch.Generator(device=dev).manual_seed(3)
+    rn = lambda *s: torch.randn(*s, device=dev, generator=gen, dtype=torch.float32)
+    q, k, v, vec = rn(n_atoms, H), rn(n_atoms, H), rn(n_atoms, 3 * H), rn(n_atoms, 3, H)
+    pk, pv = rn(E, H), rn(E, 3 * H)
+    lib = kernels.nat.load()
+    xo = torch.empty(n_atoms, H, device=dev)
+    vo = torch.empty(n_atoms, 3, H, device=dev)
+    st = kernels.nat.stream(dev)
+    ptr = kernels.nat.ptr
+
+    def launch():
+        rc = lib.tmdnet_et_message_fwd(0, n_atoms, H, 8, ptr(graph.row_ptr), ptr(graph.src), E, ptr(q), H,
+                                       ptr(k), H, ptr(v), 3 * H, ptr(vec), ptr(pk), H, ptr(pv), 3 * H, ptr(C),
+                                       ptr(u), ptr(xo), ptr(vo), ptr(order), st)
+        kernels.nat.check(rc, "tmdnet_et_message_fwd")
+
+    for _ in range(3):
+        launch()
+    torch.cuda.synchronize()
+    evs = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        launch()
+        b.record()
+        evs.append((a, b))
+    torch.cuda.synchronize()
+    ms = sum(a.elapsed_time(b) for a, b in evs) / len(evs)
+    nbytes = et_algorithmic_bytes(E, n_atoms, H)
+    gbs = nbytes / (ms * 1e-3) / 1e9
+    return {"kernel": "tmdnet_et_message_fwd (k_fwd<float,2,ORD>)",
+            "workload": f"periodic water box, {n_atoms} atoms, L={L:.1f} A, cutoff 5, E={E}, H={H}, fp32",
+            "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
+            "bytes_per_launch": nbytes, "ms_per_launch": round(ms, 4), "launches": reps}
+
+
+def cpu_baseline(model, args, z, pos, batch, seconds):
+    from oracle import model_oracle as O
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    cores = max(1, min(cores, 16))
+    torch.set_num_threads(cores)
+    sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+    cfg = dict(args)
+    O.energy_forces(sd, cfg, z, pos, batch, dtype=torch.float32)  # warm-up
+    n = 0
+    t0 = time.perf_counter()
+    while True:
+        O.energy_forces(sd, cfg, z, pos, batch, dtype=torch.float32)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= seconds or n >= 200:
+            break
+    mols = int(batch.max()) + 1
+    return {"value": round(mols * n / el, 2), "unit": "molecules/s", "cores": cores, "kind": "port",
+            "sample": f"oracle/model_oracle.py (PyTorch-CPU restatement of the reference ET path), "
+                      f"{n} energy+force calls on the same {mols} molecules / weights, float32, "
+                      f"{el:.1f} s, torch threads={cores}"}
+
+
+def main():
+    a = parse()
+    ws, rank, dev = setup_dist()
+    from torchmdnet import kernels
+    from torchmdnet.models.model import create_model
+    from torchmdnet.training import LNNPStep
+
+    args = et_args(a.channels)
+    torch.manual_seed(0)
+    model = create_model(args).to(dev)
+    z, pos, batch = qm9_like(a.batch, gen_seed=1 + rank)
+    n_atoms = z.shape[0]
+    zd, posd, batchd = z.to(dev), pos.float().to(dev), batch.to(dev)
+
+    if a.mode == "train":
+        gy = torch.Generator().manual_seed(100 + rank)
+        y_lab = torch.randn(a.batch, 1, generator=gy).to(dev)
+        f_lab = torch.randn(n_atoms, 3, generator=gy).to(dev)
+        trainer = LNNPStep(model, lr=4e-4, group=None)
+
+        def step():
+            trainer.step(zd, posd, batchd, y_lab, f_lab)
+    else:
+        def step():
+            y, f = model(zd, posd, batchd)
+            return y, f
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    barrier(ws)
+    probe = []
+    kernels.EVENT_PROBE = probe
+    torch.cuda.synchronize()
+    barrier(ws)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize()
+    barrier(ws)
+    el = time.perf_counter() - t0
+    kernels.EVENT_PROBE = None
+    el = max_over_ranks(el, ws, dev)
+
+    mols = a.batch * ws * a.steps
+    out = {
+        "metric": "molecules/sec (energy+force) ET-QM9" + (" training step" if a.mode == "train" else ""),
+        "value": round(mols / el, 2),
+        "unit": "molecules/s",
+        "n_gpus": ws,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(1000 * el / a.steps, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic (SURVEY.md 8(d) QM9-like molecules, random-init weights)",
+        "config": {"workload": "ET-QM9 energy+forces (TorchMD_Net derivative=True)" if a.mode == "infer"
+                   else "ET-QM9 force-matching training step (E+F MSE, double backward, RCCL all-reduce, AdamW)",
+                   "model": "equivariant-transformer", "embedding_dimension": a.channels, "num_layers": 8,
+                   "num_rbf": 64, "num_heads": 8, "cutoff": 5.0, "molecules_per_gpu": a.batch,
+                   "atoms_per_gpu": n_atoms, "global_batch": a.batch * ws, "parallelism": f"dp{ws}"},
+    }
+    if rank == 0 and probe:
+        H = a.channels
+        ms = sum(e0.elapsed_time(e1) for e0, e1, *_ in probe) / len(probe)
+        E, N = probe[0][2], probe[0][3]
+        nbytes = et_algorithmic_bytes(E, N, H)
+        gbs = nbytes / (ms * 1e-3) / 1e9
+        out["roofline_c2"] = {"kernel": "tmdnet_et_message_fwd (k_fwd<float,2>)",
+                              "workload": f"metric batch, N={N}, E={E} (working set fits Infinity Cache)",
+                              "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                              "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                              "bytes_per_launch": nbytes, "ms_per_launch": round(ms, 5),
+                              "launches": len(probe)}
+    if rank == 0 and not a.no_roofline:
+        out["roofline"] = roofline_probe(a.roofline_atoms, a.roofline_reps, a.channels, dev)
+    if rank == 0 and ws == 1 and not a.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(model, args, z, pos, batch, a.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if ws > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -86,11 +86,13 @@ __device__ __forceinline__ void act(const T* base, bool has, T (&x)[V], T (&s)[V
 }
 
 // ------------------------------------------------------------------ forward
-template <typename T, int V>
+// ORD: destinations visited in the caller's `order` (e.g. cell-sorted for large periodic systems,
+// so the waves in flight at any time gather from a compact spatial window of source rows).
+template <typename T, int V, bool ORD>
 __global__ __launch_bounds__(256) void k_fwd(Args<T> A) {
   const int w = blockIdx.x * (blockDim.x / TMD_WAVE) + threadIdx.x / TMD_WAVE;
   if (w >= A.n) return;
-  const int t = A.order ? A.order[w] : w;
+  const int t = ORD ? A.order[w] : w;
   const int lane = lane_id();
   const bool on = lane < A.L;
   const int c0 = on ? lane * V : 0;
@@ -443,7 +445,8 @@ static int launch_v(int V, int n, AT A, hipStream_t st) {
   return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
 }
 
-template <typename T, int V> struct KFwd { static constexpr auto fn = k_fwd<T, V>; };
+template <typename T, int V> struct KFwd { static constexpr auto fn = k_fwd<T, V, false>; };
+template <typename T, int V> struct KFwdOrd { static constexpr auto fn = k_fwd<T, V, true>; };
 template <typename T, int V> struct KBwdDst { static constexpr auto fn = k_bwd_dst<T, V>; };
 template <typename T, int V> struct KBwdSrc { static constexpr auto fn = k_bwd_src<T, V>; };
 template <typename T, int V> struct KNbFwd { static constexpr auto fn = k_nb_fwd<T, V>; };
@@ -486,7 +489,7 @@ static int fwd(int n, int H, int heads, const int32_t* row_ptr, const int32_t* s
   if (rc) return rc;
   A.xo = (T*)xo;
   A.veco = (T*)veco;
-  return launch_v<T, KFwd>(V, n, A, st);
+  return order ? launch_v<T, KFwdOrd>(V, n, A, st) : launch_v<T, KFwd>(V, n, A, st);
 }
 
 template <typename T>

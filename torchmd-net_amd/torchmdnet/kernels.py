@@ -15,6 +15,10 @@ from torch.autograd import Function
 
 from . import _native as nat
 
+# Optional live kernel timing (bench.py): when a list is installed here, the ET message forward
+# launches are bracketed by HIP events recorded on the launching stream.
+EVENT_PROBE = None
+
 
 # ----------------------------------------------------------------------------- neighbour graph
 class EdgeGraph:
@@ -385,12 +389,19 @@ class _ETMessage(Function):
         N, H = q.shape
         xo = torch.empty((N, H), dtype=q.dtype, device=q.device)
         vo = torch.empty((N, 3, H), dtype=q.dtype, device=q.device)
+        probe = EVENT_PROBE
+        if probe is not None:
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            ev0.record()
         rc = lib.tmdnet_et_message_fwd(nat.dtype_code(q.dtype), N, H, heads, nat.ptr(graph.row_ptr),
                                        nat.ptr(graph.src), graph.n_edges, nat.ptr(q), _ld(q), nat.ptr(k),
                                        _ld(k), nat.ptr(v), _ld(v), nat.ptr(vec), nat.ptr(pk), _ld(pk),
                                        nat.ptr(pv), _ld(pv), nat.ptr(C), nat.ptr(u), nat.ptr(xo),
                                        nat.ptr(vo), None, nat.stream(q.device))
         nat.check(rc, "tmdnet_et_message_fwd")
+        if probe is not None:
+            ev1.record()
+            probe.append((ev0, ev1, graph.n_edges, N, H))
         ctx.graph = graph
         ctx.heads = heads
         ctx.save_for_backward(q, k, v, vec, pk, pv, C, u)
