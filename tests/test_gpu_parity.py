@@ -297,7 +297,7 @@ def test_et_edge_kernel_gradcheck():
     z, pos, batch = O.qm9_like(2)
     pos = pos.to(DEV)
     g = kernels.build_graph(pos, batch.to(DEV), 0.0, 5.0, 64 * pos.shape[0], loop=True)
-    N, H, heads, E = pos.shape[0], 16, 2, g.n_edges
+    N, H, heads, E = pos.shape[0], 16, 2, g.n_edges  # H < 32: idle half-wave lanes
     o = dict(dtype=torch.float64, device=DEV, requires_grad=True)
     q, k = torch.randn(N, H, **o), torch.randn(N, H, **o)
     v = torch.randn(N, 3 * H, **o)
@@ -374,3 +374,73 @@ def test_tensornet_c3_padded_matches_fixture():
                   torch.tensor(d["batch"], device=DEV))
     assert _rel(y.detach().cpu(), d["y"]) < 1e-4
     assert _rel(neg_dy.detach().cpu(), d["neg_dy"]) < 1e-4
+
+
+# ----------------------------------------------------------------------------- HIP graphs
+def test_graphed_energy_forces_matches_eager():
+    from torchmdnet.graphs import GraphedEnergyForces
+    from torchmdnet.models.model import create_model
+    _seed()
+    m = create_model(yaml_args("equivariant-transformer", embedding_dimension=128, derivative=True,
+                               output_model="Scalar")).to(DEV)
+    z, pos, batch = O.qm9_like(16)
+    z, pos, batch = z.to(DEV), pos.float().to(DEV), batch.to(DEV)
+    gm = GraphedEnergyForces(m, z, pos, batch)
+    gen = torch.Generator(device=DEV).manual_seed(5)
+    for _ in range(3):
+        p2 = pos + 0.05 * torch.randn(pos.shape, device=DEV, generator=gen)
+        y, f = gm(p2)
+        y, f = y.clone(), f.clone()
+        gm.check_capacity()
+        gm.release()
+        ye, fe = m(z, p2.clone(), batch)
+        for d in gm.dists:
+            d.static_capacity = gm.edge_capacity
+        assert _rel(y.detach().cpu(), ye.detach().cpu()) < 1e-5
+        assert _rel(f.detach().cpu(), fe.detach().cpu()) < 1e-5
+    gm.release()
+
+
+def test_static_capacity_training_grads_match_dynamic():
+    """Padding rows of the static-capacity graph must not leak into weight gradients."""
+    from torchmdnet.models.model import create_model
+    _seed()
+    m = create_model(yaml_args("equivariant-transformer", embedding_dimension=32, num_layers=2, num_rbf=16,
+                               num_heads=4, derivative=True, output_model="Scalar", precision=64)).to(DEV)
+    z, pos, batch = O.qm9_like(3)
+    z, pos, batch = z.to(DEV), pos.to(DEV), batch.to(DEV)
+    grads = []
+    for cap in (None, 4096):
+        m.representation_model.distance.static_capacity = cap
+        y, f = m(z, pos.clone(), batch)
+        loss = (y ** 2).sum() + (f ** 2).sum()
+        grads.append(torch.autograd.grad(loss, [p for p in m.parameters()], allow_unused=True))
+    m.representation_model.distance.static_capacity = None
+    for a, b in zip(*grads):
+        if a is None:
+            assert b is None or torch.count_nonzero(b) == 0
+            continue
+        assert torch.allclose(a, b, rtol=1e-9, atol=1e-11)
+
+
+def test_large_system_spatial_reorder_is_transparent():
+    from torchmdnet import kernels
+    from torchmdnet.models.model import create_model
+    _seed()
+    m = create_model(yaml_args("equivariant-transformer", embedding_dimension=32, num_layers=1, num_rbf=16,
+                               num_heads=4, derivative=True, output_model="Scalar", max_num_neighbors=128,
+                               precision=64)).to(DEV)
+    n = 20000
+    L = (n / 0.1003) ** (1 / 3)
+    g = torch.Generator().manual_seed(1)
+    pos = (torch.rand(n, 3, generator=g, dtype=torch.float64) * L).to(DEV)
+    z = torch.randint(1, 9, (n,), generator=g).to(DEV)
+    batch = torch.zeros(n, dtype=torch.long, device=DEV)
+    out = []
+    for reorder in (True, False):
+        m.representation_model.reorder_atoms = reorder
+        y, f = m(z, pos.clone(), batch)
+        out.append((y.detach(), f.detach()))
+    assert n >= kernels.REORDER_MIN_ATOMS
+    assert _rel(out[0][0].cpu(), out[1][0].cpu()) < 1e-10
+    assert _rel(out[0][1].cpu(), out[1][1].cpu()) < 1e-9

@@ -1,0 +1,136 @@
+"""Kernel micro-benchmark (GPU): ET message fwd / bwd and TN kernels at C2 (32 QM9-like molecules)
+and C5 (50k-atom water box) scale, HIP-event timed, with a correctness check against the composite
+PyTorch restatement.  Usage: python tools/kbench.py [--c5-atoms N] [--reps R]"""
+import argparse
+import math
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "torchmd-net_amd"), ROOT]
+import torch  # noqa: E402
+from torchmdnet import kernels  # noqa: E402
+from bench import qm9_like, et_algorithmic_bytes  # noqa: E402
+
+
+def graph_c2(dev):
+    z, pos, batch = qm9_like(32, 1)
+    return kernels.build_graph(pos.float().to(dev), batch.to(dev), 0.0, 5.0, 64 * len(z), loop=True)
+
+
+def morton3(c):
+    def spread(x):
+        x = x & 0x3FF
+        x = (x | (x << 16)) & 0x030000FF
+        x = (x | (x << 8)) & 0x0300F00F
+        x = (x | (x << 4)) & 0x030C30C3
+        x = (x | (x << 2)) & 0x09249249
+        return x
+    return spread(c[:, 0]) | (spread(c[:, 1]) << 1) | (spread(c[:, 2]) << 2)
+
+
+def graph_c5(n, dev, order="cell"):
+    g = torch.Generator().manual_seed(7)
+    L = (n / 0.1003) ** (1 / 3)
+    pos = (torch.rand(n, 3, generator=g, dtype=torch.float64) * L).float()
+    # renumber atoms in cell order (spatially coherent numbering, as MD engines / PDB files give)
+    nc = max(3, int(L / 5.0))
+    cell = torch.clamp((pos / (L / nc)).long(), 0, nc - 1)
+    if order == "morton":
+        key = morton3(cell)
+    elif order == "random":
+        key = torch.randperm(n, generator=g)
+    else:
+        key = (cell[:, 2] * nc + cell[:, 1]) * nc + cell[:, 0]
+    pos = pos[torch.argsort(key)].contiguous().to(dev)
+    return kernels.build_graph(pos, torch.zeros(n, dtype=torch.long, device=dev), 0.0, 5.0, 128 * n,
+                               loop=True, strategy="cell", box=torch.eye(3) * L)
+
+
+def timeit(fn, reps):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / reps * 1e3  # us
+
+
+def et_inputs(g, H, dev):
+    N, E = g.n_nodes, g.n_edges
+    gen = torch.Generator(device=dev).manual_seed(3)
+    rn = lambda *s: torch.randn(*s, device=dev, generator=gen)
+    T = g.transpose.long()
+    sym = lambda x: ((x + x[T]) * 0.5).contiguous()
+    r = g.distances.detach()
+    C = 0.5 * (torch.cos(r * math.pi / 5.0) + 1.0)
+    u = (g.deltas.detach() / torch.where(r > 0, r, torch.ones_like(r)).unsqueeze(1)).contiguous()
+    return dict(q=rn(N, H), k=rn(N, H), v=rn(N, 3 * H), vec=rn(N, 3, H), pk=sym(rn(E, H)), pv=sym(rn(E, 3 * H)),
+                C=C, u=u)
+
+
+def run_et(name, g, H, reps, dev, check):
+    x = et_inputs(g, H, dev)
+    args = [x[k] for k in ("q", "k", "v", "vec", "pk", "pv", "C", "u")]
+    N, E = g.n_nodes, g.n_edges
+    fwd = lambda: kernels._ETMessage.forward(_Ctx(), *args, g, 8)
+    gx, gv = torch.randn(N, H, device=dev), torch.randn(N, 3, H, device=dev)
+    bwd = lambda: kernels._ETMessageBwd.forward(_Ctx(), gx, gv, *args, g, 8)
+    tf = timeit(fwd, reps)
+    tb = timeit(bwd, reps)
+    B = et_algorithmic_bytes(E, N, H)
+    print(f"{name}: N={N} E={E}  fwd {tf:8.1f} us {B / tf / 1e3:7.1f} GB/s ({B / tf / 1e3 / 80:5.1f}%)  "
+          f"bwd(dst+src) {tb:8.1f} us")
+    if check:
+        xo, vo = fwd()
+        xr, vr = kernels.et_message_composite(*args, g.src.long(), g.dst.long(), N, 8)
+        e1 = ((xo - xr).abs().max() / xr.abs().max()).item()
+        e2 = ((vo - vr).abs().max() / vr.abs().max()).item()
+        outs = bwd()
+        ins = [a.detach().requires_grad_(True) for a in args]
+        with torch.enable_grad():
+            xr, vr = kernels.et_message_composite(*ins, g.src.long(), g.dst.long(), N, 8)
+            ref = torch.autograd.grad((xr, vr), ins, (gx, gv))
+        T = g.transpose.long()
+        errs = []
+        for nm, a, b in zip("q k v vec pk pv C u".split(), outs, ref):
+            if nm in ("pk", "pv", "C"):
+                a, b = a + a[T], b + b[T]
+            if nm == "u":
+                a, b = a - a[T], b - b[T]
+            errs.append(((a - b).abs().max() / b.abs().max().clamp(min=1e-30)).item())
+        print(f"   check fwd {e1:.1e} {e2:.1e}  bwd max rel {max(errs):.1e}")
+        assert max(e1, e2, max(errs)) < 1e-4
+
+
+class _Ctx:
+    def save_for_backward(self, *a):
+        pass
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--c5-atoms", type=int, default=50001)
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--no-c5", action="store_true")
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    g2 = graph_c2(dev)
+    run_et("C2 ET", g2, 128, 200, dev, True)
+    if not a.no_c5:
+        for order in ("morton", "random"):
+            g5 = graph_c5(a.c5_atoms, dev, order)
+            for nt, cs in ((0, 1), (1, 1), (0, 2), (1, 2), (1, 4)):
+                os.environ["TMDNET_NT"] = str(nt)
+                os.environ["TMDNET_CS"] = str(cs)
+                run_et(f"C5 ET order={order} nt={nt} cs={cs}", g5, 128, a.reps, dev, order == "morton")
+            del g5
+            torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()

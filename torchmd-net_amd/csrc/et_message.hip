@@ -16,6 +16,7 @@
 //     gk, gv, gvec without a transpose scatter or atomics.
 #include "common.h"
 #include "tmdnet.h"
+#include <stdlib.h>
 
 namespace tmd {
 namespace et {
@@ -28,20 +29,44 @@ template <> struct Vec<double, 1> { using t = double; };
 template <> struct Vec<double, 2> { using t = double2; };
 template <> struct Vec<double, 4> { using t = double4; };
 
-template <typename T, int V> __device__ __forceinline__ void ldv(T (&o)[V], const T* p) {
+template <typename T, int V> __device__ __forceinline__ void ldv(T (&o)[V], const T* p);
+template <typename T, int V> __device__ __forceinline__ void ldv_(T (&o)[V], const T* p) {
   using VT = typename Vec<T, V>::t;
   const VT x = *reinterpret_cast<const VT*>(p);
   if constexpr (V == 1) { o[0] = x; }
   else if constexpr (V == 2) { o[0] = x.x; o[1] = x.y; }
   else { o[0] = x.x; o[1] = x.y; o[2] = x.z; o[3] = x.w; }
 }
-template <typename T, int V> __device__ __forceinline__ void stv(T* p, const T (&o)[V]) {
+template <typename T, int V> __device__ __forceinline__ void ldv(T (&o)[V], const T* p) {
+  if constexpr (V == 8) {
+    T a[4], b[4];
+    ldv_<T, 4>(a, p);
+    ldv_<T, 4>(b, p + 4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { o[i] = a[i]; o[4 + i] = b[i]; }
+  } else {
+    ldv_<T, V>(o, p);
+  }
+}
+template <typename T, int V> __device__ __forceinline__ void stv(T* p, const T (&o)[V]);
+template <typename T, int V> __device__ __forceinline__ void stv_(T* p, const T (&o)[V]) {
   using VT = typename Vec<T, V>::t;
   VT x;
   if constexpr (V == 1) { x = o[0]; }
   else if constexpr (V == 2) { x.x = o[0]; x.y = o[1]; }
   else { x.x = o[0]; x.y = o[1]; x.z = o[2]; x.w = o[3]; }
   *reinterpret_cast<VT*>(p) = x;
+}
+template <typename T, int V> __device__ __forceinline__ void stv(T* p, const T (&o)[V]) {
+  if constexpr (V == 8) {
+    T a[4], b[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { a[i] = o[i]; b[i] = o[4 + i]; }
+    stv_<T, 4>(p, a);
+    stv_<T, 4>(p + 4, b);
+  } else {
+    stv_<T, V>(p, o);
+  }
 }
 template <typename T, int V> __device__ __forceinline__ void zero(T (&o)[V]) {
 #pragma unroll
@@ -50,6 +75,9 @@ template <typename T, int V> __device__ __forceinline__ void zero(T (&o)[V]) {
 
 template <typename T> struct Args {
   int n, H, d, L, lph, cap;
+  int xcd;      // XCD-contiguous block remap (on: +10-15 % on C5-scale graphs)
+  int nt;       // non-temporal loads of the per-edge stream (measured slower on gfx950: off)
+  int HC;       // channels per channel group (H / CS)
   const int32_t* row_ptr;
   const int32_t* src;
   const int32_t* order;
@@ -69,10 +97,33 @@ template <typename T> struct Args {
 };
 
 // silu of the pre-activation, or 1 when the projection is absent
+template <typename T, int V> struct NVec { typedef T t __attribute__((ext_vector_type(V))); };
+template <typename T, int V> __device__ __forceinline__ void ldv_nt_(T (&o)[V], const T* p) {
+  if constexpr (V == 1) {
+    o[0] = __builtin_nontemporal_load(p);
+  } else {
+    using VT = typename NVec<T, V>::t;
+    const VT x = __builtin_nontemporal_load(reinterpret_cast<const VT*>(p));
+#pragma unroll
+    for (int i = 0; i < V; ++i) o[i] = x[i];
+  }
+}
+template <typename T, int V> __device__ __forceinline__ void ldv_nt(T (&o)[V], const T* p) {
+  if constexpr (V == 8) {
+    T a[4], b[4];
+    ldv_nt_<T, 4>(a, p);
+    ldv_nt_<T, 4>(b, p + 4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { o[i] = a[i]; o[4 + i] = b[i]; }
+  } else {
+    ldv_nt_<T, V>(o, p);
+  }
+}
+
 template <typename T, int V>
-__device__ __forceinline__ void act(const T* base, bool has, T (&x)[V], T (&s)[V], T (&ds)[V]) {
+__device__ __forceinline__ void act(const T* base, bool has, T (&x)[V], T (&s)[V], T (&ds)[V], bool nt = false) {
   if (has) {
-    ldv<T, V>(x, base);
+    if (nt) ldv_nt<T, V>(x, base); else ldv<T, V>(x, base);
 #pragma unroll
     for (int i = 0; i < V; ++i) {
       Silu<T> f(x[i]);
@@ -85,62 +136,144 @@ __device__ __forceinline__ void act(const T* base, bool has, T (&x)[V], T (&s)[V
   }
 }
 
-// ------------------------------------------------------------------ forward
-// ORD: destinations visited in the caller's `order` (e.g. cell-sorted for large periodic systems,
-// so the waves in flight at any time gather from a compact spatial window of source rows).
-template <typename T, int V, bool ORD>
-__global__ __launch_bounds__(256) void k_fwd(Args<T> A) {
-  const int w = blockIdx.x * (blockDim.x / TMD_WAVE) + threadIdx.x / TMD_WAVE;
-  if (w >= A.n) return;
-  const int t = ORD ? A.order[w] : w;
+
+// Work decomposition shared by the three kernels.
+//   * a 256-thread block = 4 waves; S waves cooperate on one node (S in {1, 2, 4}), so a block owns
+//     4/S nodes; the S partial results are summed through LDS at the end;
+//   * inside a wave, groups of L lanes ("edge slots") each stream their own edge: a lane owns V
+//     contiguous channels (16-byte loads at H = 128, fp32), so one wave instruction covers 64/L
+//     edges (2 with L = 32);
+//   * CS channel groups: each wave covers H/CS channels of its node (heads are independent);
+//   * row bounds and the node index are wave-uniform (readfirstlane): scalar loads.
+
+// XCD-contiguous remap (bijective, cdna_hip_programming.md §5 "XCD swizzle"): blocks are dealt
+// round-robin over the 8 XCDs; remapping gives each XCD one contiguous range of logical blocks, so
+// the source rows its waves gather (neighbours of nearby nodes) are shared in that XCD's L2.
+__device__ __forceinline__ int xcd_block(int xcd) {
+  const int nwg = gridDim.x, b = blockIdx.x;
+  if (!xcd || nwg < 16) return b;
+  const int q = nwg / 8, r = nwg % 8, x = b % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+struct Geo {
+  int node;  // node owned by this wave (-1: idle wave of a partially filled block)
+  int sub;   // wave index within the node's group [0, S)
+  int es;    // edge slot of this lane (lanes [es*L, (es+1)*L) stream one edge)
+  int el;    // lane within the edge slot
+  int cg;    // channel group of this wave [0, CS)
+};
+
+// Logical block -> (channel group, node block).  With the XCD-contiguous remap the CS channel
+// groups of one node range run on DIFFERENT XCDs, so each XCD's L2 holds only its channel slice of
+// the gathered source rows (the per-XCD working set shrinks CS-fold).
+template <int S, int CS, bool ORD>
+__device__ __forceinline__ Geo geo(int n, int L, const int32_t* order, int xcd) {
+  Geo g;
+  const int wid = threadIdx.x >> 6;
+  const int npb = 4 / S;
+  const int nbn = (n + npb - 1) / npb;
+  const int lb = xcd_block(xcd);
+  g.cg = CS > 1 ? __builtin_amdgcn_readfirstlane(lb / nbn) : 0;
+  const int w = __builtin_amdgcn_readfirstlane((CS > 1 ? lb % nbn : lb) * npb + wid / S);
+  g.sub = __builtin_amdgcn_readfirstlane(wid % S);
+  g.node = w < n ? (ORD ? __builtin_amdgcn_readfirstlane(order[w]) : w) : -1;
   const int lane = lane_id();
-  const bool on = lane < A.L;
-  const int c0 = on ? lane * V : 0;
+  g.es = lane / L;
+  g.el = lane % L;
+  return g;
+}
+
+template <typename T, int V> __device__ __forceinline__ void xor_slots(T (&a)[V], int L) {
+  for (int o = L; o < TMD_WAVE; o <<= 1)
+#pragma unroll
+    for (int i = 0; i < V; ++i) a[i] += __shfl_xor(a[i], o);
+}
+
+// Sum NV per-lane values over the S waves of a node through LDS; the result lands in wave sub==0.
+template <typename T, int S, int NV>
+__device__ __forceinline__ void reduce_waves(T (&a)[NV], int sub, T* lds) {
+  if constexpr (S > 1) {
+    const int wid = threadIdx.x >> 6, lane = lane_id();
+    const int base = (wid - sub) * 64 * NV;  // group's slab
+    if (sub > 0) {
+#pragma unroll
+      for (int i = 0; i < NV; ++i) lds[base + (sub * NV + i) * 64 + lane] = a[i];
+    }
+    __syncthreads();
+    if (sub == 0) {
+#pragma unroll
+      for (int s2 = 1; s2 < S; ++s2)
+#pragma unroll
+        for (int i = 0; i < NV; ++i) a[i] += lds[base + (s2 * NV + i) * 64 + lane];
+    }
+  }
+}
+
+// ------------------------------------------------------------------ forward
+// ORD: nodes visited in the caller's `order` (cell order for large periodic systems, so the waves in
+// flight gather from a compact spatial window of source rows).
+template <typename T, int V, int S, int CS, bool ORD>
+__global__ __launch_bounds__(256) void k_fwd(Args<T> A) {
+  __shared__ T lds[S > 1 ? 4 * 64 * 4 * V : 1];
+  const Geo G = geo<S, CS, ORD>(A.n, A.L, A.order, A.xcd);
+  const int t = G.node;
+  const bool on = true;
+  const int EPW = TMD_WAVE / A.L;  // edges per wave instruction
+  const int c0 = G.cg * A.HC + G.el * V;
   const int hh = c0 / A.d, cc = c0 % A.d;
   const int vo = hh * 3 * A.d + cc;
   const bool hk = A.pk != nullptr, hv = A.pv != nullptr;
-  T q[V];
-  ldv<T, V>(q, A.q + (size_t)t * A.ldq + c0);
   T ax[V], a0[V], a1[V], a2[V];
   zero(ax); zero(a0); zero(a1); zero(a2);
-  const int b = min(A.row_ptr[t], A.cap), e = min(A.row_ptr[t + 1], A.cap);
-  for (int k = b; k < e; ++k) {
-    const int s = A.src[k];
-    const T Ce = A.C[k];
-    const T u0 = A.u[3 * k], u1 = A.u[3 * k + 1], u2 = A.u[3 * k + 2];
-    T kk[V], px[V], dk[V], dd[V];
-    ldv<T, V>(kk, A.k + (size_t)s * A.ldk + c0);
-    act<T, V>(A.pk + (size_t)k * A.ldpk + c0, hk, px, dk, dd);
-    T part = T(0);
+  if (t >= 0) {
+    T q[V];
+    ldv<T, V>(q, A.q + (size_t)t * A.ldq + c0);
+    const int b = min(A.row_ptr[t], A.cap), e = min(A.row_ptr[t + 1], A.cap);
+    for (int k = b + EPW * G.sub + G.es; k < e; k += EPW * S) {
+      const int s = A.src[k];
+      const T Ce = A.C[k];
+      const T u0 = A.u[3 * k], u1 = A.u[3 * k + 1], u2 = A.u[3 * k + 2];
+      T kk[V], px[V], dk[V], dd[V];
+      ldv<T, V>(kk, A.k + (size_t)s * A.ldk + c0);
+      act<T, V>(A.pk + (size_t)k * A.ldpk + c0, hk, px, dk, dd, A.nt);
+      const T* vs = A.v + (size_t)s * A.ldv + vo;
+      const T* pvs = A.pv + (size_t)k * A.ldpv + vo;
+      T vx[V], v1[V], v2[V], dvx[V], dv1[V], dv2[V];
+      ldv<T, V>(vx, vs);
+      ldv<T, V>(v1, vs + A.d);
+      ldv<T, V>(v2, vs + 2 * A.d);
+      act<T, V>(pvs, hv, px, dvx, dd, A.nt);
+      act<T, V>(pvs + A.d, hv, px, dv1, dd, A.nt);
+      act<T, V>(pvs + 2 * A.d, hv, px, dv2, dd, A.nt);
+      const T* vecs = A.vec + (size_t)s * 3 * A.H + c0;
+      T w0[V], w1[V], w2[V];
+      ldv<T, V>(w0, vecs);
+      ldv<T, V>(w1, vecs + A.H);
+      ldv<T, V>(w2, vecs + 2 * A.H);
+      T part = T(0);
 #pragma unroll
-    for (int i = 0; i < V; ++i) part += q[i] * kk[i] * dk[i];
-    part = group_sum(part, A.lph);
-    const Silu<T> sa(part);
-    const T a = sa.s * Ce;
-    const T* vs = A.v + (size_t)s * A.ldv + vo;
-    const T* pvs = A.pv + (size_t)k * A.ldpv + vo;
-    T vx[V], v1[V], v2[V], dvx[V], dv1[V], dv2[V];
-    ldv<T, V>(vx, vs);
-    ldv<T, V>(v1, vs + A.d);
-    ldv<T, V>(v2, vs + 2 * A.d);
-    act<T, V>(pvs, hv, px, dvx, dd);
-    act<T, V>(pvs + A.d, hv, px, dv1, dd);
-    act<T, V>(pvs + 2 * A.d, hv, px, dv2, dd);
-    const T* vecs = A.vec + (size_t)s * 3 * A.H + c0;
-    T w0[V], w1[V], w2[V];
-    ldv<T, V>(w0, vecs);
-    ldv<T, V>(w1, vecs + A.H);
-    ldv<T, V>(w2, vecs + 2 * A.H);
+      for (int i = 0; i < V; ++i) part += q[i] * kk[i] * dk[i];
+      part = group_sum(part, A.lph);
+      const Silu<T> sa(part);
+      const T a = sa.s * Ce;
 #pragma unroll
-    for (int i = 0; i < V; ++i) {
-      ax[i] += vx[i] * dvx[i] * a;
-      const T v1e = v1[i] * dv1[i], v2e = v2[i] * dv2[i];
-      a0[i] += w0[i] * v1e + v2e * u0;
-      a1[i] += w1[i] * v1e + v2e * u1;
-      a2[i] += w2[i] * v1e + v2e * u2;
+      for (int i = 0; i < V; ++i) {
+        ax[i] += vx[i] * dvx[i] * a;
+        const T v1e = v1[i] * dv1[i], v2e = v2[i] * dv2[i];
+        a0[i] += w0[i] * v1e + v2e * u0;
+        a1[i] += w1[i] * v1e + v2e * u1;
+        a2[i] += w2[i] * v1e + v2e * u2;
+      }
     }
   }
-  if (on) {
+  xor_slots(ax, A.L); xor_slots(a0, A.L); xor_slots(a1, A.L); xor_slots(a2, A.L);
+  T all[4 * V];
+#pragma unroll
+  for (int i = 0; i < V; ++i) { all[i] = ax[i]; all[V + i] = a0[i]; all[2 * V + i] = a1[i]; all[3 * V + i] = a2[i]; }
+  reduce_waves<T, S, 4 * V>(all, G.sub, lds);
+  if (t >= 0 && G.sub == 0 && on && G.es == 0) {
+#pragma unroll
+    for (int i = 0; i < V; ++i) { ax[i] = all[i]; a0[i] = all[V + i]; a1[i] = all[2 * V + i]; a2[i] = all[3 * V + i]; }
     stv<T, V>(A.xo + (size_t)t * A.H + c0, ax);
     T* vo_ = A.veco + (size_t)t * 3 * A.H + c0;
     stv<T, V>(vo_, a0);
@@ -150,171 +283,187 @@ __global__ __launch_bounds__(256) void k_fwd(Args<T> A) {
 }
 
 // ------------------------------------------------------------------ backward, destination pass
-template <typename T, int V>
+template <typename T, int V, int S, int CS>
 __global__ __launch_bounds__(256) void k_bwd_dst(Args<T> A) {
-  const int w = blockIdx.x * (blockDim.x / TMD_WAVE) + threadIdx.x / TMD_WAVE;
-  if (w >= A.n) return;
-  const int t = A.order ? A.order[w] : w;
-  const int lane = lane_id();
-  const bool on = lane < A.L;
-  const int c0 = on ? lane * V : 0;
+  __shared__ T lds[S > 1 ? 4 * 64 * V : 1];
+  const Geo G = geo<S, CS, false>(A.n, A.L, nullptr, A.xcd);
+  const int t = G.node;
+  const bool on = true;
+  const int EPW = TMD_WAVE / A.L;  // edges per wave instruction
+  const int c0 = G.cg * A.HC + G.el * V;
   const int hh = c0 / A.d, cc = c0 % A.d;
   const int vo = hh * 3 * A.d + cc;
   const bool hk = A.pk != nullptr, hv = A.pv != nullptr;
-  const bool head_leader = on && (lane % A.lph) == 0;
-  T q[V], gx[V], g0[V], g1[V], g2[V];
-  ldv<T, V>(q, A.q + (size_t)t * A.ldq + c0);
-  ldv<T, V>(gx, A.gx + (size_t)t * A.H + c0);
-  const T* gvt = A.gvec + (size_t)t * 3 * A.H + c0;
-  ldv<T, V>(g0, gvt);
-  ldv<T, V>(g1, gvt + A.H);
-  ldv<T, V>(g2, gvt + 2 * A.H);
+  const bool head_leader = on && (G.el % A.lph) == 0;
   T gq[V];
   zero(gq);
-  const int b = min(A.row_ptr[t], A.cap), e = min(A.row_ptr[t + 1], A.cap);
-  for (int k = b; k < e; ++k) {
-    const int s = A.src[k];
-    const T Ce = A.C[k];
-    const T u0 = A.u[3 * k], u1 = A.u[3 * k + 1], u2 = A.u[3 * k + 2];
-    T kk[V], pk[V], dk[V], ddk[V];
-    ldv<T, V>(kk, A.k + (size_t)s * A.ldk + c0);
-    act<T, V>(A.pk + (size_t)k * A.ldpk + c0, hk, pk, dk, ddk);
-    T part = T(0);
+  if (t >= 0) {
+    T q[V], gx[V], g0[V], g1[V], g2[V];
+    ldv<T, V>(q, A.q + (size_t)t * A.ldq + c0);
+    ldv<T, V>(gx, A.gx + (size_t)t * A.H + c0);
+    const T* gvt = A.gvec + (size_t)t * 3 * A.H + c0;
+    ldv<T, V>(g0, gvt);
+    ldv<T, V>(g1, gvt + A.H);
+    ldv<T, V>(g2, gvt + 2 * A.H);
+    const int b = min(A.row_ptr[t], A.cap), e = min(A.row_ptr[t + 1], A.cap);
+    for (int k = b + EPW * G.sub + G.es; k < e; k += EPW * S) {
+      const int s = A.src[k];
+      const T Ce = A.C[k];
+      const T u0 = A.u[3 * k], u1 = A.u[3 * k + 1], u2 = A.u[3 * k + 2];
+      T kk[V], pk[V], dk[V], ddk[V];
+      ldv<T, V>(kk, A.k + (size_t)s * A.ldk + c0);
+      act<T, V>(A.pk + (size_t)k * A.ldpk + c0, hk, pk, dk, ddk, A.nt);
+      const T* vs = A.v + (size_t)s * A.ldv + vo;
+      const T* pvs = A.pv + (size_t)k * A.ldpv + vo;
+      T vx[V], v1[V], v2[V], px[V], p1[V], p2[V], dvx[V], dv1[V], dv2[V], ddx[V], dd1[V], dd2[V];
+      ldv<T, V>(vx, vs);
+      ldv<T, V>(v1, vs + A.d);
+      ldv<T, V>(v2, vs + 2 * A.d);
+      act<T, V>(pvs, hv, px, dvx, ddx, A.nt);
+      act<T, V>(pvs + A.d, hv, p1, dv1, dd1, A.nt);
+      act<T, V>(pvs + 2 * A.d, hv, p2, dv2, dd2, A.nt);
+      const T* vecs = A.vec + (size_t)s * 3 * A.H + c0;
+      T w0[V], w1[V], w2[V];
+      ldv<T, V>(w0, vecs);
+      ldv<T, V>(w1, vecs + A.H);
+      ldv<T, V>(w2, vecs + 2 * A.H);
+      T part = T(0), ga = T(0), gu0 = T(0), gu1 = T(0), gu2 = T(0);
 #pragma unroll
-    for (int i = 0; i < V; ++i) part += q[i] * kk[i] * dk[i];
-    part = group_sum(part, A.lph);
-    const Silu<T> sa(part);
-    const T a = sa.s * Ce;
-    const T* vs = A.v + (size_t)s * A.ldv + vo;
-    const T* pvs = A.pv + (size_t)k * A.ldpv + vo;
-    T vx[V], v1[V], v2[V], px[V], p1[V], p2[V], dvx[V], dv1[V], dv2[V], ddx[V], dd1[V], dd2[V];
-    ldv<T, V>(vx, vs);
-    ldv<T, V>(v1, vs + A.d);
-    ldv<T, V>(v2, vs + 2 * A.d);
-    act<T, V>(pvs, hv, px, dvx, ddx);
-    act<T, V>(pvs + A.d, hv, p1, dv1, dd1);
-    act<T, V>(pvs + 2 * A.d, hv, p2, dv2, dd2);
-    const T* vecs = A.vec + (size_t)s * 3 * A.H + c0;
-    T w0[V], w1[V], w2[V];
-    ldv<T, V>(w0, vecs);
-    ldv<T, V>(w1, vecs + A.H);
-    ldv<T, V>(w2, vecs + 2 * A.H);
-    T ga = T(0), gu0 = T(0), gu1 = T(0), gu2 = T(0);
+      for (int i = 0; i < V; ++i) {
+        part += q[i] * kk[i] * dk[i];
+        ga += gx[i] * vx[i] * dvx[i];
+        const T v2e = v2[i] * dv2[i];
+        gu0 += g0[i] * v2e;
+        gu1 += g1[i] * v2e;
+        gu2 += g2[i] * v2e;
+      }
+      part = group_sum(part, A.lph);
+      ga = group_sum(ga, A.lph);
+      const Silu<T> sa(part);
+      const T a = sa.s * Ce;
+      const T gs = ga * Ce * sa.d(part);
+      T gpk[V], gpx[V], gp1[V], gp2[V];
 #pragma unroll
-    for (int i = 0; i < V; ++i) {
-      ga += gx[i] * vx[i] * dvx[i];
-      const T v2e = v2[i] * dv2[i];
-      gu0 += g0[i] * v2e;
-      gu1 += g1[i] * v2e;
-      gu2 += g2[i] * v2e;
-    }
-    ga = group_sum(ga, A.lph);
-    const T gs = ga * Ce * sa.d(part);
-    T gpk[V], gpx[V], gp1[V], gp2[V];
-#pragma unroll
-    for (int i = 0; i < V; ++i) {
-      gq[i] += gs * kk[i] * dk[i];
-      gpk[i] = gs * q[i] * kk[i] * ddk[i];
-      gpx[i] = gx[i] * a * vx[i] * ddx[i];
-      const T gv1e = g0[i] * w0[i] + g1[i] * w1[i] + g2[i] * w2[i];
-      gp1[i] = gv1e * v1[i] * dd1[i];
-      const T gv2e = g0[i] * u0 + g1[i] * u1 + g2[i] * u2;
-      gp2[i] = gv2e * v2[i] * dd2[i];
-    }
-    T gc = head_leader ? ga * sa.s : T(0);
-    gc = wave_sum(gc);
-    gu0 = wave_sum(on ? gu0 : T(0));
-    gu1 = wave_sum(on ? gu1 : T(0));
-    gu2 = wave_sum(on ? gu2 : T(0));
-    if (on) {
-      if (hk) stv<T, V>(A.gpk + (size_t)k * A.H + c0, gpk);
-      if (hv) {
-        T* gp = A.gpv + (size_t)k * 3 * A.H + vo;
-        stv<T, V>(gp, gpx);
-        stv<T, V>(gp + A.d, gp1);
-        stv<T, V>(gp + 2 * A.d, gp2);
+      for (int i = 0; i < V; ++i) {
+        gq[i] += gs * kk[i] * dk[i];
+        gpk[i] = gs * q[i] * kk[i] * ddk[i];
+        gpx[i] = gx[i] * a * vx[i] * ddx[i];
+        const T gv1e = g0[i] * w0[i] + g1[i] * w1[i] + g2[i] * w2[i];
+        gp1[i] = gv1e * v1[i] * dd1[i];
+        const T gv2e = g0[i] * u0 + g1[i] * u1 + g2[i] * u2;
+        gp2[i] = gv2e * v2[i] * dd2[i];
+      }
+      const T gc = group_sum(head_leader ? ga * sa.s : T(0), A.L);
+      gu0 = group_sum(gu0, A.L);
+      gu1 = group_sum(gu1, A.L);
+      gu2 = group_sum(gu2, A.L);
+      if (on) {
+        if (hk) stv<T, V>(A.gpk + (size_t)k * A.H + c0, gpk);
+        if (hv) {
+          T* gp = A.gpv + (size_t)k * 3 * A.H + vo;
+          stv<T, V>(gp, gpx);
+          stv<T, V>(gp + A.d, gp1);
+          stv<T, V>(gp + 2 * A.d, gp2);
+        }
+      }
+      if (G.el == 0) {
+        A.gC[k] = gc;
+        A.gu[3 * k] = gu0;
+        A.gu[3 * k + 1] = gu1;
+        A.gu[3 * k + 2] = gu2;
       }
     }
-    if (lane == 0) {
-      A.gC[k] = gc;
-      A.gu[3 * k] = gu0;
-      A.gu[3 * k + 1] = gu1;
-      A.gu[3 * k + 2] = gu2;
-    }
   }
-  if (on) stv<T, V>(A.gq + (size_t)t * A.H + c0, gq);
+  xor_slots(gq, A.L);
+  reduce_waves<T, S, V>(gq, G.sub, lds);
+  if (t >= 0 && G.sub == 0 && on && G.es == 0) stv<T, V>(A.gq + (size_t)t * A.H + c0, gq);
 }
 
 // ------------------------------------------------------------------ backward, source pass
-// Wave owns node j as SOURCE.  Row j lists edges m->j; each is read as its reverse j->m
+// A wave group owns node j as SOURCE.  Row j lists edges m->j; each is read as its reverse j->m
 // (same dk/dv/cutoff, unit vector negated), m being the destination whose q/gx/gvec are gathered.
-template <typename T, int V>
+template <typename T, int V, int S, int CS>
 __global__ __launch_bounds__(256) void k_bwd_src(Args<T> A) {
-  const int w = blockIdx.x * (blockDim.x / TMD_WAVE) + threadIdx.x / TMD_WAVE;
-  if (w >= A.n) return;
-  const int j = A.order ? A.order[w] : w;
-  const int lane = lane_id();
-  const bool on = lane < A.L;
-  const int c0 = on ? lane * V : 0;
+  __shared__ T lds[S > 1 ? 4 * 64 * 7 * V : 1];
+  const Geo G = geo<S, CS, false>(A.n, A.L, nullptr, A.xcd);
+  const int j = G.node;
+  const bool on = true;
+  const int EPW = TMD_WAVE / A.L;  // edges per wave instruction
+  const int c0 = G.cg * A.HC + G.el * V;
   const int hh = c0 / A.d, cc = c0 % A.d;
   const int vo = hh * 3 * A.d + cc;
   const bool hk = A.pk != nullptr, hv = A.pv != nullptr;
-  T kk[V], vx[V], v1[V], v2[V], w0[V], w1[V], w2[V];
-  ldv<T, V>(kk, A.k + (size_t)j * A.ldk + c0);
-  const T* vj = A.v + (size_t)j * A.ldv + vo;
-  ldv<T, V>(vx, vj);
-  ldv<T, V>(v1, vj + A.d);
-  ldv<T, V>(v2, vj + 2 * A.d);
-  const T* vecj = A.vec + (size_t)j * 3 * A.H + c0;
-  ldv<T, V>(w0, vecj);
-  ldv<T, V>(w1, vecj + A.H);
-  ldv<T, V>(w2, vecj + 2 * A.H);
   T gk[V], gvx[V], gv1[V], gv2[V], gw0[V], gw1[V], gw2[V];
   zero(gk); zero(gvx); zero(gv1); zero(gv2); zero(gw0); zero(gw1); zero(gw2);
-  const int b = min(A.row_ptr[j], A.cap), e = min(A.row_ptr[j + 1], A.cap);
-  for (int k = b; k < e; ++k) {
-    const int m = A.src[k];
-    const T Ce = A.C[k];
-    const T u0 = -A.u[3 * k], u1 = -A.u[3 * k + 1], u2 = -A.u[3 * k + 2];
-    T qm[V], gxm[V], g0[V], g1[V], g2[V], pk[V], dk[V], ddk[V];
-    ldv<T, V>(qm, A.q + (size_t)m * A.ldq + c0);
-    ldv<T, V>(gxm, A.gx + (size_t)m * A.H + c0);
-    const T* gvm = A.gvec + (size_t)m * 3 * A.H + c0;
-    ldv<T, V>(g0, gvm);
-    ldv<T, V>(g1, gvm + A.H);
-    ldv<T, V>(g2, gvm + 2 * A.H);
-    act<T, V>(A.pk + (size_t)k * A.ldpk + c0, hk, pk, dk, ddk);
-    const T* pvs = A.pv + (size_t)k * A.ldpv + vo;
-    T px[V], dvx[V], dv1[V], dv2[V], dd[V];
-    act<T, V>(pvs, hv, px, dvx, dd);
-    act<T, V>(pvs + A.d, hv, px, dv1, dd);
-    act<T, V>(pvs + 2 * A.d, hv, px, dv2, dd);
-    T part = T(0), ga = T(0);
+  if (j >= 0) {
+    T kk[V], vx[V], v1[V], v2[V], w0[V], w1[V], w2[V];
+    ldv<T, V>(kk, A.k + (size_t)j * A.ldk + c0);
+    const T* vj = A.v + (size_t)j * A.ldv + vo;
+    ldv<T, V>(vx, vj);
+    ldv<T, V>(v1, vj + A.d);
+    ldv<T, V>(v2, vj + 2 * A.d);
+    const T* vecj = A.vec + (size_t)j * 3 * A.H + c0;
+    ldv<T, V>(w0, vecj);
+    ldv<T, V>(w1, vecj + A.H);
+    ldv<T, V>(w2, vecj + 2 * A.H);
+    const int b = min(A.row_ptr[j], A.cap), e = min(A.row_ptr[j + 1], A.cap);
+    for (int k = b + EPW * G.sub + G.es; k < e; k += EPW * S) {
+      const int m = A.src[k];
+      const T Ce = A.C[k];
+      const T u0 = -A.u[3 * k], u1 = -A.u[3 * k + 1], u2 = -A.u[3 * k + 2];
+      T qm[V], gxm[V], g0[V], g1[V], g2[V], pk[V], dk[V], ddk[V];
+      ldv<T, V>(qm, A.q + (size_t)m * A.ldq + c0);
+      ldv<T, V>(gxm, A.gx + (size_t)m * A.H + c0);
+      const T* gvm = A.gvec + (size_t)m * 3 * A.H + c0;
+      ldv<T, V>(g0, gvm);
+      ldv<T, V>(g1, gvm + A.H);
+      ldv<T, V>(g2, gvm + 2 * A.H);
+      act<T, V>(A.pk + (size_t)k * A.ldpk + c0, hk, pk, dk, ddk, A.nt);
+      const T* pvs = A.pv + (size_t)k * A.ldpv + vo;
+      T px[V], dvx[V], dv1[V], dv2[V], dd[V];
+      act<T, V>(pvs, hv, px, dvx, dd, A.nt);
+      act<T, V>(pvs + A.d, hv, px, dv1, dd, A.nt);
+      act<T, V>(pvs + 2 * A.d, hv, px, dv2, dd, A.nt);
+      T part = T(0), ga = T(0);
 #pragma unroll
-    for (int i = 0; i < V; ++i) {
-      part += qm[i] * kk[i] * dk[i];
-      ga += gxm[i] * vx[i] * dvx[i];
-    }
-    part = group_sum(part, A.lph);
-    ga = group_sum(ga, A.lph);
-    const Silu<T> sa(part);
-    const T a = sa.s * Ce;
-    const T gs = ga * Ce * sa.d(part);
+      for (int i = 0; i < V; ++i) {
+        part += qm[i] * kk[i] * dk[i];
+        ga += gxm[i] * vx[i] * dvx[i];
+      }
+      part = group_sum(part, A.lph);
+      ga = group_sum(ga, A.lph);
+      const Silu<T> sa(part);
+      const T a = sa.s * Ce;
+      const T gs = ga * Ce * sa.d(part);
 #pragma unroll
-    for (int i = 0; i < V; ++i) {
-      gk[i] += gs * qm[i] * dk[i];
-      gvx[i] += gxm[i] * a * dvx[i];
-      const T gv1e = g0[i] * w0[i] + g1[i] * w1[i] + g2[i] * w2[i];
-      gv1[i] += gv1e * dv1[i];
-      const T gv2e = g0[i] * u0 + g1[i] * u1 + g2[i] * u2;
-      gv2[i] += gv2e * dv2[i];
-      const T v1e = v1[i] * dv1[i];
-      gw0[i] += g0[i] * v1e;
-      gw1[i] += g1[i] * v1e;
-      gw2[i] += g2[i] * v1e;
+      for (int i = 0; i < V; ++i) {
+        gk[i] += gs * qm[i] * dk[i];
+        gvx[i] += gxm[i] * a * dvx[i];
+        const T gv1e = g0[i] * w0[i] + g1[i] * w1[i] + g2[i] * w2[i];
+        gv1[i] += gv1e * dv1[i];
+        const T gv2e = g0[i] * u0 + g1[i] * u1 + g2[i] * u2;
+        gv2[i] += gv2e * dv2[i];
+        const T v1e = v1[i] * dv1[i];
+        gw0[i] += g0[i] * v1e;
+        gw1[i] += g1[i] * v1e;
+        gw2[i] += g2[i] * v1e;
+      }
     }
   }
-  if (on) {
+  xor_slots(gk, A.L); xor_slots(gvx, A.L); xor_slots(gv1, A.L); xor_slots(gv2, A.L); xor_slots(gw0, A.L); xor_slots(gw1, A.L); xor_slots(gw2, A.L);
+  T all[7 * V];
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    all[i] = gk[i]; all[V + i] = gvx[i]; all[2 * V + i] = gv1[i]; all[3 * V + i] = gv2[i];
+    all[4 * V + i] = gw0[i]; all[5 * V + i] = gw1[i]; all[6 * V + i] = gw2[i];
+  }
+  reduce_waves<T, S, 7 * V>(all, G.sub, lds);
+  if (j >= 0 && G.sub == 0 && on && G.es == 0) {
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+      gk[i] = all[i]; gvx[i] = all[V + i]; gv1[i] = all[2 * V + i]; gv2[i] = all[3 * V + i];
+      gw0[i] = all[4 * V + i]; gw1[i] = all[5 * V + i]; gw2[i] = all[6 * V + i];
+    }
     stv<T, V>(A.gk + (size_t)j * A.H + c0, gk);
     T* gvj = A.gv + (size_t)j * 3 * A.H + vo;
     stv<T, V>(gvj, gvx);
@@ -445,10 +594,64 @@ static int launch_v(int V, int n, AT A, hipStream_t st) {
   return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
 }
 
-template <typename T, int V> struct KFwd { static constexpr auto fn = k_fwd<T, V, false>; };
-template <typename T, int V> struct KFwdOrd { static constexpr auto fn = k_fwd<T, V, true>; };
-template <typename T, int V> struct KBwdDst { static constexpr auto fn = k_bwd_dst<T, V>; };
-template <typename T, int V> struct KBwdSrc { static constexpr auto fn = k_bwd_src<T, V>; };
+// ET launch: V = H/32 channels per lane (half-wave per edge), S waves per node (small systems get
+// S = 4 so that e.g. a 678-atom QM9 batch still puts ~2.7k waves on the 256 CUs).
+static inline int et_waves_per_node(int n, int bytes_per_lane_vec) {
+  if (bytes_per_lane_vec > 32) return 1;
+  if (n < 4096) return 4;
+  if (n < 8192) return 2;
+  return 1;
+}
+
+template <typename T, int V, int S, int KIND, bool ORD>
+static int et_launch_vs(Args<T> A, hipStream_t st) {
+  // channel groups: split heads across XCDs for large systems (L2 working-set), not for the
+  // destination pass (its per-edge channel sums would need a cross-group combine)
+  // channel groups (CS = 2 / 4) are supported by the kernels but measured neutral (+-1 %) on the
+  // C5 water box (tools/kbench.py), so one group is used.
+  int cs = 1;
+  if (KIND == 1 || A.H % (cs * V) || (A.H / cs / V) & (A.H / cs / V - 1) || A.H / cs / V < A.lph ||
+      A.H / cs / V > 64)
+    cs = 1;
+  A.HC = A.H / cs;
+  A.L = A.HC / V;
+  if (A.L > 64 || (A.L & (A.L - 1))) return kUnsupported;
+  const int nbn = (A.n + (4 / S) - 1) / (4 / S);
+  const dim3 g(nbn * cs), b(256);
+  if (cs == 4) {
+    if (KIND == 0) hipLaunchKernelGGL((k_fwd<T, V, S, 4, ORD>), g, b, 0, st, A);
+    else hipLaunchKernelGGL((k_bwd_src<T, V, S, 4>), g, b, 0, st, A);
+  } else if (cs == 2) {
+    if (KIND == 0) hipLaunchKernelGGL((k_fwd<T, V, S, 2, ORD>), g, b, 0, st, A);
+    else hipLaunchKernelGGL((k_bwd_src<T, V, S, 2>), g, b, 0, st, A);
+  } else {
+    if (KIND == 0) hipLaunchKernelGGL((k_fwd<T, V, S, 1, ORD>), g, b, 0, st, A);
+    else if (KIND == 1) hipLaunchKernelGGL((k_bwd_dst<T, V, S, 1>), g, b, 0, st, A);
+    else hipLaunchKernelGGL((k_bwd_src<T, V, S, 1>), g, b, 0, st, A);
+  }
+  return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
+}
+
+template <typename T, int V, int KIND, bool ORD>
+static int et_launch_v(const Args<T>& A, hipStream_t st) {
+  const int S = et_waves_per_node(A.n, (int)sizeof(T) * V);
+  if (S == 4) return et_launch_vs<T, V, (sizeof(T) * V <= 32 ? 4 : 1), KIND, ORD>(A, st);
+  if (S == 2) return et_launch_vs<T, V, (sizeof(T) * V <= 32 ? 2 : 1), KIND, ORD>(A, st);
+  return et_launch_vs<T, V, 1, KIND, ORD>(A, st);
+}
+
+template <typename T, int KIND, bool ORD>
+static int et_launch(int V, const Args<T>& A, hipStream_t st) {
+  if (A.n <= 0) return kOk;
+  switch (V) {
+    case 1: return et_launch_v<T, 1, KIND, ORD>(A, st);
+    case 2: return et_launch_v<T, 2, KIND, ORD>(A, st);
+    case 4: return et_launch_v<T, 4, KIND, ORD>(A, st);
+    case 8: return et_launch_v<T, 8, KIND, ORD>(A, st);
+  }
+  return kUnsupported;
+}
+
 template <typename T, int V> struct KNbFwd { static constexpr auto fn = k_nb_fwd<T, V>; };
 template <typename T, int V> struct KNbDst { static constexpr auto fn = k_nb_bwd_dst<T, V>; };
 template <typename T, int V> struct KNbSrc { static constexpr auto fn = k_nb_bwd_src<T, V>; };
@@ -459,18 +662,24 @@ static int setup(Args<T>& A, int n, int H, int heads, const int32_t* row_ptr, co
                  const void* vec, const void* pk, int ldpk, const void* pv, int ldpv, const void* C,
                  const void* u, const int32_t* order, int& V) {
   if (H <= 0 || heads <= 0 || H % heads) return kBadArgument;
-  V = pick_vec(H);
+  if (H % 32 == 0) V = H / 32;  // channels per lane, one edge per half-wave
+  else if (H < 32) V = 1;       // fewer channels than half-wave lanes: idle lanes
+  else return kUnsupported;
+
+  if (V != 1 && V != 2 && V != 4 && V != 8) return kUnsupported;
   const int d = H / heads;
-  while (V > 1 && (d % V)) V >>= 1;
-  if (H / V > TMD_WAVE) return kUnsupported;
+  if (d % V) return kUnsupported;
   const int lph = d / V;
-  if (lph & (lph - 1)) return kUnsupported;  // head must be a power-of-two lane group
-  if (!aligned<T>(q, ldq, V) || !aligned<T>(k, ldk, V) || !aligned<T>(v, ldv_, V) ||
-      !aligned<T>(pk, ldpk, V) || !aligned<T>(pv, ldpv, V) || !aligned<T>(vec, H, V))
+  if (lph & (lph - 1)) return kUnsupported;  // a head must be a power-of-two lane group
+  const int VA = V > 4 ? 4 : V;               // vector width of one load
+  if (!aligned<T>(q, ldq, VA) || !aligned<T>(k, ldk, VA) || !aligned<T>(v, ldv_, VA) ||
+      !aligned<T>(pk, ldpk, VA) || !aligned<T>(pv, ldpv, VA) || !aligned<T>(vec, H, VA))
     return kBadArgument;
   A = Args<T>{};
-  A.n = n; A.H = H; A.d = d; A.L = H / V; A.lph = lph; A.cap = cap;
+  A.n = n; A.H = H; A.d = d; A.L = H / V; A.HC = H; A.lph = lph; A.cap = cap;
   A.row_ptr = row_ptr; A.src = src; A.order = order;
+  A.xcd = 1;
+  A.nt = 0;
   A.q = (const T*)q; A.ldq = ldq; A.k = (const T*)k; A.ldk = ldk; A.v = (const T*)v; A.ldv = ldv_;
   A.vec = (const T*)vec; A.pk = (const T*)pk; A.ldpk = ldpk; A.pv = (const T*)pv; A.ldpv = ldpv;
   A.C = (const T*)C; A.u = (const T*)u;
@@ -489,7 +698,7 @@ static int fwd(int n, int H, int heads, const int32_t* row_ptr, const int32_t* s
   if (rc) return rc;
   A.xo = (T*)xo;
   A.veco = (T*)veco;
-  return order ? launch_v<T, KFwdOrd>(V, n, A, st) : launch_v<T, KFwd>(V, n, A, st);
+  return order ? et_launch<T, 0, true>(V, A, st) : et_launch<T, 0, false>(V, A, st);
 }
 
 template <typename T>
@@ -507,9 +716,9 @@ static int bwd(int n, int H, int heads, const int32_t* row_ptr, const int32_t* s
   A.gx = (const T*)gx; A.gvec = (const T*)gvec;
   A.gq = (T*)gq; A.gk = (T*)gk; A.gv = (T*)gv; A.gveci = (T*)gveci;
   A.gpk = (T*)gpk; A.gpv = (T*)gpv; A.gC = (T*)gC; A.gu = (T*)gu;
-  rc = launch_v<T, KBwdDst>(V, n, A, st);
+  rc = et_launch<T, 1, false>(V, A, st);
   if (rc) return rc;
-  return launch_v<T, KBwdSrc>(V, n, A, st);
+  return et_launch<T, 2, false>(V, A, st);
 }
 
 template <typename T>

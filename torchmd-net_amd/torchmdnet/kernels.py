@@ -31,7 +31,7 @@ class EdgeGraph:
     """
 
     def __init__(self, n_nodes, row_ptr, src, dst, transpose, deltas, distances, num_pairs,
-                 symmetric):
+                 symmetric, static=False):
         self.n_nodes = n_nodes
         self.row_ptr = row_ptr
         self.src = src
@@ -43,6 +43,14 @@ class EdgeGraph:
         self.symmetric = symmetric
         self.cutoff = None  # per-edge CosineCutoff, filled by the model (same for every layer)
         self._edge_index = None
+        # static (HIP-graph) mode: per-edge tensors are sized to the capacity, slots beyond the found
+        # pairs are inert padding (no CSR row references them) and every per-edge gradient buffer is
+        # zero-filled so padding rows contribute nothing to the weight-gradient GEMMs.
+        self.static = static
+        self.num_pairs_dev = None
+
+    def alloc_edge_grad(self, shape, dtype, device):
+        return (torch.zeros if self.static else torch.empty)(shape, dtype=dtype, device=device)
 
     @property
     def n_edges(self):
@@ -191,7 +199,7 @@ class _NeighborGeomBwd(Function):
     def backward(ctx, ggpos):
         pos, gd, gr, deltas, distances = ctx.saved_tensors
         graph = ctx.graph
-        src, dst = graph.src.long(), graph.dst.long()
+        src, dst = graph.src.long().clamp(min=0), graph.dst.long().clamp(min=0)  # padding -> 0 (masked)
         with torch.enable_grad():
             p = pos.detach().requires_grad_(True)
             gd_ = (torch.zeros_like(deltas) if gd is None else gd.detach()).requires_grad_(True)
@@ -208,10 +216,12 @@ class _NeighborGeomBwd(Function):
 
 
 def build_graph(pos, batch, cutoff_lower, cutoff_upper, max_num_pairs, loop=True, strategy="brute",
-                box=None, check_errors=True):
+                box=None, check_errors=True, static_capacity=None):
     """Symmetric (include_transpose) neighbour graph with CSR rows, transpose map and autograd
     deltas/distances.  Mirrors OptimizedDistance(return_vecs=True, resize_to_fit=True) semantics
-    (reference models/utils.py:207-269): one host sync reads num_pairs for the overflow check."""
+    (reference models/utils.py:207-269): one host sync reads num_pairs for the overflow check.
+    With ``static_capacity`` the graph is sync-free and HIP-graph capturable: every per-edge tensor
+    has ``static_capacity`` rows; overflow is reported on the device (``graph.overflow``)."""
     use_periodic = box is not None and box.numel() > 0
     if use_periodic:
         validate_box(box, cutoff_upper)
@@ -220,6 +230,19 @@ def build_graph(pos, batch, cutoff_lower, cutoff_upper, max_num_pairs, loop=True
         box = torch.tensor([[lbox, 0, 0], [0, lbox, 0], [0, 0, lbox]], dtype=torch.float64)
     if strategy == "brute" and pos.shape[0] >= 32768:
         strategy = "shared"
+    if static_capacity is not None:
+        cap = int(static_capacity)
+        nb, dl, dist, num, row_ptr, tr = neighbor_pairs_raw(
+            strategy, pos, batch, box, use_periodic, cutoff_lower, cutoff_upper, cap, loop,
+            True, pad_output=True, want_csr=True)
+        graph = EdgeGraph(pos.shape[0], row_ptr, nb[0], nb[1], tr, None, None, None, symmetric=True,
+                          static=True)
+        graph.num_pairs_dev = num
+        graph.overflow = num > cap
+        deltas, distances = _NeighborGeom.apply(pos, graph, dl, dist)
+        graph.deltas = deltas
+        graph.distances = distances
+        return graph
     nb, dl, dist, num, row_ptr, tr = neighbor_pairs_raw(
         strategy, pos, batch, box, use_periodic, cutoff_lower, cutoff_upper, max_num_pairs, loop,
         True, pad_output=False, want_csr=True)
@@ -364,6 +387,8 @@ def et_message_composite(q, k, v, vec, pk, pv, C, u, src, dst, n_nodes, heads):
     """PyTorch restatement of torchmd_et.py:314-347 (used for the second-order backward only)."""
     H = q.shape[1]
     d = H // heads
+    valid = (src >= 0).to(q.dtype)  # static-capacity padding slots (-1) carry no message
+    src, dst = src.clamp(min=0), dst.clamp(min=0)
     qi = q.index_select(0, dst).view(-1, heads, d)
     kj = k.index_select(0, src).view(-1, heads, d)
     s = qi * kj
@@ -374,9 +399,9 @@ def et_message_composite(q, k, v, vec, pk, pv, C, u, src, dst, n_nodes, heads):
     if pv is not None:
         vj = vj * F.silu(pv).view(-1, heads, 3 * d)
     x, v1, v2 = torch.split(vj, d, dim=2)
-    xm = x * attn.unsqueeze(2)
+    xm = x * (attn * valid.unsqueeze(1)).unsqueeze(2)
     vecj = vec.index_select(0, src).view(-1, 3, heads, d)
-    vm = vecj * v1.unsqueeze(1) + v2.unsqueeze(1) * u.view(-1, 3, 1, 1)
+    vm = (vecj * v1.unsqueeze(1) + v2.unsqueeze(1) * u.view(-1, 3, 1, 1)) * valid.view(-1, 1, 1, 1)
     xo = torch.zeros((n_nodes, heads, d), dtype=q.dtype, device=q.device).index_add(0, dst, xm)
     vo = torch.zeros((n_nodes, 3, heads, d), dtype=q.dtype, device=q.device).index_add(0, dst, vm)
     return xo.view(n_nodes, H), vo.view(n_nodes, 3, H)
@@ -435,10 +460,11 @@ class _ETMessageBwd(Function):
         gk = torch.empty((N, H), **o)
         gv = torch.empty((N, 3 * H), **o)
         gw = torch.empty((N, 3, H), **o)
-        gpk = torch.empty((E, H), **o) if pk is not None else torch.zeros(0, **o)
-        gpv = torch.empty((E, 3 * H), **o) if pv is not None else torch.zeros(0, **o)
-        gC = torch.empty((E,), **o)
-        gu = torch.empty((E, 3), **o)
+        ge = graph.alloc_edge_grad
+        gpk = ge((E, H), q.dtype, q.device) if pk is not None else torch.zeros(0, **o)
+        gpv = ge((E, 3 * H), q.dtype, q.device) if pv is not None else torch.zeros(0, **o)
+        gC = ge((E,), q.dtype, q.device)
+        gu = ge((E, 3), q.dtype, q.device)
         rc = lib.tmdnet_et_message_bwd(
             nat.dtype_code(q.dtype), N, H, heads, nat.ptr(graph.row_ptr), nat.ptr(graph.src), E,
             nat.ptr(q), _ld(q), nat.ptr(k), _ld(k), nat.ptr(v), _ld(v), nat.ptr(vec), nat.ptr(pk),
@@ -484,7 +510,8 @@ def et_message(q, k, v, vec, pk, pv, C, u, graph, heads):
 
 # ----------------------------------------------------------------------------- neighbour embedding
 def nbr_embed_composite(x, w, C, src, dst, n_nodes):
-    keep = (src != dst).to(x.dtype).unsqueeze(1)
+    keep = ((src != dst) & (src >= 0)).to(x.dtype).unsqueeze(1)
+    src, dst = src.clamp(min=0), dst.clamp(min=0)
     m = x.index_select(0, src) * (w * C.unsqueeze(1)) * keep
     return torch.zeros((n_nodes, x.shape[1]), dtype=x.dtype, device=x.device).index_add(0, dst, m)
 
@@ -519,8 +546,8 @@ class _NbrEmbedBwd(Function):
         N, H = x.shape
         E = graph.n_edges
         gx = torch.empty_like(x, memory_format=torch.contiguous_format)
-        gw = torch.empty((E, H), dtype=x.dtype, device=x.device)
-        gC = torch.empty((E,), dtype=x.dtype, device=x.device)
+        gw = graph.alloc_edge_grad((E, H), x.dtype, x.device)
+        gC = graph.alloc_edge_grad((E,), x.dtype, x.device)
         rc = lib.tmdnet_nbr_embed_bwd(nat.dtype_code(x.dtype), N, H, nat.ptr(graph.row_ptr),
                                       nat.ptr(graph.src), E, nat.ptr(x), _ld(x), nat.ptr(w), _ld(w),
                                       nat.ptr(C), nat.ptr(gout), nat.ptr(gx), nat.ptr(gw), nat.ptr(gC),
@@ -723,3 +750,32 @@ def tn_embed(P, Q, W, C, u, graph):
 
 def tn_message(ea, I, A, S, graph):
     return _TNMessage.apply(_rowmajor(ea), I.contiguous(), A.contiguous(), S.contiguous(), graph)
+
+
+# ----------------------------------------------------------------------------- spatial order
+REORDER_MIN_ATOMS = 16384
+
+
+def _spread10(x):
+    x = x & 0x3FF
+    x = (x | (x << 16)) & 0x030000FF
+    x = (x | (x << 8)) & 0x0300F00F
+    x = (x | (x << 4)) & 0x030C30C3
+    x = (x | (x << 2)) & 0x09249249
+    return x
+
+
+def spatial_permutation(pos, batch, cell_size, box=None):
+    """Permutation that renumbers atoms molecule-major, then by the Morton (Z-order) index of their
+    cutoff-sized cell.  Edge kernels gather source rows of spatial neighbours; with this numbering
+    the waves in flight on one XCD touch a compact window of rows (L2 reuse): +25-30 % on the
+    C5 water box vs random numbering (tools/kbench.py).  Sync-free (device argsort)."""
+    p = pos.detach()
+    if box is not None and box.numel() == 9:
+        L = torch.diagonal(box.to(p.device, p.dtype))
+        p = p - torch.floor(p / L) * L
+    lo = p.min(dim=0).values
+    c = torch.clamp(((p - lo) / float(cell_size)).long(), 0, 1023)
+    key = _spread10(c[:, 0]) | (_spread10(c[:, 1]) << 1) | (_spread10(c[:, 2]) << 2)
+    key = key + batch.to(torch.long) * (1 << 31)
+    return torch.argsort(key, stable=True)

@@ -78,6 +78,7 @@ class TensorNet(nn.Module):
         self.out_norm = nn.LayerNorm(3 * hidden_channels, dtype=dtype)
         self.act = act_class()
         self.static_shapes = static_shapes
+        self.reorder_atoms = True
         self.distance = OptimizedDistance(cutoff_lower, cutoff_upper, max_num_pairs=-max_num_neighbors,
                                           return_vecs=True, loop=True, check_errors=False,
                                           resize_to_fit=not self.static_shapes, long_edge_index=True)
@@ -92,6 +93,17 @@ class TensorNet(nn.Module):
 
     def forward(self, z: Tensor, pos: Tensor, batch: Tensor, q: Optional[Tensor] = None,
                 s: Optional[Tensor] = None) -> Tuple[Tensor, Optional[Tensor], Tensor, Tensor, Tensor]:
+        if self.reorder_atoms and z.shape[0] >= kernels.REORDER_MIN_ATOMS and not self.static_shapes:
+            # (static_shapes keeps the caller's numbering: its padding semantics single out atom 0)
+            perm = kernels.spatial_permutation(pos, batch, self.cutoff_upper,
+                                               self.distance.box if self.distance.use_periodic else None)
+            inv = torch.empty_like(perm)
+            inv[perm] = torch.arange(perm.numel(), device=perm.device)
+            x = self._forward(z[perm], pos.index_select(0, perm), batch[perm])
+            return x[inv], None, z, pos, batch
+        return self._forward(z, pos, batch), None, z, pos, batch
+
+    def _forward(self, z: Tensor, pos: Tensor, batch: Tensor) -> Tensor:
         graph = self.distance.graph(pos, batch)
         cap = self.distance._max_pairs(pos.shape[0])
         graph.self0_mult = float(1 + max(0, cap - graph.num_pairs)) if self.static_shapes else 1.0
@@ -110,8 +122,7 @@ class TensorNet(nn.Module):
         I, A, S = decompose_tensor(X)
         x = torch.cat((tensor_norm(I), tensor_norm(A), tensor_norm(S)), dim=-1)
         x = self.out_norm(x)
-        x = self.act(self.linear(x))
-        return x, None, z, pos, batch
+        return self.act(self.linear(x))
 
 
 def _check_symmetric_graph(edge_index, n):

@@ -70,6 +70,7 @@ class TorchMD_ET(nn.Module):
             self.attention_layers.append(layer)
 
         self.out_norm = nn.LayerNorm(hidden_channels, dtype=dtype)
+        self.reorder_atoms = True
         self.reset_parameters()
 
     def reset_parameters(self):
@@ -83,6 +84,20 @@ class TorchMD_ET(nn.Module):
 
     def forward(self, z: Tensor, pos: Tensor, batch: Tensor, q: Optional[Tensor] = None,
                 s: Optional[Tensor] = None) -> Tuple[Tensor, Tensor, Tensor, Tensor, Tensor]:
+        perm = None
+        if self.reorder_atoms and z.shape[0] >= kernels.REORDER_MIN_ATOMS:
+            # large systems: compute in a spatially coherent atom numbering (edge-kernel locality);
+            # outputs are returned in the caller's order, forces flow back through the gather.
+            perm = kernels.spatial_permutation(pos, batch, self.cutoff_upper,
+                                               self.distance.box if self.distance.use_periodic else None)
+            inv = torch.empty_like(perm)
+            inv[perm] = torch.arange(perm.numel(), device=perm.device)
+            x, vec = self._forward(z[perm], pos.index_select(0, perm), batch[perm])
+            return x[inv], vec[inv], z, pos, batch
+        x, vec = self._forward(z, pos, batch)
+        return x, vec, z, pos, batch
+
+    def _forward(self, z: Tensor, pos: Tensor, batch: Tensor):
         x = self.embedding(z)
         graph = self.distance.graph(pos, batch)
         de = self.distance_expansion
@@ -103,7 +118,7 @@ class TorchMD_ET(nn.Module):
             x = x + dx
             vec = vec + dvec
         x = self.out_norm(x)
-        return x, vec, z, pos, batch
+        return x, vec
 
     def __repr__(self):
         return (f"{self.__class__.__name__}(hidden_channels={self.hidden_channels}, "

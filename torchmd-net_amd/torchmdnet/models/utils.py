@@ -195,6 +195,8 @@ class OptimizedDistance(torch.nn.Module):
         self.box = self.box.cpu()
         self.check_errors = check_errors
         self.long_edge_index = long_edge_index
+        # HIP-graph mode (torchmdnet.graphs): fixed edge capacity, no host synchronisation
+        self.static_capacity = None
 
     def _max_pairs(self, n):
         return -self.max_num_pairs * n if self.max_num_pairs < 0 else self.max_num_pairs
@@ -233,9 +235,12 @@ class OptimizedDistance(torch.nn.Module):
         strategy = self.strategy
         if strategy == "cell" and not self.use_periodic:
             box = None
-        return kernels.build_graph(pos, batch, self.cutoff_lower, self.cutoff_upper,
-                                   self._max_pairs(pos.shape[0]), loop=self.loop, strategy=strategy,
-                                   box=box, check_errors=self.check_errors)
+        g = kernels.build_graph(pos, batch, self.cutoff_lower, self.cutoff_upper,
+                                self._max_pairs(pos.shape[0]), loop=self.loop, strategy=strategy,
+                                box=box, check_errors=self.check_errors,
+                                static_capacity=self.static_capacity)
+        self.last_graph = g
+        return g
 
 
 class NeighborEmbedding(nn.Module):
