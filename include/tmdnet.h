@@ -25,6 +25,7 @@ enum { TMDNET_OK = 0, TMDNET_BAD_ARGUMENT = 1, TMDNET_UNSUPPORTED = 2, TMDNET_LA
 enum { TMDNET_F32 = 0, TMDNET_F64 = 1 };
 enum { TMDNET_NL_BRUTE = 0, TMDNET_NL_SHARED = 1, TMDNET_NL_CELL = 2 };
 enum { TMDNET_RBF_EXPNORM = 0, TMDNET_RBF_GAUSS = 1 };
+enum { TMDNET_ACC_VEC_RESIDUAL = 1, TMDNET_ACC_EDGE = 2 };
 
 /* ------------------------------------------------------------------------------------------
  * Neighbour list.  Replaces torchmdnet_neighbors::get_neighbor_pairs
@@ -100,14 +101,32 @@ int tmdnet_et_message_fwd(int dtype, int n_nodes, int hidden, int heads, const i
                           void* x_out, void* vec_out, const int32_t* order, void* stream);
 /* Backward (two CSR passes, no atomics): destination pass -> gq, gpk, gpv, gcut, gunit; source
  * pass (requires a symmetric edge list, dk/dv/cutoff functions of |r| only) -> gk, gv, gvec_in.
- * grad buffers are overwritten; gpk/gpv are gradients of the PRE-activation projections. */
+ * Gradients are written with the leading dimension of the matching input (gq: ld_q, gk: ld_k,
+ * gv: ld_v, gpk: ld_pk, gpv: ld_pv), so they can land directly in fused [q|k|v] / [dk|dv]
+ * gradient buffers; gpk/gpv are gradients of the PRE-activation projections.
+ * vec_in may be NULL (vec == 0, the first layer): its terms vanish and gvec_in is not written
+ * (gvec_in may also be NULL).  accumulate (TMDNET_ACC_* bits): VEC_RESIDUAL -> gvec_in =
+ * grad_vec + message part (the layer's identity residual); EDGE -> gcut/gunit are accumulated
+ * (+=) instead of overwritten (one buffer shared by all layers).  Other buffers: overwritten. */
 int tmdnet_et_message_bwd(int dtype, int n_nodes, int hidden, int heads, const int32_t* row_ptr,
                           const int32_t* src, int max_pairs, const void* q, int ld_q, const void* k,
                           int ld_k, const void* v, int ld_v, const void* vec_in, const void* pk,
                           int ld_pk, const void* pv, int ld_pv, const void* cutoff, const void* unit,
                           const void* grad_x, const void* grad_vec, void* gq, void* gk, void* gv,
                           void* gvec_in, void* gpk, void* gpv, void* gcut, void* gunit,
-                          const int32_t* order, void* stream);
+                          int accumulate, const int32_t* order, void* stream);
+
+/* ET layer epilogue (reference torchmd_et.py:278-280, 309-311 + residuals 181-184), fused:
+ *   vecp = vec_proj(vec) [N][3][3H] = [v1|v2|v3], o = o_proj(x_agg) [N][3H] = [o1|o2|o3]
+ *   x_out = x + (sum_a v1*v2) * o2 + o3;  vec_out = vec + v3 * o1 + vec_agg.
+ * vec and vecp may be NULL (vec == 0). */
+int tmdnet_et_epilogue_fwd(int dtype, int n_nodes, int hidden, const void* x, const void* vec,
+                           const void* vecp, const void* o, const void* vec_agg, void* x_out,
+                           void* vec_out, void* stream);
+/* Backward of the epilogue: grad_vecp [N][3][3H], grad_o [N][3H] (x, vec, vec_agg pass through). */
+int tmdnet_et_epilogue_bwd(int dtype, int n_nodes, int hidden, const void* grad_x,
+                           const void* grad_vec, const void* vecp, const void* o, void* grad_vecp,
+                           void* grad_o, void* stream);
 
 /* Neighbour embedding aggregation (reference NeighborEmbedding.forward/message,
  *   models/utils.py:73-108):  out[t] = sum_{e in row t, src!=dst} X[src[e]] * W[e] * C[e]

@@ -1,0 +1,230 @@
+"""CPU check of the ET stack's hand-scheduled forward/backward ORCHESTRATION (torchmdnet/et_stack.py).
+
+The four native launches the stack makes (ET message fwd/bwd, epilogue fwd/bwd) are replaced, in
+this test only, by composite PyTorch emulations with the kernels' documented buffer semantics
+(strided gradient outputs, TMDNET_ACC_* accumulation, vec == NULL).  What is verified is everything
+around them: fused/stacked GEMMs, gradient accumulation across layers, layer-norm backward, the
+weight-gradient gating and the composite double backward, against plain autograd over the
+reference math.  The kernels themselves are checked on the GPU (test_gpu_parity.py).
+"""
+import math
+
+import pytest
+import torch
+
+from torchmdnet import _native as nat
+from torchmdnet import et_stack as ES
+from torchmdnet import kernels
+from torchmdnet.models.torchmd_et import EquivariantMultiHeadAttention
+
+DT = torch.float64
+
+
+def _fake_fwd(q, k, v, vec, pk, pv, C, u, graph, heads, xo, vo):
+    N, H = q.shape
+    vec_ = torch.zeros((N, 3, H), dtype=q.dtype) if vec is None else vec
+    a, b = kernels.et_message_composite(q, k, v, vec_, pk, pv, C, u, graph.src.long(), graph.dst.long(),
+                                        N, heads)
+    xo.copy_(a)
+    vo.copy_(b)
+
+
+def _fake_bwd(q, k, v, vec, pk, pv, C, u, graph, heads, gx, gvec, gq, gk, gv, gw, gpk, gpv, gC, gu,
+              accumulate=0):
+    N, H = q.shape
+    with torch.enable_grad():
+        ins = [None if t is None else t.detach().clone().requires_grad_(True)
+               for t in (q, k, v, vec, pk, pv, C, u)]
+        vec_ = torch.zeros((N, 3, H), dtype=q.dtype) if vec is None else ins[3]
+        xo, vo = kernels.et_message_composite(ins[0], ins[1], ins[2], vec_, ins[4], ins[5], ins[6], ins[7],
+                                              graph.src.long(), graph.dst.long(), N, heads)
+        live = [t for t in ins if t is not None]
+        g = torch.autograd.grad((xo, vo), live, (gx, gvec), allow_unused=True)
+    it = iter(g)
+    g = [next(it) if t is not None else None for t in ins]
+    z = lambda t, ref: torch.zeros_like(ref) if t is None else t  # noqa: E731
+    gq.copy_(z(g[0], q))
+    gk.copy_(z(g[1], k))
+    gv.copy_(z(g[2], v))
+    if gw is not None:
+        gw.copy_(z(g[3], gw) + (gvec if accumulate & nat.ACC_VEC_RESIDUAL else 0))
+    if gpk is not None:
+        gpk.copy_(z(g[4], pk))
+    if gpv is not None:
+        gpv.copy_(z(g[5], pv))
+    if accumulate & nat.ACC_EDGE:
+        gC.add_(g[6])
+        gu.add_(g[7])
+    else:
+        gC.copy_(g[6])
+        gu.copy_(g[7])
+
+
+def _fake_epi_fwd(x, vec, vecp, o, veca):
+    H = x.shape[1]
+    o1, o2, o3 = o[:, :H], o[:, H:2 * H], o[:, 2 * H:]
+    if vecp is None:
+        return x + o3, veca.clone()
+    v1, v2, v3 = vecp[..., :H], vecp[..., H:2 * H], vecp[..., 2 * H:]
+    return x + (v1 * v2).sum(1) * o2 + o3, vec + v3 * o1.unsqueeze(1) + veca
+
+
+def _fake_epi_bwd(gx, gvec, vecp, o, g_vecp, g_o):
+    H = gx.shape[1]
+    o1, o2 = o[:, :H], o[:, H:2 * H]
+    if vecp is None:
+        g_o.zero_()
+        g_o[:, 2 * H:] = gx
+        return
+    v1, v2, v3 = vecp[..., :H], vecp[..., H:2 * H], vecp[..., 2 * H:]
+    g_o[:, :H] = (gvec * v3).sum(1)
+    g_o[:, H:2 * H] = gx * (v1 * v2).sum(1)
+    g_o[:, 2 * H:] = gx
+    gd = (gx * o2).unsqueeze(1)
+    g_vecp[..., :H] = gd * v2
+    g_vecp[..., H:2 * H] = gd * v1
+    g_vecp[..., 2 * H:] = gvec * o1.unsqueeze(1)
+
+
+@pytest.fixture
+def emulated(monkeypatch):
+    monkeypatch.setattr(kernels, "et_message_fwd_launch", _fake_fwd)
+    monkeypatch.setattr(kernels, "et_message_bwd_launch", _fake_bwd)
+    monkeypatch.setattr(ES, "_epilogue_fwd", _fake_epi_fwd)
+    monkeypatch.setattr(ES, "_epilogue_bwd", _fake_epi_bwd)
+
+
+def _system(n_mol=3, seed=0, cutoff=4.0):
+    g = torch.Generator().manual_seed(seed)
+    sizes = [5, 7, 4][:n_mol]
+    pos = torch.cat([torch.randn(s, 3, generator=g, dtype=DT) * 1.3 for s in sizes])
+    batch = torch.cat([torch.full((s,), i, dtype=torch.long) for i, s in enumerate(sizes)])
+    d = (pos[:, None] - pos[None]).norm(dim=-1)
+    adj = (d < cutoff) & (batch[:, None] == batch[None])
+    ei = adj.nonzero().t().contiguous()  # includes self loops (loop=True)
+    graph, perm = kernels.EdgeGraph.from_edge_index(ei, pos.shape[0])
+    ei = ei[:, perm]
+    vecs = pos[ei[0]] - pos[ei[1]]
+    r = vecs.norm(dim=-1)
+    return pos.shape[0], graph, r, vecs
+
+
+def _inputs(n, graph, r, vecs, H, R, seed=1):
+    g = torch.Generator().manual_seed(seed)
+    mu = torch.linspace(0, 4, R, dtype=DT)
+    f = torch.exp(-((r[:, None] - mu) ** 2))  # symmetric per-edge features
+    C = 0.5 * (torch.cos(r * math.pi / 4.0) + 1.0)
+    u = torch.where((r > 0)[:, None], vecs / torch.where(r > 0, r, torch.ones_like(r))[:, None], vecs)
+    x = torch.randn(n, H, generator=g, dtype=DT)
+    return x, f, C, u
+
+
+def _layers(n_layers, H, R, heads, infl, seed=2):
+    torch.manual_seed(seed)
+    layers = torch.nn.ModuleList([
+        EquivariantMultiHeadAttention(H, R, infl, heads, torch.nn.SiLU, "silu", 0.0, 4.0, DT)
+        for _ in range(n_layers)])
+    with torch.no_grad():  # non-trivial biases / norms
+        for p in layers.parameters():
+            p.add_(0.1 * torch.randn_like(p))
+    return layers
+
+
+def _meta_for(layers, graph):
+    l0 = layers[0]
+    return ES._Meta(graph, l0.num_heads, l0.hidden_channels, l0.dk_proj is not None, l0.dv_proj is not None,
+                    len(layers), None, None)
+
+
+@pytest.mark.parametrize("infl", ["both", "keys", "values", "none"])
+def test_stack_forward_and_grads_match_composite(emulated, infl):
+    H, R, heads = 16, 8, 4
+    n, graph, r, vecs = _system()
+    x, f, C, u = _inputs(n, graph, r, vecs, H, R)
+    layers = _layers(3, H, R, heads, infl)
+    params = [p for l in layers for p in ES.layer_params(l)]
+    leaves = [t.clone().requires_grad_(True) for t in (x, f, C, u)]
+    xo, vo = ES.et_stack(layers, leaves[0], graph, leaves[1], leaves[2], leaves[3])
+    meta = _meta_for(layers, graph)
+    ref_leaves = [t.clone().requires_grad_(True) for t in (x, f, C, u)]
+    xr, vr = ES.composite_stack(meta, *ref_leaves, params)
+    assert torch.allclose(xo, xr, atol=1e-12) and torch.allclose(vo, vr, atol=1e-12)
+    gx, gv = torch.randn_like(xo), torch.randn_like(vo)
+    wrt = leaves if infl != "none" else [leaves[0], leaves[2], leaves[3]]
+    rwrt = ref_leaves if infl != "none" else [ref_leaves[0], ref_leaves[2], ref_leaves[3]]
+    a = torch.autograd.grad((xo, vo), wrt + params, (gx, gv), allow_unused=True)
+    b = torch.autograd.grad((xr, vr), rwrt + params, (gx, gv), allow_unused=True)
+    for i, (ga, gb) in enumerate(zip(a, b)):
+        if gb is None:
+            assert ga is None or torch.count_nonzero(ga) == 0, i
+            continue
+        assert torch.allclose(ga, gb, atol=1e-11, rtol=1e-9), i
+
+
+def test_stack_stacked_parameters_alias_and_survive_updates(emulated):
+    H, R, heads = 16, 8, 4
+    n, graph, r, vecs = _system()
+    x, f, C, u = _inputs(n, graph, r, vecs, H, R)
+    layers = _layers(2, H, R, heads, "both")
+    ES.et_stack(layers, x, graph, f, C, u)
+    lw = layers[0]._stacked
+    qkv = lw.bufs["qkv_w"]
+    assert layers[0].k_proj.weight.data_ptr() == qkv.data_ptr() + H * H * qkv.element_size()
+    with torch.no_grad():  # optimiser-style in-place update shows through the stacked buffer
+        layers[0].k_proj.weight.add_(1.0)
+    assert torch.equal(qkv[H:2 * H], layers[0].k_proj.weight)
+    sd = {k: v.clone() for k, v in layers.state_dict().items()}
+    layers.load_state_dict(sd)
+    assert lw.bufs["qkv_w"] is qkv  # in-place load keeps the aliasing
+
+
+def test_stack_force_pass_skips_weight_grads_but_training_gets_them(emulated):
+    """autograd.grad wrt inputs: weight gradients not requested -> not computed; loss.backward
+    through a create_graph force pass -> weight gradients equal the composite reference."""
+    H, R, heads = 16, 8, 4
+    n, graph, r, vecs = _system()
+    x, f, C, u = _inputs(n, graph, r, vecs, H, R)
+    layers = _layers(2, H, R, heads, "both")
+    params = [p for l in layers for p in ES.layer_params(l)]
+    calls = []
+    orig = ES._backward_layers
+
+    def spy(meta, gX, gV, f_, C_, u_, params_, acts, need_ws):
+        calls.append(tuple(need_ws))
+        return orig(meta, gX, gV, f_, C_, u_, params_, acts, need_ws)
+
+    ES._backward_layers = spy
+    try:
+        outs = []
+        for fused in (True, False):
+            leaves = [t.clone().requires_grad_(True) for t in (x, f, C, u)]
+            if fused:
+                xo, vo = ES.et_stack(layers, leaves[0], graph, leaves[1], leaves[2], leaves[3])
+            else:
+                xo, vo = ES.composite_stack(_meta_for(layers, graph), *leaves, params)
+            e = (xo ** 2).sum() + (vo ** 2).sum()
+            g = torch.autograd.grad(e, leaves, create_graph=True)
+            loss = e + sum((gi ** 2).sum() for gi in g)
+            for p in params:
+                p.grad = None
+            loss.backward()
+            outs.append([p.grad.clone() for p in params])
+    finally:
+        ES._backward_layers = orig
+    assert calls[0] == (False, False)  # the force pass
+    assert calls[1] == (True, True)    # loss.backward
+    for a, b in zip(*outs):
+        assert torch.allclose(a, b, atol=1e-10, rtol=1e-8)
+
+
+def test_stack_partial_parameter_request(emulated):
+    H, R, heads = 16, 8, 4
+    n, graph, r, vecs = _system()
+    x, f, C, u = _inputs(n, graph, r, vecs, H, R)
+    layers = _layers(2, H, R, heads, "both")
+    xo, vo = ES.et_stack(layers, x, graph, f, C, u)
+    (g,) = torch.autograd.grad(xo.sum() + vo.sum(), [layers[1].o_proj.weight])
+    xr, vr = ES.composite_stack(_meta_for(layers, graph), x, f, C, u,
+                                [p for l in layers for p in ES.layer_params(l)])
+    (gr,) = torch.autograd.grad(xr.sum() + vr.sum(), [layers[1].o_proj.weight])
+    assert torch.allclose(g, gr, atol=1e-11)

@@ -444,3 +444,33 @@ def test_large_system_spatial_reorder_is_transparent():
     assert n >= kernels.REORDER_MIN_ATOMS
     assert _rel(out[0][0].cpu(), out[1][0].cpu()) < 1e-10
     assert _rel(out[0][1].cpu(), out[1][1].cpu()) < 1e-9
+
+
+@pytest.mark.parametrize("infl", ["both", "keys", "values", "none"])
+def test_et_fused_stack_matches_per_layer_path(infl):
+    """et_stack (one autograd node, fused GEMMs + HIP epilogue) == the per-layer module path:
+    energies, forces and force-loss training gradients (double backward), fp64."""
+    from torchmdnet.models.model import create_model
+    _seed()
+    m = create_model(yaml_args("equivariant-transformer", embedding_dimension=64, num_layers=3, num_rbf=16,
+                               num_heads=4, derivative=True, output_model="Scalar", precision=64,
+                               distance_influence=infl)).to(DEV)
+    z, pos, batch = O.qm9_like(4)
+    z, pos, batch = z.to(DEV), pos.to(DEV), batch.to(DEV)
+    res = []
+    for fused in (True, False):
+        m.representation_model.fused_stack = fused
+        y, f = m(z, pos.clone(), batch)
+        loss = (y ** 2).sum() + (f ** 2).sum()
+        m.zero_grad(set_to_none=True)
+        loss.backward()
+        res.append((y.detach(), f.detach(), [None if p.grad is None else p.grad.clone() for p in m.parameters()]))
+    m.representation_model.fused_stack = True
+    (y1, f1, g1), (y2, f2, g2) = res
+    assert _rel(y1.cpu(), y2.cpu()) < 1e-10
+    assert _rel(f1.cpu(), f2.cpu()) < 1e-10
+    for a, b in zip(g1, g2):
+        if a is None or b is None:
+            assert (a is None or torch.count_nonzero(a) == 0) and (b is None or torch.count_nonzero(b) == 0)
+            continue
+        assert _rel(a.cpu(), b.cpu()) < 1e-9  # norm-relative: gradients reach 1e13 here

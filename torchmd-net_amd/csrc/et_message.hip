@@ -94,6 +94,7 @@ template <typename T> struct Args {
   // backward inputs / outputs
   const T* gx; const T* gvec;
   T* gq; T* gk; T* gv; T* gveci; T* gpk; T* gpv; T* gC; T* gu;
+  int acc;  // TMDNET_ACC_* flags of the backward
 };
 
 // silu of the pre-activation, or 1 when the projection is absent
@@ -222,7 +223,7 @@ __global__ __launch_bounds__(256) void k_fwd(Args<T> A) {
   const int c0 = G.cg * A.HC + G.el * V;
   const int hh = c0 / A.d, cc = c0 % A.d;
   const int vo = hh * 3 * A.d + cc;
-  const bool hk = A.pk != nullptr, hv = A.pv != nullptr;
+  const bool hk = A.pk != nullptr, hv = A.pv != nullptr, hw = A.vec != nullptr;
   T ax[V], a0[V], a1[V], a2[V];
   zero(ax); zero(a0); zero(a1); zero(a2);
   if (t >= 0) {
@@ -245,11 +246,15 @@ __global__ __launch_bounds__(256) void k_fwd(Args<T> A) {
       act<T, V>(pvs, hv, px, dvx, dd, A.nt);
       act<T, V>(pvs + A.d, hv, px, dv1, dd, A.nt);
       act<T, V>(pvs + 2 * A.d, hv, px, dv2, dd, A.nt);
-      const T* vecs = A.vec + (size_t)s * 3 * A.H + c0;
       T w0[V], w1[V], w2[V];
-      ldv<T, V>(w0, vecs);
-      ldv<T, V>(w1, vecs + A.H);
-      ldv<T, V>(w2, vecs + 2 * A.H);
+      if (hw) {
+        const T* vecs = A.vec + (size_t)s * 3 * A.H + c0;
+        ldv<T, V>(w0, vecs);
+        ldv<T, V>(w1, vecs + A.H);
+        ldv<T, V>(w2, vecs + 2 * A.H);
+      } else {
+        zero(w0); zero(w1); zero(w2);
+      }
       T part = T(0);
 #pragma unroll
       for (int i = 0; i < V; ++i) part += q[i] * kk[i] * dk[i];
@@ -293,7 +298,7 @@ __global__ __launch_bounds__(256) void k_bwd_dst(Args<T> A) {
   const int c0 = G.cg * A.HC + G.el * V;
   const int hh = c0 / A.d, cc = c0 % A.d;
   const int vo = hh * 3 * A.d + cc;
-  const bool hk = A.pk != nullptr, hv = A.pv != nullptr;
+  const bool hk = A.pk != nullptr, hv = A.pv != nullptr, hw = A.vec != nullptr;
   const bool head_leader = on && (G.el % A.lph) == 0;
   T gq[V];
   zero(gq);
@@ -322,11 +327,15 @@ __global__ __launch_bounds__(256) void k_bwd_dst(Args<T> A) {
       act<T, V>(pvs, hv, px, dvx, ddx, A.nt);
       act<T, V>(pvs + A.d, hv, p1, dv1, dd1, A.nt);
       act<T, V>(pvs + 2 * A.d, hv, p2, dv2, dd2, A.nt);
-      const T* vecs = A.vec + (size_t)s * 3 * A.H + c0;
       T w0[V], w1[V], w2[V];
-      ldv<T, V>(w0, vecs);
-      ldv<T, V>(w1, vecs + A.H);
-      ldv<T, V>(w2, vecs + 2 * A.H);
+      if (hw) {
+        const T* vecs = A.vec + (size_t)s * 3 * A.H + c0;
+        ldv<T, V>(w0, vecs);
+        ldv<T, V>(w1, vecs + A.H);
+        ldv<T, V>(w2, vecs + 2 * A.H);
+      } else {
+        zero(w0); zero(w1); zero(w2);
+      }
       T part = T(0), ga = T(0), gu0 = T(0), gu1 = T(0), gu2 = T(0);
 #pragma unroll
       for (int i = 0; i < V; ++i) {
@@ -358,25 +367,32 @@ __global__ __launch_bounds__(256) void k_bwd_dst(Args<T> A) {
       gu1 = group_sum(gu1, A.L);
       gu2 = group_sum(gu2, A.L);
       if (on) {
-        if (hk) stv<T, V>(A.gpk + (size_t)k * A.H + c0, gpk);
+        if (hk) stv<T, V>(A.gpk + (size_t)k * A.ldpk + c0, gpk);
         if (hv) {
-          T* gp = A.gpv + (size_t)k * 3 * A.H + vo;
+          T* gp = A.gpv + (size_t)k * A.ldpv + vo;
           stv<T, V>(gp, gpx);
           stv<T, V>(gp + A.d, gp1);
           stv<T, V>(gp + 2 * A.d, gp2);
         }
       }
       if (G.el == 0) {
-        A.gC[k] = gc;
-        A.gu[3 * k] = gu0;
-        A.gu[3 * k + 1] = gu1;
-        A.gu[3 * k + 2] = gu2;
+        if (A.acc & TMDNET_ACC_EDGE) {
+          A.gC[k] += gc;
+          A.gu[3 * k] += gu0;
+          A.gu[3 * k + 1] += gu1;
+          A.gu[3 * k + 2] += gu2;
+        } else {
+          A.gC[k] = gc;
+          A.gu[3 * k] = gu0;
+          A.gu[3 * k + 1] = gu1;
+          A.gu[3 * k + 2] = gu2;
+        }
       }
     }
   }
   xor_slots(gq, A.L);
   reduce_waves<T, S, V>(gq, G.sub, lds);
-  if (t >= 0 && G.sub == 0 && on && G.es == 0) stv<T, V>(A.gq + (size_t)t * A.H + c0, gq);
+  if (t >= 0 && G.sub == 0 && on && G.es == 0) stv<T, V>(A.gq + (size_t)t * A.ldq + c0, gq);
 }
 
 // ------------------------------------------------------------------ backward, source pass
@@ -392,7 +408,7 @@ __global__ __launch_bounds__(256) void k_bwd_src(Args<T> A) {
   const int c0 = G.cg * A.HC + G.el * V;
   const int hh = c0 / A.d, cc = c0 % A.d;
   const int vo = hh * 3 * A.d + cc;
-  const bool hk = A.pk != nullptr, hv = A.pv != nullptr;
+  const bool hk = A.pk != nullptr, hv = A.pv != nullptr, hw = A.vec != nullptr;
   T gk[V], gvx[V], gv1[V], gv2[V], gw0[V], gw1[V], gw2[V];
   zero(gk); zero(gvx); zero(gv1); zero(gv2); zero(gw0); zero(gw1); zero(gw2);
   if (j >= 0) {
@@ -402,10 +418,14 @@ __global__ __launch_bounds__(256) void k_bwd_src(Args<T> A) {
     ldv<T, V>(vx, vj);
     ldv<T, V>(v1, vj + A.d);
     ldv<T, V>(v2, vj + 2 * A.d);
-    const T* vecj = A.vec + (size_t)j * 3 * A.H + c0;
-    ldv<T, V>(w0, vecj);
-    ldv<T, V>(w1, vecj + A.H);
-    ldv<T, V>(w2, vecj + 2 * A.H);
+    if (hw) {
+      const T* vecj = A.vec + (size_t)j * 3 * A.H + c0;
+      ldv<T, V>(w0, vecj);
+      ldv<T, V>(w1, vecj + A.H);
+      ldv<T, V>(w2, vecj + 2 * A.H);
+    } else {
+      zero(w0); zero(w1); zero(w2);
+    }
     const int b = min(A.row_ptr[j], A.cap), e = min(A.row_ptr[j + 1], A.cap);
     for (int k = b + EPW * G.sub + G.es; k < e; k += EPW * S) {
       const int m = A.src[k];
@@ -464,15 +484,26 @@ __global__ __launch_bounds__(256) void k_bwd_src(Args<T> A) {
       gk[i] = all[i]; gvx[i] = all[V + i]; gv1[i] = all[2 * V + i]; gv2[i] = all[3 * V + i];
       gw0[i] = all[4 * V + i]; gw1[i] = all[5 * V + i]; gw2[i] = all[6 * V + i];
     }
-    stv<T, V>(A.gk + (size_t)j * A.H + c0, gk);
-    T* gvj = A.gv + (size_t)j * 3 * A.H + vo;
+    stv<T, V>(A.gk + (size_t)j * A.ldk + c0, gk);
+    T* gvj = A.gv + (size_t)j * A.ldv + vo;
     stv<T, V>(gvj, gvx);
     stv<T, V>(gvj + A.d, gv1);
     stv<T, V>(gvj + 2 * A.d, gv2);
-    T* gwj = A.gveci + (size_t)j * 3 * A.H + c0;
-    stv<T, V>(gwj, gw0);
-    stv<T, V>(gwj + A.H, gw1);
-    stv<T, V>(gwj + 2 * A.H, gw2);
+    if (A.gveci != nullptr) {
+      if (A.acc & TMDNET_ACC_VEC_RESIDUAL) {  // gvec_in = grad_vec (residual path) + message part
+        const T* gr = A.gvec + (size_t)j * 3 * A.H + c0;
+        T r0[V], r1[V], r2[V];
+        ldv<T, V>(r0, gr);
+        ldv<T, V>(r1, gr + A.H);
+        ldv<T, V>(r2, gr + 2 * A.H);
+#pragma unroll
+        for (int i = 0; i < V; ++i) { gw0[i] += r0[i]; gw1[i] += r1[i]; gw2[i] += r2[i]; }
+      }
+      T* gwj = A.gveci + (size_t)j * 3 * A.H + c0;
+      stv<T, V>(gwj, gw0);
+      stv<T, V>(gwj + A.H, gw1);
+      stv<T, V>(gwj + 2 * A.H, gw2);
+    }
   }
 }
 
@@ -706,8 +737,8 @@ static int bwd(int n, int H, int heads, const int32_t* row_ptr, const int32_t* s
                const void* q, int ldq, const void* k, int ldk, const void* v, int ldv_,
                const void* vec, const void* pk, int ldpk, const void* pv, int ldpv, const void* C,
                const void* u, const void* gx, const void* gvec, void* gq, void* gk, void* gv,
-               void* gveci, void* gpk, void* gpv, void* gC, void* gu, const int32_t* order,
-               hipStream_t st) {
+               void* gveci, void* gpk, void* gpv, void* gC, void* gu, int acc,
+               const int32_t* order, hipStream_t st) {
   Args<T> A;
   int V;
   int rc = setup<T>(A, n, H, heads, row_ptr, src, cap, q, ldq, k, ldk, v, ldv_, vec, pk, ldpk, pv,
@@ -716,6 +747,7 @@ static int bwd(int n, int H, int heads, const int32_t* row_ptr, const int32_t* s
   A.gx = (const T*)gx; A.gvec = (const T*)gvec;
   A.gq = (T*)gq; A.gk = (T*)gk; A.gv = (T*)gv; A.gveci = (T*)gveci;
   A.gpk = (T*)gpk; A.gpv = (T*)gpv; A.gC = (T*)gC; A.gu = (T*)gu;
+  A.acc = acc;
   rc = et_launch<T, 1, false>(V, A, st);
   if (rc) return rc;
   return et_launch<T, 2, false>(V, A, st);
@@ -761,16 +793,17 @@ extern "C" int tmdnet_et_message_bwd(int dtype, int n_nodes, int hidden, int hea
                                      const void* pv, int ld_pv, const void* cutoff, const void* unit,
                                      const void* grad_x, const void* grad_vec, void* gq, void* gk,
                                      void* gv, void* gvec_in, void* gpk, void* gpv, void* gcut,
-                                     void* gunit, const int32_t* order, void* stream) {
+                                     void* gunit, int accumulate, const int32_t* order,
+                                     void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (dtype == TMDNET_F32)
     return et::bwd<float>(n_nodes, hidden, heads, row_ptr, src, max_pairs, q, ld_q, k, ld_k, v, ld_v,
                           vec_in, pk, ld_pk, pv, ld_pv, cutoff, unit, grad_x, grad_vec, gq, gk, gv,
-                          gvec_in, gpk, gpv, gcut, gunit, order, st);
+                          gvec_in, gpk, gpv, gcut, gunit, accumulate, order, st);
   if (dtype == TMDNET_F64)
     return et::bwd<double>(n_nodes, hidden, heads, row_ptr, src, max_pairs, q, ld_q, k, ld_k, v, ld_v,
                            vec_in, pk, ld_pk, pv, ld_pv, cutoff, unit, grad_x, grad_vec, gq, gk, gv,
-                           gvec_in, gpk, gpv, gcut, gunit, order, st);
+                           gvec_in, gpk, gpv, gcut, gunit, accumulate, order, st);
   return kUnsupported;
 }
 

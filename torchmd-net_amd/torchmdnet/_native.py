@@ -15,6 +15,7 @@ _LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "lib
 F32, F64 = 0, 1
 NL_BRUTE, NL_SHARED, NL_CELL = 0, 1, 2
 RBF_EXPNORM, RBF_GAUSS = 0, 1
+ACC_VEC_RESIDUAL, ACC_EDGE = 1, 2
 
 _STATUS = {1: "bad argument", 2: "unsupported configuration", 3: "kernel launch failed",
            4: "workspace too small"}
@@ -33,7 +34,9 @@ SIGNATURES = {
     "tmdnet_edge_geom_bwd": (I, [I, I, I, I, P, P, P, P, P, P, D, D, P, P, P, P, P, P]),
     "tmdnet_et_message_fwd": (I, [I, I, I, I, P, P, I, P, I, P, I, P, I, P, P, I, P, I, P, P, P, P, P, P]),
     "tmdnet_et_message_bwd": (I, [I, I, I, I, P, P, I, P, I, P, I, P, I, P, P, I, P, I, P, P, P, P,
-                                  P, P, P, P, P, P, P, P, P, P]),
+                                  P, P, P, P, P, P, P, P, I, P, P]),
+    "tmdnet_et_epilogue_fwd": (I, [I, I, I, P, P, P, P, P, P, P, P]),
+    "tmdnet_et_epilogue_bwd": (I, [I, I, I, P, P, P, P, P, P, P]),
     "tmdnet_nbr_embed_fwd": (I, [I, I, I, P, P, I, P, I, P, I, P, P, P]),
     "tmdnet_nbr_embed_bwd": (I, [I, I, I, P, P, I, P, I, P, I, P, P, P, P, P, P]),
     "tmdnet_tn_embed_fwd": (I, [I, I, I, P, P, I, D, P, P, P, I, P, P, P, P, P, P]),

@@ -1,0 +1,367 @@
+"""The ET interaction stack as ONE autograd node with a hand-scheduled backward.
+
+Covers ``TorchMD_ET.forward``'s layer loop (reference models/torchmd_et.py:177-184) with every
+``EquivariantMultiHeadAttention.forward`` inside it (torchmd_et.py:293-321).  Per layer the forward
+is 7 launches:
+
+    native_layer_norm -> [q|k|v] GEMM (one, on the stacked q/k/v weights) -> vec_proj GEMM
+    -> [dk|dv] GEMM (one, on the stacked dk/dv weights) -> tmdnet_et_message_fwd -> o_proj GEMM
+    -> tmdnet_et_epilogue_fwd (vec_dot, o-gating, both residuals)
+
+and the backward, hand-scheduled on the same stream, 8-9 launches:
+
+    tmdnet_et_epilogue_bwd -> g_o @ W_o -> tmdnet_et_message_bwd (gradients written straight into
+    the stacked [q|k|v] / [dk|dv] gradient buffers; the vec residual and the cutoff / unit-vector
+    gradients of all layers accumulated in-kernel) -> addmm_ into g_edge_attr (shared by all
+    layers) -> addmm_ of the vec_proj backward into g_vec -> g_qkv @ W_qkv -> layer-norm backward.
+
+Weight-gradient GEMMs run only when the current backward will actually deliver them (the
+parameters' AccumulateGrad node is scheduled, ``torch._C._will_engine_execute_node``): a force
+evaluation (``autograd.grad(E, pos, create_graph=True)``) skips them, ``loss.backward()`` computes
+them.  The reference achieves none of this: it runs ~25 separate PyTorch kernels per layer forward
+and autograd's generic per-op backward.
+
+The backward is itself a Function so forces stay differentiable (training on forces); its own
+backward (second order) recomputes the stack with composite PyTorch ops and differentiates twice.
+"""
+import torch
+import torch.nn.functional as F
+from torch.autograd import Function
+
+from . import _native as nat
+from . import kernels
+
+_EPS = 1e-5  # nn.LayerNorm default (reference torchmd_et.py:223)
+
+
+def _stack_views(params):
+    """Make ``params`` (same trailing shape, same dtype/device) consecutive row blocks of one
+    buffer, in place (``p.data`` becomes a view; Parameters, optimiser references and state_dict
+    keys are unchanged).  Returns the buffer."""
+    buf = torch.cat([p.detach() for p in params], 0)
+    off = 0
+    for p in params:
+        n = p.shape[0]
+        p.data = buf[off:off + n]
+        off += n
+    return buf
+
+
+def _is_stacked(buf, params):
+    if buf is None:
+        return False
+    es = buf.element_size()
+    row = buf[0].numel() if buf.dim() > 1 else 1
+    off = 0
+    for p in params:
+        if p.device != buf.device or p.dtype != buf.dtype or not p.is_contiguous() \
+                or p.data_ptr() != buf.data_ptr() + off * row * es:
+            return False
+        off += p.shape[0]
+    return off == buf.shape[0]
+
+
+class LayerWeights:
+    """Stacked views of one EquivariantMultiHeadAttention's projections.
+
+    ``qkv_w`` [5H, H] = [q_proj; k_proj; v_proj] weights, ``dkv_w`` [(H|3H|4H), R] = [dk_proj;
+    dv_proj]; the Parameters themselves alias row blocks of these buffers, so no per-step
+    concatenation happens."""
+
+    def __init__(self, layer):
+        self.layer = layer
+        self.bufs = {}
+        self._acc = None  # (param ids, AccumulateGrad nodes) cache
+
+    def acc_nodes(self, params):
+        """AccumulateGrad nodes of ``params`` (the layer's), cached.  Holding them keeps the
+        parameters' accumulators alive, so they only change when a parameter is replaced or moved
+        (``.to()`` resets the accumulator); one lookup per call detects both."""
+        key = tuple((id(p), p.requires_grad) for p in params)
+        i = next(i for i, p in enumerate(params) if p.requires_grad)
+        node = params[i].view_as(params[i]).grad_fn.next_functions[0][0]
+        if self._acc is None or self._acc[0] != key or self._acc[1][i] is not node:
+            self._acc = (key, [p.view_as(p).grad_fn.next_functions[0][0] if p.requires_grad else None
+                               for p in params])
+        return self._acc[1]
+
+    def _get(self, name, params):
+        buf = self.bufs.get(name)
+        if not _is_stacked(buf, params):
+            buf = _stack_views(params)
+            self.bufs[name] = buf
+        return buf
+
+    def fused(self):
+        L = self.layer
+        qkv_w = self._get("qkv_w", [L.q_proj.weight, L.k_proj.weight, L.v_proj.weight])
+        qkv_b = self._get("qkv_b", [L.q_proj.bias, L.k_proj.bias, L.v_proj.bias])
+        dk = [m for m in (L.dk_proj, L.dv_proj) if m is not None]
+        dkv_w = self._get("dkv_w", [m.weight for m in dk]) if dk else None
+        dkv_b = self._get("dkv_b", [m.bias for m in dk]) if dk else None
+        return qkv_w, qkv_b, dkv_w, dkv_b
+
+
+def layer_params(layer):
+    """Flat parameter list of one layer, in the order the stack Function consumes it."""
+    ps = [layer.layernorm.weight, layer.layernorm.bias, layer.q_proj.weight, layer.q_proj.bias,
+          layer.k_proj.weight, layer.k_proj.bias, layer.v_proj.weight, layer.v_proj.bias,
+          layer.vec_proj.weight, layer.o_proj.weight, layer.o_proj.bias]
+    if layer.dk_proj is not None:
+        ps += [layer.dk_proj.weight, layer.dk_proj.bias]
+    if layer.dv_proj is not None:
+        ps += [layer.dv_proj.weight, layer.dv_proj.bias]
+    return ps
+
+
+class _Meta:
+    """Non-tensor context of one stack call."""
+
+    def __init__(self, graph, heads, H, hk, hv, n_layers, fused, acc_nodes):
+        self.graph = graph
+        self.heads = heads
+        self.H = H
+        self.hk = hk
+        self.hv = hv
+        self.n_layers = n_layers
+        self.fused = fused  # per layer (qkv_w, qkv_b, dkv_w, dkv_b) stacked views
+        self.acc_nodes = acc_nodes  # per layer: AccumulateGrad nodes of its parameters (or None)
+        self.np = 11 + 2 * int(hk) + 2 * int(hv)  # parameters per layer
+
+    def split(self, params):
+        return [params[i * self.np:(i + 1) * self.np] for i in range(self.n_layers)]
+
+
+def _epilogue_fwd(x, vec, vecp, o, veca):
+    lib = nat.load()
+    N, H = x.shape
+    xo = torch.empty_like(x)
+    vo = torch.empty_like(veca)
+    rc = lib.tmdnet_et_epilogue_fwd(nat.dtype_code(x.dtype), N, H, nat.ptr(x), nat.ptr(vec),
+                                    nat.ptr(vecp), nat.ptr(o), nat.ptr(veca), nat.ptr(xo), nat.ptr(vo),
+                                    nat.stream(x.device))
+    nat.check(rc, "tmdnet_et_epilogue_fwd")
+    return xo, vo
+
+
+def _epilogue_bwd(gx, gvec, vecp, o, g_vecp, g_o):
+    lib = nat.load()
+    N, H = gx.shape
+    rc = lib.tmdnet_et_epilogue_bwd(nat.dtype_code(gx.dtype), N, H, nat.ptr(gx), nat.ptr(gvec),
+                                    nat.ptr(vecp), nat.ptr(o), nat.ptr(g_vecp), nat.ptr(g_o),
+                                    nat.stream(gx.device))
+    nat.check(rc, "tmdnet_et_epilogue_bwd")
+
+
+def _forward_layers(meta, x, f, C, u, params):
+    """HIP/GEMM forward; returns outputs and the per-layer activations the backward needs."""
+    H = meta.H
+    N = x.shape[0]
+    vec = None
+    acts = []
+    for l, p in enumerate(meta.split(params)):
+        ln_w, ln_b = p[0], p[1]
+        vec_w, o_w, o_b = p[8], p[9], p[10]
+        qkv_w, qkv_b, dkv_w, dkv_b = meta.fused[l]
+        xn, mean, rstd = torch.native_layer_norm(x, [H], ln_w, ln_b, _EPS)
+        qkv = torch.addmm(qkv_b, xn, qkv_w.t())
+        vecp = None if vec is None else torch.mm(vec.view(3 * N, H), vec_w.t()).view(N, 3, 3 * H)
+        pkv = torch.addmm(dkv_b, f, dkv_w.t()) if dkv_w is not None else None
+        pk = pkv[:, :H] if meta.hk else None
+        pv = pkv[:, H * int(meta.hk):] if meta.hv else None
+        xa = torch.empty((N, H), dtype=x.dtype, device=x.device)
+        veca = torch.empty((N, 3, H), dtype=x.dtype, device=x.device)
+        kernels.et_message_fwd_launch(qkv[:, :H], qkv[:, H:2 * H], qkv[:, 2 * H:], vec, pk, pv, C, u,
+                                      meta.graph, meta.heads, xa, veca)
+        o = torch.addmm(o_b, xa, o_w.t())
+        x_new, vec_new = _epilogue_fwd(x, vec, vecp, o, veca)
+        acts.append((x, vec, xn, mean, rstd, qkv, vecp, pkv, xa, o))
+        x, vec = x_new, vec_new
+    return x, vec, acts
+
+
+def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws):
+    """Hand-scheduled first-order backward.  Returns (g_x, g_f, g_C, g_u, g_params)."""
+    H = meta.H
+    N = gX.shape[0]
+    graph = meta.graph
+    E = graph.n_edges
+    o = dict(dtype=gX.dtype, device=gX.device)
+    g_C = torch.zeros((E,), **o)
+    g_u = torch.zeros((E, 3), **o)
+    has_e = meta.hk or meta.hv
+    g_pkv = graph.alloc_edge_grad((E, (int(meta.hk) + 3 * int(meta.hv)) * H), gX.dtype, gX.device) \
+        if has_e else None
+    g_f = None
+    g_qkv = torch.empty((N, 5 * H), **o)
+    g_o = torch.empty((N, 3 * H), **o)
+    g_vecp = torch.empty((N, 3, 3 * H), **o)
+    gvec_bufs = [torch.empty((N, 3, H), **o), torch.empty((N, 3, H), **o)]
+    layers = meta.split(params)
+    g_params = [None] * len(params)
+    for l in reversed(range(meta.n_layers)):
+        p = layers[l]
+        x, vec, xn, mean, rstd, qkv, vecp, pkv, xa, o_ = acts[l]
+        ln_w, ln_b = p[0], p[1]
+        vec_w, o_w = p[8], p[9]
+        qkv_w, _, dkv_w, _ = meta.fused[l]
+        _epilogue_bwd(gX, gV, vecp, o_, g_vecp, g_o)
+        g_xa = torch.mm(g_o, o_w)
+        pk = pkv[:, :H] if meta.hk else None
+        pv = pkv[:, H * int(meta.hk):] if meta.hv else None
+        gpk = g_pkv[:, :H] if meta.hk else None
+        gpv = g_pkv[:, H * int(meta.hk):] if meta.hv else None
+        g_vec_in = gvec_bufs[l % 2] if vec is not None else None
+        kernels.et_message_bwd_launch(
+            qkv[:, :H], qkv[:, H:2 * H], qkv[:, 2 * H:], vec, pk, pv, C, u, graph, meta.heads, g_xa, gV,
+            g_qkv[:, :H], g_qkv[:, H:2 * H], g_qkv[:, 2 * H:], g_vec_in, gpk, gpv, g_C, g_u,
+            accumulate=nat.ACC_VEC_RESIDUAL | nat.ACC_EDGE)
+        if has_e:
+            if g_f is None:
+                g_f = torch.mm(g_pkv, dkv_w)
+            else:
+                g_f.addmm_(g_pkv, dkv_w)
+        if vec is not None:
+            g_vec_in.view(3 * N, H).addmm_(g_vecp.view(3 * N, 3 * H), vec_w)
+        g_xn = torch.mm(g_qkv, qkv_w)
+        need_w = need_ws[l]
+        g_x, g_lnw, g_lnb = torch.ops.aten.native_layer_norm_backward(g_xn, x, [H], mean, rstd, ln_w, ln_b,
+                                                             [True, need_w, need_w])
+        g_x.add_(gX)
+        if need_w:
+            base = l * meta.np
+            g_qkv_w = torch.mm(g_qkv.t(), xn)
+            g_qkv_b = g_qkv.sum(0)
+            gp = [g_lnw, g_lnb, g_qkv_w[:H], g_qkv_b[:H], g_qkv_w[H:2 * H], g_qkv_b[H:2 * H],
+                  g_qkv_w[2 * H:], g_qkv_b[2 * H:],
+                  (torch.mm(g_vecp.view(3 * N, 3 * H).t(), vec.view(3 * N, H)) if vec is not None
+                   else torch.zeros((3 * H, H), **o)),
+                  torch.mm(g_o.t(), xa), g_o.sum(0)]
+            if has_e:
+                g_dkv_w = torch.mm(g_pkv.t(), f)
+                g_dkv_b = g_pkv.sum(0)
+                if meta.hk:
+                    gp += [g_dkv_w[:H], g_dkv_b[:H]]
+                if meta.hv:
+                    a = H * int(meta.hk)
+                    gp += [g_dkv_w[a:], g_dkv_b[a:]]
+            g_params[base:base + meta.np] = gp
+        gX = g_x
+        gV = g_vec_in
+    return gX, g_f, g_C, g_u, g_params
+
+
+def composite_stack(meta, x, f, C, u, params):
+    """Reference math in plain PyTorch GPU ops (second-order backward only)."""
+    H = meta.H
+    graph = meta.graph
+    src, dst = graph.src.long(), graph.dst.long()
+    N = x.shape[0]
+    vec = torch.zeros((N, 3, H), dtype=x.dtype, device=x.device)
+    for p in meta.split(params):
+        ln_w, ln_b, q_w, q_b, k_w, k_b, v_w, v_b, vec_w, o_w, o_b = p[:11]
+        rest = list(p[11:])
+        xn = F.layer_norm(x, (H,), ln_w, ln_b, _EPS)
+        q, k, v = F.linear(xn, q_w, q_b), F.linear(xn, k_w, k_b), F.linear(xn, v_w, v_b)
+        vec1, vec2, vec3 = torch.split(F.linear(vec, vec_w), H, dim=-1)
+        vec_dot = (vec1 * vec2).sum(dim=1)
+        pk = F.linear(f, rest.pop(0), rest.pop(0)) if meta.hk else None
+        pv = F.linear(f, rest.pop(0), rest.pop(0)) if meta.hv else None
+        xa, veca = kernels.et_message_composite(q, k, v, vec, pk, pv, C, u, src, dst, N, meta.heads)
+        o1, o2, o3 = torch.split(F.linear(xa, o_w, o_b), H, dim=1)
+        x = x + vec_dot * o2 + o3
+        vec = vec + vec3 * o1.unsqueeze(1) + veca
+    return x, vec
+
+
+def _will_run(node):
+    if node is None:  # parameter without requires_grad
+        return False
+    try:
+        return bool(torch._C._will_engine_execute_node(node))
+    except RuntimeError:
+        return True
+
+
+class _ETStack(Function):
+    @staticmethod
+    def forward(ctx, meta, x, f, C, u, *params):
+        x_out, vec_out, acts = _forward_layers(meta, x, f, C, u, params)
+        ctx.meta = meta
+        ctx.acts = acts
+        ctx.save_for_backward(x, f, C, u, *params)
+        return x_out, vec_out
+
+    @staticmethod
+    def backward(ctx, gX, gV):
+        x, f, C, u, *params = ctx.saved_tensors
+        meta = ctx.meta
+        need_w = tuple(nodes is not None and any(_will_run(n) for n in nodes) for nodes in meta.acc_nodes)
+        if gX is None:
+            gX = torch.zeros_like(x)
+        if gV is None:
+            gV = torch.zeros((x.shape[0], 3, meta.H), dtype=x.dtype, device=x.device)
+        outs = _ETStackBwd.apply(meta, ctx.acts, need_w, gX.contiguous(), gV.contiguous(), x, f, C, u,
+                                 *params)
+        g_x, g_f, g_C, g_u = outs[:4]
+        return (None, g_x, g_f, g_C, g_u) + tuple(outs[4:])
+
+
+class _ETStackBwd(Function):
+    @staticmethod
+    def forward(ctx, meta, acts, need_w, gX, gV, x, f, C, u, *params):
+        if not meta.graph.symmetric:
+            raise RuntimeError("torchmd-net_amd: the ET backward source pass needs a symmetric edge "
+                               "list (include_transpose=True, no capacity overflow)")
+        g_x, g_f, g_C, g_u, g_params = _backward_layers(meta, gX, gV, f, C, u, params, acts, need_w)
+        ctx.meta = meta
+        ctx.save_for_backward(gX, gV, x, f, C, u, *params)
+        return (g_x, g_f, g_C, g_u) + tuple(g_params)
+
+    @staticmethod
+    def backward(ctx, *ggs):
+        saved = ctx.saved_tensors
+        meta = ctx.meta
+        with torch.enable_grad():
+            leaves = [None if t is None else t.detach().requires_grad_(True) for t in saved]
+            gX, gV, x, f, C, u = leaves[:6]
+            params = leaves[6:]
+            xo, vo = composite_stack(meta, x, f, C, u, params)
+            wrt = [x, f, C, u] + params
+            live = [t for t in wrt if t is not None]
+            first = torch.autograd.grad((xo, vo), live, (gX, gV), create_graph=True, allow_unused=True)
+            it = iter(first)
+            first_full = [next(it) if t is not None else None for t in wrt]
+            sel = [(fg, g) for fg, g in zip(first_full, ggs) if fg is not None and g is not None]
+            ins = [t for t in leaves if t is not None]
+            n_out = 3 + len(leaves)
+            if not sel:
+                return (None,) * n_out
+            second = torch.autograd.grad([fg for fg, _ in sel], ins, [g for _, g in sel],
+                                         create_graph=True, allow_unused=True)
+        it = iter(second)
+        res = [next(it) if t is not None else None for t in leaves]
+        return (None, None, None) + tuple(res)
+
+
+def et_stack(layers, x, graph, f, C, u):
+    """Run ``layers`` (EquivariantMultiHeadAttention modules) as one node.  Returns (x, vec) after
+    the last residual update (reference torchmd_et.py:180-184)."""
+    l0 = layers[0]
+    H, heads = l0.hidden_channels, l0.num_heads
+    hk, hv = l0.dk_proj is not None, l0.dv_proj is not None
+    fused, params, acc = [], [], []
+    grad_on = torch.is_grad_enabled()
+    for layer in layers:
+        layer._check_supported()
+        if layer._stacked is None:
+            layer._stacked = LayerWeights(layer)
+        fused.append(layer._stacked.fused())
+        lp = layer_params(layer)
+        params += lp
+        acc.append(layer._stacked.acc_nodes(lp) if (grad_on and any(p.requires_grad for p in lp))
+                   else None)
+    meta = _Meta(graph, heads, H, hk, hv, len(layers), fused, acc)
+    x = x.contiguous()
+    f = f.contiguous() if (hk or hv) else None
+    return _ETStack.apply(meta, x, f, C.contiguous(), u.contiguous(), *params)

@@ -374,6 +374,48 @@ def _ld(t):
     return 0 if t is None else t.stride(0)
 
 
+def rows_like(t, alloc=torch.empty):
+    """Gradient buffer with the same row stride as ``t`` (kernels write gradients with the input's
+    leading dimension)."""
+    if t is None:
+        return None
+    if t.stride(0) == t.shape[1]:
+        return alloc(tuple(t.shape), dtype=t.dtype, device=t.device)
+    return alloc((t.shape[0], t.stride(0)), dtype=t.dtype, device=t.device)[:, :t.shape[1]]
+
+
+def et_message_fwd_launch(q, k, v, vec, pk, pv, C, u, graph, heads, xo, vo):
+    """One ``tmdnet_et_message_fwd`` launch (vec may be None: vec == 0)."""
+    lib = nat.load()
+    N, H = q.shape
+    probe = EVENT_PROBE
+    if probe is not None:
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record()
+    rc = lib.tmdnet_et_message_fwd(nat.dtype_code(q.dtype), N, H, heads, nat.ptr(graph.row_ptr),
+                                   nat.ptr(graph.src), graph.n_edges, nat.ptr(q), _ld(q), nat.ptr(k),
+                                   _ld(k), nat.ptr(v), _ld(v), nat.ptr(vec), nat.ptr(pk), _ld(pk),
+                                   nat.ptr(pv), _ld(pv), nat.ptr(C), nat.ptr(u), nat.ptr(xo),
+                                   nat.ptr(vo), None, nat.stream(q.device))
+    nat.check(rc, "tmdnet_et_message_fwd")
+    if probe is not None:
+        ev1.record()
+        probe.append((ev0, ev1, graph.n_edges, N, H))
+
+
+def et_message_bwd_launch(q, k, v, vec, pk, pv, C, u, graph, heads, gx, gvec, gq, gk, gv, gw, gpk,
+                          gpv, gC, gu, accumulate=0):
+    lib = nat.load()
+    N, H = q.shape
+    rc = lib.tmdnet_et_message_bwd(
+        nat.dtype_code(q.dtype), N, H, heads, nat.ptr(graph.row_ptr), nat.ptr(graph.src), graph.n_edges,
+        nat.ptr(q), _ld(q), nat.ptr(k), _ld(k), nat.ptr(v), _ld(v), nat.ptr(vec), nat.ptr(pk),
+        _ld(pk), nat.ptr(pv), _ld(pv), nat.ptr(C), nat.ptr(u), nat.ptr(gx), nat.ptr(gvec),
+        nat.ptr(gq), nat.ptr(gk), nat.ptr(gv), nat.ptr(gw), nat.ptr(gpk), nat.ptr(gpv),
+        nat.ptr(gC), nat.ptr(gu), int(accumulate), None, nat.stream(q.device))
+    nat.check(rc, "tmdnet_et_message_bwd")
+
+
 def _rowmajor(t):
     """Rows may be strided (e.g. views into a fused projection) but elements must be contiguous."""
     if t is None:
@@ -410,23 +452,10 @@ def et_message_composite(q, k, v, vec, pk, pv, C, u, src, dst, n_nodes, heads):
 class _ETMessage(Function):
     @staticmethod
     def forward(ctx, q, k, v, vec, pk, pv, C, u, graph, heads):
-        lib = nat.load()
         N, H = q.shape
         xo = torch.empty((N, H), dtype=q.dtype, device=q.device)
         vo = torch.empty((N, 3, H), dtype=q.dtype, device=q.device)
-        probe = EVENT_PROBE
-        if probe is not None:
-            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            ev0.record()
-        rc = lib.tmdnet_et_message_fwd(nat.dtype_code(q.dtype), N, H, heads, nat.ptr(graph.row_ptr),
-                                       nat.ptr(graph.src), graph.n_edges, nat.ptr(q), _ld(q), nat.ptr(k),
-                                       _ld(k), nat.ptr(v), _ld(v), nat.ptr(vec), nat.ptr(pk), _ld(pk),
-                                       nat.ptr(pv), _ld(pv), nat.ptr(C), nat.ptr(u), nat.ptr(xo),
-                                       nat.ptr(vo), None, nat.stream(q.device))
-        nat.check(rc, "tmdnet_et_message_fwd")
-        if probe is not None:
-            ev1.record()
-            probe.append((ev0, ev1, graph.n_edges, N, H))
+        et_message_fwd_launch(q, k, v, vec, pk, pv, C, u, graph, heads, xo, vo)
         ctx.graph = graph
         ctx.heads = heads
         ctx.save_for_backward(q, k, v, vec, pk, pv, C, u)
@@ -452,27 +481,22 @@ class _ETMessageBwd(Function):
         if not graph.symmetric:
             raise RuntimeError("torchmd-net_amd: the ET backward source pass needs a symmetric edge "
                                "list (include_transpose=True, no capacity overflow)")
-        lib = nat.load()
         N, H = q.shape
         E = graph.n_edges
         o = dict(dtype=q.dtype, device=q.device)
-        gq = torch.empty((N, H), **o)
-        gk = torch.empty((N, H), **o)
-        gv = torch.empty((N, 3 * H), **o)
+        gq, gk, gv = rows_like(q), rows_like(k), rows_like(v)
         gw = torch.empty((N, 3, H), **o)
-        ge = graph.alloc_edge_grad
-        gpk = ge((E, H), q.dtype, q.device) if pk is not None else torch.zeros(0, **o)
-        gpv = ge((E, 3 * H), q.dtype, q.device) if pv is not None else torch.zeros(0, **o)
+        ge = lambda shape, dtype, device: graph.alloc_edge_grad(shape, dtype, device)  # noqa: E731
+        gpk = rows_like(pk, ge) if pk is not None else None
+        gpv = rows_like(pv, ge) if pv is not None else None
         gC = ge((E,), q.dtype, q.device)
         gu = ge((E, 3), q.dtype, q.device)
-        rc = lib.tmdnet_et_message_bwd(
-            nat.dtype_code(q.dtype), N, H, heads, nat.ptr(graph.row_ptr), nat.ptr(graph.src), E,
-            nat.ptr(q), _ld(q), nat.ptr(k), _ld(k), nat.ptr(v), _ld(v), nat.ptr(vec), nat.ptr(pk),
-            _ld(pk), nat.ptr(pv), _ld(pv), nat.ptr(C), nat.ptr(u), nat.ptr(gx), nat.ptr(gvec),
-            nat.ptr(gq), nat.ptr(gk), nat.ptr(gv), nat.ptr(gw),
-            nat.ptr(gpk) if pk is not None else None, nat.ptr(gpv) if pv is not None else None,
-            nat.ptr(gC), nat.ptr(gu), None, nat.stream(q.device))
-        nat.check(rc, "tmdnet_et_message_bwd")
+        et_message_bwd_launch(q, k, v, vec, pk, pv, C, u, graph, heads, gx, gvec, gq, gk, gv, gw,
+                              gpk, gpv, gC, gu)
+        if gpk is None:
+            gpk = torch.zeros(0, **o)
+        if gpv is None:
+            gpv = torch.zeros(0, **o)
         ctx.graph = graph
         ctx.heads = heads
         ctx.save_for_backward(gx, gvec, q, k, v, vec, pk, pv, C, u)

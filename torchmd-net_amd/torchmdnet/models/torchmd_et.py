@@ -16,6 +16,7 @@ import torch
 from torch import Tensor, nn
 
 from .. import kernels
+from ..et_stack import et_stack
 from .utils import (CosineCutoff, NeighborEmbedding, OptimizedDistance, act_class_mapping, as_graph,
                     rbf_class_mapping)
 
@@ -71,6 +72,7 @@ class TorchMD_ET(nn.Module):
 
         self.out_norm = nn.LayerNorm(hidden_channels, dtype=dtype)
         self.reorder_atoms = True
+        self.fused_stack = True
         self.reset_parameters()
 
     def reset_parameters(self):
@@ -112,6 +114,11 @@ class TorchMD_ET(nn.Module):
         graph.cutoff = C
         if self.neighbor_embedding is not None:
             x = self.neighbor_embedding(z, x, graph, graph.distances, edge_attr, cutoff=C)
+        if self.fused_stack and len(self.attention_layers) > 0:
+            # all layers as one autograd node (et_stack.py): fused GEMMs, HIP epilogue, hand-scheduled
+            # backward; same math as the loop below
+            x, vec = et_stack(self.attention_layers, x, graph, edge_attr, C, d_ij)
+            return self.out_norm(x), vec
         vec = torch.zeros(x.size(0), 3, x.size(1), device=x.device, dtype=x.dtype)
         for attn in self.attention_layers:
             dx, dvec = attn(x, vec, graph, graph.distances, edge_attr, d_ij)
@@ -158,6 +165,7 @@ class EquivariantMultiHeadAttention(nn.Module):
         self.dv_proj = None
         if distance_influence in ["values", "both"]:
             self.dv_proj = nn.Linear(num_rbf, hidden_channels * 3, dtype=dtype)
+        self._stacked = None  # et_stack.LayerWeights: q/k/v and dk/dv parameters as stacked views
         self.reset_parameters()
 
     def jittable(self):
