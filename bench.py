@@ -48,7 +48,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--roofline-atoms", type=int, default=50001)
-    ap.add_argument("--roofline-reps", type=int, default=20)
+    ap.add_argument("--roofline-reps", type=int, default=50)
     ap.add_argument("--eager", action="store_true", help="no HIP-graph capture (infer mode)")
     return ap.parse_args()
 
@@ -140,18 +140,18 @@ def roofline_probe(n_atoms, reps, H, dev):
                                        ptr(u), ptr(xo), ptr(vo), None, st)
         kernels.nat.check(rc, "tmdnet_et_message_fwd")
 
-    for _ in range(3):
+    for _ in range(5):
         launch()
     torch.cuda.synchronize()
-    evs = []
+    # back-to-back launches between one pair of HIP events recorded on the launch stream: the
+    # average launch duration, comparable with rocprofv3's per-kernel average
+    a0, b0 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a0.record()
     for _ in range(reps):
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record()
         launch()
-        b.record()
-        evs.append((a, b))
+    b0.record()
     torch.cuda.synchronize()
-    ms = sum(a.elapsed_time(b) for a, b in evs) / len(evs)
+    ms = a0.elapsed_time(b0) / reps
     nbytes = et_algorithmic_bytes(E, n_atoms, H)
     gbs = nbytes / (ms * 1e-3) / 1e9
     return {"kernel": "tmdnet_et_message_fwd (k_fwd<float,4,1,1,false>)",

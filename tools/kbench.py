@@ -117,20 +117,56 @@ def main():
     ap.add_argument("--c5-atoms", type=int, default=50001)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--no-c5", action="store_true")
+    ap.add_argument("--variants", default="", help="comma list of ENV=value kernel switches to A/B")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     g2 = graph_c2(dev)
-    run_et("C2 ET", g2, 128, 200, dev, True)
+    variants = [v for v in a.variants.split(",") if v]
+    for var in variants or [""]:
+        if var:
+            k, val = var.split("=")
+            os.environ[k] = val
+        run_et(f"C2 ET {var}", g2, 128, 200, dev, True)
     if not a.no_c5:
-        for order in ("morton", "random"):
-            g5 = graph_c5(a.c5_atoms, dev, order)
-            for nt, cs in ((0, 1), (1, 1), (0, 2), (1, 2), (1, 4)):
-                os.environ["TMDNET_NT"] = str(nt)
-                os.environ["TMDNET_CS"] = str(cs)
-                run_et(f"C5 ET order={order} nt={nt} cs={cs}", g5, 128, a.reps, dev, order == "morton")
-            del g5
-            torch.cuda.empty_cache()
+        g5 = graph_c5(a.c5_atoms, dev, "morton")
+        for var in variants or [""]:
+            if var:
+                k, val = var.split("=")
+                os.environ[k] = val
+            run_et(f"C5 ET morton {var}", g5, 128, a.reps, dev, True)
 
-
-if __name__ == "__main__":
+if __name__ == "__main__" and not os.environ.get("KBENCH_DECOMPOSE"):
     main()
+
+
+def decompose(g, H, reps, dev, heads=8):
+    """C5 fwd time split: full / no per-edge stream (pk=pv=None) / gathers from own row only."""
+    x = et_inputs(g, H, dev)
+    N = g.n_nodes
+    xo = torch.empty(N, H, device=dev)
+    vo = torch.empty(N, 3, H, device=dev)
+    full = lambda gr, pk, pv: kernels.et_message_fwd_launch(x["q"], x["k"], x["v"], x["vec"], pk, pv, x["C"],  # noqa
+                                                           x["u"], gr, heads, xo, vo)
+    t_full = timeit(lambda: full(g, x["pk"], x["pv"]), reps)
+    t_nostream = timeit(lambda: full(g, None, None), reps)
+    import copy
+    g_self = copy.copy(g)
+    g_self.src = g.dst.clone()  # every gather hits the destination's own row (perfect locality)
+    t_self = timeit(lambda: full(g_self, x["pk"], x["pv"]), reps)
+    t_self_ns = timeit(lambda: full(g_self, None, None), reps)
+    E = g.n_edges
+    t_sum = timeit(lambda: (x["pk"].sum(), x["pv"].sum()), reps)
+    buf = torch.empty(E * 4 * H, device=dev)
+    t_copy = timeit(lambda: (buf[:E * H].copy_(x["pk"].view(-1)), buf[E * H:].copy_(x["pv"].view(-1))), reps)
+    print(f"   plain torch over the same stream: sum {t_sum:.0f} us ({E * 16 * H / t_sum / 1e3:.0f} GB/s read), "
+          f"copy {t_copy:.0f} us ({2 * E * 16 * H / t_copy / 1e3:.0f} GB/s r+w)")
+    print(f"decompose heads={heads} N={N} E={E}: full {t_full:.0f} us | no dk/dv stream {t_nostream:.0f} us | "
+          f"self-gathers {t_self:.0f} us | self-gathers, no stream {t_self_ns:.0f} us | "
+          f"stream bytes {E * 16 * H / 1e9:.2f} GB")
+
+
+if __name__ == "__main__" and os.environ.get("KBENCH_DECOMPOSE"):
+    _dev = torch.device("cuda", 0)
+    _g = graph_c5(50001, _dev, "morton")
+    for _h in (8, 2, 1):
+        decompose(_g, 128, 20, _dev, _h)

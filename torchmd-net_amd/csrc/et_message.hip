@@ -16,7 +16,6 @@
 //     gk, gv, gvec without a transpose scatter or atomics.
 #include "common.h"
 #include "tmdnet.h"
-#include <stdlib.h>
 
 namespace tmd {
 namespace et {
@@ -76,7 +75,6 @@ template <typename T, int V> __device__ __forceinline__ void zero(T (&o)[V]) {
 template <typename T> struct Args {
   int n, H, d, L, lph, cap;
   int xcd;      // XCD-contiguous block remap (on: +10-15 % on C5-scale graphs)
-  int nt;       // non-temporal loads of the per-edge stream (measured slower on gfx950: off)
   int HC;       // channels per channel group (H / CS)
   const int32_t* row_ptr;
   const int32_t* src;
@@ -97,46 +95,27 @@ template <typename T> struct Args {
   int acc;  // TMDNET_ACC_* flags of the backward
 };
 
-// silu of the pre-activation, or 1 when the projection is absent
-template <typename T, int V> struct NVec { typedef T t __attribute__((ext_vector_type(V))); };
-template <typename T, int V> __device__ __forceinline__ void ldv_nt_(T (&o)[V], const T* p) {
-  if constexpr (V == 1) {
-    o[0] = __builtin_nontemporal_load(p);
-  } else {
-    using VT = typename NVec<T, V>::t;
-    const VT x = __builtin_nontemporal_load(reinterpret_cast<const VT*>(p));
-#pragma unroll
-    for (int i = 0; i < V; ++i) o[i] = x[i];
-  }
-}
-template <typename T, int V> __device__ __forceinline__ void ldv_nt(T (&o)[V], const T* p) {
-  if constexpr (V == 8) {
-    T a[4], b[4];
-    ldv_nt_<T, 4>(a, p);
-    ldv_nt_<T, 4>(b, p + 4);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) { o[i] = a[i]; o[4 + i] = b[i]; }
-  } else {
-    ldv_nt_<T, V>(o, p);
-  }
-}
-
+// SiLU of a pre-activation row segment already in registers (or 1 / 0 when the projection is
+// absent).  Loads and activations are kept apart on purpose: every per-edge load of an edge is
+// issued before the first activation, so an edge costs one memory round trip, not one per load.
 template <typename T, int V>
-__device__ __forceinline__ void act(const T* base, bool has, T (&x)[V], T (&s)[V], T (&ds)[V], bool nt = false) {
-  if (has) {
-    if (nt) ldv_nt<T, V>(x, base); else ldv<T, V>(x, base);
+__device__ __forceinline__ void act(const T (&x)[V], bool has, T (&s)[V], T (&ds)[V]) {
 #pragma unroll
-    for (int i = 0; i < V; ++i) {
+  for (int i = 0; i < V; ++i) {
+    if (has) {
       Silu<T> f(x[i]);
       s[i] = f.s;
       ds[i] = f.d(x[i]);
+    } else {
+      s[i] = T(1);
+      ds[i] = T(0);
     }
-  } else {
-#pragma unroll
-    for (int i = 0; i < V; ++i) { x[i] = T(0); s[i] = T(1); ds[i] = T(0); }
   }
 }
-
+// Branch-free optional load: an absent projection reads a valid dummy row (result ignored).
+template <typename T> __device__ __forceinline__ const T* opt(const T* p, size_t off, const T* dummy) {
+  return p ? p + off : dummy;
+}
 
 // Work decomposition shared by the three kernels.
 //   * a 256-thread block = 4 waves; S waves cooperate on one node (S in {1, 2, 4}), so a block owns
@@ -210,6 +189,82 @@ __device__ __forceinline__ void reduce_waves(T (&a)[NV], int sub, T* lds) {
   }
 }
 
+// Row traversal with the per-edge scalars (source index, cutoff, unit vector) fetched once per
+// chunk of 64 edges by one coalesced load per lane and handed to the edge slots by cross-lane
+// permutes: the gathers of an edge then depend on ONE memory round trip instead of two.  The
+// chunk and slot loops are wave-uniform (permutes need every lane active); a slot past the end of
+// the row skips the body.
+template <typename T, int S, typename F>
+__device__ __forceinline__ void edge_chunks(const Args<T>& A, int b, int e, int EPW, const Geo& G,
+                                            F&& body) {
+  const int lane = lane_id();
+  for (int c = b; c < e; c += TMD_WAVE) {
+    const int n = min(TMD_WAVE, e - c);
+    int s_r = 0;
+    T C_r = T(0), u0_r = T(0), u1_r = T(0), u2_r = T(0);
+    if (lane < n) {
+      const int k = c + lane;
+      s_r = A.src[k];
+      C_r = A.C[k];
+      u0_r = A.u[3 * k];
+      u1_r = A.u[3 * k + 1];
+      u2_r = A.u[3 * k + 2];
+    }
+    for (int j0 = EPW * G.sub; j0 < n; j0 += EPW * S) {
+      const int j = j0 + G.es;
+      const int jj = j < n ? j : n - 1;
+      const int s = __shfl(s_r, jj);
+      const T Ce = __shfl(C_r, jj), u0 = __shfl(u0_r, jj), u1 = __shfl(u1_r, jj), u2 = __shfl(u2_r, jj);
+      if (j < n) body(c + j, s, Ce, u0, u1, u2);
+    }
+  }
+}
+
+// The same traversal with the per-edge STREAM (dk/dv rows, read once) software-pipelined PD edges
+// ahead: `ld(k, st)` loads edge k's stream rows into registers; `body(k, s, C, u0, u1, u2, st, pre)`
+// issues its source gathers, then calls `pre()` -- which issues the NEXT edge's stream loads -- and
+// only then consumes data.  Loads retire in issue order, so waiting for this edge's gathers leaves
+// the next edges' stream in flight (a counted vmcnt).  PD = 1 is used: C5 fwd 1.44 -> 1.35-1.41 ms;
+// PD = 2 measured equal in interleaved runs (tools/kbench.py) at 18 more VGPRs.
+// The prefetch is unconditional (clamped to the chunk's last edge) so the wait count is static.
+template <typename T, int S, int PD, typename St, typename LD, typename F>
+__device__ __forceinline__ void edge_chunks_pf(const Args<T>& A, int b, int e, int EPW, const Geo& G,
+                                               LD&& ld, F&& body) {
+  const int lane = lane_id();
+  St cur, nxt, nx2;
+  const int step = EPW * S;
+  for (int c = b; c < e; c += TMD_WAVE) {
+    const int n = min(TMD_WAVE, e - c);
+    int s_r = 0;
+    T C_r = T(0), u0_r = T(0), u1_r = T(0), u2_r = T(0);
+    if (lane < n) {
+      const int k = c + lane;
+      s_r = A.src[k];
+      C_r = A.C[k];
+      u0_r = A.u[3 * k];
+      u1_r = A.u[3 * k + 1];
+      u2_r = A.u[3 * k + 2];
+    }
+    int j0 = EPW * G.sub;
+    if (j0 < n) {  // PD edges of stream in flight ahead of the one being consumed
+      ld(c + min(j0 + G.es, n - 1), cur);
+      if constexpr (PD == 2) ld(c + min(j0 + step + G.es, n - 1), nxt);
+    }
+    for (; j0 < n; j0 += step) {
+      const int j = j0 + G.es;
+      const int jj = j < n ? j : n - 1;
+      const int s = __shfl(s_r, jj);
+      const T Ce = __shfl(C_r, jj), u0 = __shfl(u0_r, jj), u1 = __shfl(u1_r, jj), u2 = __shfl(u2_r, jj);
+      const int kn = c + min(j0 + PD * step + G.es, n - 1);
+      auto pre = [&]() { ld(kn, PD == 2 ? nx2 : nxt); };
+      if (j < n) body(c + j, s, Ce, u0, u1, u2, cur, pre);
+      else pre();
+      cur = nxt;
+      if constexpr (PD == 2) nxt = nx2;
+    }
+  }
+}
+
 // ------------------------------------------------------------------ forward
 // ORD: nodes visited in the caller's `order` (cell order for large periodic systems, so the waves in
 // flight gather from a compact spatial window of source rows).
@@ -224,37 +279,43 @@ __global__ __launch_bounds__(256) void k_fwd(Args<T> A) {
   const int hh = c0 / A.d, cc = c0 % A.d;
   const int vo = hh * 3 * A.d + cc;
   const bool hk = A.pk != nullptr, hv = A.pv != nullptr, hw = A.vec != nullptr;
+  const int pvd = hv ? A.d : 0, vcd = hw ? A.H : 0;  // branch-free optional loads
+  (void)vcd;
   T ax[V], a0[V], a1[V], a2[V];
   zero(ax); zero(a0); zero(a1); zero(a2);
   if (t >= 0) {
     T q[V];
     ldv<T, V>(q, A.q + (size_t)t * A.ldq + c0);
     const int b = min(A.row_ptr[t], A.cap), e = min(A.row_ptr[t + 1], A.cap);
-    for (int k = b + EPW * G.sub + G.es; k < e; k += EPW * S) {
-      const int s = A.src[k];
-      const T Ce = A.C[k];
-      const T u0 = A.u[3 * k], u1 = A.u[3 * k + 1], u2 = A.u[3 * k + 2];
-      T kk[V], px[V], dk[V], dd[V];
+    const T* dummy = A.q + (size_t)t * A.ldq;  // valid row for absent optional inputs
+    struct St { T k[V], x[V], a[V], b[V]; };  // one edge's dk/dv stream (pre-activations)
+    auto ld = [&](int k, St& st) {
+      ldv<T, V>(st.k, opt(A.pk, (size_t)k * A.ldpk + c0, dummy + c0));
+      const T* pvs = opt(A.pv, (size_t)k * A.ldpv + vo, dummy);
+      ldv<T, V>(st.x, pvs);
+      ldv<T, V>(st.a, pvs + pvd);
+      ldv<T, V>(st.b, pvs + 2 * pvd);
+    };
+    auto body = [&](int k, int s, T Ce, T u0, T u1, T u2, const St& st, auto&& pre) {
+      (void)k;
+      // source gathers (k, v, vec) for this edge, then the next edge's stream, then the math
+      T kk[V], vx[V], v1[V], v2[V], w0[V], w1[V], w2[V];
       ldv<T, V>(kk, A.k + (size_t)s * A.ldk + c0);
-      act<T, V>(A.pk + (size_t)k * A.ldpk + c0, hk, px, dk, dd, A.nt);
       const T* vs = A.v + (size_t)s * A.ldv + vo;
-      const T* pvs = A.pv + (size_t)k * A.ldpv + vo;
-      T vx[V], v1[V], v2[V], dvx[V], dv1[V], dv2[V];
       ldv<T, V>(vx, vs);
       ldv<T, V>(v1, vs + A.d);
       ldv<T, V>(v2, vs + 2 * A.d);
-      act<T, V>(pvs, hv, px, dvx, dd, A.nt);
-      act<T, V>(pvs + A.d, hv, px, dv1, dd, A.nt);
-      act<T, V>(pvs + 2 * A.d, hv, px, dv2, dd, A.nt);
-      T w0[V], w1[V], w2[V];
-      if (hw) {
-        const T* vecs = A.vec + (size_t)s * 3 * A.H + c0;
-        ldv<T, V>(w0, vecs);
-        ldv<T, V>(w1, vecs + A.H);
-        ldv<T, V>(w2, vecs + 2 * A.H);
-      } else {
-        zero(w0); zero(w1); zero(w2);
-      }
+      const T* vecs = hw ? A.vec + (size_t)s * 3 * A.H + c0 : dummy + c0;
+      ldv<T, V>(w0, vecs);
+      ldv<T, V>(w1, vecs + vcd);
+      ldv<T, V>(w2, vecs + 2 * vcd);
+      pre();
+      if (!hw) { zero(w0); zero(w1); zero(w2); }
+      T dk[V], dvx[V], dv1[V], dv2[V], dd[V];
+      act<T, V>(st.k, hk, dk, dd);
+      act<T, V>(st.x, hv, dvx, dd);
+      act<T, V>(st.a, hv, dv1, dd);
+      act<T, V>(st.b, hv, dv2, dd);
       T part = T(0);
 #pragma unroll
       for (int i = 0; i < V; ++i) part += q[i] * kk[i] * dk[i];
@@ -269,7 +330,8 @@ __global__ __launch_bounds__(256) void k_fwd(Args<T> A) {
         a1[i] += w1[i] * v1e + v2e * u1;
         a2[i] += w2[i] * v1e + v2e * u2;
       }
-    }
+    };
+    edge_chunks_pf<T, S, 1, St>(A, b, e, EPW, G, ld, body);
   }
   xor_slots(ax, A.L); xor_slots(a0, A.L); xor_slots(a1, A.L); xor_slots(a2, A.L);
   T all[4 * V];
@@ -299,6 +361,8 @@ __global__ __launch_bounds__(256) void k_bwd_dst(Args<T> A) {
   const int hh = c0 / A.d, cc = c0 % A.d;
   const int vo = hh * 3 * A.d + cc;
   const bool hk = A.pk != nullptr, hv = A.pv != nullptr, hw = A.vec != nullptr;
+  const int pvd = hv ? A.d : 0, vcd = hw ? A.H : 0;  // branch-free optional loads
+  (void)vcd;
   const bool head_leader = on && (G.el % A.lph) == 0;
   T gq[V];
   zero(gq);
@@ -311,31 +375,37 @@ __global__ __launch_bounds__(256) void k_bwd_dst(Args<T> A) {
     ldv<T, V>(g1, gvt + A.H);
     ldv<T, V>(g2, gvt + 2 * A.H);
     const int b = min(A.row_ptr[t], A.cap), e = min(A.row_ptr[t + 1], A.cap);
-    for (int k = b + EPW * G.sub + G.es; k < e; k += EPW * S) {
-      const int s = A.src[k];
-      const T Ce = A.C[k];
-      const T u0 = A.u[3 * k], u1 = A.u[3 * k + 1], u2 = A.u[3 * k + 2];
-      T kk[V], pk[V], dk[V], ddk[V];
+    const T* dummy = A.q + (size_t)t * A.ldq;
+    const bool acc_edge = (A.acc & TMDNET_ACC_EDGE) && G.el == 0;
+    auto body = [&](int k, int s, T Ce, T u0, T u1, T u2) {
+      T oc = T(0), ou0 = T(0), ou1 = T(0), ou2 = T(0);  // accumulate mode: issued with the loads
+      if (acc_edge) {
+        oc = A.gC[k];
+        ou0 = A.gu[3 * k];
+        ou1 = A.gu[3 * k + 1];
+        ou2 = A.gu[3 * k + 2];
+      }
+      T kk[V], pk[V], vx[V], v1[V], v2[V], px[V], p1[V], p2[V], w0[V], w1[V], w2[V];
       ldv<T, V>(kk, A.k + (size_t)s * A.ldk + c0);
-      act<T, V>(A.pk + (size_t)k * A.ldpk + c0, hk, pk, dk, ddk, A.nt);
+      ldv<T, V>(pk, opt(A.pk, (size_t)k * A.ldpk + c0, dummy + c0));
       const T* vs = A.v + (size_t)s * A.ldv + vo;
-      const T* pvs = A.pv + (size_t)k * A.ldpv + vo;
-      T vx[V], v1[V], v2[V], px[V], p1[V], p2[V], dvx[V], dv1[V], dv2[V], ddx[V], dd1[V], dd2[V];
+      const T* pvs = opt(A.pv, (size_t)k * A.ldpv + vo, dummy);
       ldv<T, V>(vx, vs);
       ldv<T, V>(v1, vs + A.d);
       ldv<T, V>(v2, vs + 2 * A.d);
-      act<T, V>(pvs, hv, px, dvx, ddx, A.nt);
-      act<T, V>(pvs + A.d, hv, p1, dv1, dd1, A.nt);
-      act<T, V>(pvs + 2 * A.d, hv, p2, dv2, dd2, A.nt);
-      T w0[V], w1[V], w2[V];
-      if (hw) {
-        const T* vecs = A.vec + (size_t)s * 3 * A.H + c0;
-        ldv<T, V>(w0, vecs);
-        ldv<T, V>(w1, vecs + A.H);
-        ldv<T, V>(w2, vecs + 2 * A.H);
-      } else {
-        zero(w0); zero(w1); zero(w2);
-      }
+      ldv<T, V>(px, pvs);
+      ldv<T, V>(p1, pvs + pvd);
+      ldv<T, V>(p2, pvs + 2 * pvd);
+      const T* vecs = hw ? A.vec + (size_t)s * 3 * A.H + c0 : dummy + c0;
+      ldv<T, V>(w0, vecs);
+      ldv<T, V>(w1, vecs + vcd);
+      ldv<T, V>(w2, vecs + 2 * vcd);
+      if (!hw) { zero(w0); zero(w1); zero(w2); }
+      T dk[V], ddk[V], dvx[V], dv1[V], dv2[V], ddx[V], dd1[V], dd2[V];
+      act<T, V>(pk, hk, dk, ddk);
+      act<T, V>(px, hv, dvx, ddx);
+      act<T, V>(p1, hv, dv1, dd1);
+      act<T, V>(p2, hv, dv2, dd2);
       T part = T(0), ga = T(0), gu0 = T(0), gu1 = T(0), gu2 = T(0);
 #pragma unroll
       for (int i = 0; i < V; ++i) {
@@ -376,19 +446,13 @@ __global__ __launch_bounds__(256) void k_bwd_dst(Args<T> A) {
         }
       }
       if (G.el == 0) {
-        if (A.acc & TMDNET_ACC_EDGE) {
-          A.gC[k] += gc;
-          A.gu[3 * k] += gu0;
-          A.gu[3 * k + 1] += gu1;
-          A.gu[3 * k + 2] += gu2;
-        } else {
-          A.gC[k] = gc;
-          A.gu[3 * k] = gu0;
-          A.gu[3 * k + 1] = gu1;
-          A.gu[3 * k + 2] = gu2;
-        }
+        A.gC[k] = oc + gc;
+        A.gu[3 * k] = ou0 + gu0;
+        A.gu[3 * k + 1] = ou1 + gu1;
+        A.gu[3 * k + 2] = ou2 + gu2;
       }
-    }
+    };
+    edge_chunks<T, S>(A, b, e, EPW, G, body);
   }
   xor_slots(gq, A.L);
   reduce_waves<T, S, V>(gq, G.sub, lds);
@@ -409,6 +473,8 @@ __global__ __launch_bounds__(256) void k_bwd_src(Args<T> A) {
   const int hh = c0 / A.d, cc = c0 % A.d;
   const int vo = hh * 3 * A.d + cc;
   const bool hk = A.pk != nullptr, hv = A.pv != nullptr, hw = A.vec != nullptr;
+  const int pvd = hv ? A.d : 0, vcd = hw ? A.H : 0;  // branch-free optional loads
+  (void)vcd;
   T gk[V], gvx[V], gv1[V], gv2[V], gw0[V], gw1[V], gw2[V];
   zero(gk); zero(gvx); zero(gv1); zero(gv2); zero(gw0); zero(gw1); zero(gw2);
   if (j >= 0) {
@@ -427,23 +493,26 @@ __global__ __launch_bounds__(256) void k_bwd_src(Args<T> A) {
       zero(w0); zero(w1); zero(w2);
     }
     const int b = min(A.row_ptr[j], A.cap), e = min(A.row_ptr[j + 1], A.cap);
-    for (int k = b + EPW * G.sub + G.es; k < e; k += EPW * S) {
-      const int m = A.src[k];
-      const T Ce = A.C[k];
-      const T u0 = -A.u[3 * k], u1 = -A.u[3 * k + 1], u2 = -A.u[3 * k + 2];
-      T qm[V], gxm[V], g0[V], g1[V], g2[V], pk[V], dk[V], ddk[V];
+    const T* dummy = A.k + (size_t)j * A.ldk;
+    auto body = [&](int k, int m, T Ce, T u0, T u1, T u2) {
+      u0 = -u0; u1 = -u1; u2 = -u2;  // the reversed edge j->m
+      T qm[V], gxm[V], g0[V], g1[V], g2[V], pk[V], px[V], p1[V], p2[V];
       ldv<T, V>(qm, A.q + (size_t)m * A.ldq + c0);
       ldv<T, V>(gxm, A.gx + (size_t)m * A.H + c0);
       const T* gvm = A.gvec + (size_t)m * 3 * A.H + c0;
       ldv<T, V>(g0, gvm);
       ldv<T, V>(g1, gvm + A.H);
       ldv<T, V>(g2, gvm + 2 * A.H);
-      act<T, V>(A.pk + (size_t)k * A.ldpk + c0, hk, pk, dk, ddk, A.nt);
-      const T* pvs = A.pv + (size_t)k * A.ldpv + vo;
-      T px[V], dvx[V], dv1[V], dv2[V], dd[V];
-      act<T, V>(pvs, hv, px, dvx, dd, A.nt);
-      act<T, V>(pvs + A.d, hv, px, dv1, dd, A.nt);
-      act<T, V>(pvs + 2 * A.d, hv, px, dv2, dd, A.nt);
+      ldv<T, V>(pk, opt(A.pk, (size_t)k * A.ldpk + c0, dummy + c0));
+      const T* pvs = opt(A.pv, (size_t)k * A.ldpv + vo, dummy);
+      ldv<T, V>(px, pvs);
+      ldv<T, V>(p1, pvs + pvd);
+      ldv<T, V>(p2, pvs + 2 * pvd);
+      T dk[V], ddk[V], dvx[V], dv1[V], dv2[V], dd[V];
+      act<T, V>(pk, hk, dk, ddk);
+      act<T, V>(px, hv, dvx, dd);
+      act<T, V>(p1, hv, dv1, dd);
+      act<T, V>(p2, hv, dv2, dd);
       T part = T(0), ga = T(0);
 #pragma unroll
       for (int i = 0; i < V; ++i) {
@@ -468,7 +537,8 @@ __global__ __launch_bounds__(256) void k_bwd_src(Args<T> A) {
         gw1[i] += g1[i] * v1e;
         gw2[i] += g2[i] * v1e;
       }
-    }
+    };
+    edge_chunks<T, S>(A, b, e, EPW, G, body);
   }
   xor_slots(gk, A.L); xor_slots(gvx, A.L); xor_slots(gv1, A.L); xor_slots(gv2, A.L); xor_slots(gw0, A.L); xor_slots(gw1, A.L); xor_slots(gw2, A.L);
   T all[7 * V];
@@ -649,17 +719,9 @@ static int et_launch_vs(Args<T> A, hipStream_t st) {
   if (A.L > 64 || (A.L & (A.L - 1))) return kUnsupported;
   const int nbn = (A.n + (4 / S) - 1) / (4 / S);
   const dim3 g(nbn * cs), b(256);
-  if (cs == 4) {
-    if (KIND == 0) hipLaunchKernelGGL((k_fwd<T, V, S, 4, ORD>), g, b, 0, st, A);
-    else hipLaunchKernelGGL((k_bwd_src<T, V, S, 4>), g, b, 0, st, A);
-  } else if (cs == 2) {
-    if (KIND == 0) hipLaunchKernelGGL((k_fwd<T, V, S, 2, ORD>), g, b, 0, st, A);
-    else hipLaunchKernelGGL((k_bwd_src<T, V, S, 2>), g, b, 0, st, A);
-  } else {
-    if (KIND == 0) hipLaunchKernelGGL((k_fwd<T, V, S, 1, ORD>), g, b, 0, st, A);
-    else if (KIND == 1) hipLaunchKernelGGL((k_bwd_dst<T, V, S, 1>), g, b, 0, st, A);
-    else hipLaunchKernelGGL((k_bwd_src<T, V, S, 1>), g, b, 0, st, A);
-  }
+  if (KIND == 0) hipLaunchKernelGGL((k_fwd<T, V, S, 1, ORD>), g, b, 0, st, A);
+  else if (KIND == 1) hipLaunchKernelGGL((k_bwd_dst<T, V, S, 1>), g, b, 0, st, A);
+  else hipLaunchKernelGGL((k_bwd_src<T, V, S, 1>), g, b, 0, st, A);
   return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
 }
 
@@ -710,7 +772,6 @@ static int setup(Args<T>& A, int n, int H, int heads, const int32_t* row_ptr, co
   A.n = n; A.H = H; A.d = d; A.L = H / V; A.HC = H; A.lph = lph; A.cap = cap;
   A.row_ptr = row_ptr; A.src = src; A.order = order;
   A.xcd = 1;
-  A.nt = 0;
   A.q = (const T*)q; A.ldq = ldq; A.k = (const T*)k; A.ldk = ldk; A.v = (const T*)v; A.ldv = ldv_;
   A.vec = (const T*)vec; A.pk = (const T*)pk; A.ldpk = ldpk; A.pv = (const T*)pv; A.ldpv = ldpv;
   A.C = (const T*)C; A.u = (const T*)u;
