@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--roofline-atoms", type=int, default=50001)
     ap.add_argument("--roofline-reps", type=int, default=50)
     ap.add_argument("--eager", action="store_true", help="no HIP-graph capture (infer mode)")
+    ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 --pmc traffic passes")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
 
@@ -107,8 +109,9 @@ def et_algorithmic_bytes(E, N, H, s=4):
     return E * (4 + 4 + 12 + 4 * H * s) + N * (12 * H * s + 4)
 
 
-def roofline_probe(n_atoms, reps, H, dev):
-    """ET edge-aggregation forward on a C5-scale water box."""
+def probe_workload(n_atoms, H, dev):
+    """ET edge-aggregation forward on a C5-scale water box: returns a launcher of
+    ONE tmdnet_et_message_fwd call plus (E, L)."""
     from torchmdnet import kernels
     g = torch.Generator().manual_seed(7)
     L = (n_atoms / 0.1003) ** (1.0 / 3.0)
@@ -140,6 +143,58 @@ def roofline_probe(n_atoms, reps, H, dev):
                                        ptr(u), ptr(xo), ptr(vo), None, st)
         kernels.nat.check(rc, "tmdnet_et_message_fwd")
 
+    return launch, E, L
+
+
+PROBE_KERNEL = "k_fwd<float, 4, 1, 1, false>"
+
+
+def pmc_traffic(a):
+    """HBM-side bytes per launch of the probe kernel from rocprofv3 counters, one counter per pass
+    (MI355X_MICROARCH.md 'HBM'): FETCH_SIZE (KiB; gfx950 tallies 16-B/lane reads at half their bytes ->
+    x2) + WRITE_SIZE (KiB, exact for 16-B/lane stores).  FETCH_SIZE counts L2 misses served by the
+    Infinity Cache too, so this is L2->fabric traffic, an upper bound on HBM bytes.  Runs the probe in
+    a child process under rocprofv3; returns (bytes, detail) or (None, reason)."""
+    import csv
+    import glob
+    import shutil
+    import subprocess
+    import tempfile
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(prof):
+        return None, "rocprofv3 not found"
+    out = {}
+    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = tempfile.mkdtemp(prefix="tmdnet_pmc_")
+        cmd = [prof, "--pmc", ctr, "--output-format", "csv", "-d", d, "-o", "pmc", "--", sys.executable,
+               os.path.abspath(__file__), "--pmc-child", "--roofline-atoms", str(a.roofline_atoms),
+               "--channels", str(a.channels)]
+        try:
+            subprocess.run(cmd, timeout=300, check=True, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
+                           env=dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp")))
+        except (subprocess.SubprocessError, OSError) as e:
+            shutil.rmtree(d, ignore_errors=True)
+            return None, f"rocprofv3 {ctr} pass failed: {type(e).__name__}"
+        vals = []
+        for f in glob.glob(os.path.join(d, "**", "*counter_collection*.csv"), recursive=True):
+            for r in csv.DictReader(open(f)):
+                if PROBE_KERNEL in r.get("Kernel_Name", "") and r.get("Counter_Name") == ctr:
+                    vals.append(float(r["Counter_Value"]))
+        shutil.rmtree(d, ignore_errors=True)
+        if not vals:
+            return None, f"no {ctr} records for {PROBE_KERNEL}"
+        vals = vals[2:] or vals  # drop warm-up dispatches
+        out[ctr] = sum(vals) / len(vals) * 1024.0
+    fetch = 2.0 * out["FETCH_SIZE"]
+    return fetch + out["WRITE_SIZE"], {"fetch_bytes": round(fetch), "write_bytes": round(out["WRITE_SIZE"]),
+                                       "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), "
+                                                 "FETCH x2 (gfx950 16-B/lane correction); includes "
+                                                 "Infinity-Cache hits"}
+
+
+def roofline_probe(a, dev):
+    n_atoms, reps, H = a.roofline_atoms, a.roofline_reps, a.channels
+    launch, E, L = probe_workload(n_atoms, H, dev)
     for _ in range(5):
         launch()
     torch.cuda.synchronize()
@@ -154,12 +209,17 @@ def roofline_probe(n_atoms, reps, H, dev):
     ms = a0.elapsed_time(b0) / reps
     nbytes = et_algorithmic_bytes(E, n_atoms, H)
     gbs = nbytes / (ms * 1e-3) / 1e9
-    return {"kernel": "tmdnet_et_message_fwd (k_fwd<float,4,1,1,false>)",
+    res = {"kernel": "tmdnet_et_message_fwd (k_fwd<float,4,1,1,false>)",
             "workload": f"periodic water box, {n_atoms} atoms (Morton-renumbered as the model does), "
                         f"L={L:.1f} A, cutoff 5, E={E}, H={H}, fp32",
             "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
             "bytes_per_launch": nbytes, "ms_per_launch": round(ms, 4), "launches": reps}
+    if not a.no_pmc:
+        traffic, detail = pmc_traffic(a)
+        res["traffic"] = None if traffic is None else round(traffic)
+        res["traffic_detail"] = detail
+    return res
 
 
 def cpu_baseline(model, args, z, pos, batch, seconds):
@@ -190,6 +250,14 @@ def cpu_baseline(model, args, z, pos, batch, seconds):
 
 def main():
     a = parse()
+    if a.pmc_child:  # profiled child of pmc_traffic(): the probe kernel only
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda", 0)
+        launch, _, _ = probe_workload(a.roofline_atoms, a.channels, dev)
+        for _ in range(8):
+            launch()
+        torch.cuda.synchronize()
+        return
     ws, rank, dev = setup_dist()
     from torchmdnet import kernels
     from torchmdnet.models.model import create_model
@@ -289,7 +357,7 @@ def main():
                               "bytes_per_launch": nbytes, "ms_per_launch": round(ms, 5),
                               "launches": len(probe)}
     if rank == 0 and not a.no_roofline:
-        out["roofline"] = roofline_probe(a.roofline_atoms, a.roofline_reps, a.channels, dev)
+        out["roofline"] = roofline_probe(a, dev)
     if rank == 0 and ws == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(model, args, z, pos, batch, a.cpu_seconds)
     if rank == 0:
