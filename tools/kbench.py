@@ -10,6 +10,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "torchmd-net_amd"), ROOT]
 import torch  # noqa: E402
 from torchmdnet import kernels  # noqa: E402
+if os.environ.get("KBENCH_LIB"):  # A/B against another build (tools/build_ab.sh)
+    kernels.nat._LIB_PATH = os.path.abspath(os.environ["KBENCH_LIB"])
 from bench import qm9_like, et_algorithmic_bytes  # noqa: E402
 
 

@@ -189,39 +189,11 @@ __device__ __forceinline__ void reduce_waves(T (&a)[NV], int sub, T* lds) {
   }
 }
 
-// Row traversal with the per-edge scalars (source index, cutoff, unit vector) fetched once per
-// chunk of 64 edges by one coalesced load per lane and handed to the edge slots by cross-lane
-// permutes: the gathers of an edge then depend on ONE memory round trip instead of two.  The
-// chunk and slot loops are wave-uniform (permutes need every lane active); a slot past the end of
-// the row skips the body.
-template <typename T, int S, typename F>
-__device__ __forceinline__ void edge_chunks(const Args<T>& A, int b, int e, int EPW, const Geo& G,
-                                            F&& body) {
-  const int lane = lane_id();
-  for (int c = b; c < e; c += TMD_WAVE) {
-    const int n = min(TMD_WAVE, e - c);
-    int s_r = 0;
-    T C_r = T(0), u0_r = T(0), u1_r = T(0), u2_r = T(0);
-    if (lane < n) {
-      const int k = c + lane;
-      s_r = A.src[k];
-      C_r = A.C[k];
-      u0_r = A.u[3 * k];
-      u1_r = A.u[3 * k + 1];
-      u2_r = A.u[3 * k + 2];
-    }
-    for (int j0 = EPW * G.sub; j0 < n; j0 += EPW * S) {
-      const int j = j0 + G.es;
-      const int jj = j < n ? j : n - 1;
-      const int s = __shfl(s_r, jj);
-      const T Ce = __shfl(C_r, jj), u0 = __shfl(u0_r, jj), u1 = __shfl(u1_r, jj), u2 = __shfl(u2_r, jj);
-      if (j < n) body(c + j, s, Ce, u0, u1, u2);
-    }
-  }
-}
-
-// The same traversal with the per-edge STREAM (dk/dv rows, read once) software-pipelined PD edges
-// ahead: `ld(k, st)` loads edge k's stream rows into registers; `body(k, s, C, u0, u1, u2, st, pre)`
+// Row traversal.  The per-edge scalars (source index, cutoff, unit vector) are fetched once per chunk
+// of 64 edges by one coalesced load per lane and handed to the edge slots by cross-lane permutes, so
+// an edge's gathers depend on ONE memory round trip, not two.  The chunk and slot loops are
+// wave-uniform (permutes need every lane active); a slot past the end of the row skips the body.
+// The per-edge STREAM (dk/dv rows, read once) is software-pipelined PD edges ahead: `ld(k, st)` loads edge k's stream rows into registers; `body(k, s, C, u0, u1, u2, st, pre)`
 // issues its source gathers, then calls `pre()` -- which issues the NEXT edge's stream loads -- and
 // only then consumes data.  Loads retire in issue order, so waiting for this edge's gathers leaves
 // the next edges' stream in flight (a counted vmcnt).  PD = 1 is used: C5 fwd 1.44 -> 1.35-1.41 ms;
@@ -377,7 +349,15 @@ __global__ __launch_bounds__(256) void k_bwd_dst(Args<T> A) {
     const int b = min(A.row_ptr[t], A.cap), e = min(A.row_ptr[t + 1], A.cap);
     const T* dummy = A.q + (size_t)t * A.ldq;
     const bool acc_edge = (A.acc & TMDNET_ACC_EDGE) && G.el == 0;
-    auto body = [&](int k, int s, T Ce, T u0, T u1, T u2) {
+    struct St { T k[V], x[V], a[V], b[V]; };
+    auto ld = [&](int k, St& st) {
+      ldv<T, V>(st.k, opt(A.pk, (size_t)k * A.ldpk + c0, dummy + c0));
+      const T* pvs = opt(A.pv, (size_t)k * A.ldpv + vo, dummy);
+      ldv<T, V>(st.x, pvs);
+      ldv<T, V>(st.a, pvs + pvd);
+      ldv<T, V>(st.b, pvs + 2 * pvd);
+    };
+    auto body = [&](int k, int s, T Ce, T u0, T u1, T u2, const St& st, auto&& pre) {
       T oc = T(0), ou0 = T(0), ou1 = T(0), ou2 = T(0);  // accumulate mode: issued with the loads
       if (acc_edge) {
         oc = A.gC[k];
@@ -385,22 +365,22 @@ __global__ __launch_bounds__(256) void k_bwd_dst(Args<T> A) {
         ou1 = A.gu[3 * k + 1];
         ou2 = A.gu[3 * k + 2];
       }
-      T kk[V], pk[V], vx[V], v1[V], v2[V], px[V], p1[V], p2[V], w0[V], w1[V], w2[V];
+      T kk[V], vx[V], v1[V], v2[V], w0[V], w1[V], w2[V];
       ldv<T, V>(kk, A.k + (size_t)s * A.ldk + c0);
-      ldv<T, V>(pk, opt(A.pk, (size_t)k * A.ldpk + c0, dummy + c0));
       const T* vs = A.v + (size_t)s * A.ldv + vo;
-      const T* pvs = opt(A.pv, (size_t)k * A.ldpv + vo, dummy);
       ldv<T, V>(vx, vs);
       ldv<T, V>(v1, vs + A.d);
       ldv<T, V>(v2, vs + 2 * A.d);
-      ldv<T, V>(px, pvs);
-      ldv<T, V>(p1, pvs + pvd);
-      ldv<T, V>(p2, pvs + 2 * pvd);
       const T* vecs = hw ? A.vec + (size_t)s * 3 * A.H + c0 : dummy + c0;
       ldv<T, V>(w0, vecs);
       ldv<T, V>(w1, vecs + vcd);
       ldv<T, V>(w2, vecs + 2 * vcd);
+      pre();
       if (!hw) { zero(w0); zero(w1); zero(w2); }
+      const T (&pk)[V] = st.k;
+      const T (&px)[V] = st.x;
+      const T (&p1)[V] = st.a;
+      const T (&p2)[V] = st.b;
       T dk[V], ddk[V], dvx[V], dv1[V], dv2[V], ddx[V], dd1[V], dd2[V];
       act<T, V>(pk, hk, dk, ddk);
       act<T, V>(px, hv, dvx, ddx);
@@ -452,7 +432,7 @@ __global__ __launch_bounds__(256) void k_bwd_dst(Args<T> A) {
         A.gu[3 * k + 2] = ou2 + gu2;
       }
     };
-    edge_chunks<T, S>(A, b, e, EPW, G, body);
+    edge_chunks_pf<T, S, 1, St>(A, b, e, EPW, G, ld, body);
   }
   xor_slots(gq, A.L);
   reduce_waves<T, S, V>(gq, G.sub, lds);
@@ -494,20 +474,29 @@ __global__ __launch_bounds__(256) void k_bwd_src(Args<T> A) {
     }
     const int b = min(A.row_ptr[j], A.cap), e = min(A.row_ptr[j + 1], A.cap);
     const T* dummy = A.k + (size_t)j * A.ldk;
-    auto body = [&](int k, int m, T Ce, T u0, T u1, T u2) {
+    struct St { T k[V], x[V], a[V], b[V]; };
+    auto ld = [&](int k, St& st) {
+      ldv<T, V>(st.k, opt(A.pk, (size_t)k * A.ldpk + c0, dummy + c0));
+      const T* pvs = opt(A.pv, (size_t)k * A.ldpv + vo, dummy);
+      ldv<T, V>(st.x, pvs);
+      ldv<T, V>(st.a, pvs + pvd);
+      ldv<T, V>(st.b, pvs + 2 * pvd);
+    };
+    auto body = [&](int k, int m, T Ce, T u0, T u1, T u2, const St& st, auto&& pre) {
       u0 = -u0; u1 = -u1; u2 = -u2;  // the reversed edge j->m
-      T qm[V], gxm[V], g0[V], g1[V], g2[V], pk[V], px[V], p1[V], p2[V];
+      (void)k;
+      T qm[V], gxm[V], g0[V], g1[V], g2[V];
       ldv<T, V>(qm, A.q + (size_t)m * A.ldq + c0);
       ldv<T, V>(gxm, A.gx + (size_t)m * A.H + c0);
       const T* gvm = A.gvec + (size_t)m * 3 * A.H + c0;
       ldv<T, V>(g0, gvm);
       ldv<T, V>(g1, gvm + A.H);
       ldv<T, V>(g2, gvm + 2 * A.H);
-      ldv<T, V>(pk, opt(A.pk, (size_t)k * A.ldpk + c0, dummy + c0));
-      const T* pvs = opt(A.pv, (size_t)k * A.ldpv + vo, dummy);
-      ldv<T, V>(px, pvs);
-      ldv<T, V>(p1, pvs + pvd);
-      ldv<T, V>(p2, pvs + 2 * pvd);
+      pre();
+      const T (&pk)[V] = st.k;
+      const T (&px)[V] = st.x;
+      const T (&p1)[V] = st.a;
+      const T (&p2)[V] = st.b;
       T dk[V], ddk[V], dvx[V], dv1[V], dv2[V], dd[V];
       act<T, V>(pk, hk, dk, ddk);
       act<T, V>(px, hv, dvx, dd);
@@ -538,7 +527,7 @@ __global__ __launch_bounds__(256) void k_bwd_src(Args<T> A) {
         gw2[i] += g2[i] * v1e;
       }
     };
-    edge_chunks<T, S>(A, b, e, EPW, G, body);
+    edge_chunks_pf<T, S, 1, St>(A, b, e, EPW, G, ld, body);
   }
   xor_slots(gk, A.L); xor_slots(gvx, A.L); xor_slots(gv1, A.L); xor_slots(gv2, A.L); xor_slots(gw0, A.L); xor_slots(gw1, A.L); xor_slots(gw2, A.L);
   T all[7 * V];
