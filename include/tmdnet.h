@@ -143,27 +143,34 @@ int tmdnet_nbr_embed_bwd(int dtype, int n_nodes, int hidden, const int32_t* row_
 /* ------------------------------------------------------------------------------------------
  * TensorNet edge kernels (reference models/tensornet.py:287-332).  Tensors are [N][H][3][3].
  * self0_mult >= 1: multiplicity of atom 0's self loop (static_shapes padding emulation,
- * tensornet.py:215-221; 1 = no padding).  Both require the symmetric CSR list.
+ * tensornet.py:215-221; 1 = no padding).  If pad_pairs (device int32, the pair count found by
+ * tmdnet_nl_build) is non-NULL the multiplicity is computed on the device instead:
+ * 1 + max(0, pad_capacity - *pad_pairs) (no host sync: HIP-graph capturable).  Both require the
+ * symmetric CSR list.
  * Embedding:  I/A/S[n] = sum_{edges e with reference edge_index[0]==n} (P[n] + Q[dst]) * W_k[e] * C[e]
  *             * {Id, skew(u[e]), sym(u[e])},  W = [E][3H] = distance_proj1|2|3(rbf) (pre-cutoff),
  *             P = emb(z) Wa^T + b, Q = emb(z) Wb^T  (emb2 split into its two input halves). */
 int tmdnet_tn_embed_fwd(int dtype, int n_nodes, int hidden, const int32_t* row_ptr,
-                        const int32_t* src, int max_pairs, double self0_mult, const void* P,
+                        const int32_t* src, int max_pairs, double self0_mult,
+                        const int32_t* pad_pairs, int pad_capacity, const void* P,
                         const void* Q, const void* W, int ld_w, const void* cutoff, const void* unit,
                         void* I, void* A, void* S, void* stream);
 int tmdnet_tn_embed_bwd(int dtype, int n_nodes, int hidden, const int32_t* row_ptr,
-                        const int32_t* src, int max_pairs, double self0_mult, const void* P,
+                        const int32_t* src, int max_pairs, double self0_mult,
+                        const int32_t* pad_pairs, int pad_capacity, const void* P,
                         const void* Q, const void* W, int ld_w, const void* cutoff, const void* unit,
                         const void* gI, const void* gA, const void* gS, void* gP, void* gQ, void* gW,
                         void* gcut, void* gunit, void* stream);
 /* Message: msg[n] = sum_{edges e with edge_index[0]==n} ea[e,h,0] I[m] + ea[e,h,1] A[m] + ea[e,h,2] S[m],
  * m = edge_index[1][e]; edge_attr [E][3H] interleaved (h, component) as reshape(E, H, 3). */
 int tmdnet_tn_message_fwd(int dtype, int n_nodes, int hidden, const int32_t* row_ptr,
-                          const int32_t* src, int max_pairs, double self0_mult, const void* edge_attr,
+                          const int32_t* src, int max_pairs, double self0_mult,
+                          const int32_t* pad_pairs, int pad_capacity, const void* edge_attr,
                           int ld_ea, const void* I, const void* A, const void* S, void* msg,
                           void* stream);
 int tmdnet_tn_message_bwd(int dtype, int n_nodes, int hidden, const int32_t* row_ptr,
-                          const int32_t* src, int max_pairs, double self0_mult, const void* edge_attr,
+                          const int32_t* src, int max_pairs, double self0_mult,
+                          const int32_t* pad_pairs, int pad_capacity, const void* edge_attr,
                           int ld_ea, const void* I, const void* A, const void* S, const void* grad_msg,
                           void* g_edge_attr, void* gI, void* gA, void* gS, void* stream);
 

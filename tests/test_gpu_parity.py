@@ -474,3 +474,31 @@ def test_et_fused_stack_matches_per_layer_path(infl):
             assert (a is None or torch.count_nonzero(a) == 0) and (b is None or torch.count_nonzero(b) == 0)
             continue
         assert _rel(a.cpu(), b.cpu()) < 1e-9  # norm-relative: gradients reach 1e13 here
+
+
+@pytest.mark.parametrize("static_shapes", [True, False])
+def test_graphed_tensornet_matches_eager(static_shapes):
+    """TensorNet under HIP-graph capture; with static_shapes the reference's padding multiplicity on
+    atom 0 is computed on the device from the pair count (no host sync)."""
+    from torchmdnet.graphs import GraphedEnergyForces
+    from torchmdnet.models.model import create_model
+    _seed()
+    m = create_model(yaml_args("tensornet", embedding_dimension=64, num_layers=2, num_rbf=16, derivative=True,
+                               output_model="Scalar", max_num_neighbors=32)).to(DEV)
+    m.representation_model.static_shapes = static_shapes
+    z, pos, batch = O.qm9_like(6)
+    z, pos, batch = z.to(DEV), pos.float().to(DEV), batch.to(DEV)
+    gm = GraphedEnergyForces(m, z, pos, batch)
+    gen = torch.Generator(device=DEV).manual_seed(9)
+    for _ in range(2):
+        p2 = pos + 0.05 * torch.randn(pos.shape, device=DEV, generator=gen)
+        y, f = gm(p2)
+        y, f = y.clone(), f.clone()
+        gm.check_capacity()
+        gm.release()
+        ye, fe = m(z, p2.clone(), batch)
+        for d in gm.dists:
+            d.static_capacity = gm.edge_capacity
+        assert _rel(y.detach().cpu(), ye.detach().cpu()) < 1e-5
+        assert _rel(f.detach().cpu(), fe.detach().cpu()) < 1e-5
+    gm.release()

@@ -61,6 +61,11 @@ __device__ __forceinline__ void dsymm(const T (&g)[9], T x, T y, T z, T& dx, T& 
   dy = (g[3] + g[1]) * x + (g[4] + g[4]) * y + (g[5] + g[7]) * z - tr * y;
   dz = (g[6] + g[2]) * x + (g[7] + g[5]) * y + (g[8] + g[8]) * z - tr * z;
 }
+template <typename T> struct Args;
+// Multiplicity of atom 0's self loop.  With a device pair count (static_shapes under HIP-graph
+// capture) it is computed here: 1 + (reference padding capacity - pairs found), a uniform scalar load.
+template <typename T> __device__ __forceinline__ T mult0_of(const Args<T>& A);
+
 template <typename T> __device__ __forceinline__ T dot9(const T (&a)[9], const T (&b)[9]) {
   T s = T(0);
 #pragma unroll
@@ -71,6 +76,8 @@ template <typename T> __device__ __forceinline__ T dot9(const T (&a)[9], const T
 template <typename T> struct Args {
   int n, H, nblk, cap;
   T mult0;
+  const int32_t* npd;  // device num_pairs: mult0 = 1 + max(0, padcap - *npd) (HIP-graph capturable)
+  int padcap;
   const int32_t* row_ptr;
   const int32_t* src;
   // embedding
@@ -88,6 +95,12 @@ template <typename T> struct Args {
   const T* gmsg;
   T* gea; T* gTi; T* gTa; T* gTs;
 };
+
+template <typename T> __device__ __forceinline__ T mult0_of(const Args<T>& A) {
+  if (A.npd == nullptr) return A.mult0;
+  const int pad = A.padcap - __builtin_amdgcn_readfirstlane(A.npd[0]);
+  return T(1 + (pad > 0 ? pad : 0));
+}
 
 __device__ __forceinline__ void wave_node(int nblk, int& node, int& ch0) {
   const int w = blockIdx.x * (blockDim.x / TMD_WAVE) + threadIdx.x / TMD_WAVE;
@@ -111,7 +124,7 @@ __global__ __launch_bounds__(256) void k_embed_fwd(Args<T> A) {
   const int b = min(A.row_ptr[n], A.cap), e = min(A.row_ptr[n + 1], A.cap);
   for (int k = b; k < e; ++k) {
     const int m = A.src[k];
-    const T mult = (m == n && n == 0) ? A.mult0 : T(1);
+    const T mult = (m == n && n == 0) ? mult0_of(A) : T(1);
     const T zc = (Pn + A.Q[(size_t)m * A.H + hc]) * A.C[k] * mult;
     const T* wr = A.W + (size_t)k * A.ldw;
     const T w1 = wr[hc], w2 = wr[A.H + hc], w3 = wr[2 * A.H + hc];
@@ -162,7 +175,7 @@ __global__ __launch_bounds__(256) void k_embed_bwd_dst(Args<T> A) {
   const int b = min(A.row_ptr[n], A.cap), e = min(A.row_ptr[n + 1], A.cap);
   for (int k = b; k < e; ++k) {
     const int m = A.src[k];
-    const T mult = (m == n && n == 0) ? A.mult0 : T(1);
+    const T mult = (m == n && n == 0) ? mult0_of(A) : T(1);
     const T Ck = A.C[k];
     const T ux = -A.u[3 * k], uy = -A.u[3 * k + 1], uz = -A.u[3 * k + 2];
     T sk[9], sy[9];
@@ -226,7 +239,7 @@ __global__ __launch_bounds__(256) void k_embed_bwd_src(Args<T> A) {
   const int b = min(A.row_ptr[m], A.cap), e = min(A.row_ptr[m + 1], A.cap);
   for (int k = b; k < e; ++k) {
     const int n = A.src[k];  // row edge n->m; its reverse m->n contributed Q[m] to I/A/S[n]
-    const T mult = (m == n && n == 0) ? A.mult0 : T(1);
+    const T mult = (m == n && n == 0) ? mult0_of(A) : T(1);
     const size_t o = ((size_t)n * A.H + hc) * 9;
     T gI[9], gA[9], gS[9];
     ld9(gI, A.gI + o);
@@ -261,7 +274,7 @@ __global__ __launch_bounds__(256) void k_msg_fwd(Args<T> A) {
   const int b = min(A.row_ptr[n], A.cap), e = min(A.row_ptr[n + 1], A.cap);
   for (int k = b; k < e; ++k) {
     const int m = A.src[k];
-    const T mult = (m == n && n == 0) ? A.mult0 : T(1);
+    const T mult = (m == n && n == 0) ? mult0_of(A) : T(1);
     const T* er = A.ea + (size_t)k * A.ldea + 3 * hc;
     const T f0 = er[0] * mult, f1 = er[1] * mult, f2 = er[2] * mult;
     const size_t o = ((size_t)m * A.H + hc) * 9;
@@ -289,7 +302,7 @@ __global__ __launch_bounds__(256) void k_msg_bwd_dst(Args<T> A) {
   const int b = min(A.row_ptr[n], A.cap), e = min(A.row_ptr[n + 1], A.cap);
   for (int k = b; k < e; ++k) {
     const int m = A.src[k];
-    const T mult = (m == n && n == 0) ? A.mult0 : T(1);
+    const T mult = (m == n && n == 0) ? mult0_of(A) : T(1);
     const size_t o = ((size_t)m * A.H + hc) * 9;
     T ti[9], ta[9], ts[9];
     ld9(ti, A.Ti + o);
@@ -319,7 +332,7 @@ __global__ __launch_bounds__(256) void k_msg_bwd_src(Args<T> A) {
   const int b = min(A.row_ptr[m], A.cap), e = min(A.row_ptr[m + 1], A.cap);
   for (int k = b; k < e; ++k) {
     const int n = A.src[k];
-    const T mult = (m == n && n == 0) ? A.mult0 : T(1);
+    const T mult = (m == n && n == 0) ? mult0_of(A) : T(1);
     const T* er = A.ea + (size_t)k * A.ldea + 3 * hc;
     const T f0 = er[0] * mult, f1 = er[1] * mult, f2 = er[2] * mult;
     T g[9];
@@ -349,9 +362,11 @@ static int launch(void (*k)(Args<T>), const Args<T>& A, hipStream_t st) {
 }
 
 template <typename T>
-static Args<T> base(int n, int H, const int32_t* row_ptr, const int32_t* src, int cap, double mult0) {
+static Args<T> base(int n, int H, const int32_t* row_ptr, const int32_t* src, int cap, double mult0,
+                    const int32_t* npd, int padcap) {
   Args<T> A{};
   A.n = n; A.H = H; A.nblk = (H + TMD_WAVE - 1) / TMD_WAVE; A.cap = cap; A.mult0 = (T)mult0;
+  A.npd = npd; A.padcap = padcap;
   A.row_ptr = row_ptr; A.src = src;
   return A;
 }
@@ -374,12 +389,14 @@ using namespace tmd;
 
 extern "C" int tmdnet_tn_embed_fwd(int dtype, int n_nodes, int hidden, const int32_t* row_ptr,
                                    const int32_t* src, int max_pairs, double self0_mult,
+                                   const int32_t* pad_pairs, int pad_capacity,
                                    const void* P, const void* Q, const void* W, int ld_w,
                                    const void* cutoff, const void* unit, void* I, void* A, void* S,
                                    void* stream) {
   hipStream_t st = (hipStream_t)stream;
   TN_DISPATCH(dtype, {
-    auto a = tn::base<T>(n_nodes, hidden, row_ptr, src, max_pairs, self0_mult);
+    auto a = tn::base<T>(n_nodes, hidden, row_ptr, src, max_pairs, self0_mult, pad_pairs,
+                                 pad_capacity);
     a.P = (const T*)P; a.Q = (const T*)Q; a.W = (const T*)W; a.ldw = ld_w;
     a.C = (const T*)cutoff; a.u = (const T*)unit; a.I = (T*)I; a.A = (T*)A; a.S = (T*)S;
     return tn::launch<T>(tn::k_embed_fwd<T>, a, st);
@@ -388,13 +405,15 @@ extern "C" int tmdnet_tn_embed_fwd(int dtype, int n_nodes, int hidden, const int
 
 extern "C" int tmdnet_tn_embed_bwd(int dtype, int n_nodes, int hidden, const int32_t* row_ptr,
                                    const int32_t* src, int max_pairs, double self0_mult,
+                                   const int32_t* pad_pairs, int pad_capacity,
                                    const void* P, const void* Q, const void* W, int ld_w,
                                    const void* cutoff, const void* unit, const void* gI,
                                    const void* gA, const void* gS, void* gP, void* gQ, void* gW,
                                    void* gcut, void* gunit, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   TN_DISPATCH(dtype, {
-    auto a = tn::base<T>(n_nodes, hidden, row_ptr, src, max_pairs, self0_mult);
+    auto a = tn::base<T>(n_nodes, hidden, row_ptr, src, max_pairs, self0_mult, pad_pairs,
+                                 pad_capacity);
     a.P = (const T*)P; a.Q = (const T*)Q; a.W = (const T*)W; a.ldw = ld_w;
     a.C = (const T*)cutoff; a.u = (const T*)unit;
     a.gI = (const T*)gI; a.gA = (const T*)gA; a.gS = (const T*)gS;
@@ -415,11 +434,13 @@ extern "C" int tmdnet_tn_embed_bwd(int dtype, int n_nodes, int hidden, const int
 
 extern "C" int tmdnet_tn_message_fwd(int dtype, int n_nodes, int hidden, const int32_t* row_ptr,
                                      const int32_t* src, int max_pairs, double self0_mult,
+                                   const int32_t* pad_pairs, int pad_capacity,
                                      const void* edge_attr, int ld_ea, const void* I, const void* A,
                                      const void* S, void* msg, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   TN_DISPATCH(dtype, {
-    auto a = tn::base<T>(n_nodes, hidden, row_ptr, src, max_pairs, self0_mult);
+    auto a = tn::base<T>(n_nodes, hidden, row_ptr, src, max_pairs, self0_mult, pad_pairs,
+                                 pad_capacity);
     a.ea = (const T*)edge_attr; a.ldea = ld_ea;
     a.Ti = (const T*)I; a.Ta = (const T*)A; a.Ts = (const T*)S; a.msg = (T*)msg;
     return tn::launch<T>(tn::k_msg_fwd<T>, a, st);
@@ -428,12 +449,14 @@ extern "C" int tmdnet_tn_message_fwd(int dtype, int n_nodes, int hidden, const i
 
 extern "C" int tmdnet_tn_message_bwd(int dtype, int n_nodes, int hidden, const int32_t* row_ptr,
                                      const int32_t* src, int max_pairs, double self0_mult,
+                                   const int32_t* pad_pairs, int pad_capacity,
                                      const void* edge_attr, int ld_ea, const void* I, const void* A,
                                      const void* S, const void* grad_msg, void* g_edge_attr,
                                      void* gI, void* gA, void* gS, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   TN_DISPATCH(dtype, {
-    auto a = tn::base<T>(n_nodes, hidden, row_ptr, src, max_pairs, self0_mult);
+    auto a = tn::base<T>(n_nodes, hidden, row_ptr, src, max_pairs, self0_mult, pad_pairs,
+                                 pad_capacity);
     a.ea = (const T*)edge_attr; a.ldea = ld_ea;
     a.Ti = (const T*)I; a.Ta = (const T*)A; a.Ts = (const T*)S;
     a.gmsg = (const T*)grad_msg; a.gea = (T*)g_edge_attr;

@@ -27,9 +27,6 @@ class GraphedEnergyForces:
         if not model.derivative:
             raise ValueError("GraphedEnergyForces captures TorchMD_Net(derivative=True)")
         rep = model.representation_model
-        if getattr(rep, "static_shapes", False):
-            raise NotImplementedError("TensorNet static_shapes padding needs a device-side multiplicity; "
-                                      "capture TensorNet with static_shapes=False")
         self.model = model
         dev = pos.device
         self.z = z.clone()

@@ -604,8 +604,22 @@ def nbr_embed(x, w, C, graph):
 
 
 # ----------------------------------------------------------------------------- TensorNet
+def _self0_args(graph):
+    """(host multiplicity, device pair count, padding capacity) for the TN kernels' atom-0 self loop
+    (static_shapes emulation).  ``graph.self0_dev`` = (num_pairs tensor, capacity) selects the
+    device-side form used under HIP-graph capture."""
+    dev = getattr(graph, "self0_dev", None)
+    if dev is not None:
+        return 1.0, nat.ptr(dev[0]), int(dev[1])
+    return float(getattr(graph, "self0_mult", 1.0)), None, 0
+
+
 def _self0_weight(graph, like):
     w = torch.ones(graph.n_edges, dtype=like.dtype, device=like.device)
+    dev = getattr(graph, "self0_dev", None)
+    if dev is not None:
+        m = (1 + (dev[1] - dev[0].to(torch.int64)).clamp(min=0)).to(like.dtype)
+        return torch.where((graph.src == 0) & (graph.dst == 0), m.expand_as(w), w)
     m = getattr(graph, "self0_mult", 1.0)
     if m != 1.0:
         w = torch.where((graph.src == 0) & (graph.dst == 0), torch.full_like(w, m), w)
@@ -625,10 +639,11 @@ def _sym(v):
 
 def tn_embed_composite(P, Q, W, C, u, graph):
     """tensornet.py:295-315 in reference orientation (scatter to edge_index[0])."""
-    src, dst = graph.src.long(), graph.dst.long()
+    valid = (graph.src >= 0).to(P.dtype)  # static-capacity padding slots (-1) carry nothing
+    src, dst = graph.src.long().clamp(min=0), graph.dst.long().clamp(min=0)
     H = P.shape[1]
     N = graph.n_nodes
-    wt = (_self0_weight(graph, C) * C).unsqueeze(1)
+    wt = (_self0_weight(graph, C) * C * valid).unsqueeze(1)
     z = (P.index_select(0, src) + Q.index_select(0, dst)) * wt
     W1, W2, W3 = W[:, :H], W[:, H:2 * H], W[:, 2 * H:]
     eye = torch.eye(3, dtype=P.dtype, device=P.device)
@@ -641,9 +656,10 @@ def tn_embed_composite(P, Q, W, C, u, graph):
 
 def tn_message_composite(ea, I, A, S, graph):
     """tensornet.py:329-332 (gather edge_index[1], scatter edge_index[0]) for the three components."""
-    src, dst = graph.src.long(), graph.dst.long()
+    valid = (graph.src >= 0).to(I.dtype)
+    src, dst = graph.src.long().clamp(min=0), graph.dst.long().clamp(min=0)
     N, H = I.shape[0], I.shape[1]
-    f = (ea.view(-1, H, 3) * _self0_weight(graph, ea).view(-1, 1, 1))
+    f = (ea.view(-1, H, 3) * (_self0_weight(graph, ea) * valid).view(-1, 1, 1))
     m = f[..., 0, None, None] * I.index_select(0, dst) + f[..., 1, None, None] * A.index_select(0, dst) \
         + f[..., 2, None, None] * S.index_select(0, dst)
     return torch.zeros((N, H, 3, 3), dtype=I.dtype, device=I.device).index_add(0, src, m)
@@ -657,7 +673,7 @@ class _TNEmbed(Function):
         o = dict(dtype=P.dtype, device=P.device)
         I, A, S = (torch.empty((N, H, 3, 3), **o) for _ in range(3))
         rc = lib.tmdnet_tn_embed_fwd(nat.dtype_code(P.dtype), N, H, nat.ptr(graph.row_ptr), nat.ptr(graph.src),
-                                     graph.n_edges, float(getattr(graph, "self0_mult", 1.0)), nat.ptr(P),
+                                     graph.n_edges, *_self0_args(graph), nat.ptr(P),
                                      nat.ptr(Q), nat.ptr(W), _ld(W), nat.ptr(C), nat.ptr(u), nat.ptr(I),
                                      nat.ptr(A), nat.ptr(S), nat.stream(P.device))
         nat.check(rc, "tmdnet_tn_embed_fwd")
@@ -686,7 +702,7 @@ class _TNEmbedBwd(Function):
         gW = torch.empty((E, 3 * H), **o)
         gC, gu = torch.empty((E,), **o), torch.empty((E, 3), **o)
         rc = lib.tmdnet_tn_embed_bwd(nat.dtype_code(P.dtype), N, H, nat.ptr(graph.row_ptr), nat.ptr(graph.src), E,
-                                     float(getattr(graph, "self0_mult", 1.0)), nat.ptr(P), nat.ptr(Q), nat.ptr(W),
+                                     *_self0_args(graph), nat.ptr(P), nat.ptr(Q), nat.ptr(W),
                                      _ld(W), nat.ptr(C), nat.ptr(u), nat.ptr(gI), nat.ptr(gA), nat.ptr(gS),
                                      nat.ptr(gP), nat.ptr(gQ), nat.ptr(gW), nat.ptr(gC), nat.ptr(gu),
                                      nat.stream(P.device))
@@ -718,7 +734,7 @@ class _TNMessage(Function):
         N, H = I.shape[0], I.shape[1]
         msg = torch.empty((N, H, 3, 3), dtype=I.dtype, device=I.device)
         rc = lib.tmdnet_tn_message_fwd(nat.dtype_code(I.dtype), N, H, nat.ptr(graph.row_ptr), nat.ptr(graph.src),
-                                       graph.n_edges, float(getattr(graph, "self0_mult", 1.0)), nat.ptr(ea),
+                                       graph.n_edges, *_self0_args(graph), nat.ptr(ea),
                                        _ld(ea), nat.ptr(I), nat.ptr(A), nat.ptr(S), nat.ptr(msg),
                                        nat.stream(I.device))
         nat.check(rc, "tmdnet_tn_message_fwd")
@@ -744,7 +760,7 @@ class _TNMessageBwd(Function):
         gea = torch.empty((E, 3 * H), dtype=I.dtype, device=I.device)
         gI, gA, gS = (torch.empty_like(I) for _ in range(3))
         rc = lib.tmdnet_tn_message_bwd(nat.dtype_code(I.dtype), N, H, nat.ptr(graph.row_ptr), nat.ptr(graph.src), E,
-                                       float(getattr(graph, "self0_mult", 1.0)), nat.ptr(ea), _ld(ea), nat.ptr(I),
+                                       *_self0_args(graph), nat.ptr(ea), _ld(ea), nat.ptr(I),
                                        nat.ptr(A), nat.ptr(S), nat.ptr(gmsg), nat.ptr(gea), nat.ptr(gI),
                                        nat.ptr(gA), nat.ptr(gS), nat.stream(I.device))
         nat.check(rc, "tmdnet_tn_message_bwd")

@@ -106,7 +106,11 @@ class TensorNet(nn.Module):
     def _forward(self, z: Tensor, pos: Tensor, batch: Tensor) -> Tensor:
         graph = self.distance.graph(pos, batch)
         cap = self.distance._max_pairs(pos.shape[0])
-        graph.self0_mult = float(1 + max(0, cap - graph.num_pairs)) if self.static_shapes else 1.0
+        if self.static_shapes and graph.static:
+            # capture mode: the padding count stays on the device (no host sync)
+            graph.self0_dev = (graph.num_pairs_dev, cap)
+        else:
+            graph.self0_mult = float(1 + max(0, cap - graph.num_pairs)) if self.static_shapes else 1.0
         de = self.distance_expansion
         if self.trainable_rbf and torch.is_grad_enabled():
             edge_attr = de(graph.distances)
