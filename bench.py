@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--roofline-reps", type=int, default=50)
     ap.add_argument("--eager", action="store_true", help="no HIP-graph capture (infer mode)")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 --pmc traffic passes")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="skip the secondary lines (TensorNet C3 graph replay, ET training step)")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
@@ -222,6 +224,73 @@ def roofline_probe(a, dev):
     return res
 
 
+def timed_loop(step, warmup, steps, ws, dev):
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    barrier(ws)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    barrier(ws)
+    return max_over_ranks(time.perf_counter() - t0, ws, dev)
+
+
+def rmd17_like(n_mol, gen_seed):
+    """aspirin C9H8O4 x n_mol, pos = randn * 1.6 A."""
+    g = torch.Generator().manual_seed(gen_seed)
+    z1 = torch.tensor([6] * 9 + [1] * 8 + [8] * 4, dtype=torch.long)
+    z = z1.repeat(n_mol)
+    pos = torch.randn(z.shape[0], 3, generator=g, dtype=torch.float64) * 1.6
+    batch = torch.arange(n_mol, dtype=torch.long).repeat_interleave(z1.shape[0])
+    return z, pos, batch
+
+
+def secondary_tensornet(a, ws, rank, dev):
+    """C3: TensorNet-rMD17 (8 x 21 atoms, O(3), static_shapes as the reference default), energy +
+    forces, HIP-graph replay, molecules/s over all ranks."""
+    import yaml
+    from torchmdnet.graphs import GraphedEnergyForces
+    from torchmdnet.models.model import create_model
+    with open(os.path.join(ROOT, "tests", "golden", "configs", "tensornet_rmd17.yaml")) as f:
+        args = yaml.safe_load(f)
+    args.update(prior_model=None, precision=32, derivative=True)
+    torch.manual_seed(0)
+    model = create_model(args).to(dev)
+    n_mol = 8
+    z, pos, batch = rmd17_like(n_mol, 1 + rank)
+    z, pos, batch = z.to(dev), pos.float().to(dev), batch.to(dev)
+    gm = GraphedEnergyForces(model, z, pos, batch)
+    el = timed_loop(lambda: gm(pos), a.warmup, a.steps, ws, dev)
+    gm.check_capacity()
+    gm.release()
+    return {"workload": "TensorNet-rMD17 energy+forces (C3: 8 x aspirin, O(3), static_shapes), hip-graph replay",
+            "value": round(n_mol * ws * a.steps / el, 2), "unit": "molecules/s",
+            "ms_per_step": round(1000 * el / a.steps, 4), "atoms_per_gpu": int(z.shape[0])}
+
+
+def secondary_train(a, ws, rank, dev):
+    """ET-QM9 training step (E+F MSE with forces via create_graph, backward incl. the double
+    backward, one fused RCCL all-reduce of the gradients when ws > 1, AdamW)."""
+    from torchmdnet.models.model import create_model
+    from torchmdnet.training import LNNPStep
+    torch.manual_seed(0)
+    model = create_model(et_args(a.channels)).to(dev)
+    z, pos, batch = qm9_like(a.batch, gen_seed=1 + rank)
+    gy = torch.Generator().manual_seed(100 + rank)
+    y_lab = torch.randn(a.batch, 1, generator=gy).to(dev)
+    f_lab = torch.randn(z.shape[0], 3, generator=gy).to(dev)
+    z, pos, batch = z.to(dev), pos.float().to(dev), batch.to(dev)
+    trainer = LNNPStep(model, lr=4e-4)
+    steps = max(5, a.steps // 5)
+    el = timed_loop(lambda: trainer.step(z, pos, batch, y_lab, f_lab), max(2, a.warmup // 2), steps, ws, dev)
+    return {"workload": "ET-QM9 training step (E+F MSE, double backward, "
+                        + ("RCCL all-reduce, " if ws > 1 else "") + "AdamW), eager",
+            "value": round(a.batch * ws * steps / el, 2), "unit": "molecules/s",
+            "ms_per_step": round(1000 * el / steps, 4), "steps": steps, "parallelism": f"dp{ws}"}
+
+
 def cpu_baseline(model, args, z, pos, batch, seconds):
     from oracle import model_oracle as O
     try:
@@ -356,6 +425,10 @@ def main():
                               "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
                               "bytes_per_launch": nbytes, "ms_per_launch": round(ms, 5),
                               "launches": len(probe)}
+    if a.mode == "infer" and not a.no_secondary:
+        sec = {"tensornet_c3": secondary_tensornet(a, ws, rank, dev), "et_train_step": secondary_train(a, ws, rank, dev)}
+        if rank == 0:
+            out["secondary"] = sec
     if rank == 0 and not a.no_roofline:
         out["roofline"] = roofline_probe(a, dev)
     if rank == 0 and ws == 1 and not a.no_cpu_baseline:

@@ -129,6 +129,26 @@ class TensorNet(nn.Module):
         return self.act(self.linear(x))
 
 
+def _mm33(a, b):
+    """Per-channel 3x3 matrix product of (..., 3, 3) tensors (reference: torch.matmul /
+    torch.matrix_power, tensornet.py:382-389).  torch.matmul maps this onto a batched GEMM of N*H
+    3x3x3 problems (~160-200 us each at C3); a broadcast multiply-and-reduce is two elementwise
+    passes (and autograd-friendly to any order)."""
+    return (a.unsqueeze(-1) * b.unsqueeze(-3)).sum(-2)
+
+
+def _mix(linear, X):
+    """``linear`` over the channel axis of (N, H, 3, 3) tensors -- the reference's
+    ``linear(X.permute(0, 2, 3, 1)).permute(0, 3, 1, 2)`` (tensornet.py:318-320, 354-356, 372-374).
+    Applied to that permuted view, hipBLASLt runs a strided-batched GEMM of N tiny 9 x H x H problems
+    (~190 us each at C3); here the tensor is copied channel-last once and mixed by ONE (9N x H) GEMM
+    (~10 us with both copies)."""
+    N, H = X.shape[0], X.shape[1]
+    Xt = X.reshape(N, H, 9).transpose(1, 2).reshape(N * 9, H)
+    Y = torch.mm(Xt, linear.weight.t())
+    return Y.view(N, 9, H).transpose(1, 2).reshape(N, H, 3, 3)
+
+
 def _check_symmetric_graph(edge_index, n):
     graph, perm = as_graph(edge_index, n)
     return graph, perm
@@ -183,9 +203,9 @@ class TensorEmbedding(nn.Module):
         Q = torch.nn.functional.linear(Z, self.emb2.weight[:, H:])
         I, A, S = kernels.tn_embed(P, Q, W, C, edge_vec_norm, graph)
         norm = self.init_norm(tensor_norm(I + A + S))
-        I = self.linears_tensor[0](I.permute(0, 2, 3, 1)).permute(0, 3, 1, 2)
-        A = self.linears_tensor[1](A.permute(0, 2, 3, 1)).permute(0, 3, 1, 2)
-        S = self.linears_tensor[2](S.permute(0, 2, 3, 1)).permute(0, 3, 1, 2)
+        I = _mix(self.linears_tensor[0], I)
+        A = _mix(self.linears_tensor[1], A)
+        S = _mix(self.linears_tensor[2], S)
         for linear_scalar in self.linears_scalar:
             norm = self.act(linear_scalar(norm))
         norm = norm.reshape(norm.shape[0], self.hidden_channels, 3)
@@ -227,22 +247,22 @@ class Interaction(nn.Module):
         edge_attr = edge_attr * C.view(-1, 1)
         X = X / (tensor_norm(X) + 1)[..., None, None]
         I, A, S = decompose_tensor(X)
-        I = self.linears_tensor[0](I.permute(0, 2, 3, 1)).permute(0, 3, 1, 2)
-        A = self.linears_tensor[1](A.permute(0, 2, 3, 1)).permute(0, 3, 1, 2)
-        S = self.linears_tensor[2](S.permute(0, 2, 3, 1)).permute(0, 3, 1, 2)
+        I = _mix(self.linears_tensor[0], I)
+        A = _mix(self.linears_tensor[1], A)
+        S = _mix(self.linears_tensor[2], S)
         Y = I + A + S
         msg = kernels.tn_message(edge_attr, I, A, S, graph)
         if self.equivariance_invariance_group == "O(3)":
-            A = torch.matmul(msg, Y)
-            B = torch.matmul(Y, msg)
+            A = _mm33(msg, Y)
+            B = _mm33(Y, msg)
             I, A, S = decompose_tensor(A + B)
         if self.equivariance_invariance_group == "SO(3)":
-            B = torch.matmul(Y, msg)
+            B = _mm33(Y, msg)
             I, A, S = decompose_tensor(2 * B)
         normp1 = (tensor_norm(I + A + S) + 1)[..., None, None]
         I, A, S = I / normp1, A / normp1, S / normp1
-        I = self.linears_tensor[3](I.permute(0, 2, 3, 1)).permute(0, 3, 1, 2)
-        A = self.linears_tensor[4](A.permute(0, 2, 3, 1)).permute(0, 3, 1, 2)
-        S = self.linears_tensor[5](S.permute(0, 2, 3, 1)).permute(0, 3, 1, 2)
+        I = _mix(self.linears_tensor[3], I)
+        A = _mix(self.linears_tensor[4], A)
+        S = _mix(self.linears_tensor[5], S)
         dX = I + A + S
-        return X + dX + torch.matrix_power(dX, 2)
+        return X + dX + _mm33(dX, dX)
