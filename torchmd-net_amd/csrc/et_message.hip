@@ -129,8 +129,7 @@ template <typename T> __device__ __forceinline__ const T* opt(const T* p, size_t
 // XCD-contiguous remap (bijective, cdna_hip_programming.md §5 "XCD swizzle"): blocks are dealt
 // round-robin over the 8 XCDs; remapping gives each XCD one contiguous range of logical blocks, so
 // the source rows its waves gather (neighbours of nearby nodes) are shared in that XCD's L2.
-__device__ __forceinline__ int xcd_block(int xcd) {
-  const int nwg = gridDim.x, b = blockIdx.x;
+__device__ __forceinline__ int xcd_block(int b, int nwg, int xcd) {
   if (!xcd || nwg < 16) return b;
   const int q = nwg / 8, r = nwg % 8, x = b % 8;
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
@@ -147,12 +146,12 @@ struct Geo {
 // groups of one node range run on DIFFERENT XCDs, so each XCD's L2 holds only its channel slice of
 // the gathered source rows (the per-XCD working set shrinks CS-fold).
 template <int S, int CS, bool ORD>
-__device__ __forceinline__ Geo geo(int n, int L, const int32_t* order, int xcd) {
+__device__ __forceinline__ Geo geo(int n, int L, const int32_t* order, int xcd, int blk, int nwg) {
   Geo g;
   const int wid = threadIdx.x >> 6;
   const int npb = 4 / S;
   const int nbn = (n + npb - 1) / npb;
-  const int lb = xcd_block(xcd);
+  const int lb = xcd_block(blk, nwg, xcd);
   g.cg = CS > 1 ? __builtin_amdgcn_readfirstlane(lb / nbn) : 0;
   const int w = __builtin_amdgcn_readfirstlane((CS > 1 ? lb % nbn : lb) * npb + wid / S);
   g.sub = __builtin_amdgcn_readfirstlane(wid % S);
@@ -243,7 +242,7 @@ __device__ __forceinline__ void edge_chunks_pf(const Args<T>& A, int b, int e, i
 template <typename T, int V, int S, int CS, bool ORD>
 __global__ __launch_bounds__(256) void k_fwd(Args<T> A) {
   __shared__ T lds[S > 1 ? 4 * 64 * 4 * V : 1];
-  const Geo G = geo<S, CS, ORD>(A.n, A.L, A.order, A.xcd);
+  const Geo G = geo<S, CS, ORD>(A.n, A.L, A.order, A.xcd, blockIdx.x, gridDim.x);
   const int t = G.node;
   const bool on = true;
   const int EPW = TMD_WAVE / A.L;  // edges per wave instruction
@@ -323,9 +322,9 @@ __global__ __launch_bounds__(256) void k_fwd(Args<T> A) {
 
 // ------------------------------------------------------------------ backward, destination pass
 template <typename T, int V, int S, int CS>
-__global__ __launch_bounds__(256) void k_bwd_dst(Args<T> A) {
+__device__ __forceinline__ void bwd_dst_body(const Args<T>& A, int blk, int nwg) {
   __shared__ T lds[S > 1 ? 4 * 64 * V : 1];
-  const Geo G = geo<S, CS, false>(A.n, A.L, nullptr, A.xcd);
+  const Geo G = geo<S, CS, false>(A.n, A.L, nullptr, A.xcd, blk, nwg);
   const int t = G.node;
   const bool on = true;
   const int EPW = TMD_WAVE / A.L;  // edges per wave instruction
@@ -443,9 +442,9 @@ __global__ __launch_bounds__(256) void k_bwd_dst(Args<T> A) {
 // A wave group owns node j as SOURCE.  Row j lists edges m->j; each is read as its reverse j->m
 // (same dk/dv/cutoff, unit vector negated), m being the destination whose q/gx/gvec are gathered.
 template <typename T, int V, int S, int CS>
-__global__ __launch_bounds__(256) void k_bwd_src(Args<T> A) {
+__device__ __forceinline__ void bwd_src_body(const Args<T>& A, int blk, int nwg) {
   __shared__ T lds[S > 1 ? 4 * 64 * 7 * V : 1];
-  const Geo G = geo<S, CS, false>(A.n, A.L, nullptr, A.xcd);
+  const Geo G = geo<S, CS, false>(A.n, A.L, nullptr, A.xcd, blk, nwg);
   const int j = G.node;
   const bool on = true;
   const int EPW = TMD_WAVE / A.L;  // edges per wave instruction
@@ -564,6 +563,24 @@ __global__ __launch_bounds__(256) void k_bwd_src(Args<T> A) {
       stv<T, V>(gwj + 2 * A.H, gw2);
     }
   }
+}
+
+template <typename T, int V, int S, int CS>
+__global__ __launch_bounds__(256) void k_bwd_dst(Args<T> A) {
+  bwd_dst_body<T, V, S, CS>(A, blockIdx.x, gridDim.x);
+}
+template <typename T, int V, int S, int CS>
+__global__ __launch_bounds__(256) void k_bwd_src(Args<T> A) {
+  bwd_src_body<T, V, S, CS>(A, blockIdx.x, gridDim.x);
+}
+// Both passes in ONE grid (they only read the same inputs): blocks [0, split) run the destination
+// pass, [split, 2 split) the source pass.  Used for small systems, where one pass alone leaves most
+// of the chip idle and the launch gap between the two passes is a visible share of the layer.
+template <typename T, int V, int S, int CS>
+__global__ __launch_bounds__(256) void k_bwd_both(Args<T> A) {
+  const int split = (int)gridDim.x / 2;
+  if ((int)blockIdx.x < split) bwd_dst_body<T, V, S, CS>(A, blockIdx.x, split);
+  else bwd_src_body<T, V, S, CS>(A, blockIdx.x - split, split);
 }
 
 // ------------------------------------------------------------------ neighbour embedding
@@ -710,9 +727,13 @@ static int et_launch_vs(Args<T> A, hipStream_t st) {
   const dim3 g(nbn * cs), b(256);
   if (KIND == 0) hipLaunchKernelGGL((k_fwd<T, V, S, 1, ORD>), g, b, 0, st, A);
   else if (KIND == 1) hipLaunchKernelGGL((k_bwd_dst<T, V, S, 1>), g, b, 0, st, A);
-  else hipLaunchKernelGGL((k_bwd_src<T, V, S, 1>), g, b, 0, st, A);
+  else if (KIND == 2) hipLaunchKernelGGL((k_bwd_src<T, V, S, 1>), g, b, 0, st, A);
+  else hipLaunchKernelGGL((k_bwd_both<T, V, S, 1>), dim3(2 * nbn), b, 0, st, A);
   return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
 }
+
+// below this many nodes the two backward passes share one grid (k_bwd_both)
+static constexpr int kBwdFuseNodes = 16384;
 
 template <typename T, int V, int KIND, bool ORD>
 static int et_launch_v(const Args<T>& A, hipStream_t st) {
@@ -798,6 +819,7 @@ static int bwd(int n, int H, int heads, const int32_t* row_ptr, const int32_t* s
   A.gq = (T*)gq; A.gk = (T*)gk; A.gv = (T*)gv; A.gveci = (T*)gveci;
   A.gpk = (T*)gpk; A.gpv = (T*)gpv; A.gC = (T*)gC; A.gu = (T*)gu;
   A.acc = acc;
+  if (n < kBwdFuseNodes) return et_launch<T, 3, false>(V, A, st);
   rc = et_launch<T, 1, false>(V, A, st);
   if (rc) return rc;
   return et_launch<T, 2, false>(V, A, st);
