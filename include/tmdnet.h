@@ -107,7 +107,8 @@ int tmdnet_et_message_fwd(int dtype, int n_nodes, int hidden, int heads, const i
  * vec_in may be NULL (vec == 0, the first layer): its terms vanish and gvec_in is not written
  * (gvec_in may also be NULL).  accumulate (TMDNET_ACC_* bits): VEC_RESIDUAL -> gvec_in =
  * grad_vec + message part (the layer's identity residual); EDGE -> gcut/gunit are accumulated
- * (+=) instead of overwritten (one buffer shared by all layers).  Other buffers: overwritten. */
+ * (+=) instead of overwritten (one buffer shared by all layers).  Other buffers: overwritten; rows
+ * [row_ptr[n_nodes], max_pairs) of gpk / gpv (static-capacity padding) are set to zero. */
 int tmdnet_et_message_bwd(int dtype, int n_nodes, int hidden, int heads, const int32_t* row_ptr,
                           const int32_t* src, int max_pairs, const void* q, int ld_q, const void* k,
                           int ld_k, const void* v, int ld_v, const void* vec_in, const void* pk,
@@ -115,6 +116,22 @@ int tmdnet_et_message_bwd(int dtype, int n_nodes, int hidden, int heads, const i
                           const void* grad_x, const void* grad_vec, void* gq, void* gk, void* gv,
                           void* gvec_in, void* gpk, void* gpv, void* gcut, void* gunit,
                           int accumulate, const int32_t* order, void* stream);
+
+/* Second-order backward: the VJP of tmdnet_et_message_bwd (forces differentiated again, reference
+ * model.py:286-298 with create_graph=True).  gg_* are the cotangents of that call's outputs (gq, gk,
+ * gv, gvec_in, gpk, gpv, gcut, gunit; all required, dense, zeros where unused; gg_q/gg_k [N][H],
+ * gg_v [N][3H], gg_vec [N][3][H], gg_pk/gg_pv with leading dimensions).  Outputs: d_grad_x, d_grad_vec,
+ * d_q, d_k [N][H], d_v [N][3H], d_vec [N][3][H] (d_k, d_v, d_vec accumulated with atomics: zero them
+ * first; d_vec may be NULL when vec_in is NULL), d_pk [E][H], d_pv [E][3H], d_cut [E], d_unit [E][3]. */
+int tmdnet_et_message_bwd2(int dtype, int n_nodes, int hidden, int heads, const int32_t* row_ptr,
+                           const int32_t* src, int max_pairs, const void* q, int ld_q, const void* k,
+                           int ld_k, const void* v, int ld_v, const void* vec_in, const void* pk,
+                           int ld_pk, const void* pv, int ld_pv, const void* cutoff, const void* unit,
+                           const void* grad_x, const void* grad_vec, const void* gg_q, const void* gg_k,
+                           const void* gg_v, const void* gg_vec, const void* gg_pk, int ld_ggpk,
+                           const void* gg_pv, int ld_ggpv, const void* gg_cut, const void* gg_unit,
+                           void* d_grad_x, void* d_grad_vec, void* d_q, void* d_k, void* d_v,
+                           void* d_vec, void* d_pk, void* d_pv, void* d_cut, void* d_unit, void* stream);
 
 /* ET layer epilogue (reference torchmd_et.py:278-280, 309-311 + residuals 181-184), fused:
  *   vecp = vec_proj(vec) [N][3][3H] = [v1|v2|v3], o = o_proj(x_agg) [N][3H] = [o1|o2|o3]

@@ -86,10 +86,15 @@ def _fake_epi_bwd(gx, gvec, vecp, o, g_vecp, g_o):
     g_vecp[..., 2 * H:] = gvec * o1.unsqueeze(1)
 
 
+def _fake_bwd2(ctx, ggs):
+    return kernels._ETMessageBwd.composite_backward(ctx, *ggs)
+
+
 @pytest.fixture
 def emulated(monkeypatch):
     monkeypatch.setattr(kernels, "et_message_fwd_launch", _fake_fwd)
     monkeypatch.setattr(kernels, "et_message_bwd_launch", _fake_bwd)
+    monkeypatch.setattr(kernels, "et_message_bwd2", _fake_bwd2)
     monkeypatch.setattr(ES, "_epilogue_fwd", _fake_epi_fwd)
     monkeypatch.setattr(ES, "_epilogue_bwd", _fake_epi_bwd)
 
@@ -136,8 +141,11 @@ def _meta_for(layers, graph):
                     len(layers), None, None)
 
 
+@pytest.mark.parametrize("batched", [True, False])
 @pytest.mark.parametrize("infl", ["both", "keys", "values", "none"])
-def test_stack_forward_and_grads_match_composite(emulated, infl):
+def test_stack_forward_and_grads_match_composite(emulated, monkeypatch, infl, batched):
+    if not batched:  # per-layer dk/dv GEMMs (the large-system path)
+        monkeypatch.setattr(ES, "BATCH_DKV_BYTES", 0)
     H, R, heads = 16, 8, 4
     n, graph, r, vecs = _system()
     x, f, C, u = _inputs(n, graph, r, vecs, H, R)
@@ -170,6 +178,8 @@ def test_stack_stacked_parameters_alias_and_survive_updates(emulated):
     lw = layers[0]._stacked
     qkv = lw.bufs["qkv_w"]
     assert layers[0].k_proj.weight.data_ptr() == qkv.data_ptr() + H * H * qkv.element_size()
+    dkv = layers._tmd_stack.bufs["w"]  # all layers' [dk; dv] rows: layer 1's dk after layer 0's 4H rows
+    assert layers[1].dk_proj.weight.data_ptr() == dkv.data_ptr() + 4 * H * R * dkv.element_size()
     with torch.no_grad():  # optimiser-style in-place update shows through the stacked buffer
         layers[0].k_proj.weight.add_(1.0)
     assert torch.equal(qkv[H:2 * H], layers[0].k_proj.weight)
@@ -178,12 +188,16 @@ def test_stack_stacked_parameters_alias_and_survive_updates(emulated):
     assert lw.bufs["qkv_w"] is qkv  # in-place load keeps the aliasing
 
 
-def test_stack_force_pass_skips_weight_grads_but_training_gets_them(emulated):
+@pytest.mark.parametrize("batched", [True, False])
+def test_stack_force_pass_skips_weight_grads_but_training_gets_them(emulated, monkeypatch, batched):
     """autograd.grad wrt inputs: weight gradients not requested -> not computed; loss.backward
-    through a create_graph force pass -> weight gradients equal the composite reference."""
+    through a create_graph force pass -> weight gradients equal the composite reference (the second
+    order re-runs the layers with the message Functions)."""
     H, R, heads = 16, 8, 4
     n, graph, r, vecs = _system()
     x, f, C, u = _inputs(n, graph, r, vecs, H, R)
+    if not batched:
+        monkeypatch.setattr(ES, "BATCH_DKV_BYTES", 0)
     layers = _layers(2, H, R, heads, "both")
     params = [p for l in layers for p in ES.layer_params(l)]
     calls = []

@@ -502,3 +502,42 @@ def test_graphed_tensornet_matches_eager(static_shapes):
         assert _rel(y.detach().cpu(), ye.detach().cpu()) < 1e-5
         assert _rel(f.detach().cpu(), fe.detach().cpu()) < 1e-5
     gm.release()
+
+
+@pytest.mark.parametrize("infl", ["both", "none"])
+def test_et_message_second_order_kernel_matches_composite(infl):
+    """tmdnet_et_message_bwd2 (the VJP of the HIP first backward) == double backward through the
+    PyTorch restatement, fp64, all ten inputs (gx, gvec, q, k, v, vec, pk, pv, C, u)."""
+    from torchmdnet import kernels
+    torch.manual_seed(0)
+    z, pos, batch = O.qm9_like(2)
+    pos = pos.to(DEV)
+    g = kernels.build_graph(pos, batch.to(DEV), 0.0, 5.0, 64 * pos.shape[0], loop=True)
+    N, H, heads, E = pos.shape[0], 32, 4, g.n_edges
+    o = dict(dtype=torch.float64, device=DEV)
+    T = g.transpose.long()
+    sym = lambda t: ((t + t[T]) / 2).detach().requires_grad_(True)  # noqa: E731
+    q, k = torch.randn(N, H, **o).requires_grad_(True), torch.randn(N, H, **o).requires_grad_(True)
+    v = torch.randn(N, 3 * H, **o).requires_grad_(True)
+    vec = torch.randn(N, 3, H, **o).requires_grad_(True)
+    pk = sym(torch.randn(E, H, **o)) if infl == "both" else None
+    pv = sym(torch.randn(E, 3 * H, **o)) if infl == "both" else None
+    C = sym(torch.rand(E, **o))
+    r = g.distances.detach()
+    u = (g.deltas.detach() / torch.where(r > 0, r, torch.ones_like(r)).unsqueeze(1)).requires_grad_(True)
+    gx, gvec = torch.randn(N, H, **o).requires_grad_(True), torch.randn(N, 3, H, **o).requires_grad_(True)
+    ins = [t for t in (gx, gvec, q, k, v, vec, pk, pv, C, u) if t is not None]
+    outs = kernels._ETMessageBwd.apply(gx, gvec, q, k, v, vec, pk, pv, C, u, g, heads)
+    outs = [t for t in outs if t.numel()]
+    gg = [torch.randn_like(t) for t in outs]
+    a = torch.autograd.grad(outs, ins, gg, allow_unused=True)
+    src, dst = g.src.long(), g.dst.long()
+    xo, vo = kernels.et_message_composite(q, k, v, vec, pk, pv, C, u, src, dst, N, heads)
+    prim = [t for t in (q, k, v, vec, pk, pv, C, u) if t is not None]
+    first = torch.autograd.grad((xo, vo), prim, (gx, gvec), create_graph=True)
+    b = torch.autograd.grad(first, ins, gg, allow_unused=True)
+    names = [n for n, t in zip("gx gvec q k v vec pk pv C u".split(), (gx, gvec, q, k, v, vec, pk, pv, C, u))
+             if t is not None]
+    for n, ga, gb in zip(names, a, b):
+        gb = torch.zeros_like(ga) if gb is None else gb
+        assert torch.allclose(ga, gb, atol=1e-10, rtol=1e-8), n

@@ -54,6 +54,8 @@ template <typename T> struct Silu {
     s = x * sig;
   }
   __device__ __forceinline__ T d(T x) const { return sig * (T(1) + x * (T(1) - sig)); }
+  // second derivative: s(1-s)(2 + x(1-2s))
+  __device__ __forceinline__ T dd(T x) const { return sig * (T(1) - sig) * (T(2) + x * (T(1) - T(2) * sig)); }
 };
 
 }  // namespace tmd

@@ -321,6 +321,26 @@ __global__ __launch_bounds__(256) void k_fwd(Args<T> A) {
 }
 
 // ------------------------------------------------------------------ backward, destination pass
+// Static-capacity edge lists: rows [row_ptr[n], cap) of gpk / gpv belong to no CSR row.  They are
+// zeroed here (spread over the grid) so the weight-gradient GEMMs over all `cap` rows see zeros
+// without a memset of the whole buffer.
+template <typename T>
+__device__ __forceinline__ void zero_pad_rows(const Args<T>& A, int blk, int nwg) {
+  const int e0 = min(A.row_ptr[A.n], A.cap);
+  if (e0 >= A.cap) return;
+  const long long rows = A.cap - e0;
+  const long long tid = (long long)blk * blockDim.x + threadIdx.x, nth = (long long)nwg * blockDim.x;
+  if (A.gpk) {
+    for (long long i = tid; i < rows * A.H; i += nth)
+      A.gpk[(size_t)(e0 + i / A.H) * A.ldpk + i % A.H] = T(0);
+  }
+  if (A.gpv) {
+    const int w = 3 * A.H;
+    for (long long i = tid; i < rows * w; i += nth)
+      A.gpv[(size_t)(e0 + i / w) * A.ldpv + i % w] = T(0);
+  }
+}
+
 template <typename T, int V, int S, int CS>
 __device__ __forceinline__ void bwd_dst_body(const Args<T>& A, int blk, int nwg) {
   __shared__ T lds[S > 1 ? 4 * 64 * V : 1];
@@ -436,6 +456,7 @@ __device__ __forceinline__ void bwd_dst_body(const Args<T>& A, int blk, int nwg)
   xor_slots(gq, A.L);
   reduce_waves<T, S, V>(gq, G.sub, lds);
   if (t >= 0 && G.sub == 0 && on && G.es == 0) stv<T, V>(A.gq + (size_t)t * A.ldq + c0, gq);
+  zero_pad_rows(A, blk, nwg);
 }
 
 // ------------------------------------------------------------------ backward, source pass
@@ -581,6 +602,191 @@ __global__ __launch_bounds__(256) void k_bwd_both(Args<T> A) {
   const int split = (int)gridDim.x / 2;
   if ((int)blockIdx.x < split) bwd_dst_body<T, V, S, CS>(A, blockIdx.x, split);
   else bwd_src_body<T, V, S, CS>(A, blockIdx.x - split, split);
+}
+
+// ------------------------------------------------------------------ second-order backward
+// VJP of tmdnet_et_message_bwd (needed when forces are differentiated again: force-matching
+// training, reference model.py:286-298 with create_graph=True).  With gg* the cotangents of the
+// first backward's outputs (gq, gk, gv, gvec_in, gpk, gpv, gcut, gunit), per edge e = (t <- s) and
+// head h (part = q.k.dk, ga = gx.vx.dvx, sil/sd/sdd = silu and its derivatives of part):
+//   S = sum_c ggq k dk + ggk q dk + ggpk q k dk'        X = sum_c ggvx gx dvx + ggpvx gx vx dvx'
+//   P = C ga sdd S + C sd X + ggC ga sd                   G = C sd S + ggC sil
+//   d/dq   += P k dk + gs (ggk dk + ggpk k dk')           (gs = ga C sd, a = sil C)
+//   d/dk_s += P q dk + gs (ggq dk + ggpk q dk')
+//   d/dpk   = P q k dk' + gs ((ggq k + ggk q) dk' + ggpk q k dk'')
+//   d/dgx  += G vx dvx + a (ggvx dvx + ggpvx vx dvx')
+//   d/dvx_s+= G gx dvx + a ggpvx gx dvx'
+//   d/dpvx  = G gx vx dvx' + a (ggvx gx dvx' + ggpvx gx vx dvx'')
+//   d/dC    = sum_h ga sd S + sil X
+// and for the vector channels (G1 = sum_a gvec_a w_a, G2 = sum_a gvec_a u_a, U = sum_a ggu_a gvec_a,
+// B1 = ggv1 dv1 + ggpv1 v1 dv1', B2 = ggv2 dv2 + ggpv2 v2 dv2'):
+//   d/dgvec_a += w_a B1 + u_a B2 + ggw_a v1 dv1 + ggu_a v2 dv2       d/dw_a,s += gvec_a B1
+//   d/dv1_s   += G1 ggpv1 dv1' + sum_a ggw_a gvec_a dv1              d/du_a    = sum_c gvec_a B2
+//   d/dpv1     = G1 (ggv1 dv1' + ggpv1 v1 dv1'') + sum_a ggw_a gvec_a v1 dv1'
+//   d/dv2_s   += G2 ggpv2 dv2' + U dv2
+//   d/dpv2     = G2 (ggv2 dv2' + ggpv2 v2 dv2'') + U v2 dv2'
+// One destination-row pass: destination-node terms accumulate in registers, per-edge terms are
+// stored, source-node terms (k, v, vec) are added with atomics into zero-initialised buffers (this
+// path runs only in training, where the reference's CUDA scatter is atomic as well).
+template <typename T> struct Args2 {
+  Args<T> a;                                       // primal inputs (q, k, v, vec, pk, pv, C, u) + gx, gvec
+  const T* ggq; const T* ggk; const T* ggv; const T* ggw;   // node cotangents ([N][H], [N][H], [N][3H], [N][3][H])
+  const T* ggpk; int ldggpk; const T* ggpv; int ldggpv;     // edge cotangents
+  const T* ggC; const T* ggu;
+  T* o_gx; T* o_gvec; T* o_q; T* o_k; T* o_v; T* o_vec;       // node outputs (o_k, o_v, o_vec: atomics)
+  T* o_pk; T* o_pv; T* o_C; T* o_u;                          // edge outputs ([E][H], [E][3H], [E], [E][3])
+};
+
+template <typename T, int V>
+__global__ __launch_bounds__(256) void k_bwd2(Args2<T> B) {
+  const Args<T>& A = B.a;
+  const Geo G = geo<1, 1, false>(A.n, A.L, nullptr, A.xcd, blockIdx.x, gridDim.x);
+  const int t = G.node;
+  if (t < 0) return;
+  const int EPW = TMD_WAVE / A.L;
+  const int c0 = G.el * V;
+  const int hh = c0 / A.d, cc = c0 % A.d;
+  const int vo = hh * 3 * A.d + cc;
+  const bool hk = A.pk != nullptr, hv = A.pv != nullptr, hw = A.vec != nullptr;
+  const bool head_leader = (G.el % A.lph) == 0;
+  T q[V], gx[V], g0[V], g1[V], g2[V], ggq[V];
+  ldv<T, V>(q, A.q + (size_t)t * A.ldq + c0);
+  ldv<T, V>(gx, A.gx + (size_t)t * A.H + c0);
+  ldv<T, V>(g0, A.gvec + (size_t)t * 3 * A.H + c0);
+  ldv<T, V>(g1, A.gvec + (size_t)t * 3 * A.H + A.H + c0);
+  ldv<T, V>(g2, A.gvec + (size_t)t * 3 * A.H + 2 * A.H + c0);
+  ldv<T, V>(ggq, B.ggq + (size_t)t * A.H + c0);
+  T oq[V], ogx[V], og0[V], og1[V], og2[V];
+  zero(oq); zero(ogx); zero(og0); zero(og1); zero(og2);
+  const int b = min(A.row_ptr[t], A.cap), e = min(A.row_ptr[t + 1], A.cap);
+  for (int k = b + G.es; k < e; k += EPW) {
+    const int s = A.src[k];
+    const T Ce = A.C[k];
+    const T u0 = A.u[3 * k], u1 = A.u[3 * k + 1], u2 = A.u[3 * k + 2];
+    const T ggC = B.ggC[k];
+    const T gu0 = B.ggu[3 * k], gu1 = B.ggu[3 * k + 1], gu2 = B.ggu[3 * k + 2];
+    T kk[V], ggk[V], vx[V], v1[V], v2[V], ggvx[V], ggv1[V], ggv2[V], w0[V], w1[V], w2[V];
+    T ggw0[V], ggw1[V], ggw2[V], rk[V], rx[V], r1[V], r2[V], ggpk[V], ggpx[V], ggp1[V], ggp2[V];
+    ldv<T, V>(kk, A.k + (size_t)s * A.ldk + c0);
+    ldv<T, V>(ggk, B.ggk + (size_t)s * A.H + c0);
+    const T* vs = A.v + (size_t)s * A.ldv + vo;
+    ldv<T, V>(vx, vs); ldv<T, V>(v1, vs + A.d); ldv<T, V>(v2, vs + 2 * A.d);
+    const T* gvs = B.ggv + (size_t)s * 3 * A.H + vo;
+    ldv<T, V>(ggvx, gvs); ldv<T, V>(ggv1, gvs + A.d); ldv<T, V>(ggv2, gvs + 2 * A.d);
+    if (hw) {
+      const T* ws = A.vec + (size_t)s * 3 * A.H + c0;
+      ldv<T, V>(w0, ws); ldv<T, V>(w1, ws + A.H); ldv<T, V>(w2, ws + 2 * A.H);
+    } else {
+      zero(w0); zero(w1); zero(w2);
+    }
+    const T* gws = B.ggw + (size_t)s * 3 * A.H + c0;
+    ldv<T, V>(ggw0, gws); ldv<T, V>(ggw1, gws + A.H); ldv<T, V>(ggw2, gws + 2 * A.H);
+    if (hk) {
+      ldv<T, V>(rk, A.pk + (size_t)k * A.ldpk + c0);
+      ldv<T, V>(ggpk, B.ggpk + (size_t)k * B.ldggpk + c0);
+    } else {
+      zero(rk); zero(ggpk);
+    }
+    if (hv) {
+      const T* ps = A.pv + (size_t)k * A.ldpv + vo;
+      ldv<T, V>(rx, ps); ldv<T, V>(r1, ps + A.d); ldv<T, V>(r2, ps + 2 * A.d);
+      const T* gps = B.ggpv + (size_t)k * B.ldggpv + vo;
+      ldv<T, V>(ggpx, gps); ldv<T, V>(ggp1, gps + A.d); ldv<T, V>(ggp2, gps + 2 * A.d);
+    } else {
+      zero(rx); zero(r1); zero(r2); zero(ggpx); zero(ggp1); zero(ggp2);
+    }
+    // activations with first and second derivatives (an absent projection is the constant 1)
+    T dk[V], dk1[V], dk2[V], dx[V], dx1[V], dx2[V], d1[V], d11[V], d12[V], d2[V], d21[V], d22[V];
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+      if (hk) { Silu<T> f(rk[i]); dk[i] = f.s; dk1[i] = f.d(rk[i]); dk2[i] = f.dd(rk[i]); }
+      else { dk[i] = T(1); dk1[i] = T(0); dk2[i] = T(0); }
+      if (hv) {
+        Silu<T> fx(rx[i]); dx[i] = fx.s; dx1[i] = fx.d(rx[i]); dx2[i] = fx.dd(rx[i]);
+        Silu<T> f1(r1[i]); d1[i] = f1.s; d11[i] = f1.d(r1[i]); d12[i] = f1.dd(r1[i]);
+        Silu<T> f2(r2[i]); d2[i] = f2.s; d21[i] = f2.d(r2[i]); d22[i] = f2.dd(r2[i]);
+      } else {
+        dx[i] = d1[i] = d2[i] = T(1); dx1[i] = d11[i] = d21[i] = T(0); dx2[i] = d12[i] = d22[i] = T(0);
+      }
+    }
+    T part = T(0), ga = T(0), S = T(0), X = T(0);
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+      part += q[i] * kk[i] * dk[i];
+      ga += gx[i] * vx[i] * dx[i];
+      S += ggq[i] * kk[i] * dk[i] + ggk[i] * q[i] * dk[i] + ggpk[i] * q[i] * kk[i] * dk1[i];
+      X += ggvx[i] * gx[i] * dx[i] + ggpx[i] * gx[i] * vx[i] * dx1[i];
+    }
+    part = group_sum(part, A.lph);
+    ga = group_sum(ga, A.lph);
+    S = group_sum(S, A.lph);
+    X = group_sum(X, A.lph);
+    const Silu<T> sa(part);
+    const T sil = sa.s, sd = sa.d(part), sdd = sa.dd(part);
+    const T gs = ga * Ce * sd, a = sil * Ce;
+    const T P = Ce * ga * sdd * S + Ce * sd * X + ggC * ga * sd;
+    const T Gm = Ce * sd * S + ggC * sil;
+    const T gC = group_sum(head_leader ? ga * sd * S + sil * X : T(0), A.L);
+    T ok_[V], opk[V], ovx[V], opx[V], ov1[V], op1[V], ov2[V], op2[V], ow0[V], ow1[V], ow2[V];
+    T gua0 = T(0), gua1 = T(0), gua2 = T(0);
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+      oq[i] += P * kk[i] * dk[i] + gs * (ggk[i] * dk[i] + ggpk[i] * kk[i] * dk1[i]);
+      ok_[i] = P * q[i] * dk[i] + gs * (ggq[i] * dk[i] + ggpk[i] * q[i] * dk1[i]);
+      opk[i] = P * q[i] * kk[i] * dk1[i] +
+               gs * ((ggq[i] * kk[i] + ggk[i] * q[i]) * dk1[i] + ggpk[i] * q[i] * kk[i] * dk2[i]);
+      ogx[i] += Gm * vx[i] * dx[i] + a * (ggvx[i] * dx[i] + ggpx[i] * vx[i] * dx1[i]);
+      ovx[i] = Gm * gx[i] * dx[i] + a * ggpx[i] * gx[i] * dx1[i];
+      opx[i] = Gm * gx[i] * vx[i] * dx1[i] + a * (ggvx[i] * gx[i] * dx1[i] + ggpx[i] * gx[i] * vx[i] * dx2[i]);
+      const T G1 = g0[i] * w0[i] + g1[i] * w1[i] + g2[i] * w2[i];
+      const T G2 = g0[i] * u0 + g1[i] * u1 + g2[i] * u2;
+      const T U = gu0 * g0[i] + gu1 * g1[i] + gu2 * g2[i];
+      const T Wg = ggw0[i] * g0[i] + ggw1[i] * g1[i] + ggw2[i] * g2[i];
+      const T B1 = ggv1[i] * d1[i] + ggp1[i] * v1[i] * d11[i];
+      const T B2 = ggv2[i] * d2[i] + ggp2[i] * v2[i] * d21[i];
+      const T v1e = v1[i] * d1[i], v2e = v2[i] * d2[i];
+      og0[i] += w0[i] * B1 + u0 * B2 + ggw0[i] * v1e + gu0 * v2e;
+      og1[i] += w1[i] * B1 + u1 * B2 + ggw1[i] * v1e + gu1 * v2e;
+      og2[i] += w2[i] * B1 + u2 * B2 + ggw2[i] * v1e + gu2 * v2e;
+      ow0[i] = g0[i] * B1; ow1[i] = g1[i] * B1; ow2[i] = g2[i] * B1;
+      gua0 += g0[i] * B2; gua1 += g1[i] * B2; gua2 += g2[i] * B2;
+      ov1[i] = G1 * ggp1[i] * d11[i] + Wg * d1[i];
+      op1[i] = G1 * (ggv1[i] * d11[i] + ggp1[i] * v1[i] * d12[i]) + Wg * v1[i] * d11[i];
+      ov2[i] = G2 * ggp2[i] * d21[i] + U * d2[i];
+      op2[i] = G2 * (ggv2[i] * d21[i] + ggp2[i] * v2[i] * d22[i]) + U * v2[i] * d21[i];
+    }
+    gua0 = group_sum(gua0, A.L);
+    gua1 = group_sum(gua1, A.L);
+    gua2 = group_sum(gua2, A.L);
+    // per-edge outputs
+    if (hk) stv<T, V>(B.o_pk + (size_t)k * A.H + c0, opk);
+    if (hv) {
+      T* op = B.o_pv + (size_t)k * 3 * A.H + vo;
+      stv<T, V>(op, opx); stv<T, V>(op + A.d, op1); stv<T, V>(op + 2 * A.d, op2);
+    }
+    if (G.el == 0) {
+      B.o_C[k] = gC;
+      B.o_u[3 * k] = gua0; B.o_u[3 * k + 1] = gua1; B.o_u[3 * k + 2] = gua2;
+    }
+    // source-node outputs (atomics)
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+      atomicAdd(B.o_k + (size_t)s * A.H + c0 + i, ok_[i]);
+      T* ov = B.o_v + (size_t)s * 3 * A.H + vo + i;
+      atomicAdd(ov, ovx[i]); atomicAdd(ov + A.d, ov1[i]); atomicAdd(ov + 2 * A.d, ov2[i]);
+      if (B.o_vec) {
+        T* ow = B.o_vec + (size_t)s * 3 * A.H + c0 + i;
+        atomicAdd(ow, ow0[i]); atomicAdd(ow + A.H, ow1[i]); atomicAdd(ow + 2 * A.H, ow2[i]);
+      }
+    }
+  }
+  xor_slots(oq, A.L); xor_slots(ogx, A.L); xor_slots(og0, A.L); xor_slots(og1, A.L); xor_slots(og2, A.L);
+  if (G.es == 0) {
+    stv<T, V>(B.o_q + (size_t)t * A.H + c0, oq);
+    stv<T, V>(B.o_gx + (size_t)t * A.H + c0, ogx);
+    T* og = B.o_gvec + (size_t)t * 3 * A.H + c0;
+    stv<T, V>(og, og0); stv<T, V>(og + A.H, og1); stv<T, V>(og + 2 * A.H, og2);
+  }
 }
 
 // ------------------------------------------------------------------ neighbour embedding
@@ -826,6 +1032,43 @@ static int bwd(int n, int H, int heads, const int32_t* row_ptr, const int32_t* s
 }
 
 template <typename T>
+static int bwd2(int n, int H, int heads, const int32_t* row_ptr, const int32_t* src, int cap,
+                const void* q, int ldq, const void* k, int ldk, const void* v, int ldv_,
+                const void* vec, const void* pk, int ldpk, const void* pv, int ldpv, const void* C,
+                const void* u, const void* gx, const void* gvec, const void* ggq, const void* ggk,
+                const void* ggv, const void* ggw, const void* ggpk, int ldggpk, const void* ggpv,
+                int ldggpv, const void* ggC, const void* ggu, void* o_gx, void* o_gvec, void* o_q,
+                void* o_k, void* o_v, void* o_vec, void* o_pk, void* o_pv, void* o_C, void* o_u,
+                hipStream_t st) {
+  Args2<T> B{};
+  int V;
+  int rc = setup<T>(B.a, n, H, heads, row_ptr, src, cap, q, ldq, k, ldk, v, ldv_, vec, pk, ldpk, pv,
+                    ldpv, C, u, nullptr, V);
+  if (rc) return rc;
+  // narrower lanes than the first-order kernels (V = H/64: one edge per wave instruction): this
+  // kernel keeps ~22 row segments of an edge live
+  if (H % 64 == 0) V = H / 64;
+  const int d = H / heads;
+  if ((V != 1 && V != 2 && V != 4) || d % V || ((d / V) & (d / V - 1))) return kUnsupported;
+  B.a.L = H / V;
+  B.a.lph = d / V;
+  if (B.a.L > 64 || (B.a.L & (B.a.L - 1))) return kUnsupported;
+  if (!aligned<T>(ggpk, ldggpk, V) || !aligned<T>(ggpv, ldggpv, V)) return kBadArgument;
+  B.a.gx = (const T*)gx; B.a.gvec = (const T*)gvec;
+  B.ggq = (const T*)ggq; B.ggk = (const T*)ggk; B.ggv = (const T*)ggv; B.ggw = (const T*)ggw;
+  B.ggpk = (const T*)ggpk; B.ldggpk = ldggpk; B.ggpv = (const T*)ggpv; B.ldggpv = ldggpv;
+  B.ggC = (const T*)ggC; B.ggu = (const T*)ggu;
+  B.o_gx = (T*)o_gx; B.o_gvec = (T*)o_gvec; B.o_q = (T*)o_q; B.o_k = (T*)o_k; B.o_v = (T*)o_v;
+  B.o_vec = (T*)o_vec; B.o_pk = (T*)o_pk; B.o_pv = (T*)o_pv; B.o_C = (T*)o_C; B.o_u = (T*)o_u;
+  if (n <= 0) return kOk;
+  const dim3 g((n + 3) / 4), b(256);
+  if (V == 1) hipLaunchKernelGGL((k_bwd2<T, 1>), g, b, 0, st, B);
+  else if (V == 2) hipLaunchKernelGGL((k_bwd2<T, 2>), g, b, 0, st, B);
+  else hipLaunchKernelGGL((k_bwd2<T, 4>), g, b, 0, st, B);
+  return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
+}
+
+template <typename T>
 static int nb_setup(NbArgs<T>& A, int n, int H, const int32_t* row_ptr, const int32_t* src, int cap,
                     const void* x, int ldx, const void* w, int ldw, const void* C, int& V) {
   V = pick_vec(H);
@@ -876,6 +1119,27 @@ extern "C" int tmdnet_et_message_bwd(int dtype, int n_nodes, int hidden, int hea
     return et::bwd<double>(n_nodes, hidden, heads, row_ptr, src, max_pairs, q, ld_q, k, ld_k, v, ld_v,
                            vec_in, pk, ld_pk, pv, ld_pv, cutoff, unit, grad_x, grad_vec, gq, gk, gv,
                            gvec_in, gpk, gpv, gcut, gunit, accumulate, order, st);
+  return kUnsupported;
+}
+
+extern "C" int tmdnet_et_message_bwd2(
+    int dtype, int n_nodes, int hidden, int heads, const int32_t* row_ptr, const int32_t* src,
+    int max_pairs, const void* q, int ld_q, const void* k, int ld_k, const void* v, int ld_v,
+    const void* vec_in, const void* pk, int ld_pk, const void* pv, int ld_pv, const void* cutoff,
+    const void* unit, const void* grad_x, const void* grad_vec, const void* gg_q, const void* gg_k,
+    const void* gg_v, const void* gg_vec, const void* gg_pk, int ld_ggpk, const void* gg_pv,
+    int ld_ggpv, const void* gg_cut, const void* gg_unit, void* d_grad_x, void* d_grad_vec,
+    void* d_q, void* d_k, void* d_v, void* d_vec, void* d_pk, void* d_pv, void* d_cut,
+    void* d_unit, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+#define TMD_BWD2(T)                                                                              \
+  return et::bwd2<T>(n_nodes, hidden, heads, row_ptr, src, max_pairs, q, ld_q, k, ld_k, v, ld_v, \
+                     vec_in, pk, ld_pk, pv, ld_pv, cutoff, unit, grad_x, grad_vec, gg_q, gg_k,   \
+                     gg_v, gg_vec, gg_pk, ld_ggpk, gg_pv, ld_ggpv, gg_cut, gg_unit, d_grad_x,    \
+                     d_grad_vec, d_q, d_k, d_v, d_vec, d_pk, d_pv, d_cut, d_unit, st)
+  if (dtype == TMDNET_F32) TMD_BWD2(float);
+  if (dtype == TMDNET_F64) TMD_BWD2(double);
+#undef TMD_BWD2
   return kUnsupported;
 }
 

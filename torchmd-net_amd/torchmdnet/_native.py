@@ -35,6 +35,8 @@ SIGNATURES = {
     "tmdnet_et_message_fwd": (I, [I, I, I, I, P, P, I, P, I, P, I, P, I, P, P, I, P, I, P, P, P, P, P, P]),
     "tmdnet_et_message_bwd": (I, [I, I, I, I, P, P, I, P, I, P, I, P, I, P, P, I, P, I, P, P, P, P,
                                   P, P, P, P, P, P, P, P, I, P, P]),
+    "tmdnet_et_message_bwd2": (I, [I, I, I, I, P, P, I, P, I, P, I, P, I, P, P, I, P, I, P, P, P, P,
+                                   P, P, P, P, P, I, P, I, P, P, P, P, P, P, P, P, P, P, P, P, P]),
     "tmdnet_et_epilogue_fwd": (I, [I, I, I, P, P, P, P, P, P, P, P]),
     "tmdnet_et_epilogue_bwd": (I, [I, I, I, P, P, P, P, P, P, P]),
     "tmdnet_nbr_embed_fwd": (I, [I, I, I, P, P, I, P, I, P, I, P, P, P]),

@@ -96,10 +96,35 @@ class LayerWeights:
         L = self.layer
         qkv_w = self._get("qkv_w", [L.q_proj.weight, L.k_proj.weight, L.v_proj.weight])
         qkv_b = self._get("qkv_b", [L.q_proj.bias, L.k_proj.bias, L.v_proj.bias])
-        dk = [m for m in (L.dk_proj, L.dv_proj) if m is not None]
-        dkv_w = self._get("dkv_w", [m.weight for m in dk]) if dk else None
-        dkv_b = self._get("dkv_b", [m.bias for m in dk]) if dk else None
-        return qkv_w, qkv_b, dkv_w, dkv_b
+        return qkv_w, qkv_b
+
+
+class StackWeights:
+    """The dk/dv projections of ALL layers as row blocks of one [L*D, R] weight (D = H | 3H | 4H)
+    and one [L*D] bias: layer l's [dk; dv] is rows [l*D, (l+1)*D).  They only read the edge
+    features, so small systems compute every layer's projection with ONE GEMM up front (and the
+    edge-feature gradient with one GEMM at the end of the backward)."""
+
+    def __init__(self, layers):
+        self.layers = layers
+        self.bufs = {}
+
+    def _get(self, name, params):
+        buf = self.bufs.get(name)
+        if not _is_stacked(buf, params):
+            buf = _stack_views(params)
+            self.bufs[name] = buf
+        return buf
+
+    def dkv(self):
+        mods = [m for layer in self.layers for m in (layer.dk_proj, layer.dv_proj) if m is not None]
+        if not mods:
+            return None, None
+        return self._get("w", [m.weight for m in mods]), self._get("b", [m.bias for m in mods])
+
+
+# Batch every layer's dk/dv projection into one GEMM while its output (E x L*D fp32) stays below this.
+BATCH_DKV_BYTES = 2 << 30
 
 
 def layer_params(layer):
@@ -117,19 +142,29 @@ def layer_params(layer):
 class _Meta:
     """Non-tensor context of one stack call."""
 
-    def __init__(self, graph, heads, H, hk, hv, n_layers, fused, acc_nodes):
+    def __init__(self, graph, heads, H, hk, hv, n_layers, fused, acc_nodes, dkv_w=None, dkv_b=None,
+                 batched=False):
         self.graph = graph
         self.heads = heads
         self.H = H
         self.hk = hk
         self.hv = hv
         self.n_layers = n_layers
-        self.fused = fused  # per layer (qkv_w, qkv_b, dkv_w, dkv_b) stacked views
+        self.fused = fused  # per layer (qkv_w, qkv_b) stacked views
+        self.D = (int(hk) + 3 * int(hv)) * H  # dk/dv rows per layer
+        self.dkv_w, self.dkv_b = dkv_w, dkv_b  # all layers' [dk; dv] (StackWeights)
+        self.batched = batched  # one GEMM for every layer's projection
         self.acc_nodes = acc_nodes  # per layer: AccumulateGrad nodes of its parameters (or None)
         self.np = 11 + 2 * int(hk) + 2 * int(hv)  # parameters per layer
 
     def split(self, params):
         return [params[i * self.np:(i + 1) * self.np] for i in range(self.n_layers)]
+
+    def dkv_layer(self, l):
+        if self.dkv_w is None:
+            return None, None
+        a, b = l * self.D, (l + 1) * self.D
+        return self.dkv_w[a:b], self.dkv_b[a:b]
 
 
 def _epilogue_fwd(x, vec, vecp, o, veca):
@@ -159,14 +194,20 @@ def _forward_layers(meta, x, f, C, u, params):
     N = x.shape[0]
     vec = None
     acts = []
+    D = meta.D
+    pkv_all = torch.addmm(meta.dkv_b, f, meta.dkv_w.t()) if (meta.batched and D) else None
     for l, p in enumerate(meta.split(params)):
         ln_w, ln_b = p[0], p[1]
         vec_w, o_w, o_b = p[8], p[9], p[10]
-        qkv_w, qkv_b, dkv_w, dkv_b = meta.fused[l]
+        qkv_w, qkv_b = meta.fused[l]
+        dkv_w, dkv_b = meta.dkv_layer(l)
         xn, mean, rstd = torch.native_layer_norm(x, [H], ln_w, ln_b, _EPS)
         qkv = torch.addmm(qkv_b, xn, qkv_w.t())
         vecp = None if vec is None else torch.mm(vec.view(3 * N, H), vec_w.t()).view(N, 3, 3 * H)
-        pkv = torch.addmm(dkv_b, f, dkv_w.t()) if dkv_w is not None else None
+        if pkv_all is not None:
+            pkv = pkv_all[:, l * D:(l + 1) * D]
+        else:
+            pkv = torch.addmm(dkv_b, f, dkv_w.t()) if dkv_w is not None else None
         pk = pkv[:, :H] if meta.hk else None
         pv = pkv[:, H * int(meta.hk):] if meta.hv else None
         xa = torch.empty((N, H), dtype=x.dtype, device=x.device)
@@ -190,8 +231,10 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws):
     g_C = torch.zeros((E,), **o)
     g_u = torch.zeros((E, 3), **o)
     has_e = meta.hk or meta.hv
-    g_pkv = graph.alloc_edge_grad((E, (int(meta.hk) + 3 * int(meta.hv)) * H), gX.dtype, gX.device) \
-        if has_e else None
+    D = meta.D
+    # padding rows of a static-capacity list are zeroed by the kernel: no memset needed
+    if has_e:
+        g_pkv_all = torch.empty((E, meta.n_layers * D if meta.batched else D), **o)
     g_f = None
     g_qkv = torch.empty((N, 5 * H), **o)
     g_o = torch.empty((N, 3 * H), **o)
@@ -204,7 +247,10 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws):
         x, vec, xn, mean, rstd, qkv, vecp, pkv, xa, o_ = acts[l]
         ln_w, ln_b = p[0], p[1]
         vec_w, o_w = p[8], p[9]
-        qkv_w, _, dkv_w, _ = meta.fused[l]
+        qkv_w, _ = meta.fused[l]
+        dkv_w, _ = meta.dkv_layer(l)
+        if has_e:
+            g_pkv = g_pkv_all[:, l * D:(l + 1) * D] if meta.batched else g_pkv_all
         _epilogue_bwd(gX, gV, vecp, o_, g_vecp, g_o)
         g_xa = torch.mm(g_o, o_w)
         pk = pkv[:, :H] if meta.hk else None
@@ -216,7 +262,7 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws):
             qkv[:, :H], qkv[:, H:2 * H], qkv[:, 2 * H:], vec, pk, pv, C, u, graph, meta.heads, g_xa, gV,
             g_qkv[:, :H], g_qkv[:, H:2 * H], g_qkv[:, 2 * H:], g_vec_in, gpk, gpv, g_C, g_u,
             accumulate=nat.ACC_VEC_RESIDUAL | nat.ACC_EDGE)
-        if has_e:
+        if has_e and not meta.batched:
             if g_f is None:
                 g_f = torch.mm(g_pkv, dkv_w)
             else:
@@ -237,22 +283,41 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws):
                   (torch.mm(g_vecp.view(3 * N, 3 * H).t(), vec.view(3 * N, H)) if vec is not None
                    else torch.zeros((3 * H, H), **o)),
                   torch.mm(g_o.t(), xa), g_o.sum(0)]
-            if has_e:
-                g_dkv_w = torch.mm(g_pkv.t(), f)
-                g_dkv_b = g_pkv.sum(0)
-                if meta.hk:
-                    gp += [g_dkv_w[:H], g_dkv_b[:H]]
-                if meta.hv:
-                    a = H * int(meta.hk)
-                    gp += [g_dkv_w[a:], g_dkv_b[a:]]
-            g_params[base:base + meta.np] = gp
+            if has_e and not meta.batched:
+                gp += _dkv_param_grads(meta, torch.mm(g_pkv.t(), f), g_pkv.sum(0))
+            g_params[base:base + len(gp)] = gp  # batched mode: dk/dv grads filled after the loop
         gX = g_x
         gV = g_vec_in
+    if has_e and meta.batched:  # every layer's edge-feature / projection gradients in one GEMM each
+        g_f = torch.mm(g_pkv_all, meta.dkv_w)
+        if any(need_ws):
+            g_w_all = torch.mm(g_pkv_all.t(), f)
+            g_b_all = g_pkv_all.sum(0)
+            for l in range(meta.n_layers):
+                if need_ws[l]:
+                    base = l * meta.np + 11
+                    a, b = l * D, (l + 1) * D
+                    gl = _dkv_param_grads(meta, g_w_all[a:b], g_b_all[a:b])
+                    g_params[base:base + len(gl)] = gl
     return gX, g_f, g_C, g_u, g_params
 
 
-def composite_stack(meta, x, f, C, u, params):
-    """Reference math in plain PyTorch GPU ops (second-order backward only)."""
+def _dkv_param_grads(meta, g_w, g_b):
+    """[dk_w, dk_b, dv_w, dv_b] (those present) from one layer's [dk; dv] gradient rows."""
+    H = meta.H
+    out = []
+    if meta.hk:
+        out += [g_w[:H], g_b[:H]]
+    if meta.hv:
+        a = H * int(meta.hk)
+        out += [g_w[a:], g_b[a:]]
+    return out
+
+
+def composite_stack(meta, x, f, C, u, params, message=None):
+    """Reference math (torchmd_et.py:177-184, 293-321) as differentiable ops.  ``message`` is the
+    ET message implementation: the HIP autograd Functions (``kernels.et_message``, whose backward
+    and second-order backward are HIP kernels) or, by default, the plain PyTorch restatement."""
     H = meta.H
     graph = meta.graph
     src, dst = graph.src.long(), graph.dst.long()
@@ -267,7 +332,10 @@ def composite_stack(meta, x, f, C, u, params):
         vec_dot = (vec1 * vec2).sum(dim=1)
         pk = F.linear(f, rest.pop(0), rest.pop(0)) if meta.hk else None
         pv = F.linear(f, rest.pop(0), rest.pop(0)) if meta.hv else None
-        xa, veca = kernels.et_message_composite(q, k, v, vec, pk, pv, C, u, src, dst, N, meta.heads)
+        if message is None:
+            xa, veca = kernels.et_message_composite(q, k, v, vec, pk, pv, C, u, src, dst, N, meta.heads)
+        else:
+            xa, veca = message(q, k, v, vec, pk, pv, C, u)
         o1, o2, o3 = torch.split(F.linear(xa, o_w, o_b), H, dim=1)
         x = x + vec_dot * o2 + o3
         vec = vec + vec3 * o1.unsqueeze(1) + veca
@@ -320,13 +388,21 @@ class _ETStackBwd(Function):
 
     @staticmethod
     def backward(ctx, *ggs):
+        """Second order (force-matching training): the layers are re-run with the HIP message
+        Functions and differentiated twice, so the message's second order runs the HIP kernel
+        tmdnet_et_message_bwd2 and the node ops PyTorch's GEMM / layer-norm double backwards."""
         saved = ctx.saved_tensors
         meta = ctx.meta
+        graph, heads = meta.graph, meta.heads
+
+        def message(q, k, v, vec, pk, pv, C_, u_):
+            return kernels.et_message(q, k, v, vec, pk, pv, C_, u_, graph, heads)
+
         with torch.enable_grad():
             leaves = [None if t is None else t.detach().requires_grad_(True) for t in saved]
             gX, gV, x, f, C, u = leaves[:6]
             params = leaves[6:]
-            xo, vo = composite_stack(meta, x, f, C, u, params)
+            xo, vo = composite_stack(meta, x, f, C, u, params, message=message)
             wrt = [x, f, C, u] + params
             live = [t for t in wrt if t is not None]
             first = torch.autograd.grad((xo, vo), live, (gX, gV), create_graph=True, allow_unused=True)
@@ -352,6 +428,11 @@ def et_stack(layers, x, graph, f, C, u):
     hk, hv = l0.dk_proj is not None, l0.dv_proj is not None
     fused, params, acc = [], [], []
     grad_on = torch.is_grad_enabled()
+    sw = getattr(layers, "_tmd_stack", None)
+    if sw is None or sw.layers is not layers:
+        sw = StackWeights(layers)
+        layers._tmd_stack = sw
+    dkv_w, dkv_b = sw.dkv()
     for layer in layers:
         layer._check_supported()
         if layer._stacked is None:
@@ -361,7 +442,9 @@ def et_stack(layers, x, graph, f, C, u):
         params += lp
         acc.append(layer._stacked.acc_nodes(lp) if (grad_on and any(p.requires_grad for p in lp))
                    else None)
-    meta = _Meta(graph, heads, H, hk, hv, len(layers), fused, acc)
+    D = (int(hk) + 3 * int(hv)) * H
+    batched = D > 0 and graph.n_edges * len(layers) * D * x.element_size() <= BATCH_DKV_BYTES
+    meta = _Meta(graph, heads, H, hk, hv, len(layers), fused, acc, dkv_w, dkv_b, batched)
     x = x.contiguous()
     f = f.contiguous() if (hk or hv) else None
     return _ETStack.apply(meta, x, f, C.contiguous(), u.contiguous(), *params)

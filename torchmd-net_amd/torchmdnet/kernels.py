@@ -504,6 +504,11 @@ class _ETMessageBwd(Function):
 
     @staticmethod
     def backward(ctx, *ggs):
+        return et_message_bwd2(ctx, ggs)
+
+    @staticmethod
+    def composite_backward(ctx, *ggs):
+        """Second order by recompute + autograd over the PyTorch restatement (tests only)."""
         saved = ctx.saved_tensors
         graph = ctx.graph
         src, dst = graph.src.long(), graph.dst.long()
@@ -525,6 +530,43 @@ class _ETMessageBwd(Function):
         it = iter(second)
         res = [next(it) if t is not None else None for t in leaves]
         return tuple(res) + (None, None)
+
+
+def et_message_bwd2(ctx, ggs):
+    """HIP second-order backward of the ET message (``tmdnet_et_message_bwd2``).  Its own backward
+    (third order) is not implemented."""
+    gx, gvec, q, k, v, vec, pk, pv, C, u = ctx.saved_tensors
+    graph = ctx.graph
+    lib = nat.load()
+    N, H = q.shape
+    E = graph.n_edges
+    o = dict(dtype=q.dtype, device=q.device)
+
+    def dense(g, shape):
+        return torch.zeros(shape, **o) if (g is None or g.numel() == 0) else g.contiguous()
+
+    ggq, ggk, ggv = dense(ggs[0], (N, H)), dense(ggs[1], (N, H)), dense(ggs[2], (N, 3 * H))
+    ggw = dense(ggs[3], (N, 3, H))
+    ggpk = dense(ggs[4], (E, H)) if pk is not None else None
+    ggpv = dense(ggs[5], (E, 3 * H)) if pv is not None else None
+    ggC, ggu = dense(ggs[6], (E,)), dense(ggs[7], (E, 3))
+    d_gx, d_gvec, d_q = torch.empty((N, H), **o), torch.empty((N, 3, H), **o), torch.empty((N, H), **o)
+    d_k, d_v, d_vec = torch.zeros((N, H), **o), torch.zeros((N, 3 * H), **o), torch.zeros((N, 3, H), **o)
+    d_pk = torch.zeros((E, H), **o) if pk is not None else None
+    d_pv = torch.zeros((E, 3 * H), **o) if pv is not None else None
+    d_C, d_u = torch.zeros((E,), **o), torch.zeros((E, 3), **o)
+    qc, kc, vc = q.contiguous(), k.contiguous(), v.contiguous()
+    pkc = None if pk is None else pk.contiguous()
+    pvc = None if pv is None else pv.contiguous()
+    rc = lib.tmdnet_et_message_bwd2(
+        nat.dtype_code(q.dtype), N, H, ctx.heads, nat.ptr(graph.row_ptr), nat.ptr(graph.src), E,
+        nat.ptr(qc), H, nat.ptr(kc), H, nat.ptr(vc), 3 * H, nat.ptr(vec), nat.ptr(pkc), H, nat.ptr(pvc), 3 * H,
+        nat.ptr(C), nat.ptr(u), nat.ptr(gx), nat.ptr(gvec), nat.ptr(ggq), nat.ptr(ggk), nat.ptr(ggv),
+        nat.ptr(ggw), nat.ptr(ggpk), H, nat.ptr(ggpv), 3 * H, nat.ptr(ggC), nat.ptr(ggu), nat.ptr(d_gx),
+        nat.ptr(d_gvec), nat.ptr(d_q), nat.ptr(d_k), nat.ptr(d_v), nat.ptr(d_vec), nat.ptr(d_pk),
+        nat.ptr(d_pv), nat.ptr(d_C), nat.ptr(d_u), nat.stream(q.device))
+    nat.check(rc, "tmdnet_et_message_bwd2")
+    return (d_gx, d_gvec, d_q, d_k, d_v, d_vec, d_pk, d_pv, d_C, d_u, None, None)
 
 
 def et_message(q, k, v, vec, pk, pv, C, u, graph, heads):
