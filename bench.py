@@ -53,6 +53,8 @@ def parse():
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 --pmc traffic passes")
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip the secondary lines (TensorNet C3 graph replay, ET training step)")
+    ap.add_argument("--graphed-train", action="store_true",
+                    help="also time the HIP-graph-captured training step (training.GraphedTrainStep)")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
@@ -142,13 +144,15 @@ def probe_workload(n_atoms, H, dev):
     def launch():
         rc = lib.tmdnet_et_message_fwd(0, n_atoms, H, 8, ptr(graph.row_ptr), ptr(graph.src), E, ptr(q), H,
                                        ptr(k), H, ptr(v), 3 * H, ptr(vec), ptr(pk), H, ptr(pv), 3 * H, ptr(C),
-                                       ptr(u), ptr(xo), ptr(vo), None, st)
+                                       ptr(u), ptr(xo), ptr(vo), PROBE_FLAGS, None, st)
         kernels.nat.check(rc, "tmdnet_et_message_fwd")
 
     return launch, E, L
 
 
 PROBE_KERNEL = "k_fwd<float, 4, 1, 1, false>"
+# the model runs large graphs with planar v / dv rows (et_stack.PLANAR_MIN_EDGES): probe that layout
+PROBE_FLAGS = 4  # TMDNET_ET_V_PLANAR
 
 
 def pmc_traffic(a):
@@ -224,6 +228,11 @@ def roofline_probe(a, dev):
     return res
 
 
+def phase(msg):
+    """Progress line on stderr (the JSON result line is the only stdout output)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def timed_loop(step, warmup, steps, ws, dev):
     for _ in range(warmup):
         step()
@@ -282,13 +291,25 @@ def secondary_train(a, ws, rank, dev):
     y_lab = torch.randn(a.batch, 1, generator=gy).to(dev)
     f_lab = torch.randn(z.shape[0], 3, generator=gy).to(dev)
     z, pos, batch = z.to(dev), pos.float().to(dev), batch.to(dev)
+    from torchmdnet.training import GraphedTrainStep
+    steps = max(10, a.steps // 2)
+    phase("train: eager steps")
     trainer = LNNPStep(model, lr=4e-4)
-    steps = max(5, a.steps // 5)
-    el = timed_loop(lambda: trainer.step(z, pos, batch, y_lab, f_lab), max(2, a.warmup // 2), steps, ws, dev)
-    return {"workload": "ET-QM9 training step (E+F MSE, double backward, "
-                        + ("RCCL all-reduce, " if ws > 1 else "") + "AdamW), eager",
-            "value": round(a.batch * ws * steps / el, 2), "unit": "molecules/s",
-            "ms_per_step": round(1000 * el / steps, 4), "steps": steps, "parallelism": f"dp{ws}"}
+    el = timed_loop(lambda: trainer.step(z, pos, batch, y_lab, f_lab), max(3, a.warmup // 2), steps, ws, dev)
+    res = {"workload": "ET-QM9 training step (E+F MSE, double backward, "
+                       + ("fused RCCL all-reduce, " if ws > 1 else "") + "AdamW), eager",
+           "value": round(a.batch * ws * steps / el, 2), "unit": "molecules/s",
+           "ms_per_step": round(1000 * el / steps, 4), "steps": steps, "parallelism": f"dp{ws}"}
+    if a.graphed_train:
+        phase("train: graph-captured step")
+        del trainer
+        gtr = GraphedTrainStep(model, z, pos, batch, y_lab, f_lab, lr=4e-4)
+        el = timed_loop(lambda: gtr.step(), max(3, a.warmup // 2), steps, ws, dev)
+        gtr.check_capacity()
+        gtr.release()
+        res["graphed"] = {"value": round(a.batch * ws * steps / el, 2), "ms_per_step": round(1000 * el / steps, 4),
+                          "execution": "fwd + force pass + double backward in one HIP graph; all-reduce + AdamW eager"}
+    return res
 
 
 def cpu_baseline(model, args, z, pos, batch, seconds):
@@ -364,6 +385,7 @@ def main():
             it[0] += 1
             return gm(pool[it[0] % len(pool)])
 
+    phase(f"main: {a.mode} {'eager' if (a.eager or a.mode == 'train') else 'hip-graph'} timing")
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
@@ -426,12 +448,17 @@ def main():
                               "bytes_per_launch": nbytes, "ms_per_launch": round(ms, 5),
                               "launches": len(probe)}
     if a.mode == "infer" and not a.no_secondary:
-        sec = {"tensornet_c3": secondary_tensornet(a, ws, rank, dev), "et_train_step": secondary_train(a, ws, rank, dev)}
+        phase("secondary: TensorNet C3")
+        sec = {"tensornet_c3": secondary_tensornet(a, ws, rank, dev)}
+        phase("secondary: ET training step")
+        sec["et_train_step"] = secondary_train(a, ws, rank, dev)
         if rank == 0:
             out["secondary"] = sec
     if rank == 0 and not a.no_roofline:
+        phase("roofline probe (C5 water box)")
         out["roofline"] = roofline_probe(a, dev)
     if rank == 0 and ws == 1 and not a.no_cpu_baseline:
+        phase("CPU baseline")
         out["cpu_baseline"] = cpu_baseline(model, args, z, pos, batch, a.cpu_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -26,6 +26,11 @@ enum { TMDNET_F32 = 0, TMDNET_F64 = 1 };
 enum { TMDNET_NL_BRUTE = 0, TMDNET_NL_SHARED = 1, TMDNET_NL_CELL = 2 };
 enum { TMDNET_RBF_EXPNORM = 0, TMDNET_RBF_GAUSS = 1 };
 enum { TMDNET_ACC_VEC_RESIDUAL = 1, TMDNET_ACC_EDGE = 2 };
+/* v / pv row layout flag of the ET message entry points: planar rows [x | v1 | v2] of H channels each
+ * instead of the reference's per-head interleave [h][x|v1|v2] of d channels (torchmd_et.py:282-291).
+ * Planar rows make every 16-byte-per-lane load of a row segment contiguous (measured 4-7 % on the C5
+ * forward).  Gradients of v / pv are written in the same layout. */
+enum { TMDNET_ET_V_PLANAR = 4 };
 
 /* ------------------------------------------------------------------------------------------
  * Neighbour list.  Replaces torchmdnet_neighbors::get_neighbor_pairs
@@ -98,7 +103,7 @@ int tmdnet_et_message_fwd(int dtype, int n_nodes, int hidden, int heads, const i
                           const int32_t* src, int max_pairs, const void* q, int ld_q, const void* k,
                           int ld_k, const void* v, int ld_v, const void* vec_in, const void* pk,
                           int ld_pk, const void* pv, int ld_pv, const void* cutoff, const void* unit,
-                          void* x_out, void* vec_out, const int32_t* order, void* stream);
+                          void* x_out, void* vec_out, int flags, const int32_t* order, void* stream);
 /* Backward (two CSR passes, no atomics): destination pass -> gq, gpk, gpv, gcut, gunit; source
  * pass (requires a symmetric edge list, dk/dv/cutoff functions of |r| only) -> gk, gv, gvec_in.
  * Gradients are written with the leading dimension of the matching input (gq: ld_q, gk: ld_k,
@@ -115,7 +120,8 @@ int tmdnet_et_message_bwd(int dtype, int n_nodes, int hidden, int heads, const i
                           int ld_pk, const void* pv, int ld_pv, const void* cutoff, const void* unit,
                           const void* grad_x, const void* grad_vec, void* gq, void* gk, void* gv,
                           void* gvec_in, void* gpk, void* gpv, void* gcut, void* gunit,
-                          int accumulate, const int32_t* order, void* stream);
+                          int accumulate, const int32_t* order, void* stream);  /* accumulate may also
+                                                   carry TMDNET_ET_V_PLANAR */
 
 /* Second-order backward: the VJP of tmdnet_et_message_bwd (forces differentiated again, reference
  * model.py:286-298 with create_graph=True).  gg_* are the cotangents of that call's outputs (gq, gk,
@@ -131,7 +137,8 @@ int tmdnet_et_message_bwd2(int dtype, int n_nodes, int hidden, int heads, const 
                            const void* gg_v, const void* gg_vec, const void* gg_pk, int ld_ggpk,
                            const void* gg_pv, int ld_ggpv, const void* gg_cut, const void* gg_unit,
                            void* d_grad_x, void* d_grad_vec, void* d_q, void* d_k, void* d_v,
-                           void* d_vec, void* d_pk, void* d_pv, void* d_cut, void* d_unit, void* stream);
+                           void* d_vec, void* d_pk, void* d_pv, void* d_cut, void* d_unit, int flags,
+                           void* stream);
 
 /* ET layer epilogue (reference torchmd_et.py:278-280, 309-311 + residuals 181-184), fused:
  *   vecp = vec_proj(vec) [N][3][3H] = [v1|v2|v3], o = o_proj(x_agg) [N][3H] = [o1|o2|o3]

@@ -20,8 +20,24 @@ from torchmdnet.models.torchmd_et import EquivariantMultiHeadAttention
 DT = torch.float64
 
 
-def _fake_fwd(q, k, v, vec, pk, pv, C, u, graph, heads, xo, vo):
+def _to_inter(t, H, heads, planar):
+    """planar [x|v1|v2] H-blocks -> reference per-head interleave (columns)."""
+    if t is None or not planar:
+        return t
+    inv = torch.argsort(ES._v_perm(H, heads, t.device))
+    return t[:, inv]
+
+
+def _to_planar(g, H, heads, planar):
+    if g is None or not planar:
+        return g
+    return g[:, ES._v_perm(H, heads, g.device)]
+
+
+def _fake_fwd(q, k, v, vec, pk, pv, C, u, graph, heads, xo, vo, flags=0):
     N, H = q.shape
+    planar = bool(flags & nat.ET_V_PLANAR)
+    v, pv = _to_inter(v, H, heads, planar), _to_inter(pv, H, heads, planar)
     vec_ = torch.zeros((N, 3, H), dtype=q.dtype) if vec is None else vec
     a, b = kernels.et_message_composite(q, k, v, vec_, pk, pv, C, u, graph.src.long(), graph.dst.long(),
                                         N, heads)
@@ -32,6 +48,8 @@ def _fake_fwd(q, k, v, vec, pk, pv, C, u, graph, heads, xo, vo):
 def _fake_bwd(q, k, v, vec, pk, pv, C, u, graph, heads, gx, gvec, gq, gk, gv, gw, gpk, gpv, gC, gu,
               accumulate=0):
     N, H = q.shape
+    planar = bool(accumulate & nat.ET_V_PLANAR)
+    v, pv = _to_inter(v, H, heads, planar), _to_inter(pv, H, heads, planar)
     with torch.enable_grad():
         ins = [None if t is None else t.detach().clone().requires_grad_(True)
                for t in (q, k, v, vec, pk, pv, C, u)]
@@ -45,13 +63,13 @@ def _fake_bwd(q, k, v, vec, pk, pv, C, u, graph, heads, gx, gvec, gq, gk, gv, gw
     z = lambda t, ref: torch.zeros_like(ref) if t is None else t  # noqa: E731
     gq.copy_(z(g[0], q))
     gk.copy_(z(g[1], k))
-    gv.copy_(z(g[2], v))
+    gv.copy_(_to_planar(z(g[2], v), H, heads, planar))
     if gw is not None:
         gw.copy_(z(g[3], gw) + (gvec if accumulate & nat.ACC_VEC_RESIDUAL else 0))
     if gpk is not None:
         gpk.copy_(z(g[4], pk))
     if gpv is not None:
-        gpv.copy_(z(g[5], pv))
+        gpv.copy_(_to_planar(z(g[5], pv), H, heads, planar))
     if accumulate & nat.ACC_EDGE:
         gC.add_(g[6])
         gu.add_(g[7])
@@ -141,11 +159,14 @@ def _meta_for(layers, graph):
                     len(layers), None, None)
 
 
+@pytest.mark.parametrize("planar", [False, True])
 @pytest.mark.parametrize("batched", [True, False])
 @pytest.mark.parametrize("infl", ["both", "keys", "values", "none"])
-def test_stack_forward_and_grads_match_composite(emulated, monkeypatch, infl, batched):
+def test_stack_forward_and_grads_match_composite(emulated, monkeypatch, infl, batched, planar):
     if not batched:  # per-layer dk/dv GEMMs (the large-system path)
         monkeypatch.setattr(ES, "BATCH_DKV_BYTES", 0)
+    if planar:  # planar v / dv rows (permuted weight rows; the large-system path)
+        monkeypatch.setattr(ES, "PLANAR_MIN_EDGES", 0)
     H, R, heads = 16, 8, 4
     n, graph, r, vecs = _system()
     x, f, C, u = _inputs(n, graph, r, vecs, H, R)

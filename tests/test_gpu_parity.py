@@ -446,11 +446,16 @@ def test_large_system_spatial_reorder_is_transparent():
     assert _rel(out[0][1].cpu(), out[1][1].cpu()) < 1e-9
 
 
+@pytest.mark.parametrize("planar", [False, True])
 @pytest.mark.parametrize("infl", ["both", "keys", "values", "none"])
-def test_et_fused_stack_matches_per_layer_path(infl):
+def test_et_fused_stack_matches_per_layer_path(infl, planar, monkeypatch):
     """et_stack (one autograd node, fused GEMMs + HIP epilogue) == the per-layer module path:
-    energies, forces and force-loss training gradients (double backward), fp64."""
+    energies, forces and force-loss training gradients (double backward), fp64.  planar: the
+    large-graph TMDNET_ET_V_PLANAR layout forced on."""
+    from torchmdnet import et_stack
     from torchmdnet.models.model import create_model
+    if planar:
+        monkeypatch.setattr(et_stack, "PLANAR_MIN_EDGES", 0)
     _seed()
     m = create_model(yaml_args("equivariant-transformer", embedding_dimension=64, num_layers=3, num_rbf=16,
                                num_heads=4, derivative=True, output_model="Scalar", precision=64,
@@ -541,3 +546,35 @@ def test_et_message_second_order_kernel_matches_composite(infl):
     for n, ga, gb in zip(names, a, b):
         gb = torch.zeros_like(ga) if gb is None else gb
         assert torch.allclose(ga, gb, atol=1e-10, rtol=1e-8), n
+
+
+def test_graphed_train_step_matches_eager():
+    """GraphedTrainStep (forward + force pass + double backward in one HIP graph) produces the same
+    loss and parameter gradients as the eager LNNPStep, fp64."""
+    from torchmdnet.models.model import create_model
+    from torchmdnet.training import GraphedTrainStep, LNNPStep
+    _seed()
+    args = yaml_args("equivariant-transformer", embedding_dimension=32, num_layers=2, num_rbf=16, num_heads=4,
+                     derivative=True, output_model="Scalar", precision=64)
+    m = create_model(args).to(DEV)
+    z, pos, batch = O.qm9_like(4)
+    z, pos, batch = z.to(DEV), pos.to(DEV), batch.to(DEV)
+    y = torch.randn(4, 1, dtype=torch.float64, device=DEV)
+    f = torch.randn(pos.shape, dtype=torch.float64, device=DEV)
+    ref = LNNPStep(m, lr=0.0)
+    ref.opt.zero_grad(set_to_none=True)
+    loss_ref = ref.loss(z, pos, batch, y, f)
+    ref.backward(loss_ref)
+    g_ref = [p.grad.clone() for p in m.parameters()]
+    del loss_ref  # a live loss keeps its autograd graph (and the AccumulateGrad nodes) alive
+    gtr = GraphedTrainStep(m, z, pos, batch, y, f, lr=0.0)
+    p2 = pos + 0.01
+    gtr.step(pos=p2)
+    g_graph = [p.grad.clone() for p in m.parameters()]
+    gtr.check_capacity()
+    gtr.release()
+    ref.opt.zero_grad(set_to_none=True)
+    ref.backward(ref.loss(z, p2, batch, y, f))
+    for a, b in zip(g_graph, [p.grad for p in m.parameters()]):
+        assert torch.allclose(a, b, rtol=1e-9, atol=1e-11)
+    assert g_ref[0].shape == g_graph[0].shape

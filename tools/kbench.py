@@ -172,3 +172,12 @@ if __name__ == "__main__" and os.environ.get("KBENCH_DECOMPOSE"):
     _g = graph_c5(50001, _dev, "morton")
     for _h in (8, 2, 1):
         decompose(_g, 128, 20, _dev, _h)
+    # interleaved vs planar v / dv rows, same graph, alternating
+    x = et_inputs(_g, 128, _dev)
+    N = _g.n_nodes
+    xo, vo = torch.empty(N, 128, device=_dev), torch.empty(N, 3, 128, device=_dev)
+    for rep_ in range(3):
+        for fl in (0, 4):
+            t = timeit(lambda: kernels.et_message_fwd_launch(x["q"], x["k"], x["v"], x["vec"], x["pk"], x["pv"],
+                                                             x["C"], x["u"], _g, 8, xo, vo, fl), 20)
+            print(f"fwd flags={fl}: {t:.0f} us")

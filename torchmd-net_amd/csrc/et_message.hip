@@ -93,6 +93,8 @@ template <typename T> struct Args {
   const T* gx; const T* gvec;
   T* gq; T* gk; T* gv; T* gveci; T* gpk; T* gpv; T* gC; T* gu;
   int acc;  // TMDNET_ACC_* flags of the backward
+  int planar;  // TMDNET_ET_V_PLANAR: v / pv rows are [x | v1 | v2] H-blocks (else per-head [x|v1|v2] d-blocks)
+  int vst;     // distance between the x, v1, v2 parts of a v / pv row: H (planar) or d
 };
 
 // SiLU of a pre-activation row segment already in registers (or 1 / 0 when the projection is
@@ -248,9 +250,9 @@ __global__ __launch_bounds__(256) void k_fwd(Args<T> A) {
   const int EPW = TMD_WAVE / A.L;  // edges per wave instruction
   const int c0 = G.cg * A.HC + G.el * V;
   const int hh = c0 / A.d, cc = c0 % A.d;
-  const int vo = hh * 3 * A.d + cc;
+  const int vo = A.planar ? c0 : hh * 3 * A.d + cc;
   const bool hk = A.pk != nullptr, hv = A.pv != nullptr, hw = A.vec != nullptr;
-  const int pvd = hv ? A.d : 0, vcd = hw ? A.H : 0;  // branch-free optional loads
+  const int pvd = hv ? A.vst : 0, vcd = hw ? A.H : 0;  // branch-free optional loads
   (void)vcd;
   T ax[V], a0[V], a1[V], a2[V];
   zero(ax); zero(a0); zero(a1); zero(a2);
@@ -274,8 +276,8 @@ __global__ __launch_bounds__(256) void k_fwd(Args<T> A) {
       ldv<T, V>(kk, A.k + (size_t)s * A.ldk + c0);
       const T* vs = A.v + (size_t)s * A.ldv + vo;
       ldv<T, V>(vx, vs);
-      ldv<T, V>(v1, vs + A.d);
-      ldv<T, V>(v2, vs + 2 * A.d);
+      ldv<T, V>(v1, vs + A.vst);
+      ldv<T, V>(v2, vs + 2 * A.vst);
       const T* vecs = hw ? A.vec + (size_t)s * 3 * A.H + c0 : dummy + c0;
       ldv<T, V>(w0, vecs);
       ldv<T, V>(w1, vecs + vcd);
@@ -350,9 +352,9 @@ __device__ __forceinline__ void bwd_dst_body(const Args<T>& A, int blk, int nwg)
   const int EPW = TMD_WAVE / A.L;  // edges per wave instruction
   const int c0 = G.cg * A.HC + G.el * V;
   const int hh = c0 / A.d, cc = c0 % A.d;
-  const int vo = hh * 3 * A.d + cc;
+  const int vo = A.planar ? c0 : hh * 3 * A.d + cc;
   const bool hk = A.pk != nullptr, hv = A.pv != nullptr, hw = A.vec != nullptr;
-  const int pvd = hv ? A.d : 0, vcd = hw ? A.H : 0;  // branch-free optional loads
+  const int pvd = hv ? A.vst : 0, vcd = hw ? A.H : 0;  // branch-free optional loads
   (void)vcd;
   const bool head_leader = on && (G.el % A.lph) == 0;
   T gq[V];
@@ -388,8 +390,8 @@ __device__ __forceinline__ void bwd_dst_body(const Args<T>& A, int blk, int nwg)
       ldv<T, V>(kk, A.k + (size_t)s * A.ldk + c0);
       const T* vs = A.v + (size_t)s * A.ldv + vo;
       ldv<T, V>(vx, vs);
-      ldv<T, V>(v1, vs + A.d);
-      ldv<T, V>(v2, vs + 2 * A.d);
+      ldv<T, V>(v1, vs + A.vst);
+      ldv<T, V>(v2, vs + 2 * A.vst);
       const T* vecs = hw ? A.vec + (size_t)s * 3 * A.H + c0 : dummy + c0;
       ldv<T, V>(w0, vecs);
       ldv<T, V>(w1, vecs + vcd);
@@ -440,8 +442,8 @@ __device__ __forceinline__ void bwd_dst_body(const Args<T>& A, int blk, int nwg)
         if (hv) {
           T* gp = A.gpv + (size_t)k * A.ldpv + vo;
           stv<T, V>(gp, gpx);
-          stv<T, V>(gp + A.d, gp1);
-          stv<T, V>(gp + 2 * A.d, gp2);
+          stv<T, V>(gp + A.vst, gp1);
+          stv<T, V>(gp + 2 * A.vst, gp2);
         }
       }
       if (G.el == 0) {
@@ -471,9 +473,9 @@ __device__ __forceinline__ void bwd_src_body(const Args<T>& A, int blk, int nwg)
   const int EPW = TMD_WAVE / A.L;  // edges per wave instruction
   const int c0 = G.cg * A.HC + G.el * V;
   const int hh = c0 / A.d, cc = c0 % A.d;
-  const int vo = hh * 3 * A.d + cc;
+  const int vo = A.planar ? c0 : hh * 3 * A.d + cc;
   const bool hk = A.pk != nullptr, hv = A.pv != nullptr, hw = A.vec != nullptr;
-  const int pvd = hv ? A.d : 0, vcd = hw ? A.H : 0;  // branch-free optional loads
+  const int pvd = hv ? A.vst : 0, vcd = hw ? A.H : 0;  // branch-free optional loads
   (void)vcd;
   T gk[V], gvx[V], gv1[V], gv2[V], gw0[V], gw1[V], gw2[V];
   zero(gk); zero(gvx); zero(gv1); zero(gv2); zero(gw0); zero(gw1); zero(gw2);
@@ -482,8 +484,8 @@ __device__ __forceinline__ void bwd_src_body(const Args<T>& A, int blk, int nwg)
     ldv<T, V>(kk, A.k + (size_t)j * A.ldk + c0);
     const T* vj = A.v + (size_t)j * A.ldv + vo;
     ldv<T, V>(vx, vj);
-    ldv<T, V>(v1, vj + A.d);
-    ldv<T, V>(v2, vj + 2 * A.d);
+    ldv<T, V>(v1, vj + A.vst);
+    ldv<T, V>(v2, vj + 2 * A.vst);
     if (hw) {
       const T* vecj = A.vec + (size_t)j * 3 * A.H + c0;
       ldv<T, V>(w0, vecj);
@@ -566,8 +568,8 @@ __device__ __forceinline__ void bwd_src_body(const Args<T>& A, int blk, int nwg)
     stv<T, V>(A.gk + (size_t)j * A.ldk + c0, gk);
     T* gvj = A.gv + (size_t)j * A.ldv + vo;
     stv<T, V>(gvj, gvx);
-    stv<T, V>(gvj + A.d, gv1);
-    stv<T, V>(gvj + 2 * A.d, gv2);
+    stv<T, V>(gvj + A.vst, gv1);
+    stv<T, V>(gvj + 2 * A.vst, gv2);
     if (A.gveci != nullptr) {
       if (A.acc & TMDNET_ACC_VEC_RESIDUAL) {  // gvec_in = grad_vec (residual path) + message part
         const T* gr = A.gvec + (size_t)j * 3 * A.H + c0;
@@ -637,29 +639,31 @@ template <typename T> struct Args2 {
   T* o_pk; T* o_pv; T* o_C; T* o_u;                          // edge outputs ([E][H], [E][3H], [E], [E][3])
 };
 
-template <typename T, int V>
+template <typename T, int V, int S>
 __global__ __launch_bounds__(256) void k_bwd2(Args2<T> B) {
+  __shared__ T lds[S > 1 ? 4 * 64 * 5 * V : 1];
   const Args<T>& A = B.a;
-  const Geo G = geo<1, 1, false>(A.n, A.L, nullptr, A.xcd, blockIdx.x, gridDim.x);
+  const Geo G = geo<S, 1, false>(A.n, A.L, nullptr, A.xcd, blockIdx.x, gridDim.x);
   const int t = G.node;
-  if (t < 0) return;
+  if (S == 1 && t < 0) return;
   const int EPW = TMD_WAVE / A.L;
   const int c0 = G.el * V;
   const int hh = c0 / A.d, cc = c0 % A.d;
-  const int vo = hh * 3 * A.d + cc;
+  const int vo = A.planar ? c0 : hh * 3 * A.d + cc;
   const bool hk = A.pk != nullptr, hv = A.pv != nullptr, hw = A.vec != nullptr;
   const bool head_leader = (G.el % A.lph) == 0;
   T q[V], gx[V], g0[V], g1[V], g2[V], ggq[V];
+  T oq[V], ogx[V], og0[V], og1[V], og2[V];
+  zero(oq); zero(ogx); zero(og0); zero(og1); zero(og2);
+  if (t >= 0) {
   ldv<T, V>(q, A.q + (size_t)t * A.ldq + c0);
   ldv<T, V>(gx, A.gx + (size_t)t * A.H + c0);
   ldv<T, V>(g0, A.gvec + (size_t)t * 3 * A.H + c0);
   ldv<T, V>(g1, A.gvec + (size_t)t * 3 * A.H + A.H + c0);
   ldv<T, V>(g2, A.gvec + (size_t)t * 3 * A.H + 2 * A.H + c0);
   ldv<T, V>(ggq, B.ggq + (size_t)t * A.H + c0);
-  T oq[V], ogx[V], og0[V], og1[V], og2[V];
-  zero(oq); zero(ogx); zero(og0); zero(og1); zero(og2);
   const int b = min(A.row_ptr[t], A.cap), e = min(A.row_ptr[t + 1], A.cap);
-  for (int k = b + G.es; k < e; k += EPW) {
+  for (int k = b + EPW * G.sub + G.es; k < e; k += EPW * S) {
     const int s = A.src[k];
     const T Ce = A.C[k];
     const T u0 = A.u[3 * k], u1 = A.u[3 * k + 1], u2 = A.u[3 * k + 2];
@@ -670,9 +674,9 @@ __global__ __launch_bounds__(256) void k_bwd2(Args2<T> B) {
     ldv<T, V>(kk, A.k + (size_t)s * A.ldk + c0);
     ldv<T, V>(ggk, B.ggk + (size_t)s * A.H + c0);
     const T* vs = A.v + (size_t)s * A.ldv + vo;
-    ldv<T, V>(vx, vs); ldv<T, V>(v1, vs + A.d); ldv<T, V>(v2, vs + 2 * A.d);
+    ldv<T, V>(vx, vs); ldv<T, V>(v1, vs + A.vst); ldv<T, V>(v2, vs + 2 * A.vst);
     const T* gvs = B.ggv + (size_t)s * 3 * A.H + vo;
-    ldv<T, V>(ggvx, gvs); ldv<T, V>(ggv1, gvs + A.d); ldv<T, V>(ggv2, gvs + 2 * A.d);
+    ldv<T, V>(ggvx, gvs); ldv<T, V>(ggv1, gvs + A.vst); ldv<T, V>(ggv2, gvs + 2 * A.vst);
     if (hw) {
       const T* ws = A.vec + (size_t)s * 3 * A.H + c0;
       ldv<T, V>(w0, ws); ldv<T, V>(w1, ws + A.H); ldv<T, V>(w2, ws + 2 * A.H);
@@ -689,9 +693,9 @@ __global__ __launch_bounds__(256) void k_bwd2(Args2<T> B) {
     }
     if (hv) {
       const T* ps = A.pv + (size_t)k * A.ldpv + vo;
-      ldv<T, V>(rx, ps); ldv<T, V>(r1, ps + A.d); ldv<T, V>(r2, ps + 2 * A.d);
+      ldv<T, V>(rx, ps); ldv<T, V>(r1, ps + A.vst); ldv<T, V>(r2, ps + 2 * A.vst);
       const T* gps = B.ggpv + (size_t)k * B.ldggpv + vo;
-      ldv<T, V>(ggpx, gps); ldv<T, V>(ggp1, gps + A.d); ldv<T, V>(ggp2, gps + 2 * A.d);
+      ldv<T, V>(ggpx, gps); ldv<T, V>(ggp1, gps + A.vst); ldv<T, V>(ggp2, gps + 2 * A.vst);
     } else {
       zero(rx); zero(r1); zero(r2); zero(ggpx); zero(ggp1); zero(ggp2);
     }
@@ -709,24 +713,24 @@ __global__ __launch_bounds__(256) void k_bwd2(Args2<T> B) {
         dx[i] = d1[i] = d2[i] = T(1); dx1[i] = d11[i] = d21[i] = T(0); dx2[i] = d12[i] = d22[i] = T(0);
       }
     }
-    T part = T(0), ga = T(0), S = T(0), X = T(0);
+    T part = T(0), ga = T(0), Sh = T(0), Xh = T(0);
 #pragma unroll
     for (int i = 0; i < V; ++i) {
       part += q[i] * kk[i] * dk[i];
       ga += gx[i] * vx[i] * dx[i];
-      S += ggq[i] * kk[i] * dk[i] + ggk[i] * q[i] * dk[i] + ggpk[i] * q[i] * kk[i] * dk1[i];
-      X += ggvx[i] * gx[i] * dx[i] + ggpx[i] * gx[i] * vx[i] * dx1[i];
+      Sh += ggq[i] * kk[i] * dk[i] + ggk[i] * q[i] * dk[i] + ggpk[i] * q[i] * kk[i] * dk1[i];
+      Xh += ggvx[i] * gx[i] * dx[i] + ggpx[i] * gx[i] * vx[i] * dx1[i];
     }
     part = group_sum(part, A.lph);
     ga = group_sum(ga, A.lph);
-    S = group_sum(S, A.lph);
-    X = group_sum(X, A.lph);
+    Sh = group_sum(Sh, A.lph);
+    Xh = group_sum(Xh, A.lph);
     const Silu<T> sa(part);
     const T sil = sa.s, sd = sa.d(part), sdd = sa.dd(part);
     const T gs = ga * Ce * sd, a = sil * Ce;
-    const T P = Ce * ga * sdd * S + Ce * sd * X + ggC * ga * sd;
-    const T Gm = Ce * sd * S + ggC * sil;
-    const T gC = group_sum(head_leader ? ga * sd * S + sil * X : T(0), A.L);
+    const T P = Ce * ga * sdd * Sh + Ce * sd * Xh + ggC * ga * sd;
+    const T Gm = Ce * sd * Sh + ggC * sil;
+    const T gC = group_sum(head_leader ? ga * sd * Sh + sil * Xh : T(0), A.L);
     T ok_[V], opk[V], ovx[V], opx[V], ov1[V], op1[V], ov2[V], op2[V], ow0[V], ow1[V], ow2[V];
     T gua0 = T(0), gua1 = T(0), gua2 = T(0);
 #pragma unroll
@@ -762,7 +766,7 @@ __global__ __launch_bounds__(256) void k_bwd2(Args2<T> B) {
     if (hk) stv<T, V>(B.o_pk + (size_t)k * A.H + c0, opk);
     if (hv) {
       T* op = B.o_pv + (size_t)k * 3 * A.H + vo;
-      stv<T, V>(op, opx); stv<T, V>(op + A.d, op1); stv<T, V>(op + 2 * A.d, op2);
+      stv<T, V>(op, opx); stv<T, V>(op + A.vst, op1); stv<T, V>(op + 2 * A.vst, op2);
     }
     if (G.el == 0) {
       B.o_C[k] = gC;
@@ -773,15 +777,26 @@ __global__ __launch_bounds__(256) void k_bwd2(Args2<T> B) {
     for (int i = 0; i < V; ++i) {
       atomicAdd(B.o_k + (size_t)s * A.H + c0 + i, ok_[i]);
       T* ov = B.o_v + (size_t)s * 3 * A.H + vo + i;
-      atomicAdd(ov, ovx[i]); atomicAdd(ov + A.d, ov1[i]); atomicAdd(ov + 2 * A.d, ov2[i]);
+      atomicAdd(ov, ovx[i]); atomicAdd(ov + A.vst, ov1[i]); atomicAdd(ov + 2 * A.vst, ov2[i]);
       if (B.o_vec) {
         T* ow = B.o_vec + (size_t)s * 3 * A.H + c0 + i;
         atomicAdd(ow, ow0[i]); atomicAdd(ow + A.H, ow1[i]); atomicAdd(ow + 2 * A.H, ow2[i]);
       }
     }
   }
+  }  // t >= 0
   xor_slots(oq, A.L); xor_slots(ogx, A.L); xor_slots(og0, A.L); xor_slots(og1, A.L); xor_slots(og2, A.L);
-  if (G.es == 0) {
+  T all[5 * V];
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    all[i] = oq[i]; all[V + i] = ogx[i]; all[2 * V + i] = og0[i]; all[3 * V + i] = og1[i]; all[4 * V + i] = og2[i];
+  }
+  reduce_waves<T, S, 5 * V>(all, G.sub, lds);
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    oq[i] = all[i]; ogx[i] = all[V + i]; og0[i] = all[2 * V + i]; og1[i] = all[3 * V + i]; og2[i] = all[4 * V + i];
+  }
+  if (t >= 0 && G.sub == 0 && G.es == 0) {
     stv<T, V>(B.o_q + (size_t)t * A.H + c0, oq);
     stv<T, V>(B.o_gx + (size_t)t * A.H + c0, ogx);
     T* og = B.o_gvec + (size_t)t * 3 * A.H + c0;
@@ -986,6 +1001,7 @@ static int setup(Args<T>& A, int n, int H, int heads, const int32_t* row_ptr, co
     return kBadArgument;
   A = Args<T>{};
   A.n = n; A.H = H; A.d = d; A.L = H / V; A.HC = H; A.lph = lph; A.cap = cap;
+  A.planar = 0; A.vst = d;
   A.row_ptr = row_ptr; A.src = src; A.order = order;
   A.xcd = 1;
   A.q = (const T*)q; A.ldq = ldq; A.k = (const T*)k; A.ldk = ldk; A.v = (const T*)v; A.ldv = ldv_;
@@ -998,12 +1014,13 @@ template <typename T>
 static int fwd(int n, int H, int heads, const int32_t* row_ptr, const int32_t* src, int cap,
                const void* q, int ldq, const void* k, int ldk, const void* v, int ldv_,
                const void* vec, const void* pk, int ldpk, const void* pv, int ldpv, const void* C,
-               const void* u, void* xo, void* veco, const int32_t* order, hipStream_t st) {
+               const void* u, void* xo, void* veco, int flags, const int32_t* order, hipStream_t st) {
   Args<T> A;
   int V;
   int rc = setup<T>(A, n, H, heads, row_ptr, src, cap, q, ldq, k, ldk, v, ldv_, vec, pk, ldpk, pv,
                     ldpv, C, u, order, V);
   if (rc) return rc;
+  if (flags & TMDNET_ET_V_PLANAR) { A.planar = 1; A.vst = H; }
   A.xo = (T*)xo;
   A.veco = (T*)veco;
   return order ? et_launch<T, 0, true>(V, A, st) : et_launch<T, 0, false>(V, A, st);
@@ -1025,6 +1042,7 @@ static int bwd(int n, int H, int heads, const int32_t* row_ptr, const int32_t* s
   A.gq = (T*)gq; A.gk = (T*)gk; A.gv = (T*)gv; A.gveci = (T*)gveci;
   A.gpk = (T*)gpk; A.gpv = (T*)gpv; A.gC = (T*)gC; A.gu = (T*)gu;
   A.acc = acc;
+  if (acc & TMDNET_ET_V_PLANAR) { A.planar = 1; A.vst = H; }
   if (n < kBwdFuseNodes) return et_launch<T, 3, false>(V, A, st);
   rc = et_launch<T, 1, false>(V, A, st);
   if (rc) return rc;
@@ -1039,7 +1057,7 @@ static int bwd2(int n, int H, int heads, const int32_t* row_ptr, const int32_t* 
                 const void* ggv, const void* ggw, const void* ggpk, int ldggpk, const void* ggpv,
                 int ldggpv, const void* ggC, const void* ggu, void* o_gx, void* o_gvec, void* o_q,
                 void* o_k, void* o_v, void* o_vec, void* o_pk, void* o_pv, void* o_C, void* o_u,
-                hipStream_t st) {
+                int flags, hipStream_t st) {
   Args2<T> B{};
   int V;
   int rc = setup<T>(B.a, n, H, heads, row_ptr, src, cap, q, ldq, k, ldk, v, ldv_, vec, pk, ldpk, pv,
@@ -1054,6 +1072,7 @@ static int bwd2(int n, int H, int heads, const int32_t* row_ptr, const int32_t* 
   B.a.lph = d / V;
   if (B.a.L > 64 || (B.a.L & (B.a.L - 1))) return kUnsupported;
   if (!aligned<T>(ggpk, ldggpk, V) || !aligned<T>(ggpv, ldggpv, V)) return kBadArgument;
+  if (flags & TMDNET_ET_V_PLANAR) { B.a.planar = 1; B.a.vst = H; }
   B.a.gx = (const T*)gx; B.a.gvec = (const T*)gvec;
   B.ggq = (const T*)ggq; B.ggk = (const T*)ggk; B.ggv = (const T*)ggv; B.ggw = (const T*)ggw;
   B.ggpk = (const T*)ggpk; B.ldggpk = ldggpk; B.ggpv = (const T*)ggpv; B.ldggpv = ldggpv;
@@ -1061,10 +1080,13 @@ static int bwd2(int n, int H, int heads, const int32_t* row_ptr, const int32_t* 
   B.o_gx = (T*)o_gx; B.o_gvec = (T*)o_gvec; B.o_q = (T*)o_q; B.o_k = (T*)o_k; B.o_v = (T*)o_v;
   B.o_vec = (T*)o_vec; B.o_pk = (T*)o_pk; B.o_pv = (T*)o_pv; B.o_C = (T*)o_C; B.o_u = (T*)o_u;
   if (n <= 0) return kOk;
-  const dim3 g((n + 3) / 4), b(256);
-  if (V == 1) hipLaunchKernelGGL((k_bwd2<T, 1>), g, b, 0, st, B);
-  else if (V == 2) hipLaunchKernelGGL((k_bwd2<T, 2>), g, b, 0, st, B);
-  else hipLaunchKernelGGL((k_bwd2<T, 4>), g, b, 0, st, B);
+  const int S = n < 4096 ? 4 : (n < 8192 ? 2 : 1);  // waves per node (small systems: fill the chip)
+  const dim3 g((n + 4 / S - 1) / (4 / S)), b(256);
+#define TMD_L2(VV, SS) hipLaunchKernelGGL((k_bwd2<T, VV, SS>), g, b, 0, st, B)
+  if (V == 1) { if (S == 4) TMD_L2(1, 4); else if (S == 2) TMD_L2(1, 2); else TMD_L2(1, 1); }
+  else if (V == 2) { if (S == 4) TMD_L2(2, 4); else if (S == 2) TMD_L2(2, 2); else TMD_L2(2, 1); }
+  else { if (S == 4) TMD_L2(4, 4); else if (S == 2) TMD_L2(4, 2); else TMD_L2(4, 1); }
+#undef TMD_L2
   return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
 }
 
@@ -1090,14 +1112,15 @@ extern "C" int tmdnet_et_message_fwd(int dtype, int n_nodes, int hidden, int hea
                                      const void* q, int ld_q, const void* k, int ld_k, const void* v,
                                      int ld_v, const void* vec_in, const void* pk, int ld_pk,
                                      const void* pv, int ld_pv, const void* cutoff, const void* unit,
-                                     void* x_out, void* vec_out, const int32_t* order, void* stream) {
+                                     void* x_out, void* vec_out, int flags, const int32_t* order,
+                                     void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (dtype == TMDNET_F32)
     return et::fwd<float>(n_nodes, hidden, heads, row_ptr, src, max_pairs, q, ld_q, k, ld_k, v, ld_v,
-                          vec_in, pk, ld_pk, pv, ld_pv, cutoff, unit, x_out, vec_out, order, st);
+                          vec_in, pk, ld_pk, pv, ld_pv, cutoff, unit, x_out, vec_out, flags, order, st);
   if (dtype == TMDNET_F64)
     return et::fwd<double>(n_nodes, hidden, heads, row_ptr, src, max_pairs, q, ld_q, k, ld_k, v, ld_v,
-                           vec_in, pk, ld_pk, pv, ld_pv, cutoff, unit, x_out, vec_out, order, st);
+                           vec_in, pk, ld_pk, pv, ld_pv, cutoff, unit, x_out, vec_out, flags, order, st);
   return kUnsupported;
 }
 
@@ -1130,13 +1153,13 @@ extern "C" int tmdnet_et_message_bwd2(
     const void* gg_v, const void* gg_vec, const void* gg_pk, int ld_ggpk, const void* gg_pv,
     int ld_ggpv, const void* gg_cut, const void* gg_unit, void* d_grad_x, void* d_grad_vec,
     void* d_q, void* d_k, void* d_v, void* d_vec, void* d_pk, void* d_pv, void* d_cut,
-    void* d_unit, void* stream) {
+    void* d_unit, int flags, void* stream) {
   hipStream_t st = (hipStream_t)stream;
 #define TMD_BWD2(T)                                                                              \
   return et::bwd2<T>(n_nodes, hidden, heads, row_ptr, src, max_pairs, q, ld_q, k, ld_k, v, ld_v, \
                      vec_in, pk, ld_pk, pv, ld_pv, cutoff, unit, grad_x, grad_vec, gg_q, gg_k,   \
                      gg_v, gg_vec, gg_pk, ld_ggpk, gg_pv, ld_ggpv, gg_cut, gg_unit, d_grad_x,    \
-                     d_grad_vec, d_q, d_k, d_v, d_vec, d_pk, d_pv, d_cut, d_unit, st)
+                     d_grad_vec, d_q, d_k, d_v, d_vec, d_pk, d_pv, d_cut, d_unit, flags, st)
   if (dtype == TMDNET_F32) TMD_BWD2(float);
   if (dtype == TMDNET_F64) TMD_BWD2(double);
 #undef TMD_BWD2

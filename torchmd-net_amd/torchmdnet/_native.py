@@ -16,6 +16,7 @@ F32, F64 = 0, 1
 NL_BRUTE, NL_SHARED, NL_CELL = 0, 1, 2
 RBF_EXPNORM, RBF_GAUSS = 0, 1
 ACC_VEC_RESIDUAL, ACC_EDGE = 1, 2
+ET_V_PLANAR = 4
 
 _STATUS = {1: "bad argument", 2: "unsupported configuration", 3: "kernel launch failed",
            4: "workspace too small"}
@@ -32,11 +33,11 @@ SIGNATURES = {
     "tmdnet_nl_backward": (I, [I, I, P, P, I, P, P, P, P, P, P]),
     "tmdnet_edge_geom_fwd": (I, [I, I, I, I, P, P, P, P, P, P, D, D, P, P, P, P]),
     "tmdnet_edge_geom_bwd": (I, [I, I, I, I, P, P, P, P, P, P, D, D, P, P, P, P, P, P]),
-    "tmdnet_et_message_fwd": (I, [I, I, I, I, P, P, I, P, I, P, I, P, I, P, P, I, P, I, P, P, P, P, P, P]),
+    "tmdnet_et_message_fwd": (I, [I, I, I, I, P, P, I, P, I, P, I, P, I, P, P, I, P, I, P, P, P, P, I, P, P]),
     "tmdnet_et_message_bwd": (I, [I, I, I, I, P, P, I, P, I, P, I, P, I, P, P, I, P, I, P, P, P, P,
                                   P, P, P, P, P, P, P, P, I, P, P]),
     "tmdnet_et_message_bwd2": (I, [I, I, I, I, P, P, I, P, I, P, I, P, I, P, P, I, P, I, P, P, P, P,
-                                   P, P, P, P, P, I, P, I, P, P, P, P, P, P, P, P, P, P, P, P, P]),
+                                   P, P, P, P, P, I, P, I, P, P, P, P, P, P, P, P, P, P, P, P, I, P]),
     "tmdnet_et_epilogue_fwd": (I, [I, I, I, P, P, P, P, P, P, P, P]),
     "tmdnet_et_epilogue_bwd": (I, [I, I, I, P, P, P, P, P, P, P]),
     "tmdnet_nbr_embed_fwd": (I, [I, I, I, P, P, I, P, I, P, I, P, P, P]),

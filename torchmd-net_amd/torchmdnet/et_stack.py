@@ -71,19 +71,6 @@ class LayerWeights:
     def __init__(self, layer):
         self.layer = layer
         self.bufs = {}
-        self._acc = None  # (param ids, AccumulateGrad nodes) cache
-
-    def acc_nodes(self, params):
-        """AccumulateGrad nodes of ``params`` (the layer's), cached.  Holding them keeps the
-        parameters' accumulators alive, so they only change when a parameter is replaced or moved
-        (``.to()`` resets the accumulator); one lookup per call detects both."""
-        key = tuple((id(p), p.requires_grad) for p in params)
-        i = next(i for i, p in enumerate(params) if p.requires_grad)
-        node = params[i].view_as(params[i]).grad_fn.next_functions[0][0]
-        if self._acc is None or self._acc[0] != key or self._acc[1][i] is not node:
-            self._acc = (key, [p.view_as(p).grad_fn.next_functions[0][0] if p.requires_grad else None
-                               for p in params])
-        return self._acc[1]
 
     def _get(self, name, params):
         buf = self.bufs.get(name)
@@ -125,6 +112,40 @@ class StackWeights:
 
 # Batch every layer's dk/dv projection into one GEMM while its output (E x L*D fp32) stays below this.
 BATCH_DKV_BYTES = 2 << 30
+# From this many edges on, v / dv rows are produced in the planar layout [x | v1 | v2] (H-blocks,
+# TMDNET_ET_V_PLANAR) by permuting the weight rows once per forward: contiguous row segments for the
+# edge kernels' 16-byte loads (+4-7 % on the C5 forward); below it the two small gathers are not worth it.
+PLANAR_MIN_EDGES = 131072
+
+_PERMS = {}
+
+
+def _v_perm(H, heads, device):
+    """Row j of the planar [x | v1 | v2] block = row perm[j] of the reference per-head interleave
+    [h][x|v1|v2] (torchmd_et.py:282-291, 299-303)."""
+    key = ("v", H, heads, str(device))
+    if key not in _PERMS:
+        d = H // heads
+        j = torch.arange(3 * H)
+        part, rem = j // H, j % H
+        _PERMS[key] = (rem // d * 3 * d + part * d + rem % d).to(device)
+    return _PERMS[key]
+
+
+def _planar_perms(meta, device):
+    """(qkv row perm, its inverse, all-layer dk/dv row perm, its inverse) for the planar layout."""
+    key = ("stack", meta.H, meta.heads, meta.n_layers, meta.hk, meta.hv, str(device))
+    if key not in _PERMS:
+        H = meta.H
+        vp = _v_perm(H, meta.heads, device)
+        qkv = torch.cat([torch.arange(2 * H, device=device), 2 * H + vp])
+        per = ([torch.arange(H, device=device)] if meta.hk else []) + \
+            ([H * int(meta.hk) + vp] if meta.hv else [])
+        one = torch.cat(per) if per else torch.zeros(0, dtype=torch.long, device=device)
+        dkv = torch.cat([l * meta.D + one for l in range(meta.n_layers)])
+        inv = lambda p: torch.empty_like(p).scatter_(0, p, torch.arange(p.numel(), device=device))  # noqa
+        _PERMS[key] = (qkv, inv(qkv), dkv, inv(dkv), one, inv(one))
+    return _PERMS[key]
 
 
 def layer_params(layer):
@@ -142,7 +163,7 @@ def layer_params(layer):
 class _Meta:
     """Non-tensor context of one stack call."""
 
-    def __init__(self, graph, heads, H, hk, hv, n_layers, fused, acc_nodes, dkv_w=None, dkv_b=None,
+    def __init__(self, graph, heads, H, hk, hv, n_layers, fused, acc_nodes=None, dkv_w=None, dkv_b=None,
                  batched=False):
         self.graph = graph
         self.heads = heads
@@ -154,17 +175,32 @@ class _Meta:
         self.D = (int(hk) + 3 * int(hv)) * H  # dk/dv rows per layer
         self.dkv_w, self.dkv_b = dkv_w, dkv_b  # all layers' [dk; dv] (StackWeights)
         self.batched = batched  # one GEMM for every layer's projection
-        self.acc_nodes = acc_nodes  # per layer: AccumulateGrad nodes of its parameters (or None)
+        self.planar = False     # TMDNET_ET_V_PLANAR row layout for v / dv (set by et_stack)
+        self.flags = 0
+        self.qkv_eff = fused    # the weights the GEMMs use (row-permuted copies when planar)
+        self.dkv_eff = (dkv_w, dkv_b)
         self.np = 11 + 2 * int(hk) + 2 * int(hv)  # parameters per layer
 
     def split(self, params):
         return [params[i * self.np:(i + 1) * self.np] for i in range(self.n_layers)]
 
     def dkv_layer(self, l):
-        if self.dkv_w is None:
+        w, b_ = self.dkv_eff
+        if w is None:
             return None, None
         a, b = l * self.D, (l + 1) * self.D
-        return self.dkv_w[a:b], self.dkv_b[a:b]
+        return w[a:b], b_[a:b]
+
+    def refresh_effective(self):
+        """Row-permuted copies of the stacked weights for the planar layout (once per forward, so
+        in-place parameter updates are always seen; two small gathers per layer)."""
+        if not self.planar:
+            self.qkv_eff, self.dkv_eff = self.fused, (self.dkv_w, self.dkv_b)
+            return
+        qp, _, dp, _, _, _ = self.perms
+        self.qkv_eff = [(w.index_select(0, qp), b.index_select(0, qp)) for w, b in self.fused]
+        self.dkv_eff = (self.dkv_w.index_select(0, dp), self.dkv_b.index_select(0, dp)) \
+            if self.dkv_w is not None else (None, None)
 
 
 def _epilogue_fwd(x, vec, vecp, o, veca):
@@ -195,11 +231,12 @@ def _forward_layers(meta, x, f, C, u, params):
     vec = None
     acts = []
     D = meta.D
-    pkv_all = torch.addmm(meta.dkv_b, f, meta.dkv_w.t()) if (meta.batched and D) else None
+    meta.refresh_effective()
+    pkv_all = torch.addmm(meta.dkv_eff[1], f, meta.dkv_eff[0].t()) if (meta.batched and D) else None
     for l, p in enumerate(meta.split(params)):
         ln_w, ln_b = p[0], p[1]
         vec_w, o_w, o_b = p[8], p[9], p[10]
-        qkv_w, qkv_b = meta.fused[l]
+        qkv_w, qkv_b = meta.qkv_eff[l]
         dkv_w, dkv_b = meta.dkv_layer(l)
         xn, mean, rstd = torch.native_layer_norm(x, [H], ln_w, ln_b, _EPS)
         qkv = torch.addmm(qkv_b, xn, qkv_w.t())
@@ -213,7 +250,7 @@ def _forward_layers(meta, x, f, C, u, params):
         xa = torch.empty((N, H), dtype=x.dtype, device=x.device)
         veca = torch.empty((N, 3, H), dtype=x.dtype, device=x.device)
         kernels.et_message_fwd_launch(qkv[:, :H], qkv[:, H:2 * H], qkv[:, 2 * H:], vec, pk, pv, C, u,
-                                      meta.graph, meta.heads, xa, veca)
+                                      meta.graph, meta.heads, xa, veca, meta.flags)
         o = torch.addmm(o_b, xa, o_w.t())
         x_new, vec_new = _epilogue_fwd(x, vec, vecp, o, veca)
         acts.append((x, vec, xn, mean, rstd, qkv, vecp, pkv, xa, o))
@@ -247,7 +284,7 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws):
         x, vec, xn, mean, rstd, qkv, vecp, pkv, xa, o_ = acts[l]
         ln_w, ln_b = p[0], p[1]
         vec_w, o_w = p[8], p[9]
-        qkv_w, _ = meta.fused[l]
+        qkv_w, _ = meta.qkv_eff[l]
         dkv_w, _ = meta.dkv_layer(l)
         if has_e:
             g_pkv = g_pkv_all[:, l * D:(l + 1) * D] if meta.batched else g_pkv_all
@@ -261,7 +298,7 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws):
         kernels.et_message_bwd_launch(
             qkv[:, :H], qkv[:, H:2 * H], qkv[:, 2 * H:], vec, pk, pv, C, u, graph, meta.heads, g_xa, gV,
             g_qkv[:, :H], g_qkv[:, H:2 * H], g_qkv[:, 2 * H:], g_vec_in, gpk, gpv, g_C, g_u,
-            accumulate=nat.ACC_VEC_RESIDUAL | nat.ACC_EDGE)
+            accumulate=nat.ACC_VEC_RESIDUAL | nat.ACC_EDGE | meta.flags)
         if has_e and not meta.batched:
             if g_f is None:
                 g_f = torch.mm(g_pkv, dkv_w)
@@ -278,21 +315,31 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws):
             base = l * meta.np
             g_qkv_w = torch.mm(g_qkv.t(), xn)
             g_qkv_b = g_qkv.sum(0)
+            if meta.planar:  # back to the parameters' (reference) row order
+                qinv = meta.perms[1]
+                g_qkv_w, g_qkv_b = g_qkv_w.index_select(0, qinv), g_qkv_b.index_select(0, qinv)
             gp = [g_lnw, g_lnb, g_qkv_w[:H], g_qkv_b[:H], g_qkv_w[H:2 * H], g_qkv_b[H:2 * H],
                   g_qkv_w[2 * H:], g_qkv_b[2 * H:],
                   (torch.mm(g_vecp.view(3 * N, 3 * H).t(), vec.view(3 * N, H)) if vec is not None
                    else torch.zeros((3 * H, H), **o)),
                   torch.mm(g_o.t(), xa), g_o.sum(0)]
             if has_e and not meta.batched:
-                gp += _dkv_param_grads(meta, torch.mm(g_pkv.t(), f), g_pkv.sum(0))
+                g_w, g_b = torch.mm(g_pkv.t(), f), g_pkv.sum(0)
+                if meta.planar:
+                    oinv = meta.perms[5]
+                    g_w, g_b = g_w.index_select(0, oinv), g_b.index_select(0, oinv)
+                gp += _dkv_param_grads(meta, g_w, g_b)
             g_params[base:base + len(gp)] = gp  # batched mode: dk/dv grads filled after the loop
         gX = g_x
         gV = g_vec_in
     if has_e and meta.batched:  # every layer's edge-feature / projection gradients in one GEMM each
-        g_f = torch.mm(g_pkv_all, meta.dkv_w)
+        g_f = torch.mm(g_pkv_all, meta.dkv_eff[0])
         if any(need_ws):
             g_w_all = torch.mm(g_pkv_all.t(), f)
             g_b_all = g_pkv_all.sum(0)
+            if meta.planar:
+                dinv = meta.perms[3]
+                g_w_all, g_b_all = g_w_all.index_select(0, dinv), g_b_all.index_select(0, dinv)
             for l in range(meta.n_layers):
                 if need_ws[l]:
                     base = l * meta.np + 11
@@ -323,15 +370,25 @@ def composite_stack(meta, x, f, C, u, params, message=None):
     src, dst = graph.src.long(), graph.dst.long()
     N = x.shape[0]
     vec = torch.zeros((N, 3, H), dtype=x.dtype, device=x.device)
-    for p in meta.split(params):
+    layers = meta.split(params)
+    D = meta.D
+    # every layer's dk/dv projection as ONE GEMM (differentiable cat of the parameters): one
+    # weight-gradient GEMM over the E rows instead of one per layer and projection
+    pkv_all = None
+    if D:
+        rest = [p[11:] for p in layers]
+        w_all = torch.cat([w for r in rest for w in r[0::2]], 0)
+        b_all = torch.cat([b for r in rest for b in r[1::2]], 0)
+        pkv_all = F.linear(f, w_all, b_all)
+    for l, p in enumerate(layers):
         ln_w, ln_b, q_w, q_b, k_w, k_b, v_w, v_b, vec_w, o_w, o_b = p[:11]
-        rest = list(p[11:])
         xn = F.layer_norm(x, (H,), ln_w, ln_b, _EPS)
         q, k, v = F.linear(xn, q_w, q_b), F.linear(xn, k_w, k_b), F.linear(xn, v_w, v_b)
         vec1, vec2, vec3 = torch.split(F.linear(vec, vec_w), H, dim=-1)
         vec_dot = (vec1 * vec2).sum(dim=1)
-        pk = F.linear(f, rest.pop(0), rest.pop(0)) if meta.hk else None
-        pv = F.linear(f, rest.pop(0), rest.pop(0)) if meta.hv else None
+        pkv = pkv_all[:, l * D:(l + 1) * D] if D else None
+        pk = pkv[:, :H] if meta.hk else None
+        pv = pkv[:, H * int(meta.hk):] if meta.hv else None
         if message is None:
             xa, veca = kernels.et_message_composite(q, k, v, vec, pk, pv, C, u, src, dst, N, meta.heads)
         else:
@@ -364,7 +421,14 @@ class _ETStack(Function):
     def backward(ctx, gX, gV):
         x, f, C, u, *params = ctx.saved_tensors
         meta = ctx.meta
-        need_w = tuple(nodes is not None and any(_will_run(n) for n in nodes) for nodes in meta.acc_nodes)
+        # which layers' weight gradients does THIS backward deliver?  The parameters' AccumulateGrad
+        # nodes are this node's own last next edges; nothing is cached across
+        # iterations -- an AccumulateGrad node kept alive from an earlier step stays bound to the
+        # stream it was created on and breaks HIP-graph capture of later steps.
+        nf = ctx.next_functions  # one entry per tensor argument (a None edge-feature input has none)
+        off = len(nf) - len(params)
+        need_w = tuple(any(_will_run(nf[off + l * meta.np + j][0]) for j in range(meta.np))
+                       for l in range(meta.n_layers))
         if gX is None:
             gX = torch.zeros_like(x)
         if gV is None:
@@ -426,8 +490,7 @@ def et_stack(layers, x, graph, f, C, u):
     l0 = layers[0]
     H, heads = l0.hidden_channels, l0.num_heads
     hk, hv = l0.dk_proj is not None, l0.dv_proj is not None
-    fused, params, acc = [], [], []
-    grad_on = torch.is_grad_enabled()
+    fused, params = [], []
     sw = getattr(layers, "_tmd_stack", None)
     if sw is None or sw.layers is not layers:
         sw = StackWeights(layers)
@@ -438,13 +501,13 @@ def et_stack(layers, x, graph, f, C, u):
         if layer._stacked is None:
             layer._stacked = LayerWeights(layer)
         fused.append(layer._stacked.fused())
-        lp = layer_params(layer)
-        params += lp
-        acc.append(layer._stacked.acc_nodes(lp) if (grad_on and any(p.requires_grad for p in lp))
-                   else None)
+        params += layer_params(layer)
     D = (int(hk) + 3 * int(hv)) * H
     batched = D > 0 and graph.n_edges * len(layers) * D * x.element_size() <= BATCH_DKV_BYTES
-    meta = _Meta(graph, heads, H, hk, hv, len(layers), fused, acc, dkv_w, dkv_b, batched)
+    meta = _Meta(graph, heads, H, hk, hv, len(layers), fused, None, dkv_w, dkv_b, batched)
+    if graph.n_edges >= PLANAR_MIN_EDGES:
+        meta.planar, meta.flags = True, nat.ET_V_PLANAR
+        meta.perms = _planar_perms(meta, x.device)
     x = x.contiguous()
     f = f.contiguous() if (hk or hv) else None
     return _ETStack.apply(meta, x, f, C.contiguous(), u.contiguous(), *params)

@@ -61,7 +61,7 @@ class GraphedEnergyForces:
             self.y, self.neg_dy = model(self.z, self.pos, self.batch)
         torch.cuda.synchronize(dev)
         # device flag written by every replay (lives in the graph's memory pool)
-        self.overflow = rep.distance.last_graph.overflow
+        self.overflow = rep.distance.last_overflow
         self.dists = dists
 
     def __call__(self, pos=None):

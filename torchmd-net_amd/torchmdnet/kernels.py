@@ -384,8 +384,8 @@ def rows_like(t, alloc=torch.empty):
     return alloc((t.shape[0], t.stride(0)), dtype=t.dtype, device=t.device)[:, :t.shape[1]]
 
 
-def et_message_fwd_launch(q, k, v, vec, pk, pv, C, u, graph, heads, xo, vo):
-    """One ``tmdnet_et_message_fwd`` launch (vec may be None: vec == 0)."""
+def et_message_fwd_launch(q, k, v, vec, pk, pv, C, u, graph, heads, xo, vo, flags=0):
+    """One ``tmdnet_et_message_fwd`` launch (vec may be None: vec == 0; flags: nat.ET_V_PLANAR)."""
     lib = nat.load()
     N, H = q.shape
     probe = EVENT_PROBE
@@ -396,7 +396,7 @@ def et_message_fwd_launch(q, k, v, vec, pk, pv, C, u, graph, heads, xo, vo):
                                    nat.ptr(graph.src), graph.n_edges, nat.ptr(q), _ld(q), nat.ptr(k),
                                    _ld(k), nat.ptr(v), _ld(v), nat.ptr(vec), nat.ptr(pk), _ld(pk),
                                    nat.ptr(pv), _ld(pv), nat.ptr(C), nat.ptr(u), nat.ptr(xo),
-                                   nat.ptr(vo), None, nat.stream(q.device))
+                                   nat.ptr(vo), int(flags), None, nat.stream(q.device))
     nat.check(rc, "tmdnet_et_message_fwd")
     if probe is not None:
         ev1.record()
@@ -564,7 +564,7 @@ def et_message_bwd2(ctx, ggs):
         nat.ptr(C), nat.ptr(u), nat.ptr(gx), nat.ptr(gvec), nat.ptr(ggq), nat.ptr(ggk), nat.ptr(ggv),
         nat.ptr(ggw), nat.ptr(ggpk), H, nat.ptr(ggpv), 3 * H, nat.ptr(ggC), nat.ptr(ggu), nat.ptr(d_gx),
         nat.ptr(d_gvec), nat.ptr(d_q), nat.ptr(d_k), nat.ptr(d_v), nat.ptr(d_vec), nat.ptr(d_pk),
-        nat.ptr(d_pv), nat.ptr(d_C), nat.ptr(d_u), nat.stream(q.device))
+        nat.ptr(d_pv), nat.ptr(d_C), nat.ptr(d_u), 0, nat.stream(q.device))
     nat.check(rc, "tmdnet_et_message_bwd2")
     return (d_gx, d_gvec, d_q, d_k, d_v, d_vec, d_pk, d_pv, d_C, d_u, None, None)
 

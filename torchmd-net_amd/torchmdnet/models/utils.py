@@ -239,7 +239,11 @@ class OptimizedDistance(torch.nn.Module):
                                 self._max_pairs(pos.shape[0]), loop=self.loop, strategy=strategy,
                                 box=box, check_errors=self.check_errors,
                                 static_capacity=self.static_capacity)
-        self.last_graph = g
+        # keep only the device-side status of the last build (static-capacity overflow flag, pair
+        # count): holding the graph itself would keep its autograd history -- and the positions'
+        # AccumulateGrad node -- alive across steps, which breaks HIP-graph capture of later steps
+        self.last_overflow = getattr(g, "overflow", None)
+        self.last_num_pairs = g.num_pairs_dev if g.num_pairs_dev is not None else g.num_pairs
         return g
 
 

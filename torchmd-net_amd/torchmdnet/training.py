@@ -70,10 +70,16 @@ class LNNPStep:
             loss = loss + self.neg_dy_weight * F.mse_loss(pred_neg_dy, neg_dy)
         return loss
 
+    def backward(self, loss):
+        # gradients of the parameters only: the positions are a leaf too (forces need them), but
+        # accumulating a position gradient nobody reads is wasted work -- and under HIP-graph
+        # capture the positions' AccumulateGrad would run across streams
+        loss.backward(inputs=self.reduce.params)
+
     def step(self, z, pos, batch, y, neg_dy):
         self.opt.zero_grad(set_to_none=False)
         loss = self.loss(z, pos, batch, y, neg_dy)
-        loss.backward()
+        self.backward(loss)
         self.reduce()
         if self.lr_warmup_steps and self.global_step < self.lr_warmup_steps:
             scale = min(1.0, float(self.global_step + 1) / float(self.lr_warmup_steps))
@@ -82,3 +88,87 @@ class LNNPStep:
         self.opt.step()
         self.global_step += 1
         return loss.detach()
+
+
+class GraphedTrainStep(LNNPStep):
+    """LNNPStep with the forward, the force pass and the whole (double) backward captured in ONE
+    HIP graph for a fixed batch layout (same z / batch / label shapes every step, e.g. a padded or
+    fixed-size loader).  Per step: copy the inputs in, replay, then the fused RCCL all-reduce and
+    AdamW run eagerly (the collective stays outside the graph).  The neighbour list runs in its
+    static-capacity mode (capacity = margin x the warm-up pair count, device overflow flag checked by
+    ``check_capacity``); the molecule count of ``reduce`` is frozen from warm-up as in inference
+    capture (reference output_modules.py:27-43).  Replaces ~3k autograd-issued launches per step.
+
+    Drop every reference to an earlier loss / autograd graph of this model before constructing it:
+    a live graph keeps the parameters' AccumulateGrad nodes (bound to the stream they were created
+    on) alive, and a capture that reaches them across streams is invalid."""
+
+    def __init__(self, model, z, pos, batch, y, neg_dy, margin=1.25, warmup=3, **kw):
+        import math
+        super().__init__(model, **kw)
+        from .graphs import _distance_modules
+        self.z, self.batch = z.clone(), batch.clone()
+        self.pos = pos.detach().clone()
+        self.y = y.detach().clone()
+        self.neg_dy = neg_dy.detach().clone()
+        dev = pos.device
+        rep = model.representation_model
+        # eager warm-up on a CLONE of the positions (sizes the edge capacity, freezes the molecule
+        # count of reduce): the captured positions' AccumulateGrad must not be created on the
+        # default stream before the capture
+        self.opt.zero_grad(set_to_none=True)
+        self.backward(self.loss(self.z, self.pos.clone(), self.batch, self.y, self.neg_dy))
+        g = rep.distance.graph(self.pos.clone(), self.batch)
+        self.edge_capacity = int(math.ceil(g.num_pairs * margin / 256.0) * 256)
+        del g
+        self.dists = _distance_modules(model)
+        for d in self.dists:
+            d.static_capacity = self.edge_capacity
+        try:
+            torch.autograd.graph.set_warn_on_accumulate_grad_stream_mismatch(False)
+        except AttributeError:
+            pass
+        s = torch.cuda.Stream(device=dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                self.opt.zero_grad(set_to_none=True)
+                self.backward(self.loss(self.z, self.pos, self.batch, self.y, self.neg_dy))
+        torch.cuda.current_stream(dev).wait_stream(s)
+        torch.cuda.synchronize(dev)
+        # the parameter gradients are graph OUTPUTS (autograd.grad, as make_graphed_callables does):
+        # no AccumulateGrad node runs inside the capture; after each replay .grad points at them
+        self.opt.zero_grad(set_to_none=True)
+        params = self.reduce.params
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.static_loss = self.loss(self.z, self.pos, self.batch, self.y, self.neg_dy)
+            grads = torch.autograd.grad(self.static_loss, params, allow_unused=True)
+        torch.cuda.synchronize(dev)
+        self.static_grads = [torch.zeros_like(p) if g is None else g for p, g in zip(params, grads)]
+        self.overflow = rep.distance.last_overflow
+
+    def step(self, z=None, pos=None, batch=None, y=None, neg_dy=None):
+        with torch.no_grad():
+            for dst, src in ((self.pos, pos), (self.y, y), (self.neg_dy, neg_dy)):
+                if src is not None:
+                    dst.copy_(src)
+        self.graph.replay()
+        for p, g in zip(self.reduce.params, self.static_grads):
+            p.grad = g
+        self.reduce()
+        if self.lr_warmup_steps and self.global_step < self.lr_warmup_steps:
+            scale = min(1.0, float(self.global_step + 1) / float(self.lr_warmup_steps))
+            for g in self.opt.param_groups:
+                g["lr"] = scale * self.lr
+        self.opt.step()
+        self.global_step += 1
+        return self.static_loss.detach()
+
+    def check_capacity(self):
+        if bool(self.overflow.item()):
+            raise RuntimeError(f"neighbour pairs exceed the captured edge capacity {self.edge_capacity}")
+
+    def release(self):
+        for d in self.dists:
+            d.static_capacity = None
