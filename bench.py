@@ -85,9 +85,15 @@ def et_args(channels):
 
 
 def setup_dist():
+    """One process per GPU (torchrun), RCCL.  TMDNET_BENCH_REHEARSAL=1 (testing only) runs every
+    rank on cuda:0 over gloo, to rehearse the multi-rank code path on a one-GPU machine."""
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if ws > 1 and os.environ.get("TMDNET_BENCH_REHEARSAL") == "1":
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo")
+        return ws, rank, torch.device("cuda", 0)
     if ws > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
