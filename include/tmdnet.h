@@ -64,6 +64,19 @@ int tmdnet_nl_backward(int dtype, int n_atoms, const int32_t* row_ptr, const int
                        int max_pairs, const void* grad_deltas, const void* grad_distances,
                        const void* deltas, const void* distances, void* grad_pos, void* stream);
 
+/* Second order of tmdnet_nl_backward (the double backward the reference gets by differentiating
+ * NeighborAutograd::backward's index_add pair, neighbors_cuda.cu:43-71).  gg_pos [n][3] is the
+ * cotangent of grad_pos.  Per edge e = (src -> dst) with w = gg[src]-gg[dst], u = delta/r:
+ *   d_grad_deltas[e] = w,  d_grad_distances[e] = u.w  (0 when r == 0),
+ *   d_pos[n] = sum_{e in row n} h[T[e]] - h[e],  h[e] = grad_distances[e]/r (w - u (u.w)).
+ * grad_distances NULL = zero (d_pos = 0).  d_grad_deltas / d_grad_distances may be NULL (not
+ * computed); when given, all max_pairs rows are written (padding slots 0).  Same list
+ * requirements as tmdnet_nl_backward. */
+int tmdnet_nl_backward2(int dtype, int n_atoms, const int32_t* row_ptr, const int32_t* src,
+                        const int32_t* transpose_map, int max_pairs, const void* grad_distances,
+                        const void* deltas, const void* distances, const void* gg_pos, void* d_pos,
+                        void* d_grad_deltas, void* d_grad_distances, void* stream);
+
 /* ------------------------------------------------------------------------------------------
  * Edge geometry: radial basis + cosine cutoff + unit vectors, fused.  Replaces
  *   ExpNormalSmearing.forward / GaussianSmearing.forward (reference models/utils.py:339-344,

@@ -146,6 +146,49 @@ def test_neighbor_grads_match_oracle(dtype, box):
     assert _rel(gp.cpu(), gref) < tol
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+@pytest.mark.parametrize("box", [None, "tric"])
+def test_neighbor_second_and_third_order_match_oracle(dtype, box):
+    """Double backward (HIP tmdnet_nl_backward2) and third order (its composite backward) of the
+    neighbour op vs plain autograd on the CPU over the same pairs (reference: the CUDA op's
+    backward is differentiable, neighbors_cuda.cu:43-71)."""
+    from torchmdnet.models.utils import OptimizedDistance
+    torch.manual_seed(97)
+    n, lbox = 90, 7.0
+    pos = (torch.rand(n, 3, dtype=dtype) * lbox).to(DEV).requires_grad_(True)
+    batch = torch.repeat_interleave(torch.arange(2), torch.tensor([40, 50])).to(DEV)
+    boxt = None if box is None else torch.tensor([[lbox, 0, 0], [0.1, lbox, 0], [0.3, 0.2, lbox]], dtype=dtype)
+    nl = OptimizedDistance(cutoff_upper=3.0, max_num_pairs=-64, loop=True, return_vecs=True, box=boxt)
+    ei, ew, ev = nl(pos, batch)
+    w = torch.randn(ew.shape[0], dtype=dtype, device=DEV).requires_grad_(True)
+    wv = torch.randn(ev.shape[0], 3, dtype=dtype, device=DEV).requires_grad_(True)
+    c = torch.randn(n, 3, dtype=dtype, device=DEV)
+    (gp,) = torch.autograd.grad((ew.pow(2) * w).sum() + (ev * wv).sum(), pos, create_graph=True)
+    l2 = (gp * c).sum() + gp.pow(2).sum()
+    g2 = torch.autograd.grad(l2, (pos, w, wv), create_graph=True)
+    l3 = sum((g * torch.ones_like(g)).sum() for g in g2) + g2[0].pow(2).sum()
+    g3 = torch.autograd.grad(l3, (pos, w, wv))
+    # oracle on the CPU, fp64
+    p64 = pos.detach().cpu().double().requires_grad_(True)
+    w64 = w.detach().cpu().double().requires_grad_(True)
+    wv64 = wv.detach().cpu().double().requires_grad_(True)
+    nb = ei.cpu()
+    shift = (ev.detach().cpu().double() - (p64[nb[0]] - p64[nb[1]])).detach()
+    dl = p64[nb[0]] - p64[nb[1]] + shift
+    selfe = nb[0] == nb[1]
+    r = torch.where(selfe, torch.zeros(len(selfe), dtype=torch.float64),
+                    torch.where(selfe, torch.ones(len(selfe), dtype=torch.float64), (dl * dl).sum(1)).sqrt())
+    (gq,) = torch.autograd.grad((r.pow(2) * w64).sum() + (dl * wv64).sum(), p64, create_graph=True)
+    c64 = c.cpu().double()
+    m2 = (gq * c64).sum() + gq.pow(2).sum()
+    q2 = torch.autograd.grad(m2, (p64, w64, wv64), create_graph=True)
+    m3 = sum((g * torch.ones_like(g)).sum() for g in q2) + q2[0].pow(2).sum()
+    q3 = torch.autograd.grad(m3, (p64, w64, wv64))
+    tol = 1e-4 if dtype == torch.float32 else 1e-9
+    for a, b in zip(g2 + g3, q2 + q3):
+        assert _rel(a.detach().cpu(), b.detach()) < tol
+
+
 def test_csr_graph_invariants():
     from torchmdnet import kernels
     z, pos, batch = O.qm9_like(8)

@@ -359,6 +359,63 @@ __global__ void k_nl_backward(int n, const int* __restrict__ row_ptr, const int3
   gpos[3 * t + 2] = acc.z;
 }
 
+// Second order of k_nl_backward (the double backward of NeighborAutograd's index_add pair,
+// reference neighbors_cuda.cu:25-89, which the reference differentiates through autograd).  With
+// gg = cotangent of gpos and, per edge e = (s -> t), w = gg[s] - gg[t], u = dl/r:
+//   d_gd[e] = w,   d_gr[e] = u.w,   d_dl[e] = gr/r (w - u (u.w))      (all 0 when r == 0)
+//   d_pos[n] = sum_{e in row n} d_dl[T(e)] - d_dl[e]        (the scatter of k_nl_backward)
+// T(e) = (t -> s) sees w(T(e)) = -w(e), so one gather of gg per edge serves both directions.
+template <typename T>
+__device__ __forceinline__ V3<T> edge_grad2(int e, V3<T> w, const T* gr, const T* dl, const T* r,
+                                            T& uw) {
+  const T re = r[e];
+  if (re == T(0)) {
+    uw = T(0);
+    return {T(0), T(0), T(0)};
+  }
+  const T inv = T(1) / re;
+  const V3<T> u{dl[3 * e + 0] * inv, dl[3 * e + 1] * inv, dl[3 * e + 2] * inv};
+  uw = u.x * w.x + u.y * w.y + u.z * w.z;
+  const T c = gr ? gr[e] * inv : T(0);
+  return {c * (w.x - u.x * uw), c * (w.y - u.y * uw), c * (w.z - u.z * uw)};
+}
+
+template <typename T>
+__global__ void k_nl_backward2(int n, const int* __restrict__ row_ptr, const int32_t* __restrict__ src,
+                               const int32_t* __restrict__ tr, int cap, const T* __restrict__ gr,
+                               const T* __restrict__ dl, const T* __restrict__ r,
+                               const T* __restrict__ gg, T* __restrict__ dpos, T* __restrict__ dgd,
+                               T* __restrict__ dgr) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const int b = min(row_ptr[t], cap), e = min(row_ptr[t + 1], cap);
+  const V3<T> gt{gg[3 * t + 0], gg[3 * t + 1], gg[3 * t + 2]};
+  V3<T> acc{T(0), T(0), T(0)};
+  for (int k = b; k < e; ++k) {
+    const int s = src[k];
+    const V3<T> w{gg[3 * s + 0] - gt.x, gg[3 * s + 1] - gt.y, gg[3 * s + 2] - gt.z};
+    T uw;
+    const V3<T> dm = edge_grad2(k, w, gr, dl, r, uw);
+    acc.x -= dm.x; acc.y -= dm.y; acc.z -= dm.z;
+    if (dgd) {
+      const bool live = r[k] != T(0);
+      dgd[3 * k + 0] = live ? w.x : T(0);
+      dgd[3 * k + 1] = live ? w.y : T(0);
+      dgd[3 * k + 2] = live ? w.z : T(0);
+    }
+    if (dgr) dgr[k] = uw;
+    const int k2 = tr[k];
+    if (k2 >= 0) {
+      T uw2;
+      const V3<T> dp = edge_grad2(k2, V3<T>{-w.x, -w.y, -w.z}, gr, dl, r, uw2);
+      acc.x += dp.x; acc.y += dp.y; acc.z += dp.z;
+    }
+  }
+  dpos[3 * t + 0] = acc.x;
+  dpos[3 * t + 1] = acc.y;
+  dpos[3 * t + 2] = acc.z;
+}
+
 // ---------------------------------------------------------------- host side
 #define TMD_CHECK(x)                               \
   do {                                             \
@@ -545,6 +602,35 @@ extern "C" int tmdnet_nl_backward(int dtype, int n_atoms, const int32_t* row_ptr
     hipLaunchKernelGGL(nl::k_nl_backward<double>, g, dim3(tb), 0, st, n_atoms, row_ptr, transpose_map,
                        max_pairs, (const double*)grad_deltas, (const double*)grad_distances,
                        (const double*)deltas, (const double*)distances, (double*)grad_pos);
+  else
+    return kUnsupported;
+  return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
+}
+
+extern "C" int tmdnet_nl_backward2(int dtype, int n_atoms, const int32_t* row_ptr, const int32_t* src,
+                                   const int32_t* transpose_map, int max_pairs,
+                                   const void* grad_distances, const void* deltas,
+                                   const void* distances, const void* gg_pos, void* d_pos,
+                                   void* d_grad_deltas, void* d_grad_distances, void* stream) {
+  if (n_atoms <= 0 || max_pairs < 0 || !row_ptr || !src || !transpose_map || !gg_pos || !d_pos)
+    return kBadArgument;
+  hipStream_t st = (hipStream_t)stream;
+  const size_t es = dtype == TMDNET_F64 ? 8 : 4;
+  // padding slots belong to no CSR row: their gradients are zero
+  if (d_grad_deltas) TMD_CHECK(hipMemsetAsync(d_grad_deltas, 0, es * 3 * (size_t)max_pairs, st));
+  if (d_grad_distances) TMD_CHECK(hipMemsetAsync(d_grad_distances, 0, es * (size_t)max_pairs, st));
+  const int tb = 256;
+  dim3 g((n_atoms + tb - 1) / tb);
+  if (dtype == TMDNET_F32)
+    hipLaunchKernelGGL(nl::k_nl_backward2<float>, g, dim3(tb), 0, st, n_atoms, row_ptr, src, transpose_map,
+                       max_pairs, (const float*)grad_distances, (const float*)deltas,
+                       (const float*)distances, (const float*)gg_pos, (float*)d_pos,
+                       (float*)d_grad_deltas, (float*)d_grad_distances);
+  else if (dtype == TMDNET_F64)
+    hipLaunchKernelGGL(nl::k_nl_backward2<double>, g, dim3(tb), 0, st, n_atoms, row_ptr, src, transpose_map,
+                       max_pairs, (const double*)grad_distances, (const double*)deltas,
+                       (const double*)distances, (const double*)gg_pos, (double*)d_pos,
+                       (double*)d_grad_deltas, (double*)d_grad_distances);
   else
     return kUnsupported;
   return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;

@@ -31,6 +31,7 @@ SIGNATURES = {
     "tmdnet_nl_workspace_bytes": (SZ, [I, I, P, D]),
     "tmdnet_nl_build": (I, [I, I, P, P, I, P, I, D, D, I, I, I, P, P, P, P, P, P, I, P, SZ, P]),
     "tmdnet_nl_backward": (I, [I, I, P, P, I, P, P, P, P, P, P]),
+    "tmdnet_nl_backward2": (I, [I, I, P, P, P, I, P, P, P, P, P, P, P, P]),
     "tmdnet_edge_geom_fwd": (I, [I, I, I, I, P, P, P, P, P, P, D, D, P, P, P, P]),
     "tmdnet_edge_geom_bwd": (I, [I, I, I, I, P, P, P, P, P, P, D, D, P, P, P, P, P, P]),
     "tmdnet_et_message_fwd": (I, [I, I, I, I, P, P, I, P, I, P, I, P, I, P, P, I, P, I, P, P, P, P, I, P, P]),

@@ -198,21 +198,82 @@ class _NeighborGeomBwd(Function):
     @staticmethod
     def backward(ctx, ggpos):
         pos, gd, gr, deltas, distances = ctx.saved_tensors
+        d_pos, d_gd, d_gr = _NeighborGeomBwd2.apply(pos, ggpos, gd, gr, deltas, distances, ctx.graph)
+        return d_pos, (d_gd if gd is not None else None), (d_gr if gr is not None else None), \
+            None, None, None
+
+
+def nl_backward_composite(pos, gd, gr, deltas, distances, src, dst):
+    """Differentiable restatement of tmdnet_nl_backward (reference neighbors_cuda.cu:43-71):
+    g = gd + delta/r*gr (0 where r == 0); dpos = index_add(src, g) - index_add(dst, g)."""
+    s, d = src.long().clamp(min=0), dst.long().clamp(min=0)  # padding slots have r == 0 (masked)
+    shift = (deltas - (pos.index_select(0, s) - pos.index_select(0, d))).detach()
+    dl = pos.index_select(0, s) - pos.index_select(0, d) + shift
+    zero = distances == 0
+    r = torch.where(zero, torch.ones_like(distances), (dl * dl).sum(1)).sqrt()  # no 0/0 through sqrt(0)
+    g = torch.zeros_like(dl) if gd is None else gd
+    if gr is not None:
+        g = g + dl / r.unsqueeze(1) * gr.unsqueeze(1)
+    g = torch.where(zero.unsqueeze(1), torch.zeros_like(dl), g)
+    return torch.zeros_like(pos).index_add(0, s, g).index_add(0, d, -g)
+
+
+def nl_backward2_composite(pos, ggpos, gr, deltas, distances, src, dst):
+    """Differentiable restatement of tmdnet_nl_backward2: (d_pos, d_gd, d_gr) = the gradient of
+    <ggpos, nl_backward_composite(pos, gd, gr, ...)> w.r.t. (pos, gd, gr)."""
+    s, d = src.long().clamp(min=0), dst.long().clamp(min=0)
+    live = ((distances != 0) & (src >= 0)).to(pos.dtype).unsqueeze(1)
+    shift = (deltas - (pos.index_select(0, s) - pos.index_select(0, d))).detach()
+    dl = pos.index_select(0, s) - pos.index_select(0, d) + shift
+    r = torch.where(distances == 0, torch.ones_like(distances), (dl * dl).sum(1)).sqrt()
+    u = dl / r.unsqueeze(1)
+    w = (ggpos.index_select(0, s) - ggpos.index_select(0, d)) * live
+    uw = (u * w).sum(1, keepdim=True)
+    d_pos = torch.zeros_like(pos)
+    if gr is not None:
+        h = (gr / r).unsqueeze(1) * (w - u * uw)
+        d_pos = d_pos.index_add(0, s, h).index_add(0, d, -h)
+    return d_pos, w, uw.squeeze(1)
+
+
+class _NeighborGeomBwd2(Function):
+    """Second order of the neighbour op (HIP tmdnet_nl_backward2); its own backward (third order)
+    differentiates the composite."""
+
+    @staticmethod
+    def forward(ctx, pos, ggpos, gd, gr, deltas, distances, graph):
+        lib = nat.load()
+        n = pos.shape[0]
+        cap = graph.n_edges
+        d_pos = torch.empty_like(pos)
+        d_gd = torch.empty((cap, 3), dtype=pos.dtype, device=pos.device) if gd is not None else None
+        d_gr = torch.empty((cap,), dtype=pos.dtype, device=pos.device) if gr is not None else None
+        gg = ggpos.contiguous()
+        rc = lib.tmdnet_nl_backward2(nat.dtype_code(pos.dtype), n, nat.ptr(graph.row_ptr), nat.ptr(graph.src),
+                                     nat.ptr(graph.transpose), cap, nat.ptr(gr), nat.ptr(deltas),
+                                     nat.ptr(distances), nat.ptr(gg), nat.ptr(d_pos), nat.ptr(d_gd),
+                                     nat.ptr(d_gr), nat.stream(pos.device))
+        nat.check(rc, "tmdnet_nl_backward2")
+        ctx.graph = graph
+        ctx.has = (gd is not None, gr is not None)
+        ctx.save_for_backward(pos, gg, gr, deltas, distances)
+        return d_pos, d_gd, d_gr
+
+    @staticmethod
+    def backward(ctx, g_dpos, g_dgd, g_dgr):
+        pos, gg, gr, deltas, distances = ctx.saved_tensors
         graph = ctx.graph
-        src, dst = graph.src.long().clamp(min=0), graph.dst.long().clamp(min=0)  # padding -> 0 (masked)
         with torch.enable_grad():
             p = pos.detach().requires_grad_(True)
-            gd_ = (torch.zeros_like(deltas) if gd is None else gd.detach()).requires_grad_(True)
-            gr_ = (torch.zeros_like(distances) if gr is None else gr.detach()).requires_grad_(True)
-            shift = (deltas - (pos[src] - pos[dst])).detach()
-            dl = p[src] - p[dst] + shift
-            zero = (distances == 0).unsqueeze(1)
-            r = torch.where(zero.squeeze(1), torch.ones_like(distances), (dl * dl).sum(1).sqrt())
-            g = torch.where(zero, torch.zeros_like(dl), gd_ + dl / r.unsqueeze(1) * gr_.unsqueeze(1))
-            out = torch.zeros_like(p).index_add(0, src, g).index_add(0, dst, -g)
-            grads = torch.autograd.grad(out, (p, gd_, gr_), ggpos, create_graph=True, allow_unused=True)
-        return grads[0], (grads[1] if gd is not None else None), (grads[2] if gr is not None else None), \
-            None, None, None
+            g_ = gg.detach().requires_grad_(True)
+            r_ = None if gr is None else gr.detach().requires_grad_(True)
+            outs = nl_backward2_composite(p, g_, r_, deltas, distances, graph.src, graph.dst)
+            pairs = [(o, go) for o, go in zip(outs, (g_dpos, g_dgd, g_dgr)) if go is not None]
+            ins = (p, g_) + ((r_,) if r_ is not None else ())
+            grads = torch.autograd.grad([o for o, _ in pairs], ins, [go for _, go in pairs],
+                                        create_graph=True, allow_unused=True)
+        d_gr = grads[2] if r_ is not None else None
+        return grads[0], grads[1], None, d_gr, None, None, None
 
 
 def build_graph(pos, batch, cutoff_lower, cutoff_upper, max_num_pairs, loop=True, strategy="brute",
