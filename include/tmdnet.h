@@ -165,6 +165,22 @@ int tmdnet_et_epilogue_bwd(int dtype, int n_nodes, int hidden, const void* grad_
                            const void* grad_vec, const void* vecp, const void* o, void* grad_vecp,
                            void* grad_o, void* stream);
 
+/* ------------------------------------------------------------------------------------------
+ * EquivariantScalar output head (reference models/output_modules.py:80-115 with two
+ * GatedEquivariantBlocks, models/utils.py:456-522: H -> H/2 with scalar SiLU, then H/2 -> 1;
+ * intermediate = hidden; SiLU activations), fused per atom.
+ * weights[12] = block 1: vec1_proj.weight [H][H], vec2_proj.weight [H/2][H], update_net[0].weight
+ *   [H][2H], update_net[0].bias [H], update_net[2].weight [H][H], update_net[2].bias [H];
+ *   block 2: the same six for H/2 (vec2_proj.weight [1][H/2], update_net[2].weight [2][H/2]).
+ * x [N][H], vec [N][3][H] -> y [N] (the atom output before std / reduce; the head's "+ 0 * sum vec"
+ * term is dropped).  jac_x [N][H], jac_vec [N][3][H] (both NULL or both given): dy_n / d(x_n, vec_n),
+ * zero where a vector norm is zero (torch.norm's backward).  H even, <= ~500 (LDS). */
+int tmdnet_eq_head_fwd(int dtype, int n_atoms, int hidden, const void* x, const void* vec,
+                       const void* const* weights, void* y, void* jac_x, void* jac_vec, void* stream);
+/* grad_x = grad_y[n] * jac_x[n], grad_vec = grad_y[n] * jac_vec[n] (the head's backward). */
+int tmdnet_eq_head_bwd(int dtype, int n_atoms, int hidden, const void* grad_y, const void* jac_x,
+                       const void* jac_vec, void* grad_x, void* grad_vec, void* stream);
+
 /* Neighbour embedding aggregation (reference NeighborEmbedding.forward/message,
  *   models/utils.py:73-108):  out[t] = sum_{e in row t, src!=dst} X[src[e]] * W[e] * C[e]
  *   X: [N][H] (ld_x), W: [E][H] (ld_w) = distance_proj(rbf) pre-cutoff, C: [E], out [N][H]. */

@@ -1,0 +1,135 @@
+"""Fused EquivariantScalar head (csrc/eq_head.hip): the composite restatement against the
+module-by-module blocks on CPU, then the HIP kernel (outputs, per-atom Jacobian, first and second
+order gradients) against that composite on the GPU.  Reference: output_modules.py:80-115,
+utils.py:456-522."""
+import pytest
+import torch
+
+from torchmdnet import kernels
+from torchmdnet.models.output_modules import EquivariantScalar
+
+DEV = torch.device("cuda", 0)
+
+
+def _head(H, dtype, seed=0):
+    torch.manual_seed(seed)
+    head = EquivariantScalar(H, dtype=dtype)
+    # non-zero biases so every term is exercised (reset_parameters zeroes them)
+    for b in head.output_network:
+        for m in (b.update_net[0], b.update_net[2]):
+            m.bias.data.normal_(0, 0.3)
+    return head
+
+
+def _inputs(N, H, dtype, device="cpu", seed=1):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(N, H, generator=g, dtype=dtype)
+    vec = torch.randn(N, 3, H, generator=g, dtype=dtype)
+    vec[2] = 0  # an isolated atom: zero vector features (the reference's masked rows)
+    return x.to(device), vec.to(device)
+
+
+def _blocks(head, x, vec):
+    for layer in head.output_network:
+        x, vec = layer(x, vec)
+    return x + vec.sum() * 0
+
+
+def test_composite_matches_blocks_cpu():
+    head = _head(32, torch.float64)
+    assert kernels.eq_head_fusable(head.output_network)
+    x, vec = _inputs(7, 32, torch.float64)
+    x.requires_grad_(True)
+    vec.requires_grad_(True)
+    ps = kernels.eq_head_params(head.output_network)
+    y_ref = _blocks(head, x, vec)
+    y = kernels.eq_head_composite(x, vec, ps)
+    assert torch.allclose(y, y_ref, rtol=1e-12, atol=1e-12)
+    w = torch.randn_like(y)
+    g_ref = torch.autograd.grad((y_ref * w).sum(), [x, vec] + ps)
+    g = torch.autograd.grad((y * w).sum(), [x, vec] + ps)
+    for a, b in zip(g, g_ref):
+        assert torch.isfinite(a).all()
+        assert torch.allclose(a, b, rtol=1e-10, atol=1e-12)
+    assert torch.all(g[1][2] == 0)  # zero rows get zero gradient, as the reference's mask
+
+
+def _rel(a, b):
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype,H,tol", [(torch.float64, 128, 1e-11), (torch.float32, 128, 2e-5),
+                                         (torch.float64, 48, 1e-11), (torch.float32, 256, 2e-5)])
+def test_hip_head_matches_composite(dtype, H, tol):
+    head = _head(H, dtype).to(DEV)
+    ps = kernels.eq_head_params(head.output_network)
+    N = 37  # not a multiple of the atom tile
+    x, vec = _inputs(N, H, dtype, DEV)
+    x.requires_grad_(True)
+    vec.requires_grad_(True)
+    y = kernels.eq_scalar_head(x, vec, head.output_network)
+    y_ref = kernels.eq_head_composite(x, vec, ps)
+    assert _rel(y, y_ref) < tol
+    gy = torch.randn_like(y)
+    # inference-style backward (positions only): the Jacobian path, no weight gradients
+    gx, gv = torch.autograd.grad(y, (x, vec), gy, retain_graph=True)
+    rx, rv = torch.autograd.grad(y_ref, (x, vec), gy, retain_graph=True)
+    assert _rel(gx, rx) < tol and _rel(gv, rv) < tol
+    assert torch.all(gv[2] == 0)
+    # weight gradients (training's energy term) and second order (force term)
+    g1 = torch.autograd.grad(y, [x, vec] + ps, gy, create_graph=True)
+    r1 = torch.autograd.grad(y_ref, [x, vec] + ps, gy, create_graph=True)
+    for a, b in zip(g1, r1):
+        assert _rel(a, b) < tol
+    cx, cv = torch.randn_like(x), torch.randn_like(vec)
+    l2 = (g1[0] * cx).sum() + (g1[1] * cv).sum()
+    m2 = (r1[0] * cx).sum() + (r1[1] * cv).sum()
+    g2 = torch.autograd.grad(l2, [x, vec] + ps, allow_unused=True)
+    r2 = torch.autograd.grad(m2, [x, vec] + ps, allow_unused=True)
+    for a, b in zip(g2, r2):
+        if b is None:
+            assert a is None or a.abs().max() == 0
+            continue
+        assert _rel(a, b) < 10 * tol
+
+
+@pytest.mark.gpu
+def test_model_uses_fused_head_and_matches_blocks():
+    """create_model's ET + EquivariantScalar routes through the HIP head; energies and forces equal
+    the module-by-module head on the same representation (fp64)."""
+    from conftest import yaml_args
+    from oracle import model_oracle as O
+    from torchmdnet.models.model import create_model
+    args = yaml_args("equivariant-transformer", embedding_dimension=64, num_layers=2, num_rbf=16, num_heads=4,
+                     derivative=True, output_model="Scalar", precision=64)
+    torch.manual_seed(3)
+    m = create_model(args).to(DEV)
+    z, pos, batch = O.qm9_like(6)
+    z, pos, batch = z.to(DEV), pos.to(DEV), batch.to(DEV)
+    calls = []
+    orig = kernels.eq_scalar_head
+
+    def spy(*a):
+        calls.append(1)
+        return orig(*a)
+
+    kernels.eq_scalar_head = spy
+    try:
+        y, f = m(z, pos, batch)
+    finally:
+        kernels.eq_scalar_head = orig
+    assert calls
+    out = m.output_model
+    pr = EquivariantScalar.pre_reduce
+
+    def unfused(self, x, v, z_, pos_, batch_):
+        return _blocks(self, x, v)
+
+    EquivariantScalar.pre_reduce = unfused
+    try:
+        y2, f2 = m(z, pos, batch)
+    finally:
+        EquivariantScalar.pre_reduce = pr
+    assert out is m.output_model
+    assert _rel(y, y2) < 1e-11 and _rel(f, f2) < 1e-10

@@ -1,0 +1,376 @@
+// EquivariantScalar output head, fused: the two GatedEquivariantBlocks of reference
+// models/output_modules.py:80-115 (blocks: models/utils.py:456-522) for a tile of atoms per
+// workgroup, plus -- in the same pass -- the per-atom Jacobian of the atom's output y_n with respect
+// to its inputs (x_n, vec_n).  The head is purely per-atom and ends in ONE scalar per atom, so the
+// backward of the energy (forces) is y's cotangent times that Jacobian: the ~60 small GEMM /
+// elementwise launches of the head's forward and backward become one launch here and one scale
+// kernel in the backward.
+//
+// Block(Hi -> O, intermediate I = Hi), per atom (a = 0..2 the Cartesian axis):
+//   vb[a] = W1 vec[a]           (Hi x Hi)      v2[a] = W2 vec[a]      (O x Hi)
+//   vec1  = |vb| over a          (0 gradient where |vb| = 0, as torch.norm's backward)
+//   u = U1 [x | vec1] + b1       (Hi x 2Hi)    s = SiLU(u)
+//   o = U2 s + b2                (2O x Hi)     xo = o[:O], vo = o[O:]
+//   x' = scalar_act ? SiLU(xo) : xo,           vec'[a] = vo * v2[a]
+// EquivariantScalar = Block(H -> H/2, scalar_act) then Block(H/2 -> 1); y = x'' (+ 0 * sum vec'').
+//
+// Mapping: 256 threads, NT atoms per workgroup, every intermediate in LDS.  Row products
+// (out[j] = sum_k W[j][k] in[k]) give one output row per thread with the input broadcast from LDS;
+// transposed products of the backward (out[k] = sum_i W[i][k] g[i]) give one column per thread, so
+// consecutive threads read consecutive weights.  Weights (~0.4 MB at H = 128) stay L2-resident
+// across workgroups.
+#include "common.h"
+#include "tmdnet.h"
+
+namespace tmd {
+namespace head {
+
+template <typename T>
+struct Weights {
+  const T *w1, *w2, *u1w, *u1b, *u2w, *u2b;  // block 1 (H -> H/2)
+  const T *v1, *v2, *p1w, *p1b, *p2w, *p2b;  // block 2 (H/2 -> 1)
+};
+
+template <typename T>
+__device__ __forceinline__ T sig(T x) { return T(1) / (T(1) + exp(-x)); }
+template <>
+__device__ __forceinline__ float sig<float>(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
+
+// out[t][r][j] = bias[j] + sum_k W[j][k] in[t][r][k] for j < J (rows of A) then rows of B (J2 rows,
+// written to out2), r < R vectors per atom; atom stride P, vector stride ld.
+template <typename T, int NT, int R>
+__device__ __forceinline__ void rows2(const T* __restrict__ A, const T* __restrict__ ab, int J,
+                                      const T* __restrict__ B, const T* __restrict__ bb, int J2, int K,
+                                      const T* in, int ldi, T* out, int ldo, T* out2, int ldo2, int P) {
+  for (int j = threadIdx.x; j < J + J2; j += blockDim.x) {
+    const bool first = j < J;
+    const int jj = first ? j : j - J;
+    const T* w = first ? A + (size_t)jj * K : B + (size_t)jj * K;
+    const T* bp = first ? ab : bb;
+    const T b0 = bp ? bp[jj] : T(0);
+    T acc[NT][R];
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int r = 0; r < R; ++r) acc[t][r] = b0;
+    for (int k = 0; k < K; ++k) {
+      const T wk = w[k];
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < R; ++r) acc[t][r] += wk * in[t * P + r * ldi + k];
+    }
+    T* o = first ? out : out2;
+    const int ld = first ? ldo : ldo2;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int r = 0; r < R; ++r) o[t * P + r * ld + jj] = acc[t][r];
+  }
+}
+
+// out[t][r][k] = sum_i A[i][k] g[t][r][i] (+ sum_i B[i][k] g2[t][r][i]) for k < K; A, B row
+// strides lda, ldb.  Destination: LDS (atom stride P) or global (atom stride gstride, atoms t < nt).
+template <typename T, int NT, int R>
+__device__ __forceinline__ void cols2(const T* __restrict__ A, int lda, int I, const T* g, int ldg,
+                                      const T* __restrict__ B, int ldb, int I2, const T* g2, int ldg2,
+                                      int K, T* out, int ldo, int P, int nt, size_t gstride, bool global) {
+  for (int k = threadIdx.x; k < K; k += blockDim.x) {
+    T acc[NT][R];
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int r = 0; r < R; ++r) acc[t][r] = T(0);
+    for (int i = 0; i < I; ++i) {
+      const T wk = A[(size_t)i * lda + k];
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < R; ++r) acc[t][r] += wk * g[t * P + r * ldg + i];
+    }
+    for (int i = 0; i < I2; ++i) {
+      const T wk = B[(size_t)i * ldb + k];
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < R; ++r) acc[t][r] += wk * g2[t * P + r * ldg2 + i];
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      if (global && t >= nt) continue;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        if (global)
+          out[t * gstride + r * ldo + k] = acc[t][r];
+        else
+          out[t * P + r * ldo + k] = acc[t][r];
+      }
+    }
+  }
+}
+
+// LDS layout of one atom (units of T); H = hidden, O = H/2 (block-1 output = block-2 input), Q = O.
+struct Layout {
+  int v, h, vb, v2, u, s, o, v1, h2, vb2, v22, u2, s2, o2;      // forward
+  int gu2, gh2, gvb2, gv1, go, gu, gvec1, gvb, gv2;             // backward
+  int P;
+  __host__ __device__ Layout(int H) {
+    const int O = H / 2, Q = O;
+    int p = 0;
+    v = p;    p += 3 * H;
+    h = p;    p += 2 * H;   // [x | vec1]
+    vb = p;   p += 3 * H;
+    v2 = p;   p += 3 * O;
+    u = p;    p += H;
+    s = p;    p += H;
+    o = p;    p += 2 * O;   // [xo | vo]
+    v1 = p;   p += 3 * O;
+    h2 = p;   p += 2 * Q;   // [x1 | vec1']
+    vb2 = p;  p += 3 * Q;
+    v22 = p;  p += 4;
+    u2 = p;   p += Q;
+    s2 = p;   p += Q;
+    o2 = p;   p += 4;
+    gu2 = p;  p += Q;
+    gh2 = p;  p += 2 * Q;
+    gvb2 = p; p += 3 * Q;
+    gv1 = p;  p += 3 * O;
+    go = p;   p += 2 * O;
+    gu = p;   p += H;
+    gvec1 = p; p += H;
+    gvb = p;  p += 3 * H;
+    gv2 = p;  p += 3 * O;
+    P = p | 1;  // odd atom stride: atoms of one tile land in different banks
+  }
+};
+
+template <typename T, int NT>
+__global__ __launch_bounds__(256) void k_eq_head(int n, int H, const T* __restrict__ x,
+                                                 const T* __restrict__ vec, Weights<T> W,
+                                                 T* __restrict__ y, T* __restrict__ jx,
+                                                 T* __restrict__ jv) {
+  extern __shared__ __align__(16) unsigned char smem_raw[];
+  T* sm = reinterpret_cast<T*>(smem_raw);
+  const Layout L(H);
+  const int P = L.P, O = H / 2, Q = O;
+  const int n0 = blockIdx.x * NT;
+  const int nt = min(NT, n - n0);
+  const int tid = threadIdx.x, bs = blockDim.x;
+
+  // stage x -> h[0:H], vec -> v (rows of absent atoms are zero)
+  for (int i = tid; i < NT * 4 * H; i += bs) {
+    const int t = i / (4 * H), c = i - t * 4 * H;
+    const bool live = t < nt;
+    if (c < H)
+      sm[t * P + L.h + c] = live ? x[(size_t)(n0 + t) * H + c] : T(0);
+    else
+      sm[t * P + L.v + c - H] = live ? vec[(size_t)(n0 + t) * 3 * H + c - H] : T(0);
+  }
+  __syncthreads();
+
+  // ---------------- block 1 forward
+  rows2<T, NT, 3>(W.w1, nullptr, H, W.w2, nullptr, O, H, sm + L.v, H, sm + L.vb, H, sm + L.v2, O, P);
+  __syncthreads();
+  for (int i = tid; i < NT * H; i += bs) {
+    const int t = i / H, c = i - t * H;
+    const T* vb = sm + t * P + L.vb;
+    const T a0 = vb[c], a1 = vb[H + c], a2 = vb[2 * H + c];
+    sm[t * P + L.h + H + c] = sqrt(a0 * a0 + a1 * a1 + a2 * a2);
+  }
+  __syncthreads();
+  rows2<T, NT, 1>(W.u1w, W.u1b, H, nullptr, nullptr, 0, 2 * H, sm + L.h, 0, sm + L.u, 0, nullptr, 0, P);
+  __syncthreads();
+  for (int i = tid; i < NT * H; i += bs) {
+    const int t = i / H, c = i - t * H;
+    const T u = sm[t * P + L.u + c];
+    sm[t * P + L.s + c] = u * sig(u);
+  }
+  __syncthreads();
+  rows2<T, NT, 1>(W.u2w, W.u2b, 2 * O, nullptr, nullptr, 0, H, sm + L.s, 0, sm + L.o, 0, nullptr, 0, P);
+  __syncthreads();
+  for (int i = tid; i < NT * O; i += bs) {
+    const int t = i / O, c = i - t * O;
+    T* a = sm + t * P;
+    const T xo = a[L.o + c], vo = a[L.o + O + c];
+    a[L.h2 + c] = xo * sig(xo);  // scalar activation of block 1
+#pragma unroll
+    for (int r = 0; r < 3; ++r) a[L.v1 + r * O + c] = vo * a[L.v2 + r * O + c];
+  }
+  __syncthreads();
+
+  // ---------------- block 2 forward (Q = O inputs, 1 output)
+  rows2<T, NT, 3>(W.v1, nullptr, Q, W.v2, nullptr, 1, O, sm + L.v1, O, sm + L.vb2, Q, sm + L.v22, 1, P);
+  __syncthreads();
+  for (int i = tid; i < NT * Q; i += bs) {
+    const int t = i / Q, c = i - t * Q;
+    const T* vb = sm + t * P + L.vb2;
+    const T a0 = vb[c], a1 = vb[Q + c], a2 = vb[2 * Q + c];
+    sm[t * P + L.h2 + Q + c] = sqrt(a0 * a0 + a1 * a1 + a2 * a2);
+  }
+  __syncthreads();
+  rows2<T, NT, 1>(W.p1w, W.p1b, Q, nullptr, nullptr, 0, 2 * Q, sm + L.h2, 0, sm + L.u2, 0, nullptr, 0, P);
+  __syncthreads();
+  for (int i = tid; i < NT * Q; i += bs) {
+    const int t = i / Q, c = i - t * Q;
+    const T u = sm[t * P + L.u2 + c];
+    const T sg = sig(u);
+    sm[t * P + L.s2 + c] = u * sg;
+    // backward seed: dy/do2 = (1, 0) -> g_s2 = p2w[0][:]; g_u2 = g_s2 * SiLU'(u2)
+    sm[t * P + L.gu2 + c] = W.p2w[c] * sg * (T(1) + u * (T(1) - sg));
+  }
+  __syncthreads();
+  rows2<T, NT, 1>(W.p2w, W.p2b, 1, nullptr, nullptr, 0, Q, sm + L.s2, 0, sm + L.o2, 0, nullptr, 0, P);
+  __syncthreads();
+  if (tid < nt) y[n0 + tid] = sm[tid * P + L.o2];
+  if (jx == nullptr) return;
+
+  // ---------------- reverse pass for J = d y / d (x, vec), seed dy = 1 (vec'' enters y as 0 * sum)
+  // block 2: g_h2 = P1^T g_u2
+  cols2<T, NT, 1>(W.p1w, 2 * Q, Q, sm + L.gu2, 0, nullptr, 0, 0, nullptr, 0, 2 * Q, sm + L.gh2, 0, P, nt, 0,
+                  false);
+  __syncthreads();
+  for (int i = tid; i < NT * Q; i += bs) {
+    const int t = i / Q, c = i - t * Q;
+    T* a = sm + t * P;
+    const T nrm = a[L.h2 + Q + c];
+    const T sc = nrm > T(0) ? a[L.gh2 + Q + c] / nrm : T(0);
+#pragma unroll
+    for (int r = 0; r < 3; ++r) a[L.gvb2 + r * Q + c] = sc * a[L.vb2 + r * Q + c];
+  }
+  __syncthreads();
+  // g_v1 = V1^T g_vb2 (the vec'' gate contributes nothing: its cotangent is 0)
+  cols2<T, NT, 3>(W.v1, O, Q, sm + L.gvb2, Q, nullptr, 0, 0, nullptr, 0, O, sm + L.gv1, O, P, nt, 0, false);
+  __syncthreads();
+  // block 1 gate: g_xo = g_x1 SiLU'(xo), g_vo = sum_a g_v1 v2, g_v2 = g_v1 vo
+  for (int i = tid; i < NT * O; i += bs) {
+    const int t = i / O, c = i - t * O;
+    T* a = sm + t * P;
+    const T xo = a[L.o + c], vo = a[L.o + O + c];
+    const T sg = sig(xo);
+    a[L.go + c] = a[L.gh2 + c] * sg * (T(1) + xo * (T(1) - sg));
+    T gvo = T(0);
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      const T g = a[L.gv1 + r * O + c];
+      gvo += g * a[L.v2 + r * O + c];
+      a[L.gv2 + r * O + c] = g * vo;
+    }
+    a[L.go + O + c] = gvo;
+  }
+  __syncthreads();
+  // g_s = U2^T g_o, g_u = g_s SiLU'(u)
+  cols2<T, NT, 1>(W.u2w, H, 2 * O, sm + L.go, 0, nullptr, 0, 0, nullptr, 0, H, sm + L.gu, 0, P, nt, 0, false);
+  __syncthreads();
+  for (int i = tid; i < NT * H; i += bs) {
+    const int t = i / H, c = i - t * H;
+    T* a = sm + t * P;
+    const T u = a[L.u + c];
+    const T sg = sig(u);
+    a[L.gu + c] *= sg * (T(1) + u * (T(1) - sg));
+  }
+  __syncthreads();
+  // g_h = U1^T g_u (U1 is [H][2H]): the x half is J_x (global), the vec1 half stays in LDS
+  cols2<T, NT, 1>(W.u1w, 2 * H, H, sm + L.gu, 0, nullptr, 0, 0, nullptr, 0, H, jx + (size_t)n0 * H, 0, P, nt,
+                  (size_t)H, true);
+  cols2<T, NT, 1>(W.u1w + H, 2 * H, H, sm + L.gu, 0, nullptr, 0, 0, nullptr, 0, H, sm + L.gvec1, 0, P, nt, 0,
+                  false);
+  __syncthreads();
+  for (int i = tid; i < NT * H; i += bs) {
+    const int t = i / H, c = i - t * H;
+    T* a = sm + t * P;
+    const T nrm = a[L.h + H + c];
+    const T sc = nrm > T(0) ? a[L.gvec1 + c] / nrm : T(0);
+#pragma unroll
+    for (int r = 0; r < 3; ++r) a[L.gvb + r * H + c] = sc * a[L.vb + r * H + c];
+  }
+  __syncthreads();
+  // J_vec[a] = W1^T g_vb[a] + W2^T g_v2[a]
+  cols2<T, NT, 3>(W.w1, H, H, sm + L.gvb, H, W.w2, H, O, sm + L.gv2, O, H, jv + (size_t)n0 * 3 * H, H, P,
+                  nt, (size_t)3 * H, true);
+}
+
+// g_x[n] = g_y[n] J_x[n],  g_vec[n] = g_y[n] J_vec[n]
+template <typename T>
+__global__ void k_scale(int n, int H, const T* __restrict__ gy, const T* __restrict__ jx,
+                        const T* __restrict__ jv, T* __restrict__ gx, T* __restrict__ gv) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)n * 4 * H) return;
+  const int t = (int)(i / (4 * H)), c = (int)(i - (long long)t * 4 * H);
+  const T g = gy[t];
+  if (c < H)
+    gx[(size_t)t * H + c] = g * jx[(size_t)t * H + c];
+  else
+    gv[(size_t)t * 3 * H + c - H] = g * jv[(size_t)t * 3 * H + c - H];
+}
+
+}  // namespace head
+}  // namespace tmd
+
+using namespace tmd;
+
+static int head_tile(int dtype, int H, size_t* smem) {
+  const size_t es = dtype == TMDNET_F64 ? 8 : 4;
+  const size_t per = (size_t)head::Layout(H).P * es;
+  for (int nt = 4; nt >= 1; nt /= 2)
+    if (nt * per <= 64 * 1024) {
+      *smem = nt * per;
+      return nt;
+    }
+  return 0;
+}
+
+template <typename T>
+static int launch_head(int n, int H, const void* x, const void* vec, const void* const* w, void* y,
+                       void* jx, void* jv, int nt, size_t smem, hipStream_t st) {
+  head::Weights<T> W{(const T*)w[0], (const T*)w[1], (const T*)w[2], (const T*)w[3],
+                     (const T*)w[4], (const T*)w[5], (const T*)w[6], (const T*)w[7],
+                     (const T*)w[8], (const T*)w[9], (const T*)w[10], (const T*)w[11]};
+  dim3 g((n + nt - 1) / nt), b(256);
+  if (nt == 4)
+    hipLaunchKernelGGL((head::k_eq_head<T, 4>), g, b, smem, st, n, H, (const T*)x, (const T*)vec, W,
+                       (T*)y, (T*)jx, (T*)jv);
+  else if (nt == 2)
+    hipLaunchKernelGGL((head::k_eq_head<T, 2>), g, b, smem, st, n, H, (const T*)x, (const T*)vec, W,
+                       (T*)y, (T*)jx, (T*)jv);
+  else
+    hipLaunchKernelGGL((head::k_eq_head<T, 1>), g, b, smem, st, n, H, (const T*)x, (const T*)vec, W,
+                       (T*)y, (T*)jx, (T*)jv);
+  return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
+}
+
+extern "C" int tmdnet_eq_head_fwd(int dtype, int n_atoms, int hidden, const void* x, const void* vec,
+                                  const void* const* weights, void* y, void* jac_x, void* jac_vec,
+                                  void* stream) {
+  if (n_atoms < 0 || hidden < 2 || hidden % 2 || !x || !vec || !weights || !y) return kBadArgument;
+  if ((jac_x == nullptr) != (jac_vec == nullptr)) return kBadArgument;
+  for (int i = 0; i < 12; ++i)
+    if (!weights[i]) return kBadArgument;
+  if (n_atoms == 0) return kOk;
+  size_t smem = 0;
+  const int nt = head_tile(dtype, hidden, &smem);
+  if (nt == 0) return kUnsupported;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == TMDNET_F32) return launch_head<float>(n_atoms, hidden, x, vec, weights, y, jac_x, jac_vec, nt, smem, st);
+  if (dtype == TMDNET_F64) return launch_head<double>(n_atoms, hidden, x, vec, weights, y, jac_x, jac_vec, nt, smem, st);
+  return kUnsupported;
+}
+
+extern "C" int tmdnet_eq_head_bwd(int dtype, int n_atoms, int hidden, const void* grad_y,
+                                  const void* jac_x, const void* jac_vec, void* grad_x, void* grad_vec,
+                                  void* stream) {
+  if (n_atoms < 0 || hidden < 1 || !grad_y || !jac_x || !jac_vec || !grad_x || !grad_vec) return kBadArgument;
+  const long long work = (long long)n_atoms * 4 * hidden;
+  if (work == 0) return kOk;
+  const int tb = 256;
+  dim3 g((unsigned)((work + tb - 1) / tb));
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == TMDNET_F32)
+    hipLaunchKernelGGL(head::k_scale<float>, g, dim3(tb), 0, st, n_atoms, hidden, (const float*)grad_y,
+                       (const float*)jac_x, (const float*)jac_vec, (float*)grad_x, (float*)grad_vec);
+  else if (dtype == TMDNET_F64)
+    hipLaunchKernelGGL(head::k_scale<double>, g, dim3(tb), 0, st, n_atoms, hidden, (const double*)grad_y,
+                       (const double*)jac_x, (const double*)jac_vec, (double*)grad_x, (double*)grad_vec);
+  else
+    return kUnsupported;
+  return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
+}

@@ -922,3 +922,136 @@ def spatial_permutation(pos, batch, cell_size, box=None):
     key = _spread10(c[:, 0]) | (_spread10(c[:, 1]) << 1) | (_spread10(c[:, 2]) << 2)
     key = key + batch.to(torch.long) * (1 << 31)
     return torch.argsort(key, stable=True)
+
+
+# ----------------------------------------------------------------------------- EquivariantScalar head
+def eq_head_params(blocks):
+    """The 12 tensors tmdnet_eq_head_fwd consumes, in its order (include/tmdnet.h)."""
+    ps = []
+    for b in blocks:
+        ps += [b.vec1_proj.weight, b.vec2_proj.weight, b.update_net[0].weight, b.update_net[0].bias,
+               b.update_net[2].weight, b.update_net[2].bias]
+    return ps
+
+
+def eq_head_fusable(blocks):
+    """Two GatedEquivariantBlocks H -> H/2 (scalar SiLU) -> 1, SiLU update nets, intermediate = hidden
+    (EquivariantScalar's configuration, reference output_modules.py:80-100)."""
+    if len(blocks) != 2:
+        return False
+    b1, b2 = blocks
+    H = b1.vec1_proj.in_features
+    shapes_ok = (H % 2 == 0 and b1.out_channels == H // 2 and b2.out_channels == 1
+                 and b2.vec1_proj.in_features == H // 2
+                 and b1.update_net[0].out_features == H and b2.update_net[0].out_features == H // 2)
+    acts_ok = all(isinstance(b.update_net[1], torch.nn.SiLU) for b in blocks) \
+        and isinstance(b1.act, torch.nn.SiLU) and b2.act is None
+    return bool(shapes_ok and acts_ok and all(b.update_net[0].bias is not None for b in blocks))
+
+
+def masked_norm(vb):
+    """|vb| over the axis dim (-2) with the reference's zero-row exclusion (utils.py:500-512:
+    rows whose vectors are all zero keep 0 and get no gradient of any order), sync-free."""
+    nz = (vb != 0).flatten(1).any(dim=1).view(-1, 1, 1)
+    nrm = torch.linalg.vector_norm(torch.where(nz, vb, torch.ones_like(vb)), dim=-2)
+    return torch.where(nz.view(-1, 1), nrm, torch.zeros_like(nrm))
+
+
+def eq_head_composite(x, vec, params):
+    """Differentiable restatement of the two gated blocks (reference utils.py:492-522): the vector
+    norm's gradient is 0 where the norm is 0 (the reference masks zero rows, utils.py:500-512)."""
+    for blk, scalar_act in ((0, True), (1, False)):
+        w1, w2, u1w, u1b, u2w, u2b = params[6 * blk:6 * blk + 6]
+        vec1 = masked_norm(torch.matmul(vec, w1.t()))
+        vec2 = torch.matmul(vec, w2.t())
+        o = F.linear(F.silu(F.linear(torch.cat([x, vec1], dim=-1), u1w, u1b)), u2w, u2b)
+        xo, vo = torch.split(o, w2.shape[0], dim=-1)
+        vec = vo.unsqueeze(1) * vec2
+        x = F.silu(xo) if scalar_act else xo
+    return x + vec.sum() * 0  # keeps every parameter in the graph (zero, not None, gradients)
+
+
+def _will_run(node):
+    if node is None:
+        return False
+    try:
+        return bool(torch._C._will_engine_execute_node(node))
+    except RuntimeError:
+        return True
+
+
+class _EqHead(Function):
+    """(x, vec, *head params) -> y [N, 1]; the HIP kernel also returns dy/dx, dy/dvec per atom."""
+
+    @staticmethod
+    def forward(ctx, x, vec, *params):
+        lib = nat.load()
+        N, H = x.shape
+        x, vec = x.contiguous(), vec.contiguous()
+        y = torch.empty((N, 1), dtype=x.dtype, device=x.device)
+        want_j = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
+        jx = torch.empty_like(x) if want_j else None
+        jv = torch.empty_like(vec) if want_j else None
+        ws = (ctypes.c_void_p * 12)(*[p.data_ptr() for p in params])
+        rc = lib.tmdnet_eq_head_fwd(nat.dtype_code(x.dtype), N, H, nat.ptr(x), nat.ptr(vec), ws, nat.ptr(y),
+                                    nat.ptr(jx), nat.ptr(jv), nat.stream(x.device))
+        nat.check(rc, "tmdnet_eq_head_fwd")
+        ctx.save_for_backward(x, vec, jx, jv, *params)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, vec, jx, jv, *params = ctx.saved_tensors
+        nf = ctx.next_functions
+        off = len(nf) - len(params)
+        need_w = any(_will_run(nf[off + i][0]) for i in range(len(params)))
+        outs = _EqHeadBwd.apply(need_w, gy.contiguous(), jx, jv, x, vec, *params)
+        return outs
+
+
+class _EqHeadBwd(Function):
+    """First-order backward of the head: g_x, g_vec = g_y * Jacobian (HIP); the weight gradients
+    (training only) and every second-order term come from the composite."""
+
+    @staticmethod
+    def forward(ctx, need_w, gy, jx, jv, x, vec, *params):
+        lib = nat.load()
+        N, H = x.shape
+        gx = torch.empty_like(x)
+        gv = torch.empty_like(vec)
+        if jx is None:
+            raise RuntimeError("torchmd-net_amd: head Jacobian was not computed in the forward")
+        rc = lib.tmdnet_eq_head_bwd(nat.dtype_code(x.dtype), N, H, nat.ptr(gy), nat.ptr(jx), nat.ptr(jv),
+                                    nat.ptr(gx), nat.ptr(gv), nat.stream(x.device))
+        nat.check(rc, "tmdnet_eq_head_bwd")
+        g_params = [None] * len(params)
+        if need_w:
+            with torch.enable_grad():
+                ps = [p.detach().requires_grad_(True) for p in params]
+                y = eq_head_composite(x.detach(), vec.detach(), ps)
+                g_params = list(torch.autograd.grad(y, ps, gy, allow_unused=True))
+        ctx.save_for_backward(gy, x, vec, *params)
+        return (gx, gv) + tuple(g_params)
+
+    @staticmethod
+    def backward(ctx, ggx, ggv, *ggp):
+        saved = ctx.saved_tensors
+        with torch.enable_grad():
+            leaves = [t.detach().requires_grad_(True) for t in saved]
+            gy, x, vec = leaves[:3]
+            ps = leaves[3:]
+            y = eq_head_composite(x, vec, ps)
+            first = torch.autograd.grad(y, [x, vec] + ps, gy, create_graph=True, allow_unused=True)
+            sel = [(f, g) for f, g in zip(first, (ggx, ggv) + tuple(ggp)) if f is not None and g is not None]
+            if not sel:
+                return (None,) * (6 + len(ps))
+            second = torch.autograd.grad([f for f, _ in sel], leaves, [g for _, g in sel],
+                                         create_graph=torch.is_grad_enabled(), allow_unused=True)
+        d_gy, d_x, d_vec = second[:3]
+        return (None, d_gy, None, None, d_x, d_vec) + tuple(second[3:])
+
+
+def eq_scalar_head(x, vec, blocks):
+    """EquivariantScalar.pre_reduce's two gated blocks through the fused HIP head."""
+    nat.require_gpu(x, "eq_scalar_head")
+    return _EqHead.apply(x, vec, *eq_head_params(blocks))

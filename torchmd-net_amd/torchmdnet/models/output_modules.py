@@ -9,6 +9,7 @@ from typing import Optional
 import torch
 from torch import nn
 
+from .. import kernels
 from .utils import GatedEquivariantBlock, act_class_mapping, check_stream_capturing
 from ..utils import atomic_masses
 
@@ -94,6 +95,10 @@ class EquivariantScalar(OutputModel):
             layer.reset_parameters()
 
     def pre_reduce(self, x, v, z, pos, batch):
+        if x.is_cuda and type(self) is EquivariantScalar and kernels.eq_head_fusable(self.output_network):
+            # both gated blocks + the per-atom Jacobian in one HIP kernel (csrc/eq_head.hip); the
+            # reference's "+ 0 * v.sum()" only keeps v in the autograd graph and adds nothing
+            return kernels.eq_scalar_head(x, v, self.output_network)
         for layer in self.output_network:
             x, v = layer(x, v)
         return x + v.sum() * 0

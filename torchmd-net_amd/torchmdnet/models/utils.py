@@ -318,14 +318,10 @@ class GatedEquivariantBlock(nn.Module):
         self.update_net[2].bias.data.fill_(0)
 
     def forward(self, x, v):
-        vec1_buffer = self.vec1_proj(v)
         # zero rows (isolated atoms) are excluded from the norm so their gradient is not NaN; the
         # reference does this with a host-synchronising boolean mask (utils.py:499-512), this is the
-        # sync-free equivalent (same values, same zero gradient on those rows).
-        sq = (vec1_buffer * vec1_buffer).sum(dim=-2)
-        nz = (vec1_buffer != 0).flatten(1).any(dim=1, keepdim=True)
-        safe = torch.where(nz, sq, torch.ones_like(sq))
-        vec1 = torch.where(nz, torch.sqrt(safe), torch.zeros_like(sq))
+        # sync-free equivalent (same values, same zero gradients on those rows)
+        vec1 = kernels.masked_norm(self.vec1_proj(v))
         vec2 = self.vec2_proj(v)
         x = torch.cat([x, vec1], dim=-1)
         x, v = torch.split(self.update_net(x), self.out_channels, dim=-1)
