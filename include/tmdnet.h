@@ -177,6 +177,18 @@ int tmdnet_et_epilogue_bwd(int dtype, int n_nodes, int hidden, const void* grad_
  * zero where a vector norm is zero (torch.norm's backward).  H even, <= ~500 (LDS). */
 int tmdnet_eq_head_fwd(int dtype, int n_atoms, int hidden, const void* x, const void* vec,
                        const void* const* weights, void* y, void* jac_x, void* jac_vec, void* stream);
+/* Backward with weight gradients (training): recomputes the head and writes grad_x, grad_vec
+ * (= grad_y[n] * Jacobian) plus the per-atom factors saves[11] of every weight gradient, each a
+ * GEMM over atoms (layouts, O = Q = H/2):
+ *   0 a1 [N][3][H+O] = [g_vb | g_v2]   -> [dW1; dW2] = a1^T vec           (rows = N*3)
+ *   1 gu [N][H], 2 hext [N][2H+1] = [x | vec1 | 1]   -> [dU1 | db1] = gu^T hext
+ *   3 go [N][2O], 4 sext [N][H+1] = [s | 1]          -> [dU2 | db2] = go^T sext
+ *   5 a2 [N][3][Q+1] = [g_vb2 | 0], 6 v1 [N][3][O]   -> [dV1; dV2] = a2^T v1 (rows = N*3)
+ *   7 gu2 [N][Q], 8 h2ext [N][2Q+1]                  -> [dP1 | db1'] = gu2^T h2ext
+ *   9 go2 [N][2] = [g_y | 0], 10 s2ext [N][Q+1]      -> [dP2 | db2'] = go2^T s2ext */
+int tmdnet_eq_head_bwd_weights(int dtype, int n_atoms, int hidden, const void* x, const void* vec,
+                               const void* const* weights, const void* grad_y, void* grad_x,
+                               void* grad_vec, void* const* saves, void* stream);
 /* grad_x = grad_y[n] * jac_x[n], grad_vec = grad_y[n] * jac_vec[n] (the head's backward). */
 int tmdnet_eq_head_bwd(int dtype, int n_atoms, int hidden, const void* grad_y, const void* jac_x,
                        const void* jac_vec, void* grad_x, void* grad_vec, void* stream);

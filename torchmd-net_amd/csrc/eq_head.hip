@@ -31,6 +31,23 @@ struct Weights {
   const T *v1, *v2, *p1w, *p1b, *p2w, *p2b;  // block 2 (H/2 -> 1)
 };
 
+// Per-atom factors of the weight gradients (weights mode; NULL = not written).  Each weight gradient
+// is then one GEMM over atoms, e.g. dU1|db1 = gu^T [x | vec1 | 1].
+template <typename T>
+struct Saves {
+  T* a1;     // [N][3][H+O]   [g_vb | g_v2]         -> [dW1; dW2] = a1^T vec
+  T* gu;     // [N][H]                              -> [dU1 | db1] = gu^T hext
+  T* hext;   // [N][2H+1]     [x | vec1 | 1]
+  T* go;     // [N][2O]                             -> [dU2 | db2] = go^T sext
+  T* sext;   // [N][H+1]      [s | 1]
+  T* a2;     // [N][3][Q+1]   [g_vb2 | 0]           -> [dV1; dV2] = a2^T v1
+  T* v1;     // [N][3][O]
+  T* gu2;    // [N][Q]                              -> [dP1 | db1'] = gu2^T h2ext
+  T* h2ext;  // [N][2Q+1]     [x1 | vec1' | 1]
+  T* go2;    // [N][2]        [g_y | 0]             -> [dP2 | db2'] = go2^T s2ext
+  T* s2ext;  // [N][Q+1]      [s2 | 1]
+};
+
 template <typename T>
 __device__ __forceinline__ T sig(T x) { return T(1) / (T(1) + exp(-x)); }
 template <>
@@ -144,11 +161,14 @@ struct Layout {
   }
 };
 
+// y may be NULL; jx / jv receive d(seed * y)/d(x, vec) with seed = gy[n] (gy NULL: 1, i.e. the
+// Jacobian).  S: weight-gradient factors (weights mode), all NULL otherwise.
 template <typename T, int NT>
 __global__ __launch_bounds__(256) void k_eq_head(int n, int H, const T* __restrict__ x,
                                                  const T* __restrict__ vec, Weights<T> W,
                                                  T* __restrict__ y, T* __restrict__ jx,
-                                                 T* __restrict__ jv) {
+                                                 T* __restrict__ jv, const T* __restrict__ gy,
+                                                 Saves<T> S) {
   extern __shared__ __align__(16) unsigned char smem_raw[];
   T* sm = reinterpret_cast<T*>(smem_raw);
   const Layout L(H);
@@ -215,13 +235,14 @@ __global__ __launch_bounds__(256) void k_eq_head(int n, int H, const T* __restri
     const T u = sm[t * P + L.u2 + c];
     const T sg = sig(u);
     sm[t * P + L.s2 + c] = u * sg;
-    // backward seed: dy/do2 = (1, 0) -> g_s2 = p2w[0][:]; g_u2 = g_s2 * SiLU'(u2)
-    sm[t * P + L.gu2 + c] = W.p2w[c] * sg * (T(1) + u * (T(1) - sg));
+    // backward seed: dy/do2 = (seed, 0) -> g_s2 = seed p2w[0][:]; g_u2 = g_s2 * SiLU'(u2)
+    const T seed = gy ? (t < nt ? gy[n0 + t] : T(0)) : T(1);
+    sm[t * P + L.gu2 + c] = seed * W.p2w[c] * sg * (T(1) + u * (T(1) - sg));
   }
   __syncthreads();
   rows2<T, NT, 1>(W.p2w, W.p2b, 1, nullptr, nullptr, 0, Q, sm + L.s2, 0, sm + L.o2, 0, nullptr, 0, P);
   __syncthreads();
-  if (tid < nt) y[n0 + tid] = sm[tid * P + L.o2];
+  if (y && tid < nt) y[n0 + tid] = sm[tid * P + L.o2];
   if (jx == nullptr) return;
 
   // ---------------- reverse pass for J = d y / d (x, vec), seed dy = 1 (vec'' enters y as 0 * sum)
@@ -287,6 +308,48 @@ __global__ __launch_bounds__(256) void k_eq_head(int n, int H, const T* __restri
   // J_vec[a] = W1^T g_vb[a] + W2^T g_v2[a]
   cols2<T, NT, 3>(W.w1, H, H, sm + L.gvb, H, W.w2, H, O, sm + L.gv2, O, H, jv + (size_t)n0 * 3 * H, H, P,
                   nt, (size_t)3 * H, true);
+  if (S.a1 == nullptr) return;
+  // weights mode: every LDS buffer is still intact (no aliasing); dump the per-atom factors
+  const int wa1 = H + O, wa2 = Q + 1;
+  for (int i = tid; i < nt * 3 * wa1; i += bs) {
+    const int t = i / (3 * wa1), r = (i / wa1) % 3, c = i % wa1;
+    const T* a = sm + t * P;
+    S.a1[(size_t)(n0 + t) * 3 * wa1 + r * wa1 + c] = c < H ? a[L.gvb + r * H + c] : a[L.gv2 + r * O + c - H];
+  }
+  for (int i = tid; i < nt * 3 * wa2; i += bs) {
+    const int t = i / (3 * wa2), r = (i / wa2) % 3, c = i % wa2;
+    S.a2[(size_t)(n0 + t) * 3 * wa2 + r * wa2 + c] = c < Q ? sm[t * P + L.gvb2 + r * Q + c] : T(0);
+  }
+  for (int i = tid; i < nt * 3 * O; i += bs) {
+    const int t = i / (3 * O), c = i % (3 * O);
+    S.v1[(size_t)(n0 + t) * 3 * O + c] = sm[t * P + L.v1 + c];
+  }
+  for (int i = tid; i < nt * (2 * H + 1); i += bs) {
+    const int t = i / (2 * H + 1), c = i % (2 * H + 1);
+    S.hext[(size_t)(n0 + t) * (2 * H + 1) + c] = c < 2 * H ? sm[t * P + L.h + c] : T(1);
+  }
+  for (int i = tid; i < nt * (H + 1); i += bs) {
+    const int t = i / (H + 1), c = i % (H + 1);
+    S.sext[(size_t)(n0 + t) * (H + 1) + c] = c < H ? sm[t * P + L.s + c] : T(1);
+    if (c < H) S.gu[(size_t)(n0 + t) * H + c] = sm[t * P + L.gu + c];
+  }
+  for (int i = tid; i < nt * 2 * O; i += bs) {
+    const int t = i / (2 * O), c = i % (2 * O);
+    S.go[(size_t)(n0 + t) * 2 * O + c] = sm[t * P + L.go + c];
+  }
+  for (int i = tid; i < nt * (2 * Q + 1); i += bs) {
+    const int t = i / (2 * Q + 1), c = i % (2 * Q + 1);
+    S.h2ext[(size_t)(n0 + t) * (2 * Q + 1) + c] = c < 2 * Q ? sm[t * P + L.h2 + c] : T(1);
+  }
+  for (int i = tid; i < nt * (Q + 1); i += bs) {
+    const int t = i / (Q + 1), c = i % (Q + 1);
+    S.s2ext[(size_t)(n0 + t) * (Q + 1) + c] = c < Q ? sm[t * P + L.s2 + c] : T(1);
+    if (c < Q) S.gu2[(size_t)(n0 + t) * Q + c] = sm[t * P + L.gu2 + c];
+  }
+  if (tid < nt) {
+    S.go2[(size_t)(n0 + tid) * 2] = gy ? gy[n0 + tid] : T(1);
+    S.go2[(size_t)(n0 + tid) * 2 + 1] = T(0);
+  }
 }
 
 // g_x[n] = g_y[n] J_x[n],  g_vec[n] = g_y[n] J_vec[n]
@@ -321,20 +384,25 @@ static int head_tile(int dtype, int H, size_t* smem) {
 
 template <typename T>
 static int launch_head(int n, int H, const void* x, const void* vec, const void* const* w, void* y,
-                       void* jx, void* jv, int nt, size_t smem, hipStream_t st) {
+                       void* jx, void* jv, const void* gy, void* const* sv, int nt, size_t smem,
+                       hipStream_t st) {
+  head::Saves<T> S{};
+  if (sv)
+    S = head::Saves<T>{(T*)sv[0], (T*)sv[1], (T*)sv[2], (T*)sv[3], (T*)sv[4], (T*)sv[5],
+                       (T*)sv[6], (T*)sv[7], (T*)sv[8], (T*)sv[9], (T*)sv[10]};
   head::Weights<T> W{(const T*)w[0], (const T*)w[1], (const T*)w[2], (const T*)w[3],
                      (const T*)w[4], (const T*)w[5], (const T*)w[6], (const T*)w[7],
                      (const T*)w[8], (const T*)w[9], (const T*)w[10], (const T*)w[11]};
   dim3 g((n + nt - 1) / nt), b(256);
   if (nt == 4)
     hipLaunchKernelGGL((head::k_eq_head<T, 4>), g, b, smem, st, n, H, (const T*)x, (const T*)vec, W,
-                       (T*)y, (T*)jx, (T*)jv);
+                       (T*)y, (T*)jx, (T*)jv, (const T*)gy, S);
   else if (nt == 2)
     hipLaunchKernelGGL((head::k_eq_head<T, 2>), g, b, smem, st, n, H, (const T*)x, (const T*)vec, W,
-                       (T*)y, (T*)jx, (T*)jv);
+                       (T*)y, (T*)jx, (T*)jv, (const T*)gy, S);
   else
     hipLaunchKernelGGL((head::k_eq_head<T, 1>), g, b, smem, st, n, H, (const T*)x, (const T*)vec, W,
-                       (T*)y, (T*)jx, (T*)jv);
+                       (T*)y, (T*)jx, (T*)jv, (const T*)gy, S);
   return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
 }
 
@@ -350,8 +418,35 @@ extern "C" int tmdnet_eq_head_fwd(int dtype, int n_atoms, int hidden, const void
   const int nt = head_tile(dtype, hidden, &smem);
   if (nt == 0) return kUnsupported;
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == TMDNET_F32) return launch_head<float>(n_atoms, hidden, x, vec, weights, y, jac_x, jac_vec, nt, smem, st);
-  if (dtype == TMDNET_F64) return launch_head<double>(n_atoms, hidden, x, vec, weights, y, jac_x, jac_vec, nt, smem, st);
+  if (dtype == TMDNET_F32)
+    return launch_head<float>(n_atoms, hidden, x, vec, weights, y, jac_x, jac_vec, nullptr, nullptr, nt, smem, st);
+  if (dtype == TMDNET_F64)
+    return launch_head<double>(n_atoms, hidden, x, vec, weights, y, jac_x, jac_vec, nullptr, nullptr, nt, smem, st);
+  return kUnsupported;
+}
+
+extern "C" int tmdnet_eq_head_bwd_weights(int dtype, int n_atoms, int hidden, const void* x,
+                                          const void* vec, const void* const* weights,
+                                          const void* grad_y, void* grad_x, void* grad_vec,
+                                          void* const* saves, void* stream) {
+  if (n_atoms < 0 || hidden < 2 || hidden % 2 || !x || !vec || !weights || !grad_y || !grad_x ||
+      !grad_vec || !saves)
+    return kBadArgument;
+  for (int i = 0; i < 12; ++i)
+    if (!weights[i]) return kBadArgument;
+  for (int i = 0; i < 11; ++i)
+    if (!saves[i]) return kBadArgument;
+  if (n_atoms == 0) return kOk;
+  size_t smem = 0;
+  const int nt = head_tile(dtype, hidden, &smem);
+  if (nt == 0) return kUnsupported;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == TMDNET_F32)
+    return launch_head<float>(n_atoms, hidden, x, vec, weights, nullptr, grad_x, grad_vec, grad_y, saves, nt,
+                              smem, st);
+  if (dtype == TMDNET_F64)
+    return launch_head<double>(n_atoms, hidden, x, vec, weights, nullptr, grad_x, grad_vec, grad_y, saves, nt,
+                               smem, st);
   return kUnsupported;
 }
 

@@ -1009,6 +1009,38 @@ class _EqHead(Function):
         return outs
 
 
+def _eq_head_weight_grads(lib, x, vec, params, gy, gx, gv):
+    """tmdnet_eq_head_bwd_weights (g_x, g_vec and the per-atom factors) + one GEMM per weight pair."""
+    N, H = x.shape
+    O = Q = H // 2
+    o = dict(dtype=x.dtype, device=x.device)
+    a1 = torch.empty((N, 3, H + O), **o)
+    gu = torch.empty((N, H), **o)
+    hext = torch.empty((N, 2 * H + 1), **o)
+    go = torch.empty((N, 2 * O), **o)
+    sext = torch.empty((N, H + 1), **o)
+    a2 = torch.empty((N, 3, Q + 1), **o)
+    v1 = torch.empty((N, 3, O), **o)
+    gu2 = torch.empty((N, Q), **o)
+    h2ext = torch.empty((N, 2 * Q + 1), **o)
+    go2 = torch.empty((N, 2), **o)
+    s2ext = torch.empty((N, Q + 1), **o)
+    saves = [a1, gu, hext, go, sext, a2, v1, gu2, h2ext, go2, s2ext]
+    ws = (ctypes.c_void_p * 12)(*[p.data_ptr() for p in params])
+    sv = (ctypes.c_void_p * 11)(*[t.data_ptr() for t in saves])
+    rc = lib.tmdnet_eq_head_bwd_weights(nat.dtype_code(x.dtype), N, H, nat.ptr(x), nat.ptr(vec), ws,
+                                        nat.ptr(gy), nat.ptr(gx), nat.ptr(gv), sv, nat.stream(x.device))
+    nat.check(rc, "tmdnet_eq_head_bwd_weights")
+    dw12 = a1.view(3 * N, H + O).t() @ vec.reshape(3 * N, H)
+    du1 = gu.t() @ hext
+    du2 = go.t() @ sext
+    dv12 = a2.view(3 * N, Q + 1).t() @ v1.view(3 * N, O)
+    dp1 = gu2.t() @ h2ext
+    dp2 = go2.t() @ s2ext
+    return [dw12[:H], dw12[H:], du1[:, :2 * H], du1[:, 2 * H], du2[:, :H], du2[:, H],
+            dv12[:Q], dv12[Q:], dp1[:, :2 * Q], dp1[:, 2 * Q], dp2[:, :Q], dp2[:, Q]]
+
+
 class _EqHeadBwd(Function):
     """First-order backward of the head: g_x, g_vec = g_y * Jacobian (HIP); the weight gradients
     (training only) and every second-order term come from the composite."""
@@ -1019,17 +1051,15 @@ class _EqHeadBwd(Function):
         N, H = x.shape
         gx = torch.empty_like(x)
         gv = torch.empty_like(vec)
-        if jx is None:
-            raise RuntimeError("torchmd-net_amd: head Jacobian was not computed in the forward")
-        rc = lib.tmdnet_eq_head_bwd(nat.dtype_code(x.dtype), N, H, nat.ptr(gy), nat.ptr(jx), nat.ptr(jv),
-                                    nat.ptr(gx), nat.ptr(gv), nat.stream(x.device))
-        nat.check(rc, "tmdnet_eq_head_bwd")
         g_params = [None] * len(params)
         if need_w:
-            with torch.enable_grad():
-                ps = [p.detach().requires_grad_(True) for p in params]
-                y = eq_head_composite(x.detach(), vec.detach(), ps)
-                g_params = list(torch.autograd.grad(y, ps, gy, allow_unused=True))
+            g_params = _eq_head_weight_grads(lib, x, vec, params, gy, gx, gv)
+        else:
+            if jx is None:
+                raise RuntimeError("torchmd-net_amd: head Jacobian was not computed in the forward")
+            rc = lib.tmdnet_eq_head_bwd(nat.dtype_code(x.dtype), N, H, nat.ptr(gy), nat.ptr(jx), nat.ptr(jv),
+                                        nat.ptr(gx), nat.ptr(gv), nat.stream(x.device))
+            nat.check(rc, "tmdnet_eq_head_bwd")
         ctx.save_for_backward(gy, x, vec, *params)
         return (gx, gv) + tuple(g_params)
 
