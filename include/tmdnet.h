@@ -174,7 +174,7 @@ int tmdnet_et_epilogue_bwd(int dtype, int n_nodes, int hidden, const void* grad_
  *   block 2: the same six for H/2 (vec2_proj.weight [1][H/2], update_net[2].weight [2][H/2]).
  * x [N][H], vec [N][3][H] -> y [N] (the atom output before std / reduce; the head's "+ 0 * sum vec"
  * term is dropped).  jac_x [N][H], jac_vec [N][3][H] (both NULL or both given): dy_n / d(x_n, vec_n),
- * zero where a vector norm is zero (torch.norm's backward).  H even, <= ~500 (LDS). */
+ * zero where a vector norm is zero (torch.norm's backward).  H a multiple of 4, <= ~500 (LDS). */
 int tmdnet_eq_head_fwd(int dtype, int n_atoms, int hidden, const void* x, const void* vec,
                        const void* const* weights, void* y, void* jac_x, void* jac_vec, void* stream);
 /* Backward with weight gradients (training): recomputes the head and writes grad_x, grad_vec

@@ -19,6 +19,8 @@
 // transposed products of the backward (out[k] = sum_i W[i][k] g[i]) give one column per thread, so
 // consecutive threads read consecutive weights.  Weights (~0.4 MB at H = 128) stay L2-resident
 // across workgroups.
+#include <cstdlib>
+
 #include "common.h"
 #include "tmdnet.h"
 
@@ -54,74 +56,144 @@ template <>
 __device__ __forceinline__ float sig<float>(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
 
 // out[t][r][j] = bias[j] + sum_k W[j][k] in[t][r][k] for j < J (rows of A) then rows of B (J2 rows,
-// written to out2), r < R vectors per atom; atom stride P, vector stride ld.
-template <typename T, int NT, int R>
+// written to out2), r < R vectors per atom; atom stride P, vector stride ld.  Each thread owns JT
+// rows; VEC: K, ldi, P multiples of 4 -> one 16-byte weight load per row and one broadcast
+// ds_read_b128 per (atom, vector) feed 4*JT FMAs.
+template <typename T, int NT, int R, int JT, bool VEC>
 __device__ __forceinline__ void rows2(const T* __restrict__ A, const T* __restrict__ ab, int J,
                                       const T* __restrict__ B, const T* __restrict__ bb, int J2, int K,
                                       const T* in, int ldi, T* out, int ldo, T* out2, int ldo2, int P) {
-  for (int j = threadIdx.x; j < J + J2; j += blockDim.x) {
-    const bool first = j < J;
-    const int jj = first ? j : j - J;
-    const T* w = first ? A + (size_t)jj * K : B + (size_t)jj * K;
-    const T* bp = first ? ab : bb;
-    const T b0 = bp ? bp[jj] : T(0);
-    T acc[NT][R];
+  using V4 = T __attribute__((ext_vector_type(4)));
+  const int JJ = J + J2;
+  for (int j0 = threadIdx.x * JT; j0 < JJ; j0 += blockDim.x * JT) {
+    const T* w[JT];
+    T acc[JT][NT][R];
 #pragma unroll
-    for (int t = 0; t < NT; ++t)
-#pragma unroll
-      for (int r = 0; r < R; ++r) acc[t][r] = b0;
-    for (int k = 0; k < K; ++k) {
-      const T wk = w[k];
+    for (int q = 0; q < JT; ++q) {
+      const int j = j0 + q;
+      const bool ok = j < JJ, first = j < J;
+      const int jj = first ? j : j - J;
+      w[q] = !ok ? A : first ? A + (size_t)jj * K : B + (size_t)jj * K;  // dead rows read row 0
+      const T* bp = first ? ab : bb;
+      const T b0 = (ok && bp) ? bp[jj] : T(0);
 #pragma unroll
       for (int t = 0; t < NT; ++t)
 #pragma unroll
-        for (int r = 0; r < R; ++r) acc[t][r] += wk * in[t * P + r * ldi + k];
+        for (int r = 0; r < R; ++r) acc[q][t][r] = b0;
     }
-    T* o = first ? out : out2;
-    const int ld = first ? ldo : ldo2;
+    if (VEC) {
+#pragma unroll 4
+      for (int k = 0; k < K; k += 4) {
+        V4 wv[JT];
 #pragma unroll
-    for (int t = 0; t < NT; ++t)
+        for (int q = 0; q < JT; ++q) wv[q] = *reinterpret_cast<const V4*>(w[q] + k);
 #pragma unroll
-      for (int r = 0; r < R; ++r) o[t * P + r * ld + jj] = acc[t][r];
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            const V4 iv = *reinterpret_cast<const V4*>(in + t * P + r * ldi + k);
+#pragma unroll
+            for (int q = 0; q < JT; ++q)
+              acc[q][t][r] += wv[q].x * iv.x + wv[q].y * iv.y + wv[q].z * iv.z + wv[q].w * iv.w;
+          }
+      }
+    } else {
+#pragma unroll 8
+      for (int k = 0; k < K; ++k) {
+        T wv[JT];
+#pragma unroll
+        for (int q = 0; q < JT; ++q) wv[q] = w[q][k];
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            const T iv = in[t * P + r * ldi + k];
+#pragma unroll
+            for (int q = 0; q < JT; ++q) acc[q][t][r] += wv[q] * iv;
+          }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < JT; ++q) {
+      const int j = j0 + q;
+      if (j >= JJ) continue;
+      const bool first = j < J;
+      T* o = first ? out + j : out2 + (j - J);
+      const int ld = first ? ldo : ldo2;
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < R; ++r) o[t * P + r * ld] = acc[q][t][r];
+    }
   }
 }
 
-// out[t][r][k] = sum_i A[i][k] g[t][r][i] (+ sum_i B[i][k] g2[t][r][i]) for k < K; A, B row
-// strides lda, ldb.  Destination: LDS (atom stride P) or global (atom stride gstride, atoms t < nt).
-template <typename T, int NT, int R>
+// out[t][r][k] = sum_i A[i][k] g[t][r][i] (+ sum_i B[i][k] g2[t][r][i]) for k < K (K even); A, B row
+// strides lda, ldb (even).  Each thread owns 2 adjacent columns (one 8-byte weight load per i);
+// VEC: I, ldg, P multiples of 4 -> broadcast ds_read_b128 of g.  Destination: LDS (atom stride P) or
+// global (atom stride gstride, atoms t < nt).
+template <typename T, int NT, int R, bool VEC>
+__device__ __forceinline__ void cols_part(T (&acc)[2][NT][R], const T* __restrict__ A, int lda, int I,
+                                          const T* g, int ldg, int k0, int P) {
+  using V2 = T __attribute__((ext_vector_type(2)));
+  using V4 = T __attribute__((ext_vector_type(4)));
+  if (VEC && (I & 3) == 0) {
+#pragma unroll 2
+    for (int i = 0; i < I; i += 4) {
+      V2 wv[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) wv[q] = *reinterpret_cast<const V2*>(A + (size_t)(i + q) * lda + k0);
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const V4 gv = *reinterpret_cast<const V4*>(g + t * P + r * ldg + i);
+          acc[0][t][r] += wv[0].x * gv.x + wv[1].x * gv.y + wv[2].x * gv.z + wv[3].x * gv.w;
+          acc[1][t][r] += wv[0].y * gv.x + wv[1].y * gv.y + wv[2].y * gv.z + wv[3].y * gv.w;
+        }
+    }
+  } else {
+#pragma unroll 8
+    for (int i = 0; i < I; ++i) {
+      const V2 wv = *reinterpret_cast<const V2*>(A + (size_t)i * lda + k0);
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const T gv = g[t * P + r * ldg + i];
+          acc[0][t][r] += wv.x * gv;
+          acc[1][t][r] += wv.y * gv;
+        }
+    }
+  }
+}
+
+template <typename T, int NT, int R, bool VEC>
 __device__ __forceinline__ void cols2(const T* __restrict__ A, int lda, int I, const T* g, int ldg,
                                       const T* __restrict__ B, int ldb, int I2, const T* g2, int ldg2,
                                       int K, T* out, int ldo, int P, int nt, size_t gstride, bool global) {
-  for (int k = threadIdx.x; k < K; k += blockDim.x) {
-    T acc[NT][R];
+  for (int k0 = threadIdx.x * 2; k0 < K; k0 += blockDim.x * 2) {
+    T acc[2][NT][R];
 #pragma unroll
-    for (int t = 0; t < NT; ++t)
-#pragma unroll
-      for (int r = 0; r < R; ++r) acc[t][r] = T(0);
-    for (int i = 0; i < I; ++i) {
-      const T wk = A[(size_t)i * lda + k];
+    for (int q = 0; q < 2; ++q)
 #pragma unroll
       for (int t = 0; t < NT; ++t)
 #pragma unroll
-        for (int r = 0; r < R; ++r) acc[t][r] += wk * g[t * P + r * ldg + i];
-    }
-    for (int i = 0; i < I2; ++i) {
-      const T wk = B[(size_t)i * ldb + k];
-#pragma unroll
-      for (int t = 0; t < NT; ++t)
-#pragma unroll
-        for (int r = 0; r < R; ++r) acc[t][r] += wk * g2[t * P + r * ldg2 + i];
-    }
+        for (int r = 0; r < R; ++r) acc[q][t][r] = T(0);
+    cols_part<T, NT, R, VEC>(acc, A, lda, I, g, ldg, k0, P);
+    if (I2 > 0) cols_part<T, NT, R, VEC>(acc, B, ldb, I2, g2, ldg2, k0, P);
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       if (global && t >= nt) continue;
 #pragma unroll
-      for (int r = 0; r < R; ++r) {
-        if (global)
-          out[t * gstride + r * ldo + k] = acc[t][r];
-        else
-          out[t * P + r * ldo + k] = acc[t][r];
-      }
+      for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          if (global)
+            out[t * gstride + r * ldo + k0 + q] = acc[q][t][r];
+          else
+            out[t * P + r * ldo + k0 + q] = acc[q][t][r];
+        }
     }
   }
 }
@@ -157,13 +229,13 @@ struct Layout {
     gvec1 = p; p += H;
     gvb = p;  p += 3 * H;
     gv2 = p;  p += 3 * O;
-    P = p | 1;  // odd atom stride: atoms of one tile land in different banks
+    P = (p + 3) & ~3;  // 16-byte aligned atoms (broadcast reads: no bank conflicts to avoid)
   }
 };
 
 // y may be NULL; jx / jv receive d(seed * y)/d(x, vec) with seed = gy[n] (gy NULL: 1, i.e. the
 // Jacobian).  S: weight-gradient factors (weights mode), all NULL otherwise.
-template <typename T, int NT>
+template <typename T, int NT, bool VEC>
 __global__ __launch_bounds__(256) void k_eq_head(int n, int H, const T* __restrict__ x,
                                                  const T* __restrict__ vec, Weights<T> W,
                                                  T* __restrict__ y, T* __restrict__ jx,
@@ -189,7 +261,7 @@ __global__ __launch_bounds__(256) void k_eq_head(int n, int H, const T* __restri
   __syncthreads();
 
   // ---------------- block 1 forward
-  rows2<T, NT, 3>(W.w1, nullptr, H, W.w2, nullptr, O, H, sm + L.v, H, sm + L.vb, H, sm + L.v2, O, P);
+  rows2<T, NT, 3, 2, VEC>(W.w1, nullptr, H, W.w2, nullptr, O, H, sm + L.v, H, sm + L.vb, H, sm + L.v2, O, P);
   __syncthreads();
   for (int i = tid; i < NT * H; i += bs) {
     const int t = i / H, c = i - t * H;
@@ -198,7 +270,7 @@ __global__ __launch_bounds__(256) void k_eq_head(int n, int H, const T* __restri
     sm[t * P + L.h + H + c] = sqrt(a0 * a0 + a1 * a1 + a2 * a2);
   }
   __syncthreads();
-  rows2<T, NT, 1>(W.u1w, W.u1b, H, nullptr, nullptr, 0, 2 * H, sm + L.h, 0, sm + L.u, 0, nullptr, 0, P);
+  rows2<T, NT, 1, 2, VEC>(W.u1w, W.u1b, H, nullptr, nullptr, 0, 2 * H, sm + L.h, 0, sm + L.u, 0, nullptr, 0, P);
   __syncthreads();
   for (int i = tid; i < NT * H; i += bs) {
     const int t = i / H, c = i - t * H;
@@ -206,7 +278,7 @@ __global__ __launch_bounds__(256) void k_eq_head(int n, int H, const T* __restri
     sm[t * P + L.s + c] = u * sig(u);
   }
   __syncthreads();
-  rows2<T, NT, 1>(W.u2w, W.u2b, 2 * O, nullptr, nullptr, 0, H, sm + L.s, 0, sm + L.o, 0, nullptr, 0, P);
+  rows2<T, NT, 1, 2, VEC>(W.u2w, W.u2b, 2 * O, nullptr, nullptr, 0, H, sm + L.s, 0, sm + L.o, 0, nullptr, 0, P);
   __syncthreads();
   for (int i = tid; i < NT * O; i += bs) {
     const int t = i / O, c = i - t * O;
@@ -219,7 +291,7 @@ __global__ __launch_bounds__(256) void k_eq_head(int n, int H, const T* __restri
   __syncthreads();
 
   // ---------------- block 2 forward (Q = O inputs, 1 output)
-  rows2<T, NT, 3>(W.v1, nullptr, Q, W.v2, nullptr, 1, O, sm + L.v1, O, sm + L.vb2, Q, sm + L.v22, 1, P);
+  rows2<T, NT, 3, 2, VEC>(W.v1, nullptr, Q, W.v2, nullptr, 1, O, sm + L.v1, O, sm + L.vb2, Q, sm + L.v22, 1, P);
   __syncthreads();
   for (int i = tid; i < NT * Q; i += bs) {
     const int t = i / Q, c = i - t * Q;
@@ -228,7 +300,7 @@ __global__ __launch_bounds__(256) void k_eq_head(int n, int H, const T* __restri
     sm[t * P + L.h2 + Q + c] = sqrt(a0 * a0 + a1 * a1 + a2 * a2);
   }
   __syncthreads();
-  rows2<T, NT, 1>(W.p1w, W.p1b, Q, nullptr, nullptr, 0, 2 * Q, sm + L.h2, 0, sm + L.u2, 0, nullptr, 0, P);
+  rows2<T, NT, 1, 2, VEC>(W.p1w, W.p1b, Q, nullptr, nullptr, 0, 2 * Q, sm + L.h2, 0, sm + L.u2, 0, nullptr, 0, P);
   __syncthreads();
   for (int i = tid; i < NT * Q; i += bs) {
     const int t = i / Q, c = i - t * Q;
@@ -240,14 +312,14 @@ __global__ __launch_bounds__(256) void k_eq_head(int n, int H, const T* __restri
     sm[t * P + L.gu2 + c] = seed * W.p2w[c] * sg * (T(1) + u * (T(1) - sg));
   }
   __syncthreads();
-  rows2<T, NT, 1>(W.p2w, W.p2b, 1, nullptr, nullptr, 0, Q, sm + L.s2, 0, sm + L.o2, 0, nullptr, 0, P);
+  rows2<T, NT, 1, 2, VEC>(W.p2w, W.p2b, 1, nullptr, nullptr, 0, Q, sm + L.s2, 0, sm + L.o2, 0, nullptr, 0, P);
   __syncthreads();
   if (y && tid < nt) y[n0 + tid] = sm[tid * P + L.o2];
   if (jx == nullptr) return;
 
   // ---------------- reverse pass for J = d y / d (x, vec), seed dy = 1 (vec'' enters y as 0 * sum)
   // block 2: g_h2 = P1^T g_u2
-  cols2<T, NT, 1>(W.p1w, 2 * Q, Q, sm + L.gu2, 0, nullptr, 0, 0, nullptr, 0, 2 * Q, sm + L.gh2, 0, P, nt, 0,
+  cols2<T, NT, 1, VEC>(W.p1w, 2 * Q, Q, sm + L.gu2, 0, nullptr, 0, 0, nullptr, 0, 2 * Q, sm + L.gh2, 0, P, nt, 0,
                   false);
   __syncthreads();
   for (int i = tid; i < NT * Q; i += bs) {
@@ -260,7 +332,7 @@ __global__ __launch_bounds__(256) void k_eq_head(int n, int H, const T* __restri
   }
   __syncthreads();
   // g_v1 = V1^T g_vb2 (the vec'' gate contributes nothing: its cotangent is 0)
-  cols2<T, NT, 3>(W.v1, O, Q, sm + L.gvb2, Q, nullptr, 0, 0, nullptr, 0, O, sm + L.gv1, O, P, nt, 0, false);
+  cols2<T, NT, 3, VEC>(W.v1, O, Q, sm + L.gvb2, Q, nullptr, 0, 0, nullptr, 0, O, sm + L.gv1, O, P, nt, 0, false);
   __syncthreads();
   // block 1 gate: g_xo = g_x1 SiLU'(xo), g_vo = sum_a g_v1 v2, g_v2 = g_v1 vo
   for (int i = tid; i < NT * O; i += bs) {
@@ -280,7 +352,7 @@ __global__ __launch_bounds__(256) void k_eq_head(int n, int H, const T* __restri
   }
   __syncthreads();
   // g_s = U2^T g_o, g_u = g_s SiLU'(u)
-  cols2<T, NT, 1>(W.u2w, H, 2 * O, sm + L.go, 0, nullptr, 0, 0, nullptr, 0, H, sm + L.gu, 0, P, nt, 0, false);
+  cols2<T, NT, 1, VEC>(W.u2w, H, 2 * O, sm + L.go, 0, nullptr, 0, 0, nullptr, 0, H, sm + L.gu, 0, P, nt, 0, false);
   __syncthreads();
   for (int i = tid; i < NT * H; i += bs) {
     const int t = i / H, c = i - t * H;
@@ -291,9 +363,9 @@ __global__ __launch_bounds__(256) void k_eq_head(int n, int H, const T* __restri
   }
   __syncthreads();
   // g_h = U1^T g_u (U1 is [H][2H]): the x half is J_x (global), the vec1 half stays in LDS
-  cols2<T, NT, 1>(W.u1w, 2 * H, H, sm + L.gu, 0, nullptr, 0, 0, nullptr, 0, H, jx + (size_t)n0 * H, 0, P, nt,
+  cols2<T, NT, 1, VEC>(W.u1w, 2 * H, H, sm + L.gu, 0, nullptr, 0, 0, nullptr, 0, H, jx + (size_t)n0 * H, 0, P, nt,
                   (size_t)H, true);
-  cols2<T, NT, 1>(W.u1w + H, 2 * H, H, sm + L.gu, 0, nullptr, 0, 0, nullptr, 0, H, sm + L.gvec1, 0, P, nt, 0,
+  cols2<T, NT, 1, VEC>(W.u1w + H, 2 * H, H, sm + L.gu, 0, nullptr, 0, 0, nullptr, 0, H, sm + L.gvec1, 0, P, nt, 0,
                   false);
   __syncthreads();
   for (int i = tid; i < NT * H; i += bs) {
@@ -306,7 +378,7 @@ __global__ __launch_bounds__(256) void k_eq_head(int n, int H, const T* __restri
   }
   __syncthreads();
   // J_vec[a] = W1^T g_vb[a] + W2^T g_v2[a]
-  cols2<T, NT, 3>(W.w1, H, H, sm + L.gvb, H, W.w2, H, O, sm + L.gv2, O, H, jv + (size_t)n0 * 3 * H, H, P,
+  cols2<T, NT, 3, VEC>(W.w1, H, H, sm + L.gvb, H, W.w2, H, O, sm + L.gv2, O, H, jv + (size_t)n0 * 3 * H, H, P,
                   nt, (size_t)3 * H, true);
   if (S.a1 == nullptr) return;
   // weights mode: every LDS buffer is still intact (no aliasing); dump the per-atom factors
@@ -371,10 +443,15 @@ __global__ void k_scale(int n, int H, const T* __restrict__ gy, const T* __restr
 
 using namespace tmd;
 
-static int head_tile(int dtype, int H, size_t* smem) {
+// Atoms per workgroup: the kernel is latency-bound (~20 dependent product phases), so small systems
+// want many workgroups (1 atom each); from ~2k atoms 2 atoms share each weight load (measured on
+// MI355X: 56 us at 580 atoms with 1, 41 ns/atom at 50k atoms with 2; 4 is slower at every size).
+static int head_tile(int dtype, int H, int n, size_t* smem) {
   const size_t es = dtype == TMDNET_F64 ? 8 : 4;
   const size_t per = (size_t)head::Layout(H).P * es;
-  for (int nt = 4; nt >= 1; nt /= 2)
+  int cap = n < 2048 ? 1 : 2;
+  if (const char* e = getenv("TMDNET_HEAD_NT")) cap = atoi(e) >= 4 ? 4 : atoi(e) >= 2 ? 2 : 1;  // tuning
+  for (int nt = cap; nt >= 1; nt /= 2)
     if (nt * per <= 64 * 1024) {
       *smem = nt * per;
       return nt;
@@ -394,28 +471,33 @@ static int launch_head(int n, int H, const void* x, const void* vec, const void*
                      (const T*)w[4], (const T*)w[5], (const T*)w[6], (const T*)w[7],
                      (const T*)w[8], (const T*)w[9], (const T*)w[10], (const T*)w[11]};
   dim3 g((n + nt - 1) / nt), b(256);
-  if (nt == 4)
-    hipLaunchKernelGGL((head::k_eq_head<T, 4>), g, b, smem, st, n, H, (const T*)x, (const T*)vec, W,
-                       (T*)y, (T*)jx, (T*)jv, (const T*)gy, S);
-  else if (nt == 2)
-    hipLaunchKernelGGL((head::k_eq_head<T, 2>), g, b, smem, st, n, H, (const T*)x, (const T*)vec, W,
-                       (T*)y, (T*)jx, (T*)jv, (const T*)gy, S);
-  else
-    hipLaunchKernelGGL((head::k_eq_head<T, 1>), g, b, smem, st, n, H, (const T*)x, (const T*)vec, W,
-                       (T*)y, (T*)jx, (T*)jv, (const T*)gy, S);
+  const bool vec4 = H % 8 == 0;  // every LDS offset / row length a multiple of 4
+#define TMD_HEAD_LAUNCH(NT_, V_)                                                                     \
+  hipLaunchKernelGGL((head::k_eq_head<T, NT_, V_>), g, b, smem, st, n, H, (const T*)x, (const T*)vec, W, \
+                     (T*)y, (T*)jx, (T*)jv, (const T*)gy, S)
+  if (vec4) {
+    if (nt == 4) TMD_HEAD_LAUNCH(4, true);
+    else if (nt == 2) TMD_HEAD_LAUNCH(2, true);
+    else TMD_HEAD_LAUNCH(1, true);
+  } else {
+    if (nt == 4) TMD_HEAD_LAUNCH(4, false);
+    else if (nt == 2) TMD_HEAD_LAUNCH(2, false);
+    else TMD_HEAD_LAUNCH(1, false);
+  }
+#undef TMD_HEAD_LAUNCH
   return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
 }
 
 extern "C" int tmdnet_eq_head_fwd(int dtype, int n_atoms, int hidden, const void* x, const void* vec,
                                   const void* const* weights, void* y, void* jac_x, void* jac_vec,
                                   void* stream) {
-  if (n_atoms < 0 || hidden < 2 || hidden % 2 || !x || !vec || !weights || !y) return kBadArgument;
+  if (n_atoms < 0 || hidden < 4 || hidden % 4 || !x || !vec || !weights || !y) return kBadArgument;
   if ((jac_x == nullptr) != (jac_vec == nullptr)) return kBadArgument;
   for (int i = 0; i < 12; ++i)
     if (!weights[i]) return kBadArgument;
   if (n_atoms == 0) return kOk;
   size_t smem = 0;
-  const int nt = head_tile(dtype, hidden, &smem);
+  const int nt = head_tile(dtype, hidden, n_atoms, &smem);
   if (nt == 0) return kUnsupported;
   hipStream_t st = (hipStream_t)stream;
   if (dtype == TMDNET_F32)
@@ -429,7 +511,7 @@ extern "C" int tmdnet_eq_head_bwd_weights(int dtype, int n_atoms, int hidden, co
                                           const void* vec, const void* const* weights,
                                           const void* grad_y, void* grad_x, void* grad_vec,
                                           void* const* saves, void* stream) {
-  if (n_atoms < 0 || hidden < 2 || hidden % 2 || !x || !vec || !weights || !grad_y || !grad_x ||
+  if (n_atoms < 0 || hidden < 4 || hidden % 4 || !x || !vec || !weights || !grad_y || !grad_x ||
       !grad_vec || !saves)
     return kBadArgument;
   for (int i = 0; i < 12; ++i)
@@ -438,7 +520,7 @@ extern "C" int tmdnet_eq_head_bwd_weights(int dtype, int n_atoms, int hidden, co
     if (!saves[i]) return kBadArgument;
   if (n_atoms == 0) return kOk;
   size_t smem = 0;
-  const int nt = head_tile(dtype, hidden, &smem);
+  const int nt = head_tile(dtype, hidden, n_atoms, &smem);
   if (nt == 0) return kUnsupported;
   hipStream_t st = (hipStream_t)stream;
   if (dtype == TMDNET_F32)

@@ -941,7 +941,7 @@ def eq_head_fusable(blocks):
         return False
     b1, b2 = blocks
     H = b1.vec1_proj.in_features
-    shapes_ok = (H % 2 == 0 and b1.out_channels == H // 2 and b2.out_channels == 1
+    shapes_ok = (H % 4 == 0 and b1.out_channels == H // 2 and b2.out_channels == 1
                  and b2.vec1_proj.in_features == H // 2
                  and b1.update_net[0].out_features == H and b2.update_net[0].out_features == H // 2)
     acts_ok = all(isinstance(b.update_net[1], torch.nn.SiLU) for b in blocks) \
