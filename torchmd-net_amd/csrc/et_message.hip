@@ -817,6 +817,33 @@ template <typename T> struct NbArgs {
   T* gx; T* gw; T* gC;
 };
 
+// Edge loop of the neighbour-embedding kernels: a row's src / C for up to 64 edges arrive in one
+// coalesced load and are broadcast by shuffle; NB_U edges are processed per step so their row loads
+// are in flight together (one edge at a time left these kernels latency-bound).
+constexpr int NB_U = 4;
+
+template <typename T, typename F>
+__device__ __forceinline__ void nb_edges(const NbArgs<T>& A, int row, F&& body) {
+  const int lane = lane_id();
+  const int b = min(A.row_ptr[row], A.cap), e = min(A.row_ptr[row + 1], A.cap);
+  for (int base = b; base < e; base += TMD_WAVE) {
+    const int cnt = min(TMD_WAVE, e - base);
+    const int s_l = lane < cnt ? A.src[base + lane] : -1;
+    const T c_l = lane < cnt ? A.C[base + lane] : T(0);
+    for (int q = 0; q < cnt; q += NB_U) {
+      int sq[NB_U];
+      T cq[NB_U];
+#pragma unroll
+      for (int u = 0; u < NB_U; ++u) {
+        sq[u] = __shfl(s_l, (q + u) & (TMD_WAVE - 1));
+        cq[u] = __shfl(c_l, (q + u) & (TMD_WAVE - 1));
+        if (q + u >= cnt) sq[u] = -1;  // past the row end
+      }
+      body(base + q, sq, cq);
+    }
+  }
+}
+
 template <typename T, int V>
 __global__ __launch_bounds__(256) void k_nb_fwd(NbArgs<T> A) {
   const int t = blockIdx.x * (blockDim.x / TMD_WAVE) + threadIdx.x / TMD_WAVE;
@@ -826,17 +853,23 @@ __global__ __launch_bounds__(256) void k_nb_fwd(NbArgs<T> A) {
   const int c0 = on ? lane * V : 0;
   T acc[V];
   zero(acc);
-  const int b = min(A.row_ptr[t], A.cap), e = min(A.row_ptr[t + 1], A.cap);
-  for (int k = b; k < e; ++k) {
-    const int s = A.src[k];
-    if (s == t) continue;
-    const T Ce = A.C[k];
-    T xs[V], wk[V];
-    ldv<T, V>(xs, A.x + (size_t)s * A.ldx + c0);
-    ldv<T, V>(wk, A.w + (size_t)k * A.ldw + c0);
+  nb_edges(A, t, [&](int k0, const int (&sq)[NB_U], const T (&cq)[NB_U]) {
+    T xs[NB_U][V], wk[NB_U][V];
 #pragma unroll
-    for (int i = 0; i < V; ++i) acc[i] += xs[i] * (wk[i] * Ce);
-  }
+    for (int u = 0; u < NB_U; ++u) {
+      const bool live = sq[u] >= 0 && sq[u] != t;
+      const int s = live ? sq[u] : t, k = live ? k0 + u : k0;
+      ldv<T, V>(xs[u], A.x + (size_t)s * A.ldx + c0);
+      ldv<T, V>(wk[u], A.w + (size_t)k * A.ldw + c0);
+      const T ce = live ? cq[u] : T(0);
+#pragma unroll
+      for (int i = 0; i < V; ++i) wk[u][i] *= ce;
+    }
+#pragma unroll
+    for (int u = 0; u < NB_U; ++u)
+#pragma unroll
+      for (int i = 0; i < V; ++i) acc[i] += xs[u][i] * wk[u][i];
+  });
   if (on) stv<T, V>(A.out + (size_t)t * A.H + c0, acc);
 }
 
@@ -850,28 +883,39 @@ __global__ __launch_bounds__(256) void k_nb_bwd_dst(NbArgs<T> A) {
   const int c0 = on ? lane * V : 0;
   T go[V];
   ldv<T, V>(go, A.gout + (size_t)t * A.H + c0);
-  const int b = min(A.row_ptr[t], A.cap), e = min(A.row_ptr[t + 1], A.cap);
-  for (int k = b; k < e; ++k) {
-    const int s = A.src[k];
-    T gw[V];
-    T gc = T(0);
-    if (s == t) {
-      zero(gw);
-    } else {
-      const T Ce = A.C[k];
-      T xs[V], wk[V];
-      ldv<T, V>(xs, A.x + (size_t)s * A.ldx + c0);
-      ldv<T, V>(wk, A.w + (size_t)k * A.ldw + c0);
+  nb_edges(A, t, [&](int k0, const int (&sq)[NB_U], const T (&cq)[NB_U]) {
+    T xs[NB_U][V], wk[NB_U][V], gc[NB_U];
+#pragma unroll
+    for (int u = 0; u < NB_U; ++u) {
+      const bool valid = sq[u] >= 0;
+      const bool live = valid && sq[u] != t;
+      const int s = live ? sq[u] : t, k = valid ? k0 + u : k0;
+      ldv<T, V>(xs[u], A.x + (size_t)s * A.ldx + c0);
+      ldv<T, V>(wk[u], A.w + (size_t)k * A.ldw + c0);
+    }
+#pragma unroll
+    for (int u = 0; u < NB_U; ++u) {
+      const bool valid = sq[u] >= 0;
+      const bool live = valid && sq[u] != t;
+      const T ce = live ? cq[u] : T(0);
+      T gw[V];
+      gc[u] = T(0);
 #pragma unroll
       for (int i = 0; i < V; ++i) {
-        gw[i] = go[i] * xs[i] * Ce;
-        gc += go[i] * xs[i] * wk[i];
+        gw[i] = go[i] * xs[u][i] * ce;
+        gc[u] += go[i] * xs[u][i] * wk[u][i];
       }
+      if (!live) gc[u] = T(0);
+      if (on && valid) stv<T, V>(A.gw + (size_t)(k0 + u) * A.H + c0, gw);
     }
-    gc = wave_sum(on ? gc : T(0));
-    if (on) stv<T, V>(A.gw + (size_t)k * A.H + c0, gw);
-    if (lane == 0) A.gC[k] = gc;
-  }
+#pragma unroll
+    for (int u = 0; u < NB_U; ++u) gc[u] = wave_sum(on ? gc[u] : T(0));
+    if (lane == 0) {
+#pragma unroll
+      for (int u = 0; u < NB_U; ++u)
+        if (sq[u] >= 0) A.gC[k0 + u] = gc[u];
+    }
+  });
 }
 
 // source pass: gx[j] = sum_{reverse edges j->m} gout[m] * w[e] * C[e]
@@ -884,17 +928,23 @@ __global__ __launch_bounds__(256) void k_nb_bwd_src(NbArgs<T> A) {
   const int c0 = on ? lane * V : 0;
   T acc[V];
   zero(acc);
-  const int b = min(A.row_ptr[j], A.cap), e = min(A.row_ptr[j + 1], A.cap);
-  for (int k = b; k < e; ++k) {
-    const int m = A.src[k];
-    if (m == j) continue;
-    const T Ce = A.C[k];
-    T gm[V], wk[V];
-    ldv<T, V>(gm, A.gout + (size_t)m * A.H + c0);
-    ldv<T, V>(wk, A.w + (size_t)k * A.ldw + c0);
+  nb_edges(A, j, [&](int k0, const int (&sq)[NB_U], const T (&cq)[NB_U]) {
+    T gm[NB_U][V], wk[NB_U][V];
 #pragma unroll
-    for (int i = 0; i < V; ++i) acc[i] += gm[i] * (wk[i] * Ce);
-  }
+    for (int u = 0; u < NB_U; ++u) {
+      const bool live = sq[u] >= 0 && sq[u] != j;
+      const int m = live ? sq[u] : j, k = live ? k0 + u : k0;
+      ldv<T, V>(gm[u], A.gout + (size_t)m * A.H + c0);
+      ldv<T, V>(wk[u], A.w + (size_t)k * A.ldw + c0);
+      const T ce = live ? cq[u] : T(0);
+#pragma unroll
+      for (int i = 0; i < V; ++i) wk[u][i] *= ce;
+    }
+#pragma unroll
+    for (int u = 0; u < NB_U; ++u)
+#pragma unroll
+      for (int i = 0; i < V; ++i) acc[i] += gm[u][i] * wk[u][i];
+  });
   if (on) stv<T, V>(A.gx + (size_t)j * A.H + c0, acc);
 }
 

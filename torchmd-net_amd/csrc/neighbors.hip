@@ -337,26 +337,44 @@ __device__ __forceinline__ V3<T> edge_grad(int e, const T* gd, const T* gr, cons
   return g;
 }
 
+// 16 lanes per atom stride over its CSR row; partial sums meet in a 16-lane xor-shuffle reduction
+// (fixed order: deterministic).  One thread per atom left ~40 us on a 600-atom batch (serial rows).
+constexpr int kNlLanes = 16;
+
+template <typename T>
+__device__ __forceinline__ T group_sum16(T v) {
+#pragma unroll
+  for (int off = kNlLanes / 2; off > 0; off >>= 1) v += __shfl_xor(v, off, kNlLanes);
+  return v;
+}
+
 template <typename T>
 __global__ void k_nl_backward(int n, const int* __restrict__ row_ptr, const int32_t* __restrict__ tr,
                               int cap, const T* __restrict__ gd, const T* __restrict__ gr,
                               const T* __restrict__ dl, const T* __restrict__ r, T* __restrict__ gpos) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= n) return;
-  const int b = min(row_ptr[t], cap), e = min(row_ptr[t + 1], cap);
+  const int gt = blockIdx.x * blockDim.x + threadIdx.x;
+  const int t = gt / kNlLanes, lane = gt % kNlLanes;
   V3<T> acc{T(0), T(0), T(0)};
-  for (int k = b; k < e; ++k) {
-    const V3<T> gm = edge_grad(k, gd, gr, dl, r);
-    acc.x -= gm.x; acc.y -= gm.y; acc.z -= gm.z;
-    const int k2 = tr[k];
-    if (k2 >= 0) {
-      const V3<T> gp = edge_grad(k2, gd, gr, dl, r);
-      acc.x += gp.x; acc.y += gp.y; acc.z += gp.z;
+  if (t < n) {
+    const int b = min(row_ptr[t], cap), e = min(row_ptr[t + 1], cap);
+    for (int k = b + lane; k < e; k += kNlLanes) {
+      const V3<T> gm = edge_grad(k, gd, gr, dl, r);
+      acc.x -= gm.x; acc.y -= gm.y; acc.z -= gm.z;
+      const int k2 = tr[k];
+      if (k2 >= 0) {
+        const V3<T> gp = edge_grad(k2, gd, gr, dl, r);
+        acc.x += gp.x; acc.y += gp.y; acc.z += gp.z;
+      }
     }
   }
-  gpos[3 * t + 0] = acc.x;
-  gpos[3 * t + 1] = acc.y;
-  gpos[3 * t + 2] = acc.z;
+  acc.x = group_sum16(acc.x);
+  acc.y = group_sum16(acc.y);
+  acc.z = group_sum16(acc.z);
+  if (t < n && lane == 0) {
+    gpos[3 * t + 0] = acc.x;
+    gpos[3 * t + 1] = acc.y;
+    gpos[3 * t + 2] = acc.z;
+  }
 }
 
 // Second order of k_nl_backward (the double backward of NeighborAutograd's index_add pair,
@@ -386,34 +404,41 @@ __global__ void k_nl_backward2(int n, const int* __restrict__ row_ptr, const int
                                const T* __restrict__ dl, const T* __restrict__ r,
                                const T* __restrict__ gg, T* __restrict__ dpos, T* __restrict__ dgd,
                                T* __restrict__ dgr) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= n) return;
-  const int b = min(row_ptr[t], cap), e = min(row_ptr[t + 1], cap);
-  const V3<T> gt{gg[3 * t + 0], gg[3 * t + 1], gg[3 * t + 2]};
+  const int gt = blockIdx.x * blockDim.x + threadIdx.x;
+  const int t = gt / kNlLanes, lane = gt % kNlLanes;
   V3<T> acc{T(0), T(0), T(0)};
-  for (int k = b; k < e; ++k) {
-    const int s = src[k];
-    const V3<T> w{gg[3 * s + 0] - gt.x, gg[3 * s + 1] - gt.y, gg[3 * s + 2] - gt.z};
-    T uw;
-    const V3<T> dm = edge_grad2(k, w, gr, dl, r, uw);
-    acc.x -= dm.x; acc.y -= dm.y; acc.z -= dm.z;
-    if (dgd) {
-      const bool live = r[k] != T(0);
-      dgd[3 * k + 0] = live ? w.x : T(0);
-      dgd[3 * k + 1] = live ? w.y : T(0);
-      dgd[3 * k + 2] = live ? w.z : T(0);
-    }
-    if (dgr) dgr[k] = uw;
-    const int k2 = tr[k];
-    if (k2 >= 0) {
-      T uw2;
-      const V3<T> dp = edge_grad2(k2, V3<T>{-w.x, -w.y, -w.z}, gr, dl, r, uw2);
-      acc.x += dp.x; acc.y += dp.y; acc.z += dp.z;
+  if (t < n) {
+    const int b = min(row_ptr[t], cap), e = min(row_ptr[t + 1], cap);
+    const V3<T> gt3{gg[3 * t + 0], gg[3 * t + 1], gg[3 * t + 2]};
+    for (int k = b + lane; k < e; k += kNlLanes) {
+      const int s = src[k];
+      const V3<T> w{gg[3 * s + 0] - gt3.x, gg[3 * s + 1] - gt3.y, gg[3 * s + 2] - gt3.z};
+      T uw;
+      const V3<T> dm = edge_grad2(k, w, gr, dl, r, uw);
+      acc.x -= dm.x; acc.y -= dm.y; acc.z -= dm.z;
+      if (dgd) {
+        const bool live = r[k] != T(0);
+        dgd[3 * k + 0] = live ? w.x : T(0);
+        dgd[3 * k + 1] = live ? w.y : T(0);
+        dgd[3 * k + 2] = live ? w.z : T(0);
+      }
+      if (dgr) dgr[k] = uw;
+      const int k2 = tr[k];
+      if (k2 >= 0) {
+        T uw2;
+        const V3<T> dp = edge_grad2(k2, V3<T>{-w.x, -w.y, -w.z}, gr, dl, r, uw2);
+        acc.x += dp.x; acc.y += dp.y; acc.z += dp.z;
+      }
     }
   }
-  dpos[3 * t + 0] = acc.x;
-  dpos[3 * t + 1] = acc.y;
-  dpos[3 * t + 2] = acc.z;
+  acc.x = group_sum16(acc.x);
+  acc.y = group_sum16(acc.y);
+  acc.z = group_sum16(acc.z);
+  if (t < n && lane == 0) {
+    dpos[3 * t + 0] = acc.x;
+    dpos[3 * t + 1] = acc.y;
+    dpos[3 * t + 2] = acc.z;
+  }
 }
 
 // ---------------------------------------------------------------- host side
@@ -593,7 +618,7 @@ extern "C" int tmdnet_nl_backward(int dtype, int n_atoms, const int32_t* row_ptr
                                   void* stream) {
   hipStream_t st = (hipStream_t)stream;
   const int tb = 256;
-  dim3 g((n_atoms + tb - 1) / tb);
+  dim3 g((unsigned)(((size_t)n_atoms * nl::kNlLanes + tb - 1) / tb));
   if (dtype == TMDNET_F32)
     hipLaunchKernelGGL(nl::k_nl_backward<float>, g, dim3(tb), 0, st, n_atoms, row_ptr, transpose_map,
                        max_pairs, (const float*)grad_deltas, (const float*)grad_distances,
@@ -620,7 +645,7 @@ extern "C" int tmdnet_nl_backward2(int dtype, int n_atoms, const int32_t* row_pt
   if (d_grad_deltas) TMD_CHECK(hipMemsetAsync(d_grad_deltas, 0, es * 3 * (size_t)max_pairs, st));
   if (d_grad_distances) TMD_CHECK(hipMemsetAsync(d_grad_distances, 0, es * (size_t)max_pairs, st));
   const int tb = 256;
-  dim3 g((n_atoms + tb - 1) / tb);
+  dim3 g((unsigned)(((size_t)n_atoms * nl::kNlLanes + tb - 1) / tb));
   if (dtype == TMDNET_F32)
     hipLaunchKernelGGL(nl::k_nl_backward2<float>, g, dim3(tb), 0, st, n_atoms, row_ptr, src, transpose_map,
                        max_pairs, (const float*)grad_distances, (const float*)deltas,
