@@ -165,6 +165,22 @@ int tmdnet_et_epilogue_bwd(int dtype, int n_nodes, int hidden, const void* grad_
                            const void* grad_vec, const void* vecp, const void* o, void* grad_vecp,
                            void* grad_o, void* stream);
 
+/* Epilogue of layer l fused with the LayerNorm of layer l+1 (torchmd_et.py:262; biased variance,
+ * rstd = 1/sqrt(var + eps), as torch.native_layer_norm).  o == NULL: LayerNorm only (of x; x_out,
+ * vec_out unused).  ln_w == NULL: epilogue only.  xn [N][H], mean [N], rstd [N]. */
+int tmdnet_et_epilogue_ln_fwd(int dtype, int n_nodes, int hidden, const void* x, const void* vec,
+                              const void* vecp, const void* o, const void* vec_agg, const void* ln_w,
+                              const void* ln_b, double eps, void* x_out, void* vec_out, void* xn,
+                              void* mean, void* rstd, void* stream);
+/* grad_x = grad_res + LayerNorm backward of grad_xn (input x, saved mean / rstd, weight ln_w; no
+ * weight gradients); when o != NULL, then the epilogue backward of the previous layer with
+ * (grad_x, grad_vec, vecp, o) -> grad_vecp, grad_o (as tmdnet_et_epilogue_bwd; vecp NULL = first
+ * layer). */
+int tmdnet_ln_bwd_epilogue(int dtype, int n_nodes, int hidden, const void* grad_xn, const void* x,
+                           const void* mean, const void* rstd, const void* ln_w, const void* grad_res,
+                           void* grad_x, const void* grad_vec, const void* vecp, const void* o,
+                           void* grad_vecp, void* grad_o, void* stream);
+
 /* ------------------------------------------------------------------------------------------
  * EquivariantScalar output head (reference models/output_modules.py:80-115 with two
  * GatedEquivariantBlocks, models/utils.py:456-522: H -> H/2 with scalar SiLU, then H/2 -> 1;

@@ -104,6 +104,26 @@ def _fake_epi_bwd(gx, gvec, vecp, o, g_vecp, g_o):
     g_vecp[..., 2 * H:] = gvec * o1.unsqueeze(1)
 
 
+def _fake_epi_ln(x, vec, vecp, o, veca, ln_w, ln_b):
+    """tmdnet_et_epilogue_ln_fwd restated: epilogue (if o) then the next layer's LayerNorm."""
+    xo = vo = None
+    if o is not None:
+        xo, vo = _fake_epi_fwd(x, vec, vecp, o, veca)
+        x = xo
+    xn, mean, rstd = torch.native_layer_norm(x, [x.shape[1]], ln_w, ln_b, ES._EPS)
+    return xo, vo, xn, mean, rstd
+
+
+def _fake_ln_bwd_epi(g_xn, x, mean, rstd, ln_w, g_res, g_vec, vecp, o, g_vecp, g_o):
+    """tmdnet_ln_bwd_epilogue restated: residual + LayerNorm backward, then the previous epilogue."""
+    g_x, _, _ = torch.ops.aten.native_layer_norm_backward(g_xn, x, [x.shape[1]], mean, rstd, ln_w, None,
+                                                          [True, False, False])
+    g_x = g_x + g_res
+    if o is not None:
+        _fake_epi_bwd(g_x, g_vec, vecp, o, g_vecp, g_o)
+    return g_x
+
+
 def _fake_bwd2(ctx, ggs):
     return kernels._ETMessageBwd.composite_backward(ctx, *ggs)
 
@@ -115,6 +135,8 @@ def emulated(monkeypatch):
     monkeypatch.setattr(kernels, "et_message_bwd2", _fake_bwd2)
     monkeypatch.setattr(ES, "_epilogue_fwd", _fake_epi_fwd)
     monkeypatch.setattr(ES, "_epilogue_bwd", _fake_epi_bwd)
+    monkeypatch.setattr(ES, "_epi_ln", _fake_epi_ln)
+    monkeypatch.setattr(ES, "_ln_bwd_epi", _fake_ln_bwd_epi)
 
 
 def _system(n_mol=3, seed=0, cutoff=4.0):

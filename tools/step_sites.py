@@ -19,7 +19,8 @@ z, pos, batch = z.to(dev), pos.float().to(dev), batch.to(dev)
 for _ in range(4):
     y, f = model(z, pos, batch)
 torch.cuda.synchronize()
-with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True) as prof:
+with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True,
+             record_shapes=True) as prof:
     y, f = model(z, pos, batch)
     torch.cuda.synchronize()
 prof.export_chrome_trace(sys.argv[1])

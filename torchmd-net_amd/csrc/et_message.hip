@@ -14,6 +14,8 @@
 //     that walks the same CSR rows as reversed edges (valid for the symmetric lists the model
 //     builds: dk, dv, cutoff are functions of |r| only and unit vectors flip sign), giving
 //     gk, gv, gvec without a transpose scatter or atomics.
+#include <cstdlib>
+
 #include "common.h"
 #include "tmdnet.h"
 
@@ -976,6 +978,7 @@ static int launch_v(int V, int n, AT A, hipStream_t st) {
 // S = 4 so that e.g. a 678-atom QM9 batch still puts ~2.7k waves on the 256 CUs).
 static inline int et_waves_per_node(int n, int bytes_per_lane_vec) {
   if (bytes_per_lane_vec > 32) return 1;
+  if (const char* e = getenv("TMDNET_ET_S")) return atoi(e) >= 4 ? 4 : atoi(e) >= 2 ? 2 : 1;  // tuning
   if (n < 4096) return 4;
   if (n < 8192) return 2;
   return 1;
@@ -1093,7 +1096,8 @@ static int bwd(int n, int H, int heads, const int32_t* row_ptr, const int32_t* s
   A.gpk = (T*)gpk; A.gpv = (T*)gpv; A.gC = (T*)gC; A.gu = (T*)gu;
   A.acc = acc;
   if (acc & TMDNET_ET_V_PLANAR) { A.planar = 1; A.vst = H; }
-  if (n < kBwdFuseNodes) return et_launch<T, 3, false>(V, A, st);
+  static const int fuse_nodes = getenv("TMDNET_ET_FUSE") ? atoi(getenv("TMDNET_ET_FUSE")) : kBwdFuseNodes;
+  if (n < fuse_nodes) return et_launch<T, 3, false>(V, A, st);
   rc = et_launch<T, 1, false>(V, A, st);
   if (rc) return rc;
   return et_launch<T, 2, false>(V, A, st);

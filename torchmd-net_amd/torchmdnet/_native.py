@@ -41,6 +41,8 @@ SIGNATURES = {
                                    P, P, P, P, P, I, P, I, P, P, P, P, P, P, P, P, P, P, P, P, I, P]),
     "tmdnet_et_epilogue_fwd": (I, [I, I, I, P, P, P, P, P, P, P, P]),
     "tmdnet_et_epilogue_bwd": (I, [I, I, I, P, P, P, P, P, P, P]),
+    "tmdnet_et_epilogue_ln_fwd": (I, [I, I, I, P, P, P, P, P, P, P, D, P, P, P, P, P, P]),
+    "tmdnet_ln_bwd_epilogue": (I, [I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P]),
     "tmdnet_eq_head_fwd": (I, [I, I, I, P, P, P, P, P, P, P]),
     "tmdnet_eq_head_bwd": (I, [I, I, I, P, P, P, P, P, P]),
     "tmdnet_eq_head_bwd_weights": (I, [I, I, I, P, P, P, P, P, P, P, P]),

@@ -224,6 +224,38 @@ def _epilogue_bwd(gx, gvec, vecp, o, g_vecp, g_o):
     nat.check(rc, "tmdnet_et_epilogue_bwd")
 
 
+def _epi_ln(x, vec, vecp, o, veca, ln_w, ln_b):
+    """tmdnet_et_epilogue_ln_fwd: this layer's epilogue (o not None) and the next layer's LayerNorm
+    in one pass.  Returns (x_out, vec_out, xn, mean, rstd); o None: LayerNorm of x only."""
+    lib = nat.load()
+    N, H = x.shape
+    xo = torch.empty_like(x) if o is not None else None
+    vo = torch.empty_like(veca) if o is not None else None
+    xn = torch.empty_like(x)
+    mean = torch.empty((N, 1), dtype=x.dtype, device=x.device)
+    rstd = torch.empty((N, 1), dtype=x.dtype, device=x.device)
+    rc = lib.tmdnet_et_epilogue_ln_fwd(nat.dtype_code(x.dtype), N, H, nat.ptr(x), nat.ptr(vec), nat.ptr(vecp),
+                                       nat.ptr(o), nat.ptr(veca), nat.ptr(ln_w), nat.ptr(ln_b), _EPS,
+                                       nat.ptr(xo), nat.ptr(vo), nat.ptr(xn), nat.ptr(mean), nat.ptr(rstd),
+                                       nat.stream(x.device))
+    nat.check(rc, "tmdnet_et_epilogue_ln_fwd")
+    return xo, vo, xn, mean, rstd
+
+
+def _ln_bwd_epi(g_xn, x, mean, rstd, ln_w, g_res, g_vec, vecp, o, g_vecp, g_o):
+    """tmdnet_ln_bwd_epilogue: g_x = g_res + LayerNorm backward (no weight gradients), then the
+    previous layer's epilogue backward into g_vecp / g_o (o None: skipped)."""
+    lib = nat.load()
+    N, H = x.shape
+    g_x = torch.empty_like(g_res)
+    rc = lib.tmdnet_ln_bwd_epilogue(nat.dtype_code(x.dtype), N, H, nat.ptr(g_xn), nat.ptr(x), nat.ptr(mean),
+                                    nat.ptr(rstd), nat.ptr(ln_w), nat.ptr(g_res), nat.ptr(g_x), nat.ptr(g_vec),
+                                    nat.ptr(vecp), nat.ptr(o), nat.ptr(g_vecp), nat.ptr(g_o),
+                                    nat.stream(x.device))
+    nat.check(rc, "tmdnet_ln_bwd_epilogue")
+    return g_x
+
+
 def _forward_layers(meta, x, f, C, u, params):
     """HIP/GEMM forward; returns outputs and the per-layer activations the backward needs."""
     H = meta.H
@@ -233,12 +265,13 @@ def _forward_layers(meta, x, f, C, u, params):
     D = meta.D
     meta.refresh_effective()
     pkv_all = torch.addmm(meta.dkv_eff[1], f, meta.dkv_eff[0].t()) if (meta.batched and D) else None
-    for l, p in enumerate(meta.split(params)):
-        ln_w, ln_b = p[0], p[1]
+    layers = meta.split(params)
+    # layer l's LayerNorm is computed by layer l-1's epilogue kernel (layer 0: LayerNorm alone)
+    _, _, xn, mean, rstd = _epi_ln(x, None, None, None, None, layers[0][0], layers[0][1])
+    for l, p in enumerate(layers):
         vec_w, o_w, o_b = p[8], p[9], p[10]
         qkv_w, qkv_b = meta.qkv_eff[l]
         dkv_w, dkv_b = meta.dkv_layer(l)
-        xn, mean, rstd = torch.native_layer_norm(x, [H], ln_w, ln_b, _EPS)
         qkv = torch.addmm(qkv_b, xn, qkv_w.t())
         vecp = None if vec is None else torch.mm(vec.view(3 * N, H), vec_w.t()).view(N, 3, 3 * H)
         if pkv_all is not None:
@@ -252,9 +285,11 @@ def _forward_layers(meta, x, f, C, u, params):
         kernels.et_message_fwd_launch(qkv[:, :H], qkv[:, H:2 * H], qkv[:, 2 * H:], vec, pk, pv, C, u,
                                       meta.graph, meta.heads, xa, veca, meta.flags)
         o = torch.addmm(o_b, xa, o_w.t())
-        x_new, vec_new = _epilogue_fwd(x, vec, vecp, o, veca)
         acts.append((x, vec, xn, mean, rstd, qkv, vecp, pkv, xa, o))
-        x, vec = x_new, vec_new
+        if l + 1 < len(layers):
+            x, vec, xn, mean, rstd = _epi_ln(x, vec, vecp, o, veca, layers[l + 1][0], layers[l + 1][1])
+        else:
+            x, vec = _epilogue_fwd(x, vec, vecp, o, veca)
     return x, vec, acts
 
 
@@ -279,6 +314,7 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws):
     gvec_bufs = [torch.empty((N, 3, H), **o), torch.empty((N, 3, H), **o)]
     layers = meta.split(params)
     g_params = [None] * len(params)
+    epi_done = False  # this layer's epilogue backward already ran (fused into the next layer's LN bwd)
     for l in reversed(range(meta.n_layers)):
         p = layers[l]
         x, vec, xn, mean, rstd, qkv, vecp, pkv, xa, o_ = acts[l]
@@ -288,7 +324,8 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws):
         dkv_w, _ = meta.dkv_layer(l)
         if has_e:
             g_pkv = g_pkv_all[:, l * D:(l + 1) * D] if meta.batched else g_pkv_all
-        _epilogue_bwd(gX, gV, vecp, o_, g_vecp, g_o)
+        if not epi_done:
+            _epilogue_bwd(gX, gV, vecp, o_, g_vecp, g_o)
         g_xa = torch.mm(g_o, o_w)
         pk = pkv[:, :H] if meta.hk else None
         pv = pkv[:, H * int(meta.hk):] if meta.hv else None
@@ -308,9 +345,16 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws):
             g_vec_in.view(3 * N, H).addmm_(g_vecp.view(3 * N, 3 * H), vec_w)
         g_xn = torch.mm(g_qkv, qkv_w)
         need_w = need_ws[l]
-        g_x, g_lnw, g_lnb = torch.ops.aten.native_layer_norm_backward(g_xn, x, [H], mean, rstd, ln_w, ln_b,
-                                                             [True, need_w, need_w])
-        g_x.add_(gX)
+        if need_w:  # LayerNorm weight gradients: PyTorch's backward
+            g_x, g_lnw, g_lnb = torch.ops.aten.native_layer_norm_backward(g_xn, x, [H], mean, rstd, ln_w, ln_b,
+                                                                 [True, True, True])
+            g_x.add_(gX)
+            epi_done = False
+        else:  # LayerNorm backward + residual + the previous layer's epilogue backward, one kernel
+            prev = acts[l - 1] if l > 0 else None
+            g_x = _ln_bwd_epi(g_xn, x, mean, rstd, ln_w, gX, g_vec_in,
+                              prev[6] if prev else None, prev[9] if prev else None, g_vecp, g_o)
+            epi_done = prev is not None
         if need_w:
             base = l * meta.np
             g_qkv_w = torch.mm(g_qkv.t(), xn)
