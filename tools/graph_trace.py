@@ -1,0 +1,38 @@
+"""Graph-replayed ET-QM9 energy+force steps (the bench workload) bracketed by marker kernels, for
+rocprofv3 --kernel-trace (tools/trace_summary.py lists the kernels of the marked replay).
+usage: graph_trace.py [et|tn]"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "torchmd-net_amd"), ROOT]
+import torch  # noqa: E402
+import yaml  # noqa: E402
+
+from bench import et_args, qm9_like  # noqa: E402
+from torchmdnet.graphs import GraphedEnergyForces  # noqa: E402
+from torchmdnet.models.model import create_model  # noqa: E402
+
+dev = torch.device("cuda", 0)
+torch.manual_seed(0)
+which = sys.argv[1] if len(sys.argv) > 1 else "et"
+if which == "et":
+    model = create_model(et_args(128)).to(dev)
+    z, pos, batch = qm9_like(32, 1)
+else:
+    from bench import rmd17_like
+    with open(os.path.join(ROOT, "tests", "golden", "configs", "tensornet_rmd17.yaml")) as f:
+        args = yaml.safe_load(f)
+    args.update(prior_model=None, precision=32, derivative=True)
+    model = create_model(args).to(dev)
+    z, pos, batch = rmd17_like(8, 1)
+z, pos, batch = z.to(dev), pos.float().to(dev), batch.to(dev)
+gm = GraphedEnergyForces(model, z, pos, batch)
+for _ in range(5):
+    gm(pos)
+torch.cuda.synchronize()
+torch.cuda._sleep(100)
+gm(pos)
+torch.cuda._sleep(100)
+torch.cuda.synchronize()
+gm.release()
