@@ -222,38 +222,80 @@ int tmdnet_nbr_embed_bwd(int dtype, int n_nodes, int hidden, const int32_t* row_
                          void* gcut, void* stream);
 
 /* ------------------------------------------------------------------------------------------
- * TensorNet edge kernels (reference models/tensornet.py:287-332).  Tensors are [N][H][3][3].
- * self0_mult >= 1: multiplicity of atom 0's self loop (static_shapes padding emulation,
+ * TensorNet edge kernels (reference models/tensornet.py:287-332).
+ * Tensors are COMPACT and component-major, [9][N][H]: per channel the coefficients
+ * c = [i, a01, a02, a12, s00, s11, s01, s02, s12] of X = i Id + A + S (A antisymmetric, S symmetric
+ * traceless; reference decompose_tensor, tensornet.py:47-52), rows 0 / 1-3 / 4-8 being the I / A / S
+ * parts.  self0_mult >= 1: multiplicity of atom 0's self loop (static_shapes padding emulation,
  * tensornet.py:215-221; 1 = no padding).  If pad_pairs (device int32, the pair count found by
  * tmdnet_nl_build) is non-NULL the multiplicity is computed on the device instead:
  * 1 + max(0, pad_capacity - *pad_pairs) (no host sync: HIP-graph capturable).  Both require the
  * symmetric CSR list.
- * Embedding:  I/A/S[n] = sum_{edges e with reference edge_index[0]==n} (P[n] + Q[dst]) * W_k[e] * C[e]
- *             * {Id, skew(u[e]), sym(u[e])},  W = [E][3H] = distance_proj1|2|3(rbf) (pre-cutoff),
- *             P = emb(z) Wa^T + b, Q = emb(z) Wb^T  (emb2 split into its two input halves). */
+ * Embedding (replaces TensorEmbedding._get_tensor_messages + the scatter, tensornet.py:295-315):
+ *   I/A/S[n] = sum_{edges e with reference edge_index[0]==n} (P[n] + Q[dst]) * W_k[e] * C[e]
+ *              * {Id, skew(u[e]), sym(u[e])},  W = [E][3H] = distance_proj1|2|3(rbf) (pre-cutoff),
+ *   P = emb(z) Wa^T + b, Q = emb(z) Wb^T  (emb2 split into its two input halves); out [9][N][H]. */
 int tmdnet_tn_embed_fwd(int dtype, int n_nodes, int hidden, const int32_t* row_ptr,
                         const int32_t* src, int max_pairs, double self0_mult,
                         const int32_t* pad_pairs, int pad_capacity, const void* P,
                         const void* Q, const void* W, int ld_w, const void* cutoff, const void* unit,
-                        void* I, void* A, void* S, void* stream);
+                        void* out, void* stream);
+/* Backward: gP, gQ [N][H], gW [E][3H], gcut [E], gunit [E][3] from grad_out [9][N][H]; overwritten. */
 int tmdnet_tn_embed_bwd(int dtype, int n_nodes, int hidden, const int32_t* row_ptr,
                         const int32_t* src, int max_pairs, double self0_mult,
                         const int32_t* pad_pairs, int pad_capacity, const void* P,
                         const void* Q, const void* W, int ld_w, const void* cutoff, const void* unit,
-                        const void* gI, const void* gA, const void* gS, void* gP, void* gQ, void* gW,
-                        void* gcut, void* gunit, void* stream);
-/* Message: msg[n] = sum_{edges e with edge_index[0]==n} ea[e,h,0] I[m] + ea[e,h,1] A[m] + ea[e,h,2] S[m],
- * m = edge_index[1][e]; edge_attr [E][3H] interleaved (h, component) as reshape(E, H, 3). */
+                        const void* grad_out, void* gP, void* gQ, void* gW, void* gcut, void* gunit,
+                        void* stream);
+/* Message (replaces tensor_message_passing, tensornet.py:329-332):
+ *   msg[n] = sum_{edges e with edge_index[0]==n} ea[e,h,0] I[m] + ea[e,h,1] A[m] + ea[e,h,2] S[m],
+ * m = edge_index[1][e]; edge_attr [E][3H] interleaved (h, component) as reshape(E, H, 3);
+ * comp and msg [9][N][H] (the message of compact tensors is compact). */
 int tmdnet_tn_message_fwd(int dtype, int n_nodes, int hidden, const int32_t* row_ptr,
                           const int32_t* src, int max_pairs, double self0_mult,
                           const int32_t* pad_pairs, int pad_capacity, const void* edge_attr,
-                          int ld_ea, const void* I, const void* A, const void* S, void* msg,
-                          void* stream);
+                          int ld_ea, const void* comp, void* msg, void* stream);
+/* Backward: g_edge_attr [E][3H] (destination pass), g_comp [9][N][H] (source pass); overwritten. */
 int tmdnet_tn_message_bwd(int dtype, int n_nodes, int hidden, const int32_t* row_ptr,
                           const int32_t* src, int max_pairs, double self0_mult,
                           const int32_t* pad_pairs, int pad_capacity, const void* edge_attr,
-                          int ld_ea, const void* I, const void* A, const void* S, const void* grad_msg,
-                          void* g_edge_attr, void* gI, void* gA, void* gS, void* stream);
+                          int ld_ea, const void* comp, const void* grad_msg, void* g_edge_attr,
+                          void* g_comp, void* stream);
+
+/* TensorNet per-channel node algebra, one fused pass each (replaces the reference's elementwise
+ * PyTorch chains).  X / "full" tensors are [N][H][3][3]; compact ones [9][N][H] as above.
+ *   op                 a            b             out
+ *   TN_PRE             X            -             decomp(X / (|X|^2+1))          tensornet.py:391-392
+ *   TN_POST_O3         Y (compact)  msg (compact) decomp(Z)/(|Z|^2+1), Z=msg Y+Y msg  tensornet.py:398-406
+ *   TN_POST_SO3        Y            msg           same, Z = 2 Y msg
+ *   TN_RESID           X            D (compact)   X/(|X|^2+1) + D + D D           tensornet.py:391,410
+ *   TN_NORMS           X            -             [N][3H] = (|I|^2 | |A|^2 | |S|^2)  tensornet.py:230-231
+ *   TN_ENORM           c (compact)  -             [N][H] = |I+A+S|^2              tensornet.py:317
+ *   TN_EOUT            c (compact)  f [N][H][3]   f_I I + f_A A + f_S S  (full)   tensornet.py:321-326
+ * Backward: ga / gb = VJP w.r.t. a / b from grad_out (same layouts as a / b / out); grad_add
+ * (optional, layout of a) is added to ga. */
+#define TMDNET_TN_PRE 0
+#define TMDNET_TN_POST_O3 1
+#define TMDNET_TN_POST_SO3 2
+#define TMDNET_TN_RESID 3
+#define TMDNET_TN_NORMS 4
+#define TMDNET_TN_ENORM 5
+#define TMDNET_TN_EOUT 6
+int tmdnet_tn_node_fwd(int dtype, int op, int n_nodes, int hidden, const void* a, const void* b,
+                       void* out, void* stream);
+int tmdnet_tn_node_bwd(int dtype, int op, int n_nodes, int hidden, const void* a, const void* b,
+                       const void* grad_out, const void* grad_add, void* ga, void* gb,
+                       void* stream);
+
+/* SiLU with an optional per-row scale (TensorNet edge MLP `act(linear(.)) * C`,
+ * tensornet.py:385-389; the scalar MLPs of the embedding, output and Scalar head).
+ *   out[r][c] = silu(x[r][c]) * (row_scale ? row_scale[r] : 1)     (x row stride ld_x, out dense)
+ * Backward: grad_x[r][c] = grad_out[r][c] * row_scale[r] * silu'(x[r][c]) (dense);
+ *           grad_scale[r] = sum_c grad_out[r][c] * silu(x[r][c]) (optional). */
+int tmdnet_silu_fwd(int dtype, int rows, int cols, const void* x, int ld_x, const void* row_scale,
+                    void* out, void* stream);
+int tmdnet_silu_bwd(int dtype, int rows, int cols, const void* x, int ld_x, const void* row_scale,
+                    const void* grad_out, int ld_g, void* grad_x, void* grad_scale, void* stream);
 
 /* Library identification (for load checks). */
 const char* tmdnet_build_info(void);

@@ -28,7 +28,8 @@ def test_header_declares_entry_points():
     for name in ("tmdnet_nl_build", "tmdnet_nl_backward", "tmdnet_edge_geom_fwd", "tmdnet_edge_geom_bwd",
                  "tmdnet_et_message_fwd", "tmdnet_et_message_bwd", "tmdnet_nbr_embed_fwd",
                  "tmdnet_nbr_embed_bwd", "tmdnet_tn_embed_fwd", "tmdnet_tn_embed_bwd",
-                 "tmdnet_tn_message_fwd", "tmdnet_tn_message_bwd", "tmdnet_nl_workspace_bytes",
+                 "tmdnet_tn_message_fwd", "tmdnet_tn_message_bwd", "tmdnet_tn_node_fwd", "tmdnet_tn_node_bwd", "tmdnet_silu_fwd", "tmdnet_silu_bwd",
+                 "tmdnet_nl_workspace_bytes",
                  "tmdnet_build_info"):
         assert name in d, name
 

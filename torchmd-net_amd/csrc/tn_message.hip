@@ -10,71 +10,27 @@
 //     I[n] += Zij W1 C Id,  A[n] += Zij W2 C skew(u(n->m)),  S[n] += Zij W3 C sym(u(n->m)),
 //     with u(n->m) = -u(e') for the row edge e' = m->n and W, C functions of |r| only;
 //   * message:    msg[n] += ea(e',h,0) I[m] + ea(e',h,1) A[m] + ea(e',h,2) S[m].
-// Tensors are (N, H, 3, 3) row-major: a lane owns one channel's 9 contiguous values.
+//
+// Layout: COMPACT and component-major, [9][N][H] (tn_node.h): row 0 the isotropic coefficient i
+// (I = i Id), rows 1-3 the antisymmetric part (a01, a02, a12), rows 4-8 the symmetric traceless
+// part (s00, s11, s01, s02, s12).  I, A, S of one channel are disjoint rows of one buffer, the
+// channel mixes of the reference (tensornet.py:318-320, 354-356) are plain GEMMs over those rows,
+// and a lane's 9 loads are 9 coalesced 256-byte row segments (the reference's [N][H][3][3] I, A,
+// S tensors are 27 values per channel, 18 of them redundant).
 // `mult0` (>= 1) is the multiplicity of atom 0's self loop: the reference's static_shapes mode
 // turns every (-1,-1) padding slot of the CUDA neighbour list into an extra (0,0) edge with r = 0
 // (tensornet.py:215-221), i.e. (max_num_pairs - num_pairs) more copies of that self loop.
 // Backward = destination pass (own outputs + per-edge grads) + source pass (gathered inputs' grads).
 #include "common.h"
 #include "tmdnet.h"
+#include "tn_node.h"
 
 namespace tmd {
 namespace tn {
 
-template <typename T> struct M3 {
-  T v[9];
-};
-
-template <typename T> __device__ __forceinline__ void ld9(T (&o)[9], const T* p) {
-#pragma unroll
-  for (int i = 0; i < 9; ++i) o[i] = p[i];
-}
-template <typename T> __device__ __forceinline__ void st9(T* p, const T (&o)[9]) {
-#pragma unroll
-  for (int i = 0; i < 9; ++i) p[i] = o[i];
-}
-
-// skew(v) = [[0,-v2,v1],[v2,0,-v0],[-v1,v0,0]]  (tensornet.py:16-34)
-template <typename T> __device__ __forceinline__ void skew(T (&m)[9], T x, T y, T z) {
-  m[0] = T(0); m[1] = -z; m[2] = y;
-  m[3] = z; m[4] = T(0); m[5] = -x;
-  m[6] = -y; m[7] = x; m[8] = T(0);
-}
-// sym(v) = v v^T - |v|^2/3 Id  (tensornet.py:37-44)
-template <typename T> __device__ __forceinline__ void symm(T (&m)[9], T x, T y, T z) {
-  const T tr = (x * x + y * y + z * z) / T(3);
-  m[0] = x * x - tr; m[1] = x * y; m[2] = x * z;
-  m[3] = y * x; m[4] = y * y - tr; m[5] = y * z;
-  m[6] = z * x; m[7] = z * y; m[8] = z * z - tr;
-}
-// d<G, skew(v)>/dv
-template <typename T> __device__ __forceinline__ void dskew(const T (&g)[9], T& dx, T& dy, T& dz) {
-  dx = g[7] - g[5];
-  dy = g[2] - g[6];
-  dz = g[3] - g[1];
-}
-// d<G, sym(v)>/dv = (G + G^T) v - 2 v tr(G) / 3
-template <typename T>
-__device__ __forceinline__ void dsymm(const T (&g)[9], T x, T y, T z, T& dx, T& dy, T& dz) {
-  const T tr = (g[0] + g[4] + g[8]) * (T(2) / T(3));
-  dx = (g[0] + g[0]) * x + (g[1] + g[3]) * y + (g[2] + g[6]) * z - tr * x;
-  dy = (g[3] + g[1]) * x + (g[4] + g[4]) * y + (g[5] + g[7]) * z - tr * y;
-  dz = (g[6] + g[2]) * x + (g[7] + g[5]) * y + (g[8] + g[8]) * z - tr * z;
-}
-template <typename T> struct Args;
-// Multiplicity of atom 0's self loop.  With a device pair count (static_shapes under HIP-graph
-// capture) it is computed here: 1 + (reference padding capacity - pairs found), a uniform scalar load.
-template <typename T> __device__ __forceinline__ T mult0_of(const Args<T>& A);
-
-template <typename T> __device__ __forceinline__ T dot9(const T (&a)[9], const T (&b)[9]) {
-  T s = T(0);
-#pragma unroll
-  for (int i = 0; i < 9; ++i) s += a[i] * b[i];
-  return s;
-}
-
 template <typename T> struct Args {
   int n, H, nblk, cap;
+  size_t nh;                // component stride of the compact layout (N * H)
   T mult0;
   const int32_t* npd;  // device num_pairs: mult0 = 1 + max(0, padcap - *npd) (HIP-graph capturable)
   int padcap;
@@ -85,17 +41,19 @@ template <typename T> struct Args {
   const T* W; int ldw;      // [E][3H] (W1 | W2 | W3), pre-cutoff
   const T* C;               // [E]
   const T* u;               // [E][3]
-  T* I; T* A; T* S;         // [N][H][9]
-  const T* gI; const T* gA; const T* gS;
+  T* E;                     // [9][N][H]
+  const T* gE;
   T* gP; T* gQ; T* gW; T* gC; T* gu;
   // message
   const T* ea; int ldea;    // [E][3H] interleaved (h, c)
-  const T* Ti; const T* Ta; const T* Ts;  // [N][H][9]
-  T* msg;
+  const T* Tc;              // [9][N][H]
+  T* msg;                   // [9][N][H]
   const T* gmsg;
-  T* gea; T* gTi; T* gTa; T* gTs;
+  T* gea; T* gT;
 };
 
+// Multiplicity of atom 0's self loop.  With a device pair count (static_shapes under HIP-graph
+// capture) it is computed here: 1 + (reference padding capacity - pairs found), a uniform scalar load.
 template <typename T> __device__ __forceinline__ T mult0_of(const Args<T>& A) {
   if (A.npd == nullptr) return A.mult0;
   const int pad = A.padcap - __builtin_amdgcn_readfirstlane(A.npd[0]);
@@ -108,6 +66,37 @@ __device__ __forceinline__ void wave_node(int nblk, int& node, int& ch0) {
   ch0 = (w % nblk) * TMD_WAVE;
 }
 
+template <typename T> __device__ __forceinline__ void ldc(T (&o)[9], const T* p, size_t nh) {
+#pragma unroll
+  for (int k = 0; k < 9; ++k) o[k] = p[k * nh];
+}
+template <typename T> __device__ __forceinline__ void stc(T* p, size_t nh, const T (&o)[9]) {
+#pragma unroll
+  for (int k = 0; k < 9; ++k) p[k * nh] = o[k];
+}
+
+// compact coordinates of skew(v) = [[0,-z,y],[z,0,-x],[-y,x,0]]  (tensornet.py:16-34)
+template <typename T> __device__ __forceinline__ void skew_c(T (&a)[3], T x, T y, T z) {
+  a[0] = -z; a[1] = y; a[2] = -x;
+}
+// compact coordinates of sym(v) = v v^T - |v|^2/3 Id  (tensornet.py:37-44)
+template <typename T> __device__ __forceinline__ void sym_c(T (&s)[5], T x, T y, T z) {
+  const T tr = (x * x + y * y + z * z) / T(3);
+  s[0] = x * x - tr; s[1] = y * y - tr; s[2] = x * y; s[3] = x * z; s[4] = y * z;
+}
+// d<g, skew_c(v)>/dv
+template <typename T> __device__ __forceinline__ void dskew_c(const T* g, T& dx, T& dy, T& dz) {
+  dx = -g[2]; dy = g[1]; dz = -g[0];
+}
+// d<g, sym_c(v)>/dv
+template <typename T>
+__device__ __forceinline__ void dsym_c(const T* g, T x, T y, T z, T& dx, T& dy, T& dz) {
+  const T t = (g[0] + g[1]) * (T(2) / T(3));
+  dx = T(2) * g[0] * x - t * x + g[2] * y + g[3] * z;
+  dy = T(2) * g[1] * y - t * y + g[2] * x + g[4] * z;
+  dz = -t * z + g[3] * x + g[4] * y;
+}
+
 // ---------------------------------------------------------------- embedding forward
 template <typename T>
 __global__ __launch_bounds__(256) void k_embed_fwd(Args<T> A) {
@@ -118,34 +107,26 @@ __global__ __launch_bounds__(256) void k_embed_fwd(Args<T> A) {
   const bool on = h < A.H;
   const int hc = on ? h : 0;
   const T Pn = A.P[(size_t)n * A.H + hc];
-  T aI = T(0), aA[9], aS[9];
+  T acc[9];
 #pragma unroll
-  for (int i = 0; i < 9; ++i) { aA[i] = T(0); aS[i] = T(0); }
+  for (int k = 0; k < 9; ++k) acc[k] = T(0);
   const int b = min(A.row_ptr[n], A.cap), e = min(A.row_ptr[n + 1], A.cap);
   for (int k = b; k < e; ++k) {
     const int m = A.src[k];
     const T mult = (m == n && n == 0) ? mult0_of(A) : T(1);
     const T zc = (Pn + A.Q[(size_t)m * A.H + hc]) * A.C[k] * mult;
     const T* wr = A.W + (size_t)k * A.ldw;
-    const T w1 = wr[hc], w2 = wr[A.H + hc], w3 = wr[2 * A.H + hc];
-    const T ux = -A.u[3 * k], uy = -A.u[3 * k + 1], uz = -A.u[3 * k + 2];
-    T sk[9], sy[9];
-    skew(sk, ux, uy, uz);
-    symm(sy, ux, uy, uz);
-    aI += zc * w1;
+    const T w1 = wr[hc] * zc, w2 = wr[A.H + hc] * zc, w3 = wr[2 * A.H + hc] * zc;
+    T sk[3], sy[5];
+    skew_c(sk, -A.u[3 * k], -A.u[3 * k + 1], -A.u[3 * k + 2]);
+    sym_c(sy, -A.u[3 * k], -A.u[3 * k + 1], -A.u[3 * k + 2]);
+    acc[0] += w1;
 #pragma unroll
-    for (int i = 0; i < 9; ++i) {
-      aA[i] += zc * w2 * sk[i];
-      aS[i] += zc * w3 * sy[i];
-    }
+    for (int i = 0; i < 3; ++i) acc[1 + i] += w2 * sk[i];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) acc[4 + i] += w3 * sy[i];
   }
-  if (on) {
-    const size_t o = ((size_t)n * A.H + h) * 9;
-    T mI[9] = {aI, T(0), T(0), T(0), aI, T(0), T(0), T(0), aI};
-    st9(A.I + o, mI);
-    st9(A.A + o, aA);
-    st9(A.S + o, aS);
-  }
+  if (on) stc(A.E + (size_t)n * A.H + h, A.nh, acc);
 }
 
 // ---------------------------------------------------------------- embedding backward
@@ -156,19 +137,12 @@ __global__ __launch_bounds__(256) void k_embed_bwd_dst(Args<T> A) {
   const int n = blockIdx.x * (blockDim.x / TMD_WAVE) + threadIdx.x / TMD_WAVE;
   if (n >= A.n) return;
   const int lane = lane_id();
-  T gi[NB], gPn[NB];
-  T gA[NB][9], gS[NB][9];
-  T Pn[NB];
+  T g[NB][9], gPn[NB], Pn[NB];
 #pragma unroll
   for (int c = 0; c < NB; ++c) {
     const int h = c * TMD_WAVE + lane;
     const int hc = h < A.H ? h : 0;
-    const size_t o = ((size_t)n * A.H + hc) * 9;
-    T gI[9];
-    ld9(gI, A.gI + o);
-    ld9(gA[c], A.gA + o);
-    ld9(gS[c], A.gS + o);
-    gi[c] = gI[0] + gI[4] + gI[8];
+    ldc(g[c], A.gE + (size_t)n * A.H + hc, A.nh);
     Pn[c] = A.P[(size_t)n * A.H + hc];
     gPn[c] = T(0);
   }
@@ -178,9 +152,9 @@ __global__ __launch_bounds__(256) void k_embed_bwd_dst(Args<T> A) {
     const T mult = (m == n && n == 0) ? mult0_of(A) : T(1);
     const T Ck = A.C[k];
     const T ux = -A.u[3 * k], uy = -A.u[3 * k + 1], uz = -A.u[3 * k + 2];
-    T sk[9], sy[9];
-    skew(sk, ux, uy, uz);
-    symm(sy, ux, uy, uz);
+    T sk[3], sy[5];
+    skew_c(sk, ux, uy, uz);
+    sym_c(sy, ux, uy, uz);
     const T* wr = A.W + (size_t)k * A.ldw;
     T* gw = A.gW + (size_t)k * 3 * A.H;
     T gc = T(0), gux = T(0), guy = T(0), guz = T(0);
@@ -191,7 +165,10 @@ __global__ __launch_bounds__(256) void k_embed_bwd_dst(Args<T> A) {
       const int hc = on ? h : 0;
       const T z = Pn[c] + A.Q[(size_t)m * A.H + hc];
       const T w1 = wr[hc], w2 = wr[A.H + hc], w3 = wr[2 * A.H + hc];
-      const T g1 = gi[c] * mult, g2 = dot9(gA[c], sk) * mult, g3 = dot9(gS[c], sy) * mult;
+      const T g1 = g[c][0] * mult;
+      const T g2 = (g[c][1] * sk[0] + g[c][2] * sk[1] + g[c][3] * sk[2]) * mult;
+      const T g3 = (g[c][4] * sy[0] + g[c][5] * sy[1] + g[c][6] * sy[2] + g[c][7] * sy[3] +
+                    g[c][8] * sy[4]) * mult;
       gPn[c] += (g1 * w1 + g2 * w2 + g3 * w3) * Ck;
       if (on) {
         gw[h] = g1 * z * Ck;
@@ -200,8 +177,8 @@ __global__ __launch_bounds__(256) void k_embed_bwd_dst(Args<T> A) {
         gc += (g1 * w1 + g2 * w2 + g3 * w3) * z;
         // gradient w.r.t. the row edge's u (= -u(n->m)): chain through the sign flip
         T dax, day, daz, dsx, dsy, dsz;
-        dskew(gA[c], dax, day, daz);
-        dsymm(gS[c], ux, uy, uz, dsx, dsy, dsz);
+        dskew_c(&g[c][1], dax, day, daz);
+        dsym_c(&g[c][4], ux, uy, uz, dsx, dsy, dsz);
         const T a2 = z * w2 * Ck * mult, a3 = z * w3 * Ck * mult;
         gux -= a2 * dax + a3 * dsx;
         guy -= a2 * day + a3 * dsy;
@@ -238,23 +215,20 @@ __global__ __launch_bounds__(256) void k_embed_bwd_src(Args<T> A) {
   T gQm = T(0);
   const int b = min(A.row_ptr[m], A.cap), e = min(A.row_ptr[m + 1], A.cap);
   for (int k = b; k < e; ++k) {
-    const int n = A.src[k];  // row edge n->m; its reverse m->n contributed Q[m] to I/A/S[n]
+    const int n = A.src[k];  // row edge n->m; its reverse m->n contributed Q[m] to E[n]
     const T mult = (m == n && n == 0) ? mult0_of(A) : T(1);
-    const size_t o = ((size_t)n * A.H + hc) * 9;
-    T gI[9], gA[9], gS[9];
-    ld9(gI, A.gI + o);
-    ld9(gA, A.gA + o);
-    ld9(gS, A.gS + o);
+    T g[9];
+    ldc(g, A.gE + (size_t)n * A.H + hc, A.nh);
     // u of the reversed edge's own row edge (m->n as seen from row n) is -u(k); the embedding
     // used skew/sym of -(that) = u(k)
-    const T ux = A.u[3 * k], uy = A.u[3 * k + 1], uz = A.u[3 * k + 2];
-    T sk[9], sy[9];
-    skew(sk, ux, uy, uz);
-    symm(sy, ux, uy, uz);
+    T sk[3], sy[5];
+    skew_c(sk, A.u[3 * k], A.u[3 * k + 1], A.u[3 * k + 2]);
+    sym_c(sy, A.u[3 * k], A.u[3 * k + 1], A.u[3 * k + 2]);
     const T* wr = A.W + (size_t)k * A.ldw;
     const T w1 = wr[hc], w2 = wr[A.H + hc], w3 = wr[2 * A.H + hc];
-    const T g = (gI[0] + gI[4] + gI[8]) * w1 + dot9(gA, sk) * w2 + dot9(gS, sy) * w3;
-    gQm += g * A.C[k] * mult;
+    const T gg = g[0] * w1 + (g[1] * sk[0] + g[2] * sk[1] + g[3] * sk[2]) * w2 +
+                 (g[4] * sy[0] + g[5] * sy[1] + g[6] * sy[2] + g[7] * sy[3] + g[8] * sy[4]) * w3;
+    gQm += gg * A.C[k] * mult;
   }
   if (on) A.gQ[(size_t)m * A.H + h] = gQm;
 }
@@ -270,22 +244,19 @@ __global__ __launch_bounds__(256) void k_msg_fwd(Args<T> A) {
   const int hc = on ? h : 0;
   T acc[9];
 #pragma unroll
-  for (int i = 0; i < 9; ++i) acc[i] = T(0);
+  for (int k = 0; k < 9; ++k) acc[k] = T(0);
   const int b = min(A.row_ptr[n], A.cap), e = min(A.row_ptr[n + 1], A.cap);
   for (int k = b; k < e; ++k) {
     const int m = A.src[k];
     const T mult = (m == n && n == 0) ? mult0_of(A) : T(1);
     const T* er = A.ea + (size_t)k * A.ldea + 3 * hc;
     const T f0 = er[0] * mult, f1 = er[1] * mult, f2 = er[2] * mult;
-    const size_t o = ((size_t)m * A.H + hc) * 9;
-    T ti[9], ta[9], ts[9];
-    ld9(ti, A.Ti + o);
-    ld9(ta, A.Ta + o);
-    ld9(ts, A.Ts + o);
+    T t[9];
+    ldc(t, A.Tc + (size_t)m * A.H + hc, A.nh);
 #pragma unroll
-    for (int i = 0; i < 9; ++i) acc[i] += f0 * ti[i] + f1 * ta[i] + f2 * ts[i];
+    for (int i = 0; i < 9; ++i) acc[i] += node::ctype_scale(i, f0, f1, f2) * t[i];
   }
-  if (on) st9(A.msg + ((size_t)n * A.H + h) * 9, acc);
+  if (on) stc(A.msg + (size_t)n * A.H + h, A.nh, acc);
 }
 
 // destination pass: gea[e'] = <gmsg[n], {I,A,S}[m]>
@@ -298,26 +269,23 @@ __global__ __launch_bounds__(256) void k_msg_bwd_dst(Args<T> A) {
   const bool on = h < A.H;
   const int hc = on ? h : 0;
   T g[9];
-  ld9(g, A.gmsg + ((size_t)n * A.H + hc) * 9);
+  ldc(g, A.gmsg + (size_t)n * A.H + hc, A.nh);
   const int b = min(A.row_ptr[n], A.cap), e = min(A.row_ptr[n + 1], A.cap);
   for (int k = b; k < e; ++k) {
     const int m = A.src[k];
     const T mult = (m == n && n == 0) ? mult0_of(A) : T(1);
-    const size_t o = ((size_t)m * A.H + hc) * 9;
-    T ti[9], ta[9], ts[9];
-    ld9(ti, A.Ti + o);
-    ld9(ta, A.Ta + o);
-    ld9(ts, A.Ts + o);
+    T t[9];
+    ldc(t, A.Tc + (size_t)m * A.H + hc, A.nh);
     if (on) {
       T* gr = A.gea + (size_t)k * 3 * A.H + 3 * h;
-      gr[0] = dot9(g, ti) * mult;
-      gr[1] = dot9(g, ta) * mult;
-      gr[2] = dot9(g, ts) * mult;
+      gr[0] = g[0] * t[0] * mult;
+      gr[1] = (g[1] * t[1] + g[2] * t[2] + g[3] * t[3]) * mult;
+      gr[2] = (g[4] * t[4] + g[5] * t[5] + g[6] * t[6] + g[7] * t[7] + g[8] * t[8]) * mult;
     }
   }
 }
 
-// source pass: g{I,A,S}[m] = sum over reversed edges ea * gmsg[n]
+// source pass: gT[m] = sum over reversed edges ea * gmsg[n]
 template <typename T>
 __global__ __launch_bounds__(256) void k_msg_bwd_src(Args<T> A) {
   int m, ch0;
@@ -326,9 +294,9 @@ __global__ __launch_bounds__(256) void k_msg_bwd_src(Args<T> A) {
   const int h = ch0 + lane_id();
   const bool on = h < A.H;
   const int hc = on ? h : 0;
-  T ai[9], aa[9], as[9];
+  T acc[9];
 #pragma unroll
-  for (int i = 0; i < 9; ++i) { ai[i] = T(0); aa[i] = T(0); as[i] = T(0); }
+  for (int k = 0; k < 9; ++k) acc[k] = T(0);
   const int b = min(A.row_ptr[m], A.cap), e = min(A.row_ptr[m + 1], A.cap);
   for (int k = b; k < e; ++k) {
     const int n = A.src[k];
@@ -336,20 +304,11 @@ __global__ __launch_bounds__(256) void k_msg_bwd_src(Args<T> A) {
     const T* er = A.ea + (size_t)k * A.ldea + 3 * hc;
     const T f0 = er[0] * mult, f1 = er[1] * mult, f2 = er[2] * mult;
     T g[9];
-    ld9(g, A.gmsg + ((size_t)n * A.H + hc) * 9);
+    ldc(g, A.gmsg + (size_t)n * A.H + hc, A.nh);
 #pragma unroll
-    for (int i = 0; i < 9; ++i) {
-      ai[i] += f0 * g[i];
-      aa[i] += f1 * g[i];
-      as[i] += f2 * g[i];
-    }
+    for (int i = 0; i < 9; ++i) acc[i] += node::ctype_scale(i, f0, f1, f2) * g[i];
   }
-  if (on) {
-    const size_t o = ((size_t)m * A.H + h) * 9;
-    st9(A.gTi + o, ai);
-    st9(A.gTa + o, aa);
-    st9(A.gTs + o, as);
-  }
+  if (on) stc(A.gT + (size_t)m * A.H + h, A.nh, acc);
 }
 
 template <typename T>
@@ -366,6 +325,7 @@ static Args<T> base(int n, int H, const int32_t* row_ptr, const int32_t* src, in
                     const int32_t* npd, int padcap) {
   Args<T> A{};
   A.n = n; A.H = H; A.nblk = (H + TMD_WAVE - 1) / TMD_WAVE; A.cap = cap; A.mult0 = (T)mult0;
+  A.nh = (size_t)n * H;
   A.npd = npd; A.padcap = padcap;
   A.row_ptr = row_ptr; A.src = src;
   return A;
@@ -391,14 +351,13 @@ extern "C" int tmdnet_tn_embed_fwd(int dtype, int n_nodes, int hidden, const int
                                    const int32_t* src, int max_pairs, double self0_mult,
                                    const int32_t* pad_pairs, int pad_capacity,
                                    const void* P, const void* Q, const void* W, int ld_w,
-                                   const void* cutoff, const void* unit, void* I, void* A, void* S,
-                                   void* stream) {
+                                   const void* cutoff, const void* unit, void* out, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   TN_DISPATCH(dtype, {
     auto a = tn::base<T>(n_nodes, hidden, row_ptr, src, max_pairs, self0_mult, pad_pairs,
-                                 pad_capacity);
+                         pad_capacity);
     a.P = (const T*)P; a.Q = (const T*)Q; a.W = (const T*)W; a.ldw = ld_w;
-    a.C = (const T*)cutoff; a.u = (const T*)unit; a.I = (T*)I; a.A = (T*)A; a.S = (T*)S;
+    a.C = (const T*)cutoff; a.u = (const T*)unit; a.E = (T*)out;
     return tn::launch<T>(tn::k_embed_fwd<T>, a, st);
   })
 }
@@ -407,16 +366,16 @@ extern "C" int tmdnet_tn_embed_bwd(int dtype, int n_nodes, int hidden, const int
                                    const int32_t* src, int max_pairs, double self0_mult,
                                    const int32_t* pad_pairs, int pad_capacity,
                                    const void* P, const void* Q, const void* W, int ld_w,
-                                   const void* cutoff, const void* unit, const void* gI,
-                                   const void* gA, const void* gS, void* gP, void* gQ, void* gW,
-                                   void* gcut, void* gunit, void* stream) {
+                                   const void* cutoff, const void* unit, const void* grad_out,
+                                   void* gP, void* gQ, void* gW, void* gcut, void* gunit,
+                                   void* stream) {
   hipStream_t st = (hipStream_t)stream;
   TN_DISPATCH(dtype, {
     auto a = tn::base<T>(n_nodes, hidden, row_ptr, src, max_pairs, self0_mult, pad_pairs,
-                                 pad_capacity);
+                         pad_capacity);
     a.P = (const T*)P; a.Q = (const T*)Q; a.W = (const T*)W; a.ldw = ld_w;
     a.C = (const T*)cutoff; a.u = (const T*)unit;
-    a.gI = (const T*)gI; a.gA = (const T*)gA; a.gS = (const T*)gS;
+    a.gE = (const T*)grad_out;
     a.gP = (T*)gP; a.gQ = (T*)gQ; a.gW = (T*)gW; a.gC = (T*)gcut; a.gu = (T*)gunit;
     int rc;
     {
@@ -434,33 +393,32 @@ extern "C" int tmdnet_tn_embed_bwd(int dtype, int n_nodes, int hidden, const int
 
 extern "C" int tmdnet_tn_message_fwd(int dtype, int n_nodes, int hidden, const int32_t* row_ptr,
                                      const int32_t* src, int max_pairs, double self0_mult,
-                                   const int32_t* pad_pairs, int pad_capacity,
-                                     const void* edge_attr, int ld_ea, const void* I, const void* A,
-                                     const void* S, void* msg, void* stream) {
+                                     const int32_t* pad_pairs, int pad_capacity,
+                                     const void* edge_attr, int ld_ea, const void* comp, void* msg,
+                                     void* stream) {
   hipStream_t st = (hipStream_t)stream;
   TN_DISPATCH(dtype, {
     auto a = tn::base<T>(n_nodes, hidden, row_ptr, src, max_pairs, self0_mult, pad_pairs,
-                                 pad_capacity);
+                         pad_capacity);
     a.ea = (const T*)edge_attr; a.ldea = ld_ea;
-    a.Ti = (const T*)I; a.Ta = (const T*)A; a.Ts = (const T*)S; a.msg = (T*)msg;
+    a.Tc = (const T*)comp; a.msg = (T*)msg;
     return tn::launch<T>(tn::k_msg_fwd<T>, a, st);
   })
 }
 
 extern "C" int tmdnet_tn_message_bwd(int dtype, int n_nodes, int hidden, const int32_t* row_ptr,
                                      const int32_t* src, int max_pairs, double self0_mult,
-                                   const int32_t* pad_pairs, int pad_capacity,
-                                     const void* edge_attr, int ld_ea, const void* I, const void* A,
-                                     const void* S, const void* grad_msg, void* g_edge_attr,
-                                     void* gI, void* gA, void* gS, void* stream) {
+                                     const int32_t* pad_pairs, int pad_capacity,
+                                     const void* edge_attr, int ld_ea, const void* comp,
+                                     const void* grad_msg, void* g_edge_attr, void* g_comp,
+                                     void* stream) {
   hipStream_t st = (hipStream_t)stream;
   TN_DISPATCH(dtype, {
     auto a = tn::base<T>(n_nodes, hidden, row_ptr, src, max_pairs, self0_mult, pad_pairs,
-                                 pad_capacity);
+                         pad_capacity);
     a.ea = (const T*)edge_attr; a.ldea = ld_ea;
-    a.Ti = (const T*)I; a.Ta = (const T*)A; a.Ts = (const T*)S;
-    a.gmsg = (const T*)grad_msg; a.gea = (T*)g_edge_attr;
-    a.gTi = (T*)gI; a.gTa = (T*)gA; a.gTs = (T*)gS;
+    a.Tc = (const T*)comp;
+    a.gmsg = (const T*)grad_msg; a.gea = (T*)g_edge_attr; a.gT = (T*)g_comp;
     int rc = tn::launch<T>(tn::k_msg_bwd_dst<T>, a, st);
     if (rc) return rc;
     return tn::launch<T>(tn::k_msg_bwd_src<T>, a, st);

@@ -506,6 +506,7 @@ class _ETStackBwd(Function):
         def message(q, k, v, vec, pk, pv, C_, u_):
             return kernels.et_message(q, k, v, vec, pk, pv, C_, u_, graph, heads)
 
+        _create = torch.is_grad_enabled()  # third order only if the caller builds a graph
         with torch.enable_grad():
             leaves = [None if t is None else t.detach().requires_grad_(True) for t in saved]
             gX, gV, x, f, C, u = leaves[:6]
@@ -522,7 +523,7 @@ class _ETStackBwd(Function):
             if not sel:
                 return (None,) * n_out
             second = torch.autograd.grad([fg for fg, _ in sel], ins, [g for _, g in sel],
-                                         create_graph=True, allow_unused=True)
+                                         create_graph=_create, allow_unused=True)
         it = iter(second)
         res = [next(it) if t is not None else None for t in leaves]
         return (None, None, None) + tuple(res)

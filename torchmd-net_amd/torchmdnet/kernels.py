@@ -404,6 +404,7 @@ class _EdgeGeomBwd(Function):
         cl, cu, rbf_type = ctx.cfg
         graph = ctx.graph
         selfmask = graph.src == graph.dst
+        _create = torch.is_grad_enabled()  # third order only if the caller builds a graph
         with torch.enable_grad():
             dl = deltas.detach().requires_grad_(True)
             r = dist.detach().requires_grad_(True)
@@ -418,7 +419,7 @@ class _EdgeGeomBwd(Function):
             if not sel:
                 return (None,) * 11
             second = torch.autograd.grad([f for f, _ in sel], inputs, [g for _, g in sel],
-                                         create_graph=True, allow_unused=True)
+                                         create_graph=_create, allow_unused=True)
         it = iter(second[2:])
         gups = [next(it) if u is not None else None for u in ups]
         return (second[0], second[1], gups[0], gups[1], gups[2], None, None, None, None, None, None)
@@ -573,6 +574,7 @@ class _ETMessageBwd(Function):
         saved = ctx.saved_tensors
         graph = ctx.graph
         src, dst = graph.src.long(), graph.dst.long()
+        _create = torch.is_grad_enabled()  # third order only if the caller builds a graph
         with torch.enable_grad():
             leaves = [None if t is None else t.detach().requires_grad_(True) for t in saved]
             gx, gvec, q, k, v, vec, pk, pv, C, u = leaves
@@ -587,7 +589,7 @@ class _ETMessageBwd(Function):
             if not sel:
                 return (None,) * 12
             second = torch.autograd.grad([f for f, _ in sel], ins, [g for _, g in sel],
-                                         create_graph=True, allow_unused=True)
+                                         create_graph=_create, allow_unused=True)
         it = iter(second)
         res = [next(it) if t is not None else None for t in leaves]
         return tuple(res) + (None, None)
@@ -689,6 +691,7 @@ class _NbrEmbedBwd(Function):
         gout, x, w, C = ctx.saved_tensors
         graph = ctx.graph
         src, dst = graph.src.long(), graph.dst.long()
+        _create = torch.is_grad_enabled()  # third order only if the caller builds a graph
         with torch.enable_grad():
             leaves = [t.detach().requires_grad_(True) for t in (gout, x, w, C)]
             go, x_, w_, C_ = leaves
@@ -698,12 +701,77 @@ class _NbrEmbedBwd(Function):
             if not sel:
                 return (None,) * 5
             second = torch.autograd.grad([f for f, _ in sel], leaves, [g for _, g in sel],
-                                         create_graph=True, allow_unused=True)
+                                         create_graph=_create, allow_unused=True)
         return tuple(second) + (None,)
 
 
 def nbr_embed(x, w, C, graph):
     return _NbrEmbed.apply(_rowmajor(x), _rowmajor(w), C.contiguous(), graph)
+
+
+# ----------------------------------------------------------------------------- activation
+def silu_launch(x, scale, out):
+    lib = nat.load()
+    rows, cols = x.shape
+    rc = lib.tmdnet_silu_fwd(nat.dtype_code(x.dtype), rows, cols, nat.ptr(x), x.stride(0), nat.ptr(scale),
+                             nat.ptr(out), nat.stream(x.device))
+    nat.check(rc, "tmdnet_silu_fwd")
+
+
+def silu_bwd_launch(x, scale, g, gx, gscale):
+    lib = nat.load()
+    rows, cols = x.shape
+    rc = lib.tmdnet_silu_bwd(nat.dtype_code(x.dtype), rows, cols, nat.ptr(x), x.stride(0), nat.ptr(scale),
+                             nat.ptr(g), g.stride(0), nat.ptr(gx), nat.ptr(gscale), nat.stream(x.device))
+    nat.check(rc, "tmdnet_silu_bwd")
+
+
+def _silu_composite(x, scale):
+    y = torch.nn.functional.silu(x)
+    return y if scale is None else y * scale.unsqueeze(1)
+
+
+class _Silu(Function):
+    @staticmethod
+    def forward(ctx, x, scale):
+        out = torch.empty(x.shape, dtype=x.dtype, device=x.device)
+        silu_launch(x, scale, out)
+        ctx.save_for_backward(x, scale)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        x, scale = ctx.saved_tensors
+        return _SiluBwd.apply(g.contiguous(), x, scale, ctx.needs_input_grad[1])
+
+
+class _SiluBwd(Function):
+    @staticmethod
+    def forward(ctx, g, x, scale, want_scale):
+        gx = torch.empty(x.shape, dtype=x.dtype, device=x.device)
+        gs = torch.empty(x.shape[0], dtype=x.dtype, device=x.device) if want_scale else None
+        silu_bwd_launch(x, scale, g, gx, gs)
+        ctx.save_for_backward(g, x, scale)
+        return gx, gs
+
+    @staticmethod
+    def backward(ctx, ggx, ggs):
+        g, x, scale = ctx.saved_tensors
+        from .tn_node import _double_backward
+        if scale is None:
+            d = _double_backward(lambda a: _silu_composite(a, None), [x], [g], [ggx])
+            return d[0], d[1], None, None
+        d = _double_backward(_silu_composite, [x, scale], [g], [ggx, ggs])
+        return d[0], d[1], d[2], None
+
+
+def fused_act(act, x, scale=None):
+    """``act(x) * scale[:, None]`` (scale optional) for a 2-D ``x``; SiLU on a ROCm device runs as one
+    HIP pass forward and one backward (``tmdnet_silu_*``), any other activation as the module."""
+    if isinstance(act, torch.nn.SiLU) and x.is_cuda and x.dim() == 2 and x.stride(1) == 1:
+        return _Silu.apply(x, None if scale is None else scale.contiguous())
+    y = act(x)
+    return y if scale is None else y * scale.view(-1, 1)
 
 
 # ----------------------------------------------------------------------------- TensorNet
@@ -740,8 +808,20 @@ def _sym(v):
     return 0.5 * (t + t.transpose(-2, -1)) - t.diagonal(dim1=-2, dim2=-1).mean(-1)[..., None, None] * eye
 
 
+def _skew_c(u):
+    """compact coordinates (a01, a02, a12) of skew(u) (tensornet.py:16-34)."""
+    return torch.stack((-u[:, 2], u[:, 1], -u[:, 0]), dim=1)
+
+
+def _sym_c(u):
+    """compact coordinates (s00, s11, s01, s02, s12) of sym(u) = u u^T - |u|^2/3 Id (tensornet.py:37-44)."""
+    tr = (u * u).sum(1) / 3
+    return torch.stack((u[:, 0] * u[:, 0] - tr, u[:, 1] * u[:, 1] - tr, u[:, 0] * u[:, 1],
+                        u[:, 0] * u[:, 2], u[:, 1] * u[:, 2]), dim=1)
+
+
 def tn_embed_composite(P, Q, W, C, u, graph):
-    """tensornet.py:295-315 in reference orientation (scatter to edge_index[0])."""
+    """tensornet.py:295-315 in reference orientation (scatter to edge_index[0]); compact [9, N, H]."""
     valid = (graph.src >= 0).to(P.dtype)  # static-capacity padding slots (-1) carry nothing
     src, dst = graph.src.long().clamp(min=0), graph.dst.long().clamp(min=0)
     H = P.shape[1]
@@ -749,150 +829,168 @@ def tn_embed_composite(P, Q, W, C, u, graph):
     wt = (_self0_weight(graph, C) * C * valid).unsqueeze(1)
     z = (P.index_select(0, src) + Q.index_select(0, dst)) * wt
     W1, W2, W3 = W[:, :H], W[:, H:2 * H], W[:, 2 * H:]
-    eye = torch.eye(3, dtype=P.dtype, device=P.device)
-    zero = torch.zeros((N, H, 3, 3), dtype=P.dtype, device=P.device)
-    I = zero.index_add(0, src, (z * W1)[..., None, None] * eye)
-    A = zero.index_add(0, src, (z * W2)[..., None, None] * _skew(u)[:, None])
-    S = zero.index_add(0, src, (z * W3)[..., None, None] * _sym(u)[:, None])
-    return I, A, S
+    coef = [z * W1] + [(z * W2) * a.unsqueeze(1) for a in _skew_c(u).unbind(1)] \
+        + [(z * W3) * s.unsqueeze(1) for s in _sym_c(u).unbind(1)]
+    zero = torch.zeros((N, H), dtype=P.dtype, device=P.device)
+    return torch.stack([zero.index_add(0, src, c) for c in coef], dim=0)
 
 
-def tn_message_composite(ea, I, A, S, graph):
-    """tensornet.py:329-332 (gather edge_index[1], scatter edge_index[0]) for the three components."""
-    valid = (graph.src >= 0).to(I.dtype)
+def tn_message_composite(ea, Tc, graph):
+    """tensornet.py:329-332 (gather edge_index[1], scatter edge_index[0]) on compact [9, N, H] tensors."""
+    valid = (graph.src >= 0).to(Tc.dtype)
     src, dst = graph.src.long().clamp(min=0), graph.dst.long().clamp(min=0)
-    N, H = I.shape[0], I.shape[1]
-    f = (ea.view(-1, H, 3) * (_self0_weight(graph, ea) * valid).view(-1, 1, 1))
-    m = f[..., 0, None, None] * I.index_select(0, dst) + f[..., 1, None, None] * A.index_select(0, dst) \
-        + f[..., 2, None, None] * S.index_select(0, dst)
-    return torch.zeros((N, H, 3, 3), dtype=I.dtype, device=I.device).index_add(0, src, m)
+    N, H = Tc.shape[1], Tc.shape[2]
+    f = (ea.reshape(-1, H, 3) * (_self0_weight(graph, ea) * valid).view(-1, 1, 1))
+    zero = torch.zeros((N, H), dtype=Tc.dtype, device=Tc.device)
+    rows = [zero.index_add(0, src, f[..., 0 if k == 0 else (1 if k < 4 else 2)] * Tc[k].index_select(0, dst))
+            for k in range(9)]
+    return torch.stack(rows, dim=0)
+
+
+def tn_embed_fwd_launch(P, Q, W, C, u, graph, out):
+    lib = nat.load()
+    N, H = P.shape
+    rc = lib.tmdnet_tn_embed_fwd(nat.dtype_code(P.dtype), N, H, nat.ptr(graph.row_ptr), nat.ptr(graph.src),
+                                 graph.n_edges, *_self0_args(graph), nat.ptr(P), nat.ptr(Q), nat.ptr(W), _ld(W),
+                                 nat.ptr(C), nat.ptr(u), nat.ptr(out), nat.stream(P.device))
+    nat.check(rc, "tmdnet_tn_embed_fwd")
+
+
+def tn_embed_bwd_launch(P, Q, W, C, u, graph, gE, gP, gQ, gW, gC, gu):
+    lib = nat.load()
+    N, H = P.shape
+    rc = lib.tmdnet_tn_embed_bwd(nat.dtype_code(P.dtype), N, H, nat.ptr(graph.row_ptr), nat.ptr(graph.src),
+                                 graph.n_edges, *_self0_args(graph), nat.ptr(P), nat.ptr(Q), nat.ptr(W), _ld(W),
+                                 nat.ptr(C), nat.ptr(u), nat.ptr(gE), nat.ptr(gP), nat.ptr(gQ), nat.ptr(gW),
+                                 nat.ptr(gC), nat.ptr(gu), nat.stream(P.device))
+    nat.check(rc, "tmdnet_tn_embed_bwd")
+
+
+def tn_message_fwd_launch(ea, Tc, graph, out):
+    lib = nat.load()
+    N, H = Tc.shape[1], Tc.shape[2]
+    rc = lib.tmdnet_tn_message_fwd(nat.dtype_code(Tc.dtype), N, H, nat.ptr(graph.row_ptr), nat.ptr(graph.src),
+                                   graph.n_edges, *_self0_args(graph), nat.ptr(ea), _ld(ea), nat.ptr(Tc),
+                                   nat.ptr(out), nat.stream(Tc.device))
+    nat.check(rc, "tmdnet_tn_message_fwd")
+
+
+def tn_message_bwd_launch(ea, Tc, graph, gmsg, gea, gT):
+    lib = nat.load()
+    N, H = Tc.shape[1], Tc.shape[2]
+    rc = lib.tmdnet_tn_message_bwd(nat.dtype_code(Tc.dtype), N, H, nat.ptr(graph.row_ptr), nat.ptr(graph.src),
+                                   graph.n_edges, *_self0_args(graph), nat.ptr(ea), _ld(ea), nat.ptr(Tc),
+                                   nat.ptr(gmsg), nat.ptr(gea), nat.ptr(gT), nat.stream(Tc.device))
+    nat.check(rc, "tmdnet_tn_message_bwd")
 
 
 class _TNEmbed(Function):
     @staticmethod
     def forward(ctx, P, Q, W, C, u, graph):
-        lib = nat.load()
         N, H = P.shape
-        o = dict(dtype=P.dtype, device=P.device)
-        I, A, S = (torch.empty((N, H, 3, 3), **o) for _ in range(3))
-        rc = lib.tmdnet_tn_embed_fwd(nat.dtype_code(P.dtype), N, H, nat.ptr(graph.row_ptr), nat.ptr(graph.src),
-                                     graph.n_edges, *_self0_args(graph), nat.ptr(P),
-                                     nat.ptr(Q), nat.ptr(W), _ld(W), nat.ptr(C), nat.ptr(u), nat.ptr(I),
-                                     nat.ptr(A), nat.ptr(S), nat.stream(P.device))
-        nat.check(rc, "tmdnet_tn_embed_fwd")
+        out = torch.empty((9, N, H), dtype=P.dtype, device=P.device)
+        tn_embed_fwd_launch(P, Q, W, C, u, graph, out)
         ctx.graph = graph
         ctx.save_for_backward(P, Q, W, C, u)
-        return I, A, S
+        return out
 
     @staticmethod
-    def backward(ctx, gI, gA, gS):
+    def backward(ctx, gE):
         P, Q, W, C, u = ctx.saved_tensors
-        z = lambda g: torch.zeros((P.shape[0], P.shape[1], 3, 3), dtype=P.dtype, device=P.device) if g is None else g.contiguous()
-        outs = _TNEmbedBwd.apply(z(gI), z(gA), z(gS), P, Q, W, C, u, ctx.graph)
+        outs = _TNEmbedBwd.apply(gE.contiguous(), P, Q, W, C, u, ctx.graph)
         return tuple(outs) + (None,)
 
 
 class _TNEmbedBwd(Function):
     @staticmethod
-    def forward(ctx, gI, gA, gS, P, Q, W, C, u, graph):
+    def forward(ctx, gE, P, Q, W, C, u, graph):
         if not graph.symmetric:
             raise RuntimeError("torchmd-net_amd: TensorNet backward needs a symmetric edge list")
-        lib = nat.load()
         N, H = P.shape
         E = graph.n_edges
         o = dict(dtype=P.dtype, device=P.device)
         gP, gQ = torch.empty((N, H), **o), torch.empty((N, H), **o)
         gW = torch.empty((E, 3 * H), **o)
         gC, gu = torch.empty((E,), **o), torch.empty((E, 3), **o)
-        rc = lib.tmdnet_tn_embed_bwd(nat.dtype_code(P.dtype), N, H, nat.ptr(graph.row_ptr), nat.ptr(graph.src), E,
-                                     *_self0_args(graph), nat.ptr(P), nat.ptr(Q), nat.ptr(W),
-                                     _ld(W), nat.ptr(C), nat.ptr(u), nat.ptr(gI), nat.ptr(gA), nat.ptr(gS),
-                                     nat.ptr(gP), nat.ptr(gQ), nat.ptr(gW), nat.ptr(gC), nat.ptr(gu),
-                                     nat.stream(P.device))
-        nat.check(rc, "tmdnet_tn_embed_bwd")
+        tn_embed_bwd_launch(P, Q, W, C, u, graph, gE, gP, gQ, gW, gC, gu)
         ctx.graph = graph
-        ctx.save_for_backward(gI, gA, gS, P, Q, W, C, u)
+        ctx.save_for_backward(gE, P, Q, W, C, u)
         return gP, gQ, gW, gC, gu
 
     @staticmethod
     def backward(ctx, *ggs):
         saved = ctx.saved_tensors
+        _create = torch.is_grad_enabled()  # third order only if the caller builds a graph
         with torch.enable_grad():
             leaves = [t.detach().requires_grad_(True) for t in saved]
-            gI, gA, gS, P, Q, W, C, u = leaves
-            I, A, S = tn_embed_composite(P, Q, W, C, u, ctx.graph)
-            first = torch.autograd.grad((I, A, S), (P, Q, W, C, u), (gI, gA, gS), create_graph=True)
+            gE, P, Q, W, C, u = leaves
+            E_ = tn_embed_composite(P, Q, W, C, u, ctx.graph)
+            first = torch.autograd.grad(E_, (P, Q, W, C, u), gE, create_graph=True)
             sel = [(f, g) for f, g in zip(first, ggs) if g is not None]
             if not sel:
-                return (None,) * 9
+                return (None,) * 7
             second = torch.autograd.grad([f for f, _ in sel], leaves, [g for _, g in sel],
-                                         create_graph=True, allow_unused=True)
+                                         create_graph=_create, allow_unused=True)
         return tuple(second) + (None,)
 
 
 class _TNMessage(Function):
     @staticmethod
-    def forward(ctx, ea, I, A, S, graph):
-        lib = nat.load()
-        N, H = I.shape[0], I.shape[1]
-        msg = torch.empty((N, H, 3, 3), dtype=I.dtype, device=I.device)
-        rc = lib.tmdnet_tn_message_fwd(nat.dtype_code(I.dtype), N, H, nat.ptr(graph.row_ptr), nat.ptr(graph.src),
-                                       graph.n_edges, *_self0_args(graph), nat.ptr(ea),
-                                       _ld(ea), nat.ptr(I), nat.ptr(A), nat.ptr(S), nat.ptr(msg),
-                                       nat.stream(I.device))
-        nat.check(rc, "tmdnet_tn_message_fwd")
+    def forward(ctx, ea, Tc, graph):
+        msg = torch.empty_like(Tc)
+        tn_message_fwd_launch(ea, Tc, graph, msg)
         ctx.graph = graph
-        ctx.save_for_backward(ea, I, A, S)
+        ctx.save_for_backward(ea, Tc)
         return msg
 
     @staticmethod
     def backward(ctx, gmsg):
-        ea, I, A, S = ctx.saved_tensors
-        outs = _TNMessageBwd.apply(gmsg.contiguous(), ea, I, A, S, ctx.graph)
+        ea, Tc = ctx.saved_tensors
+        outs = _TNMessageBwd.apply(gmsg.contiguous(), ea, Tc, ctx.graph)
         return tuple(outs) + (None,)
 
 
 class _TNMessageBwd(Function):
     @staticmethod
-    def forward(ctx, gmsg, ea, I, A, S, graph):
+    def forward(ctx, gmsg, ea, Tc, graph):
         if not graph.symmetric:
             raise RuntimeError("torchmd-net_amd: TensorNet backward needs a symmetric edge list")
-        lib = nat.load()
-        N, H = I.shape[0], I.shape[1]
         E = graph.n_edges
-        gea = torch.empty((E, 3 * H), dtype=I.dtype, device=I.device)
-        gI, gA, gS = (torch.empty_like(I) for _ in range(3))
-        rc = lib.tmdnet_tn_message_bwd(nat.dtype_code(I.dtype), N, H, nat.ptr(graph.row_ptr), nat.ptr(graph.src), E,
-                                       *_self0_args(graph), nat.ptr(ea), _ld(ea), nat.ptr(I),
-                                       nat.ptr(A), nat.ptr(S), nat.ptr(gmsg), nat.ptr(gea), nat.ptr(gI),
-                                       nat.ptr(gA), nat.ptr(gS), nat.stream(I.device))
-        nat.check(rc, "tmdnet_tn_message_bwd")
+        H = Tc.shape[2]
+        gea = torch.empty((E, 3 * H), dtype=Tc.dtype, device=Tc.device)
+        gT = torch.empty_like(Tc)
+        tn_message_bwd_launch(ea, Tc, graph, gmsg, gea, gT)
         ctx.graph = graph
-        ctx.save_for_backward(gmsg, ea, I, A, S)
-        return gea, gI, gA, gS
+        ctx.save_for_backward(gmsg, ea, Tc)
+        return gea, gT
 
     @staticmethod
     def backward(ctx, *ggs):
         saved = ctx.saved_tensors
+        _create = torch.is_grad_enabled()  # third order only if the caller builds a graph
         with torch.enable_grad():
             leaves = [t.detach().requires_grad_(True) for t in saved]
-            gmsg, ea, I, A, S = leaves
-            msg = tn_message_composite(ea, I, A, S, ctx.graph)
-            first = torch.autograd.grad(msg, (ea, I, A, S), gmsg, create_graph=True)
+            gmsg, ea, Tc = leaves
+            msg = tn_message_composite(ea, Tc, ctx.graph)
+            first = torch.autograd.grad(msg, (ea, Tc), gmsg, create_graph=True)
             sel = [(f, g) for f, g in zip(first, ggs) if g is not None]
             if not sel:
-                return (None,) * 6
+                return (None,) * 4
             second = torch.autograd.grad([f for f, _ in sel], leaves, [g for _, g in sel],
-                                         create_graph=True, allow_unused=True)
+                                         create_graph=_create, allow_unused=True)
         return tuple(second) + (None,)
 
 
 def tn_embed(P, Q, W, C, u, graph):
+    """Embedding aggregation -> compact [9, N, H] (I | A | S rows)."""
+    nat.require_gpu(P, "tn_embed")
     return _TNEmbed.apply(P.contiguous(), Q.contiguous(), _rowmajor(W), C.contiguous(), u.contiguous(), graph)
 
 
-def tn_message(ea, I, A, S, graph):
-    return _TNMessage.apply(_rowmajor(ea), I.contiguous(), A.contiguous(), S.contiguous(), graph)
+def tn_message(ea, Tc, graph):
+    """Tensor message passing on a compact [9, N, H] tensor -> compact message."""
+    nat.require_gpu(Tc, "tn_message")
+    return _TNMessage.apply(_rowmajor(ea), Tc.contiguous(), graph)
 
 
 # ----------------------------------------------------------------------------- spatial order
@@ -1066,6 +1164,7 @@ class _EqHeadBwd(Function):
     @staticmethod
     def backward(ctx, ggx, ggv, *ggp):
         saved = ctx.saved_tensors
+        _create = torch.is_grad_enabled()  # third order only if the caller builds a graph
         with torch.enable_grad():
             leaves = [t.detach().requires_grad_(True) for t in saved]
             gy, x, vec = leaves[:3]
@@ -1076,7 +1175,7 @@ class _EqHeadBwd(Function):
             if not sel:
                 return (None,) * (6 + len(ps))
             second = torch.autograd.grad([f for f, _ in sel], leaves, [g for _, g in sel],
-                                         create_graph=torch.is_grad_enabled(), allow_unused=True)
+                                         create_graph=_create, allow_unused=True)
         d_gy, d_x, d_vec = second[:3]
         return (None, d_gy, None, None, d_x, d_vec) + tuple(second[3:])
 

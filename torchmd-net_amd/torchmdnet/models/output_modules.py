@@ -76,7 +76,8 @@ class Scalar(OutputModel):
         self.output_network[2].bias.data.fill_(0)
 
     def pre_reduce(self, x, v: Optional[torch.Tensor], z, pos, batch):
-        return self.output_network(x)
+        net = self.output_network
+        return net[2](kernels.fused_act(net[1], net[0](x)))
 
 
 class EquivariantScalar(OutputModel):

@@ -13,7 +13,7 @@ from typing import Optional, Tuple
 import torch
 from torch import Tensor, nn
 
-from .. import kernels
+from .. import kernels, tn_node
 from .utils import CosineCutoff, OptimizedDistance, act_class_mapping, as_graph, rbf_class_mapping
 
 # reference tensornet.py:13-14 sets TF32 matmul globally; gfx950 has no TF32/xf32 path, so fp32
@@ -123,30 +123,9 @@ class TensorNet(nn.Module):
         X = self.tensor_embedding(z, graph, graph.distances, edge_vec, edge_attr)
         for layer in self.layers:
             X = layer(X, graph, graph.distances, edge_attr)
-        I, A, S = decompose_tensor(X)
-        x = torch.cat((tensor_norm(I), tensor_norm(A), tensor_norm(S)), dim=-1)
+        x = tn_node.norms(X)  # cat(|I|^2, |A|^2, |S|^2) of decompose_tensor(X), one fused pass
         x = self.out_norm(x)
-        return self.act(self.linear(x))
-
-
-def _mm33(a, b):
-    """Per-channel 3x3 matrix product of (..., 3, 3) tensors (reference: torch.matmul /
-    torch.matrix_power, tensornet.py:382-389).  torch.matmul maps this onto a batched GEMM of N*H
-    3x3x3 problems (~160-200 us each at C3); a broadcast multiply-and-reduce is two elementwise
-    passes (and autograd-friendly to any order)."""
-    return (a.unsqueeze(-1) * b.unsqueeze(-3)).sum(-2)
-
-
-def _mix(linear, X):
-    """``linear`` over the channel axis of (N, H, 3, 3) tensors -- the reference's
-    ``linear(X.permute(0, 2, 3, 1)).permute(0, 3, 1, 2)`` (tensornet.py:318-320, 354-356, 372-374).
-    Applied to that permuted view, hipBLASLt runs a strided-batched GEMM of N tiny 9 x H x H problems
-    (~190 us each at C3); here the tensor is copied channel-last once and mixed by ONE (9N x H) GEMM
-    (~10 us with both copies)."""
-    N, H = X.shape[0], X.shape[1]
-    Xt = X.reshape(N, H, 9).transpose(1, 2).reshape(N * 9, H)
-    Y = torch.mm(Xt, linear.weight.t())
-    return Y.view(N, 9, H).transpose(1, 2).reshape(N, H, 3, 3)
+        return kernels.fused_act(self.act, self.linear(x))
 
 
 def _check_symmetric_graph(edge_index, n):
@@ -201,16 +180,14 @@ class TensorEmbedding(nn.Module):
         Z = self.emb(z)
         P = torch.nn.functional.linear(Z, self.emb2.weight[:, :H], self.emb2.bias)
         Q = torch.nn.functional.linear(Z, self.emb2.weight[:, H:])
-        I, A, S = kernels.tn_embed(P, Q, W, C, edge_vec_norm, graph)
-        norm = self.init_norm(tensor_norm(I + A + S))
-        I = _mix(self.linears_tensor[0], I)
-        A = _mix(self.linears_tensor[1], A)
-        S = _mix(self.linears_tensor[2], S)
+        Ec = kernels.tn_embed(P, Q, W, C, edge_vec_norm, graph)  # compact [9, N, H]: I | A | S rows
+        norm = self.init_norm(tn_node.enorm(Ec))
+        lt = self.linears_tensor
+        Ec = tn_node.mix3(Ec, lt[0].weight, lt[1].weight, lt[2].weight)
         for linear_scalar in self.linears_scalar:
-            norm = self.act(linear_scalar(norm))
-        norm = norm.reshape(norm.shape[0], self.hidden_channels, 3)
-        I, A, S = new_radial_tensor(I, A, S, norm[..., 0], norm[..., 1], norm[..., 2])
-        return I + A + S
+            norm = kernels.fused_act(self.act, linear_scalar(norm))
+        # new_radial_tensor(I, A, S, norm[..., 0], norm[..., 1], norm[..., 2]) and I + A + S
+        return tn_node.eout(Ec, norm)
 
 
 class Interaction(nn.Module):
@@ -242,27 +219,14 @@ class Interaction(nn.Module):
         if perm is not None:
             edge_weight, edge_attr = edge_weight[perm], edge_attr[perm]
         C = graph.cutoff if (perm is None and graph.cutoff is not None) else self.cutoff(edge_weight)
-        for linear_scalar in self.linears_scalar:
-            edge_attr = self.act(linear_scalar(edge_attr))
-        edge_attr = edge_attr * C.view(-1, 1)
-        X = X / (tensor_norm(X) + 1)[..., None, None]
-        I, A, S = decompose_tensor(X)
-        I = _mix(self.linears_tensor[0], I)
-        A = _mix(self.linears_tensor[1], A)
-        S = _mix(self.linears_tensor[2], S)
-        Y = I + A + S
-        msg = kernels.tn_message(edge_attr, I, A, S, graph)
-        if self.equivariance_invariance_group == "O(3)":
-            A = _mm33(msg, Y)
-            B = _mm33(Y, msg)
-            I, A, S = decompose_tensor(A + B)
-        if self.equivariance_invariance_group == "SO(3)":
-            B = _mm33(Y, msg)
-            I, A, S = decompose_tensor(2 * B)
-        normp1 = (tensor_norm(I + A + S) + 1)[..., None, None]
-        I, A, S = I / normp1, A / normp1, S / normp1
-        I = _mix(self.linears_tensor[3], I)
-        A = _mix(self.linears_tensor[4], A)
-        S = _mix(self.linears_tensor[5], S)
-        dX = I + A + S
-        return X + dX + _mm33(dX, dX)
+        for linear_scalar in self.linears_scalar[:-1]:
+            edge_attr = kernels.fused_act(self.act, linear_scalar(edge_attr))
+        edge_attr = kernels.fused_act(self.act, self.linears_scalar[-1](edge_attr), C)  # act(.) * C
+        lt = self.linears_tensor
+        # X / (|X|^2 + 1), decompose, three channel mixes -> Y as compact [9, N, H] (I | A | S rows)
+        Yc = tn_node.mix3(tn_node.pre(X), lt[0].weight, lt[1].weight, lt[2].weight)
+        msg = kernels.tn_message(edge_attr, Yc, graph)
+        # decompose(msg Y + Y msg) (O(3)) or decompose(2 Y msg) (SO(3)), / (|.|^2 + 1), three mixes
+        Dc = tn_node.mix3(tn_node.post(Yc, msg, self.equivariance_invariance_group),
+                          lt[3].weight, lt[4].weight, lt[5].weight)
+        return tn_node.resid(X, Dc)  # X / (|X|^2 + 1) + dX + dX dX (X was reassigned, :391)
