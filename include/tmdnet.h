@@ -297,6 +297,14 @@ int tmdnet_silu_fwd(int dtype, int rows, int cols, const void* x, int ld_x, cons
 int tmdnet_silu_bwd(int dtype, int rows, int cols, const void* x, int ld_x, const void* row_scale,
                     const void* grad_out, int ld_g, void* grad_x, void* grad_scale, void* stream);
 
+/* Per-molecule energy (TorchMD_Net.forward, model.py:263-283 with output_modules.py:27-43):
+ *   y[b] = *mean + *std * sum_{n: batch[n] = b} x[n],  b < n_mol <= 8192  (std / mean: device
+ *   scalars, NULL = 1 / 0; batch int64).  Backward: grad_x[n] = *std * grad_y[batch[n]]. */
+int tmdnet_atom_sum_fwd(int dtype, int n_atoms, int n_mol, const void* x, const int64_t* batch,
+                        const void* std_, const void* mean, void* y, void* stream);
+int tmdnet_atom_sum_bwd(int dtype, int n_atoms, int n_mol, const void* grad_y, const int64_t* batch,
+                        const void* std_, void* grad_x, void* stream);
+
 /* Library identification (for load checks). */
 const char* tmdnet_build_info(void);
 

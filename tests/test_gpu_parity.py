@@ -731,3 +731,27 @@ def test_fused_silu_matches_torch(dtype, tol, scaled):
     h2 = torch.autograd.grad(sum((b ** 2).sum() for b in g2), ins)
     for a, b in zip(h1, h2):
         assert _rel(a.detach().cpu(), b.detach().cpu()) < 10 * tol
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float64, 1e-13), (torch.float32, 1e-6)])
+def test_atom_sum_matches_scatter(dtype, tol):
+    """tmdnet_atom_sum_* (x * std, per-molecule sum, + mean) == the reference scatter path, forward,
+    backward and second order (unsorted batch included)."""
+    from torchmdnet import kernels
+    _lib_loaded()
+    torch.manual_seed(6)
+    n, B = 1000, 37
+    batch = torch.randint(0, B, (n,), device=DEV)
+    x = torch.randn(n, 1, dtype=dtype, device=DEV, requires_grad=True)
+    std, mean = torch.tensor(1.7, dtype=dtype, device=DEV), torch.tensor(-0.3, dtype=dtype, device=DEV)
+    y = kernels.atom_sum(x, batch, B, std, mean)
+    yr = torch.zeros(B, 1, dtype=dtype, device=DEV).index_add(0, batch, x * std) + mean
+    assert _rel(y.detach().cpu(), yr.detach().cpu()) < tol
+    g = torch.randn_like(yr)
+    (g1,) = torch.autograd.grad(y, x, g, create_graph=True)
+    (g2,) = torch.autograd.grad(yr, x, g, create_graph=True)
+    assert _rel(g1.detach().cpu(), g2.detach().cpu()) < tol
+    w = torch.randn_like(g1)
+    (h1,) = torch.autograd.grad((g1 * w).sum() * (g1 ** 2).sum(), x, allow_unused=True)
+    (h2,) = torch.autograd.grad((g2 * w).sum() * (g2 ** 2).sum(), x, allow_unused=True)
+    assert (h1 is None) == (h2 is None)

@@ -127,6 +127,37 @@ __global__ void k_segments(const int64_t* __restrict__ batch, int n, const int* 
   seg[2 * t + 1] = lo;
 }
 
+// Small systems: the sortedness check and the segments in ONE single-workgroup launch (replaces a
+// memset + k_batch_unsorted + k_segments; three launch latencies are most of the build at QM9 size).
+__global__ __launch_bounds__(1024) void k_prologue(const int64_t* __restrict__ batch, int n,
+                                                   int* __restrict__ seg) {
+  int local = 0;
+  for (int i = threadIdx.x; i + 1 < n; i += blockDim.x) local |= batch[i] > batch[i + 1];
+  const bool unsorted = __syncthreads_or(local);
+  for (int t = threadIdx.x; t < n; t += blockDim.x) {
+    if (unsorted) {
+      seg[2 * t] = 0;
+      seg[2 * t + 1] = n;
+      continue;
+    }
+    const int64_t b = batch[t];
+    int lo = 0, hi = t;
+    while (lo < hi) {
+      int m = (lo + hi) >> 1;
+      if (batch[m] < b) lo = m + 1; else hi = m;
+    }
+    seg[2 * t] = lo;
+    lo = t + 1;
+    hi = n;
+    while (lo < hi) {
+      int m = (lo + hi) >> 1;
+      if (batch[m] <= b) lo = m + 1; else hi = m;
+    }
+    seg[2 * t + 1] = lo;
+  }
+}
+static constexpr int kPrologueMaxAtoms = 16384;
+
 // ---------------------------------------------------------------- all-pairs (brute / shared)
 // One wave64 per destination; 64 candidates per iteration; ballot counts/compacts.
 template <typename T, bool FILL>
@@ -194,16 +225,28 @@ __global__ __launch_bounds__(1024) void k_scan(const int* __restrict__ counts, i
   }
 }
 
-// ---------------------------------------------------------------- transpose map
-template <bool SORTED_ROWS>
-__global__ void k_transpose(const int32_t* __restrict__ nb, const int* __restrict__ row_ptr, int cap,
-                            const int* __restrict__ num_pairs, int32_t* __restrict__ tr) {
+// ---------------------------------------------------------------- transpose map + padding
+// One pass over the capacity: slots past the pairs found get the reference padding (-1 / 0,
+// common.cuh:70-76) when `pad` (replaces three capacity-sized memsets), found slots their transpose.
+template <typename T, bool SORTED_ROWS>
+__global__ void k_transpose(int32_t* __restrict__ nb, const int* __restrict__ row_ptr, int cap,
+                            const int* __restrict__ num_pairs, int32_t* __restrict__ tr, int pad,
+                            T* __restrict__ dlt, T* __restrict__ dist) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= cap) return;
-  if (e >= num_pairs[0]) {  // unwritten slot (pad_output=0 leaves it uninitialised)
-    tr[e] = -1;
+  if (e >= num_pairs[0]) {  // unwritten slot
+    if (pad) {
+      nb[e] = -1;
+      nb[cap + e] = -1;
+      dlt[3 * e] = T(0);
+      dlt[3 * e + 1] = T(0);
+      dlt[3 * e + 2] = T(0);
+      dist[e] = T(0);
+    }
+    if (tr) tr[e] = -1;
     return;
   }
+  if (!tr) return;
   const int s = nb[e];
   const int t = nb[cap + e];
   if (s < 0) {
@@ -528,11 +571,6 @@ static int build(int strategy, const T* pos, const int64_t* batch, int n, const 
   P.loop = loop;
   P.transpose = transpose;
 
-  if (pad) {
-    TMD_CHECK(hipMemsetAsync(nb, 0xFF, sizeof(int32_t) * 2 * (size_t)cap, st));
-    TMD_CHECK(hipMemsetAsync(dlt, 0, sizeof(T) * 3 * (size_t)cap, st));
-    TMD_CHECK(hipMemsetAsync(dist, 0, sizeof(T) * (size_t)cap, st));
-  }
   const int tb = 256;
   if (strategy == TMDNET_NL_CELL) {
     CellDims cd;
@@ -558,19 +596,25 @@ static int build(int strategy, const T* pos, const int64_t* batch, int n, const 
     hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, counts, n, row_ptr, num_pairs);
     hipLaunchKernelGGL((k_cell_pairs<T, true>), dim3((n + tb - 1) / tb), dim3(tb), 0, st, P, G, skeys,
                        svals, cstart, cend, counts, row_ptr, cap, nb, dlt, dist);
-    if (tr)
-      hipLaunchKernelGGL(k_transpose<false>, dim3((cap + tb - 1) / tb), dim3(tb), 0, st, nb, row_ptr, cap, num_pairs, tr);
+    if (tr || pad)
+      hipLaunchKernelGGL((k_transpose<T, false>), dim3((cap + tb - 1) / tb), dim3(tb), 0, st, nb, row_ptr, cap,
+                         num_pairs, tr, pad, dlt, dist);
   } else {
-    TMD_CHECK(hipMemsetAsync(flag, 0, sizeof(int), st));
-    hipLaunchKernelGGL(k_batch_unsorted, dim3((n + tb - 1) / tb), dim3(tb), 0, st, batch, n, flag);
-    hipLaunchKernelGGL(k_segments, dim3((n + tb - 1) / tb), dim3(tb), 0, st, batch, n, flag, seg);
+    if (n <= kPrologueMaxAtoms) {
+      hipLaunchKernelGGL(k_prologue, dim3(1), dim3(1024), 0, st, batch, n, seg);
+    } else {
+      TMD_CHECK(hipMemsetAsync(flag, 0, sizeof(int), st));
+      hipLaunchKernelGGL(k_batch_unsorted, dim3((n + tb - 1) / tb), dim3(tb), 0, st, batch, n, flag);
+      hipLaunchKernelGGL(k_segments, dim3((n + tb - 1) / tb), dim3(tb), 0, st, batch, n, flag, seg);
+    }
     const int wpb = tb / TMD_WAVE;
     const dim3 g((n + wpb - 1) / wpb);
     hipLaunchKernelGGL((k_pairs<T, false>), g, dim3(tb), 0, st, P, seg, counts, row_ptr, cap, nb, dlt, dist);
     hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, counts, n, row_ptr, num_pairs);
     hipLaunchKernelGGL((k_pairs<T, true>), g, dim3(tb), 0, st, P, seg, counts, row_ptr, cap, nb, dlt, dist);
-    if (tr)
-      hipLaunchKernelGGL(k_transpose<true>, dim3((cap + tb - 1) / tb), dim3(tb), 0, st, nb, row_ptr, cap, num_pairs, tr);
+    if (tr || pad)
+      hipLaunchKernelGGL((k_transpose<T, true>), dim3((cap + tb - 1) / tb), dim3(tb), 0, st, nb, row_ptr, cap,
+                         num_pairs, tr, pad, dlt, dist);
   }
   return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
 }

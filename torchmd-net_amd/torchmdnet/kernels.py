@@ -276,6 +276,18 @@ class _NeighborGeomBwd2(Function):
         return grads[0], grads[1], None, d_gr, None, None, None
 
 
+class DeviceOverflow:
+    """Capacity-overflow status of a static-capacity build, read on demand (``.item()`` syncs) from
+    the device pair count -- no comparison kernel inside a captured step."""
+
+    def __init__(self, num_pairs_dev, capacity):
+        self.num = num_pairs_dev
+        self.capacity = int(capacity)
+
+    def item(self):
+        return int(self.num.item()) > self.capacity
+
+
 def build_graph(pos, batch, cutoff_lower, cutoff_upper, max_num_pairs, loop=True, strategy="brute",
                 box=None, check_errors=True, static_capacity=None):
     """Symmetric (include_transpose) neighbour graph with CSR rows, transpose map and autograd
@@ -299,7 +311,7 @@ def build_graph(pos, batch, cutoff_lower, cutoff_upper, max_num_pairs, loop=True
         graph = EdgeGraph(pos.shape[0], row_ptr, nb[0], nb[1], tr, None, None, None, symmetric=True,
                           static=True)
         graph.num_pairs_dev = num
-        graph.overflow = num > cap
+        graph.overflow = DeviceOverflow(num, cap)
         deltas, distances = _NeighborGeom.apply(pos, graph, dl, dist)
         graph.deltas = deltas
         graph.distances = distances
@@ -772,6 +784,59 @@ def fused_act(act, x, scale=None):
         return _Silu.apply(x, None if scale is None else scale.contiguous())
     y = act(x)
     return y if scale is None else y * scale.view(-1, 1)
+
+
+# ----------------------------------------------------------------------------- energy reduction
+ATOM_SUM_MAX_MOLECULES = 8192
+
+
+def _atom_sum_composite(x, batch, n_mol, std, mean):
+    out = torch.zeros((n_mol,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device).index_add(0, batch, x * std)
+    return out + mean
+
+
+class _AtomSum(Function):
+    """y[b] = mean + std * sum_{batch[n] = b} x[n] (TorchMD_Net.forward: `x * std`, reduce, `+ mean`)."""
+
+    @staticmethod
+    def forward(ctx, x, batch, n_mol, std, mean):
+        lib = nat.load()
+        y = torch.empty((n_mol, 1), dtype=x.dtype, device=x.device)
+        rc = lib.tmdnet_atom_sum_fwd(nat.dtype_code(x.dtype), x.shape[0], n_mol, nat.ptr(x), nat.ptr(batch),
+                                     nat.ptr(std), nat.ptr(mean), nat.ptr(y), nat.stream(x.device))
+        nat.check(rc, "tmdnet_atom_sum_fwd")
+        ctx.n_mol = n_mol
+        ctx.save_for_backward(batch, std)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        batch, std = ctx.saved_tensors
+        return _AtomSumBwd.apply(gy.contiguous(), batch, std, ctx.n_mol), None, None, None, None
+
+
+class _AtomSumBwd(Function):
+    @staticmethod
+    def forward(ctx, gy, batch, std, n_mol):
+        lib = nat.load()
+        gx = torch.empty((batch.shape[0], 1), dtype=gy.dtype, device=gy.device)
+        rc = lib.tmdnet_atom_sum_bwd(nat.dtype_code(gy.dtype), batch.shape[0], n_mol, nat.ptr(gy), nat.ptr(batch),
+                                     nat.ptr(std), nat.ptr(gx), nat.stream(gy.device))
+        nat.check(rc, "tmdnet_atom_sum_bwd")
+        ctx.n_mol = n_mol
+        ctx.save_for_backward(batch, std)
+        return gx
+
+    @staticmethod
+    def backward(ctx, ggx):  # linear in gy: its adjoint is the reduction again (std a buffer)
+        batch, std = ctx.saved_tensors
+        return _atom_sum_composite(ggx, batch, ctx.n_mol, std, torch.zeros_like(std)), None, None, None
+
+
+def atom_sum(x, batch, n_mol, std, mean):
+    """Fused ``reduce(x * std) + mean`` of TorchMD_Net.forward for a [N, 1] per-atom output."""
+    nat.require_gpu(x, "atom_sum")
+    return _AtomSum.apply(x.contiguous(), batch, int(n_mol), std, mean)
 
 
 # ----------------------------------------------------------------------------- TensorNet

@@ -159,14 +159,20 @@ class TorchMD_Net(nn.Module):
             pos.requires_grad_(True)
         x, v, z, pos, batch = self.representation_model(z, pos, batch, q=q, s=s)
         x = self.output_model.pre_reduce(x, v, z, pos, batch)
-        if self.std is not None:
-            x = x * self.std
-        if self.prior_model is not None:
-            for prior in self.prior_model:
-                x = prior.pre_reduce(x, z, pos, batch, extra_args)
-        x = self.output_model.reduce(x, batch)
-        if self.mean is not None:
-            x = x + self.mean
+        fused = None
+        if self.prior_model is None:  # x * std, reduce and + mean in one pass (one more for the backward)
+            fused = self.output_model.fused_reduce(x, batch, self.std, self.mean)
+        if fused is not None:
+            x = fused
+        else:
+            if self.std is not None:
+                x = x * self.std
+            if self.prior_model is not None:
+                for prior in self.prior_model:
+                    x = prior.pre_reduce(x, z, pos, batch, extra_args)
+            x = self.output_model.reduce(x, batch)
+            if self.mean is not None:
+                x = x + self.mean
         y = self.output_model.post_reduce(x)
         if self.prior_model is not None:
             for prior in self.prior_model:

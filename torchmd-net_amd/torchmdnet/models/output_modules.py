@@ -45,13 +45,28 @@ class OutputModel(nn.Module, metaclass=ABCMeta):
     def pre_reduce(self, x, v, z, pos, batch):
         return
 
-    def reduce(self, x, batch):
+    def _dim_size(self, x, batch):
         is_capturing = x.is_cuda and check_stream_capturing()
         if not x.is_cuda or not is_capturing:
             self.dim_size = int(batch.max().item() + 1)
         if is_capturing:
             assert self.dim_size > 0, "Warming up is needed before capturing the model into a CUDA graph"
-        return scatter(x, batch, dim=0, dim_size=self.dim_size, reduce=self.reduce_op)
+        return self.dim_size
+
+    def reduce(self, x, batch):
+        return scatter(x, batch, dim=0, dim_size=self._dim_size(x, batch), reduce=self.reduce_op)
+
+    def fused_reduce(self, x, batch, std, mean):
+        """``reduce(x * std) + mean`` as one HIP pass (TorchMD_Net.forward without priors), or None
+        when this head's reduction is not the plain per-molecule sum."""
+        if not (x.is_cuda and self.reduce_op in ("sum", "add") and x.dim() == 2 and x.shape[1] == 1
+                and type(self).reduce is OutputModel.reduce and batch.dtype == torch.int64
+                and std is not None and mean is not None and std.numel() == 1 and mean.numel() == 1):
+            return None
+        n_mol = self._dim_size(x, batch)
+        if n_mol > kernels.ATOM_SUM_MAX_MOLECULES:
+            return None
+        return kernels.atom_sum(x, batch, n_mol, std.to(x.dtype), mean.to(x.dtype))
 
     def post_reduce(self, x):
         return x
