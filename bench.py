@@ -33,6 +33,7 @@ for p in (os.path.join(ROOT, "torchmd-net_amd"), ROOT):
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
+MFMA_F32_PEAK_TFS = 157.3  # MI355X dense fp32 MFMA (v_mfma_f32_16x16x4_f32) spec, MI355X_MICROARCH.md
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 
 
@@ -232,6 +233,40 @@ def roofline_probe(a, dev):
         res["traffic"] = None if traffic is None else round(traffic)
         res["traffic_detail"] = detail
     return res
+
+
+def mfma_probe(E_c5, E_c2, H, R, dev):
+    """MFMA utilisation of the feature-mix GEMMs (north_star: 'MFMA utilisation on the feature mixes
+    against gfx950 peak'): the dk/dv projection Linear_{R->4H} over the edges (the largest FLOP term,
+    SURVEY.md 8(a) a13) as the model issues it -- per layer at C5 scale, all 8 layers stacked into one
+    GEMM at C2 -- fp32 in/out (hipBLASLt on v_mfma_f32_16x16x4_f32), HIP-event timed."""
+    res = {}
+    for tag, E, cols in (("c5_per_layer", E_c5, 4 * H), ("c2_stacked_8_layers", E_c2, 8 * 4 * H)):
+        gen = torch.Generator(device=dev).manual_seed(5)
+        f = torch.randn(E, R, device=dev, generator=gen)
+        w = torch.randn(cols, R, device=dev, generator=gen)
+        b = torch.randn(cols, device=dev, generator=gen)
+        out = torch.empty(E, cols, device=dev)
+        for _ in range(3):
+            torch.addmm(b, f, w.t(), out=out)
+        torch.cuda.synchronize()
+        reps = 10 if E > 100000 else 50
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            torch.addmm(b, f, w.t(), out=out)
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / reps
+        tf = 2.0 * E * R * cols / (ms * 1e-3) / 1e12
+        res[tag] = {"gemm": f"[{E} x {R}] @ [{R} x {cols}] + bias, fp32", "ms_per_launch": round(ms, 4),
+                    "achieved": round(tf, 2), "frac": round(tf / MFMA_F32_PEAK_TFS, 4),
+                    "output_bytes": E * cols * 4,
+                    "output_write_bound_ms": round(E * cols * 4 / (HBM_PEAK_GBS * 1e9) * 1e3, 4)}
+        del f, w, b, out
+    return {"kernel": "dk/dv projection GEMM (SURVEY 8(a) a13)", "bound": "mfma", "unit": "TFLOP/s",
+            "peak": MFMA_F32_PEAK_TFS, "dtype": "fp32 (the reference computes in fp32; gfx950 has no xf32)",
+            **res}
 
 
 def phase(msg):
@@ -492,6 +527,10 @@ def main():
     if rank == 0 and not a.no_roofline:
         phase("roofline probe (C5 water box)")
         out["roofline"] = roofline_probe(a, dev)
+        phase("MFMA probe (dk/dv projection GEMM)")
+        E_c5 = int(out["roofline"]["workload"].split("E=")[1].split(",")[0])
+        E_c2 = int(probe[0][2]) if probe else 12548
+        out["mfma"] = mfma_probe(E_c5, E_c2, a.channels, 64, dev)
     if rank == 0 and ws == 1 and not a.no_cpu_baseline:
         phase("CPU baseline")
         out["cpu_baseline"] = cpu_baseline(model, args, z, pos, batch, a.cpu_seconds)

@@ -23,3 +23,57 @@ atomic_masses = np.array([
     267.122, 268.126, 271.134, 270.133, 269.1338, 278.156, 281.165, 281.166,
     285.177, 286.182, 289.19, 289.194, 293.204, 293.208, 294.214,
 ])
+
+
+class MissingEnergyException(Exception):
+    pass
+
+
+def train_val_test_split(dset_len, train_size, val_size, test_size, seed, order=None):
+    """Reference torchmdnet/utils.py:54-116: sizes as counts or fractions (one may be None = the
+    rest), a seeded numpy permutation (``np.random.default_rng(seed)``), or a fixed ``order``."""
+    sizes = [train_size, val_size, test_size]
+    if sum(s is None for s in sizes) > 1:
+        raise AssertionError("Only one of train_size, val_size, test_size is allowed to be None.")
+    is_float = [isinstance(s, float) for s in sizes]
+    sizes = [round(dset_len * s) if f else s for s, f in zip(sizes, is_float)]
+    if None in sizes:
+        k = sizes.index(None)
+        sizes[k] = dset_len - sum(s for s in sizes if s is not None)
+    if sum(sizes) > dset_len:  # rounding overshoot: take one from the last fractional split
+        for k in (2, 1, 0):
+            if is_float[k]:
+                sizes[k] -= 1
+                break
+    train_size, val_size, test_size = sizes
+    if min(sizes) < 0:
+        raise AssertionError(f"One of training ({train_size}), validation ({val_size}) or testing "
+                             f"({test_size}) splits ended up with a negative size.")
+    total = sum(sizes)
+    if dset_len < total:
+        raise AssertionError(f"The dataset ({dset_len}) is smaller than the combined split sizes ({total}).")
+    if total < dset_len:
+        import warnings
+        warnings.warn(f"{dset_len - total} samples were excluded from the dataset")
+    idxs = np.arange(dset_len, dtype=int)
+    if order is None:
+        idxs = np.random.default_rng(seed).permutation(idxs)
+    parts = [idxs[:train_size], idxs[train_size:train_size + val_size], idxs[train_size + val_size:total]]
+    if order is not None:
+        parts = [[order[i] for i in p] for p in parts]
+    return tuple(np.array(p) for p in parts)
+
+
+def make_splits(dataset_len, train_size, val_size, test_size, seed, filename=None, splits=None, order=None):
+    """Reference torchmdnet/utils.py:119-146: load ``splits`` (npz with idx_train/val/test) or draw
+    them, optionally save to ``filename``; returns three int64 tensors."""
+    import torch
+    if splits is not None:
+        s = np.load(splits)
+        idx_train, idx_val, idx_test = s["idx_train"], s["idx_val"], s["idx_test"]
+    else:
+        idx_train, idx_val, idx_test = train_val_test_split(dataset_len, train_size, val_size, test_size,
+                                                            seed, order)
+    if filename is not None:
+        np.savez(filename, idx_train=idx_train, idx_val=idx_val, idx_test=idx_test)
+    return torch.from_numpy(idx_train), torch.from_numpy(idx_val), torch.from_numpy(idx_test)
