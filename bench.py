@@ -151,7 +151,7 @@ def probe_workload(n_atoms, H, dev):
     def launch():
         rc = lib.tmdnet_et_message_fwd(0, n_atoms, H, 8, ptr(graph.row_ptr), ptr(graph.src), E, ptr(q), H,
                                        ptr(k), H, ptr(v), 3 * H, ptr(vec), ptr(pk), H, ptr(pv), 3 * H, ptr(C),
-                                       ptr(u), ptr(xo), ptr(vo), PROBE_FLAGS, None, st)
+                                       ptr(u), ptr(xo), ptr(vo), PROBE_FLAGS, None, None, st)
         kernels.nat.check(rc, "tmdnet_et_message_fwd")
 
     return launch, E, L
@@ -235,13 +235,15 @@ def roofline_probe(a, dev):
     return res
 
 
-def mfma_probe(E_c5, E_c2, H, R, dev):
+def mfma_probe(E_c5, N_c5, E_c2, N_c2, H, R, dev):
     """MFMA utilisation of the feature-mix GEMMs (north_star: 'MFMA utilisation on the feature mixes
-    against gfx950 peak'): the dk/dv projection Linear_{R->4H} over the edges (the largest FLOP term,
-    SURVEY.md 8(a) a13) as the model issues it -- per layer at C5 scale, all 8 layers stacked into one
-    GEMM at C2 -- fp32 in/out (hipBLASLt on v_mfma_f32_16x16x4_f32), HIP-event timed."""
+    against gfx950 peak'): the dk/dv projection Linear_{R->4H} (the largest FLOP term, SURVEY.md 8(a)
+    a13) as the model issues it -- over the (E + N) / 2 edge PAIRS (both directions share a row,
+    et_stack.PAIR_ROWS), per layer at C5 scale, all 8 layers stacked into one GEMM at C2 -- fp32
+    in/out (hipBLASLt on v_mfma_f32_16x16x4_f32), HIP-event timed."""
     res = {}
-    for tag, E, cols in (("c5_per_layer", E_c5, 4 * H), ("c2_stacked_8_layers", E_c2, 8 * 4 * H)):
+    for tag, E, cols in (("c5_per_layer", (E_c5 + N_c5) // 2, 4 * H),
+                         ("c2_stacked_8_layers", (E_c2 + N_c2) // 2, 8 * 4 * H)):
         gen = torch.Generator(device=dev).manual_seed(5)
         f = torch.randn(E, R, device=dev, generator=gen)
         w = torch.randn(cols, R, device=dev, generator=gen)
@@ -529,8 +531,8 @@ def main():
         out["roofline"] = roofline_probe(a, dev)
         phase("MFMA probe (dk/dv projection GEMM)")
         E_c5 = int(out["roofline"]["workload"].split("E=")[1].split(",")[0])
-        E_c2 = int(probe[0][2]) if probe else 12548
-        out["mfma"] = mfma_probe(E_c5, E_c2, a.channels, 64, dev)
+        E_c2, N_c2 = (int(probe[0][2]), int(probe[0][3])) if probe else (12548, 678)
+        out["mfma"] = mfma_probe(E_c5, a.roofline_atoms, E_c2, N_c2, a.channels, 64, dev)
     if rank == 0 and ws == 1 and not a.no_cpu_baseline:
         phase("CPU baseline")
         out["cpu_baseline"] = cpu_baseline(model, args, z, pos, batch, a.cpu_seconds)

@@ -109,14 +109,18 @@ int tmdnet_edge_geom_bwd(int dtype, int n_edges, int num_rbf, int rbf_type, cons
  *   q,k: [N][H] (ld_q, ld_k); v: [N][3H] head-interleaved [x|v1|v2] (ld_v); vec_in, vec: [N][3][H];
  *   pk: [E][H] (ld_pk), pv: [E][3H] (ld_pv): PRE-activation dk/dv projections (NULL = factor 1, i.e.
  *   distance_influence without keys / values).  x: [N][H].  `order` (nullable) permutes the
- *   destinations processed (locality only; results identical).
+ *   destinations processed (locality only; results identical).  `pk_rows` (nullable): edge e reads
+ *   its projection from pk / pv row pk_rows[e] instead of row e -- dk/dv depend on |r| only, so the
+ *   two directions of a pair share one row (tmdnet_pair_index) and the projection GEMM runs over
+ *   (E + N) / 2 rows instead of E.  Gradient outputs (gpk / gpv of the backward) stay per edge.
  * One wave64 per destination; outputs written once; no atomics; deterministic.
  */
 int tmdnet_et_message_fwd(int dtype, int n_nodes, int hidden, int heads, const int32_t* row_ptr,
                           const int32_t* src, int max_pairs, const void* q, int ld_q, const void* k,
                           int ld_k, const void* v, int ld_v, const void* vec_in, const void* pk,
                           int ld_pk, const void* pv, int ld_pv, const void* cutoff, const void* unit,
-                          void* x_out, void* vec_out, int flags, const int32_t* order, void* stream);
+                          void* x_out, void* vec_out, int flags, const int32_t* pk_rows,
+                          const int32_t* order, void* stream);
 /* Backward (two CSR passes, no atomics): destination pass -> gq, gpk, gpv, gcut, gunit; source
  * pass (requires a symmetric edge list, dk/dv/cutoff functions of |r| only) -> gk, gv, gvec_in.
  * Gradients are written with the leading dimension of the matching input (gq: ld_q, gk: ld_k,
@@ -133,8 +137,8 @@ int tmdnet_et_message_bwd(int dtype, int n_nodes, int hidden, int heads, const i
                           int ld_pk, const void* pv, int ld_pv, const void* cutoff, const void* unit,
                           const void* grad_x, const void* grad_vec, void* gq, void* gk, void* gv,
                           void* gvec_in, void* gpk, void* gpv, void* gcut, void* gunit,
-                          int accumulate, const int32_t* order, void* stream);  /* accumulate may also
-                                                   carry TMDNET_ET_V_PLANAR */
+                          int accumulate, const int32_t* pk_rows, const int32_t* order,
+                          void* stream);  /* accumulate may also carry TMDNET_ET_V_PLANAR */
 
 /* Second-order backward: the VJP of tmdnet_et_message_bwd (forces differentiated again, reference
  * model.py:286-298 with create_graph=True).  gg_* are the cotangents of that call's outputs (gq, gk,
@@ -304,6 +308,20 @@ int tmdnet_atom_sum_fwd(int dtype, int n_atoms, int n_mol, const void* x, const 
                         const void* std_, const void* mean, void* y, void* stream);
 int tmdnet_atom_sum_bwd(int dtype, int n_atoms, int n_mol, const void* grad_y, const int64_t* batch,
                         const void* std_, void* grad_x, void* stream);
+
+/* Pair numbering of a symmetric CSR edge list (for pk_rows above).  Canonical edges are those
+ * with src >= dst (self loops and one direction of every pair), numbered row by row in CSR order;
+ * pair_row[e] = the pair number of e (the canonical edge's for the other direction), pair_edge[p]
+ * = the canonical edge of pair p.  Slots p >= the number of pairs (up to n_pair_slots) and edge
+ * slots past *num_pairs (static capacity; num_pairs NULL: row_ptr[n]) get 0.  Requires the
+ * transpose map.  sorted_rows != 0 (rows in ascending source order, the brute / shared lists;
+ * needs dst) selects a 3-launch closed-form path, else 4 wave-per-row passes.
+ * Workspace: tmdnet_pair_index_workspace_bytes(n_nodes). */
+size_t tmdnet_pair_index_workspace_bytes(int n_nodes);
+int tmdnet_pair_index(int n_nodes, const int32_t* row_ptr, const int32_t* src, const int32_t* dst,
+                      const int32_t* transpose, int max_pairs, const int32_t* num_pairs, int sorted_rows,
+                      int32_t* pair_row, int32_t* pair_edge, int n_pair_slots, void* workspace,
+                      size_t workspace_bytes, void* stream);
 
 /* Library identification (for load checks). */
 const char* tmdnet_build_info(void);

@@ -34,7 +34,35 @@ def _to_planar(g, H, heads, planar):
     return g[:, ES._v_perm(H, heads, g.device)]
 
 
-def _fake_fwd(q, k, v, vec, pk, pv, C, u, graph, heads, xo, vo, flags=0):
+def _expand_rows(pk, pv, pk_rows):
+    """Pair-shared projection rows -> per-edge rows (the kernels' pk_rows indirection)."""
+    if pk_rows is None:
+        return pk, pv
+    r = pk_rows.long()
+    return (None if pk is None else pk.index_select(0, r)), (None if pv is None else pv.index_select(0, r))
+
+
+def pair_index_composite(graph):
+    """tmdnet_pair_index restated: canonical edges (src >= dst) numbered row by row in CSR order;
+    the other direction takes its reverse's number; unused pair slots point at edge 0."""
+    E, N = graph.n_edges, graph.n_nodes
+    src, dst, tr = graph.src.long(), graph.dst.long(), graph.transpose.long()
+    canon = src >= dst
+    pid = torch.cumsum(canon.long(), 0) - 1  # CSR order = row by row, in-row order kept
+    pair_row = torch.where(canon, pid, pid[tr.clamp(min=0)])
+    pair_edge = torch.zeros((E + N) // 2, dtype=torch.long)
+    pair_edge[pid[canon]] = torch.nonzero(canon).flatten()
+    return pair_row.to(torch.int32), pair_edge.to(torch.int32)
+
+
+def _fake_pair_index(graph, pair_row, pair_edge):
+    r, e = pair_index_composite(graph)
+    pair_row.copy_(r)
+    pair_edge.copy_(e)
+
+
+def _fake_fwd(q, k, v, vec, pk, pv, C, u, graph, heads, xo, vo, flags=0, pk_rows=None):
+    pk, pv = _expand_rows(pk, pv, pk_rows)
     N, H = q.shape
     planar = bool(flags & nat.ET_V_PLANAR)
     v, pv = _to_inter(v, H, heads, planar), _to_inter(pv, H, heads, planar)
@@ -46,7 +74,8 @@ def _fake_fwd(q, k, v, vec, pk, pv, C, u, graph, heads, xo, vo, flags=0):
 
 
 def _fake_bwd(q, k, v, vec, pk, pv, C, u, graph, heads, gx, gvec, gq, gk, gv, gw, gpk, gpv, gC, gu,
-              accumulate=0):
+              accumulate=0, pk_rows=None):
+    pk, pv = _expand_rows(pk, pv, pk_rows)
     N, H = q.shape
     planar = bool(accumulate & nat.ET_V_PLANAR)
     v, pv = _to_inter(v, H, heads, planar), _to_inter(pv, H, heads, planar)
@@ -131,6 +160,7 @@ def _fake_bwd2(ctx, ggs):
 @pytest.fixture
 def emulated(monkeypatch):
     monkeypatch.setattr(kernels, "et_message_fwd_launch", _fake_fwd)
+    monkeypatch.setattr(kernels, "pair_index_launch", _fake_pair_index)
     monkeypatch.setattr(kernels, "et_message_bwd_launch", _fake_bwd)
     monkeypatch.setattr(kernels, "et_message_bwd2", _fake_bwd2)
     monkeypatch.setattr(ES, "_epilogue_fwd", _fake_epi_fwd)

@@ -755,3 +755,92 @@ def test_atom_sum_matches_scatter(dtype, tol):
     (h1,) = torch.autograd.grad((g1 * w).sum(), g)
     (h2,) = torch.autograd.grad((g2 * w).sum(), g)
     assert _rel(h1.cpu(), h2.cpu()) < tol
+
+
+def test_training_harness_fit_on_gpu(tmp_path):
+    """LNNP + DataModule + fit with the real ET model on the GPU: two epochs over
+    synthetic QM9-like molecules, finite decreasing-or-flat losses, checkpoint reloads."""
+    from torchmdnet import data as D
+    from torchmdnet import module as M
+    from torchmdnet.models.model import load_model
+    _lib_loaded()
+    _seed()
+    z, pos, batch = O.qm9_like(24)
+    items = []
+    g = torch.Generator().manual_seed(2)
+    for m in range(24):
+        sel = batch == m
+        items.append(D.Data(z=z[sel], pos=pos[sel].float(), y=torch.randn(1, generator=g),
+                            neg_dy=torch.randn(int(sel.sum()), 3, generator=g)))
+
+    class DS(torch.utils.data.Dataset):
+        def __len__(self):
+            return len(items)
+
+        def __getitem__(self, i):
+            return D.Data(**{k: v.clone() for k, v in items[i].to_dict().items()})
+
+    args = yaml_args("equivariant-transformer", embedding_dimension=64, num_layers=2, num_rbf=16, num_heads=4,
+                     derivative=True, lr=5e-4, lr_metric="val_total_mse_loss")
+    lnnp = M.LNNP(args)
+    lnnp.model.to(DEV)
+    dm = D.DataModule(dict(batch_size=8, inference_batch_size=8, train_size=16, val_size=8, test_size=0, seed=1,
+                           precision=32), dataset=DS())
+    dm.setup()
+    hist = M.fit(lnnp, dm, epochs=2, device=DEV, checkpoint=str(tmp_path / "c.ckpt"))
+    assert all(np.isfinite(h["train_total_mse_loss"]) and np.isfinite(h["val_total_mse_loss"]) for h in hist)
+    m2 = load_model(str(tmp_path / "c.ckpt"), device=DEV)
+    b = D.collate([dm.val_dataset[i] for i in range(4)]).to(DEV)
+    y1, f1 = lnnp.model(b.z, b.pos.clone(), b.batch)
+    y2, f2 = m2(b.z, b.pos.clone(), b.batch)
+    assert _rel(y1.detach().cpu(), y2.detach().cpu()) < 1e-6
+
+
+@pytest.mark.parametrize("static", [False, True])
+def test_pair_index_matches_composite(static):
+    """tmdnet_pair_index (canonical src >= dst edges numbered in CSR order, the reverse direction
+    sharing the number) == its restatement, on a QM9 batch and a periodic cell-list box; dynamic and
+    static-capacity graphs."""
+    from torchmdnet import kernels
+    from test_et_stack_cpu import pair_index_composite
+    _lib_loaded()
+    for sysname in ("qm9", "box"):
+        if sysname == "qm9":
+            z, pos, batch = O.qm9_like(20)
+            pos, batch, box, strat = pos.float().to(DEV), batch.to(DEV), None, "brute"
+        else:
+            g = torch.Generator().manual_seed(3)
+            L = 25.0
+            pos = (torch.rand(1500, 3, generator=g) * L).to(DEV)
+            batch = torch.zeros(1500, dtype=torch.long, device=DEV)
+            box, strat = torch.eye(3) * L, "cell"
+        n = pos.shape[0]
+        graph = kernels.build_graph(pos, batch, 0.0, 5.0, 128 * n, loop=True, strategy=strat, box=box,
+                                    static_capacity=(None if not static else 96 * n))
+        pr, pe = kernels.pair_index(graph)
+        E = graph.n_edges
+        if graph.sorted_rows:  # the closed-form path == the wave-per-row path
+            graph._pairs, graph.sorted_rows = None, False
+            pr2, pe2 = kernels.pair_index(graph)
+            assert torch.equal(pr, pr2) and torch.equal(pe, pe2)
+        if static:
+            ve = int(graph.num_pairs_dev.item())
+            sub = kernels.EdgeGraph(n, graph.row_ptr, graph.src[:ve], graph.dst[:ve], graph.transpose[:ve], None,
+                                    None, ve, True)
+            rr, re = pair_index_composite(_cpu(sub))
+            assert torch.equal(pr[:ve].cpu(), rr) and torch.count_nonzero(pr[ve:]) == 0
+            P = (ve + n) // 2
+            assert torch.equal(pe[:P].cpu(), re[:P])
+        else:
+            rr, re = pair_index_composite(_cpu(graph))
+            assert torch.equal(pr.cpu(), rr) and torch.equal(pe.cpu(), re)
+        # both directions of every pair read the same row; a row's canonical edge is one of them
+        tr = graph.transpose[:E].long()
+        ok = tr >= 0
+        assert torch.equal(pr[ok], pr[tr[ok]])
+
+
+def _cpu(graph):
+    from torchmdnet import kernels
+    return kernels.EdgeGraph(graph.n_nodes, graph.row_ptr.cpu(), graph.src.cpu(), graph.dst.cpu(),
+                             graph.transpose.cpu(), None, None, graph.num_pairs, True)

@@ -87,6 +87,7 @@ template <typename T> struct Args {
   const T* vec;
   const T* pk; int ldpk;
   const T* pv; int ldpv;
+  const int32_t* prow;  // row of pk / pv holding edge e's projection (pair-shared rows); NULL: row e
   const T* C;
   const T* u;
   // forward outputs
@@ -210,27 +211,28 @@ __device__ __forceinline__ void edge_chunks_pf(const Args<T>& A, int b, int e, i
   const int step = EPW * S;
   for (int c = b; c < e; c += TMD_WAVE) {
     const int n = min(TMD_WAVE, e - c);
-    int s_r = 0;
+    int s_r = 0, p_r = c + lane;
     T C_r = T(0), u0_r = T(0), u1_r = T(0), u2_r = T(0);
     if (lane < n) {
       const int k = c + lane;
       s_r = A.src[k];
+      if (A.prow) p_r = A.prow[k];
       C_r = A.C[k];
       u0_r = A.u[3 * k];
       u1_r = A.u[3 * k + 1];
       u2_r = A.u[3 * k + 2];
     }
     int j0 = EPW * G.sub;
-    if (j0 < n) {  // PD edges of stream in flight ahead of the one being consumed
-      ld(c + min(j0 + G.es, n - 1), cur);
-      if constexpr (PD == 2) ld(c + min(j0 + step + G.es, n - 1), nxt);
+    if (j0 < n) {  // PD edges of stream in flight ahead of the one being consumed (ld takes ROWS)
+      ld(__shfl(p_r, min(j0 + G.es, n - 1)), cur);
+      if constexpr (PD == 2) ld(__shfl(p_r, min(j0 + step + G.es, n - 1)), nxt);
     }
     for (; j0 < n; j0 += step) {
       const int j = j0 + G.es;
       const int jj = j < n ? j : n - 1;
       const int s = __shfl(s_r, jj);
       const T Ce = __shfl(C_r, jj), u0 = __shfl(u0_r, jj), u1 = __shfl(u1_r, jj), u2 = __shfl(u2_r, jj);
-      const int kn = c + min(j0 + PD * step + G.es, n - 1);
+      const int kn = __shfl(p_r, min(j0 + PD * step + G.es, n - 1));  // next edge's stream row
       auto pre = [&]() { ld(kn, PD == 2 ? nx2 : nxt); };
       if (j < n) body(c + j, s, Ce, u0, u1, u2, cur, pre);
       else pre();
@@ -1037,7 +1039,7 @@ template <typename T>
 static int setup(Args<T>& A, int n, int H, int heads, const int32_t* row_ptr, const int32_t* src,
                  int cap, const void* q, int ldq, const void* k, int ldk, const void* v, int ldv_,
                  const void* vec, const void* pk, int ldpk, const void* pv, int ldpv, const void* C,
-                 const void* u, const int32_t* order, int& V) {
+                 const void* u, const int32_t* order, int& V, const int32_t* prow = nullptr) {
   if (H <= 0 || heads <= 0 || H % heads) return kBadArgument;
   if (H % 32 == 0) V = H / 32;  // channels per lane, one edge per half-wave
   else if (H < 32) V = 1;       // fewer channels than half-wave lanes: idle lanes
@@ -1059,6 +1061,7 @@ static int setup(Args<T>& A, int n, int H, int heads, const int32_t* row_ptr, co
   A.xcd = 1;
   A.q = (const T*)q; A.ldq = ldq; A.k = (const T*)k; A.ldk = ldk; A.v = (const T*)v; A.ldv = ldv_;
   A.vec = (const T*)vec; A.pk = (const T*)pk; A.ldpk = ldpk; A.pv = (const T*)pv; A.ldpv = ldpv;
+  A.prow = prow;
   A.C = (const T*)C; A.u = (const T*)u;
   return kOk;
 }
@@ -1067,11 +1070,12 @@ template <typename T>
 static int fwd(int n, int H, int heads, const int32_t* row_ptr, const int32_t* src, int cap,
                const void* q, int ldq, const void* k, int ldk, const void* v, int ldv_,
                const void* vec, const void* pk, int ldpk, const void* pv, int ldpv, const void* C,
-               const void* u, void* xo, void* veco, int flags, const int32_t* order, hipStream_t st) {
+               const void* u, void* xo, void* veco, int flags, const int32_t* prow, const int32_t* order,
+               hipStream_t st) {
   Args<T> A;
   int V;
   int rc = setup<T>(A, n, H, heads, row_ptr, src, cap, q, ldq, k, ldk, v, ldv_, vec, pk, ldpk, pv,
-                    ldpv, C, u, order, V);
+                    ldpv, C, u, order, V, prow);
   if (rc) return rc;
   if (flags & TMDNET_ET_V_PLANAR) { A.planar = 1; A.vst = H; }
   A.xo = (T*)xo;
@@ -1085,11 +1089,11 @@ static int bwd(int n, int H, int heads, const int32_t* row_ptr, const int32_t* s
                const void* vec, const void* pk, int ldpk, const void* pv, int ldpv, const void* C,
                const void* u, const void* gx, const void* gvec, void* gq, void* gk, void* gv,
                void* gveci, void* gpk, void* gpv, void* gC, void* gu, int acc,
-               const int32_t* order, hipStream_t st) {
+               const int32_t* prow, const int32_t* order, hipStream_t st) {
   Args<T> A;
   int V;
   int rc = setup<T>(A, n, H, heads, row_ptr, src, cap, q, ldq, k, ldk, v, ldv_, vec, pk, ldpk, pv,
-                    ldpv, C, u, order, V);
+                    ldpv, C, u, order, V, prow);
   if (rc) return rc;
   A.gx = (const T*)gx; A.gvec = (const T*)gvec;
   A.gq = (T*)gq; A.gk = (T*)gk; A.gv = (T*)gv; A.gveci = (T*)gveci;
@@ -1166,15 +1170,16 @@ extern "C" int tmdnet_et_message_fwd(int dtype, int n_nodes, int hidden, int hea
                                      const void* q, int ld_q, const void* k, int ld_k, const void* v,
                                      int ld_v, const void* vec_in, const void* pk, int ld_pk,
                                      const void* pv, int ld_pv, const void* cutoff, const void* unit,
-                                     void* x_out, void* vec_out, int flags, const int32_t* order,
-                                     void* stream) {
+                                     void* x_out, void* vec_out, int flags, const int32_t* pk_rows,
+                                     const int32_t* order, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (dtype == TMDNET_F32)
     return et::fwd<float>(n_nodes, hidden, heads, row_ptr, src, max_pairs, q, ld_q, k, ld_k, v, ld_v,
-                          vec_in, pk, ld_pk, pv, ld_pv, cutoff, unit, x_out, vec_out, flags, order, st);
+                          vec_in, pk, ld_pk, pv, ld_pv, cutoff, unit, x_out, vec_out, flags, pk_rows, order, st);
   if (dtype == TMDNET_F64)
     return et::fwd<double>(n_nodes, hidden, heads, row_ptr, src, max_pairs, q, ld_q, k, ld_k, v, ld_v,
-                           vec_in, pk, ld_pk, pv, ld_pv, cutoff, unit, x_out, vec_out, flags, order, st);
+                           vec_in, pk, ld_pk, pv, ld_pv, cutoff, unit, x_out, vec_out, flags, pk_rows, order,
+                           st);
   return kUnsupported;
 }
 
@@ -1185,17 +1190,17 @@ extern "C" int tmdnet_et_message_bwd(int dtype, int n_nodes, int hidden, int hea
                                      const void* pv, int ld_pv, const void* cutoff, const void* unit,
                                      const void* grad_x, const void* grad_vec, void* gq, void* gk,
                                      void* gv, void* gvec_in, void* gpk, void* gpv, void* gcut,
-                                     void* gunit, int accumulate, const int32_t* order,
-                                     void* stream) {
+                                     void* gunit, int accumulate, const int32_t* pk_rows,
+                                     const int32_t* order, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (dtype == TMDNET_F32)
     return et::bwd<float>(n_nodes, hidden, heads, row_ptr, src, max_pairs, q, ld_q, k, ld_k, v, ld_v,
                           vec_in, pk, ld_pk, pv, ld_pv, cutoff, unit, grad_x, grad_vec, gq, gk, gv,
-                          gvec_in, gpk, gpv, gcut, gunit, accumulate, order, st);
+                          gvec_in, gpk, gpv, gcut, gunit, accumulate, pk_rows, order, st);
   if (dtype == TMDNET_F64)
     return et::bwd<double>(n_nodes, hidden, heads, row_ptr, src, max_pairs, q, ld_q, k, ld_k, v, ld_v,
                            vec_in, pk, ld_pk, pv, ld_pv, cutoff, unit, grad_x, grad_vec, gq, gk, gv,
-                           gvec_in, gpk, gpv, gcut, gunit, accumulate, order, st);
+                           gvec_in, gpk, gpv, gcut, gunit, accumulate, pk_rows, order, st);
   return kUnsupported;
 }
 

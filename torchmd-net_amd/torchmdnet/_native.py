@@ -34,9 +34,12 @@ SIGNATURES = {
     "tmdnet_nl_backward2": (I, [I, I, P, P, P, I, P, P, P, P, P, P, P, P]),
     "tmdnet_edge_geom_fwd": (I, [I, I, I, I, P, P, P, P, P, P, D, D, P, P, P, P]),
     "tmdnet_edge_geom_bwd": (I, [I, I, I, I, P, P, P, P, P, P, D, D, P, P, P, P, P, P]),
-    "tmdnet_et_message_fwd": (I, [I, I, I, I, P, P, I, P, I, P, I, P, I, P, P, I, P, I, P, P, P, P, I, P, P]),
+    "tmdnet_et_message_fwd": (I, [I, I, I, I, P, P, I, P, I, P, I, P, I, P, P, I, P, I, P, P, P, P, I, P, P,
+                                  P]),
     "tmdnet_et_message_bwd": (I, [I, I, I, I, P, P, I, P, I, P, I, P, I, P, P, I, P, I, P, P, P, P,
-                                  P, P, P, P, P, P, P, P, I, P, P]),
+                                  P, P, P, P, P, P, P, P, I, P, P, P]),
+    "tmdnet_pair_index_workspace_bytes": (SZ, [I]),
+    "tmdnet_pair_index": (I, [I, P, P, P, P, I, P, I, P, P, I, P, SZ, P]),
     "tmdnet_et_message_bwd2": (I, [I, I, I, I, P, P, I, P, I, P, I, P, I, P, P, I, P, I, P, P, P, P,
                                    P, P, P, P, P, I, P, I, P, P, P, P, P, P, P, P, P, P, P, P, I, P]),
     "tmdnet_et_epilogue_fwd": (I, [I, I, I, P, P, P, P, P, P, P, P]),

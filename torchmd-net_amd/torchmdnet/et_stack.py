@@ -116,6 +116,8 @@ BATCH_DKV_BYTES = 2 << 30
 # TMDNET_ET_V_PLANAR) by permuting the weight rows once per forward: contiguous row segments for the
 # edge kernels' 16-byte loads (+4-7 % on the C5 forward); below it the two small gathers are not worth it.
 PLANAR_MIN_EDGES = 131072
+# dk/dv projection rows shared by the two directions of an edge pair (halves the projection GEMM)
+PAIR_ROWS = True
 
 _PERMS = {}
 
@@ -180,6 +182,8 @@ class _Meta:
         self.qkv_eff = fused    # the weights the GEMMs use (row-permuted copies when planar)
         self.dkv_eff = (dkv_w, dkv_b)
         self.np = 11 + 2 * int(hk) + 2 * int(hv)  # parameters per layer
+        self.pairs = None       # (pair_row, pair_edge) of the graph: pair-shared dk/dv rows
+        self.pk_rows = None
 
     def split(self, params):
         return [params[i * self.np:(i + 1) * self.np] for i in range(self.n_layers)]
@@ -264,7 +268,12 @@ def _forward_layers(meta, x, f, C, u, params):
     acts = []
     D = meta.D
     meta.refresh_effective()
-    pkv_all = torch.addmm(meta.dkv_eff[1], f, meta.dkv_eff[0].t()) if (meta.batched and D) else None
+    # the projections depend on |r| only: one row per edge PAIR ((E + N) / 2 rows), read by both
+    # directions through pk_rows (bit-identical to the per-edge projection)
+    fp = f
+    if D and meta.pairs is not None:
+        fp = f.index_select(0, meta.pairs[1])
+    pkv_all = torch.addmm(meta.dkv_eff[1], fp, meta.dkv_eff[0].t()) if (meta.batched and D) else None
     layers = meta.split(params)
     # layer l's LayerNorm is computed by layer l-1's epilogue kernel (layer 0: LayerNorm alone)
     _, _, xn, mean, rstd = _epi_ln(x, None, None, None, None, layers[0][0], layers[0][1])
@@ -277,13 +286,13 @@ def _forward_layers(meta, x, f, C, u, params):
         if pkv_all is not None:
             pkv = pkv_all[:, l * D:(l + 1) * D]
         else:
-            pkv = torch.addmm(dkv_b, f, dkv_w.t()) if dkv_w is not None else None
+            pkv = torch.addmm(dkv_b, fp, dkv_w.t()) if dkv_w is not None else None
         pk = pkv[:, :H] if meta.hk else None
         pv = pkv[:, H * int(meta.hk):] if meta.hv else None
         xa = torch.empty((N, H), dtype=x.dtype, device=x.device)
         veca = torch.empty((N, 3, H), dtype=x.dtype, device=x.device)
         kernels.et_message_fwd_launch(qkv[:, :H], qkv[:, H:2 * H], qkv[:, 2 * H:], vec, pk, pv, C, u,
-                                      meta.graph, meta.heads, xa, veca, meta.flags)
+                                      meta.graph, meta.heads, xa, veca, meta.flags, meta.pk_rows)
         o = torch.addmm(o_b, xa, o_w.t())
         acts.append((x, vec, xn, mean, rstd, qkv, vecp, pkv, xa, o))
         if l + 1 < len(layers):
@@ -335,7 +344,7 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws):
         kernels.et_message_bwd_launch(
             qkv[:, :H], qkv[:, H:2 * H], qkv[:, 2 * H:], vec, pk, pv, C, u, graph, meta.heads, g_xa, gV,
             g_qkv[:, :H], g_qkv[:, H:2 * H], g_qkv[:, 2 * H:], g_vec_in, gpk, gpv, g_C, g_u,
-            accumulate=nat.ACC_VEC_RESIDUAL | nat.ACC_EDGE | meta.flags)
+            accumulate=nat.ACC_VEC_RESIDUAL | nat.ACC_EDGE | meta.flags, pk_rows=meta.pk_rows)
         if has_e and not meta.batched:
             if g_f is None:
                 g_f = torch.mm(g_pkv, dkv_w)
@@ -553,6 +562,9 @@ def et_stack(layers, x, graph, f, C, u):
     if graph.n_edges >= PLANAR_MIN_EDGES:
         meta.planar, meta.flags = True, nat.ET_V_PLANAR
         meta.perms = _planar_perms(meta, x.device)
+    if D and PAIR_ROWS and graph.symmetric and graph.transpose is not None:
+        meta.pairs = kernels.pair_index(graph)
+        meta.pk_rows = meta.pairs[0]
     x = x.contiguous()
     f = f.contiguous() if (hk or hv) else None
     return _ETStack.apply(meta, x, f, C.contiguous(), u.contiguous(), *params)

@@ -312,6 +312,7 @@ def build_graph(pos, batch, cutoff_lower, cutoff_upper, max_num_pairs, loop=True
                           static=True)
         graph.num_pairs_dev = num
         graph.overflow = DeviceOverflow(num, cap)
+        graph.sorted_rows = strategy != "cell"  # brute / shared rows list sources ascending
         deltas, distances = _NeighborGeom.apply(pos, graph, dl, dist)
         graph.deltas = deltas
         graph.distances = distances
@@ -326,6 +327,7 @@ def build_graph(pos, batch, cutoff_lower, cutoff_upper, max_num_pairs, loop=True
     E = min(num_pairs, cap)
     graph = EdgeGraph(pos.shape[0], row_ptr, nb[0, :E], nb[1, :E], tr[:E], None, None, num_pairs,
                       symmetric=num_pairs <= cap)
+    graph.sorted_rows = strategy != "cell"  # brute / shared rows list sources ascending
     deltas, distances = _NeighborGeom.apply(pos, graph, dl[:E], dist[:E])
     graph.deltas = deltas
     graph.distances = distances
@@ -458,8 +460,9 @@ def rows_like(t, alloc=torch.empty):
     return alloc((t.shape[0], t.stride(0)), dtype=t.dtype, device=t.device)[:, :t.shape[1]]
 
 
-def et_message_fwd_launch(q, k, v, vec, pk, pv, C, u, graph, heads, xo, vo, flags=0):
-    """One ``tmdnet_et_message_fwd`` launch (vec may be None: vec == 0; flags: nat.ET_V_PLANAR)."""
+def et_message_fwd_launch(q, k, v, vec, pk, pv, C, u, graph, heads, xo, vo, flags=0, pk_rows=None):
+    """One ``tmdnet_et_message_fwd`` launch (vec may be None: vec == 0; flags: nat.ET_V_PLANAR;
+    pk_rows: edge e reads pk / pv row pk_rows[e], the pair-shared rows of ``pair_index``)."""
     lib = nat.load()
     N, H = q.shape
     probe = EVENT_PROBE
@@ -470,7 +473,7 @@ def et_message_fwd_launch(q, k, v, vec, pk, pv, C, u, graph, heads, xo, vo, flag
                                    nat.ptr(graph.src), graph.n_edges, nat.ptr(q), _ld(q), nat.ptr(k),
                                    _ld(k), nat.ptr(v), _ld(v), nat.ptr(vec), nat.ptr(pk), _ld(pk),
                                    nat.ptr(pv), _ld(pv), nat.ptr(C), nat.ptr(u), nat.ptr(xo),
-                                   nat.ptr(vo), int(flags), None, nat.stream(q.device))
+                                   nat.ptr(vo), int(flags), nat.ptr(pk_rows), None, nat.stream(q.device))
     nat.check(rc, "tmdnet_et_message_fwd")
     if probe is not None:
         ev1.record()
@@ -478,7 +481,7 @@ def et_message_fwd_launch(q, k, v, vec, pk, pv, C, u, graph, heads, xo, vo, flag
 
 
 def et_message_bwd_launch(q, k, v, vec, pk, pv, C, u, graph, heads, gx, gvec, gq, gk, gv, gw, gpk,
-                          gpv, gC, gu, accumulate=0):
+                          gpv, gC, gu, accumulate=0, pk_rows=None):
     lib = nat.load()
     N, H = q.shape
     rc = lib.tmdnet_et_message_bwd(
@@ -486,8 +489,35 @@ def et_message_bwd_launch(q, k, v, vec, pk, pv, C, u, graph, heads, gx, gvec, gq
         nat.ptr(q), _ld(q), nat.ptr(k), _ld(k), nat.ptr(v), _ld(v), nat.ptr(vec), nat.ptr(pk),
         _ld(pk), nat.ptr(pv), _ld(pv), nat.ptr(C), nat.ptr(u), nat.ptr(gx), nat.ptr(gvec),
         nat.ptr(gq), nat.ptr(gk), nat.ptr(gv), nat.ptr(gw), nat.ptr(gpk), nat.ptr(gpv),
-        nat.ptr(gC), nat.ptr(gu), int(accumulate), None, nat.stream(q.device))
+        nat.ptr(gC), nat.ptr(gu), int(accumulate), nat.ptr(pk_rows), None, nat.stream(q.device))
     nat.check(rc, "tmdnet_et_message_bwd")
+
+
+def pair_index_launch(graph, pair_row, pair_edge):
+    lib = nat.load()
+    n = graph.n_nodes
+    ws = torch.empty(int(lib.tmdnet_pair_index_workspace_bytes(n)), dtype=torch.uint8, device=pair_row.device)
+    rc = lib.tmdnet_pair_index(n, nat.ptr(graph.row_ptr), nat.ptr(graph.src), nat.ptr(graph.dst),
+                               nat.ptr(graph.transpose), graph.n_edges, nat.ptr(graph.num_pairs_dev),
+                               int(getattr(graph, "sorted_rows", False)), nat.ptr(pair_row),
+                               nat.ptr(pair_edge), pair_edge.shape[0], nat.ptr(ws), ws.numel(),
+                               nat.stream(pair_row.device))
+    nat.check(rc, "tmdnet_pair_index")
+
+
+def pair_index(graph):
+    """(pair_row [E], pair_edge [P]) of a symmetric graph, cached on it: the two directions of a
+    pair share one dk/dv projection row (tmdnet_pair_index).  P = (E + N) // 2 slots bound the pair
+    count (every pair but the self loops has two edges); unused slots point at edge 0."""
+    cached = getattr(graph, "_pairs", None)
+    if cached is not None:
+        return cached
+    dev = graph.src.device
+    pair_row = torch.empty(graph.n_edges, dtype=torch.int32, device=dev)
+    pair_edge = torch.empty((graph.n_edges + graph.n_nodes) // 2, dtype=torch.int32, device=dev)
+    pair_index_launch(graph, pair_row, pair_edge)
+    graph._pairs = (pair_row, pair_edge)
+    return graph._pairs
 
 
 def _rowmajor(t):
