@@ -323,6 +323,14 @@ int tmdnet_pair_index(int n_nodes, const int32_t* row_ptr, const int32_t* src, c
                       int32_t* pair_row, int32_t* pair_edge, int n_pair_slots, void* workspace,
                       size_t workspace_bytes, void* stream);
 
+/* Grouped small fp32 GEMM on the f32 MFMA (node feature mixes of the ET layer, torchmd_et.py:272-312):
+ * up to 4 independent problems in one launch.  Problem i: dims[8i..8i+7] = {M, N, K, lda, ldb, ldc,
+ * trans_b, beta}, ptrs[4i..4i+3] = {A, B, bias (nullable), C}:
+ *   C[M][N] = beta * C + A[M][K] op(B) + bias[N],  op(B) = B^T for B [N][K] (trans_b) else B [K][N].
+ * Requirements: K % 64 == 0, lda % 4 == 0, A 16-byte aligned (and B when trans_b); else
+ * TMDNET_UNSUPPORTED (callers use the library GEMM).  Exact fp32 arithmetic. */
+int tmdnet_gemm_f32(int n_problems, const int* dims, const void* const* ptrs, void* stream);
+
 /* Library identification (for load checks). */
 const char* tmdnet_build_info(void);
 

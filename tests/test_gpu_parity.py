@@ -844,3 +844,31 @@ def _cpu(graph):
     from torchmdnet import kernels
     return kernels.EdgeGraph(graph.n_nodes, graph.row_ptr.cpu(), graph.src.cpu(), graph.dst.cpu(),
                              graph.transpose.cpu(), None, None, graph.num_pairs, True)
+
+
+def test_grouped_gemm_matches_torch():
+    """tmdnet_gemm_f32 (grouped, split-K MFMA f32) == torch fp64 GEMMs at the ET node shapes:
+    NT with bias ([q|k|v], o_proj), NT without (vec_proj), NN (input gradients), NN accumulate."""
+    from torchmdnet import kernels
+    _lib_loaded()
+    torch.manual_seed(8)
+    N, H = 678, 128
+    f = dict(dtype=torch.float32, device=DEV)
+    xn, vec, xa = torch.randn(N, H, **f), torch.randn(3 * N, H, **f), torch.randn(N, H, **f)
+    wqkv, bqkv = torch.randn(5 * H, H, **f) / 11, torch.randn(5 * H, **f)
+    wvec, wo, bo = torch.randn(3 * H, H, **f) / 11, torch.randn(3 * H, H, **f) / 11, torch.randn(3 * H, **f)
+    g_qkv, g_vecp = torch.randn(N, 5 * H, **f), torch.randn(3 * N, 3 * H, **f)
+    g_vec0 = torch.randn(3 * N, H, **f)
+    qkv, vecp, o = torch.empty(N, 5 * H, **f), torch.empty(3 * N, 3 * H, **f), torch.empty(N, 3 * H, **f)
+    g_xn, g_vec = torch.empty(N, H, **f), g_vec0.clone()
+    assert kernels.gemm_launch([(xn, wqkv, True, bqkv, qkv, False), (vec, wvec, True, None, vecp, False)])
+    assert kernels.gemm_launch([(xa, wo, True, bo, o, False)])
+    assert kernels.gemm_launch([(g_qkv, wqkv, False, None, g_xn, False), (g_vecp, wvec, False, None, g_vec, True)])
+    d = lambda t: t.double()  # noqa: E731
+    refs = [(qkv, d(xn) @ d(wqkv).t() + d(bqkv)), (vecp, d(vec) @ d(wvec).t()), (o, d(xa) @ d(wo).t() + d(bo)),
+            (g_xn, d(g_qkv) @ d(wqkv)), (g_vec, d(g_vec0) + d(g_vecp) @ d(wvec))]
+    for got, ref in refs:
+        assert _rel(got.cpu(), ref.cpu()) < 2e-6
+    # outside the envelope (K % 64): not launched
+    assert not kernels.gemm_launch([(torch.randn(5, 96, **f), torch.randn(7, 96, **f), True, None,
+                                     torch.empty(5, 7, **f), False)])

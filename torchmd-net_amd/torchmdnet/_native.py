@@ -61,6 +61,7 @@ SIGNATURES = {
     "tmdnet_silu_bwd": (I, [I, I, I, P, I, P, P, I, P, P, P]),
     "tmdnet_atom_sum_fwd": (I, [I, I, I, P, P, P, P, P, P]),
     "tmdnet_atom_sum_bwd": (I, [I, I, I, P, P, P, P, P]),
+    "tmdnet_gemm_f32": (I, [I, P, P, P]),
     "tmdnet_build_info": (ctypes.c_char_p, []),
 }
 

@@ -281,8 +281,14 @@ def _forward_layers(meta, x, f, C, u, params):
         vec_w, o_w, o_b = p[8], p[9], p[10]
         qkv_w, qkv_b = meta.qkv_eff[l]
         dkv_w, dkv_b = meta.dkv_layer(l)
-        qkv = torch.addmm(qkv_b, xn, qkv_w.t())
-        vecp = None if vec is None else torch.mm(vec.view(3 * N, H), vec_w.t()).view(N, 3, 3 * H)
+        # [q|k|v] and vec_proj in ONE launch (tmdnet_gemm_f32; library GEMMs outside its envelope)
+        qkv = torch.empty((N, qkv_w.shape[0]), dtype=x.dtype, device=x.device)
+        probs = [(xn, qkv_w, True, qkv_b, qkv, False)]
+        vecp = None
+        if vec is not None:
+            vecp = torch.empty((N, 3, 3 * H), dtype=x.dtype, device=x.device)
+            probs.append((vec.view(3 * N, H), vec_w, True, None, vecp.view(3 * N, 3 * H), False))
+        kernels.gemm_group(probs)
         if pkv_all is not None:
             pkv = pkv_all[:, l * D:(l + 1) * D]
         else:
@@ -293,7 +299,8 @@ def _forward_layers(meta, x, f, C, u, params):
         veca = torch.empty((N, 3, H), dtype=x.dtype, device=x.device)
         kernels.et_message_fwd_launch(qkv[:, :H], qkv[:, H:2 * H], qkv[:, 2 * H:], vec, pk, pv, C, u,
                                       meta.graph, meta.heads, xa, veca, meta.flags, meta.pk_rows)
-        o = torch.addmm(o_b, xa, o_w.t())
+        o = torch.empty((N, o_w.shape[0]), dtype=x.dtype, device=x.device)
+        kernels.gemm_group([(xa, o_w, True, o_b, o, False)])
         acts.append((x, vec, xn, mean, rstd, qkv, vecp, pkv, xa, o))
         if l + 1 < len(layers):
             x, vec, xn, mean, rstd = _epi_ln(x, vec, vecp, o, veca, layers[l + 1][0], layers[l + 1][1])
@@ -335,7 +342,8 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws):
             g_pkv = g_pkv_all[:, l * D:(l + 1) * D] if meta.batched else g_pkv_all
         if not epi_done:
             _epilogue_bwd(gX, gV, vecp, o_, g_vecp, g_o)
-        g_xa = torch.mm(g_o, o_w)
+        g_xa = torch.empty((N, H), **o)
+        kernels.gemm_group([(g_o, o_w, False, None, g_xa, False)])
         pk = pkv[:, :H] if meta.hk else None
         pv = pkv[:, H * int(meta.hk):] if meta.hv else None
         gpk = g_pkv[:, :H] if meta.hk else None
@@ -350,9 +358,12 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws):
                 g_f = torch.mm(g_pkv, dkv_w)
             else:
                 g_f.addmm_(g_pkv, dkv_w)
+        # vec_proj^T (accumulated into g_vec) and [q|k|v]^T in ONE launch
+        g_xn = torch.empty((N, H), **o)
+        probs = [(g_qkv, qkv_w, False, None, g_xn, False)]
         if vec is not None:
-            g_vec_in.view(3 * N, H).addmm_(g_vecp.view(3 * N, 3 * H), vec_w)
-        g_xn = torch.mm(g_qkv, qkv_w)
+            probs.append((g_vecp.view(3 * N, 3 * H), vec_w, False, None, g_vec_in.view(3 * N, H), True))
+        kernels.gemm_group(probs)
         need_w = need_ws[l]
         if need_w:  # LayerNorm weight gradients: PyTorch's backward
             g_x, g_lnw, g_lnb = torch.ops.aten.native_layer_norm_backward(g_xn, x, [H], mean, rstd, ln_w, ln_b,

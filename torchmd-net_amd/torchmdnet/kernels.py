@@ -816,6 +816,52 @@ def fused_act(act, x, scale=None):
     return y if scale is None else y * scale.view(-1, 1)
 
 
+# ----------------------------------------------------------------------------- small grouped GEMM
+GEMM_UNSUPPORTED = 2
+GEMM_MAX_ROWS = 16384  # above this the library GEMM's large tiles win (C5-size systems)
+
+
+def gemm_launch(problems):
+    """``tmdnet_gemm_f32``: up to 4 problems (A, B, trans_b, bias, C, beta) in one launch,
+    C = beta C + A op(B) + bias.  Returns False (nothing launched) when a problem is outside the
+    kernel's envelope (non-fp32, K % 64, alignment); the caller then uses the library GEMM."""
+    if any(A.dtype != torch.float32 or A.shape[0] > GEMM_MAX_ROWS for A, *_ in problems):
+        return False
+    lib = nat.load()
+    n = len(problems)
+    dims = (ctypes.c_int * (8 * n))()
+    ptrs = (ctypes.c_void_p * (4 * n))()
+    for i, (A, B, tb, bias, C, beta) in enumerate(problems):
+        if A.stride(1) != 1 or B.stride(1) != 1 or C.stride(1) != 1:
+            return False
+        dims[8 * i:8 * i + 8] = [A.shape[0], C.shape[1], A.shape[1], A.stride(0), B.stride(0), C.stride(0),
+                                 int(tb), int(beta)]
+        ptrs[4 * i:4 * i + 4] = [A.data_ptr(), B.data_ptr(), None if bias is None else bias.data_ptr(),
+                                 C.data_ptr()]
+    rc = lib.tmdnet_gemm_f32(n, dims, ptrs, nat.stream(problems[0][0].device))
+    if rc == GEMM_UNSUPPORTED:
+        return False
+    nat.check(rc, "tmdnet_gemm_f32")
+    return True
+
+
+def gemm_group(problems):
+    """The node feature-mix GEMMs of one step, grouped into one launch when the kernel supports
+    them (fp32); otherwise each through the library GEMM (fp64 parity runs)."""
+    if gemm_launch(problems):
+        return
+    for A, B, tb, bias, C, beta in problems:
+        Bop = B.t() if tb else B
+        if beta:
+            C.addmm_(A, Bop)
+            if bias is not None:
+                C.add_(bias)
+        elif bias is not None:
+            torch.addmm(bias, A, Bop, out=C)
+        else:
+            torch.mm(A, Bop, out=C)
+
+
 # ----------------------------------------------------------------------------- energy reduction
 ATOM_SUM_MAX_MOLECULES = 8192
 
