@@ -327,6 +327,51 @@ def rmd17_like(n_mol, gen_seed):
     return z, pos, batch
 
 
+def spice_like(n_mol, gen_seed):
+    """SPICE-like, 16 x 40 atoms, z = randint(1, 9), pos = randn * 2.5 A."""
+    g = torch.Generator().manual_seed(gen_seed)
+    z = torch.randint(1, 9, (n_mol * 40,), generator=g)
+    pos = torch.randn(n_mol * 40, 3, generator=g, dtype=torch.float64) * 2.5
+    batch = torch.arange(n_mol).repeat_interleave(40)
+    return z, pos, batch
+
+
+def secondary_spice(a, ws, rank, dev):
+    """C4: ET-SPICE (examples/ET-SPICE.yaml: 128 ch, 5 layers, cutoff 10, 128 neighbours), 16 x 40-atom
+    molecules per GPU: energy + forces (HIP-graph replay) and the training step (E+F loss with the
+    config's y / neg_dy weights 0.5 / 0.5, double backward, fused RCCL all-reduce, AdamW, eager)."""
+    import yaml
+    from torchmdnet.graphs import GraphedEnergyForces
+    from torchmdnet.models.model import create_model
+    from torchmdnet.training import LNNPStep
+    with open(os.path.join(ROOT, "tests", "golden", "configs", "et_spice.yaml")) as f:
+        args = yaml.safe_load(f)
+    args.update(prior_model=None, precision=32, derivative=True, output_model="Scalar")
+    torch.manual_seed(0)
+    model = create_model(args).to(dev)
+    n_mol = 16
+    z, pos, batch = spice_like(n_mol, 1 + rank)
+    z, pos, batch = z.to(dev), pos.float().to(dev), batch.to(dev)
+    gm = GraphedEnergyForces(model, z, pos, batch)
+    el = timed_loop(lambda: gm(pos), a.warmup, a.steps, ws, dev)
+    gm.check_capacity()
+    gm.release()
+    res = {"workload": "ET-SPICE energy+forces (C4: 16 x 40 atoms, 5 layers, cutoff 10), hip-graph replay",
+           "value": round(n_mol * ws * a.steps / el, 2), "unit": "molecules/s",
+           "ms_per_step": round(1000 * el / a.steps, 4), "atoms_per_gpu": int(z.shape[0])}
+    gy = torch.Generator().manual_seed(200 + rank)
+    y_lab = torch.randn(n_mol, 1, generator=gy).to(dev)
+    f_lab = torch.randn(z.shape[0], 3, generator=gy).to(dev)
+    trainer = LNNPStep(model, lr=1e-4, y_weight=0.5, neg_dy_weight=0.5)
+    steps = max(10, a.steps // 2)
+    el = timed_loop(lambda: trainer.step(z, pos, batch, y_lab, f_lab), max(3, a.warmup // 2), steps, ws, dev)
+    res["train_step"] = {"workload": "ET-SPICE training step (E+F MSE 0.5/0.5, double backward, "
+                                     + ("fused RCCL all-reduce, " if ws > 1 else "") + "AdamW), eager",
+                         "value": round(n_mol * ws * steps / el, 2), "unit": "molecules/s",
+                         "ms_per_step": round(1000 * el / steps, 4), "parallelism": f"dp{ws}"}
+    return res
+
+
 def secondary_tensornet(a, ws, rank, dev):
     """C3: TensorNet-rMD17 (8 x 21 atoms, O(3), static_shapes as the reference default), energy +
     forces, HIP-graph replay, molecules/s over all ranks."""
@@ -550,6 +595,8 @@ def main():
         sec = {"tensornet_c3": secondary_tensornet(a, ws, rank, dev)}
         phase("secondary: ET training step")
         sec["et_train_step"] = secondary_train(a, ws, rank, dev)
+        phase("secondary: ET-SPICE C4")
+        sec["et_spice_c4"] = secondary_spice(a, ws, rank, dev)
         phase("secondary: ET C5 water box")
         sec["et_water_box_c5"] = secondary_water_box(a, ws, rank, dev)
         if rank == 0:
