@@ -92,6 +92,11 @@ int tmdnet_edge_geom_fwd(int dtype, int n_edges, int num_rbf, int rbf_type, cons
                          void* cutoff, void* unit, void* stream);
 /* Backward: given grad_rbf [E][R], grad_cutoff [E], grad_unit [E][3] (each nullable) produce
  * grad_dist [E] and grad_deltas [E][3] (both overwritten). */
+/* d rbf_k / d r of edges rows[p] (rows NULL: edge p), out [n_rows][R] -- the RBF derivative the ET
+ * force pass contracts with the dk/dv projection (tmdnet_et_message_bwd's dpk / dpv rows). */
+int tmdnet_rbf_deriv(int dtype, int num_rbf, int rbf_type, const void* dist, const void* mu,
+                     const void* beta, double cutoff_lower, double cutoff_upper, const int32_t* rows,
+                     int n_rows, void* out, void* stream);
 int tmdnet_edge_geom_bwd(int dtype, int n_edges, int num_rbf, int rbf_type, const int32_t* src,
                          const int32_t* dst, const void* deltas, const void* dist, const void* mu,
                          const void* beta, double cutoff_lower, double cutoff_upper,
@@ -137,8 +142,13 @@ int tmdnet_et_message_bwd(int dtype, int n_nodes, int hidden, int heads, const i
                           int ld_pk, const void* pv, int ld_pv, const void* cutoff, const void* unit,
                           const void* grad_x, const void* grad_vec, void* gq, void* gk, void* gv,
                           void* gvec_in, void* gpk, void* gpv, void* gcut, void* gunit,
-                          int accumulate, const int32_t* pk_rows, const int32_t* order,
+                          const void* dpk, const void* dpv, void* gdist, int accumulate,
+                          const int32_t* pk_rows, const int32_t* order,
                           void* stream);  /* accumulate may also carry TMDNET_ET_V_PLANAR */
+/* "dr mode" of the backward (gdist non-NULL, requires TMDNET_ACC_EDGE): instead of storing gpk / gpv
+ * (then NULL), the projection gradient of every edge is contracted in-kernel with dpk = d pk / d r,
+ * dpv = d pv / d r (rows and layout of pk / pv, read through pk_rows) and accumulated into
+ * gdist[e] -- the force pass then needs neither the E x 4H gradient nor its GEMM. */
 
 /* Second-order backward: the VJP of tmdnet_et_message_bwd (forces differentiated again, reference
  * model.py:286-298 with create_graph=True).  gg_* are the cotangents of that call's outputs (gq, gk,

@@ -74,8 +74,9 @@ def _fake_fwd(q, k, v, vec, pk, pv, C, u, graph, heads, xo, vo, flags=0, pk_rows
 
 
 def _fake_bwd(q, k, v, vec, pk, pv, C, u, graph, heads, gx, gvec, gq, gk, gv, gw, gpk, gpv, gC, gu,
-              accumulate=0, pk_rows=None):
+              accumulate=0, pk_rows=None, dpk=None, dpv=None, g_r=None):
     pk, pv = _expand_rows(pk, pv, pk_rows)
+    dpk, dpv = _expand_rows(dpk, dpv, pk_rows)
     N, H = q.shape
     planar = bool(accumulate & nat.ET_V_PLANAR)
     v, pv = _to_inter(v, H, heads, planar), _to_inter(pv, H, heads, planar)
@@ -99,6 +100,12 @@ def _fake_bwd(q, k, v, vec, pk, pv, C, u, graph, heads, gx, gvec, gq, gk, gv, gw
         gpk.copy_(z(g[4], pk))
     if gpv is not None:
         gpv.copy_(_to_planar(z(g[5], pv), H, heads, planar))
+    if g_r is not None:  # dr mode: <g_pk, dpk> + <g_pv, dpv> per edge (dpv in the kernel's row layout)
+        assert gpk is None and gpv is None and accumulate & nat.ACC_EDGE
+        if dpk is not None:
+            g_r.add_((z(g[4], pk) * dpk).sum(1))
+        if dpv is not None:
+            g_r.add_((_to_planar(z(g[5], pv), H, heads, planar) * dpv).sum(1))
     if accumulate & nat.ACC_EDGE:
         gC.add_(g[6])
         gu.add_(g[7])
@@ -153,6 +160,18 @@ def _fake_ln_bwd_epi(g_xn, x, mean, rstd, ln_w, g_res, g_vec, vecp, o, g_vecp, g
     return g_x
 
 
+def _fake_rbf_deriv(r, mu, beta, cl, cu, rbf_type, rows, out):
+    rr = r if rows is None else r.index_select(0, rows.long())
+    cols = []
+    for k in range(mu.shape[0]):  # f_k(r_e) depends on r_e only: d/dr of the column sum
+        with torch.enable_grad():
+            x = rr.detach().clone().requires_grad_(True)
+            fk = kernels.rbf_composite(x, mu, beta, cl, cu, rbf_type)[:, k]
+            (g,) = torch.autograd.grad(fk.sum(), x)
+        cols.append(g)
+    out.copy_(torch.stack(cols, 1))
+
+
 def _fake_bwd2(ctx, ggs):
     return kernels._ETMessageBwd.composite_backward(ctx, *ggs)
 
@@ -163,6 +182,7 @@ def emulated(monkeypatch):
     monkeypatch.setattr(kernels, "pair_index_launch", _fake_pair_index)
     monkeypatch.setattr(kernels, "et_message_bwd_launch", _fake_bwd)
     monkeypatch.setattr(kernels, "et_message_bwd2", _fake_bwd2)
+    monkeypatch.setattr(kernels, "rbf_deriv_launch", _fake_rbf_deriv)
     monkeypatch.setattr(ES, "_epilogue_fwd", _fake_epi_fwd)
     monkeypatch.setattr(ES, "_epilogue_bwd", _fake_epi_bwd)
     monkeypatch.setattr(ES, "_epi_ln", _fake_epi_ln)
@@ -276,9 +296,9 @@ def test_stack_force_pass_skips_weight_grads_but_training_gets_them(emulated, mo
     calls = []
     orig = ES._backward_layers
 
-    def spy(meta, gX, gV, f_, C_, u_, params_, acts, need_ws):
+    def spy(meta, gX, gV, f_, C_, u_, params_, acts, need_ws, **kw):
         calls.append(tuple(need_ws))
-        return orig(meta, gX, gV, f_, C_, u_, params_, acts, need_ws)
+        return orig(meta, gX, gV, f_, C_, u_, params_, acts, need_ws, **kw)
 
     ES._backward_layers = spy
     try:
@@ -315,3 +335,54 @@ def test_stack_partial_parameter_request(emulated):
                                 [p for l in layers for p in ES.layer_params(l)])
     (gr,) = torch.autograd.grad(xr.sum() + vr.sum(), [layers[1].o_proj.weight])
     assert torch.allclose(g, gr, atol=1e-11)
+
+
+@pytest.mark.parametrize("rbf_type", [nat.RBF_GAUSS, nat.RBF_EXPNORM])
+@pytest.mark.parametrize("planar", [False, True])
+@pytest.mark.parametrize("batched", [True, False])
+@pytest.mark.parametrize("infl", ["both", "keys", "values"])
+def test_stack_dr_mode_force_pass_and_second_order(emulated, monkeypatch, infl, batched, planar, rbf_type):
+    """Force pass with f = rbf(r) declared (the ET model's fixed basis): the stack returns the edge
+    gradient on r directly (dr mode, no projection gradient); forces and the force-matching second
+    order (weight gradients through a create_graph force pass) equal plain autograd."""
+    monkeypatch.setattr(ES, "DR_MODE", "1")  # also on the stacked (batched) projection path
+    if not batched:
+        monkeypatch.setattr(ES, "BATCH_DKV_BYTES", 0)
+    if planar:
+        monkeypatch.setattr(ES, "PLANAR_MIN_EDGES", 0)
+    H, R, heads = 16, 8, 4
+    cl, cu = 0.0, 4.0
+    n, graph, r, vecs = _system()
+    x, _, C, u = _inputs(n, graph, r, vecs, H, R)
+    if rbf_type == nat.RBF_GAUSS:
+        mu, beta = torch.linspace(0, 4, R, dtype=DT), torch.full((R,), -1.0, dtype=DT)
+    else:
+        mu, beta = torch.linspace(math.exp(-4.0), 1.0, R, dtype=DT), torch.full((R,), 3.0, dtype=DT)
+    layers = _layers(2, H, R, heads, infl)
+    params = [p for l in layers for p in ES.layer_params(l)]
+    modes = []
+    orig = ES._backward_layers
+
+    def spy(*a, **kw):
+        modes.append(kw.get("dr", False))
+        return orig(*a, **kw)
+
+    monkeypatch.setattr(ES, "_backward_layers", spy)
+    outs = []
+    for fused in (True, False):
+        rl, xl, Cl, ul = (t.clone().requires_grad_(True) for t in (r, x, C, u))
+        f = kernels.rbf_composite(rl, mu, beta, cl, cu, rbf_type)
+        if fused:
+            xo, vo = ES.et_stack(layers, xl, graph, f, Cl, ul, rbf=(rl, mu, beta, cl, cu, rbf_type))
+        else:
+            xo, vo = ES.composite_stack(_meta_for(layers, graph), xl, f, Cl, ul, params)
+        e = (xo ** 2).sum() + 0.3 * (vo ** 2).sum()
+        g = torch.autograd.grad(e, [rl, xl, Cl, ul], create_graph=True)
+        loss = e + sum((gi ** 2).sum() for gi in g)
+        for p in params:
+            p.grad = None
+        loss.backward()
+        outs.append([t.detach().clone() for t in g] + [p.grad.clone() for p in params])
+    assert modes[0] is True and modes[1] is False  # force pass in dr mode, loss.backward not
+    for i, (a, b) in enumerate(zip(*outs)):
+        assert torch.allclose(a, b, atol=1e-10, rtol=1e-8), i

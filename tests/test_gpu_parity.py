@@ -374,6 +374,49 @@ def test_et_edge_kernel_gradcheck():
         assert torch.allclose(ga, gb, atol=1e-10, rtol=1e-9), name
 
 
+@pytest.mark.parametrize("planar", [False, True])
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_et_bwd_dr_mode_matches_projection_gradient(dtype, planar):
+    """dr mode of tmdnet_et_message_bwd (the force pass): g_r[e] = <g_pk[e], dpk[row(e)]> +
+    <g_pv[e], dpv[row(e)]> of the plain backward over the pair-shared rows, every other output
+    unchanged."""
+    from torchmdnet import _native as nat
+    from torchmdnet import kernels
+    torch.manual_seed(0)
+    z, pos, batch = O.qm9_like(4)
+    g = kernels.build_graph(pos.to(DEV).to(dtype), batch.to(DEV), 0.0, 5.0, 64 * pos.shape[0], loop=True)
+    N, H, heads, E = pos.shape[0], 64, 8, g.n_edges
+    pr, pe = kernels.pair_index(g)
+    o = dict(dtype=dtype, device=DEV)
+    P = pe.shape[0]
+    q, k, v, vec = torch.randn(N, H, **o), torch.randn(N, H, **o), torch.randn(N, 3 * H, **o), torch.randn(N, 3, H, **o)
+    pkv, dpkv = torch.randn(P, 4 * H, **o), torch.randn(P, 4 * H, **o)
+    C, u = torch.rand(E, **o), torch.randn(E, 3, **o)
+    gx, gvec = torch.randn(N, H, **o), torch.randn(N, 3, H, **o)
+    flags = nat.ACC_VEC_RESIDUAL | nat.ACC_EDGE | (nat.ET_V_PLANAR if planar else 0)
+
+    def run(dr):
+        gq, gk, gv, gw = (torch.empty(N, H, **o), torch.empty(N, H, **o), torch.empty(N, 3 * H, **o),
+                          torch.empty(N, 3, H, **o))
+        gC, gu = torch.zeros(E, **o), torch.zeros(E, 3, **o)
+        gpkv = None if dr else torch.empty(E, 4 * H, **o)
+        gr = torch.zeros(E, **o) if dr else None
+        kernels.et_message_bwd_launch(
+            q, k, v, vec, pkv[:, :H], pkv[:, H:], C, u, g, heads, gx, gvec, gq, gk, gv, gw,
+            None if dr else gpkv[:, :H], None if dr else gpkv[:, H:], gC, gu, accumulate=flags, pk_rows=pr,
+            dpk=dpkv[:, :H] if dr else None, dpv=dpkv[:, H:] if dr else None, g_r=gr)
+        return [gq, gk, gv, gw, gC, gu], gpkv, gr
+
+    base, gpkv, _ = run(False)
+    drs, _, gr = run(True)
+    torch.cuda.synchronize()
+    tol = 1e-12 if dtype == torch.float64 else 1e-5
+    for a, b in zip(base, drs):
+        assert _rel(a.cpu(), b.cpu()) < tol
+    ref = (gpkv * dpkv.index_select(0, pr.long())).sum(1)
+    assert _rel(gr.cpu(), ref.cpu()) < (1e-12 if dtype == torch.float64 else 1e-5)
+
+
 # ----------------------------------------------------------------------------- TensorNet
 @pytest.mark.parametrize("name", ["tn_tiny_o3_static_f64", "tn_tiny_so3_static_f64", "tn_tiny_o3_dyn_f64",
                                   "tn_tiny_so3_dyn_f64", "tn_tiny_o3_static_f32"])
@@ -489,14 +532,17 @@ def test_large_system_spatial_reorder_is_transparent():
     assert _rel(out[0][1].cpu(), out[1][1].cpu()) < 1e-9
 
 
+@pytest.mark.parametrize("dr", ["auto", "0"])
 @pytest.mark.parametrize("planar", [False, True])
 @pytest.mark.parametrize("infl", ["both", "keys", "values", "none"])
-def test_et_fused_stack_matches_per_layer_path(infl, planar, monkeypatch):
+def test_et_fused_stack_matches_per_layer_path(infl, planar, dr, monkeypatch):
     """et_stack (one autograd node, fused GEMMs + HIP epilogue) == the per-layer module path:
     energies, forces and force-loss training gradients (double backward), fp64.  planar: the
-    large-graph TMDNET_ET_V_PLANAR layout forced on."""
+    large-graph TMDNET_ET_V_PLANAR layout forced on; dr "auto": the force pass in dr mode (its second
+    order re-forms the features from r), "0": the projection-gradient path."""
     from torchmdnet import et_stack
     from torchmdnet.models.model import create_model
+    monkeypatch.setattr(et_stack, "DR_MODE", dr)
     if planar:
         monkeypatch.setattr(et_stack, "PLANAR_MIN_EDGES", 0)
     _seed()

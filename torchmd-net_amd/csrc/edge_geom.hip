@@ -135,6 +135,19 @@ __global__ __launch_bounds__(256) void k_bwd(Cfg<T> P, const T* __restrict__ gf,
   }
 }
 
+// d f_k / d r of the edges rows[p] (rows NULL: p itself), [n_rows][R]: the edge-feature derivative the
+// ET force pass contracts with the projection gradient (et_stack, "dr mode")
+template <typename T>
+__global__ void k_deriv(Cfg<T> P, const int32_t* __restrict__ rows, int n_rows, T* __restrict__ out) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)n_rows * P.R) return;
+  const int p = (int)(i / P.R), k = (int)(i % P.R);
+  const int e = rows ? rows[p] : p;
+  T v, dv;
+  basis(P, P.r[e], k, v, dv);
+  out[i] = dv;
+}
+
 template <typename T>
 static Cfg<T> make(int E, int R, int type, const int32_t* src, const int32_t* dst, const void* dl,
                    const void* r, const void* mu, const void* beta, double cl, double cu) {
@@ -190,6 +203,28 @@ extern "C" int tmdnet_edge_geom_bwd(int dtype, int n_edges, int num_rbf, int rbf
     auto P = geom::make<double>(n_edges, num_rbf, rbf_type, src, dst, deltas, dist, mu, beta, cutoff_lower, cutoff_upper);
     hipLaunchKernelGGL(geom::k_bwd<double>, dim3(blocks), dim3(tb), 0, st, P, (const double*)grad_rbf,
                        (const double*)grad_cutoff, (const double*)grad_unit, (double*)grad_dist, (double*)grad_deltas);
+  } else {
+    return kUnsupported;
+  }
+  return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
+}
+
+extern "C" int tmdnet_rbf_deriv(int dtype, int num_rbf, int rbf_type, const void* dist, const void* mu,
+                                const void* beta, double cutoff_lower, double cutoff_upper,
+                                const int32_t* rows, int n_rows, void* out, void* stream) {
+  if (n_rows < 0 || num_rbf <= 0 || !dist || !mu || !beta || !out) return kBadArgument;
+  if (n_rows == 0) return kOk;
+  hipStream_t st = (hipStream_t)stream;
+  const long long work = (long long)n_rows * num_rbf;
+  const dim3 g((unsigned)((work + 255) / 256));
+  if (dtype == TMDNET_F32) {
+    auto P = geom::make<float>(0, num_rbf, rbf_type, nullptr, nullptr, nullptr, dist, mu, beta, cutoff_lower,
+                               cutoff_upper);
+    hipLaunchKernelGGL(geom::k_deriv<float>, g, dim3(256), 0, st, P, rows, n_rows, (float*)out);
+  } else if (dtype == TMDNET_F64) {
+    auto P = geom::make<double>(0, num_rbf, rbf_type, nullptr, nullptr, nullptr, dist, mu, beta, cutoff_lower,
+                                cutoff_upper);
+    hipLaunchKernelGGL(geom::k_deriv<double>, g, dim3(256), 0, st, P, rows, n_rows, (double*)out);
   } else {
     return kUnsupported;
   }

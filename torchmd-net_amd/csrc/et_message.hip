@@ -88,6 +88,9 @@ template <typename T> struct Args {
   const T* pk; int ldpk;
   const T* pv; int ldpv;
   const int32_t* prow;  // row of pk / pv holding edge e's projection (pair-shared rows); NULL: row e
+  const T* dpk;         // "dr mode" (backward): d pk / d r, d pv / d r rows (layout of pk / pv); the
+  const T* dpv;         // projection gradient is contracted with them into gr[e] instead of stored
+  T* gr;                // [E] accumulated d/d r (dr mode)
   const T* C;
   const T* u;
   // forward outputs
@@ -347,7 +350,7 @@ __device__ __forceinline__ void zero_pad_rows(const Args<T>& A, int blk, int nwg
   }
 }
 
-template <typename T, int V, int S, int CS>
+template <typename T, int V, int S, int CS, bool DR>
 __device__ __forceinline__ void bwd_dst_body(const Args<T>& A, int blk, int nwg) {
   __shared__ T lds[S > 1 ? 4 * 64 * V : 1];
   const Geo G = geo<S, CS, false>(A.n, A.L, nullptr, A.xcd, blk, nwg);
@@ -374,21 +377,25 @@ __device__ __forceinline__ void bwd_dst_body(const Args<T>& A, int blk, int nwg)
     const int b = min(A.row_ptr[t], A.cap), e = min(A.row_ptr[t + 1], A.cap);
     const T* dummy = A.q + (size_t)t * A.ldq;
     const bool acc_edge = (A.acc & TMDNET_ACC_EDGE) && G.el == 0;
-    struct St { T k[V], x[V], a[V], b[V]; };
+    // dr mode (DR): the edge's (pair) row index rides along; d pk / d r, d pv / d r are loaded in
+    // the body with the source-row gathers (prefetching them too costs occupancy: 183 vs 157 VGPRs)
+    struct St { T k[V], x[V], a[V], b[V]; int row; };
     auto ld = [&](int k, St& st) {
       ldv<T, V>(st.k, opt(A.pk, (size_t)k * A.ldpk + c0, dummy + c0));
       const T* pvs = opt(A.pv, (size_t)k * A.ldpv + vo, dummy);
       ldv<T, V>(st.x, pvs);
       ldv<T, V>(st.a, pvs + pvd);
       ldv<T, V>(st.b, pvs + 2 * pvd);
+      st.row = k;
     };
     auto body = [&](int k, int s, T Ce, T u0, T u1, T u2, const St& st, auto&& pre) {
-      T oc = T(0), ou0 = T(0), ou1 = T(0), ou2 = T(0);  // accumulate mode: issued with the loads
+      T oc = T(0), ou0 = T(0), ou1 = T(0), ou2 = T(0), orr = T(0);  // accumulate mode: issued with the loads
       if (acc_edge) {
         oc = A.gC[k];
         ou0 = A.gu[3 * k];
         ou1 = A.gu[3 * k + 1];
         ou2 = A.gu[3 * k + 2];
+        if constexpr (DR) orr = A.gr[k];
       }
       T kk[V], vx[V], v1[V], v2[V], w0[V], w1[V], w2[V];
       ldv<T, V>(kk, A.k + (size_t)s * A.ldk + c0);
@@ -400,6 +407,14 @@ __device__ __forceinline__ void bwd_dst_body(const Args<T>& A, int blk, int nwg)
       ldv<T, V>(w0, vecs);
       ldv<T, V>(w1, vecs + vcd);
       ldv<T, V>(w2, vecs + 2 * vcd);
+      T dpk_[DR ? V : 1], dpx_[DR ? V : 1], dp1_[DR ? V : 1], dp2_[DR ? V : 1];
+      if constexpr (DR) {
+        ldv<T, V>(dpk_, opt(A.dpk, (size_t)st.row * A.ldpk + c0, dummy + c0));
+        const T* dps = opt(A.dpv, (size_t)st.row * A.ldpv + vo, dummy);
+        ldv<T, V>(dpx_, dps);
+        ldv<T, V>(dp1_, dps + pvd);
+        ldv<T, V>(dp2_, dps + 2 * pvd);
+      }
       pre();
       if (!hw) { zero(w0); zero(w1); zero(w2); }
       const T (&pk)[V] = st.k;
@@ -441,13 +456,22 @@ __device__ __forceinline__ void bwd_dst_body(const Args<T>& A, int blk, int nwg)
       gu0 = group_sum(gu0, A.L);
       gu1 = group_sum(gu1, A.L);
       gu2 = group_sum(gu2, A.L);
-      if (on) {
-        if (hk) stv<T, V>(A.gpk + (size_t)k * A.ldpk + c0, gpk);
-        if (hv) {
-          T* gp = A.gpv + (size_t)k * A.ldpv + vo;
-          stv<T, V>(gp, gpx);
-          stv<T, V>(gp + A.vst, gp1);
-          stv<T, V>(gp + 2 * A.vst, gp2);
+      T grr = T(0);
+      if constexpr (DR) {  // d/dr through the projections: <g_pk, d pk/dr> + <g_pv, d pv/dr>
+#pragma unroll
+        for (int i = 0; i < V; ++i)
+          grr += (hk ? gpk[i] * dpk_[i] : T(0)) +
+                 (hv ? gpx[i] * dpx_[i] + gp1[i] * dp1_[i] + gp2[i] * dp2_[i] : T(0));
+        grr = group_sum(grr, A.L);
+      } else {
+        if (on) {
+          if (hk) stv<T, V>(A.gpk + (size_t)k * A.ldpk + c0, gpk);
+          if (hv) {
+            T* gp = A.gpv + (size_t)k * A.ldpv + vo;
+            stv<T, V>(gp, gpx);
+            stv<T, V>(gp + A.vst, gp1);
+            stv<T, V>(gp + 2 * A.vst, gp2);
+          }
         }
       }
       if (G.el == 0) {
@@ -455,6 +479,7 @@ __device__ __forceinline__ void bwd_dst_body(const Args<T>& A, int blk, int nwg)
         A.gu[3 * k] = ou0 + gu0;
         A.gu[3 * k + 1] = ou1 + gu1;
         A.gu[3 * k + 2] = ou2 + gu2;
+        if constexpr (DR) A.gr[k] = orr + grr;
       }
     };
     edge_chunks_pf<T, S, 1, St>(A, b, e, EPW, G, ld, body);
@@ -592,9 +617,14 @@ __device__ __forceinline__ void bwd_src_body(const Args<T>& A, int blk, int nwg)
   }
 }
 
-template <typename T, int V, int S, int CS>
-__global__ __launch_bounds__(256) void k_bwd_dst(Args<T> A) {
-  bwd_dst_body<T, V, S, CS>(A, blockIdx.x, gridDim.x);
+// (fp32 dr variants: 3 waves / SIMD asked for -- they sit a few VGPRs above the 168 that allow it;
+// 12 B/lane spill, measured faster than 2 waves)
+template <typename T, int V, bool DR>
+constexpr int bwd_min_waves() { return (DR && sizeof(T) == 4 && V <= 4) ? 3 : 1; }
+
+template <typename T, int V, int S, int CS, bool DR>
+__global__ __launch_bounds__(256, (bwd_min_waves<T, V, DR>())) void k_bwd_dst(Args<T> A) {
+  bwd_dst_body<T, V, S, CS, DR>(A, blockIdx.x, gridDim.x);
 }
 template <typename T, int V, int S, int CS>
 __global__ __launch_bounds__(256) void k_bwd_src(Args<T> A) {
@@ -603,10 +633,10 @@ __global__ __launch_bounds__(256) void k_bwd_src(Args<T> A) {
 // Both passes in ONE grid (they only read the same inputs): blocks [0, split) run the destination
 // pass, [split, 2 split) the source pass.  Used for small systems, where one pass alone leaves most
 // of the chip idle and the launch gap between the two passes is a visible share of the layer.
-template <typename T, int V, int S, int CS>
-__global__ __launch_bounds__(256) void k_bwd_both(Args<T> A) {
+template <typename T, int V, int S, int CS, bool DR>
+__global__ __launch_bounds__(256, (bwd_min_waves<T, V, DR>())) void k_bwd_both(Args<T> A) {
   const int split = (int)gridDim.x / 2;
-  if ((int)blockIdx.x < split) bwd_dst_body<T, V, S, CS>(A, blockIdx.x, split);
+  if ((int)blockIdx.x < split) bwd_dst_body<T, V, S, CS, DR>(A, blockIdx.x, split);
   else bwd_src_body<T, V, S, CS>(A, blockIdx.x - split, split);
 }
 
@@ -1002,9 +1032,11 @@ static int et_launch_vs(Args<T> A, hipStream_t st) {
   const int nbn = (A.n + (4 / S) - 1) / (4 / S);
   const dim3 g(nbn * cs), b(256);
   if (KIND == 0) hipLaunchKernelGGL((k_fwd<T, V, S, 1, ORD>), g, b, 0, st, A);
-  else if (KIND == 1) hipLaunchKernelGGL((k_bwd_dst<T, V, S, 1>), g, b, 0, st, A);
+  else if (KIND == 1) hipLaunchKernelGGL((k_bwd_dst<T, V, S, 1, false>), g, b, 0, st, A);
   else if (KIND == 2) hipLaunchKernelGGL((k_bwd_src<T, V, S, 1>), g, b, 0, st, A);
-  else hipLaunchKernelGGL((k_bwd_both<T, V, S, 1>), dim3(2 * nbn), b, 0, st, A);
+  else if (KIND == 3) hipLaunchKernelGGL((k_bwd_both<T, V, S, 1, false>), dim3(2 * nbn), b, 0, st, A);
+  else if (KIND == 4) hipLaunchKernelGGL((k_bwd_dst<T, V, S, 1, true>), g, b, 0, st, A);
+  else hipLaunchKernelGGL((k_bwd_both<T, V, S, 1, true>), dim3(2 * nbn), b, 0, st, A);
   return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
 }
 
@@ -1088,8 +1120,8 @@ static int bwd(int n, int H, int heads, const int32_t* row_ptr, const int32_t* s
                const void* q, int ldq, const void* k, int ldk, const void* v, int ldv_,
                const void* vec, const void* pk, int ldpk, const void* pv, int ldpv, const void* C,
                const void* u, const void* gx, const void* gvec, void* gq, void* gk, void* gv,
-               void* gveci, void* gpk, void* gpv, void* gC, void* gu, int acc,
-               const int32_t* prow, const int32_t* order, hipStream_t st) {
+               void* gveci, void* gpk, void* gpv, void* gC, void* gu, const void* dpk, const void* dpv,
+               void* gr, int acc, const int32_t* prow, const int32_t* order, hipStream_t st) {
   Args<T> A;
   int V;
   int rc = setup<T>(A, n, H, heads, row_ptr, src, cap, q, ldq, k, ldk, v, ldv_, vec, pk, ldpk, pv,
@@ -1098,11 +1130,15 @@ static int bwd(int n, int H, int heads, const int32_t* row_ptr, const int32_t* s
   A.gx = (const T*)gx; A.gvec = (const T*)gvec;
   A.gq = (T*)gq; A.gk = (T*)gk; A.gv = (T*)gv; A.gveci = (T*)gveci;
   A.gpk = (T*)gpk; A.gpv = (T*)gpv; A.gC = (T*)gC; A.gu = (T*)gu;
+  A.dpk = (const T*)dpk; A.dpv = (const T*)dpv; A.gr = (T*)gr;
   A.acc = acc;
   if (acc & TMDNET_ET_V_PLANAR) { A.planar = 1; A.vst = H; }
+  const bool dr = gr != nullptr;
+  if (dr && ((A.pk && !dpk) || (A.pv && !dpv) || !(acc & TMDNET_ACC_EDGE))) return kBadArgument;
+  if (!dr && ((A.pk && !gpk) || (A.pv && !gpv))) return kBadArgument;
   static const int fuse_nodes = getenv("TMDNET_ET_FUSE") ? atoi(getenv("TMDNET_ET_FUSE")) : kBwdFuseNodes;
-  if (n < fuse_nodes) return et_launch<T, 3, false>(V, A, st);
-  rc = et_launch<T, 1, false>(V, A, st);
+  if (n < fuse_nodes) return dr ? et_launch<T, 5, false>(V, A, st) : et_launch<T, 3, false>(V, A, st);
+  rc = dr ? et_launch<T, 4, false>(V, A, st) : et_launch<T, 1, false>(V, A, st);
   if (rc) return rc;
   return et_launch<T, 2, false>(V, A, st);
 }
@@ -1190,17 +1226,18 @@ extern "C" int tmdnet_et_message_bwd(int dtype, int n_nodes, int hidden, int hea
                                      const void* pv, int ld_pv, const void* cutoff, const void* unit,
                                      const void* grad_x, const void* grad_vec, void* gq, void* gk,
                                      void* gv, void* gvec_in, void* gpk, void* gpv, void* gcut,
-                                     void* gunit, int accumulate, const int32_t* pk_rows,
-                                     const int32_t* order, void* stream) {
+                                     void* gunit, const void* dpk, const void* dpv, void* gdist,
+                                     int accumulate, const int32_t* pk_rows, const int32_t* order,
+                                     void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (dtype == TMDNET_F32)
     return et::bwd<float>(n_nodes, hidden, heads, row_ptr, src, max_pairs, q, ld_q, k, ld_k, v, ld_v,
                           vec_in, pk, ld_pk, pv, ld_pv, cutoff, unit, grad_x, grad_vec, gq, gk, gv,
-                          gvec_in, gpk, gpv, gcut, gunit, accumulate, pk_rows, order, st);
+                          gvec_in, gpk, gpv, gcut, gunit, dpk, dpv, gdist, accumulate, pk_rows, order, st);
   if (dtype == TMDNET_F64)
     return et::bwd<double>(n_nodes, hidden, heads, row_ptr, src, max_pairs, q, ld_q, k, ld_k, v, ld_v,
                            vec_in, pk, ld_pk, pv, ld_pv, cutoff, unit, grad_x, grad_vec, gq, gk, gv,
-                           gvec_in, gpk, gpv, gcut, gunit, accumulate, pk_rows, order, st);
+                           gvec_in, gpk, gpv, gcut, gunit, dpk, dpv, gdist, accumulate, pk_rows, order, st);
   return kUnsupported;
 }
 

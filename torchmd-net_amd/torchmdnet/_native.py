@@ -37,7 +37,8 @@ SIGNATURES = {
     "tmdnet_et_message_fwd": (I, [I, I, I, I, P, P, I, P, I, P, I, P, I, P, P, I, P, I, P, P, P, P, I, P, P,
                                   P]),
     "tmdnet_et_message_bwd": (I, [I, I, I, I, P, P, I, P, I, P, I, P, I, P, P, I, P, I, P, P, P, P,
-                                  P, P, P, P, P, P, P, P, I, P, P, P]),
+                                  P, P, P, P, P, P, P, P, P, P, P, I, P, P, P]),
+    "tmdnet_rbf_deriv": (I, [I, I, I, P, P, P, D, D, P, I, P, P]),
     "tmdnet_pair_index_workspace_bytes": (SZ, [I]),
     "tmdnet_pair_index": (I, [I, P, P, P, P, I, P, I, P, P, I, P, SZ, P]),
     "tmdnet_et_message_bwd2": (I, [I, I, I, I, P, P, I, P, I, P, I, P, I, P, P, I, P, I, P, P, P, P,

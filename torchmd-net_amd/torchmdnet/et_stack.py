@@ -24,6 +24,8 @@ and autograd's generic per-op backward.
 The backward is itself a Function so forces stay differentiable (training on forces); its own
 backward (second order) recomputes the stack with composite PyTorch ops and differentiates twice.
 """
+import os
+
 import torch
 import torch.nn.functional as F
 from torch.autograd import Function
@@ -118,6 +120,12 @@ BATCH_DKV_BYTES = 2 << 30
 PLANAR_MIN_EDGES = 131072
 # dk/dv projection rows shared by the two directions of an edge pair (halves the projection GEMM)
 PAIR_ROWS = True
+# "dr mode" force pass (see _backward_layers): on whenever the force pass needs no weight gradient
+# and the features are a fixed basis of r (also under create_graph, which the reference force pass
+# always uses: the second order then re-forms f from r by the composite basis).  Measured on
+# MI355X: C2 1.076 -> 1.063 ms, C4 0.932 -> 0.917 ms, C5 73.9 -> 71.3 ms; the eager training step
+# is within its run-to-run noise (29-35 ms).  TMDNET_DR=0 turns it off.
+DR_MODE = os.environ.get("TMDNET_DR", "auto")
 
 _PERMS = {}
 
@@ -184,6 +192,7 @@ class _Meta:
         self.np = 11 + 2 * int(hk) + 2 * int(hv)  # parameters per layer
         self.pairs = None       # (pair_row, pair_edge) of the graph: pair-shared dk/dv rows
         self.pk_rows = None
+        self.rbf = None         # (mu, beta, cutoff_lower, cutoff_upper, rbf_type): f = rbf(r) ("dr mode")
 
     def split(self, params):
         return [params[i * self.np:(i + 1) * self.np] for i in range(self.n_layers)]
@@ -309,8 +318,14 @@ def _forward_layers(meta, x, f, C, u, params):
     return x, vec, acts
 
 
-def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws):
-    """Hand-scheduled first-order backward.  Returns (g_x, g_f, g_C, g_u, g_params)."""
+def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws, r=None, dr=False):
+    """Hand-scheduled first-order backward.  Returns (g_x, g_f, g_C, g_u, g_r, g_params).
+
+    ``dr`` ("dr mode", the force pass: no weight gradients, f = rbf(r)): the projection gradient is
+    never materialised.  d pkv / d r = (d f / d r) W^T is formed once per pair row (one GEMM the
+    size of the forward projection) and the message backward contracts the per-edge projection
+    gradient with it in-kernel, accumulating g_r -- instead of writing the E x (layers * D) gradient
+    and reading it back through the edge-feature GEMM.  g_f is then None."""
     H = meta.H
     N = gX.shape[0]
     graph = meta.graph
@@ -320,8 +335,14 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws):
     g_u = torch.zeros((E, 3), **o)
     has_e = meta.hk or meta.hv
     D = meta.D
+    g_r = None
+    if dr:
+        assert has_e and not any(need_ws) and meta.rbf is not None
+        g_r = torch.zeros((E,), **o)
+        fdp = kernels.rbf_deriv(r, *meta.rbf, rows=meta.pairs[1] if meta.pairs is not None else None)
+        dpkv_all = torch.mm(fdp, meta.dkv_eff[0].t()) if meta.batched else None
     # padding rows of a static-capacity list are zeroed by the kernel: no memset needed
-    if has_e:
+    elif has_e:
         g_pkv_all = torch.empty((E, meta.n_layers * D if meta.batched else D), **o)
     g_f = None
     g_qkv = torch.empty((N, 5 * H), **o)
@@ -338,22 +359,28 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws):
         vec_w, o_w = p[8], p[9]
         qkv_w, _ = meta.qkv_eff[l]
         dkv_w, _ = meta.dkv_layer(l)
-        if has_e:
+        gpk = gpv = dpk = dpv = None
+        if dr:
+            dpkv = dpkv_all[:, l * D:(l + 1) * D] if meta.batched else torch.mm(fdp, dkv_w.t())
+            dpk = dpkv[:, :H] if meta.hk else None
+            dpv = dpkv[:, H * int(meta.hk):] if meta.hv else None
+        elif has_e:
             g_pkv = g_pkv_all[:, l * D:(l + 1) * D] if meta.batched else g_pkv_all
+            gpk = g_pkv[:, :H] if meta.hk else None
+            gpv = g_pkv[:, H * int(meta.hk):] if meta.hv else None
         if not epi_done:
             _epilogue_bwd(gX, gV, vecp, o_, g_vecp, g_o)
         g_xa = torch.empty((N, H), **o)
         kernels.gemm_group([(g_o, o_w, False, None, g_xa, False)])
         pk = pkv[:, :H] if meta.hk else None
         pv = pkv[:, H * int(meta.hk):] if meta.hv else None
-        gpk = g_pkv[:, :H] if meta.hk else None
-        gpv = g_pkv[:, H * int(meta.hk):] if meta.hv else None
         g_vec_in = gvec_bufs[l % 2] if vec is not None else None
         kernels.et_message_bwd_launch(
             qkv[:, :H], qkv[:, H:2 * H], qkv[:, 2 * H:], vec, pk, pv, C, u, graph, meta.heads, g_xa, gV,
             g_qkv[:, :H], g_qkv[:, H:2 * H], g_qkv[:, 2 * H:], g_vec_in, gpk, gpv, g_C, g_u,
-            accumulate=nat.ACC_VEC_RESIDUAL | nat.ACC_EDGE | meta.flags, pk_rows=meta.pk_rows)
-        if has_e and not meta.batched:
+            accumulate=nat.ACC_VEC_RESIDUAL | nat.ACC_EDGE | meta.flags, pk_rows=meta.pk_rows,
+            dpk=dpk, dpv=dpv, g_r=g_r)
+        if has_e and not meta.batched and not dr:
             if g_f is None:
                 g_f = torch.mm(g_pkv, dkv_w)
             else:
@@ -396,7 +423,7 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws):
             g_params[base:base + len(gp)] = gp  # batched mode: dk/dv grads filled after the loop
         gX = g_x
         gV = g_vec_in
-    if has_e and meta.batched:  # every layer's edge-feature / projection gradients in one GEMM each
+    if has_e and meta.batched and not dr:  # every layer's edge-feature / projection gradients in one GEMM each
         g_f = torch.mm(g_pkv_all, meta.dkv_eff[0])
         if any(need_ws):
             g_w_all = torch.mm(g_pkv_all.t(), f)
@@ -410,7 +437,7 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws):
                     a, b = l * D, (l + 1) * D
                     gl = _dkv_param_grads(meta, g_w_all[a:b], g_b_all[a:b])
                     g_params[base:base + len(gl)] = gl
-    return gX, g_f, g_C, g_u, g_params
+    return gX, g_f, g_C, g_u, g_r, g_params
 
 
 def _dkv_param_grads(meta, g_w, g_b):
@@ -474,16 +501,16 @@ def _will_run(node):
 
 class _ETStack(Function):
     @staticmethod
-    def forward(ctx, meta, x, f, C, u, *params):
+    def forward(ctx, meta, x, f, C, u, r, *params):
         x_out, vec_out, acts = _forward_layers(meta, x, f, C, u, params)
         ctx.meta = meta
         ctx.acts = acts
-        ctx.save_for_backward(x, f, C, u, *params)
+        ctx.save_for_backward(x, f, C, u, r, *params)
         return x_out, vec_out
 
     @staticmethod
     def backward(ctx, gX, gV):
-        x, f, C, u, *params = ctx.saved_tensors
+        x, f, C, u, r, *params = ctx.saved_tensors
         meta = ctx.meta
         # which layers' weight gradients does THIS backward deliver?  The parameters' AccumulateGrad
         # nodes are this node's own last next edges; nothing is cached across
@@ -497,28 +524,37 @@ class _ETStack(Function):
             gX = torch.zeros_like(x)
         if gV is None:
             gV = torch.zeros((x.shape[0], 3, meta.H), dtype=x.dtype, device=x.device)
-        outs = _ETStackBwd.apply(meta, ctx.acts, need_w, gX.contiguous(), gV.contiguous(), x, f, C, u,
-                                 *params)
-        g_x, g_f, g_C, g_u = outs[:4]
-        return (None, g_x, g_f, g_C, g_u) + tuple(outs[4:])
+        # dr mode: the distances (not the features) take the edge-feature gradient -- only when no
+        # weight gradient needs the projection gradient (the force pass)
+        dr = bool(meta.rbf is not None and ctx.needs_input_grad[5] and meta.D and not any(need_w))
+        if DR_MODE in ("0", "off"):
+            dr = False
+        outs = _ETStackBwd.apply(meta, ctx.acts, need_w, dr, gX.contiguous(), gV.contiguous(), x, f, C, u,
+                                 r, *params)
+        g_x, g_f, g_C, g_u, g_r = outs[:5]
+        return (None, g_x, g_f, g_C, g_u, g_r) + tuple(outs[5:])
 
 
 class _ETStackBwd(Function):
     @staticmethod
-    def forward(ctx, meta, acts, need_w, gX, gV, x, f, C, u, *params):
+    def forward(ctx, meta, acts, need_w, dr, gX, gV, x, f, C, u, r, *params):
         if not meta.graph.symmetric:
             raise RuntimeError("torchmd-net_amd: the ET backward source pass needs a symmetric edge "
                                "list (include_transpose=True, no capacity overflow)")
-        g_x, g_f, g_C, g_u, g_params = _backward_layers(meta, gX, gV, f, C, u, params, acts, need_w)
+        g_x, g_f, g_C, g_u, g_r, g_params = _backward_layers(meta, gX, gV, f, C, u, params, acts, need_w,
+                                                             r=r, dr=dr)
         ctx.meta = meta
-        ctx.save_for_backward(gX, gV, x, f, C, u, *params)
-        return (g_x, g_f, g_C, g_u) + tuple(g_params)
+        ctx.dr = dr
+        ctx.save_for_backward(gX, gV, x, f, C, u, r, *params)
+        return (g_x, g_f, g_C, g_u, g_r) + tuple(g_params)
 
     @staticmethod
     def backward(ctx, *ggs):
         """Second order (force-matching training): the layers are re-run with the HIP message
         Functions and differentiated twice, so the message's second order runs the HIP kernel
-        tmdnet_et_message_bwd2 and the node ops PyTorch's GEMM / layer-norm double backwards."""
+        tmdnet_et_message_bwd2 and the node ops PyTorch's GEMM / layer-norm double backwards.  In dr
+        mode the features are re-formed from r by the differentiable basis (the first-order output
+        was g_r, so the second order must see f's dependence on r)."""
         saved = ctx.saved_tensors
         meta = ctx.meta
         graph, heads = meta.graph, meta.heads
@@ -529,29 +565,34 @@ class _ETStackBwd(Function):
         _create = torch.is_grad_enabled()  # third order only if the caller builds a graph
         with torch.enable_grad():
             leaves = [None if t is None else t.detach().requires_grad_(True) for t in saved]
-            gX, gV, x, f, C, u = leaves[:6]
-            params = leaves[6:]
-            xo, vo = composite_stack(meta, x, f, C, u, params, message=message)
-            wrt = [x, f, C, u] + params
+            gX, gV, x, f, C, u, r = leaves[:7]
+            params = leaves[7:]
+            f_in = kernels.rbf_composite(r, *meta.rbf) if ctx.dr else f
+            xo, vo = composite_stack(meta, x, f_in, C, u, params, message=message)
+            wrt = [x, f, C, u, r] + params
             live = [t for t in wrt if t is not None]
             first = torch.autograd.grad((xo, vo), live, (gX, gV), create_graph=True, allow_unused=True)
             it = iter(first)
             first_full = [next(it) if t is not None else None for t in wrt]
             sel = [(fg, g) for fg, g in zip(first_full, ggs) if fg is not None and g is not None]
             ins = [t for t in leaves if t is not None]
-            n_out = 3 + len(leaves)
+            n_out = 4 + len(leaves)
             if not sel:
                 return (None,) * n_out
             second = torch.autograd.grad([fg for fg, _ in sel], ins, [g for _, g in sel],
                                          create_graph=_create, allow_unused=True)
         it = iter(second)
         res = [next(it) if t is not None else None for t in leaves]
-        return (None, None, None) + tuple(res)
+        return (None, None, None, None) + tuple(res)
 
 
-def et_stack(layers, x, graph, f, C, u):
+def et_stack(layers, x, graph, f, C, u, rbf=None):
     """Run ``layers`` (EquivariantMultiHeadAttention modules) as one node.  Returns (x, vec) after
-    the last residual update (reference torchmd_et.py:180-184)."""
+    the last residual update (reference torchmd_et.py:180-184).
+
+    ``rbf`` = (r, mu, beta, cutoff_lower, cutoff_upper, rbf_type) declares f = rbf(r) with a fixed
+    (non-trainable) basis, which lets the force pass take its edge gradient straight to r ("dr mode",
+    _backward_layers)."""
     l0 = layers[0]
     H, heads = l0.hidden_channels, l0.num_heads
     hk, hv = l0.dk_proj is not None, l0.dv_proj is not None
@@ -576,6 +617,10 @@ def et_stack(layers, x, graph, f, C, u):
     if D and PAIR_ROWS and graph.symmetric and graph.transpose is not None:
         meta.pairs = kernels.pair_index(graph)
         meta.pk_rows = meta.pairs[0]
+    r = None
+    if rbf is not None and D:
+        r, mu, beta, cl, cu, rbf_type = rbf
+        meta.rbf = (mu.detach(), beta.detach(), float(cl), float(cu), int(rbf_type))
     x = x.contiguous()
     f = f.contiguous() if (hk or hv) else None
-    return _ETStack.apply(meta, x, f, C.contiguous(), u.contiguous(), *params)
+    return _ETStack.apply(meta, x, f, C.contiguous(), u.contiguous(), r, *params)

@@ -439,6 +439,29 @@ class _EdgeGeomBwd(Function):
         return (second[0], second[1], gups[0], gups[1], gups[2], None, None, None, None, None, None)
 
 
+def rbf_deriv_launch(r, mu, beta, cl, cu, rbf_type, rows, out):
+    lib = nat.load()
+    rc = lib.tmdnet_rbf_deriv(nat.dtype_code(r.dtype), mu.shape[0], rbf_type, nat.ptr(r), nat.ptr(mu),
+                              nat.ptr(beta), float(cl), float(cu), nat.ptr(rows), out.shape[0], nat.ptr(out),
+                              nat.stream(r.device))
+    nat.check(rc, "tmdnet_rbf_deriv")
+
+
+def rbf_deriv(r, mu, beta, cl, cu, rbf_type, rows=None):
+    """d f / d r [n, R] of the RBF features (the fused edge-geometry basis) at r[rows] (rows None:
+    every edge) -- tmdnet_rbf_deriv."""
+    n = r.shape[0] if rows is None else rows.shape[0]
+    out = torch.empty((n, mu.shape[0]), dtype=r.dtype, device=r.device)
+    if n:
+        rbf_deriv_launch(r.detach(), mu.detach(), beta.detach(), cl, cu, rbf_type, rows, out)
+    return out
+
+
+def rbf_composite(r, mu, beta, cl, cu, rbf_type):
+    """Differentiable PyTorch RBF features of distances r (same basis as tmdnet_edge_geom_fwd)."""
+    return _edge_geom_composite(None, r, None, mu, beta, cl, cu, rbf_type, (True, False, False))[0]
+
+
 def edge_geometry(graph, mu, beta, cutoff_lower, cutoff_upper, rbf_type, want=(True, True, True)):
     """(rbf [E,R], cutoff [E], unit vectors [E,3]) of the graph's edges, fused (one HIP kernel)."""
     return _EdgeGeom.apply(graph.deltas, graph.distances, graph, mu.detach(), beta.detach(),
@@ -481,7 +504,8 @@ def et_message_fwd_launch(q, k, v, vec, pk, pv, C, u, graph, heads, xo, vo, flag
 
 
 def et_message_bwd_launch(q, k, v, vec, pk, pv, C, u, graph, heads, gx, gvec, gq, gk, gv, gw, gpk,
-                          gpv, gC, gu, accumulate=0, pk_rows=None):
+                          gpv, gC, gu, accumulate=0, pk_rows=None, dpk=None, dpv=None, g_r=None):
+    """dr mode (g_r given): gpk / gpv stay None and <g_pk, dpk> + <g_pv, dpv> accumulates into g_r."""
     lib = nat.load()
     N, H = q.shape
     rc = lib.tmdnet_et_message_bwd(
@@ -489,7 +513,8 @@ def et_message_bwd_launch(q, k, v, vec, pk, pv, C, u, graph, heads, gx, gvec, gq
         nat.ptr(q), _ld(q), nat.ptr(k), _ld(k), nat.ptr(v), _ld(v), nat.ptr(vec), nat.ptr(pk),
         _ld(pk), nat.ptr(pv), _ld(pv), nat.ptr(C), nat.ptr(u), nat.ptr(gx), nat.ptr(gvec),
         nat.ptr(gq), nat.ptr(gk), nat.ptr(gv), nat.ptr(gw), nat.ptr(gpk), nat.ptr(gpv),
-        nat.ptr(gC), nat.ptr(gu), int(accumulate), nat.ptr(pk_rows), None, nat.stream(q.device))
+        nat.ptr(gC), nat.ptr(gu), nat.ptr(dpk), nat.ptr(dpv), nat.ptr(g_r), int(accumulate),
+        nat.ptr(pk_rows), None, nat.stream(q.device))
     nat.check(rc, "tmdnet_et_message_bwd")
 
 

@@ -117,7 +117,10 @@ class TorchMD_ET(nn.Module):
         if self.fused_stack and len(self.attention_layers) > 0:
             # all layers as one autograd node (et_stack.py): fused GEMMs, HIP epilogue, hand-scheduled
             # backward; same math as the loop below
-            x, vec = et_stack(self.attention_layers, x, graph, edge_attr, C, d_ij)
+            rbf = None
+            if not (self.trainable_rbf and torch.is_grad_enabled()):  # fixed basis: f = rbf(r)
+                rbf = (graph.distances, *de.kernel_params(), self.cutoff_lower, self.cutoff_upper, de.rbf_type)
+            x, vec = et_stack(self.attention_layers, x, graph, edge_attr, C, d_ij, rbf=rbf)
             return self.out_norm(x), vec
         vec = torch.zeros(x.size(0), 3, x.size(1), device=x.device, dtype=x.dtype)
         for attn in self.attention_layers:
