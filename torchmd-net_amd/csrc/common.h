@@ -18,6 +18,15 @@ enum Status : int {
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & (TMD_WAVE - 1); }
 
+// XCD-contiguous block remap (bijective, cdna_hip_programming.md §5 "XCD swizzle"): hardware deals
+// workgroups round-robin over the 8 XCDs; the remap gives each XCD one contiguous range of logical
+// blocks, so data shared by neighbouring logical blocks stays in that XCD's L2.
+__device__ __forceinline__ int xcd_remap(int b, int nwg) {
+  if (nwg < 16) return b;
+  const int q = nwg / 8, r = nwg % 8, x = b % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+
 // Number of set bits of `mask` strictly below this lane (exclusive lane prefix of a ballot).
 __device__ __forceinline__ int lane_prefix(unsigned long long mask) {
   unsigned lo = __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u);

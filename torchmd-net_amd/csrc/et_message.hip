@@ -134,14 +134,9 @@ template <typename T> __device__ __forceinline__ const T* opt(const T* p, size_t
 //   * CS channel groups: each wave covers H/CS channels of its node (heads are independent);
 //   * row bounds and the node index are wave-uniform (readfirstlane): scalar loads.
 
-// XCD-contiguous remap (bijective, cdna_hip_programming.md §5 "XCD swizzle"): blocks are dealt
-// round-robin over the 8 XCDs; remapping gives each XCD one contiguous range of logical blocks, so
-// the source rows its waves gather (neighbours of nearby nodes) are shared in that XCD's L2.
-__device__ __forceinline__ int xcd_block(int b, int nwg, int xcd) {
-  if (!xcd || nwg < 16) return b;
-  const int q = nwg / 8, r = nwg % 8, x = b % 8;
-  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
-}
+// XCD-contiguous remap (common.h xcd_remap): the source rows a node range's waves gather
+// (neighbours of nearby nodes) are shared in that XCD's L2.
+__device__ __forceinline__ int xcd_block(int b, int nwg, int xcd) { return xcd ? xcd_remap(b, nwg) : b; }
 struct Geo {
   int node;  // node owned by this wave (-1: idle wave of a partially filled block)
   int sub;   // wave index within the node's group [0, S)
