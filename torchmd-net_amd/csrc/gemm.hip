@@ -5,16 +5,19 @@
 // a serial K loop over few workgroups.  Here:
 //   * up to four independent problems share ONE launch (q|k|v with vec_proj in the forward,
 //     vec_proj^T with [q|k|v]^T in the backward) -- one kernel boundary instead of two;
-//   * a 256-thread workgroup owns a 32 x 32 output tile with K split over its four waves, the
+//   * a workgroup owns a 32 x 32 output tile with K split over its 4 (K < 256) or 16 waves, the
 //     partial tiles summed in LDS; a wave issues all loads of its K slice up front (16-byte loads
 //     along K): about one memory round trip per tile, then 2 x 2 MFMA tiles per k-step (a 64 x 64
-//     mode, `split = 0`, a quadrant per wave over the whole K, is kept but unused: slower here);
+//     tile with a quadrant per wave over the whole K measured slower);
 //   * the K order inside an MFMA k-step is a free relabelling (A and B use the same one): lane l
 //     feeds k = k0 + 4 (l >> 4) + j at step j, so a lane's four A (and NT-B) values of a 16-wide
 //     K block are ONE float4 load.
 //   C = beta * C + A op(B) + bias,  A [M][K] (lda), op(B) = B^T with B [N][K] (nn.Linear weight,
 //   `trans_b`) or B [K][N];  exact fp32 (MFMA f32 is an fmaf chain; only the summation order differs
 //   from the library GEMM).
+#include <cstdio>
+#include <cstdlib>
+
 #include "common.h"
 #include "tmdnet.h"
 
@@ -23,7 +26,6 @@ namespace gemm {
 
 struct Prob {
   int M, N, K, lda, ldb, ldc, trans_b, beta;
-  int split;  // 0: 64 x 64 tile, a 32 x 32 quadrant per wave, full K; 1: 32 x 32 tile, K split in 4
   const float* A;
   const float* B;
   const float* bias;
@@ -98,8 +100,9 @@ __device__ __forceinline__ void store(const Prob& P, int gr, int gc, float v) {
   *out = v;
 }
 
-__global__ __launch_bounds__(256) void k_gemm(Group G) {
-  __shared__ float part[4][32][33];
+template <int NW>  // waves per 32 x 32 tile, K split NW ways
+__global__ __launch_bounds__(NW * 64) void k_gemm(Group G) {
+  __shared__ float part[NW][32][33];
   int pi = 0;
 #pragma unroll
   for (int i = 1; i < 4; ++i)
@@ -114,20 +117,8 @@ __global__ __launch_bounds__(256) void k_gemm(Group G) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
   // C/D map of the 16x16 MFMA tile: col = lane & 15, row = 4 (lane >> 4) + i
-  if (!P.split) {
-    const int r0 = (t / P.tiles_n) * 64 + 32 * (w >> 1), c0 = (t % P.tiles_n) * 64 + 32 * (w & 1);
-    slice(P, r0, c0, 0, nkb, acc);
-#pragma unroll
-    for (int bi = 0; bi < 2; ++bi)
-#pragma unroll
-      for (int bj = 0; bj < 2; ++bj)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          store(P, r0 + bi * 16 + 4 * (lane >> 4) + i, c0 + bj * 16 + (lane & 15), acc[bi][bj][i]);
-    return;
-  }
   const int r0 = (t / P.tiles_n) * 32, c0 = (t % P.tiles_n) * 32;
-  const int per = (nkb + 3) / 4;  // blocks per wave
+  const int per = (nkb + NW - 1) / NW;  // blocks per wave
   const int kb0 = w * per;
   slice(P, r0, c0, kb0, max(0, min(per, nkb - kb0)), acc);
 #pragma unroll
@@ -139,7 +130,10 @@ __global__ __launch_bounds__(256) void k_gemm(Group G) {
   __syncthreads();
   for (int e = threadIdx.x; e < 32 * 32; e += blockDim.x) {
     const int r = e >> 5, c = e & 31;
-    store(P, r0 + r, c0 + c, part[0][r][c] + part[1][r][c] + part[2][r][c] + part[3][r][c]);
+    float v = 0.f;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) v += part[i][r][c];
+    store(P, r0 + r, c0 + c, v);
   }
 }
 
@@ -167,13 +161,28 @@ extern "C" int tmdnet_gemm_f32(int n_problems, const int* dims, const void* cons
     if ((((uintptr_t)P.A) & 15) || (P.trans_b && (((uintptr_t)P.B) & 15))) return kUnsupported;
     // (a 64 x 64 tile with the whole K per wave measured slower for every ET shape at QM9 size --
     // 16.5 vs 13 us for [q|k|v] + vec_proj: f32 MFMA is 1/16 of the bf16 rate, so the per-wave MFMA
-    // chain, not the loads, sets the tile time; split K keeps four waves on every tile)
-    P.split = 1;
-    const int tile = P.split ? 32 : 64;
+    // chain, not the loads, sets the tile time; split K keeps four or more waves on every tile)
+    const int tile = 32;
     P.tiles_n = (P.N + tile - 1) / tile;
     P.tile0 = tiles;
     tiles += ((P.M + tile - 1) / tile) * P.tiles_n;
   }
-  hipLaunchKernelGGL(gemm::k_gemm, dim3(tiles), dim3(256), 0, (hipStream_t)stream, G);
+  // K split over 16 waves from K = 256 (the backward's K = 3H / 5H products): a wave's slice is 2-3
+  // K blocks, one load batch, and 4x the waves hide the load latency (4 waves below: the K = H
+  // mixes).  Measured C2 step: 4/4 waves 1.062 ms, 4/8 1.044, 4/16 1.039, 2/16 1.064, 8/8 1.069.
+  static int nw_small = 4, nw_large = 16;  // TMDNET_GEMM_NW="small,large" (tuning)
+  static const bool env_read = [] {
+    if (const char* e = getenv("TMDNET_GEMM_NW")) sscanf(e, "%d,%d", &nw_small, &nw_large);
+    return true;
+  }();
+  (void)env_read;
+  int kmax = 0;
+  for (int i = 0; i < n_problems; ++i) kmax = max(kmax, G.p[i].K);
+  const int nw = kmax >= 256 ? nw_large : nw_small;
+  hipStream_t st = (hipStream_t)stream;
+  if (nw <= 2) hipLaunchKernelGGL(gemm::k_gemm<2>, dim3(tiles), dim3(128), 0, st, G);
+  else if (nw >= 16) hipLaunchKernelGGL(gemm::k_gemm<16>, dim3(tiles), dim3(1024), 0, st, G);
+  else if (nw >= 8) hipLaunchKernelGGL(gemm::k_gemm<8>, dim3(tiles), dim3(512), 0, st, G);
+  else hipLaunchKernelGGL(gemm::k_gemm<4>, dim3(tiles), dim3(256), 0, st, G);
   return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
 }
