@@ -187,7 +187,7 @@ int tmdnet_et_epilogue_ln_fwd(int dtype, int n_nodes, int hidden, const void* x,
                               const void* ln_b, double eps, void* x_out, void* vec_out, void* xn,
                               void* mean, void* rstd, void* stream);
 /* grad_x = grad_res + LayerNorm backward of grad_xn (input x, saved mean / rstd, weight ln_w; no
- * weight gradients); when o != NULL, then the epilogue backward of the previous layer with
+ * weight gradients; grad_res NULL: no residual, e.g. the model's final out_norm); when o != NULL, then the epilogue backward of the previous layer with
  * (grad_x, grad_vec, vecp, o) -> grad_vecp, grad_o (as tmdnet_et_epilogue_bwd; vecp NULL = first
  * layer). */
 int tmdnet_ln_bwd_epilogue(int dtype, int n_nodes, int hidden, const void* grad_xn, const void* x,

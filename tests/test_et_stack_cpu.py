@@ -154,7 +154,8 @@ def _fake_ln_bwd_epi(g_xn, x, mean, rstd, ln_w, g_res, g_vec, vecp, o, g_vecp, g
     """tmdnet_ln_bwd_epilogue restated: residual + LayerNorm backward, then the previous epilogue."""
     g_x, _, _ = torch.ops.aten.native_layer_norm_backward(g_xn, x, [x.shape[1]], mean, rstd, ln_w, None,
                                                           [True, False, False])
-    g_x = g_x + g_res
+    if g_res is not None:
+        g_x = g_x + g_res
     if o is not None:
         _fake_epi_bwd(g_x, g_vec, vecp, o, g_vecp, g_o)
     return g_x
@@ -384,5 +385,44 @@ def test_stack_dr_mode_force_pass_and_second_order(emulated, monkeypatch, infl, 
         loss.backward()
         outs.append([t.detach().clone() for t in g] + [p.grad.clone() for p in params])
     assert modes[0] is True and modes[1] is False  # force pass in dr mode, loss.backward not
+    for i, (a, b) in enumerate(zip(*outs)):
+        assert torch.allclose(a, b, atol=1e-10, rtol=1e-8), i
+
+
+@pytest.mark.parametrize("batched", [True, False])
+def test_stack_fused_out_norm(emulated, monkeypatch, batched):
+    """The model's out_norm fused into the last epilogue (et_stack(out_norm=...)): outputs, the force
+    pass (LayerNorm + epilogue backward in one kernel, dr mode), and training gradients of every
+    parameter including the norm's (loss.backward through a create_graph force pass)."""
+    if not batched:
+        monkeypatch.setattr(ES, "BATCH_DKV_BYTES", 0)
+    H, R, heads = 16, 8, 4
+    n, graph, r, vecs = _system()
+    x, _, C, u = _inputs(n, graph, r, vecs, H, R)
+    mu, beta = torch.linspace(0, 4, R, dtype=DT), torch.full((R,), -1.0, dtype=DT)
+    layers = _layers(2, H, R, heads, "both")
+    norm = torch.nn.LayerNorm(H, dtype=DT)
+    with torch.no_grad():
+        norm.weight.add_(0.2 * torch.randn(H, dtype=DT))
+        norm.bias.add_(0.1 * torch.randn(H, dtype=DT))
+    params = [p for l in layers for p in ES.layer_params(l)] + [norm.weight, norm.bias]
+    outs = []
+    for fused in (True, False):
+        rl, xl, Cl, ul = (t.clone().requires_grad_(True) for t in (r, x, C, u))
+        f = kernels.rbf_composite(rl, mu, beta, 0.0, 4.0, nat.RBF_GAUSS)
+        if fused:
+            xo, vo = ES.et_stack(layers, xl, graph, f, Cl, ul, rbf=(rl, mu, beta, 0.0, 4.0, nat.RBF_GAUSS),
+                                 out_norm=norm)
+        else:
+            xo, vo = ES.composite_stack(_meta_for(layers, graph), xl, f, Cl, ul, params[:-2])
+            xo = norm(xo)
+        e = (xo ** 3).sum() + 0.3 * (vo ** 2).sum()
+        g = torch.autograd.grad(e, [rl, xl, Cl, ul], create_graph=True)
+        loss = e + sum((gi ** 2).sum() for gi in g)
+        for p in params:
+            p.grad = None
+        loss.backward()
+        outs.append([xo.detach().clone(), vo.detach().clone()] + [t.detach().clone() for t in g] +
+                    [p.grad.clone() for p in params])
     for i, (a, b) in enumerate(zip(*outs)):
         assert torch.allclose(a, b, atol=1e-10, rtol=1e-8), i

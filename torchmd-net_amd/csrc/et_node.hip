@@ -208,7 +208,7 @@ __global__ __launch_bounds__(256) void k_epi_ln_fwd(int n, int H, const T* __res
   }
 }
 
-// g_x = g_res + LN_bwd(g_xn) (no weight gradients); then, when o != NULL, the epilogue backward of
+// g_x = g_res + LN_bwd(g_xn) (no weight gradients; g_res NULL: none); then, when o != NULL, the epilogue backward of
 // the previous layer with (g_x, gvec): g_vecp [N][3][3H] (vecp NULL: first layer), g_o [N][3H].
 template <typename T, int CPL>
 __global__ __launch_bounds__(256) void k_ln_bwd_epi(int n, int H, const T* __restrict__ gxn,
@@ -239,7 +239,7 @@ __global__ __launch_bounds__(256) void k_ln_bwd_epi(int n, int H, const T* __res
   for (int i = 0; i < CPL; ++i) {
     const int c = lane + 64 * i;
     if (c >= H) continue;
-    const T g = gres[(size_t)t * H + c] + rs * (gh[i] - m1 - xh[i] * m2);
+    const T g = (gres ? gres[(size_t)t * H + c] : T(0)) + rs * (gh[i] - m1 - xh[i] * m2);
     gx[(size_t)t * H + c] = g;
     if (!o) continue;
     const T* ot = o + (size_t)t * 3 * H;
@@ -317,8 +317,7 @@ extern "C" int tmdnet_ln_bwd_epilogue(int dtype, int n_nodes, int hidden, const 
                                       const void* grad_res, void* grad_x, const void* grad_vec,
                                       const void* vecp, const void* o, void* grad_vecp, void* grad_o,
                                       void* stream) {
-  if (n_nodes < 0 || hidden <= 0 || !grad_xn || !x || !mean || !rstd || !ln_w || !grad_res || !grad_x)
-    return kBadArgument;
+  if (n_nodes < 0 || hidden <= 0 || !grad_xn || !x || !mean || !rstd || !ln_w || !grad_x) return kBadArgument;
   if (o && (!grad_o || (vecp && (!grad_vec || !grad_vecp)))) return kBadArgument;
   if (n_nodes == 0) return kOk;
   hipStream_t st = (hipStream_t)stream;

@@ -193,6 +193,7 @@ class _Meta:
         self.pairs = None       # (pair_row, pair_edge) of the graph: pair-shared dk/dv rows
         self.pk_rows = None
         self.rbf = None         # (mu, beta, cutoff_lower, cutoff_upper, rbf_type): f = rbf(r) ("dr mode")
+        self.out_norm = False   # the model's final LayerNorm fused into the last epilogue (2 trailing params)
 
     def split(self, params):
         return [params[i * self.np:(i + 1) * self.np] for i in range(self.n_layers)]
@@ -256,11 +257,11 @@ def _epi_ln(x, vec, vecp, o, veca, ln_w, ln_b):
 
 
 def _ln_bwd_epi(g_xn, x, mean, rstd, ln_w, g_res, g_vec, vecp, o, g_vecp, g_o):
-    """tmdnet_ln_bwd_epilogue: g_x = g_res + LayerNorm backward (no weight gradients), then the
-    previous layer's epilogue backward into g_vecp / g_o (o None: skipped)."""
+    """tmdnet_ln_bwd_epilogue: g_x = g_res + LayerNorm backward (no weight gradients; g_res None: no
+    residual), then the previous layer's epilogue backward into g_vecp / g_o (o None: skipped)."""
     lib = nat.load()
     N, H = x.shape
-    g_x = torch.empty_like(g_res)
+    g_x = torch.empty_like(g_xn)
     rc = lib.tmdnet_ln_bwd_epilogue(nat.dtype_code(x.dtype), N, H, nat.ptr(g_xn), nat.ptr(x), nat.ptr(mean),
                                     nat.ptr(rstd), nat.ptr(ln_w), nat.ptr(g_res), nat.ptr(g_x), nat.ptr(g_vec),
                                     nat.ptr(vecp), nat.ptr(o), nat.ptr(g_vecp), nat.ptr(g_o),
@@ -313,6 +314,9 @@ def _forward_layers(meta, x, f, C, u, params):
         acts.append((x, vec, xn, mean, rstd, qkv, vecp, pkv, xa, o))
         if l + 1 < len(layers):
             x, vec, xn, mean, rstd = _epi_ln(x, vec, vecp, o, veca, layers[l + 1][0], layers[l + 1][1])
+        elif meta.out_norm:  # last epilogue + the model's out_norm (torchmd_et.py:186) in one kernel
+            x_pre, vec, x, mean, rstd = _epi_ln(x, vec, vecp, o, veca, params[-2], params[-1])
+            acts.append((x_pre, mean, rstd))
         else:
             x, vec = _epilogue_fwd(x, vec, vecp, o, veca)
     return x, vec, acts
@@ -331,14 +335,15 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws, r=None, dr=Fa
     graph = meta.graph
     E = graph.n_edges
     o = dict(dtype=gX.dtype, device=gX.device)
-    g_C = torch.zeros((E,), **o)
-    g_u = torch.zeros((E, 3), **o)
     has_e = meta.hk or meta.hv
     D = meta.D
+    # the kernels accumulate the edge gradients (g_C, g_u, g_r) across layers: one zeroed buffer
+    zbuf = torch.zeros(((5 if dr else 4) * E,), **o)
+    g_C, g_u = zbuf[:E], zbuf[E:4 * E].view(E, 3)
     g_r = None
     if dr:
         assert has_e and not any(need_ws) and meta.rbf is not None
-        g_r = torch.zeros((E,), **o)
+        g_r = zbuf[4 * E:]
         fdp = kernels.rbf_deriv(r, *meta.rbf, rows=meta.pairs[1] if meta.pairs is not None else None)
         dpkv_all = torch.mm(fdp, meta.dkv_eff[0].t()) if meta.batched else None
     # padding rows of a static-capacity list are zeroed by the kernel: no memset needed
@@ -352,6 +357,16 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws, r=None, dr=Fa
     layers = meta.split(params)
     g_params = [None] * len(params)
     epi_done = False  # this layer's epilogue backward already ran (fused into the next layer's LN bwd)
+    if meta.out_norm:  # gX is the gradient of LN(x_out): back through out_norm first
+        x_pre, mean_o, rstd_o = acts[meta.n_layers]
+        last = acts[meta.n_layers - 1]
+        if need_ws[meta.n_layers]:
+            gX, g_onw, g_onb = torch.ops.aten.native_layer_norm_backward(
+                gX, x_pre, [H], mean_o, rstd_o, params[-2], params[-1], [True, True, True])
+            g_params[-2:] = [g_onw, g_onb]
+        else:  # LayerNorm backward + the last layer's epilogue backward, one kernel
+            gX = _ln_bwd_epi(gX, x_pre, mean_o, rstd_o, params[-2], None, gV, last[6], last[9], g_vecp, g_o)
+            epi_done = True
     for l in reversed(range(meta.n_layers)):
         p = layers[l]
         x, vec, xn, mean, rstd, qkv, vecp, pkv, xa, o_ = acts[l]
@@ -425,7 +440,7 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws, r=None, dr=Fa
         gV = g_vec_in
     if has_e and meta.batched and not dr:  # every layer's edge-feature / projection gradients in one GEMM each
         g_f = torch.mm(g_pkv_all, meta.dkv_eff[0])
-        if any(need_ws):
+        if any(need_ws[:meta.n_layers]):
             g_w_all = torch.mm(g_pkv_all.t(), f)
             g_b_all = g_pkv_all.sum(0)
             if meta.planar:
@@ -487,6 +502,8 @@ def composite_stack(meta, x, f, C, u, params, message=None):
         o1, o2, o3 = torch.split(F.linear(xa, o_w, o_b), H, dim=1)
         x = x + vec_dot * o2 + o3
         vec = vec + vec3 * o1.unsqueeze(1) + veca
+    if meta.out_norm:
+        x = F.layer_norm(x, (H,), params[-2], params[-1], _EPS)
     return x, vec
 
 
@@ -520,6 +537,9 @@ class _ETStack(Function):
         off = len(nf) - len(params)
         need_w = tuple(any(_will_run(nf[off + l * meta.np + j][0]) for j in range(meta.np))
                        for l in range(meta.n_layers))
+        if meta.out_norm:  # one more entry: the fused out_norm's weight / bias
+            base = off + meta.n_layers * meta.np
+            need_w += (_will_run(nf[base][0]) or _will_run(nf[base + 1][0]),)
         if gX is None:
             gX = torch.zeros_like(x)
         if gV is None:
@@ -586,13 +606,14 @@ class _ETStackBwd(Function):
         return (None, None, None, None) + tuple(res)
 
 
-def et_stack(layers, x, graph, f, C, u, rbf=None):
+def et_stack(layers, x, graph, f, C, u, rbf=None, out_norm=None):
     """Run ``layers`` (EquivariantMultiHeadAttention modules) as one node.  Returns (x, vec) after
     the last residual update (reference torchmd_et.py:180-184).
 
     ``rbf`` = (r, mu, beta, cutoff_lower, cutoff_upper, rbf_type) declares f = rbf(r) with a fixed
     (non-trainable) basis, which lets the force pass take its edge gradient straight to r ("dr mode",
-    _backward_layers)."""
+    _backward_layers).  ``out_norm`` (nn.LayerNorm(H), the model's final norm) is applied to x inside
+    the last layer's epilogue kernel."""
     l0 = layers[0]
     H, heads = l0.hidden_channels, l0.num_heads
     hk, hv = l0.dk_proj is not None, l0.dv_proj is not None
@@ -617,6 +638,11 @@ def et_stack(layers, x, graph, f, C, u, rbf=None):
     if D and PAIR_ROWS and graph.symmetric and graph.transpose is not None:
         meta.pairs = kernels.pair_index(graph)
         meta.pk_rows = meta.pairs[0]
+    if out_norm is not None:
+        if not (out_norm.elementwise_affine and tuple(out_norm.normalized_shape) == (H,) and out_norm.eps == _EPS):
+            raise ValueError("et_stack: out_norm must be an affine nn.LayerNorm(H) with eps 1e-5")
+        meta.out_norm = True
+        params += [out_norm.weight, out_norm.bias]
     r = None
     if rbf is not None and D:
         r, mu, beta, cl, cu, rbf_type = rbf

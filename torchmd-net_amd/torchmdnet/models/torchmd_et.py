@@ -120,8 +120,11 @@ class TorchMD_ET(nn.Module):
             rbf = None
             if not (self.trainable_rbf and torch.is_grad_enabled()):  # fixed basis: f = rbf(r)
                 rbf = (graph.distances, *de.kernel_params(), self.cutoff_lower, self.cutoff_upper, de.rbf_type)
-            x, vec = et_stack(self.attention_layers, x, graph, edge_attr, C, d_ij, rbf=rbf)
-            return self.out_norm(x), vec
+            on = self.out_norm
+            fuse_norm = on.elementwise_affine and on.eps == 1e-5
+            x, vec = et_stack(self.attention_layers, x, graph, edge_attr, C, d_ij, rbf=rbf,
+                              out_norm=on if fuse_norm else None)
+            return (x if fuse_norm else on(x)), vec
         vec = torch.zeros(x.size(0), 3, x.size(1), device=x.device, dtype=x.dtype)
         for attn in self.attention_layers:
             dx, dvec = attn(x, vec, graph, graph.distances, edge_attr, d_ij)
