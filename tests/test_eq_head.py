@@ -59,9 +59,11 @@ def _rel(a, b):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("nt", ["1", "2"])  # atoms per workgroup (TMDNET_HEAD_NT; 2 from 2k atoms)
 @pytest.mark.parametrize("dtype,H,tol", [(torch.float64, 128, 1e-11), (torch.float32, 128, 2e-5),
                                          (torch.float64, 48, 1e-11), (torch.float32, 256, 2e-5)])
-def test_hip_head_matches_composite(dtype, H, tol):
+def test_hip_head_matches_composite(dtype, H, tol, nt, monkeypatch):
+    monkeypatch.setenv("TMDNET_HEAD_NT", nt)
     head = _head(H, dtype).to(DEV)
     ps = kernels.eq_head_params(head.output_network)
     N = 37  # not a multiple of the atom tile
