@@ -54,8 +54,8 @@ def parse():
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 --pmc traffic passes")
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip the secondary lines (TensorNet C3 graph replay, ET training step)")
-    ap.add_argument("--graphed-train", action="store_true",
-                    help="also time the HIP-graph-captured training step (training.GraphedTrainStep)")
+    ap.add_argument("--no-graphed-train", dest="graphed_train", action="store_false",
+                    help="skip the HIP-graph-captured training step (training.GraphedTrainStep; N=1 only)")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
@@ -443,15 +443,22 @@ def secondary_train(a, ws, rank, dev):
                        + ("fused RCCL all-reduce, " if ws > 1 else "") + "AdamW), eager",
            "value": round(a.batch * ws * steps / el, 2), "unit": "molecules/s",
            "ms_per_step": round(1000 * el / steps, 4), "steps": steps, "parallelism": f"dp{ws}"}
-    if a.graphed_train:
+    if a.graphed_train and ws == 1:
         phase("train: graph-captured step")
         del trainer
-        gtr = GraphedTrainStep(model, z, pos, batch, y_lab, f_lab, lr=4e-4)
-        el = timed_loop(lambda: gtr.step(), max(3, a.warmup // 2), steps, ws, dev)
-        gtr.check_capacity()
-        gtr.release()
-        res["graphed"] = {"value": round(a.batch * ws * steps / el, 2), "ms_per_step": round(1000 * el / steps, 4),
-                          "execution": "fwd + force pass + double backward in one HIP graph; all-reduce + AdamW eager"}
+        try:
+            gtr = GraphedTrainStep(model, z, pos, batch, y_lab, f_lab, lr=4e-4)
+            el = timed_loop(lambda: gtr.step(), max(3, a.warmup // 2), steps, ws, dev)
+            gtr.check_capacity()
+            gtr.release()
+            res["graphed"] = {
+                "value": round(a.batch * ws * steps / el, 2), "unit": "molecules/s",
+                "ms_per_step": round(1000 * el / steps, 4), "edge_capacity": gtr.edge_capacity,
+                "execution": "fwd + force pass + double backward in one HIP graph; AdamW eager",
+                "validated": "tools/graphed_train_check.py: loss and gradients vs the eager step at this size "
+                             "(profiles/r01_graphed_train_check.json)"}
+        except RuntimeError as exc:  # the eager line above stands on its own
+            res["graphed"] = {"error": str(exc)[:300]}
     return res
 
 

@@ -779,6 +779,31 @@ def test_fused_silu_matches_torch(dtype, tol, scaled):
         assert _rel(a.detach().cpu(), b.detach().cpu()) < 10 * tol
 
 
+@pytest.mark.parametrize("strategy", ["brute", "shared"])
+def test_neighbor_unsorted_batch_scans_all_atoms(strategy):
+    """An unsorted `batch` (the reference accepts it) is detected on the device in the segment pass
+    and every destination then scans all atoms: the pair set equals the brute-force one."""
+    from torchmdnet.neighbors import get_neighbor_pairs_kernel
+    _lib_loaded()
+    g = torch.Generator().manual_seed(11)
+    n, cut = 300, 3.0
+    pos = torch.randn(n, 3, generator=g, dtype=torch.float64) * 2.0
+    batch = torch.randint(0, 5, (n,), generator=g)
+    assert bool((batch[1:] < batch[:-1]).any())
+    nb, _, dist, num = get_neighbor_pairs_kernel(strategy, pos.to(DEV), batch.to(DEV), torch.empty((0, 0)), False,
+                                                 0.0, cut, n * n, True, True)
+    P = int(num.item())
+    got = {(int(s), int(t)) for s, t in nb[:, :P].t().cpu().tolist()}
+    d = torch.cdist(pos, pos)
+    ok = (batch[:, None] == batch[None, :]) & ((d < cut) | torch.eye(n, dtype=torch.bool))
+    near = (d - cut).abs() < 1e-9
+    ref = {(int(s), int(t)) for s, t in ok.nonzero().tolist()}
+    amb = {(int(s), int(t)) for s, t in near.nonzero().tolist()}
+    assert got - amb == ref - amb
+    s, t = nb[0, :P].cpu().long(), nb[1, :P].cpu().long()
+    assert torch.allclose(dist[:P].cpu(), (pos[s] - pos[t]).norm(dim=1), atol=1e-12)
+
+
 @pytest.mark.parametrize("dtype,tol", [(torch.float64, 1e-13), (torch.float32, 1e-6)])
 def test_atom_sum_matches_scatter(dtype, tol):
     """tmdnet_atom_sum_* (x * std, per-molecule sum, + mean) == the reference scatter path, forward,

@@ -67,6 +67,7 @@ template <typename T> struct Params {
   V3<T> L;
   T cl2, cu2;
   int loop, transpose;
+  const int* unsorted;  // brute/shared: set by k_segments when `batch` descends somewhere
 };
 
 // Directed edge s -> t (neighbors[0]=s, neighbors[1]=t): delta = pos[s] - pos[t] (minimum image).
@@ -96,22 +97,16 @@ __device__ __forceinline__ bool accept(const Params<T>& P, int s, int t, int64_t
 }
 
 // ---------------------------------------------------------------- batch segments (no host sync)
-__global__ void k_batch_unsorted(const int64_t* __restrict__ batch, int n, int* __restrict__ flag) {
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i + 1 < n && batch[i] > batch[i + 1]) atomicOr(flag, 1);
-}
-
-// seg[2t], seg[2t+1] = candidate range of destination t.
-__global__ void k_segments(const int64_t* __restrict__ batch, int n, const int* __restrict__ flag,
+// seg[2t], seg[2t+1] = candidate range of destination t, by binary search as if `batch` were sorted;
+// in the same pass every thread checks its neighbour pair and raises `flag` on a descent.  The
+// pair kernels read the flag and fall back to all candidates [0, n) when it is set (the reference
+// accepts unsorted batches), so the searched ranges are only used when they are valid.
+__global__ void k_segments(const int64_t* __restrict__ batch, int n, int* __restrict__ flag,
                            int* __restrict__ seg) {
   int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n) return;
-  if (*flag) {
-    seg[2 * t] = 0;
-    seg[2 * t + 1] = n;
-    return;
-  }
   const int64_t b = batch[t];
+  if (t + 1 < n && b > batch[t + 1]) atomicOr(flag, 1);
   int lo = 0, hi = t;  // first index with batch == b
   while (lo < hi) {
     int m = (lo + hi) >> 1;
@@ -138,7 +133,8 @@ __global__ __launch_bounds__(256) void k_pairs(Params<T> P, const int* __restric
   const int t = blockIdx.x * (blockDim.x / TMD_WAVE) + threadIdx.x / TMD_WAVE;
   if (t >= P.n) return;
   const int lane = lane_id();
-  const int lo = seg[2 * t], hi = seg[2 * t + 1];
+  const bool all = *P.unsorted != 0;  // unsorted batch: every atom is a candidate
+  const int lo = all ? 0 : seg[2 * t], hi = all ? P.n : seg[2 * t + 1];
   const V3<T> pt = load3(P.pos, t);
   const int64_t bt = P.batch[t];
   int off = FILL ? row_ptr[t] : 0;
@@ -570,10 +566,10 @@ static int build(int strategy, const T* pos, const int64_t* batch, int n, const 
       hipLaunchKernelGGL((k_transpose<T, false>), dim3((cap + tb - 1) / tb), dim3(tb), 0, st, nb, row_ptr, cap,
                          num_pairs, tr, pad, dlt, dist);
   } else {
-    // (a single-workgroup fusion of these three launches measured slower: 25 us against 14 us at
-    // 678 atoms -- its binary searches become dependent-load chains on one CU)
+    // (a single-workgroup fusion of the segment search and the count pass measured slower: 25 us
+    // against 14 us at 678 atoms -- its binary searches become dependent-load chains on one CU)
     TMD_CHECK(hipMemsetAsync(flag, 0, sizeof(int), st));
-    hipLaunchKernelGGL(k_batch_unsorted, dim3((n + tb - 1) / tb), dim3(tb), 0, st, batch, n, flag);
+    P.unsorted = flag;
     hipLaunchKernelGGL(k_segments, dim3((n + tb - 1) / tb), dim3(tb), 0, st, batch, n, flag, seg);
     const int wpb = tb / TMD_WAVE;
     const dim3 g((n + wpb - 1) / wpb);
