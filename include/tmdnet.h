@@ -54,6 +54,17 @@ int tmdnet_nl_build(int dtype, int strategy, const void* pos, const int64_t* bat
                     int max_pairs, int loop, int include_transpose, int32_t* neighbors, void* deltas,
                     void* distances, int32_t* num_pairs, int32_t* row_ptr, int32_t* transpose_map,
                     int pad_output, void* workspace, size_t workspace_bytes, void* stream);
+/* tmdnet_nl_build plus the pair numbering of tmdnet_pair_index in the same launches (sorted rows:
+ * brute / shared strategies, include_transpose with a transpose_map): pair_row [max_pairs] and
+ * pair_edge [n_pair_slots] as tmdnet_pair_index fills them, with no extra launch (the canonical
+ * counts ride on the count pass, their scan on the row scan, the numbers on the transpose pass).
+ * The cell strategy returns TMDNET_BAD_ARGUMENT here (use tmdnet_pair_index). */
+int tmdnet_nl_build_paired(int dtype, int strategy, const void* pos, const int64_t* batch, int n_atoms,
+                           const double* box9, int use_periodic, double cutoff_lower, double cutoff_upper,
+                           int max_pairs, int loop, int include_transpose, int32_t* neighbors, void* deltas,
+                           void* distances, int32_t* num_pairs, int32_t* row_ptr, int32_t* transpose_map,
+                           int pad_output, void* workspace, size_t workspace_bytes, int32_t* pair_row,
+                           int32_t* pair_edge, int n_pair_slots, void* stream);
 
 /* Backward of the neighbour op w.r.t. positions (reference NeighborAutograd::backward,
  * neighbors_cuda.cu:43-71) as a segmented CSR reduction (no atomics, deterministic):

@@ -894,6 +894,11 @@ def test_pair_index_matches_composite(static):
             graph._pairs, graph.sorted_rows = None, False
             pr2, pe2 = kernels.pair_index(graph)
             assert torch.equal(pr, pr2) and torch.equal(pe, pe2)
+            # == the numbering produced inside the build (tmdnet_nl_build_paired)
+            fg = kernels.build_graph(pos, batch, 0.0, 5.0, 128 * n, loop=True, strategy=strat, box=box,
+                                     static_capacity=(None if not static else 96 * n), pairs=True)
+            fr, fe = fg._pairs
+            assert torch.equal(fr, pr) and torch.equal(fe, pe)
         if static:
             ve = int(graph.num_pairs_dev.item())
             sub = kernels.EdgeGraph(n, graph.row_ptr, graph.src[:ve], graph.dst[:ve], graph.transpose[:ve], None,

@@ -125,11 +125,13 @@ __global__ void k_segments(const int64_t* __restrict__ batch, int n, int* __rest
 
 // ---------------------------------------------------------------- all-pairs (brute / shared)
 // One wave64 per destination; 64 candidates per iteration; ballot counts/compacts.
+// Count pass with `ccounts`: also the number of canonical sources (s >= t) per row -- the pair
+// numbering of the sorted rows (see k_transpose) needs nothing else.
 template <typename T, bool FILL>
 __global__ __launch_bounds__(256) void k_pairs(Params<T> P, const int* __restrict__ seg,
                                                int* __restrict__ counts, const int* __restrict__ row_ptr,
                                                int cap, int32_t* __restrict__ nb, T* __restrict__ dlt,
-                                               T* __restrict__ dist) {
+                                               T* __restrict__ dist, int* __restrict__ ccounts) {
   const int t = blockIdx.x * (blockDim.x / TMD_WAVE) + threadIdx.x / TMD_WAVE;
   if (t >= P.n) return;
   const int lane = lane_id();
@@ -138,12 +140,14 @@ __global__ __launch_bounds__(256) void k_pairs(Params<T> P, const int* __restric
   const V3<T> pt = load3(P.pos, t);
   const int64_t bt = P.batch[t];
   int off = FILL ? row_ptr[t] : 0;
+  int coff = 0;
   for (int base = lo; base < hi; base += TMD_WAVE) {
     const int s = base + lane;
     V3<T> d;
     T d2;
     const bool ok = s < hi && accept(P, s, t, bt, pt, d, d2);
     const unsigned long long m = __ballot(ok);
+    if (!FILL && ccounts) coff += __popcll(__ballot(ok && s >= t));
     if (FILL) {
       const int slot = off + lane_prefix(m);
       if (ok && slot < cap) {
@@ -157,15 +161,18 @@ __global__ __launch_bounds__(256) void k_pairs(Params<T> P, const int* __restric
     }
     off += __popcll(m);
   }
-  if (!FILL && lane == 0) counts[t] = off;
+  if (!FILL && lane == 0) {
+    counts[t] = off;
+    if (ccounts) ccounts[t] = coff;
+  }
 }
 
 // ---------------------------------------------------------------- exclusive scan (one block)
 // counts[0..n) -> row_ptr[0..n], num_pairs[0] = total.  n is at most a few million atoms; one
 // 1024-thread block with per-thread serial chunks is a few microseconds at these sizes.
-__global__ __launch_bounds__(1024) void k_scan(const int* __restrict__ counts, int n,
-                                               int* __restrict__ row_ptr, int* __restrict__ num_pairs) {
-  __shared__ long long part[1024];
+// (`ccounts` non-NULL: the canonical counts are scanned the same way into pair_ptr[0..n].)
+__device__ __forceinline__ void block_scan(long long* part, const int* __restrict__ counts, int n,
+                                           int* __restrict__ out, int* __restrict__ total) {
   const int tid = threadIdx.x;
   const int chunk = (n + 1023) / 1024;
   const int b = tid * chunk;
@@ -182,23 +189,50 @@ __global__ __launch_bounds__(1024) void k_scan(const int* __restrict__ counts, i
   }
   long long run = part[tid] - s;
   for (int i = b; i < e; ++i) {
-    row_ptr[i] = (int)run;
+    out[i] = (int)run;
     run += counts[i];
   }
   if (tid == 1023) {
-    row_ptr[n] = (int)part[1023];
-    num_pairs[0] = (int)part[1023];
+    out[n] = (int)part[1023];
+    if (total) total[0] = (int)part[1023];
+  }
+}
+
+__global__ __launch_bounds__(1024) void k_scan(const int* __restrict__ counts, int n, int* __restrict__ row_ptr,
+                                               int* __restrict__ num_pairs, const int* __restrict__ ccounts,
+                                               int* __restrict__ pair_ptr) {
+  __shared__ long long part[1024];
+  block_scan(part, counts, n, row_ptr, num_pairs);
+  if (ccounts) {
+    __syncthreads();
+    block_scan(part, ccounts, n, pair_ptr, nullptr);
   }
 }
 
 // ---------------------------------------------------------------- transpose map + padding
 // One pass over the capacity: slots past the pairs found get the reference padding (-1 / 0,
 // common.cuh:70-76) when `pad` (replaces three capacity-sized memsets), found slots their transpose.
+//
+// Pair numbering (Pairs::prow non-NULL, sorted rows only; the same numbers as tmdnet_pair_index):
+// the canonical edge of a pair is the direction with src >= dst, numbered row by row in CSR order;
+// in a row sorted by source the canonical edges are its suffix, so edge e's number is closed-form:
+// row r = min(src, dst), k = e if canonical else T(e),  pid = pair_ptr[r] + k - (row_end(r) - cc[r]).
+// Slots past the pair count point at edge 0; a pid outside the slots (capacity-truncated list) reads
+// row 0 and is reported by the capacity check.
+struct Pairs {
+  const int* pair_ptr;  // exclusive scan of the canonical counts, [n + 1]
+  const int* cc;        // canonical count per row
+  int32_t* prow;        // [cap]   pair row of every edge
+  int32_t* pedge;       // [slots] canonical edge of every pair
+  int slots, n;
+};
+
 template <typename T, bool SORTED_ROWS>
 __global__ void k_transpose(int32_t* __restrict__ nb, const int* __restrict__ row_ptr, int cap,
                             const int* __restrict__ num_pairs, int32_t* __restrict__ tr, int pad,
-                            T* __restrict__ dlt, T* __restrict__ dist) {
+                            T* __restrict__ dlt, T* __restrict__ dist, Pairs PR) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (PR.prow && e < PR.slots && e >= PR.pair_ptr[PR.n]) PR.pedge[e] = 0;
   if (e >= cap) return;
   if (e >= num_pairs[0]) {  // unwritten slot
     if (pad) {
@@ -210,32 +244,40 @@ __global__ void k_transpose(int32_t* __restrict__ nb, const int* __restrict__ ro
       dist[e] = T(0);
     }
     if (tr) tr[e] = -1;
+    if (PR.prow) PR.prow[e] = 0;
     return;
   }
   if (!tr) return;
   const int s = nb[e];
   const int t = nb[cap + e];
-  if (s < 0) {
-    tr[e] = -1;
-    return;
-  }
-  if (s == t) {
-    tr[e] = e;
-    return;
-  }
-  int lo = row_ptr[s], hi = min(row_ptr[s + 1], cap);
   int found = -1;
-  if (SORTED_ROWS) {
-    while (lo < hi) {
-      int m = (lo + hi) >> 1;
-      if (nb[m] < t) lo = m + 1; else hi = m;
+  if (s == t) {
+    found = e;
+  } else if (s >= 0) {
+    int lo = row_ptr[s], hi = min(row_ptr[s + 1], cap);
+    if (SORTED_ROWS) {
+      while (lo < hi) {
+        int m = (lo + hi) >> 1;
+        if (nb[m] < t) lo = m + 1; else hi = m;
+      }
+      if (lo < min(row_ptr[s + 1], cap) && nb[lo] == t) found = lo;
+    } else {
+      for (int k = lo; k < hi; ++k)
+        if (nb[k] == t) { found = k; break; }
     }
-    if (lo < min(row_ptr[s + 1], cap) && nb[lo] == t) found = lo;
-  } else {
-    for (int k = lo; k < hi; ++k)
-      if (nb[k] == t) { found = k; break; }
   }
   tr[e] = found;
+  if (SORTED_ROWS && PR.prow) {
+    int pid = 0;
+    const bool canon = s >= t;
+    const int r = canon ? t : s, k = canon ? e : found;
+    if (s >= 0 && k >= 0) {
+      pid = PR.pair_ptr[r] + k - (min(row_ptr[r + 1], cap) - PR.cc[r]);
+      if (pid < 0 || pid >= PR.slots) pid = 0;
+      else if (canon) PR.pedge[pid] = e;
+    }
+    PR.prow[e] = pid;
+  }
 }
 
 // ---------------------------------------------------------------- cell list
@@ -479,7 +521,7 @@ static size_t cub_sort_bytes(int n) {
 }
 
 struct Layout {
-  size_t flag, seg, counts, rowp, keys, vals, skeys, svals, cstart, cend, cub, total;
+  size_t flag, seg, counts, rowp, cc, pairp, keys, vals, skeys, svals, cstart, cend, cub, total;
   size_t cub_bytes;
   int ncells;
 };
@@ -491,6 +533,8 @@ static Layout layout(int n, int strategy, const double* box, double cut) {
   L.seg = o; o += align16(sizeof(int) * 2 * (size_t)n);
   L.counts = o; o += align16(sizeof(int) * ((size_t)n + 1));
   L.rowp = o; o += align16(sizeof(int) * ((size_t)n + 1));
+  L.cc = o; o += align16(sizeof(int) * ((size_t)n + 1));
+  L.pairp = o; o += align16(sizeof(int) * ((size_t)n + 1));
   if (strategy == TMDNET_NL_CELL) {
     CellDims cd{3, 3, 3};
     cell_dims(box, cut, cd);
@@ -512,14 +556,18 @@ template <typename T>
 static int build(int strategy, const T* pos, const int64_t* batch, int n, const double* box,
                  int periodic, double cl, double cu, int cap, int loop, int transpose, int32_t* nb,
                  T* dlt, T* dist, int32_t* num_pairs, int32_t* row_ptr_out, int32_t* tr, int pad,
-                 char* ws, size_t ws_bytes, hipStream_t st) {
+                 char* ws, size_t ws_bytes, int32_t* prow, int32_t* pedge, int slots, hipStream_t st) {
   if (n <= 0 || cap <= 0 || !(cu > 0)) return kBadArgument;
+  if (prow && (!pedge || slots <= 0 || !tr || !transpose || strategy == TMDNET_NL_CELL)) return kBadArgument;
   const Layout Lo = layout(n, strategy, box, cu);
   if (ws_bytes < Lo.total) return kWorkspaceTooSmall;
   int* flag = (int*)(ws + Lo.flag);
   int* seg = (int*)(ws + Lo.seg);
   int* counts = (int*)(ws + Lo.counts);
   int* row_ptr = row_ptr_out ? row_ptr_out : (int*)(ws + Lo.rowp);
+  int* cc = prow ? (int*)(ws + Lo.cc) : nullptr;
+  int* pairp = prow ? (int*)(ws + Lo.pairp) : nullptr;
+  Pairs PR{pairp, cc, prow, pedge, slots, n};
 
   Params<T> P{};
   P.pos = pos;
@@ -559,12 +607,12 @@ static int build(int strategy, const T* pos, const int64_t* batch, int n, const 
     hipLaunchKernelGGL(k_cell_bounds, dim3((n + tb - 1) / tb), dim3(tb), 0, st, skeys, n, cstart, cend);
     hipLaunchKernelGGL((k_cell_pairs<T, false>), dim3((n + tb - 1) / tb), dim3(tb), 0, st, P, G, skeys,
                        svals, cstart, cend, counts, row_ptr, cap, nb, dlt, dist);
-    hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, counts, n, row_ptr, num_pairs);
+    hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, counts, n, row_ptr, num_pairs, nullptr, nullptr);
     hipLaunchKernelGGL((k_cell_pairs<T, true>), dim3((n + tb - 1) / tb), dim3(tb), 0, st, P, G, skeys,
                        svals, cstart, cend, counts, row_ptr, cap, nb, dlt, dist);
     if (tr || pad)
       hipLaunchKernelGGL((k_transpose<T, false>), dim3((cap + tb - 1) / tb), dim3(tb), 0, st, nb, row_ptr, cap,
-                         num_pairs, tr, pad, dlt, dist);
+                         num_pairs, tr, pad, dlt, dist, PR);
   } else {
     // (a single-workgroup fusion of the segment search and the count pass measured slower: 25 us
     // against 14 us at 678 atoms -- its binary searches become dependent-load chains on one CU)
@@ -573,12 +621,13 @@ static int build(int strategy, const T* pos, const int64_t* batch, int n, const 
     hipLaunchKernelGGL(k_segments, dim3((n + tb - 1) / tb), dim3(tb), 0, st, batch, n, flag, seg);
     const int wpb = tb / TMD_WAVE;
     const dim3 g((n + wpb - 1) / wpb);
-    hipLaunchKernelGGL((k_pairs<T, false>), g, dim3(tb), 0, st, P, seg, counts, row_ptr, cap, nb, dlt, dist);
-    hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, counts, n, row_ptr, num_pairs);
-    hipLaunchKernelGGL((k_pairs<T, true>), g, dim3(tb), 0, st, P, seg, counts, row_ptr, cap, nb, dlt, dist);
+    hipLaunchKernelGGL((k_pairs<T, false>), g, dim3(tb), 0, st, P, seg, counts, row_ptr, cap, nb, dlt, dist, cc);
+    hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, counts, n, row_ptr, num_pairs, cc, pairp);
+    hipLaunchKernelGGL((k_pairs<T, true>), g, dim3(tb), 0, st, P, seg, counts, row_ptr, cap, nb, dlt, dist,
+                       nullptr);
     if (tr || pad)
-      hipLaunchKernelGGL((k_transpose<T, true>), dim3((cap + tb - 1) / tb), dim3(tb), 0, st, nb, row_ptr, cap,
-                         num_pairs, tr, pad, dlt, dist);
+      hipLaunchKernelGGL((k_transpose<T, true>), dim3((max(cap, prow ? slots : 0) + tb - 1) / tb), dim3(tb), 0, st,
+                         nb, row_ptr, cap, num_pairs, tr, pad, dlt, dist, PR);
   }
   return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
 }
@@ -594,6 +643,30 @@ extern "C" size_t tmdnet_nl_workspace_bytes(int n_atoms, int strategy, const dou
   return nl::layout(n_atoms, strategy, box9 ? box9 : unit, cutoff_upper).total;
 }
 
+static int nl_build_any(int dtype, int strategy, const void* pos, const int64_t* batch, int n_atoms,
+                        const double* box9, int use_periodic, double cutoff_lower, double cutoff_upper,
+                        int max_pairs, int loop, int include_transpose, int32_t* neighbors, void* deltas,
+                        void* distances, int32_t* num_pairs, int32_t* row_ptr, int32_t* transpose_map,
+                        int pad_output, void* workspace, size_t workspace_bytes, int32_t* pair_row,
+                        int32_t* pair_edge, int n_pair_slots, void* stream) {
+  if (strategy != TMDNET_NL_BRUTE && strategy != TMDNET_NL_SHARED && strategy != TMDNET_NL_CELL)
+    return kBadArgument;
+  double unit[9] = {0};
+  const double* box = box9 ? box9 : unit;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == TMDNET_F32)
+    return nl::build<float>(strategy, (const float*)pos, batch, n_atoms, box, use_periodic, cutoff_lower,
+                            cutoff_upper, max_pairs, loop, include_transpose, neighbors, (float*)deltas,
+                            (float*)distances, num_pairs, row_ptr, transpose_map, pad_output, (char*)workspace,
+                            workspace_bytes, pair_row, pair_edge, n_pair_slots, st);
+  if (dtype == TMDNET_F64)
+    return nl::build<double>(strategy, (const double*)pos, batch, n_atoms, box, use_periodic, cutoff_lower,
+                             cutoff_upper, max_pairs, loop, include_transpose, neighbors, (double*)deltas,
+                             (double*)distances, num_pairs, row_ptr, transpose_map, pad_output,
+                             (char*)workspace, workspace_bytes, pair_row, pair_edge, n_pair_slots, st);
+  return kUnsupported;
+}
+
 extern "C" int tmdnet_nl_build(int dtype, int strategy, const void* pos, const int64_t* batch,
                                int n_atoms, const double* box9, int use_periodic,
                                double cutoff_lower, double cutoff_upper, int max_pairs, int loop,
@@ -601,22 +674,23 @@ extern "C" int tmdnet_nl_build(int dtype, int strategy, const void* pos, const i
                                void* distances, int32_t* num_pairs, int32_t* row_ptr,
                                int32_t* transpose_map, int pad_output, void* workspace,
                                size_t workspace_bytes, void* stream) {
-  if (strategy != TMDNET_NL_BRUTE && strategy != TMDNET_NL_SHARED && strategy != TMDNET_NL_CELL)
-    return kBadArgument;
-  double unit[9] = {0};
-  const double* box = box9 ? box9 : unit;
-  hipStream_t st = (hipStream_t)stream;
-  if (dtype == TMDNET_F32)
-    return nl::build<float>(strategy, (const float*)pos, batch, n_atoms, box, use_periodic,
-                            cutoff_lower, cutoff_upper, max_pairs, loop, include_transpose,
-                            neighbors, (float*)deltas, (float*)distances, num_pairs, row_ptr,
-                            transpose_map, pad_output, (char*)workspace, workspace_bytes, st);
-  if (dtype == TMDNET_F64)
-    return nl::build<double>(strategy, (const double*)pos, batch, n_atoms, box, use_periodic,
-                             cutoff_lower, cutoff_upper, max_pairs, loop, include_transpose,
-                             neighbors, (double*)deltas, (double*)distances, num_pairs, row_ptr,
-                             transpose_map, pad_output, (char*)workspace, workspace_bytes, st);
-  return kUnsupported;
+  return nl_build_any(dtype, strategy, pos, batch, n_atoms, box9, use_periodic, cutoff_lower, cutoff_upper,
+                      max_pairs, loop, include_transpose, neighbors, deltas, distances, num_pairs, row_ptr,
+                      transpose_map, pad_output, workspace, workspace_bytes, nullptr, nullptr, 0, stream);
+}
+
+extern "C" int tmdnet_nl_build_paired(int dtype, int strategy, const void* pos, const int64_t* batch,
+                                      int n_atoms, const double* box9, int use_periodic, double cutoff_lower,
+                                      double cutoff_upper, int max_pairs, int loop, int include_transpose,
+                                      int32_t* neighbors, void* deltas, void* distances, int32_t* num_pairs,
+                                      int32_t* row_ptr, int32_t* transpose_map, int pad_output,
+                                      void* workspace, size_t workspace_bytes, int32_t* pair_row,
+                                      int32_t* pair_edge, int n_pair_slots, void* stream) {
+  if (!pair_row || !pair_edge || n_pair_slots <= 0) return kBadArgument;
+  return nl_build_any(dtype, strategy, pos, batch, n_atoms, box9, use_periodic, cutoff_lower, cutoff_upper,
+                      max_pairs, loop, include_transpose, neighbors, deltas, distances, num_pairs, row_ptr,
+                      transpose_map, pad_output, workspace, workspace_bytes, pair_row, pair_edge, n_pair_slots,
+                      stream);
 }
 
 extern "C" int tmdnet_nl_backward(int dtype, int n_atoms, const int32_t* row_ptr,

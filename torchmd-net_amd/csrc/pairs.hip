@@ -61,7 +61,7 @@ __device__ __forceinline__ void row_assign(const P& p, int t) {
     const unsigned long long m = __ballot(canon);
     if (canon) {
       const int pid = base + lane_prefix(m);
-      p.prow[k] = pid;
+      p.prow[k] = pid < p.slots ? pid : 0;  // (truncated lists: see k_fill_sorted)
       if (pid < p.slots) p.pedge[pid] = k;
     } else if (live) {
       p.prow[k] = -1;
@@ -152,7 +152,10 @@ __global__ __launch_bounds__(256) void k_fill_sorted(P p) {
         if (s >= t && pid < p.slots) p.pedge[pid] = i;
       }
     }
-    p.prow[i] = pid;
+    // a capacity-truncated list can hold more canonical edges than slots (its kept rows are a
+    // prefix, canonical-heavy): such rows read slot 0, never past the buffer (the overflow is
+    // reported by the capacity check)
+    p.prow[i] = pid < p.slots ? pid : 0;
   }
   if (i < p.slots && i >= total) p.pedge[i] = 0;
 }

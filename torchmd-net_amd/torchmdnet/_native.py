@@ -30,6 +30,7 @@ SZ = ctypes.c_size_t
 SIGNATURES = {
     "tmdnet_nl_workspace_bytes": (SZ, [I, I, P, D]),
     "tmdnet_nl_build": (I, [I, I, P, P, I, P, I, D, D, I, I, I, P, P, P, P, P, P, I, P, SZ, P]),
+    "tmdnet_nl_build_paired": (I, [I, I, P, P, I, P, I, D, D, I, I, I, P, P, P, P, P, P, I, P, SZ, P, P, I, P]),
     "tmdnet_nl_backward": (I, [I, I, P, P, I, P, P, P, P, P, P]),
     "tmdnet_nl_backward2": (I, [I, I, P, P, P, I, P, P, P, P, P, P, P, P]),
     "tmdnet_edge_geom_fwd": (I, [I, I, I, I, P, P, P, P, P, P, D, D, P, P, P, P]),

@@ -98,8 +98,10 @@ _STRATEGY = {"brute": nat.NL_BRUTE, "shared": nat.NL_SHARED, "cell": nat.NL_CELL
 
 
 def neighbor_pairs_raw(strategy, pos, batch, box, use_periodic, cutoff_lower, cutoff_upper,
-                       max_pairs, loop, include_transpose, pad_output=True, want_csr=False):
-    """Launch ``tmdnet_nl_build``.  Returns (neighbors, deltas, distances, num_pairs, row_ptr, T)."""
+                       max_pairs, loop, include_transpose, pad_output=True, want_csr=False, pairs_out=None):
+    """Launch ``tmdnet_nl_build``.  Returns (neighbors, deltas, distances, num_pairs, row_ptr, T).
+    ``pairs_out`` = (pair_row [max_pairs], pair_edge [slots]) int32: also number the edge pairs in the
+    same launches (``tmdnet_nl_build_paired``; sorted-row strategies with the transpose map)."""
     lib = nat.load()
     nat.require_gpu(pos, "get_neighbor_pairs")
     if strategy not in _STRATEGY:
@@ -136,12 +138,19 @@ def neighbor_pairs_raw(strategy, pos, batch, box, use_periodic, cutoff_lower, cu
     num = torch.empty((1,), dtype=torch.int32, device=dev)
     row_ptr = torch.empty((n + 1,), dtype=torch.int32, device=dev) if want_csr else None
     tr = torch.empty((cap,), dtype=torch.int32, device=dev) if (want_csr and include_transpose) else None
-    rc = lib.tmdnet_nl_build(nat.dtype_code(pos.dtype), st, nat.ptr(pos), nat.ptr(batch), n, box9,
-                             int(bool(use_periodic)), float(cutoff_lower), float(cutoff_upper), cap,
-                             int(bool(loop)), int(bool(include_transpose)), nat.ptr(nb), nat.ptr(dl),
-                             nat.ptr(dist), nat.ptr(num), nat.ptr(row_ptr), nat.ptr(tr),
-                             int(bool(pad_output)), nat.ptr(ws), int(ws.numel()), nat.stream(dev))
-    nat.check(rc, "tmdnet_nl_build")
+    args = (nat.dtype_code(pos.dtype), st, nat.ptr(pos), nat.ptr(batch), n, box9, int(bool(use_periodic)),
+            float(cutoff_lower), float(cutoff_upper), cap, int(bool(loop)), int(bool(include_transpose)),
+            nat.ptr(nb), nat.ptr(dl), nat.ptr(dist), nat.ptr(num), nat.ptr(row_ptr), nat.ptr(tr),
+            int(bool(pad_output)), nat.ptr(ws), int(ws.numel()))
+    if pairs_out is not None:
+        pr, pe = pairs_out
+        if tr is None or st == nat.NL_CELL or pr.shape[0] != cap:
+            raise RuntimeError("pair numbering in the build needs sorted rows and the transpose map")
+        rc = lib.tmdnet_nl_build_paired(*args, nat.ptr(pr), nat.ptr(pe), pe.shape[0], nat.stream(dev))
+        nat.check(rc, "tmdnet_nl_build_paired")
+    else:
+        rc = lib.tmdnet_nl_build(*args, nat.stream(dev))
+        nat.check(rc, "tmdnet_nl_build")
     return nb, dl, dist, num, row_ptr, tr
 
 
@@ -289,12 +298,14 @@ class DeviceOverflow:
 
 
 def build_graph(pos, batch, cutoff_lower, cutoff_upper, max_num_pairs, loop=True, strategy="brute",
-                box=None, check_errors=True, static_capacity=None):
+                box=None, check_errors=True, static_capacity=None, pairs=False):
     """Symmetric (include_transpose) neighbour graph with CSR rows, transpose map and autograd
     deltas/distances.  Mirrors OptimizedDistance(return_vecs=True, resize_to_fit=True) semantics
     (reference models/utils.py:207-269): one host sync reads num_pairs for the overflow check.
     With ``static_capacity`` the graph is sync-free and HIP-graph capturable: every per-edge tensor
-    has ``static_capacity`` rows; overflow is reported on the device (``graph.overflow``)."""
+    has ``static_capacity`` rows; overflow is reported on the device (``graph.overflow``).
+    ``pairs``: the pair numbering of ``pair_index`` is produced by the build itself (sorted-row
+    strategies; the cell list numbers them lazily with tmdnet_pair_index)."""
     use_periodic = box is not None and box.numel() > 0
     if use_periodic:
         validate_box(box, cutoff_upper)
@@ -303,23 +314,31 @@ def build_graph(pos, batch, cutoff_lower, cutoff_upper, max_num_pairs, loop=True
         box = torch.tensor([[lbox, 0, 0], [0, lbox, 0], [0, 0, lbox]], dtype=torch.float64)
     if strategy == "brute" and pos.shape[0] >= 32768:
         strategy = "shared"
+    n = pos.shape[0]
+    fused_pairs = None
+    if pairs and strategy != "cell":
+        c = int(static_capacity) if static_capacity is not None else int(max_num_pairs)
+        fused_pairs = (torch.empty((c,), dtype=torch.int32, device=pos.device),
+                       torch.empty(((c + n) // 2,), dtype=torch.int32, device=pos.device))
     if static_capacity is not None:
         cap = int(static_capacity)
         nb, dl, dist, num, row_ptr, tr = neighbor_pairs_raw(
             strategy, pos, batch, box, use_periodic, cutoff_lower, cutoff_upper, cap, loop,
-            True, pad_output=True, want_csr=True)
+            True, pad_output=True, want_csr=True, pairs_out=fused_pairs)
         graph = EdgeGraph(pos.shape[0], row_ptr, nb[0], nb[1], tr, None, None, None, symmetric=True,
                           static=True)
         graph.num_pairs_dev = num
         graph.overflow = DeviceOverflow(num, cap)
         graph.sorted_rows = strategy != "cell"  # brute / shared rows list sources ascending
+        if fused_pairs is not None:
+            graph._pairs = fused_pairs
         deltas, distances = _NeighborGeom.apply(pos, graph, dl, dist)
         graph.deltas = deltas
         graph.distances = distances
         return graph
     nb, dl, dist, num, row_ptr, tr = neighbor_pairs_raw(
         strategy, pos, batch, box, use_periodic, cutoff_lower, cutoff_upper, max_num_pairs, loop,
-        True, pad_output=False, want_csr=True)
+        True, pad_output=False, want_csr=True, pairs_out=fused_pairs)
     num_pairs = int(num.item())
     cap = int(max_num_pairs)
     if check_errors and num_pairs > cap:
@@ -328,6 +347,8 @@ def build_graph(pos, batch, cutoff_lower, cutoff_upper, max_num_pairs, loop=True
     graph = EdgeGraph(pos.shape[0], row_ptr, nb[0, :E], nb[1, :E], tr[:E], None, None, num_pairs,
                       symmetric=num_pairs <= cap)
     graph.sorted_rows = strategy != "cell"  # brute / shared rows list sources ascending
+    if fused_pairs is not None and graph.symmetric:  # the numbering of the kept prefix of rows
+        graph._pairs = (fused_pairs[0][:E], fused_pairs[1][:(E + n) // 2])
     deltas, distances = _NeighborGeom.apply(pos, graph, dl[:E], dist[:E])
     graph.deltas = deltas
     graph.distances = distances

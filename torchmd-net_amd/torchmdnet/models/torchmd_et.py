@@ -58,6 +58,7 @@ class TorchMD_ET(nn.Module):
         self.embedding = nn.Embedding(self.max_z, hidden_channels, dtype=dtype)
         self.distance = OptimizedDistance(cutoff_lower, cutoff_upper, max_num_pairs=-max_num_neighbors,
                                           return_vecs=True, loop=True, long_edge_index=True)
+        self.distance.pair_rows = True  # the layer stack's pair-shared dk/dv rows (et_stack.PAIR_ROWS)
         self.distance_expansion = rbf_class_mapping[rbf_type](cutoff_lower, cutoff_upper, num_rbf, trainable_rbf)
         self.neighbor_embedding = (
             NeighborEmbedding(hidden_channels, num_rbf, cutoff_lower, cutoff_upper, self.max_z, dtype).jittable()

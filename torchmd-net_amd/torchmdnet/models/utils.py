@@ -197,6 +197,8 @@ class OptimizedDistance(torch.nn.Module):
         self.long_edge_index = long_edge_index
         # HIP-graph mode (torchmdnet.graphs): fixed edge capacity, no host synchronisation
         self.static_capacity = None
+        # graph(): number the edge pairs in the build itself (the ET consumer sets it; sorted rows)
+        self.pair_rows = False
 
     def _max_pairs(self, n):
         return -self.max_num_pairs * n if self.max_num_pairs < 0 else self.max_num_pairs
@@ -238,7 +240,7 @@ class OptimizedDistance(torch.nn.Module):
         g = kernels.build_graph(pos, batch, self.cutoff_lower, self.cutoff_upper,
                                 self._max_pairs(pos.shape[0]), loop=self.loop, strategy=strategy,
                                 box=box, check_errors=self.check_errors,
-                                static_capacity=self.static_capacity)
+                                static_capacity=self.static_capacity, pairs=self.pair_rows)
         # keep only the device-side status of the last build (static-capacity overflow flag, pair
         # count): holding the graph itself would keep its autograd history -- and the positions'
         # AccumulateGrad node -- alive across steps, which breaks HIP-graph capture of later steps
