@@ -101,6 +101,13 @@ int tmdnet_edge_geom_fwd(int dtype, int n_edges, int num_rbf, int rbf_type, cons
                          const int32_t* dst, const void* deltas, const void* dist, const void* mu,
                          const void* beta, double cutoff_lower, double cutoff_upper, void* rbf,
                          void* cutoff, void* unit, void* stream);
+/* tmdnet_edge_geom_fwd plus the RBF features of the edges rows[p] into rbf_rows [n_rows][num_rbf]
+ * in the same launch (the ET layer stack's pair rows: replaces a gather of rbf). */
+int tmdnet_edge_geom_fwd_rows(int dtype, int n_edges, int num_rbf, int rbf_type, const int32_t* src,
+                              const int32_t* dst, const void* deltas, const void* dist, const void* mu,
+                              const void* beta, double cutoff_lower, double cutoff_upper, void* rbf,
+                              void* cutoff, void* unit, const int32_t* rows, int n_rows, void* rbf_rows,
+                              void* stream);
 /* Backward: given grad_rbf [E][R], grad_cutoff [E], grad_unit [E][3] (each nullable) produce
  * grad_dist [E] and grad_deltas [E][3] (both overwritten). */
 /* d rbf_k / d r of edges rows[p] (rows NULL: edge p), out [n_rows][R] -- the RBF derivative the ET

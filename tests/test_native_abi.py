@@ -31,6 +31,7 @@ def test_header_declares_entry_points():
                  "tmdnet_tn_message_fwd", "tmdnet_tn_message_bwd", "tmdnet_tn_node_fwd", "tmdnet_tn_node_bwd", "tmdnet_silu_fwd", "tmdnet_silu_bwd",
                  "tmdnet_atom_sum_fwd", "tmdnet_atom_sum_bwd", "tmdnet_gemm_f32", "tmdnet_pair_index",
                  "tmdnet_rbf_deriv", "tmdnet_nl_build_paired",
+                 "tmdnet_edge_geom_fwd_rows",
                  "tmdnet_nl_workspace_bytes",
                  "tmdnet_build_info"):
         assert name in d, name

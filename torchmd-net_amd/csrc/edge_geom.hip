@@ -59,8 +59,11 @@ __device__ __forceinline__ void basis(const Cfg<T>& P, T r, int k, T& f, T& df) 
   }
 }
 
+// rows != NULL: also the features of the edges rows[p] into frows [n_rows][R] (the pair rows the ET
+// projection GEMM reads; replaces a gather of f)
 template <typename T>
-__global__ void k_fwd(Cfg<T> P, T* __restrict__ f, T* __restrict__ C, T* __restrict__ u) {
+__global__ void k_fwd(Cfg<T> P, T* __restrict__ f, T* __restrict__ C, T* __restrict__ u,
+                      const int32_t* __restrict__ rows, int n_rows, T* __restrict__ frows) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long nf = f ? (long long)P.E * P.R : 0;
   if (i < nf) {
@@ -68,6 +71,12 @@ __global__ void k_fwd(Cfg<T> P, T* __restrict__ f, T* __restrict__ C, T* __restr
     T v, dv;
     basis(P, P.r[e], k, v, dv);
     f[i] = v;
+  }
+  if (rows && i < (long long)n_rows * P.R) {
+    const int p = (int)(i / P.R), k = (int)(i % P.R);
+    T v, dv;
+    basis(P, P.r[rows[p]], k, v, dv);
+    frows[i] = v;
   }
   if (i < P.E) {
     const int e = (int)i;
@@ -163,26 +172,48 @@ static Cfg<T> make(int E, int R, int type, const int32_t* src, const int32_t* ds
 
 using namespace tmd;
 
+static int geom_fwd(int dtype, int n_edges, int num_rbf, int rbf_type, const int32_t* src, const int32_t* dst,
+                    const void* deltas, const void* dist, const void* mu, const void* beta, double cutoff_lower,
+                    double cutoff_upper, void* rbf, void* cutoff, void* unit, const int32_t* rows, int n_rows,
+                    void* rbf_rows, void* stream) {
+  if (n_edges <= 0) return kOk;
+  hipStream_t st = (hipStream_t)stream;
+  long long work = rbf ? (long long)n_edges * num_rbf : n_edges;
+  if (rows) work = std::max(work, (long long)n_rows * num_rbf);
+  const int tb = 256;
+  dim3 g((unsigned)((work + tb - 1) / tb));
+  if (dtype == TMDNET_F32) {
+    auto P = geom::make<float>(n_edges, num_rbf, rbf_type, src, dst, deltas, dist, mu, beta, cutoff_lower, cutoff_upper);
+    hipLaunchKernelGGL(geom::k_fwd<float>, g, dim3(tb), 0, st, P, (float*)rbf, (float*)cutoff, (float*)unit, rows,
+                       n_rows, (float*)rbf_rows);
+  } else if (dtype == TMDNET_F64) {
+    auto P = geom::make<double>(n_edges, num_rbf, rbf_type, src, dst, deltas, dist, mu, beta, cutoff_lower, cutoff_upper);
+    hipLaunchKernelGGL(geom::k_fwd<double>, g, dim3(tb), 0, st, P, (double*)rbf, (double*)cutoff, (double*)unit, rows,
+                       n_rows, (double*)rbf_rows);
+  } else {
+    return kUnsupported;
+  }
+  return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
+}
+
 extern "C" int tmdnet_edge_geom_fwd(int dtype, int n_edges, int num_rbf, int rbf_type,
                                     const int32_t* src, const int32_t* dst, const void* deltas,
                                     const void* dist, const void* mu, const void* beta,
                                     double cutoff_lower, double cutoff_upper, void* rbf, void* cutoff,
                                     void* unit, void* stream) {
-  if (n_edges <= 0) return kOk;
-  hipStream_t st = (hipStream_t)stream;
-  const long long work = rbf ? (long long)n_edges * num_rbf : n_edges;
-  const int tb = 256;
-  dim3 g((unsigned)((work + tb - 1) / tb));
-  if (dtype == TMDNET_F32) {
-    auto P = geom::make<float>(n_edges, num_rbf, rbf_type, src, dst, deltas, dist, mu, beta, cutoff_lower, cutoff_upper);
-    hipLaunchKernelGGL(geom::k_fwd<float>, g, dim3(tb), 0, st, P, (float*)rbf, (float*)cutoff, (float*)unit);
-  } else if (dtype == TMDNET_F64) {
-    auto P = geom::make<double>(n_edges, num_rbf, rbf_type, src, dst, deltas, dist, mu, beta, cutoff_lower, cutoff_upper);
-    hipLaunchKernelGGL(geom::k_fwd<double>, g, dim3(tb), 0, st, P, (double*)rbf, (double*)cutoff, (double*)unit);
-  } else {
-    return kUnsupported;
-  }
-  return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
+  return geom_fwd(dtype, n_edges, num_rbf, rbf_type, src, dst, deltas, dist, mu, beta, cutoff_lower, cutoff_upper,
+                  rbf, cutoff, unit, nullptr, 0, nullptr, stream);
+}
+
+extern "C" int tmdnet_edge_geom_fwd_rows(int dtype, int n_edges, int num_rbf, int rbf_type,
+                                         const int32_t* src, const int32_t* dst, const void* deltas,
+                                         const void* dist, const void* mu, const void* beta,
+                                         double cutoff_lower, double cutoff_upper, void* rbf, void* cutoff,
+                                         void* unit, const int32_t* rows, int n_rows, void* rbf_rows,
+                                         void* stream) {
+  if (!rows || n_rows < 0 || (n_rows > 0 && !rbf_rows)) return kBadArgument;
+  return geom_fwd(dtype, n_edges, num_rbf, rbf_type, src, dst, deltas, dist, mu, beta, cutoff_lower, cutoff_upper,
+                  rbf, cutoff, unit, rows, n_rows, rbf_rows, stream);
 }
 
 extern "C" int tmdnet_edge_geom_bwd(int dtype, int n_edges, int num_rbf, int rbf_type,

@@ -34,6 +34,7 @@ SIGNATURES = {
     "tmdnet_nl_backward": (I, [I, I, P, P, I, P, P, P, P, P, P]),
     "tmdnet_nl_backward2": (I, [I, I, P, P, P, I, P, P, P, P, P, P, P, P]),
     "tmdnet_edge_geom_fwd": (I, [I, I, I, I, P, P, P, P, P, P, D, D, P, P, P, P]),
+    "tmdnet_edge_geom_fwd_rows": (I, [I, I, I, I, P, P, P, P, P, P, D, D, P, P, P, P, I, P, P]),
     "tmdnet_edge_geom_bwd": (I, [I, I, I, I, P, P, P, P, P, P, D, D, P, P, P, P, P, P]),
     "tmdnet_et_message_fwd": (I, [I, I, I, I, P, P, I, P, I, P, I, P, I, P, P, I, P, I, P, P, P, P, I, P, P,
                                   P]),

@@ -194,6 +194,7 @@ class _Meta:
         self.pk_rows = None
         self.rbf = None         # (mu, beta, cutoff_lower, cutoff_upper, rbf_type): f = rbf(r) ("dr mode")
         self.out_norm = False   # the model's final LayerNorm fused into the last epilogue (2 trailing params)
+        self.f_pairs = None     # f at the pair rows, when the caller produced it with the features
 
     def split(self, params):
         return [params[i * self.np:(i + 1) * self.np] for i in range(self.n_layers)]
@@ -282,7 +283,7 @@ def _forward_layers(meta, x, f, C, u, params):
     # directions through pk_rows (bit-identical to the per-edge projection)
     fp = f
     if D and meta.pairs is not None:
-        fp = f.index_select(0, meta.pairs[1])
+        fp = meta.f_pairs if meta.f_pairs is not None else f.index_select(0, meta.pairs[1])
     pkv_all = torch.addmm(meta.dkv_eff[1], fp, meta.dkv_eff[0].t()) if (meta.batched and D) else None
     layers = meta.split(params)
     # layer l's LayerNorm is computed by layer l-1's epilogue kernel (layer 0: LayerNorm alone)
@@ -606,14 +607,15 @@ class _ETStackBwd(Function):
         return (None, None, None, None) + tuple(res)
 
 
-def et_stack(layers, x, graph, f, C, u, rbf=None, out_norm=None):
+def et_stack(layers, x, graph, f, C, u, rbf=None, out_norm=None, f_pairs=None):
     """Run ``layers`` (EquivariantMultiHeadAttention modules) as one node.  Returns (x, vec) after
     the last residual update (reference torchmd_et.py:180-184).
 
     ``rbf`` = (r, mu, beta, cutoff_lower, cutoff_upper, rbf_type) declares f = rbf(r) with a fixed
     (non-trainable) basis, which lets the force pass take its edge gradient straight to r ("dr mode",
     _backward_layers).  ``out_norm`` (nn.LayerNorm(H), the model's final norm) is applied to x inside
-    the last layer's epilogue kernel."""
+    the last layer's epilogue kernel.  ``f_pairs`` = f at the graph's pair rows (``pair_index``
+    numbering), when already produced with f (tmdnet_edge_geom_fwd_rows); else gathered here."""
     l0 = layers[0]
     H, heads = l0.hidden_channels, l0.num_heads
     hk, hv = l0.dk_proj is not None, l0.dv_proj is not None
@@ -638,6 +640,8 @@ def et_stack(layers, x, graph, f, C, u, rbf=None, out_norm=None):
     if D and PAIR_ROWS and graph.symmetric and graph.transpose is not None:
         meta.pairs = kernels.pair_index(graph)
         meta.pk_rows = meta.pairs[0]
+        if f_pairs is not None and f_pairs.shape[0] == meta.pairs[1].shape[0]:
+            meta.f_pairs = f_pairs.detach()
     if out_norm is not None:
         if not (out_norm.elementwise_affine and tuple(out_norm.normalized_shape) == (H,) and out_norm.eps == _EPS):
             raise ValueError("et_stack: out_norm must be an affine nn.LayerNorm(H) with eps 1e-5")

@@ -387,17 +387,21 @@ def _edge_geom_composite(deltas, dist, selfmask, mu, beta, cl, cu, rbf_type, wan
 
 class _EdgeGeom(Function):
     @staticmethod
-    def forward(ctx, deltas, dist, graph, mu, beta, cl, cu, rbf_type, want):
+    def forward(ctx, deltas, dist, graph, mu, beta, cl, cu, rbf_type, want, rows_out=None):
         lib = nat.load()
         E = dist.shape[0]
         R = mu.shape[0]
         f = torch.empty((E, R), dtype=dist.dtype, device=dist.device) if want[0] else None
         C = torch.empty((E,), dtype=dist.dtype, device=dist.device) if want[1] else None
         u = torch.empty((E, 3), dtype=dist.dtype, device=dist.device) if want[2] else None
-        rc = lib.tmdnet_edge_geom_fwd(nat.dtype_code(dist.dtype), E, R, rbf_type, nat.ptr(graph.src),
-                                      nat.ptr(graph.dst), nat.ptr(deltas), nat.ptr(dist), nat.ptr(mu),
-                                      nat.ptr(beta), float(cl), float(cu), nat.ptr(f), nat.ptr(C),
-                                      nat.ptr(u), nat.stream(dist.device))
+        args = (nat.dtype_code(dist.dtype), E, R, rbf_type, nat.ptr(graph.src), nat.ptr(graph.dst), nat.ptr(deltas),
+                nat.ptr(dist), nat.ptr(mu), nat.ptr(beta), float(cl), float(cu), nat.ptr(f), nat.ptr(C), nat.ptr(u))
+        if rows_out is not None:  # also f at rows (written in place, no autograd: a forward-only copy)
+            rows, frows = rows_out
+            rc = lib.tmdnet_edge_geom_fwd_rows(*args, nat.ptr(rows), rows.shape[0], nat.ptr(frows),
+                                               nat.stream(dist.device))
+        else:
+            rc = lib.tmdnet_edge_geom_fwd(*args, nat.stream(dist.device))
         nat.check(rc, "tmdnet_edge_geom_fwd")
         ctx.graph = graph
         ctx.cfg = (cl, cu, rbf_type, want)
@@ -409,7 +413,7 @@ class _EdgeGeom(Function):
         deltas, dist, mu, beta = ctx.saved_tensors
         cl, cu, rbf_type, want = ctx.cfg
         g_dl, g_r = _EdgeGeomBwd.apply(deltas, dist, gf, gC, gu, ctx.graph, mu, beta, cl, cu, rbf_type)
-        return g_dl, g_r, None, None, None, None, None, None, None
+        return g_dl, g_r, None, None, None, None, None, None, None, None
 
 
 class _EdgeGeomBwd(Function):
@@ -483,10 +487,17 @@ def rbf_composite(r, mu, beta, cl, cu, rbf_type):
     return _edge_geom_composite(None, r, None, mu, beta, cl, cu, rbf_type, (True, False, False))[0]
 
 
-def edge_geometry(graph, mu, beta, cutoff_lower, cutoff_upper, rbf_type, want=(True, True, True)):
-    """(rbf [E,R], cutoff [E], unit vectors [E,3]) of the graph's edges, fused (one HIP kernel)."""
-    return _EdgeGeom.apply(graph.deltas, graph.distances, graph, mu.detach(), beta.detach(),
-                           float(cutoff_lower), float(cutoff_upper), rbf_type, tuple(want))
+def edge_geometry(graph, mu, beta, cutoff_lower, cutoff_upper, rbf_type, want=(True, True, True), rows=None):
+    """(rbf [E,R], cutoff [E], unit vectors [E,3]) of the graph's edges, fused (one HIP kernel).
+    ``rows`` (int32 [P]): also returns the rbf rows of those edges [P,R] from the same launch (a
+    forward-only tensor: gradients flow through the per-edge rbf), as a fourth value."""
+    rows_out = None
+    if rows is not None:
+        rows_out = (rows, torch.empty((rows.shape[0], mu.shape[0]), dtype=graph.distances.dtype,
+                                      device=graph.distances.device))
+    out = _EdgeGeom.apply(graph.deltas, graph.distances, graph, mu.detach(), beta.detach(),
+                          float(cutoff_lower), float(cutoff_upper), rbf_type, tuple(want), rows_out)
+    return out if rows is None else tuple(out) + (rows_out[1],)
 
 
 # ----------------------------------------------------------------------------- ET message

@@ -103,6 +103,7 @@ class TorchMD_ET(nn.Module):
     def _forward(self, z: Tensor, pos: Tensor, batch: Tensor):
         x = self.embedding(z)
         graph = self.distance.graph(pos, batch)
+        f_pairs = None
         de = self.distance_expansion
         if self.trainable_rbf and torch.is_grad_enabled():
             # trainable basis: parameters need gradients -> differentiable torch basis on the GPU
@@ -110,8 +111,12 @@ class TorchMD_ET(nn.Module):
             _, C, d_ij = kernels.edge_geometry(graph, *de.kernel_params(), self.cutoff_lower,
                                                self.cutoff_upper, de.rbf_type, want=(False, True, True))
         else:
-            edge_attr, C, d_ij = kernels.edge_geometry(graph, *de.kernel_params(), self.cutoff_lower,
-                                                       self.cutoff_upper, de.rbf_type)
+            pairs = getattr(graph, "_pairs", None)  # numbered by the neighbour build (sorted rows)
+            rows = pairs[1] if (pairs is not None and self.fused_stack and len(self.attention_layers)) else None
+            geo = kernels.edge_geometry(graph, *de.kernel_params(), self.cutoff_lower, self.cutoff_upper,
+                                        de.rbf_type, rows=rows)
+            edge_attr, C, d_ij = geo[:3]
+            f_pairs = geo[3] if rows is not None else None
         graph.cutoff = C
         if self.neighbor_embedding is not None:
             x = self.neighbor_embedding(z, x, graph, graph.distances, edge_attr, cutoff=C)
@@ -124,7 +129,7 @@ class TorchMD_ET(nn.Module):
             on = self.out_norm
             fuse_norm = on.elementwise_affine and on.eps == 1e-5
             x, vec = et_stack(self.attention_layers, x, graph, edge_attr, C, d_ij, rbf=rbf,
-                              out_norm=on if fuse_norm else None)
+                              out_norm=on if fuse_norm else None, f_pairs=f_pairs)
             return (x if fuse_norm else on(x)), vec
         vec = torch.zeros(x.size(0), 3, x.size(1), device=x.device, dtype=x.dtype)
         for attn in self.attention_layers:
