@@ -246,12 +246,17 @@ int tmdnet_eq_head_bwd(int dtype, int n_atoms, int hidden, const void* grad_y, c
  *   X: [N][H] (ld_x), W: [E][H] (ld_w) = distance_proj(rbf) pre-cutoff, C: [E], out [N][H]. */
 int tmdnet_nbr_embed_fwd(int dtype, int n_nodes, int hidden, const int32_t* row_ptr,
                          const int32_t* src, int max_pairs, const void* x, int ld_x, const void* w,
-                         int ld_w, const void* cutoff, void* out, void* stream);
-/* Backward: gx[s] (source pass, symmetric list), gw[e], gcut[e] (destination pass); overwritten. */
+                         int ld_w, const void* cutoff, void* out, int ld_out, const void* x_self,
+                         void* out_self, void* stream);
+/* Backward: gx[s] (source pass, symmetric list), gw[e], gcut[e] (destination pass); overwritten.
+ * ld_out / ld_grad_out: row strides of out / grad_out (0 = hidden), so the output can be the right
+ * half of the combine Linear's [x | x_nb] input (reference utils.py:108) and its gradient read from
+ * that layout in place; x_self / out_self (both or neither): the forward also copies x_self [n][hidden]
+ * rows into out_self (stride ld_out), the left half -- the concatenation costs no launch. */
 int tmdnet_nbr_embed_bwd(int dtype, int n_nodes, int hidden, const int32_t* row_ptr,
                          const int32_t* src, int max_pairs, const void* x, int ld_x, const void* w,
-                         int ld_w, const void* cutoff, const void* grad_out, void* gx, void* gw,
-                         void* gcut, void* stream);
+                         int ld_w, const void* cutoff, const void* grad_out, int ld_grad_out, void* gx,
+                         void* gw, void* gcut, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * TensorNet edge kernels (reference models/tensornet.py:287-332).

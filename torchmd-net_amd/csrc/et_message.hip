@@ -841,8 +841,9 @@ template <typename T> struct NbArgs {
   const T* x; int ldx;
   const T* w; int ldw;
   const T* C;
-  T* out;
-  const T* gout;
+  T* out; int ldo;         // output rows (ldo >= H: e.g. the right half of the combine input)
+  const T* xself; T* oself;  // optional row copy xself[t] -> oself[t] (stride ldo): the left half
+  const T* gout; int ldg;  // incoming gradient rows
   T* gx; T* gw; T* gC;
 };
 
@@ -899,7 +900,12 @@ __global__ __launch_bounds__(256) void k_nb_fwd(NbArgs<T> A) {
 #pragma unroll
       for (int i = 0; i < V; ++i) acc[i] += xs[u][i] * wk[u][i];
   });
-  if (on) stv<T, V>(A.out + (size_t)t * A.H + c0, acc);
+  if (on) stv<T, V>(A.out + (size_t)t * A.ldo + c0, acc);
+  if (on && A.xself) {  // the combine Linear's [x | x_nb] input in one buffer: no concatenation
+    T xv[V];
+    ldv<T, V>(xv, A.xself + (size_t)t * A.H + c0);
+    stv<T, V>(A.oself + (size_t)t * A.ldo + c0, xv);
+  }
 }
 
 // destination pass: gw[e] = gout[t] * x[s] * C[e], gC[e] = sum_c gout[t] x[s] w[e]
@@ -911,7 +917,7 @@ __global__ __launch_bounds__(256) void k_nb_bwd_dst(NbArgs<T> A) {
   const bool on = lane < A.L;
   const int c0 = on ? lane * V : 0;
   T go[V];
-  ldv<T, V>(go, A.gout + (size_t)t * A.H + c0);
+  ldv<T, V>(go, A.gout + (size_t)t * A.ldg + c0);
   nb_edges(A, t, [&](int k0, const int (&sq)[NB_U], const T (&cq)[NB_U]) {
     T xs[NB_U][V], wk[NB_U][V], gc[NB_U];
 #pragma unroll
@@ -963,7 +969,7 @@ __global__ __launch_bounds__(256) void k_nb_bwd_src(NbArgs<T> A) {
     for (int u = 0; u < NB_U; ++u) {
       const bool live = sq[u] >= 0 && sq[u] != j;
       const int m = live ? sq[u] : j, k = live ? k0 + u : k0;
-      ldv<T, V>(gm[u], A.gout + (size_t)m * A.H + c0);
+      ldv<T, V>(gm[u], A.gout + (size_t)m * A.ldg + c0);
       ldv<T, V>(wk[u], A.w + (size_t)k * A.ldw + c0);
       const T ce = live ? cq[u] : T(0);
 #pragma unroll
@@ -1259,24 +1265,36 @@ extern "C" int tmdnet_et_message_bwd2(
 
 template <typename T>
 static int nb_fwd_t(int n, int H, const int32_t* row_ptr, const int32_t* src, int cap, const void* x,
-                    int ldx, const void* w, int ldw, const void* C, void* out, hipStream_t st) {
+                    int ldx, const void* w, int ldw, const void* C, void* out, int ldo, const void* xself,
+                    void* oself, hipStream_t st) {
   et::NbArgs<T> A;
   int V;
   int rc = et::nb_setup<T>(A, n, H, row_ptr, src, cap, x, ldx, w, ldw, C, V);
   if (rc) return rc;
+  if (!out) return kBadArgument;
   A.out = (T*)out;
+  A.ldo = ldo ? ldo : H;
+  if (A.ldo < H || !et::aligned<T>(out, A.ldo, V)) return kBadArgument;
+  if ((xself == nullptr) != (oself == nullptr) || !et::aligned<T>(xself, H, V) ||
+      !et::aligned<T>(oself, A.ldo, V))
+    return kBadArgument;
+  A.xself = (const T*)xself;
+  A.oself = (T*)oself;
   return et::launch_v<T, et::KNbFwd>(V, n, A, st);
 }
 
 template <typename T>
 static int nb_bwd_t(int n, int H, const int32_t* row_ptr, const int32_t* src, int cap, const void* x,
-                    int ldx, const void* w, int ldw, const void* C, const void* gout, void* gx,
+                    int ldx, const void* w, int ldw, const void* C, const void* gout, int ldg, void* gx,
                     void* gw, void* gC, hipStream_t st) {
   et::NbArgs<T> A;
   int V;
   int rc = et::nb_setup<T>(A, n, H, row_ptr, src, cap, x, ldx, w, ldw, C, V);
   if (rc) return rc;
+  if (!gout) return kBadArgument;
   A.gout = (const T*)gout;
+  A.ldg = ldg ? ldg : H;
+  if (A.ldg < H || !et::aligned<T>(gout, A.ldg, V)) return kBadArgument;
   A.gx = (T*)gx; A.gw = (T*)gw; A.gC = (T*)gC;
   rc = et::launch_v<T, et::KNbDst>(V, n, A, st);
   if (rc) return rc;
@@ -1285,20 +1303,21 @@ static int nb_bwd_t(int n, int H, const int32_t* row_ptr, const int32_t* src, in
 
 extern "C" int tmdnet_nbr_embed_fwd(int dtype, int n_nodes, int hidden, const int32_t* row_ptr,
                                     const int32_t* src, int max_pairs, const void* x, int ld_x,
-                                    const void* w, int ld_w, const void* cutoff, void* out, void* stream) {
+                                    const void* w, int ld_w, const void* cutoff, void* out, int ld_out,
+                                    const void* x_self, void* out_self, void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == TMDNET_F32) return nb_fwd_t<float>(n_nodes, hidden, row_ptr, src, max_pairs, x, ld_x, w, ld_w, cutoff, out, st);
-  if (dtype == TMDNET_F64) return nb_fwd_t<double>(n_nodes, hidden, row_ptr, src, max_pairs, x, ld_x, w, ld_w, cutoff, out, st);
+  if (dtype == TMDNET_F32) return nb_fwd_t<float>(n_nodes, hidden, row_ptr, src, max_pairs, x, ld_x, w, ld_w, cutoff, out, ld_out, x_self, out_self, st);
+  if (dtype == TMDNET_F64) return nb_fwd_t<double>(n_nodes, hidden, row_ptr, src, max_pairs, x, ld_x, w, ld_w, cutoff, out, ld_out, x_self, out_self, st);
   return kUnsupported;
 }
 
 extern "C" int tmdnet_nbr_embed_bwd(int dtype, int n_nodes, int hidden, const int32_t* row_ptr,
                                     const int32_t* src, int max_pairs, const void* x, int ld_x,
                                     const void* w, int ld_w, const void* cutoff, const void* grad_out,
-                                    void* gx, void* gw, void* gcut, void* stream) {
+                                    int ld_grad_out, void* gx, void* gw, void* gcut, void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == TMDNET_F32) return nb_bwd_t<float>(n_nodes, hidden, row_ptr, src, max_pairs, x, ld_x, w, ld_w, cutoff, grad_out, gx, gw, gcut, st);
-  if (dtype == TMDNET_F64) return nb_bwd_t<double>(n_nodes, hidden, row_ptr, src, max_pairs, x, ld_x, w, ld_w, cutoff, grad_out, gx, gw, gcut, st);
+  if (dtype == TMDNET_F32) return nb_bwd_t<float>(n_nodes, hidden, row_ptr, src, max_pairs, x, ld_x, w, ld_w, cutoff, grad_out, ld_grad_out, gx, gw, gcut, st);
+  if (dtype == TMDNET_F64) return nb_bwd_t<double>(n_nodes, hidden, row_ptr, src, max_pairs, x, ld_x, w, ld_w, cutoff, grad_out, ld_grad_out, gx, gw, gcut, st);
   return kUnsupported;
 }
 

@@ -52,8 +52,8 @@ SIGNATURES = {
     "tmdnet_eq_head_fwd": (I, [I, I, I, P, P, P, P, P, P, P]),
     "tmdnet_eq_head_bwd": (I, [I, I, I, P, P, P, P, P, P]),
     "tmdnet_eq_head_bwd_weights": (I, [I, I, I, P, P, P, P, P, P, P, P]),
-    "tmdnet_nbr_embed_fwd": (I, [I, I, I, P, P, I, P, I, P, I, P, P, P]),
-    "tmdnet_nbr_embed_bwd": (I, [I, I, I, P, P, I, P, I, P, I, P, P, P, P, P, P]),
+    "tmdnet_nbr_embed_fwd": (I, [I, I, I, P, P, I, P, I, P, I, P, P, I, P, P, P]),
+    "tmdnet_nbr_embed_bwd": (I, [I, I, I, P, P, I, P, I, P, I, P, P, I, P, P, P, P]),
     "tmdnet_tn_embed_fwd": (I, [I, I, I, P, P, I, D, P, I, P, P, P, I, P, P, P, P]),
     "tmdnet_tn_embed_bwd": (I, [I, I, I, P, P, I, D, P, I, P, P, P, I, P, P, P, P, P, P, P, P, P]),
     "tmdnet_tn_message_fwd": (I, [I, I, I, P, P, I, D, P, I, P, I, P, P, P]),

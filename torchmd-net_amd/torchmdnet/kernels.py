@@ -745,24 +745,39 @@ def nbr_embed_composite(x, w, C, src, dst, n_nodes):
 
 
 class _NbrEmbed(Function):
+    """x_nb = nbr_embed(x, w, C); with x_self the output is [x_self | x_nb] ([N, 2H], the combine
+    Linear's input, reference utils.py:108) written by the same kernel."""
+
     @staticmethod
-    def forward(ctx, x, w, C, graph):
+    def forward(ctx, x, w, C, graph, x_self=None):
         lib = nat.load()
         N, H = x.shape
-        out = torch.empty((N, H), dtype=x.dtype, device=x.device)
+        if x_self is None:
+            buf = out = torch.empty((N, H), dtype=x.dtype, device=x.device)
+        else:
+            buf = torch.empty((N, 2 * H), dtype=x.dtype, device=x.device)
+            out = buf[:, H:]
         rc = lib.tmdnet_nbr_embed_fwd(nat.dtype_code(x.dtype), N, H, nat.ptr(graph.row_ptr),
                                       nat.ptr(graph.src), graph.n_edges, nat.ptr(x), _ld(x), nat.ptr(w),
-                                      _ld(w), nat.ptr(C), nat.ptr(out), nat.stream(x.device))
+                                      _ld(w), nat.ptr(C), nat.ptr(out), out.stride(0), nat.ptr(x_self),
+                                      None if x_self is None else nat.ptr(buf), nat.stream(x.device))
         nat.check(rc, "tmdnet_nbr_embed_fwd")
         ctx.graph = graph
+        ctx.has_self = x_self is not None
         ctx.save_for_backward(x, w, C)
-        return out
+        return buf
 
     @staticmethod
     def backward(ctx, gout):
         x, w, C = ctx.saved_tensors
-        gx, gw, gC = _NbrEmbedBwd.apply(gout.contiguous(), x, w, C, ctx.graph)
-        return gx, gw, gC, None
+        H = x.shape[1]
+        g_self = None
+        if gout.stride(-1) != 1:
+            gout = gout.contiguous()
+        if ctx.has_self:  # the two halves are read in place (row stride 2H)
+            g_self, gout = gout[:, :H], gout[:, H:]
+        gx, gw, gC = _NbrEmbedBwd.apply(gout, x, w, C, ctx.graph)
+        return gx, gw, gC, None, g_self
 
 
 class _NbrEmbedBwd(Function):
@@ -774,12 +789,12 @@ class _NbrEmbedBwd(Function):
         N, H = x.shape
         E = graph.n_edges
         gx = torch.empty_like(x, memory_format=torch.contiguous_format)
-        gw = graph.alloc_edge_grad((E, H), x.dtype, x.device)
-        gC = graph.alloc_edge_grad((E,), x.dtype, x.device)
+        zbuf = graph.alloc_edge_grad((E * (H + 1),), x.dtype, x.device)  # one zero fill for both
+        gw, gC = zbuf[:E * H].view(E, H), zbuf[E * H:]
         rc = lib.tmdnet_nbr_embed_bwd(nat.dtype_code(x.dtype), N, H, nat.ptr(graph.row_ptr),
                                       nat.ptr(graph.src), E, nat.ptr(x), _ld(x), nat.ptr(w), _ld(w),
-                                      nat.ptr(C), nat.ptr(gout), nat.ptr(gx), nat.ptr(gw), nat.ptr(gC),
-                                      nat.stream(x.device))
+                                      nat.ptr(C), nat.ptr(gout), gout.stride(0), nat.ptr(gx), nat.ptr(gw),
+                                      nat.ptr(gC), nat.stream(x.device))
         nat.check(rc, "tmdnet_nbr_embed_bwd")
         ctx.graph = graph
         ctx.save_for_backward(gout, x, w, C)
@@ -804,8 +819,11 @@ class _NbrEmbedBwd(Function):
         return tuple(second) + (None,)
 
 
-def nbr_embed(x, w, C, graph):
-    return _NbrEmbed.apply(_rowmajor(x), _rowmajor(w), C.contiguous(), graph)
+def nbr_embed(x, w, C, graph, x_self=None):
+    """Neighbour-embedding aggregation (reference utils.py:100-107); ``x_self`` given: returns
+    ``cat([x_self, x_nb], 1)`` from the same launch."""
+    return _NbrEmbed.apply(_rowmajor(x), _rowmajor(w), C.contiguous(), graph,
+                           None if x_self is None else x_self.contiguous())
 
 
 # ----------------------------------------------------------------------------- activation

@@ -280,8 +280,8 @@ class NeighborEmbedding(nn.Module):
             edge_weight, edge_attr = edge_weight[perm], edge_attr[perm]
         C = cutoff if cutoff is not None else self.cutoff(edge_weight)
         W = self.distance_proj(edge_attr)
-        x_neighbors = kernels.nbr_embed(self.embedding(z), W, C, graph)
-        return self.combine(torch.cat([x, x_neighbors], dim=1))
+        # [x | x_nb] comes out of the aggregation kernel itself (no concatenation launch)
+        return self.combine(kernels.nbr_embed(self.embedding(z), W, C, graph, x_self=x))
 
 
 def as_graph(edge_index, n_nodes):
