@@ -178,9 +178,11 @@ class TorchMD_Net(nn.Module):
             for prior in self.prior_model:
                 y = prior.post_reduce(y, z, pos, batch, extra_args)
         if self.derivative:
-            grad_outputs: List[Optional[torch.Tensor]] = [torch.ones_like(y)]
-            dy = grad([y], [pos], grad_outputs=grad_outputs, create_graph=True, retain_graph=True)[0]
-            if dy is None:
+            # -dy/dpos directly: the backward is seeded with -1 instead of negating its result (sign
+            # flips are exact; one elementwise launch fewer than the reference's `-dy`, model.py:298)
+            grad_outputs: List[Optional[torch.Tensor]] = [torch.full_like(y, -1.0)]
+            neg_dy = grad([y], [pos], grad_outputs=grad_outputs, create_graph=True, retain_graph=True)[0]
+            if neg_dy is None:
                 raise RuntimeError("Autograd returned None for the force prediction.")
-            return y, -dy
+            return y, neg_dy
         return y, None
