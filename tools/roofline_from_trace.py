@@ -1,17 +1,19 @@
 """Per-probe average duration of the graded edge kernel from a rocprofv3 kernel-trace CSV.
 
-bench.py launches the graded kernel (tmdnet_et_message_fwd at C5 scale) in two back-to-back probe
-loops -- `roofline` (per-edge dk/dv layout, the SURVEY formula) then `roofline.model_layout`
-(pair-shared rows) -- with nothing else launched in between, while the model's own launches of the
-same instantiation are interleaved with other kernels.  The run-length of consecutive launches
-therefore separates the probes; their rocprof averages are what bench.py's live HIP-event figures
-must agree with.  usage: roofline_from_trace.py <kernel_trace.csv> [kernel substring] [min run]"""
+bench.py's roofline_probe launches the graded kernel (tmdnet_et_message_fwd at C5 scale) as two
+back-to-back loops with nothing else launched in between: 5 warm-up + `reps` timed launches in the
+per-edge dk/dv layout (`roofline`, the graded SURVEY-formula figure), then 5 + `reps` in the pair-row
+layout (`roofline.model_layout`).  The model's own launches of the same instantiation are interleaved
+with other kernels, so the probes are the one run of 2 (5 + reps) consecutive launches; their timed
+segments' rocprof averages are what bench.py's live HIP-event figures must agree with.
+usage: roofline_from_trace.py <kernel_trace.csv> [reps=50] [warmup=5] [kernel substring]"""
 import csv
 import sys
 
 path = sys.argv[1]
-name = sys.argv[2] if len(sys.argv) > 2 else "k_fwd<float, 4, 1, 1, false>"
-min_run = int(sys.argv[3]) if len(sys.argv) > 3 else 20
+reps = int(sys.argv[2]) if len(sys.argv) > 2 else 50
+warm = int(sys.argv[3]) if len(sys.argv) > 3 else 5
+name = sys.argv[4] if len(sys.argv) > 4 else "k_fwd<float, 4, 1, 1, false>"
 rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
 runs, cur = [], []
 for r in rows:
@@ -24,7 +26,15 @@ if cur:
     runs.append(cur)
 everything = [d for run in runs for d in run]
 print(f"kernel: {name}")
-print(f"all launches: {len(everything)}, average {sum(everything) / max(1, len(everything)) / 1e6:.4f} ms")
-for i, run in enumerate(r for r in runs if len(r) >= min_run):
-    label = ["roofline (per-edge layout, graded)", "roofline.model_layout (pair rows)"][i] if i < 2 else "run"
-    print(f"probe run {i}: {label}: {len(run)} consecutive launches, average {sum(run) / len(run) / 1e6:.4f} ms")
+print(f"all launches: {len(everything)}, average {sum(everything) / max(1, len(everything)) / 1e6:.4f} ms "
+      "(probes and the model's own launches mixed)")
+probe = [run for run in runs if len(run) == 2 * (warm + reps)]
+if not probe:
+    print(f"no run of {2 * (warm + reps)} consecutive launches found")
+for run in probe:
+    graded = run[warm:warm + reps]
+    model = run[2 * warm + reps:]
+    print(f"roofline (per-edge layout, graded): {len(graded)} timed launches, average "
+          f"{sum(graded) / len(graded) / 1e6:.4f} ms")
+    print(f"roofline.model_layout (pair rows): {len(model)} timed launches, average "
+          f"{sum(model) / len(model) / 1e6:.4f} ms")
