@@ -228,6 +228,70 @@ def test_cell_list_matches_brute_water_box():
     assert (a.transpose >= 0).all()
 
 
+def test_et_c4_spice_matches_oracle():
+    """C4 (ET-SPICE config: 128 ch, 5 layers, 64 RBF, cutoff 10, 128 neighbours; 16 x 40-atom
+    SPICE-like molecules) fp32 on the GPU vs the fp64 oracle: energies and forces 1e-4."""
+    import yaml
+    from torchmdnet.models.model import create_model
+    with open(os.path.join(GOLDEN, "configs", "et_spice.yaml")) as f:
+        args = yaml.safe_load(f)
+    args.update(prior_model=None, precision=32, derivative=True, output_model="Scalar")
+    _seed()
+    m = create_model(args)
+    g = torch.Generator().manual_seed(1)
+    z = torch.randint(1, 9, (16 * 40,), generator=g)
+    pos = torch.randn(16 * 40, 3, generator=g, dtype=torch.float64) * 2.5
+    batch = torch.arange(16).repeat_interleave(40)
+    y_ref, f_ref = O.energy_forces(m.state_dict(), dict(args), z, pos, batch)
+    m = m.to(DEV)
+    y, f = m(z.to(DEV), pos.float().to(DEV), batch.to(DEV))
+    assert _rel(y.detach().cpu(), y_ref.detach()) < 1e-4
+    assert _rel(f.detach().cpu(), f_ref) < 1e-4
+
+
+def test_et_c5_water_box_invariants():
+    """C5 size (50,001-atom periodic water box, ~2.7 M edges; no oracle finishes at this size): the
+    size-independent properties of the ET energy, fp64 -- the forces sum to zero (translation
+    invariance), a rigid translation of every atom leaves energy and forces unchanged (periodic
+    minimum image), and the forces are the negative energy gradient (central finite difference along
+    a random direction).  Exercises the cell list, Morton renumbering, pair rows, planar rows and the
+    dr-mode force pass at full size."""
+    from torchmdnet.models.model import create_model
+    torch.manual_seed(0)
+    n = 50001
+    m = create_model(yaml_args("equivariant-transformer", embedding_dimension=128, num_layers=4, num_rbf=32,
+                               num_heads=8, max_num_neighbors=128, derivative=True, output_model="Scalar",
+                               precision=64)).to(DEV)
+    g = torch.Generator().manual_seed(7)
+    L = (n / 0.1003) ** (1.0 / 3.0)
+    pos = (torch.rand(n, 3, generator=g, dtype=torch.float64) * L).to(DEV)
+    z = torch.tensor([8, 1, 1], dtype=torch.long).repeat(n // 3 + 1)[:n].to(DEV)
+    batch = torch.zeros(n, dtype=torch.long, device=DEV)
+    d = m.representation_model.distance
+    d.box = torch.eye(3, dtype=torch.float64) * L
+    d.use_periodic = True
+    d.strategy = "cell"
+
+    def ef(p):
+        y, f = m(z, p, batch)
+        return y.detach().sum().item(), f.detach()
+
+    e0, f0 = ef(pos.clone())
+    assert torch.isfinite(f0).all()
+    assert f0.sum(0).abs().max().item() < 1e-9 * f0.abs().sum().item()
+    shift = torch.tensor([1.3, -0.7, 2.9], dtype=torch.float64, device=DEV)
+    e1, f1 = ef(pos + shift)
+    assert abs(e1 - e0) < 1e-10 * abs(e0)
+    assert _rel(f1.cpu(), f0.cpu()) < 1e-8
+    dirn = torch.randn(n, 3, generator=g, dtype=torch.float64).to(DEV)
+    dirn /= dirn.norm()
+    eps = 1e-4
+    ep, _ = ef(pos + eps * dirn)
+    em, _ = ef(pos - eps * dirn)
+    fd = (ep - em) / (2 * eps)
+    assert abs(fd + (f0 * dirn).sum().item()) < 1e-5 * max(1.0, abs(fd))
+
+
 # ----------------------------------------------------------------------------- ET model
 def _et_cfg_args(H, L, R, heads, maxnb=32, precision=32):
     return yaml_args("equivariant-transformer", embedding_dimension=H, num_layers=L, num_rbf=R, num_heads=heads,
