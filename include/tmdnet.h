@@ -153,7 +153,7 @@ int tmdnet_et_message_fwd(int dtype, int n_nodes, int hidden, int heads, const i
  * (gvec_in may also be NULL).  accumulate (TMDNET_ACC_* bits): VEC_RESIDUAL -> gvec_in =
  * grad_vec + message part (the layer's identity residual); EDGE -> gcut/gunit are accumulated
  * (+=) instead of overwritten (one buffer shared by all layers).  Other buffers: overwritten; rows
- * [row_ptr[n_nodes], max_pairs) of gpk / gpv (static-capacity padding) are set to zero. */
+ * [row_ptr[n_nodes], max_pairs) of gpk / gpv (static-capacity padding) are set to zero, and so are those rows of gcut / gunit. */
 int tmdnet_et_message_bwd(int dtype, int n_nodes, int hidden, int heads, const int32_t* row_ptr,
                           const int32_t* src, int max_pairs, const void* q, int ld_q, const void* k,
                           int ld_k, const void* v, int ld_v, const void* vec_in, const void* pk,
@@ -173,7 +173,8 @@ int tmdnet_et_message_bwd(int dtype, int n_nodes, int hidden, int heads, const i
  * gv, gvec_in, gpk, gpv, gcut, gunit; all required, dense, zeros where unused; gg_q/gg_k [N][H],
  * gg_v [N][3H], gg_vec [N][3][H], gg_pk/gg_pv with leading dimensions).  Outputs: d_grad_x, d_grad_vec,
  * d_q, d_k [N][H], d_v [N][3H], d_vec [N][3][H] (d_k, d_v, d_vec accumulated with atomics: zero them
- * first; d_vec may be NULL when vec_in is NULL), d_pk [E][H], d_pv [E][3H], d_cut [E], d_unit [E][3]. */
+ * first; d_vec may be NULL when vec_in is NULL), d_pk [E][H], d_pv [E][3H], d_cut [E], d_unit [E][3]
+ * (every row written, static-capacity padding rows [row_ptr[n_nodes], max_pairs) with zeros). */
 int tmdnet_et_message_bwd2(int dtype, int n_nodes, int hidden, int heads, const int32_t* row_ptr,
                            const int32_t* src, int max_pairs, const void* q, int ld_q, const void* k,
                            int ld_k, const void* v, int ld_v, const void* vec_in, const void* pk,

@@ -343,6 +343,10 @@ __device__ __forceinline__ void zero_pad_rows(const Args<T>& A, int blk, int nwg
     for (long long i = tid; i < rows * w; i += nth)
       A.gpv[(size_t)(e0 + i / w) * A.ldpv + i % w] = T(0);
   }
+  if (A.gC)
+    for (long long i = tid; i < rows; i += nth) A.gC[e0 + i] = T(0);
+  if (A.gu)
+    for (long long i = tid; i < rows * 3; i += nth) A.gu[3 * (size_t)e0 + i] = T(0);
 }
 
 template <typename T, int V, int S, int CS, bool DR>
@@ -674,6 +678,19 @@ __global__ __launch_bounds__(256) void k_bwd2(Args2<T> B) {
   const Args<T>& A = B.a;
   const Geo G = geo<S, 1, false>(A.n, A.L, nullptr, A.xcd, blockIdx.x, gridDim.x);
   const int t = G.node;
+  {  // static-capacity padding rows [row_ptr[n], cap) of the per-edge outputs: zero (no memset)
+    const int e0 = min(A.row_ptr[A.n], A.cap);
+    const long long rows = A.cap - e0;
+    const long long tid = (long long)blockIdx.x * blockDim.x + threadIdx.x, nth = (long long)gridDim.x * blockDim.x;
+    if (rows > 0) {
+      if (B.o_pk)
+        for (long long i = tid; i < rows * A.H; i += nth) B.o_pk[(size_t)e0 * A.H + i] = T(0);
+      if (B.o_pv)
+        for (long long i = tid; i < rows * 3 * A.H; i += nth) B.o_pv[(size_t)e0 * 3 * A.H + i] = T(0);
+      for (long long i = tid; i < rows; i += nth) B.o_C[e0 + i] = T(0);
+      for (long long i = tid; i < rows * 3; i += nth) B.o_u[3 * (size_t)e0 + i] = T(0);
+    }
+  }
   if (S == 1 && t < 0) return;
   const int EPW = TMD_WAVE / A.L;
   const int c0 = G.el * V;

@@ -647,11 +647,11 @@ class _ETMessageBwd(Function):
         o = dict(dtype=q.dtype, device=q.device)
         gq, gk, gv = rows_like(q), rows_like(k), rows_like(v)
         gw = torch.empty((N, 3, H), **o)
-        ge = lambda shape, dtype, device: graph.alloc_edge_grad(shape, dtype, device)  # noqa: E731
-        gpk = rows_like(pk, ge) if pk is not None else None
-        gpv = rows_like(pv, ge) if pv is not None else None
-        gC = ge((E,), q.dtype, q.device)
-        gu = ge((E, 3), q.dtype, q.device)
+        # every row is written (static-capacity padding rows with zeros by the kernel): no memsets
+        gpk = rows_like(pk) if pk is not None else None
+        gpv = rows_like(pv) if pv is not None else None
+        gC = torch.empty((E,), **o)
+        gu = torch.empty((E, 3), **o)
         et_message_bwd_launch(q, k, v, vec, pk, pv, C, u, graph, heads, gx, gvec, gq, gk, gv, gw,
                               gpk, gpv, gC, gu)
         if gpk is None:
@@ -707,24 +707,27 @@ def et_message_bwd2(ctx, ggs):
     def dense(g, shape):
         return torch.zeros(shape, **o) if (g is None or g.numel() == 0) else g.contiguous()
 
+    def rows(g, shape):  # edge cotangents may be row-strided views (read through their leading dimension)
+        return torch.zeros(shape, **o) if (g is None or g.numel() == 0) else _rowmajor(g)
+
     ggq, ggk, ggv = dense(ggs[0], (N, H)), dense(ggs[1], (N, H)), dense(ggs[2], (N, 3 * H))
     ggw = dense(ggs[3], (N, 3, H))
-    ggpk = dense(ggs[4], (E, H)) if pk is not None else None
-    ggpv = dense(ggs[5], (E, 3 * H)) if pv is not None else None
+    ggpk = rows(ggs[4], (E, H)) if pk is not None else None
+    ggpv = rows(ggs[5], (E, 3 * H)) if pv is not None else None
     ggC, ggu = dense(ggs[6], (E,)), dense(ggs[7], (E, 3))
     d_gx, d_gvec, d_q = torch.empty((N, H), **o), torch.empty((N, 3, H), **o), torch.empty((N, H), **o)
     d_k, d_v, d_vec = torch.zeros((N, H), **o), torch.zeros((N, 3 * H), **o), torch.zeros((N, 3, H), **o)
-    d_pk = torch.zeros((E, H), **o) if pk is not None else None
-    d_pv = torch.zeros((E, 3 * H), **o) if pv is not None else None
-    d_C, d_u = torch.zeros((E,), **o), torch.zeros((E, 3), **o)
-    qc, kc, vc = q.contiguous(), k.contiguous(), v.contiguous()
-    pkc = None if pk is None else pk.contiguous()
-    pvc = None if pv is None else pv.contiguous()
+    # per-edge outputs: every row written (padding rows with zeros by the kernel)
+    d_pk = torch.empty((E, H), **o) if pk is not None else None
+    d_pv = torch.empty((E, 3 * H), **o) if pv is not None else None
+    d_C, d_u = torch.empty((E,), **o), torch.empty((E, 3), **o)
+    qc, kc, vc, pkc, pvc = (_rowmajor(t) for t in (q, k, v, pk, pv))  # read in place through ld
     rc = lib.tmdnet_et_message_bwd2(
         nat.dtype_code(q.dtype), N, H, ctx.heads, nat.ptr(graph.row_ptr), nat.ptr(graph.src), E,
-        nat.ptr(qc), H, nat.ptr(kc), H, nat.ptr(vc), 3 * H, nat.ptr(vec), nat.ptr(pkc), H, nat.ptr(pvc), 3 * H,
+        nat.ptr(qc), _ld(qc), nat.ptr(kc), _ld(kc), nat.ptr(vc), _ld(vc), nat.ptr(vec), nat.ptr(pkc), _ld(pkc),
+        nat.ptr(pvc), _ld(pvc),
         nat.ptr(C), nat.ptr(u), nat.ptr(gx), nat.ptr(gvec), nat.ptr(ggq), nat.ptr(ggk), nat.ptr(ggv),
-        nat.ptr(ggw), nat.ptr(ggpk), H, nat.ptr(ggpv), 3 * H, nat.ptr(ggC), nat.ptr(ggu), nat.ptr(d_gx),
+        nat.ptr(ggw), nat.ptr(ggpk), _ld(ggpk), nat.ptr(ggpv), _ld(ggpv), nat.ptr(ggC), nat.ptr(ggu), nat.ptr(d_gx),
         nat.ptr(d_gvec), nat.ptr(d_q), nat.ptr(d_k), nat.ptr(d_v), nat.ptr(d_vec), nat.ptr(d_pk),
         nat.ptr(d_pv), nat.ptr(d_C), nat.ptr(d_u), 0, nat.stream(q.device))
     nat.check(rc, "tmdnet_et_message_bwd2")
