@@ -592,6 +592,15 @@ class _ETStackBwd(Function):
             return kernels.et_message(q, k, v, vec, pk, pv, C_, u_, graph, heads)
 
         _create = torch.is_grad_enabled()  # third order only if the caller builds a graph
+        n_out = 4 + len(saved)
+        # inputs whose gradient this backward must deliver: asked for AND consumed downstream (a
+        # training step's loss.backward(inputs=params) never runs the position branch, so the
+        # cutoff / unit-vector / distance gradients -- E-sized work -- are skipped)
+        nf = iter(ctx.next_functions)  # one entry per tensor argument (None arguments have none)
+        want = []
+        for i, t in enumerate(saved):
+            node = next(nf)[0] if t is not None else None
+            want.append(t is not None and ctx.needs_input_grad[4 + i] and _will_run(node))
         with torch.enable_grad():
             leaves = [None if t is None else t.detach().requires_grad_(True) for t in saved]
             gX, gV, x, f, C, u, r = leaves[:7]
@@ -599,19 +608,21 @@ class _ETStackBwd(Function):
             f_in = kernels.rbf_composite(r, *meta.rbf) if ctx.dr else f
             xo, vo = composite_stack(meta, x, f_in, C, u, params, message=message)
             wrt = [x, f, C, u, r] + params
-            live = [t for t in wrt if t is not None]
-            first = torch.autograd.grad((xo, vo), live, (gX, gV), create_graph=True, allow_unused=True)
-            it = iter(first)
-            first_full = [next(it) if t is not None else None for t in wrt]
-            sel = [(fg, g) for fg, g in zip(first_full, ggs) if fg is not None and g is not None]
-            ins = [t for t in leaves if t is not None]
-            n_out = 4 + len(leaves)
+            # first-order gradients only for the outputs that received a cotangent (the force pass's
+            # parameter gradients are never formed: their cotangents are None)
+            pick = [i for i, (t, g) in enumerate(zip(wrt, ggs)) if t is not None and g is not None]
+            ins = [t for t, w in zip(leaves, want) if w]
+            if not pick or not ins:
+                return (None,) * n_out
+            first = torch.autograd.grad((xo, vo), [wrt[i] for i in pick], (gX, gV), create_graph=True,
+                                        allow_unused=True)
+            sel = [(fg, ggs[i]) for fg, i in zip(first, pick) if fg is not None]
             if not sel:
                 return (None,) * n_out
             second = torch.autograd.grad([fg for fg, _ in sel], ins, [g for _, g in sel],
                                          create_graph=_create, allow_unused=True)
         it = iter(second)
-        res = [next(it) if t is not None else None for t in leaves]
+        res = [next(it) if w else None for w in want]
         return (None, None, None, None) + tuple(res)
 
 
