@@ -56,16 +56,19 @@ template <>
 __device__ __forceinline__ float sig<float>(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
 
 // out[t][r][j] = bias[j] + sum_k W[j][k] in[t][r][k] for j < J (rows of A) then rows of B (J2 rows,
-// written to out2), r < R vectors per atom; atom stride P, vector stride ld.  Each thread owns JT
-// rows; VEC: K, ldi, P multiples of 4 -> one 16-byte weight load per row and one broadcast
-// ds_read_b128 per (atom, vector) feed 4*JT FMAs.
-template <typename T, int NT, int R, int JT, bool VEC>
+// written to out2), r < R vectors per atom; atom stride P, vector stride ld.  Each group of KS
+// adjacent lanes owns JT rows and splits K between its lanes (interleaved 4-wide chunks, then an
+// xor-shuffle sum): the narrow products (64-128 rows) still occupy the whole workgroup and each
+// lane's dependent chain is K/KS long.  VEC: K, ldi, P multiples of 4 -> one 16-byte weight load
+// per row and one broadcast ds_read_b128 per (atom, vector) feed 4*JT FMAs.
+template <typename T, int NT, int R, int JT, bool VEC, int KS = 1>
 __device__ __forceinline__ void rows2(const T* __restrict__ A, const T* __restrict__ ab, int J,
                                       const T* __restrict__ B, const T* __restrict__ bb, int J2, int K,
                                       const T* in, int ldi, T* out, int ldo, T* out2, int ldo2, int P) {
   using V4 = T __attribute__((ext_vector_type(4)));
   const int JJ = J + J2;
-  for (int j0 = threadIdx.x * JT; j0 < JJ; j0 += blockDim.x * JT) {
+  const int ks = threadIdx.x % KS;
+  for (int j0 = (threadIdx.x / KS) * JT; j0 < JJ; j0 += (blockDim.x / KS) * JT) {
     const T* w[JT];
     T acc[JT][NT][R];
 #pragma unroll
@@ -75,7 +78,7 @@ __device__ __forceinline__ void rows2(const T* __restrict__ A, const T* __restri
       const int jj = first ? j : j - J;
       w[q] = !ok ? A : first ? A + (size_t)jj * K : B + (size_t)jj * K;  // dead rows read row 0
       const T* bp = first ? ab : bb;
-      const T b0 = (ok && bp) ? bp[jj] : T(0);
+      const T b0 = (ok && bp && ks == 0) ? bp[jj] : T(0);
 #pragma unroll
       for (int t = 0; t < NT; ++t)
 #pragma unroll
@@ -83,7 +86,7 @@ __device__ __forceinline__ void rows2(const T* __restrict__ A, const T* __restri
     }
     if (VEC) {
 #pragma unroll 4
-      for (int k = 0; k < K; k += 4) {
+      for (int k = 4 * ks; k < K; k += 4 * KS) {
         V4 wv[JT];
 #pragma unroll
         for (int q = 0; q < JT; ++q) wv[q] = *reinterpret_cast<const V4*>(w[q] + k);
@@ -99,7 +102,7 @@ __device__ __forceinline__ void rows2(const T* __restrict__ A, const T* __restri
       }
     } else {
 #pragma unroll 8
-      for (int k = 0; k < K; ++k) {
+      for (int k = ks; k < K; k += KS) {
         T wv[JT];
 #pragma unroll
         for (int q = 0; q < JT; ++q) wv[q] = w[q][k];
@@ -112,6 +115,17 @@ __device__ __forceinline__ void rows2(const T* __restrict__ A, const T* __restri
             for (int q = 0; q < JT; ++q) acc[q][t][r] += wv[q] * iv;
           }
       }
+    }
+    if constexpr (KS > 1) {
+#pragma unroll
+      for (int q = 0; q < JT; ++q)
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int o = 1; o < KS; o <<= 1) acc[q][t][r] += __shfl_xor(acc[q][t][r], o);
+      if (ks) continue;
     }
 #pragma unroll
     for (int q = 0; q < JT; ++q) {
@@ -261,7 +275,7 @@ __global__ __launch_bounds__(256) void k_eq_head(int n, int H, const T* __restri
   __syncthreads();
 
   // ---------------- block 1 forward
-  rows2<T, NT, 3, 2, VEC>(W.w1, nullptr, H, W.w2, nullptr, O, H, sm + L.v, H, sm + L.vb, H, sm + L.v2, O, P);
+  rows2<T, NT, 3, 2, VEC, 2>(W.w1, nullptr, H, W.w2, nullptr, O, H, sm + L.v, H, sm + L.vb, H, sm + L.v2, O, P);
   __syncthreads();
   for (int i = tid; i < NT * H; i += bs) {
     const int t = i / H, c = i - t * H;
@@ -270,7 +284,7 @@ __global__ __launch_bounds__(256) void k_eq_head(int n, int H, const T* __restri
     sm[t * P + L.h + H + c] = sqrt(a0 * a0 + a1 * a1 + a2 * a2);
   }
   __syncthreads();
-  rows2<T, NT, 1, 2, VEC>(W.u1w, W.u1b, H, nullptr, nullptr, 0, 2 * H, sm + L.h, 0, sm + L.u, 0, nullptr, 0, P);
+  rows2<T, NT, 1, 2, VEC, 4>(W.u1w, W.u1b, H, nullptr, nullptr, 0, 2 * H, sm + L.h, 0, sm + L.u, 0, nullptr, 0, P);
   __syncthreads();
   for (int i = tid; i < NT * H; i += bs) {
     const int t = i / H, c = i - t * H;
@@ -278,7 +292,7 @@ __global__ __launch_bounds__(256) void k_eq_head(int n, int H, const T* __restri
     sm[t * P + L.s + c] = u * sig(u);
   }
   __syncthreads();
-  rows2<T, NT, 1, 2, VEC>(W.u2w, W.u2b, 2 * O, nullptr, nullptr, 0, H, sm + L.s, 0, sm + L.o, 0, nullptr, 0, P);
+  rows2<T, NT, 1, 2, VEC, 4>(W.u2w, W.u2b, 2 * O, nullptr, nullptr, 0, H, sm + L.s, 0, sm + L.o, 0, nullptr, 0, P);
   __syncthreads();
   for (int i = tid; i < NT * O; i += bs) {
     const int t = i / O, c = i - t * O;
@@ -291,7 +305,7 @@ __global__ __launch_bounds__(256) void k_eq_head(int n, int H, const T* __restri
   __syncthreads();
 
   // ---------------- block 2 forward (Q = O inputs, 1 output)
-  rows2<T, NT, 3, 2, VEC>(W.v1, nullptr, Q, W.v2, nullptr, 1, O, sm + L.v1, O, sm + L.vb2, Q, sm + L.v22, 1, P);
+  rows2<T, NT, 3, 2, VEC, 4>(W.v1, nullptr, Q, W.v2, nullptr, 1, O, sm + L.v1, O, sm + L.vb2, Q, sm + L.v22, 1, P);
   __syncthreads();
   for (int i = tid; i < NT * Q; i += bs) {
     const int t = i / Q, c = i - t * Q;
@@ -300,7 +314,7 @@ __global__ __launch_bounds__(256) void k_eq_head(int n, int H, const T* __restri
     sm[t * P + L.h2 + Q + c] = sqrt(a0 * a0 + a1 * a1 + a2 * a2);
   }
   __syncthreads();
-  rows2<T, NT, 1, 2, VEC>(W.p1w, W.p1b, Q, nullptr, nullptr, 0, 2 * Q, sm + L.h2, 0, sm + L.u2, 0, nullptr, 0, P);
+  rows2<T, NT, 1, 2, VEC, 8>(W.p1w, W.p1b, Q, nullptr, nullptr, 0, 2 * Q, sm + L.h2, 0, sm + L.u2, 0, nullptr, 0, P);
   __syncthreads();
   for (int i = tid; i < NT * Q; i += bs) {
     const int t = i / Q, c = i - t * Q;
@@ -312,7 +326,7 @@ __global__ __launch_bounds__(256) void k_eq_head(int n, int H, const T* __restri
     sm[t * P + L.gu2 + c] = seed * W.p2w[c] * sg * (T(1) + u * (T(1) - sg));
   }
   __syncthreads();
-  rows2<T, NT, 1, 2, VEC>(W.p2w, W.p2b, 1, nullptr, nullptr, 0, Q, sm + L.s2, 0, sm + L.o2, 0, nullptr, 0, P);
+  rows2<T, NT, 1, 2, VEC, 16>(W.p2w, W.p2b, 1, nullptr, nullptr, 0, Q, sm + L.s2, 0, sm + L.o2, 0, nullptr, 0, P);
   __syncthreads();
   if (y && tid < nt) y[n0 + tid] = sm[tid * P + L.o2];
   if (jx == nullptr) return;
