@@ -8,7 +8,21 @@ SRCS     := $(wildcard $(PKG)/csrc/*.hip)
 OBJS     := $(patsubst $(PKG)/csrc/%.hip,build/hip/%.o,$(SRCS))
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Iinclude -I$(PKG)/csrc -Wall -Wno-unused-function
 
+DBGLIB   := $(LIBDIR)/libtmdnet_hip_debug.so
+DBGOBJS  := $(patsubst $(PKG)/csrc/%.hip,build/hip_dbg/%.o,$(SRCS))
+
 all: $(LIB) oracle
+
+# index-range checks in the CSR kernels (TMD_DCHECK); load with TMDNET_LIB=debug
+debug: $(DBGLIB)
+
+build/hip_dbg/%.o: $(PKG)/csrc/%.hip $(wildcard $(PKG)/csrc/*.h) include/tmdnet.h
+	@mkdir -p build/hip_dbg
+	$(HIPCC) $(HIPFLAGS) -DTMDNET_DEBUG_INDEX -c $< -o $@
+
+$(DBGLIB): $(DBGOBJS)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $(DBGOBJS) -o $@
 
 build/hip/%.o: $(PKG)/csrc/%.hip $(wildcard $(PKG)/csrc/*.h) include/tmdnet.h
 	@mkdir -p build/hip
@@ -22,7 +36,7 @@ oracle:
 	$(MAKE) -C oracle
 
 clean:
-	rm -rf build $(LIB)
+	rm -rf build $(LIB) $(DBGLIB)
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle clean
+.PHONY: all oracle clean debug

@@ -2,7 +2,8 @@
 """Benchmark: ET-QM9 (128 channels, 8 layers, 64 RBF, cutoff 5) energy + forces, molecules/s.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--mode infer|train]
-  (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
+  (N > 1 without a launcher: bench.py starts N rank processes itself through torch.distributed.run
+   before anything touches a GPU; under torchrun, WORLD_SIZE must equal N)
 
 One step = TorchMD_Net.forward with derivative=True (y and -dy/dpos, create_graph=True exactly as
 reference models/model.py:286-298) on a batch of 32 synthetic QM9-like molecules resident in HBM
@@ -11,6 +12,10 @@ adds the force-matching loss, double backward, the fused RCCL gradient all-reduc
 Weak scaling: every rank processes its own batch; value = molecules of all ranks / max-rank time.
 
 Also reported (rank 0):
+  ddp_train    -- the data-parallel TRAINING step at this N: ET-SPICE C4, 16 x 40
+                  atoms per GPU, E+F loss, forces with create_graph, double backward, ONE fused RCCL
+                  all-reduce of the gradients, fused AdamW; HIP-graph replay of fwd + double backward on
+                  every rank; molecules/s of all ranks / max-rank time (weak scaling).
   roofline     -- the ET edge-aggregation kernel (tmdnet_et_message_fwd) on a C5-scale periodic
                   water box (50,001 atoms, ~2.7 M edges), HIP events on the launching stream;
                   algorithmic bytes per launch = E*(20 + 16H) + N*(48H + 4)  (SURVEY.md §8(d)).
@@ -55,7 +60,11 @@ def parse():
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip the secondary lines (TensorNet C3 graph replay, ET training step)")
     ap.add_argument("--no-graphed-train", dest="graphed_train", action="store_false",
-                    help="skip the HIP-graph-captured training step (training.GraphedTrainStep; N=1 only)")
+                    help="skip the HIP-graph-captured ET-QM9 training step (training.GraphedTrainStep)")
+    ap.add_argument("--no-ddp-train", dest="ddp_train", action="store_false",
+                    help="skip the ddp_train line (ET-SPICE graphed training step + all-reduce)")
+    ap.add_argument("--cpu-extra-seconds", type=float, default=6.0,
+                    help="CPU sample per extra baseline config (C2 training, C3, C4, C5 1500-atom box)")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
@@ -83,6 +92,59 @@ def et_args(channels):
     args.update(prior_model=None, embedding_dimension=channels, derivative=True, output_model="Scalar",
                 precision=32)
     return args
+
+
+def maybe_spawn(a):
+    """--gpus N > 1 without a launcher: start N ranks (one process per GPU) through
+    torch.distributed.run as a CHILD and exit with its code.  Runs before any GPU call (this parent
+    never initialises HIP).  Under a launcher, WORLD_SIZE must equal N."""
+    ws_env = os.environ.get("WORLD_SIZE")
+    if ws_env is not None:
+        if int(ws_env) != a.gpus:
+            print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={ws_env}", file=sys.stderr)
+            sys.exit(2)
+        return
+    if a.gpus <= 1:
+        return
+    import socket
+    import subprocess
+    s_ = socket.socket()
+    s_.bind(("127.0.0.1", 0))
+    port = s_.getsockname()[1]
+    s_.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    phase(f"spawning {a.gpus} ranks: {' '.join(cmd[1:6])} ...")
+    sys.exit(subprocess.call(cmd))
+
+
+def host_cpu_info():
+    """CPU model, physical cores of the machine, and the threads this process may use."""
+    model, phys = None, set()
+    try:
+        cur = {}
+        for line in open("/proc/cpuinfo"):
+            if ":" not in line:
+                if "core id" in cur:
+                    phys.add((cur.get("physical id"), cur["core id"]))
+                cur = {}
+                continue
+            k, v = (x.strip() for x in line.split(":", 1))
+            cur[k] = v
+            if k == "model name" and model is None:
+                model = v
+        if "core id" in cur:
+            phys.add((cur.get("physical id"), cur["core id"]))
+    except OSError:
+        pass
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS")
+    threads = min(aff, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else aff
+    return {"cpu_model": model, "physical_cores_machine": len(phys) or None, "logical_cpus": os.cpu_count(),
+            "affinity_cpus": aff, "omp_num_threads_env": omp, "threads_used": threads}
 
 
 def setup_dist():
@@ -336,19 +398,21 @@ def spice_like(n_mol, gen_seed):
     return z, pos, batch
 
 
-def secondary_spice(a, ws, rank, dev):
-    """C4: ET-SPICE (examples/ET-SPICE.yaml: 128 ch, 5 layers, cutoff 10, 128 neighbours), 16 x 40-atom
-    molecules per GPU: energy + forces (HIP-graph replay) and the training step (E+F loss with the
-    config's y / neg_dy weights 0.5 / 0.5, double backward, fused RCCL all-reduce, AdamW, eager)."""
+def spice_model_args():
     import yaml
-    from torchmdnet.graphs import GraphedEnergyForces
-    from torchmdnet.models.model import create_model
-    from torchmdnet.training import LNNPStep
     with open(os.path.join(ROOT, "tests", "golden", "configs", "et_spice.yaml")) as f:
         args = yaml.safe_load(f)
     args.update(prior_model=None, precision=32, derivative=True, output_model="Scalar")
+    return args
+
+
+def secondary_spice(a, ws, rank, dev):
+    """C4: ET-SPICE (examples/ET-SPICE.yaml: 128 ch, 5 layers, cutoff 10, 128 neighbours), 16 x 40-atom
+    molecules per GPU: energy + forces, HIP-graph replay."""
+    from torchmdnet.graphs import GraphedEnergyForces
+    from torchmdnet.models.model import create_model
     torch.manual_seed(0)
-    model = create_model(args).to(dev)
+    model = create_model(spice_model_args()).to(dev)
     n_mol = 16
     z, pos, batch = spice_like(n_mol, 1 + rank)
     z, pos, batch = z.to(dev), pos.float().to(dev), batch.to(dev)
@@ -356,20 +420,39 @@ def secondary_spice(a, ws, rank, dev):
     el = timed_loop(lambda: gm(pos), a.warmup, a.steps, ws, dev)
     gm.check_capacity()
     gm.release()
-    res = {"workload": "ET-SPICE energy+forces (C4: 16 x 40 atoms, 5 layers, cutoff 10), hip-graph replay",
-           "value": round(n_mol * ws * a.steps / el, 2), "unit": "molecules/s",
-           "ms_per_step": round(1000 * el / a.steps, 4), "atoms_per_gpu": int(z.shape[0])}
+    return {"workload": "ET-SPICE energy+forces (C4: 16 x 40 atoms, 5 layers, cutoff 10), hip-graph replay",
+            "value": round(n_mol * ws * a.steps / el, 2), "unit": "molecules/s",
+            "ms_per_step": round(1000 * el / a.steps, 4), "atoms_per_gpu": int(z.shape[0])}
+
+
+def ddp_train(a, ws, rank, dev):
+    """The data-parallel training step of SURVEY.md 8(e) at this N: ET-SPICE C4 (16 x 40 atoms per
+    GPU, y / neg_dy weights 0.5 / 0.5 of ET-SPICE.yaml), forward + force pass + double backward
+    replayed from one HIP graph per rank, ONE fused RCCL all-reduce of the 4.9 MB gradient, fused
+    AdamW.  Every rank starts from rank 0's weights (broadcast) with its own molecules."""
+    from torchmdnet.models.model import create_model
+    from torchmdnet.training import GraphedTrainStep
+    torch.manual_seed(0)
+    model = create_model(spice_model_args()).to(dev)
+    n_mol = 16
+    z, pos, batch = spice_like(n_mol, 1 + rank)
+    z, pos, batch = z.to(dev), pos.float().to(dev), batch.to(dev)
     gy = torch.Generator().manual_seed(200 + rank)
     y_lab = torch.randn(n_mol, 1, generator=gy).to(dev)
     f_lab = torch.randn(z.shape[0], 3, generator=gy).to(dev)
-    trainer = LNNPStep(model, lr=1e-4, y_weight=0.5, neg_dy_weight=0.5)
-    steps = max(10, a.steps // 2)
-    el = timed_loop(lambda: trainer.step(z, pos, batch, y_lab, f_lab), max(3, a.warmup // 2), steps, ws, dev)
-    res["train_step"] = {"workload": "ET-SPICE training step (E+F MSE 0.5/0.5, double backward, "
-                                     + ("fused RCCL all-reduce, " if ws > 1 else "") + "AdamW), eager",
-                         "value": round(n_mol * ws * steps / el, 2), "unit": "molecules/s",
-                         "ms_per_step": round(1000 * el / steps, 4), "parallelism": f"dp{ws}"}
-    return res
+    tr = GraphedTrainStep(model, z, pos, batch, y_lab, f_lab, lr=1e-4, y_weight=0.5, neg_dy_weight=0.5)
+    nparam = int(tr.reduce.flat.numel() - 1)
+    steps = a.steps
+    el = timed_loop(lambda: tr.step(), a.warmup, steps, ws, dev)
+    tr.check_capacity()
+    tr.release()
+    return {"workload": "ET-SPICE training step (C4: 16 x 40 atoms per GPU, E+F MSE 0.5/0.5, double backward"
+                        + (", ONE fused RCCL all-reduce" if ws > 1 else "") + ", fused AdamW)",
+            "value": round(n_mol * ws * steps / el, 2), "unit": "molecules/s", "n_gpus": ws,
+            "ms_per_step": round(1000 * el / steps, 4), "steps": steps, "scaling": "weak",
+            "parallelism": f"dp{ws}", "grad_allreduce_bytes": nparam * 4,
+            "execution": "fwd + force pass + double backward in one HIP graph per rank; all-reduce + AdamW eager",
+            "edge_capacity": tr.edge_capacity}
 
 
 def secondary_tensornet(a, ws, rank, dev):
@@ -443,7 +526,7 @@ def secondary_train(a, ws, rank, dev):
                        + ("fused RCCL all-reduce, " if ws > 1 else "") + "AdamW), eager",
            "value": round(a.batch * ws * steps / el, 2), "unit": "molecules/s",
            "ms_per_step": round(1000 * el / steps, 4), "steps": steps, "parallelism": f"dp{ws}"}
-    if a.graphed_train and ws == 1:
+    if a.graphed_train:
         phase("train: graph-captured step")
         del trainer
         try:
@@ -454,38 +537,114 @@ def secondary_train(a, ws, rank, dev):
             res["graphed"] = {
                 "value": round(a.batch * ws * steps / el, 2), "unit": "molecules/s",
                 "ms_per_step": round(1000 * el / steps, 4), "edge_capacity": gtr.edge_capacity,
-                "execution": "fwd + force pass + double backward in one HIP graph; AdamW eager",
-                "validated": "tools/graphed_train_check.py: loss and gradients vs the eager step at this size "
-                             "(profiles/r01_graphed_train_check.json)"}
+                "execution": "fwd + force pass + double backward in one HIP graph; "
+                             + ("RCCL all-reduce + " if ws > 1 else "") + "fused AdamW eager"}
         except RuntimeError as exc:  # the eager line above stands on its own
             res["graphed"] = {"error": str(exc)[:300]}
     return res
 
 
-def cpu_baseline(model, args, z, pos, batch, seconds):
-    from oracle import model_oracle as O
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except AttributeError:
-        cores = os.cpu_count() or 1
-    cores = max(1, min(cores, 16))
-    torch.set_num_threads(cores)
-    sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
-    cfg = dict(args)
-    O.energy_forces(sd, cfg, z, pos, batch, dtype=torch.float32)  # warm-up
+def _time_cpu(fn, seconds, max_calls=200):
+    fn()  # warm-up
     n = 0
     t0 = time.perf_counter()
     while True:
-        O.energy_forces(sd, cfg, z, pos, batch, dtype=torch.float32)
+        fn()
         n += 1
         el = time.perf_counter() - t0
-        if el >= seconds or n >= 200:
-            break
+        if el >= seconds or n >= max_calls:
+            return n, el
+
+
+def _cpu_sd(model):
+    return {k: v.detach().cpu() for k, v in model.state_dict().items()}
+
+
+def cpu_baseline(model, args, z, pos, batch, seconds):
+    """C2 energy + forces with oracle/model_oracle.py on the host cores (the headline CPU line).
+    Threads: every CPU this process may use, capped by the box's OMP_NUM_THREADS share."""
+    from oracle import model_oracle as O
+    info = host_cpu_info()
+    cores = info["threads_used"]
+    torch.set_num_threads(cores)
+    sd = _cpu_sd(model)
+    n, el = _time_cpu(lambda: O.energy_forces(sd, dict(args), z, pos, batch, dtype=torch.float32,
+                                                 create_graph=True), seconds)
     mols = int(batch.max()) + 1
     return {"value": round(mols * n / el, 2), "unit": "molecules/s", "cores": cores, "kind": "port",
+            "host": info,
+            "calibration": "profiles/r02_cpu_calibration.json (restatement vs the shimmed reference, same "
+                           "8 cores of the build container)",
             "sample": f"oracle/model_oracle.py (PyTorch-CPU restatement of the reference ET path), "
                       f"{n} energy+force calls on the same {mols} molecules / weights, float32, "
                       f"{el:.1f} s, torch threads={cores}"}
+
+
+def cpu_baseline_extra(a, model, args, z, pos, batch):
+    """the CPU path on the other configs, each a bounded sample with the same thread
+    count: C2 training step, C3 TensorNet-rMD17, C4 ET-SPICE, C5 as a 1500-atom periodic water box
+    (the 50k-atom system is CPU-infeasible for the reference: its O(N^2) pair list needs > 62 GB
+    above ~2k atoms)."""
+    import yaml
+    from oracle import model_oracle as O
+    from torchmdnet.models.model import create_model
+    secs = a.cpu_extra_seconds
+    out = {}
+    # C2 training step: E+F MSE (forces with create_graph), double backward, AdamW
+    sd = _cpu_sd(model)
+    pnames = {k for k, _ in model.named_parameters()}
+    leaf = {k: (v.clone().requires_grad_(True) if k in pnames else v) for k, v in sd.items()}
+    opt = torch.optim.AdamW([leaf[k] for k in sorted(pnames)], lr=4e-4)
+    gy = torch.Generator().manual_seed(100)
+    nmol = int(batch.max()) + 1
+    y_lab = torch.randn(nmol, 1, generator=gy)
+    f_lab = torch.randn(z.shape[0], 3, generator=gy)
+
+    def train_step():
+        opt.zero_grad()
+        y, f = O.energy_forces(leaf, dict(args), z, pos, batch, dtype=torch.float32, create_graph=True)
+        loss = torch.nn.functional.mse_loss(y, y_lab) + torch.nn.functional.mse_loss(f, f_lab)
+        loss.backward()
+        opt.step()
+    n, el = _time_cpu(train_step, secs)
+    out["c2_train_step"] = {"value": round(nmol * n / el, 2), "unit": "molecules/s",
+                            "sample": f"{n} ET-QM9 training steps (E+F MSE, double backward, AdamW), {el:.1f} s"}
+    # C3 TensorNet-rMD17, 8 x aspirin (reference CPU semantics: the CPU op never pads)
+    with open(os.path.join(ROOT, "tests", "golden", "configs", "tensornet_rmd17.yaml")) as f:
+        targs = yaml.safe_load(f)
+    targs.update(prior_model=None, precision=32, derivative=True)
+    torch.manual_seed(0)
+    tm = create_model(targs)
+    zt, pt, bt = rmd17_like(8, 1)
+    n, el = _time_cpu(lambda: O.energy_forces(_cpu_sd(tm), dict(targs), zt, pt.float(), bt, dtype=torch.float32,
+                                              static_shapes=False, create_graph=True), secs)
+    out["c3_tensornet_rmd17"] = {"value": round(8 * n / el, 2), "unit": "molecules/s",
+                                 "sample": f"{n} energy+force calls, 8 x aspirin, {el:.1f} s"}
+    # C4 ET-SPICE, 16 x 40 atoms
+    sargs = spice_model_args()
+    torch.manual_seed(0)
+    sm = create_model(sargs)
+    zs, ps, bs = spice_like(16, 1)
+    ssd = _cpu_sd(sm)
+    n, el = _time_cpu(lambda: O.energy_forces(ssd, dict(sargs), zs, ps.float(), bs, dtype=torch.float32,
+                                                    create_graph=True), secs)
+    out["c4_et_spice"] = {"value": round(16 * n / el, 2), "unit": "molecules/s",
+                          "sample": f"{n} energy+force calls, 16 x 40 atoms, {el:.1f} s"}
+    # C5 water box at 1500 atoms (periodic, cutoff 5, ET-QM9 weights of the headline model)
+    nb = 1500
+    g = torch.Generator().manual_seed(7)
+    L = (nb / 0.1003) ** (1.0 / 3.0)
+    pw = (torch.rand(nb, 3, generator=g, dtype=torch.float64) * L).float()
+    zw = torch.tensor([8, 1, 1], dtype=torch.long).repeat(nb // 3 + 1)[:nb]
+    bw = torch.zeros(nb, dtype=torch.long)
+    wargs = dict(args, box=[[L, 0, 0], [0, L, 0], [0, 0, L]])
+    n, el = _time_cpu(lambda: O.energy_forces(sd, wargs, zw, pw, bw, dtype=torch.float32, create_graph=True),
+                      secs)
+    out["c5_water_box_1500"] = {"value": round(nb * n / el, 1), "unit": "atoms/s",
+                                "sample": f"{n} energy+force calls, {nb}-atom periodic water box L={L:.1f} A, "
+                                          f"{el:.1f} s",
+                                "c5_50k": "CPU-infeasible for the reference (O(N^2) CPU pair list)"}
+    return out
 
 
 def main():
@@ -498,6 +657,7 @@ def main():
             launch()
         torch.cuda.synchronize()
         return
+    maybe_spawn(a)
     ws, rank, dev = setup_dist()
     from torchmdnet import kernels
     from torchmdnet.models.model import create_model
@@ -608,6 +768,11 @@ def main():
         sec["et_water_box_c5"] = secondary_water_box(a, ws, rank, dev)
         if rank == 0:
             out["secondary"] = sec
+    if a.mode == "infer" and a.ddp_train:
+        phase("ddp_train: ET-SPICE graphed training step")
+        dt = ddp_train(a, ws, rank, dev)
+        if rank == 0:
+            out["ddp_train"] = dt
     if rank == 0 and not a.no_roofline:
         phase("roofline probe (C5 water box)")
         out["roofline"] = roofline_probe(a, dev)
@@ -618,6 +783,9 @@ def main():
     if rank == 0 and ws == 1 and not a.no_cpu_baseline:
         phase("CPU baseline")
         out["cpu_baseline"] = cpu_baseline(model, args, z, pos, batch, a.cpu_seconds)
+        if a.cpu_extra_seconds > 0:
+            phase("CPU baseline: other configs")
+            out["cpu_baseline"]["other_configs"] = cpu_baseline_extra(a, model, args, z, pos, batch)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if ws > 1:

@@ -109,21 +109,31 @@ def layer_norm(sd, name, x):
 
 
 # ----------------------------------------------------------------------------- graph
-def edge_geometry(pos, batch, cl, cu, max_pairs=None, loop=True, pad_static=False):
+def edge_geometry(pos, batch, cl, cu, max_pairs=None, loop=True, pad_static=False, box=None):
     """Edges (src=nb[0], dst=nb[1]) + differentiable deltas / distances (self loops: constant 0, as
     the reference CPU op appends them without a norm).  ``pad_static`` emulates the CUDA op's
-    (-1,-1) padding up to ``max_pairs`` remapped to (0,0) edges by TensorNet (tensornet.py:215-221)."""
-    nb, _, _ = neighbors(pos.detach().cpu().numpy(), batch.cpu().numpy(), cl, cu, loop=loop,
-                         include_transpose=True)
+    (-1,-1) padding up to ``max_pairs`` remapped to (0,0) edges by TensorNet (tensornet.py:215-221).
+    ``box`` (3x3, reduced form): periodic minimum-image deltas (neighbors_cpu.cpp:69-78), carried as
+    the constant image shift added to the differentiable pos[src] - pos[dst]."""
+    nb, ref_dl, _ = neighbors(pos.detach().cpu().numpy(), batch.cpu().numpy(), cl, cu, loop=loop,
+                              include_transpose=True, box=box)
     src = torch.as_tensor(nb[0])
     dst = torch.as_tensor(nb[1])
+    shift = None
+    if box is not None:
+        raw = (pos.detach().index_select(0, src) - pos.detach().index_select(0, dst)).double()
+        shift = (torch.as_tensor(ref_dl) - raw).to(pos.dtype)
     if pad_static:
         npad = int(max_pairs) - src.numel()
         assert npad >= 0, "fixture overflowed capacity"
         src = torch.cat([src, torch.zeros(npad, dtype=src.dtype)])
         dst = torch.cat([dst, torch.zeros(npad, dtype=dst.dtype)])
+        if shift is not None:
+            shift = torch.cat([shift, torch.zeros(npad, 3, dtype=shift.dtype)])
     self_edge = src == dst
     dl = pos.index_select(0, src) - pos.index_select(0, dst)
+    if shift is not None:
+        dl = dl + shift
     dl = torch.where(self_edge.unsqueeze(1), torch.zeros_like(dl), dl)
     sq = (dl * dl).sum(1)
     r = torch.where(self_edge, torch.zeros_like(sq), torch.where(self_edge, torch.ones_like(sq), sq).sqrt())
@@ -138,7 +148,7 @@ def et_representation(sd, cfg, z, pos, batch, prefix="representation_model.", ho
     cl, cu = cfg["cutoff_lower"], cfg["cutoff_upper"]
     N = z.shape[0]
     x = sd[p("embedding.weight")][z]
-    src, dst, dl, r, self_edge = edge_geometry(pos, batch, cl, cu)
+    src, dst, dl, r, self_edge = edge_geometry(pos, batch, cl, cu, box=cfg.get("box"))
     if cfg.get("rbf_type", "expnorm") == "expnorm":
         f = expnorm(r, sd[p("distance_expansion.means")], sd[p("distance_expansion.betas")], cl, cu)
     else:

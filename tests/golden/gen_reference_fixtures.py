@@ -283,8 +283,55 @@ def gen_seed_checksums():
     save("seed1234_qm9.npz", res)
 
 
+# --------------------------------------------------------------------------- edge cases (round 2)
+def gen_edge_cases():
+    """ET with a lower cutoff (shifted CosineCutoff, neighbour lower bound; reference
+    models/utils.py:362-390, neighbors_cpu.cpp:82-86) and ET with the Atomref prior of ET-QM9.yaml
+    (priors/atomref.py:8-42) with non-zero per-element references."""
+    for name, extra in (("et_tiny_cl2_f64.npz", dict(cutoff_lower=2.0, cutoff_upper=5.0)),
+                        ("et_tiny_atomref_f64.npz", dict(prior_model="Atomref", prior_args={"max_z": 100}))):
+        args = base_args("equivariant-transformer", embedding_dimension=32, num_layers=2, num_rbf=16,
+                         num_heads=4, max_num_neighbors=32, derivative=True, output_model="Scalar",
+                         precision=64)
+        args.update(extra)
+        seed_everything(1234)
+        model = create_model(args)
+        if "prior_model" in extra:
+            g = torch.Generator().manual_seed(77)
+            w = model.prior_model[0].atomref.weight
+            w.data.copy_(torch.randn(w.shape, generator=g, dtype=w.dtype))
+        z, pos, batch = qm9_like(3)
+        res = run_model(model, z, pos, batch, torch.float64)
+        res.update(state_dict_arrays(model))
+        save(name, res)
+
+
+def gen_splits():
+    """utils.make_splits / train_val_test_split index sets (reference torchmdnet/utils.py:54-139)."""
+    from torchmdnet.utils import make_splits
+    res = {}
+    cases = [(1000, 0.8, 0.1, None, 1), (100, 50, 20, 30, 2), (200, 0.5, 0.25, 0.25, 3),
+             (131, 0.7, 0.2, 0.1, 4), (57, None, 10, 0.2, 5), (1000, 800, None, 0.1, 12345)]
+    for k, (n, tr, va, te, seed) in enumerate(cases):
+        a, b, c = make_splits(n, tr, va, te, seed)
+        res[f"s{k}/args"] = np.array([n, -1 if tr is None else tr, -1 if va is None else va,
+                                      -1 if te is None else te, seed], dtype=np.float64)
+        res[f"s{k}/is_float"] = np.array([isinstance(x, float) for x in (tr, va, te)])
+        res[f"s{k}/train"], res[f"s{k}/val"], res[f"s{k}/test"] = a.numpy(), b.numpy(), c.numpy()
+    order = np.random.default_rng(9).permutation(50)
+    a, b, c = make_splits(50, 30, 10, 10, 0, order=order)
+    res["order/order"] = order
+    res["order/train"], res["order/val"], res["order/test"] = a.numpy(), b.numpy(), c.numpy()
+    res["ncases"] = np.array([len(cases)])
+    save("splits_ref.npz", res)
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["neighbors", "et", "tensornet", "seed"]
+    which = sys.argv[1:] or ["neighbors", "et", "tensornet", "seed", "edge", "splits"]
+    if "edge" in which:
+        gen_edge_cases()
+    if "splits" in which:
+        gen_splits()
     if "neighbors" in which:
         gen_neighbors()
     if "et" in which:

@@ -57,3 +57,78 @@ def test_grad_allreduce_is_mean_of_ranks():
         assert torch.allclose(ra, mean, atol=1e-6)
         assert torch.allclose(rb, mean, atol=1e-6)
     assert m0 == m1 == 2.0
+
+
+class _ToyPotential(torch.nn.Module):
+    """Energy + forces with the TorchMD_Net.forward contract (y [B,1], neg_dy [N,3], forces through
+    create_graph autograd), small enough for CPU ranks."""
+
+    def __init__(self):
+        super().__init__()
+        self.emb = torch.nn.Embedding(10, 8)
+        self.mlp = torch.nn.Sequential(torch.nn.Linear(11, 16), torch.nn.SiLU(), torch.nn.Linear(16, 1))
+
+    def forward(self, z, pos, batch):
+        pos = pos.requires_grad_(True) if not pos.requires_grad else pos
+        h = torch.cat([self.emb(z), pos.pow(2)], dim=1)
+        x = self.mlp(h)
+        y = torch.zeros(int(batch.max()) + 1, 1, dtype=x.dtype).index_add(0, batch, x)
+        (dy,) = torch.autograd.grad(y.sum(), pos, create_graph=True)
+        return y, -dy
+
+
+def _train_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from torchmdnet.training import LNNPStep
+    torch.manual_seed(100 + rank)  # DIFFERENT initial weights on every rank
+    model = _ToyPotential()
+    init = [p.detach().clone() for p in model.parameters()]
+    trainer = LNNPStep(model, lr=1e-2, lr_warmup_steps=3)  # broadcasts rank 0's weights
+    after_bcast = [p.detach().clone() for p in model.parameters()]
+    views_ok = all(p.grad is not None and p.grad.data_ptr() == v.data_ptr()
+                   for p, v in zip(trainer.reduce.params, trainer.reduce.views))
+    g = torch.Generator().manual_seed(7 + rank)  # every rank its own molecules
+    losses = []
+    for _ in range(5):
+        z = torch.randint(1, 10, (12,), generator=g)
+        pos = torch.randn(12, 3, generator=g)
+        batch = torch.arange(3).repeat_interleave(4)
+        y = torch.randn(3, generator=g)  # 1-D labels: unsqueezed like reference module.py:147-148
+        f = torch.randn(12, 3, generator=g)
+        losses.append(float(trainer.step(z, pos, batch, y, f)))
+    final = [p.detach().clone() for p in model.parameters()]
+    npy = lambda ts: [t.numpy() for t in ts]  # by value: the rank may exit before the parent reads
+    out.put((rank, npy(init), npy(after_bcast), npy(final), views_ok, losses, trainer.opt.param_groups[0]["lr"]))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(180)
+def test_lnnp_step_broadcasts_and_keeps_replicas_identical():
+    """DDP semantics (reference scripts/train.py:175-189): rank 1 starts from different weights, the
+    trainer broadcasts rank 0's, every step averages the gradients in one all-reduce over the flat
+    buffer the .grad tensors are views of, so the replicas stay bit-identical while training on
+    disjoint data."""
+    import sys
+    from conftest import PKG
+    sys.path.insert(0, PKG)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_train_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {r: rest for r, *rest in (q.get(timeout=160) for _ in procs)}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (i0, b0, f0, v0, l0, lr0), (i1, b1, f1, v1, l1, lr1) = res[0], res[1]
+    eq = lambda x, y: all((a == b).all() for a, b in zip(x, y))
+    assert not eq(i0, i1)  # started different
+    assert eq(b0, b1)  # broadcast
+    assert eq(b0, i0)  # ... of rank 0's weights
+    assert eq(f0, f1)  # identical after 5 steps
+    assert not eq(f0, b0)  # and they did train
+    assert v0 and v1
+    assert l0 != l1  # on different data
+    assert lr0 == lr1 == pytest.approx(1e-2)  # warm-up over 3 steps reached the base LR

@@ -40,15 +40,23 @@ def _lib_loaded():
 
 
 # ----------------------------------------------------------------------------- neighbour op
-def _sets_equal_excluding_boundary(nb, dist, ref_nb, ref_dist, cutoff, eps=1e-6):
-    def keep(nbx, dx):
-        m = np.abs(dx - cutoff) > eps * max(cutoff, 1.0)
-        return nbx[:, m]
-    a = keep(nb, dist)
-    b = keep(ref_nb, ref_dist)
-    a = a[:, np.lexsort(a)]
-    b = b[:, np.lexsort(b)]
-    return a.shape == b.shape and np.array_equal(a, b)
+def _match_pairs(nb, dl, dist, ref_nb, ref_dl, ref_dist, cutoff, n, tol, eps=1e-6):
+    """Pair-by-pair comparison with the reference: every pair found by only one side must lie within
+    eps of the cutoff (CPU reference compares |d| < cu, the GPU rule d^2 < cu^2, so such a pair may
+    flip); every common pair must have the same deltas and distance (relative tol).  Returns the
+    number of boundary flips (0 in practice: the count is then exact)."""
+    band = eps * max(cutoff, 1.0)
+    a = nb[0].astype(np.int64) * (n + 1) + nb[1]
+    b = ref_nb[0].astype(np.int64) * (n + 1) + ref_nb[1]
+    assert len(np.unique(a)) == len(a) and len(np.unique(b)) == len(b)
+    _, ia, ib = np.intersect1d(a, b, return_indices=True)
+    only_a = np.setdiff1d(np.arange(len(a)), ia)
+    only_b = np.setdiff1d(np.arange(len(b)), ib)
+    assert np.all(np.abs(dist[only_a] - cutoff) <= band), ("extra pairs", nb[:, only_a], dist[only_a])
+    assert np.all(np.abs(ref_dist[only_b] - cutoff) <= band), ("missing pairs", ref_nb[:, only_b], ref_dist[only_b])
+    assert np.allclose(dist[ia], ref_dist[ib], rtol=tol, atol=tol)
+    assert np.allclose(dl[ia], ref_dl[ib], rtol=tol, atol=tol)
+    return len(only_a) + len(only_b)
 
 
 @pytest.mark.parametrize("strategy", ["brute", "shared", "cell"])
@@ -56,7 +64,7 @@ def test_neighbor_op_matches_reference_fixtures(strategy):
     from torchmdnet.neighbors import get_neighbor_pairs_kernel
     _lib_loaded()
     d = golden("neighbors_ref.npz")
-    n_checked = 0
+    n_checked = n_flips = 0
     for k in range(int(d["ncases"][0])):
         cutoff, loop, tr, periodic = d[f"c{k}/params"]
         box = d[f"c{k}/box"]
@@ -69,32 +77,25 @@ def test_neighbor_op_matches_reference_fixtures(strategy):
         if periodic:
             boxt = torch.tensor(box, dtype=pos.dtype)
         elif strategy == "cell":
+            # no box: the caller passes a 3*cutoff box with use_periodic=False (reference
+            # utils.py:199-202); the 3x3x3 cell grid then makes every atom a candidate of every
+            # atom, and the distances are not wrapped, so the list equals the plain one
             boxt = torch.tensor(np.eye(3) * 3 * cutoff, dtype=pos.dtype)
-            if 3 * cutoff < 2 * cutoff:
-                continue
         else:
             boxt = torch.empty((0, 0), dtype=pos.dtype)
-        if strategy == "cell" and not periodic:
-            # the reference cell list without a box wraps positions into a 3*cutoff box
-            # (utils.py:199-202), which only matches the plain list when every molecule fits it
-            continue
         nb, dl, dist, num = get_neighbor_pairs_kernel(strategy, pos, batch, boxt, bool(periodic), 0.0, float(cutoff),
                                                       cap, bool(loop), bool(tr))
         P = int(num[0].item())
-        assert P == ref_nb.shape[1] or abs(P - ref_nb.shape[1]) <= 2, (k, P, ref_nb.shape)
         nbh = nb[:, :P].cpu().numpy().astype(np.int64)
         assert (nb[:, P:] == -1).all() and (dist[P:] == 0).all() and (dl[P:] == 0).all()
-        dh = dist[:P].cpu().numpy()
-        assert _sets_equal_excluding_boundary(nbh, dh, ref_nb, d[f"c{k}/distances"], cutoff), k
-        # deltas / distances of matched pairs
-        nbs, dls, ds = O.sort_pairs(nbh, dl[:P].cpu().numpy(), dh)
-        rnb, rdl, rds = ref_nb, d[f"c{k}/deltas"], d[f"c{k}/distances"]
-        if nbs.shape == rnb.shape and np.array_equal(nbs, rnb):
-            tol = 1e-5 if pos.dtype == torch.float32 else 1e-12
-            assert np.allclose(ds, rds, rtol=tol, atol=tol), k
-            assert np.allclose(dls, rdl, rtol=tol, atol=tol), k
+        tol = 1e-5 if pos.dtype == torch.float32 else 1e-12
+        flips = _match_pairs(nbh, dl[:P].cpu().numpy(), dist[:P].cpu().numpy(), ref_nb, d[f"c{k}/deltas"],
+                             d[f"c{k}/distances"], float(cutoff), pos.shape[0], tol)
+        assert P == ref_nb.shape[1] + 0 or flips > 0, (k, P, ref_nb.shape)
+        n_flips += flips
         n_checked += 1
     assert n_checked > 0
+    assert n_flips == 0  # no boundary pair in the fixture grid: counts and pair sets exactly equal
 
 
 def test_neighbor_op_capacity_and_errors():

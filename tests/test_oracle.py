@@ -158,3 +158,44 @@ def test_tensornet_c3_padded_fixture():
     y, neg_dy = O.energy_forces(sd, dict(args), d["z"], d["pos"], d["batch"], static_shapes=True)
     assert np.allclose(y.detach().numpy(), d["y"], rtol=1e-4, atol=1e-5)
     assert np.allclose(neg_dy.numpy(), d["neg_dy"], rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("name,extra", [("et_tiny_cl2_f64", dict(cutoff_lower=2.0)),
+                                        ("et_tiny_atomref_f64", {})])
+def test_et_oracle_matches_reference_edge_cases(name, extra):
+    """Lower cutoff 2 A (shifted CosineCutoff + the neighbour list's lower bound, reference
+    models/utils.py:362-390, neighbors_cpu.cpp:82-86) and the Atomref prior with non-zero
+    per-element values (priors/atomref.py:8-42): outputs and the force-loss double backward."""
+    d = golden(name + ".npz")
+    sd = {k: torch.tensor(v, requires_grad=v.dtype.kind == "f") for k, v in state_dict_from(d).items()}
+    cfg = _et_cfg(32, 2, 16, 4)
+    cfg.update(extra)
+    y, neg_dy = O.energy_forces(sd, cfg, d["z"], d["pos"], d["batch"], create_graph=True)
+    assert np.allclose(y.detach().numpy(), d["y"], rtol=1e-10, atol=1e-10)
+    assert np.allclose(neg_dy.detach().numpy(), d["neg_dy"], rtol=1e-10, atol=1e-9)
+    loss = (y ** 2).sum() + (neg_dy ** 2).sum()
+    names = [k for k in d.files if k.startswith("g2/")]
+    grads = torch.autograd.grad(loss, [sd[k[3:]] for k in names], allow_unused=True)
+    for k, g in zip(names, grads):
+        if g is None:
+            assert np.allclose(d[k], 0), k
+        else:
+            assert np.allclose(g.detach().numpy(), d[k], rtol=1e-8, atol=1e-10), k
+
+
+def test_splits_match_reference():
+    """utils.make_splits / train_val_test_split == the reference's index sets
+    (torchmdnet/utils.py:54-139), counts and fractions, a None size, a fixed order."""
+    from torchmdnet.utils import make_splits
+    d = golden("splits_ref.npz")
+    for k in _cases(d):
+        n, tr, va, te, seed = d[f"s{k}/args"]
+        isf = d[f"s{k}/is_float"]
+        conv = lambda v, f: None if v == -1 else (float(v) if f else int(v))
+        a, b, c = make_splits(int(n), conv(tr, isf[0]), conv(va, isf[1]), conv(te, isf[2]), int(seed))
+        assert np.array_equal(a.numpy(), d[f"s{k}/train"]), k
+        assert np.array_equal(b.numpy(), d[f"s{k}/val"]), k
+        assert np.array_equal(c.numpy(), d[f"s{k}/test"]), k
+    a, b, c = make_splits(50, 30, 10, 10, 0, order=d["order/order"])
+    for x, key in ((a, "train"), (b, "val"), (c, "test")):
+        assert np.array_equal(x.numpy(), d[f"order/{key}"])

@@ -5,6 +5,16 @@
 
 #define TMD_WAVE 64
 
+// Index-range checks of the CSR kernels, compiled only into the debug library (`make debug`:
+// -DTMDNET_DEBUG_INDEX, lib/libtmdnet_hip_debug.so).  A failing check aborts the kernel (device
+// assert), naming the file and line.  The product library compiles them out.
+#ifdef TMDNET_DEBUG_INDEX
+#include <assert.h>
+#define TMD_DCHECK(c) assert(c)
+#else
+#define TMD_DCHECK(c) ((void)0)
+#endif
+
 namespace tmd {
 
 // ---- status codes returned across the C ABI (never throw across it) ----

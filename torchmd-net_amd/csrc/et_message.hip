@@ -214,6 +214,7 @@ __device__ __forceinline__ void edge_chunks_pf(const Args<T>& A, int b, int e, i
     if (lane < n) {
       const int k = c + lane;
       s_r = A.src[k];
+      TMD_DCHECK(s_r >= 0 && s_r < A.n);
       if (A.prow) p_r = A.prow[k];
       C_r = A.C[k];
       u0_r = A.u[3 * k];
@@ -711,6 +712,7 @@ __global__ __launch_bounds__(256) void k_bwd2(Args2<T> B) {
   const int b = min(A.row_ptr[t], A.cap), e = min(A.row_ptr[t + 1], A.cap);
   for (int k = b + EPW * G.sub + G.es; k < e; k += EPW * S) {
     const int s = A.src[k];
+    TMD_DCHECK(s >= 0 && s < A.n);
     const T Ce = A.C[k];
     const T u0 = A.u[3 * k], u1 = A.u[3 * k + 1], u2 = A.u[3 * k + 2];
     const T ggC = B.ggC[k];
@@ -876,6 +878,7 @@ __device__ __forceinline__ void nb_edges(const NbArgs<T>& A, int row, F&& body) 
   for (int base = b; base < e; base += TMD_WAVE) {
     const int cnt = min(TMD_WAVE, e - base);
     const int s_l = lane < cnt ? A.src[base + lane] : -1;
+    TMD_DCHECK(lane >= cnt || (s_l >= 0 && s_l < A.n));
     const T c_l = lane < cnt ? A.C[base + lane] : T(0);
     for (int q = 0; q < cnt; q += NB_U) {
       int sq[NB_U];

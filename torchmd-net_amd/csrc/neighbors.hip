@@ -463,6 +463,7 @@ __global__ void k_nl_backward2(int n, const int* __restrict__ row_ptr, const int
     const V3<T> gt3{gg[3 * t + 0], gg[3 * t + 1], gg[3 * t + 2]};
     for (int k = b + lane; k < e; k += kNlLanes) {
       const int s = src[k];
+      TMD_DCHECK(s >= 0 && s < n);
       const V3<T> w{gg[3 * s + 0] - gt3.x, gg[3 * s + 1] - gt3.y, gg[3 * s + 2] - gt3.z};
       T uw;
       const V3<T> dm = edge_grad2(k, w, gr, dl, r, uw);
@@ -475,6 +476,7 @@ __global__ void k_nl_backward2(int n, const int* __restrict__ row_ptr, const int
       }
       if (dgr) dgr[k] = uw;
       const int k2 = tr[k];
+      TMD_DCHECK(k2 >= -1 && k2 < cap);
       if (k2 >= 0) {
         T uw2;
         const V3<T> dp = edge_grad2(k2, V3<T>{-w.x, -w.y, -w.z}, gr, dl, r, uw2);

@@ -113,6 +113,7 @@ __global__ __launch_bounds__(256) void k_embed_fwd(Args<T> A) {
   const int b = min(A.row_ptr[n], A.cap), e = min(A.row_ptr[n + 1], A.cap);
   for (int k = b; k < e; ++k) {
     const int m = A.src[k];
+    TMD_DCHECK(m >= 0 && m < A.n);
     const T mult = (m == n && n == 0) ? mult0_of(A) : T(1);
     const T zc = (Pn + A.Q[(size_t)m * A.H + hc]) * A.C[k] * mult;
     const T* wr = A.W + (size_t)k * A.ldw;
@@ -149,6 +150,7 @@ __global__ __launch_bounds__(256) void k_embed_bwd_dst(Args<T> A) {
   const int b = min(A.row_ptr[n], A.cap), e = min(A.row_ptr[n + 1], A.cap);
   for (int k = b; k < e; ++k) {
     const int m = A.src[k];
+    TMD_DCHECK(m >= 0 && m < A.n);
     const T mult = (m == n && n == 0) ? mult0_of(A) : T(1);
     const T Ck = A.C[k];
     const T ux = -A.u[3 * k], uy = -A.u[3 * k + 1], uz = -A.u[3 * k + 2];
@@ -216,6 +218,7 @@ __global__ __launch_bounds__(256) void k_embed_bwd_src(Args<T> A) {
   const int b = min(A.row_ptr[m], A.cap), e = min(A.row_ptr[m + 1], A.cap);
   for (int k = b; k < e; ++k) {
     const int n = A.src[k];  // row edge n->m; its reverse m->n contributed Q[m] to E[n]
+    TMD_DCHECK(n >= 0 && n < A.n);
     const T mult = (m == n && n == 0) ? mult0_of(A) : T(1);
     T g[9];
     ldc(g, A.gE + (size_t)n * A.H + hc, A.nh);
@@ -248,6 +251,7 @@ __global__ __launch_bounds__(256) void k_msg_fwd(Args<T> A) {
   const int b = min(A.row_ptr[n], A.cap), e = min(A.row_ptr[n + 1], A.cap);
   for (int k = b; k < e; ++k) {
     const int m = A.src[k];
+    TMD_DCHECK(m >= 0 && m < A.n);
     const T mult = (m == n && n == 0) ? mult0_of(A) : T(1);
     const T* er = A.ea + (size_t)k * A.ldea + 3 * hc;
     const T f0 = er[0] * mult, f1 = er[1] * mult, f2 = er[2] * mult;
@@ -273,6 +277,7 @@ __global__ __launch_bounds__(256) void k_msg_bwd_dst(Args<T> A) {
   const int b = min(A.row_ptr[n], A.cap), e = min(A.row_ptr[n + 1], A.cap);
   for (int k = b; k < e; ++k) {
     const int m = A.src[k];
+    TMD_DCHECK(m >= 0 && m < A.n);
     const T mult = (m == n && n == 0) ? mult0_of(A) : T(1);
     T t[9];
     ldc(t, A.Tc + (size_t)m * A.H + hc, A.nh);
@@ -300,6 +305,7 @@ __global__ __launch_bounds__(256) void k_msg_bwd_src(Args<T> A) {
   const int b = min(A.row_ptr[m], A.cap), e = min(A.row_ptr[m + 1], A.cap);
   for (int k = b; k < e; ++k) {
     const int n = A.src[k];
+    TMD_DCHECK(n >= 0 && n < A.n);
     const T mult = (m == n && n == 0) ? mult0_of(A) : T(1);
     const T* er = A.ea + (size_t)k * A.ldea + 3 * hc;
     const T f0 = er[0] * mult, f1 = er[1] * mult, f2 = er[2] * mult;

@@ -10,7 +10,9 @@ import os
 
 import torch
 
-_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libtmdnet_hip.so")
+# TMDNET_LIB=debug selects the build with the CSR kernels' index-range checks (`make debug`)
+_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib",
+                         "libtmdnet_hip_debug.so" if os.environ.get("TMDNET_LIB") == "debug" else "libtmdnet_hip.so")
 
 F32, F64 = 0, 1
 NL_BRUTE, NL_SHARED, NL_CELL = 0, 1, 2

@@ -215,7 +215,10 @@ class _NeighborGeomBwd(Function):
 def nl_backward_composite(pos, gd, gr, deltas, distances, src, dst):
     """Differentiable restatement of tmdnet_nl_backward (reference neighbors_cuda.cu:43-71):
     g = gd + delta/r*gr (0 where r == 0); dpos = index_add(src, g) - index_add(dst, g)."""
-    s, d = src.long().clamp(min=0), dst.long().clamp(min=0)  # padding slots have r == 0 (masked)
+    # padding slots (-1) have r == 0 and are masked; the upper clamp keeps any out-of-range slot
+    # (there is none by the build's contract, tests/test_gpu_capture.py) from becoming a fault
+    n = pos.shape[0]
+    s, d = src.long().clamp(0, n - 1), dst.long().clamp(0, n - 1)
     shift = (deltas - (pos.index_select(0, s) - pos.index_select(0, d))).detach()
     dl = pos.index_select(0, s) - pos.index_select(0, d) + shift
     zero = distances == 0
@@ -230,8 +233,9 @@ def nl_backward_composite(pos, gd, gr, deltas, distances, src, dst):
 def nl_backward2_composite(pos, ggpos, gr, deltas, distances, src, dst):
     """Differentiable restatement of tmdnet_nl_backward2: (d_pos, d_gd, d_gr) = the gradient of
     <ggpos, nl_backward_composite(pos, gd, gr, ...)> w.r.t. (pos, gd, gr)."""
-    s, d = src.long().clamp(min=0), dst.long().clamp(min=0)
-    live = ((distances != 0) & (src >= 0)).to(pos.dtype).unsqueeze(1)
+    n = pos.shape[0]
+    s, d = src.long().clamp(0, n - 1), dst.long().clamp(0, n - 1)
+    live = ((distances != 0) & (src >= 0) & (src < n) & (dst >= 0) & (dst < n)).to(pos.dtype).unsqueeze(1)
     shift = (deltas - (pos.index_select(0, s) - pos.index_select(0, d))).detach()
     dl = pos.index_select(0, s) - pos.index_select(0, d) + shift
     r = torch.where(distances == 0, torch.ones_like(distances), (dl * dl).sum(1)).sqrt()

@@ -2,49 +2,95 @@
 
 Reference: LNNP.step (torchmdnet/module.py:130-179: energy / force MSE, weighted), optimizer_step
 linear LR warm-up (module.py:181-193), AdamW (module.py:40-59), DDP over NCCL
-(scripts/train.py:175-189).
+(scripts/train.py:175-189; DDP broadcasts rank 0's parameters and buffers when it wraps the model).
 
-MI355X design: one process per GPU (torchrun), RCCL ("nccl" backend) over xGMI.  The gradients of
-ET-QM9-128 are 7.5 MB, ET-SPICE 4.9 MB: ONE flat all-reduce per step (a single ring pass bounded by
-one 153 GB/s xGMI link is ~50 us) instead of DDP's bucket hooks, which at this size only add launch
-overhead.  Gradients are flattened into a persistent buffer (no per-step allocation).
+MI355X design: one process per GPU (torchrun or ``bench.py --gpus N``), RCCL ("nccl" backend) over
+xGMI.  The gradients of ET-QM9-128 are 7.5 MB, ET-SPICE 4.9 MB: ONE flat all-reduce per step (a
+single ring pass bounded by one 153 GB/s xGMI link is ~50 us) instead of DDP's bucket hooks, which
+at this size only add launches.  Every parameter's ``.grad`` IS a view of that flat buffer, so
+autograd accumulates straight into it and the all-reduce needs no copies in or out.  AdamW is the
+fused multi-tensor kernel; its ``found_inf`` input skips a step on the device (no host sync) when a
+static-capacity neighbour list overflowed on any rank.
 """
 import torch
 import torch.distributed as dist
 import torch.nn.functional as F
 
 
+def _world(group=None):
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_world_size(group)
+    return 1
+
+
+def broadcast_parameters(module, src=0, group=None):
+    """Copy rank ``src``'s parameters and floating buffers to every rank (what DDP does when it wraps
+    the model, so replicas start identical whatever their seeds).  One flat broadcast."""
+    if _world(group) == 1:
+        return
+    ts = [t for t in list(module.parameters()) + list(module.buffers()) if t.is_floating_point()]
+    if not ts:
+        return
+    with torch.no_grad():
+        by_dtype = {}
+        for t in ts:
+            by_dtype.setdefault(t.dtype, []).append(t)
+        for dtype in sorted(by_dtype, key=str):
+            group_ts = by_dtype[dtype]
+            flat = torch.cat([t.detach().reshape(-1) for t in group_ts])
+            dist.broadcast(flat, src, group=group)
+            off = 0
+            for t in group_ts:
+                n = t.numel()
+                t.copy_(flat[off:off + n].view_as(t))
+                off += n
+
+
 class GradAllReduce:
-    """Fused average of all parameter gradients across the process group (one RCCL call)."""
+    """Fused average of all parameter gradients across the process group (one RCCL call).
+
+    ``flat`` holds every gradient plus one trailing slot, the step-skip flag (> 0 after the sum when
+    any rank flagged its step).  ``p.grad`` of every parameter is bound to its view of ``flat``:
+    backward accumulates in place, ``__call__`` all-reduces the buffer itself.  A ``.grad`` that is
+    not the view (set to None by ``zero_grad``, or replaced by a caller) is copied in and rebound."""
 
     def __init__(self, params, group=None):
         self.params = [p for p in params if p.requires_grad]
         self.group = group
         n = sum(p.numel() for p in self.params)
         dev = self.params[0].device
-        self.flat = torch.zeros(n, dtype=self.params[0].dtype, device=dev)
+        self.flat = torch.zeros(n + 1, dtype=self.params[0].dtype, device=dev)
+        self.views = []
+        off = 0
+        for p in self.params:
+            self.views.append(self.flat[off:off + p.numel()].view_as(p))
+            off += p.numel()
+        self.flag = self.flat[n:]
+        self.bind()
+
+    def bind(self):
+        """Make every ``p.grad`` the flat buffer's view (keeping the current gradient values)."""
+        with torch.no_grad():
+            for p, v in zip(self.params, self.views):
+                g = p.grad
+                if g is None:
+                    v.zero_()
+                elif g.data_ptr() != v.data_ptr():
+                    v.copy_(g)
+                p.grad = v
 
     def __call__(self):
-        if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(self.group) == 1:
+        if _world(self.group) == 1:
             return
-        off = 0
-        views = []
-        for p in self.params:
-            n = p.numel()
-            v = self.flat[off:off + n]
-            if p.grad is None:
-                v.zero_()
-            else:
-                v.copy_(p.grad.reshape(-1))
-            views.append(v)
-            off += n
+        self.bind()
         dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=self.group)
-        self.flat.div_(dist.get_world_size(self.group))
-        for p, v in zip(self.params, views):
-            if p.grad is None:
-                p.grad = v.view_as(p).clone()
-            else:
-                p.grad.copy_(v.view_as(p))
+        self.flat.div_(_world(self.group))
+
+
+def _adamw(params, lr, weight_decay):
+    dev = params[0].device
+    # the fused multi-tensor AdamW (one launch per dtype group; honours found_inf on the device)
+    return torch.optim.AdamW(params, lr=lr, weight_decay=weight_decay, fused=dev.type == "cuda")
 
 
 class LNNPStep:
@@ -57,14 +103,17 @@ class LNNPStep:
         self.neg_dy_weight = neg_dy_weight
         self.lr = lr
         self.lr_warmup_steps = lr_warmup_steps
-        self.opt = torch.optim.AdamW(model.parameters(), lr=lr, weight_decay=weight_decay)
+        broadcast_parameters(model, 0, group)
         self.reduce = GradAllReduce(model.parameters(), group)
+        self.opt = _adamw(self.reduce.params, lr, weight_decay)
         self.global_step = 0
 
     def loss(self, z, pos, batch, y, neg_dy):
         pred, pred_neg_dy = self.model(z, pos, batch)
         loss = 0.0
         if self.y_weight > 0:
+            if y.ndim == 1:  # reference module.py:147-148
+                y = y.unsqueeze(1)
             loss = loss + self.y_weight * F.mse_loss(pred, y)
         if self.neg_dy_weight > 0 and pred_neg_dy is not None:
             loss = loss + self.neg_dy_weight * F.mse_loss(pred_neg_dy, neg_dy)
@@ -76,15 +125,18 @@ class LNNPStep:
         # capture the positions' AccumulateGrad would run across streams
         loss.backward(inputs=self.reduce.params)
 
-    def step(self, z, pos, batch, y, neg_dy):
-        self.opt.zero_grad(set_to_none=False)
-        loss = self.loss(z, pos, batch, y, neg_dy)
-        self.backward(loss)
-        self.reduce()
+    def _warmup_lr(self):
         if self.lr_warmup_steps and self.global_step < self.lr_warmup_steps:
             scale = min(1.0, float(self.global_step + 1) / float(self.lr_warmup_steps))
             for g in self.opt.param_groups:
                 g["lr"] = scale * self.lr
+
+    def step(self, z, pos, batch, y, neg_dy):
+        self.opt.zero_grad(set_to_none=False)  # zeroes the flat buffer's views in place
+        loss = self.loss(z, pos, batch, y, neg_dy)
+        self.backward(loss)
+        self.reduce()
+        self._warmup_lr()
         self.opt.step()
         self.global_step += 1
         return loss.detach()
@@ -94,10 +146,13 @@ class GraphedTrainStep(LNNPStep):
     """LNNPStep with the forward, the force pass and the whole (double) backward captured in ONE
     HIP graph for a fixed batch layout (same z / batch / label shapes every step, e.g. a padded or
     fixed-size loader).  Per step: copy the inputs in, replay, then the fused RCCL all-reduce and
-    AdamW run eagerly (the collective stays outside the graph).  The neighbour list runs in its
-    static-capacity mode (capacity = margin x the warm-up pair count, device overflow flag checked by
-    ``check_capacity``); the molecule count of ``reduce`` is frozen from warm-up as in inference
-    capture (reference output_modules.py:27-43).  Replaces ~3k autograd-issued launches per step.
+    the fused AdamW run eagerly (the collective stays outside the graph).  The neighbour list runs in
+    its static-capacity mode (capacity = margin x the warm-up pair count); the molecule count of
+    ``reduce`` is frozen from warm-up as in inference capture (reference output_modules.py:27-43).
+    The graph writes the parameter gradients straight into the all-reduce buffer (one multi-tensor
+    copy) and raises the buffer's skip flag when the pair count exceeded the capacity; the flag is
+    summed over ranks with the gradients and AdamW skips the step on the device when it is set
+    (weights untouched; ``skipped_steps`` counts them, ``check_capacity`` raises).
 
     Drop every reference to an earlier loss / autograd graph of this model before constructing it:
     a live graph keeps the parameters' AccumulateGrad nodes (bound to the stream they were created
@@ -137,37 +192,59 @@ class GraphedTrainStep(LNNPStep):
         torch.cuda.current_stream(dev).wait_stream(s)
         torch.cuda.synchronize(dev)
         # the parameter gradients are graph OUTPUTS (autograd.grad, as make_graphed_callables does):
-        # no AccumulateGrad node runs inside the capture; after each replay .grad points at them
+        # no AccumulateGrad node runs inside the capture; the graph copies them into the flat buffer
         self.opt.zero_grad(set_to_none=True)
         params = self.reduce.params
+        self.reduce.flat.zero_()
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
             self.static_loss = self.loss(self.z, self.pos, self.batch, self.y, self.neg_dy)
             grads = torch.autograd.grad(self.static_loss, params, allow_unused=True)
+            pairs = [(v, g) for v, g in zip(self.reduce.views, grads) if g is not None]
+            torch._foreach_copy_([v for v, _ in pairs], [g for _, g in pairs])
+            ov = rep.distance.last_overflow
+            self.reduce.flag.copy_(ov.num.reshape(1) > ov.capacity)
         torch.cuda.synchronize(dev)
-        self.static_grads = [torch.zeros_like(p) if g is None else g for p, g in zip(params, grads)]
+        del grads, pairs
+        self.reduce.bind()
         self.overflow = rep.distance.last_overflow
+        self.found_inf = torch.zeros((), dtype=torch.float32, device=dev)
+        self.skip_count = torch.zeros((), dtype=torch.float32, device=dev)
+        self.opt.found_inf = self.found_inf
+        self.opt.grad_scale = None
 
     def step(self, z=None, pos=None, batch=None, y=None, neg_dy=None):
         with torch.no_grad():
-            for dst, src in ((self.pos, pos), (self.y, y), (self.neg_dy, neg_dy)):
-                if src is not None:
-                    dst.copy_(src)
+            for name, dst, src in (("z", self.z, z), ("pos", self.pos, pos), ("batch", self.batch, batch),
+                                   ("y", self.y, y), ("neg_dy", self.neg_dy, neg_dy)):
+                if src is None:
+                    continue
+                if name == "y" and src.ndim == 1:
+                    src = src.unsqueeze(1)
+                if src.shape != dst.shape:
+                    raise ValueError(f"GraphedTrainStep: {name} has shape {tuple(src.shape)}, the captured "
+                                     f"layout is {tuple(dst.shape)}")
+                dst.copy_(src)
         self.graph.replay()
-        for p, g in zip(self.reduce.params, self.static_grads):
-            p.grad = g
         self.reduce()
-        if self.lr_warmup_steps and self.global_step < self.lr_warmup_steps:
-            scale = min(1.0, float(self.global_step + 1) / float(self.lr_warmup_steps))
-            for g in self.opt.param_groups:
-                g["lr"] = scale * self.lr
+        # skip flag (> 0 on any rank) -> AdamW's found_inf (exactly 1.0 or 0.0)
+        self.found_inf.copy_(self.reduce.flag[0].sign())
+        self.skip_count.add_(self.found_inf)
+        self._warmup_lr()
         self.opt.step()
         self.global_step += 1
         return self.static_loss.detach()
 
+    @property
+    def skipped_steps(self):
+        return int(self.skip_count.item())
+
     def check_capacity(self):
-        if bool(self.overflow.item()):
-            raise RuntimeError(f"neighbour pairs exceed the captured edge capacity {self.edge_capacity}")
+        """Raises (host sync) if a replay's neighbour list exceeded the captured capacity: the
+        latest step, or any earlier one (whose AdamW update was skipped)."""
+        if bool(self.overflow.item()) or self.skipped_steps:
+            raise RuntimeError(f"neighbour pairs exceed the captured edge capacity {self.edge_capacity} "
+                               f"({self.skipped_steps} optimizer steps skipped)")
 
     def release(self):
         for d in self.dists:
