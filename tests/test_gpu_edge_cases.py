@@ -127,6 +127,8 @@ def test_gated_eq_gradients_isolated_atom():
     z = torch.tensor([1, 1, 8], device=DEV)
     pos = torch.tensor([[0, 0, 0], [0, 1, 0], [10, 0, 0]], dtype=torch.float, device=DEV)
     _, forces = model(z, pos)
-    (deriv,) = torch.autograd.grad(forces.sum(), model.representation_model.embedding.weight)
-    assert not deriv.isnan().any()
-    assert deriv.abs().sum() > 0
+    emb = model.representation_model.embedding.weight
+    (deriv,) = torch.autograd.grad(forces.sum(), emb, retain_graph=True)
+    assert not deriv.isnan().any()  # (sum F = 0 by translation invariance: this gradient is 0)
+    (deriv2,) = torch.autograd.grad(forces.pow(2).sum(), emb)  # a force loss that does depend on it
+    assert torch.isfinite(deriv2).all() and deriv2.abs().sum() > 0
