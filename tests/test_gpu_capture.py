@@ -20,7 +20,7 @@ DEV = "cuda"
 def _lib_loaded():
     from torchmdnet import _native
     _native.load()
-    assert "libtmdnet_hip.so" in open("/proc/self/maps").read()
+    assert "libtmdnet_hip" in open("/proc/self/maps").read()  # product or debug build
 
 
 def _ref_neighbors(pos, batch, loop, include_transpose, cutoff, box):

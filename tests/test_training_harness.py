@@ -220,7 +220,7 @@ def _fit_worker(rank, world, port, out):
     shard = list(iter(dm.loader("train").sampler))
     hist = M_.fit(lnnp, dm, epochs=2, device="cpu")
     flat = torch.cat([p.detach().reshape(-1) for p in lnnp.model.parameters()])
-    out.put((rank, shard, flat, hist[-1]["val_total_mse_loss"]))
+    out.put((rank, shard, flat.numpy(), hist[-1]["val_total_mse_loss"]))
     dist.destroy_process_group()
 
 
@@ -238,5 +238,5 @@ def test_fit_data_parallel_gloo():
         assert p.exitcode == 0
     (s0, w0, v0), (s1, w1, v1) = res[0], res[1]
     assert not set(s0) & set(s1) and len(set(s0) | set(s1)) == 12  # disjoint shards covering the split
-    assert torch.allclose(w0, w1, atol=1e-6)  # averaged gradients keep the replicas identical
+    assert abs(w0 - w1).max() <= 1e-6  # averaged gradients keep the replicas identical
     assert abs(v0 - v1) < 1e-9  # epoch metrics are rank-averaged
