@@ -11,7 +11,18 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Iinclude -I$(PKG)/csrc 
 DBGLIB   := $(LIBDIR)/libtmdnet_hip_debug.so
 DBGOBJS  := $(patsubst $(PKG)/csrc/%.hip,build/hip_dbg/%.o,$(SRCS))
 
-all: $(LIB) oracle
+# the PyTorch dispatcher boundary (TORCH_LIBRARY ops over the C ABI): host C++, g++ + torch headers
+TORCH_DIR := $(shell python3 -c "import os, torch; print(os.path.dirname(torch.__file__))" 2>/dev/null)
+TLIB     := $(LIBDIR)/libtmdnet_torch.so
+TFLAGS   := -O2 -std=c++17 -fPIC -shared -D__HIP_PLATFORM_AMD__=1 -DUSE_ROCM=1 -Iinclude \
+            -I$(TORCH_DIR)/include -I$(TORCH_DIR)/include/torch/csrc/api/include -I/opt/rocm/include
+TLIBS    := -L$(TORCH_DIR)/lib -L$(LIBDIR) -ltorch -ltorch_cpu -lc10 -lc10_hip -ltorch_hip -ltmdnet_hip \
+            -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,$(TORCH_DIR)/lib
+
+all: $(LIB) $(TLIB) oracle
+
+$(TLIB): $(PKG)/csrc/torch_ops.cpp include/tmdnet.h $(LIB)
+	g++ $(TFLAGS) $< -o $@ $(TLIBS)
 
 # index-range checks in the CSR kernels (TMD_DCHECK); load with TMDNET_LIB=debug
 debug: $(DBGLIB)
@@ -36,7 +47,7 @@ oracle:
 	$(MAKE) -C oracle
 
 clean:
-	rm -rf build $(LIB) $(DBGLIB)
+	rm -rf build $(LIB) $(DBGLIB) $(TLIB)
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle clean debug

@@ -75,6 +75,15 @@ int tmdnet_nl_backward(int dtype, int n_atoms, const int32_t* row_ptr, const int
                        int max_pairs, const void* grad_deltas, const void* grad_distances,
                        const void* deltas, const void* distances, void* grad_pos, void* stream);
 
+/* The same backward for ANY list the op returns (half lists with include_transpose=0, capacity-
+ * truncated lists, padding slots -1): one lane per slot of neighbors [2][max_pairs], g scattered to
+ * both ends with atomics, exactly the reference's index_add_ pair (neighbors_cuda.cu:58-68; so,
+ * like it, the fp summation order is not fixed).  grad_pos [n_atoms][3] is zeroed, then
+ * accumulated.  Used by the raw torchmdnet_neighbors::get_neighbor_pairs op (libtmdnet_torch.so). */
+int tmdnet_nl_backward_edges(int dtype, int n_atoms, const int32_t* neighbors, int max_pairs,
+                             const void* grad_deltas, const void* grad_distances, const void* deltas,
+                             const void* distances, void* grad_pos, void* stream);
+
 /* Second order of tmdnet_nl_backward (the double backward the reference gets by differentiating
  * NeighborAutograd::backward's index_add pair, neighbors_cuda.cu:43-71).  gg_pos [n][3] is the
  * cotangent of grad_pos.  Per edge e = (src -> dst) with w = gg[src]-gg[dst], u = delta/r:

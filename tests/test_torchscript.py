@@ -1,0 +1,238 @@
+"""TorchScript / dispatcher boundary (GPU): ``libtmdnet_torch.so`` registers the reference's
+``torchmdnet_neighbors::get_neighbor_pairs`` and the ``tmdnet::*`` model-path operators with
+TORCH_LIBRARY, so ``torch.jit.script`` sees them.
+
+Ports of reference tests/test_neighbors.py:470-546 (test_jit_script_compatible) and
+tests/test_model.py:42-84 (test_torchscript / test_torchscript_dynamic_shapes: energy, forces and a
+second derivative of the scripted model), plus: scripted == eager model (fp32 1e-4 relative, the
+north_star bar; fp64 against the oracle 1e-9), force-matching parameter gradients through the
+scripted model, a jit.save / jit.load round trip, and the raw op's backward against the reference's
+index_add expression to the second order (gradcheck / gradgradcheck in fp64).
+"""
+import io
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import yaml_args
+from oracle import model_oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _rel(a, b):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-12))
+
+
+def _torch_lib_loaded():
+    from torchmdnet import _native
+    _native.load_torch_ops()
+    maps = open("/proc/self/maps").read()
+    assert "libtmdnet_torch.so" in maps and "libtmdnet_hip" in maps
+
+
+# ----------------------------------------------------------------------------- raw neighbour op
+GRID = [(s, nb, loop, tr, bt) for s in ("brute", "shared", "cell") for nb in (1, 128) for loop in (True, False)
+        for tr in (True, False) for bt in (None, "triclinic", "rectangular")
+        if not (bt == "triclinic" and s == "cell")]
+
+
+@pytest.mark.parametrize("strategy,n_batches,loop,include_transpose,box_type", GRID)
+def test_jit_script_compatible(strategy, n_batches, loop, include_transpose, box_type):
+    """Reference test_neighbors.py:470-530: a scripted OptimizedDistance returns the reference pairs."""
+    from torchmdnet.models.utils import OptimizedDistance
+    _torch_lib_loaded()
+    torch.manual_seed(4321)
+    n_per = torch.randint(3, 100, size=(n_batches,))
+    batch = torch.repeat_interleave(torch.arange(n_batches, dtype=torch.int64), n_per).to(DEV)
+    lbox, cutoff = 10.0, 1.0
+    pos = torch.rand(int(n_per.sum()), 3, device=DEV) * lbox
+    pos[0, :] = 0.0
+    pos[1, :] = 0.0
+    pos.requires_grad_(True)
+    box = None if box_type is None else torch.tensor([[lbox, 0.0, 0.0], [0.0, lbox, 0.0], [0.0, 0.0, lbox]]).to(DEV)
+    rnb, rdl, rd = O.neighbors(pos.detach().cpu().double().numpy(), batch.cpu().numpy(), 0.0, cutoff, loop=loop,
+                               include_transpose=include_transpose,
+                               box=None if box is None else box.cpu().double().numpy(), sq_compare=True)
+    rnb, rdl, rd = O.sort_pairs(rnb, rdl, rd)
+    nl = torch.jit.script(OptimizedDistance(cutoff_lower=0.0, loop=loop, cutoff_upper=cutoff,
+                                            max_num_pairs=rnb.shape[1], strategy=strategy, box=box,
+                                            return_vecs=True, include_transpose=include_transpose))
+    neighbors, distances, vecs = nl(pos, batch)
+    nb, dl, d = O.sort_pairs(neighbors.cpu().numpy(), vecs.detach().cpu().numpy(), distances.detach().cpu().numpy())
+    assert nb.shape == rnb.shape
+    assert np.array_equal(nb, rnb)
+    assert np.allclose(d, rd, atol=1e-5) and np.allclose(dl, rdl, atol=1e-5)
+
+
+def _ref_backward(nb, dl, dist, gd, gr, n):
+    """The reference's NeighborAutograd::backward (neighbors_cuda.cu:43-71) in plain torch."""
+    zero = dist == 0
+    g = gd.masked_fill(zero.unsqueeze(-1), 0) + dl / dist.masked_fill(zero, 1).unsqueeze(-1) * \
+        gr.masked_fill(zero, 0).unsqueeze(-1)
+    ei = nb.long().masked_fill(zero.unsqueeze(0), n)
+    ei = ei.masked_fill(ei < 0, n)
+    out = torch.zeros((n + 1, 3), dtype=dl.dtype, device=dl.device)
+    return out.index_add(0, ei[0], g).index_add(0, ei[1], -g)[:n]
+
+
+@pytest.mark.parametrize("include_transpose", [True, False])
+def test_raw_op_backward_matches_reference_expression(include_transpose):
+    from torchmdnet.neighbors import get_neighbor_pairs_kernel as op
+    _torch_lib_loaded()
+    torch.manual_seed(7)
+    n = 300
+    pos = (torch.rand(n, 3, device=DEV, dtype=torch.float64) * 6).requires_grad_(True)
+    batch = torch.zeros(n, dtype=torch.long, device=DEV)
+    nb, dl, d, num = op("brute", pos, batch, torch.empty(0, 0), False, 0.0, 2.0, 40000, True, include_transpose)
+    assert int(num) < 40000
+    gd = torch.randn_like(dl)
+    gr = torch.randn_like(d)
+    gpos, = torch.autograd.grad([dl, d], [pos], [gd, gr])
+    ref = _ref_backward(nb, dl.detach(), d.detach(), gd, gr, n)
+    assert _rel(gpos, ref) < 1e-12
+
+
+def test_raw_op_gradgradcheck():
+    """Second (and first) order of the raw op, fp64 finite differences (the reference differentiates
+    its index_add backward by autograd; here the backward is a HIP kernel whose own backward is
+    written out)."""
+    from torchmdnet.neighbors import get_neighbor_pairs_kernel as op
+    _torch_lib_loaded()
+    torch.manual_seed(11)
+    n = 24
+    pos = (torch.rand(n, 3, device=DEV, dtype=torch.float64) * 3).requires_grad_(True)
+    batch = torch.zeros(n, dtype=torch.long, device=DEV)
+    box = torch.empty(0, 0)
+
+    def f(p):
+        nb, dl, d, num = op("brute", p, batch, box, False, 0.0, 1.5, 1000, True, True)
+        return dl, d
+
+    # the first-order kernel accumulates with atomics (as the reference's index_add_): fp64 sums in a
+    # varying order, hence a round-off-sized reentrancy tolerance
+    assert torch.autograd.gradcheck(f, (pos,), eps=1e-6, atol=1e-7, nondet_tol=1e-12)
+    assert torch.autograd.gradgradcheck(f, (pos,), eps=1e-6, atol=1e-7, nondet_tol=1e-12)
+
+
+# ----------------------------------------------------------------------------- scripted model
+def _et_model(channels=128, layers=8, prior=None, dtype=torch.float32):
+    from torchmdnet.models.model import create_model
+    args = yaml_args("equivariant-transformer")
+    if prior:
+        args.update(prior_args={"max_z": 100})
+    args.update(prior_model=prior, embedding_dimension=channels, num_layers=layers, derivative=True,
+                precision=64 if dtype == torch.float64 else 32)
+    torch.manual_seed(0)
+    return create_model(args), args
+
+
+def _batch(n_mol=8, dtype=torch.float32, seed=3):
+    z, pos, batch = O.qm9_like(n_mol, seed)
+    return z.to(DEV), pos.to(dtype).to(DEV), batch.to(DEV)
+
+
+def test_torchscript_et_matches_eager_fp32():
+    _torch_lib_loaded()
+    model, _ = _et_model()
+    model = model.to(DEV)
+    scripted = torch.jit.script(model)
+    z, pos, batch = _batch()
+    y_e, f_e = model(z, pos.clone(), batch)
+    y_s, f_s = scripted(z, pos.clone(), batch)
+    assert _rel(y_s, y_e) < 1e-4
+    assert _rel(f_s, f_e) < 1e-4
+
+
+def test_torchscript_et_fp64_matches_oracle():
+    _torch_lib_loaded()
+    model, args = _et_model(channels=64, layers=3, dtype=torch.float64)
+    z, pos, batch = O.qm9_like(4, 5)
+    y_ref, f_ref = O.energy_forces(model.state_dict(), dict(args), z, pos, batch)
+    scripted = torch.jit.script(model.to(DEV))
+    y, f = scripted(z.to(DEV), pos.to(DEV), batch.to(DEV))
+    assert _rel(y, y_ref) < 1e-9
+    assert _rel(f, f_ref) < 1e-9
+
+
+def test_torchscript_second_derivative():
+    """Reference test_model.py:42-62: d(neg_dy)/d pos through the scripted model, against eager."""
+    _torch_lib_loaded()
+    model, _ = _et_model(channels=64, layers=3)
+    model = model.to(DEV)
+    scripted = torch.jit.script(model)
+    z, pos, batch = _batch(4)
+    outs = []
+    for m in (model, scripted):
+        p = pos.clone().requires_grad_(True)
+        y, neg_dy = m(z, p, batch)
+        ddy, = torch.autograd.grad([neg_dy], [p], grad_outputs=[torch.ones_like(neg_dy)])
+        outs.append(ddy)
+    assert _rel(outs[1], outs[0]) < 1e-4
+
+
+def test_torchscript_dynamic_shapes():
+    """Reference test_model.py:64-84: one scripted model, five different batch layouts."""
+    _torch_lib_loaded()
+    model, _ = _et_model(channels=64, layers=3)
+    scripted = torch.jit.script(model.to(DEV))
+    z, pos, batch = O.qm9_like(3, 9)
+    for rep in range(5):
+        zi = z.repeat_interleave(rep + 1).to(DEV)
+        pi = pos.float().repeat_interleave(rep + 1, dim=0).to(DEV)
+        pi = pi + 0.05 * torch.randn_like(pi)
+        bi = torch.randint(0, 10, (zi.shape[0],)).sort()[0].to(DEV)
+        pi.requires_grad_(True)
+        y, neg_dy = scripted(zi, pi, bi)
+        ddy, = torch.autograd.grad([neg_dy], [pi], grad_outputs=[torch.ones_like(neg_dy)])
+        assert torch.isfinite(y).all() and torch.isfinite(neg_dy).all() and torch.isfinite(ddy).all()
+        y_e, f_e = model(zi, pi.detach().clone(), bi)
+        assert _rel(y, y_e) < 1e-4 and _rel(neg_dy, f_e) < 1e-4
+
+
+def test_torchscript_force_matching_gradients():
+    """Training through the scripted model (energy + force loss, parameter gradients by double
+    backward) equals the eager model's."""
+    _torch_lib_loaded()
+    model, _ = _et_model(channels=64, layers=2, prior="Atomref")
+    with torch.no_grad():  # non-zero per-element offsets
+        model.prior_model[0].atomref.weight.uniform_(-1, 1)
+    model = model.to(DEV)
+    scripted = torch.jit.script(model)
+    z, pos, batch = _batch(6)
+    torch.manual_seed(1)
+    y_t = torch.randn(6, 1, device=DEV)
+    f_t = torch.randn_like(pos)
+    grads = []
+    for m in (model, scripted):
+        params = [p for p in m.parameters() if p.requires_grad]
+        y, neg_dy = m(z, pos.clone(), batch)
+        loss = ((y - y_t) ** 2).mean() + ((neg_dy - f_t) ** 2).mean()
+        grads.append(torch.autograd.grad(loss, params, allow_unused=True))
+    n_checked = 0
+    for ge, gs in zip(*grads):
+        if ge is None:
+            assert gs is None or gs.abs().max() == 0
+            continue
+        assert _rel(gs, ge) < 2e-4
+        n_checked += 1
+    assert n_checked > 20
+
+
+def test_torchscript_save_load_roundtrip():
+    _torch_lib_loaded()
+    model, _ = _et_model(channels=64, layers=2)
+    scripted = torch.jit.script(model.to(DEV))
+    buf = io.BytesIO()
+    torch.jit.save(scripted, buf)
+    buf.seek(0)
+    loaded = torch.jit.load(buf, map_location=DEV)
+    z, pos, batch = _batch(4)
+    y0, f0 = scripted(z, pos.clone(), batch)
+    y1, f1 = loaded(z, pos.clone(), batch)
+    assert torch.equal(y0, y1) and torch.equal(f0, f1)
+    assert set(loaded.state_dict()) == set(model.state_dict())

@@ -744,3 +744,54 @@ extern "C" int tmdnet_nl_backward2(int dtype, int n_atoms, const int32_t* row_pt
     return kUnsupported;
   return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
 }
+
+// ---------------------------------------------------------------- backward over a plain edge list
+// The raw op's backward (reference NeighborAutograd::backward, neighbors_cuda.cu:43-71) for any list
+// the op returns -- half lists (include_transpose=0) and capacity-truncated ones included, where the
+// CSR pass above does not apply: one lane per edge slot, g = gdelta + delta/r*gr (0 for r == 0 and
+// padding), scattered to both ends with atomics (the reference's index_add_ pair).
+namespace tmd {
+namespace nl {
+template <typename T>
+__global__ void k_nl_backward_edges(int n, const int32_t* __restrict__ nb, int cap, const T* __restrict__ gd,
+                                    const T* __restrict__ gr, const T* __restrict__ dl,
+                                    const T* __restrict__ r, T* __restrict__ gpos) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= cap) return;
+  const int s = nb[e], t = nb[cap + e];
+  if (s < 0 || t < 0 || s >= n || t >= n) return;
+  const V3<T> g = edge_grad(e, gd, gr, dl, r);
+  if (g.x == T(0) && g.y == T(0) && g.z == T(0)) return;
+  atomicAdd(gpos + 3 * s + 0, g.x);
+  atomicAdd(gpos + 3 * s + 1, g.y);
+  atomicAdd(gpos + 3 * s + 2, g.z);
+  atomicAdd(gpos + 3 * t + 0, -g.x);
+  atomicAdd(gpos + 3 * t + 1, -g.y);
+  atomicAdd(gpos + 3 * t + 2, -g.z);
+}
+}  // namespace nl
+}  // namespace tmd
+
+extern "C" int tmdnet_nl_backward_edges(int dtype, int n_atoms, const int32_t* neighbors, int max_pairs,
+                                        const void* grad_deltas, const void* grad_distances,
+                                        const void* deltas, const void* distances, void* grad_pos,
+                                        void* stream) {
+  if (n_atoms <= 0 || max_pairs < 0 || !neighbors || !grad_pos) return kBadArgument;
+  hipStream_t st = (hipStream_t)stream;
+  const size_t es = dtype == TMDNET_F64 ? 8 : 4;
+  TMD_CHECK(hipMemsetAsync(grad_pos, 0, es * 3 * (size_t)n_atoms, st));
+  if (max_pairs == 0) return kOk;
+  const int tb = 256;
+  dim3 g((unsigned)((max_pairs + tb - 1) / tb));
+  if (dtype == TMDNET_F32)
+    hipLaunchKernelGGL(nl::k_nl_backward_edges<float>, g, dim3(tb), 0, st, n_atoms, neighbors, max_pairs,
+                       (const float*)grad_deltas, (const float*)grad_distances, (const float*)deltas,
+                       (const float*)distances, (float*)grad_pos);
+  else if (dtype == TMDNET_F64)
+    hipLaunchKernelGGL(nl::k_nl_backward_edges<double>, g, dim3(tb), 0, st, n_atoms, neighbors, max_pairs,
+                       (const double*)grad_deltas, (const double*)grad_distances, (const double*)deltas,
+                       (const double*)distances, (double*)grad_pos);
+  else
+    return kUnsupported;
+  return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
+}

@@ -35,6 +35,7 @@ SIGNATURES = {
     "tmdnet_nl_build_paired": (I, [I, I, P, P, I, P, I, D, D, I, I, I, P, P, P, P, P, P, I, P, SZ, P, P, I, P]),
     "tmdnet_nl_backward": (I, [I, I, P, P, I, P, P, P, P, P, P]),
     "tmdnet_nl_backward2": (I, [I, I, P, P, P, I, P, P, P, P, P, P, P, P]),
+    "tmdnet_nl_backward_edges": (I, [I, I, P, I, P, P, P, P, P, P]),
     "tmdnet_edge_geom_fwd": (I, [I, I, I, I, P, P, P, P, P, P, D, D, P, P, P, P]),
     "tmdnet_edge_geom_fwd_rows": (I, [I, I, I, I, P, P, P, P, P, P, D, D, P, P, P, P, I, P, P]),
     "tmdnet_edge_geom_bwd": (I, [I, I, I, I, P, P, P, P, P, P, D, D, P, P, P, P, P, P]),
@@ -71,6 +72,21 @@ SIGNATURES = {
 }
 
 _lib = None
+_torch_ops_loaded = False
+_TORCH_OPS_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libtmdnet_torch.so")
+
+
+def load_torch_ops():
+    """Register the dispatcher operators of ``lib/libtmdnet_torch.so`` (csrc/torch_ops.cpp):
+    ``torchmdnet_neighbors::get_neighbor_pairs`` (the reference schema) and the ``tmdnet::*`` ops of
+    the TorchScript model path.  Raises if the library is absent (no fallback)."""
+    global _torch_ops_loaded
+    if _torch_ops_loaded:
+        return
+    if not os.path.exists(_TORCH_OPS_PATH):
+        raise RuntimeError(f"torchmd-net_amd: operator library not found at {_TORCH_OPS_PATH}; run `make`")
+    torch.ops.load_library(_TORCH_OPS_PATH)
+    _torch_ops_loaded = True
 
 
 def library_path():

@@ -157,6 +157,8 @@ class TorchMD_Net(nn.Module):
         batch = torch.zeros_like(z) if batch is None else batch
         if self.derivative:
             pos.requires_grad_(True)
+        if torch.jit.is_scripting():
+            return self._forward_script(z, pos, batch, q, s, extra_args)
         x, v, z, pos, batch = self.representation_model(z, pos, batch, q=q, s=s)
         x = self.output_model.pre_reduce(x, v, z, pos, batch)
         fused = None
@@ -185,4 +187,31 @@ class TorchMD_Net(nn.Module):
             if neg_dy is None:
                 raise RuntimeError("Autograd returned None for the force prediction.")
             return y, neg_dy
+        return y, None
+
+    def _forward_script(self, z: Tensor, pos: Tensor, batch: Tensor, q: Optional[Tensor], s: Optional[Tensor],
+                        extra_args: Optional[Dict[str, Tensor]]) -> Tuple[Tensor, Optional[Tensor]]:
+        """TorchScript body: reference model.py:252-300 line for line (the representation model's
+        scripted path runs the HIP operators of libtmdnet_torch.so)."""
+        x, v, z, pos, batch = self.representation_model(z, pos, batch, q=q, s=s)
+        x = self.output_model.pre_reduce(x, v, z, pos, batch)
+        if self.std is not None:
+            x = x * self.std
+        prior_model = self.prior_model
+        if prior_model is not None:
+            for prior in prior_model:
+                x = prior.pre_reduce(x, z, pos, batch, extra_args)
+        x = self.output_model.reduce(x, batch)
+        if self.mean is not None:
+            x = x + self.mean
+        y = self.output_model.post_reduce(x)
+        if prior_model is not None:
+            for prior in prior_model:
+                y = prior.post_reduce(y, z, pos, batch, extra_args)
+        if self.derivative:
+            grad_outputs: List[Optional[torch.Tensor]] = [torch.ones_like(y)]
+            dy = grad([y], [pos], grad_outputs=grad_outputs, create_graph=True, retain_graph=True)[0]
+            if dy is None:
+                raise RuntimeError("Autograd returned None for the force prediction.")
+            return y, -dy
         return y, None

@@ -54,6 +54,14 @@ class OutputModel(nn.Module, metaclass=ABCMeta):
         return self.dim_size
 
     def reduce(self, x, batch):
+        if torch.jit.is_scripting():  # reference output_modules.py:27-43 (scatter sum / mean)
+            dim_size = int(batch.max().item()) + 1
+            out = torch.zeros([dim_size] + x.shape[1:], dtype=x.dtype, device=x.device).index_add(0, batch, x)
+            if self.reduce_op == "mean":
+                cnt = torch.zeros(dim_size, dtype=x.dtype, device=x.device).index_add(
+                    0, batch, torch.ones(batch.shape[0], dtype=x.dtype, device=x.device))
+                out = out / cnt.clamp(min=1).view([dim_size] + [1] * (x.dim() - 1))
+            return out
         return scatter(x, batch, dim=0, dim_size=self._dim_size(x, batch), reduce=self.reduce_op)
 
     def fused_reduce(self, x, batch, std, mean):
@@ -91,6 +99,8 @@ class Scalar(OutputModel):
         self.output_network[2].bias.data.fill_(0)
 
     def pre_reduce(self, x, v: Optional[torch.Tensor], z, pos, batch):
+        if torch.jit.is_scripting():
+            return self.output_network(x)
         net = self.output_network
         return net[2](kernels.fused_act(net[1], net[0](x)))
 
@@ -111,6 +121,10 @@ class EquivariantScalar(OutputModel):
             layer.reset_parameters()
 
     def pre_reduce(self, x, v, z, pos, batch):
+        if torch.jit.is_scripting():  # reference output_modules.py:98-103
+            for layer in self.output_network:
+                x, v = layer(x, v)
+            return x + v.sum() * 0
         if x.is_cuda and type(self) is EquivariantScalar and kernels.eq_head_fusable(self.output_network):
             # both gated blocks + the per-atom Jacobian in one HIP kernel (csrc/eq_head.hip); the
             # reference's "+ 0 * v.sum()" only keeps v in the autograd graph and adds nothing

@@ -85,8 +85,16 @@ class TorchMD_ET(nn.Module):
             attn.reset_parameters()
         self.out_norm.reset_parameters()
 
+    def __prepare_scriptable__(self):
+        for attn in self.attention_layers:
+            attn._check_supported()
+        return self
+
     def forward(self, z: Tensor, pos: Tensor, batch: Tensor, q: Optional[Tensor] = None,
                 s: Optional[Tensor] = None) -> Tuple[Tensor, Tensor, Tensor, Tensor, Tensor]:
+        if torch.jit.is_scripting():
+            x, vec = self._forward_script(z, pos, batch)
+            return x, vec, z, pos, batch
         perm = None
         if self.reorder_atoms and z.shape[0] >= kernels.REORDER_MIN_ATOMS:
             # large systems: compute in a spatially coherent atom numbering (edge-kernel locality);
@@ -99,6 +107,35 @@ class TorchMD_ET(nn.Module):
             return x[inv], vec[inv], z, pos, batch
         x, vec = self._forward(z, pos, batch)
         return x, vec, z, pos, batch
+
+    def _forward_script(self, z: Tensor, pos: Tensor, batch: Tensor) -> Tuple[Tensor, Tensor]:
+        """TorchScript path (torch.jit.script(model)): the reference layer loop
+        (torchmd_et.py:160-190) over the dispatcher operators of libtmdnet_torch.so -- neighbour
+        list, edge geometry, neighbour embedding and the ET message are the HIP kernels with C++
+        autograd (differentiable twice: forces and force-matching training); the node projections are
+        ATen GEMMs."""
+        x = self.embedding(z)
+        d = self.distance
+        row_ptr, src, dst, tr, deltas, dist, num_pairs = torch.ops.tmdnet.neighbor_graph(
+            pos, batch, d.box, d.use_periodic, float(d.cutoff_lower), float(d.cutoff_upper),
+            d._max_pairs(pos.shape[0]), d.loop, d.strategy, d.check_errors, -1)
+        de = self.distance_expansion
+        mu, beta = de.kernel_params()
+        trainable = self.trainable_rbf and torch.is_grad_enabled()
+        f, C, u = torch.ops.tmdnet.edge_geometry(deltas, dist, src, dst, mu, beta, float(self.cutoff_lower),
+                                                 float(self.cutoff_upper), de.rbf_type, not trainable)
+        if trainable:  # trainable basis: differentiable ATen features (the parameters need gradients)
+            f = de(dist)
+        ne = self.neighbor_embedding
+        if ne is not None:
+            x = ne.script_forward(z, x, row_ptr, src, dst, f, C)
+        vec = torch.zeros(x.size(0), 3, x.size(1), device=x.device, dtype=x.dtype)
+        for attn in self.attention_layers:
+            dx, dvec = attn.script_forward(x, vec, row_ptr, src, dst, f, C, u)
+            x = x + dx
+            vec = vec + dvec
+        x = self.out_norm(x)
+        return x, vec
 
     def _forward(self, z: Tensor, pos: Tensor, batch: Tensor):
         x = self.embedding(z)
@@ -206,7 +243,30 @@ class EquivariantMultiHeadAttention(nn.Module):
             raise NotImplementedError("torchmd-net_amd: the fused ET edge kernel implements SiLU for "
                                       "activation and attn_activation (the reference default)")
 
-    def forward(self, x, vec, edge_index, r_ij, f_ij, d_ij):
+    def script_forward(self, x: Tensor, vec: Tensor, row_ptr: Tensor, src: Tensor, dst: Tensor, f_ij: Tensor,
+                       C: Tensor, d_ij: Tensor) -> Tuple[Tensor, Tensor]:
+        """TorchScript path: reference torchmd_et.py:293-321 with message + aggregate as
+        ``tmdnet::et_message`` (HIP, C++ autograd)."""
+        x = self.layernorm(x)
+        q = self.q_proj(x)
+        k = self.k_proj(x)
+        v = self.v_proj(x)
+        vec1, vec2, vec3 = torch.split(self.vec_proj(vec), self.hidden_channels, dim=-1)
+        vec_dot = (vec1 * vec2).sum(dim=1)
+        pk: Optional[Tensor] = None
+        pv: Optional[Tensor] = None
+        if self.dk_proj is not None:
+            pk = self.dk_proj(f_ij)
+        if self.dv_proj is not None:
+            pv = self.dv_proj(f_ij)
+        xa, veca = torch.ops.tmdnet.et_message(q, k, v, vec, pk, pv, C, d_ij, row_ptr, src, dst, self.num_heads)
+        o1, o2, o3 = torch.split(self.o_proj(xa), self.hidden_channels, dim=1)
+        return vec_dot * o2 + o3, vec3 * o1.unsqueeze(1) + veca
+
+    def forward(self, x: Tensor, vec: Tensor, edge_index: Tensor, r_ij: Tensor, f_ij: Tensor,
+                d_ij: Tensor) -> Tuple[Tensor, Tensor]:
+        if torch.jit.is_scripting():
+            raise RuntimeError("scripted EquivariantMultiHeadAttention: use script_forward (CSR graph)")
         self._check_supported()
         graph, perm = as_graph(edge_index, x.shape[0])
         if perm is not None:

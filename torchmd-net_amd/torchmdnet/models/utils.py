@@ -30,6 +30,8 @@ class CosineCutoff(nn.Module):
         self.cutoff_upper = cutoff_upper
 
     def forward(self, distances: Tensor) -> Tensor:
+        if torch.jit.is_scripting():
+            return _cos_cut(distances, float(self.cutoff_lower), float(self.cutoff_upper))
         nat.require_gpu(distances, "CosineCutoff")
         return _rbf_cutoff_only(distances, self.cutoff_lower, self.cutoff_upper)
 
@@ -71,6 +73,7 @@ class GaussianSmearing(nn.Module):
             self.register_buffer("offset", offset)
 
     rbf_type = nat.RBF_GAUSS
+    __constants__ = ["rbf_type"]
 
     def _initial_params(self):
         offset = torch.linspace(self.cutoff_lower, self.cutoff_upper, self.num_rbf, dtype=self.dtype)
@@ -85,7 +88,10 @@ class GaussianSmearing(nn.Module):
     def kernel_params(self):
         return self.offset, self.coeff.reshape(1).expand(self.num_rbf).contiguous()
 
-    def forward(self, dist):
+    def forward(self, dist: Tensor) -> Tensor:
+        if torch.jit.is_scripting():  # reference utils.py:298-300
+            d = dist.unsqueeze(-1) - self.offset
+            return torch.exp(self.coeff * torch.pow(d, 2))
         nat.require_gpu(dist, "GaussianSmearing")
         if self.trainable and torch.is_grad_enabled():
             d = dist.unsqueeze(-1) - self.offset
@@ -97,6 +103,7 @@ class ExpNormalSmearing(nn.Module):
     """Reference utils.py:303-344 (PhysNet expnorm basis)."""
 
     rbf_type = nat.RBF_EXPNORM
+    __constants__ = ["rbf_type"]
 
     def __init__(self, cutoff_lower=0.0, cutoff_upper=5.0, num_rbf=50, trainable=True, dtype=torch.float32):
         super().__init__()
@@ -129,7 +136,11 @@ class ExpNormalSmearing(nn.Module):
     def kernel_params(self):
         return self.means, self.betas
 
-    def forward(self, dist):
+    def forward(self, dist: Tensor) -> Tensor:
+        if torch.jit.is_scripting():  # reference utils.py:339-344
+            d = dist.unsqueeze(-1)
+            return _cos_cut(d, 0.0, float(self.cutoff_upper)) * torch.exp(
+                -self.betas * (torch.exp(self.alpha * (-d + self.cutoff_lower)) - self.means) ** 2)
         nat.require_gpu(dist, "ExpNormalSmearing")
         if self.trainable and torch.is_grad_enabled():
             d = dist.unsqueeze(-1)
@@ -138,8 +149,12 @@ class ExpNormalSmearing(nn.Module):
         return _rbf_only(self, dist)
 
 
-def _cos_cut(r, cl, cu):
-    return kernels._cosine_cutoff_torch(r, cl, cu)
+def _cos_cut(r: Tensor, cl: float, cu: float) -> Tensor:
+    """CosineCutoff in ATen ops (reference utils.py:368-390)."""
+    if cl > 0:
+        c = 0.5 * (torch.cos(math.pi * (2 * (r - cl) / (cu - cl) + 1.0)) + 1.0)
+        return c * (r < cu).to(r.dtype) * (r > cl).to(r.dtype)
+    return 0.5 * (torch.cos(r * math.pi / cu) + 1.0) * (r < cu).to(r.dtype)
 
 
 def _rbf_only(module, dist):
@@ -200,7 +215,7 @@ class OptimizedDistance(torch.nn.Module):
         # graph(): number the edge pairs in the build itself (the ET consumer sets it; sorted rows)
         self.pair_rows = False
 
-    def _max_pairs(self, n):
+    def _max_pairs(self, n: int) -> int:
         return -self.max_num_pairs * n if self.max_num_pairs < 0 else self.max_num_pairs
 
     def forward(self, pos: Tensor, batch: Optional[Tensor] = None) -> Tuple[Tensor, Tensor, Optional[Tensor]]:
@@ -274,7 +289,17 @@ class NeighborEmbedding(nn.Module):
         self.distance_proj.bias.data.fill_(0)
         self.combine.bias.data.fill_(0)
 
-    def forward(self, z, x, edge_index, edge_weight, edge_attr, cutoff=None):
+    def script_forward(self, z: Tensor, x: Tensor, row_ptr: Tensor, src: Tensor, dst: Tensor, edge_attr: Tensor,
+                       C: Tensor) -> Tensor:
+        """TorchScript path: reference utils.py:90-108 with the aggregation as ``tmdnet::nbr_embed``."""
+        W = self.distance_proj(edge_attr)
+        x_nb = torch.ops.tmdnet.nbr_embed(self.embedding(z), W, C, row_ptr, src, dst)
+        return self.combine(torch.cat([x, x_nb], dim=1))
+
+    def forward(self, z: Tensor, x: Tensor, edge_index: Tensor, edge_weight: Tensor, edge_attr: Tensor,
+                cutoff: Optional[Tensor] = None) -> Tensor:
+        if torch.jit.is_scripting():
+            raise RuntimeError("scripted NeighborEmbedding: use script_forward (CSR graph)")
         graph, perm = as_graph(edge_index, x.shape[0])
         if perm is not None:
             edge_weight, edge_attr = edge_weight[perm], edge_attr[perm]
