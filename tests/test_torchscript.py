@@ -236,3 +236,64 @@ def test_torchscript_save_load_roundtrip():
     y1, f1 = loaded(z, pos.clone(), batch)
     assert torch.equal(y0, y1) and torch.equal(f0, f1)
     assert set(loaded.state_dict()) == set(model.state_dict())
+
+
+# ----------------------------------------------------------------------------- scripted TensorNet
+def _tn_model(group="O(3)", static_shapes=True, dtype=torch.float32):
+    from torchmdnet.models.model import create_model
+    args = yaml_args("tensornet", derivative=True, equivariance_invariance_group=group,
+                     precision=64 if dtype == torch.float64 else 32)
+    torch.manual_seed(0)
+    m = create_model(args)
+    m.representation_model.static_shapes = static_shapes  # (create_model does not take it, as the reference)
+    return m, args
+
+
+@pytest.mark.parametrize("group", ["O(3)", "SO(3)"])
+def test_torchscript_tensornet_matches_eager(group):
+    """Reference test_model.py:42-62 for TensorNet (static_shapes, the reference default): energy,
+    forces and the second derivative of the scripted model equal the eager HIP path."""
+    _torch_lib_loaded()
+    model, _ = _tn_model(group)
+    model = model.to(DEV)
+    scripted = torch.jit.script(model)
+    z, pos, batch = _batch(6)
+    res = []
+    for m in (model, scripted):
+        p = pos.clone().requires_grad_(True)
+        y, neg_dy = m(z, p, batch)
+        ddy, = torch.autograd.grad([neg_dy], [p], grad_outputs=[torch.ones_like(neg_dy)])
+        res.append((y, neg_dy, ddy))
+    for a, b in zip(res[1], res[0]):
+        assert _rel(a, b) < 1e-4
+
+
+@pytest.mark.parametrize("static_shapes", [True, False])
+def test_torchscript_tensornet_fp64_matches_oracle(static_shapes):
+    _torch_lib_loaded()
+    model, args = _tn_model(dtype=torch.float64, static_shapes=static_shapes)
+    z, pos, batch = O.qm9_like(3, 4)
+    y_ref, f_ref = O.energy_forces(model.state_dict(), dict(args), z, pos, batch, static_shapes=static_shapes)
+    scripted = torch.jit.script(model.to(DEV))
+    y, f = scripted(z.to(DEV), pos.to(DEV), batch.to(DEV))
+    assert _rel(y, y_ref) < 1e-9
+    assert _rel(f, f_ref) < 1e-9
+
+
+def test_torchscript_tensornet_force_matching_gradients():
+    _torch_lib_loaded()
+    model, _ = _tn_model("O(3)")
+    model = model.to(DEV)
+    scripted = torch.jit.script(model)
+    z, pos, batch = _batch(4)
+    torch.manual_seed(2)
+    y_t, f_t = torch.randn(4, 1, device=DEV), torch.randn_like(pos)
+    grads = []
+    for m in (model, scripted):
+        params = [p for p in m.parameters() if p.requires_grad]
+        y, neg_dy = m(z, pos.clone(), batch)
+        loss = ((y - y_t) ** 2).mean() + ((neg_dy - f_t) ** 2).mean()
+        grads.append(torch.autograd.grad(loss, params, allow_unused=True))
+    for ge, gs in zip(*grads):
+        if ge is not None:
+            assert _rel(gs, ge) < 2e-4

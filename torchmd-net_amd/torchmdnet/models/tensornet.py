@@ -44,6 +44,39 @@ def tensor_norm(tensor):
     return (tensor ** 2).sum((-2, -1))
 
 
+# ----------------------------------------------------------------------------- TorchScript path
+# Compact-tensor algebra in ATen ops (tn_node.op_composite, written for TorchScript): the scripted
+# model runs the edge work through the tmdnet::tn_embed / tmdnet::tn_message operators (HIP, C++
+# autograd) and this node algebra through ATen.
+def _s_full9(c: Tensor) -> Tensor:
+    i, a01, a02, a12, s00, s11, s01, s02, s12 = c[0], c[1], c[2], c[3], c[4], c[5], c[6], c[7], c[8]
+    F = torch.stack((i + s00, a01 + s01, a02 + s02, s01 - a01, i + s11, a12 + s12,
+                     s02 - a02, s12 - a12, i - s00 - s11), dim=-1)
+    return F.view(F.shape[0], F.shape[1], 3, 3)
+
+
+def _s_decomp9(X: Tensor) -> Tensor:
+    f = X.reshape(X.shape[0], X.shape[1], 9)
+    i = (f[..., 0] + f[..., 4] + f[..., 8]) / 3
+    return torch.stack((i, 0.5 * (f[..., 1] - f[..., 3]), 0.5 * (f[..., 2] - f[..., 6]),
+                        0.5 * (f[..., 5] - f[..., 7]), f[..., 0] - i, f[..., 4] - i,
+                        0.5 * (f[..., 1] + f[..., 3]), 0.5 * (f[..., 2] + f[..., 6]),
+                        0.5 * (f[..., 5] + f[..., 7])), dim=0)
+
+
+def _s_mm33(a: Tensor, b: Tensor) -> Tensor:
+    return (a.unsqueeze(-1) * b.unsqueeze(-3)).sum(-2)
+
+
+def _s_tnorm(t: Tensor) -> Tensor:
+    return (t ** 2).sum((-2, -1))
+
+
+def _s_mix3(c: Tensor, w0: Tensor, w1: Tensor, w2: Tensor) -> Tensor:
+    return torch.cat((torch.matmul(c[0:1], w0.t()), torch.matmul(c[1:4], w1.t()),
+                      torch.matmul(c[4:9], w2.t())), dim=0)
+
+
 class TensorNet(nn.Module):
     def __init__(self, hidden_channels=128, num_layers=2, num_rbf=32, rbf_type="expnorm",
                  trainable_rbf=False, activation="silu", cutoff_lower=0, cutoff_upper=4.5,
@@ -93,6 +126,8 @@ class TensorNet(nn.Module):
 
     def forward(self, z: Tensor, pos: Tensor, batch: Tensor, q: Optional[Tensor] = None,
                 s: Optional[Tensor] = None) -> Tuple[Tensor, Optional[Tensor], Tensor, Tensor, Tensor]:
+        if torch.jit.is_scripting():
+            return self._forward_script(z, pos, batch), None, z, pos, batch
         if self.reorder_atoms and z.shape[0] >= kernels.REORDER_MIN_ATOMS and not self.static_shapes:
             # (static_shapes keeps the caller's numbering: its padding semantics single out atom 0)
             perm = kernels.spatial_permutation(pos, batch, self.cutoff_upper,
@@ -102,6 +137,33 @@ class TensorNet(nn.Module):
             x = self._forward(z[perm], pos.index_select(0, perm), batch[perm])
             return x[inv], None, z, pos, batch
         return self._forward(z, pos, batch), None, z, pos, batch
+
+    def _forward_script(self, z: Tensor, pos: Tensor, batch: Tensor) -> Tensor:
+        """TorchScript path: reference tensornet.py:200-232 over the libtmdnet_torch.so operators."""
+        d = self.distance
+        cap = d._max_pairs(pos.shape[0])
+        row_ptr, src, dst, tr, deltas, dist, num_pairs = torch.ops.tmdnet.neighbor_graph(
+            pos, batch, d.box, d.use_periodic, float(d.cutoff_lower), float(d.cutoff_upper), cap, d.loop,
+            d.strategy, d.check_errors, -1)
+        # static_shapes: the reference's padded slots are (0, 0) edges at r = 0 -- multiplicity of atom 0's
+        # self loop (one host read of the pair count, as the reference's resize_to_fit=False path shapes)
+        m = float(1 + max(0, cap - int(num_pairs.item()))) if self.static_shapes else 1.0
+        de = self.distance_expansion
+        mu, beta = de.kernel_params()
+        trainable = self.trainable_rbf and torch.is_grad_enabled()
+        f, C, u = torch.ops.tmdnet.edge_geometry(deltas, dist, src, dst, mu, beta, float(self.cutoff_lower),
+                                                 float(self.cutoff_upper), de.rbf_type, not trainable)
+        if trainable:
+            f = de(dist)
+        X = self.tensor_embedding.script_forward(z, row_ptr, src, dst, f, C, u, m)
+        for layer in self.layers:
+            X = layer.script_forward(X, row_ptr, src, dst, f, C, m)
+        c = _s_decomp9(X)
+        nI = 3 * c[0] ** 2
+        nA = 2 * (c[1] ** 2 + c[2] ** 2 + c[3] ** 2)
+        nS = c[4] ** 2 + c[5] ** 2 + (c[4] + c[5]) ** 2 + 2 * (c[6] ** 2 + c[7] ** 2 + c[8] ** 2)
+        x = self.out_norm(torch.cat((nI, nA, nS), dim=-1))
+        return self.act(self.linear(x))
 
     def _forward(self, z: Tensor, pos: Tensor, batch: Tensor) -> Tensor:
         graph = self.distance.graph(pos, batch)
@@ -167,8 +229,30 @@ class TensorEmbedding(nn.Module):
             linear.reset_parameters()
         self.init_norm.reset_parameters()
 
-    def forward(self, z: Tensor, edge_index, edge_weight: Tensor, edge_vec_norm: Tensor,
+    def script_forward(self, z: Tensor, row_ptr: Tensor, src: Tensor, dst: Tensor, edge_attr: Tensor, C: Tensor,
+                       u: Tensor, m: float) -> Tensor:
+        """TorchScript path: reference tensornet.py:295-326 (edge aggregation = tmdnet::tn_embed)."""
+        H = self.hidden_channels
+        W = torch.nn.functional.linear(
+            edge_attr, torch.cat([self.distance_proj1.weight, self.distance_proj2.weight, self.distance_proj3.weight]),
+            torch.cat([self.distance_proj1.bias, self.distance_proj2.bias, self.distance_proj3.bias]))
+        Z = self.emb(z)
+        P = torch.nn.functional.linear(Z, self.emb2.weight[:, :H], self.emb2.bias)
+        Q = torch.nn.functional.linear(Z, self.emb2.weight[:, H:])
+        Ec = torch.ops.tmdnet.tn_embed(P, Q, W, C, u, row_ptr, src, dst, m)
+        norm = self.init_norm(_s_tnorm(_s_full9(Ec)))
+        Ec = _s_mix3(Ec, self.linears_tensor[0].weight, self.linears_tensor[1].weight, self.linears_tensor[2].weight)
+        for linear_scalar in self.linears_scalar:
+            norm = self.act(linear_scalar(norm))
+        f = norm.view(norm.shape[0], -1, 3)
+        scale = torch.stack([f[..., 0], f[..., 1], f[..., 1], f[..., 1], f[..., 2], f[..., 2], f[..., 2],
+                             f[..., 2], f[..., 2]], dim=0)
+        return _s_full9(Ec * scale)
+
+    def forward(self, z: Tensor, edge_index: Tensor, edge_weight: Tensor, edge_vec_norm: Tensor,
                 edge_attr: Tensor) -> Tensor:
+        if torch.jit.is_scripting():
+            raise RuntimeError("scripted TensorEmbedding: use script_forward (CSR graph)")
         graph, perm = _check_symmetric_graph(edge_index, z.shape[0])
         if perm is not None:
             edge_weight, edge_vec_norm, edge_attr = edge_weight[perm], edge_vec_norm[perm], edge_attr[perm]
@@ -214,7 +298,28 @@ class Interaction(nn.Module):
         for linear in self.linears_tensor:
             linear.reset_parameters()
 
-    def forward(self, X: Tensor, edge_index, edge_weight: Tensor, edge_attr: Tensor) -> Tensor:
+    def script_forward(self, X: Tensor, row_ptr: Tensor, src: Tensor, dst: Tensor, edge_attr: Tensor, C: Tensor,
+                       m: float) -> Tensor:
+        """TorchScript path: reference tensornet.py:378-410 (message passing = tmdnet::tn_message)."""
+        for linear_scalar in self.linears_scalar:
+            edge_attr = self.act(linear_scalar(edge_attr))
+        edge_attr = edge_attr * C.view(-1, 1)
+        lt = self.linears_tensor
+        Xn = X / (_s_tnorm(X) + 1)[..., None, None]
+        Yc = _s_mix3(_s_decomp9(Xn), lt[0].weight, lt[1].weight, lt[2].weight)
+        msg = torch.ops.tmdnet.tn_message(edge_attr, Yc, row_ptr, src, dst, m)
+        Y, M = _s_full9(Yc), _s_full9(msg)
+        if self.equivariance_invariance_group == "O(3)":
+            Z = _s_mm33(M, Y) + _s_mm33(Y, M)
+        else:
+            Z = 2 * _s_mm33(Y, M)
+        Dc = _s_mix3(_s_decomp9(Z) / (_s_tnorm(Z) + 1), lt[3].weight, lt[4].weight, lt[5].weight)
+        D = _s_full9(Dc)
+        return Xn + D + _s_mm33(D, D)
+
+    def forward(self, X: Tensor, edge_index: Tensor, edge_weight: Tensor, edge_attr: Tensor) -> Tensor:
+        if torch.jit.is_scripting():
+            raise RuntimeError("scripted Interaction: use script_forward (CSR graph)")
         graph, perm = _check_symmetric_graph(edge_index, X.shape[0])
         if perm is not None:
             edge_weight, edge_attr = edge_weight[perm], edge_attr[perm]
