@@ -126,6 +126,9 @@ PAIR_ROWS = True
 # MI355X: C2 1.076 -> 1.063 ms, C4 0.932 -> 0.917 ms, C5 73.9 -> 71.3 ms; the eager training step
 # is within its run-to-run noise (29-35 ms).  TMDNET_DR=0 turns it off.
 DR_MODE = os.environ.get("TMDNET_DR", "auto")
+# second order of the force pass (force-matching training): "hand" = the hand-scheduled adjoint
+# (_second_order), "composite" = autograd over the recomputed stack (the reference for tests / A-B)
+SECOND_ORDER = os.environ.get("TMDNET_ET_SECOND_ORDER", "hand")
 
 _PERMS = {}
 
@@ -323,14 +326,25 @@ def _forward_layers(meta, x, f, C, u, params):
     return x, vec, acts
 
 
-def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws, r=None, dr=False):
+def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws, r=None, dr=False, record=None, inject=None,
+                     seed_pre_norm=False):
     """Hand-scheduled first-order backward.  Returns (g_x, g_f, g_C, g_u, g_r, g_params).
 
     ``dr`` ("dr mode", the force pass: no weight gradients, f = rbf(r)): the projection gradient is
     never materialised.  d pkv / d r = (d f / d r) W^T is formed once per pair row (one GEMM the
     size of the forward projection) and the message backward contracts the per-edge projection
     gradient with it in-kernel, accumulating g_r -- instead of writing the E x (layers * D) gradient
-    and reading it back through the edge-feature GEMM.  g_f is then None."""
+    and reading it back through the edge-feature GEMM.  g_f is then None.
+
+    For the hand-scheduled second order (``_second_order``):
+      * ``record`` (a list): every layer's backward intermediates are kept in fresh buffers and
+        appended as a dict (layer L-1 first): the seeds gX / gV the layer's step receives, g_o,
+        g_vecp, g_xa, g_qkv, g_xn; and ``record`` gets the attribute-like entry {"g_pkv": ...} last;
+      * ``inject`` (dict of per-layer lists): extra cotangents of the forward's intermediates added
+        where the backward forms their gradients -- "o", "vecp", "qkv" (node), "pkv" (edge rows of
+        the layer's projection), "vec" (the layer's vec input), "x" (the layer's x input);
+      * ``seed_pre_norm``: with the fused out_norm, gX is the gradient of the norm's INPUT (skip its
+        backward)."""
     H = meta.H
     N = gX.shape[0]
     graph = meta.graph
@@ -338,6 +352,14 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws, r=None, dr=Fa
     o = dict(dtype=gX.dtype, device=gX.device)
     has_e = meta.hk or meta.hv
     D = meta.D
+    rec = record is not None
+    inj = inject or {}
+    assert not (rec and dr), "recording needs the materialised projection gradient (no dr mode)"
+
+    def injected(key, l):
+        lst = inj.get(key)
+        return None if lst is None else lst[l]
+
     # the kernels accumulate the edge gradients (g_C, g_u, g_r) across layers: one zeroed buffer
     zbuf = torch.zeros(((5 if dr else 4) * E,), **o)
     g_C, g_u = zbuf[:E], zbuf[E:4 * E].view(E, 3)
@@ -349,16 +371,17 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws, r=None, dr=Fa
         dpkv_all = torch.mm(fdp, meta.dkv_eff[0].t()) if meta.batched else None
     # padding rows of a static-capacity list are zeroed by the kernel: no memset needed
     elif has_e:
-        g_pkv_all = torch.empty((E, meta.n_layers * D if meta.batched else D), **o)
+        g_pkv_all = torch.empty((E, meta.n_layers * D if (meta.batched or rec) else D), **o)
     g_f = None
-    g_qkv = torch.empty((N, 5 * H), **o)
-    g_o = torch.empty((N, 3 * H), **o)
-    g_vecp = torch.empty((N, 3, 3 * H), **o)
-    gvec_bufs = [torch.empty((N, 3, H), **o), torch.empty((N, 3, H), **o)]
+    new = lambda shape: torch.empty(shape, **o)  # noqa: E731
+    g_qkv = new((N, 5 * H))
+    g_o = new((N, 3 * H))
+    g_vecp = new((N, 3, 3 * H))
+    gvec_bufs = [new((N, 3, H)), new((N, 3, H))]
     layers = meta.split(params)
     g_params = [None] * len(params)
     epi_done = False  # this layer's epilogue backward already ran (fused into the next layer's LN bwd)
-    if meta.out_norm:  # gX is the gradient of LN(x_out): back through out_norm first
+    if meta.out_norm and not seed_pre_norm:  # gX is the gradient of LN(x_out): back through out_norm first
         x_pre, mean_o, rstd_o = acts[meta.n_layers]
         last = acts[meta.n_layers - 1]
         if need_ws[meta.n_layers]:
@@ -381,11 +404,17 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws, r=None, dr=Fa
             dpk = dpkv[:, :H] if meta.hk else None
             dpv = dpkv[:, H * int(meta.hk):] if meta.hv else None
         elif has_e:
-            g_pkv = g_pkv_all[:, l * D:(l + 1) * D] if meta.batched else g_pkv_all
+            g_pkv = g_pkv_all[:, l * D:(l + 1) * D] if (meta.batched or rec) else g_pkv_all
             gpk = g_pkv[:, :H] if meta.hk else None
             gpv = g_pkv[:, H * int(meta.hk):] if meta.hv else None
+        if rec:
+            step = {"gX": gX, "gV": gV}
         if not epi_done:
             _epilogue_bwd(gX, gV, vecp, o_, g_vecp, g_o)
+        if injected("o", l) is not None:
+            g_o.add_(injected("o", l))
+            if vecp is not None:
+                g_vecp.add_(injected("vecp", l))
         g_xa = torch.empty((N, H), **o)
         kernels.gemm_group([(g_o, o_w, False, None, g_xa, False)])
         pk = pkv[:, :H] if meta.hk else None
@@ -396,7 +425,13 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws, r=None, dr=Fa
             g_qkv[:, :H], g_qkv[:, H:2 * H], g_qkv[:, 2 * H:], g_vec_in, gpk, gpv, g_C, g_u,
             accumulate=nat.ACC_VEC_RESIDUAL | nat.ACC_EDGE | meta.flags, pk_rows=meta.pk_rows,
             dpk=dpk, dpv=dpv, g_r=g_r)
-        if has_e and not meta.batched and not dr:
+        if injected("qkv", l) is not None:
+            g_qkv.add_(injected("qkv", l))
+        if has_e and not dr and injected("pkv", l) is not None:
+            g_pkv.add_(injected("pkv", l))
+        if g_vec_in is not None and injected("vec", l) is not None:
+            g_vec_in.add_(injected("vec", l))
+        if has_e and not (meta.batched or rec) and not dr:
             if g_f is None:
                 g_f = torch.mm(g_pkv, dkv_w)
             else:
@@ -407,15 +442,21 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws, r=None, dr=Fa
         if vec is not None:
             probs.append((g_vecp.view(3 * N, 3 * H), vec_w, False, None, g_vec_in.view(3 * N, H), True))
         kernels.gemm_group(probs)
+        if rec:
+            step.update(g_o=g_o, g_vecp=g_vecp if vec is not None else None, g_xa=g_xa, g_qkv=g_qkv, g_xn=g_xn)
+            record.append(step)
+            g_qkv, g_o, g_vecp = new((N, 5 * H)), new((N, 3 * H)), new((N, 3, 3 * H))
+            gvec_bufs = [new((N, 3, H)), new((N, 3, H))]
         need_w = need_ws[l]
+        g_res = gX if injected("x", l) is None else gX + injected("x", l)
         if need_w:  # LayerNorm weight gradients: PyTorch's backward
             g_x, g_lnw, g_lnb = torch.ops.aten.native_layer_norm_backward(g_xn, x, [H], mean, rstd, ln_w, ln_b,
                                                                  [True, True, True])
-            g_x.add_(gX)
+            g_x.add_(g_res)
             epi_done = False
         else:  # LayerNorm backward + residual + the previous layer's epilogue backward, one kernel
             prev = acts[l - 1] if l > 0 else None
-            g_x = _ln_bwd_epi(g_xn, x, mean, rstd, ln_w, gX, g_vec_in,
+            g_x = _ln_bwd_epi(g_xn, x, mean, rstd, ln_w, g_res, g_vec_in,
                               prev[6] if prev else None, prev[9] if prev else None, g_vecp, g_o)
             epi_done = prev is not None
         if need_w:
@@ -430,7 +471,7 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws, r=None, dr=Fa
                   (torch.mm(g_vecp.view(3 * N, 3 * H).t(), vec.view(3 * N, H)) if vec is not None
                    else torch.zeros((3 * H, H), **o)),
                   torch.mm(g_o.t(), xa), g_o.sum(0)]
-            if has_e and not meta.batched:
+            if has_e and not (meta.batched or rec):
                 g_w, g_b = torch.mm(g_pkv.t(), f), g_pkv.sum(0)
                 if meta.planar:
                     oinv = meta.perms[5]
@@ -439,8 +480,10 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws, r=None, dr=Fa
             g_params[base:base + len(gp)] = gp  # batched mode: dk/dv grads filled after the loop
         gX = g_x
         gV = g_vec_in
-    if has_e and meta.batched and not dr:  # every layer's edge-feature / projection gradients in one GEMM each
+    if has_e and (meta.batched or rec) and not dr:  # every layer's edge-feature / projection gradients in one GEMM each
         g_f = torch.mm(g_pkv_all, meta.dkv_eff[0])
+        if rec:
+            record.append({"g_pkv": g_pkv_all})
         if any(need_ws[:meta.n_layers]):
             g_w_all = torch.mm(g_pkv_all.t(), f)
             g_b_all = g_pkv_all.sum(0)
@@ -454,6 +497,218 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws, r=None, dr=Fa
                     gl = _dkv_param_grads(meta, g_w_all[a:b], g_b_all[a:b])
                     g_params[base:base + len(gl)] = gl
     return gX, g_f, g_C, g_u, g_r, g_params
+
+
+def ln_adjoint(gbar, x, mean, rstd, w, g_y):
+    """VJP of the LayerNorm backward g_x = LNB(g_y, x) = rstd (a - mean(a) - xh mean(a xh)), a = g_y w
+    (no residual) for the cotangent ``gbar`` of g_x.  Returns (gbar_gy, x_bar, w_bar):
+      gbar_gy = w J0 gbar (J0 v = rstd (v - mean v - xh mean(v xh)), the LayerNorm Jacobian without w);
+      x_bar   = -S rstd^2 xh / H - rstd/H ((a.xh) J0 gbar + (gbar.xh) J0 a),
+                S = gbar.a - (sum gbar)(sum a)/H - (gbar.xh)(a.xh)/H   (row-wise sums);
+      w_bar   = sum over rows of g_y * J0 gbar."""
+    H = x.shape[1]
+    xh = (x - mean) * rstd
+
+    def J0(v):
+        return rstd * (v - v.mean(1, keepdim=True) - xh * (v * xh).mean(1, keepdim=True))
+
+    a = g_y * w
+    Jg = J0(gbar)
+    axh = (a * xh).sum(1, keepdim=True)
+    gxh = (gbar * xh).sum(1, keepdim=True)
+    S = (gbar * a).sum(1, keepdim=True) - gbar.sum(1, keepdim=True) * a.sum(1, keepdim=True) / H - gxh * axh / H
+    x_bar = -S * rstd * rstd * xh / H - (rstd / H) * (axh * Jg + gxh * J0(a))
+    return w * Jg, x_bar, (g_y * Jg).sum(0)
+
+
+def epi_adjoint(gb_o, gb_vecp, gX, gV, vecp, o):
+    """VJP of the epilogue backward (tmdnet_et_epilogue_bwd: g_o1 = sum_a gV v3, g_o2 = gX (v1.v2),
+    g_o3 = gX, g_v1 = gX o2 v2, g_v2 = gX o2 v1, g_v3 = gV o1) for the cotangents gb_o [N, 3H],
+    gb_vecp [N, 3, 3H] of its outputs.  Returns (gbar_gX, gbar_gV, vecp_bar, o_bar); vecp None (the
+    first layer: vec = 0): only gbar_gX = gb_o3 is non-zero."""
+    H = gX.shape[1]
+    if vecp is None:
+        return gb_o[:, 2 * H:], None, None, torch.zeros_like(o)
+    o1, o2 = o[:, :H], o[:, H:2 * H]
+    v1, v2, v3 = vecp[..., :H], vecp[..., H:2 * H], vecp[..., 2 * H:]
+    b1, b2, b3 = gb_o[:, :H], gb_o[:, H:2 * H], gb_o[:, 2 * H:]
+    c1, c2, c3 = gb_vecp[..., :H], gb_vecp[..., H:2 * H], gb_vecp[..., 2 * H:]
+    cross = (c1 * v2 + c2 * v1).sum(1)
+    gbar_gX = b2 * (v1 * v2).sum(1) + b3 + o2 * cross
+    gbar_gV = b1.unsqueeze(1) * v3 + c3 * o1.unsqueeze(1)
+    gxo2 = (gX * o2).unsqueeze(1)
+    bgx = (b2 * gX).unsqueeze(1)
+    vecp_bar = torch.cat((bgx * v2 + c2 * gxo2, bgx * v1 + c1 * gxo2, b1.unsqueeze(1) * gV), dim=-1)
+    o_bar = torch.cat(((c3 * gV).sum(1), gX * cross, torch.zeros_like(gX)), dim=1)
+    return gbar_gX, gbar_gV, vecp_bar, o_bar
+
+
+def hand_second_order_ok(meta, dr, need_w, ggs_params):
+    """The hand-scheduled second order covers the force-pass node (no weight gradients in its
+    outputs) in the reference row layout; otherwise the composite recompute runs."""
+    return (not meta.planar and not any(need_w) and all(g is None for g in ggs_params)
+            and (not dr or meta.rbf is not None))
+
+
+def _second_order(ctx, ggs, want):
+    """Hand-scheduled second order of the force pass (the VJP of _backward_layers for the cotangents
+    ``ggs`` of its outputs g_x, g_f, g_C, g_u, g_r), replacing autograd's double differentiation of
+    the recomputed stack (~2.6k small kernels per ET-QM9 training step).  Three passes:
+
+    1. re-run the first-order backward without dr mode, recording every layer's intermediates
+       (seeds, g_o, g_vecp, g_xa, g_qkv, g_xn, the per-edge projection gradient);
+    2. the ADJOINT of that backward, in forward layer order: per layer the LayerNorm-backward VJP
+       (``ln_adjoint``), the two node GEMMs' transposes, the message backward's VJP
+       (tmdnet_et_message_bwd2, HIP), the o-GEMM transpose and the epilogue-backward VJP
+       (``epi_adjoint``).  It yields the cotangents of the seeds gX / gV (returned), of the weights
+       the backward multiplies by, and of every forward intermediate (x, vec, [q|k|v], projection,
+       vecp, o);
+    3. one more first-order backward through the forward layers with those intermediate cotangents
+       injected where the backward forms their gradients (``inject``), giving the gradients of the
+       stack's inputs and weights.
+
+    ``want`` (per saved input gX, gV, x, f, C, u, r, *params): which gradients the engine consumes."""
+    saved = ctx.saved_tensors
+    gX, gV, x, f, C, u, r = saved[:7]
+    params = list(saved[7:])
+    meta = ctx.meta
+    acts = ctx.acts
+    L, H, D = meta.n_layers, meta.H, meta.D
+    N, E = x.shape[0], meta.graph.n_edges
+    graph = meta.graph
+    o = dict(dtype=x.dtype, device=x.device)
+    has_e = bool(meta.hk or meta.hv)
+    gg_x, gg_f, gg_C, gg_u, gg_r = ggs[:5]
+    layers = meta.split(params)
+    need_none = (False,) * (L + int(meta.out_norm))
+    # 1. the force pass again, recorded (its outputs are those of the dr-mode pass up to round-off)
+    rec = []
+    _, g_f0, _, _, _, _ = _backward_layers(meta, gX, gV, f, C, u, params, acts, need_none, record=rec)
+    g_pkv_all = rec.pop()["g_pkv"] if has_e else None
+    rec = rec[::-1]  # layer 0 first
+    W_all = meta.dkv_eff[0]
+    # cotangent of the summed edge-feature gradient g_f = g_pkv_all W_all
+    gb_f = gg_f
+    r_bar = None
+    if ctx.dr and gg_r is not None and has_e:
+        fdp = kernels.rbf_deriv(r, *meta.rbf)
+        gb_r_f = gg_r.unsqueeze(1) * fdp
+        gb_f = gb_r_f if gb_f is None else gb_f + gb_r_f
+        if want[6]:  # d/dr of g_r = <g_f, df/dr>: the RBF's second derivative (composite)
+            with torch.enable_grad():
+                rr = r.detach().requires_grad_(True)
+                fd, = torch.autograd.grad(kernels.rbf_composite(rr, *meta.rbf), rr, g_f0.detach(),
+                                          create_graph=True)
+                r_bar, = torch.autograd.grad(fd, rr, gg_r)
+    gb_pkv_all = torch.mm(gb_f, W_all.t()) if (gb_f is not None and has_e) else None
+    W_bar = {}
+
+    def acc(key, val):
+        W_bar[key] = val if key not in W_bar else W_bar[key] + val
+
+    if gb_f is not None and has_e:
+        acc("dkv", torch.mm(g_pkv_all.t(), gb_f))
+    pr = meta.pairs[0].long() if meta.pairs is not None else None
+    inj = {k: [None] * L for k in ("o", "vecp", "qkv", "pkv", "vec", "x")}
+    C_bar = torch.zeros((E,), **o)
+    u_bar = torch.zeros((E, 3), **o)
+    gbar_x = gg_x if gg_x is not None else torch.zeros((N, H), **o)
+    gbar_v = None
+    ggC = gg_C if gg_C is not None else torch.zeros((E,), **o)
+    ggu = gg_u if gg_u is not None else torch.zeros((E, 3), **o)
+    # 2. the adjoint pass, layer 0 first
+    for l in range(L):
+        p = layers[l]
+        R = rec[l]
+        x_l, vec_l, xn, mean, rstd, qkv, vecp, pkv, xa, o_ = acts[l]
+        ln_w, vec_w, o_w = p[0], p[8], p[9]
+        qkv_w = meta.qkv_eff[l][0]
+        gb_gxn, inj["x"][l], wb_ln = ln_adjoint(gbar_x, x_l, mean, rstd, ln_w, R["g_xn"])
+        acc(("ln", l), wb_ln)
+        gb_gX = gbar_x  # the residual g_x = gX + ...
+        gb_gqkv = torch.mm(gb_gxn, qkv_w.t())
+        acc(("qkv", l), torch.mm(R["g_qkv"].t(), gb_gxn))
+        gb_gvecp = None
+        if vec_l is not None and gbar_v is not None:
+            gb_gvecp = torch.matmul(gbar_v, vec_w.t())
+            acc(("vec", l), torch.mm(R["g_vecp"].reshape(3 * N, 3 * H).t(), gbar_v.reshape(3 * N, H)))
+        gb_gV = gbar_v  # the vec residual g_vec = gV + ...
+        # message backward VJP (per-edge projection rows)
+        pk = pv = None
+        if has_e:
+            pke = pkv if pr is None else pkv.index_select(0, pr)
+            pk = pke[:, :H] if meta.hk else None
+            pv = pke[:, H * int(meta.hk):] if meta.hv else None
+        gbl = gb_pkv_all[:, l * D:(l + 1) * D] if gb_pkv_all is not None else None
+        ggs_m = (gb_gqkv[:, :H], gb_gqkv[:, H:2 * H], gb_gqkv[:, 2 * H:],
+                 gbar_v if vec_l is not None else None,
+                 gbl[:, :H] if (gbl is not None and meta.hk) else None,
+                 gbl[:, H * int(meta.hk):] if (gbl is not None and meta.hv) else None, ggC, ggu)
+        d_gxa, d_gvec, d_q, d_k, d_v, d_vec, d_pk, d_pv, d_C, d_u = kernels.et_message_bwd2_launch(
+            qkv[:, :H], qkv[:, H:2 * H], qkv[:, 2 * H:], vec_l, pk, pv, C, u, graph, meta.heads,
+            R["g_xa"], R["gV"] if R["gV"] is not None else torch.zeros((N, 3, H), **o), ggs_m)
+        inj["qkv"][l] = torch.cat((d_q, d_k, d_v), dim=1)
+        if has_e:
+            inj["pkv"][l] = torch.cat([t for t in (d_pk, d_pv) if t is not None], dim=1)
+        inj["vec"][l] = d_vec
+        C_bar.add_(d_C)
+        u_bar.add_(d_u)
+        gb_gV = d_gvec if gb_gV is None else gb_gV + d_gvec
+        gb_go = torch.mm(d_gxa, o_w.t())
+        acc(("o", l), torch.mm(R["g_o"].t(), d_gxa))
+        if gb_gvecp is None and vecp is not None:
+            gb_gvecp = torch.zeros((N, 3, 3 * H), **o)
+        e_gX, e_gV, inj["vecp"][l], inj["o"][l] = epi_adjoint(gb_go, gb_gvecp, R["gX"], R["gV"], vecp, o_)
+        gbar_x = gb_gX + e_gX
+        gbar_v = gb_gV if e_gV is None else gb_gV + e_gV
+    # the seeds: through the fused out_norm's backward first
+    seed_x = None
+    on_bar = None
+    if meta.out_norm:
+        x_pre, mean_o, rstd_o = acts[L]
+        gb_gXin, seed_x, wb_on = ln_adjoint(gbar_x, x_pre, mean_o, rstd_o, params[-2], gX)
+        on_bar = wb_on
+        gbar_x = gb_gXin
+    # 3. the backward through the forward layers with the injected cotangents
+    need_w = tuple(bool(w) for w in _layer_wants(meta, want[7:]))
+    g_x, g_f, g_C, g_u, _, g_params = _backward_layers(
+        meta, seed_x if seed_x is not None else torch.zeros((N, H), **o), torch.zeros((N, 3, H), **o),
+        f, C, u, params, acts, need_w, inject=inj, seed_pre_norm=meta.out_norm)
+    g_C = g_C + C_bar
+    g_u = g_u + u_bar
+    # weight cotangents of the first pass's products, added to the parameters' gradients
+    g_params = list(g_params)
+
+    def addp(i, val):
+        if val is not None and want[7 + i]:
+            g_params[i] = val if g_params[i] is None else g_params[i] + val
+
+    for l in range(L):
+        base = l * meta.np
+        addp(base, W_bar.get(("ln", l)))
+        wq = W_bar.get(("qkv", l))
+        if wq is not None:
+            addp(base + 2, wq[:H])
+            addp(base + 4, wq[H:2 * H])
+            addp(base + 6, wq[2 * H:])
+        addp(base + 8, W_bar.get(("vec", l)))
+        addp(base + 9, W_bar.get(("o", l)))
+        if "dkv" in W_bar:
+            for j, gw in enumerate(_dkv_param_grads(meta, W_bar["dkv"][l * D:(l + 1) * D],
+                                                   torch.zeros((D,), **o))[0::2]):
+                addp(base + 11 + 2 * j, gw)
+    if on_bar is not None:
+        addp(len(params) - 2, on_bar)
+    res = [gbar_x, gbar_v, g_x, g_f, g_C, g_u, r_bar] + g_params
+    return [t if w else None for t, w in zip(res, want)]
+
+
+def _layer_wants(meta, want_params):
+    """Per-layer (and out_norm) weight-gradient request from the per-parameter ``want`` flags."""
+    out = [any(want_params[l * meta.np:(l + 1) * meta.np]) for l in range(meta.n_layers)]
+    if meta.out_norm:
+        out.append(any(want_params[-2:]))
+    return out
 
 
 def _dkv_param_grads(meta, g_w, g_b):
@@ -574,6 +829,8 @@ class _ETStackBwd(Function):
                                                              r=r, dr=dr)
         ctx.meta = meta
         ctx.dr = dr
+        ctx.acts = acts
+        ctx.need_w = need_w
         ctx.save_for_backward(gX, gV, x, f, C, u, r, *params)
         return (g_x, g_f, g_C, g_u, g_r) + tuple(g_params)
 
@@ -601,6 +858,10 @@ class _ETStackBwd(Function):
         for i, t in enumerate(saved):
             node = next(nf)[0] if t is not None else None
             want.append(t is not None and ctx.needs_input_grad[4 + i] and _will_run(node))
+        if SECOND_ORDER != "composite" and not _create and hand_second_order_ok(meta, ctx.dr, ctx.need_w, ggs[5:]):
+            if not any(want):
+                return (None,) * n_out
+            return (None, None, None, None) + tuple(_second_order(ctx, ggs, want))
         with torch.enable_grad():
             leaves = [None if t is None else t.detach().requires_grad_(True) for t in saved]
             gX, gV, x, f, C, u, r = leaves[:7]

@@ -698,11 +698,12 @@ class _ETMessageBwd(Function):
         return tuple(res) + (None, None)
 
 
-def et_message_bwd2(ctx, ggs):
-    """HIP second-order backward of the ET message (``tmdnet_et_message_bwd2``).  Its own backward
-    (third order) is not implemented."""
-    gx, gvec, q, k, v, vec, pk, pv, C, u = ctx.saved_tensors
-    graph = ctx.graph
+def et_message_bwd2_launch(q, k, v, vec, pk, pv, C, u, graph, heads, gx, gvec, ggs, flags=0):
+    """One ``tmdnet_et_message_bwd2`` launch: the VJP of tmdnet_et_message_bwd (without the vec
+    residual) at primals (q, k, v, vec, pk, pv, C, u) and seeds (gx, gvec), for the cotangents
+    ``ggs`` = (gg_q, gg_k, gg_v, gg_vec, gg_pk, gg_pv, gg_C, gg_u) of its outputs (None / empty =
+    zero).  pk / pv are per-edge rows (no pair indirection).  Returns (d_gx, d_gvec, d_q, d_k, d_v,
+    d_vec, d_pk, d_pv, d_C, d_u); d_vec is None when vec is None, d_pk / d_pv when pk / pv are."""
     lib = nat.load()
     N, H = q.shape
     E = graph.n_edges
@@ -720,22 +721,32 @@ def et_message_bwd2(ctx, ggs):
     ggpv = rows(ggs[5], (E, 3 * H)) if pv is not None else None
     ggC, ggu = dense(ggs[6], (E,)), dense(ggs[7], (E, 3))
     d_gx, d_gvec, d_q = torch.empty((N, H), **o), torch.empty((N, 3, H), **o), torch.empty((N, H), **o)
-    d_k, d_v, d_vec = torch.zeros((N, H), **o), torch.zeros((N, 3 * H), **o), torch.zeros((N, 3, H), **o)
+    d_k, d_v = torch.zeros((N, H), **o), torch.zeros((N, 3 * H), **o)
+    d_vec = torch.zeros((N, 3, H), **o) if vec is not None else None
     # per-edge outputs: every row written (padding rows with zeros by the kernel)
     d_pk = torch.empty((E, H), **o) if pk is not None else None
     d_pv = torch.empty((E, 3 * H), **o) if pv is not None else None
     d_C, d_u = torch.empty((E,), **o), torch.empty((E, 3), **o)
     qc, kc, vc, pkc, pvc = (_rowmajor(t) for t in (q, k, v, pk, pv))  # read in place through ld
+    gxc, gvc = gx.contiguous(), gvec.contiguous()
     rc = lib.tmdnet_et_message_bwd2(
-        nat.dtype_code(q.dtype), N, H, ctx.heads, nat.ptr(graph.row_ptr), nat.ptr(graph.src), E,
+        nat.dtype_code(q.dtype), N, H, heads, nat.ptr(graph.row_ptr), nat.ptr(graph.src), E,
         nat.ptr(qc), _ld(qc), nat.ptr(kc), _ld(kc), nat.ptr(vc), _ld(vc), nat.ptr(vec), nat.ptr(pkc), _ld(pkc),
         nat.ptr(pvc), _ld(pvc),
-        nat.ptr(C), nat.ptr(u), nat.ptr(gx), nat.ptr(gvec), nat.ptr(ggq), nat.ptr(ggk), nat.ptr(ggv),
+        nat.ptr(C), nat.ptr(u), nat.ptr(gxc), nat.ptr(gvc), nat.ptr(ggq), nat.ptr(ggk), nat.ptr(ggv),
         nat.ptr(ggw), nat.ptr(ggpk), _ld(ggpk), nat.ptr(ggpv), _ld(ggpv), nat.ptr(ggC), nat.ptr(ggu), nat.ptr(d_gx),
         nat.ptr(d_gvec), nat.ptr(d_q), nat.ptr(d_k), nat.ptr(d_v), nat.ptr(d_vec), nat.ptr(d_pk),
-        nat.ptr(d_pv), nat.ptr(d_C), nat.ptr(d_u), 0, nat.stream(q.device))
+        nat.ptr(d_pv), nat.ptr(d_C), nat.ptr(d_u), int(flags), nat.stream(q.device))
     nat.check(rc, "tmdnet_et_message_bwd2")
-    return (d_gx, d_gvec, d_q, d_k, d_v, d_vec, d_pk, d_pv, d_C, d_u, None, None)
+    return d_gx, d_gvec, d_q, d_k, d_v, d_vec, d_pk, d_pv, d_C, d_u
+
+
+def et_message_bwd2(ctx, ggs):
+    """HIP second-order backward of the ET message (``tmdnet_et_message_bwd2``).  Its own backward
+    (third order) is not implemented."""
+    gx, gvec, q, k, v, vec, pk, pv, C, u = ctx.saved_tensors
+    out = et_message_bwd2_launch(q, k, v, vec, pk, pv, C, u, ctx.graph, ctx.heads, gx, gvec, ggs)
+    return tuple(out) + (None, None)
 
 
 def et_message(q, k, v, vec, pk, pv, C, u, graph, heads):
