@@ -223,6 +223,23 @@ int tmdnet_ln_bwd_epilogue(int dtype, int n_nodes, int hidden, const void* grad_
                            void* grad_x, const void* grad_vec, const void* vecp, const void* o,
                            void* grad_vecp, void* grad_o, void* stream);
 
+/* Second order of the layer tail (force-matching training, et_stack._second_order): layer l's
+ * epilogue-backward VJP fused with layer l+1's LayerNorm-backward VJP, one wave per node.
+ * Epilogue part (o != NULL): cotangents gb_o [N][3H], gb_vecp [N][3][3H] of tmdnet_et_epilogue_bwd's
+ * outputs at (grad_x, grad_vec, vecp, o) -> gbar_x_out = gbar_x_in + its grad_x cotangent,
+ * gbar_vec_out = gbar_vec_in (NULL = 0) + its grad_vec cotangent, vecp_bar, o_bar (the primal
+ * cotangents); vecp NULL (first layer): only gb_o's third block reaches gbar_x_out.
+ * LayerNorm part (ln_w != NULL): the VJP of g_x = LNB(grad_xn, x) (tmdnet_ln_bwd_epilogue without
+ * residual) for the cotangent gbar_x_out (o NULL: gbar_x_in) -> gbar_grad_xn, x_bar, and the per-row
+ * products w_bar_rows [N][H] whose column sum is ln_w's cotangent.  mean / rstd as saved by the
+ * forward.  Every output written (no accumulation besides the *_in terms). */
+int tmdnet_et_adjoint_epi_ln(int dtype, int n_nodes, int hidden, const void* gb_o, const void* gb_vecp,
+                             const void* grad_x, const void* grad_vec, const void* vecp, const void* o,
+                             const void* gbar_x_in, const void* gbar_vec_in, void* gbar_x_out,
+                             void* gbar_vec_out, void* vecp_bar, void* o_bar, const void* x, const void* mean,
+                             const void* rstd, const void* ln_w, const void* grad_xn, void* gbar_grad_xn,
+                             void* x_bar, void* w_bar_rows, void* stream);
+
 /* ------------------------------------------------------------------------------------------
  * EquivariantScalar output head (reference models/output_modules.py:80-115 with two
  * GatedEquivariantBlocks, models/utils.py:456-522: H -> H/2 with scalar SiLU, then H/2 -> 1;

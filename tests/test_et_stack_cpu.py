@@ -208,6 +208,7 @@ def emulated(monkeypatch):
     monkeypatch.setattr(kernels, "et_message_bwd_launch", _fake_bwd)
     monkeypatch.setattr(kernels, "et_message_bwd2", _fake_bwd2)
     monkeypatch.setattr(kernels, "et_message_bwd2_launch", _fake_bwd2_launch)
+    monkeypatch.setattr(ES, "adjoint_epi_ln_launch", ES.adjoint_epi_ln_composite)
     monkeypatch.setattr(kernels, "rbf_deriv_launch", _fake_rbf_deriv)
     monkeypatch.setattr(ES, "_epilogue_fwd", _fake_epi_fwd)
     monkeypatch.setattr(ES, "_epilogue_bwd", _fake_epi_bwd)

@@ -1,6 +1,6 @@
 """Graph-replayed ET-QM9 energy+force steps (the bench workload) bracketed by marker kernels, for
 rocprofv3 --kernel-trace (tools/trace_summary.py lists the kernels of the marked replay).
-usage: graph_trace.py [et|tn]"""
+usage: graph_trace.py [et|tn|train]   (train: the replay of the captured ET-QM9 training step)"""
 import os
 import sys
 
@@ -16,7 +16,7 @@ from torchmdnet.models.model import create_model  # noqa: E402
 dev = torch.device("cuda", 0)
 torch.manual_seed(0)
 which = sys.argv[1] if len(sys.argv) > 1 else "et"
-if which == "et":
+if which in ("et", "train"):
     model = create_model(et_args(128)).to(dev)
     z, pos, batch = qm9_like(32, 1)
 else:
@@ -27,6 +27,21 @@ else:
     model = create_model(args).to(dev)
     z, pos, batch = rmd17_like(8, 1)
 z, pos, batch = z.to(dev), pos.float().to(dev), batch.to(dev)
+if which == "train":
+    from torchmdnet.training import GraphedTrainStep
+    g = torch.Generator().manual_seed(200)
+    y_lab = torch.randn(32, 1, generator=g).to(dev)
+    f_lab = torch.randn(z.shape[0], 3, generator=g).to(dev)
+    tr = GraphedTrainStep(model, z, pos, batch, y_lab, f_lab, lr=1e-4)
+    for _ in range(3):
+        tr.graph.replay()
+    torch.cuda.synchronize()
+    torch.cuda._sleep(100)
+    tr.graph.replay()
+    torch.cuda._sleep(100)
+    torch.cuda.synchronize()
+    tr.release()
+    sys.exit(0)
 gm = GraphedEnergyForces(model, z, pos, batch)
 for _ in range(5):
     gm(pos)

@@ -271,6 +271,126 @@ __global__ __launch_bounds__(256) void k_ln_bwd_epi(int n, int H, const T* __res
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Second order (force-matching training): the adjoint of the backward's node tail, fused per node
+// (one wave per node, CPL channels per lane).  Layer l's epilogue-backward VJP and layer l+1's
+// LayerNorm-backward VJP are adjacent in the adjoint pass (et_stack._second_order), so one kernel:
+//   epilogue part (o != NULL), for cotangents gb_o [N][3H], gb_vecp [N][3][3H] of (g_o, g_vecp) =
+//   EPI_BWD(gX, gV; vecp, o):
+//     gbar_x_out  = gbar_x_in + gb_o2 dot + gb_o3 + o2 sum_a(c1 v2 + c2 v1)
+//     gbar_vec_out = gbar_vec_in + gb_o1 v3 + c3 o1
+//     vecp_bar = [gb_o2 gX v2 + c2 gX o2 | gb_o2 gX v1 + c1 gX o2 | gb_o1 gV],
+//     o_bar = [sum_a c3 gV | gX sum_a(c1 v2 + c2 v1) | 0]        (c = gb_vecp; vecp NULL: only gb_o3)
+//   LayerNorm part (ln_w != NULL), for the cotangent g = gbar_x_out (o NULL: gbar_x_in) of
+//   g_x = LNB(g_y, x) = rstd (a - mean a - xh mean(a xh)), a = g_y w:
+//     gbar_gy = w J0 g,  J0 v = rstd (v - mean v - xh mean(v xh))
+//     x_bar   = -S rstd^2 xh / H - rstd/H ((a.xh) J0 g + (g.xh) J0 a),
+//               S = g.a - (sum g)(sum a)/H - (g.xh)(a.xh)/H
+//     w_rows  = g_y J0 g   (per row; the weight cotangent is its column sum)
+template <typename T, int CPL>
+__global__ __launch_bounds__(256) void k_adj_epi_ln(
+    int n, int H, const T* __restrict__ gbo, const T* __restrict__ gbvp, const T* __restrict__ gX,
+    const T* __restrict__ gV, const T* __restrict__ vecp, const T* __restrict__ o, const T* __restrict__ gbx_in,
+    const T* __restrict__ gbv_in, T* __restrict__ gbx_out, T* __restrict__ gbv_out, T* __restrict__ vpbar,
+    T* __restrict__ obar, const T* __restrict__ x, const T* __restrict__ mean, const T* __restrict__ rstd,
+    const T* __restrict__ lw, const T* __restrict__ gy, T* __restrict__ gbgy, T* __restrict__ xbar,
+    T* __restrict__ wrows) {
+  const int t = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+  const int lane = threadIdx.x & 63;
+  if (t >= n) return;
+  T g[CPL];
+#pragma unroll
+  for (int i = 0; i < CPL; ++i) {
+    const int c = lane + 64 * i;
+    g[i] = T(0);
+    if (c >= H) continue;
+    const size_t ix = (size_t)t * H + c;
+    T gb = gbx_in[ix];
+    if (o) {
+      const T* ot = o + (size_t)t * 3 * H;
+      const T* bo = gbo + (size_t)t * 3 * H;
+      const T o1 = ot[c], o2 = ot[H + c];
+      const T b1 = bo[c], b2 = bo[H + c], b3 = bo[2 * H + c];
+      T* ob = obar + (size_t)t * 3 * H;
+      if (!vecp) {
+        gb += b3;
+        ob[c] = T(0);
+        ob[H + c] = T(0);
+        ob[2 * H + c] = T(0);
+        if (gbv_out) {
+#pragma unroll
+          for (int a = 0; a < 3; ++a) {
+            const size_t iv = ((size_t)t * 3 + a) * H + c;
+            gbv_out[iv] = gbv_in ? gbv_in[iv] : T(0);
+          }
+        }
+      } else {
+        const T* vp = vecp + (size_t)t * 9 * H;
+        const T* cb = gbvp + (size_t)t * 9 * H;
+        T* vb = vpbar + (size_t)t * 9 * H;
+        const T gx = gX[ix];
+        T dot = T(0), cross = T(0), o1b = T(0);
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+          const T v1 = vp[a * 3 * H + c], v2 = vp[a * 3 * H + H + c], v3 = vp[a * 3 * H + 2 * H + c];
+          const T c1 = cb[a * 3 * H + c], c2 = cb[a * 3 * H + H + c], c3 = cb[a * 3 * H + 2 * H + c];
+          const size_t iv = ((size_t)t * 3 + a) * H + c;
+          const T gv = gV[iv];
+          dot += v1 * v2;
+          cross += c1 * v2 + c2 * v1;
+          o1b += c3 * gv;
+          gbv_out[iv] = (gbv_in ? gbv_in[iv] : T(0)) + b1 * v3 + c3 * o1;
+          vb[a * 3 * H + c] = b2 * gx * v2 + c2 * gx * o2;
+          vb[a * 3 * H + H + c] = b2 * gx * v1 + c1 * gx * o2;
+          vb[a * 3 * H + 2 * H + c] = b1 * gv;
+        }
+        gb += b2 * dot + b3 + o2 * cross;
+        ob[c] = o1b;
+        ob[H + c] = gx * cross;
+        ob[2 * H + c] = T(0);
+      }
+      gbx_out[ix] = gb;
+    }
+    g[i] = gb;
+  }
+  if (!lw) return;
+  const T mu = mean[t], rs = rstd[t];
+  T xh[CPL], av[CPL];
+  T sg = T(0), sa = T(0), sgx = T(0), sax = T(0), sga = T(0);
+#pragma unroll
+  for (int i = 0; i < CPL; ++i) {
+    const int c = lane + 64 * i;
+    xh[i] = av[i] = T(0);
+    if (c >= H) continue;
+    const size_t ix = (size_t)t * H + c;
+    xh[i] = (x[ix] - mu) * rs;
+    av[i] = gy[ix] * lw[c];
+    sg += g[i];
+    sa += av[i];
+    sgx += g[i] * xh[i];
+    sax += av[i] * xh[i];
+    sga += g[i] * av[i];
+  }
+  sg = wsum(sg);
+  sa = wsum(sa);
+  sgx = wsum(sgx);
+  sax = wsum(sax);
+  sga = wsum(sga);
+  const T iH = T(1) / T(H);
+  const T S = sga - sg * sa * iH - sgx * sax * iH;
+#pragma unroll
+  for (int i = 0; i < CPL; ++i) {
+    const int c = lane + 64 * i;
+    if (c >= H) continue;
+    const size_t ix = (size_t)t * H + c;
+    const T jg = rs * (g[i] - sg * iH - xh[i] * sgx * iH);
+    const T ja = rs * (av[i] - sa * iH - xh[i] * sax * iH);
+    gbgy[ix] = lw[c] * jg;
+    xbar[ix] = -S * rs * rs * xh[i] * iH - rs * iH * (sax * jg + sgx * ja);
+    wrows[ix] = gy[ix] * jg;
+  }
+}
+
 }  // namespace epi
 }  // namespace tmd
 
@@ -288,6 +408,7 @@ static int launch_cpl(int n, int H, hipStream_t st, A... args) {
 
 template <typename T, int C> struct KEpiLn { static constexpr auto fn = epi::k_epi_ln_fwd<T, C>; };
 template <typename T, int C> struct KLnBwd { static constexpr auto fn = epi::k_ln_bwd_epi<T, C>; };
+template <typename T, int C> struct KAdj { static constexpr auto fn = epi::k_adj_epi_ln<T, C>; };
 
 extern "C" int tmdnet_et_epilogue_ln_fwd(int dtype, int n_nodes, int hidden, const void* x, const void* vec,
                                          const void* vecp, const void* o, const void* vec_agg,
@@ -332,5 +453,31 @@ extern "C" int tmdnet_ln_bwd_epilogue(int dtype, int n_nodes, int hidden, const 
                                       (const double*)grad_res, (double*)grad_x, (const double*)grad_vec,
                                       (const double*)vecp, (const double*)o, (double*)grad_vecp,
                                       (double*)grad_o);
+  return kUnsupported;
+}
+
+extern "C" int tmdnet_et_adjoint_epi_ln(int dtype, int n_nodes, int hidden, const void* gb_o, const void* gb_vecp,
+                                        const void* grad_x, const void* grad_vec, const void* vecp, const void* o,
+                                        const void* gbar_x_in, const void* gbar_vec_in, void* gbar_x_out,
+                                        void* gbar_vec_out, void* vecp_bar, void* o_bar, const void* x,
+                                        const void* mean, const void* rstd, const void* ln_w, const void* grad_xn,
+                                        void* gbar_grad_xn, void* x_bar, void* w_bar_rows, void* stream) {
+  if (n_nodes < 0 || hidden <= 0 || !gbar_x_in) return kBadArgument;
+  if (o && (!gb_o || !gbar_x_out || !o_bar || (vecp && (!gb_vecp || !grad_x || !grad_vec || !gbar_vec_out ||
+                                                        !vecp_bar))))
+    return kBadArgument;
+  if (ln_w && (!x || !mean || !rstd || !grad_xn || !gbar_grad_xn || !x_bar || !w_bar_rows)) return kBadArgument;
+  if (!o && !ln_w) return kBadArgument;
+  if (n_nodes == 0) return kOk;
+  hipStream_t st = (hipStream_t)stream;
+#define TMD_ADJ(T)                                                                                            \
+  return launch_cpl<T, KAdj>(n_nodes, hidden, st, (const T*)gb_o, (const T*)gb_vecp, (const T*)grad_x,       \
+                             (const T*)grad_vec, (const T*)vecp, (const T*)o, (const T*)gbar_x_in,            \
+                             (const T*)gbar_vec_in, (T*)gbar_x_out, (T*)gbar_vec_out, (T*)vecp_bar, (T*)o_bar, \
+                             (const T*)x, (const T*)mean, (const T*)rstd, (const T*)ln_w, (const T*)grad_xn,  \
+                             (T*)gbar_grad_xn, (T*)x_bar, (T*)w_bar_rows)
+  if (dtype == TMDNET_F32) TMD_ADJ(float);
+  if (dtype == TMDNET_F64) TMD_ADJ(double);
+#undef TMD_ADJ
   return kUnsupported;
 }

@@ -25,6 +25,7 @@ The backward is itself a Function so forces stay differentiable (training on for
 backward (second order) recomputes the stack with composite PyTorch ops and differentiates twice.
 """
 import os
+import weakref
 
 import torch
 import torch.nn.functional as F
@@ -381,6 +382,7 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws, r=None, dr=Fa
     layers = meta.split(params)
     g_params = [None] * len(params)
     epi_done = False  # this layer's epilogue backward already ran (fused into the next layer's LN bwd)
+    x_top = inj.get("x_top")  # a cotangent of the last epilogue's output (the out_norm input)
     if meta.out_norm and not seed_pre_norm:  # gX is the gradient of LN(x_out): back through out_norm first
         x_pre, mean_o, rstd_o = acts[meta.n_layers]
         last = acts[meta.n_layers - 1]
@@ -388,9 +390,15 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws, r=None, dr=Fa
             gX, g_onw, g_onb = torch.ops.aten.native_layer_norm_backward(
                 gX, x_pre, [H], mean_o, rstd_o, params[-2], params[-1], [True, True, True])
             g_params[-2:] = [g_onw, g_onb]
+            if x_top is not None:
+                gX = gX + x_top
+        elif x_top is not None:  # LayerNorm backward + the injected cotangent (epilogue in the loop)
+            gX = _ln_bwd_epi(gX, x_pre, mean_o, rstd_o, params[-2], x_top, None, None, None, None, None)
         else:  # LayerNorm backward + the last layer's epilogue backward, one kernel
             gX = _ln_bwd_epi(gX, x_pre, mean_o, rstd_o, params[-2], None, gV, last[6], last[9], g_vecp, g_o)
             epi_done = True
+    elif x_top is not None:
+        gX = gX + x_top
     for l in reversed(range(meta.n_layers)):
         p = layers[l]
         x, vec, xn, mean, rstd, qkv, vecp, pkv, xa, o_ = acts[l]
@@ -543,6 +551,57 @@ def epi_adjoint(gb_o, gb_vecp, gX, gV, vecp, o):
     return gbar_gX, gbar_gV, vecp_bar, o_bar
 
 
+def adjoint_epi_ln_launch(epi, gbar_x_in, gbar_vec_in, ln):
+    """One ``tmdnet_et_adjoint_epi_ln`` launch: layer l's epilogue-backward VJP (``epi`` = (gb_o,
+    gb_vecp, gX, gV, vecp, o) or None) fused with the next LayerNorm-backward VJP (``ln`` = (x, mean,
+    rstd, ln_w, g_y) or None).  Returns (gbar_x_out, gbar_vec_out, vecp_bar, o_bar, gbar_gy, x_bar,
+    w_bar) with w_bar the weight cotangent (column sum of the kernel's per-row products).  The Python
+    ``epi_adjoint`` / ``ln_adjoint`` restate it (CPU tests)."""
+    lib = nat.load()
+    N, H = gbar_x_in.shape
+    o_ = dict(dtype=gbar_x_in.dtype, device=gbar_x_in.device)
+    gb_o = gb_vecp = gX = gV = vecp = o = None
+    gbx_out = gbv_out = vpbar = obar = None
+    if epi is not None:
+        gb_o, gb_vecp, gX, gV, vecp, o = epi
+        gbx_out = torch.empty((N, H), **o_)
+        obar = torch.empty((N, 3 * H), **o_)
+        if vecp is not None or gbar_vec_in is not None:
+            gbv_out = torch.empty((N, 3, H), **o_)
+        if vecp is not None:
+            vpbar = torch.empty((N, 3, 3 * H), **o_)
+    x = mean = rstd = w = gy = gbgy = xbar = wrows = None
+    if ln is not None:
+        x, mean, rstd, w, gy = ln
+        gbgy, xbar, wrows = torch.empty((N, H), **o_), torch.empty((N, H), **o_), torch.empty((N, H), **o_)
+    c = lambda t: None if t is None else t.contiguous()  # noqa: E731
+    args = [c(t) for t in (gb_o, gb_vecp, gX, gV, vecp, o, gbar_x_in, gbar_vec_in)]
+    rc = lib.tmdnet_et_adjoint_epi_ln(nat.dtype_code(gbar_x_in.dtype), N, H, *[nat.ptr(t) for t in args],
+                                      nat.ptr(gbx_out), nat.ptr(gbv_out), nat.ptr(vpbar), nat.ptr(obar),
+                                      *[nat.ptr(c(t)) for t in (x, mean, rstd, w, gy)], nat.ptr(gbgy),
+                                      nat.ptr(xbar), nat.ptr(wrows), nat.stream(gbar_x_in.device))
+    nat.check(rc, "tmdnet_et_adjoint_epi_ln")
+    if epi is None:
+        gbx_out, gbv_out = gbar_x_in, gbar_vec_in
+    return gbx_out, gbv_out, vpbar, obar, gbgy, xbar, \
+        (wrows.sum(0) if wrows is not None else None)
+
+
+def adjoint_epi_ln_composite(epi, gbar_x_in, gbar_vec_in, ln):
+    """``adjoint_epi_ln_launch`` restated with ``epi_adjoint`` / ``ln_adjoint`` (CPU tests)."""
+    gbx, gbv, vpbar, obar = gbar_x_in, gbar_vec_in, None, None
+    if epi is not None:
+        e_x, e_v, vpbar, obar = epi_adjoint(*epi)
+        gbx = gbar_x_in + e_x
+        if e_v is not None:
+            gbv = e_v if gbar_vec_in is None else gbar_vec_in + e_v
+    gbgy = xbar = wb = None
+    if ln is not None:
+        x, mean, rstd, w, gy = ln
+        gbgy, xbar, wb = ln_adjoint(gbx, x, mean, rstd, w, gy)
+    return gbx, gbv, vpbar, obar, gbgy, xbar, wb
+
+
 def hand_second_order_ok(meta, dr, need_w, ggs_params):
     """The hand-scheduled second order covers the force-pass node (no weight gradients in its
     outputs) in the reference row layout; otherwise the composite recompute runs."""
@@ -616,23 +675,34 @@ def _second_order(ctx, ggs, want):
     gbar_v = None
     ggC = gg_C if gg_C is not None else torch.zeros((E,), **o)
     ggu = gg_u if gg_u is not None else torch.zeros((E, 3), **o)
-    # 2. the adjoint pass, layer 0 first
+
+    def ln_of(l):  # the LayerNorm whose backward-VJP follows layer l-1's epilogue VJP
+        if l < L:
+            a = acts[l]
+            return (a[0], a[3], a[4], layers[l][0], rec[l]["g_xn"])
+        if meta.out_norm:
+            x_pre, mean_o, rstd_o = acts[L]
+            return (x_pre, mean_o, rstd_o, params[-2], gX)
+        return None
+
+    # 2. the adjoint pass, layer 0 first (layer 0's LayerNorm VJP alone, then per layer the node GEMM
+    # transposes, the message VJP and the fused epilogue VJP + next LayerNorm VJP)
+    _, _, _, _, gb_gxn, inj["x"][0], wb = adjoint_epi_ln_launch(None, gbar_x, None, ln_of(0))
+    acc(("ln", 0), wb)
+    seed_x = None
+    on_bar = None
     for l in range(L):
         p = layers[l]
         R = rec[l]
         x_l, vec_l, xn, mean, rstd, qkv, vecp, pkv, xa, o_ = acts[l]
-        ln_w, vec_w, o_w = p[0], p[8], p[9]
+        vec_w, o_w = p[8], p[9]
         qkv_w = meta.qkv_eff[l][0]
-        gb_gxn, inj["x"][l], wb_ln = ln_adjoint(gbar_x, x_l, mean, rstd, ln_w, R["g_xn"])
-        acc(("ln", l), wb_ln)
-        gb_gX = gbar_x  # the residual g_x = gX + ...
         gb_gqkv = torch.mm(gb_gxn, qkv_w.t())
         acc(("qkv", l), torch.mm(R["g_qkv"].t(), gb_gxn))
         gb_gvecp = None
         if vec_l is not None and gbar_v is not None:
             gb_gvecp = torch.matmul(gbar_v, vec_w.t())
             acc(("vec", l), torch.mm(R["g_vecp"].reshape(3 * N, 3 * H).t(), gbar_v.reshape(3 * N, H)))
-        gb_gV = gbar_v  # the vec residual g_vec = gV + ...
         # message backward VJP (per-edge projection rows)
         pk = pv = None
         if has_e:
@@ -653,37 +723,52 @@ def _second_order(ctx, ggs, want):
         inj["vec"][l] = d_vec
         C_bar.add_(d_C)
         u_bar.add_(d_u)
-        gb_gV = d_gvec if gb_gV is None else gb_gV + d_gvec
+        gb_gV = d_gvec if gbar_v is None else gbar_v + d_gvec  # the vec residual g_vec = gV + ...
         gb_go = torch.mm(d_gxa, o_w.t())
         acc(("o", l), torch.mm(R["g_o"].t(), d_gxa))
         if gb_gvecp is None and vecp is not None:
             gb_gvecp = torch.zeros((N, 3, 3 * H), **o)
-        e_gX, e_gV, inj["vecp"][l], inj["o"][l] = epi_adjoint(gb_go, gb_gvecp, R["gX"], R["gV"], vecp, o_)
-        gbar_x = gb_gX + e_gX
-        gbar_v = gb_gV if e_gV is None else gb_gV + e_gV
-    # the seeds: through the fused out_norm's backward first
-    seed_x = None
-    on_bar = None
-    if meta.out_norm:
-        x_pre, mean_o, rstd_o = acts[L]
-        gb_gXin, seed_x, wb_on = ln_adjoint(gbar_x, x_pre, mean_o, rstd_o, params[-2], gX)
-        on_bar = wb_on
-        gbar_x = gb_gXin
-    # 3. the backward through the forward layers with the injected cotangents
+        nxt = ln_of(l + 1)
+        gbar_x, gbar_v, inj["vecp"][l], inj["o"][l], gb_gxn, xb, wb = adjoint_epi_ln_launch(
+            (gb_go, gb_gvecp, R["gX"], R["gV"], vecp, o_), gbar_x, gb_gV, nxt)
+        if l + 1 < L:
+            inj["x"][l + 1] = xb
+            acc(("ln", l + 1), wb)
+        elif nxt is not None:  # the fused out_norm: its input's cotangent seeds pass 3
+            seed_x, on_bar = xb, wb
+            gbar_x = gb_gxn
+    # 3. the backward through the forward layers with the injected cotangents.  When the forward
+    # node's own backward runs later in this same pass (training: the energy loss and the head's
+    # second order reach it), the injections are handed to it (meta.pending) and it runs ONE
+    # backward for both -- no second pass, and no engine-side sums of two parameter gradients.
+    ref = getattr(meta, "fwd_node", None)
+    node = ref() if ref is not None else None
+    if node is not None and _will_run(node):
+        inj["x_top"] = seed_x
+        meta.pending = {"inj": inj, "W_bar": W_bar, "on_bar": on_bar, "C_bar": C_bar, "u_bar": u_bar}
+        res = [gbar_x, gbar_v, None, None, None, None, r_bar] + [None] * len(params)
+        return [t if w else None for t, w in zip(res, want)]
     need_w = tuple(bool(w) for w in _layer_wants(meta, want[7:]))
     g_x, g_f, g_C, g_u, _, g_params = _backward_layers(
         meta, seed_x if seed_x is not None else torch.zeros((N, H), **o), torch.zeros((N, 3, H), **o),
         f, C, u, params, acts, need_w, inject=inj, seed_pre_norm=meta.out_norm)
     g_C = g_C + C_bar
     g_u = g_u + u_bar
-    # weight cotangents of the first pass's products, added to the parameters' gradients
-    g_params = list(g_params)
+    g_params = _apply_w_bar(meta, list(g_params), W_bar, on_bar, lambda i: want[7 + i])
+    res = [gbar_x, gbar_v, g_x, g_f, g_C, g_u, r_bar] + g_params
+    return [t if w else None for t, w in zip(res, want)]
+
+
+def _apply_w_bar(meta, g_params, W_bar, on_bar, wanted):
+    """Add the adjoint pass's weight cotangents (the weights the first-order backward multiplies by:
+    LayerNorm weights, [q|k|v], vec_proj, o_proj, dk/dv, out_norm) to the parameters' gradients."""
+    H, D = meta.H, meta.D
 
     def addp(i, val):
-        if val is not None and want[7 + i]:
+        if val is not None and wanted(i):
             g_params[i] = val if g_params[i] is None else g_params[i] + val
 
-    for l in range(L):
+    for l in range(meta.n_layers):
         base = l * meta.np
         addp(base, W_bar.get(("ln", l)))
         wq = W_bar.get(("qkv", l))
@@ -694,13 +779,12 @@ def _second_order(ctx, ggs, want):
         addp(base + 8, W_bar.get(("vec", l)))
         addp(base + 9, W_bar.get(("o", l)))
         if "dkv" in W_bar:
-            for j, gw in enumerate(_dkv_param_grads(meta, W_bar["dkv"][l * D:(l + 1) * D],
-                                                   torch.zeros((D,), **o))[0::2]):
+            wl = W_bar["dkv"][l * D:(l + 1) * D]
+            for j, gw in enumerate(_dkv_param_grads(meta, wl, wl[:, 0])[0::2]):
                 addp(base + 11 + 2 * j, gw)
     if on_bar is not None:
-        addp(len(params) - 2, on_bar)
-    res = [gbar_x, gbar_v, g_x, g_f, g_C, g_u, r_bar] + g_params
-    return [t if w else None for t, w in zip(res, want)]
+        addp(len(g_params) - 2, on_bar)
+    return g_params
 
 
 def _layer_wants(meta, want_params):
@@ -786,6 +870,8 @@ class _ETStack(Function):
         x_out, vec_out, acts = _forward_layers(meta, x, f, C, u, params)
         ctx.meta = meta
         ctx.acts = acts
+        meta.fwd_node = weakref.ref(ctx)  # the second order hands its injections to this node's backward
+        meta.pending = None
         ctx.save_for_backward(x, f, C, u, r, *params)
         return x_out, vec_out
 
@@ -810,23 +896,32 @@ class _ETStack(Function):
             gV = torch.zeros((x.shape[0], 3, meta.H), dtype=x.dtype, device=x.device)
         # dr mode: the distances (not the features) take the edge-feature gradient -- only when no
         # weight gradient needs the projection gradient (the force pass)
+        pending, meta.pending = getattr(meta, "pending", None), None
         dr = bool(meta.rbf is not None and ctx.needs_input_grad[5] and meta.D and not any(need_w))
-        if DR_MODE in ("0", "off"):
+        if DR_MODE in ("0", "off") or pending is not None:
             dr = False
-        outs = _ETStackBwd.apply(meta, ctx.acts, need_w, dr, gX.contiguous(), gV.contiguous(), x, f, C, u,
-                                 r, *params)
+        outs = _ETStackBwd.apply(meta, ctx.acts, need_w, dr, pending, gX.contiguous(), gV.contiguous(), x, f, C,
+                                 u, r, *params)
         g_x, g_f, g_C, g_u, g_r = outs[:5]
         return (None, g_x, g_f, g_C, g_u, g_r) + tuple(outs[5:])
 
 
 class _ETStackBwd(Function):
     @staticmethod
-    def forward(ctx, meta, acts, need_w, dr, gX, gV, x, f, C, u, r, *params):
+    def forward(ctx, meta, acts, need_w, dr, pending, gX, gV, x, f, C, u, r, *params):
         if not meta.graph.symmetric:
             raise RuntimeError("torchmd-net_amd: the ET backward source pass needs a symmetric edge "
                                "list (include_transpose=True, no capacity overflow)")
         g_x, g_f, g_C, g_u, g_r, g_params = _backward_layers(meta, gX, gV, f, C, u, params, acts, need_w,
-                                                             r=r, dr=dr)
+                                                             r=r, dr=dr,
+                                                             inject=pending["inj"] if pending else None)
+        if pending is not None:  # the second order's contributions (et_stack._second_order)
+            g_C = g_C + pending["C_bar"]
+            g_u = g_u + pending["u_bar"]
+            wl = list(need_w)
+            g_params = _apply_w_bar(meta, list(g_params), pending["W_bar"], pending["on_bar"],
+                                    lambda i: wl[min(i // meta.np, len(wl) - 1)] if i < meta.n_layers * meta.np
+                                    else wl[-1])
         ctx.meta = meta
         ctx.dr = dr
         ctx.acts = acts
@@ -849,7 +944,7 @@ class _ETStackBwd(Function):
             return kernels.et_message(q, k, v, vec, pk, pv, C_, u_, graph, heads)
 
         _create = torch.is_grad_enabled()  # third order only if the caller builds a graph
-        n_out = 4 + len(saved)
+        n_out = 5 + len(saved)
         # inputs whose gradient this backward must deliver: asked for AND consumed downstream (a
         # training step's loss.backward(inputs=params) never runs the position branch, so the
         # cutoff / unit-vector / distance gradients -- E-sized work -- are skipped)
@@ -857,11 +952,11 @@ class _ETStackBwd(Function):
         want = []
         for i, t in enumerate(saved):
             node = next(nf)[0] if t is not None else None
-            want.append(t is not None and ctx.needs_input_grad[4 + i] and _will_run(node))
+            want.append(t is not None and ctx.needs_input_grad[5 + i] and _will_run(node))
         if SECOND_ORDER != "composite" and not _create and hand_second_order_ok(meta, ctx.dr, ctx.need_w, ggs[5:]):
             if not any(want):
                 return (None,) * n_out
-            return (None, None, None, None) + tuple(_second_order(ctx, ggs, want))
+            return (None,) * 5 + tuple(_second_order(ctx, ggs, want))
         with torch.enable_grad():
             leaves = [None if t is None else t.detach().requires_grad_(True) for t in saved]
             gX, gV, x, f, C, u, r = leaves[:7]
@@ -884,7 +979,7 @@ class _ETStackBwd(Function):
                                          create_graph=_create, allow_unused=True)
         it = iter(second)
         res = [next(it) if w else None for w in want]
-        return (None, None, None, None) + tuple(res)
+        return (None,) * 5 + tuple(res)
 
 
 def et_stack(layers, x, graph, f, C, u, rbf=None, out_norm=None, f_pairs=None):
