@@ -119,6 +119,20 @@ int tmdnet_edge_geom_fwd_rows(int dtype, int n_edges, int num_rbf, int rbf_type,
                               void* stream);
 /* Backward: given grad_rbf [E][R], grad_cutoff [E], grad_unit [E][3] (each nullable) produce
  * grad_dist [E] and grad_deltas [E][3] (both overwritten). */
+/* Second order of tmdnet_edge_geom_bwd (force-matching training; replaces autograd's double
+ * differentiation of reference utils.py:303-390 and the d_ij normalisation, torchmd_et.py:173-174):
+ * the VJP of (grad_deltas, grad_dist) for their cotangents gg_deltas [E][3], gg_dist [E] (NULL = 0),
+ * with respect to grad_rbf, grad_cutoff, grad_unit, dist, deltas (outputs; NULL = not wanted):
+ *   d_grad_rbf[e][k] = gg_dist f_k'(r)   d_grad_cutoff = gg_dist C'(r)
+ *   d_dist = gg_dist (sum_k grad_rbf_k f_k''(r) + grad_cutoff C''(r))
+ *   d_grad_unit, d_deltas: the unit vector's Jacobian and its derivative (self edges: identity, 0). */
+int tmdnet_edge_geom_bwd2(int dtype, int n_edges, int num_rbf, int rbf_type, const int32_t* src,
+                          const int32_t* dst, const void* deltas, const void* dist, const void* mu,
+                          const void* beta, double cutoff_lower, double cutoff_upper,
+                          const void* grad_rbf, const void* grad_cutoff, const void* grad_unit,
+                          const void* gg_deltas, const void* gg_dist, void* d_grad_rbf,
+                          void* d_grad_cutoff, void* d_grad_unit, void* d_dist, void* d_deltas,
+                          void* stream);
 /* d rbf_k / d r of edges rows[p] (rows NULL: edge p), out [n_rows][R] -- the RBF derivative the ET
  * force pass contracts with the dk/dv projection (tmdnet_et_message_bwd's dpk / dpv rows). */
 int tmdnet_rbf_deriv(int dtype, int num_rbf, int rbf_type, const void* dist, const void* mu,
@@ -264,6 +278,18 @@ int tmdnet_eq_head_fwd(int dtype, int n_atoms, int hidden, const void* x, const 
 int tmdnet_eq_head_bwd_weights(int dtype, int n_atoms, int hidden, const void* x, const void* vec,
                                const void* const* weights, const void* grad_y, void* grad_x,
                                void* grad_vec, void* const* saves, void* stream);
+/* Second order of the head's backward (force-matching training; replaces the double differentiation
+ * of the gated blocks, reference models/utils.py:492-522 under module.py:130-179's force loss).  For
+ * cotangents (tan_x [N][H], tan_vec [N][3][H]; NULL = 0) of (grad_x, grad_vec) = grad_y[n] * J(x, vec):
+ *   d_x, d_vec = grad_y[n] * d/dt J(x + t tan_x, vec + t tan_vec)   (Hessian-vector product)
+ *   d_grad_y[n] = <tan_x, J_x> + <tan_vec, J_vec>                    (NULL = not written)
+ * saves[12] (NULL = no weight terms): the layouts of tmdnet_eq_head_bwd_weights for 2N atoms
+ * ([tangent half ; plain half]) plus saves[11] = vv [2][N][3][H] = [vec ; tan_vec]; each weight's
+ * second-order term is then one GEMM over 2N (6N) rows, e.g. [dW1; dW2] = a1^T vv. */
+int tmdnet_eq_head_hvp(int dtype, int n_atoms, int hidden, const void* x, const void* vec,
+                       const void* const* weights, const void* grad_y, const void* tan_x,
+                       const void* tan_vec, void* d_x, void* d_vec, void* d_grad_y,
+                       void* const* saves, void* stream);
 /* grad_x = grad_y[n] * jac_x[n], grad_vec = grad_y[n] * jac_vec[n] (the head's backward). */
 int tmdnet_eq_head_bwd(int dtype, int n_atoms, int hidden, const void* grad_y, const void* jac_x,
                        const void* jac_vec, void* grad_x, void* grad_vec, void* stream);
@@ -284,6 +310,16 @@ int tmdnet_nbr_embed_bwd(int dtype, int n_nodes, int hidden, const int32_t* row_
                          const int32_t* src, int max_pairs, const void* x, int ld_x, const void* w,
                          int ld_w, const void* cutoff, const void* grad_out, int ld_grad_out, void* gx,
                          void* gw, void* gcut, void* stream);
+/* Second order of the neighbour embedding (force-matching training; replaces autograd's double
+ * differentiation of reference utils.py:100-107): the VJP of (gx, gw, gcut) = tmdnet_nbr_embed_bwd(...)
+ * for cotangents gg_x [N][H], gg_w [E][H], gg_cut [E] (NULL = 0), with respect to grad_out (d_grad_out
+ * [N][H]), x (d_x [N][H], source pass over the reversed edges transpose[e]), w (d_w [E][H]) and the
+ * cutoff (d_cut [E]); outputs NULL = not wanted, edge outputs written for every slot < row_ptr[N]. */
+int tmdnet_nbr_embed_bwd2(int dtype, int n_nodes, int hidden, const int32_t* row_ptr,
+                          const int32_t* src, const int32_t* transpose, int max_pairs, const void* x,
+                          int ld_x, const void* w, int ld_w, const void* cutoff, const void* grad_out,
+                          int ld_grad_out, const void* gg_x, const void* gg_w, const void* gg_cut,
+                          void* d_grad_out, void* d_x, void* d_w, void* d_cut, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * TensorNet edge kernels (reference models/tensornet.py:287-332).

@@ -135,3 +135,35 @@ def test_model_uses_fused_head_and_matches_blocks():
         EquivariantScalar.pre_reduce = pr
     assert out is m.output_model
     assert _rel(y, y2) < 1e-11 and _rel(f, f2) < 1e-10
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype,H,N,tol", [(torch.float64, 128, 37, 1e-11), (torch.float32, 128, 2100, 5e-5),
+                                           (torch.float64, 48, 5, 1e-11)])
+def test_head_second_order_hand_matches_composite(dtype, H, N, tol, monkeypatch):
+    """tmdnet_eq_head_hvp (forward-over-reverse in one kernel + the weight-term GEMMs) against
+    autograd's double differentiation of the composite: the force-loss second order of the head
+    for every input (x, vec, the seed g_y) and weight; N = 2100 runs two atoms per workgroup."""
+    head = _head(H, dtype).to(DEV)
+    ps = kernels.eq_head_params(head.output_network)
+    x, vec = _inputs(N, H, dtype, DEV)
+    gy = torch.randn(N, 1, dtype=dtype, device=DEV)
+    cx, cv = torch.randn_like(x), torch.randn_like(vec)
+
+    def run(mode):
+        monkeypatch.setattr(kernels, "HEAD_SECOND_ORDER", mode)
+        xs, vs = x.clone().requires_grad_(True), vec.clone().requires_grad_(True)
+        g = gy.clone().requires_grad_(True)
+        y = kernels.eq_scalar_head(xs, vs, head.output_network)
+        gx, gv = torch.autograd.grad(y, (xs, vs), g, create_graph=True)  # the force pass (no weight grads)
+        l2 = (gx * cx).sum() + (gv * cv).sum()
+        return torch.autograd.grad(l2, [xs, vs, g] + ps, allow_unused=True)
+
+    hand, comp = run("hand"), run("composite")
+    for i, (a, b) in enumerate(zip(hand, comp)):
+        if b is None or b.abs().max() == 0:
+            assert a is None or a.abs().max() == 0, i
+            continue
+        assert a is not None and torch.isfinite(a).all(), i
+        assert _rel(a, b) < tol, (i, _rel(a, b))
+    assert torch.all(hand[1][2] == 0)  # the isolated atom's masked rows get nothing of any order

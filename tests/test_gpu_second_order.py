@@ -86,3 +86,73 @@ def test_hand_second_order_on_model(monkeypatch, dr, out_norm):
         assert _rel(a, b) < 1e-9
         n += 1
     assert n > 30
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float64, 1e-11), (torch.float32, 2e-5)])
+@pytest.mark.parametrize("rbf,cl", [("expnorm", 0.0), ("expnorm", 0.7), ("gauss", 0.0)])
+def test_edge_geometry_second_order_hand_matches_composite(monkeypatch, dtype, tol, rbf, cl):
+    """tmdnet_edge_geom_bwd2 against autograd's double differentiation of the composite geometry
+    (RBF basis, cosine cutoff incl. the shifted form, unit vectors, self edges), every input."""
+    import types
+    from torchmdnet import _native as nat
+    from torchmdnet import kernels as K
+    torch.manual_seed(0)
+    E, R, cu = 3000, 64, 5.0
+    src = torch.randint(0, 100, (E,), device=DEV, dtype=torch.int32)
+    dst = torch.randint(0, 100, (E,), device=DEV, dtype=torch.int32)
+    dst[:50] = src[:50]
+    deltas = torch.randn(E, 3, device=DEV, dtype=dtype) * 2.2
+    deltas[src == dst] = 0
+    dist = deltas.norm(dim=1)
+    if rbf == "expnorm":
+        start = torch.exp(torch.scalar_tensor(-cu + cl, dtype=dtype))
+        mu = torch.linspace(float(start), 1, R, dtype=dtype, device=DEV)
+        beta = torch.full((R,), float((2 / R * (1 - start)) ** -2), dtype=dtype, device=DEV)
+        rtype = nat.RBF_EXPNORM
+    else:
+        mu = torch.linspace(cl, cu, R, dtype=dtype, device=DEV)
+        beta = torch.full((R,), -0.5 / float(mu[1] - mu[0]) ** 2, dtype=dtype, device=DEV)
+        rtype = nat.RBF_GAUSS
+    graph = types.SimpleNamespace(src=src, dst=dst)
+    gf0, gC0, gu0 = torch.randn(E, R, device=DEV, dtype=dtype), torch.randn(E, device=DEV, dtype=dtype), \
+        torch.randn(E, 3, device=DEV, dtype=dtype)
+    c1, c2 = torch.randn(E, 3, device=DEV, dtype=dtype), torch.randn(E, device=DEV, dtype=dtype)
+    out = []
+    for mode in ("hand", "composite"):
+        monkeypatch.setattr(K, "HEAD_SECOND_ORDER", mode)
+        leaves = [t.clone().requires_grad_(True) for t in (deltas, dist, gf0, gC0, gu0)]
+        g_dl, g_r = K._EdgeGeomBwd.apply(*leaves, graph, mu, beta, cl, cu, rtype)
+        loss = (g_dl * c1).sum() + (g_r * c2).sum()
+        out.append(torch.autograd.grad(loss, leaves, allow_unused=True))
+    for i, (a, b) in enumerate(zip(*out)):
+        assert a is not None and b is not None, i
+        assert torch.isfinite(a).all(), i
+        assert _rel(a, b) < tol, (i, _rel(a, b))
+
+
+def test_neighbor_embedding_second_order_hand_matches_composite(monkeypatch):
+    """tmdnet_nbr_embed_bwd2 (destination pass + source pass over the reversed edges) against autograd's
+    double differentiation of the composite, fp64, with non-symmetric cotangents on every output."""
+    from torchmdnet import kernels
+    torch.manual_seed(4)
+    z, pos, batch = O.qm9_like(3)
+    g = kernels.build_graph(pos.to(DEV), batch.to(DEV), 0.0, 5.0, 64 * pos.shape[0], loop=True)
+    N, H, E = pos.shape[0], 64, g.n_edges
+    T = g.transpose.long()
+    x0 = torch.randn(N, H, dtype=torch.float64, device=DEV)
+    w0 = torch.randn(E, H, dtype=torch.float64, device=DEV)
+    w0 = (w0 + w0[T]) / 2
+    C0 = torch.rand(E, dtype=torch.float64, device=DEV)
+    C0 = (C0 + C0[T]) / 2
+    go0 = torch.randn(N, H, dtype=torch.float64, device=DEV)
+    wts = [torch.randn(N, H, dtype=torch.float64, device=DEV), torch.randn(E, H, dtype=torch.float64, device=DEV),
+           torch.randn(E, dtype=torch.float64, device=DEV)]
+    res = []
+    for mode in ("hand", "composite"):
+        monkeypatch.setattr(kernels, "HEAD_SECOND_ORDER", mode)
+        leaves = [t.clone().requires_grad_(True) for t in (go0, x0, w0, C0)]
+        a = kernels._NbrEmbedBwd.apply(*leaves, g)
+        res.append(torch.autograd.grad(sum((t * u).sum() for t, u in zip(a, wts)), leaves, allow_unused=True))
+    for i, (p_, q_) in enumerate(zip(*res)):
+        assert p_ is not None and q_ is not None, i
+        assert _rel(p_, q_) < 1e-11, (i, _rel(p_, q_))

@@ -38,6 +38,43 @@ template <typename T> __device__ __forceinline__ void cosine_cutoff(T r, T cl, T
   }
 }
 
+// CosineCutoff with its first and second derivatives w.r.t. r
+template <typename T> __device__ __forceinline__ void cosine_cutoff2(T r, T cl, T cu, T& c, T& dc, T& d2c) {
+  const bool in = cl > T(0) ? (r < cu) && (r > cl) : r < cu;
+  const T w = cl > T(0) ? T(2) * pi<T>() / (cu - cl) : pi<T>() / cu;
+  const T arg = cl > T(0) ? pi<T>() * (T(2) * (r - cl) / (cu - cl) + T(1)) : r * pi<T>() / cu;
+  const T cs = cos(arg);
+  c = in ? T(0.5) * (cs + T(1)) : T(0);
+  dc = in ? T(-0.5) * sin(arg) * w : T(0);
+  d2c = in ? T(-0.5) * cs * w * w : T(0);
+}
+
+// basis value, d/dr and d2/dr2 (the force-loss second order)
+template <typename T>
+__device__ __forceinline__ void basis2(const Cfg<T>& P, T r, int k, T& f, T& df, T& d2f) {
+  if (P.type == TMDNET_RBF_EXPNORM) {
+    T c0, dc0, d2c0;
+    cosine_cutoff2<T>(r, T(0), P.cu, c0, dc0, d2c0);
+    const T u = exp(P.alpha * (P.cl - r));
+    const T du = -P.alpha * u, d2u = P.alpha * P.alpha * u;
+    const T b = P.beta[k];
+    const T z = u - P.mu[k];
+    const T g = exp(-b * z * z);
+    const T q = T(-2) * b * z * du;  // dg = g q
+    const T dg = g * q;
+    const T d2g = g * (q * q - T(2) * b * (du * du + z * d2u));
+    f = c0 * g;
+    df = dc0 * g + c0 * dg;
+    d2f = d2c0 * g + T(2) * dc0 * dg + c0 * d2g;
+  } else {
+    const T z = r - P.mu[k];
+    const T coeff = P.beta[0];
+    f = exp(coeff * z * z);
+    df = f * T(2) * coeff * z;
+    d2f = f * (T(4) * coeff * coeff * z * z + T(2) * coeff);
+  }
+}
+
 // basis value and d/dr
 template <typename T>
 __device__ __forceinline__ void basis(const Cfg<T>& P, T r, int k, T& f, T& df) {
@@ -140,6 +177,66 @@ __global__ __launch_bounds__(256) void k_bwd(Cfg<T> P, const T* __restrict__ gf,
       gdl[3 * e] = gx;
       gdl[3 * e + 1] = gy;
       gdl[3 * e + 2] = gz;
+    }
+  }
+}
+
+// Second order of k_bwd (force-loss training): the VJP of (g_dl, g_r) = bwd(dl, r, gf, gC, gu) for
+// cotangents (gg_dl, gg_r).  With u = dl/n (n = |dl|, non-self edges), P = I - u u^T, g_dl = P gu / n:
+//   d_gf[k] = gg_r f_k'(r)      d_gC = gg_r C'(r)      d_r = gg_r (sum_k gf_k f_k''(r) + gC C''(r))
+//   d_gu    = P gg_dl / n       d_dl = -[(u.gu) P gg + (u.gg) P gu + A u] / n^2,
+//   A = gg.gu - (u.gg)(u.gu);   self edges: d_gu = gg_dl, d_dl = 0.  Output pointers may be NULL.
+template <typename T>
+__global__ __launch_bounds__(256) void k_bwd2(Cfg<T> P, const T* __restrict__ gf, const T* __restrict__ gC,
+                                              const T* __restrict__ gu, const T* __restrict__ ggdl,
+                                              const T* __restrict__ ggr, T* __restrict__ dgf, T* __restrict__ dgC,
+                                              T* __restrict__ dgu, T* __restrict__ dr, T* __restrict__ ddl) {
+  const int lane = lane_id();
+  const int nw = gridDim.x * (blockDim.x / TMD_WAVE);
+  for (int e = blockIdx.x * (blockDim.x / TMD_WAVE) + threadIdx.x / TMD_WAVE; e < P.E; e += nw) {
+    const T r = P.r[e];
+    const T g_r = ggr ? ggr[e] : T(0);
+    T acc = T(0);
+    if (dgf || (dr && gf)) {
+      for (int k = lane; k < P.R; k += TMD_WAVE) {
+        T v, dv, d2v;
+        basis2(P, r, k, v, dv, d2v);
+        if (dgf) dgf[(long long)e * P.R + k] = g_r * dv;
+        if (gf) acc += gf[(long long)e * P.R + k] * d2v;
+      }
+      if (dr && gf) acc = wave_sum(acc);
+    }
+    if (lane != 0) continue;
+    if (dgC || dr) {
+      T c, dc, d2c;
+      cosine_cutoff2<T>(r, P.cl, P.cu, c, dc, d2c);
+      if (dgC) dgC[e] = g_r * dc;
+      if (dr) dr[e] = g_r * (acc + (gC ? gC[e] * d2c : T(0)));
+    }
+    if (!dgu && !ddl) continue;
+    const T a = ggdl ? ggdl[3 * e] : T(0), b = ggdl ? ggdl[3 * e + 1] : T(0), c = ggdl ? ggdl[3 * e + 2] : T(0);
+    T o[3] = {a, b, c}, d[3] = {T(0), T(0), T(0)};
+    if (P.src[e] != P.dst[e]) {
+      const T x = P.dl[3 * e], y = P.dl[3 * e + 1], z = P.dl[3 * e + 2];
+      const T n = sqrt(x * x + y * y + z * z);
+      const T u[3] = {x / n, y / n, z / n};
+      const T ug = u[0] * a + u[1] * b + u[2] * c;
+      const T gv[3] = {gu ? gu[3 * e] : T(0), gu ? gu[3 * e + 1] : T(0), gu ? gu[3 * e + 2] : T(0)};
+      const T uq = u[0] * gv[0] + u[1] * gv[1] + u[2] * gv[2];
+      const T A = a * gv[0] + b * gv[1] + c * gv[2] - ug * uq;
+      const T in2 = T(1) / (n * n);
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const T pg = o[j] - u[j] * ug, pq = gv[j] - u[j] * uq;
+        d[j] = -(uq * pg + ug * pq + A * u[j]) * in2;
+        o[j] = pg / n;
+      }
+    }
+    if (dgu) {
+      dgu[3 * e] = o[0]; dgu[3 * e + 1] = o[1]; dgu[3 * e + 2] = o[2];
+    }
+    if (ddl) {
+      ddl[3 * e] = d[0]; ddl[3 * e + 1] = d[1]; ddl[3 * e + 2] = d[2];
     }
   }
 }
@@ -259,5 +356,35 @@ extern "C" int tmdnet_rbf_deriv(int dtype, int num_rbf, int rbf_type, const void
   } else {
     return kUnsupported;
   }
+  return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
+}
+
+extern "C" int tmdnet_edge_geom_bwd2(int dtype, int n_edges, int num_rbf, int rbf_type,
+                                     const int32_t* src, const int32_t* dst, const void* deltas,
+                                     const void* dist, const void* mu, const void* beta,
+                                     double cutoff_lower, double cutoff_upper, const void* grad_rbf,
+                                     const void* grad_cutoff, const void* grad_unit, const void* gg_deltas,
+                                     const void* gg_dist, void* d_grad_rbf, void* d_grad_cutoff,
+                                     void* d_grad_unit, void* d_dist, void* d_deltas, void* stream) {
+  if (n_edges < 0 || num_rbf <= 0 || !src || !dst || !deltas || !dist || !mu || !beta) return kBadArgument;
+  if (n_edges == 0) return kOk;
+  hipStream_t st = (hipStream_t)stream;
+  const int tb = 256;
+  const int blocks = (int)std::min<long long>(((long long)n_edges + 3) / 4, 256LL * 64);
+#define TMD_GEOM_BWD2(T_)                                                                                      \
+  {                                                                                                            \
+    auto P = geom::make<T_>(n_edges, num_rbf, rbf_type, src, dst, deltas, dist, mu, beta, cutoff_lower,        \
+                            cutoff_upper);                                                                     \
+    hipLaunchKernelGGL(geom::k_bwd2<T_>, dim3(blocks), dim3(tb), 0, st, P, (const T_*)grad_rbf,                \
+                       (const T_*)grad_cutoff, (const T_*)grad_unit, (const T_*)gg_deltas, (const T_*)gg_dist, \
+                       (T_*)d_grad_rbf, (T_*)d_grad_cutoff, (T_*)d_grad_unit, (T_*)d_dist, (T_*)d_deltas);     \
+  }
+  if (dtype == TMDNET_F32)
+    TMD_GEOM_BWD2(float)
+  else if (dtype == TMDNET_F64)
+    TMD_GEOM_BWD2(double)
+  else
+    return kUnsupported;
+#undef TMD_GEOM_BWD2
   return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
 }

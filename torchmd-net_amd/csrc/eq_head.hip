@@ -438,6 +438,322 @@ __global__ __launch_bounds__(256) void k_eq_head(int n, int H, const T* __restri
   }
 }
 
+// ---------------------------------------------------------------------------------------------------
+// Second order (force-matching training).  The first-order backward maps (g_y, x, vec) to
+// (g_x, g_vec) = g_y * J(x, vec); its VJP for cotangents (t_x, t_vec) of (g_x, g_vec) is, because the
+// Hessian is symmetric, the DIRECTIONAL derivative of that gradient along (t_x, t_vec):
+// forward-over-reverse.  Per atom: the forward, the tangent forward (dotted quantities), the reverse
+// seeded with g_y and its tangent, all in LDS:
+//   d_x, d_vec = g_y * d/dt [J](x + t t_x, vec + t t_vec)        (the HVP)
+//   d_g_y      = <t_x, J_x> + <t_vec, J_vec> = ydot                (the tangent of y)
+//   d W       = d/dt of the weight gradient of g_y * y, each a GEMM over [tangent rows ; plain rows]:
+//               e.g. d U1 = sum_n gdot_u (x) [h | 1] + g_u (x) [hdot | 0].
+// SiLU'(u) = s (1 + u (1 - s)), SiLU''(u) = s (1 - s) (2 + u (1 - 2 s)), s = sigmoid(u).  The norm's
+// tangent and its gradient's tangent are 0 where the norm is 0 (the reference masks those rows).
+template <typename T>
+__device__ __forceinline__ T dsilu(T u) {
+  const T s = sig(u);
+  return s * (T(1) + u * (T(1) - s));
+}
+template <typename T>
+__device__ __forceinline__ T d2silu(T u) {
+  const T s = sig(u);
+  return s * (T(1) - s) * (T(2) + u * (T(1) - T(2) * s));
+}
+
+// Layout plus g_s (U2^T g_o before SiLU') and the tangent buffers (prefix t).
+struct Layout2 : Layout {
+  int gs, th, tv, tvb, tv2, tu, ts, to, th2, tv1, tvb2, tu2, ts2;          // tangent forward
+  int tgu2, tgh2, tgvb2, tgv1, tgo, tgv2, tgs, tgu, tgvec1, tgvb;          // tangent reverse
+  int P2;
+  __host__ __device__ Layout2(int H) : Layout(H) {
+    const int O = H / 2, Q = O;
+    int p = P;
+    gs = p;     p += H;
+    th = p;     p += 2 * H;  // [t_x | vec1dot]
+    tv = p;     p += 3 * H;
+    tvb = p;    p += 3 * H;
+    tv2 = p;    p += 3 * O;
+    tu = p;     p += H;
+    ts = p;     p += H;
+    to = p;     p += 2 * O;
+    th2 = p;    p += 2 * Q;
+    tv1 = p;    p += 3 * O;
+    tvb2 = p;   p += 3 * Q;
+    tu2 = p;    p += Q;
+    ts2 = p;    p += Q;
+    tgu2 = p;   p += Q;
+    tgh2 = p;   p += 2 * Q;
+    tgvb2 = p;  p += 3 * Q;
+    tgv1 = p;   p += 3 * O;
+    tgo = p;    p += 2 * O;
+    tgv2 = p;   p += 3 * O;
+    tgs = p;    p += H;
+    tgu = p;    p += H;
+    tgvec1 = p; p += H;
+    tgvb = p;   p += 3 * H;
+    P2 = (p + 3) & ~3;
+  }
+};
+
+// Per-atom factors of the weight-gradient tangents: every array holds 2N atoms, [tangent half (atoms
+// 0..N-1) ; plain half (N..2N-1)], so each weight's tangent is ONE GEMM over 2N (or 6N) rows with the
+// layouts of Saves; vv [2][N][3][H] = [vec ; t_vec] is the second operand of [dW1; dW2].
+template <typename T>
+struct Saves2 {
+  Saves<T> s;
+  T* vv;
+};
+
+template <typename T, int NT, bool VEC>
+__global__ __launch_bounds__(256) void k_eq_head_hvp(int n, int H, const T* __restrict__ x,
+                                                     const T* __restrict__ vec, Weights<T> W,
+                                                     const T* __restrict__ gy, const T* __restrict__ tx,
+                                                     const T* __restrict__ tvec, T* __restrict__ dx,
+                                                     T* __restrict__ dvec, T* __restrict__ dgy, Saves2<T> S2) {
+  extern __shared__ __align__(16) unsigned char smem_raw[];
+  T* sm = reinterpret_cast<T*>(smem_raw);
+  const Layout2 L(H);
+  const int P = L.P2, O = H / 2, Q = O;
+  const int n0 = blockIdx.x * NT;
+  const int nt = min(NT, n - n0);
+  const int tid = threadIdx.x, bs = blockDim.x;
+
+  // stage x -> h[0:H], vec -> v, t_x -> th[0:H], t_vec -> tv (absent atoms / tangents: zero)
+  for (int i = tid; i < NT * 8 * H; i += bs) {
+    const int t = i / (8 * H), c0 = i - t * 8 * H;
+    const bool live = t < nt, tang = c0 >= 4 * H;
+    const int c = tang ? c0 - 4 * H : c0;
+    const T* src = c < H ? (tang ? tx : x) : (tang ? tvec : vec);
+    T val = T(0);
+    if (live && src) val = c < H ? src[(size_t)(n0 + t) * H + c] : src[(size_t)(n0 + t) * 3 * H + c - H];
+    sm[t * P + (c < H ? (tang ? L.th : L.h) + c : (tang ? L.tv : L.v) + c - H)] = val;
+  }
+  __syncthreads();
+
+  // ---------------- forward (block 1, block 2 up to s2; the gate vec'' does not reach y)
+  rows2<T, NT, 3, 2, VEC, 2>(W.w1, nullptr, H, W.w2, nullptr, O, H, sm + L.v, H, sm + L.vb, H, sm + L.v2, O, P);
+  rows2<T, NT, 3, 2, VEC, 2>(W.w1, nullptr, H, W.w2, nullptr, O, H, sm + L.tv, H, sm + L.tvb, H, sm + L.tv2, O, P);
+  __syncthreads();
+  for (int i = tid; i < NT * H; i += bs) {
+    const int t = i / H, c = i - t * H;
+    T* a = sm + t * P;
+    const T b0 = a[L.vb + c], b1 = a[L.vb + H + c], b2 = a[L.vb + 2 * H + c];
+    const T nrm = sqrt(b0 * b0 + b1 * b1 + b2 * b2);
+    a[L.h + H + c] = nrm;
+    a[L.th + H + c] = nrm > T(0)
+        ? (b0 * a[L.tvb + c] + b1 * a[L.tvb + H + c] + b2 * a[L.tvb + 2 * H + c]) / nrm : T(0);
+  }
+  __syncthreads();
+  rows2<T, NT, 1, 2, VEC, 4>(W.u1w, W.u1b, H, W.u1w, nullptr, 0, 2 * H, sm + L.h, 0, sm + L.u, 0, nullptr, 0, P);
+  rows2<T, NT, 1, 2, VEC, 4>(W.u1w, nullptr, H, W.u1w, nullptr, 0, 2 * H, sm + L.th, 0, sm + L.tu, 0, nullptr, 0, P);
+  __syncthreads();
+  for (int i = tid; i < NT * H; i += bs) {
+    const int t = i / H, c = i - t * H;
+    T* a = sm + t * P;
+    const T u = a[L.u + c];
+    a[L.s + c] = u * sig(u);
+    a[L.ts + c] = dsilu(u) * a[L.tu + c];
+  }
+  __syncthreads();
+  rows2<T, NT, 1, 2, VEC, 4>(W.u2w, W.u2b, 2 * O, W.u2w, nullptr, 0, H, sm + L.s, 0, sm + L.o, 0, nullptr, 0, P);
+  rows2<T, NT, 1, 2, VEC, 4>(W.u2w, nullptr, 2 * O, W.u2w, nullptr, 0, H, sm + L.ts, 0, sm + L.to, 0, nullptr, 0, P);
+  __syncthreads();
+  for (int i = tid; i < NT * O; i += bs) {
+    const int t = i / O, c = i - t * O;
+    T* a = sm + t * P;
+    const T xo = a[L.o + c], vo = a[L.o + O + c], txo = a[L.to + c], tvo = a[L.to + O + c];
+    a[L.h2 + c] = xo * sig(xo);
+    a[L.th2 + c] = dsilu(xo) * txo;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      a[L.v1 + r * O + c] = vo * a[L.v2 + r * O + c];
+      a[L.tv1 + r * O + c] = tvo * a[L.v2 + r * O + c] + vo * a[L.tv2 + r * O + c];
+    }
+  }
+  __syncthreads();
+  rows2<T, NT, 3, 2, VEC, 4>(W.v1, nullptr, Q, W.v1, nullptr, 0, O, sm + L.v1, O, sm + L.vb2, Q, sm + L.vb2, Q, P);
+  rows2<T, NT, 3, 2, VEC, 4>(W.v1, nullptr, Q, W.v1, nullptr, 0, O, sm + L.tv1, O, sm + L.tvb2, Q, sm + L.tvb2, Q, P);
+  __syncthreads();
+  for (int i = tid; i < NT * Q; i += bs) {
+    const int t = i / Q, c = i - t * Q;
+    T* a = sm + t * P;
+    const T b0 = a[L.vb2 + c], b1 = a[L.vb2 + Q + c], b2 = a[L.vb2 + 2 * Q + c];
+    const T nrm = sqrt(b0 * b0 + b1 * b1 + b2 * b2);
+    a[L.h2 + Q + c] = nrm;
+    a[L.th2 + Q + c] = nrm > T(0)
+        ? (b0 * a[L.tvb2 + c] + b1 * a[L.tvb2 + Q + c] + b2 * a[L.tvb2 + 2 * Q + c]) / nrm : T(0);
+  }
+  __syncthreads();
+  rows2<T, NT, 1, 2, VEC, 8>(W.p1w, W.p1b, Q, W.p1w, nullptr, 0, 2 * Q, sm + L.h2, 0, sm + L.u2, 0, nullptr, 0, P);
+  rows2<T, NT, 1, 2, VEC, 8>(W.p1w, nullptr, Q, W.p1w, nullptr, 0, 2 * Q, sm + L.th2, 0, sm + L.tu2, 0, nullptr, 0, P);
+  __syncthreads();
+  for (int i = tid; i < NT * Q; i += bs) {
+    const int t = i / Q, c = i - t * Q;
+    T* a = sm + t * P;
+    const T u = a[L.u2 + c], tu = a[L.tu2 + c];
+    const T seed = t < nt ? gy[n0 + t] : T(0);
+    a[L.s2 + c] = u * sig(u);
+    a[L.ts2 + c] = dsilu(u) * tu;
+    // g_s2 = seed P2[0][:] (constant in x, vec): g_u2 = g_s2 SiLU'(u2), its tangent g_s2 SiLU''(u2) u2dot
+    a[L.gu2 + c] = seed * W.p2w[c] * dsilu(u);
+    a[L.tgu2 + c] = seed * W.p2w[c] * d2silu(u) * tu;
+  }
+  __syncthreads();
+
+  // ---------------- reverse and its tangent (the transposed products shared in pairs)
+  cols2<T, NT, 1, VEC>(W.p1w, 2 * Q, Q, sm + L.gu2, 0, nullptr, 0, 0, nullptr, 0, 2 * Q, sm + L.gh2, 0, P, nt, 0,
+                       false);
+  cols2<T, NT, 1, VEC>(W.p1w, 2 * Q, Q, sm + L.tgu2, 0, nullptr, 0, 0, nullptr, 0, 2 * Q, sm + L.tgh2, 0, P, nt, 0,
+                       false);
+  __syncthreads();
+  for (int i = tid; i < NT * Q; i += bs) {
+    const int t = i / Q, c = i - t * Q;
+    T* a = sm + t * P;
+    const T nrm = a[L.h2 + Q + c];
+    const T inv = nrm > T(0) ? T(1) / nrm : T(0);
+    const T gn = a[L.gh2 + Q + c] * inv, tgn = a[L.tgh2 + Q + c] * inv, tn = a[L.th2 + Q + c] * inv;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      const T b = a[L.vb2 + r * Q + c];
+      a[L.gvb2 + r * Q + c] = gn * b;
+      a[L.tgvb2 + r * Q + c] = tgn * b + gn * (a[L.tvb2 + r * Q + c] - b * tn);
+    }
+  }
+  __syncthreads();
+  cols2<T, NT, 3, VEC>(W.v1, O, Q, sm + L.gvb2, Q, nullptr, 0, 0, nullptr, 0, O, sm + L.gv1, O, P, nt, 0, false);
+  cols2<T, NT, 3, VEC>(W.v1, O, Q, sm + L.tgvb2, Q, nullptr, 0, 0, nullptr, 0, O, sm + L.tgv1, O, P, nt, 0, false);
+  __syncthreads();
+  for (int i = tid; i < NT * O; i += bs) {
+    const int t = i / O, c = i - t * O;
+    T* a = sm + t * P;
+    const T xo = a[L.o + c], vo = a[L.o + O + c], txo = a[L.to + c], tvo = a[L.to + O + c];
+    const T gx1 = a[L.gh2 + c], tgx1 = a[L.tgh2 + c];
+    const T d1 = dsilu(xo);
+    a[L.go + c] = gx1 * d1;
+    a[L.tgo + c] = tgx1 * d1 + gx1 * d2silu(xo) * txo;
+    T gvo = T(0), tgvo = T(0);
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      const T g = a[L.gv1 + r * O + c], tg = a[L.tgv1 + r * O + c];
+      const T v2 = a[L.v2 + r * O + c], tv2 = a[L.tv2 + r * O + c];
+      gvo += g * v2;
+      tgvo += tg * v2 + g * tv2;
+      a[L.gv2 + r * O + c] = g * vo;
+      a[L.tgv2 + r * O + c] = tg * vo + g * tvo;
+    }
+    a[L.go + O + c] = gvo;
+    a[L.tgo + O + c] = tgvo;
+  }
+  __syncthreads();
+  cols2<T, NT, 1, VEC>(W.u2w, H, 2 * O, sm + L.go, 0, nullptr, 0, 0, nullptr, 0, H, sm + L.gs, 0, P, nt, 0, false);
+  cols2<T, NT, 1, VEC>(W.u2w, H, 2 * O, sm + L.tgo, 0, nullptr, 0, 0, nullptr, 0, H, sm + L.tgs, 0, P, nt, 0, false);
+  __syncthreads();
+  for (int i = tid; i < NT * H; i += bs) {
+    const int t = i / H, c = i - t * H;
+    T* a = sm + t * P;
+    const T u = a[L.u + c], gsv = a[L.gs + c];
+    const T d1 = dsilu(u);
+    a[L.gu + c] = gsv * d1;
+    a[L.tgu + c] = a[L.tgs + c] * d1 + gsv * d2silu(u) * a[L.tu + c];
+  }
+  __syncthreads();
+  // U1^T: the x half of the tangent is d_x (global); the vec1 halves stay in LDS
+  cols2<T, NT, 1, VEC>(W.u1w, 2 * H, H, sm + L.tgu, 0, nullptr, 0, 0, nullptr, 0, H, dx + (size_t)n0 * H, 0, P, nt,
+                       (size_t)H, true);
+  cols2<T, NT, 1, VEC>(W.u1w + H, 2 * H, H, sm + L.gu, 0, nullptr, 0, 0, nullptr, 0, H, sm + L.gvec1, 0, P, nt, 0,
+                       false);
+  cols2<T, NT, 1, VEC>(W.u1w + H, 2 * H, H, sm + L.tgu, 0, nullptr, 0, 0, nullptr, 0, H, sm + L.tgvec1, 0, P, nt, 0,
+                       false);
+  __syncthreads();
+  for (int i = tid; i < NT * H; i += bs) {
+    const int t = i / H, c = i - t * H;
+    T* a = sm + t * P;
+    const T nrm = a[L.h + H + c];
+    const T inv = nrm > T(0) ? T(1) / nrm : T(0);
+    const T gn = a[L.gvec1 + c] * inv, tgn = a[L.tgvec1 + c] * inv, tn = a[L.th + H + c] * inv;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      const T b = a[L.vb + r * H + c];
+      a[L.gvb + r * H + c] = gn * b;
+      a[L.tgvb + r * H + c] = tgn * b + gn * (a[L.tvb + r * H + c] - b * tn);
+    }
+  }
+  __syncthreads();
+  // d_vec[a] = W1^T gdot_vb[a] + W2^T gdot_v2[a]
+  cols2<T, NT, 3, VEC>(W.w1, H, H, sm + L.tgvb, H, W.w2, H, O, sm + L.tgv2, O, H, dvec + (size_t)n0 * 3 * H, H, P,
+                       nt, (size_t)3 * H, true);
+  // d_g_y = ydot = P2[0][:] . s2dot
+  if (dgy && tid < nt) {
+    const T* a = sm + tid * P;
+    T acc = T(0);
+    for (int c = 0; c < Q; ++c) acc += W.p2w[c] * a[L.ts2 + c];
+    dgy[n0 + tid] = acc;
+  }
+  if (S2.vv == nullptr) return;
+  const Saves<T> S = S2.s;
+  // tangent half at atom n0 + t, plain half at n + n0 + t
+  const int wa1 = H + O, wa2 = Q + 1;
+  for (int i = tid; i < nt * 2 * 3 * wa1; i += bs) {
+    const int half = i / (nt * 3 * wa1), j = i - half * nt * 3 * wa1;
+    const int t = j / (3 * wa1), r = (j / wa1) % 3, c = j % wa1;
+    const T* a = sm + t * P;
+    const int gvb = half ? L.gvb : L.tgvb, gv2 = half ? L.gv2 : L.tgv2;
+    S.a1[((size_t)half * n + n0 + t) * 3 * wa1 + r * wa1 + c] = c < H ? a[gvb + r * H + c] : a[gv2 + r * O + c - H];
+  }
+  for (int i = tid; i < nt * 2 * 3 * H; i += bs) {
+    const int half = i / (nt * 3 * H), j = i - half * nt * 3 * H;
+    const int t = j / (3 * H), c = j % (3 * H);
+    S2.vv[((size_t)half * n + n0 + t) * 3 * H + c] = sm[t * P + (half ? L.tv : L.v) + c];
+  }
+  for (int i = tid; i < nt * 2 * 3 * wa2; i += bs) {
+    const int half = i / (nt * 3 * wa2), j = i - half * nt * 3 * wa2;
+    const int t = j / (3 * wa2), r = (j / wa2) % 3, c = j % wa2;
+    S.a2[((size_t)half * n + n0 + t) * 3 * wa2 + r * wa2 + c] =
+        c < Q ? sm[t * P + (half ? L.gvb2 : L.tgvb2) + r * Q + c] : T(0);
+  }
+  for (int i = tid; i < nt * 2 * 3 * O; i += bs) {
+    const int half = i / (nt * 3 * O), j = i - half * nt * 3 * O;
+    const int t = j / (3 * O), c = j % (3 * O);
+    S.v1[((size_t)half * n + n0 + t) * 3 * O + c] = sm[t * P + (half ? L.tv1 : L.v1) + c];
+  }
+  for (int i = tid; i < nt * 2 * (2 * H + 1); i += bs) {
+    const int half = i / (nt * (2 * H + 1)), j = i - half * nt * (2 * H + 1);
+    const int t = j / (2 * H + 1), c = j % (2 * H + 1);
+    S.hext[((size_t)half * n + n0 + t) * (2 * H + 1) + c] =
+        c < 2 * H ? sm[t * P + (half ? L.th : L.h) + c] : T(half ? 0 : 1);
+  }
+  for (int i = tid; i < nt * 2 * (H + 1); i += bs) {
+    const int half = i / (nt * (H + 1)), j = i - half * nt * (H + 1);
+    const int t = j / (H + 1), c = j % (H + 1);
+    S.sext[((size_t)half * n + n0 + t) * (H + 1) + c] = c < H ? sm[t * P + (half ? L.ts : L.s) + c] : T(half ? 0 : 1);
+    if (c < H) S.gu[((size_t)half * n + n0 + t) * H + c] = sm[t * P + (half ? L.gu : L.tgu) + c];
+  }
+  for (int i = tid; i < nt * 2 * 2 * O; i += bs) {
+    const int half = i / (nt * 2 * O), j = i - half * nt * 2 * O;
+    const int t = j / (2 * O), c = j % (2 * O);
+    S.go[((size_t)half * n + n0 + t) * 2 * O + c] = sm[t * P + (half ? L.go : L.tgo) + c];
+  }
+  for (int i = tid; i < nt * 2 * (2 * Q + 1); i += bs) {
+    const int half = i / (nt * (2 * Q + 1)), j = i - half * nt * (2 * Q + 1);
+    const int t = j / (2 * Q + 1), c = j % (2 * Q + 1);
+    S.h2ext[((size_t)half * n + n0 + t) * (2 * Q + 1) + c] =
+        c < 2 * Q ? sm[t * P + (half ? L.th2 : L.h2) + c] : T(half ? 0 : 1);
+  }
+  for (int i = tid; i < nt * 2 * (Q + 1); i += bs) {
+    const int half = i / (nt * (Q + 1)), j = i - half * nt * (Q + 1);
+    const int t = j / (Q + 1), c = j % (Q + 1);
+    S.s2ext[((size_t)half * n + n0 + t) * (Q + 1) + c] =
+        c < Q ? sm[t * P + (half ? L.ts2 : L.s2) + c] : T(half ? 0 : 1);
+    if (c < Q) S.gu2[((size_t)half * n + n0 + t) * Q + c] = sm[t * P + (half ? L.gu2 : L.tgu2) + c];
+  }
+  if (tid < 2 * nt) {
+    const int half = tid / nt, t = tid % nt;
+    S.go2[((size_t)half * n + n0 + t) * 2] = half ? gy[n0 + t] : T(0);
+    S.go2[((size_t)half * n + n0 + t) * 2 + 1] = T(0);
+  }
+}
+
 // g_x[n] = g_y[n] J_x[n],  g_vec[n] = g_y[n] J_vec[n]
 template <typename T>
 __global__ void k_scale(int n, int H, const T* __restrict__ gy, const T* __restrict__ jx,
@@ -543,6 +859,61 @@ extern "C" int tmdnet_eq_head_bwd_weights(int dtype, int n_atoms, int hidden, co
   if (dtype == TMDNET_F64)
     return launch_head<double>(n_atoms, hidden, x, vec, weights, nullptr, grad_x, grad_vec, grad_y, saves, nt,
                                smem, st);
+  return kUnsupported;
+}
+
+template <typename T>
+static int launch_head_hvp(int n, int H, const void* x, const void* vec, const void* const* w, const void* gy,
+                           const void* tx, const void* tvec, void* dx, void* dvec, void* dgy, void* const* sv,
+                           hipStream_t st) {
+  head::Saves2<T> S{};
+  if (sv)
+    S = head::Saves2<T>{{(T*)sv[0], (T*)sv[1], (T*)sv[2], (T*)sv[3], (T*)sv[4], (T*)sv[5], (T*)sv[6], (T*)sv[7],
+                         (T*)sv[8], (T*)sv[9], (T*)sv[10]},
+                        (T*)sv[11]};
+  head::Weights<T> W{(const T*)w[0], (const T*)w[1], (const T*)w[2], (const T*)w[3],
+                     (const T*)w[4], (const T*)w[5], (const T*)w[6], (const T*)w[7],
+                     (const T*)w[8], (const T*)w[9], (const T*)w[10], (const T*)w[11]};
+  const size_t per = (size_t)head::Layout2(H).P2 * sizeof(T);
+  // one atom per workgroup below 2048 atoms (latency-bound chain), two above when they fit 64 KB
+  const int nt = (n >= 2048 && 2 * per <= 64 * 1024) ? 2 : 1;
+  if (per > 64 * 1024) return kUnsupported;
+  const size_t smem = nt * per;
+  dim3 g((n + nt - 1) / nt), b(256);
+  const bool vec4 = H % 8 == 0;
+#define TMD_HVP_LAUNCH(NT_, V_)                                                                            \
+  hipLaunchKernelGGL((head::k_eq_head_hvp<T, NT_, V_>), g, b, smem, st, n, H, (const T*)x, (const T*)vec, W, \
+                     (const T*)gy, (const T*)tx, (const T*)tvec, (T*)dx, (T*)dvec, (T*)dgy, S)
+  if (vec4) {
+    if (nt == 2) TMD_HVP_LAUNCH(2, true);
+    else TMD_HVP_LAUNCH(1, true);
+  } else {
+    if (nt == 2) TMD_HVP_LAUNCH(2, false);
+    else TMD_HVP_LAUNCH(1, false);
+  }
+#undef TMD_HVP_LAUNCH
+  return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
+}
+
+extern "C" int tmdnet_eq_head_hvp(int dtype, int n_atoms, int hidden, const void* x, const void* vec,
+                                  const void* const* weights, const void* grad_y, const void* tan_x,
+                                  const void* tan_vec, void* d_x, void* d_vec, void* d_grad_y,
+                                  void* const* saves, void* stream) {
+  if (n_atoms < 0 || hidden < 4 || hidden % 4 || !x || !vec || !weights || !grad_y || !d_x || !d_vec)
+    return kBadArgument;
+  for (int i = 0; i < 12; ++i)
+    if (!weights[i]) return kBadArgument;
+  if (saves)
+    for (int i = 0; i < 12; ++i)
+      if (!saves[i]) return kBadArgument;
+  if (n_atoms == 0) return kOk;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == TMDNET_F32)
+    return launch_head_hvp<float>(n_atoms, hidden, x, vec, weights, grad_y, tan_x, tan_vec, d_x, d_vec, d_grad_y,
+                                  saves, st);
+  if (dtype == TMDNET_F64)
+    return launch_head_hvp<double>(n_atoms, hidden, x, vec, weights, grad_y, tan_x, tan_vec, d_x, d_vec, d_grad_y,
+                                   saves, st);
   return kUnsupported;
 }
 

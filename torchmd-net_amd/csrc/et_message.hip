@@ -864,6 +864,11 @@ template <typename T> struct NbArgs {
   const T* xself; T* oself;  // optional row copy xself[t] -> oself[t] (stride ldo): the left half
   const T* gout; int ldg;  // incoming gradient rows
   T* gx; T* gw; T* gC;
+  // second order (k_nb_bwd2_*): cotangents of gx / gw / gC (NULL = 0), their VJP outputs, and the
+  // transpose map tr[e] = index of the reversed edge
+  const T* ggx; const T* ggw; const T* ggC;
+  T* dgout; T* dx; T* dw; T* dC;
+  const int32_t* tr;
 };
 
 // Edge loop of the neighbour-embedding kernels: a row's src / C for up to 64 edges arrive in one
@@ -1003,6 +1008,97 @@ __global__ __launch_bounds__(256) void k_nb_bwd_src(NbArgs<T> A) {
   if (on) stv<T, V>(A.gx + (size_t)j * A.H + c0, acc);
 }
 
+// Second order of the neighbour embedding (force-matching training; the forward is trilinear in
+// (x, w, C), so its backward's VJP for cotangents (ggx, ggw, ggC) of (gx, gw, gC) is):
+//   d_gout[t] = sum_{e in row t} ggx[s] w_e C_e + x[s] (ggw_e C_e + ggC_e w_e)
+//   d_w[e]    = C_e ggx[s] gout[t] + ggC_e gout[t] x[s]
+//   d_C[e]    = sum_c gout[t] (ggx[s] w_e + ggw_e x[s])                       (destination pass)
+//   d_x[s]    = sum_{e: src_e = s} gout[dst_e] (ggw_e C_e + ggC_e w_e)         (source pass: the
+//               edges leaving s are the reverses tr[e'] of the edges e' of row s)
+// Self loops (and padding) contribute nothing, as in the forward.
+template <typename T, int V>
+__global__ __launch_bounds__(256) void k_nb_bwd2_dst(NbArgs<T> A) {
+  const int t = blockIdx.x * (blockDim.x / TMD_WAVE) + threadIdx.x / TMD_WAVE;
+  if (t >= A.n) return;
+  const int lane = lane_id();
+  const bool on = lane < A.L;
+  const int c0 = on ? lane * V : 0;
+  T go[V], acc[V];
+  ldv<T, V>(go, A.gout + (size_t)t * A.ldg + c0);
+  zero(acc);
+  nb_edges(A, t, [&](int k0, const int (&sq)[NB_U], const T (&cq)[NB_U]) {
+    T xs[NB_U][V], wk[NB_U][V], gxs[NB_U][V], gwk[NB_U][V], gck[NB_U], dc[NB_U];
+#pragma unroll
+    for (int u = 0; u < NB_U; ++u) {
+      const bool valid = sq[u] >= 0;
+      const bool live = valid && sq[u] != t;
+      const int s = live ? sq[u] : t, k = valid ? k0 + u : k0;
+      ldv<T, V>(xs[u], A.x + (size_t)s * A.ldx + c0);
+      ldv<T, V>(wk[u], A.w + (size_t)k * A.ldw + c0);
+      if (A.ggx) ldv<T, V>(gxs[u], A.ggx + (size_t)s * A.H + c0); else zero(gxs[u]);
+      if (A.ggw) ldv<T, V>(gwk[u], A.ggw + (size_t)k * A.H + c0); else zero(gwk[u]);
+      gck[u] = (A.ggC && live) ? A.ggC[k] : T(0);
+    }
+#pragma unroll
+    for (int u = 0; u < NB_U; ++u) {
+      const bool valid = sq[u] >= 0;
+      const bool live = valid && sq[u] != t;
+      const T ce = live ? cq[u] : T(0), gc = gck[u];
+      T dw[V];
+      dc[u] = T(0);
+#pragma unroll
+      for (int i = 0; i < V; ++i) {
+        acc[i] += ce * (gxs[u][i] * wk[u][i] + xs[u][i] * gwk[u][i]) + gc * xs[u][i] * wk[u][i];
+        dw[i] = live ? go[i] * (ce * gxs[u][i] + gc * xs[u][i]) : T(0);
+        dc[u] += go[i] * (gxs[u][i] * wk[u][i] + gwk[u][i] * xs[u][i]);
+      }
+      if (!live) dc[u] = T(0);
+      if (on && valid && A.dw) stv<T, V>(A.dw + (size_t)(k0 + u) * A.H + c0, dw);
+    }
+    if (A.dC) {
+#pragma unroll
+      for (int u = 0; u < NB_U; ++u) dc[u] = wave_sum(on ? dc[u] : T(0));
+      if (lane == 0) {
+#pragma unroll
+        for (int u = 0; u < NB_U; ++u)
+          if (sq[u] >= 0) A.dC[k0 + u] = dc[u];
+      }
+    }
+  });
+  if (on && A.dgout) stv<T, V>(A.dgout + (size_t)t * A.H + c0, acc);
+}
+
+template <typename T, int V>
+__global__ __launch_bounds__(256) void k_nb_bwd2_src(NbArgs<T> A) {
+  const int j = blockIdx.x * (blockDim.x / TMD_WAVE) + threadIdx.x / TMD_WAVE;
+  if (j >= A.n) return;
+  const int lane = lane_id();
+  const bool on = lane < A.L;
+  const int c0 = on ? lane * V : 0;
+  T acc[V];
+  zero(acc);
+  nb_edges(A, j, [&](int k0, const int (&sq)[NB_U], const T (&cq)[NB_U]) {
+    T gm[NB_U][V], wk[NB_U][V], gwk[NB_U][V], ck[NB_U], gck[NB_U];
+#pragma unroll
+    for (int u = 0; u < NB_U; ++u) {
+      const bool live = sq[u] >= 0 && sq[u] != j;
+      const int m = live ? sq[u] : j;
+      const int k = live ? A.tr[k0 + u] : k0;  // the edge j -> m
+      TMD_DCHECK(!live || (k >= 0 && k < A.cap));
+      ldv<T, V>(gm[u], A.gout + (size_t)m * A.ldg + c0);
+      ldv<T, V>(wk[u], A.w + (size_t)k * A.ldw + c0);
+      if (A.ggw) ldv<T, V>(gwk[u], A.ggw + (size_t)k * A.H + c0); else zero(gwk[u]);
+      ck[u] = live ? A.C[k] : T(0);
+      gck[u] = (live && A.ggC) ? A.ggC[k] : T(0);
+    }
+#pragma unroll
+    for (int u = 0; u < NB_U; ++u)
+#pragma unroll
+      for (int i = 0; i < V; ++i) acc[i] += gm[u][i] * (gwk[u][i] * ck[u] + gck[u] * wk[u][i]);
+  });
+  if (on) stv<T, V>(A.dx + (size_t)j * A.H + c0, acc);
+}
+
 // ------------------------------------------------------------------ host helpers
 static inline int pick_vec(int H) {
   if (H % 256 == 0) return 4;
@@ -1087,6 +1183,8 @@ static int et_launch(int V, const Args<T>& A, hipStream_t st) {
 template <typename T, int V> struct KNbFwd { static constexpr auto fn = k_nb_fwd<T, V>; };
 template <typename T, int V> struct KNbDst { static constexpr auto fn = k_nb_bwd_dst<T, V>; };
 template <typename T, int V> struct KNbSrc { static constexpr auto fn = k_nb_bwd_src<T, V>; };
+template <typename T, int V> struct KNb2Dst { static constexpr auto fn = k_nb_bwd2_dst<T, V>; };
+template <typename T, int V> struct KNb2Src { static constexpr auto fn = k_nb_bwd2_src<T, V>; };
 
 template <typename T>
 static int setup(Args<T>& A, int n, int H, int heads, const int32_t* row_ptr, const int32_t* src,
@@ -1338,6 +1436,46 @@ extern "C" int tmdnet_nbr_embed_bwd(int dtype, int n_nodes, int hidden, const in
   hipStream_t st = (hipStream_t)stream;
   if (dtype == TMDNET_F32) return nb_bwd_t<float>(n_nodes, hidden, row_ptr, src, max_pairs, x, ld_x, w, ld_w, cutoff, grad_out, ld_grad_out, gx, gw, gcut, st);
   if (dtype == TMDNET_F64) return nb_bwd_t<double>(n_nodes, hidden, row_ptr, src, max_pairs, x, ld_x, w, ld_w, cutoff, grad_out, ld_grad_out, gx, gw, gcut, st);
+  return kUnsupported;
+}
+
+template <typename T>
+static int nb_bwd2_t(int n, int H, const int32_t* row_ptr, const int32_t* src, const int32_t* tr, int cap,
+                     const void* x, int ldx, const void* w, int ldw, const void* C, const void* gout, int ldg,
+                     const void* ggx, const void* ggw, const void* ggC, void* dgout, void* dx, void* dw, void* dC,
+                     hipStream_t st) {
+  et::NbArgs<T> A;
+  int V;
+  int rc = et::nb_setup<T>(A, n, H, row_ptr, src, cap, x, ldx, w, ldw, C, V);
+  if (rc) return rc;
+  if (!gout || !C || (dx && !tr)) return kBadArgument;
+  A.gout = (const T*)gout;
+  A.ldg = ldg ? ldg : H;
+  if (A.ldg < H || !et::aligned<T>(gout, A.ldg, V) || !et::aligned<T>(ggx, H, V) || !et::aligned<T>(ggw, H, V))
+    return kBadArgument;
+  A.ggx = (const T*)ggx; A.ggw = (const T*)ggw; A.ggC = (const T*)ggC;
+  A.dgout = (T*)dgout; A.dx = (T*)dx; A.dw = (T*)dw; A.dC = (T*)dC; A.tr = tr;
+  if (dgout || dw || dC) {
+    rc = et::launch_v<T, et::KNb2Dst>(V, n, A, st);
+    if (rc) return rc;
+  }
+  if (dx) return et::launch_v<T, et::KNb2Src>(V, n, A, st);
+  return kOk;
+}
+
+extern "C" int tmdnet_nbr_embed_bwd2(int dtype, int n_nodes, int hidden, const int32_t* row_ptr,
+                                     const int32_t* src, const int32_t* transpose, int max_pairs,
+                                     const void* x, int ld_x, const void* w, int ld_w, const void* cutoff,
+                                     const void* grad_out, int ld_grad_out, const void* gg_x, const void* gg_w,
+                                     const void* gg_cut, void* d_grad_out, void* d_x, void* d_w, void* d_cut,
+                                     void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+#define TMD_NB2(T)                                                                                              \
+  return nb_bwd2_t<T>(n_nodes, hidden, row_ptr, src, transpose, max_pairs, x, ld_x, w, ld_w, cutoff, grad_out, \
+                      ld_grad_out, gg_x, gg_w, gg_cut, d_grad_out, d_x, d_w, d_cut, st)
+  if (dtype == TMDNET_F32) TMD_NB2(float);
+  if (dtype == TMDNET_F64) TMD_NB2(double);
+#undef TMD_NB2
   return kUnsupported;
 }
 

@@ -39,6 +39,7 @@ SIGNATURES = {
     "tmdnet_edge_geom_fwd": (I, [I, I, I, I, P, P, P, P, P, P, D, D, P, P, P, P]),
     "tmdnet_edge_geom_fwd_rows": (I, [I, I, I, I, P, P, P, P, P, P, D, D, P, P, P, P, I, P, P]),
     "tmdnet_edge_geom_bwd": (I, [I, I, I, I, P, P, P, P, P, P, D, D, P, P, P, P, P, P]),
+    "tmdnet_edge_geom_bwd2": (I, [I, I, I, I, P, P, P, P, P, P, D, D, P, P, P, P, P, P, P, P, P, P, P]),
     "tmdnet_et_message_fwd": (I, [I, I, I, I, P, P, I, P, I, P, I, P, I, P, P, I, P, I, P, P, P, P, I, P, P,
                                   P]),
     "tmdnet_et_message_bwd": (I, [I, I, I, I, P, P, I, P, I, P, I, P, I, P, P, I, P, I, P, P, P, P,
@@ -56,8 +57,10 @@ SIGNATURES = {
     "tmdnet_eq_head_fwd": (I, [I, I, I, P, P, P, P, P, P, P]),
     "tmdnet_eq_head_bwd": (I, [I, I, I, P, P, P, P, P, P]),
     "tmdnet_eq_head_bwd_weights": (I, [I, I, I, P, P, P, P, P, P, P, P]),
+    "tmdnet_eq_head_hvp": (I, [I, I, I, P, P, P, P, P, P, P, P, P, P, P]),
     "tmdnet_nbr_embed_fwd": (I, [I, I, I, P, P, I, P, I, P, I, P, P, I, P, P, P]),
     "tmdnet_nbr_embed_bwd": (I, [I, I, I, P, P, I, P, I, P, I, P, P, I, P, P, P, P]),
+    "tmdnet_nbr_embed_bwd2": (I, [I, I, I, P, P, P, I, P, I, P, I, P, P, I, P, P, P, P, P, P, P, P]),
     "tmdnet_tn_embed_fwd": (I, [I, I, I, P, P, I, D, P, I, P, P, P, I, P, P, P, P]),
     "tmdnet_tn_embed_bwd": (I, [I, I, I, P, P, I, D, P, I, P, P, P, I, P, P, P, P, P, P, P, P, P]),
     "tmdnet_tn_message_fwd": (I, [I, I, I, P, P, I, D, P, I, P, I, P, P, P]),

@@ -8,12 +8,17 @@ force-loss training; that second-order step is expressed with composite PyTorch 
 """
 import ctypes
 import math
+import os
 
 import torch
 import torch.nn.functional as F
 from torch.autograd import Function
 
 from . import _native as nat
+
+# second orders written out by hand ("hand", default) or autograd over the composites ("composite":
+# the reference's double differentiation, kept for A/B checks)
+HEAD_SECOND_ORDER = os.environ.get("TMDNET_HEAD_SECOND_ORDER", "hand")
 
 # Optional live kernel timing (bench.py): when a list is installed here, the ET message forward
 # launches are bracketed by HIP events recorded on the launching stream.
@@ -446,8 +451,28 @@ class _EdgeGeomBwd(Function):
         deltas, dist, gf, gC, gu, mu, beta = ctx.saved_tensors
         cl, cu, rbf_type = ctx.cfg
         graph = ctx.graph
-        selfmask = graph.src == graph.dst
         _create = torch.is_grad_enabled()  # third order only if the caller builds a graph
+        if not _create and HEAD_SECOND_ORDER != "composite":
+            # tmdnet_edge_geom_bwd2: only the gradients the engine will consume (a training step's
+            # loss.backward(inputs=params) never reaches the positions: no d_dist / d_deltas)
+            nf = iter(ctx.next_functions)
+            want = []
+            for i, t in enumerate((deltas, dist, gf, gC, gu)):
+                node = next(nf)[0] if i < 2 or t is not None else None
+                want.append(t is not None and ctx.needs_input_grad[i] and _will_run(node))
+            if not any(want):
+                return (None,) * 11
+            o = [torch.empty_like(t) if w else None for t, w in zip((deltas, dist, gf, gC, gu), want)]
+            lib = nat.load()
+            rc = lib.tmdnet_edge_geom_bwd2(
+                nat.dtype_code(dist.dtype), dist.shape[0], mu.shape[0], rbf_type, nat.ptr(graph.src),
+                nat.ptr(graph.dst), nat.ptr(deltas), nat.ptr(dist), nat.ptr(mu), nat.ptr(beta), float(cl), float(cu),
+                nat.ptr(gf), nat.ptr(gC), nat.ptr(gu), nat.ptr(None if gg_dl is None else gg_dl.contiguous()),
+                nat.ptr(None if gg_r is None else gg_r.contiguous()), nat.ptr(o[2]), nat.ptr(o[3]), nat.ptr(o[4]),
+                nat.ptr(o[1]), nat.ptr(o[0]), nat.stream(dist.device))
+            nat.check(rc, "tmdnet_edge_geom_bwd2")
+            return (o[0], o[1], o[2], o[3], o[4], None, None, None, None, None, None)
+        selfmask = graph.src == graph.dst
         with torch.enable_grad():
             dl = deltas.detach().requires_grad_(True)
             r = dist.detach().requires_grad_(True)
@@ -822,8 +847,30 @@ class _NbrEmbedBwd(Function):
     def backward(ctx, ggx, ggw, ggC):
         gout, x, w, C = ctx.saved_tensors
         graph = ctx.graph
-        src, dst = graph.src.long(), graph.dst.long()
         _create = torch.is_grad_enabled()  # third order only if the caller builds a graph
+        if not _create and HEAD_SECOND_ORDER != "composite" and graph.transpose is not None:
+            nodes = [e[0] for e in ctx.next_functions]  # one per tensor input: gout, x, w, C
+            want = [bool(ctx.needs_input_grad[i]) and _will_run(nodes[i]) for i in range(4)]
+            if not any(want):
+                return (None,) * 5
+            N, H = x.shape
+            E = graph.n_edges
+            d_go = torch.empty((N, H), dtype=x.dtype, device=x.device) if want[0] else None
+            d_x = torch.empty((N, H), dtype=x.dtype, device=x.device) if want[1] else None
+            # edge outputs: the static-capacity padding slots stay zero (one zero-filled buffer)
+            zb = graph.alloc_edge_grad((E * (H + 1),), x.dtype, x.device) if (want[2] or want[3]) else None
+            d_w = zb[:E * H].view(E, H) if want[2] else None
+            d_C = zb[E * H:] if want[3] else None
+            lib = nat.load()
+            rc = lib.tmdnet_nbr_embed_bwd2(
+                nat.dtype_code(x.dtype), N, H, nat.ptr(graph.row_ptr), nat.ptr(graph.src), nat.ptr(graph.transpose),
+                E, nat.ptr(x), _ld(x), nat.ptr(w), _ld(w), nat.ptr(C), nat.ptr(gout), gout.stride(0),
+                nat.ptr(None if ggx is None else ggx.contiguous()), nat.ptr(None if ggw is None else ggw.contiguous()),
+                nat.ptr(None if ggC is None else ggC.contiguous()), nat.ptr(d_go), nat.ptr(d_x), nat.ptr(d_w),
+                nat.ptr(d_C), nat.stream(x.device))
+            nat.check(rc, "tmdnet_nbr_embed_bwd2")
+            return d_go, d_x, d_w, d_C, None
+        src, dst = graph.src.long(), graph.dst.long()
         with torch.enable_grad():
             leaves = [t.detach().requires_grad_(True) for t in (gout, x, w, C)]
             go, x_, w_, C_ = leaves
@@ -1392,6 +1439,7 @@ class _EqHeadBwd(Function):
             rc = lib.tmdnet_eq_head_bwd(nat.dtype_code(x.dtype), N, H, nat.ptr(gy), nat.ptr(jx), nat.ptr(jv),
                                         nat.ptr(gx), nat.ptr(gv), nat.stream(x.device))
             nat.check(rc, "tmdnet_eq_head_bwd")
+        ctx.set_materialize_grads(False)  # unused outputs (the weight gradients) stay None
         ctx.save_for_backward(gy, x, vec, *params)
         return (gx, gv) + tuple(g_params)
 
@@ -1399,6 +1447,12 @@ class _EqHeadBwd(Function):
     def backward(ctx, ggx, ggv, *ggp):
         saved = ctx.saved_tensors
         _create = torch.is_grad_enabled()  # third order only if the caller builds a graph
+        if not _create and all(g is None for g in ggp) and HEAD_SECOND_ORDER != "composite":
+            gy, x, vec, *params = saved
+            need_p = [ctx.needs_input_grad[6 + i] for i in range(len(params))]
+            d_gy, d_x, d_vec, d_p = eq_head_hvp(x, vec, params, gy, ggx, ggv, ctx.needs_input_grad[1], any(need_p))
+            d_p = [g if w else None for g, w in zip(d_p, need_p)] if d_p is not None else [None] * len(params)
+            return (None, d_gy, None, None, d_x, d_vec) + tuple(d_p)
         with torch.enable_grad():
             leaves = [t.detach().requires_grad_(True) for t in saved]
             gy, x, vec = leaves[:3]
@@ -1412,6 +1466,49 @@ class _EqHeadBwd(Function):
                                          create_graph=_create, allow_unused=True)
         d_gy, d_x, d_vec = second[:3]
         return (None, d_gy, None, None, d_x, d_vec) + tuple(second[3:])
+
+
+def eq_head_hvp(x, vec, params, gy, tx, tv, want_gy=True, want_w=True):
+    """Second order of the head's backward (tmdnet_eq_head_hvp, forward-over-reverse in one kernel):
+    returns (d_gy [N,1] or None, d_x, d_vec, [12 weight terms] or None) for the cotangents (tx, tv)
+    of (g_x, g_vec) = gy * J(x, vec); each weight term is one GEMM over the kernel's per-atom
+    factors ([tangent rows ; plain rows], the layouts of _eq_head_weight_grads)."""
+    lib = nat.load()
+    N, H = x.shape
+    O = Q = H // 2
+    o = dict(dtype=x.dtype, device=x.device)
+    d_x = torch.empty_like(x)
+    d_vec = torch.empty_like(vec)
+    d_gy = torch.empty((N, 1), **o) if want_gy else None
+    tx = None if tx is None else tx.contiguous()
+    tv = None if tv is None else tv.contiguous()
+    saves = None
+    sv = None
+    if want_w:
+        n2 = 2 * N
+        saves = [torch.empty((n2, 3, H + O), **o), torch.empty((n2, H), **o), torch.empty((n2, 2 * H + 1), **o),
+                 torch.empty((n2, 2 * O), **o), torch.empty((n2, H + 1), **o), torch.empty((n2, 3, Q + 1), **o),
+                 torch.empty((n2, 3, O), **o), torch.empty((n2, Q), **o), torch.empty((n2, 2 * Q + 1), **o),
+                 torch.empty((n2, 2), **o), torch.empty((n2, Q + 1), **o), torch.empty((n2, 3, H), **o)]
+        sv = (ctypes.c_void_p * 12)(*[t.data_ptr() for t in saves])
+    ws = (ctypes.c_void_p * 12)(*[p.data_ptr() for p in params])
+    rc = lib.tmdnet_eq_head_hvp(nat.dtype_code(x.dtype), N, H, nat.ptr(x), nat.ptr(vec), ws, nat.ptr(gy.contiguous()),
+                                nat.ptr(tx), nat.ptr(tv), nat.ptr(d_x), nat.ptr(d_vec), nat.ptr(d_gy), sv,
+                                nat.stream(x.device))
+    nat.check(rc, "tmdnet_eq_head_hvp")
+    if saves is None:
+        return d_gy, d_x, d_vec, None
+    a1, gu, hext, go, sext, a2, v1, gu2, h2ext, go2, s2ext, vv = saves
+    n2 = 2 * N
+    dw12 = a1.view(3 * n2, H + O).t() @ vv.view(3 * n2, H)
+    du1 = gu.t() @ hext
+    du2 = go.t() @ sext
+    dv12 = a2.view(3 * n2, Q + 1).t() @ v1.view(3 * n2, O)
+    dp1 = gu2.t() @ h2ext
+    dp2 = go2.t() @ s2ext
+    d_p = [dw12[:H], dw12[H:], du1[:, :2 * H], du1[:, 2 * H], du2[:, :H], du2[:, H],
+           dv12[:Q], dv12[Q:], dp1[:, :2 * Q], dp1[:, 2 * Q], dp2[:, :Q], dp2[:, Q]]
+    return d_gy, d_x, d_vec, d_p
 
 
 def eq_scalar_head(x, vec, blocks):
