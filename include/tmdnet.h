@@ -31,6 +31,9 @@ enum { TMDNET_ACC_VEC_RESIDUAL = 1, TMDNET_ACC_EDGE = 2 };
  * Planar rows make every 16-byte-per-lane load of a row segment contiguous (measured 4-7 % on the C5
  * forward).  Gradients of v / pv are written in the same layout. */
 enum { TMDNET_ET_V_PLANAR = 4 };
+/* tmdnet_et_message_bwd2_ex flags: accumulate d_cut / d_unit (ACC_EDGE) and d_grad_vec (ACC_GVEC)
+ * into the caller's buffers instead of overwriting them. */
+enum { TMDNET_BWD2_ACC_EDGE = 8, TMDNET_BWD2_ACC_GVEC = 16 };
 
 /* ------------------------------------------------------------------------------------------
  * Neighbour list.  Replaces torchmdnet_neighbors::get_neighbor_pairs
@@ -208,6 +211,23 @@ int tmdnet_et_message_bwd2(int dtype, int n_nodes, int hidden, int heads, const 
                            void* d_grad_x, void* d_grad_vec, void* d_q, void* d_k, void* d_v,
                            void* d_vec, void* d_pk, void* d_pv, void* d_cut, void* d_unit, int flags,
                            void* stream);
+/* tmdnet_et_message_bwd2 with row strides for the node cotangents / outputs (0 = dense) -- so the
+ * cotangents can be column blocks of one [N][5H] buffer and d_q | d_k | d_v written into one -- and
+ * a DETERMINISTIC source pass: with transpose (the reversed-edge map of tmdnet_nl_build) and
+ * edge_scratch ([max_pairs][7][hidden] elements, 16-byte aligned) the source-node terms of every edge
+ * are stored as a scratch row and summed per node over the reversed edges by a second kernel (no
+ * atomics; d_k, d_v, d_vec are overwritten, no zero fill needed).  transpose / edge_scratch NULL:
+ * atomics as tmdnet_et_message_bwd2.  flags: TMDNET_ET_V_PLANAR | TMDNET_BWD2_ACC_*. */
+int tmdnet_et_message_bwd2_ex(
+    int dtype, int n_nodes, int hidden, int heads, const int32_t* row_ptr, const int32_t* src,
+    const int32_t* transpose, int max_pairs, const void* q, int ld_q, const void* k, int ld_k,
+    const void* v, int ld_v, const void* vec_in, const void* pk, int ld_pk, const void* pv, int ld_pv,
+    const void* cutoff, const void* unit, const void* grad_x, const void* grad_vec, const void* gg_q,
+    int ld_ggq, const void* gg_k, int ld_ggk, const void* gg_v, int ld_ggv, const void* gg_vec,
+    const void* gg_pk, int ld_ggpk, const void* gg_pv, int ld_ggpv, const void* gg_cut,
+    const void* gg_unit, void* d_grad_x, void* d_grad_vec, void* d_q, int ld_dq, void* d_k, int ld_dk,
+    void* d_v, int ld_dv, void* d_vec, void* d_pk, int ld_dpk, void* d_pv, int ld_dpv, void* d_cut,
+    void* d_unit, void* edge_scratch, int flags, void* stream);
 
 /* ET layer epilogue (reference torchmd_et.py:278-280, 309-311 + residuals 181-184), fused:
  *   vecp = vec_proj(vec) [N][3][3H] = [v1|v2|v3], o = o_proj(x_agg) [N][3H] = [o1|o2|o3]

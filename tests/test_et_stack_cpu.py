@@ -177,8 +177,28 @@ def _fake_bwd2(ctx, ggs):
     return kernels._ETMessageBwd.composite_backward(ctx, *ggs)
 
 
-def _fake_bwd2_launch(q, k, v, vec, pk, pv, C, u, graph, heads, gx, gvec, ggs, flags=0):
-    """tmdnet_et_message_bwd2 restated: the VJP of the message backward by double autograd."""
+def _fake_bwd2_launch(q, k, v, vec, pk, pv, C, u, graph, heads, gx, gvec, ggs, flags=0, out=None):
+    """tmdnet_et_message_bwd2_ex restated: the VJP of the message backward by double autograd (``out``
+    buffers filled / accumulated as the launch wrapper does)."""
+    res = _fake_bwd2_core(q, k, v, vec, pk, pv, C, u, graph, heads, gx, gvec, ggs)
+    if not out:
+        return res
+    d_gx, d_gvec, d_q, d_k, d_v, d_vec, d_pk, d_pv, d_C, d_u = res
+    if "qkv" in out:
+        out["qkv"].copy_(torch.cat((d_q, d_k, d_v), 1))
+    if "pkv" in out:
+        out["pkv"].copy_(torch.cat([t for t in (d_pk, d_pv) if t is not None], 1))
+    if "C" in out:
+        out["C"].add_(d_C)
+        out["u"].add_(d_u)
+        d_C, d_u = out["C"], out["u"]
+    if "gvec" in out:
+        out["gvec"].add_(d_gvec)
+        d_gvec = out["gvec"]
+    return d_gx, d_gvec, d_q, d_k, d_v, d_vec, d_pk, d_pv, d_C, d_u
+
+
+def _fake_bwd2_core(q, k, v, vec, pk, pv, C, u, graph, heads, gx, gvec, ggs):
     N, H = q.shape
     vec_ = torch.zeros((N, 3, H), dtype=q.dtype) if vec is None else vec
     with torch.enable_grad():

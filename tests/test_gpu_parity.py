@@ -663,11 +663,15 @@ def test_graphed_tensornet_matches_eager(static_shapes):
     gm.release()
 
 
+@pytest.mark.parametrize("src_pass", ["deterministic", "atomic"])
 @pytest.mark.parametrize("infl", ["both", "none"])
-def test_et_message_second_order_kernel_matches_composite(infl):
-    """tmdnet_et_message_bwd2 (the VJP of the HIP first backward) == double backward through the
-    PyTorch restatement, fp64, all ten inputs (gx, gvec, q, k, v, vec, pk, pv, C, u)."""
+def test_et_message_second_order_kernel_matches_composite(infl, src_pass, monkeypatch):
+    """tmdnet_et_message_bwd2_ex (the VJP of the HIP first backward) == double backward through the
+    PyTorch restatement, fp64, all ten inputs (gx, gvec, q, k, v, vec, pk, pv, C, u); the source-node
+    terms summed by the scratch-row source pass over the reversed edges, or by atomics."""
     from torchmdnet import kernels
+    if src_pass == "atomic":
+        monkeypatch.setattr(kernels, "BWD2_SCRATCH_MAX_BYTES", 0)
     torch.manual_seed(0)
     z, pos, batch = O.qm9_like(2)
     pos = pos.to(DEV)

@@ -662,15 +662,23 @@ __global__ __launch_bounds__(256, (bwd_min_waves<T, V, DR>())) void k_bwd_both(A
 //   d/dv2_s   += G2 ggpv2 dv2' + U dv2
 //   d/dpv2     = G2 (ggv2 dv2' + ggpv2 v2 dv2'') + U v2 dv2'
 // One destination-row pass: destination-node terms accumulate in registers, per-edge terms are
-// stored, source-node terms (k, v, vec) are added with atomics into zero-initialised buffers (this
-// path runs only in training, where the reference's CUDA scatter is atomic as well).
+// stored.  The source-node terms (k, v, vec) of edge e are either stored as a row of the per-edge
+// scratch src[e] = [k (H) | v (3H, the v row layout) | vec (3H)] and summed per source node by
+// k_bwd2_src over the reversed edges (deterministic, no atomics, no zero fills), or -- without a
+// transpose map / scratch -- added with atomics into zero-initialised buffers.
 template <typename T> struct Args2 {
   Args<T> a;                                       // primal inputs (q, k, v, vec, pk, pv, C, u) + gx, gvec
   const T* ggq; const T* ggk; const T* ggv; const T* ggw;   // node cotangents ([N][H], [N][H], [N][3H], [N][3][H])
+  int ldggq, ldggk, ldggv;                                  // (row strides)
   const T* ggpk; int ldggpk; const T* ggpv; int ldggpv;     // edge cotangents
   const T* ggC; const T* ggu;
-  T* o_gx; T* o_gvec; T* o_q; T* o_k; T* o_v; T* o_vec;       // node outputs (o_k, o_v, o_vec: atomics)
+  T* o_gx; T* o_gvec; T* o_q; T* o_k; T* o_v; T* o_vec;       // node outputs
+  int ldoq, ldok, ldov;
   T* o_pk; T* o_pv; T* o_C; T* o_u;                          // edge outputs ([E][H], [E][3H], [E], [E][3])
+  int ldopk, ldopv;
+  T* o_src;               // per-edge source terms [E][7H] (NULL: atomics)
+  const int32_t* tr;      // transpose map (k_bwd2_src)
+  int acc_edge, acc_gvec; // accumulate o_C / o_u (and o_gvec) into the caller's buffers
 };
 
 template <typename T, int V, int S>
@@ -685,11 +693,15 @@ __global__ __launch_bounds__(256) void k_bwd2(Args2<T> B) {
     const long long tid = (long long)blockIdx.x * blockDim.x + threadIdx.x, nth = (long long)gridDim.x * blockDim.x;
     if (rows > 0) {
       if (B.o_pk)
-        for (long long i = tid; i < rows * A.H; i += nth) B.o_pk[(size_t)e0 * A.H + i] = T(0);
+        for (long long i = tid; i < rows * A.H; i += nth)
+          B.o_pk[(size_t)(e0 + i / A.H) * B.ldopk + i % A.H] = T(0);
       if (B.o_pv)
-        for (long long i = tid; i < rows * 3 * A.H; i += nth) B.o_pv[(size_t)e0 * 3 * A.H + i] = T(0);
-      for (long long i = tid; i < rows; i += nth) B.o_C[e0 + i] = T(0);
-      for (long long i = tid; i < rows * 3; i += nth) B.o_u[3 * (size_t)e0 + i] = T(0);
+        for (long long i = tid; i < rows * 3 * A.H; i += nth)
+          B.o_pv[(size_t)(e0 + i / (3 * A.H)) * B.ldopv + i % (3 * A.H)] = T(0);
+      if (!B.acc_edge) {  // accumulating: the caller's padding rows stay as they are (zero)
+        for (long long i = tid; i < rows; i += nth) B.o_C[e0 + i] = T(0);
+        for (long long i = tid; i < rows * 3; i += nth) B.o_u[3 * (size_t)e0 + i] = T(0);
+      }
     }
   }
   if (S == 1 && t < 0) return;
@@ -708,7 +720,7 @@ __global__ __launch_bounds__(256) void k_bwd2(Args2<T> B) {
   ldv<T, V>(g0, A.gvec + (size_t)t * 3 * A.H + c0);
   ldv<T, V>(g1, A.gvec + (size_t)t * 3 * A.H + A.H + c0);
   ldv<T, V>(g2, A.gvec + (size_t)t * 3 * A.H + 2 * A.H + c0);
-  ldv<T, V>(ggq, B.ggq + (size_t)t * A.H + c0);
+  ldv<T, V>(ggq, B.ggq + (size_t)t * B.ldggq + c0);
   const int b = min(A.row_ptr[t], A.cap), e = min(A.row_ptr[t + 1], A.cap);
   for (int k = b + EPW * G.sub + G.es; k < e; k += EPW * S) {
     const int s = A.src[k];
@@ -720,10 +732,10 @@ __global__ __launch_bounds__(256) void k_bwd2(Args2<T> B) {
     T kk[V], ggk[V], vx[V], v1[V], v2[V], ggvx[V], ggv1[V], ggv2[V], w0[V], w1[V], w2[V];
     T ggw0[V], ggw1[V], ggw2[V], rk[V], rx[V], r1[V], r2[V], ggpk[V], ggpx[V], ggp1[V], ggp2[V];
     ldv<T, V>(kk, A.k + (size_t)s * A.ldk + c0);
-    ldv<T, V>(ggk, B.ggk + (size_t)s * A.H + c0);
+    ldv<T, V>(ggk, B.ggk + (size_t)s * B.ldggk + c0);
     const T* vs = A.v + (size_t)s * A.ldv + vo;
     ldv<T, V>(vx, vs); ldv<T, V>(v1, vs + A.vst); ldv<T, V>(v2, vs + 2 * A.vst);
-    const T* gvs = B.ggv + (size_t)s * 3 * A.H + vo;
+    const T* gvs = B.ggv + (size_t)s * B.ldggv + vo;
     ldv<T, V>(ggvx, gvs); ldv<T, V>(ggv1, gvs + A.vst); ldv<T, V>(ggv2, gvs + 2 * A.vst);
     if (hw) {
       const T* ws = A.vec + (size_t)s * 3 * A.H + c0;
@@ -811,24 +823,37 @@ __global__ __launch_bounds__(256) void k_bwd2(Args2<T> B) {
     gua1 = group_sum(gua1, A.L);
     gua2 = group_sum(gua2, A.L);
     // per-edge outputs
-    if (hk) stv<T, V>(B.o_pk + (size_t)k * A.H + c0, opk);
+    if (hk) stv<T, V>(B.o_pk + (size_t)k * B.ldopk + c0, opk);
     if (hv) {
-      T* op = B.o_pv + (size_t)k * 3 * A.H + vo;
+      T* op = B.o_pv + (size_t)k * B.ldopv + vo;
       stv<T, V>(op, opx); stv<T, V>(op + A.vst, op1); stv<T, V>(op + 2 * A.vst, op2);
     }
     if (G.el == 0) {
-      B.o_C[k] = gC;
-      B.o_u[3 * k] = gua0; B.o_u[3 * k + 1] = gua1; B.o_u[3 * k + 2] = gua2;
+      if (B.acc_edge) {
+        B.o_C[k] += gC;
+        B.o_u[3 * k] += gua0; B.o_u[3 * k + 1] += gua1; B.o_u[3 * k + 2] += gua2;
+      } else {
+        B.o_C[k] = gC;
+        B.o_u[3 * k] = gua0; B.o_u[3 * k + 1] = gua1; B.o_u[3 * k + 2] = gua2;
+      }
     }
-    // source-node outputs (atomics)
+    if (B.o_src) {  // source-node terms as this edge's scratch row (summed by k_bwd2_src)
+      T* sr = B.o_src + (size_t)k * 7 * A.H;
+      stv<T, V>(sr + c0, ok_);
+      T* sv = sr + A.H + vo;
+      stv<T, V>(sv, ovx); stv<T, V>(sv + A.vst, ov1); stv<T, V>(sv + 2 * A.vst, ov2);
+      T* sw = sr + 4 * A.H + c0;
+      stv<T, V>(sw, ow0); stv<T, V>(sw + A.H, ow1); stv<T, V>(sw + 2 * A.H, ow2);
+    } else {  // source-node outputs (atomics)
 #pragma unroll
-    for (int i = 0; i < V; ++i) {
-      atomicAdd(B.o_k + (size_t)s * A.H + c0 + i, ok_[i]);
-      T* ov = B.o_v + (size_t)s * 3 * A.H + vo + i;
-      atomicAdd(ov, ovx[i]); atomicAdd(ov + A.vst, ov1[i]); atomicAdd(ov + 2 * A.vst, ov2[i]);
-      if (B.o_vec) {
-        T* ow = B.o_vec + (size_t)s * 3 * A.H + c0 + i;
-        atomicAdd(ow, ow0[i]); atomicAdd(ow + A.H, ow1[i]); atomicAdd(ow + 2 * A.H, ow2[i]);
+      for (int i = 0; i < V; ++i) {
+        atomicAdd(B.o_k + (size_t)s * B.ldok + c0 + i, ok_[i]);
+        T* ov = B.o_v + (size_t)s * B.ldov + vo + i;
+        atomicAdd(ov, ovx[i]); atomicAdd(ov + A.vst, ov1[i]); atomicAdd(ov + 2 * A.vst, ov2[i]);
+        if (B.o_vec) {
+          T* ow = B.o_vec + (size_t)s * 3 * A.H + c0 + i;
+          atomicAdd(ow, ow0[i]); atomicAdd(ow + A.H, ow1[i]); atomicAdd(ow + 2 * A.H, ow2[i]);
+        }
       }
     }
   }
@@ -845,10 +870,52 @@ __global__ __launch_bounds__(256) void k_bwd2(Args2<T> B) {
     oq[i] = all[i]; ogx[i] = all[V + i]; og0[i] = all[2 * V + i]; og1[i] = all[3 * V + i]; og2[i] = all[4 * V + i];
   }
   if (t >= 0 && G.sub == 0 && G.es == 0) {
-    stv<T, V>(B.o_q + (size_t)t * A.H + c0, oq);
+    stv<T, V>(B.o_q + (size_t)t * B.ldoq + c0, oq);
     stv<T, V>(B.o_gx + (size_t)t * A.H + c0, ogx);
     T* og = B.o_gvec + (size_t)t * 3 * A.H + c0;
+    if (B.acc_gvec) {
+      T p0[V], p1[V], p2[V];
+      ldv<T, V>(p0, og); ldv<T, V>(p1, og + A.H); ldv<T, V>(p2, og + 2 * A.H);
+#pragma unroll
+      for (int i = 0; i < V; ++i) { og0[i] += p0[i]; og1[i] += p1[i]; og2[i] += p2[i]; }
+    }
     stv<T, V>(og, og0); stv<T, V>(og + A.H, og1); stv<T, V>(og + 2 * A.H, og2);
+  }
+}
+
+// Source pass of the second order: node j's k / v / vec terms are the sum of the scratch rows of the
+// edges leaving j, i.e. the reverses tr[e'] of the edges e' of row j.  One wave per node, 4 columns
+// per lane, the row's edges unrolled by 4 so their loads are in flight together.
+template <typename T>
+__global__ __launch_bounds__(256) void k_bwd2_src(Args2<T> B) {
+  using V4 = T __attribute__((ext_vector_type(4)));
+  const Args<T>& A = B.a;
+  const int j = blockIdx.x * (blockDim.x / TMD_WAVE) + threadIdx.x / TMD_WAVE;
+  if (j >= A.n) return;
+  const int lane = lane_id();
+  const int W = 7 * A.H, b = min(A.row_ptr[j], A.cap), e = min(A.row_ptr[j + 1], A.cap);
+  for (int c = 4 * lane; c < W; c += 4 * TMD_WAVE) {
+    V4 acc = {T(0), T(0), T(0), T(0)};
+    int i = b;
+    for (; i + 4 <= e; i += 4) {
+      V4 r[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int k = B.tr[i + u];
+        TMD_DCHECK(k >= 0 && k < A.cap);
+        r[u] = *reinterpret_cast<const V4*>(B.o_src + (size_t)k * W + c);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc += r[u];
+    }
+    for (; i < e; ++i) acc += *reinterpret_cast<const V4*>(B.o_src + (size_t)B.tr[i] * W + c);
+    T* dst;
+    if (c < A.H) dst = B.o_k + (size_t)j * B.ldok + c;
+    else if (c < 4 * A.H) dst = B.o_v + (size_t)j * B.ldov + (c - A.H);
+    else if (B.o_vec) dst = B.o_vec + (size_t)j * 3 * A.H + (c - 4 * A.H);
+    else continue;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) dst[u] = acc[u];
   }
 }
 
@@ -1262,6 +1329,12 @@ static int bwd(int n, int H, int heads, const int32_t* row_ptr, const int32_t* s
   return et_launch<T, 2, false>(V, A, st);
 }
 
+struct Bwd2Ex {  // the strides / accumulation / source-pass extras of tmdnet_et_message_bwd2_ex
+  int ldggq, ldggk, ldggv, ldoq, ldok, ldov, ldopk, ldopv;
+  const int32_t* tr;
+  void* scratch;
+};
+
 template <typename T>
 static int bwd2(int n, int H, int heads, const int32_t* row_ptr, const int32_t* src, int cap,
                 const void* q, int ldq, const void* k, int ldk, const void* v, int ldv_,
@@ -1270,7 +1343,7 @@ static int bwd2(int n, int H, int heads, const int32_t* row_ptr, const int32_t* 
                 const void* ggv, const void* ggw, const void* ggpk, int ldggpk, const void* ggpv,
                 int ldggpv, const void* ggC, const void* ggu, void* o_gx, void* o_gvec, void* o_q,
                 void* o_k, void* o_v, void* o_vec, void* o_pk, void* o_pv, void* o_C, void* o_u,
-                int flags, hipStream_t st) {
+                int flags, hipStream_t st, const Bwd2Ex* ex = nullptr) {
   Args2<T> B{};
   int V;
   int rc = setup<T>(B.a, n, H, heads, row_ptr, src, cap, q, ldq, k, ldk, v, ldv_, vec, pk, ldpk, pv,
@@ -1292,6 +1365,30 @@ static int bwd2(int n, int H, int heads, const int32_t* row_ptr, const int32_t* 
   B.ggC = (const T*)ggC; B.ggu = (const T*)ggu;
   B.o_gx = (T*)o_gx; B.o_gvec = (T*)o_gvec; B.o_q = (T*)o_q; B.o_k = (T*)o_k; B.o_v = (T*)o_v;
   B.o_vec = (T*)o_vec; B.o_pk = (T*)o_pk; B.o_pv = (T*)o_pv; B.o_C = (T*)o_C; B.o_u = (T*)o_u;
+  B.ldggq = B.ldok = B.ldoq = H; B.ldggk = H; B.ldggv = B.ldov = 3 * H; B.ldopk = H; B.ldopv = 3 * H;
+  if (ex) {
+    auto pick = [](int x, int dflt) { return x ? x : dflt; };
+    B.ldggq = pick(ex->ldggq, H); B.ldggk = pick(ex->ldggk, H); B.ldggv = pick(ex->ldggv, 3 * H);
+    B.ldoq = pick(ex->ldoq, H); B.ldok = pick(ex->ldok, H); B.ldov = pick(ex->ldov, 3 * H);
+    B.ldopk = pick(ex->ldopk, H); B.ldopv = pick(ex->ldopv, 3 * H);
+    if (B.ldggq < H || B.ldggk < H || B.ldggv < 3 * H || B.ldoq < H || B.ldok < H || B.ldov < 3 * H ||
+        B.ldopk < H || B.ldopv < 3 * H)
+      return kBadArgument;
+    if (!aligned<T>(ggq, B.ldggq, V) || !aligned<T>(ggk, B.ldggk, V) || !aligned<T>(ggv, B.ldggv, V) ||
+        !aligned<T>(o_q, B.ldoq, V) || !aligned<T>(o_pk, B.ldopk, V) || !aligned<T>(o_pv, B.ldopv, V))
+      return kBadArgument;
+    if ((ex->tr == nullptr) != (ex->scratch == nullptr)) return kBadArgument;
+    if (ex->scratch) {
+      // the source pass stores 4-wide rows: 16-byte aligned node rows and scratch
+      if (H % 4 || B.ldok % 4 || B.ldov % 4 || ((uintptr_t)o_k % (4 * sizeof(T))) ||
+          ((uintptr_t)o_v % (4 * sizeof(T))) || ((uintptr_t)ex->scratch % (4 * sizeof(T))))
+        return kBadArgument;
+      B.tr = ex->tr;
+      B.o_src = (T*)ex->scratch;
+    }
+  }
+  B.acc_edge = (flags & TMDNET_BWD2_ACC_EDGE) ? 1 : 0;
+  B.acc_gvec = (flags & TMDNET_BWD2_ACC_GVEC) ? 1 : 0;
   if (n <= 0) return kOk;
   const int S = n < 4096 ? 4 : (n < 8192 ? 2 : 1);  // waves per node (small systems: fill the chip)
   const dim3 g((n + 4 / S - 1) / (4 / S)), b(256);
@@ -1300,6 +1397,11 @@ static int bwd2(int n, int H, int heads, const int32_t* row_ptr, const int32_t* 
   else if (V == 2) { if (S == 4) TMD_L2(2, 4); else if (S == 2) TMD_L2(2, 2); else TMD_L2(2, 1); }
   else { if (S == 4) TMD_L2(4, 4); else if (S == 2) TMD_L2(4, 2); else TMD_L2(4, 1); }
 #undef TMD_L2
+  if (hipGetLastError() != hipSuccess) return kLaunchFailed;
+  if (B.o_src) {
+    const int wpb = 256 / TMD_WAVE;
+    hipLaunchKernelGGL(k_bwd2_src<T>, dim3((n + wpb - 1) / wpb), dim3(256), 0, st, B);
+  }
   return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
 }
 
@@ -1375,6 +1477,29 @@ extern "C" int tmdnet_et_message_bwd2(
                      vec_in, pk, ld_pk, pv, ld_pv, cutoff, unit, grad_x, grad_vec, gg_q, gg_k,   \
                      gg_v, gg_vec, gg_pk, ld_ggpk, gg_pv, ld_ggpv, gg_cut, gg_unit, d_grad_x,    \
                      d_grad_vec, d_q, d_k, d_v, d_vec, d_pk, d_pv, d_cut, d_unit, flags, st)
+  if (dtype == TMDNET_F32) TMD_BWD2(float);
+  if (dtype == TMDNET_F64) TMD_BWD2(double);
+#undef TMD_BWD2
+  return kUnsupported;
+}
+
+extern "C" int tmdnet_et_message_bwd2_ex(
+    int dtype, int n_nodes, int hidden, int heads, const int32_t* row_ptr, const int32_t* src,
+    const int32_t* transpose, int max_pairs, const void* q, int ld_q, const void* k, int ld_k,
+    const void* v, int ld_v, const void* vec_in, const void* pk, int ld_pk, const void* pv, int ld_pv,
+    const void* cutoff, const void* unit, const void* grad_x, const void* grad_vec, const void* gg_q,
+    int ld_ggq, const void* gg_k, int ld_ggk, const void* gg_v, int ld_ggv, const void* gg_vec,
+    const void* gg_pk, int ld_ggpk, const void* gg_pv, int ld_ggpv, const void* gg_cut,
+    const void* gg_unit, void* d_grad_x, void* d_grad_vec, void* d_q, int ld_dq, void* d_k, int ld_dk,
+    void* d_v, int ld_dv, void* d_vec, void* d_pk, int ld_dpk, void* d_pv, int ld_dpv, void* d_cut,
+    void* d_unit, void* edge_scratch, int flags, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  const et::Bwd2Ex ex{ld_ggq, ld_ggk, ld_ggv, ld_dq, ld_dk, ld_dv, ld_dpk, ld_dpv, transpose, edge_scratch};
+#define TMD_BWD2(T)                                                                              \
+  return et::bwd2<T>(n_nodes, hidden, heads, row_ptr, src, max_pairs, q, ld_q, k, ld_k, v, ld_v, \
+                     vec_in, pk, ld_pk, pv, ld_pv, cutoff, unit, grad_x, grad_vec, gg_q, gg_k,   \
+                     gg_v, gg_vec, gg_pk, ld_ggpk, gg_pv, ld_ggpv, gg_cut, gg_unit, d_grad_x,    \
+                     d_grad_vec, d_q, d_k, d_v, d_vec, d_pk, d_pv, d_cut, d_unit, flags, st, &ex)
   if (dtype == TMDNET_F32) TMD_BWD2(float);
   if (dtype == TMDNET_F64) TMD_BWD2(double);
 #undef TMD_BWD2

@@ -19,6 +19,7 @@ NL_BRUTE, NL_SHARED, NL_CELL = 0, 1, 2
 RBF_EXPNORM, RBF_GAUSS = 0, 1
 ACC_VEC_RESIDUAL, ACC_EDGE = 1, 2
 ET_V_PLANAR = 4
+BWD2_ACC_EDGE, BWD2_ACC_GVEC = 8, 16
 
 _STATUS = {1: "bad argument", 2: "unsupported configuration", 3: "kernel launch failed",
            4: "workspace too small"}
@@ -49,6 +50,9 @@ SIGNATURES = {
     "tmdnet_pair_index": (I, [I, P, P, P, P, I, P, I, P, P, I, P, SZ, P]),
     "tmdnet_et_message_bwd2": (I, [I, I, I, I, P, P, I, P, I, P, I, P, I, P, P, I, P, I, P, P, P, P,
                                    P, P, P, P, P, I, P, I, P, P, P, P, P, P, P, P, P, P, P, P, I, P]),
+    "tmdnet_et_message_bwd2_ex": (I, [I, I, I, I, P, P, P, I, P, I, P, I, P, I, P, P, I, P, I, P, P, P, P,
+                                      P, I, P, I, P, I, P, P, I, P, I, P, P,
+                                      P, P, P, I, P, I, P, I, P, P, I, P, I, P, P, P, I, P]),
     "tmdnet_et_epilogue_fwd": (I, [I, I, I, P, P, P, P, P, P, P, P]),
     "tmdnet_et_epilogue_bwd": (I, [I, I, I, P, P, P, P, P, P, P]),
     "tmdnet_et_epilogue_ln_fwd": (I, [I, I, I, P, P, P, P, P, P, P, D, P, P, P, P, P, P]),

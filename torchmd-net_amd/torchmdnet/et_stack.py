@@ -697,12 +697,17 @@ def _second_order(ctx, ggs, want):
         x_l, vec_l, xn, mean, rstd, qkv, vecp, pkv, xa, o_ = acts[l]
         vec_w, o_w = p[8], p[9]
         qkv_w = meta.qkv_eff[l][0]
-        gb_gqkv = torch.mm(gb_gxn, qkv_w.t())
+        # the two input-side transposes in one grouped launch: gb_gqkv = gb_gxn qkv_w^T, gb_gvecp =
+        # gbar_v vec_w^T
+        gb_gqkv = torch.empty((N, qkv_w.shape[0]), **o)
+        probs = [(gb_gxn, qkv_w, True, None, gb_gqkv, False)]
         acc(("qkv", l), torch.mm(R["g_qkv"].t(), gb_gxn))
         gb_gvecp = None
         if vec_l is not None and gbar_v is not None:
-            gb_gvecp = torch.matmul(gbar_v, vec_w.t())
+            gb_gvecp = torch.empty((N, 3, 3 * H), **o)
+            probs.append((gbar_v.reshape(3 * N, H), vec_w, True, None, gb_gvecp.view(3 * N, 3 * H), False))
             acc(("vec", l), torch.mm(R["g_vecp"].reshape(3 * N, 3 * H).t(), gbar_v.reshape(3 * N, H)))
+        kernels.gemm_group(probs)
         # message backward VJP (per-edge projection rows)
         pk = pv = None
         if has_e:
@@ -714,17 +719,21 @@ def _second_order(ctx, ggs, want):
                  gbar_v if vec_l is not None else None,
                  gbl[:, :H] if (gbl is not None and meta.hk) else None,
                  gbl[:, H * int(meta.hk):] if (gbl is not None and meta.hv) else None, ggC, ggu)
+        # d_q | d_k | d_v and d_pk | d_pv written straight into the injection buffers, the cutoff /
+        # unit-vector cotangents accumulated into C_bar / u_bar by the kernel
+        outs = {"qkv": torch.empty((N, 5 * H), **o), "C": C_bar, "u": u_bar}
+        if has_e:
+            outs["pkv"] = torch.empty((E, D), **o)
         d_gxa, d_gvec, d_q, d_k, d_v, d_vec, d_pk, d_pv, d_C, d_u = kernels.et_message_bwd2_launch(
             qkv[:, :H], qkv[:, H:2 * H], qkv[:, 2 * H:], vec_l, pk, pv, C, u, graph, meta.heads,
-            R["g_xa"], R["gV"] if R["gV"] is not None else torch.zeros((N, 3, H), **o), ggs_m)
-        inj["qkv"][l] = torch.cat((d_q, d_k, d_v), dim=1)
+            R["g_xa"], R["gV"] if R["gV"] is not None else torch.zeros((N, 3, H), **o), ggs_m, out=outs)
+        inj["qkv"][l] = outs["qkv"]
         if has_e:
-            inj["pkv"][l] = torch.cat([t for t in (d_pk, d_pv) if t is not None], dim=1)
+            inj["pkv"][l] = outs["pkv"]
         inj["vec"][l] = d_vec
-        C_bar.add_(d_C)
-        u_bar.add_(d_u)
         gb_gV = d_gvec if gbar_v is None else gbar_v + d_gvec  # the vec residual g_vec = gV + ...
-        gb_go = torch.mm(d_gxa, o_w.t())
+        gb_go = torch.empty((N, o_w.shape[0]), **o)
+        kernels.gemm_group([(d_gxa, o_w, True, None, gb_go, False)])
         acc(("o", l), torch.mm(R["g_o"].t(), d_gxa))
         if gb_gvecp is None and vecp is not None:
             gb_gvecp = torch.zeros((N, 3, 3 * H), **o)

@@ -723,46 +723,81 @@ class _ETMessageBwd(Function):
         return tuple(res) + (None, None)
 
 
-def et_message_bwd2_launch(q, k, v, vec, pk, pv, C, u, graph, heads, gx, gvec, ggs, flags=0):
-    """One ``tmdnet_et_message_bwd2`` launch: the VJP of tmdnet_et_message_bwd (without the vec
+# the deterministic source pass of tmdnet_et_message_bwd2_ex stores 7H values per edge: used up to
+# this scratch size (beyond it the atomic source terms keep the memory flat)
+BWD2_SCRATCH_MAX_BYTES = 2 << 30
+
+
+def et_message_bwd2_launch(q, k, v, vec, pk, pv, C, u, graph, heads, gx, gvec, ggs, flags=0, out=None):
+    """One ``tmdnet_et_message_bwd2_ex`` launch: the VJP of tmdnet_et_message_bwd (without the vec
     residual) at primals (q, k, v, vec, pk, pv, C, u) and seeds (gx, gvec), for the cotangents
     ``ggs`` = (gg_q, gg_k, gg_v, gg_vec, gg_pk, gg_pv, gg_C, gg_u) of its outputs (None / empty =
-    zero).  pk / pv are per-edge rows (no pair indirection).  Returns (d_gx, d_gvec, d_q, d_k, d_v,
-    d_vec, d_pk, d_pv, d_C, d_u); d_vec is None when vec is None, d_pk / d_pv when pk / pv are."""
+    zero; node cotangents may be column blocks of a wider buffer).  pk / pv are per-edge rows (no pair
+    indirection).  Returns (d_gx, d_gvec, d_q, d_k, d_v, d_vec, d_pk, d_pv, d_C, d_u); d_vec is None
+    when vec is None, d_pk / d_pv when pk / pv are.
+
+    ``out`` (optional dict) names caller buffers: "qkv" [N, 5H] receives d_q | d_k | d_v, "pkv" [E, D]
+    d_pk | d_pv, "C" / "u" are ACCUMULATED into (d_C / d_u returned as those buffers), "gvec" receives
+    d_gvec added to its contents.  With the graph's transpose map the source-node terms are summed by
+    the deterministic source pass (per-edge scratch), otherwise by atomics into zeroed buffers."""
     lib = nat.load()
+    out = out or {}
     N, H = q.shape
     E = graph.n_edges
     o = dict(dtype=q.dtype, device=q.device)
 
-    def dense(g, shape):
-        return torch.zeros(shape, **o) if (g is None or g.numel() == 0) else g.contiguous()
-
-    def rows(g, shape):  # edge cotangents may be row-strided views (read through their leading dimension)
+    def dense(g, shape):  # rows may be strided (read through the leading dimension)
         return torch.zeros(shape, **o) if (g is None or g.numel() == 0) else _rowmajor(g)
 
     ggq, ggk, ggv = dense(ggs[0], (N, H)), dense(ggs[1], (N, H)), dense(ggs[2], (N, 3 * H))
-    ggw = dense(ggs[3], (N, 3, H))
-    ggpk = rows(ggs[4], (E, H)) if pk is not None else None
-    ggpv = rows(ggs[5], (E, 3 * H)) if pv is not None else None
-    ggC, ggu = dense(ggs[6], (E,)), dense(ggs[7], (E, 3))
-    d_gx, d_gvec, d_q = torch.empty((N, H), **o), torch.empty((N, 3, H), **o), torch.empty((N, H), **o)
-    d_k, d_v = torch.zeros((N, H), **o), torch.zeros((N, 3 * H), **o)
-    d_vec = torch.zeros((N, 3, H), **o) if vec is not None else None
+    ggw = dense(ggs[3], (N, 3, H)).contiguous()
+    ggpk = dense(ggs[4], (E, H)) if pk is not None else None
+    ggpv = dense(ggs[5], (E, 3 * H)) if pv is not None else None
+    ggC, ggu = dense(ggs[6], (E,)).contiguous(), dense(ggs[7], (E, 3)).contiguous()
+    scratch = None
+    if graph.transpose is not None and E * 7 * H * q.element_size() <= BWD2_SCRATCH_MAX_BYTES:
+        scratch = torch.empty((E, 7 * H), **o)
+    new_node = torch.empty if scratch is not None else torch.zeros  # atomics need zeroed buffers
+    d_gx = torch.empty((N, H), **o)
+    if "qkv" in out:
+        d_qkv = out["qkv"]
+        if scratch is None:
+            d_qkv[:, H:].zero_()
+        d_q, d_k, d_v = d_qkv[:, :H], d_qkv[:, H:2 * H], d_qkv[:, 2 * H:5 * H]
+    else:
+        d_q, d_k, d_v = torch.empty((N, H), **o), new_node((N, H), **o), new_node((N, 3 * H), **o)
+    d_vec = new_node((N, 3, H), **o) if vec is not None else None
+    if "gvec" in out:
+        d_gvec = out["gvec"]
+        flags |= nat.BWD2_ACC_GVEC
+    else:
+        d_gvec = torch.empty((N, 3, H), **o)
     # per-edge outputs: every row written (padding rows with zeros by the kernel)
-    d_pk = torch.empty((E, H), **o) if pk is not None else None
-    d_pv = torch.empty((E, 3 * H), **o) if pv is not None else None
-    d_C, d_u = torch.empty((E,), **o), torch.empty((E, 3), **o)
+    d_pk = d_pv = None
+    if "pkv" in out:
+        hk_w = H if pk is not None else 0
+        d_pk = out["pkv"][:, :H] if pk is not None else None
+        d_pv = out["pkv"][:, hk_w:hk_w + 3 * H] if pv is not None else None
+    else:
+        d_pk = torch.empty((E, H), **o) if pk is not None else None
+        d_pv = torch.empty((E, 3 * H), **o) if pv is not None else None
+    if "C" in out:
+        d_C, d_u = out["C"], out["u"]
+        flags |= nat.BWD2_ACC_EDGE
+    else:
+        d_C, d_u = torch.empty((E,), **o), torch.empty((E, 3), **o)
     qc, kc, vc, pkc, pvc = (_rowmajor(t) for t in (q, k, v, pk, pv))  # read in place through ld
     gxc, gvc = gx.contiguous(), gvec.contiguous()
-    rc = lib.tmdnet_et_message_bwd2(
-        nat.dtype_code(q.dtype), N, H, heads, nat.ptr(graph.row_ptr), nat.ptr(graph.src), E,
-        nat.ptr(qc), _ld(qc), nat.ptr(kc), _ld(kc), nat.ptr(vc), _ld(vc), nat.ptr(vec), nat.ptr(pkc), _ld(pkc),
-        nat.ptr(pvc), _ld(pvc),
-        nat.ptr(C), nat.ptr(u), nat.ptr(gxc), nat.ptr(gvc), nat.ptr(ggq), nat.ptr(ggk), nat.ptr(ggv),
-        nat.ptr(ggw), nat.ptr(ggpk), _ld(ggpk), nat.ptr(ggpv), _ld(ggpv), nat.ptr(ggC), nat.ptr(ggu), nat.ptr(d_gx),
-        nat.ptr(d_gvec), nat.ptr(d_q), nat.ptr(d_k), nat.ptr(d_v), nat.ptr(d_vec), nat.ptr(d_pk),
-        nat.ptr(d_pv), nat.ptr(d_C), nat.ptr(d_u), int(flags), nat.stream(q.device))
-    nat.check(rc, "tmdnet_et_message_bwd2")
+    P = nat.ptr
+    rc = lib.tmdnet_et_message_bwd2_ex(
+        nat.dtype_code(q.dtype), N, H, heads, P(graph.row_ptr), P(graph.src),
+        P(graph.transpose if scratch is not None else None), E,
+        P(qc), _ld(qc), P(kc), _ld(kc), P(vc), _ld(vc), P(vec), P(pkc), _ld(pkc), P(pvc), _ld(pvc),
+        P(C), P(u), P(gxc), P(gvc), P(ggq), _ld(ggq), P(ggk), _ld(ggk), P(ggv), _ld(ggv), P(ggw),
+        P(ggpk), _ld(ggpk), P(ggpv), _ld(ggpv), P(ggC), P(ggu), P(d_gx), P(d_gvec),
+        P(d_q), _ld(d_q), P(d_k), _ld(d_k), P(d_v), _ld(d_v), P(d_vec), P(d_pk), _ld(d_pk), P(d_pv), _ld(d_pv),
+        P(d_C), P(d_u), P(scratch), int(flags), nat.stream(q.device))
+    nat.check(rc, "tmdnet_et_message_bwd2_ex")
     return d_gx, d_gvec, d_q, d_k, d_v, d_vec, d_pk, d_pv, d_C, d_u
 
 
