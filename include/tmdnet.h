@@ -256,6 +256,14 @@ int tmdnet_ln_bwd_epilogue(int dtype, int n_nodes, int hidden, const void* grad_
                            const void* mean, const void* rstd, const void* ln_w, const void* grad_res,
                            void* grad_x, const void* grad_vec, const void* vecp, const void* o,
                            void* grad_vecp, void* grad_o, void* stream);
+/* tmdnet_ln_bwd_epilogue that also writes w_rows [N][H] = grad_xn * xhat, the per-row terms of the
+ * LayerNorm weight gradient (its column sum; the bias gradient is the column sum of grad_xn), so a
+ * training backward keeps the fused kernel and forms every layer's weight gradients in one batched
+ * reduction (et_stack._backward_layers). */
+int tmdnet_ln_bwd_epilogue_w(int dtype, int n_nodes, int hidden, const void* grad_xn, const void* x,
+                             const void* mean, const void* rstd, const void* ln_w, const void* grad_res,
+                             void* grad_x, const void* grad_vec, const void* vecp, const void* o,
+                             void* grad_vecp, void* grad_o, void* w_rows, void* stream);
 
 /* Second order of the layer tail (force-matching training, et_stack._second_order): layer l's
  * epilogue-backward VJP fused with layer l+1's LayerNorm-backward VJP, one wave per node.

@@ -140,20 +140,27 @@ def _fake_epi_bwd(gx, gvec, vecp, o, g_vecp, g_o):
     g_vecp[..., 2 * H:] = gvec * o1.unsqueeze(1)
 
 
-def _fake_epi_ln(x, vec, vecp, o, veca, ln_w, ln_b):
+def _fake_epi_ln(x, vec, vecp, o, veca, ln_w, ln_b, xn_out=None, vo_out=None):
     """tmdnet_et_epilogue_ln_fwd restated: epilogue (if o) then the next layer's LayerNorm."""
     xo = vo = None
     if o is not None:
         xo, vo = _fake_epi_fwd(x, vec, vecp, o, veca)
         x = xo
+        if vo_out is not None:
+            vo = vo_out.copy_(vo)
     xn, mean, rstd = torch.native_layer_norm(x, [x.shape[1]], ln_w, ln_b, ES._EPS)
+    if xn_out is not None:
+        xn = xn_out.copy_(xn)
     return xo, vo, xn, mean, rstd
 
 
-def _fake_ln_bwd_epi(g_xn, x, mean, rstd, ln_w, g_res, g_vec, vecp, o, g_vecp, g_o):
-    """tmdnet_ln_bwd_epilogue restated: residual + LayerNorm backward, then the previous epilogue."""
+def _fake_ln_bwd_epi(g_xn, x, mean, rstd, ln_w, g_res, g_vec, vecp, o, g_vecp, g_o, wrows=None):
+    """tmdnet_ln_bwd_epilogue_w restated: residual + LayerNorm backward, then the previous epilogue
+    (and the LayerNorm weight gradient's row terms)."""
     g_x, _, _ = torch.ops.aten.native_layer_norm_backward(g_xn, x, [x.shape[1]], mean, rstd, ln_w, None,
                                                           [True, False, False])
+    if wrows is not None:
+        wrows.copy_(g_xn * (x - mean) * rstd)
     if g_res is not None:
         g_x = g_x + g_res
     if o is not None:
@@ -184,6 +191,8 @@ def _fake_bwd2_launch(q, k, v, vec, pk, pv, C, u, graph, heads, gx, gvec, ggs, f
     if not out:
         return res
     d_gx, d_gvec, d_q, d_k, d_v, d_vec, d_pk, d_pv, d_C, d_u = res
+    if "gx" in out:
+        d_gx = out["gx"].copy_(d_gx)
     if "qkv" in out:
         out["qkv"].copy_(torch.cat((d_q, d_k, d_v), 1))
     if "pkv" in out:

@@ -217,7 +217,7 @@ __global__ __launch_bounds__(256) void k_ln_bwd_epi(int n, int H, const T* __res
                                                     const T* __restrict__ gres, T* __restrict__ gx,
                                                     const T* __restrict__ gvec, const T* __restrict__ vecp,
                                                     const T* __restrict__ o, T* __restrict__ gvecp,
-                                                    T* __restrict__ go) {
+                                                    T* __restrict__ go, T* __restrict__ wrows) {
   const int t = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
   const int lane = threadIdx.x & 63;
   if (t >= n) return;
@@ -230,7 +230,9 @@ __global__ __launch_bounds__(256) void k_ln_bwd_epi(int n, int H, const T* __res
     gh[i] = xh[i] = T(0);
     if (c >= H) continue;
     xh[i] = (x[(size_t)t * H + c] - mu) * rs;
-    gh[i] = gxn[(size_t)t * H + c] * lw[c];
+    const T gn = gxn[(size_t)t * H + c];
+    if (wrows) wrows[(size_t)t * H + c] = gn * xh[i];  // the LayerNorm weight gradient's row term
+    gh[i] = gn * lw[c];
     s1 += gh[i];
     s2 += gh[i] * xh[i];
   }
@@ -433,11 +435,26 @@ extern "C" int tmdnet_et_epilogue_ln_fwd(int dtype, int n_nodes, int hidden, con
   return kUnsupported;
 }
 
+extern "C" int tmdnet_ln_bwd_epilogue_w(int dtype, int n_nodes, int hidden, const void* grad_xn, const void* x,
+                                        const void* mean, const void* rstd, const void* ln_w,
+                                        const void* grad_res, void* grad_x, const void* grad_vec,
+                                        const void* vecp, const void* o, void* grad_vecp, void* grad_o,
+                                        void* w_rows, void* stream);
+
 extern "C" int tmdnet_ln_bwd_epilogue(int dtype, int n_nodes, int hidden, const void* grad_xn, const void* x,
                                       const void* mean, const void* rstd, const void* ln_w,
                                       const void* grad_res, void* grad_x, const void* grad_vec,
                                       const void* vecp, const void* o, void* grad_vecp, void* grad_o,
                                       void* stream) {
+  return tmdnet_ln_bwd_epilogue_w(dtype, n_nodes, hidden, grad_xn, x, mean, rstd, ln_w, grad_res, grad_x,
+                                  grad_vec, vecp, o, grad_vecp, grad_o, nullptr, stream);
+}
+
+extern "C" int tmdnet_ln_bwd_epilogue_w(int dtype, int n_nodes, int hidden, const void* grad_xn, const void* x,
+                                        const void* mean, const void* rstd, const void* ln_w,
+                                        const void* grad_res, void* grad_x, const void* grad_vec,
+                                        const void* vecp, const void* o, void* grad_vecp, void* grad_o,
+                                        void* w_rows, void* stream) {
   if (n_nodes < 0 || hidden <= 0 || !grad_xn || !x || !mean || !rstd || !ln_w || !grad_x) return kBadArgument;
   if (o && (!grad_o || (vecp && (!grad_vec || !grad_vecp)))) return kBadArgument;
   if (n_nodes == 0) return kOk;
@@ -446,13 +463,14 @@ extern "C" int tmdnet_ln_bwd_epilogue(int dtype, int n_nodes, int hidden, const 
     return launch_cpl<float, KLnBwd>(n_nodes, hidden, st, (const float*)grad_xn, (const float*)x,
                                      (const float*)mean, (const float*)rstd, (const float*)ln_w,
                                      (const float*)grad_res, (float*)grad_x, (const float*)grad_vec,
-                                     (const float*)vecp, (const float*)o, (float*)grad_vecp, (float*)grad_o);
+                                     (const float*)vecp, (const float*)o, (float*)grad_vecp, (float*)grad_o,
+                                     (float*)w_rows);
   if (dtype == TMDNET_F64)
     return launch_cpl<double, KLnBwd>(n_nodes, hidden, st, (const double*)grad_xn, (const double*)x,
                                       (const double*)mean, (const double*)rstd, (const double*)ln_w,
                                       (const double*)grad_res, (double*)grad_x, (const double*)grad_vec,
                                       (const double*)vecp, (const double*)o, (double*)grad_vecp,
-                                      (double*)grad_o);
+                                      (double*)grad_o, (double*)w_rows);
   return kUnsupported;
 }
 

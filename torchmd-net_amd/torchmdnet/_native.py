@@ -57,6 +57,7 @@ SIGNATURES = {
     "tmdnet_et_epilogue_bwd": (I, [I, I, I, P, P, P, P, P, P, P]),
     "tmdnet_et_epilogue_ln_fwd": (I, [I, I, I, P, P, P, P, P, P, P, D, P, P, P, P, P, P]),
     "tmdnet_ln_bwd_epilogue": (I, [I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P]),
+    "tmdnet_ln_bwd_epilogue_w": (I, [I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P]),
     "tmdnet_et_adjoint_epi_ln": (I, [I, I, I] + [P] * 21),
     "tmdnet_eq_head_fwd": (I, [I, I, I, P, P, P, P, P, P, P]),
     "tmdnet_eq_head_bwd": (I, [I, I, I, P, P, P, P, P, P]),

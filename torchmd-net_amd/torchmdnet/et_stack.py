@@ -243,14 +243,15 @@ def _epilogue_bwd(gx, gvec, vecp, o, g_vecp, g_o):
     nat.check(rc, "tmdnet_et_epilogue_bwd")
 
 
-def _epi_ln(x, vec, vecp, o, veca, ln_w, ln_b):
+def _epi_ln(x, vec, vecp, o, veca, ln_w, ln_b, xn_out=None, vo_out=None):
     """tmdnet_et_epilogue_ln_fwd: this layer's epilogue (o not None) and the next layer's LayerNorm
-    in one pass.  Returns (x_out, vec_out, xn, mean, rstd); o None: LayerNorm of x only."""
+    in one pass.  Returns (x_out, vec_out, xn, mean, rstd); o None: LayerNorm of x only.  xn_out /
+    vo_out: caller buffers for xn / vec_out (the layer-stacked activations)."""
     lib = nat.load()
     N, H = x.shape
     xo = torch.empty_like(x) if o is not None else None
-    vo = torch.empty_like(veca) if o is not None else None
-    xn = torch.empty_like(x)
+    vo = (vo_out if vo_out is not None else torch.empty_like(veca)) if o is not None else None
+    xn = xn_out if xn_out is not None else torch.empty_like(x)
     mean = torch.empty((N, 1), dtype=x.dtype, device=x.device)
     rstd = torch.empty((N, 1), dtype=x.dtype, device=x.device)
     rc = lib.tmdnet_et_epilogue_ln_fwd(nat.dtype_code(x.dtype), N, H, nat.ptr(x), nat.ptr(vec), nat.ptr(vecp),
@@ -261,17 +262,18 @@ def _epi_ln(x, vec, vecp, o, veca, ln_w, ln_b):
     return xo, vo, xn, mean, rstd
 
 
-def _ln_bwd_epi(g_xn, x, mean, rstd, ln_w, g_res, g_vec, vecp, o, g_vecp, g_o):
-    """tmdnet_ln_bwd_epilogue: g_x = g_res + LayerNorm backward (no weight gradients; g_res None: no
-    residual), then the previous layer's epilogue backward into g_vecp / g_o (o None: skipped)."""
+def _ln_bwd_epi(g_xn, x, mean, rstd, ln_w, g_res, g_vec, vecp, o, g_vecp, g_o, wrows=None):
+    """tmdnet_ln_bwd_epilogue_w: g_x = g_res + LayerNorm backward (g_res None: no residual), then the
+    previous layer's epilogue backward into g_vecp / g_o (o None: skipped); ``wrows`` (optional
+    [N, H]) receives g_xn * xhat, the row terms of the LayerNorm weight gradient."""
     lib = nat.load()
     N, H = x.shape
     g_x = torch.empty_like(g_xn)
-    rc = lib.tmdnet_ln_bwd_epilogue(nat.dtype_code(x.dtype), N, H, nat.ptr(g_xn), nat.ptr(x), nat.ptr(mean),
-                                    nat.ptr(rstd), nat.ptr(ln_w), nat.ptr(g_res), nat.ptr(g_x), nat.ptr(g_vec),
-                                    nat.ptr(vecp), nat.ptr(o), nat.ptr(g_vecp), nat.ptr(g_o),
-                                    nat.stream(x.device))
-    nat.check(rc, "tmdnet_ln_bwd_epilogue")
+    rc = lib.tmdnet_ln_bwd_epilogue_w(nat.dtype_code(x.dtype), N, H, nat.ptr(g_xn), nat.ptr(x), nat.ptr(mean),
+                                      nat.ptr(rstd), nat.ptr(ln_w), nat.ptr(g_res), nat.ptr(g_x), nat.ptr(g_vec),
+                                      nat.ptr(vecp), nat.ptr(o), nat.ptr(g_vecp), nat.ptr(g_o), nat.ptr(wrows),
+                                      nat.stream(x.device))
+    nat.check(rc, "tmdnet_ln_bwd_epilogue_w")
     return g_x
 
 
@@ -290,8 +292,15 @@ def _forward_layers(meta, x, f, C, u, params):
         fp = meta.f_pairs if meta.f_pairs is not None else f.index_select(0, meta.pairs[1])
     pkv_all = torch.addmm(meta.dkv_eff[1], fp, meta.dkv_eff[0].t()) if (meta.batched and D) else None
     layers = meta.split(params)
+    L = len(layers)
+    od = dict(dtype=x.dtype, device=x.device)
+    # the activations the weight gradients multiply, stacked over layers (one batched GEMM per weight
+    # kind in the backward): layer l's LayerNorm output, aggregated x and vec input (layer 0: none)
+    xn_all, xa_all = torch.empty((L, N, H), **od), torch.empty((L, N, H), **od)
+    vec_all = torch.empty((L, N, 3, H), **od)
+    meta.stk = (xn_all, xa_all, vec_all)
     # layer l's LayerNorm is computed by layer l-1's epilogue kernel (layer 0: LayerNorm alone)
-    _, _, xn, mean, rstd = _epi_ln(x, None, None, None, None, layers[0][0], layers[0][1])
+    _, _, xn, mean, rstd = _epi_ln(x, None, None, None, None, layers[0][0], layers[0][1], xn_out=xn_all[0])
     for l, p in enumerate(layers):
         vec_w, o_w, o_b = p[8], p[9], p[10]
         qkv_w, qkv_b = meta.qkv_eff[l]
@@ -310,7 +319,7 @@ def _forward_layers(meta, x, f, C, u, params):
             pkv = torch.addmm(dkv_b, fp, dkv_w.t()) if dkv_w is not None else None
         pk = pkv[:, :H] if meta.hk else None
         pv = pkv[:, H * int(meta.hk):] if meta.hv else None
-        xa = torch.empty((N, H), dtype=x.dtype, device=x.device)
+        xa = xa_all[l]
         veca = torch.empty((N, 3, H), dtype=x.dtype, device=x.device)
         kernels.et_message_fwd_launch(qkv[:, :H], qkv[:, H:2 * H], qkv[:, 2 * H:], vec, pk, pv, C, u,
                                       meta.graph, meta.heads, xa, veca, meta.flags, meta.pk_rows)
@@ -318,7 +327,8 @@ def _forward_layers(meta, x, f, C, u, params):
         kernels.gemm_group([(xa, o_w, True, o_b, o, False)])
         acts.append((x, vec, xn, mean, rstd, qkv, vecp, pkv, xa, o))
         if l + 1 < len(layers):
-            x, vec, xn, mean, rstd = _epi_ln(x, vec, vecp, o, veca, layers[l + 1][0], layers[l + 1][1])
+            x, vec, xn, mean, rstd = _epi_ln(x, vec, vecp, o, veca, layers[l + 1][0], layers[l + 1][1],
+                                             xn_out=xn_all[l + 1], vo_out=vec_all[l + 1])
         elif meta.out_norm:  # last epilogue + the model's out_norm (torchmd_et.py:186) in one kernel
             x_pre, vec, x, mean, rstd = _epi_ln(x, vec, vecp, o, veca, params[-2], params[-1])
             acts.append((x_pre, mean, rstd))
@@ -375,9 +385,13 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws, r=None, dr=Fa
         g_pkv_all = torch.empty((E, meta.n_layers * D if (meta.batched or rec) else D), **o)
     g_f = None
     new = lambda shape: torch.empty(shape, **o)  # noqa: E731
-    g_qkv = new((N, 5 * H))
-    g_o = new((N, 3 * H))
-    g_vecp = new((N, 3, 3 * H))
+    L = meta.n_layers
+    # per-layer gradients stacked over layers: the record keeps every layer's, and the weight
+    # gradients are formed for all layers at once after the loop (_node_weight_grads)
+    g_qkv_all, g_o_all = new((L, N, 5 * H)), new((L, N, 3 * H))
+    g_vecp_all, g_xn_all = new((L, N, 3, 3 * H)), new((L, N, H))
+    any_w = any(need_ws[:L])
+    ln_rows = new((L, N, H)) if any_w else None
     gvec_bufs = [new((N, 3, H)), new((N, 3, H))]
     layers = meta.split(params)
     g_params = [None] * len(params)
@@ -395,7 +409,8 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws, r=None, dr=Fa
         elif x_top is not None:  # LayerNorm backward + the injected cotangent (epilogue in the loop)
             gX = _ln_bwd_epi(gX, x_pre, mean_o, rstd_o, params[-2], x_top, None, None, None, None, None)
         else:  # LayerNorm backward + the last layer's epilogue backward, one kernel
-            gX = _ln_bwd_epi(gX, x_pre, mean_o, rstd_o, params[-2], None, gV, last[6], last[9], g_vecp, g_o)
+            gX = _ln_bwd_epi(gX, x_pre, mean_o, rstd_o, params[-2], None, gV, last[6], last[9], g_vecp_all[L - 1],
+                             g_o_all[L - 1])
             epi_done = True
     elif x_top is not None:
         gX = gX + x_top
@@ -406,6 +421,7 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws, r=None, dr=Fa
         vec_w, o_w = p[8], p[9]
         qkv_w, _ = meta.qkv_eff[l]
         dkv_w, _ = meta.dkv_layer(l)
+        g_qkv, g_o, g_vecp = g_qkv_all[l], g_o_all[l], g_vecp_all[l]
         gpk = gpv = dpk = dpv = None
         if dr:
             dpkv = dpkv_all[:, l * D:(l + 1) * D] if meta.batched else torch.mm(fdp, dkv_w.t())
@@ -445,7 +461,7 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws, r=None, dr=Fa
             else:
                 g_f.addmm_(g_pkv, dkv_w)
         # vec_proj^T (accumulated into g_vec) and [q|k|v]^T in ONE launch
-        g_xn = torch.empty((N, H), **o)
+        g_xn = g_xn_all[l]
         probs = [(g_qkv, qkv_w, False, None, g_xn, False)]
         if vec is not None:
             probs.append((g_vecp.view(3 * N, 3 * H), vec_w, False, None, g_vec_in.view(3 * N, H), True))
@@ -453,47 +469,40 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws, r=None, dr=Fa
         if rec:
             step.update(g_o=g_o, g_vecp=g_vecp if vec is not None else None, g_xa=g_xa, g_qkv=g_qkv, g_xn=g_xn)
             record.append(step)
-            g_qkv, g_o, g_vecp = new((N, 5 * H)), new((N, 3 * H)), new((N, 3, 3 * H))
             gvec_bufs = [new((N, 3, H)), new((N, 3, H))]
         need_w = need_ws[l]
         g_res = gX if injected("x", l) is None else gX + injected("x", l)
-        if need_w:  # LayerNorm weight gradients: PyTorch's backward
-            g_x, g_lnw, g_lnb = torch.ops.aten.native_layer_norm_backward(g_xn, x, [H], mean, rstd, ln_w, ln_b,
-                                                                 [True, True, True])
-            g_x.add_(g_res)
-            epi_done = False
-        else:  # LayerNorm backward + residual + the previous layer's epilogue backward, one kernel
-            prev = acts[l - 1] if l > 0 else None
-            g_x = _ln_bwd_epi(g_xn, x, mean, rstd, ln_w, g_res, g_vec_in,
-                              prev[6] if prev else None, prev[9] if prev else None, g_vecp, g_o)
-            epi_done = prev is not None
-        if need_w:
+        # LayerNorm backward + residual + the previous layer's epilogue backward, one kernel (with the
+        # row terms of the LayerNorm weight gradient when weights are wanted)
+        prev = acts[l - 1] if l > 0 else None
+        g_x = _ln_bwd_epi(g_xn, x, mean, rstd, ln_w, g_res, g_vec_in,
+                          prev[6] if prev else None, prev[9] if prev else None,
+                          g_vecp_all[l - 1] if prev else None, g_o_all[l - 1] if prev else None,
+                          wrows=ln_rows[l] if any_w else None)
+        epi_done = prev is not None
+        if need_w and has_e and not (meta.batched or rec):
             base = l * meta.np
-            g_qkv_w = torch.mm(g_qkv.t(), xn)
-            g_qkv_b = g_qkv.sum(0)
-            if meta.planar:  # back to the parameters' (reference) row order
-                qinv = meta.perms[1]
-                g_qkv_w, g_qkv_b = g_qkv_w.index_select(0, qinv), g_qkv_b.index_select(0, qinv)
-            gp = [g_lnw, g_lnb, g_qkv_w[:H], g_qkv_b[:H], g_qkv_w[H:2 * H], g_qkv_b[H:2 * H],
-                  g_qkv_w[2 * H:], g_qkv_b[2 * H:],
-                  (torch.mm(g_vecp.view(3 * N, 3 * H).t(), vec.view(3 * N, H)) if vec is not None
-                   else torch.zeros((3 * H, H), **o)),
-                  torch.mm(g_o.t(), xa), g_o.sum(0)]
-            if has_e and not (meta.batched or rec):
-                g_w, g_b = torch.mm(g_pkv.t(), f), g_pkv.sum(0)
-                if meta.planar:
-                    oinv = meta.perms[5]
-                    g_w, g_b = g_w.index_select(0, oinv), g_b.index_select(0, oinv)
-                gp += _dkv_param_grads(meta, g_w, g_b)
-            g_params[base:base + len(gp)] = gp  # batched mode: dk/dv grads filled after the loop
+            g_w, g_b = torch.mm(g_pkv.t(), f), g_pkv.sum(0)
+            if meta.planar:
+                oinv = meta.perms[5]
+                g_w, g_b = g_w.index_select(0, oinv), g_b.index_select(0, oinv)
+            gl = _dkv_param_grads(meta, g_w, g_b)
+            g_params[base + 11:base + 11 + len(gl)] = gl
         gX = g_x
         gV = g_vec_in
+    adj = inj.get("W")  # the adjoint pass's weight terms (force-loss second order)
+    if any_w:
+        _node_weight_grads(meta, g_params, need_ws, g_qkv_all, g_o_all, g_vecp_all, g_xn_all, ln_rows, adj)
+    if rec:
+        record.append({"g_pkv": None, "stacks": (g_qkv_all, g_o_all, g_vecp_all)})
     if has_e and (meta.batched or rec) and not dr:  # every layer's edge-feature / projection gradients in one GEMM each
         g_f = torch.mm(g_pkv_all, meta.dkv_eff[0])
         if rec:
-            record.append({"g_pkv": g_pkv_all})
+            record[-1]["g_pkv"] = g_pkv_all
         if any(need_ws[:meta.n_layers]):
             g_w_all = torch.mm(g_pkv_all.t(), f)
+            if adj is not None and adj.get("dkv") is not None:  # + the adjoint's g_pkv^T gb_f
+                g_w_all.addmm_(adj["dkv"][0].t(), adj["dkv"][1])
             g_b_all = g_pkv_all.sum(0)
             if meta.planar:
                 dinv = meta.perms[3]
@@ -505,6 +514,42 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws, r=None, dr=Fa
                     gl = _dkv_param_grads(meta, g_w_all[a:b], g_b_all[a:b])
                     g_params[base:base + len(gl)] = gl
     return gX, g_f, g_C, g_u, g_r, g_params
+
+
+def _node_weight_grads(meta, g_params, need_ws, g_qkv_all, g_o_all, g_vecp_all, g_xn_all, ln_rows, adj):
+    """Every layer's LayerNorm, [q|k|v], vec_proj and o_proj weight gradients at once: one batched GEMM
+    per weight kind over the layer-stacked activations of the forward (meta.stk) and one reduction per
+    bias (instead of ~8 launches per layer); ``adj`` (the adjoint pass's stacked factors, force-loss
+    second order) is accumulated by the same batched GEMMs (baddbmm)."""
+    L, N, H = meta.n_layers, g_xn_all.shape[1], meta.H
+    xn_all, xa_all, vec_all = meta.stk
+    W_qkv = torch.bmm(g_qkv_all.transpose(1, 2), xn_all)
+    W_o = torch.bmm(g_o_all.transpose(1, 2), xa_all)
+    W_vec = torch.zeros((L, 3 * H, H), dtype=g_xn_all.dtype, device=g_xn_all.device)
+    if L > 1:  # layer 0 has no vec input (vec = 0): its vec_proj gradient is zero
+        torch.bmm(g_vecp_all[1:].view(L - 1, 3 * N, 3 * H).transpose(1, 2), vec_all[1:].view(L - 1, 3 * N, H),
+                  out=W_vec[1:])
+    W_ln = ln_rows.sum(1)
+    if adj is not None:
+        A, B = adj["qkv"]
+        W_qkv.baddbmm_(A.transpose(1, 2), B)
+        A, B = adj["o"]
+        W_o.baddbmm_(A.transpose(1, 2), B)
+        if adj.get("vec") is not None and L > 1:
+            A, B = adj["vec"]
+            W_vec[1:].baddbmm_(A[1:].view(L - 1, 3 * N, 3 * H).transpose(1, 2), B[1:].view(L - 1, 3 * N, H))
+        W_ln.add_(adj["ln"].sum(1))
+    B_qkv, B_o, B_ln = g_qkv_all.sum(1), g_o_all.sum(1), g_xn_all.sum(1)
+    if meta.planar:  # back to the parameters' (reference) row order
+        qinv = meta.perms[1]
+        W_qkv, B_qkv = W_qkv.index_select(1, qinv), B_qkv.index_select(1, qinv)
+    for l in range(L):
+        if not need_ws[l]:
+            continue
+        base = l * meta.np
+        wq, bq = W_qkv[l], B_qkv[l]
+        g_params[base:base + 11] = [W_ln[l], B_ln[l], wq[:H], bq[:H], wq[H:2 * H], bq[H:2 * H], wq[2 * H:],
+                                    bq[2 * H:], W_vec[l], W_o[l], B_o[l]]
 
 
 def ln_adjoint(gbar, x, mean, rstd, w, g_y):
@@ -551,13 +596,16 @@ def epi_adjoint(gb_o, gb_vecp, gX, gV, vecp, o):
     return gbar_gX, gbar_gV, vecp_bar, o_bar
 
 
-def adjoint_epi_ln_launch(epi, gbar_x_in, gbar_vec_in, ln):
+def adjoint_epi_ln_launch(epi, gbar_x_in, gbar_vec_in, ln, outs=None):
     """One ``tmdnet_et_adjoint_epi_ln`` launch: layer l's epilogue-backward VJP (``epi`` = (gb_o,
     gb_vecp, gX, gV, vecp, o) or None) fused with the next LayerNorm-backward VJP (``ln`` = (x, mean,
     rstd, ln_w, g_y) or None).  Returns (gbar_x_out, gbar_vec_out, vecp_bar, o_bar, gbar_gy, x_bar,
     w_bar) with w_bar the weight cotangent (column sum of the kernel's per-row products).  The Python
-    ``epi_adjoint`` / ``ln_adjoint`` restate it (CPU tests)."""
+    ``epi_adjoint`` / ``ln_adjoint`` restate it (CPU tests).  ``outs`` (optional dict): caller buffers
+    "gbgy" (gbar_gy), "gbv" (gbar_vec_out), "wrows" (the per-row weight terms: w_bar is then None and
+    the caller sums the rows)."""
     lib = nat.load()
+    outs = outs or {}
     N, H = gbar_x_in.shape
     o_ = dict(dtype=gbar_x_in.dtype, device=gbar_x_in.device)
     gb_o = gb_vecp = gX = gV = vecp = o = None
@@ -567,13 +615,15 @@ def adjoint_epi_ln_launch(epi, gbar_x_in, gbar_vec_in, ln):
         gbx_out = torch.empty((N, H), **o_)
         obar = torch.empty((N, 3 * H), **o_)
         if vecp is not None or gbar_vec_in is not None:
-            gbv_out = torch.empty((N, 3, H), **o_)
+            gbv_out = outs["gbv"] if outs.get("gbv") is not None else torch.empty((N, 3, H), **o_)
         if vecp is not None:
             vpbar = torch.empty((N, 3, 3 * H), **o_)
     x = mean = rstd = w = gy = gbgy = xbar = wrows = None
     if ln is not None:
         x, mean, rstd, w, gy = ln
-        gbgy, xbar, wrows = torch.empty((N, H), **o_), torch.empty((N, H), **o_), torch.empty((N, H), **o_)
+        gbgy = outs["gbgy"] if outs.get("gbgy") is not None else torch.empty((N, H), **o_)
+        wrows = outs["wrows"] if outs.get("wrows") is not None else torch.empty((N, H), **o_)
+        xbar = torch.empty((N, H), **o_)
     c = lambda t: None if t is None else t.contiguous()  # noqa: E731
     args = [c(t) for t in (gb_o, gb_vecp, gX, gV, vecp, o, gbar_x_in, gbar_vec_in)]
     rc = lib.tmdnet_et_adjoint_epi_ln(nat.dtype_code(gbar_x_in.dtype), N, H, *[nat.ptr(t) for t in args],
@@ -584,11 +634,26 @@ def adjoint_epi_ln_launch(epi, gbar_x_in, gbar_vec_in, ln):
     if epi is None:
         gbx_out, gbv_out = gbar_x_in, gbar_vec_in
     return gbx_out, gbv_out, vpbar, obar, gbgy, xbar, \
-        (wrows.sum(0) if wrows is not None else None)
+        (wrows.sum(0) if (wrows is not None and outs.get("wrows") is None) else None)
 
 
-def adjoint_epi_ln_composite(epi, gbar_x_in, gbar_vec_in, ln):
+def adjoint_epi_ln_composite(epi, gbar_x_in, gbar_vec_in, ln, outs=None):
     """``adjoint_epi_ln_launch`` restated with ``epi_adjoint`` / ``ln_adjoint`` (CPU tests)."""
+    if outs:
+        res = list(adjoint_epi_ln_composite(epi, gbar_x_in, gbar_vec_in, ln))
+        if outs.get("gbv") is not None and res[1] is not None:
+            outs["gbv"].copy_(res[1])
+            res[1] = outs["gbv"]
+        if outs.get("gbgy") is not None and res[4] is not None:
+            outs["gbgy"].copy_(res[4])
+            res[4] = outs["gbgy"]
+        if outs.get("wrows") is not None and ln is not None:
+            x, mean, rstd, w, gy = ln
+            xh = (x - mean) * rstd
+            J0 = lambda v: rstd * (v - v.mean(1, keepdim=True) - xh * (v * xh).mean(1, keepdim=True))  # noqa: E731
+            outs["wrows"].copy_(gy * J0(res[0]))
+            res[6] = None
+        return tuple(res)
     gbx, gbv, vpbar, obar = gbar_x_in, gbar_vec_in, None, None
     if epi is not None:
         e_x, e_v, vpbar, obar = epi_adjoint(*epi)
@@ -643,7 +708,9 @@ def _second_order(ctx, ggs, want):
     # 1. the force pass again, recorded (its outputs are those of the dr-mode pass up to round-off)
     rec = []
     _, g_f0, _, _, _, _ = _backward_layers(meta, gX, gV, f, C, u, params, acts, need_none, record=rec)
-    g_pkv_all = rec.pop()["g_pkv"] if has_e else None
+    tail = rec.pop()
+    g_pkv_all = tail["g_pkv"] if has_e else None
+    rg_qkv_all, rg_o_all, rg_vecp_all = tail["stacks"]
     rec = rec[::-1]  # layer 0 first
     W_all = meta.dkv_eff[0]
     # cotangent of the summed edge-feature gradient g_f = g_pkv_all W_all
@@ -665,10 +732,19 @@ def _second_order(ctx, ggs, want):
     def acc(key, val):
         W_bar[key] = val if key not in W_bar else W_bar[key] + val
 
-    if gb_f is not None and has_e:
-        acc("dkv", torch.mm(g_pkv_all.t(), gb_f))
-    pr = meta.pairs[0].long() if meta.pairs is not None else None
     inj = {k: [None] * L for k in ("o", "vecp", "qkv", "pkv", "vec", "x")}
+    # the weight cotangents of the backward's node GEMMs / LayerNorms are formed batched over layers by
+    # pass 3 (_node_weight_grads): here only their factors, stacked per layer
+    gbgxn_all, dgxa_all, wrows_all = (torch.empty((L, N, H), **o) for _ in range(3))
+    gbv_all = torch.empty((L, N, 3, H), **o)
+    inj["W"] = {"qkv": (rg_qkv_all, gbgxn_all), "o": (rg_o_all, dgxa_all), "vec": (rg_vecp_all, gbv_all),
+                "ln": wrows_all, "dkv": None}
+    if gb_f is not None and has_e:
+        if meta.batched:
+            inj["W"]["dkv"] = (g_pkv_all, gb_f)  # accumulated into pass 3's edge-feature weight GEMM
+        else:
+            acc("dkv", torch.mm(g_pkv_all.t(), gb_f))
+    pr = meta.pairs[0].long() if meta.pairs is not None else None
     C_bar = torch.zeros((E,), **o)
     u_bar = torch.zeros((E, 3), **o)
     gbar_x = gg_x if gg_x is not None else torch.zeros((N, H), **o)
@@ -687,8 +763,8 @@ def _second_order(ctx, ggs, want):
 
     # 2. the adjoint pass, layer 0 first (layer 0's LayerNorm VJP alone, then per layer the node GEMM
     # transposes, the message VJP and the fused epilogue VJP + next LayerNorm VJP)
-    _, _, _, _, gb_gxn, inj["x"][0], wb = adjoint_epi_ln_launch(None, gbar_x, None, ln_of(0))
-    acc(("ln", 0), wb)
+    _, _, _, _, gb_gxn, inj["x"][0], _ = adjoint_epi_ln_launch(None, gbar_x, None, ln_of(0),
+                                                                outs={"gbgy": gbgxn_all[0], "wrows": wrows_all[0]})
     seed_x = None
     on_bar = None
     for l in range(L):
@@ -701,12 +777,12 @@ def _second_order(ctx, ggs, want):
         # gbar_v vec_w^T
         gb_gqkv = torch.empty((N, qkv_w.shape[0]), **o)
         probs = [(gb_gxn, qkv_w, True, None, gb_gqkv, False)]
-        acc(("qkv", l), torch.mm(R["g_qkv"].t(), gb_gxn))
         gb_gvecp = None
         if vec_l is not None and gbar_v is not None:
             gb_gvecp = torch.empty((N, 3, 3 * H), **o)
             probs.append((gbar_v.reshape(3 * N, H), vec_w, True, None, gb_gvecp.view(3 * N, 3 * H), False))
-            acc(("vec", l), torch.mm(R["g_vecp"].reshape(3 * N, 3 * H).t(), gbar_v.reshape(3 * N, H)))
+        elif l > 0:  # no vec cotangent reached this layer: its vec_proj weight term is zero
+            gbv_all[l].zero_()
         kernels.gemm_group(probs)
         # message backward VJP (per-edge projection rows)
         pk = pv = None
@@ -721,7 +797,7 @@ def _second_order(ctx, ggs, want):
                  gbl[:, H * int(meta.hk):] if (gbl is not None and meta.hv) else None, ggC, ggu)
         # d_q | d_k | d_v and d_pk | d_pv written straight into the injection buffers, the cutoff /
         # unit-vector cotangents accumulated into C_bar / u_bar by the kernel
-        outs = {"qkv": torch.empty((N, 5 * H), **o), "C": C_bar, "u": u_bar}
+        outs = {"qkv": torch.empty((N, 5 * H), **o), "C": C_bar, "u": u_bar, "gx": dgxa_all[l]}
         if has_e:
             outs["pkv"] = torch.empty((E, D), **o)
         d_gxa, d_gvec, d_q, d_k, d_v, d_vec, d_pk, d_pv, d_C, d_u = kernels.et_message_bwd2_launch(
@@ -734,15 +810,14 @@ def _second_order(ctx, ggs, want):
         gb_gV = d_gvec if gbar_v is None else gbar_v + d_gvec  # the vec residual g_vec = gV + ...
         gb_go = torch.empty((N, o_w.shape[0]), **o)
         kernels.gemm_group([(d_gxa, o_w, True, None, gb_go, False)])
-        acc(("o", l), torch.mm(R["g_o"].t(), d_gxa))
         if gb_gvecp is None and vecp is not None:
             gb_gvecp = torch.zeros((N, 3, 3 * H), **o)
         nxt = ln_of(l + 1)
+        nx = {"gbgy": gbgxn_all[l + 1], "gbv": gbv_all[l + 1], "wrows": wrows_all[l + 1]} if l + 1 < L else None
         gbar_x, gbar_v, inj["vecp"][l], inj["o"][l], gb_gxn, xb, wb = adjoint_epi_ln_launch(
-            (gb_go, gb_gvecp, R["gX"], R["gV"], vecp, o_), gbar_x, gb_gV, nxt)
+            (gb_go, gb_gvecp, R["gX"], R["gV"], vecp, o_), gbar_x, gb_gV, nxt, outs=nx)
         if l + 1 < L:
             inj["x"][l + 1] = xb
-            acc(("ln", l + 1), wb)
         elif nxt is not None:  # the fused out_norm: its input's cotangent seeds pass 3
             seed_x, on_bar = xb, wb
             gbar_x = gb_gxn
@@ -777,16 +852,8 @@ def _apply_w_bar(meta, g_params, W_bar, on_bar, wanted):
         if val is not None and wanted(i):
             g_params[i] = val if g_params[i] is None else g_params[i] + val
 
-    for l in range(meta.n_layers):
+    for l in range(meta.n_layers):  # (the node weights' terms are added by _node_weight_grads)
         base = l * meta.np
-        addp(base, W_bar.get(("ln", l)))
-        wq = W_bar.get(("qkv", l))
-        if wq is not None:
-            addp(base + 2, wq[:H])
-            addp(base + 4, wq[H:2 * H])
-            addp(base + 6, wq[2 * H:])
-        addp(base + 8, W_bar.get(("vec", l)))
-        addp(base + 9, W_bar.get(("o", l)))
         if "dkv" in W_bar:
             wl = W_bar["dkv"][l * D:(l + 1) * D]
             for j, gw in enumerate(_dkv_param_grads(meta, wl, wl[:, 0])[0::2]):

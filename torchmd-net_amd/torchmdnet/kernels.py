@@ -736,7 +736,7 @@ def et_message_bwd2_launch(q, k, v, vec, pk, pv, C, u, graph, heads, gx, gvec, g
     indirection).  Returns (d_gx, d_gvec, d_q, d_k, d_v, d_vec, d_pk, d_pv, d_C, d_u); d_vec is None
     when vec is None, d_pk / d_pv when pk / pv are.
 
-    ``out`` (optional dict) names caller buffers: "qkv" [N, 5H] receives d_q | d_k | d_v, "pkv" [E, D]
+    ``out`` (optional dict) names caller buffers: "gx" [N, H] receives d_gx, "qkv" [N, 5H] d_q | d_k | d_v, "pkv" [E, D]
     d_pk | d_pv, "C" / "u" are ACCUMULATED into (d_C / d_u returned as those buffers), "gvec" receives
     d_gvec added to its contents.  With the graph's transpose map the source-node terms are summed by
     the deterministic source pass (per-edge scratch), otherwise by atomics into zeroed buffers."""
@@ -758,7 +758,7 @@ def et_message_bwd2_launch(q, k, v, vec, pk, pv, C, u, graph, heads, gx, gvec, g
     if graph.transpose is not None and E * 7 * H * q.element_size() <= BWD2_SCRATCH_MAX_BYTES:
         scratch = torch.empty((E, 7 * H), **o)
     new_node = torch.empty if scratch is not None else torch.zeros  # atomics need zeroed buffers
-    d_gx = torch.empty((N, H), **o)
+    d_gx = out["gx"] if "gx" in out else torch.empty((N, H), **o)
     if "qkv" in out:
         d_qkv = out["qkv"]
         if scratch is None:
