@@ -26,6 +26,10 @@ enum { TMDNET_F32 = 0, TMDNET_F64 = 1 };
 enum { TMDNET_NL_BRUTE = 0, TMDNET_NL_SHARED = 1, TMDNET_NL_CELL = 2 };
 enum { TMDNET_RBF_EXPNORM = 0, TMDNET_RBF_GAUSS = 1 };
 enum { TMDNET_ACC_VEC_RESIDUAL = 1, TMDNET_ACC_EDGE = 2 };
+/* tmdnet_et_message_bwd accumulate bit: ADD the node gradients (gq, gk, gv, gvec_in) and the edge
+ * gradients (gpk, gpv) to the output buffers' contents (the second order injects its cotangents there
+ * first) instead of overwriting them. */
+enum { TMDNET_ACC_GRADS = 32 };
 /* v / pv row layout flag of the ET message entry points: planar rows [x | v1 | v2] of H channels each
  * instead of the reference's per-head interleave [h][x|v1|v2] of d channels (torchmd_et.py:282-291).
  * Planar rows make every 16-byte-per-lane load of a row segment contiguous (measured 4-7 % on the C5
@@ -240,6 +244,11 @@ int tmdnet_et_epilogue_fwd(int dtype, int n_nodes, int hidden, const void* x, co
 int tmdnet_et_epilogue_bwd(int dtype, int n_nodes, int hidden, const void* grad_x,
                            const void* grad_vec, const void* vecp, const void* o, void* grad_vecp,
                            void* grad_o, void* stream);
+/* tmdnet_et_epilogue_bwd with accumulate != 0: grad_vecp / grad_o are ADDED to (they hold the cotangents
+ * the force-loss second order injects; et_stack._backward_layers). */
+int tmdnet_et_epilogue_bwd_acc(int dtype, int n_nodes, int hidden, const void* grad_x, const void* grad_vec,
+                               const void* vecp, const void* o, void* grad_vecp, void* grad_o,
+                               int accumulate, void* stream);
 
 /* Epilogue of layer l fused with the LayerNorm of layer l+1 (torchmd_et.py:262; biased variance,
  * rstd = 1/sqrt(var + eps), as torch.native_layer_norm).  o == NULL: LayerNorm only (of x; x_out,
@@ -262,8 +271,10 @@ int tmdnet_ln_bwd_epilogue(int dtype, int n_nodes, int hidden, const void* grad_
  * reduction (et_stack._backward_layers). */
 int tmdnet_ln_bwd_epilogue_w(int dtype, int n_nodes, int hidden, const void* grad_xn, const void* x,
                              const void* mean, const void* rstd, const void* ln_w, const void* grad_res,
-                             void* grad_x, const void* grad_vec, const void* vecp, const void* o,
-                             void* grad_vecp, void* grad_o, void* w_rows, void* stream);
+                             const void* grad_res2, void* grad_x, const void* grad_vec, const void* vecp,
+                             const void* o, void* grad_vecp, void* grad_o, void* w_rows, int accumulate,
+                             void* stream);
+/* (grad_res2: a second residual term, NULL = none; accumulate != 0: grad_vecp / grad_o are ADDED to.) */
 
 /* Second order of the layer tail (force-matching training, et_stack._second_order): layer l's
  * epilogue-backward VJP fused with layer l+1's LayerNorm-backward VJP, one wave per node.

@@ -91,15 +91,17 @@ def _fake_bwd(q, k, v, vec, pk, pv, C, u, graph, heads, gx, gvec, gq, gk, gv, gw
     it = iter(g)
     g = [next(it) if t is not None else None for t in ins]
     z = lambda t, ref: torch.zeros_like(ref) if t is None else t  # noqa: E731
-    gq.copy_(z(g[0], q))
-    gk.copy_(z(g[1], k))
-    gv.copy_(_to_planar(z(g[2], v), H, heads, planar))
+    ag = bool(accumulate & nat.ACC_GRADS)
+    put = (lambda d, val: d.add_(val)) if ag else (lambda d, val: d.copy_(val))  # noqa: E731
+    put(gq, z(g[0], q))
+    put(gk, z(g[1], k))
+    put(gv, _to_planar(z(g[2], v), H, heads, planar))
     if gw is not None:
-        gw.copy_(z(g[3], gw) + (gvec if accumulate & nat.ACC_VEC_RESIDUAL else 0))
+        put(gw, z(g[3], gw) + (gvec if accumulate & nat.ACC_VEC_RESIDUAL else 0))
     if gpk is not None:
-        gpk.copy_(z(g[4], pk))
+        put(gpk, z(g[4], pk))
     if gpv is not None:
-        gpv.copy_(_to_planar(z(g[5], pv), H, heads, planar))
+        put(gpv, _to_planar(z(g[5], pv), H, heads, planar))
     if g_r is not None:  # dr mode: <g_pk, dpk> + <g_pv, dpv> per edge (dpv in the kernel's row layout)
         assert gpk is None and gpv is None and accumulate & nat.ACC_EDGE
         if dpk is not None:
@@ -123,7 +125,15 @@ def _fake_epi_fwd(x, vec, vecp, o, veca):
     return x + (v1 * v2).sum(1) * o2 + o3, vec + v3 * o1.unsqueeze(1) + veca
 
 
-def _fake_epi_bwd(gx, gvec, vecp, o, g_vecp, g_o):
+def _fake_epi_bwd(gx, gvec, vecp, o, g_vecp, g_o, acc=False):
+    if acc:  # accumulate: run into scratch and add
+        tv = None if g_vecp is None else torch.zeros_like(g_vecp)
+        to = torch.zeros_like(g_o)
+        _fake_epi_bwd(gx, gvec, vecp, o, tv, to)
+        g_o.add_(to)
+        if vecp is not None:
+            g_vecp.add_(tv)
+        return
     H = gx.shape[1]
     o1, o2 = o[:, :H], o[:, H:2 * H]
     if vecp is None:
@@ -154,7 +164,8 @@ def _fake_epi_ln(x, vec, vecp, o, veca, ln_w, ln_b, xn_out=None, vo_out=None):
     return xo, vo, xn, mean, rstd
 
 
-def _fake_ln_bwd_epi(g_xn, x, mean, rstd, ln_w, g_res, g_vec, vecp, o, g_vecp, g_o, wrows=None):
+def _fake_ln_bwd_epi(g_xn, x, mean, rstd, ln_w, g_res, g_vec, vecp, o, g_vecp, g_o, wrows=None, g_res2=None,
+                     acc=False):
     """tmdnet_ln_bwd_epilogue_w restated: residual + LayerNorm backward, then the previous epilogue
     (and the LayerNorm weight gradient's row terms)."""
     g_x, _, _ = torch.ops.aten.native_layer_norm_backward(g_xn, x, [x.shape[1]], mean, rstd, ln_w, None,
@@ -163,8 +174,10 @@ def _fake_ln_bwd_epi(g_xn, x, mean, rstd, ln_w, g_res, g_vec, vecp, o, g_vecp, g
         wrows.copy_(g_xn * (x - mean) * rstd)
     if g_res is not None:
         g_x = g_x + g_res
+    if g_res2 is not None:
+        g_x = g_x + g_res2
     if o is not None:
-        _fake_epi_bwd(g_x, g_vec, vecp, o, g_vecp, g_o)
+        _fake_epi_bwd(g_x, g_vec, vecp, o, g_vecp, g_o, acc=acc)
     return g_x
 
 

@@ -69,6 +69,18 @@ template <typename T, int V> __device__ __forceinline__ void stv(T* p, const T (
     stv_<T, V>(p, o);
   }
 }
+// store, or (acc: the buffer already holds cotangents injected by the second order) add to it
+template <typename T, int V> __device__ __forceinline__ void stv_acc(T* p, const T (&o)[V], bool acc) {
+  if (acc) {
+    T q[V];
+    ldv<T, V>(q, p);
+#pragma unroll
+    for (int i = 0; i < V; ++i) q[i] += o[i];
+    stv<T, V>(p, q);
+  } else {
+    stv<T, V>(p, o);
+  }
+}
 template <typename T, int V> __device__ __forceinline__ void zero(T (&o)[V]) {
 #pragma unroll
   for (int i = 0; i < V; ++i) o[i] = T(0);
@@ -465,12 +477,13 @@ __device__ __forceinline__ void bwd_dst_body(const Args<T>& A, int blk, int nwg)
         grr = group_sum(grr, A.L);
       } else {
         if (on) {
-          if (hk) stv<T, V>(A.gpk + (size_t)k * A.ldpk + c0, gpk);
+          const bool ag = A.acc & TMDNET_ACC_GRADS;
+          if (hk) stv_acc<T, V>(A.gpk + (size_t)k * A.ldpk + c0, gpk, ag);
           if (hv) {
             T* gp = A.gpv + (size_t)k * A.ldpv + vo;
-            stv<T, V>(gp, gpx);
-            stv<T, V>(gp + A.vst, gp1);
-            stv<T, V>(gp + 2 * A.vst, gp2);
+            stv_acc<T, V>(gp, gpx, ag);
+            stv_acc<T, V>(gp + A.vst, gp1, ag);
+            stv_acc<T, V>(gp + 2 * A.vst, gp2, ag);
           }
         }
       }
@@ -486,7 +499,8 @@ __device__ __forceinline__ void bwd_dst_body(const Args<T>& A, int blk, int nwg)
   }
   xor_slots(gq, A.L);
   reduce_waves<T, S, V>(gq, G.sub, lds);
-  if (t >= 0 && G.sub == 0 && on && G.es == 0) stv<T, V>(A.gq + (size_t)t * A.ldq + c0, gq);
+  if (t >= 0 && G.sub == 0 && on && G.es == 0)
+    stv_acc<T, V>(A.gq + (size_t)t * A.ldq + c0, gq, A.acc & TMDNET_ACC_GRADS);
   zero_pad_rows(A, blk, nwg);
 }
 
@@ -594,11 +608,12 @@ __device__ __forceinline__ void bwd_src_body(const Args<T>& A, int blk, int nwg)
       gk[i] = all[i]; gvx[i] = all[V + i]; gv1[i] = all[2 * V + i]; gv2[i] = all[3 * V + i];
       gw0[i] = all[4 * V + i]; gw1[i] = all[5 * V + i]; gw2[i] = all[6 * V + i];
     }
-    stv<T, V>(A.gk + (size_t)j * A.ldk + c0, gk);
+    const bool ag = A.acc & TMDNET_ACC_GRADS;
+    stv_acc<T, V>(A.gk + (size_t)j * A.ldk + c0, gk, ag);
     T* gvj = A.gv + (size_t)j * A.ldv + vo;
-    stv<T, V>(gvj, gvx);
-    stv<T, V>(gvj + A.vst, gv1);
-    stv<T, V>(gvj + 2 * A.vst, gv2);
+    stv_acc<T, V>(gvj, gvx, ag);
+    stv_acc<T, V>(gvj + A.vst, gv1, ag);
+    stv_acc<T, V>(gvj + 2 * A.vst, gv2, ag);
     if (A.gveci != nullptr) {
       if (A.acc & TMDNET_ACC_VEC_RESIDUAL) {  // gvec_in = grad_vec (residual path) + message part
         const T* gr = A.gvec + (size_t)j * 3 * A.H + c0;
@@ -610,9 +625,9 @@ __device__ __forceinline__ void bwd_src_body(const Args<T>& A, int blk, int nwg)
         for (int i = 0; i < V; ++i) { gw0[i] += r0[i]; gw1[i] += r1[i]; gw2[i] += r2[i]; }
       }
       T* gwj = A.gveci + (size_t)j * 3 * A.H + c0;
-      stv<T, V>(gwj, gw0);
-      stv<T, V>(gwj + A.H, gw1);
-      stv<T, V>(gwj + 2 * A.H, gw2);
+      stv_acc<T, V>(gwj, gw0, ag);
+      stv_acc<T, V>(gwj + A.H, gw1, ag);
+      stv_acc<T, V>(gwj + 2 * A.H, gw2, ag);
     }
   }
 }

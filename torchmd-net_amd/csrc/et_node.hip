@@ -44,10 +44,14 @@ __global__ void k_fwd(int n, int H, const T* __restrict__ x, const T* __restrict
 
 // gx, gvec: gradients of x_out, vec_out.  Writes g_vecp [N][3][3H], g_o [N][3H].
 // (the gradients of x, vec and vec_agg are gx, gvec themselves: identity, no pass needed)
+// put: store, or (acc: the output buffer holds cotangents injected by the second order) add
+template <typename T>
+__device__ __forceinline__ void put(T* p, T v, bool acc) { *p = acc ? *p + v : v; }
+
 template <typename T>
 __global__ void k_bwd(int n, int H, const T* __restrict__ gx, const T* __restrict__ gvec,
                       const T* __restrict__ vecp, const T* __restrict__ o, T* __restrict__ gvecp,
-                      T* __restrict__ go) {
+                      T* __restrict__ go, int acc) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (long long)n * H) return;
   const int t = (int)(i / H), c = (int)(i % H);
@@ -58,9 +62,9 @@ __global__ void k_bwd(int n, int H, const T* __restrict__ gx, const T* __restric
   const T g = gx[(size_t)t * H + c];
   T* gt = go + (size_t)t * 3 * H;
   if (vecp == nullptr) {
-    gt[c] = T(0);
-    gt[H + c] = T(0);
-    gt[2 * H + c] = g;
+    put(gt + c, T(0), acc);
+    put(gt + H + c, T(0), acc);
+    put(gt + 2 * H + c, g, acc);
     return;
   }
   T dot = T(0), go1 = T(0);
@@ -71,13 +75,13 @@ __global__ void k_bwd(int n, int H, const T* __restrict__ gx, const T* __restric
     const T gv = gvec[((size_t)t * 3 + a) * H + c];
     dot += v1 * v2;
     go1 += gv * v3;
-    gvp[a * 3 * H + c] = gd * v2;
-    gvp[a * 3 * H + H + c] = gd * v1;
-    gvp[a * 3 * H + 2 * H + c] = gv * o1;
+    put(gvp + a * 3 * H + c, gd * v2, acc);
+    put(gvp + a * 3 * H + H + c, gd * v1, acc);
+    put(gvp + a * 3 * H + 2 * H + c, gv * o1, acc);
   }
-  gt[c] = go1;
-  gt[H + c] = g * dot;
-  gt[2 * H + c] = g;
+  put(gt + c, go1, acc);
+  put(gt + H + c, g * dot, acc);
+  put(gt + 2 * H + c, g, acc);
 }
 
 }  // namespace epi
@@ -106,9 +110,20 @@ extern "C" int tmdnet_et_epilogue_fwd(int dtype, int n_nodes, int hidden, const 
   return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
 }
 
+extern "C" int tmdnet_et_epilogue_bwd_acc(int dtype, int n_nodes, int hidden, const void* grad_x,
+                                          const void* grad_vec, const void* vecp, const void* o,
+                                          void* grad_vecp, void* grad_o, int accumulate, void* stream);
+
 extern "C" int tmdnet_et_epilogue_bwd(int dtype, int n_nodes, int hidden, const void* grad_x,
                                       const void* grad_vec, const void* vecp, const void* o,
                                       void* grad_vecp, void* grad_o, void* stream) {
+  return tmdnet_et_epilogue_bwd_acc(dtype, n_nodes, hidden, grad_x, grad_vec, vecp, o, grad_vecp, grad_o, 0,
+                                    stream);
+}
+
+extern "C" int tmdnet_et_epilogue_bwd_acc(int dtype, int n_nodes, int hidden, const void* grad_x,
+                                          const void* grad_vec, const void* vecp, const void* o,
+                                          void* grad_vecp, void* grad_o, int accumulate, void* stream) {
   const long long work = (long long)n_nodes * hidden;
   if (work <= 0) return kOk;
   const int tb = 256;
@@ -117,11 +132,11 @@ extern "C" int tmdnet_et_epilogue_bwd(int dtype, int n_nodes, int hidden, const 
   if (dtype == TMDNET_F32)
     hipLaunchKernelGGL(epi::k_bwd<float>, g, dim3(tb), 0, st, n_nodes, hidden, (const float*)grad_x,
                        (const float*)grad_vec, (const float*)vecp, (const float*)o, (float*)grad_vecp,
-                       (float*)grad_o);
+                       (float*)grad_o, accumulate);
   else if (dtype == TMDNET_F64)
     hipLaunchKernelGGL(epi::k_bwd<double>, g, dim3(tb), 0, st, n_nodes, hidden, (const double*)grad_x,
                        (const double*)grad_vec, (const double*)vecp, (const double*)o,
-                       (double*)grad_vecp, (double*)grad_o);
+                       (double*)grad_vecp, (double*)grad_o, accumulate);
   else
     return kUnsupported;
   return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
@@ -217,7 +232,8 @@ __global__ __launch_bounds__(256) void k_ln_bwd_epi(int n, int H, const T* __res
                                                     const T* __restrict__ gres, T* __restrict__ gx,
                                                     const T* __restrict__ gvec, const T* __restrict__ vecp,
                                                     const T* __restrict__ o, T* __restrict__ gvecp,
-                                                    T* __restrict__ go, T* __restrict__ wrows) {
+                                                    T* __restrict__ go, T* __restrict__ wrows,
+                                                    const T* __restrict__ gres2, int acc) {
   const int t = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
   const int lane = threadIdx.x & 63;
   if (t >= n) return;
@@ -241,15 +257,16 @@ __global__ __launch_bounds__(256) void k_ln_bwd_epi(int n, int H, const T* __res
   for (int i = 0; i < CPL; ++i) {
     const int c = lane + 64 * i;
     if (c >= H) continue;
-    const T g = (gres ? gres[(size_t)t * H + c] : T(0)) + rs * (gh[i] - m1 - xh[i] * m2);
+    const T g = (gres ? gres[(size_t)t * H + c] : T(0)) + (gres2 ? gres2[(size_t)t * H + c] : T(0)) +
+                rs * (gh[i] - m1 - xh[i] * m2);
     gx[(size_t)t * H + c] = g;
     if (!o) continue;
     const T* ot = o + (size_t)t * 3 * H;
     T* gt = go + (size_t)t * 3 * H;
     if (!vecp) {
-      gt[c] = T(0);
-      gt[H + c] = T(0);
-      gt[2 * H + c] = g;
+      put(gt + c, T(0), acc);
+      put(gt + H + c, T(0), acc);
+      put(gt + 2 * H + c, g, acc);
       continue;
     }
     const T* vp = vecp + (size_t)t * 9 * H;
@@ -263,13 +280,13 @@ __global__ __launch_bounds__(256) void k_ln_bwd_epi(int n, int H, const T* __res
       const T gv = gvec[((size_t)t * 3 + a) * H + c];
       dot += v1 * v2;
       go1 += gv * v3;
-      gvp[a * 3 * H + c] = gd * v2;
-      gvp[a * 3 * H + H + c] = gd * v1;
-      gvp[a * 3 * H + 2 * H + c] = gv * o1;
+      put(gvp + a * 3 * H + c, gd * v2, acc);
+      put(gvp + a * 3 * H + H + c, gd * v1, acc);
+      put(gvp + a * 3 * H + 2 * H + c, gv * o1, acc);
     }
-    gt[c] = go1;
-    gt[H + c] = g * dot;
-    gt[2 * H + c] = g;
+    put(gt + c, go1, acc);
+    put(gt + H + c, g * dot, acc);
+    put(gt + 2 * H + c, g, acc);
   }
 }
 
@@ -437,24 +454,24 @@ extern "C" int tmdnet_et_epilogue_ln_fwd(int dtype, int n_nodes, int hidden, con
 
 extern "C" int tmdnet_ln_bwd_epilogue_w(int dtype, int n_nodes, int hidden, const void* grad_xn, const void* x,
                                         const void* mean, const void* rstd, const void* ln_w,
-                                        const void* grad_res, void* grad_x, const void* grad_vec,
-                                        const void* vecp, const void* o, void* grad_vecp, void* grad_o,
-                                        void* w_rows, void* stream);
+                                        const void* grad_res, const void* grad_res2, void* grad_x,
+                                        const void* grad_vec, const void* vecp, const void* o, void* grad_vecp,
+                                        void* grad_o, void* w_rows, int accumulate, void* stream);
 
 extern "C" int tmdnet_ln_bwd_epilogue(int dtype, int n_nodes, int hidden, const void* grad_xn, const void* x,
                                       const void* mean, const void* rstd, const void* ln_w,
                                       const void* grad_res, void* grad_x, const void* grad_vec,
                                       const void* vecp, const void* o, void* grad_vecp, void* grad_o,
                                       void* stream) {
-  return tmdnet_ln_bwd_epilogue_w(dtype, n_nodes, hidden, grad_xn, x, mean, rstd, ln_w, grad_res, grad_x,
-                                  grad_vec, vecp, o, grad_vecp, grad_o, nullptr, stream);
+  return tmdnet_ln_bwd_epilogue_w(dtype, n_nodes, hidden, grad_xn, x, mean, rstd, ln_w, grad_res, nullptr,
+                                  grad_x, grad_vec, vecp, o, grad_vecp, grad_o, nullptr, 0, stream);
 }
 
 extern "C" int tmdnet_ln_bwd_epilogue_w(int dtype, int n_nodes, int hidden, const void* grad_xn, const void* x,
                                         const void* mean, const void* rstd, const void* ln_w,
-                                        const void* grad_res, void* grad_x, const void* grad_vec,
-                                        const void* vecp, const void* o, void* grad_vecp, void* grad_o,
-                                        void* w_rows, void* stream) {
+                                        const void* grad_res, const void* grad_res2, void* grad_x,
+                                        const void* grad_vec, const void* vecp, const void* o, void* grad_vecp,
+                                        void* grad_o, void* w_rows, int accumulate, void* stream) {
   if (n_nodes < 0 || hidden <= 0 || !grad_xn || !x || !mean || !rstd || !ln_w || !grad_x) return kBadArgument;
   if (o && (!grad_o || (vecp && (!grad_vec || !grad_vecp)))) return kBadArgument;
   if (n_nodes == 0) return kOk;
@@ -464,13 +481,13 @@ extern "C" int tmdnet_ln_bwd_epilogue_w(int dtype, int n_nodes, int hidden, cons
                                      (const float*)mean, (const float*)rstd, (const float*)ln_w,
                                      (const float*)grad_res, (float*)grad_x, (const float*)grad_vec,
                                      (const float*)vecp, (const float*)o, (float*)grad_vecp, (float*)grad_o,
-                                     (float*)w_rows);
+                                     (float*)w_rows, (const float*)grad_res2, accumulate);
   if (dtype == TMDNET_F64)
     return launch_cpl<double, KLnBwd>(n_nodes, hidden, st, (const double*)grad_xn, (const double*)x,
                                       (const double*)mean, (const double*)rstd, (const double*)ln_w,
                                       (const double*)grad_res, (double*)grad_x, (const double*)grad_vec,
                                       (const double*)vecp, (const double*)o, (double*)grad_vecp,
-                                      (double*)grad_o, (double*)w_rows);
+                                      (double*)grad_o, (double*)w_rows, (const double*)grad_res2, accumulate);
   return kUnsupported;
 }
 

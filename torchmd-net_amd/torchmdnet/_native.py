@@ -18,6 +18,7 @@ F32, F64 = 0, 1
 NL_BRUTE, NL_SHARED, NL_CELL = 0, 1, 2
 RBF_EXPNORM, RBF_GAUSS = 0, 1
 ACC_VEC_RESIDUAL, ACC_EDGE = 1, 2
+ACC_GRADS = 32
 ET_V_PLANAR = 4
 BWD2_ACC_EDGE, BWD2_ACC_GVEC = 8, 16
 
@@ -55,9 +56,10 @@ SIGNATURES = {
                                       P, P, P, I, P, I, P, I, P, P, I, P, I, P, P, P, I, P]),
     "tmdnet_et_epilogue_fwd": (I, [I, I, I, P, P, P, P, P, P, P, P]),
     "tmdnet_et_epilogue_bwd": (I, [I, I, I, P, P, P, P, P, P, P]),
+    "tmdnet_et_epilogue_bwd_acc": (I, [I, I, I, P, P, P, P, P, P, I, P]),
     "tmdnet_et_epilogue_ln_fwd": (I, [I, I, I, P, P, P, P, P, P, P, D, P, P, P, P, P, P]),
     "tmdnet_ln_bwd_epilogue": (I, [I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P]),
-    "tmdnet_ln_bwd_epilogue_w": (I, [I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P]),
+    "tmdnet_ln_bwd_epilogue_w": (I, [I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, P]),
     "tmdnet_et_adjoint_epi_ln": (I, [I, I, I] + [P] * 21),
     "tmdnet_eq_head_fwd": (I, [I, I, I, P, P, P, P, P, P, P]),
     "tmdnet_eq_head_bwd": (I, [I, I, I, P, P, P, P, P, P]),

@@ -234,13 +234,14 @@ def _epilogue_fwd(x, vec, vecp, o, veca):
     return xo, vo
 
 
-def _epilogue_bwd(gx, gvec, vecp, o, g_vecp, g_o):
+def _epilogue_bwd(gx, gvec, vecp, o, g_vecp, g_o, acc=False):
+    """tmdnet_et_epilogue_bwd_acc: g_vecp / g_o written (acc: added to -- they hold injected cotangents)."""
     lib = nat.load()
     N, H = gx.shape
-    rc = lib.tmdnet_et_epilogue_bwd(nat.dtype_code(gx.dtype), N, H, nat.ptr(gx), nat.ptr(gvec),
-                                    nat.ptr(vecp), nat.ptr(o), nat.ptr(g_vecp), nat.ptr(g_o),
-                                    nat.stream(gx.device))
-    nat.check(rc, "tmdnet_et_epilogue_bwd")
+    rc = lib.tmdnet_et_epilogue_bwd_acc(nat.dtype_code(gx.dtype), N, H, nat.ptr(gx), nat.ptr(gvec),
+                                        nat.ptr(vecp), nat.ptr(o), nat.ptr(g_vecp), nat.ptr(g_o), int(acc),
+                                        nat.stream(gx.device))
+    nat.check(rc, "tmdnet_et_epilogue_bwd_acc")
 
 
 def _epi_ln(x, vec, vecp, o, veca, ln_w, ln_b, xn_out=None, vo_out=None):
@@ -262,17 +263,18 @@ def _epi_ln(x, vec, vecp, o, veca, ln_w, ln_b, xn_out=None, vo_out=None):
     return xo, vo, xn, mean, rstd
 
 
-def _ln_bwd_epi(g_xn, x, mean, rstd, ln_w, g_res, g_vec, vecp, o, g_vecp, g_o, wrows=None):
+def _ln_bwd_epi(g_xn, x, mean, rstd, ln_w, g_res, g_vec, vecp, o, g_vecp, g_o, wrows=None, g_res2=None, acc=False):
     """tmdnet_ln_bwd_epilogue_w: g_x = g_res + LayerNorm backward (g_res None: no residual), then the
     previous layer's epilogue backward into g_vecp / g_o (o None: skipped); ``wrows`` (optional
-    [N, H]) receives g_xn * xhat, the row terms of the LayerNorm weight gradient."""
+    [N, H]) receives g_xn * xhat, the row terms of the LayerNorm weight gradient; g_res2: a second
+    residual term; acc: g_vecp / g_o are added to (they hold injected cotangents)."""
     lib = nat.load()
     N, H = x.shape
     g_x = torch.empty_like(g_xn)
     rc = lib.tmdnet_ln_bwd_epilogue_w(nat.dtype_code(x.dtype), N, H, nat.ptr(g_xn), nat.ptr(x), nat.ptr(mean),
-                                      nat.ptr(rstd), nat.ptr(ln_w), nat.ptr(g_res), nat.ptr(g_x), nat.ptr(g_vec),
-                                      nat.ptr(vecp), nat.ptr(o), nat.ptr(g_vecp), nat.ptr(g_o), nat.ptr(wrows),
-                                      nat.stream(x.device))
+                                      nat.ptr(rstd), nat.ptr(ln_w), nat.ptr(g_res), nat.ptr(g_res2), nat.ptr(g_x),
+                                      nat.ptr(g_vec), nat.ptr(vecp), nat.ptr(o), nat.ptr(g_vecp), nat.ptr(g_o),
+                                      nat.ptr(wrows), int(acc), nat.stream(x.device))
     nat.check(rc, "tmdnet_ln_bwd_epilogue_w")
     return g_x
 
@@ -338,7 +340,7 @@ def _forward_layers(meta, x, f, C, u, params):
 
 
 def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws, r=None, dr=False, record=None, inject=None,
-                     seed_pre_norm=False):
+                     seed_pre_norm=False, want_f=True):
     """Hand-scheduled first-order backward.  Returns (g_x, g_f, g_C, g_u, g_r, g_params).
 
     ``dr`` ("dr mode", the force pass: no weight gradients, f = rbf(r)): the projection gradient is
@@ -355,7 +357,9 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws, r=None, dr=Fa
         where the backward forms their gradients -- "o", "vecp", "qkv" (node), "pkv" (edge rows of
         the layer's projection), "vec" (the layer's vec input), "x" (the layer's x input);
       * ``seed_pre_norm``: with the fused out_norm, gX is the gradient of the norm's INPUT (skip its
-        backward)."""
+        backward);
+      * ``want_f`` False: the edge-feature gradient g_f is not formed (a training step's parameter
+        backward never consumes it: f = rbf(r) has no parameters) -- one E x (layers * D) GEMM fewer."""
     H = meta.H
     N = gX.shape[0]
     graph = meta.graph
@@ -365,6 +369,8 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws, r=None, dr=Fa
     D = meta.D
     rec = record is not None
     inj = inject or {}
+    stk = inj.get("stk")  # the second order's layer-stacked injections (see below)
+    acc = stk is not None
     assert not (rec and dr), "recording needs the materialised projection gradient (no dr mode)"
 
     def injected(key, l):
@@ -382,14 +388,23 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws, r=None, dr=Fa
         dpkv_all = torch.mm(fdp, meta.dkv_eff[0].t()) if meta.batched else None
     # padding rows of a static-capacity list are zeroed by the kernel: no memset needed
     elif has_e:
-        g_pkv_all = torch.empty((E, meta.n_layers * D if (meta.batched or rec) else D), **o)
+        if acc and stk.get("pkv") is not None and (meta.batched or rec):
+            g_pkv_all = stk["pkv"]  # [E, layers * D], accumulated into
+        else:
+            g_pkv_all = torch.empty((E, meta.n_layers * D if (meta.batched or rec) else D), **o)
     g_f = None
     new = lambda shape: torch.empty(shape, **o)  # noqa: E731
     L = meta.n_layers
     # per-layer gradients stacked over layers: the record keeps every layer's, and the weight
     # gradients are formed for all layers at once after the loop (_node_weight_grads)
-    g_qkv_all, g_o_all = new((L, N, 5 * H)), new((L, N, 3 * H))
-    g_vecp_all, g_xn_all = new((L, N, 3, 3 * H)), new((L, N, H))
+    # the second order's injected cotangents of the forward intermediates (o, vecp, [q|k|v], the
+    # projection rows) arrive as layer-stacked buffers: the gradients are ACCUMULATED into them by the
+    # kernels (no separate adds)
+    if acc:
+        g_qkv_all, g_o_all, g_vecp_all = stk["qkv"], stk["o"], stk["vecp"]
+    else:
+        g_qkv_all, g_o_all, g_vecp_all = new((L, N, 5 * H)), new((L, N, 3 * H)), new((L, N, 3, 3 * H))
+    g_xn_all = new((L, N, H))
     any_w = any(need_ws[:L])
     ln_rows = new((L, N, H)) if any_w else None
     gvec_bufs = [new((N, 3, H)), new((N, 3, H))]
@@ -429,13 +444,15 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws, r=None, dr=Fa
             dpv = dpkv[:, H * int(meta.hk):] if meta.hv else None
         elif has_e:
             g_pkv = g_pkv_all[:, l * D:(l + 1) * D] if (meta.batched or rec) else g_pkv_all
+            if acc and not (meta.batched or rec):  # per-layer buffer (row stride D): start from the injection
+                g_pkv.copy_(stk["pkv"][:, l * D:(l + 1) * D])
             gpk = g_pkv[:, :H] if meta.hk else None
             gpv = g_pkv[:, H * int(meta.hk):] if meta.hv else None
         if rec:
             step = {"gX": gX, "gV": gV}
         if not epi_done:
-            _epilogue_bwd(gX, gV, vecp, o_, g_vecp, g_o)
-        if injected("o", l) is not None:
+            _epilogue_bwd(gX, gV, vecp, o_, g_vecp, g_o, acc=acc)
+        if not acc and injected("o", l) is not None:
             g_o.add_(injected("o", l))
             if vecp is not None:
                 g_vecp.add_(injected("vecp", l))
@@ -444,19 +461,24 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws, r=None, dr=Fa
         pk = pkv[:, :H] if meta.hk else None
         pv = pkv[:, H * int(meta.hk):] if meta.hv else None
         g_vec_in = gvec_bufs[l % 2] if vec is not None else None
+        if acc and vec is not None:  # the injected vec cotangent's buffer takes the gradient
+            g_vec_in = injected("vec", l) if injected("vec", l) is not None else torch.zeros((N, 3, H), **o)
         kernels.et_message_bwd_launch(
             qkv[:, :H], qkv[:, H:2 * H], qkv[:, 2 * H:], vec, pk, pv, C, u, graph, meta.heads, g_xa, gV,
             g_qkv[:, :H], g_qkv[:, H:2 * H], g_qkv[:, 2 * H:], g_vec_in, gpk, gpv, g_C, g_u,
-            accumulate=nat.ACC_VEC_RESIDUAL | nat.ACC_EDGE | meta.flags, pk_rows=meta.pk_rows,
-            dpk=dpk, dpv=dpv, g_r=g_r)
-        if injected("qkv", l) is not None:
-            g_qkv.add_(injected("qkv", l))
-        if has_e and not dr and injected("pkv", l) is not None:
-            g_pkv.add_(injected("pkv", l))
-        if g_vec_in is not None and injected("vec", l) is not None:
-            g_vec_in.add_(injected("vec", l))
+            accumulate=nat.ACC_VEC_RESIDUAL | nat.ACC_EDGE | meta.flags | (nat.ACC_GRADS if acc else 0),
+            pk_rows=meta.pk_rows, dpk=dpk, dpv=dpv, g_r=g_r)
+        if not acc:
+            if injected("qkv", l) is not None:
+                g_qkv.add_(injected("qkv", l))
+            if has_e and not dr and injected("pkv", l) is not None:
+                g_pkv.add_(injected("pkv", l))
+            if g_vec_in is not None and injected("vec", l) is not None:
+                g_vec_in.add_(injected("vec", l))
         if has_e and not (meta.batched or rec) and not dr:
-            if g_f is None:
+            if not want_f:
+                pass
+            elif g_f is None:
                 g_f = torch.mm(g_pkv, dkv_w)
             else:
                 g_f.addmm_(g_pkv, dkv_w)
@@ -471,14 +493,13 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws, r=None, dr=Fa
             record.append(step)
             gvec_bufs = [new((N, 3, H)), new((N, 3, H))]
         need_w = need_ws[l]
-        g_res = gX if injected("x", l) is None else gX + injected("x", l)
-        # LayerNorm backward + residual + the previous layer's epilogue backward, one kernel (with the
-        # row terms of the LayerNorm weight gradient when weights are wanted)
+        # LayerNorm backward + residual (+ the injected x cotangent) + the previous layer's epilogue
+        # backward, one kernel (with the row terms of the LayerNorm weight gradient when weights are wanted)
         prev = acts[l - 1] if l > 0 else None
-        g_x = _ln_bwd_epi(g_xn, x, mean, rstd, ln_w, g_res, g_vec_in,
+        g_x = _ln_bwd_epi(g_xn, x, mean, rstd, ln_w, gX, g_vec_in,
                           prev[6] if prev else None, prev[9] if prev else None,
                           g_vecp_all[l - 1] if prev else None, g_o_all[l - 1] if prev else None,
-                          wrows=ln_rows[l] if any_w else None)
+                          wrows=ln_rows[l] if any_w else None, g_res2=injected("x", l), acc=acc)
         epi_done = prev is not None
         if need_w and has_e and not (meta.batched or rec):
             base = l * meta.np
@@ -496,7 +517,7 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws, r=None, dr=Fa
     if rec:
         record.append({"g_pkv": None, "stacks": (g_qkv_all, g_o_all, g_vecp_all)})
     if has_e and (meta.batched or rec) and not dr:  # every layer's edge-feature / projection gradients in one GEMM each
-        g_f = torch.mm(g_pkv_all, meta.dkv_eff[0])
+        g_f = torch.mm(g_pkv_all, meta.dkv_eff[0]) if want_f else None
         if rec:
             record[-1]["g_pkv"] = g_pkv_all
         if any(need_ws[:meta.n_layers]):
@@ -613,11 +634,11 @@ def adjoint_epi_ln_launch(epi, gbar_x_in, gbar_vec_in, ln, outs=None):
     if epi is not None:
         gb_o, gb_vecp, gX, gV, vecp, o = epi
         gbx_out = torch.empty((N, H), **o_)
-        obar = torch.empty((N, 3 * H), **o_)
+        obar = outs["obar"] if outs.get("obar") is not None else torch.empty((N, 3 * H), **o_)
         if vecp is not None or gbar_vec_in is not None:
             gbv_out = outs["gbv"] if outs.get("gbv") is not None else torch.empty((N, 3, H), **o_)
         if vecp is not None:
-            vpbar = torch.empty((N, 3, 3 * H), **o_)
+            vpbar = outs["vpbar"] if outs.get("vpbar") is not None else torch.empty((N, 3, 3 * H), **o_)
     x = mean = rstd = w = gy = gbgy = xbar = wrows = None
     if ln is not None:
         x, mean, rstd, w, gy = ln
@@ -644,6 +665,12 @@ def adjoint_epi_ln_composite(epi, gbar_x_in, gbar_vec_in, ln, outs=None):
         if outs.get("gbv") is not None and res[1] is not None:
             outs["gbv"].copy_(res[1])
             res[1] = outs["gbv"]
+        if outs.get("obar") is not None and res[3] is not None:
+            outs["obar"].copy_(res[3])
+            res[3] = outs["obar"]
+        if outs.get("vpbar") is not None and res[2] is not None:
+            outs["vpbar"].copy_(res[2])
+            res[2] = outs["vpbar"]
         if outs.get("gbgy") is not None and res[4] is not None:
             outs["gbgy"].copy_(res[4])
             res[4] = outs["gbgy"]
@@ -707,7 +734,8 @@ def _second_order(ctx, ggs, want):
     need_none = (False,) * (L + int(meta.out_norm))
     # 1. the force pass again, recorded (its outputs are those of the dr-mode pass up to round-off)
     rec = []
-    _, g_f0, _, _, _, _ = _backward_layers(meta, gX, gV, f, C, u, params, acts, need_none, record=rec)
+    _, g_f0, _, _, _, _ = _backward_layers(meta, gX, gV, f, C, u, params, acts, need_none, record=rec,
+                                           want_f=bool(want[6]))  # g_f0: only for d/dr of g_r
     tail = rec.pop()
     g_pkv_all = tail["g_pkv"] if has_e else None
     rg_qkv_all, rg_o_all, rg_vecp_all = tail["stacks"]
@@ -737,6 +765,10 @@ def _second_order(ctx, ggs, want):
     # pass 3 (_node_weight_grads): here only their factors, stacked per layer
     gbgxn_all, dgxa_all, wrows_all = (torch.empty((L, N, H), **o) for _ in range(3))
     gbv_all = torch.empty((L, N, 3, H), **o)
+    # the injections themselves, layer-stacked: pass 3's kernels accumulate into these buffers
+    inj["stk"] = {"qkv": torch.empty((L, N, 5 * H), **o), "o": torch.empty((L, N, 3 * H), **o),
+                  "vecp": torch.empty((L, N, 3, 3 * H), **o),
+                  "pkv": torch.empty((E, L * D), **o) if has_e else None}
     inj["W"] = {"qkv": (rg_qkv_all, gbgxn_all), "o": (rg_o_all, dgxa_all), "vec": (rg_vecp_all, gbv_all),
                 "ln": wrows_all, "dkv": None}
     if gb_f is not None and has_e:
@@ -797,9 +829,9 @@ def _second_order(ctx, ggs, want):
                  gbl[:, H * int(meta.hk):] if (gbl is not None and meta.hv) else None, ggC, ggu)
         # d_q | d_k | d_v and d_pk | d_pv written straight into the injection buffers, the cutoff /
         # unit-vector cotangents accumulated into C_bar / u_bar by the kernel
-        outs = {"qkv": torch.empty((N, 5 * H), **o), "C": C_bar, "u": u_bar, "gx": dgxa_all[l]}
+        outs = {"qkv": inj["stk"]["qkv"][l], "C": C_bar, "u": u_bar, "gx": dgxa_all[l]}
         if has_e:
-            outs["pkv"] = torch.empty((E, D), **o)
+            outs["pkv"] = inj["stk"]["pkv"][:, l * D:(l + 1) * D]
         d_gxa, d_gvec, d_q, d_k, d_v, d_vec, d_pk, d_pv, d_C, d_u = kernels.et_message_bwd2_launch(
             qkv[:, :H], qkv[:, H:2 * H], qkv[:, 2 * H:], vec_l, pk, pv, C, u, graph, meta.heads,
             R["g_xa"], R["gV"] if R["gV"] is not None else torch.zeros((N, 3, H), **o), ggs_m, out=outs)
@@ -813,7 +845,9 @@ def _second_order(ctx, ggs, want):
         if gb_gvecp is None and vecp is not None:
             gb_gvecp = torch.zeros((N, 3, 3 * H), **o)
         nxt = ln_of(l + 1)
-        nx = {"gbgy": gbgxn_all[l + 1], "gbv": gbv_all[l + 1], "wrows": wrows_all[l + 1]} if l + 1 < L else None
+        nx = {"gbgy": gbgxn_all[l + 1], "gbv": gbv_all[l + 1], "wrows": wrows_all[l + 1]} if l + 1 < L else {}
+        nx["obar"] = inj["stk"]["o"][l]
+        nx["vpbar"] = inj["stk"]["vecp"][l]
         gbar_x, gbar_v, inj["vecp"][l], inj["o"][l], gb_gxn, xb, wb = adjoint_epi_ln_launch(
             (gb_go, gb_gvecp, R["gX"], R["gV"], vecp, o_), gbar_x, gb_gV, nxt, outs=nx)
         if l + 1 < L:
@@ -976,21 +1010,24 @@ class _ETStack(Function):
         dr = bool(meta.rbf is not None and ctx.needs_input_grad[5] and meta.D and not any(need_w))
         if DR_MODE in ("0", "off") or pending is not None:
             dr = False
-        outs = _ETStackBwd.apply(meta, ctx.acts, need_w, dr, pending, gX.contiguous(), gV.contiguous(), x, f, C,
-                                 u, r, *params)
+        # the edge-feature gradient only when something consumes it (never in a parameter backward)
+        want_f = f is not None and ctx.needs_input_grad[2] and _will_run(nf[1][0])
+        outs = _ETStackBwd.apply(meta, ctx.acts, need_w, dr, pending, want_f, gX.contiguous(), gV.contiguous(),
+                                 x, f, C, u, r, *params)
         g_x, g_f, g_C, g_u, g_r = outs[:5]
         return (None, g_x, g_f, g_C, g_u, g_r) + tuple(outs[5:])
 
 
 class _ETStackBwd(Function):
     @staticmethod
-    def forward(ctx, meta, acts, need_w, dr, pending, gX, gV, x, f, C, u, r, *params):
+    def forward(ctx, meta, acts, need_w, dr, pending, want_f, gX, gV, x, f, C, u, r, *params):
         if not meta.graph.symmetric:
             raise RuntimeError("torchmd-net_amd: the ET backward source pass needs a symmetric edge "
                                "list (include_transpose=True, no capacity overflow)")
         g_x, g_f, g_C, g_u, g_r, g_params = _backward_layers(meta, gX, gV, f, C, u, params, acts, need_w,
                                                              r=r, dr=dr,
-                                                             inject=pending["inj"] if pending else None)
+                                                             inject=pending["inj"] if pending else None,
+                                                             want_f=want_f)
         if pending is not None:  # the second order's contributions (et_stack._second_order)
             g_C = g_C + pending["C_bar"]
             g_u = g_u + pending["u_bar"]
@@ -1020,7 +1057,7 @@ class _ETStackBwd(Function):
             return kernels.et_message(q, k, v, vec, pk, pv, C_, u_, graph, heads)
 
         _create = torch.is_grad_enabled()  # third order only if the caller builds a graph
-        n_out = 5 + len(saved)
+        n_out = 6 + len(saved)
         # inputs whose gradient this backward must deliver: asked for AND consumed downstream (a
         # training step's loss.backward(inputs=params) never runs the position branch, so the
         # cutoff / unit-vector / distance gradients -- E-sized work -- are skipped)
@@ -1028,11 +1065,11 @@ class _ETStackBwd(Function):
         want = []
         for i, t in enumerate(saved):
             node = next(nf)[0] if t is not None else None
-            want.append(t is not None and ctx.needs_input_grad[5 + i] and _will_run(node))
+            want.append(t is not None and ctx.needs_input_grad[6 + i] and _will_run(node))
         if SECOND_ORDER != "composite" and not _create and hand_second_order_ok(meta, ctx.dr, ctx.need_w, ggs[5:]):
             if not any(want):
                 return (None,) * n_out
-            return (None,) * 5 + tuple(_second_order(ctx, ggs, want))
+            return (None,) * 6 + tuple(_second_order(ctx, ggs, want))
         with torch.enable_grad():
             leaves = [None if t is None else t.detach().requires_grad_(True) for t in saved]
             gX, gV, x, f, C, u, r = leaves[:7]
@@ -1055,7 +1092,7 @@ class _ETStackBwd(Function):
                                          create_graph=_create, allow_unused=True)
         it = iter(second)
         res = [next(it) if w else None for w in want]
-        return (None,) * 5 + tuple(res)
+        return (None,) * 6 + tuple(res)
 
 
 def et_stack(layers, x, graph, f, C, u, rbf=None, out_norm=None, f_pairs=None):
