@@ -465,6 +465,13 @@ int tmdnet_pair_index(int n_nodes, const int32_t* row_ptr, const int32_t* src, c
  * Requirements: K % 64 == 0, lda % 4 == 0, A 16-byte aligned (and B when trans_b); else
  * TMDNET_UNSUPPORTED (callers use the library GEMM).  Exact fp32 arithmetic. */
 int tmdnet_gemm_f32(int n_problems, const int* dims, const void* const* ptrs, void* stream);
+/* Grouped fp32 weight-gradient GEMM: for each of n_problems (<= 32) C (+)= A^T B + A2^T B2, the sum
+ * running over the ROWS of A [K][M] (lda), B [K][N] (ldb) and the optional second segment A2 [K2][M],
+ * B2 [K2][N]; C [M][N] (ldc).  ones1 / ones2: column N-1 of B / B2 is a column of ones (not read; with
+ * either flag set, a segment without it contributes 0 there), so C's last column is the bias gradient.  dims: 12 ints per problem {M, N, K, K2, lda, ldb, lda2, ldb2,
+ * ldc, beta, ones1, ones2}; ptrs: 5 per problem {A, B, A2, B2, C}.  (Every Linear's weight gradient
+ * has this shape: the layers' [q|k|v] / vec_proj / o_proj weights in one launch, the head's six.) */
+int tmdnet_gemm_tn_f32(int n_problems, const int* dims, const void* const* ptrs, void* stream);
 
 /* Library identification (for load checks). */
 const char* tmdnet_build_info(void);

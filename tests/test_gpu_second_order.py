@@ -156,3 +156,43 @@ def test_neighbor_embedding_second_order_hand_matches_composite(monkeypatch):
     for i, (p_, q_) in enumerate(zip(*res)):
         assert p_ is not None and q_ is not None, i
         assert _rel(p_, q_) < 1e-11, (i, _rel(p_, q_))
+
+
+def test_weight_gradient_tn_gemm_matches_library():
+    """tmdnet_gemm_tn_f32 (grouped C (+)= A^T B + A2^T B2 over rows, ones column = bias) against
+    torch fp64 on the shapes the training step uses (node weights over atoms, 3N vec rows, the head's
+    narrow factors, column sums) plus ragged sizes and the 16-wave long-K path."""
+    from torchmdnet import kernels
+    torch.manual_seed(0)
+    dev = torch.device(DEV)
+    shapes = [(678, 640, 128, True, 678), (2034, 384, 128, False, 2034), (678, 128, 0, True, 0),
+              (37, 65, 33, True, 5), (5000, 96, 64, True, 1200), (1356, 2, 65, False, 0), (3, 1, 7, False, 0)]
+    probs, refs = [], []
+    for K, M, Nb, ones, K2 in shapes:
+        A = torch.randn(K, M, device=dev)
+        B = torch.randn(K, Nb, device=dev) if Nb else None
+        N = Nb + int(ones)
+        if N == 0:
+            N, Nb, B = 7, 7, torch.randn(K, 7, device=dev)
+        C = torch.randn(M, N, device=dev)
+        C0 = C.clone()
+        p = {"A": A, "B": B, "C": C, "ones": ones}
+        Bx = B.double() if B is not None else torch.zeros((K, 0), dtype=torch.float64, device=dev)
+        if ones:
+            Bx = torch.cat((Bx, torch.ones((K, 1), dtype=torch.float64, device=dev)), 1)
+        ref = A.double().t() @ Bx
+        if K2:
+            A2, B2 = torch.randn(K2, M, device=dev), torch.randn(K2, Nb, device=dev) if Nb else None
+            p.update(A2=A2, B2=B2)
+            B2x = B2.double() if B2 is not None else torch.zeros((K2, 0), dtype=torch.float64, device=dev)
+            if ones:
+                B2x = torch.cat((B2x, torch.zeros((K2, 1), dtype=torch.float64, device=dev)), 1)
+            ref = ref + A2.double().t() @ B2x
+        if len(probs) % 2:
+            p["beta"] = True
+            ref = ref + C0.double()
+        probs.append(p)
+        refs.append(ref)
+    kernels.wgrad_tn(probs)
+    for p, ref in zip(probs, refs):
+        assert _rel(p["C"], ref) < 2e-5, (tuple(p["A"].shape), _rel(p["C"], ref))

@@ -3,7 +3,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 tag=${1:-r02_so}
-timeout -k 10 600 python -u -m pytest -m gpu -x -v --timeout 300 --timeout-method thread tests/test_gpu_second_order.py tests/test_eq_head.py tests/test_gpu_parity.py -k "adjoint or second_order or double or train or graphed or fit or force or head or neighbor_embedding" > gpurun_out/${tag}_tests.log 2>&1; rc=$?
+timeout -k 10 600 python -u -m pytest -m gpu -x -v --timeout 300 --timeout-method thread tests/test_gpu_second_order.py tests/test_eq_head.py tests/test_gpu_parity.py -k "adjoint or second_order or double or train or graphed or fit or force or head or neighbor_embedding or tn_gemm" > gpurun_out/${tag}_tests.log 2>&1; rc=$?
 tail -5 gpurun_out/${tag}_tests.log
 [ $rc -ne 0 ] && { grep -E "FAIL|Error|assert" gpurun_out/${tag}_tests.log | head -30; exit $rc; }
 timeout -k 10 600 python -u bench.py --no-cpu-baseline --no-roofline --no-pmc --steps 20 --warmup 5 > gpurun_out/${tag}_bench.json 2> gpurun_out/${tag}_bench.err || { tail -30 gpurun_out/${tag}_bench.err; exit 1; }

@@ -137,6 +137,117 @@ __global__ __launch_bounds__(NW * 64) void k_gemm(Group G) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------------
+// Grouped "TN" fp32 MFMA GEMM for weight gradients: C (+)= A^T B summed over ROWS (K = atoms, edges,
+// ...), A [K][M], B [K][N], C [M][N] -- the shape of every Linear's weight gradient (sum over samples
+// of g (x) input).  The library picks a few-workgroup tile with a serial K loop for these (e.g. 64 us
+// for [128 x 678]^T [678 x 257]); here a workgroup owns a 32 x 32 tile of C and splits K over its waves
+// (partials summed in LDS), and up to TN_MAX problems (every layer's [q|k|v] / o_proj / vec_proj
+// weights, or a head's six weights) share ONE launch.  Per problem, a second row segment (A2, B2, K2)
+// continues the K sum -- e.g. the force-loss second order's extra terms of the same weight -- and
+// `ones` (per segment) makes B's column N-1 a column of ones, i.e. C's last column the bias gradient
+// (sum of A over the rows).  Loads are scalar along the rows (the contiguous direction of A and B is
+// the output dimension): one k row of a 32-wide tile is a 128-byte segment.
+constexpr int TN_MAX = 32;
+
+struct ProbTN {
+  int M, N, K, K2, lda, ldb, lda2, ldb2, ldc, beta, ones1, ones2, tiles_n, tile0;
+  const float* A;
+  const float* B;
+  const float* A2;
+  const float* B2;
+  float* C;
+};
+
+struct GroupTN {
+  ProbTN p[TN_MAX];
+  int n;
+};
+
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void k_gemm_tn(GroupTN G) {
+  __shared__ float part[NW][32][33];
+  int pi = 0;
+  for (int i = 1; i < G.n; ++i)
+    if ((int)blockIdx.x >= G.p[i].tile0) pi = i;
+  const ProbTN& P = G.p[pi];
+  const int t = blockIdx.x - P.tile0;
+  const int w = threadIdx.x / TMD_WAVE, lane = lane_id();
+  const int lr = lane & 15, lk = lane >> 4;
+  const int r0 = (t / P.tiles_n) * 32, c0 = (t % P.tiles_n) * 32;
+  const int KT = P.K + P.K2;
+  // this wave's rows: the 16-row blocks split evenly over the waves
+  const int nkb = (KT + 15) / 16, per = (nkb + NW - 1) / NW;
+  const int k_lo = min(KT, w * per * 16), k_hi = min(KT, (w + 1) * per * 16);
+  f4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  const int ma = r0 + lr, mb = r0 + 16 + lr, na = c0 + lr, nb = c0 + 16 + lr;
+  const bool va = ma < P.M, vb = mb < P.M;
+  const bool anyones = P.ones1 || P.ones2;
+  for (int seg = 0; seg < 2; ++seg) {  // the two row segments (wave-uniform)
+    const int s0 = seg ? P.K : 0, s1 = seg ? KT : P.K;
+    const int lo = max(k_lo, s0), hi = min(k_hi, s1);
+    if (lo >= hi) continue;
+    const float* A = seg ? P.A2 : P.A;
+    const float* B = seg ? P.B2 : P.B;
+    const int lda = seg ? P.lda2 : P.lda, ldb = seg ? P.ldb2 : P.ldb;
+    const bool ones = seg ? P.ones2 : P.ones1;
+    // B column kind per lane: 0 read, 1 constant one, 2 zero
+    const int kda = na >= P.N ? 2 : (anyones && na == P.N - 1) ? (ones ? 1 : 2) : 0;
+    const int kdb = nb >= P.N ? 2 : (anyones && nb == P.N - 1) ? (ones ? 1 : 2) : 0;
+    const float* pa0 = A + (va ? ma : 0);
+    const float* pa1 = A + (vb ? mb : 0);
+    const float* pb0 = kda == 0 ? B + na : nullptr;
+    const float* pb1 = kdb == 0 ? B + nb : nullptr;
+    const float ca = kda == 1 ? 1.f : 0.f, cb = kdb == 1 ? 1.f : 0.f;
+    for (int kb = lo; kb < hi; kb += 32) {  // two 16-row blocks in flight
+      float a[2][2][4], b[2][2][4];
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int k = kb + 16 * u + 4 * lk + j;
+          const bool kv = k < hi;
+          const size_t ro = (size_t)(kv ? k - s0 : 0);
+          a[u][0][j] = (kv && va) ? pa0[ro * lda] : 0.f;
+          a[u][1][j] = (kv && vb) ? pa1[ro * lda] : 0.f;
+          b[u][0][j] = !kv ? 0.f : pb0 ? pb0[ro * ldb] : ca;
+          b[u][1][j] = !kv ? 0.f : pb1 ? pb1[ro * ldb] : cb;
+        }
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][0][j], b[u][0][j], acc[0][0], 0, 0, 0);
+          acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][0][j], b[u][1][j], acc[0][1], 0, 0, 0);
+          acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][1][j], b[u][0][j], acc[1][0], 0, 0, 0);
+          acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][1][j], b[u][1][j], acc[1][1], 0, 0, 0);
+        }
+    }
+  }
+#pragma unroll
+  for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+    for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) part[w][bi * 16 + 4 * (lane >> 4) + i][bj * 16 + (lane & 15)] = acc[bi][bj][i];
+  __syncthreads();
+  for (int e = threadIdx.x; e < 32 * 32; e += blockDim.x) {
+    const int r = e >> 5, c = e & 31;
+    const int gr = r0 + r, gc = c0 + c;
+    if (gr >= P.M || gc >= P.N) continue;
+    float v = 0.f;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) v += part[i][r][c];
+    float* out = P.C + (size_t)gr * P.ldc + gc;
+    if (P.beta) v += *out;
+    *out = v;
+  }
+}
+
 }  // namespace gemm
 }  // namespace tmd
 
@@ -184,5 +295,36 @@ extern "C" int tmdnet_gemm_f32(int n_problems, const int* dims, const void* cons
   else if (nw >= 16) hipLaunchKernelGGL(gemm::k_gemm<16>, dim3(tiles), dim3(1024), 0, st, G);
   else if (nw >= 8) hipLaunchKernelGGL(gemm::k_gemm<8>, dim3(tiles), dim3(512), 0, st, G);
   else hipLaunchKernelGGL(gemm::k_gemm<4>, dim3(tiles), dim3(256), 0, st, G);
+  return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
+}
+
+// dims: 12 ints per problem {M, N, K, K2, lda, ldb, lda2, ldb2, ldc, beta, ones1, ones2};
+// ptrs: 5 per problem {A, B, A2, B2, C} (A2 / B2 NULL when K2 = 0).
+extern "C" int tmdnet_gemm_tn_f32(int n_problems, const int* dims, const void* const* ptrs, void* stream) {
+  if (n_problems < 1 || n_problems > gemm::TN_MAX || !dims || !ptrs) return kBadArgument;
+  gemm::GroupTN G{};
+  G.n = n_problems;
+  int tiles = 0, kmax = 0;
+  for (int i = 0; i < n_problems; ++i) {
+    const int* d = dims + 12 * i;
+    gemm::ProbTN& P = G.p[i];
+    P.M = d[0]; P.N = d[1]; P.K = d[2]; P.K2 = d[3]; P.lda = d[4]; P.ldb = d[5]; P.lda2 = d[6]; P.ldb2 = d[7];
+    P.ldc = d[8]; P.beta = d[9]; P.ones1 = d[10]; P.ones2 = d[11];
+    P.A = (const float*)ptrs[5 * i]; P.B = (const float*)ptrs[5 * i + 1];
+    P.A2 = (const float*)ptrs[5 * i + 2]; P.B2 = (const float*)ptrs[5 * i + 3]; P.C = (float*)ptrs[5 * i + 4];
+    if (P.M <= 0 || P.N <= 0 || P.K < 0 || P.K2 < 0 || !P.C || P.ldc < P.N) return kBadArgument;
+    if ((P.K > 0 && (!P.A || (!P.B && !(P.ones1 && P.N == 1)) || P.lda < P.M)) ||
+        (P.K2 > 0 && (!P.A2 || (!P.B2 && !(P.ones2 && P.N == 1)) || P.lda2 < P.M)))
+      return kBadArgument;
+    P.tiles_n = (P.N + 31) / 32;
+    P.tile0 = tiles;
+    tiles += ((P.M + 31) / 32) * P.tiles_n;
+    kmax = max(kmax, P.K + P.K2);
+  }
+  hipStream_t st = (hipStream_t)stream;
+  // K split over 16 waves from 8192 rows (edge sums), 4 below (atom sums: a wave's slice stays long
+  // enough to amortise the partial-tile reduction)
+  if (kmax >= 8192) hipLaunchKernelGGL(gemm::k_gemm_tn<16>, dim3(tiles), dim3(1024), 0, st, G);
+  else hipLaunchKernelGGL(gemm::k_gemm_tn<4>, dim3(tiles), dim3(256), 0, st, G);
   return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
 }

@@ -79,6 +79,7 @@ SIGNATURES = {
     "tmdnet_atom_sum_fwd": (I, [I, I, I, P, P, P, P, P, P]),
     "tmdnet_atom_sum_bwd": (I, [I, I, I, P, P, P, P, P]),
     "tmdnet_gemm_f32": (I, [I, P, P, P]),
+    "tmdnet_gemm_tn_f32": (I, [I, P, P, P]),
     "tmdnet_build_info": (ctypes.c_char_p, []),
 }
 

@@ -1037,6 +1037,62 @@ def gemm_group(problems):
             torch.mm(A, Bop, out=C)
 
 
+def wgrad_tn(problems):
+    """Weight-gradient GEMMs C (+)= A^T B (+ A2^T B2), sums over the rows, all in one
+    ``tmdnet_gemm_tn_f32`` launch (fp32; the library per problem otherwise).  Each problem is a dict:
+    A [K, M], B [K, Nb] (or None with ``ones`` and C of one column), C [M, N], optional "beta",
+    "ones" (C's last column = the column sums of A: B is implicitly [B | 1], N = Nb + 1), "A2" / "B2" /
+    "ones2" (a second row segment of the same sum)."""
+    if not problems:
+        return
+    fp32 = all(p["A"].dtype == torch.float32 and p["A"].is_cuda for p in problems)
+    if fp32:
+        for i in range(0, len(problems), 32):
+            _wgrad_tn_launch(problems[i:i + 32])
+        return
+    for p in problems:  # fp64 (parity runs): the library
+        C = p["C"]
+        res = None
+        for A, B, ones in ((p["A"], p.get("B"), p.get("ones", False)), (p.get("A2"), p.get("B2"), p.get("ones2", False))):
+            if A is None or A.shape[0] == 0:
+                continue
+            Bx = B
+            if ones:
+                one = torch.ones((A.shape[0], 1), dtype=A.dtype, device=A.device)
+                Bx = one if B is None else torch.cat((B, one), 1)
+            elif B is not None and B.shape[1] < C.shape[1]:  # a second segment without the ones column
+                Bx = torch.cat((B, torch.zeros((A.shape[0], 1), dtype=A.dtype, device=A.device)), 1)
+            t = A.t() @ Bx
+            res = t if res is None else res + t
+        if p.get("beta"):
+            C.add_(res)
+        else:
+            C.copy_(res)
+
+
+def _wgrad_tn_launch(problems):
+    lib = nat.load()
+    n = len(problems)
+    dims = (ctypes.c_int * (12 * n))()
+    ptrs = (ctypes.c_void_p * (5 * n))()
+    keep = []
+    for i, p in enumerate(problems):
+        A, B, C = p["A"], p.get("B"), p["C"]
+        A2, B2 = p.get("A2"), p.get("B2")
+        for t in (A, B, A2, B2, C):
+            if t is not None and t.stride(-1) != 1:
+                raise RuntimeError("wgrad_tn: operands need unit column stride")
+        keep += [A, B, A2, B2, C]
+        K2 = 0 if A2 is None else A2.shape[0]
+        dims[12 * i:12 * i + 12] = [A.shape[1], C.shape[1], A.shape[0], K2, A.stride(0),
+                                    0 if B is None else B.stride(0), 0 if A2 is None else A2.stride(0),
+                                    0 if B2 is None else B2.stride(0), C.stride(0), int(bool(p.get("beta"))),
+                                    int(bool(p.get("ones"))), int(bool(p.get("ones2")))]
+        ptrs[5 * i:5 * i + 5] = [None if t is None else t.data_ptr() for t in (A, B, A2, B2, C)]
+    rc = lib.tmdnet_gemm_tn_f32(n, dims, ptrs, nat.stream(problems[0]["A"].device))
+    nat.check(rc, "tmdnet_gemm_tn_f32")
+
+
 # ----------------------------------------------------------------------------- energy reduction
 ATOM_SUM_MAX_MOLECULES = 8192
 
@@ -1423,6 +1479,18 @@ class _EqHead(Function):
         return outs
 
 
+def _head_wgrads(n, H, a1, vv, gu, hext, go, sext, a2, v1, gu2, h2ext, go2, s2ext):
+    """The head's six weight-gradient GEMMs over the n per-atom factor rows, in one grouped launch."""
+    O = Q = H // 2
+    o = dict(dtype=a1.dtype, device=a1.device)
+    outs = [torch.empty((H + O, H), **o), torch.empty((H, 2 * H + 1), **o), torch.empty((2 * O, H + 1), **o),
+            torch.empty((Q + 1, O), **o), torch.empty((Q, 2 * Q + 1), **o), torch.empty((2, Q + 1), **o)]
+    ops = [(a1.view(3 * n, H + O), vv.reshape(3 * n, H)), (gu, hext), (go, sext),
+           (a2.view(3 * n, Q + 1), v1.view(3 * n, O)), (gu2, h2ext), (go2, s2ext)]
+    wgrad_tn([{"A": A, "B": B, "C": C} for (A, B), C in zip(ops, outs)])
+    return outs
+
+
 def _eq_head_weight_grads(lib, x, vec, params, gy, gx, gv):
     """tmdnet_eq_head_bwd_weights (g_x, g_vec and the per-atom factors) + one GEMM per weight pair."""
     N, H = x.shape
@@ -1445,12 +1513,8 @@ def _eq_head_weight_grads(lib, x, vec, params, gy, gx, gv):
     rc = lib.tmdnet_eq_head_bwd_weights(nat.dtype_code(x.dtype), N, H, nat.ptr(x), nat.ptr(vec), ws,
                                         nat.ptr(gy), nat.ptr(gx), nat.ptr(gv), sv, nat.stream(x.device))
     nat.check(rc, "tmdnet_eq_head_bwd_weights")
-    dw12 = a1.view(3 * N, H + O).t() @ vec.reshape(3 * N, H)
-    du1 = gu.t() @ hext
-    du2 = go.t() @ sext
-    dv12 = a2.view(3 * N, Q + 1).t() @ v1.view(3 * N, O)
-    dp1 = gu2.t() @ h2ext
-    dp2 = go2.t() @ s2ext
+    dw12, du1, du2, dv12, dp1, dp2 = _head_wgrads(N, H, a1, vec, gu, hext, go, sext, a2, v1, gu2, h2ext, go2,
+                                                  s2ext)
     return [dw12[:H], dw12[H:], du1[:, :2 * H], du1[:, 2 * H], du2[:, :H], du2[:, H],
             dv12[:Q], dv12[Q:], dp1[:, :2 * Q], dp1[:, 2 * Q], dp2[:, :Q], dp2[:, Q]]
 
@@ -1534,13 +1598,8 @@ def eq_head_hvp(x, vec, params, gy, tx, tv, want_gy=True, want_w=True):
     if saves is None:
         return d_gy, d_x, d_vec, None
     a1, gu, hext, go, sext, a2, v1, gu2, h2ext, go2, s2ext, vv = saves
-    n2 = 2 * N
-    dw12 = a1.view(3 * n2, H + O).t() @ vv.view(3 * n2, H)
-    du1 = gu.t() @ hext
-    du2 = go.t() @ sext
-    dv12 = a2.view(3 * n2, Q + 1).t() @ v1.view(3 * n2, O)
-    dp1 = gu2.t() @ h2ext
-    dp2 = go2.t() @ s2ext
+    dw12, du1, du2, dv12, dp1, dp2 = _head_wgrads(2 * N, H, a1, vv, gu, hext, go, sext, a2, v1, gu2, h2ext, go2,
+                                                  s2ext)
     d_p = [dw12[:H], dw12[H:], du1[:, :2 * H], du1[:, 2 * H], du2[:, :H], du2[:, H],
            dv12[:Q], dv12[Q:], dp1[:, :2 * Q], dp1[:, 2 * Q], dp2[:, :Q], dp2[:, Q]]
     return d_gy, d_x, d_vec, d_p
