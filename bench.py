@@ -227,9 +227,44 @@ def probe_workload(n_atoms, H, dev):
                                        ptr(C), ptr(u), ptr(xo), ptr(vo), PROBE_FLAGS, ptr(pair_row), None, st)
         kernels.nat.check(rc, "tmdnet_et_message_fwd")
 
+    # the backward in the model's layout (destination + source CSR passes, one C-ABI call): the
+    # training form (per-edge projection gradient written) and the force-pass "dr" form (contracted
+    # with d(dk,dv)/dr of the pair rows in-kernel, g_r accumulated)
+    gx, gvec = rn(n_atoms, H), rn(n_atoms, 3, H)
+    gq, gk, gv, gw = (torch.empty(n_atoms, H, device=dev), torch.empty(n_atoms, H, device=dev),
+                      torch.empty(n_atoms, 3 * H, device=dev), torch.empty(n_atoms, 3, H, device=dev))
+    gpk, gpv = torch.empty(E, H, device=dev), torch.empty(E, 3 * H, device=dev)
+    gC, gu, gr = torch.zeros(E, device=dev), torch.zeros(E, 3, device=dev), torch.zeros(E, device=dev)
+    dpk, dpv = rn(P, H), rn(P, 3 * H)
+
+    def launch_bwd(dr=False):
+        acc = 1 | 2 | PROBE_FLAGS  # TMDNET_ACC_VEC_RESIDUAL | TMDNET_ACC_EDGE | planar rows
+        rc = lib.tmdnet_et_message_bwd(
+            0, n_atoms, H, 8, ptr(graph.row_ptr), ptr(graph.src), E, ptr(q), H, ptr(k), H, ptr(v), 3 * H,
+            ptr(vec), ptr(pk2), H, ptr(pv2), 3 * H, ptr(C), ptr(u), ptr(gx), ptr(gvec), ptr(gq), ptr(gk), ptr(gv),
+            ptr(gw), None if dr else ptr(gpk), None if dr else ptr(gpv), ptr(gC), ptr(gu),
+            ptr(dpk) if dr else None, ptr(dpv) if dr else None, ptr(gr) if dr else None, acc, ptr(pair_row), None,
+            st)
+        kernels.nat.check(rc, "tmdnet_et_message_bwd")
+
     launch.pairs = launch_pairs
+    launch.bwd = launch_bwd
     launch.n_pairs = P
     return launch, E, L
+
+
+def et_bwd_bytes(E, N, P, H, dr, s=4):
+    """Algorithmic bytes of one tmdnet_et_message_bwd call (destination + source pass) in the model's
+    pair-row layout, every tensor touched once: edge scalars (src, pair row, cutoff, unit vector) and
+    the P projection rows read; node features q, k, v, vec and the incoming gx, gvec read; gq, gk, gv,
+    gvec_in written; per edge g_cut, g_unit accumulated (read + write); training form: the per-edge
+    projection gradient written (E x 4H), dr form: d(dk,dv)/dr rows read (P x 4H) and g_r accumulated."""
+    b = E * (4 + 4 + 4 + 12) + N * 4 + P * 4 * H * s              # CSR / edge scalars, projection rows
+    b += N * (H + H + 3 * H + 3 * H + H + 3 * H) * s              # q, k, v, vec, gx, gvec
+    b += N * (H + H + 3 * H + 3 * H) * s                          # gq, gk, gv, gvec_in
+    b += 2 * E * (4 + 12)                                         # g_cut, g_unit (accumulated)
+    b += (P * 4 * H * s + 2 * E * 4) if dr else E * 4 * H * s     # dr: dpkv rows + g_r; else gpkv
+    return b
 
 
 PROBE_KERNEL = "k_fwd<float, 4, 1, 1, false>"
@@ -237,12 +272,19 @@ PROBE_KERNEL = "k_fwd<float, 4, 1, 1, false>"
 PROBE_FLAGS = 4  # TMDNET_ET_V_PLANAR
 
 
-def pmc_traffic(a):
-    """HBM-side bytes per launch of the probe kernel from rocprofv3 counters, one counter per pass
-    (MI355X_MICROARCH.md 'HBM'): FETCH_SIZE (KiB; gfx950 tallies 16-B/lane reads at half their bytes ->
-    x2) + WRITE_SIZE (KiB, exact for 16-B/lane stores).  FETCH_SIZE counts L2 misses served by the
-    Infinity Cache too, so this is L2->fabric traffic, an upper bound on HBM bytes.  Runs the probe in
-    a child process under rocprofv3; returns (bytes, detail) or (None, reason)."""
+PMC_PASSES = ("FETCH_SIZE", "WRITE_SIZE", "TCC_HIT_sum TCC_MISS_sum")
+# the child's dispatch sequence (main(), --pmc-child): probe kernel name -> [(tag, count), ...] in order
+PMC_CHILD = {"k_fwd<float, 4, 1, 1, false>": [("graded", 8), ("pairs", 8)],
+             "k_bwd_dst<": [("bwd_dst", 4), ("bwd_dst_dr", 4)], "k_bwd_src<": [("bwd_src", 4), ("bwd_src_dr", 4)]}
+
+
+def pmc_counters(a):
+    """Per-launch counters of the C5 probe kernels from rocprofv3 (one pass per entry of PMC_PASSES,
+    each in a child process running the probes in a fixed order): FETCH_SIZE / WRITE_SIZE in bytes
+    (FETCH x2: gfx950 tallies 16-B/lane reads at half their bytes, MI355X_MICROARCH.md 'HBM';
+    FETCH_SIZE counts Infinity-Cache hits too, so it is L2->fabric traffic, an upper bound on HBM
+    bytes) and the L2 hit rate TCC_HIT / (TCC_HIT + TCC_MISS).  Returns ({tag: {...}}, None) or
+    (None, reason)."""
     import csv
     import glob
     import shutil
@@ -251,10 +293,10 @@ def pmc_traffic(a):
     prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
     if not os.path.exists(prof):
         return None, "rocprofv3 not found"
-    out = {}
-    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+    res = {}
+    for pas in PMC_PASSES:
         d = tempfile.mkdtemp(prefix="tmdnet_pmc_")
-        cmd = [prof, "--pmc", ctr, "--output-format", "csv", "-d", d, "-o", "pmc", "--", sys.executable,
+        cmd = [prof, "--pmc", *pas.split(), "--output-format", "csv", "-d", d, "-o", "pmc", "--", sys.executable,
                os.path.abspath(__file__), "--pmc-child", "--roofline-atoms", str(a.roofline_atoms),
                "--channels", str(a.channels)]
         try:
@@ -262,22 +304,45 @@ def pmc_traffic(a):
                            env=dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp")))
         except (subprocess.SubprocessError, OSError) as e:
             shutil.rmtree(d, ignore_errors=True)
-            return None, f"rocprofv3 {ctr} pass failed: {type(e).__name__}"
-        vals = []
+            return None, f"rocprofv3 {pas} pass failed: {type(e).__name__}"
+        recs = {}  # (kernel key, counter) -> [(dispatch id, value)]
         for f in glob.glob(os.path.join(d, "**", "*counter_collection*.csv"), recursive=True):
             for r in csv.DictReader(open(f)):
-                if PROBE_KERNEL in r.get("Kernel_Name", "") and r.get("Counter_Name") == ctr:
-                    vals.append(float(r["Counter_Value"]))
+                name = r.get("Kernel_Name", "")
+                for key in PMC_CHILD:
+                    if key in name:
+                        did = int(r.get("Dispatch_Id", r.get("Correlation_Id", 0)) or 0)
+                        recs.setdefault((key, r.get("Counter_Name")), []).append((did, float(r["Counter_Value"])))
         shutil.rmtree(d, ignore_errors=True)
-        if not vals:
-            return None, f"no {ctr} records for {PROBE_KERNEL}"
-        vals = vals[2:] or vals  # drop warm-up dispatches
-        out[ctr] = sum(vals) / len(vals) * 1024.0
-    fetch = 2.0 * out["FETCH_SIZE"]
-    return fetch + out["WRITE_SIZE"], {"fetch_bytes": round(fetch), "write_bytes": round(out["WRITE_SIZE"]),
-                                       "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), "
-                                                 "FETCH x2 (gfx950 16-B/lane correction); includes "
-                                                 "Infinity-Cache hits"}
+        for (key, ctr), vals in recs.items():
+            vals = [v for _, v in sorted(vals)]
+            i = 0
+            for tag, cnt in PMC_CHILD[key]:
+                part = vals[i:i + cnt]
+                i += cnt
+                part = part[2:] or part  # drop warm-up dispatches
+                if part:
+                    res.setdefault(tag, {})[ctr] = sum(part) / len(part)
+    if not res:
+        return None, "no counter records for the probe kernels"
+    out = {}
+    for tag, c in res.items():
+        e = {}
+        if "FETCH_SIZE" in c:
+            e["fetch_bytes"] = round(2.0 * c["FETCH_SIZE"] * 1024.0)
+        if "WRITE_SIZE" in c:
+            e["write_bytes"] = round(c["WRITE_SIZE"] * 1024.0)
+        if "fetch_bytes" in e and "write_bytes" in e:
+            e["traffic"] = e["fetch_bytes"] + e["write_bytes"]
+        if c.get("TCC_HIT_sum") is not None and c.get("TCC_MISS_sum") is not None:
+            tot = c["TCC_HIT_sum"] + c["TCC_MISS_sum"]
+            e["l2_hit_rate"] = round(c["TCC_HIT_sum"] / tot, 4) if tot else None
+        out[tag] = e
+    return out, None
+
+
+PMC_SOURCE = ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE / TCC_HIT_sum+TCC_MISS_sum (separate passes), FETCH x2 "
+              "(gfx950 16-B/lane correction); includes Infinity-Cache hits")
 
 
 def roofline_probe(a, dev):
@@ -318,10 +383,36 @@ def roofline_probe(a, dev):
                            "distinct_bytes_per_launch": pbytes,
                            "achieved_distinct": round(pbytes / (ms_p * 1e-3) / 1e9, 1),
                            "achieved_survey_formula": round(nbytes / (ms_p * 1e-3) / 1e9, 1)}
+    # the backward (destination + source pass per call) in the model's layout, both forms
+    bwd = {}
+    for tag, dr in (("training_form", False), ("dr_force_form", True)):
+        for _ in range(3):
+            launch.bwd(dr)
+        torch.cuda.synchronize()
+        nrep = max(4, reps // 2)
+        a0.record()
+        for _ in range(nrep):
+            launch.bwd(dr)
+        b0.record()
+        torch.cuda.synchronize()
+        ms_b = a0.elapsed_time(b0) / nrep
+        bb = et_bwd_bytes(E, n_atoms, launch.n_pairs, H, dr)
+        gb = bb / (ms_b * 1e-3) / 1e9
+        bwd[tag] = {"kernels": "k_bwd_dst + k_bwd_src (one tmdnet_et_message_bwd call)" + (" , dr" if dr else ""),
+                    "ms_per_call": round(ms_b, 4), "bytes_per_call": bb, "achieved": round(gb, 1),
+                    "frac": round(gb / HBM_PEAK_GBS, 4), "calls": nrep}
+    res["backward"] = bwd
     if not a.no_pmc:
-        traffic, detail = pmc_traffic(a)
-        res["traffic"] = None if traffic is None else round(traffic)
-        res["traffic_detail"] = detail
+        pm, why = pmc_counters(a)
+        if pm is None:
+            res["traffic_detail"] = why
+        else:
+            g = pm.get("graded", {})
+            res["traffic"] = g.get("traffic")
+            res["traffic_detail"] = {**g, "source": PMC_SOURCE}
+            res["model_layout"]["pmc"] = pm.get("pairs")
+            for tag, keys in (("training_form", ("bwd_dst", "bwd_src")), ("dr_force_form", ("bwd_dst_dr", "bwd_src_dr"))):
+                bwd[tag]["pmc"] = {k: pm.get(k) for k in keys}
     return res
 
 
@@ -356,6 +447,36 @@ def mfma_probe(E_c5, N_c5, E_c2, N_c2, H, R, dev):
                     "output_bytes": E * cols * 4,
                     "output_write_bound_ms": round(E * cols * 4 / (HBM_PEAK_GBS * 1e9) * 1e3, 4)}
         del f, w, b, out
+    # the hand-written grouped node-mix GEMM (tmdnet_gemm_f32, csrc/gemm.hip) at the C2 metric batch:
+    # forward [q|k|v] + vec_proj in one launch, backward [q|k|v]^T + vec_proj^T (K split over 16 waves)
+    from torchmdnet import kernels
+    Hh, Na = H, N_c2
+    gen = torch.Generator(device=dev).manual_seed(6)
+    rn = lambda *sh: torch.randn(*sh, device=dev, generator=gen)  # noqa: E731
+    xn, vec, wq, wv = rn(Na, Hh), rn(3 * Na, Hh), rn(5 * Hh, Hh), rn(3 * Hh, Hh)
+    qkv, vecp = torch.empty(Na, 5 * Hh, device=dev), torch.empty(3 * Na, 3 * Hh, device=dev)
+    gxn, gvec = torch.empty(Na, Hh, device=dev), torch.empty(3 * Na, Hh, device=dev)
+    node = {}
+    for tag, probs, flop in (
+            ("forward_qkv_vecproj", [(xn, wq, True, None, qkv, False), (vec, wv, True, None, vecp, False)],
+             2.0 * Na * 5 * Hh * Hh + 2.0 * 3 * Na * 3 * Hh * Hh),
+            ("backward_qkvT_vecprojT", [(qkv, wq, False, None, gxn, False), (vecp, wv, False, None, gvec, True)],
+             2.0 * Na * 5 * Hh * Hh + 2.0 * 3 * Na * 3 * Hh * Hh)):
+        for _ in range(5):
+            kernels.gemm_group(probs)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(100):
+            kernels.gemm_group(probs)
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / 100
+        tf = flop / (ms * 1e-3) / 1e12
+        node[tag] = {"ms_per_launch": round(ms, 5), "flop": flop, "achieved": round(tf, 2),
+                     "frac": round(tf / MFMA_F32_PEAK_TFS, 4)}
+    res["node_mix_c2"] = {"kernel": "tmdnet_gemm_f32 (grouped split-K fp32 MFMA, csrc/gemm.hip)",
+                          "shape": f"N={Na} atoms, H={Hh}: [N x H][H x 5H] + [3N x H][H x 3H] per launch", **node}
     return {"kernel": "dk/dv projection GEMM (SURVEY 8(a) a13)", "bound": "mfma", "unit": "TFLOP/s",
             "peak": MFMA_F32_PEAK_TFS, "dtype": "fp32 (the reference computes in fp32; gfx950 has no xf32)",
             **res}
@@ -649,12 +770,18 @@ def cpu_baseline_extra(a, model, args, z, pos, batch):
 
 def main():
     a = parse()
-    if a.pmc_child:  # profiled child of pmc_traffic(): the probe kernel only
+    if a.pmc_child:  # profiled child of pmc_counters(): the probe kernels in the PMC_CHILD order
         torch.cuda.set_device(0)
         dev = torch.device("cuda", 0)
         launch, _, _ = probe_workload(a.roofline_atoms, a.channels, dev)
         for _ in range(8):
             launch()
+        for _ in range(8):
+            launch.pairs()
+        for _ in range(4):
+            launch.bwd(False)
+        for _ in range(4):
+            launch.bwd(True)
         torch.cuda.synchronize()
         return
     maybe_spawn(a)

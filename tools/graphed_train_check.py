@@ -42,7 +42,7 @@ torch.cuda.synchronize()
 gtr.check_capacity()
 rel = lambda a, b: float((a - b).norm() / b.norm().clamp_min(1e-30))  # noqa: E731
 loss_rel = abs(float(gtr.static_loss) - float(loss_ref)) / abs(float(loss_ref))
-grad_rel = max(rel(a, b) for a, b in zip(gtr.static_grads, g_ref))
+grad_rel = max(rel(a, b) for a, b in zip(gtr.reduce.views, g_ref))  # the replay writes them there
 print("replay matches", loss_rel, grad_rel, file=sys.stderr, flush=True)
 for _ in range(3):
     gtr.step()

@@ -13,10 +13,10 @@ root=$(pwd)
 out=$root/gpurun_out/prof_$tag
 mkdir -p "$out"
 export TMPDIR=/tmp
-[ "$2" = "stats-only" ] || timeout -k 10 420 python3 bench.py > "$out/bench.json" 2> "$out/bench.err"
+[ "$2" = "stats-only" ] || timeout -k 10 600 python3 bench.py > "$out/bench.json" 2> "$out/bench.err"
 cd /tmp
 rm -rf /tmp/prof_stats /tmp/prof_et /tmp/prof_tn
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/prof_stats -o run -- \
+timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/prof_stats -o run -- \
   python3 "$root/bench.py" --no-cpu-baseline --no-pmc > "$out/bench_under_rocprof.json" 2> "$out/rocprof.err"
 cp "$(find /tmp/prof_stats -name '*kernel_stats.csv' | head -1)" "$out/bench_kernel_stats.csv"
 python3 "$root/tools/roofline_from_trace.py" "$(find /tmp/prof_stats -name '*kernel_trace.csv' | head -1)" \

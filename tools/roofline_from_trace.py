@@ -38,3 +38,17 @@ for run in probe:
           f"{sum(graded) / len(graded) / 1e6:.4f} ms")
     print(f"roofline.model_layout (pair rows): {len(model)} timed launches, average "
           f"{sum(model) / len(model) / 1e6:.4f} ms")
+
+# the backward probes (bench.py roofline_probe "backward"): 3 warm-up + reps // 2 timed calls of the
+# training form, then of the dr form; each call is one k_bwd_dst and one k_bwd_src launch.  They are the
+# last launches of these kernels in the run (the model's C5 force pass runs earlier).
+nb = max(4, reps // 2)
+for kname in ("k_bwd_dst<", "k_bwd_src<"):
+    ds = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows if kname in r["Kernel_Name"]]
+    if len(ds) < 2 * (3 + nb):
+        print(f"{kname}: fewer than {2 * (3 + nb)} launches")
+        continue
+    tail = ds[-2 * (3 + nb):]
+    tr, dr = tail[3:3 + nb], tail[3 + nb + 3:]
+    print(f"backward {kname[:-1]} training form: {len(tr)} launches, average {sum(tr) / len(tr) / 1e6:.4f} ms; "
+          f"dr form: {len(dr)} launches, average {sum(dr) / len(dr) / 1e6:.4f} ms")
