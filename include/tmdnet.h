@@ -193,7 +193,7 @@ int tmdnet_et_message_bwd(int dtype, int n_nodes, int hidden, int heads, const i
                           const void* dpk, const void* dpv, void* gdist, int accumulate,
                           const int32_t* pk_rows, const int32_t* order,
                           void* stream);  /* accumulate may also carry TMDNET_ET_V_PLANAR */
-/* "dr mode" of the backward (gdist non-NULL, requires TMDNET_ACC_EDGE): instead of storing gpk / gpv
+/* "dr mode" of the backward (gdist non-NULL; with TMDNET_ACC_EDGE it accumulates, without it overwrites): instead of storing gpk / gpv
  * (then NULL), the projection gradient of every edge is contracted in-kernel with dpk = d pk / d r,
  * dpv = d pv / d r (rows and layout of pk / pv, read through pk_rows) and accumulated into
  * gdist[e] -- the force pass then needs neither the E x 4H gradient nor its GEMM. */
@@ -340,7 +340,8 @@ int tmdnet_nbr_embed_fwd(int dtype, int n_nodes, int hidden, const int32_t* row_
                          const int32_t* src, int max_pairs, const void* x, int ld_x, const void* w,
                          int ld_w, const void* cutoff, void* out, int ld_out, const void* x_self,
                          void* out_self, void* stream);
-/* Backward: gx[s] (source pass, symmetric list), gw[e], gcut[e] (destination pass); overwritten.
+/* Backward: gx[s] (source pass, symmetric list; gx NULL: not computed -- the force pass never needs it),
+ * gw[e], gcut[e] (destination pass, every slot < max_pairs written: padding slots zero); overwritten.
  * ld_out / ld_grad_out: row strides of out / grad_out (0 = hidden), so the output can be the right
  * half of the combine Linear's [x | x_nb] input (reference utils.py:108) and its gradient read from
  * that layout in place; x_self / out_self (both or neither): the forward also copies x_self [n][hidden]

@@ -103,7 +103,9 @@ def _fake_bwd(q, k, v, vec, pk, pv, C, u, graph, heads, gx, gvec, gq, gk, gv, gw
     if gpv is not None:
         put(gpv, _to_planar(z(g[5], pv), H, heads, planar))
     if g_r is not None:  # dr mode: <g_pk, dpk> + <g_pv, dpv> per edge (dpv in the kernel's row layout)
-        assert gpk is None and gpv is None and accumulate & nat.ACC_EDGE
+        assert gpk is None and gpv is None
+        if not accumulate & nat.ACC_EDGE:
+            g_r.zero_()
         if dpk is not None:
             g_r.add_((z(g[4], pk) * dpk).sum(1))
         if dpv is not None:

@@ -360,6 +360,8 @@ __device__ __forceinline__ void zero_pad_rows(const Args<T>& A, int blk, int nwg
     for (long long i = tid; i < rows; i += nth) A.gC[e0 + i] = T(0);
   if (A.gu)
     for (long long i = tid; i < rows * 3; i += nth) A.gu[3 * (size_t)e0 + i] = T(0);
+  if (A.gr)
+    for (long long i = tid; i < rows; i += nth) A.gr[e0 + i] = T(0);
 }
 
 template <typename T, int V, int S, int CS, bool DR>
@@ -900,7 +902,8 @@ __global__ __launch_bounds__(256) void k_bwd2(Args2<T> B) {
 
 // Source pass of the second order: node j's k / v / vec terms are the sum of the scratch rows of the
 // edges leaving j, i.e. the reverses tr[e'] of the edges e' of row j.  One wave per node, 4 columns
-// per lane, the row's edges unrolled by 4 so their loads are in flight together.
+// per lane, the row's edges unrolled by 4 so their loads are in flight together.  A capacity-truncated
+// list (a step the capacity check discards) leaves tr[e] = -1 where the reverse was cut off: no term.
 template <typename T>
 __global__ __launch_bounds__(256) void k_bwd2_src(Args2<T> B) {
   using V4 = T __attribute__((ext_vector_type(4)));
@@ -917,13 +920,16 @@ __global__ __launch_bounds__(256) void k_bwd2_src(Args2<T> B) {
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int k = B.tr[i + u];
-        TMD_DCHECK(k >= 0 && k < A.cap);
-        r[u] = *reinterpret_cast<const V4*>(B.o_src + (size_t)k * W + c);
+        TMD_DCHECK(k < A.cap);
+        r[u] = k >= 0 ? *reinterpret_cast<const V4*>(B.o_src + (size_t)k * W + c) : V4{T(0), T(0), T(0), T(0)};
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) acc += r[u];
     }
-    for (; i < e; ++i) acc += *reinterpret_cast<const V4*>(B.o_src + (size_t)B.tr[i] * W + c);
+    for (; i < e; ++i) {
+      const int k = B.tr[i];
+      if (k >= 0) acc += *reinterpret_cast<const V4*>(B.o_src + (size_t)k * W + c);
+    }
     T* dst;
     if (c < A.H) dst = B.o_k + (size_t)j * B.ldok + c;
     else if (c < 4 * A.H) dst = B.o_v + (size_t)j * B.ldov + (c - A.H);
@@ -1015,9 +1021,17 @@ __global__ __launch_bounds__(256) void k_nb_fwd(NbArgs<T> A) {
   }
 }
 
-// destination pass: gw[e] = gout[t] * x[s] * C[e], gC[e] = sum_c gout[t] x[s] w[e]
+// destination pass: gw[e] = gout[t] * x[s] * C[e], gC[e] = sum_c gout[t] x[s] w[e]; the static-capacity
+// padding slots [row_ptr[n], cap) of gw / gC are zeroed here too (no memset before the launch)
 template <typename T, int V>
 __global__ __launch_bounds__(256) void k_nb_bwd_dst(NbArgs<T> A) {
+  {
+    const int e0 = min(A.row_ptr[A.n], A.cap);
+    const long long rows = A.cap - e0;
+    const long long tid = (long long)blockIdx.x * blockDim.x + threadIdx.x, nth = (long long)gridDim.x * blockDim.x;
+    for (long long i = tid; i < rows * A.H; i += nth) A.gw[(size_t)e0 * A.H + i] = T(0);
+    for (long long i = tid; i < rows; i += nth) A.gC[e0 + i] = T(0);
+  }
   const int t = blockIdx.x * (blockDim.x / TMD_WAVE) + threadIdx.x / TMD_WAVE;
   if (t >= A.n) return;
   const int lane = lane_id();
@@ -1163,10 +1177,11 @@ __global__ __launch_bounds__(256) void k_nb_bwd2_src(NbArgs<T> A) {
     T gm[NB_U][V], wk[NB_U][V], gwk[NB_U][V], ck[NB_U], gck[NB_U];
 #pragma unroll
     for (int u = 0; u < NB_U; ++u) {
-      const bool live = sq[u] >= 0 && sq[u] != j;
+      const int kt = sq[u] >= 0 ? A.tr[k0 + u] : -1;  // the edge j -> m
+      const bool live = kt >= 0 && sq[u] != j;
       const int m = live ? sq[u] : j;
-      const int k = live ? A.tr[k0 + u] : k0;  // the edge j -> m
-      TMD_DCHECK(!live || (k >= 0 && k < A.cap));
+      const int k = live ? kt : k0;
+      TMD_DCHECK(!live || k < A.cap);
       ldv<T, V>(gm[u], A.gout + (size_t)m * A.ldg + c0);
       ldv<T, V>(wk[u], A.w + (size_t)k * A.ldw + c0);
       if (A.ggw) ldv<T, V>(gwk[u], A.ggw + (size_t)k * A.H + c0); else zero(gwk[u]);
@@ -1335,7 +1350,7 @@ static int bwd(int n, int H, int heads, const int32_t* row_ptr, const int32_t* s
   A.acc = acc;
   if (acc & TMDNET_ET_V_PLANAR) { A.planar = 1; A.vst = H; }
   const bool dr = gr != nullptr;
-  if (dr && ((A.pk && !dpk) || (A.pv && !dpv) || !(acc & TMDNET_ACC_EDGE))) return kBadArgument;
+  if (dr && ((A.pk && !dpk) || (A.pv && !dpv))) return kBadArgument;
   if (!dr && ((A.pk && !gpk) || (A.pv && !gpv))) return kBadArgument;
   static const int fuse_nodes = getenv("TMDNET_ET_FUSE") ? atoi(getenv("TMDNET_ET_FUSE")) : kBwdFuseNodes;
   if (n < fuse_nodes) return dr ? et_launch<T, 5, false>(V, A, st) : et_launch<T, 3, false>(V, A, st);
@@ -1554,9 +1569,10 @@ static int nb_bwd_t(int n, int H, const int32_t* row_ptr, const int32_t* src, in
   A.ldg = ldg ? ldg : H;
   if (A.ldg < H || !et::aligned<T>(gout, A.ldg, V)) return kBadArgument;
   A.gx = (T*)gx; A.gw = (T*)gw; A.gC = (T*)gC;
+  if (!gw || !gC) return kBadArgument;
   rc = et::launch_v<T, et::KNbDst>(V, n, A, st);
   if (rc) return rc;
-  return et::launch_v<T, et::KNbSrc>(V, n, A, st);
+  return gx ? et::launch_v<T, et::KNbSrc>(V, n, A, st) : kOk;  // gx NULL: the source pass is skipped
 }
 
 extern "C" int tmdnet_nbr_embed_fwd(int dtype, int n_nodes, int hidden, const int32_t* row_ptr,

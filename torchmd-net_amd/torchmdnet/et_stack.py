@@ -377,8 +377,9 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws, r=None, dr=Fa
         lst = inj.get(key)
         return None if lst is None else lst[l]
 
-    # the kernels accumulate the edge gradients (g_C, g_u, g_r) across layers: one zeroed buffer
-    zbuf = torch.zeros(((5 if dr else 4) * E,), **o)
+    # the kernels accumulate the edge gradients (g_C, g_u, g_r) across layers into one buffer; the
+    # first layer of the backward overwrites it (every slot, padding included): no zero fill
+    zbuf = torch.empty(((5 if dr else 4) * E,), **o)
     g_C, g_u = zbuf[:E], zbuf[E:4 * E].view(E, 3)
     g_r = None
     if dr:
@@ -466,7 +467,8 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws, r=None, dr=Fa
         kernels.et_message_bwd_launch(
             qkv[:, :H], qkv[:, H:2 * H], qkv[:, 2 * H:], vec, pk, pv, C, u, graph, meta.heads, g_xa, gV,
             g_qkv[:, :H], g_qkv[:, H:2 * H], g_qkv[:, 2 * H:], g_vec_in, gpk, gpv, g_C, g_u,
-            accumulate=nat.ACC_VEC_RESIDUAL | nat.ACC_EDGE | meta.flags | (nat.ACC_GRADS if acc else 0),
+            accumulate=(nat.ACC_VEC_RESIDUAL | (nat.ACC_EDGE if l < L - 1 else 0) | meta.flags
+                        | (nat.ACC_GRADS if acc else 0)),
             pk_rows=meta.pk_rows, dpk=dpk, dpv=dpv, g_r=g_r)
         if not acc:
             if injected("qkv", l) is not None:

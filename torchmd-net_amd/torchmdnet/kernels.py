@@ -854,20 +854,23 @@ class _NbrEmbed(Function):
             gout = gout.contiguous()
         if ctx.has_self:  # the two halves are read in place (row stride 2H)
             g_self, gout = gout[:, :H], gout[:, H:]
-        gx, gw, gC = _NbrEmbedBwd.apply(gout, x, w, C, ctx.graph)
+        # the embedding rows' gradient only when something consumes it (never in a force pass)
+        want_x = bool(ctx.needs_input_grad[0]) and _will_run(ctx.next_functions[0][0])
+        gx, gw, gC = _NbrEmbedBwd.apply(gout, x, w, C, ctx.graph, want_x)
         return gx, gw, gC, None, g_self
 
 
 class _NbrEmbedBwd(Function):
     @staticmethod
-    def forward(ctx, gout, x, w, C, graph):
+    def forward(ctx, gout, x, w, C, graph, want_x=True):
         if not graph.symmetric:
             raise RuntimeError("torchmd-net_amd: neighbour-embedding backward needs a symmetric edge list")
         lib = nat.load()
         N, H = x.shape
         E = graph.n_edges
-        gx = torch.empty_like(x, memory_format=torch.contiguous_format)
-        zbuf = graph.alloc_edge_grad((E * (H + 1),), x.dtype, x.device)  # one zero fill for both
+        gx = torch.empty_like(x, memory_format=torch.contiguous_format) if want_x else None
+        # every slot written by the kernel (padding slots zero): no fill
+        zbuf = torch.empty((E * (H + 1),), dtype=x.dtype, device=x.device)
         gw, gC = zbuf[:E * H].view(E, H), zbuf[E * H:]
         rc = lib.tmdnet_nbr_embed_bwd(nat.dtype_code(x.dtype), N, H, nat.ptr(graph.row_ptr),
                                       nat.ptr(graph.src), E, nat.ptr(x), _ld(x), nat.ptr(w), _ld(w),
@@ -887,7 +890,7 @@ class _NbrEmbedBwd(Function):
             nodes = [e[0] for e in ctx.next_functions]  # one per tensor input: gout, x, w, C
             want = [bool(ctx.needs_input_grad[i]) and _will_run(nodes[i]) for i in range(4)]
             if not any(want):
-                return (None,) * 5
+                return (None,) * 6
             N, H = x.shape
             E = graph.n_edges
             d_go = torch.empty((N, H), dtype=x.dtype, device=x.device) if want[0] else None
@@ -904,7 +907,7 @@ class _NbrEmbedBwd(Function):
                 nat.ptr(None if ggC is None else ggC.contiguous()), nat.ptr(d_go), nat.ptr(d_x), nat.ptr(d_w),
                 nat.ptr(d_C), nat.stream(x.device))
             nat.check(rc, "tmdnet_nbr_embed_bwd2")
-            return d_go, d_x, d_w, d_C, None
+            return d_go, d_x, d_w, d_C, None, None
         src, dst = graph.src.long(), graph.dst.long()
         with torch.enable_grad():
             leaves = [t.detach().requires_grad_(True) for t in (gout, x, w, C)]
@@ -913,10 +916,10 @@ class _NbrEmbedBwd(Function):
             first = torch.autograd.grad(out, (x_, w_, C_), go, create_graph=True)
             sel = [(f, g) for f, g in zip(first, (ggx, ggw, ggC)) if g is not None]
             if not sel:
-                return (None,) * 5
+                return (None,) * 6
             second = torch.autograd.grad([f for f, _ in sel], leaves, [g for _, g in sel],
                                          create_graph=_create, allow_unused=True)
-        return tuple(second) + (None,)
+        return tuple(second) + (None, None)
 
 
 def nbr_embed(x, w, C, graph, x_self=None):
