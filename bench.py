@@ -230,14 +230,21 @@ def probe_workload(n_atoms, H, dev):
     # the backward in the model's layout (destination + source CSR passes, one C-ABI call): the
     # training form (per-edge projection gradient written) and the force-pass "dr" form (contracted
     # with d(dk,dv)/dr of the pair rows in-kernel, g_r accumulated)
-    gx, gvec = rn(n_atoms, H), rn(n_atoms, 3, H)
-    gq, gk, gv, gw = (torch.empty(n_atoms, H, device=dev), torch.empty(n_atoms, H, device=dev),
-                      torch.empty(n_atoms, 3 * H, device=dev), torch.empty(n_atoms, 3, H, device=dev))
-    gpk, gpv = torch.empty(E, H, device=dev), torch.empty(E, 3 * H, device=dev)
-    gC, gu, gr = torch.zeros(E, device=dev), torch.zeros(E, 3, device=dev), torch.zeros(E, device=dev)
-    dpk, dpv = rn(P, H), rn(P, 3 * H)
+    # (allocated on the first backward launch: the forward probes run with only their own inputs
+    # resident, as in the model's forward)
+    bw = {}
 
     def launch_bwd(dr=False):
+        if not bw:
+            bw["gx"], bw["gvec"] = rn(n_atoms, H), rn(n_atoms, 3, H)
+            bw["gq"], bw["gk"] = torch.empty(n_atoms, H, device=dev), torch.empty(n_atoms, H, device=dev)
+            bw["gv"], bw["gw"] = torch.empty(n_atoms, 3 * H, device=dev), torch.empty(n_atoms, 3, H, device=dev)
+            bw["gpk"], bw["gpv"] = torch.empty(E, H, device=dev), torch.empty(E, 3 * H, device=dev)
+            bw["gC"], bw["gu"], bw["gr"] = (torch.zeros(E, device=dev), torch.zeros(E, 3, device=dev),
+                                            torch.zeros(E, device=dev))
+            bw["dpk"], bw["dpv"] = rn(P, H), rn(P, 3 * H)
+        gx, gvec, gq, gk, gv, gw = bw["gx"], bw["gvec"], bw["gq"], bw["gk"], bw["gv"], bw["gw"]
+        gpk, gpv, gC, gu, gr, dpk, dpv = bw["gpk"], bw["gpv"], bw["gC"], bw["gu"], bw["gr"], bw["dpk"], bw["dpv"]
         acc = 1 | 2 | PROBE_FLAGS  # TMDNET_ACC_VEC_RESIDUAL | TMDNET_ACC_EDGE | planar rows
         rc = lib.tmdnet_et_message_bwd(
             0, n_atoms, H, 8, ptr(graph.row_ptr), ptr(graph.src), E, ptr(q), H, ptr(k), H, ptr(v), 3 * H,
@@ -902,6 +909,11 @@ def main():
             out["ddp_train"] = dt
     if rank == 0 and not a.no_roofline:
         phase("roofline probe (C5 water box)")
+        # the secondary lines leave tens of GB in the caching allocator's segments: hand them back so
+        # the probe's 10+ GB of inputs are laid out as in a fresh process
+        import gc
+        gc.collect()
+        torch.cuda.empty_cache()
         out["roofline"] = roofline_probe(a, dev)
         phase("MFMA probe (dk/dv projection GEMM)")
         E_c5 = int(out["roofline"]["workload"].split("E=")[1].split(",")[0])

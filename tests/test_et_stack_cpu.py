@@ -412,11 +412,15 @@ def test_stack_partial_parameter_request(emulated):
 @pytest.mark.parametrize("planar", [False, True])
 @pytest.mark.parametrize("batched", [True, False])
 @pytest.mark.parametrize("infl", ["both", "keys", "values"])
-def test_stack_dr_mode_force_pass_and_second_order(emulated, monkeypatch, infl, batched, planar, rbf_type):
+@pytest.mark.parametrize("record", [True, False])
+def test_stack_dr_mode_force_pass_and_second_order(emulated, monkeypatch, record, infl, batched, planar, rbf_type):
     """Force pass with f = rbf(r) declared (the ET model's fixed basis): the stack returns the edge
     gradient on r directly (dr mode, no projection gradient); forces and the force-matching second
-    order (weight gradients through a create_graph force pass) equal plain autograd."""
+    order (weight gradients through a create_graph force pass) equal plain autograd.  ``record``: the
+    create_graph force pass runs the recorded training form (g_r = <g_f, df/dr>) and hands its record
+    to the hand second order (RECORD_IN_FORCE_PASS) instead of the second order re-running it."""
     monkeypatch.setattr(ES, "DR_MODE", "1")  # also on the stacked (batched) projection path
+    monkeypatch.setattr(ES, "RECORD_IN_FORCE_PASS", record)
     if not batched:
         monkeypatch.setattr(ES, "BATCH_DKV_BYTES", 0)
     if planar:
@@ -435,7 +439,7 @@ def test_stack_dr_mode_force_pass_and_second_order(emulated, monkeypatch, infl, 
     orig = ES._backward_layers
 
     def spy(*a, **kw):
-        modes.append(kw.get("dr", False))
+        modes.append((kw.get("dr", False), kw.get("record") is not None))
         return orig(*a, **kw)
 
     monkeypatch.setattr(ES, "_backward_layers", spy)
@@ -448,13 +452,18 @@ def test_stack_dr_mode_force_pass_and_second_order(emulated, monkeypatch, infl, 
         else:
             xo, vo = ES.composite_stack(_meta_for(layers, graph), xl, f, Cl, ul, params)
         e = (xo ** 2).sum() + 0.3 * (vo ** 2).sum()
-        g = torch.autograd.grad(e, [rl, xl, Cl, ul], create_graph=True)
+        with ES.second_order_expected():
+            g = torch.autograd.grad(e, [rl, xl, Cl, ul], create_graph=True)
         loss = e + sum((gi ** 2).sum() for gi in g)
         for p in params:
             p.grad = None
         loss.backward()
         outs.append([t.detach().clone() for t in g] + [p.grad.clone() for p in params])
-    assert modes[0] is True and modes[1] is False  # force pass in dr mode, loss.backward not
+    hand = not planar  # the hand second order covers the reference row layout
+    if record and hand:  # force pass recorded (training form), no re-run inside the second order
+        assert modes[0] == (False, True) and not any(rec for _, rec in modes[1:])
+    else:  # force pass in dr mode; loss.backward's passes not
+        assert modes[0] == (True, False) and not modes[1][0]
     for i, (a, b) in enumerate(zip(*outs)):
         assert torch.allclose(a, b, atol=1e-10, rtol=1e-8), i
 

@@ -49,9 +49,13 @@ def test_adjoint_epi_ln_kernel(dtype, tol, with_vec, with_epi, with_ln):
         assert _rel(ta, tb) < tol, (i, _rel(ta, tb))
 
 
+@pytest.mark.parametrize("record", [True, False])
 @pytest.mark.parametrize("dr", ["1", "0"])
 @pytest.mark.parametrize("out_norm", [True, False])
-def test_hand_second_order_on_model(monkeypatch, dr, out_norm):
+def test_hand_second_order_on_model(monkeypatch, dr, out_norm, record):
+    """Training gradients (E + F loss through the create_graph force pass) of the hand second order vs
+    autograd over the composite; ``record``: the force pass runs inside second_order_expected() (as
+    the training steps do) and hands its record to the second order instead of it being re-run."""
     from torchmdnet import et_stack as ES
     from torchmdnet.models.model import create_model
     monkeypatch.setattr(ES, "DR_MODE", dr)
@@ -75,7 +79,8 @@ def test_hand_second_order_on_model(monkeypatch, dr, out_norm):
     for mode in ("hand", "composite"):
         monkeypatch.setattr(ES, "SECOND_ORDER", mode)
         params = [p for p in model.parameters() if p.requires_grad]
-        y, neg_dy = model(z, pos.clone(), batch)
+        with ES.second_order_expected(record):
+            y, neg_dy = model(z, pos.clone(), batch)
         loss = ((y - y_t) ** 2).mean() + ((neg_dy - f_t) ** 2).mean()
         grads.append(torch.autograd.grad(loss, params, allow_unused=True))
     assert calls

@@ -917,18 +917,22 @@ __global__ __launch_bounds__(256) void k_bwd2_src(Args2<T> B) {
     int i = b;
     for (; i + 4 <= e; i += 4) {
       V4 r[4];
+      int tk[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const int k = B.tr[i + u];
-        TMD_DCHECK(k < A.cap);
-        r[u] = k >= 0 ? *reinterpret_cast<const V4*>(B.o_src + (size_t)k * W + c) : V4{T(0), T(0), T(0), T(0)};
+        tk[u] = B.tr[i + u];
+        TMD_DCHECK(tk[u] < A.cap);
+        // unconditional load (row 0 for a cut-off reverse, dropped below): the four stay in flight together
+        r[u] = *reinterpret_cast<const V4*>(B.o_src + (size_t)max(tk[u], 0) * W + c);
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) acc += r[u];
+      for (int u = 0; u < 4; ++u)
+        if (tk[u] >= 0) acc += r[u];
     }
     for (; i < e; ++i) {
       const int k = B.tr[i];
-      if (k >= 0) acc += *reinterpret_cast<const V4*>(B.o_src + (size_t)k * W + c);
+      const V4 r1 = *reinterpret_cast<const V4*>(B.o_src + (size_t)max(k, 0) * W + c);
+      if (k >= 0) acc += r1;
     }
     T* dst;
     if (c < A.H) dst = B.o_k + (size_t)j * B.ldok + c;

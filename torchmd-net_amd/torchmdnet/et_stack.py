@@ -24,6 +24,7 @@ and autograd's generic per-op backward.
 The backward is itself a Function so forces stay differentiable (training on forces); its own
 backward (second order) recomputes the stack with composite PyTorch ops and differentiates twice.
 """
+import contextlib
 import os
 import weakref
 
@@ -130,6 +131,26 @@ DR_MODE = os.environ.get("TMDNET_DR", "auto")
 # second order of the force pass (force-matching training): "hand" = the hand-scheduled adjoint
 # (_second_order), "composite" = autograd over the recomputed stack (the reference for tests / A-B)
 SECOND_ORDER = os.environ.get("TMDNET_ET_SECOND_ORDER", "hand")
+# under create_graph the force pass itself runs in the recorded training form (g_r = <g_f, df/dr>) and
+# hands its record to the hand second order, which then skips re-running it.  TMDNET_ET_RECORD=0: the
+# dr-mode force pass + a recorded re-run inside the second order (the previous scheme, for A/B)
+RECORD_IN_FORCE_PASS = os.environ.get("TMDNET_ET_RECORD", "1") not in ("0", "off")
+# ... but only inside ``second_order_expected()`` (the training steps): the reference force pass always
+# builds its graph (create_graph=True), so create_graph alone does not say a second backward follows,
+# and an energy+force evaluation must keep the cheaper dr-mode force pass
+_EXPECT_SECOND_ORDER = [False]
+
+
+@contextlib.contextmanager
+def second_order_expected(on=True):
+    """Declare that the force pass(es) run inside will be differentiated again (force-matching
+    training): the ET stack's force pass then records what the hand second order needs."""
+    prev = _EXPECT_SECOND_ORDER[0]
+    _EXPECT_SECOND_ORDER[0] = bool(on)
+    try:
+        yield
+    finally:
+        _EXPECT_SECOND_ORDER[0] = prev
 
 _PERMS = {}
 
@@ -734,10 +755,14 @@ def _second_order(ctx, ggs, want):
     gg_x, gg_f, gg_C, gg_u, gg_r = ggs[:5]
     layers = meta.split(params)
     need_none = (False,) * (L + int(meta.out_norm))
-    # 1. the force pass again, recorded (its outputs are those of the dr-mode pass up to round-off)
-    rec = []
-    _, g_f0, _, _, _, _ = _backward_layers(meta, gX, gV, f, C, u, params, acts, need_none, record=rec,
-                                           want_f=bool(want[6]))  # g_f0: only for d/dr of g_r
+    # 1. the force pass recorded: by the force pass itself when it ran under create_graph (ctx.rec),
+    # else again here (its outputs are those of the dr-mode pass up to round-off)
+    rec, g_f0 = getattr(ctx, "rec", None), getattr(ctx, "g_f0", None)
+    ctx.rec = ctx.g_f0 = None
+    if rec is None:
+        rec = []
+        _, g_f0, _, _, _, _ = _backward_layers(meta, gX, gV, f, C, u, params, acts, need_none, record=rec,
+                                               want_f=bool(want[6]))  # g_f0: only for d/dr of g_r
     tail = rec.pop()
     g_pkv_all = tail["g_pkv"] if has_e else None
     rg_qkv_all, rg_o_all, rg_vecp_all = tail["stacks"]
@@ -1014,22 +1039,36 @@ class _ETStack(Function):
             dr = False
         # the edge-feature gradient only when something consumes it (never in a parameter backward)
         want_f = f is not None and ctx.needs_input_grad[2] and _will_run(nf[1][0])
-        outs = _ETStackBwd.apply(meta, ctx.acts, need_w, dr, pending, want_f, gX.contiguous(), gV.contiguous(),
-                                 x, f, C, u, r, *params)
+        # a force pass whose own backward will be taken (create_graph: force-matching training) records
+        # its intermediates for the hand second order right here, instead of the second order re-running
+        # it: the training form (projection gradient materialised) with g_r = <g_f, df/dr> per edge
+        record = (dr and torch.is_grad_enabled() and _EXPECT_SECOND_ORDER[0] and SECOND_ORDER != "composite"
+                  and RECORD_IN_FORCE_PASS and hand_second_order_ok(meta, dr, need_w, ()))
+        outs = _ETStackBwd.apply(meta, ctx.acts, need_w, dr, pending, want_f, record, gX.contiguous(),
+                                 gV.contiguous(), x, f, C, u, r, *params)
         g_x, g_f, g_C, g_u, g_r = outs[:5]
         return (None, g_x, g_f, g_C, g_u, g_r) + tuple(outs[5:])
 
 
 class _ETStackBwd(Function):
     @staticmethod
-    def forward(ctx, meta, acts, need_w, dr, pending, want_f, gX, gV, x, f, C, u, r, *params):
+    def forward(ctx, meta, acts, need_w, dr, pending, want_f, record, gX, gV, x, f, C, u, r, *params):
         if not meta.graph.symmetric:
             raise RuntimeError("torchmd-net_amd: the ET backward source pass needs a symmetric edge "
                                "list (include_transpose=True, no capacity overflow)")
-        g_x, g_f, g_C, g_u, g_r, g_params = _backward_layers(meta, gX, gV, f, C, u, params, acts, need_w,
-                                                             r=r, dr=dr,
-                                                             inject=pending["inj"] if pending else None,
-                                                             want_f=want_f)
+        ctx.rec = None
+        if record:  # dr-mode outputs from the recorded training form (see _ETStack.backward)
+            rec = []
+            g_x, g_f0, g_C, g_u, _, g_params = _backward_layers(meta, gX, gV, f, C, u, params, acts, need_w,
+                                                                record=rec, want_f=True)
+            g_r = (g_f0 * kernels.rbf_deriv(r, *meta.rbf)).sum(1)  # (einsum lowers this to E tiny GEMMs)
+            g_f = None
+            ctx.rec, ctx.g_f0 = rec, g_f0
+        else:
+            g_x, g_f, g_C, g_u, g_r, g_params = _backward_layers(meta, gX, gV, f, C, u, params, acts, need_w,
+                                                                 r=r, dr=dr,
+                                                                 inject=pending["inj"] if pending else None,
+                                                                 want_f=want_f)
         if pending is not None:  # the second order's contributions (et_stack._second_order)
             g_C = g_C + pending["C_bar"]
             g_u = g_u + pending["u_bar"]
@@ -1059,7 +1098,7 @@ class _ETStackBwd(Function):
             return kernels.et_message(q, k, v, vec, pk, pv, C_, u_, graph, heads)
 
         _create = torch.is_grad_enabled()  # third order only if the caller builds a graph
-        n_out = 6 + len(saved)
+        n_out = 7 + len(saved)
         # inputs whose gradient this backward must deliver: asked for AND consumed downstream (a
         # training step's loss.backward(inputs=params) never runs the position branch, so the
         # cutoff / unit-vector / distance gradients -- E-sized work -- are skipped)
@@ -1067,11 +1106,11 @@ class _ETStackBwd(Function):
         want = []
         for i, t in enumerate(saved):
             node = next(nf)[0] if t is not None else None
-            want.append(t is not None and ctx.needs_input_grad[6 + i] and _will_run(node))
+            want.append(t is not None and ctx.needs_input_grad[7 + i] and _will_run(node))
         if SECOND_ORDER != "composite" and not _create and hand_second_order_ok(meta, ctx.dr, ctx.need_w, ggs[5:]):
             if not any(want):
                 return (None,) * n_out
-            return (None,) * 6 + tuple(_second_order(ctx, ggs, want))
+            return (None,) * 7 + tuple(_second_order(ctx, ggs, want))
         with torch.enable_grad():
             leaves = [None if t is None else t.detach().requires_grad_(True) for t in saved]
             gX, gV, x, f, C, u, r = leaves[:7]
@@ -1094,7 +1133,7 @@ class _ETStackBwd(Function):
                                          create_graph=_create, allow_unused=True)
         it = iter(second)
         res = [next(it) if w else None for w in want]
-        return (None,) * 6 + tuple(res)
+        return (None,) * 7 + tuple(res)
 
 
 def et_stack(layers, x, graph, f, C, u, rbf=None, out_norm=None, f_pairs=None):

@@ -21,6 +21,7 @@ import torch.distributed as dist
 from torch.nn.functional import l1_loss, mse_loss
 
 from .models.model import create_model, load_model
+from .et_stack import second_order_expected
 from .training import GradAllReduce
 
 DEFAULTS = dict(charge=False, spin=False, load_model=None, lr=4e-4, weight_decay=0.0, lr_factor=0.8,
@@ -95,7 +96,8 @@ class LNNP(torch.nn.Module):
 
     def step(self, batch, loss_fn_list, stage):
         assert len(loss_fn_list) > 0
-        with torch.set_grad_enabled(stage == "train" or self.hparams.derivative):
+        train_forces = stage == "train" and self.hparams.derivative and self.hparams.neg_dy_weight > 0
+        with torch.set_grad_enabled(stage == "train" or self.hparams.derivative), second_order_expected(train_forces):
             extra = {k: v for k, v in batch.to_dict().items() if k not in ("y", "neg_dy", "z", "pos", "batch", "q", "s")}
             y, neg_dy = self(batch.z, batch.pos, batch=batch.batch,
                              q=batch.q if self.hparams.charge else None,

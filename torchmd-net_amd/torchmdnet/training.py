@@ -16,6 +16,8 @@ import torch
 import torch.distributed as dist
 import torch.nn.functional as F
 
+from .et_stack import second_order_expected
+
 
 def _world(group=None):
     if dist.is_available() and dist.is_initialized():
@@ -109,7 +111,9 @@ class LNNPStep:
         self.global_step = 0
 
     def loss(self, z, pos, batch, y, neg_dy):
-        pred, pred_neg_dy = self.model(z, pos, batch)
+        # a force loss differentiates the force pass again: let the ET stack record for its hand second order
+        with second_order_expected(self.neg_dy_weight > 0):
+            pred, pred_neg_dy = self.model(z, pos, batch)
         loss = 0.0
         if self.y_weight > 0:
             if y.ndim == 1:  # reference module.py:147-148
