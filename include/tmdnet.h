@@ -473,6 +473,21 @@ int tmdnet_gemm_f32(int n_problems, const int* dims, const void* const* ptrs, vo
  * ldc, beta, ones1, ones2}; ptrs: 5 per problem {A, B, A2, B2, C}.  (Every Linear's weight gradient
  * has this shape: the layers' [q|k|v] / vec_proj / o_proj weights in one launch, the head's six.) */
 int tmdnet_gemm_tn_f32(int n_problems, const int* dims, const void* const* ptrs, void* stream);
+/* The same with a caller-provided workspace: groups with few output tiles over many rows (a 128 x 64
+ * weight over 12.5k edge rows is 8 tiles) are split over the rows into S chunks per tile, whose partial
+ * tiles a second launch sums in chunk order (deterministic).  workspace_bytes >=
+ * tmdnet_gemm_tn_workspace_bytes(n_problems, dims) (0: no split, workspace may be NULL). */
+size_t tmdnet_gemm_tn_workspace_bytes(int n_problems, const int* dims);
+int tmdnet_gemm_tn_f32_ws(int n_problems, const int* dims, const void* const* ptrs, void* workspace,
+                          size_t workspace_bytes, void* stream);
+/* Embedding-table gradients (the backward of nn.Embedding(num_types, H) looked up at z, as used by
+ * TorchMD_ET.embedding and NeighborEmbedding.embedding, reference torchmd_et.py:170,
+ * utils.py:92): for each of n_tables (<= 32) tables sharing the indices z[n] (int64, in [0, num_types)),
+ * out_t[m][c] (+= with accumulate) = sum over k with z[k] == m of grads_t[k][c] (row stride ld_grads[t],
+ * NULL: H); out_t [num_types][H] contiguous.  fp32, deterministic (one-hot TN GEMM, no atomics). */
+int tmdnet_embedding_bwd_f32(int n, int H, int num_types, const int64_t* z, int n_tables,
+                             const void* const* grads, const int* ld_grads, void* const* outs, int accumulate,
+                             void* stream);
 
 /* Library identification (for load checks). */
 const char* tmdnet_build_info(void);

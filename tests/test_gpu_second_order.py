@@ -201,3 +201,51 @@ def test_weight_gradient_tn_gemm_matches_library():
     kernels.wgrad_tn(probs)
     for p, ref in zip(probs, refs):
         assert _rel(p["C"], ref) < 2e-5, (tuple(p["A"].shape), _rel(p["C"], ref))
+
+
+def test_embedding_backward_one_hot_tn():
+    """tmdnet_embedding_bwd_f32 (both tables of one lookup node, one launch) against index_add in
+    fp64, incl. accumulate, strided gradient rows and types that never occur."""
+    from torchmdnet import kernels
+    torch.manual_seed(0)
+    z = torch.randint(0, 10, (678,), device=DEV)
+    z[:5] = 99
+    g1 = torch.randn(678, 128, device=DEV)
+    g2 = torch.randn(678, 256, device=DEV)[:, ::2]  # row stride 256
+    outs = kernels.embedding_bwd(z, [g1, g2], 100)
+    for g, o in zip((g1, g2), outs):
+        ref = torch.zeros(100, 128, dtype=torch.float64, device=DEV).index_add_(0, z, g.double())
+        assert _rel(o, ref) < 1e-6
+    acc = [o.clone() for o in outs]
+    kernels.embedding_bwd(z, [g1, g2], 100, out=acc, accumulate=True)
+    for a, o in zip(acc, outs):
+        assert _rel(a, 2 * o.double()) < 1e-6
+    # through the autograd node the model uses
+    w1, w2 = (torch.randn(100, 128, device=DEV, requires_grad=True) for _ in range(2))
+    x1, x2 = kernels.embedding(z, w1, w2)
+    d1, d2 = torch.autograd.grad((x1 * g1).sum() + (x2 * g1).sum(), (w1, w2))
+    ref = torch.zeros(100, 128, dtype=torch.float64, device=DEV).index_add_(0, z, g1.double())
+    assert _rel(d1, ref) < 1e-6 and _rel(d2, ref) < 1e-6
+
+
+@pytest.mark.parametrize("rows,fin,fout", [(12548, 64, 128), (678, 256, 128), (37, 7, 5)])
+def test_linear_tn_first_and_second_order(rows, fin, fout):
+    """kernels.linear (TN-GEMM weight / bias gradients, differentiable backward) against F.linear
+    in fp64 autograd: first-order gradients and the force-matching style second order (a loss on the
+    input gradient, differentiated w.r.t. the weights / bias / input-gradient seed)."""
+    import torch.nn.functional as F
+    from torchmdnet import kernels
+    torch.manual_seed(1)
+    x0 = torch.randn(rows, fin, device=DEV)
+    w0 = torch.randn(fout, fin, device=DEV) / fin ** 0.5
+    b0 = torch.randn(fout, device=DEV)
+    gy0 = torch.randn(rows, fout, device=DEV)
+    res = []
+    for lin, dt in ((kernels.linear, torch.float32), (F.linear, torch.float64)):
+        x, w, b = (t.to(dt).clone().requires_grad_(True) for t in (x0, w0, b0))
+        y = lin(x, w, b)
+        gx, = torch.autograd.grad(y, x, gy0.to(dt) * torch.tanh(y), create_graph=True)
+        loss = (y ** 2).sum() + (gx ** 2).sum()
+        res.append(torch.autograd.grad(loss, (w, b)))
+    for a, r in zip(*res):
+        assert _rel(a, r) < 1e-4

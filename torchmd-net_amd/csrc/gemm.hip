@@ -149,9 +149,13 @@ __global__ __launch_bounds__(NW * 64) void k_gemm(Group G) {
 // (sum of A over the rows).  Loads are scalar along the rows (the contiguous direction of A and B is
 // the output dimension): one k row of a 32-wide tile is a 128-byte segment.
 constexpr int TN_MAX = 32;
+// 16-row blocks whose loads are issued together per iteration (the loop is one memory round trip per
+// 16 * TN_UB rows: a wave's row slice of an edge sum is ~800-1600 rows)
+constexpr int TN_UB = 4;
 
 struct ProbTN {
   int M, N, K, K2, lda, ldb, lda2, ldb2, ldc, beta, ones1, ones2, tiles_n, tile0;
+  int onehot;  // A is an int64 index vector: A[k][m] = (A[k] == m) (embedding-table gradients)
   const float* A;
   const float* B;
   const float* A2;
@@ -162,23 +166,28 @@ struct ProbTN {
 struct GroupTN {
   ProbTN p[TN_MAX];
   int n;
+  int S;        // split-K factor: S workgroups per tile, each over a chunk of the rows
+  float* part;  // S > 1: partial tiles [tiles][S][32 * 32], summed in order by k_tn_reduce
 };
 
 template <int NW>
 __global__ __launch_bounds__(NW * 64) void k_gemm_tn(GroupTN G) {
   __shared__ float part[NW][32][33];
+  const int tg = blockIdx.x / G.S, sk = blockIdx.x % G.S;  // tile, row chunk
   int pi = 0;
   for (int i = 1; i < G.n; ++i)
-    if ((int)blockIdx.x >= G.p[i].tile0) pi = i;
+    if (tg >= G.p[i].tile0) pi = i;
   const ProbTN& P = G.p[pi];
-  const int t = blockIdx.x - P.tile0;
+  const int t = tg - P.tile0;
   const int w = threadIdx.x / TMD_WAVE, lane = lane_id();
   const int lr = lane & 15, lk = lane >> 4;
   const int r0 = (t / P.tiles_n) * 32, c0 = (t % P.tiles_n) * 32;
   const int KT = P.K + P.K2;
-  // this wave's rows: the 16-row blocks split evenly over the waves
-  const int nkb = (KT + 15) / 16, per = (nkb + NW - 1) / NW;
-  const int k_lo = min(KT, w * per * 16), k_hi = min(KT, (w + 1) * per * 16);
+  // this workgroup's rows (16-row blocks split evenly over the S chunks), then this wave's share
+  const int nkt = (KT + 15) / 16, cper = (nkt + G.S - 1) / G.S;
+  const int c_lo = min(KT, sk * cper * 16), c_hi = min(KT, (sk + 1) * cper * 16);
+  const int nkb = (c_hi - c_lo + 15) / 16, per = (nkb + NW - 1) / NW;
+  const int k_lo = min(c_hi, c_lo + w * per * 16), k_hi = min(c_hi, c_lo + (w + 1) * per * 16);
   f4 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -198,27 +207,34 @@ __global__ __launch_bounds__(NW * 64) void k_gemm_tn(GroupTN G) {
     // B column kind per lane: 0 read, 1 constant one, 2 zero
     const int kda = na >= P.N ? 2 : (anyones && na == P.N - 1) ? (ones ? 1 : 2) : 0;
     const int kdb = nb >= P.N ? 2 : (anyones && nb == P.N - 1) ? (ones ? 1 : 2) : 0;
-    const float* pa0 = A + (va ? ma : 0);
-    const float* pa1 = A + (vb ? mb : 0);
+    const int64_t* zi = P.onehot ? reinterpret_cast<const int64_t*>(A) : nullptr;  // (wave-uniform)
+    const float* pa0 = zi ? nullptr : A + (va ? ma : 0);
+    const float* pa1 = zi ? nullptr : A + (vb ? mb : 0);
     const float* pb0 = kda == 0 ? B + na : nullptr;
     const float* pb1 = kdb == 0 ? B + nb : nullptr;
     const float ca = kda == 1 ? 1.f : 0.f, cb = kdb == 1 ? 1.f : 0.f;
-    for (int kb = lo; kb < hi; kb += 32) {  // two 16-row blocks in flight
-      float a[2][2][4], b[2][2][4];
+    for (int kb = lo; kb < hi; kb += 16 * TN_UB) {  // TN_UB 16-row blocks in flight
+      float a[TN_UB][2][4], b[TN_UB][2][4];
 #pragma unroll
-      for (int u = 0; u < 2; ++u)
+      for (int u = 0; u < TN_UB; ++u)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int k = kb + 16 * u + 4 * lk + j;
           const bool kv = k < hi;
           const size_t ro = (size_t)(kv ? k - s0 : 0);
-          a[u][0][j] = (kv && va) ? pa0[ro * lda] : 0.f;
-          a[u][1][j] = (kv && vb) ? pa1[ro * lda] : 0.f;
+          if (zi) {
+            const int64_t zk = kv ? zi[ro] : -1;
+            a[u][0][j] = (va && zk == ma) ? 1.f : 0.f;
+            a[u][1][j] = (vb && zk == mb) ? 1.f : 0.f;
+          } else {
+            a[u][0][j] = (kv && va) ? pa0[ro * lda] : 0.f;
+            a[u][1][j] = (kv && vb) ? pa1[ro * lda] : 0.f;
+          }
           b[u][0][j] = !kv ? 0.f : pb0 ? pb0[ro * ldb] : ca;
           b[u][1][j] = !kv ? 0.f : pb1 ? pb1[ro * ldb] : cb;
         }
 #pragma unroll
-      for (int u = 0; u < 2; ++u)
+      for (int u = 0; u < TN_UB; ++u)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][0][j], b[u][0][j], acc[0][0], 0, 0, 0);
@@ -238,14 +254,38 @@ __global__ __launch_bounds__(NW * 64) void k_gemm_tn(GroupTN G) {
   for (int e = threadIdx.x; e < 32 * 32; e += blockDim.x) {
     const int r = e >> 5, c = e & 31;
     const int gr = r0 + r, gc = c0 + c;
-    if (gr >= P.M || gc >= P.N) continue;
     float v = 0.f;
 #pragma unroll
     for (int i = 0; i < NW; ++i) v += part[i][r][c];
+    if (G.S > 1) {  // partial tile; k_tn_reduce sums the S chunks in order (deterministic)
+      G.part[((size_t)tg * G.S + sk) * 1024 + e] = v;
+      continue;
+    }
+    if (gr >= P.M || gc >= P.N) continue;
     float* out = P.C + (size_t)gr * P.ldc + gc;
     if (P.beta) v += *out;
     *out = v;
   }
+}
+
+__global__ __launch_bounds__(256) void k_tn_reduce(GroupTN G, int tiles) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= tiles * 1024) return;
+  const int tg = i >> 10, e = i & 1023;
+  int pi = 0;
+  for (int j = 1; j < G.n; ++j)
+    if (tg >= G.p[j].tile0) pi = j;
+  const ProbTN& P = G.p[pi];
+  const int t = tg - P.tile0;
+  const int gr = (t / P.tiles_n) * 32 + (e >> 5), gc = (t % P.tiles_n) * 32 + (e & 31);
+  if (gr >= P.M || gc >= P.N) return;
+  const float* src = G.part + (size_t)tg * G.S * 1024 + e;
+  float v = 0.f;
+#pragma unroll 8
+  for (int s = 0; s < G.S; ++s) v += src[(size_t)s * 1024];
+  float* out = P.C + (size_t)gr * P.ldc + gc;
+  if (P.beta) v += *out;
+  *out = v;
 }
 
 }  // namespace gemm
@@ -298,13 +338,58 @@ extern "C" int tmdnet_gemm_f32(int n_problems, const int* dims, const void* cons
   return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
 }
 
+// split-K factor: few tiles over many rows (e.g. a 128 x 64 weight over 12.5k edges is 8 tiles)
+// leave most CUs idle; S 4-wave workgroups per tile (~1024 workgroups in all), each wave >= 64 rows
+static int tn_split(int tiles, int kmax) {
+  int S = (1024 + tiles - 1) / tiles;
+  S = min(S, max(1, kmax / (4 * 64)));
+  return max(1, min(S, 64));
+}
+
+static void launch_tn(gemm::GroupTN& G, int tiles, int kmax, float* ws, hipStream_t st) {
+  G.S = ws ? tn_split(tiles, kmax) : 1;
+  G.part = ws;
+  // unsplit: K over 16 waves from 8192 rows (edge sums), 4 below (atom sums: a wave's slice stays long
+  // enough to amortise the partial-tile reduction); split: 4 waves over each chunk
+  if (kmax >= 8192 && G.S == 1) hipLaunchKernelGGL(gemm::k_gemm_tn<16>, dim3(tiles), dim3(1024), 0, st, G);
+  else hipLaunchKernelGGL(gemm::k_gemm_tn<4>, dim3(tiles * G.S), dim3(256), 0, st, G);
+  if (G.S > 1) hipLaunchKernelGGL(gemm::k_tn_reduce, dim3((tiles * 1024 + 255) / 256), dim3(256), 0, st, G, tiles);
+}
+
+// Embedding-table gradients (reference nn.Embedding backward, used by TorchMD_ET.embedding and
+// NeighborEmbedding.embedding): out_t[m][c] (+)= sum_{k: z[k] == m} grad_t[k][c] for n_tables tables
+// sharing the indices, as one-hot TN GEMMs in ONE launch -- deterministic (no atomics), no sort.
+extern "C" int tmdnet_embedding_bwd_f32(int n, int H, int num_types, const int64_t* z, int n_tables,
+                                        const void* const* grads, const int* ld_grads, void* const* outs,
+                                        int accumulate, void* stream) {
+  if (n < 0 || H <= 0 || num_types <= 0 || n_tables < 1 || n_tables > gemm::TN_MAX || !z || !grads || !outs)
+    return kBadArgument;
+  gemm::GroupTN G{};
+  G.n = n_tables;
+  int tiles = 0;
+  for (int i = 0; i < n_tables; ++i) {
+    gemm::ProbTN& P = G.p[i];
+    if (!grads[i] || !outs[i] || (ld_grads && ld_grads[i] < H)) return kBadArgument;
+    P.M = num_types; P.N = H; P.K = n; P.K2 = 0;
+    P.lda = 1; P.ldb = ld_grads ? ld_grads[i] : H; P.ldc = H; P.beta = accumulate ? 1 : 0;
+    P.onehot = 1;
+    P.A = (const float*)z; P.B = (const float*)grads[i]; P.C = (float*)outs[i];
+    P.tiles_n = (P.N + 31) / 32;
+    P.tile0 = tiles;
+    tiles += ((P.M + 31) / 32) * P.tiles_n;
+  }
+  launch_tn(G, tiles, n, nullptr, (hipStream_t)stream);
+  return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
+}
+
 // dims: 12 ints per problem {M, N, K, K2, lda, ldb, lda2, ldb2, ldc, beta, ones1, ones2};
 // ptrs: 5 per problem {A, B, A2, B2, C} (A2 / B2 NULL when K2 = 0).
-extern "C" int tmdnet_gemm_tn_f32(int n_problems, const int* dims, const void* const* ptrs, void* stream) {
+static int tn_group(int n_problems, const int* dims, const void* const* ptrs, gemm::GroupTN& G, int& tiles,
+                    int& kmax) {
   if (n_problems < 1 || n_problems > gemm::TN_MAX || !dims || !ptrs) return kBadArgument;
-  gemm::GroupTN G{};
   G.n = n_problems;
-  int tiles = 0, kmax = 0;
+  tiles = 0;
+  kmax = 0;
   for (int i = 0; i < n_problems; ++i) {
     const int* d = dims + 12 * i;
     gemm::ProbTN& P = G.p[i];
@@ -321,10 +406,31 @@ extern "C" int tmdnet_gemm_tn_f32(int n_problems, const int* dims, const void* c
     tiles += ((P.M + 31) / 32) * P.tiles_n;
     kmax = max(kmax, P.K + P.K2);
   }
-  hipStream_t st = (hipStream_t)stream;
-  // K split over 16 waves from 8192 rows (edge sums), 4 below (atom sums: a wave's slice stays long
-  // enough to amortise the partial-tile reduction)
-  if (kmax >= 8192) hipLaunchKernelGGL(gemm::k_gemm_tn<16>, dim3(tiles), dim3(1024), 0, st, G);
-  else hipLaunchKernelGGL(gemm::k_gemm_tn<4>, dim3(tiles), dim3(256), 0, st, G);
+  return kOk;
+}
+
+extern "C" int tmdnet_gemm_tn_f32(int n_problems, const int* dims, const void* const* ptrs, void* stream) {
+  return tmdnet_gemm_tn_f32_ws(n_problems, dims, ptrs, nullptr, 0, stream);
+}
+
+extern "C" size_t tmdnet_gemm_tn_workspace_bytes(int n_problems, const int* dims) {
+  gemm::GroupTN G{};
+  int tiles = 0, kmax = 0;
+  const void* fake[5 * gemm::TN_MAX];
+  for (auto& f : fake) f = &G;  // shapes only
+  if (tn_group(n_problems, dims, fake, G, tiles, kmax) != kOk) return 0;
+  const int S = tn_split(tiles, kmax);
+  return S > 1 ? sizeof(float) * 1024 * (size_t)tiles * S : 0;
+}
+
+extern "C" int tmdnet_gemm_tn_f32_ws(int n_problems, const int* dims, const void* const* ptrs, void* workspace,
+                                     size_t workspace_bytes, void* stream) {
+  gemm::GroupTN G{};
+  int tiles = 0, kmax = 0;
+  const int rc = tn_group(n_problems, dims, ptrs, G, tiles, kmax);
+  if (rc != kOk) return rc;
+  float* ws = (float*)workspace;
+  if (ws && workspace_bytes < sizeof(float) * 1024 * (size_t)tiles * tn_split(tiles, kmax)) return kWorkspaceTooSmall;
+  launch_tn(G, tiles, kmax, ws, (hipStream_t)stream);
   return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
 }

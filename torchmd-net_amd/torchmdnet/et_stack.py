@@ -139,6 +139,9 @@ RECORD_IN_FORCE_PASS = os.environ.get("TMDNET_ET_RECORD", "1") not in ("0", "off
 # builds its graph (create_graph=True), so create_graph alone does not say a second backward follows,
 # and an energy+force evaluation must keep the cheaper dr-mode force pass
 _EXPECT_SECOND_ORDER = [False]
+# the projection's weight gradient over the edge rows (K = E, a 4096 x 64 output: FLOP-bound on the
+# fp32 MFMA): "lib" = library GEMMs + a column sum, "tn" = one split-K TN launch
+PROJ_WGRAD = os.environ.get("TMDNET_PROJ_WGRAD", "lib")
 
 
 @contextlib.contextmanager
@@ -544,10 +547,14 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws, r=None, dr=Fa
         if rec:
             record[-1]["g_pkv"] = g_pkv_all
         if any(need_ws[:meta.n_layers]):
-            g_w_all = torch.mm(g_pkv_all.t(), f)
-            if adj is not None and adj.get("dkv") is not None:  # + the adjoint's g_pkv^T gb_f
-                g_w_all.addmm_(adj["dkv"][0].t(), adj["dkv"][1])
-            g_b_all = g_pkv_all.sum(0)
+            if PROJ_WGRAD == "tn":  # weight + bias (+ the adjoint's g_pkv^T gb_f): one split-K TN launch
+                g_w_all, g_b_all = kernels._linear_wgrad(g_pkv_all, f, True, True,
+                                                         seg2=adj.get("dkv") if adj is not None else None)
+            else:
+                g_w_all = torch.mm(g_pkv_all.t(), f)
+                if adj is not None and adj.get("dkv") is not None:  # + the adjoint's g_pkv^T gb_f
+                    g_w_all.addmm_(adj["dkv"][0].t(), adj["dkv"][1])
+                g_b_all = g_pkv_all.sum(0)
             if meta.planar:
                 dinv = meta.perms[3]
                 g_w_all, g_b_all = g_w_all.index_select(0, dinv), g_b_all.index_select(0, dinv)

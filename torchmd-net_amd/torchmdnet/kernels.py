@@ -1092,8 +1092,11 @@ def _wgrad_tn_launch(problems):
                                     0 if B2 is None else B2.stride(0), C.stride(0), int(bool(p.get("beta"))),
                                     int(bool(p.get("ones"))), int(bool(p.get("ones2")))]
         ptrs[5 * i:5 * i + 5] = [None if t is None else t.data_ptr() for t in (A, B, A2, B2, C)]
-    rc = lib.tmdnet_gemm_tn_f32(n, dims, ptrs, nat.stream(problems[0]["A"].device))
-    nat.check(rc, "tmdnet_gemm_tn_f32")
+    dev = problems[0]["A"].device
+    wsb = lib.tmdnet_gemm_tn_workspace_bytes(n, dims)  # split over the rows: partial tiles
+    ws = torch.empty((max(wsb, 4) // 4,), dtype=torch.float32, device=dev) if wsb else None
+    rc = lib.tmdnet_gemm_tn_f32_ws(n, dims, ptrs, None if ws is None else ws.data_ptr(), wsb, nat.stream(dev))
+    nat.check(rc, "tmdnet_gemm_tn_f32_ws")
 
 
 # ----------------------------------------------------------------------------- energy reduction
@@ -1612,3 +1615,146 @@ def eq_scalar_head(x, vec, blocks):
     """EquivariantScalar.pre_reduce's two gated blocks through the fused HIP head."""
     nat.require_gpu(x, "eq_scalar_head")
     return _EqHead.apply(x, vec, *eq_head_params(blocks))
+
+
+# ----------------------------------------------------------------------------- embeddings and Linears
+# with hand-written weight gradients.  The library GEMM picks few-workgroup tiles with a serial K loop
+# for the "sum over rows" weight gradients of the neighbour embedding's Linears (e.g. 112 us for
+# [128 x 12548] [12548 x 64] at ET-QM9) and embedding_dense_backward sorts the indices (48 us per
+# table): both are TN GEMMs here (tmdnet_gemm_tn_f32 / tmdnet_embedding_bwd_f32), deterministic.
+def _tn_ok(*ts):
+    return all(t is None or (t.is_cuda and t.dtype == torch.float32) for t in ts)
+
+
+def embedding_bwd(z, grads, num_types, out=None, accumulate=False):
+    """Table gradients of embeddings looked up at ``z``: one launch for every (grad [n, H]) of ``grads``."""
+    H = grads[0].shape[1]
+    outs = out if out is not None else [torch.empty((num_types, H), dtype=g.dtype, device=g.device) for g in grads]
+    if not _tn_ok(*grads):
+        for g, o in zip(grads, outs):
+            if not accumulate:
+                o.zero_()
+            o.index_add_(0, z, g)
+        return outs
+    gs = [g if g.stride(1) == 1 else g.contiguous() for g in grads]
+    n = len(gs)
+    gp = (ctypes.c_void_p * n)(*[g.data_ptr() for g in gs])
+    ld = (ctypes.c_int * n)(*[g.stride(0) for g in gs])
+    op = (ctypes.c_void_p * n)(*[o.data_ptr() for o in outs])
+    rc = nat.load().tmdnet_embedding_bwd_f32(z.shape[0], H, num_types, nat.ptr(z), n, gp, ld, op,
+                                             int(bool(accumulate)), nat.stream(z.device))
+    nat.check(rc, "tmdnet_embedding_bwd_f32")
+    return outs
+
+
+class _Embedding(Function):
+    """weights[t][z] for every table t (reference nn.Embedding; TorchMD_ET's and NeighborEmbedding's
+    tables share z): both lookups one node, both table gradients one launch."""
+
+    @staticmethod
+    def forward(ctx, z, *weights):
+        ctx.save_for_backward(z)
+        ctx.shapes = [w.shape for w in weights]
+        return tuple(w.index_select(0, z) for w in weights)
+
+    @staticmethod
+    def backward(ctx, *gs):
+        z, = ctx.saved_tensors
+        live = [i for i, g in enumerate(gs) if g is not None and ctx.needs_input_grad[1 + i]]
+        res = [None] * len(gs)
+        if live:
+            if torch.is_grad_enabled():  # a graph of this gradient (third order): differentiable composite
+                for i in live:
+                    res[i] = torch.zeros(ctx.shapes[i], dtype=gs[i].dtype, device=gs[i].device).index_add(0, z, gs[i])
+            else:
+                outs = embedding_bwd(z, [gs[i] for i in live], ctx.shapes[live[0]][0])
+                for i, o in zip(live, outs):
+                    res[i] = o
+        return (None,) + tuple(res)
+
+
+def embedding(z, *weights):
+    return _Embedding.apply(z, *weights)
+
+
+class _Linear(Function):
+    """y = x W^T + b (reference nn.Linear) whose backward forms only the gradients the engine will
+    consume; its weight / bias gradient is one TN launch (bias = the ones column)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        ctx.has_b = b is not None
+        return F.linear(x, w, b)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        nf = ctx.next_functions
+        need = (ctx.needs_input_grad[0] and _will_run(nf[0][0]),
+                ctx.needs_input_grad[1] and _will_run(nf[1][0]),
+                ctx.has_b and ctx.needs_input_grad[2] and _will_run(nf[2][0]))
+        if not any(need):
+            return None, None, None
+        gx, gw, gb = _LinearBwd.apply(gy, x, w, need)
+        return gx, gw, gb
+
+
+def _linear_wgrad(gy, x, want_w, want_b, seg2=None):
+    """(g_W, g_b) = (gy^T x, sum gy) [+ seg2 = (gy2, x2): gy2^T x2] in one TN launch (fp32 CUDA)."""
+    out_f, in_f = gy.shape[1], x.shape[1]
+    if not _tn_ok(gy, x) or gy.stride(1) != 1 or x.stride(1) != 1:
+        gw = (gy.t() @ x + (seg2[0].t() @ seg2[1] if seg2 is not None else 0)) if want_w else None
+        return gw, (gy.sum(0) if want_b else None)
+    ncol = (in_f if want_w else 0) + int(bool(want_b))
+    C = torch.empty((out_f, ncol), dtype=gy.dtype, device=gy.device)
+    p = {"A": gy, "B": x if want_w else None, "C": C, "ones": bool(want_b)}
+    if seg2 is not None and want_w:
+        p.update(A2=seg2[0], B2=seg2[1], ones2=False)
+    wgrad_tn([p])
+    # contiguous parameter gradients (strided ones make every later copy a per-tensor 2-D copy)
+    return (C[:, :in_f].contiguous() if want_w else None), (C[:, ncol - 1].contiguous() if want_b else None)
+
+
+class _LinearBwd(Function):
+    """(gx, gW, gb) of _Linear, itself differentiable (force-matching training differentiates the
+    force pass): for cotangents (ggx, ggW, ggb),  d gy = ggx W + x ggW^T + ggb,  d x = gy ggW,
+    d W = gy^T ggx."""
+
+    @staticmethod
+    def forward(ctx, gy, x, w, need):
+        gx = gy @ w if need[0] else None
+        gw, gb = _linear_wgrad(gy, x, need[1], need[2]) if (need[1] or need[2]) else (None, None)
+        ctx.save_for_backward(gy, x, w)
+        return gx, gw, gb
+
+    @staticmethod
+    def backward(ctx, ggx, ggw, ggb):
+        gy, x, w = ctx.saved_tensors
+        nf = ctx.next_functions
+        want = [ctx.needs_input_grad[i] and _will_run(nf[i][0]) for i in range(3)]
+        d_gy = d_x = d_w = None
+        if want[0]:
+            parts = []
+            if ggx is not None:
+                parts.append(ggx @ w.t())
+            if ggw is not None:
+                parts.append(x @ ggw.t())
+            if ggb is not None:
+                parts.append(ggb.expand(gy.shape))
+            if parts:
+                d_gy = parts[0]
+                for t in parts[1:]:
+                    d_gy = d_gy + t
+        if want[1] and ggw is not None:
+            d_x = gy @ ggw
+        if want[2] and ggx is not None:
+            if torch.is_grad_enabled():
+                d_w = gy.t() @ ggx
+            else:
+                d_w, _ = _linear_wgrad(gy, ggx, True, False)
+        return d_gy, d_x, d_w, None
+
+
+def linear(x, w, b=None):
+    return _Linear.apply(x, w, b)

@@ -138,7 +138,14 @@ class TorchMD_ET(nn.Module):
         return x, vec
 
     def _forward(self, z: Tensor, pos: Tensor, batch: Tensor):
-        x = self.embedding(z)
+        ne = self.neighbor_embedding
+        x_ne = None
+        if z.is_cuda and ne is not None:  # both tables' lookups (and gradients) in one node
+            x, x_ne = kernels.embedding(z, self.embedding.weight, ne.embedding.weight)
+        elif z.is_cuda:
+            x, = kernels.embedding(z, self.embedding.weight)
+        else:
+            x = self.embedding(z)
         graph = self.distance.graph(pos, batch)
         f_pairs = None
         de = self.distance_expansion
@@ -156,7 +163,7 @@ class TorchMD_ET(nn.Module):
             f_pairs = geo[3] if rows is not None else None
         graph.cutoff = C
         if self.neighbor_embedding is not None:
-            x = self.neighbor_embedding(z, x, graph, graph.distances, edge_attr, cutoff=C)
+            x = self.neighbor_embedding(z, x, graph, graph.distances, edge_attr, cutoff=C, x_emb=x_ne)
         if self.fused_stack and len(self.attention_layers) > 0:
             # all layers as one autograd node (et_stack.py): fused GEMMs, HIP epilogue, hand-scheduled
             # backward; same math as the loop below

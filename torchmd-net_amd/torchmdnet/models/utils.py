@@ -297,16 +297,24 @@ class NeighborEmbedding(nn.Module):
         return self.combine(torch.cat([x, x_nb], dim=1))
 
     def forward(self, z: Tensor, x: Tensor, edge_index: Tensor, edge_weight: Tensor, edge_attr: Tensor,
-                cutoff: Optional[Tensor] = None) -> Tensor:
+                cutoff: Optional[Tensor] = None, x_emb: Optional[Tensor] = None) -> Tensor:
+        """``x_emb``: this module's embedding of ``z`` when the caller looked it up already (TorchMD_ET
+        does both tables' lookups in one node)."""
         if torch.jit.is_scripting():
             raise RuntimeError("scripted NeighborEmbedding: use script_forward (CSR graph)")
         graph, perm = as_graph(edge_index, x.shape[0])
         if perm is not None:
             edge_weight, edge_attr = edge_weight[perm], edge_attr[perm]
         C = cutoff if cutoff is not None else self.cutoff(edge_weight)
+        if x_emb is None:
+            x_emb = self.embedding(z)
+        if x.is_cuda:  # Linears with hand-written (TN GEMM) weight gradients, also in the second order
+            W = kernels.linear(edge_attr, self.distance_proj.weight, self.distance_proj.bias)
+            return kernels.linear(kernels.nbr_embed(x_emb, W, C, graph, x_self=x), self.combine.weight,
+                                  self.combine.bias)
         W = self.distance_proj(edge_attr)
         # [x | x_nb] comes out of the aggregation kernel itself (no concatenation launch)
-        return self.combine(kernels.nbr_embed(self.embedding(z), W, C, graph, x_self=x))
+        return self.combine(kernels.nbr_embed(x_emb, W, C, graph, x_self=x))
 
 
 def as_graph(edge_index, n_nodes):
