@@ -476,7 +476,9 @@ int tmdnet_gemm_tn_f32(int n_problems, const int* dims, const void* const* ptrs,
 /* The same with a caller-provided workspace: groups with few output tiles over many rows (a 128 x 64
  * weight over 12.5k edge rows is 8 tiles) are split over the rows into S chunks per tile, whose partial
  * tiles a second launch sums in chunk order (deterministic).  workspace_bytes >=
- * tmdnet_gemm_tn_workspace_bytes(n_problems, dims) (0: no split, workspace may be NULL). */
+ * tmdnet_gemm_tn_workspace_bytes(n_problems, dims) (0: no split, workspace may be NULL).  ptrs: 6 per
+ * problem {A, B, A2, B2, C, Cb}: Cb non-NULL (with ones1 / ones2) receives the ones column, i.e. the
+ * bias gradient, as a separate contiguous [M] vector (C then holds the N-1 weight columns). */
 size_t tmdnet_gemm_tn_workspace_bytes(int n_problems, const int* dims);
 int tmdnet_gemm_tn_f32_ws(int n_problems, const int* dims, const void* const* ptrs, void* workspace,
                           size_t workspace_bytes, void* stream);

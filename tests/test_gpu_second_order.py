@@ -249,3 +249,34 @@ def test_linear_tn_first_and_second_order(rows, fin, fout):
         res.append(torch.autograd.grad(loss, (w, b)))
     for a, r in zip(*res):
         assert _rel(a, r) < 1e-4
+
+
+def test_node_weight_grads_tn_match_batched_library(monkeypatch):
+    """fp32 training gradients of every parameter (E + F loss through the recorded force pass) with the
+    node weights' gradients from the grouped TN GEMMs (NODE_WGRAD=tn, biases as separate ones-column
+    outputs, adjoint terms as second row segments) against the batched library GEMMs (bmm)."""
+    from torchmdnet import et_stack as ES
+    from torchmdnet.models.model import create_model
+    args = yaml_args("equivariant-transformer", embedding_dimension=64, num_layers=3, derivative=True,
+                     precision=32)
+    torch.manual_seed(0)
+    model = create_model(args).to(DEV)
+    z, pos, batch = O.qm9_like(6, 3)
+    z, pos, batch = z.to(DEV), pos.float().to(DEV), batch.to(DEV)
+    torch.manual_seed(1)
+    y_t, f_t = torch.randn(6, 1, device=DEV), torch.randn_like(pos)
+    grads = []
+    for mode in ("tn", "bmm"):
+        monkeypatch.setattr(ES, "NODE_WGRAD", mode)
+        params = [p for p in model.parameters() if p.requires_grad]
+        with ES.second_order_expected():
+            y, neg_dy = model(z, pos.clone(), batch)
+        loss = ((y - y_t) ** 2).mean() + ((neg_dy - f_t) ** 2).mean()
+        grads.append(torch.autograd.grad(loss, params, allow_unused=True))
+    n = 0
+    for a, b in zip(*grads):
+        if b is None:
+            continue
+        assert _rel(a, b) < 1e-4
+        n += 1
+    assert n > 30

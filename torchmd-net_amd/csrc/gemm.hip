@@ -161,6 +161,7 @@ struct ProbTN {
   const float* A2;
   const float* B2;
   float* C;
+  float* Cb;  // non-NULL: column N-1 (the ones / bias column) goes to Cb[m] instead of C[m][N-1]
 };
 
 struct GroupTN {
@@ -262,7 +263,7 @@ __global__ __launch_bounds__(NW * 64) void k_gemm_tn(GroupTN G) {
       continue;
     }
     if (gr >= P.M || gc >= P.N) continue;
-    float* out = P.C + (size_t)gr * P.ldc + gc;
+    float* out = (P.Cb && gc == P.N - 1) ? P.Cb + gr : P.C + (size_t)gr * P.ldc + gc;
     if (P.beta) v += *out;
     *out = v;
   }
@@ -283,7 +284,7 @@ __global__ __launch_bounds__(256) void k_tn_reduce(GroupTN G, int tiles) {
   float v = 0.f;
 #pragma unroll 8
   for (int s = 0; s < G.S; ++s) v += src[(size_t)s * 1024];
-  float* out = P.C + (size_t)gr * P.ldc + gc;
+  float* out = (P.Cb && gc == P.N - 1) ? P.Cb + gr : P.C + (size_t)gr * P.ldc + gc;
   if (P.beta) v += *out;
   *out = v;
 }
@@ -384,7 +385,7 @@ extern "C" int tmdnet_embedding_bwd_f32(int n, int H, int num_types, const int64
 
 // dims: 12 ints per problem {M, N, K, K2, lda, ldb, lda2, ldb2, ldc, beta, ones1, ones2};
 // ptrs: 5 per problem {A, B, A2, B2, C} (A2 / B2 NULL when K2 = 0).
-static int tn_group(int n_problems, const int* dims, const void* const* ptrs, gemm::GroupTN& G, int& tiles,
+static int tn_group(int n_problems, const int* dims, const void* const* ptrs, int np, gemm::GroupTN& G, int& tiles,
                     int& kmax) {
   if (n_problems < 1 || n_problems > gemm::TN_MAX || !dims || !ptrs) return kBadArgument;
   G.n = n_problems;
@@ -395,9 +396,12 @@ static int tn_group(int n_problems, const int* dims, const void* const* ptrs, ge
     gemm::ProbTN& P = G.p[i];
     P.M = d[0]; P.N = d[1]; P.K = d[2]; P.K2 = d[3]; P.lda = d[4]; P.ldb = d[5]; P.lda2 = d[6]; P.ldb2 = d[7];
     P.ldc = d[8]; P.beta = d[9]; P.ones1 = d[10]; P.ones2 = d[11];
-    P.A = (const float*)ptrs[5 * i]; P.B = (const float*)ptrs[5 * i + 1];
-    P.A2 = (const float*)ptrs[5 * i + 2]; P.B2 = (const float*)ptrs[5 * i + 3]; P.C = (float*)ptrs[5 * i + 4];
-    if (P.M <= 0 || P.N <= 0 || P.K < 0 || P.K2 < 0 || !P.C || P.ldc < P.N) return kBadArgument;
+    const void* const* q = ptrs + (size_t)np * i;
+    P.A = (const float*)q[0]; P.B = (const float*)q[1];
+    P.A2 = (const float*)q[2]; P.B2 = (const float*)q[3]; P.C = (float*)q[4];
+    P.Cb = np > 5 ? (float*)q[5] : nullptr;
+    if (P.Cb && !(P.ones1 || P.ones2)) return kBadArgument;
+    if (P.M <= 0 || P.N <= 0 || P.K < 0 || P.K2 < 0 || !P.C || P.ldc < P.N - (P.Cb ? 1 : 0)) return kBadArgument;
     if ((P.K > 0 && (!P.A || (!P.B && !(P.ones1 && P.N == 1)) || P.lda < P.M)) ||
         (P.K2 > 0 && (!P.A2 || (!P.B2 && !(P.ones2 && P.N == 1)) || P.lda2 < P.M)))
       return kBadArgument;
@@ -409,28 +413,35 @@ static int tn_group(int n_problems, const int* dims, const void* const* ptrs, ge
   return kOk;
 }
 
+static int gemm_tn(int n_problems, const int* dims, const void* const* ptrs, int np, void* workspace,
+                   size_t workspace_bytes, void* stream) {
+  gemm::GroupTN G{};
+  int tiles = 0, kmax = 0;
+  const int rc = tn_group(n_problems, dims, ptrs, np, G, tiles, kmax);
+  if (rc != kOk) return rc;
+  float* ws = (float*)workspace;
+  if (ws && workspace_bytes < sizeof(float) * 1024 * (size_t)tiles * tn_split(tiles, kmax)) return kWorkspaceTooSmall;
+  launch_tn(G, tiles, kmax, ws, (hipStream_t)stream);
+  return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
+}
+
 extern "C" int tmdnet_gemm_tn_f32(int n_problems, const int* dims, const void* const* ptrs, void* stream) {
-  return tmdnet_gemm_tn_f32_ws(n_problems, dims, ptrs, nullptr, 0, stream);
+  return gemm_tn(n_problems, dims, ptrs, 5, nullptr, 0, stream);
 }
 
 extern "C" size_t tmdnet_gemm_tn_workspace_bytes(int n_problems, const int* dims) {
-  gemm::GroupTN G{};
-  int tiles = 0, kmax = 0;
-  const void* fake[5 * gemm::TN_MAX];
-  for (auto& f : fake) f = &G;  // shapes only
-  if (tn_group(n_problems, dims, fake, G, tiles, kmax) != kOk) return 0;
+  if (n_problems < 1 || n_problems > gemm::TN_MAX || !dims) return 0;
+  int tiles = 0, kmax = 0;  // the shapes only (tn_group's tiling)
+  for (int i = 0; i < n_problems; ++i) {
+    const int* d = dims + 12 * i;
+    tiles += ((d[0] + 31) / 32) * ((d[1] + 31) / 32);
+    kmax = max(kmax, d[2] + d[3]);
+  }
   const int S = tn_split(tiles, kmax);
   return S > 1 ? sizeof(float) * 1024 * (size_t)tiles * S : 0;
 }
 
 extern "C" int tmdnet_gemm_tn_f32_ws(int n_problems, const int* dims, const void* const* ptrs, void* workspace,
                                      size_t workspace_bytes, void* stream) {
-  gemm::GroupTN G{};
-  int tiles = 0, kmax = 0;
-  const int rc = tn_group(n_problems, dims, ptrs, G, tiles, kmax);
-  if (rc != kOk) return rc;
-  float* ws = (float*)workspace;
-  if (ws && workspace_bytes < sizeof(float) * 1024 * (size_t)tiles * tn_split(tiles, kmax)) return kWorkspaceTooSmall;
-  launch_tn(G, tiles, kmax, ws, (hipStream_t)stream);
-  return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
+  return gemm_tn(n_problems, dims, ptrs, 6, workspace, workspace_bytes, stream);
 }

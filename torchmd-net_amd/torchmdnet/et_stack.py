@@ -142,6 +142,9 @@ _EXPECT_SECOND_ORDER = [False]
 # the projection's weight gradient over the edge rows (K = E, a 4096 x 64 output: FLOP-bound on the
 # fp32 MFMA): "lib" = library GEMMs + a column sum, "tn" = one split-K TN launch
 PROJ_WGRAD = os.environ.get("TMDNET_PROJ_WGRAD", "lib")
+# the node weights' gradients (per layer [q|k|v], o_proj, vec_proj, LayerNorm, over the atoms): "tn" =
+# grouped split-K TN GEMMs with the bias columns, "bmm" = batched library GEMMs + reductions
+NODE_WGRAD = os.environ.get("TMDNET_NODE_WGRAD", "tn")
 
 
 @contextlib.contextmanager
@@ -574,6 +577,9 @@ def _node_weight_grads(meta, g_params, need_ws, g_qkv_all, g_o_all, g_vecp_all, 
     second order) is accumulated by the same batched GEMMs (baddbmm)."""
     L, N, H = meta.n_layers, g_xn_all.shape[1], meta.H
     xn_all, xa_all, vec_all = meta.stk
+    if NODE_WGRAD == "tn" and g_xn_all.is_cuda and g_xn_all.dtype == torch.float32 and not meta.planar:
+        return _node_weight_grads_tn(meta, g_params, need_ws, g_qkv_all, g_o_all, g_vecp_all, g_xn_all, ln_rows,
+                                     adj)
     W_qkv = torch.bmm(g_qkv_all.transpose(1, 2), xn_all)
     W_o = torch.bmm(g_o_all.transpose(1, 2), xa_all)
     W_vec = torch.zeros((L, 3 * H, H), dtype=g_xn_all.dtype, device=g_xn_all.device)
@@ -594,6 +600,45 @@ def _node_weight_grads(meta, g_params, need_ws, g_qkv_all, g_o_all, g_vecp_all, 
     if meta.planar:  # back to the parameters' (reference) row order
         qinv = meta.perms[1]
         W_qkv, B_qkv = W_qkv.index_select(1, qinv), B_qkv.index_select(1, qinv)
+    for l in range(L):
+        if not need_ws[l]:
+            continue
+        base = l * meta.np
+        wq, bq = W_qkv[l], B_qkv[l]
+        g_params[base:base + 11] = [W_ln[l], B_ln[l], wq[:H], bq[:H], wq[H:2 * H], bq[H:2 * H], wq[2 * H:],
+                                    bq[2 * H:], W_vec[l], W_o[l], B_o[l]]
+
+
+def _node_weight_grads_tn(meta, g_params, need_ws, g_qkv_all, g_o_all, g_vecp_all, g_xn_all, ln_rows, adj):
+    """_node_weight_grads as grouped TN GEMMs (tmdnet_gemm_tn_f32_ws): per layer the [q|k|v] and o_proj
+    weights with their biases (the ones column, written to its own vector), vec_proj, the LayerNorm
+    weight (column sums of the weight rows) and bias -- the adjoint's terms as each sum's second row
+    segment -- in two launches for all layers, instead of six batched GEMMs and seven reductions."""
+    L, N, H = meta.n_layers, g_xn_all.shape[1], meta.H
+    xn_all, xa_all, vec_all = meta.stk
+    o = dict(dtype=g_xn_all.dtype, device=g_xn_all.device)
+    W_qkv, B_qkv = torch.empty((L, g_qkv_all.shape[2], H), **o), torch.empty((L, g_qkv_all.shape[2]), **o)
+    W_o, B_o = torch.empty((L, g_o_all.shape[2], H), **o), torch.empty((L, g_o_all.shape[2]), **o)
+    W_vec = torch.empty((L, 3 * H, H), **o)
+    W_ln, B_ln = torch.empty((L, H), **o), torch.empty((L, H), **o)
+    probs = []
+    for l in range(L):
+        if not need_ws[l]:
+            continue
+        seg = lambda key: {} if adj is None or adj.get(key) is None else {"A2": adj[key][0][l], "B2": adj[key][1][l]}  # noqa: E731
+        probs.append({"A": g_qkv_all[l], "B": xn_all[l], "C": W_qkv[l], "Cb": B_qkv[l], "ones": True, **seg("qkv")})
+        probs.append({"A": g_o_all[l], "B": xa_all[l], "C": W_o[l], "Cb": B_o[l], "ones": True, **seg("o")})
+        if l > 0:
+            sv = {}
+            if adj is not None and adj.get("vec") is not None:
+                sv = {"A2": adj["vec"][0][l].view(3 * N, 3 * H), "B2": adj["vec"][1][l].view(3 * N, H)}
+            probs.append({"A": g_vecp_all[l].view(3 * N, 3 * H), "B": vec_all[l].view(3 * N, H), "C": W_vec[l], **sv})
+        else:  # layer 0 has no vec input (vec = 0): its vec_proj gradient is zero
+            W_vec[0].zero_()
+        sl = {"A2": adj["ln"][l], "ones2": True} if adj is not None else {}
+        probs.append({"A": ln_rows[l], "B": None, "C": W_ln[l].view(H, 1), "ones": True, **sl})
+        probs.append({"A": g_xn_all[l], "B": None, "C": B_ln[l].view(H, 1), "ones": True})
+    kernels.wgrad_tn(probs)
     for l in range(L):
         if not need_ws[l]:
             continue

@@ -1054,7 +1054,8 @@ def wgrad_tn(problems):
             _wgrad_tn_launch(problems[i:i + 32])
         return
     for p in problems:  # fp64 (parity runs): the library
-        C = p["C"]
+        C, Cb = p["C"], p.get("Cb")
+        ncol = C.shape[1] + int(Cb is not None)
         res = None
         for A, B, ones in ((p["A"], p.get("B"), p.get("ones", False)), (p.get("A2"), p.get("B2"), p.get("ones2", False))):
             if A is None or A.shape[0] == 0:
@@ -1063,35 +1064,39 @@ def wgrad_tn(problems):
             if ones:
                 one = torch.ones((A.shape[0], 1), dtype=A.dtype, device=A.device)
                 Bx = one if B is None else torch.cat((B, one), 1)
-            elif B is not None and B.shape[1] < C.shape[1]:  # a second segment without the ones column
+            elif B is not None and B.shape[1] < ncol:  # a second segment without the ones column
                 Bx = torch.cat((B, torch.zeros((A.shape[0], 1), dtype=A.dtype, device=A.device)), 1)
             t = A.t() @ Bx
             res = t if res is None else res + t
-        if p.get("beta"):
-            C.add_(res)
-        else:
-            C.copy_(res)
+        outs = [(C, res)] if Cb is None else [(C, res[:, :-1]), (Cb, res[:, -1])]
+        for dst, val in outs:
+            if p.get("beta"):
+                dst.add_(val)
+            else:
+                dst.copy_(val)
 
 
 def _wgrad_tn_launch(problems):
     lib = nat.load()
     n = len(problems)
     dims = (ctypes.c_int * (12 * n))()
-    ptrs = (ctypes.c_void_p * (5 * n))()
+    ptrs = (ctypes.c_void_p * (6 * n))()
     keep = []
     for i, p in enumerate(problems):
-        A, B, C = p["A"], p.get("B"), p["C"]
+        A, B, C, Cb = p["A"], p.get("B"), p["C"], p.get("Cb")
         A2, B2 = p.get("A2"), p.get("B2")
-        for t in (A, B, A2, B2, C):
+        for t in (A, B, A2, B2, C, Cb):
             if t is not None and t.stride(-1) != 1:
                 raise RuntimeError("wgrad_tn: operands need unit column stride")
-        keep += [A, B, A2, B2, C]
+        keep += [A, B, A2, B2, C, Cb]
         K2 = 0 if A2 is None else A2.shape[0]
-        dims[12 * i:12 * i + 12] = [A.shape[1], C.shape[1], A.shape[0], K2, A.stride(0),
+        # with Cb, C holds the weight columns only: N counts the ones column too
+        N = C.shape[1] + int(Cb is not None) if C.dim() == 2 else 1
+        dims[12 * i:12 * i + 12] = [A.shape[1], N, A.shape[0], K2, A.stride(0),
                                     0 if B is None else B.stride(0), 0 if A2 is None else A2.stride(0),
-                                    0 if B2 is None else B2.stride(0), C.stride(0), int(bool(p.get("beta"))),
-                                    int(bool(p.get("ones"))), int(bool(p.get("ones2")))]
-        ptrs[5 * i:5 * i + 5] = [None if t is None else t.data_ptr() for t in (A, B, A2, B2, C)]
+                                    0 if B2 is None else B2.stride(0), C.stride(0) if C.dim() == 2 else 1,
+                                    int(bool(p.get("beta"))), int(bool(p.get("ones"))), int(bool(p.get("ones2")))]
+        ptrs[6 * i:6 * i + 6] = [None if t is None else t.data_ptr() for t in (A, B, A2, B2, C, Cb)]
     dev = problems[0]["A"].device
     wsb = lib.tmdnet_gemm_tn_workspace_bytes(n, dims)  # split over the rows: partial tiles
     ws = torch.empty((max(wsb, 4) // 4,), dtype=torch.float32, device=dev) if wsb else None
@@ -1706,14 +1711,17 @@ def _linear_wgrad(gy, x, want_w, want_b, seg2=None):
     if not _tn_ok(gy, x) or gy.stride(1) != 1 or x.stride(1) != 1:
         gw = (gy.t() @ x + (seg2[0].t() @ seg2[1] if seg2 is not None else 0)) if want_w else None
         return gw, (gy.sum(0) if want_b else None)
-    ncol = (in_f if want_w else 0) + int(bool(want_b))
-    C = torch.empty((out_f, ncol), dtype=gy.dtype, device=gy.device)
-    p = {"A": gy, "B": x if want_w else None, "C": C, "ones": bool(want_b)}
-    if seg2 is not None and want_w:
-        p.update(A2=seg2[0], B2=seg2[1], ones2=False)
+    o = dict(dtype=gy.dtype, device=gy.device)
+    gw = torch.empty((out_f, in_f), **o) if want_w else None
+    gb = torch.empty((out_f,), **o) if want_b else None
+    if want_w:  # the bias (ones column) lands in its own contiguous vector
+        p = {"A": gy, "B": x, "C": gw, "Cb": gb, "ones": bool(want_b)}
+        if seg2 is not None:
+            p.update(A2=seg2[0], B2=seg2[1], ones2=False)
+    else:
+        p = {"A": gy, "B": None, "C": gb.view(out_f, 1), "ones": True}
     wgrad_tn([p])
-    # contiguous parameter gradients (strided ones make every later copy a per-tensor 2-D copy)
-    return (C[:, :in_f].contiguous() if want_w else None), (C[:, ncol - 1].contiguous() if want_b else None)
+    return gw, gb
 
 
 class _LinearBwd(Function):
