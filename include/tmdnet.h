@@ -221,7 +221,9 @@ int tmdnet_et_message_bwd2(int dtype, int n_nodes, int hidden, int heads, const 
  * edge_scratch ([max_pairs][7][hidden] elements, 16-byte aligned) the source-node terms of every edge
  * are stored as a scratch row and summed per node over the reversed edges by a second kernel (no
  * atomics; d_k, d_v, d_vec are overwritten, no zero fill needed).  transpose / edge_scratch NULL:
- * atomics as tmdnet_et_message_bwd2.  flags: TMDNET_ET_V_PLANAR | TMDNET_BWD2_ACC_*. */
+ * atomics as tmdnet_et_message_bwd2.  pk_rows (nullable, as in tmdnet_et_message_fwd): edge e's
+ * projection rows pk / pv are rows pk_rows[e] (pair-shared rows; gg_pk / gg_pv and d_pk / d_pv stay
+ * per edge).  flags: TMDNET_ET_V_PLANAR | TMDNET_BWD2_ACC_*. */
 int tmdnet_et_message_bwd2_ex(
     int dtype, int n_nodes, int hidden, int heads, const int32_t* row_ptr, const int32_t* src,
     const int32_t* transpose, int max_pairs, const void* q, int ld_q, const void* k, int ld_k,
@@ -231,7 +233,7 @@ int tmdnet_et_message_bwd2_ex(
     const void* gg_pk, int ld_ggpk, const void* gg_pv, int ld_ggpv, const void* gg_cut,
     const void* gg_unit, void* d_grad_x, void* d_grad_vec, void* d_q, int ld_dq, void* d_k, int ld_dk,
     void* d_v, int ld_dv, void* d_vec, void* d_pk, int ld_dpk, void* d_pv, int ld_dpv, void* d_cut,
-    void* d_unit, void* edge_scratch, int flags, void* stream);
+    void* d_unit, void* edge_scratch, const int32_t* pk_rows, int flags, void* stream);
 
 /* ET layer epilogue (reference torchmd_et.py:278-280, 309-311 + residuals 181-184), fused:
  *   vecp = vec_proj(vec) [N][3][3H] = [v1|v2|v3], o = o_proj(x_agg) [N][3H] = [o1|o2|o3]

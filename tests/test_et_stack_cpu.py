@@ -199,9 +199,13 @@ def _fake_bwd2(ctx, ggs):
     return kernels._ETMessageBwd.composite_backward(ctx, *ggs)
 
 
-def _fake_bwd2_launch(q, k, v, vec, pk, pv, C, u, graph, heads, gx, gvec, ggs, flags=0, out=None):
+def _fake_bwd2_launch(q, k, v, vec, pk, pv, C, u, graph, heads, gx, gvec, ggs, flags=0, out=None, pk_rows=None):
     """tmdnet_et_message_bwd2_ex restated: the VJP of the message backward by double autograd (``out``
-    buffers filled / accumulated as the launch wrapper does)."""
+    buffers filled / accumulated as the launch wrapper does; ``pk_rows``: pair-shared projection rows)."""
+    if pk_rows is not None:
+        idx = pk_rows.long()
+        pk = pk.index_select(0, idx) if pk is not None else None
+        pv = pv.index_select(0, idx) if pv is not None else None
     res = _fake_bwd2_core(q, k, v, vec, pk, pv, C, u, graph, heads, gx, gvec, ggs)
     if not out:
         return res

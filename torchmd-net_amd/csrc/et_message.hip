@@ -160,11 +160,11 @@ struct Geo {
 // Logical block -> (channel group, node block).  With the XCD-contiguous remap the CS channel
 // groups of one node range run on DIFFERENT XCDs, so each XCD's L2 holds only its channel slice of
 // the gathered source rows (the per-XCD working set shrinks CS-fold).
-template <int S, int CS, bool ORD>
+template <int S, int CS, bool ORD, int WPB = 4>  // WPB: waves per block
 __device__ __forceinline__ Geo geo(int n, int L, const int32_t* order, int xcd, int blk, int nwg) {
   Geo g;
   const int wid = threadIdx.x >> 6;
-  const int npb = 4 / S;
+  const int npb = WPB / S;
   const int nbn = (n + npb - 1) / npb;
   const int lb = xcd_block(blk, nwg, xcd);
   g.cg = CS > 1 ? __builtin_amdgcn_readfirstlane(lb / nbn) : 0;
@@ -364,7 +364,9 @@ __device__ __forceinline__ void zero_pad_rows(const Args<T>& A, int blk, int nwg
     for (long long i = tid; i < rows; i += nth) A.gr[e0 + i] = T(0);
 }
 
-template <typename T, int V, int S, int CS, bool DR>
+// AG: TMDNET_ACC_GRADS in the training form -- the injected per-edge projection cotangents are loaded
+// with the edge's other loads (not read back after the math: one memory round trip per edge fewer)
+template <typename T, int V, int S, int CS, bool DR, bool AG = false>
 __device__ __forceinline__ void bwd_dst_body(const Args<T>& A, int blk, int nwg) {
   __shared__ T lds[S > 1 ? 4 * 64 * V : 1];
   const Geo G = geo<S, CS, false>(A.n, A.L, nullptr, A.xcd, blk, nwg);
@@ -421,6 +423,16 @@ __device__ __forceinline__ void bwd_dst_body(const Args<T>& A, int blk, int nwg)
       ldv<T, V>(w0, vecs);
       ldv<T, V>(w1, vecs + vcd);
       ldv<T, V>(w2, vecs + 2 * vcd);
+      T ik[AG ? V : 1], ix[AG ? V : 1], i1[AG ? V : 1], i2[AG ? V : 1];  // injected cotangents (AG)
+      if constexpr (AG) {
+        if (hk) ldv<T, V>(ik, A.gpk + (size_t)k * A.ldpk + c0); else zero(ik);
+        if (hv) {
+          const T* gp = A.gpv + (size_t)k * A.ldpv + vo;
+          ldv<T, V>(ix, gp); ldv<T, V>(i1, gp + A.vst); ldv<T, V>(i2, gp + 2 * A.vst);
+        } else {
+          zero(ix); zero(i1); zero(i2);
+        }
+      }
       T dpk_[DR ? V : 1], dpx_[DR ? V : 1], dp1_[DR ? V : 1], dp2_[DR ? V : 1];
       if constexpr (DR) {
         ldv<T, V>(dpk_, opt(A.dpk, (size_t)st.row * A.ldpk + c0, dummy + c0));
@@ -479,7 +491,11 @@ __device__ __forceinline__ void bwd_dst_body(const Args<T>& A, int blk, int nwg)
         grr = group_sum(grr, A.L);
       } else {
         if (on) {
-          const bool ag = A.acc & TMDNET_ACC_GRADS;
+          if constexpr (AG) {
+#pragma unroll
+            for (int i = 0; i < V; ++i) { gpk[i] += ik[i]; gpx[i] += ix[i]; gp1[i] += i1[i]; gp2[i] += i2[i]; }
+          }
+          const bool ag = !AG && (A.acc & TMDNET_ACC_GRADS);
           if (hk) stv_acc<T, V>(A.gpk + (size_t)k * A.ldpk + c0, gpk, ag);
           if (hv) {
             T* gp = A.gpv + (size_t)k * A.ldpv + vo;
@@ -639,9 +655,9 @@ __device__ __forceinline__ void bwd_src_body(const Args<T>& A, int blk, int nwg)
 template <typename T, int V, bool DR>
 constexpr int bwd_min_waves() { return (DR && sizeof(T) == 4 && V <= 4) ? 3 : 1; }
 
-template <typename T, int V, int S, int CS, bool DR>
+template <typename T, int V, int S, int CS, bool DR, bool AG = false>
 __global__ __launch_bounds__(256, (bwd_min_waves<T, V, DR>())) void k_bwd_dst(Args<T> A) {
-  bwd_dst_body<T, V, S, CS, DR>(A, blockIdx.x, gridDim.x);
+  bwd_dst_body<T, V, S, CS, DR, AG>(A, blockIdx.x, gridDim.x);
 }
 template <typename T, int V, int S, int CS>
 __global__ __launch_bounds__(256) void k_bwd_src(Args<T> A) {
@@ -650,10 +666,10 @@ __global__ __launch_bounds__(256) void k_bwd_src(Args<T> A) {
 // Both passes in ONE grid (they only read the same inputs): blocks [0, split) run the destination
 // pass, [split, 2 split) the source pass.  Used for small systems, where one pass alone leaves most
 // of the chip idle and the launch gap between the two passes is a visible share of the layer.
-template <typename T, int V, int S, int CS, bool DR>
+template <typename T, int V, int S, int CS, bool DR, bool AG = false>
 __global__ __launch_bounds__(256, (bwd_min_waves<T, V, DR>())) void k_bwd_both(Args<T> A) {
   const int split = (int)gridDim.x / 2;
-  if ((int)blockIdx.x < split) bwd_dst_body<T, V, S, CS, DR>(A, blockIdx.x, split);
+  if ((int)blockIdx.x < split) bwd_dst_body<T, V, S, CS, DR, AG>(A, blockIdx.x, split);
   else bwd_src_body<T, V, S, CS>(A, blockIdx.x - split, split);
 }
 
@@ -698,11 +714,14 @@ template <typename T> struct Args2 {
   int acc_edge, acc_gvec; // accumulate o_C / o_u (and o_gvec) into the caller's buffers
 };
 
+// (S = 8: one node per 512-thread block -- the kernel's ~190 VGPRs allow two waves per SIMD, so a
+// block of 8 waves fills a CU and a node's edges spread over 8 waves instead of 4)
 template <typename T, int V, int S>
-__global__ __launch_bounds__(256) void k_bwd2(Args2<T> B) {
-  __shared__ T lds[S > 1 ? 4 * 64 * 5 * V : 1];
+__global__ __launch_bounds__(S > 4 ? 64 * S : 256) void k_bwd2(Args2<T> B) {
+  constexpr int WPB = S > 4 ? S : 4;
+  __shared__ T lds[S > 1 ? WPB * 64 * 5 * V : 1];
   const Args<T>& A = B.a;
-  const Geo G = geo<S, 1, false>(A.n, A.L, nullptr, A.xcd, blockIdx.x, gridDim.x);
+  const Geo G = geo<S, 1, false, WPB>(A.n, A.L, nullptr, A.xcd, blockIdx.x, gridDim.x);
   const int t = G.node;
   {  // static-capacity padding rows [row_ptr[n], cap) of the per-edge outputs: zero (no memset)
     const int e0 = min(A.row_ptr[A.n], A.cap);
@@ -739,13 +758,33 @@ __global__ __launch_bounds__(256) void k_bwd2(Args2<T> B) {
   ldv<T, V>(g2, A.gvec + (size_t)t * 3 * A.H + 2 * A.H + c0);
   ldv<T, V>(ggq, B.ggq + (size_t)t * B.ldggq + c0);
   const int b = min(A.row_ptr[t], A.cap), e = min(A.row_ptr[t + 1], A.cap);
-  for (int k = b + EPW * G.sub + G.es; k < e; k += EPW * S) {
-    const int s = A.src[k];
+  const int step = EPW * S;
+  // the per-edge scalars one edge ahead: the next edge's loads are in flight while this edge's rows
+  // are gathered (one memory round trip per edge instead of two)
+  int sn = 0, krn = 0;
+  T Cn = T(0), u0n = T(0), u1n = T(0), u2n = T(0), gCn = T(0), g0n = T(0), g1n = T(0), g2n = T(0);
+  auto scalars = [&](int kk_) {
+    sn = A.src[kk_];
+    krn = A.prow ? A.prow[kk_] : kk_;  // pair-shared projection rows
+    Cn = A.C[kk_];
+    u0n = A.u[3 * kk_]; u1n = A.u[3 * kk_ + 1]; u2n = A.u[3 * kk_ + 2];
+    gCn = B.ggC[kk_];
+    g0n = B.ggu[3 * kk_]; g1n = B.ggu[3 * kk_ + 1]; g2n = B.ggu[3 * kk_ + 2];
+  };
+  if (b + EPW * G.sub + G.es < e) scalars(b + EPW * G.sub + G.es);
+  for (int k = b + EPW * G.sub + G.es; k < e; k += step) {
+    const int s = sn, kr = krn;
     TMD_DCHECK(s >= 0 && s < A.n);
-    const T Ce = A.C[k];
-    const T u0 = A.u[3 * k], u1 = A.u[3 * k + 1], u2 = A.u[3 * k + 2];
-    const T ggC = B.ggC[k];
-    const T gu0 = B.ggu[3 * k], gu1 = B.ggu[3 * k + 1], gu2 = B.ggu[3 * k + 2];
+    const T Ce = Cn;
+    const T u0 = u0n, u1 = u1n, u2 = u2n;
+    const T ggC = gCn;
+    const T gu0 = g0n, gu1 = g1n, gu2 = g2n;
+    if (k + step < e) scalars(k + step);
+    T pC = T(0), pu0 = T(0), pu1 = T(0), pu2 = T(0);  // accumulated edge outputs: read with the loads
+    if (B.acc_edge && G.el == 0) {
+      pC = B.o_C[k];
+      pu0 = B.o_u[3 * k]; pu1 = B.o_u[3 * k + 1]; pu2 = B.o_u[3 * k + 2];
+    }
     T kk[V], ggk[V], vx[V], v1[V], v2[V], ggvx[V], ggv1[V], ggv2[V], w0[V], w1[V], w2[V];
     T ggw0[V], ggw1[V], ggw2[V], rk[V], rx[V], r1[V], r2[V], ggpk[V], ggpx[V], ggp1[V], ggp2[V];
     ldv<T, V>(kk, A.k + (size_t)s * A.ldk + c0);
@@ -763,13 +802,13 @@ __global__ __launch_bounds__(256) void k_bwd2(Args2<T> B) {
     const T* gws = B.ggw + (size_t)s * 3 * A.H + c0;
     ldv<T, V>(ggw0, gws); ldv<T, V>(ggw1, gws + A.H); ldv<T, V>(ggw2, gws + 2 * A.H);
     if (hk) {
-      ldv<T, V>(rk, A.pk + (size_t)k * A.ldpk + c0);
+      ldv<T, V>(rk, A.pk + (size_t)kr * A.ldpk + c0);
       ldv<T, V>(ggpk, B.ggpk + (size_t)k * B.ldggpk + c0);
     } else {
       zero(rk); zero(ggpk);
     }
     if (hv) {
-      const T* ps = A.pv + (size_t)k * A.ldpv + vo;
+      const T* ps = A.pv + (size_t)kr * A.ldpv + vo;
       ldv<T, V>(rx, ps); ldv<T, V>(r1, ps + A.vst); ldv<T, V>(r2, ps + 2 * A.vst);
       const T* gps = B.ggpv + (size_t)k * B.ldggpv + vo;
       ldv<T, V>(ggpx, gps); ldv<T, V>(ggp1, gps + A.vst); ldv<T, V>(ggp2, gps + 2 * A.vst);
@@ -846,13 +885,8 @@ __global__ __launch_bounds__(256) void k_bwd2(Args2<T> B) {
       stv<T, V>(op, opx); stv<T, V>(op + A.vst, op1); stv<T, V>(op + 2 * A.vst, op2);
     }
     if (G.el == 0) {
-      if (B.acc_edge) {
-        B.o_C[k] += gC;
-        B.o_u[3 * k] += gua0; B.o_u[3 * k + 1] += gua1; B.o_u[3 * k + 2] += gua2;
-      } else {
-        B.o_C[k] = gC;
-        B.o_u[3 * k] = gua0; B.o_u[3 * k + 1] = gua1; B.o_u[3 * k + 2] = gua2;
-      }
+      B.o_C[k] = pC + gC;
+      B.o_u[3 * k] = pu0 + gua0; B.o_u[3 * k + 1] = pu1 + gua1; B.o_u[3 * k + 2] = pu2 + gua2;
     }
     if (B.o_src) {  // source-node terms as this edge's scratch row (summed by k_bwd2_src)
       T* sr = B.o_src + (size_t)k * 7 * A.H;
@@ -1254,7 +1288,9 @@ static int et_launch_vs(Args<T> A, hipStream_t st) {
   else if (KIND == 2) hipLaunchKernelGGL((k_bwd_src<T, V, S, 1>), g, b, 0, st, A);
   else if (KIND == 3) hipLaunchKernelGGL((k_bwd_both<T, V, S, 1, false>), dim3(2 * nbn), b, 0, st, A);
   else if (KIND == 4) hipLaunchKernelGGL((k_bwd_dst<T, V, S, 1, true>), g, b, 0, st, A);
-  else hipLaunchKernelGGL((k_bwd_both<T, V, S, 1, true>), dim3(2 * nbn), b, 0, st, A);
+  else if (KIND == 5) hipLaunchKernelGGL((k_bwd_both<T, V, S, 1, true>), dim3(2 * nbn), b, 0, st, A);
+  else if (KIND == 6) hipLaunchKernelGGL((k_bwd_both<T, V, S, 1, false, true>), dim3(2 * nbn), b, 0, st, A);
+  else hipLaunchKernelGGL((k_bwd_dst<T, V, S, 1, false, true>), g, b, 0, st, A);
   return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
 }
 
@@ -1357,8 +1393,10 @@ static int bwd(int n, int H, int heads, const int32_t* row_ptr, const int32_t* s
   if (dr && ((A.pk && !dpk) || (A.pv && !dpv))) return kBadArgument;
   if (!dr && ((A.pk && !gpk) || (A.pv && !gpv))) return kBadArgument;
   static const int fuse_nodes = getenv("TMDNET_ET_FUSE") ? atoi(getenv("TMDNET_ET_FUSE")) : kBwdFuseNodes;
-  if (n < fuse_nodes) return dr ? et_launch<T, 5, false>(V, A, st) : et_launch<T, 3, false>(V, A, st);
-  rc = dr ? et_launch<T, 4, false>(V, A, st) : et_launch<T, 1, false>(V, A, st);
+  const bool ag = !dr && (acc & TMDNET_ACC_GRADS) && (A.pk || A.pv);  // injected projection cotangents
+  if (n < fuse_nodes)
+    return dr ? et_launch<T, 5, false>(V, A, st) : ag ? et_launch<T, 6, false>(V, A, st) : et_launch<T, 3, false>(V, A, st);
+  rc = dr ? et_launch<T, 4, false>(V, A, st) : ag ? et_launch<T, 7, false>(V, A, st) : et_launch<T, 1, false>(V, A, st);
   if (rc) return rc;
   return et_launch<T, 2, false>(V, A, st);
 }
@@ -1367,6 +1405,7 @@ struct Bwd2Ex {  // the strides / accumulation / source-pass extras of tmdnet_et
   int ldggq, ldggk, ldggv, ldoq, ldok, ldov, ldopk, ldopv;
   const int32_t* tr;
   void* scratch;
+  const int32_t* prow;  // pk / pv row of every edge (pair-shared rows); NULL: row e
 };
 
 template <typename T>
@@ -1420,15 +1459,22 @@ static int bwd2(int n, int H, int heads, const int32_t* row_ptr, const int32_t* 
       B.tr = ex->tr;
       B.o_src = (T*)ex->scratch;
     }
+    B.a.prow = ex->prow;
   }
   B.acc_edge = (flags & TMDNET_BWD2_ACC_EDGE) ? 1 : 0;
   B.acc_gvec = (flags & TMDNET_BWD2_ACC_GVEC) ? 1 : 0;
   if (n <= 0) return kOk;
-  const int S = n < 4096 ? 4 : (n < 8192 ? 2 : 1);  // waves per node (small systems: fill the chip)
-  const dim3 g((n + 4 / S - 1) / (4 / S)), b(256);
+  // waves per node (small systems: fill the chip); TMDNET_BWD2_S overrides (tuning)
+  static const int s_env = getenv("TMDNET_BWD2_S") ? atoi(getenv("TMDNET_BWD2_S")) : 0;
+  int S = n < 2048 ? 8 : (n < 4096 ? 4 : (n < 8192 ? 2 : 1));
+  if (s_env == 1 || s_env == 2 || s_env == 4 || s_env == 8) S = s_env;
+  if (S == 8 && V != 2) S = 4;
+  const dim3 g(S == 8 ? n : (n + 4 / S - 1) / (4 / S)), b(S == 8 ? 512 : 256);
 #define TMD_L2(VV, SS) hipLaunchKernelGGL((k_bwd2<T, VV, SS>), g, b, 0, st, B)
   if (V == 1) { if (S == 4) TMD_L2(1, 4); else if (S == 2) TMD_L2(1, 2); else TMD_L2(1, 1); }
-  else if (V == 2) { if (S == 4) TMD_L2(2, 4); else if (S == 2) TMD_L2(2, 2); else TMD_L2(2, 1); }
+  else if (V == 2) {
+    if (S == 8) TMD_L2(2, 8); else if (S == 4) TMD_L2(2, 4); else if (S == 2) TMD_L2(2, 2); else TMD_L2(2, 1);
+  }
   else { if (S == 4) TMD_L2(4, 4); else if (S == 2) TMD_L2(4, 2); else TMD_L2(4, 1); }
 #undef TMD_L2
   if (hipGetLastError() != hipSuccess) return kLaunchFailed;
@@ -1526,9 +1572,9 @@ extern "C" int tmdnet_et_message_bwd2_ex(
     const void* gg_pk, int ld_ggpk, const void* gg_pv, int ld_ggpv, const void* gg_cut,
     const void* gg_unit, void* d_grad_x, void* d_grad_vec, void* d_q, int ld_dq, void* d_k, int ld_dk,
     void* d_v, int ld_dv, void* d_vec, void* d_pk, int ld_dpk, void* d_pv, int ld_dpv, void* d_cut,
-    void* d_unit, void* edge_scratch, int flags, void* stream) {
+    void* d_unit, void* edge_scratch, const int32_t* pk_rows, int flags, void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  const et::Bwd2Ex ex{ld_ggq, ld_ggk, ld_ggv, ld_dq, ld_dk, ld_dv, ld_dpk, ld_dpv, transpose, edge_scratch};
+  const et::Bwd2Ex ex{ld_ggq, ld_ggk, ld_ggv, ld_dq, ld_dk, ld_dv, ld_dpk, ld_dpv, transpose, edge_scratch, pk_rows};
 #define TMD_BWD2(T)                                                                              \
   return et::bwd2<T>(n_nodes, hidden, heads, row_ptr, src, max_pairs, q, ld_q, k, ld_k, v, ld_v, \
                      vec_in, pk, ld_pk, pv, ld_pv, cutoff, unit, grad_x, grad_vec, gg_q, gg_k,   \

@@ -855,7 +855,6 @@ def _second_order(ctx, ggs, want):
             inj["W"]["dkv"] = (g_pkv_all, gb_f)  # accumulated into pass 3's edge-feature weight GEMM
         else:
             acc("dkv", torch.mm(g_pkv_all.t(), gb_f))
-    pr = meta.pairs[0].long() if meta.pairs is not None else None
     C_bar = torch.zeros((E,), **o)
     u_bar = torch.zeros((E, 3), **o)
     gbar_x = gg_x if gg_x is not None else torch.zeros((N, H), **o)
@@ -897,10 +896,9 @@ def _second_order(ctx, ggs, want):
         kernels.gemm_group(probs)
         # message backward VJP (per-edge projection rows)
         pk = pv = None
-        if has_e:
-            pke = pkv if pr is None else pkv.index_select(0, pr)
-            pk = pke[:, :H] if meta.hk else None
-            pv = pke[:, H * int(meta.hk):] if meta.hv else None
+        if has_e:  # the pair-shared projection rows, read through pk_rows by the kernel
+            pk = pkv[:, :H] if meta.hk else None
+            pv = pkv[:, H * int(meta.hk):] if meta.hv else None
         gbl = gb_pkv_all[:, l * D:(l + 1) * D] if gb_pkv_all is not None else None
         ggs_m = (gb_gqkv[:, :H], gb_gqkv[:, H:2 * H], gb_gqkv[:, 2 * H:],
                  gbar_v if vec_l is not None else None,
@@ -913,7 +911,8 @@ def _second_order(ctx, ggs, want):
             outs["pkv"] = inj["stk"]["pkv"][:, l * D:(l + 1) * D]
         d_gxa, d_gvec, d_q, d_k, d_v, d_vec, d_pk, d_pv, d_C, d_u = kernels.et_message_bwd2_launch(
             qkv[:, :H], qkv[:, H:2 * H], qkv[:, 2 * H:], vec_l, pk, pv, C, u, graph, meta.heads,
-            R["g_xa"], R["gV"] if R["gV"] is not None else torch.zeros((N, 3, H), **o), ggs_m, out=outs)
+            R["g_xa"], R["gV"] if R["gV"] is not None else torch.zeros((N, 3, H), **o), ggs_m, out=outs,
+            pk_rows=meta.pk_rows if has_e else None)
         inj["qkv"][l] = outs["qkv"]
         if has_e:
             inj["pkv"][l] = outs["pkv"]

@@ -728,12 +728,14 @@ class _ETMessageBwd(Function):
 BWD2_SCRATCH_MAX_BYTES = 2 << 30
 
 
-def et_message_bwd2_launch(q, k, v, vec, pk, pv, C, u, graph, heads, gx, gvec, ggs, flags=0, out=None):
+def et_message_bwd2_launch(q, k, v, vec, pk, pv, C, u, graph, heads, gx, gvec, ggs, flags=0, out=None,
+                           pk_rows=None):
     """One ``tmdnet_et_message_bwd2_ex`` launch: the VJP of tmdnet_et_message_bwd (without the vec
     residual) at primals (q, k, v, vec, pk, pv, C, u) and seeds (gx, gvec), for the cotangents
     ``ggs`` = (gg_q, gg_k, gg_v, gg_vec, gg_pk, gg_pv, gg_C, gg_u) of its outputs (None / empty =
-    zero; node cotangents may be column blocks of a wider buffer).  pk / pv are per-edge rows (no pair
-    indirection).  Returns (d_gx, d_gvec, d_q, d_k, d_v, d_vec, d_pk, d_pv, d_C, d_u); d_vec is None
+    zero; node cotangents may be column blocks of a wider buffer).  pk / pv are per-edge rows, or with
+    ``pk_rows`` the pair-shared rows edge e reads at pk_rows[e] (their cotangents / gradients stay
+    per edge).  Returns (d_gx, d_gvec, d_q, d_k, d_v, d_vec, d_pk, d_pv, d_C, d_u); d_vec is None
     when vec is None, d_pk / d_pv when pk / pv are.
 
     ``out`` (optional dict) names caller buffers: "gx" [N, H] receives d_gx, "qkv" [N, 5H] d_q | d_k | d_v, "pkv" [E, D]
@@ -796,7 +798,7 @@ def et_message_bwd2_launch(q, k, v, vec, pk, pv, C, u, graph, heads, gx, gvec, g
         P(C), P(u), P(gxc), P(gvc), P(ggq), _ld(ggq), P(ggk), _ld(ggk), P(ggv), _ld(ggv), P(ggw),
         P(ggpk), _ld(ggpk), P(ggpv), _ld(ggpv), P(ggC), P(ggu), P(d_gx), P(d_gvec),
         P(d_q), _ld(d_q), P(d_k), _ld(d_k), P(d_v), _ld(d_v), P(d_vec), P(d_pk), _ld(d_pk), P(d_pv), _ld(d_pv),
-        P(d_C), P(d_u), P(scratch), int(flags), nat.stream(q.device))
+        P(d_C), P(d_u), P(scratch), P(pk_rows), int(flags), nat.stream(q.device))
     nat.check(rc, "tmdnet_et_message_bwd2_ex")
     return d_gx, d_gvec, d_q, d_k, d_v, d_vec, d_pk, d_pv, d_C, d_u
 
