@@ -493,6 +493,15 @@ int tmdnet_embedding_bwd_f32(int n, int H, int num_types, const int64_t* z, int 
                              const void* const* grads, const int* ld_grads, void* const* outs, int accumulate,
                              void* stream);
 
+/* Energy + force MSE training loss (reference LNNP.step, module.py:130-179, mean reductions):
+ *   out[0] = w1 * mean((a1 - b1)^2) + w2 * mean((a2 - b2)^2)   over n1 / n2 elements (one launch),
+ * and its backward d1 = g w1 2 (a1 - b1) / n1, d2 = g w2 2 (a2 - b2) / n2 with g = grad_out[0] read
+ * on the device (d1 / d2 nullable). */
+int tmdnet_mse2_fwd(int dtype, int n1, const void* a1, const void* b1, double w1, int n2, const void* a2,
+                    const void* b2, double w2, void* out, void* stream);
+int tmdnet_mse2_bwd(int dtype, int n1, const void* a1, const void* b1, double w1, int n2, const void* a2,
+                    const void* b2, double w2, const void* grad_out, void* d1, void* d2, void* stream);
+
 /* Library identification (for load checks). */
 const char* tmdnet_build_info(void);
 

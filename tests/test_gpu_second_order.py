@@ -280,3 +280,23 @@ def test_node_weight_grads_tn_match_batched_library(monkeypatch):
         assert _rel(a, b) < 1e-4
         n += 1
     assert n > 30
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float64, 1e-12), (torch.float32, 1e-5)])
+def test_fused_energy_force_loss(dtype, tol):
+    """kernels.mse2 (LNNPStep's E + F loss in one launch, backward in one) against the composite
+    y_weight * mse_loss + neg_dy_weight * mse_loss: value and both prediction gradients."""
+    import torch.nn.functional as F
+    from torchmdnet import kernels
+    torch.manual_seed(3)
+    py, y = torch.randn(32, 1, device=DEV, dtype=dtype), torch.randn(32, 1, device=DEV, dtype=dtype)
+    pf, f = torch.randn(678, 3, device=DEV, dtype=dtype), torch.randn(678, 3, device=DEV, dtype=dtype)
+    res = []
+    for fn in (lambda a, b: kernels.mse2(a, y, b, f, 0.05, 0.95),
+               lambda a, b: 0.05 * F.mse_loss(a, y) + 0.95 * F.mse_loss(b, f)):
+        a, b = py.clone().requires_grad_(True), pf.clone().requires_grad_(True)
+        loss = fn(a, b)
+        ga, gb = torch.autograd.grad(3.0 * loss, (a, b))
+        res.append((loss.detach(), ga, gb))
+    for u, v in zip(*res):
+        assert _rel(u, v) < tol

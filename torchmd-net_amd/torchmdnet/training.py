@@ -16,6 +16,7 @@ import torch
 import torch.distributed as dist
 import torch.nn.functional as F
 
+from . import kernels
 from .et_stack import second_order_expected
 
 
@@ -114,10 +115,14 @@ class LNNPStep:
         # a force loss differentiates the force pass again: let the ET stack record for its hand second order
         with second_order_expected(self.neg_dy_weight > 0):
             pred, pred_neg_dy = self.model(z, pos, batch)
+        if y.ndim == 1:  # reference module.py:147-148
+            y = y.unsqueeze(1)
+        if (self.y_weight > 0 and self.neg_dy_weight > 0 and pred_neg_dy is not None and pred.is_cuda
+                and pred.shape == y.shape and pred_neg_dy.shape == neg_dy.shape):
+            # both terms in one launch (and one for their backward): kernels.mse2
+            return kernels.mse2(pred, y, pred_neg_dy, neg_dy, self.y_weight, self.neg_dy_weight)
         loss = 0.0
         if self.y_weight > 0:
-            if y.ndim == 1:  # reference module.py:147-148
-                y = y.unsqueeze(1)
             loss = loss + self.y_weight * F.mse_loss(pred, y)
         if self.neg_dy_weight > 0 and pred_neg_dy is not None:
             loss = loss + self.neg_dy_weight * F.mse_loss(pred_neg_dy, neg_dy)
