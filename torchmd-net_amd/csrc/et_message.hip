@@ -717,6 +717,8 @@ template <typename T> struct Args2 {
 // (S = 8: one node per 512-thread block -- the kernel's ~190 VGPRs allow two waves per SIMD, so a
 // block of 8 waves fills a CU and a node's edges spread over 8 waves instead of 4)
 template <typename T, int V, int S>
+// (capping the registers for more waves per SIMD spills: 4 waves/SIMD 63 -> 142 us, 3 -> 84 us per
+// layer at ET-QM9; measured and not kept)
 __global__ __launch_bounds__(S > 4 ? 64 * S : 256) void k_bwd2(Args2<T> B) {
   constexpr int WPB = S > 4 ? S : 4;
   __shared__ T lds[S > 1 ? WPB * 64 * 5 * V : 1];
