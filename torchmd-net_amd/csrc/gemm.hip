@@ -78,17 +78,21 @@ __device__ __forceinline__ void wave_tile(const Prob& P, int r0, int c0, int kb0
   }
 }
 
+// KMAX: 8 blocks per load batch for the 4- / 8-wave kernels; 4 for the 16-wave kernel, whose
+// 1024-thread blocks cap a wave at 128 VGPRs (an 8-block batch alone is 128 VGPRs of loads: it
+// spilled 75 VGPRs; the 16-wave slices of the ET shapes are 2-3 blocks anyway)
+template <int KMAX>
 __device__ __forceinline__ void slice(const Prob& P, int r0, int c0, int kb0, int mine, f4 (&acc)[2][2]) {
-  switch (min(mine, 8)) {  // a K slice of up to 8 blocks is loaded in one go
+  switch (min(mine, KMAX)) {  // a K slice of up to KMAX blocks is loaded in one go
     case 0: break;
     case 1: wave_tile<1>(P, r0, c0, kb0, mine, acc); break;
     case 2: wave_tile<2>(P, r0, c0, kb0, mine, acc); break;
     case 3: wave_tile<3>(P, r0, c0, kb0, mine, acc); break;
     case 4: wave_tile<4>(P, r0, c0, kb0, mine, acc); break;
-    case 5: wave_tile<5>(P, r0, c0, kb0, mine, acc); break;
-    case 6: wave_tile<6>(P, r0, c0, kb0, mine, acc); break;
-    case 7: wave_tile<7>(P, r0, c0, kb0, mine, acc); break;
-    default: wave_tile<8>(P, r0, c0, kb0, mine, acc); break;
+    case 5: if constexpr (KMAX >= 5) wave_tile<5>(P, r0, c0, kb0, mine, acc); break;
+    case 6: if constexpr (KMAX >= 6) wave_tile<6>(P, r0, c0, kb0, mine, acc); break;
+    case 7: if constexpr (KMAX >= 7) wave_tile<7>(P, r0, c0, kb0, mine, acc); break;
+    default: if constexpr (KMAX >= 8) wave_tile<8>(P, r0, c0, kb0, mine, acc); break;
   }
 }
 
@@ -120,7 +124,7 @@ __global__ __launch_bounds__(NW * 64) void k_gemm(Group G) {
   const int r0 = (t / P.tiles_n) * 32, c0 = (t % P.tiles_n) * 32;
   const int per = (nkb + NW - 1) / NW;  // blocks per wave
   const int kb0 = w * per;
-  slice(P, r0, c0, kb0, max(0, min(per, nkb - kb0)), acc);
+  slice<(NW >= 16 ? 4 : 8)>(P, r0, c0, kb0, max(0, min(per, nkb - kb0)), acc);
 #pragma unroll
   for (int bi = 0; bi < 2; ++bi)
 #pragma unroll
