@@ -194,9 +194,11 @@ int tmdnet_et_message_bwd(int dtype, int n_nodes, int hidden, int heads, const i
                           const int32_t* pk_rows, const int32_t* order,
                           void* stream);  /* accumulate may also carry TMDNET_ET_V_PLANAR */
 /* "dr mode" of the backward (gdist non-NULL; with TMDNET_ACC_EDGE it accumulates, without it overwrites): instead of storing gpk / gpv
- * (then NULL), the projection gradient of every edge is contracted in-kernel with dpk = d pk / d r,
+ * (then normally NULL), the projection gradient of every edge is contracted in-kernel with dpk = d pk / d r,
  * dpv = d pv / d r (rows and layout of pk / pv, read through pk_rows) and accumulated into
- * gdist[e] -- the force pass then needs neither the E x 4H gradient nor its GEMM. */
+ * gdist[e] -- the force pass then needs neither the E x 4H gradient nor its GEMM.  gpk / gpv non-NULL
+ * in dr mode: the projection gradient is stored as well (the recorded force pass of force-matching
+ * training keeps it for its second order). */
 
 /* Second-order backward: the VJP of tmdnet_et_message_bwd (forces differentiated again, reference
  * model.py:286-298 with create_graph=True).  gg_* are the cotangents of that call's outputs (gq, gk,
@@ -223,7 +225,9 @@ int tmdnet_et_message_bwd2(int dtype, int n_nodes, int hidden, int heads, const 
  * atomics; d_k, d_v, d_vec are overwritten, no zero fill needed).  transpose / edge_scratch NULL:
  * atomics as tmdnet_et_message_bwd2.  pk_rows (nullable, as in tmdnet_et_message_fwd): edge e's
  * projection rows pk / pv are rows pk_rows[e] (pair-shared rows; gg_pk / gg_pv and d_pk / d_pv stay
- * per edge).  flags: TMDNET_ET_V_PLANAR | TMDNET_BWD2_ACC_*. */
+ * per edge).  gg_pkv_scale (nullable, needs pk_rows): gg_pk / gg_pv are pair rows too, edge e's
+ * cotangent being row pk_rows[e] scaled by gg_pkv_scale[e] (the force-matching second order: the
+ * cotangent of the dr-mode g_r times d(dk,dv)/dr).  flags: TMDNET_ET_V_PLANAR | TMDNET_BWD2_ACC_*. */
 int tmdnet_et_message_bwd2_ex(
     int dtype, int n_nodes, int hidden, int heads, const int32_t* row_ptr, const int32_t* src,
     const int32_t* transpose, int max_pairs, const void* q, int ld_q, const void* k, int ld_k,
@@ -233,7 +237,8 @@ int tmdnet_et_message_bwd2_ex(
     const void* gg_pk, int ld_ggpk, const void* gg_pv, int ld_ggpv, const void* gg_cut,
     const void* gg_unit, void* d_grad_x, void* d_grad_vec, void* d_q, int ld_dq, void* d_k, int ld_dk,
     void* d_v, int ld_dv, void* d_vec, void* d_pk, int ld_dpk, void* d_pv, int ld_dpv, void* d_cut,
-    void* d_unit, void* edge_scratch, const int32_t* pk_rows, int flags, void* stream);
+    void* d_unit, void* edge_scratch, const int32_t* pk_rows, const void* gg_pkv_scale, int flags,
+    void* stream);
 
 /* ET layer epilogue (reference torchmd_et.py:278-280, 309-311 + residuals 181-184), fused:
  *   vecp = vec_proj(vec) [N][3][3H] = [v1|v2|v3], o = o_proj(x_agg) [N][3H] = [o1|o2|o3]

@@ -102,8 +102,8 @@ def _fake_bwd(q, k, v, vec, pk, pv, C, u, graph, heads, gx, gvec, gq, gk, gv, gw
         put(gpk, z(g[4], pk))
     if gpv is not None:
         put(gpv, _to_planar(z(g[5], pv), H, heads, planar))
-    if g_r is not None:  # dr mode: <g_pk, dpk> + <g_pv, dpv> per edge (dpv in the kernel's row layout)
-        assert gpk is None and gpv is None
+    if g_r is not None:  # dr mode: <g_pk, dpk> + <g_pv, dpv> per edge (dpv in the kernel's row layout);
+        # gpk / gpv given as well: the recorded force pass keeps the projection gradient (stored above)
         if not accumulate & nat.ACC_EDGE:
             g_r.zero_()
         if dpk is not None:
@@ -199,9 +199,15 @@ def _fake_bwd2(ctx, ggs):
     return kernels._ETMessageBwd.composite_backward(ctx, *ggs)
 
 
-def _fake_bwd2_launch(q, k, v, vec, pk, pv, C, u, graph, heads, gx, gvec, ggs, flags=0, out=None, pk_rows=None):
+def _fake_bwd2_launch(q, k, v, vec, pk, pv, C, u, graph, heads, gx, gvec, ggs, flags=0, out=None, pk_rows=None,
+                      gg_pkv_scale=None):
     """tmdnet_et_message_bwd2_ex restated: the VJP of the message backward by double autograd (``out``
-    buffers filled / accumulated as the launch wrapper does; ``pk_rows``: pair-shared projection rows)."""
+    buffers filled / accumulated as the launch wrapper does; ``pk_rows``: pair-shared projection rows;
+    ``gg_pkv_scale``: the projection cotangents are pair rows scaled per edge)."""
+    if gg_pkv_scale is not None:
+        idx = pk_rows.long()
+        sc = gg_pkv_scale.unsqueeze(1)
+        ggs = tuple(ggs[:4]) + tuple(None if t is None else t.index_select(0, idx) * sc for t in ggs[4:6]) + tuple(ggs[6:])
     if pk_rows is not None:
         idx = pk_rows.long()
         pk = pk.index_select(0, idx) if pk is not None else None
@@ -421,8 +427,9 @@ def test_stack_dr_mode_force_pass_and_second_order(emulated, monkeypatch, record
     """Force pass with f = rbf(r) declared (the ET model's fixed basis): the stack returns the edge
     gradient on r directly (dr mode, no projection gradient); forces and the force-matching second
     order (weight gradients through a create_graph force pass) equal plain autograd.  ``record``: the
-    create_graph force pass runs the recorded training form (g_r = <g_f, df/dr>) and hands its record
-    to the hand second order (RECORD_IN_FORCE_PASS) instead of the second order re-running it."""
+    create_graph force pass runs in dr mode keeping the projection gradient and hands its record (with
+    the pair rows' d(dk,dv)/dr, which the second order scales per edge instead of forming gb_f W^T) to
+    the hand second order (RECORD_IN_FORCE_PASS) instead of the second order re-running it."""
     monkeypatch.setattr(ES, "DR_MODE", "1")  # also on the stacked (batched) projection path
     monkeypatch.setattr(ES, "RECORD_IN_FORCE_PASS", record)
     if not batched:
@@ -464,8 +471,8 @@ def test_stack_dr_mode_force_pass_and_second_order(emulated, monkeypatch, record
         loss.backward()
         outs.append([t.detach().clone() for t in g] + [p.grad.clone() for p in params])
     hand = not planar  # the hand second order covers the reference row layout
-    if record and hand:  # force pass recorded (training form), no re-run inside the second order
-        assert modes[0] == (False, True) and not any(rec for _, rec in modes[1:])
+    if record and hand:  # force pass recorded (dr mode + kept projection gradient), no re-run later
+        assert modes[0] == (True, True) and not any(rec for _, rec in modes[1:])
     else:  # force pass in dr mode; loss.backward's passes not
         assert modes[0] == (True, False) and not modes[1][0]
     for i, (a, b) in enumerate(zip(*outs)):

@@ -489,6 +489,15 @@ __device__ __forceinline__ void bwd_dst_body(const Args<T>& A, int blk, int nwg)
           grr += (hk ? gpk[i] * dpk_[i] : T(0)) +
                  (hv ? gpx[i] * dpx_[i] + gp1[i] * dp1_[i] + gp2[i] * dp2_[i] : T(0));
         grr = group_sum(grr, A.L);
+        if (on && (A.gpk || A.gpv)) {  // the recorded force pass also keeps the projection gradient
+          if (hk && A.gpk) stv<T, V>(A.gpk + (size_t)k * A.ldpk + c0, gpk);
+          if (hv && A.gpv) {
+            T* gp = A.gpv + (size_t)k * A.ldpv + vo;
+            stv<T, V>(gp, gpx);
+            stv<T, V>(gp + A.vst, gp1);
+            stv<T, V>(gp + 2 * A.vst, gp2);
+          }
+        }
       } else {
         if (on) {
           if constexpr (AG) {
@@ -704,6 +713,8 @@ template <typename T> struct Args2 {
   const T* ggq; const T* ggk; const T* ggv; const T* ggw;   // node cotangents ([N][H], [N][H], [N][3H], [N][3][H])
   int ldggq, ldggk, ldggv;                                  // (row strides)
   const T* ggpk; int ldggpk; const T* ggpv; int ldggpv;     // edge cotangents
+  const T* ggsc;  // non-NULL: the edge cotangents are the PAIR rows ggpk / ggpv[pk_rows[e]] scaled by ggsc[e]
+                  // (force-matching: the cotangent of g_r times the pair rows' d(dk,dv)/dr)
   const T* ggC; const T* ggu;
   T* o_gx; T* o_gvec; T* o_q; T* o_k; T* o_v; T* o_vec;       // node outputs
   int ldoq, ldok, ldov;
@@ -764,10 +775,11 @@ __global__ __launch_bounds__(S > 4 ? 64 * S : 256) void k_bwd2(Args2<T> B) {
   // the per-edge scalars one edge ahead: the next edge's loads are in flight while this edge's rows
   // are gathered (one memory round trip per edge instead of two)
   int sn = 0, krn = 0;
-  T Cn = T(0), u0n = T(0), u1n = T(0), u2n = T(0), gCn = T(0), g0n = T(0), g1n = T(0), g2n = T(0);
+  T Cn = T(0), u0n = T(0), u1n = T(0), u2n = T(0), gCn = T(0), g0n = T(0), g1n = T(0), g2n = T(0), scn = T(1);
   auto scalars = [&](int kk_) {
     sn = A.src[kk_];
     krn = A.prow ? A.prow[kk_] : kk_;  // pair-shared projection rows
+    if (B.ggsc) scn = B.ggsc[kk_];
     Cn = A.C[kk_];
     u0n = A.u[3 * kk_]; u1n = A.u[3 * kk_ + 1]; u2n = A.u[3 * kk_ + 2];
     gCn = B.ggC[kk_];
@@ -776,6 +788,8 @@ __global__ __launch_bounds__(S > 4 ? 64 * S : 256) void k_bwd2(Args2<T> B) {
   if (b + EPW * G.sub + G.es < e) scalars(b + EPW * G.sub + G.es);
   for (int k = b + EPW * G.sub + G.es; k < e; k += step) {
     const int s = sn, kr = krn;
+    const T gsc = scn;
+    const int kg = B.ggsc ? kr : k;  // row of the edge cotangents
     TMD_DCHECK(s >= 0 && s < A.n);
     const T Ce = Cn;
     const T u0 = u0n, u1 = u1n, u2 = u2n;
@@ -805,17 +819,21 @@ __global__ __launch_bounds__(S > 4 ? 64 * S : 256) void k_bwd2(Args2<T> B) {
     ldv<T, V>(ggw0, gws); ldv<T, V>(ggw1, gws + A.H); ldv<T, V>(ggw2, gws + 2 * A.H);
     if (hk) {
       ldv<T, V>(rk, A.pk + (size_t)kr * A.ldpk + c0);
-      ldv<T, V>(ggpk, B.ggpk + (size_t)k * B.ldggpk + c0);
+      ldv<T, V>(ggpk, B.ggpk + (size_t)kg * B.ldggpk + c0);
     } else {
       zero(rk); zero(ggpk);
     }
     if (hv) {
       const T* ps = A.pv + (size_t)kr * A.ldpv + vo;
       ldv<T, V>(rx, ps); ldv<T, V>(r1, ps + A.vst); ldv<T, V>(r2, ps + 2 * A.vst);
-      const T* gps = B.ggpv + (size_t)k * B.ldggpv + vo;
+      const T* gps = B.ggpv + (size_t)kg * B.ldggpv + vo;
       ldv<T, V>(ggpx, gps); ldv<T, V>(ggp1, gps + A.vst); ldv<T, V>(ggp2, gps + 2 * A.vst);
     } else {
       zero(rx); zero(r1); zero(r2); zero(ggpx); zero(ggp1); zero(ggp2);
+    }
+    if (B.ggsc) {
+#pragma unroll
+      for (int i = 0; i < V; ++i) { ggpk[i] *= gsc; ggpx[i] *= gsc; ggp1[i] *= gsc; ggp2[i] *= gsc; }
     }
     // activations with first and second derivatives (an absent projection is the constant 1)
     T dk[V], dk1[V], dk2[V], dx[V], dx1[V], dx2[V], d1[V], d11[V], d12[V], d2[V], d21[V], d22[V];
@@ -1408,6 +1426,7 @@ struct Bwd2Ex {  // the strides / accumulation / source-pass extras of tmdnet_et
   const int32_t* tr;
   void* scratch;
   const int32_t* prow;  // pk / pv row of every edge (pair-shared rows); NULL: row e
+  const void* ggsc;     // per-edge scale of pair-row edge cotangents (Args2::ggsc)
 };
 
 template <typename T>
@@ -1462,6 +1481,8 @@ static int bwd2(int n, int H, int heads, const int32_t* row_ptr, const int32_t* 
       B.o_src = (T*)ex->scratch;
     }
     B.a.prow = ex->prow;
+    if (ex->ggsc && !ex->prow) return kBadArgument;
+    B.ggsc = (const T*)ex->ggsc;
   }
   B.acc_edge = (flags & TMDNET_BWD2_ACC_EDGE) ? 1 : 0;
   B.acc_gvec = (flags & TMDNET_BWD2_ACC_GVEC) ? 1 : 0;
@@ -1574,9 +1595,10 @@ extern "C" int tmdnet_et_message_bwd2_ex(
     const void* gg_pk, int ld_ggpk, const void* gg_pv, int ld_ggpv, const void* gg_cut,
     const void* gg_unit, void* d_grad_x, void* d_grad_vec, void* d_q, int ld_dq, void* d_k, int ld_dk,
     void* d_v, int ld_dv, void* d_vec, void* d_pk, int ld_dpk, void* d_pv, int ld_dpv, void* d_cut,
-    void* d_unit, void* edge_scratch, const int32_t* pk_rows, int flags, void* stream) {
+    void* d_unit, void* edge_scratch, const int32_t* pk_rows, const void* gg_pkv_scale, int flags, void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  const et::Bwd2Ex ex{ld_ggq, ld_ggk, ld_ggv, ld_dq, ld_dk, ld_dv, ld_dpk, ld_dpv, transpose, edge_scratch, pk_rows};
+  const et::Bwd2Ex ex{ld_ggq, ld_ggk, ld_ggv, ld_dq, ld_dk, ld_dv, ld_dpk, ld_dpv, transpose, edge_scratch, pk_rows,
+                      gg_pkv_scale};
 #define TMD_BWD2(T)                                                                              \
   return et::bwd2<T>(n_nodes, hidden, heads, row_ptr, src, max_pairs, q, ld_q, k, ld_k, v, ld_v, \
                      vec_in, pk, ld_pk, pv, ld_pv, cutoff, unit, grad_x, grad_vec, gg_q, gg_k,   \

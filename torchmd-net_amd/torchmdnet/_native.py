@@ -53,7 +53,7 @@ SIGNATURES = {
                                    P, P, P, P, P, I, P, I, P, P, P, P, P, P, P, P, P, P, P, P, I, P]),
     "tmdnet_et_message_bwd2_ex": (I, [I, I, I, I, P, P, P, I, P, I, P, I, P, I, P, P, I, P, I, P, P, P, P,
                                       P, I, P, I, P, I, P, P, I, P, I, P, P,
-                                      P, P, P, I, P, I, P, I, P, P, I, P, I, P, P, P, P, I, P]),
+                                      P, P, P, I, P, I, P, I, P, P, I, P, I, P, P, P, P, P, I, P]),
     "tmdnet_et_epilogue_fwd": (I, [I, I, I, P, P, P, P, P, P, P, P]),
     "tmdnet_et_epilogue_bwd": (I, [I, I, I, P, P, P, P, P, P, P]),
     "tmdnet_et_epilogue_bwd_acc": (I, [I, I, I, P, P, P, P, P, P, I, P]),

@@ -398,7 +398,6 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws, r=None, dr=Fa
     inj = inject or {}
     stk = inj.get("stk")  # the second order's layer-stacked injections (see below)
     acc = stk is not None
-    assert not (rec and dr), "recording needs the materialised projection gradient (no dr mode)"
 
     def injected(key, l):
         lst = inj.get(key)
@@ -414,8 +413,9 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws, r=None, dr=Fa
         g_r = zbuf[4 * E:]
         fdp = kernels.rbf_deriv(r, *meta.rbf, rows=meta.pairs[1] if meta.pairs is not None else None)
         dpkv_all = torch.mm(fdp, meta.dkv_eff[0].t()) if meta.batched else None
+    # dr mode recorded (the create_graph force pass): g_r in-kernel AND the projection gradient kept
     # padding rows of a static-capacity list are zeroed by the kernel: no memset needed
-    elif has_e:
+    if has_e and (not dr or rec):
         if acc and stk.get("pkv") is not None and (meta.batched or rec):
             g_pkv_all = stk["pkv"]  # [E, layers * D], accumulated into
         else:
@@ -470,7 +470,7 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws, r=None, dr=Fa
             dpkv = dpkv_all[:, l * D:(l + 1) * D] if meta.batched else torch.mm(fdp, dkv_w.t())
             dpk = dpkv[:, :H] if meta.hk else None
             dpv = dpkv[:, H * int(meta.hk):] if meta.hv else None
-        elif has_e:
+        if has_e and (not dr or rec):
             g_pkv = g_pkv_all[:, l * D:(l + 1) * D] if (meta.batched or rec) else g_pkv_all
             if acc and not (meta.batched or rec):  # per-layer buffer (row stride D): start from the injection
                 g_pkv.copy_(stk["pkv"][:, l * D:(l + 1) * D])
@@ -544,11 +544,10 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws, r=None, dr=Fa
     if any_w:
         _node_weight_grads(meta, g_params, need_ws, g_qkv_all, g_o_all, g_vecp_all, g_xn_all, ln_rows, adj)
     if rec:
-        record.append({"g_pkv": None, "stacks": (g_qkv_all, g_o_all, g_vecp_all)})
+        record.append({"g_pkv": g_pkv_all if has_e else None, "stacks": (g_qkv_all, g_o_all, g_vecp_all),
+                       "dpkv": dpkv_all if dr else None})
     if has_e and (meta.batched or rec) and not dr:  # every layer's edge-feature / projection gradients in one GEMM each
         g_f = torch.mm(g_pkv_all, meta.dkv_eff[0]) if want_f else None
-        if rec:
-            record[-1]["g_pkv"] = g_pkv_all
         if any(need_ws[:meta.n_layers]):
             if PROJ_WGRAD == "tn":  # weight + bias (+ the adjoint's g_pkv^T gb_f): one split-K TN launch
                 g_w_all, g_b_all = kernels._linear_wgrad(g_pkv_all, f, True, True,
@@ -820,6 +819,8 @@ def _second_order(ctx, ggs, want):
     rg_qkv_all, rg_o_all, rg_vecp_all = tail["stacks"]
     rec = rec[::-1]  # layer 0 first
     W_all = meta.dkv_eff[0]
+    if g_f0 is None and want[6] and has_e:  # (the recorded dr pass does not form g_f)
+        g_f0 = torch.mm(g_pkv_all, W_all)
     # cotangent of the summed edge-feature gradient g_f = g_pkv_all W_all
     gb_f = gg_f
     r_bar = None
@@ -833,7 +834,14 @@ def _second_order(ctx, ggs, want):
                 fd, = torch.autograd.grad(kernels.rbf_composite(rr, *meta.rbf), rr, g_f0.detach(),
                                           create_graph=True)
                 r_bar, = torch.autograd.grad(fd, rr, gg_r)
-    gb_pkv_all = torch.mm(gb_f, W_all.t()) if (gb_f is not None and has_e) else None
+    # the projection rows' cotangent gb_f W^T: with only the g_r term (gg_f None) it is gg_r[e] times the
+    # pair rows' d(dk,dv)/dr the recorded dr pass formed -- the message VJP scales those rows per edge
+    # (no E x layers*D product); otherwise one GEMM
+    dpkv_pairs = tail.get("dpkv") if (gg_f is None and ctx.dr and gg_r is not None and meta.pk_rows is not None) else None
+    gb_pkv_all = None
+    if dpkv_pairs is None and gb_f is not None and has_e:
+        gb_pkv_all = torch.mm(gb_f, W_all.t())
+    gr_scale = gg_r.contiguous() if dpkv_pairs is not None else None
     W_bar = {}
 
     def acc(key, val):
@@ -900,6 +908,8 @@ def _second_order(ctx, ggs, want):
             pk = pkv[:, :H] if meta.hk else None
             pv = pkv[:, H * int(meta.hk):] if meta.hv else None
         gbl = gb_pkv_all[:, l * D:(l + 1) * D] if gb_pkv_all is not None else None
+        if dpkv_pairs is not None:
+            gbl = dpkv_pairs[:, l * D:(l + 1) * D]
         ggs_m = (gb_gqkv[:, :H], gb_gqkv[:, H:2 * H], gb_gqkv[:, 2 * H:],
                  gbar_v if vec_l is not None else None,
                  gbl[:, :H] if (gbl is not None and meta.hk) else None,
@@ -912,7 +922,7 @@ def _second_order(ctx, ggs, want):
         d_gxa, d_gvec, d_q, d_k, d_v, d_vec, d_pk, d_pv, d_C, d_u = kernels.et_message_bwd2_launch(
             qkv[:, :H], qkv[:, H:2 * H], qkv[:, 2 * H:], vec_l, pk, pv, C, u, graph, meta.heads,
             R["g_xa"], R["gV"] if R["gV"] is not None else torch.zeros((N, 3, H), **o), ggs_m, out=outs,
-            pk_rows=meta.pk_rows if has_e else None)
+            pk_rows=meta.pk_rows if has_e else None, gg_pkv_scale=gr_scale)
         inj["qkv"][l] = outs["qkv"]
         if has_e:
             inj["pkv"][l] = outs["pkv"]
@@ -1108,13 +1118,11 @@ class _ETStackBwd(Function):
             raise RuntimeError("torchmd-net_amd: the ET backward source pass needs a symmetric edge "
                                "list (include_transpose=True, no capacity overflow)")
         ctx.rec = None
-        if record:  # dr-mode outputs from the recorded training form (see _ETStack.backward)
+        if record:  # dr mode, recorded: g_r in-kernel and the projection gradient kept (_ETStack.backward)
             rec = []
-            g_x, g_f0, g_C, g_u, _, g_params = _backward_layers(meta, gX, gV, f, C, u, params, acts, need_w,
-                                                                record=rec, want_f=True)
-            g_r = (g_f0 * kernels.rbf_deriv(r, *meta.rbf)).sum(1)  # (einsum lowers this to E tiny GEMMs)
-            g_f = None
-            ctx.rec, ctx.g_f0 = rec, g_f0
+            g_x, g_f, g_C, g_u, g_r, g_params = _backward_layers(meta, gX, gV, f, C, u, params, acts, need_w,
+                                                                 r=r, dr=True, record=rec, want_f=False)
+            ctx.rec, ctx.g_f0 = rec, None
         else:
             g_x, g_f, g_C, g_u, g_r, g_params = _backward_layers(meta, gX, gV, f, C, u, params, acts, need_w,
                                                                  r=r, dr=dr,

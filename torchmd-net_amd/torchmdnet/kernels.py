@@ -729,13 +729,14 @@ BWD2_SCRATCH_MAX_BYTES = 2 << 30
 
 
 def et_message_bwd2_launch(q, k, v, vec, pk, pv, C, u, graph, heads, gx, gvec, ggs, flags=0, out=None,
-                           pk_rows=None):
+                           pk_rows=None, gg_pkv_scale=None):
     """One ``tmdnet_et_message_bwd2_ex`` launch: the VJP of tmdnet_et_message_bwd (without the vec
     residual) at primals (q, k, v, vec, pk, pv, C, u) and seeds (gx, gvec), for the cotangents
     ``ggs`` = (gg_q, gg_k, gg_v, gg_vec, gg_pk, gg_pv, gg_C, gg_u) of its outputs (None / empty =
     zero; node cotangents may be column blocks of a wider buffer).  pk / pv are per-edge rows, or with
     ``pk_rows`` the pair-shared rows edge e reads at pk_rows[e] (their cotangents / gradients stay
-    per edge).  Returns (d_gx, d_gvec, d_q, d_k, d_v, d_vec, d_pk, d_pv, d_C, d_u); d_vec is None
+    per edge).  ``gg_pkv_scale`` [E] (with pk_rows): the edge cotangents gg_pk / gg_pv are PAIR rows,
+    edge e's being row pk_rows[e] scaled by gg_pkv_scale[e].  Returns (d_gx, d_gvec, d_q, d_k, d_v, d_vec, d_pk, d_pv, d_C, d_u); d_vec is None
     when vec is None, d_pk / d_pv when pk / pv are.
 
     ``out`` (optional dict) names caller buffers: "gx" [N, H] receives d_gx, "qkv" [N, 5H] d_q | d_k | d_v, "pkv" [E, D]
@@ -753,8 +754,14 @@ def et_message_bwd2_launch(q, k, v, vec, pk, pv, C, u, graph, heads, gx, gvec, g
 
     ggq, ggk, ggv = dense(ggs[0], (N, H)), dense(ggs[1], (N, H)), dense(ggs[2], (N, 3 * H))
     ggw = dense(ggs[3], (N, 3, H)).contiguous()
-    ggpk = dense(ggs[4], (E, H)) if pk is not None else None
-    ggpv = dense(ggs[5], (E, 3 * H)) if pv is not None else None
+    if gg_pkv_scale is not None:  # pair rows, read through pk_rows and scaled per edge
+        if pk_rows is None:
+            raise ValueError("gg_pkv_scale needs pk_rows")
+        ggpk = _rowmajor(ggs[4]) if pk is not None else None
+        ggpv = _rowmajor(ggs[5]) if pv is not None else None
+    else:
+        ggpk = dense(ggs[4], (E, H)) if pk is not None else None
+        ggpv = dense(ggs[5], (E, 3 * H)) if pv is not None else None
     ggC, ggu = dense(ggs[6], (E,)).contiguous(), dense(ggs[7], (E, 3)).contiguous()
     scratch = None
     if graph.transpose is not None and E * 7 * H * q.element_size() <= BWD2_SCRATCH_MAX_BYTES:
@@ -798,7 +805,7 @@ def et_message_bwd2_launch(q, k, v, vec, pk, pv, C, u, graph, heads, gx, gvec, g
         P(C), P(u), P(gxc), P(gvc), P(ggq), _ld(ggq), P(ggk), _ld(ggk), P(ggv), _ld(ggv), P(ggw),
         P(ggpk), _ld(ggpk), P(ggpv), _ld(ggpv), P(ggC), P(ggu), P(d_gx), P(d_gvec),
         P(d_q), _ld(d_q), P(d_k), _ld(d_k), P(d_v), _ld(d_v), P(d_vec), P(d_pk), _ld(d_pk), P(d_pv), _ld(d_pv),
-        P(d_C), P(d_u), P(scratch), P(pk_rows), int(flags), nat.stream(q.device))
+        P(d_C), P(d_u), P(scratch), P(pk_rows), P(gg_pkv_scale), int(flags), nat.stream(q.device))
     nat.check(rc, "tmdnet_et_message_bwd2_ex")
     return d_gx, d_gvec, d_q, d_k, d_v, d_vec, d_pk, d_pv, d_C, d_u
 
