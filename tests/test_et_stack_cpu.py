@@ -223,8 +223,12 @@ def _fake_bwd2_launch(q, k, v, vec, pk, pv, C, u, graph, heads, gx, gvec, ggs, f
     if "pkv" in out:
         out["pkv"].copy_(torch.cat([t for t in (d_pk, d_pv) if t is not None], 1))
     if "C" in out:
-        out["C"].add_(d_C)
-        out["u"].add_(d_u)
+        if out.get("edge_overwrite"):
+            out["C"].copy_(d_C)
+            out["u"].copy_(d_u)
+        else:
+            out["C"].add_(d_C)
+            out["u"].add_(d_u)
         d_C, d_u = out["C"], out["u"]
     if "gvec" in out:
         out["gvec"].add_(d_gvec)

@@ -863,8 +863,8 @@ def _second_order(ctx, ggs, want):
             inj["W"]["dkv"] = (g_pkv_all, gb_f)  # accumulated into pass 3's edge-feature weight GEMM
         else:
             acc("dkv", torch.mm(g_pkv_all.t(), gb_f))
-    C_bar = torch.zeros((E,), **o)
-    u_bar = torch.zeros((E, 3), **o)
+    C_bar = torch.empty((E,), **o)  # overwritten by layer 0's message VJP, accumulated by the others
+    u_bar = torch.empty((E, 3), **o)
     gbar_x = gg_x if gg_x is not None else torch.zeros((N, H), **o)
     gbar_v = None
     ggC = gg_C if gg_C is not None else torch.zeros((E,), **o)
@@ -916,7 +916,7 @@ def _second_order(ctx, ggs, want):
                  gbl[:, H * int(meta.hk):] if (gbl is not None and meta.hv) else None, ggC, ggu)
         # d_q | d_k | d_v and d_pk | d_pv written straight into the injection buffers, the cutoff /
         # unit-vector cotangents accumulated into C_bar / u_bar by the kernel
-        outs = {"qkv": inj["stk"]["qkv"][l], "C": C_bar, "u": u_bar, "gx": dgxa_all[l]}
+        outs = {"qkv": inj["stk"]["qkv"][l], "C": C_bar, "u": u_bar, "gx": dgxa_all[l], "edge_overwrite": l == 0}
         if has_e:
             outs["pkv"] = inj["stk"]["pkv"][:, l * D:(l + 1) * D]
         d_gxa, d_gvec, d_q, d_k, d_v, d_vec, d_pk, d_pv, d_C, d_u = kernels.et_message_bwd2_launch(
@@ -1100,6 +1100,11 @@ class _ETStack(Function):
             dr = False
         # the edge-feature gradient only when something consumes it (never in a parameter backward)
         want_f = f is not None and ctx.needs_input_grad[2] and _will_run(nf[1][0])
+        if pending is not None:  # does anything consume the cutoff / unit-vector gradients (2 adds)?
+            ti = [i for i, t in zip(range(2, 7), (f, C, u, r)) if t is not None]  # (x is always present)
+            idx = {i: 1 + j for j, i in enumerate(ti)}
+            pending["want_cu"] = any(ctx.needs_input_grad[i] and _will_run(nf[idx[i]][0]) for i in (3, 4)
+                                     if i in idx)
         # a force pass whose own backward will be taken (create_graph: force-matching training) records
         # its intermediates for the hand second order right here, instead of the second order re-running
         # it: the training form (projection gradient materialised) with g_r = <g_f, df/dr> per edge
@@ -1129,8 +1134,11 @@ class _ETStackBwd(Function):
                                                                  inject=pending["inj"] if pending else None,
                                                                  want_f=want_f)
         if pending is not None:  # the second order's contributions (et_stack._second_order)
-            g_C = g_C + pending["C_bar"]
-            g_u = g_u + pending["u_bar"]
+            if pending.get("want_cu", True):
+                g_C = g_C + pending["C_bar"]
+                g_u = g_u + pending["u_bar"]
+            else:  # nothing downstream consumes them (a training step's parameter backward)
+                g_C = g_u = None
             wl = list(need_w)
             g_params = _apply_w_bar(meta, list(g_params), pending["W_bar"], pending["on_bar"],
                                     lambda i: wl[min(i // meta.np, len(wl) - 1)] if i < meta.n_layers * meta.np

@@ -741,7 +741,8 @@ def et_message_bwd2_launch(q, k, v, vec, pk, pv, C, u, graph, heads, gx, gvec, g
 
     ``out`` (optional dict) names caller buffers: "gx" [N, H] receives d_gx, "qkv" [N, 5H] d_q | d_k | d_v, "pkv" [E, D]
     d_pk | d_pv, "C" / "u" are ACCUMULATED into (d_C / d_u returned as those buffers), "gvec" receives
-    d_gvec added to its contents.  With the graph's transpose map the source-node terms are summed by
+    d_gvec added to its contents ("edge_overwrite": True -- "C" / "u" are overwritten, padding rows
+    zeroed, instead).  With the graph's transpose map the source-node terms are summed by
     the deterministic source pass (per-edge scratch), otherwise by atomics into zeroed buffers."""
     lib = nat.load()
     out = out or {}
@@ -792,7 +793,8 @@ def et_message_bwd2_launch(q, k, v, vec, pk, pv, C, u, graph, heads, gx, gvec, g
         d_pv = torch.empty((E, 3 * H), **o) if pv is not None else None
     if "C" in out:
         d_C, d_u = out["C"], out["u"]
-        flags |= nat.BWD2_ACC_EDGE
+        if not out.get("edge_overwrite"):  # (the first launch into a buffer overwrites it: no zero fill)
+            flags |= nat.BWD2_ACC_EDGE
     else:
         d_C, d_u = torch.empty((E,), **o), torch.empty((E, 3), **o)
     qc, kc, vc, pkc, pvc = (_rowmajor(t) for t in (q, k, v, pk, pv))  # read in place through ld
