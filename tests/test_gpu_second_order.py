@@ -163,6 +163,48 @@ def test_neighbor_embedding_second_order_hand_matches_composite(monkeypatch):
         assert _rel(p_, q_) < 1e-11, (i, _rel(p_, q_))
 
 
+@pytest.mark.parametrize("use_cb", [False, True])
+def test_weight_gradient_tn_gemm_16byte_kernel(use_cb):
+    """The 64 x 64-tile, 16-byte-load TN kernel (every row 16-byte aligned): ragged M / N / K, long K
+    (split over the rows), two segments with the ones column on one of them, bias-only problems, beta,
+    and the bias written to its own vector (Cb) -- against fp64."""
+    from torchmdnet import kernels
+    torch.manual_seed(4)
+    shapes = [(678, 640, 128, True, 678), (2034, 384, 128, False, 2034), (678, 128, 0, True, 678),
+              (12548, 128, 64, True, 0), (5000, 96, 64, True, 1200), (37, 100, 36, False, 5),
+              (12548, 4096, 64, True, 12548), (3, 4, 8, True, 0)]
+    probs, refs = [], []
+    for K, M, Nb, ones, K2 in shapes:
+        A, B = torch.randn(K, M, device=DEV), (torch.randn(K, Nb, device=DEV) if Nb else None)
+        N = Nb + int(ones)
+        C = torch.randn(M, Nb if (use_cb and ones and Nb) else N, device=DEV)
+        Cb = torch.randn(M, device=DEV) if (use_cb and ones and Nb) else None
+        p = {"A": A, "B": B, "C": C, "ones": ones}
+        if Cb is not None:
+            p["Cb"] = Cb
+        Bx = B.double() if B is not None else torch.zeros((K, 0), dtype=torch.float64, device=DEV)
+        if ones:
+            Bx = torch.cat((Bx, torch.ones((K, 1), dtype=torch.float64, device=DEV)), 1)
+        ref = A.double().t() @ Bx
+        if K2 and Nb:
+            A2, B2 = torch.randn(K2, M, device=DEV), torch.randn(K2, Nb, device=DEV)
+            p.update(A2=A2, B2=B2)
+            B2x = B2.double()
+            if ones:
+                B2x = torch.cat((B2x, torch.zeros((K2, 1), dtype=torch.float64, device=DEV)), 1)
+            ref = ref + A2.double().t() @ B2x
+        beta = len(probs) % 2 == 1
+        if beta:
+            p["beta"] = True
+            ref = ref + (torch.cat((C, Cb[:, None]), 1) if Cb is not None else C).double()
+        probs.append(p)
+        refs.append(ref)
+    kernels.wgrad_tn(probs)
+    for p, ref in zip(probs, refs):
+        got = torch.cat((p["C"], p["Cb"][:, None]), 1) if p.get("Cb") is not None else p["C"]
+        assert _rel(got, ref) < 2e-5, (tuple(p["A"].shape), _rel(got, ref))
+
+
 def test_weight_gradient_tn_gemm_matches_library():
     """tmdnet_gemm_tn_f32 (grouped C (+)= A^T B + A2^T B2 over rows, ones column = bias) against
     torch fp64 on the shapes the training step uses (node weights over atoms, 3N vec rows, the head's

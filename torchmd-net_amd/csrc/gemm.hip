@@ -293,6 +293,182 @@ __global__ __launch_bounds__(256) void k_tn_reduce(GroupTN G, int tiles) {
   *out = v;
 }
 
+// ---------------------------------------------------------------------------------------------------
+// The same grouped TN GEMM with 64 x 64 tiles and 16-byte loads ("v" kernel; used when every operand
+// row is 16-byte aligned).  The MFMA's output-row / output-column labels are a free permutation: lane
+// (c, kq) of a 16x16x4 step feeds A[k0 + kq][m0 + 4c + mb] into block mb and B[k0 + kq][n0 + 4c + nb]
+// into block nb, so ONE float4 load of A and one of B per 4 rows feed 16 MFMAs (the scalar kernel
+// above: 4 loads per 4 MFMAs -- it is load-issue-bound on the node-weight shapes).  The ones column
+// is not a GEMM column here: the bias is the row sum of A, accumulated from the same A registers by
+// the first column tile.
+constexpr int TV = 64;
+constexpr int TV_PART = TV * TV + TV;  // partial tile + bias partials (split-K)
+
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void k_gemm_tn_v(GroupTN G) {
+  __shared__ float red[NW][TV][TV + 1];
+  __shared__ float redb[NW][TV];
+  const int tg = blockIdx.x / G.S, sk = blockIdx.x % G.S;
+  int pi = 0;
+  for (int i = 1; i < G.n; ++i)
+    if (tg >= G.p[i].tile0) pi = i;
+  const ProbTN& P = G.p[pi];
+  const int t = tg - P.tile0;
+  const int w = threadIdx.x / TMD_WAVE, lane = lane_id();
+  const int c = lane & 15, kq = lane >> 4;
+  const int m0 = (t / P.tiles_n) * TV, n0 = (t % P.tiles_n) * TV;
+  const bool anyones = P.ones1 || P.ones2;
+  const int Nr = anyones ? P.N - 1 : P.N;  // columns of B that are read (the ones column is the row sum)
+  const bool do_bias = anyones && (t % P.tiles_n) == 0;
+  const int KT = P.K + P.K2;
+  const int nkt = (KT + 15) / 16, cper = (nkt + G.S - 1) / G.S;
+  const int c_lo = min(KT, sk * cper * 16), c_hi = min(KT, (sk + 1) * cper * 16);
+  const int nkb = (c_hi - c_lo + 15) / 16, per = (nkb + NW - 1) / NW;
+  const int k_lo = min(c_hi, c_lo + w * per * 16), k_hi = min(c_hi, c_lo + (w + 1) * per * 16);
+  f4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  f4 rs = f4{0.f, 0.f, 0.f, 0.f};
+  const int ma = m0 + 4 * c, na = n0 + 4 * c;
+  const bool mfull = ma + 3 < P.M, nfull = na + 3 < Nr;
+  const bool gemm = n0 < Nr;  // a bias-only tile (B = ones only) skips the MFMAs
+  for (int seg = 0; seg < 2; ++seg) {
+    const int s0 = seg ? P.K : 0, s1 = seg ? KT : P.K;
+    const int lo = max(k_lo, s0), hi = min(k_hi, s1);
+    if (lo >= hi) continue;
+    const float* A = seg ? P.A2 : P.A;
+    const float* B = seg ? P.B2 : P.B;
+    const int lda = seg ? P.lda2 : P.lda, ldb = seg ? P.ldb2 : P.ldb;
+    const bool bias_seg = do_bias && (seg ? P.ones2 : P.ones1);
+    const int64_t* zi = P.onehot ? reinterpret_cast<const int64_t*>(A) : nullptr;
+    for (int kb = lo; kb < hi; kb += 16) {  // four 4-row MFMA steps, all loads first
+      f4 a[4], b[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int k = kb + 4 * u + kq;
+        const bool kv = k < hi;
+        const size_t ro = (size_t)(kv ? k - s0 : 0);
+        if (zi) {
+          const int64_t zk = kv ? zi[ro] : -1;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) a[u][i] = (zk == ma + i && ma + i < P.M) ? 1.f : 0.f;
+        } else if (kv && mfull) {
+          a[u] = *reinterpret_cast<const f4*>(A + ro * lda + ma);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) a[u][i] = (kv && ma + i < P.M) ? A[ro * lda + ma + i] : 0.f;
+        }
+        if (!gemm || !B) {
+          b[u] = f4{0.f, 0.f, 0.f, 0.f};
+        } else if (kv && nfull) {
+          b[u] = *reinterpret_cast<const f4*>(B + ro * ldb + na);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) b[u][i] = (kv && na + i < Nr) ? B[ro * ldb + na + i] : 0.f;
+        }
+      }
+      if (bias_seg) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) rs += a[u];
+      }
+      if (gemm) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+            for (int nb = 0; nb < 4; ++nb)
+              acc[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][mb], b[u][nb], acc[mb][nb], 0, 0, 0);
+      }
+    }
+  }
+  // C layout of a 16x16 block: lane holds rows 4 (lane >> 4) + i, column lane & 15 (MFMA labels)
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) red[w][4 * (4 * kq + i) + mb][4 * c + nb] = acc[mb][nb][i];
+  if (do_bias) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float v = rs[i];
+      v += __shfl_xor(v, 16);
+      v += __shfl_xor(v, 32);
+      rs[i] = v;
+    }
+    if (kq == 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) redb[w][4 * c + i] = rs[i];
+    }
+  }
+  __syncthreads();
+  float* part = G.S > 1 ? G.part + ((size_t)tg * G.S + sk) * TV_PART : nullptr;
+  for (int e = threadIdx.x; e < TV * TV; e += blockDim.x) {
+    const int r = e >> 6, cc = e & 63;
+    float v = 0.f;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) v += red[i][r][cc];
+    if (part) {
+      part[e] = v;
+      continue;
+    }
+    const int m = m0 + r, n = n0 + cc;
+    if (m >= P.M || n >= Nr) continue;
+    float* out = P.C + (size_t)m * P.ldc + n;
+    if (P.beta) v += *out;
+    *out = v;
+  }
+  if (do_bias) {
+    for (int r = threadIdx.x; r < TV; r += blockDim.x) {
+      float v = 0.f;
+#pragma unroll
+      for (int i = 0; i < NW; ++i) v += redb[i][r];
+      if (part) {
+        part[TV * TV + r] = v;
+        continue;
+      }
+      const int m = m0 + r;
+      if (m >= P.M) continue;
+      float* out = P.Cb ? P.Cb + m : P.C + (size_t)m * P.ldc + (P.N - 1);
+      if (P.beta) v += *out;
+      *out = v;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_tn_reduce_v(GroupTN G, int tiles) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= tiles * TV_PART) return;
+  const int tg = i / TV_PART, e = i - tg * TV_PART;
+  int pi = 0;
+  for (int j = 1; j < G.n; ++j)
+    if (tg >= G.p[j].tile0) pi = j;
+  const ProbTN& P = G.p[pi];
+  const int t = tg - P.tile0;
+  const int m0 = (t / P.tiles_n) * TV, n0 = (t % P.tiles_n) * TV;
+  const bool anyones = P.ones1 || P.ones2;
+  const int Nr = anyones ? P.N - 1 : P.N;
+  float* out;
+  if (e < TV * TV) {
+    const int m = m0 + (e >> 6), n = n0 + (e & 63);
+    if (m >= P.M || n >= Nr) return;
+    out = P.C + (size_t)m * P.ldc + n;
+  } else {
+    const int m = m0 + (e - TV * TV);
+    if (!anyones || (t % P.tiles_n) != 0 || m >= P.M) return;
+    out = P.Cb ? P.Cb + m : P.C + (size_t)m * P.ldc + (P.N - 1);
+  }
+  const float* src = G.part + (size_t)tg * G.S * TV_PART + e;
+  float v = 0.f;
+#pragma unroll 8
+  for (int s = 0; s < G.S; ++s) v += src[(size_t)s * TV_PART];
+  if (P.beta) v += *out;
+  *out = v;
+}
+
 }  // namespace gemm
 }  // namespace tmd
 
@@ -345,13 +521,50 @@ extern "C" int tmdnet_gemm_f32(int n_problems, const int* dims, const void* cons
 
 // split-K factor: few tiles over many rows (e.g. a 128 x 64 weight over 12.5k edges is 8 tiles)
 // leave most CUs idle; S 4-wave workgroups per tile (~1024 workgroups in all), each wave >= 64 rows
-static int tn_split(int tiles, int kmax) {
-  int S = (1024 + tiles - 1) / tiles;
+static int tn_split(int tiles, int kmax, int target = 1024) {
+  int S = (target + tiles - 1) / tiles;
   S = min(S, max(1, kmax / (4 * 64)));
   return max(1, min(S, 64));
 }
 
+// the 16-byte-load kernel needs every A / B row 16-byte aligned (one-hot A: any)
+static bool tn_vec_ok(const gemm::GroupTN& G) {
+  static const bool off = getenv("TMDNET_TN_SCALAR") != nullptr;  // A/B switch
+  if (off) return false;
+  auto al = [](const void* p, int ld) { return !p || ((((uintptr_t)p) & 15) == 0 && ld % 4 == 0); };
+  for (int i = 0; i < G.n; ++i) {
+    const gemm::ProbTN& P = G.p[i];
+    if (!(P.onehot || al(P.A, P.lda)) || !al(P.B, P.ldb)) return false;
+    if (P.K2 > 0 && (!al(P.A2, P.lda2) || !al(P.B2, P.ldb2))) return false;
+  }
+  return true;
+}
+
+// (re)number the tiles for tile edge T; returns the tile count
+static int tn_tiles(gemm::GroupTN& G, int T) {
+  int tiles = 0;
+  for (int i = 0; i < G.n; ++i) {
+    gemm::ProbTN& P = G.p[i];
+    const int nr = (T == gemm::TV && (P.ones1 || P.ones2)) ? P.N - 1 : P.N;
+    P.tiles_n = max(1, (nr + T - 1) / T);
+    P.tile0 = tiles;
+    tiles += ((P.M + T - 1) / T) * P.tiles_n;
+  }
+  return tiles;
+}
+
 static void launch_tn(gemm::GroupTN& G, int tiles, int kmax, float* ws, hipStream_t st) {
+  if (tn_vec_ok(G)) {
+    const int tv = tn_tiles(G, gemm::TV);
+    G.S = ws ? tn_split(tv, kmax) : 1;  // (512 workgroups measured slower than 1024: 259 vs 227 us per step)
+    G.part = ws;
+    if (kmax >= 8192 && G.S == 1) hipLaunchKernelGGL(gemm::k_gemm_tn_v<8>, dim3(tv), dim3(512), 0, st, G);
+    else hipLaunchKernelGGL(gemm::k_gemm_tn_v<4>, dim3(tv * G.S), dim3(256), 0, st, G);
+    if (G.S > 1)
+      hipLaunchKernelGGL(gemm::k_tn_reduce_v, dim3((tv * gemm::TV_PART + 255) / 256), dim3(256), 0, st, G, tv);
+    return;
+  }
+  tiles = tn_tiles(G, 32);
   G.S = ws ? tn_split(tiles, kmax) : 1;
   G.part = ws;
   // unsplit: K over 16 waves from 8192 rows (edge sums), 4 below (atom sums: a wave's slice stays long
@@ -424,7 +637,7 @@ static int gemm_tn(int n_problems, const int* dims, const void* const* ptrs, int
   const int rc = tn_group(n_problems, dims, ptrs, np, G, tiles, kmax);
   if (rc != kOk) return rc;
   float* ws = (float*)workspace;
-  if (ws && workspace_bytes < sizeof(float) * 1024 * (size_t)tiles * tn_split(tiles, kmax)) return kWorkspaceTooSmall;
+  if (ws && workspace_bytes < tmdnet_gemm_tn_workspace_bytes(n_problems, dims)) return kWorkspaceTooSmall;
   launch_tn(G, tiles, kmax, ws, (hipStream_t)stream);
   return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
 }
@@ -441,8 +654,16 @@ extern "C" size_t tmdnet_gemm_tn_workspace_bytes(int n_problems, const int* dims
     tiles += ((d[0] + 31) / 32) * ((d[1] + 31) / 32);
     kmax = max(kmax, d[2] + d[3]);
   }
-  const int S = tn_split(tiles, kmax);
-  return S > 1 ? sizeof(float) * 1024 * (size_t)tiles * S : 0;
+  int tv = 0;  // the 64-tile kernel's tiling (bias rides in the first column tile)
+  for (int i = 0; i < n_problems; ++i) {
+    const int* d = dims + 12 * i;
+    const int nr = (d[10] || d[11]) ? d[1] - 1 : d[1];
+    tv += ((d[0] + gemm::TV - 1) / gemm::TV) * max(1, (nr + gemm::TV - 1) / gemm::TV);
+  }
+  const int S = tn_split(tiles, kmax), Sv = tn_split(tv, kmax);
+  const size_t b32 = S > 1 ? sizeof(float) * 1024 * (size_t)tiles * S : 0;
+  const size_t bv = Sv > 1 ? sizeof(float) * gemm::TV_PART * (size_t)tv * Sv : 0;
+  return max(b32, bv);
 }
 
 extern "C" int tmdnet_gemm_tn_f32_ws(int n_problems, const int* dims, const void* const* ptrs, void* workspace,
