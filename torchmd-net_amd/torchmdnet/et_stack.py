@@ -140,8 +140,9 @@ RECORD_IN_FORCE_PASS = os.environ.get("TMDNET_ET_RECORD", "1") not in ("0", "off
 # and an energy+force evaluation must keep the cheaper dr-mode force pass
 _EXPECT_SECOND_ORDER = [False]
 # the projection's weight gradient over the edge rows (K = E, a 4096 x 64 output: FLOP-bound on the
-# fp32 MFMA): "lib" = library GEMMs + a column sum, "tn" = one split-K TN launch
-PROJ_WGRAD = os.environ.get("TMDNET_PROJ_WGRAD", "lib")
+# fp32 MFMA): "tn" = one split-K launch of the 16-byte-load TN kernel, bias included (ET-QM9 step:
+# 215 us; the scalar TN kernel took 500), "lib" = library GEMMs + a column sum (243 + 54 us)
+PROJ_WGRAD = os.environ.get("TMDNET_PROJ_WGRAD", "tn")
 # the node weights' gradients (per layer [q|k|v], o_proj, vec_proj, LayerNorm, over the atoms): "tn" =
 # grouped split-K TN GEMMs with the bias columns, "bmm" = batched library GEMMs + reductions
 NODE_WGRAD = os.environ.get("TMDNET_NODE_WGRAD", "tn")
