@@ -955,18 +955,19 @@ __global__ __launch_bounds__(S > 4 ? 64 * S : 256) void k_bwd2(Args2<T> B) {
 }
 
 // Source pass of the second order: node j's k / v / vec terms are the sum of the scratch rows of the
-// edges leaving j, i.e. the reverses tr[e'] of the edges e' of row j.  One wave per node, 4 columns
-// per lane, the row's edges unrolled by 4 so their loads are in flight together.  A capacity-truncated
+// edges leaving j, i.e. the reverses tr[e'] of the edges e' of row j.  One 256-thread block per node,
+// 4 columns per thread (7H / 4 = 224 threads at H = 128: every column group in one pass), the row's
+// edges unrolled by 4 so their loads are in flight together (one wave per node covering the columns in
+// 3.5 passes left the chip at ~3 waves per CU: 26 us per ET-QM9 layer).  A capacity-truncated
 // list (a step the capacity check discards) leaves tr[e] = -1 where the reverse was cut off: no term.
 template <typename T>
 __global__ __launch_bounds__(256) void k_bwd2_src(Args2<T> B) {
   using V4 = T __attribute__((ext_vector_type(4)));
   const Args<T>& A = B.a;
-  const int j = blockIdx.x * (blockDim.x / TMD_WAVE) + threadIdx.x / TMD_WAVE;
+  const int j = blockIdx.x;
   if (j >= A.n) return;
-  const int lane = lane_id();
   const int W = 7 * A.H, b = min(A.row_ptr[j], A.cap), e = min(A.row_ptr[j + 1], A.cap);
-  for (int c = 4 * lane; c < W; c += 4 * TMD_WAVE) {
+  for (int c = 4 * threadIdx.x; c < W; c += 4 * blockDim.x) {
     V4 acc = {T(0), T(0), T(0), T(0)};
     int i = b;
     for (; i + 4 <= e; i += 4) {
@@ -1501,10 +1502,7 @@ static int bwd2(int n, int H, int heads, const int32_t* row_ptr, const int32_t* 
   else { if (S == 4) TMD_L2(4, 4); else if (S == 2) TMD_L2(4, 2); else TMD_L2(4, 1); }
 #undef TMD_L2
   if (hipGetLastError() != hipSuccess) return kLaunchFailed;
-  if (B.o_src) {
-    const int wpb = 256 / TMD_WAVE;
-    hipLaunchKernelGGL(k_bwd2_src<T>, dim3((n + wpb - 1) / wpb), dim3(256), 0, st, B);
-  }
+  if (B.o_src) hipLaunchKernelGGL(k_bwd2_src<T>, dim3(n), dim3(256), 0, st, B);
   return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
 }
 
