@@ -1023,8 +1023,9 @@ template <typename T> struct NbArgs {
 // are in flight together (one edge at a time left these kernels latency-bound).
 constexpr int NB_U = 4;
 
+// (sub, nsub): this wave takes every nsub-th group of NB_U edges of the row (waves sharing a node)
 template <typename T, typename F>
-__device__ __forceinline__ void nb_edges(const NbArgs<T>& A, int row, F&& body) {
+__device__ __forceinline__ void nb_edges(const NbArgs<T>& A, int row, F&& body, int sub = 0, int nsub = 1) {
   const int lane = lane_id();
   const int b = min(A.row_ptr[row], A.cap), e = min(A.row_ptr[row + 1], A.cap);
   for (int base = b; base < e; base += TMD_WAVE) {
@@ -1032,7 +1033,7 @@ __device__ __forceinline__ void nb_edges(const NbArgs<T>& A, int row, F&& body) 
     const int s_l = lane < cnt ? A.src[base + lane] : -1;
     TMD_DCHECK(lane >= cnt || (s_l >= 0 && s_l < A.n));
     const T c_l = lane < cnt ? A.C[base + lane] : T(0);
-    for (int q = 0; q < cnt; q += NB_U) {
+    for (int q = sub * NB_U; q < cnt; q += NB_U * nsub) {
       int sq[NB_U];
       T cq[NB_U];
 #pragma unroll
@@ -1091,7 +1092,9 @@ __global__ __launch_bounds__(256) void k_nb_bwd_dst(NbArgs<T> A) {
     for (long long i = tid; i < rows * A.H; i += nth) A.gw[(size_t)e0 * A.H + i] = T(0);
     for (long long i = tid; i < rows; i += nth) A.gC[e0 + i] = T(0);
   }
-  const int t = blockIdx.x * (blockDim.x / TMD_WAVE) + threadIdx.x / TMD_WAVE;
+  // four waves per node, each a quarter of the row's edges (the outputs are per edge: no reduction;
+  // one wave per node left a QM9 batch at ~3 waves per CU)
+  const int t = blockIdx.x, sub = threadIdx.x / TMD_WAVE, nsub = blockDim.x / TMD_WAVE;
   if (t >= A.n) return;
   const int lane = lane_id();
   const bool on = lane < A.L;
@@ -1130,7 +1133,7 @@ __global__ __launch_bounds__(256) void k_nb_bwd_dst(NbArgs<T> A) {
       for (int u = 0; u < NB_U; ++u)
         if (sq[u] >= 0) A.gC[k0 + u] = gc[u];
     }
-  });
+  }, sub, nsub);
 }
 
 // source pass: gx[j] = sum_{reverse edges j->m} gout[m] * w[e] * C[e]
@@ -1642,7 +1645,12 @@ static int nb_bwd_t(int n, int H, const int32_t* row_ptr, const int32_t* src, in
   if (A.ldg < H || !et::aligned<T>(gout, A.ldg, V)) return kBadArgument;
   A.gx = (T*)gx; A.gw = (T*)gw; A.gC = (T*)gC;
   if (!gw || !gC) return kBadArgument;
-  rc = et::launch_v<T, et::KNbDst>(V, n, A, st);
+  if (n > 0) {  // one 4-wave block per node (k_nb_bwd_dst)
+    if (V == 1) hipLaunchKernelGGL((et::k_nb_bwd_dst<T, 1>), dim3(n), dim3(256), 0, st, A);
+    else if (V == 2) hipLaunchKernelGGL((et::k_nb_bwd_dst<T, 2>), dim3(n), dim3(256), 0, st, A);
+    else hipLaunchKernelGGL((et::k_nb_bwd_dst<T, 4>), dim3(n), dim3(256), 0, st, A);
+    rc = hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
+  }
   if (rc) return rc;
   return gx ? et::launch_v<T, et::KNbSrc>(V, n, A, st) : kOk;  // gx NULL: the source pass is skipped
 }
