@@ -25,7 +25,7 @@ step = LNNPStep(model, lr=1e-4)
 for _ in range(3):
     step.step(z, pos, batch, y, f)
 torch.cuda.synchronize()
-with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
     step.step(z, pos, batch, y, f)
     torch.cuda.synchronize()
 ev = prof.key_averages()
@@ -41,3 +41,15 @@ for t, c, k in sorted(rows, reverse=True)[:40]:
 print()
 print(ev.table(sort_by="self_cuda_time_total" if hasattr(ev[0], "self_cuda_time_total") else "self_device_time_total",
                row_limit=40, max_name_column_width=90))
+print()
+# the GEMM / reduction ops with their input shapes (which call site is the expensive one)
+gs = prof.key_averages(group_by_input_shape=True)
+rows = []
+for e in gs:
+    if e.key in ("aten::mm", "aten::addmm", "aten::bmm", "aten::baddbmm", "aten::addmm_", "aten::sum", "aten::mul",
+                 "aten::add", "aten::add_", "aten::index_select", "aten::index_add_", "aten::embedding_backward",
+                 "aten::embedding_dense_backward", "aten::fill_", "aten::copy_", "aten::cat", "aten::zeros"):
+        t = getattr(e, "device_time_total", None) or getattr(e, "cuda_time_total", 0)
+        rows.append((t, e.count, e.key, str(e.input_shapes)[:150]))
+for t, c, k, sh in sorted(rows, reverse=True)[:45]:
+    print(f"{t / 1000:9.3f} ms {c:4d}  {k:24s} {sh}")
