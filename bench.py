@@ -39,6 +39,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 MFMA_F32_PEAK_TFS = 157.3  # MI355X dense fp32 MFMA (v_mfma_f32_16x16x4_f32) spec, MI355X_MICROARCH.md
+MFMA_BF16_PEAK_TFS = 2500.0  # MI355X dense bf16 MFMA, MI355X_MICROARCH.md (no sparsity)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 
 
@@ -428,35 +429,57 @@ def mfma_probe(E_c5, N_c5, E_c2, N_c2, H, R, dev):
     against gfx950 peak'): the dk/dv projection Linear_{R->4H} (the largest FLOP term, SURVEY.md 8(a)
     a13) as the model issues it -- over the (E + N) / 2 edge PAIRS (both directions share a row,
     et_stack.PAIR_ROWS), per layer at C5 scale, all 8 layers stacked into one GEMM at C2 -- fp32
-    in/out (hipBLASLt on v_mfma_f32_16x16x4_f32), HIP-event timed."""
+    in/out, HIP-event timed: the library fp32 GEMM (hipBLASLt on v_mfma_f32_16x16x4_f32) and the
+    model's tmdnet_proj_f32 (bf16 MFMA on an exact three-piece split, fp32 accuracy: both arms' max
+    error against fp64 is reported)."""
+    from torchmdnet import kernels
     res = {}
     for tag, E, cols in (("c5_per_layer", (E_c5 + N_c5) // 2, 4 * H),
                          ("c2_stacked_8_layers", (E_c2 + N_c2) // 2, 8 * 4 * H)):
         gen = torch.Generator(device=dev).manual_seed(5)
-        f = torch.randn(E, R, device=dev, generator=gen)
-        w = torch.randn(cols, R, device=dev, generator=gen)
+        f = torch.rand(E, R, device=dev, generator=gen)  # RBF values lie in [0, 1]
+        w = torch.randn(cols, R, device=dev, generator=gen) / R ** 0.5
         b = torch.randn(cols, device=dev, generator=gen)
         out = torch.empty(E, cols, device=dev)
-        for _ in range(3):
-            torch.addmm(b, f, w.t(), out=out)
-        torch.cuda.synchronize()
-        reps = 10 if E > 100000 else 50
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(reps):
-            torch.addmm(b, f, w.t(), out=out)
-        e1.record()
-        torch.cuda.synchronize()
-        ms = e0.elapsed_time(e1) / reps
-        tf = 2.0 * E * R * cols / (ms * 1e-3) / 1e12
-        res[tag] = {"gemm": f"[{E} x {R}] @ [{R} x {cols}] + bias, fp32", "ms_per_launch": round(ms, 4),
-                    "achieved": round(tf, 2), "frac": round(tf / MFMA_F32_PEAK_TFS, 4),
-                    "output_bytes": E * cols * 4,
-                    "output_write_bound_ms": round(E * cols * 4 / (HBM_PEAK_GBS * 1e9) * 1e3, 4)}
-        del f, w, b, out
+        row = {"gemm": f"[{E} x {R}] @ [{R} x {cols}] + bias, fp32 in/out", "output_bytes": E * cols * 4,
+               "output_write_bound_ms": round(E * cols * 4 / (HBM_PEAK_GBS * 1e9) * 1e3, 4)}
+        ref = None
+        if E < 100000:  # fp64 reference for the accuracy of both arms
+            ref = torch.addmm(b.double(), f.double(), w.double().t())
+        wp = kernels.proj_split(w)  # once per forward in the model, shared by the projection GEMMs
+        for arm, fn in (("library_fp32", lambda: torch.addmm(b, f, w.t(), out=out)),
+                        ("bf16x6_split", lambda: kernels.proj(f, w, b, out=out, wp=wp)),
+                        ("weight_split", lambda: kernels.proj_split(w))):
+            for _ in range(3):
+                fn()
+            torch.cuda.synchronize()
+            reps = 10 if E > 100000 else 50
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(reps):
+                fn()
+            e1.record()
+            torch.cuda.synchronize()
+            ms = e0.elapsed_time(e1) / reps
+            tf = 2.0 * E * R * cols / (ms * 1e-3) / 1e12
+            r = {"ms_per_launch": round(ms, 4), "achieved": round(tf, 2), "frac": round(tf / MFMA_F32_PEAK_TFS, 4),
+                 "write_gbs": round(E * cols * 4 / (ms * 1e-3) / 1e9, 1)}
+            if arm == "weight_split":
+                row[arm] = {"ms_per_launch": round(ms, 4)}
+                continue
+            if arm == "bf16x6_split":  # six bf16 MFMA products per fp32 product
+                r["bf16_mfma_tfs"] = round(6 * tf, 1)
+                r["bf16_mfma_frac"] = round(6 * tf / MFMA_BF16_PEAK_TFS, 4)
+            if ref is not None:
+                r["max_abs_err_vs_fp64"] = float((out.double() - ref).abs().max())
+            row[arm] = r
+        # headline fields = the arm the model runs (kernels.PROJ)
+        row.update({k: row["bf16x6_split" if kernels.PROJ == "x3" else "library_fp32"][k]
+                    for k in ("ms_per_launch", "achieved", "frac")})
+        res[tag] = row
+        del f, w, b, out, ref, wp
     # the hand-written grouped node-mix GEMM (tmdnet_gemm_f32, csrc/gemm.hip) at the C2 metric batch:
     # forward [q|k|v] + vec_proj in one launch, backward [q|k|v]^T + vec_proj^T (K split over 16 waves)
-    from torchmdnet import kernels
     Hh, Na = H, N_c2
     gen = torch.Generator(device=dev).manual_seed(6)
     rn = lambda *sh: torch.randn(*sh, device=dev, generator=gen)  # noqa: E731
@@ -485,7 +508,8 @@ def mfma_probe(E_c5, N_c5, E_c2, N_c2, H, R, dev):
     res["node_mix_c2"] = {"kernel": "tmdnet_gemm_f32 (grouped split-K fp32 MFMA, csrc/gemm.hip)",
                           "shape": f"N={Na} atoms, H={Hh}: [N x H][H x 5H] + [3N x H][H x 3H] per launch", **node}
     return {"kernel": "dk/dv projection GEMM (SURVEY 8(a) a13)", "bound": "mfma", "unit": "TFLOP/s",
-            "peak": MFMA_F32_PEAK_TFS, "dtype": "fp32 (the reference computes in fp32; gfx950 has no xf32)",
+            "peak": MFMA_F32_PEAK_TFS,
+            "dtype": "fp32 in/out (the reference computes in fp32); tmdnet_proj_f32 forms it from exact bf16 pieces",
             **res}
 
 

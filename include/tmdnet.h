@@ -497,6 +497,21 @@ int tmdnet_gemm_tn_f32_ws(int n_problems, const int* dims, const void* const* pt
 int tmdnet_embedding_bwd_f32(int n, int H, int num_types, const int64_t* z, int n_tables,
                              const void* const* grads, const int* ld_grads, void* const* outs, int accumulate,
                              void* stream);
+/* The ET dk/dv projection of the pair rows (reference torchmd_et.py:282-291, dk_proj / dv_proj of every
+ * layer stacked along N; also its r-derivative and the force-loss adjoint), in two entry points:
+ *   tmdnet_proj_split_f32: Wp [3][N][K] (uint16 bf16 bit patterns, 8-byte aligned) = the exact
+ *     three-piece bf16 split of W [N][K] (ldw): W = Wp[0] + Wp[1] + Wp[2] elementwise, exactly;
+ *   tmdnet_proj_f32: C[M][N] = A[M][K] W[N][K]^T + bias[N] (bias nullable), fp32 in and out, W given
+ *     by its split (pieces piece_stride elements apart, so a row slice [r0, r0 + N) of a larger split
+ *     is Wp + r0 * K with the larger split's stride).
+ * Runs on the bf16 MFMA: A is split the same way in registers and the six products of pieces whose
+ * orders sum to <= 2 are accumulated in fp32 -- fp32 GEMM accuracy (not a bf16 result).  Requirements:
+ * K = 32 or 64 (split: K % 4 == 0), N % 16 == 0, lda / ldc multiples of 4, 16-byte aligned A / Wp / C /
+ * bias; else TMDNET_UNSUPPORTED (callers use the library GEMM).  Replaces the nn.Linear of
+ * torchmd_et.py:287-288 over the edges. */
+int tmdnet_proj_split_f32(int N, int K, const void* W, int ldw, void* Wp, void* stream);
+int tmdnet_proj_f32(int M, int N, int K, const void* A, int lda, const void* Wp, long long piece_stride,
+                    const void* bias, void* C, int ldc, void* stream);
 
 /* Energy + force MSE training loss (reference LNNP.step, module.py:130-179, mean reductions):
  *   out[0] = w1 * mean((a1 - b1)^2) + w2 * mean((a2 - b2)^2)   over n1 / n2 elements (one launch),

@@ -1412,6 +1412,12 @@ static int bwd(int n, int H, int heads, const int32_t* row_ptr, const int32_t* s
   A.gpk = (T*)gpk; A.gpv = (T*)gpv; A.gC = (T*)gC; A.gu = (T*)gu;
   A.dpk = (const T*)dpk; A.dpv = (const T*)dpv; A.gr = (T*)gr;
   A.acc = acc;
+  static const int bwd_v = getenv("TMDNET_ET_BWD_V") ? atoi(getenv("TMDNET_ET_BWD_V")) : 0;  // tuning
+  if (bwd_v && bwd_v < V && H % (32 * bwd_v) == 0 && H / bwd_v <= 64 && (A.d / bwd_v) > 0 &&
+      A.d % bwd_v == 0 && !((A.d / bwd_v) & (A.d / bwd_v - 1))) {
+    V = bwd_v;
+    A.lph = A.d / V;
+  }
   if (acc & TMDNET_ET_V_PLANAR) { A.planar = 1; A.vst = H; }
   const bool dr = gr != nullptr;
   if (dr && ((A.pk && !dpk) || (A.pv && !dpv))) return kBadArgument;

@@ -104,7 +104,10 @@ __device__ __forceinline__ void store(const Prob& P, int gr, int gc, float v) {
   *out = v;
 }
 
-template <int NW>  // waves per 32 x 32 tile, K split NW ways
+// NW waves per 32 x 32 tile, K split NW ways; KMAX = the load batch (K blocks) the launch's longest
+// per-wave slice needs: the register file is sized for the largest batch the kernel can issue, so a
+// K = 128 mix (2 blocks per wave) compiled with an 8-block batch ran at 160 VGPRs = 2 waves per SIMD
+template <int NW, int KMAX>
 __global__ __launch_bounds__(NW * 64) void k_gemm(Group G) {
   __shared__ float part[NW][32][33];
   int pi = 0;
@@ -124,7 +127,7 @@ __global__ __launch_bounds__(NW * 64) void k_gemm(Group G) {
   const int r0 = (t / P.tiles_n) * 32, c0 = (t % P.tiles_n) * 32;
   const int per = (nkb + NW - 1) / NW;  // blocks per wave
   const int kb0 = w * per;
-  slice<(NW >= 16 ? 4 : 8)>(P, r0, c0, kb0, max(0, min(per, nkb - kb0)), acc);
+  slice<KMAX>(P, r0, c0, kb0, max(0, min(per, nkb - kb0)), acc);
 #pragma unroll
   for (int bi = 0; bi < 2; ++bi)
 #pragma unroll
@@ -470,6 +473,153 @@ __global__ __launch_bounds__(256) void k_tn_reduce_v(GroupTN G, int tiles) {
 }
 
 }  // namespace gemm
+
+// ---------------------------------------------------------------------------------------------------
+// The ET dk/dv projection  C [M][N] = A [M][K] W[N][K]^T (+ bias)  with K = num_rbf = 32 or 64 (the
+// pair rows' RBF times every layer's stacked dk/dv weight, reference torchmd_et.py:282-291; also its
+// r-derivative and, in the force-loss second order, the adjoint gb_f W^T).  The f32-input MFMA
+// (v_mfma_f32_16x16x4_f32) delivers 1/16 of the bf16 rate, so this runs on the bf16 MFMA with fp32
+// accuracy: every operand is split EXACTLY into three bf16 pieces x = x0 + x1 + x2 (truncation: each
+// piece takes the next 8 significant bits, x - x0 and x - x0 - x1 are exact in fp32), and the six
+// products x_i y_j with i + j <= 2 -- each exact in the fp32 accumulator -- are summed, small terms
+// first.  The dropped x1 y2 + x2 y1 + x2 y2 are below 2^-23 |x||y|: the result carries fp32 GEMM
+// error (tests/test_gpu_second_order.py: error vs fp64 against the library fp32 GEMM's).
+// 6 MFMAs of 16 x 16 x 32 per 16 x 16 x 32 block of the product = 2.5 PF / 6 ~ 400 TF of fp32 work;
+// at K = 64 that is above the rate at which the output (4 bytes per 128 FLOP) can be written, so the
+// kernel is bound by the C stream.
+// Roles: the MFMA's A operand is the W tile (rows n), its B operand is A^T (columns m), so a lane's
+// four accumulator rows are four consecutive n of one output row m -> one 16-byte store.
+namespace proj {
+
+using u4 = unsigned __attribute__((ext_vector_type(4)));
+using bf8 = __bf16 __attribute__((ext_vector_type(8)));
+using f4 = float __attribute__((ext_vector_type(4)));
+
+struct Args {
+  int M, N, lda, ldc;
+  long long pstride;       // elements between the three pieces of Wp
+  const float* A;
+  const unsigned short* Wp;
+  const float* bias;
+  float* C;
+};
+
+// the three truncated bf16 pieces of x, as fp32 bit patterns with the low half zero
+__device__ __forceinline__ void split3(float x, unsigned& h, unsigned& m, unsigned& l) {
+  h = __float_as_uint(x) & 0xffff0000u;
+  const float r1 = x - __uint_as_float(h);
+  m = __float_as_uint(r1) & 0xffff0000u;
+  l = __float_as_uint(r1 - __uint_as_float(m)) & 0xffff0000u;
+}
+
+// 8 consecutive fp32 (two 16-byte loads) -> the three bf16 fragments of one MFMA operand
+__device__ __forceinline__ void split8(const float4& a, const float4& b, bf8 (&f)[3]) {
+  const float x[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  unsigned h[8], m[8], l[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) split3(x[j], h[j], m[j], l[j]);
+  u4 H, M, L;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {  // element 2p in the low half of register p
+    H[p] = (h[2 * p] >> 16) | h[2 * p + 1];
+    M[p] = (m[2 * p] >> 16) | m[2 * p + 1];
+    L[p] = (l[2 * p] >> 16) | l[2 * p + 1];
+  }
+  f[0] = __builtin_bit_cast(bf8, H);
+  f[1] = __builtin_bit_cast(bf8, M);
+  f[2] = __builtin_bit_cast(bf8, L);
+}
+
+// W [N][K] fp32 -> its three exact bf16 pieces Wp [3][N][K] (once per weight, shared by every GEMM
+// that multiplies by it: the projection, its r-derivative and the second-order adjoint)
+__global__ __launch_bounds__(256) void k_proj_split(int N, int K, const float* W, int ldw, unsigned short* Wp) {
+  const int i = blockIdx.x * 256 + threadIdx.x;  // one float4 of W
+  if (i >= N * K / 4) return;
+  const int n = i / (K / 4), k = (i % (K / 4)) * 4;
+  const float4 v = *reinterpret_cast<const float4*>(W + (size_t)n * ldw + k);
+  const float x[4] = {v.x, v.y, v.z, v.w};
+  unsigned h[4], m[4], l[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) split3(x[j], h[j], m[j], l[j]);
+  const size_t o = (size_t)n * K + k, ps = (size_t)N * K;
+  *reinterpret_cast<uint2*>(Wp + o) = make_uint2((h[0] >> 16) | h[1], (h[2] >> 16) | h[3]);
+  *reinterpret_cast<uint2*>(Wp + ps + o) = make_uint2((m[0] >> 16) | m[1], (m[2] >> 16) | m[3]);
+  *reinterpret_cast<uint2*>(Wp + 2 * ps + o) = make_uint2((l[0] >> 16) | l[1], (l[2] >> 16) | l[3]);
+}
+
+// KS = K / 32 MFMA k-steps.  A workgroup (4 waves) owns BN columns -- their W pieces (from the
+// pre-split Wp) and bias staged in LDS -- and 64 MB rows, a wave MB 16-row blocks of A split into
+// registers.  After the one barrier the waves read W fragments from LDS only: a global load inside
+// the column loop would wait behind the wave's own output stores (loads and stores share vmcnt).
+// Grid: x = column tiles (fast: the tiles of one row block run together and re-read its A rows from
+// L2), y = row tiles.
+template <int KS, int MB, int BN>
+__global__ __launch_bounds__(256) void k_proj_x3(Args P) {
+  constexpr int K = 32 * KS, LD = K + 8;  // LDS row pitch in bf16 (16-byte pad: rows shift banks)
+  __shared__ __attribute__((aligned(16))) unsigned short w[3][BN][LD];
+  __shared__ __attribute__((aligned(16))) float sb[BN];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int n0 = blockIdx.x * BN;
+  const int m0 = (blockIdx.y * 4 + wave) * (16 * MB);
+  const int nr = min(BN, P.N - n0);
+  const int kq = 8 * (lane >> 4);
+  // A rows first (their latency overlaps the W tile copy): lane holds row m0 + 16 mb + (lane & 15),
+  // k = 32 ks + kq + 0..7
+  float4 ar[MB][KS][2];
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb) {
+    const float* r = P.A + (size_t)min(m0 + 16 * mb + (lane & 15), P.M - 1) * P.lda + kq;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      ar[mb][ks][0] = *reinterpret_cast<const float4*>(r + 32 * ks);
+      ar[mb][ks][1] = *reinterpret_cast<const float4*>(r + 32 * ks + 4);
+    }
+  }
+  // W tile (3 pieces x BN rows x K bf16, 16-byte chunks; rows past N clamp) and bias -> LDS
+  constexpr int CH = K / 8;  // 16-byte chunks per row
+  for (int c = threadIdx.x; c < 3 * BN * CH; c += 256) {
+    const int p = c / (BN * CH), rc = c % (BN * CH), n = rc / CH, k = (rc % CH) * 8;
+    *reinterpret_cast<u4*>(&w[p][n][k]) =
+        *reinterpret_cast<const u4*>(P.Wp + p * P.pstride + (size_t)min(n0 + n, P.N - 1) * K + k);
+  }
+  if (threadIdx.x < BN) sb[threadIdx.x] = P.bias ? P.bias[min(n0 + (int)threadIdx.x, P.N - 1)] : 0.f;
+  bf8 a[MB][KS][3];
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) split8(ar[mb][ks][0], ar[mb][ks][1], a[mb][ks]);
+  __syncthreads();
+  if (m0 >= P.M) return;  // (after the barrier: every wave took part in the tile copy)
+  for (int nb = 0; nb < nr; nb += 16) {
+    bf8 b[KS][3];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+        b[ks][p] = *reinterpret_cast<const bf8*>(&w[p][nb + (lane & 15)][32 * ks + kq]);
+    f4 acc[MB];
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) acc[mb] = f4{0.f, 0.f, 0.f, 0.f};
+    // small terms first: (W piece, A piece) = (2,0) (1,1) (0,2) (1,0) (0,1) (0,0)
+    constexpr int TW[6] = {2, 1, 0, 1, 0, 0}, TA[6] = {0, 1, 2, 0, 1, 0};
+#pragma unroll
+    for (int t = 0; t < 6; ++t)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+        for (int mb = 0; mb < MB; ++mb)
+          acc[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[ks][TW[t]], a[mb][ks][TA[t]], acc[mb], 0, 0, 0);
+    const int nl = nb + 4 * (lane >> 4);
+    const f4 bv = *reinterpret_cast<const f4*>(&sb[nl]);
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) {
+      const int m = m0 + 16 * mb + (lane & 15);
+      if (m < P.M) *reinterpret_cast<f4*>(P.C + (size_t)m * P.ldc + n0 + nl) = acc[mb] + bv;
+    }
+  }
+}
+
+}  // namespace proj
 }  // namespace tmd
 
 using namespace tmd;
@@ -511,11 +661,35 @@ extern "C" int tmdnet_gemm_f32(int n_problems, const int* dims, const void* cons
   int kmax = 0;
   for (int i = 0; i < n_problems; ++i) kmax = max(kmax, G.p[i].K);
   const int nw = kmax >= 256 ? nw_large : nw_small;
+  // K blocks per wave of the longest problem -> the smallest load batch that covers it in one go
+  // (a longer slice loops over batches, so any KMAX is correct; the choice only sizes registers)
+  const int per = (kmax / 16 + nw - 1) / nw;
   hipStream_t st = (hipStream_t)stream;
-  if (nw <= 2) hipLaunchKernelGGL(gemm::k_gemm<2>, dim3(tiles), dim3(128), 0, st, G);
-  else if (nw >= 16) hipLaunchKernelGGL(gemm::k_gemm<16>, dim3(tiles), dim3(1024), 0, st, G);
-  else if (nw >= 8) hipLaunchKernelGGL(gemm::k_gemm<8>, dim3(tiles), dim3(512), 0, st, G);
-  else hipLaunchKernelGGL(gemm::k_gemm<4>, dim3(tiles), dim3(256), 0, st, G);
+#define TMD_GEMM_LAUNCH(NW_, KB_) hipLaunchKernelGGL((gemm::k_gemm<NW_, KB_>), dim3(tiles), dim3(NW_ * 64), 0, st, G)
+  if (nw <= 2) TMD_GEMM_LAUNCH(2, 8);
+  else if (nw >= 16) {
+    // (the 16-wave launches measured equal with 1-, 2- and 3-block batches: one 1024-thread block per
+    // CU at any of them; TMDNET_GEMM_KB16 forces one)
+    static const int kb16 = [] { const char* e = getenv("TMDNET_GEMM_KB16"); return e ? atoi(e) : 0; }();
+    const int kb = kb16 ? kb16 : per;
+    if (kb <= 1) TMD_GEMM_LAUNCH(16, 1);
+    else if (kb == 2) TMD_GEMM_LAUNCH(16, 2);
+    else if (kb == 3) TMD_GEMM_LAUNCH(16, 3);
+    else TMD_GEMM_LAUNCH(16, 4);
+  } else if (nw >= 8) {
+    if (per <= 2) TMD_GEMM_LAUNCH(8, 2);
+    else TMD_GEMM_LAUNCH(8, 8);
+  } else {
+    // a 2-block slice loaded one block at a time: 46 VGPRs = 8 waves per SIMD instead of 84 = 4,
+    // and the second load is hidden by the other resident tiles (ET-QM9 training step: the 32
+    // K = H launches 257 -> 232 us; TMDNET_GEMM_KB4=2 restores the one-batch load)
+    static const int kb4 = [] { const char* e = getenv("TMDNET_GEMM_KB4"); return e ? atoi(e) : 1; }();
+    if (per <= 2 && kb4 <= 1) TMD_GEMM_LAUNCH(4, 1);
+    else if (per <= 2) TMD_GEMM_LAUNCH(4, 2);
+    else if (per <= 4) TMD_GEMM_LAUNCH(4, 4);
+    else TMD_GEMM_LAUNCH(4, 8);
+  }
+#undef TMD_GEMM_LAUNCH
   return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
 }
 
@@ -669,4 +843,48 @@ extern "C" size_t tmdnet_gemm_tn_workspace_bytes(int n_problems, const int* dims
 extern "C" int tmdnet_gemm_tn_f32_ws(int n_problems, const int* dims, const void* const* ptrs, void* workspace,
                                      size_t workspace_bytes, void* stream) {
   return gemm_tn(n_problems, dims, ptrs, 6, workspace, workspace_bytes, stream);
+}
+
+// Wp [3][N][K] (bf16 bit patterns) = the exact three-piece split of W [N][K] (ldw), see tmd::proj.
+extern "C" int tmdnet_proj_split_f32(int N, int K, const void* W, int ldw, void* Wp, void* stream) {
+  if (N <= 0 || K <= 0 || !W || !Wp) return kBadArgument;
+  if (K % 4 || ldw < K || ldw % 4 || (((uintptr_t)W) & 15) || (((uintptr_t)Wp) & 7)) return kUnsupported;
+  const int n4 = N * K / 4;
+  hipLaunchKernelGGL(proj::k_proj_split, dim3((n4 + 255) / 256), dim3(256), 0, (hipStream_t)stream, N, K,
+                     (const float*)W, ldw, (unsigned short*)Wp);
+  return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
+}
+
+// C [M][N] = A [M][K] W [N][K]^T (+ bias [N]) from Wp = tmdnet_proj_split_f32(W) (rows of the pieces
+// piece_stride elements apart: a row slice of a larger split is Wp + row0 * K with the full stride).
+// fp32 in / out on the bf16 MFMA.  K = 32 or 64, N % 16 == 0, 16-byte aligned rows.
+extern "C" int tmdnet_proj_f32(int M, int N, int K, const void* A, int lda, const void* Wp,
+                               long long piece_stride, const void* bias, void* C, int ldc, void* stream) {
+  if (M < 0 || N <= 0 || K <= 0 || !A || !Wp || !C) return kBadArgument;
+  if (M == 0) return kOk;
+  if ((K != 32 && K != 64) || N % 16 || lda < K || ldc < N || lda % 4 || ldc % 4 || piece_stride < (long long)N * K)
+    return kUnsupported;
+  if ((((uintptr_t)A) | ((uintptr_t)Wp) | ((uintptr_t)C) | ((uintptr_t)bias)) & 15) return kUnsupported;
+  static const int mb_env = getenv("TMDNET_PROJ_MB") ? atoi(getenv("TMDNET_PROJ_MB")) : 0;  // tuning
+  static const int bn_env = getenv("TMDNET_PROJ_BN") ? atoi(getenv("TMDNET_PROJ_BN")) : 0;
+  // measured (tools/proj_time.py): C2 [6613 x 64] x [64 x 4096] 38 us at 128 x 64 tiles (library 48);
+  // C5 [1.36M x 64] x [64 x 512] 0.90 ms at 256 x 128 (library 1.07)
+  const bool big = M >= 65536;
+  const int mb = mb_env ? mb_env : (big ? 4 : 2), bn = bn_env ? bn_env : (big ? 128 : 64);
+  proj::Args P{M, N, lda, ldc, piece_stride, (const float*)A, (const unsigned short*)Wp, (const float*)bias,
+               (float*)C};
+  const dim3 g((N + bn - 1) / bn, (M + 64 * mb - 1) / (64 * mb));
+  hipStream_t st = (hipStream_t)stream;
+#define TMD_PROJ(KS_, MB_, BN_) hipLaunchKernelGGL((proj::k_proj_x3<KS_, MB_, BN_>), g, dim3(256), 0, st, P)
+  if (K == 64) {
+    if (bn >= 128) {
+      if (mb >= 4) TMD_PROJ(2, 4, 128); else TMD_PROJ(2, 2, 128);
+    } else {
+      if (mb >= 4) TMD_PROJ(2, 4, 64); else if (mb == 2) TMD_PROJ(2, 2, 64); else TMD_PROJ(2, 1, 64);
+    }
+  } else {
+    if (mb >= 4) TMD_PROJ(1, 4, 64); else TMD_PROJ(1, 2, 64);
+  }
+#undef TMD_PROJ
+  return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
 }

@@ -227,9 +227,22 @@ class _Meta:
         self.rbf = None         # (mu, beta, cutoff_lower, cutoff_upper, rbf_type): f = rbf(r) ("dr mode")
         self.out_norm = False   # the model's final LayerNorm fused into the last epilogue (2 trailing params)
         self.f_pairs = None     # f at the pair rows, when the caller produced it with the features
+        self.dkv_wp = None      # the bf16 split of dkv_eff[0] (dkv_split), once per forward
 
     def split(self, params):
         return [params[i * self.np:(i + 1) * self.np] for i in range(self.n_layers)]
+
+    def dkv_split(self):
+        """The exact bf16 split of the stacked dk/dv weight (kernels.proj_split), made once per forward
+        and shared by the projection, its r-derivative and the second-order adjoint."""
+        if self.dkv_wp is None and self.dkv_eff[0] is not None:
+            self.dkv_wp = kernels.proj_split(self.dkv_eff[0])
+        return self.dkv_wp
+
+    def dkv_proj(self, A, l=None, bias=True):
+        """A @ W.T (+ b) for the stacked dk/dv weight (l None) or layer l's rows of it."""
+        w, b = self.dkv_eff if l is None else self.dkv_layer(l)
+        return kernels.proj(A, w, b if bias else None, wp=self.dkv_split(), row0=0 if l is None else l * self.D)
 
     def dkv_layer(self, l):
         w, b_ = self.dkv_eff
@@ -241,6 +254,7 @@ class _Meta:
     def refresh_effective(self):
         """Row-permuted copies of the stacked weights for the planar layout (once per forward, so
         in-place parameter updates are always seen; two small gathers per layer)."""
+        self.dkv_wp = None
         if not self.planar:
             self.qkv_eff, self.dkv_eff = self.fused, (self.dkv_w, self.dkv_b)
             return
@@ -320,7 +334,7 @@ def _forward_layers(meta, x, f, C, u, params):
     fp = f
     if D and meta.pairs is not None:
         fp = meta.f_pairs if meta.f_pairs is not None else f.index_select(0, meta.pairs[1])
-    pkv_all = torch.addmm(meta.dkv_eff[1], fp, meta.dkv_eff[0].t()) if (meta.batched and D) else None
+    pkv_all = meta.dkv_proj(fp) if (meta.batched and D) else None
     layers = meta.split(params)
     L = len(layers)
     od = dict(dtype=x.dtype, device=x.device)
@@ -346,7 +360,7 @@ def _forward_layers(meta, x, f, C, u, params):
         if pkv_all is not None:
             pkv = pkv_all[:, l * D:(l + 1) * D]
         else:
-            pkv = torch.addmm(dkv_b, fp, dkv_w.t()) if dkv_w is not None else None
+            pkv = meta.dkv_proj(fp, l) if dkv_w is not None else None
         pk = pkv[:, :H] if meta.hk else None
         pv = pkv[:, H * int(meta.hk):] if meta.hv else None
         xa = xa_all[l]
@@ -413,7 +427,7 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws, r=None, dr=Fa
         assert has_e and not any(need_ws) and meta.rbf is not None
         g_r = zbuf[4 * E:]
         fdp = kernels.rbf_deriv(r, *meta.rbf, rows=meta.pairs[1] if meta.pairs is not None else None)
-        dpkv_all = torch.mm(fdp, meta.dkv_eff[0].t()) if meta.batched else None
+        dpkv_all = meta.dkv_proj(fdp, bias=False) if meta.batched else None
     # dr mode recorded (the create_graph force pass): g_r in-kernel AND the projection gradient kept
     # padding rows of a static-capacity list are zeroed by the kernel: no memset needed
     if has_e and (not dr or rec):
@@ -468,7 +482,7 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws, r=None, dr=Fa
         g_qkv, g_o, g_vecp = g_qkv_all[l], g_o_all[l], g_vecp_all[l]
         gpk = gpv = dpk = dpv = None
         if dr:
-            dpkv = dpkv_all[:, l * D:(l + 1) * D] if meta.batched else torch.mm(fdp, dkv_w.t())
+            dpkv = dpkv_all[:, l * D:(l + 1) * D] if meta.batched else meta.dkv_proj(fdp, l, bias=False)
             dpk = dpkv[:, :H] if meta.hk else None
             dpv = dpkv[:, H * int(meta.hk):] if meta.hv else None
         if has_e and (not dr or rec):
@@ -841,7 +855,7 @@ def _second_order(ctx, ggs, want):
     dpkv_pairs = tail.get("dpkv") if (gg_f is None and ctx.dr and gg_r is not None and meta.pk_rows is not None) else None
     gb_pkv_all = None
     if dpkv_pairs is None and gb_f is not None and has_e:
-        gb_pkv_all = torch.mm(gb_f, W_all.t())
+        gb_pkv_all = meta.dkv_proj(gb_f, bias=False)
     gr_scale = gg_r.contiguous() if dpkv_pairs is not None else None
     W_bar = {}
 

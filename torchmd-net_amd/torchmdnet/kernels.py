@@ -1051,6 +1051,52 @@ def gemm_group(problems):
             torch.mm(A, Bop, out=C)
 
 
+# ET dk/dv projection on the bf16 MFMA with an exact three-piece split (fp32 accuracy); TMDNET_PROJ=lib
+# keeps the library fp32 GEMM (A/B switch)
+PROJ = os.environ.get("TMDNET_PROJ", "x3")
+
+
+def proj_split(W):
+    """The exact three-piece bf16 split of a projection weight W [N, K] (``tmdnet_proj_split_f32``):
+    an int16 tensor [3, N, K], or None when W is outside the kernel's envelope (then ``proj`` uses the
+    library GEMM)."""
+    N, K = W.shape
+    if not (PROJ == "x3" and W.is_cuda and W.dtype == torch.float32 and W.stride(1) == 1 and K in (32, 64)
+            and N % 16 == 0):
+        return None
+    wp = torch.empty((3, N, K), dtype=torch.int16, device=W.device)
+    rc = nat.load().tmdnet_proj_split_f32(N, K, W.data_ptr(), W.stride(0), wp.data_ptr(), nat.stream(W.device))
+    if rc == GEMM_UNSUPPORTED:
+        return None
+    nat.check(rc, "tmdnet_proj_split_f32")
+    return wp
+
+
+def proj(A, W, bias=None, out=None, wp=None, row0=0):
+    """``A @ W.T (+ bias)`` for the dk/dv projection shapes (``tmdnet_proj_f32``: K = 32 / 64, fp32,
+    16-byte aligned rows, N % 16 == 0); anything else, fp64 parity runs and ``TMDNET_PROJ=lib`` use
+    the library GEMM on the same device.  ``wp``: W's split from ``proj_split`` when the caller shares
+    it between GEMMs (W = rows [row0, row0 + N) of the split weight); ``out`` receives the result."""
+    M, K = A.shape
+    N = W.shape[0]
+    if out is None:
+        out = torch.empty((M, N), dtype=A.dtype, device=A.device)
+    if (PROJ == "x3" and A.is_cuda and A.dtype == torch.float32 and A.stride(1) == 1 and out.stride(1) == 1
+            and (bias is None or bias.is_contiguous())):
+        if wp is None:
+            wp, row0 = proj_split(W), 0
+        if wp is not None:
+            rc = nat.load().tmdnet_proj_f32(M, N, K, A.data_ptr(), A.stride(0), wp[0, row0:].data_ptr(),
+                                            wp.shape[1] * K, None if bias is None else bias.data_ptr(),
+                                            out.data_ptr(), out.stride(0), nat.stream(A.device))
+            if rc != GEMM_UNSUPPORTED:
+                nat.check(rc, "tmdnet_proj_f32")
+                return out
+    if bias is not None:
+        return torch.addmm(bias, A, W.t(), out=out)
+    return torch.mm(A, W.t(), out=out)
+
+
 def wgrad_tn(problems):
     """Weight-gradient GEMMs C (+)= A^T B (+ A2^T B2), sums over the rows, all in one
     ``tmdnet_gemm_tn_f32`` launch (fp32; the library per problem otherwise).  Each problem is a dict:
