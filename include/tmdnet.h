@@ -489,6 +489,14 @@ int tmdnet_gemm_tn_f32(int n_problems, const int* dims, const void* const* ptrs,
 size_t tmdnet_gemm_tn_workspace_bytes(int n_problems, const int* dims);
 int tmdnet_gemm_tn_f32_ws(int n_problems, const int* dims, const void* const* ptrs, void* workspace,
                           size_t workspace_bytes, void* stream);
+/* Embedding lookups (the forward of nn.Embedding(num_types, H) at z, TorchMD_ET.embedding and
+ * NeighborEmbedding.embedding, reference torchmd_et.py:170, utils.py:92; replaces the two index_select
+ * gathers): for each of n_tables (<= 4) tables sharing z[n] (int64), outs_t[k][:] = tables_t[z[k]][:]
+ * (row strides ld_tables[t] / ld_outs[t], NULL: H; multiples of 4, 16-byte aligned bases) in ONE
+ * launch.  An index outside [0, num_types) asserts in the debug build and writes a zero row otherwise. */
+int tmdnet_embedding_fwd_f32(int n, int H, int num_types, const int64_t* z, int n_tables,
+                             const void* const* tables, const int* ld_tables, void* const* outs,
+                             const int* ld_outs, void* stream);
 /* Embedding-table gradients (the backward of nn.Embedding(num_types, H) looked up at z, as used by
  * TorchMD_ET.embedding and NeighborEmbedding.embedding, reference torchmd_et.py:170,
  * utils.py:92): for each of n_tables (<= 32) tables sharing the indices z[n] (int64, in [0, num_types)),

@@ -270,6 +270,25 @@ def test_embedding_backward_one_hot_tn():
     assert _rel(d1, ref) < 1e-6 and _rel(d2, ref) < 1e-6
 
 
+def test_embedding_forward_one_launch():
+    """tmdnet_embedding_fwd_f32 (both tables of the ET lookup node in one launch) bit-exact against
+    index_select: strided table rows, int32 indices, a single row and an empty index vector."""
+    from torchmdnet import kernels
+    torch.manual_seed(1)
+    w1 = torch.randn(100, 128, device=DEV)
+    w2 = torch.randn(100, 256, device=DEV)[:, :128]  # row stride 256
+    for z in (torch.randint(0, 100, (678,), device=DEV), torch.randint(0, 100, (50001,), device=DEV),
+              torch.tensor([99], device=DEV), torch.randint(0, 100, (37,), device=DEV, dtype=torch.int32),
+              torch.zeros(0, dtype=torch.int64, device=DEV)):
+        outs = kernels.embedding_fwd(z, (w1, w2))
+        for w, o in zip((w1, w2), outs):
+            assert o.shape == (z.shape[0], 128)
+            assert torch.equal(o, w.index_select(0, z.long()))
+    w3 = torch.randn(5, 12, device=DEV)  # H = 12: three float4 per row
+    z = torch.randint(0, 5, (1000,), device=DEV)
+    assert torch.equal(kernels.embedding_fwd(z, (w3,))[0], w3[z])
+
+
 @pytest.mark.parametrize("rows,fin,fout", [(12548, 64, 128), (678, 256, 128), (37, 7, 5)])
 def test_linear_tn_first_and_second_order(rows, fin, fout):
     """kernels.linear (TN-GEMM weight / bias gradients, differentiable backward) against F.linear

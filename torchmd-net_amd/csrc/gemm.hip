@@ -620,6 +620,31 @@ __global__ __launch_bounds__(256) void k_proj_x3(Args P) {
 }
 
 }  // namespace proj
+
+namespace emb {
+constexpr int MAX_TABLES = 4;
+struct Tables {
+  int n_tables, H4;  // H / 4
+  const float* t[MAX_TABLES];
+  int ldt[MAX_TABLES];
+  float* out[MAX_TABLES];
+  int ldo[MAX_TABLES];
+};
+// out_t[k][:] = table_t[z[k]][:] for every table sharing z: one thread per float4 of one output row
+// (x = node-major float4 index, y = table).  An index outside [0, num_types) is an error of the caller
+// (nn.Embedding raises): the debug build asserts it, the release build writes zeros.
+__global__ __launch_bounds__(256) void k_embed_fwd(int n, int num_types, const int64_t* __restrict__ z, Tables T) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  const int t = blockIdx.y;
+  if (i >= (long long)n * T.H4) return;
+  const int k = (int)(i / T.H4), c = (int)(i % T.H4);
+  const long long m = z[k];
+  TMD_DCHECK(m >= 0 && m < num_types);
+  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (m >= 0 && m < num_types) v = reinterpret_cast<const float4*>(T.t[t] + (size_t)m * T.ldt[t])[c];
+  reinterpret_cast<float4*>(T.out[t] + (size_t)k * T.ldo[t])[c] = v;
+}
+}  // namespace emb
 }  // namespace tmd
 
 using namespace tmd;
@@ -771,6 +796,36 @@ extern "C" int tmdnet_embedding_bwd_f32(int n, int H, int num_types, const int64
     tiles += ((P.M + 31) / 32) * P.tiles_n;
   }
   launch_tn(G, tiles, n, nullptr, (hipStream_t)stream);
+  return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
+}
+
+// Embedding lookups of n_tables tables sharing the indices z (TorchMD_ET.embedding and
+// NeighborEmbedding.embedding, reference torchmd_et.py:170, utils.py:92) in ONE launch.
+extern "C" int tmdnet_embedding_fwd_f32(int n, int H, int num_types, const int64_t* z, int n_tables,
+                                        const void* const* tables, const int* ld_tables, void* const* outs,
+                                        const int* ld_outs, void* stream) {
+  if (n < 0 || H <= 0 || num_types <= 0 || n_tables < 1 || n_tables > emb::MAX_TABLES || !tables || !outs)
+    return kBadArgument;
+  if (n == 0) return kOk;
+  if (!z) return kBadArgument;
+  if (H % 4) return kUnsupported;
+  emb::Tables T{};
+  T.n_tables = n_tables;
+  T.H4 = H / 4;
+  for (int i = 0; i < n_tables; ++i) {
+    if (!tables[i] || !outs[i]) return kBadArgument;
+    T.t[i] = (const float*)tables[i];
+    T.out[i] = (float*)outs[i];
+    T.ldt[i] = ld_tables ? ld_tables[i] : H;
+    T.ldo[i] = ld_outs ? ld_outs[i] : H;
+    if (T.ldt[i] < H || T.ldo[i] < H || T.ldt[i] % 4 || T.ldo[i] % 4) return kUnsupported;
+    if ((((uintptr_t)tables[i]) | ((uintptr_t)outs[i])) & 15) return kUnsupported;
+  }
+  const long long items = (long long)n * T.H4;
+  if (items > 2147483647LL * 256) return kUnsupported;
+  const dim3 g((unsigned)((items + 255) / 256), n_tables);
+  hipLaunchKernelGGL(emb::k_embed_fwd, g, dim3(256), 0,
+                     (hipStream_t)stream, n, num_types, z, T);
   return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
 }
 

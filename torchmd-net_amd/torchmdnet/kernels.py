@@ -1688,6 +1688,25 @@ def _tn_ok(*ts):
     return all(t is None or (t.is_cuda and t.dtype == torch.float32) for t in ts)
 
 
+def embedding_fwd(z, weights):
+    """weights[t][z] for every table (rows of H fp32): one tmdnet_embedding_fwd_f32 launch on the GPU
+    (the two lookups of TorchMD_ET / NeighborEmbedding); ``index_select`` for fp64 / CPU tensors."""
+    H = weights[0].shape[1]
+    if (not _tn_ok(*weights) or H % 4 or len(weights) > 4 or any(w.shape[1] != H for w in weights)
+            or any(w.stride(1) != 1 or w.stride(0) % 4 or w.data_ptr() % 16 for w in weights)):
+        return tuple(w.index_select(0, z) for w in weights)
+    outs = [torch.empty((z.shape[0], H), dtype=w.dtype, device=w.device) for w in weights]
+    n = len(weights)
+    tp = (ctypes.c_void_p * n)(*[w.data_ptr() for w in weights])
+    lt = (ctypes.c_int * n)(*[w.stride(0) for w in weights])
+    op = (ctypes.c_void_p * n)(*[o.data_ptr() for o in outs])
+    zc = z.to(torch.int64).contiguous()
+    rc = nat.load().tmdnet_embedding_fwd_f32(z.shape[0], H, weights[0].shape[0], nat.ptr(zc), n, tp, lt, op,
+                                             None, nat.stream(z.device))
+    nat.check(rc, "tmdnet_embedding_fwd_f32")
+    return tuple(outs)
+
+
 def embedding_bwd(z, grads, num_types, out=None, accumulate=False):
     """Table gradients of embeddings looked up at ``z``: one launch for every (grad [n, H]) of ``grads``."""
     H = grads[0].shape[1]
@@ -1717,7 +1736,7 @@ class _Embedding(Function):
     def forward(ctx, z, *weights):
         ctx.save_for_backward(z)
         ctx.shapes = [w.shape for w in weights]
-        return tuple(w.index_select(0, z) for w in weights)
+        return embedding_fwd(z, weights)
 
     @staticmethod
     def backward(ctx, *gs):
