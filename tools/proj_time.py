@@ -37,6 +37,7 @@ for tag, M, N in (("c2", 6613, 4096), ("c5", 1361000, 512)):
     us_x3 = t(lambda: kernels.proj(f, w, b, out=out, wp=wp), reps)
     us_fill = t(lambda: out.fill_(1.0), reps)
     gb = M * N * 4 / 1e9
-    print(f"{tag} MB={os.environ.get('TMDNET_PROJ_MB', '-')} BN={os.environ.get('TMDNET_PROJ_BN', '-')}: "
+    print(f"{tag} MB={os.environ.get('TMDNET_PROJ_MB', '-')} BN={os.environ.get('TMDNET_PROJ_BN', '-')} "
+          f"STG={os.environ.get('TMDNET_PROJ_STG', '-')}: "
           f"lib {us_lib:.1f} us  x3 {us_x3:.1f} us  fill {us_fill:.1f} us  ({gb / us_x3 * 1e6 / 1e3:.2f} TB/s x3, "
           f"{gb / us_fill * 1e6 / 1e3:.2f} TB/s fill)", flush=True)
