@@ -150,6 +150,21 @@ class TorchMD_Net(nn.Module):
             for prior in self.prior_model:
                 prior.reset_parameters()
 
+    @torch.jit.unused
+    def _ones_seed(self, y: Tensor) -> Tensor:
+        """The force pass's ``grad_outputs`` (ones like y, reference model.py:286-298) kept per shape /
+        dtype / device, so an energy + force evaluation does not launch a fill for it (read-only: autograd
+        never writes its seeds).  Not cached when first needed inside a HIP-graph capture (its memory
+        would belong to the graph's pool)."""
+        cache = self.__dict__.setdefault("_seed_cache", {})
+        key = (tuple(y.shape), y.dtype, y.device)
+        t = cache.get(key)
+        if t is None:
+            t = torch.ones_like(y)
+            if not (y.is_cuda and torch.cuda.is_current_stream_capturing()):
+                cache[key] = t
+        return t
+
     def forward(self, z: Tensor, pos: Tensor, batch: Optional[Tensor] = None, q: Optional[Tensor] = None,
                 s: Optional[Tensor] = None, extra_args: Optional[Dict[str, Tensor]] = None
                 ) -> Tuple[Tensor, Optional[Tensor]]:
@@ -209,7 +224,11 @@ class TorchMD_Net(nn.Module):
             for prior in prior_model:
                 y = prior.post_reduce(y, z, pos, batch, extra_args)
         if self.derivative:
-            grad_outputs: List[Optional[torch.Tensor]] = [torch.ones_like(y)]
+            if torch.jit.is_scripting():
+                seed = torch.ones_like(y)
+            else:
+                seed = self._ones_seed(y)
+            grad_outputs: List[Optional[torch.Tensor]] = [seed]
             dy = grad([y], [pos], grad_outputs=grad_outputs, create_graph=True, retain_graph=True)[0]
             if dy is None:
                 raise RuntimeError("Autograd returned None for the force prediction.")
