@@ -151,16 +151,16 @@ class TorchMD_Net(nn.Module):
                 prior.reset_parameters()
 
     @torch.jit.unused
-    def _ones_seed(self, y: Tensor) -> Tensor:
-        """The force pass's ``grad_outputs`` (ones like y, reference model.py:286-298) kept per shape /
-        dtype / device, so an energy + force evaluation does not launch a fill for it (read-only: autograd
-        never writes its seeds).  Not cached when first needed inside a HIP-graph capture (its memory
-        would belong to the graph's pool)."""
+    def _neg_seed(self, y: Tensor) -> Tensor:
+        """The force pass's ``grad_outputs`` (-1 like y, see forward) kept per shape / dtype / device, so
+        an energy + force evaluation does not launch a fill for it (read-only: autograd never writes its
+        seeds).  Not cached when first needed inside a HIP-graph capture (its memory would belong to
+        the graph's pool)."""
         cache = self.__dict__.setdefault("_seed_cache", {})
         key = (tuple(y.shape), y.dtype, y.device)
         t = cache.get(key)
         if t is None:
-            t = torch.ones_like(y)
+            t = torch.full_like(y, -1.0)
             if not (y.is_cuda and torch.cuda.is_current_stream_capturing()):
                 cache[key] = t
         return t
@@ -197,7 +197,7 @@ class TorchMD_Net(nn.Module):
         if self.derivative:
             # -dy/dpos directly: the backward is seeded with -1 instead of negating its result (sign
             # flips are exact; one elementwise launch fewer than the reference's `-dy`, model.py:298)
-            grad_outputs: List[Optional[torch.Tensor]] = [torch.full_like(y, -1.0)]
+            grad_outputs: List[Optional[torch.Tensor]] = [self._neg_seed(y)]
             neg_dy = grad([y], [pos], grad_outputs=grad_outputs, create_graph=True, retain_graph=True)[0]
             if neg_dy is None:
                 raise RuntimeError("Autograd returned None for the force prediction.")
@@ -224,11 +224,7 @@ class TorchMD_Net(nn.Module):
             for prior in prior_model:
                 y = prior.post_reduce(y, z, pos, batch, extra_args)
         if self.derivative:
-            if torch.jit.is_scripting():
-                seed = torch.ones_like(y)
-            else:
-                seed = self._ones_seed(y)
-            grad_outputs: List[Optional[torch.Tensor]] = [seed]
+            grad_outputs: List[Optional[torch.Tensor]] = [torch.ones_like(y)]
             dy = grad([y], [pos], grad_outputs=grad_outputs, create_graph=True, retain_graph=True)[0]
             if dy is None:
                 raise RuntimeError("Autograd returned None for the force prediction.")
