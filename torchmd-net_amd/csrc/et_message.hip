@@ -1323,7 +1323,9 @@ static constexpr int kBwdFuseNodes = 16384;
 
 template <typename T, int V, int KIND, bool ORD>
 static int et_launch_v(const Args<T>& A, hipStream_t st) {
-  const int S = et_waves_per_node(A.n, (int)sizeof(T) * V);
+  int S = et_waves_per_node(A.n, (int)sizeof(T) * V);
+  static const int bwd_s = getenv("TMDNET_ET_BWD_S") ? atoi(getenv("TMDNET_ET_BWD_S")) : 0;  // tuning
+  if (KIND != 0 && bwd_s && (int)sizeof(T) * V <= 32) S = bwd_s >= 4 ? 4 : bwd_s >= 2 ? 2 : 1;
   if (S == 4) return et_launch_vs<T, V, (sizeof(T) * V <= 32 ? 4 : 1), KIND, ORD>(A, st);
   if (S == 2) return et_launch_vs<T, V, (sizeof(T) * V <= 32 ? 2 : 1), KIND, ORD>(A, st);
   return et_launch_vs<T, V, 1, KIND, ORD>(A, st);
