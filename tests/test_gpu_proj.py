@@ -15,12 +15,6 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
-@pytest.fixture(autouse=True, params=["0", "1"], ids=["direct-stores", "lds-staged-stores"])
-def _store_path(request, monkeypatch):
-    """Both output-store paths of k_proj_x3 (TMDNET_PROJ_STG, read by the launcher on every call)."""
-    monkeypatch.setenv("TMDNET_PROJ_STG", request.param)
-
-
 def _check(A, W, b, out=None):
     from torchmdnet import kernels
     got = kernels.proj(A, W, b, out=out)
@@ -47,12 +41,16 @@ def test_proj_matches_fp64_like_library(M, N, K, bias):
     _check(A, W, b)
 
 
-def test_proj_large_tile_config():
-    """M >= 65536 selects the 256-row x 128-column tiles (the C5 per-layer shape), ragged M."""
+@pytest.mark.parametrize("K", [32, 64])
+def test_proj_large_tile_config(K):
+    """M >= 65536 selects the large tiles (256 rows; 128 columns at K = 64, 64 at K = 32 -- the grid
+    must follow the tile actually launched: every column written), ragged M."""
     torch.manual_seed(2)
-    A = torch.rand(70001, 64, device=DEV)
-    W = torch.randn(512, 64, device=DEV) / 8
-    _check(A, W, torch.randn(512, device=DEV))
+    A = torch.rand(70001, K, device=DEV)
+    W = torch.randn(512, K, device=DEV) / K ** 0.5
+    out = torch.full((70001, 512), float("nan"), device=DEV)
+    got = _check(A, W, torch.randn(512, device=DEV), out=out)
+    assert bool(torch.isfinite(got).all())
 
 
 def test_proj_strided_operands_and_output():

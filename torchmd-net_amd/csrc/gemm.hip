@@ -553,16 +553,13 @@ __global__ __launch_bounds__(256) void k_proj_split(int N, int K, const float* W
 // the column loop would wait behind the wave's own output stores (loads and stores share vmcnt).
 // Grid: x = column tiles (fast: the tiles of one row block run together and re-read its A rows from
 // L2), y = row tiles.
-// STG: output stores staged per wave through LDS -- two 16-column MFMA blocks (32 columns = one 128-byte
-// line per row) are written to a wave-private LDS tile and stored back row-major, 8 whole lines per
-// store instruction, instead of 16 half-line (64-byte) pieces straight from the accumulator layout.
-template <int KS, int MB, int BN, bool STG>
+// (Output stores staged per wave through LDS as whole 128-byte lines were measured and dropped: the
+// L2 already merges the half-line pieces of adjacent column blocks)
+template <int KS, int MB, int BN>
 __global__ __launch_bounds__(256) void k_proj_x3(Args P) {
   constexpr int K = 32 * KS, LD = K + 8;  // LDS row pitch in bf16 (16-byte pad: rows shift banks)
-  constexpr int SP = 36;                  // staging row pitch in floats
   __shared__ __attribute__((aligned(16))) unsigned short w[3][BN][LD];
   __shared__ __attribute__((aligned(16))) float sb[BN];
-  __shared__ __attribute__((aligned(16))) float stg[STG ? 4 : 1][STG ? 16 * MB : 1][STG ? SP : 4];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int n0 = blockIdx.x * BN;
   const int m0 = (blockIdx.y * 4 + wave) * (16 * MB);
@@ -616,31 +613,10 @@ __global__ __launch_bounds__(256) void k_proj_x3(Args P) {
           acc[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[ks][TW[t]], a[mb][ks][TA[t]], acc[mb], 0, 0, 0);
     const int nl = nb + 4 * (lane >> 4);
     const f4 bv = *reinterpret_cast<const f4*>(&sb[nl]);
-    if constexpr (STG) {
-      const int half = (nb >> 4) & 1;  // 16-column block within the 32-column line
 #pragma unroll
-      for (int mb = 0; mb < MB; ++mb)
-        *reinterpret_cast<f4*>(&stg[wave][16 * mb + (lane & 15)][16 * half + 4 * (lane >> 4)]) = acc[mb] + bv;
-      if (half || nb + 16 >= nr) {
-        // LDS executes a wave's instructions in order; the barrier only stops the compiler moving the
-        // reads above the writes (and the next block's writes above these reads)
-        __builtin_amdgcn_wave_barrier();
-        const int c0 = nb - 16 * half, ncol = 16 * (half + 1);
-        const int c = 4 * (lane & 7);
-#pragma unroll
-        for (int i = 0; i < 2 * MB; ++i) {
-          const int r = 8 * i + (lane >> 3), m = m0 + r;
-          const f4 v = *reinterpret_cast<const f4*>(&stg[wave][r][c]);
-          if (c < ncol && m < P.M) *reinterpret_cast<f4*>(P.C + (size_t)m * P.ldc + n0 + c0 + c) = v;
-        }
-        __builtin_amdgcn_wave_barrier();
-      }
-    } else {
-#pragma unroll
-      for (int mb = 0; mb < MB; ++mb) {
-        const int m = m0 + 16 * mb + (lane & 15);
-        if (m < P.M) *reinterpret_cast<f4*>(P.C + (size_t)m * P.ldc + n0 + nl) = acc[mb] + bv;
-      }
+    for (int mb = 0; mb < MB; ++mb) {
+      const int m = m0 + 16 * mb + (lane & 15);
+      if (m < P.M) *reinterpret_cast<f4*>(P.C + (size_t)m * P.ldc + n0 + nl) = acc[mb] + bv;
     }
   }
 }
@@ -948,29 +924,27 @@ extern "C" int tmdnet_proj_f32(int M, int N, int K, const void* A, int lda, cons
   if ((((uintptr_t)A) | ((uintptr_t)Wp) | ((uintptr_t)C) | ((uintptr_t)bias)) & 15) return kUnsupported;
   static const int mb_env = getenv("TMDNET_PROJ_MB") ? atoi(getenv("TMDNET_PROJ_MB")) : 0;  // tuning
   static const int bn_env = getenv("TMDNET_PROJ_BN") ? atoi(getenv("TMDNET_PROJ_BN")) : 0;
-  const char* stg_env = getenv("TMDNET_PROJ_STG");  // read per call: tests / timing flip it in-process
-  const bool stg = stg_env ? atoi(stg_env) != 0 : false;
   // measured (tools/proj_time.py): C2 [6613 x 64] x [64 x 4096] 38 us at 128 x 64 tiles (library 48);
   // C5 [1.36M x 64] x [64 x 512] 0.90 ms at 256 x 128 (library 1.07)
   const bool big = M >= 65536;
-  const int mb = mb_env ? mb_env : (big ? 4 : 2), bn = bn_env ? bn_env : (big ? 128 : 64);
+  const int mb_req = mb_env ? mb_env : (big ? 4 : 2), bn_req = bn_env ? bn_env : (big ? 128 : 64);
+  // the tile that is actually instantiated for this K (the grid is derived from it, not from the
+  // request: K = 32 has only 64-column tiles)
+  const int bn = (K == 64 && bn_req >= 128) ? 128 : 64;
+  const int mb = mb_req >= 4 ? 4 : (mb_req >= 2 || bn == 128 || K == 32) ? 2 : 1;
   proj::Args P{M, N, lda, ldc, piece_stride, (const float*)A, (const unsigned short*)Wp, (const float*)bias,
                (float*)C};
   const dim3 g((N + bn - 1) / bn, (M + 64 * mb - 1) / (64 * mb));
   hipStream_t st = (hipStream_t)stream;
-#define TMD_PROJ(KS_, MB_, BN_)                                                                  \
-  do {                                                                                            \
-    if (stg) hipLaunchKernelGGL((proj::k_proj_x3<KS_, MB_, BN_, true>), g, dim3(256), 0, st, P);  \
-    else hipLaunchKernelGGL((proj::k_proj_x3<KS_, MB_, BN_, false>), g, dim3(256), 0, st, P);     \
-  } while (0)
+#define TMD_PROJ(KS_, MB_, BN_) hipLaunchKernelGGL((proj::k_proj_x3<KS_, MB_, BN_>), g, dim3(256), 0, st, P)
   if (K == 64) {
-    if (bn >= 128) {
-      if (mb >= 4) TMD_PROJ(2, 4, 128); else TMD_PROJ(2, 2, 128);
+    if (bn == 128) {
+      if (mb == 4) TMD_PROJ(2, 4, 128); else TMD_PROJ(2, 2, 128);
     } else {
-      if (mb >= 4) TMD_PROJ(2, 4, 64); else if (mb == 2) TMD_PROJ(2, 2, 64); else TMD_PROJ(2, 1, 64);
+      if (mb == 4) TMD_PROJ(2, 4, 64); else if (mb == 2) TMD_PROJ(2, 2, 64); else TMD_PROJ(2, 1, 64);
     }
   } else {
-    if (mb >= 4) TMD_PROJ(1, 4, 64); else TMD_PROJ(1, 2, 64);
+    if (mb == 4) TMD_PROJ(1, 4, 64); else TMD_PROJ(1, 2, 64);
   }
 #undef TMD_PROJ
   return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;

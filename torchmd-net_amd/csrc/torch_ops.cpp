@@ -25,6 +25,7 @@
 //
 // Host code only (compiled by g++ against the torch headers); no torch types cross the C ABI.
 #include <ATen/ATen.h>
+#include <c10/core/DeviceGuard.h>
 #include <c10/hip/HIPStream.h>
 #include <torch/autograd.h>
 #include <torch/library.h>
@@ -957,11 +958,17 @@ struct TnMessage : public Function<TnMessage> {
 
 Tensor tn_embed(const Tensor& P, const Tensor& Q, const Tensor& W, const Tensor& C, const Tensor& u,
                 const Tensor& row_ptr, const Tensor& src, const Tensor& dst, double self0_mult) {
+  // launches, allocations and the stream on the input's device whatever the caller's current device
+  // (the autograd engine runs each backward on its device's thread with that device current)
+  const c10::OptionalDeviceGuard guard(P.device());
   return TnEmbed::apply(P, Q, W, C, u, row_ptr, src, dst, self0_mult);
 }
 
 Tensor tn_message(const Tensor& ea, const Tensor& Tc, const Tensor& row_ptr, const Tensor& src, const Tensor& dst,
                   double self0_mult) {
+  // launches, allocations and the stream on the input's device whatever the caller's current device
+  // (the autograd engine runs each backward on its device's thread with that device current)
+  const c10::OptionalDeviceGuard guard(ea.device());
   return TnMessage::apply(ea, Tc, row_ptr, src, dst, self0_mult);
 }
 
@@ -972,6 +979,9 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> get_neighbor_pairs_fwd(const std::str
                                                                   const at::Scalar& cutoff_upper,
                                                                   const at::Scalar& max_num_pairs, bool loop,
                                                                   bool include_transpose) {
+  // launches, allocations and the stream on the input's device whatever the caller's current device
+  // (the autograd engine runs each backward on its device's thread with that device current)
+  const c10::OptionalDeviceGuard guard(positions.device());
   Built B = nl_build(strategy, positions, batch, box_vectors, use_periodic, cutoff_lower.toDouble(),
                      cutoff_upper.toDouble(), max_num_pairs.toLong(), loop, include_transpose, true, false);
   return {B.nb, B.dl, B.dist, B.num};
@@ -981,6 +991,9 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> get_neighbor_pairs_autograd(
     const std::string& strategy, const Tensor& positions, const Tensor& batch, const Tensor& box_vectors,
     bool use_periodic, const at::Scalar& cutoff_lower, const at::Scalar& cutoff_upper, const at::Scalar& max_num_pairs,
     bool loop, bool include_transpose) {
+  // launches, allocations and the stream on the input's device whatever the caller's current device
+  // (the autograd engine runs each backward on its device's thread with that device current)
+  const c10::OptionalDeviceGuard guard(positions.device());
   auto r = NeighborPairs::apply(strategy, positions, batch, box_vectors, use_periodic, cutoff_lower.toDouble(),
                                 cutoff_upper.toDouble(), max_num_pairs.toLong(), loop, include_transpose);
   return {r[0], r[1], r[2], r[3]};
@@ -996,6 +1009,9 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> neighbor_grap
     const Tensor& pos, const Tensor& batch, const c10::optional<Tensor>& box, bool use_periodic, double cutoff_lower,
     double cutoff_upper, int64_t max_num_pairs, bool loop, const std::string& strategy, bool check_errors,
     int64_t static_capacity) {
+  // launches, allocations and the stream on the input's device whatever the caller's current device
+  // (the autograd engine runs each backward on its device's thread with that device current)
+  const c10::OptionalDeviceGuard guard(pos.device());
   auto r = NeighborGraph::apply(pos, batch, box.has_value() ? *box : Tensor(), use_periodic, cutoff_lower, cutoff_upper,
                                 max_num_pairs, loop, strategy, check_errors, static_capacity);
   return {r[0], r[1], r[2], r[3], r[4], r[5], r[6]};
@@ -1005,6 +1021,9 @@ std::tuple<Tensor, Tensor, Tensor> edge_geometry(const Tensor& deltas, const Ten
                                                  const Tensor& dst, const Tensor& mu, const Tensor& beta,
                                                  double cutoff_lower, double cutoff_upper, int64_t rbf_type,
                                                  bool want_rbf) {
+  // launches, allocations and the stream on the input's device whatever the caller's current device
+  // (the autograd engine runs each backward on its device's thread with that device current)
+  const c10::OptionalDeviceGuard guard(distances.device());
   auto r = EdgeGeom::apply(deltas, distances, src, dst, mu.detach().to(distances.scalar_type()).contiguous(),
                            beta.detach().to(distances.scalar_type()).contiguous(), cutoff_lower, cutoff_upper,
                            rbf_type, want_rbf);
@@ -1013,6 +1032,9 @@ std::tuple<Tensor, Tensor, Tensor> edge_geometry(const Tensor& deltas, const Ten
 
 Tensor nbr_embed(const Tensor& x, const Tensor& w, const Tensor& C, const Tensor& row_ptr, const Tensor& src,
                  const Tensor& dst) {
+  // launches, allocations and the stream on the input's device whatever the caller's current device
+  // (the autograd engine runs each backward on its device's thread with that device current)
+  const c10::OptionalDeviceGuard guard(x.device());
   return NbrEmbed::apply(x, w, C, row_ptr, src, dst);
 }
 
@@ -1020,6 +1042,9 @@ std::tuple<Tensor, Tensor> et_message(const Tensor& q, const Tensor& k, const Te
                                       const c10::optional<Tensor>& vec, const c10::optional<Tensor>& pk,
                                       const c10::optional<Tensor>& pv, const Tensor& C, const Tensor& u,
                                       const Tensor& row_ptr, const Tensor& src, const Tensor& dst, int64_t heads) {
+  // launches, allocations and the stream on the input's device whatever the caller's current device
+  // (the autograd engine runs each backward on its device's thread with that device current)
+  const c10::OptionalDeviceGuard guard(q.device());
   auto r = EtMsg::apply(q, k, v, vec.has_value() ? *vec : Tensor(), pk.has_value() ? *pk : Tensor(),
                         pv.has_value() ? *pv : Tensor(), C, u, row_ptr, src, dst, heads);
   return {r[0], r[1]};

@@ -967,6 +967,7 @@ def _second_order(ctx, ggs, want):
     if node is not None and _will_run(node):
         inj["x_top"] = seed_x
         meta.pending = {"inj": inj, "W_bar": W_bar, "on_bar": on_bar, "C_bar": C_bar, "u_bar": u_bar}
+        _HANDED_OFF.append(weakref.ref(meta))
         res = [gbar_x, gbar_v, None, None, None, None, r_bar] + [None] * len(params)
         return [t if w else None for t, w in zip(res, want)]
     need_w = tuple(bool(w) for w in _layer_wants(meta, want[7:]))
@@ -1066,6 +1067,23 @@ def composite_stack(meta, x, f, C, u, params, message=None):
     if meta.out_norm:
         x = F.layer_norm(x, (H,), params[-2], params[-1], _EPS)
     return x, vec
+
+
+# stacks whose second order handed its injected cotangents to the forward node's backward
+# (meta.pending); check_pending_consumed() after the loss backward proves they were all taken
+_HANDED_OFF = []
+
+
+def check_pending_consumed():
+    """Raise if a second order's injected cotangents were handed to a forward node whose backward then
+    never ran in the same engine pass (its parameter gradients would silently lack those terms)."""
+    left = [m for m in (ref() for ref in _HANDED_OFF) if m is not None and getattr(m, "pending", None) is not None]
+    _HANDED_OFF.clear()
+    for m in left:
+        m.pending = None
+    if left:
+        raise RuntimeError("torchmd-net_amd: the ET stack's second-order cotangents were not consumed by the "
+                           "forward node's backward (engine order); the parameter gradients are incomplete")
 
 
 def _will_run(node):

@@ -1886,4 +1886,7 @@ def mse2(a1, b1, a2, b2, w1, w2):
     nat.require_gpu(a1, "mse2")
     if a1.shape != b1.shape or a2.shape != b2.shape:
         raise ValueError("mse2: prediction and target shapes differ")
+    for t in (b1, a2, b2):  # the kernel reads all four through a1's dtype on a1's device
+        if t.dtype != a1.dtype or t.device != a1.device:
+            raise ValueError("mse2: all four tensors must be on one device and of one dtype")
     return _MSE2.apply(a1, b1.detach(), a2, b2.detach(), w1, w2)

@@ -162,8 +162,17 @@ class TorchMD_Net(nn.Module):
         if t is None:
             t = torch.full_like(y, -1.0)
             if not (y.is_cuda and torch.cuda.is_current_stream_capturing()):
+                if len(cache) >= 8:  # bounded: MD / inference over varying molecule counts
+                    cache.pop(next(iter(cache)))
                 cache[key] = t
         return t
+
+    @torch.jit.unused
+    def __getstate__(self):
+        # the force-seed cache is device scratch, not model state (torch.save / deepcopy)
+        state = self.__dict__.copy()
+        state.pop("_seed_cache", None)
+        return state
 
     def forward(self, z: Tensor, pos: Tensor, batch: Optional[Tensor] = None, q: Optional[Tensor] = None,
                 s: Optional[Tensor] = None, extra_args: Optional[Dict[str, Tensor]] = None

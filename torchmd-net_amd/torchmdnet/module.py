@@ -21,7 +21,7 @@ import torch.distributed as dist
 from torch.nn.functional import l1_loss, mse_loss
 
 from .models.model import create_model, load_model
-from .et_stack import second_order_expected
+from .et_stack import check_pending_consumed, second_order_expected
 from .training import GradAllReduce
 
 DEFAULTS = dict(charge=False, spin=False, load_model=None, lr=4e-4, weight_decay=0.0, lr_factor=0.8,
@@ -172,6 +172,7 @@ def fit(lnnp, datamodule, epochs, device, group=None, test_interval=0, log=None,
             loss = lnnp.training_step(b, i)
             params = reduce.params
             loss.backward(inputs=params)
+            check_pending_consumed()
             reduce()
             lnnp.optimizer_step(opt)
         lnnp.model.eval()

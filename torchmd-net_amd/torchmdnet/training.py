@@ -17,6 +17,7 @@ import torch.distributed as dist
 import torch.nn.functional as F
 
 from . import kernels
+from . import et_stack
 from .et_stack import second_order_expected
 
 
@@ -118,7 +119,8 @@ class LNNPStep:
         if y.ndim == 1:  # reference module.py:147-148
             y = y.unsqueeze(1)
         if (self.y_weight > 0 and self.neg_dy_weight > 0 and pred_neg_dy is not None and pred.is_cuda
-                and pred.shape == y.shape and pred_neg_dy.shape == neg_dy.shape):
+                and pred.shape == y.shape and pred_neg_dy.shape == neg_dy.shape
+                and all(t.dtype == pred.dtype and t.device == pred.device for t in (y, pred_neg_dy, neg_dy))):
             # both terms in one launch (and one for their backward): kernels.mse2
             return kernels.mse2(pred, y, pred_neg_dy, neg_dy, self.y_weight, self.neg_dy_weight)
         loss = 0.0
@@ -133,6 +135,7 @@ class LNNPStep:
         # accumulating a position gradient nobody reads is wasted work -- and under HIP-graph
         # capture the positions' AccumulateGrad would run across streams
         loss.backward(inputs=self.reduce.params)
+        et_stack.check_pending_consumed()
 
     def _warmup_lr(self):
         if self.lr_warmup_steps and self.global_step < self.lr_warmup_steps:
