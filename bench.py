@@ -258,6 +258,8 @@ def probe_workload(n_atoms, H, dev):
     launch.pairs = launch_pairs
     launch.bwd = launch_bwd
     launch.n_pairs = P
+    launch.graph, launch.inputs = graph, (q, k, v, vec, C, u)
+    launch.pair_row, launch.pair_edge = pair_row, pair_edge
     return launch, E, L
 
 

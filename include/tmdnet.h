@@ -194,7 +194,8 @@ int tmdnet_et_message_bwd(int dtype, int n_nodes, int hidden, int heads, const i
                           const int32_t* pk_rows, const int32_t* order,
                           void* stream);  /* accumulate may also carry TMDNET_ET_V_PLANAR */
 /* "dr mode" of the backward (gdist non-NULL; with TMDNET_ACC_EDGE it accumulates, without it overwrites): instead of storing gpk / gpv
- * (then normally NULL), the projection gradient of every edge is contracted in-kernel with dpk = d pk / d r,
+ * (then normally NULL), the projection gradient of every edge is contracted in-kernel with dpk = d pk / d r
+ * (dpk / dpv rows are read with ld_pk / ld_pv),
  * dpv = d pv / d r (rows and layout of pk / pv, read through pk_rows) and accumulated into
  * gdist[e] -- the force pass then needs neither the E x 4H gradient nor its GEMM.  gpk / gpv non-NULL
  * in dr mode: the projection gradient is stored as well (the recorded force pass of force-matching
@@ -520,6 +521,29 @@ int tmdnet_embedding_bwd_f32(int n, int H, int num_types, const int64_t* z, int 
 int tmdnet_proj_split_f32(int N, int K, const void* W, int ldw, void* Wp, void* stream);
 int tmdnet_proj_f32(int M, int N, int K, const void* A, int lda, const void* Wp, long long piece_stride,
                     const void* bias, void* C, int ldc, void* stream);
+
+/* The ET message with the dk/dv projection FUSED in (large graphs; reference torchmd_et.py:282-291 +
+ * :314-347, the RBF of models/utils.py:272-344 evaluated in-kernel): tmdnet_et_message_fwd's outputs
+ * without the projection rows.  Per 16-edge tile the RBF values of the distances r[e] are formed in
+ * registers and multiplied on the fp16 MFMA by the layer's weight, held in LDS for the whole launch as
+ * the image made by tmdnet_fep_split_f32 (two fp16 pieces per value after exact power-of-two scaling:
+ * fp32-GEMM accuracy).
+ *   tmdnet_fep_split_f32: W [D][R] (ldw) = the layer's [dk | dv] rows in the planar order (dk, then the
+ *     x, v1, v2 H-blocks of dv), bias [D] (nullable) -> img (tmdnet_fep_image_bytes(D, R), 16-byte
+ *     aligned), wsc [D] (accumulator scale per row), bias_out [D].
+ *   tmdnet_et_fused_fwd_f32: fp32 only; H = 128, heads = 8 (d = 16), R = 32 or 64, v in the planar
+ *     layout (TMDNET_ET_V_PLANAR), both projections present (distance_influence "both"); vec_in
+ *     nullable (layer 0); mu / beta: the RBF means / betas (gauss: offsets / coeff[0]).  Else
+ *     TMDNET_UNSUPPORTED.  One workgroup per CU (its LDS), deterministic, no atomics on outputs. */
+size_t tmdnet_fep_image_bytes(int D, int R);
+int tmdnet_fep_split_f32(int D, int R, const void* W, int ldw, const void* bias, void* img, void* wsc,
+                         void* bias_out, void* stream);
+int tmdnet_et_fused_fwd_f32(int n_nodes, int hidden, int heads, int num_rbf, const int32_t* row_ptr,
+                            const int32_t* src, int max_pairs, const void* q, int ld_q, const void* k, int ld_k,
+                            const void* v, int ld_v, const void* vec_in, const void* dist, const void* cutoff,
+                            const void* unit, const void* img, const void* wsc, const void* bias, const void* mu,
+                            const void* beta, double cutoff_lower, double cutoff_upper, int rbf_type,
+                            void* x_out, void* vec_out, void* stream);
 
 /* Energy + force MSE training loss (reference LNNP.step, module.py:130-179, mean reductions):
  *   out[0] = w1 * mean((a1 - b1)^2) + w2 * mean((a2 - b2)^2)   over n1 / n2 elements (one launch),

@@ -122,6 +122,11 @@ BATCH_DKV_BYTES = 2 << 30
 PLANAR_MIN_EDGES = 131072
 # dk/dv projection rows shared by the two directions of an edge pair (halves the projection GEMM)
 PAIR_ROWS = True
+# dk/dv projection FUSED into the forward edge kernel (tmdnet_et_fused_fwd_f32) on planar-layout graphs
+# (>= PLANAR_MIN_EDGES edges) with a fixed RBF basis of r: the projection rows are never written (C5:
+# 2.8 GB per layer, read back once per direction by the unfused kernel).  A backward that needs them
+# forms them then (_act_pkv).  TMDNET_FEP=0 turns it off.
+FEP = os.environ.get("TMDNET_FEP", "auto")
 # "dr mode" force pass (see _backward_layers): on whenever the force pass needs no weight gradient
 # and the features are a fixed basis of r (also under create_graph, which the reference force pass
 # always uses: the second order then re-forms f from r by the composite basis).  Measured on
@@ -228,6 +233,7 @@ class _Meta:
         self.out_norm = False   # the model's final LayerNorm fused into the last epilogue (2 trailing params)
         self.f_pairs = None     # f at the pair rows, when the caller produced it with the features
         self.dkv_wp = None      # the bf16 split of dkv_eff[0] (dkv_split), once per forward
+        self.fep = False        # the forward runs the fused-projection edge kernel (FEP)
 
     def split(self, params):
         return [params[i * self.np:(i + 1) * self.np] for i in range(self.n_layers)]
@@ -321,7 +327,29 @@ def _ln_bwd_epi(g_xn, x, mean, rstd, ln_w, g_res, g_vec, vecp, o, g_vecp, g_o, w
     return g_x
 
 
-def _forward_layers(meta, x, f, C, u, params):
+def _pair_f(meta, f):
+    """The edge features at the projection rows (the pair rows when the graph has them)."""
+    if meta.pairs is None:
+        return f
+    return meta.f_pairs if meta.f_pairs is not None else f.index_select(0, meta.pairs[1])
+
+
+def _act_pkv(meta, acts, l, f):
+    """Layer l's forward activations, with its projection rows formed now if the fused forward (FEP)
+    skipped them (a backward that contracts them: training form, or the unfused dr-mode pass)."""
+    a = acts[l]
+    if a[7] is None and meta.fep and meta.D:
+        if meta.batched:  # every layer's rows in one GEMM, as the unfused forward lays them out: the
+            # message backward reads d(dk,dv)/dr with the projection rows' leading dimension
+            pkv_all, D = meta.dkv_proj(_pair_f(meta, f)), meta.D
+            for j in range(meta.n_layers):
+                acts[j] = acts[j][:7] + (pkv_all[:, j * D:(j + 1) * D],) + acts[j][8:]
+        else:
+            acts[l] = a[:7] + (meta.dkv_proj(_pair_f(meta, f), l),) + a[8:]
+    return acts[l]
+
+
+def _forward_layers(meta, x, f, C, u, params, r=None):
     """HIP/GEMM forward; returns outputs and the per-layer activations the backward needs."""
     H = meta.H
     N = x.shape[0]
@@ -331,10 +359,9 @@ def _forward_layers(meta, x, f, C, u, params):
     meta.refresh_effective()
     # the projections depend on |r| only: one row per edge PAIR ((E + N) / 2 rows), read by both
     # directions through pk_rows (bit-identical to the per-edge projection)
-    fp = f
-    if D and meta.pairs is not None:
-        fp = meta.f_pairs if meta.f_pairs is not None else f.index_select(0, meta.pairs[1])
-    pkv_all = meta.dkv_proj(fp) if (meta.batched and D) else None
+    fep = meta.fep and r is not None
+    fp = _pair_f(meta, f) if (D and not fep) else f
+    pkv_all = meta.dkv_proj(fp) if (meta.batched and D and not fep) else None
     layers = meta.split(params)
     L = len(layers)
     od = dict(dtype=x.dtype, device=x.device)
@@ -357,16 +384,22 @@ def _forward_layers(meta, x, f, C, u, params):
             vecp = torch.empty((N, 3, 3 * H), dtype=x.dtype, device=x.device)
             probs.append((vec.view(3 * N, H), vec_w, True, None, vecp.view(3 * N, 3 * H), False))
         kernels.gemm_group(probs)
-        if pkv_all is not None:
-            pkv = pkv_all[:, l * D:(l + 1) * D]
-        else:
-            pkv = meta.dkv_proj(fp, l) if dkv_w is not None else None
-        pk = pkv[:, :H] if meta.hk else None
-        pv = pkv[:, H * int(meta.hk):] if meta.hv else None
         xa = xa_all[l]
         veca = torch.empty((N, 3, H), dtype=x.dtype, device=x.device)
-        kernels.et_message_fwd_launch(qkv[:, :H], qkv[:, H:2 * H], qkv[:, 2 * H:], vec, pk, pv, C, u,
-                                      meta.graph, meta.heads, xa, veca, meta.flags, meta.pk_rows)
+        if fep:  # projection fused into the edge kernel: no rows written
+            pkv = None
+            kernels.et_fused_fwd_launch(qkv[:, :H], qkv[:, H:2 * H], qkv[:, 2 * H:], vec, r, C, u,
+                                        kernels.fep_split(dkv_w, dkv_b), meta.rbf, meta.graph, meta.heads, xa,
+                                        veca)
+        else:
+            if pkv_all is not None:
+                pkv = pkv_all[:, l * D:(l + 1) * D]
+            else:
+                pkv = meta.dkv_proj(fp, l) if dkv_w is not None else None
+            pk = pkv[:, :H] if meta.hk else None
+            pv = pkv[:, H * int(meta.hk):] if meta.hv else None
+            kernels.et_message_fwd_launch(qkv[:, :H], qkv[:, H:2 * H], qkv[:, 2 * H:], vec, pk, pv, C, u,
+                                          meta.graph, meta.heads, xa, veca, meta.flags, meta.pk_rows)
         o = torch.empty((N, o_w.shape[0]), dtype=x.dtype, device=x.device)
         kernels.gemm_group([(xa, o_w, True, o_b, o, False)])
         acts.append((x, vec, xn, mean, rstd, qkv, vecp, pkv, xa, o))
@@ -474,7 +507,7 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws, r=None, dr=Fa
         gX = gX + x_top
     for l in reversed(range(meta.n_layers)):
         p = layers[l]
-        x, vec, xn, mean, rstd, qkv, vecp, pkv, xa, o_ = acts[l]
+        x, vec, xn, mean, rstd, qkv, vecp, pkv, xa, o_ = _act_pkv(meta, acts, l, f)
         ln_w, ln_b = p[0], p[1]
         vec_w, o_w = p[8], p[9]
         qkv_w, _ = meta.qkv_eff[l]
@@ -903,7 +936,7 @@ def _second_order(ctx, ggs, want):
     for l in range(L):
         p = layers[l]
         R = rec[l]
-        x_l, vec_l, xn, mean, rstd, qkv, vecp, pkv, xa, o_ = acts[l]
+        x_l, vec_l, xn, mean, rstd, qkv, vecp, pkv, xa, o_ = _act_pkv(meta, acts, l, f)
         vec_w, o_w = p[8], p[9]
         qkv_w = meta.qkv_eff[l][0]
         # the two input-side transposes in one grouped launch: gb_gqkv = gb_gxn qkv_w^T, gb_gvecp =
@@ -1098,7 +1131,7 @@ def _will_run(node):
 class _ETStack(Function):
     @staticmethod
     def forward(ctx, meta, x, f, C, u, r, *params):
-        x_out, vec_out, acts = _forward_layers(meta, x, f, C, u, params)
+        x_out, vec_out, acts = _forward_layers(meta, x, f, C, u, params, r=r)
         ctx.meta = meta
         ctx.acts = acts
         meta.fwd_node = weakref.ref(ctx)  # the second order hands its injections to this node's backward
@@ -1280,6 +1313,8 @@ def et_stack(layers, x, graph, f, C, u, rbf=None, out_norm=None, f_pairs=None):
     if rbf is not None and D:
         r, mu, beta, cl, cu, rbf_type = rbf
         meta.rbf = (mu.detach(), beta.detach(), float(cl), float(cu), int(rbf_type))
+        meta.fep = (FEP not in ("0", "off") and meta.planar and hk and hv and x.is_cuda
+                    and kernels.fep_supported(H, heads, mu.shape[0], x.dtype) and r.dtype == x.dtype)
     x = x.contiguous()
     f = f.contiguous() if (hk or hv) else None
     return _ETStack.apply(meta, x, f, C.contiguous(), u.contiguous(), r, *params)

@@ -564,9 +564,55 @@ def et_message_fwd_launch(q, k, v, vec, pk, pv, C, u, graph, heads, xo, vo, flag
         probe.append((ev0, ev1, graph.n_edges, N, H))
 
 
+def fep_split(W, b):
+    """The fused-projection weight image of one layer (``tmdnet_fep_split_f32``): W [D, R] = the
+    layer's [dk | dv] rows in the planar order, b [D].  Returns (img, wsc, bias) device tensors."""
+    lib = nat.load()
+    D, R = W.shape
+    img = torch.empty(int(lib.tmdnet_fep_image_bytes(D, R)) // 2, dtype=torch.float16, device=W.device)
+    wsc = torch.empty(D, dtype=torch.float32, device=W.device)
+    bo = torch.empty(D, dtype=torch.float32, device=W.device)
+    rc = lib.tmdnet_fep_split_f32(D, R, nat.ptr(W), _ld(W), nat.ptr(b), nat.ptr(img), nat.ptr(wsc), nat.ptr(bo),
+                                  nat.stream(W.device))
+    nat.check(rc, "tmdnet_fep_split_f32")
+    return img, wsc, bo
+
+
+def fep_supported(H, heads, R, dtype):
+    """Shapes / dtype the fused dk/dv projection kernels take (tmdnet_et_fused_fwd_f32)."""
+    return H == 128 and heads == 8 and R in (32, 64) and dtype == torch.float32
+
+
+def et_fused_fwd_launch(q, k, v, vec, r, C, u, fep, rbf, graph, heads, xo, vo):
+    """One ``tmdnet_et_fused_fwd_f32`` launch: the ET message with the dk/dv projection fused in
+    (``fep`` = fep_split(W, b) of the layer; ``rbf`` = (mu, beta, cutoff_lower, cutoff_upper, type));
+    v in the planar layout."""
+    lib = nat.load()
+    N, H = q.shape
+    mu, beta, cl, cu, rt = rbf
+    img, wsc, bo = fep
+    probe = EVENT_PROBE
+    if probe is not None:
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record()
+    rc = lib.tmdnet_et_fused_fwd_f32(N, H, heads, mu.shape[0], nat.ptr(graph.row_ptr), nat.ptr(graph.src),
+                                     graph.n_edges, nat.ptr(q), _ld(q), nat.ptr(k), _ld(k), nat.ptr(v), _ld(v),
+                                     nat.ptr(vec), nat.ptr(r), nat.ptr(C), nat.ptr(u), nat.ptr(img), nat.ptr(wsc),
+                                     nat.ptr(bo), nat.ptr(mu), nat.ptr(beta), float(cl), float(cu), int(rt),
+                                     nat.ptr(xo), nat.ptr(vo), nat.stream(q.device))
+    nat.check(rc, "tmdnet_et_fused_fwd_f32")
+    if probe is not None:
+        ev1.record()
+        probe.append((ev0, ev1, graph.n_edges, N, H))
+
+
 def et_message_bwd_launch(q, k, v, vec, pk, pv, C, u, graph, heads, gx, gvec, gq, gk, gv, gw, gpk,
                           gpv, gC, gu, accumulate=0, pk_rows=None, dpk=None, dpv=None, g_r=None):
-    """dr mode (g_r given): gpk / gpv stay None and <g_pk, dpk> + <g_pv, dpv> accumulates into g_r."""
+    """dr mode (g_r given): gpk / gpv stay None and <g_pk, dpk> + <g_pv, dpv> accumulates into g_r
+    (dpk / dpv are read with pk's / pv's leading dimensions)."""
+    if (dpk is not None and pk is not None and dpk.stride(0) != pk.stride(0)) or \
+            (dpv is not None and pv is not None and dpv.stride(0) != pv.stride(0)):
+        raise ValueError("et_message_bwd: dpk / dpv must have the row stride of pk / pv")
     lib = nat.load()
     N, H = q.shape
     rc = lib.tmdnet_et_message_bwd(
