@@ -35,6 +35,10 @@ $(DBGLIB): $(DBGOBJS)
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $(DBGOBJS) -o $@
 
+# the fused edge kernels: no SLP packing of f32 math (v_pk_* beside MFMAs costs issue cycles and,
+# here, registers: 416 -> 213 VGPR+AGPR for the unrolled variant)
+build/hip/et_fused.o build/hip_dbg/et_fused.o: HIPFLAGS += -fno-slp-vectorize
+
 build/hip/%.o: $(PKG)/csrc/%.hip $(wildcard $(PKG)/csrc/*.h) include/tmdnet.h
 	@mkdir -p build/hip
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@

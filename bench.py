@@ -714,19 +714,34 @@ def _cpu_sd(model):
     return {k: v.detach().cpu() for k, v in model.state_dict().items()}
 
 
+def cpu_threads(info):
+    """the CPU path on ALL physical host cores (torch.set_num_threads(n_phys)), within
+    the CPUs this process may use; the OMP_NUM_THREADS share of the box is timed beside it."""
+    phys = info["physical_cores_machine"] or info["affinity_cpus"]
+    return max(1, min(phys, info["affinity_cpus"]))
+
+
 def cpu_baseline(model, args, z, pos, batch, seconds):
-    """C2 energy + forces with oracle/model_oracle.py on the host cores (the headline CPU line).
-    Threads: every CPU this process may use, capped by the box's OMP_NUM_THREADS share."""
+    """C2 energy + forces with oracle/model_oracle.py on the host cores (the headline CPU line), on all
+    physical cores; the same sample at the box's OMP_NUM_THREADS share is recorded beside it."""
     from oracle import model_oracle as O
     info = host_cpu_info()
-    cores = info["threads_used"]
-    torch.set_num_threads(cores)
+    cores = cpu_threads(info)
     sd = _cpu_sd(model)
+    mols = int(batch.max()) + 1
+    share = info["threads_used"]
+    share_line = None
+    if share != cores:
+        torch.set_num_threads(share)
+        n_s, el_s = _time_cpu(lambda: O.energy_forces(sd, dict(args), z, pos, batch, dtype=torch.float32,
+                                                         create_graph=True), seconds / 2)
+        share_line = {"value": round(mols * n_s / el_s, 2), "unit": "molecules/s", "cores": share,
+                      "sample": f"{n_s} calls, {el_s:.1f} s"}
+    torch.set_num_threads(cores)
     n, el = _time_cpu(lambda: O.energy_forces(sd, dict(args), z, pos, batch, dtype=torch.float32,
                                                  create_graph=True), seconds)
-    mols = int(batch.max()) + 1
     return {"value": round(mols * n / el, 2), "unit": "molecules/s", "cores": cores, "kind": "port",
-            "host": info,
+            "host": info, "omp_share": share_line,
             "calibration": "profiles/r02_cpu_calibration.json (restatement vs the shimmed reference, same "
                            "8 cores of the build container)",
             "sample": f"oracle/model_oracle.py (PyTorch-CPU restatement of the reference ET path), "

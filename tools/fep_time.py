@@ -68,6 +68,11 @@ def main():
     def fused():
         kernels.et_fused_fwd_launch(q, k, v, vec, r, C, u, fep, (mu, beta, cl, cu, 0), g, 8, xo1, vo1)
 
+    if len(sys.argv) > 3 and sys.argv[3] == "fused_only":  # profiling: the fused launches alone
+        for _ in range(10):
+            fused()
+        torch.cuda.synchronize()
+        return
     unfused_msg()
     fused()
     torch.cuda.synchronize()

@@ -117,11 +117,12 @@ __device__ __forceinline__ rsrc_t make_rsrc(const void* p, unsigned bytes) {
 __device__ __forceinline__ float bld(rsrc_t r, int off) {
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
 }
+constexpr int kOOB = 0x7FFFFF00;  // a byte offset past every resource's range (buffer loads return 0)
 struct Gat {
   float kk[4], vx[4], v1[4], v2[4], w0[4], w1[4], w2[4];
 };
 struct Src {
-  rsrc_t k, v, vec;
+  rsrc_t q, k, v, vec;
   int ok[4], ov[4], ow[4];  // byte offsets of the lane's channel in the four source rows
 };
 // head h's values (byte offset 64 h: 16 channels of 4 bytes; v / vec parts H * 4 = 512 bytes apart)
@@ -182,6 +183,33 @@ __device__ __forceinline__ void gather_dyn(Gat& G, const Src& S, int hb) {
   }
 }
 
+// head values with the head's byte offset in an SGPR (the instruction's soffset): no per-load VALU add
+__device__ __forceinline__ float blds(rsrc_t r, int off, int soff) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, soff, 0));
+}
+__device__ __forceinline__ void gather_s(Gat& G, const Src& S, int soff) {
+  constexpr int PB = kH * 4;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    G.kk[i] = blds(S.k, S.ok[i], soff);
+    G.vx[i] = blds(S.v, S.ov[i], soff);
+    G.v1[i] = blds(S.v, S.ov[i] + PB, soff);
+    G.v2[i] = blds(S.v, S.ov[i] + 2 * PB, soff);
+    G.w0[i] = blds(S.vec, S.ow[i], soff);
+    G.w1[i] = blds(S.vec, S.ow[i] + PB, soff);
+    G.w2[i] = blds(S.vec, S.ow[i] + 2 * PB, soff);
+  }
+}
+template <int K, int N> __device__ __forceinline__ void rotate_by(float (&a)[N]) {
+  float t[K];
+#pragma unroll
+  for (int i = 0; i < K; ++i) t[i] = a[i];
+#pragma unroll
+  for (int i = 0; i + K < N; ++i) a[i] = a[i + K];
+#pragma unroll
+  for (int i = 0; i < K; ++i) a[N - K + i] = t[i];
+}
+
 template <int N> __device__ __forceinline__ void rotate(float (&a)[N]) {
   const float f = a[0];
 #pragma unroll
@@ -218,7 +246,7 @@ template <int KS>
 __device__ __forceinline__ void head_math(const Gat& X, const char* wt, const int (&wb)[KS], const float* sct,
                                           const float* sbt, int h, const h8 (&A0)[KS], const h8 (&A1)[KS], int lane,
                                           float qh, const float (&Ce)[4], const float (&ux)[4], const float (&uy)[4],
-                                          const float (&uz)[4], const float (&m)[4], float& ax, float& a0, float& a1,
+                                          const float (&uz)[4], float& ax, float& a0, float& a1,
                                           float& a2) {
   const f4 pk = block_pre<KS>(wt, wb, sct, sbt, h, A0, A1, lane);
   const f4 px = block_pre<KS>(wt, wb, sct, sbt, 8 + h, A0, A1, lane);
@@ -230,7 +258,7 @@ __device__ __forceinline__ void head_math(const Gat& X, const char* wt, const in
     const float att = row_sum16(qh * X.kk[i] * dk);
     const float a = Silu<float>(att).s * Ce[i];
     ax += X.vx[i] * Silu<float>(px[i]).s * a;
-    const float v1e = X.v1[i] * Silu<float>(p1[i]).s * m[i];
+    const float v1e = X.v1[i] * Silu<float>(p1[i]).s;
     const float v2e = X.v2[i] * Silu<float>(p2[i]).s;
     a0 += X.w0[i] * v1e + v2e * ux[i];
     a1 += X.w1[i] * v1e + v2e * uy[i];
@@ -265,6 +293,7 @@ __global__ __launch_bounds__(NW * 64, 1) void k_fwd(Fwd P) {
   const int n0 = lb * per, n1 = min(P.n, n0 + per);
   const int lane = lane_id(), c = lane & 15, g = lane >> 4;
   Src S;
+  S.q = make_rsrc(P.q, (unsigned)P.n * P.ldq * 4u);
   S.k = make_rsrc(P.k, (unsigned)P.n * P.ldk * 4u);
   S.v = make_rsrc(P.v, (unsigned)P.n * P.ldv * 4u);
   S.vec = make_rsrc(P.vec, P.vec ? (unsigned)P.n * 3u * H * 4u : 0u);
@@ -274,6 +303,7 @@ __global__ __launch_bounds__(NW * 64, 1) void k_fwd(Fwd P) {
     t = __builtin_amdgcn_readfirstlane(__shfl(t, 0)) + n0;
     if (t >= n1) break;
     const int rb = min(P.row_ptr[t], P.cap), re = min(P.row_ptr[t + 1], P.cap);
+    const int oq = (t * P.ldq + c) * 4;
     float qh[kHeads], ax[kHeads], a0[kHeads], a1[kHeads], a2[kHeads];
 #pragma unroll
     for (int h = 0; h < kHeads; ++h) {
@@ -303,21 +333,22 @@ __global__ __launch_bounds__(NW * 64, 1) void k_fwd(Fwd P) {
       }
       // the lane's four output edges (base + 4 g + i): source, cutoff, unit vector (0 past the row)
       int s[4];
-      float Ce[4], ux[4], uy[4], uz[4], m[4];
+      float Ce[4], ux[4], uy[4], uz[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int e = base + 4 * g + i;
         const bool ok = e < re;
-        s[i] = ok ? P.src[e] : t;
+        s[i] = ok ? P.src[e] : 0;
         TMD_DCHECK(s[i] >= 0 && s[i] < P.n);
-        S.ok[i] = (s[i] * P.ldk + c) * 4;
-        S.ov[i] = (s[i] * P.ldv + c) * 4;
-        S.ow[i] = (s[i] * 3 * H + c) * 4;
+        // an edge past the row gathers from beyond the resources' ranges: its loads return 0, so
+        // its k, v and vec terms vanish without masks
+        S.ok[i] = ok ? (s[i] * P.ldk + c) * 4 : kOOB;
+        S.ov[i] = ok ? (s[i] * P.ldv + c) * 4 : kOOB;
+        S.ow[i] = ok ? (s[i] * 3 * H + c) * 4 : kOOB;
         Ce[i] = ok ? P.C[e] : 0.f;
         ux[i] = ok ? P.u[3 * (size_t)e] : 0.f;
         uy[i] = ok ? P.u[3 * (size_t)e + 1] : 0.f;
         uz[i] = ok ? P.u[3 * (size_t)e + 2] : 0.f;
-        m[i] = ok ? 1.f : 0.f;
       }
       // heads unrolled; the source gathers of head h + 1 are issued before head h's MFMAs and math
       // (two register sets), and the scheduler may not mix heads (one head's registers live at a time)
@@ -340,16 +371,33 @@ __global__ __launch_bounds__(NW * 64, 1) void k_fwd(Fwd P) {
         static_for<kHeads>([&](auto hc) {
           constexpr int h = decltype(hc)::value;
           if constexpr (h + 1 < kHeads) gather<64 * (h + 1)>(G[(h + 1) & 1], S);
-          head_math<KS>(G[h & 1], wt, wb, sct, sbt, h, A0, A1, lane, qh[h], Ce, ux, uy, uz, m, ax[h], a0[h], a1[h],
+          head_math<KS>(G[h & 1], wt, wb, sct, sbt, h, A0, A1, lane, qh[h], Ce, ux, uy, uz, ax[h], a0[h], a1[h],
                         a2[h]);
           __builtin_amdgcn_sched_barrier(0);
         });
+      } else if constexpr (MODE == 3) {
+        // heads in pairs: the pair's loads carry the head offset in an SGPR, q is re-read per head (L1),
+        // the four accumulator arrays rotate by two per pair
+#pragma unroll 1
+        for (int hp = 0; hp < kHeads; hp += 2) {
+          const int sh = __builtin_amdgcn_readfirstlane(64 * hp);
+          Gat X0, X1;
+          gather_s(X0, S, sh);
+          gather_s(X1, S, sh + 64);
+          const float q0 = blds(S.q, oq, sh), q1 = blds(S.q, oq + 64, sh);
+          const char* wtp = wt + hp * 16 * R * (int)sizeof(_Float16);
+          head_math<KS>(X0, wtp, wb, sct + 16 * hp, sbt + 16 * hp, 0, A0, A1, lane, q0, Ce, ux, uy, uz, ax[0],
+                        a0[0], a1[0], a2[0]);
+          head_math<KS>(X1, wtp, wb, sct + 16 * hp, sbt + 16 * hp, 1, A0, A1, lane, q1, Ce, ux, uy, uz, ax[1],
+                        a0[1], a1[1], a2[1]);
+          rotate_by<2>(ax); rotate_by<2>(a0); rotate_by<2>(a1); rotate_by<2>(a2);
+        }
       } else {
 #pragma unroll 1
         for (int h = 0; h < kHeads; ++h) {
           Gat X;
           gather_dyn(X, S, 64 * h);
-          head_math<KS>(X, wt, wb, sct, sbt, h, A0, A1, lane, qh[0], Ce, ux, uy, uz, m, ax[0], a0[0], a1[0], a2[0]);
+          head_math<KS>(X, wt, wb, sct, sbt, h, A0, A1, lane, qh[0], Ce, ux, uy, uz, ax[0], a0[0], a1[0], a2[0]);
           rotate(qh); rotate(ax); rotate(a0); rotate(a1); rotate(a2);
         }
       }
@@ -431,14 +479,17 @@ extern "C" int tmdnet_et_fused_fwd_f32(int n, int H, int heads, int R, const int
   P.alpha = (float)(5.0 / (cutoff_upper - cutoff_lower));
   P.xo = (float*)x_out; P.veco = (float*)vec_out;
   const int nwg = fep::num_cus();
-  // tuning (TMDNET_FEP_MODE): 0 = unrolled heads, one wave per SIMD; 1 = rolled heads, two per SIMD
-  static const int mode = getenv("TMDNET_FEP_MODE") ? atoi(getenv("TMDNET_FEP_MODE")) : 1;
+  // tuning (TMDNET_FEP_MODE): 0 = unrolled heads, one wave per SIMD; 1 = rolled heads, two per SIMD;
+  // 2 = unrolled, two per SIMD; 3 = heads in pairs with SGPR head offsets
+  static const int mode = getenv("TMDNET_FEP_MODE") ? atoi(getenv("TMDNET_FEP_MODE")) : 2;
   hipStream_t st = (hipStream_t)stream;
 #define TMD_FEP(KS_, NW_, M_) hipLaunchKernelGGL((fep::k_fwd<KS_, NW_, M_>), dim3(nwg), dim3(NW_ * 64), 0, st, P)
   if (R == 64) {
-    if (mode == 0) TMD_FEP(2, 4, 0); else if (mode == 2) TMD_FEP(2, 8, 0); else TMD_FEP(2, 8, 1);
+    if (mode == 0) TMD_FEP(2, 4, 0); else if (mode == 2) TMD_FEP(2, 8, 0); else if (mode == 3) TMD_FEP(2, 8, 3);
+    else TMD_FEP(2, 8, 1);
   } else {
-    if (mode == 0) TMD_FEP(1, 4, 0); else if (mode == 2) TMD_FEP(1, 8, 0); else TMD_FEP(1, 8, 1);
+    if (mode == 0) TMD_FEP(1, 4, 0); else if (mode == 2) TMD_FEP(1, 8, 0); else if (mode == 3) TMD_FEP(1, 8, 3);
+    else TMD_FEP(1, 8, 1);
   }
 #undef TMD_FEP
   return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
