@@ -534,7 +534,10 @@ int tmdnet_proj_f32(int M, int N, int K, const void* A, int lda, const void* Wp,
  *   tmdnet_et_fused_fwd_f32: fp32 only; H = 128, heads = 8 (d = 16), R = 32 or 64, v in the planar
  *     layout (TMDNET_ET_V_PLANAR), both projections present (distance_influence "both"); vec_in
  *     nullable (layer 0); mu / beta: the RBF means / betas (gauss: offsets / coeff[0]).  Else
- *     TMDNET_UNSUPPORTED.  One workgroup per CU (its LDS), deterministic, no atomics on outputs. */
+ *     TMDNET_UNSUPPORTED.  One workgroup per CU (its LDS), deterministic, no atomics on outputs.
+ *     pkv_out (nullable): the pre-activation [dk | dv] rows are also written, for the canonical edge
+ *     (src >= dst) of every pair, to row pk_rows[e] of pkv_out [n_pair_rows][ld_pkv] -- the rows an
+ *     unfused backward reads (tmdnet_et_message_bwd with pk_rows). */
 size_t tmdnet_fep_image_bytes(int D, int R);
 int tmdnet_fep_split_f32(int D, int R, const void* W, int ldw, const void* bias, void* img, void* wsc,
                          void* bias_out, void* stream);
@@ -543,7 +546,23 @@ int tmdnet_et_fused_fwd_f32(int n_nodes, int hidden, int heads, int num_rbf, con
                             const void* v, int ld_v, const void* vec_in, const void* dist, const void* cutoff,
                             const void* unit, const void* img, const void* wsc, const void* bias, const void* mu,
                             const void* beta, double cutoff_lower, double cutoff_upper, int rbf_type,
-                            void* x_out, void* vec_out, void* stream);
+                            void* x_out, void* vec_out, void* pkv_out, int ld_pkv, const int32_t* pk_rows,
+                            long long n_pair_rows, void* stream);
+
+/* The fused message's first-order backward for the force pass ("dr mode", reference: the autograd of
+ * torchmd_et.py:282-291, :314-347 through f = rbf(r)): d pre / d r = W f'(r) is formed on the MFMA per
+ * tile beside the projection (both from the tmdnet_fep_split_f32 image), and the projection gradient is
+ * contracted with it in registers: gdist[e] = <g_pre, d pre / d r>.  Outputs as tmdnet_et_message_bwd in
+ * dr mode (destination pass: gq, gcut, gunit, gdist; source pass over the reversed edges: gk, gv
+ * (planar), gvec_in), with its accumulate bits (TMDNET_ACC_VEC_RESIDUAL / _EDGE / _GRADS).  Same
+ * envelope as tmdnet_et_fused_fwd_f32; requires a symmetric edge list. */
+int tmdnet_et_fused_bwd_f32(int n_nodes, int hidden, int heads, int num_rbf, const int32_t* row_ptr,
+                            const int32_t* src, int max_pairs, const void* q, int ld_q, const void* k, int ld_k,
+                            const void* v, int ld_v, const void* vec_in, const void* dist, const void* cutoff,
+                            const void* unit, const void* img, const void* wsc, const void* bias, const void* mu,
+                            const void* beta, double cutoff_lower, double cutoff_upper, int rbf_type,
+                            const void* grad_x, const void* grad_vec, void* gq, void* gk, void* gv, void* gvec_in,
+                            void* gcut, void* gunit, void* gdist, int accumulate, void* stream);
 
 /* Energy + force MSE training loss (reference LNNP.step, module.py:130-179, mean reductions):
  *   out[0] = w1 * mean((a1 - b1)^2) + w2 * mean((a2 - b2)^2)   over n1 / n2 elements (one launch),

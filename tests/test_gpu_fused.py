@@ -1,6 +1,7 @@
 """GPU checks of the fused dk/dv projection edge kernels (csrc/et_fused.hip, "FEP"): the ET message with
 the projection (reference torchmd_et.py:282-291) evaluated on the fp16 MFMA inside the edge kernel from
-the distances (the RBF of models/utils.py:272-344 formed in registers), on planar-layout graphs.
+the distances (the RBF of models/utils.py:272-344 formed in registers), on planar-layout graphs -- the
+forward and the force pass's backward (d pre / d r = W f'(r) on the MFMA, contracted in-kernel).
 
 Bars: the fused fp32 model against the SAME weights in fp64 (no fusion at fp64): energies 1e-5, forces
 1e-4 relative (max-abs error over max |value|: the north_star bar; the unfused fp32 path sits at
@@ -49,24 +50,40 @@ def _run(m, z, pos, L, dtype):
                                            (64, "expnorm", 0.5)])
 def test_fused_forward_matches_fp64_and_unfused(R, rbf_type, cl, monkeypatch):
     from torchmdnet import et_stack, kernels
-    calls = []
-    orig = kernels.et_fused_fwd_launch
+    calls, bcalls = [], []
+    orig, origb = kernels.et_fused_fwd_launch, kernels.et_fused_bwd_launch
 
     def counting(*a, **k):
         calls.append(1)
         return orig(*a, **k)
 
+    def counting_b(*a, **k):
+        bcalls.append(1)
+        return origb(*a, **k)
+
     monkeypatch.setattr(kernels, "et_fused_fwd_launch", counting)
+    monkeypatch.setattr(kernels, "et_fused_bwd_launch", counting_b)
+    monkeypatch.setattr(et_stack, "FEP_BWD", "fused")
+    monkeypatch.setattr(et_stack, "FUSED_BWD", True)
     z, pos, L = _water_box(3000)
     m = _model(R, rbf_type, cl)
     sd = m.state_dict()
     y, f = _run(m, z, pos, L, torch.float32)
-    assert len(calls) == 3, "the fused kernel did not run"  # one per layer
+    assert len(calls) == 3 and len(bcalls) == 3, "the fused kernels did not run"  # one per layer each
     m64 = _model(R, rbf_type, cl, precision=64)
     m64.load_state_dict({k: v.double() if v.is_floating_point() else v for k, v in sd.items()})
     y64, f64 = _run(m64, z, pos, L, torch.float64)
     assert _rel(y, y64) < 1e-5
     assert _rel(f, f64) < 1e-4
+    # the fused forward with the unfused force-pass backward: over the pair rows the fused forward wrote
+    # ("rows"), or formed by the GEMM in the backward ("lazy")
+    monkeypatch.setattr(et_stack, "FUSED_BWD", False)
+    for mode in ("rows", "lazy"):
+        monkeypatch.setattr(et_stack, "FEP_BWD", mode)
+        y1, f1 = _run(m, z, pos, L, torch.float32)
+        assert len(bcalls) == 3
+        assert _rel(y, y1) < 1e-6
+        assert _rel(f, f1) < 1e-4
     monkeypatch.setattr(et_stack, "FEP", "0")
     n0 = len(calls)
     y0, f0 = _run(m, z, pos, L, torch.float32)

@@ -47,6 +47,9 @@ def main():
     W = torch.randn(4 * H, R, device=dev, generator=gen) / R ** 0.5
     b = torch.randn(4 * H, device=dev, generator=gen) * 0.1
     q, k, v, vec, C, u = launch.inputs
+    if os.environ.get("FEP_TIME_QKV") == "strided":  # the model's layout: q | k | v views of one [N, 5H] buffer
+        qkv = torch.cat([q, k, v], 1).contiguous()
+        q, k, v = qkv[:, :H], qkv[:, H:2 * H], qkv[:, 2 * H:]
     # unfused: pair-row features -> projection GEMM -> message kernel over pair rows
     pair_row, pair_edge = launch.pair_row, launch.pair_edge
     f_pairs = kernels.rbf_composite(r.index_select(0, pair_edge.long()), mu, beta, cl, cu, 0).contiguous()
@@ -82,13 +85,56 @@ def main():
     t_proj = timed(unfused_proj, reps)
     t_msg = timed(unfused_msg, reps)
     t_fused = timed(fused, reps)
+    # the force-pass backward (dr mode): unfused = d(dk,dv)/dr GEMM over the pair rows + the dst/src passes
+    # reading both row sets; fused = tmdnet_et_fused_bwd_f32 (d pre / d r on the MFMA in-kernel)
+    fdp = kernels.rbf_deriv(r, mu, beta, cl, cu, 0, rows=pair_edge)
+    gen2 = torch.Generator(device=dev).manual_seed(5)
+    gx, gvec = torch.randn(n, H, device=dev, generator=gen2), torch.randn(n, 3, H, device=dev, generator=gen2)
+    def grads():  # gradient buffers with the row strides of q / k / v (the kernels write with them)
+        gqkv = torch.empty(n, q.stride(0), device=dev)
+        if q.stride(0) == H:  # separate contiguous q / k / v
+            gq_, gk_, gv_ = torch.empty(n, H, device=dev), torch.empty(n, H, device=dev), \
+                torch.empty(n, 3 * H, device=dev)
+        else:  # views of one [N, 5H] buffer
+            gq_, gk_, gv_ = gqkv[:, :H], gqkv[:, H:2 * H], gqkv[:, 2 * H:5 * H]
+        return [gq_, gk_, gv_, torch.empty(n, 3, H, device=dev), torch.empty(E, device=dev),
+                torch.empty(E, 3, device=dev), torch.empty(E, device=dev)]
+
+    outs = [grads() for _ in range(2)]
+
+    def unfused_dproj():
+        return kernels.proj(fdp, W, None, wp=wp)
+
+    dpkv = unfused_dproj()
+
+    def unfused_bwd():
+        gq, gk, gv, gw, gC, gu, gr = outs[0]
+        kernels.et_message_bwd_launch(q, k, v, vec, pkv[:, :H], pkv[:, H:], C, u, g, 8, gx, gvec, gq, gk, gv, gw,
+                                      None, None, gC, gu, accumulate=1 | 4, pk_rows=pair_row, dpk=dpkv[:, :H],
+                                      dpv=dpkv[:, H:], g_r=gr)
+
+    def fused_bwd():
+        gq, gk, gv, gw, gC, gu, gr = outs[1]
+        kernels.et_fused_bwd_launch(q, k, v, vec, r, C, u, fep, (mu, beta, cl, cu, 0), g, 8, gx, gvec, gq, gk, gv,
+                                    gw, gC, gu, gr, accumulate=1)
+
+    unfused_bwd()
+    fused_bwd()
+    torch.cuda.synchronize()
+    bwd_err = {nm: float((b - a).abs().max() / a.abs().max()) for nm, a, b in
+               zip("gq gk gv gvec gC gu gr".split(), outs[0], outs[1])}
+    t_dproj = timed(unfused_dproj, reps)
+    t_ubwd = timed(unfused_bwd, reps)
+    t_fbwd = timed(fused_bwd, reps)
     flop = 2.0 * E * R * 4 * H
     out = {"n_atoms": n, "edges": E, "pairs": int(pair_edge.shape[0]), "R": R,
            "max_rel_err_x": err_x, "max_rel_err_vec": err_v,
            "unfused_proj_ms": round(t_proj, 4), "unfused_msg_ms": round(t_msg, 4),
            "unfused_total_ms": round(t_proj + t_msg, 4), "fused_ms": round(t_fused, 4),
            "fused_fp32_equiv_tflops": round(flop / t_fused / 1e9, 1),
-           "fused_f16_mfma_tflops": round(3 * flop / t_fused / 1e9, 1)}
+           "fused_f16_mfma_tflops": round(3 * flop / t_fused / 1e9, 1),
+           "bwd_max_rel_err": bwd_err, "unfused_dproj_ms": round(t_dproj, 4), "unfused_bwd_ms": round(t_ubwd, 4),
+           "unfused_bwd_total_ms": round(t_dproj + t_ubwd, 4), "fused_bwd_ms": round(t_fbwd, 4)}
     print(json.dumps(out))
 
 

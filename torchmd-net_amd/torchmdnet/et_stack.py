@@ -127,6 +127,12 @@ PAIR_ROWS = True
 # 2.8 GB per layer, read back once per direction by the unfused kernel).  A backward that needs them
 # forms them then (_act_pkv).  TMDNET_FEP=0 turns it off.
 FEP = os.environ.get("TMDNET_FEP", "auto")
+# How the backward after a fused forward gets its projection: "rows" = the fused forward also writes
+# the canonical edges' pre-activation pair rows when a backward can follow (grad enabled) and the
+# unfused backward reads them; "fused" = the force-pass (dr mode) backward is fused the same way
+# (tmdnet_et_fused_bwd_f32, no rows at all); "lazy" = the backward forms the rows by the GEMM.
+FEP_BWD = os.environ.get("TMDNET_FEP_BWD", "rows")
+FUSED_BWD = FEP_BWD == "fused"
 # "dr mode" force pass (see _backward_layers): on whenever the force pass needs no weight gradient
 # and the features are a fixed basis of r (also under create_graph, which the reference force pass
 # always uses: the second order then re-forms f from r by the composite basis).  Measured on
@@ -234,6 +240,7 @@ class _Meta:
         self.f_pairs = None     # f at the pair rows, when the caller produced it with the features
         self.dkv_wp = None      # the bf16 split of dkv_eff[0] (dkv_split), once per forward
         self.fep = False        # the forward runs the fused-projection edge kernel (FEP)
+        self.fep_imgs = None    # per layer: its weight image (kernels.fep_split), made by the forward
 
     def split(self, params):
         return [params[i * self.np:(i + 1) * self.np] for i in range(self.n_layers)]
@@ -349,7 +356,7 @@ def _act_pkv(meta, acts, l, f):
     return acts[l]
 
 
-def _forward_layers(meta, x, f, C, u, params, r=None):
+def _forward_layers(meta, x, f, C, u, params, r=None, want_bwd=False):
     """HIP/GEMM forward; returns outputs and the per-layer activations the backward needs."""
     H = meta.H
     N = x.shape[0]
@@ -362,6 +369,11 @@ def _forward_layers(meta, x, f, C, u, params, r=None):
     fep = meta.fep and r is not None
     fp = _pair_f(meta, f) if (D and not fep) else f
     pkv_all = meta.dkv_proj(fp) if (meta.batched and D and not fep) else None
+    # the fused forward writes the pair rows itself when the unfused backward will want them
+    fep_rows = (fep and FEP_BWD == "rows" and want_bwd and meta.pk_rows is not None
+                and meta.pairs is not None)
+    if fep_rows and meta.batched:
+        pkv_all = torch.empty((meta.pairs[1].shape[0], meta.n_layers * D), dtype=x.dtype, device=x.device)
     layers = meta.split(params)
     L = len(layers)
     od = dict(dtype=x.dtype, device=x.device)
@@ -386,11 +398,17 @@ def _forward_layers(meta, x, f, C, u, params, r=None):
         kernels.gemm_group(probs)
         xa = xa_all[l]
         veca = torch.empty((N, 3, H), dtype=x.dtype, device=x.device)
-        if fep:  # projection fused into the edge kernel: no rows written
+        if fep:  # projection fused into the edge kernel (its rows written only for an unfused backward)
             pkv = None
+            if fep_rows:
+                pkv = pkv_all[:, l * D:(l + 1) * D] if pkv_all is not None else \
+                    torch.empty((meta.pairs[1].shape[0], D), dtype=x.dtype, device=x.device)
+            if l == 0:
+                meta.fep_imgs = []
+            meta.fep_imgs.append(kernels.fep_split(dkv_w, dkv_b))
             kernels.et_fused_fwd_launch(qkv[:, :H], qkv[:, H:2 * H], qkv[:, 2 * H:], vec, r, C, u,
-                                        kernels.fep_split(dkv_w, dkv_b), meta.rbf, meta.graph, meta.heads, xa,
-                                        veca)
+                                        meta.fep_imgs[l], meta.rbf, meta.graph, meta.heads, xa, veca,
+                                        pkv_out=pkv, pk_rows=meta.pk_rows if fep_rows else None)
         else:
             if pkv_all is not None:
                 pkv = pkv_all[:, l * D:(l + 1) * D]
@@ -456,11 +474,16 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws, r=None, dr=Fa
     zbuf = torch.empty(((5 if dr else 4) * E,), **o)
     g_C, g_u = zbuf[:E], zbuf[E:4 * E].view(E, 3)
     g_r = None
+    # the fused force-pass backward (tmdnet_et_fused_bwd_f32) after a fused forward: d pre / d r formed
+    # in-kernel, no projection rows at all
+    fused = (dr and meta.fep and not rec and not inj and meta.fep_imgs is not None and FUSED_BWD
+             and all(a[7] is None for a in acts[:meta.n_layers]))
     if dr:
         assert has_e and not any(need_ws) and meta.rbf is not None
         g_r = zbuf[4 * E:]
-        fdp = kernels.rbf_deriv(r, *meta.rbf, rows=meta.pairs[1] if meta.pairs is not None else None)
-        dpkv_all = meta.dkv_proj(fdp, bias=False) if meta.batched else None
+        if not fused:
+            fdp = kernels.rbf_deriv(r, *meta.rbf, rows=meta.pairs[1] if meta.pairs is not None else None)
+            dpkv_all = meta.dkv_proj(fdp, bias=False) if meta.batched else None
     # dr mode recorded (the create_graph force pass): g_r in-kernel AND the projection gradient kept
     # padding rows of a static-capacity list are zeroed by the kernel: no memset needed
     if has_e and (not dr or rec):
@@ -507,14 +530,14 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws, r=None, dr=Fa
         gX = gX + x_top
     for l in reversed(range(meta.n_layers)):
         p = layers[l]
-        x, vec, xn, mean, rstd, qkv, vecp, pkv, xa, o_ = _act_pkv(meta, acts, l, f)
+        x, vec, xn, mean, rstd, qkv, vecp, pkv, xa, o_ = acts[l] if fused else _act_pkv(meta, acts, l, f)
         ln_w, ln_b = p[0], p[1]
         vec_w, o_w = p[8], p[9]
         qkv_w, _ = meta.qkv_eff[l]
         dkv_w, _ = meta.dkv_layer(l)
         g_qkv, g_o, g_vecp = g_qkv_all[l], g_o_all[l], g_vecp_all[l]
         gpk = gpv = dpk = dpv = None
-        if dr:
+        if dr and not fused:
             dpkv = dpkv_all[:, l * D:(l + 1) * D] if meta.batched else meta.dkv_proj(fdp, l, bias=False)
             dpk = dpkv[:, :H] if meta.hk else None
             dpv = dpkv[:, H * int(meta.hk):] if meta.hv else None
@@ -534,17 +557,22 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws, r=None, dr=Fa
                 g_vecp.add_(injected("vecp", l))
         g_xa = torch.empty((N, H), **o)
         kernels.gemm_group([(g_o, o_w, False, None, g_xa, False)])
-        pk = pkv[:, :H] if meta.hk else None
-        pv = pkv[:, H * int(meta.hk):] if meta.hv else None
         g_vec_in = gvec_bufs[l % 2] if vec is not None else None
         if acc and vec is not None:  # the injected vec cotangent's buffer takes the gradient
             g_vec_in = injected("vec", l) if injected("vec", l) is not None else torch.zeros((N, 3, H), **o)
-        kernels.et_message_bwd_launch(
-            qkv[:, :H], qkv[:, H:2 * H], qkv[:, 2 * H:], vec, pk, pv, C, u, graph, meta.heads, g_xa, gV,
-            g_qkv[:, :H], g_qkv[:, H:2 * H], g_qkv[:, 2 * H:], g_vec_in, gpk, gpv, g_C, g_u,
-            accumulate=(nat.ACC_VEC_RESIDUAL | (nat.ACC_EDGE if l < L - 1 else 0) | meta.flags
-                        | (nat.ACC_GRADS if acc else 0)),
-            pk_rows=meta.pk_rows, dpk=dpk, dpv=dpv, g_r=g_r)
+        flags = (nat.ACC_VEC_RESIDUAL | (nat.ACC_EDGE if l < L - 1 else 0) | meta.flags
+                 | (nat.ACC_GRADS if acc else 0))
+        if fused:
+            kernels.et_fused_bwd_launch(qkv[:, :H], qkv[:, H:2 * H], qkv[:, 2 * H:], vec, r, C, u, meta.fep_imgs[l],
+                                        meta.rbf, graph, meta.heads, g_xa, gV, g_qkv[:, :H], g_qkv[:, H:2 * H],
+                                        g_qkv[:, 2 * H:], g_vec_in, g_C, g_u, g_r, accumulate=flags)
+        else:
+            pk = pkv[:, :H] if meta.hk else None
+            pv = pkv[:, H * int(meta.hk):] if meta.hv else None
+            kernels.et_message_bwd_launch(
+                qkv[:, :H], qkv[:, H:2 * H], qkv[:, 2 * H:], vec, pk, pv, C, u, graph, meta.heads, g_xa, gV,
+                g_qkv[:, :H], g_qkv[:, H:2 * H], g_qkv[:, 2 * H:], g_vec_in, gpk, gpv, g_C, g_u,
+                accumulate=flags, pk_rows=meta.pk_rows, dpk=dpk, dpv=dpv, g_r=g_r)
         if not acc:
             if injected("qkv", l) is not None:
                 g_qkv.add_(injected("qkv", l))
@@ -1131,7 +1159,8 @@ def _will_run(node):
 class _ETStack(Function):
     @staticmethod
     def forward(ctx, meta, x, f, C, u, r, *params):
-        x_out, vec_out, acts = _forward_layers(meta, x, f, C, u, params, r=r)
+        # (autograd is off inside forward: whether a backward can follow is what the inputs say)
+        x_out, vec_out, acts = _forward_layers(meta, x, f, C, u, params, r=r, want_bwd=any(ctx.needs_input_grad))
         ctx.meta = meta
         ctx.acts = acts
         meta.fwd_node = weakref.ref(ctx)  # the second order hands its injections to this node's backward

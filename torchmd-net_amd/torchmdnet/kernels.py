@@ -583,10 +583,11 @@ def fep_supported(H, heads, R, dtype):
     return H == 128 and heads == 8 and R in (32, 64) and dtype == torch.float32
 
 
-def et_fused_fwd_launch(q, k, v, vec, r, C, u, fep, rbf, graph, heads, xo, vo):
+def et_fused_fwd_launch(q, k, v, vec, r, C, u, fep, rbf, graph, heads, xo, vo, pkv_out=None, pk_rows=None):
     """One ``tmdnet_et_fused_fwd_f32`` launch: the ET message with the dk/dv projection fused in
     (``fep`` = fep_split(W, b) of the layer; ``rbf`` = (mu, beta, cutoff_lower, cutoff_upper, type));
-    v in the planar layout."""
+    v in the planar layout.  ``pkv_out`` [P, >= 4H] (with ``pk_rows``): also write the canonical edges'
+    pre-activation rows there (the pair rows an unfused backward reads)."""
     lib = nat.load()
     N, H = q.shape
     mu, beta, cl, cu, rt = rbf
@@ -599,11 +600,31 @@ def et_fused_fwd_launch(q, k, v, vec, r, C, u, fep, rbf, graph, heads, xo, vo):
                                      graph.n_edges, nat.ptr(q), _ld(q), nat.ptr(k), _ld(k), nat.ptr(v), _ld(v),
                                      nat.ptr(vec), nat.ptr(r), nat.ptr(C), nat.ptr(u), nat.ptr(img), nat.ptr(wsc),
                                      nat.ptr(bo), nat.ptr(mu), nat.ptr(beta), float(cl), float(cu), int(rt),
-                                     nat.ptr(xo), nat.ptr(vo), nat.stream(q.device))
+                                     nat.ptr(xo), nat.ptr(vo), nat.ptr(pkv_out), _ld(pkv_out), nat.ptr(pk_rows),
+                                     0 if pkv_out is None else pkv_out.shape[0], nat.stream(q.device))
     nat.check(rc, "tmdnet_et_fused_fwd_f32")
     if probe is not None:
         ev1.record()
         probe.append((ev0, ev1, graph.n_edges, N, H))
+
+
+def et_fused_bwd_launch(q, k, v, vec, r, C, u, fep, rbf, graph, heads, gx, gvec, gq, gk, gv, gw, gC, gu, g_r,
+                        accumulate=0):
+    """``tmdnet_et_fused_bwd_f32``: the fused message's force-pass backward (dr mode: g_r accumulated,
+    no projection rows); gradients land in the given buffers with their inputs' row strides."""
+    if gq.stride(0) != q.stride(0) or gk.stride(0) != k.stride(0) or gv.stride(0) != v.stride(0):
+        raise ValueError("et_fused_bwd: gradients must have the row strides of q / k / v")
+    lib = nat.load()
+    N, H = q.shape
+    mu, beta, cl, cu, rt = rbf
+    img, wsc, bo = fep
+    rc = lib.tmdnet_et_fused_bwd_f32(N, H, heads, mu.shape[0], nat.ptr(graph.row_ptr), nat.ptr(graph.src),
+                                     graph.n_edges, nat.ptr(q), _ld(q), nat.ptr(k), _ld(k), nat.ptr(v), _ld(v),
+                                     nat.ptr(vec), nat.ptr(r), nat.ptr(C), nat.ptr(u), nat.ptr(img), nat.ptr(wsc),
+                                     nat.ptr(bo), nat.ptr(mu), nat.ptr(beta), float(cl), float(cu), int(rt),
+                                     nat.ptr(gx), nat.ptr(gvec), nat.ptr(gq), nat.ptr(gk), nat.ptr(gv), nat.ptr(gw),
+                                     nat.ptr(gC), nat.ptr(gu), nat.ptr(g_r), int(accumulate), nat.stream(q.device))
+    nat.check(rc, "tmdnet_et_fused_bwd_f32")
 
 
 def et_message_bwd_launch(q, k, v, vec, pk, pv, C, u, graph, heads, gx, gvec, gq, gk, gv, gw, gpk,
@@ -613,6 +634,10 @@ def et_message_bwd_launch(q, k, v, vec, pk, pv, C, u, graph, heads, gx, gvec, gq
     if (dpk is not None and pk is not None and dpk.stride(0) != pk.stride(0)) or \
             (dpv is not None and pv is not None and dpv.stride(0) != pv.stride(0)):
         raise ValueError("et_message_bwd: dpk / dpv must have the row stride of pk / pv")
+    # the kernels write each gradient with its input's row stride (gq: q's, gk: k's, gv: v's, gpk: pk's)
+    for gt, t in ((gq, q), (gk, k), (gv, v), (gpk, pk), (gpv, pv)):
+        if gt is not None and t is not None and gt.stride(0) != t.stride(0):
+            raise ValueError("et_message_bwd: gradient buffers must have the row strides of their inputs")
     lib = nat.load()
     N, H = q.shape
     rc = lib.tmdnet_et_message_bwd(
