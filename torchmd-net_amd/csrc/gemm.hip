@@ -666,7 +666,8 @@ extern "C" int tmdnet_gemm_f32(int n_problems, const int* dims, const void* cons
     P.bias = (const float*)ptrs[4 * i + 2];
     P.C = (float*)ptrs[4 * i + 3];
     if (P.M <= 0 || P.N <= 0 || P.K <= 0 || !P.A || !P.B || !P.C) return kBadArgument;
-    if (P.K % 64 || P.lda % 4 || (P.trans_b && P.ldb % 4) || P.lda < P.K || P.ldc < P.N) return kUnsupported;
+    // K in 16-wide blocks (a wave's K slice may be empty: K = 32 over 4 waves leaves two idle)
+    if (P.K % 16 || P.lda % 4 || (P.trans_b && P.ldb % 4) || P.lda < P.K || P.ldc < P.N) return kUnsupported;
     if ((((uintptr_t)P.A) & 15) || (P.trans_b && (((uintptr_t)P.B) & 15))) return kUnsupported;
     // (a 64 x 64 tile with the whole K per wave measured slower for every ET shape at QM9 size --
     // 16.5 vs 13 us for [q|k|v] + vec_proj: f32 MFMA is 1/16 of the bf16 rate, so the per-wave MFMA

@@ -1084,8 +1084,9 @@ GEMM_MAX_ROWS = 16384  # above this the library GEMM's large tiles win (C5-size 
 def gemm_launch(problems):
     """``tmdnet_gemm_f32``: up to 4 problems (A, B, trans_b, bias, C, beta) in one launch,
     C = beta C + A op(B) + bias.  Returns False (nothing launched) when a problem is outside the
-    kernel's envelope (non-fp32, K % 64, alignment); the caller then uses the library GEMM."""
-    if any(A.dtype != torch.float32 or A.shape[0] > GEMM_MAX_ROWS for A, *_ in problems):
+    kernel's envelope (non-fp32, empty, K % 16, alignment); the caller then uses the library GEMM."""
+    if any(A.dtype != torch.float32 or not 0 < A.shape[0] <= GEMM_MAX_ROWS or A.shape[1] == 0 or C.shape[1] == 0
+           for A, _, _, _, C, _ in problems):
         return False
     lib = nat.load()
     n = len(problems)
@@ -1837,6 +1838,10 @@ class _Linear(Function):
     def forward(ctx, x, w, b):
         ctx.save_for_backward(x, w)
         ctx.has_b = b is not None
+        if x.dim() == 2 and x.is_cuda and x.dtype == torch.float32:  # hand-written MFMA GEMM (tmdnet_gemm_f32)
+            y = torch.empty((x.shape[0], w.shape[0]), dtype=x.dtype, device=x.device)
+            if gemm_launch([(x, w, True, b, y, False)]):
+                return y
         return F.linear(x, w, b)
 
     @staticmethod
@@ -1878,7 +1883,12 @@ class _LinearBwd(Function):
 
     @staticmethod
     def forward(ctx, gy, x, w, need):
-        gx = gy @ w if need[0] else None
+        gx = None
+        if need[0]:
+            gy = gy.contiguous()
+            gx = torch.empty((gy.shape[0], w.shape[1]), dtype=gy.dtype, device=gy.device)
+            if not (gy.is_cuda and gemm_launch([(gy, w, False, None, gx, False)])):
+                torch.mm(gy, w, out=gx)
         gw, gb = _linear_wgrad(gy, x, need[1], need[2]) if (need[1] or need[2]) else (None, None)
         ctx.save_for_backward(gy, x, w)
         return gx, gw, gb

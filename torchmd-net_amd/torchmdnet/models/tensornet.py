@@ -187,7 +187,7 @@ class TensorNet(nn.Module):
             X = layer(X, graph, graph.distances, edge_attr)
         x = tn_node.norms(X)  # cat(|I|^2, |A|^2, |S|^2) of decompose_tensor(X), one fused pass
         x = self.out_norm(x)
-        return kernels.fused_act(self.act, self.linear(x))
+        return kernels.fused_act(self.act, kernels.linear(x, self.linear.weight, self.linear.bias))
 
 
 def _check_symmetric_graph(edge_index, n):
@@ -258,18 +258,20 @@ class TensorEmbedding(nn.Module):
             edge_weight, edge_vec_norm, edge_attr = edge_weight[perm], edge_vec_norm[perm], edge_attr[perm]
         C = graph.cutoff if (perm is None and graph.cutoff is not None) else self.cutoff(edge_weight)
         H = self.hidden_channels
-        W = torch.nn.functional.linear(
+        # the Linears as kernels.linear: the hand-written MFMA GEMMs (tmdnet_gemm_f32 forward and input
+        # gradient, the grouped TN kernel for weight gradients) instead of the library's small-GEMM tiles
+        W = kernels.linear(
             edge_attr, torch.cat([self.distance_proj1.weight, self.distance_proj2.weight, self.distance_proj3.weight]),
             torch.cat([self.distance_proj1.bias, self.distance_proj2.bias, self.distance_proj3.bias]))
         Z = self.emb(z)
-        P = torch.nn.functional.linear(Z, self.emb2.weight[:, :H], self.emb2.bias)
-        Q = torch.nn.functional.linear(Z, self.emb2.weight[:, H:])
+        P = kernels.linear(Z, self.emb2.weight[:, :H], self.emb2.bias)
+        Q = kernels.linear(Z, self.emb2.weight[:, H:])
         Ec = kernels.tn_embed(P, Q, W, C, edge_vec_norm, graph)  # compact [9, N, H]: I | A | S rows
         norm = self.init_norm(tn_node.enorm(Ec))
         lt = self.linears_tensor
         Ec = tn_node.mix3(Ec, lt[0].weight, lt[1].weight, lt[2].weight)
         for linear_scalar in self.linears_scalar:
-            norm = kernels.fused_act(self.act, linear_scalar(norm))
+            norm = kernels.fused_act(self.act, kernels.linear(norm, linear_scalar.weight, linear_scalar.bias))
         # new_radial_tensor(I, A, S, norm[..., 0], norm[..., 1], norm[..., 2]) and I + A + S
         return tn_node.eout(Ec, norm)
 
@@ -324,9 +326,10 @@ class Interaction(nn.Module):
         if perm is not None:
             edge_weight, edge_attr = edge_weight[perm], edge_attr[perm]
         C = graph.cutoff if (perm is None and graph.cutoff is not None) else self.cutoff(edge_weight)
-        for linear_scalar in self.linears_scalar[:-1]:
-            edge_attr = kernels.fused_act(self.act, linear_scalar(edge_attr))
-        edge_attr = kernels.fused_act(self.act, self.linears_scalar[-1](edge_attr), C)  # act(.) * C
+        ls = self.linears_scalar
+        for linear_scalar in ls[:-1]:
+            edge_attr = kernels.fused_act(self.act, kernels.linear(edge_attr, linear_scalar.weight, linear_scalar.bias))
+        edge_attr = kernels.fused_act(self.act, kernels.linear(edge_attr, ls[-1].weight, ls[-1].bias), C)  # act(.) * C
         lt = self.linears_tensor
         # X / (|X|^2 + 1), decompose, three channel mixes -> Y as compact [9, N, H] (I | A | S rows)
         Yc = tn_node.mix3(tn_node.pre(X), lt[0].weight, lt[1].weight, lt[2].weight)

@@ -20,6 +20,7 @@ import torch
 from torch.autograd import Function
 
 from . import _native as nat
+from . import kernels
 
 PRE, POST_O3, POST_SO3, RESID, NORMS, ENORM, EOUT = range(7)
 
@@ -245,8 +246,10 @@ class _Mix3(Function):
     def forward(ctx, c, w0, w1, w2):
         c = c.contiguous()
         out = torch.empty((9, c.shape[1], w0.shape[0]), dtype=c.dtype, device=c.device)
-        for src, w, dst in zip(_blocks(c), (w0, w1, w2), _blocks(out)):
-            torch.mm(src, w.t(), out=dst)
+        probs = [(src, w, True, None, dst, False) for src, w, dst in zip(_blocks(c), (w0, w1, w2), _blocks(out))]
+        if not (c.is_cuda and kernels.gemm_launch(probs)):  # the three mixes in one hand-written launch
+            for src, w, _, _, dst, _ in probs:
+                torch.mm(src, w.t(), out=dst)
         ctx.save_for_backward(c, w0, w1, w2)
         return out
 
@@ -262,10 +265,15 @@ class _Mix3Bwd(Function):
     @staticmethod
     def forward(ctx, need_w, gout, c, w0, w1, w2):
         gc = torch.empty_like(c)
-        gws = []
-        for g, src, w, dst, need in zip(_blocks(gout), _blocks(c), (w0, w1, w2), _blocks(gc), need_w):
-            torch.mm(g, w, out=dst)
-            gws.append(torch.mm(g.t(), src) if need else None)
+        ws = (w0, w1, w2)
+        probs = [(g, w, False, None, dst, False) for g, w, dst in zip(_blocks(gout), ws, _blocks(gc))]
+        if not (c.is_cuda and kernels.gemm_launch(probs)):  # input gradients: one launch
+            for g, w, _, _, dst, _ in probs:
+                torch.mm(g, w, out=dst)
+        # weight gradients: one grouped TN launch (sums over the rows)
+        gws = [torch.empty_like(w) if need else None for w, need in zip(ws, need_w)]
+        tn = [{"A": g, "B": src, "C": gw} for g, src, gw in zip(_blocks(gout), _blocks(c), gws) if gw is not None]
+        kernels.wgrad_tn(tn)
         ctx.save_for_backward(gout, c, w0, w1, w2)
         return (gc,) + tuple(gws)
 
