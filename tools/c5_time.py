@@ -36,15 +36,23 @@ def main():
     for _ in range(2):
         y, f = model(z, pos, batch)
     torch.cuda.synchronize()
+    m0 = torch.cuda.memory_stats()
     t0 = time.perf_counter()
+    host = 0.0
     for _ in range(steps):
+        h0 = time.perf_counter()
         y, f = model(z, pos, batch)
+        host += time.perf_counter() - h0  # host time to enqueue (the queue may back up: an upper bound)
     torch.cuda.synchronize()
     el = (time.perf_counter() - t0) / steps
+    m1 = torch.cuda.memory_stats()
+    mem = {k: m1.get(k, 0) - m0.get(k, 0) for k in ("num_device_alloc", "num_device_free", "num_alloc_retries")}
+    mem["peak_gb"] = round(torch.cuda.max_memory_allocated() / 2 ** 30, 1)
+    mem["host_ms_per_eval"] = round(1000 * host / steps, 2)
     print(json.dumps({"fep": os.environ.get("TMDNET_FEP", "auto"), "fep_bwd": os.environ.get("TMDNET_FEP_BWD", "rows"),
                       "ms_per_eval": round(1000 * el, 2), "atoms_per_s": round(n / el, 1),
-                      "energy": float(y.sum()), "force_absmax": float(f.abs().max()),
-                      "force_sum": [float(v) for v in f.double().sum(0)]}))
+                      "energy": float(y.detach().sum()), "force_absmax": float(f.abs().max()),
+                      "force_sum": [float(v) for v in f.double().sum(0)], **mem}))
 
 
 if __name__ == "__main__":

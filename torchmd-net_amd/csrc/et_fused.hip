@@ -257,12 +257,16 @@ __device__ __forceinline__ void head_math(const Gat& X, const char* wt, const in
   const f4 p1 = block_pre<KS>(wt, wb, sct, sbt, 16 + h, A0, A1, lane);
   const f4 p2 = block_pre<KS>(wt, wb, sct, sbt, 24 + h, A0, A1, lane);
   if (Rp) {  // the canonical edges' projection rows (column 16 blk + channel; other edges: out of range)
+    // (the element goes through a scalar first: __builtin_bit_cast of a vector-element lvalue reads
+    // element 0 whatever the index -- every edge of a lane group stored edge 0's row)
     const f4 pb[4] = {pk, px, p1, p2};
 #pragma unroll
     for (int b = 0; b < 4; ++b)
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, pb[b][i]), *Rp, op[i] + 64 * (8 * b + h), 0, 0);
+      for (int i = 0; i < 4; ++i) {
+        const float val = pb[b][i];
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(val), *Rp, op[i] + 64 * (8 * b + h), 0, 0);
+      }
   }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
