@@ -43,7 +43,7 @@ def _run(m, z, pos, L, dtype):
     d.use_periodic = True
     d.strategy = "cell"
     y, f = m(z.to(DEV), pos.to(dtype).to(DEV), torch.zeros_like(z).to(DEV))
-    return y.detach(), f.detach()
+    return y.detach(), None if f is None else f.detach()
 
 
 @pytest.mark.parametrize("R,rbf_type,cl", [(64, "expnorm", 0.0), (32, "expnorm", 0.0), (64, "gauss", 0.0),
@@ -82,8 +82,20 @@ def test_fused_forward_matches_fp64_and_unfused(R, rbf_type, cl, monkeypatch):
         monkeypatch.setattr(et_stack, "FEP_BWD", mode)
         y1, f1 = _run(m, z, pos, L, torch.float32)
         assert len(bcalls) == 3
-        assert _rel(y, y1) < 1e-6
+        assert _rel(y, y1) < 1e-5
         assert _rel(f, f1) < 1e-4
+    # default ("off"): with a backward to follow the forward is the unfused one; energy only -> fused
+    monkeypatch.setattr(et_stack, "FEP_BWD", "off")
+    n0 = len(calls)
+    y2, f2 = _run(m, z, pos, L, torch.float32)
+    assert len(calls) == n0
+    assert _rel(y, y2) < 1e-5 and _rel(f, f2) < 1e-4
+    m.derivative = False
+    with torch.no_grad():
+        y3, _ = _run(m, z, pos, L, torch.float32)
+    m.derivative = True
+    assert len(calls) == n0 + 3
+    assert _rel(y, y3) < 1e-5
     monkeypatch.setattr(et_stack, "FEP", "0")
     n0 = len(calls)
     y0, f0 = _run(m, z, pos, L, torch.float32)

@@ -1057,6 +1057,12 @@ def test_grouped_gemm_matches_torch():
             (g_xn, d(g_qkv) @ d(wqkv)), (g_vec, d(g_vec0) + d(g_vecp) @ d(wvec))]
     for got, ref in refs:
         assert _rel(got.cpu(), ref.cpu()) < 2e-6
-    # outside the envelope (K % 64): not launched
-    assert not kernels.gemm_launch([(torch.randn(5, 96, **f), torch.randn(7, 96, **f), True, None,
+    # K in 16-wide blocks (TensorNet's K = 32 / 96 Linears: some waves of a tile get no K block)
+    for K in (16, 32, 96):
+        a, b, bias = torch.randn(37, K, **f), torch.randn(70, K, **f), torch.randn(70, **f)
+        c = torch.empty(37, 70, **f)
+        assert kernels.gemm_launch([(a, b, True, bias, c, False)])
+        assert _rel(c.cpu(), (d(a) @ d(b).t() + d(bias)).cpu()) < 2e-6
+    # outside the envelope (K % 16): not launched
+    assert not kernels.gemm_launch([(torch.randn(5, 72, **f), torch.randn(7, 72, **f), True, None,
                                      torch.empty(5, 7, **f), False)])

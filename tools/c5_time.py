@@ -49,7 +49,7 @@ def main():
     mem = {k: m1.get(k, 0) - m0.get(k, 0) for k in ("num_device_alloc", "num_device_free", "num_alloc_retries")}
     mem["peak_gb"] = round(torch.cuda.max_memory_allocated() / 2 ** 30, 1)
     mem["host_ms_per_eval"] = round(1000 * host / steps, 2)
-    print(json.dumps({"fep": os.environ.get("TMDNET_FEP", "auto"), "fep_bwd": os.environ.get("TMDNET_FEP_BWD", "rows"),
+    print(json.dumps({"fep": os.environ.get("TMDNET_FEP", "auto"), "fep_bwd": os.environ.get("TMDNET_FEP_BWD", "off"),
                       "ms_per_eval": round(1000 * el, 2), "atoms_per_s": round(n / el, 1),
                       "energy": float(y.detach().sum()), "force_absmax": float(f.abs().max()),
                       "force_sum": [float(v) for v in f.double().sum(0)], **mem}))

@@ -127,11 +127,14 @@ PAIR_ROWS = True
 # 2.8 GB per layer, read back once per direction by the unfused kernel).  A backward that needs them
 # forms them then (_act_pkv).  TMDNET_FEP=0 turns it off.
 FEP = os.environ.get("TMDNET_FEP", "auto")
-# How the backward after a fused forward gets its projection: "rows" = the fused forward also writes
-# the canonical edges' pre-activation pair rows when a backward can follow (grad enabled) and the
-# unfused backward reads them; "fused" = the force-pass (dr mode) backward is fused the same way
-# (tmdnet_et_fused_bwd_f32, no rows at all); "lazy" = the backward forms the rows by the GEMM.
-FEP_BWD = os.environ.get("TMDNET_FEP_BWD", "rows")
+# When a backward can follow (grad enabled), how it gets the projection: "off" (default) = the
+# forward is the unfused one (projection GEMM + message kernel); "rows" = the fused forward also
+# writes the canonical edges' pre-activation pair rows and the unfused backward reads them; "fused" =
+# the force-pass (dr mode) backward is fused the same way (tmdnet_et_fused_bwd_f32, no rows at all:
+# 20 vs 67 GB peak at C5); "lazy" = the backward forms the rows by the GEMM.  Measured C5 energy +
+# forces (tools/c5_modes.sh, r03): off 69.2, rows 69.6, fused 71.8, lazy 72.4 ms -- the fused
+# forward (1.45 vs 0.91 + 1.17 ms per layer) pays only when no rows are needed (energy only).
+FEP_BWD = os.environ.get("TMDNET_FEP_BWD", "off")
 FUSED_BWD = FEP_BWD == "fused"
 # "dr mode" force pass (see _backward_layers): on whenever the force pass needs no weight gradient
 # and the features are a fixed basis of r (also under create_graph, which the reference force pass
@@ -241,6 +244,7 @@ class _Meta:
         self.dkv_wp = None      # the bf16 split of dkv_eff[0] (dkv_split), once per forward
         self.fep = False        # the forward runs the fused-projection edge kernel (FEP)
         self.fep_imgs = None    # per layer: its weight image (kernels.fep_split), made by the forward
+        self.grad_mode = True   # torch.is_grad_enabled() where the stack was called (a backward can follow)
 
     def split(self, params):
         return [params[i * self.np:(i + 1) * self.np] for i in range(self.n_layers)]
@@ -345,7 +349,7 @@ def _act_pkv(meta, acts, l, f):
     """Layer l's forward activations, with its projection rows formed now if the fused forward (FEP)
     skipped them (a backward that contracts them: training form, or the unfused dr-mode pass)."""
     a = acts[l]
-    if a[7] is None and meta.fep and meta.D:
+    if a[7] is None and meta.fep_imgs is not None and meta.D:
         if meta.batched:  # every layer's rows in one GEMM, as the unfused forward lays them out: the
             # message backward reads d(dk,dv)/dr with the projection rows' leading dimension
             pkv_all, D = meta.dkv_proj(_pair_f(meta, f)), meta.D
@@ -366,7 +370,9 @@ def _forward_layers(meta, x, f, C, u, params, r=None, want_bwd=False):
     meta.refresh_effective()
     # the projections depend on |r| only: one row per edge PAIR ((E + N) / 2 rows), read by both
     # directions through pk_rows (bit-identical to the per-edge projection)
-    fep = meta.fep and r is not None
+    fep = meta.fep and r is not None and (FEP_BWD != "off" or not want_bwd)
+    if not fep:
+        meta.fep_imgs = None  # (the backward's fused path keys on them: none from an earlier forward)
     fp = _pair_f(meta, f) if (D and not fep) else f
     pkv_all = meta.dkv_proj(fp) if (meta.batched and D and not fep) else None
     # the fused forward writes the pair rows itself when the unfused backward will want them
@@ -1159,8 +1165,10 @@ def _will_run(node):
 class _ETStack(Function):
     @staticmethod
     def forward(ctx, meta, x, f, C, u, r, *params):
-        # (autograd is off inside forward: whether a backward can follow is what the inputs say)
-        x_out, vec_out, acts = _forward_layers(meta, x, f, C, u, params, r=r, want_bwd=any(ctx.needs_input_grad))
+        # (autograd is off inside forward: whether a backward can follow is the caller's grad mode and
+        # what the inputs say -- needs_input_grad alone follows requires_grad, also under no_grad)
+        want = meta.grad_mode and any(ctx.needs_input_grad)
+        x_out, vec_out, acts = _forward_layers(meta, x, f, C, u, params, r=r, want_bwd=want)
         ctx.meta = meta
         ctx.acts = acts
         meta.fwd_node = weakref.ref(ctx)  # the second order hands its injections to this node's backward
@@ -1346,4 +1354,5 @@ def et_stack(layers, x, graph, f, C, u, rbf=None, out_norm=None, f_pairs=None):
                     and kernels.fep_supported(H, heads, mu.shape[0], x.dtype) and r.dtype == x.dtype)
     x = x.contiguous()
     f = f.contiguous() if (hk or hv) else None
+    meta.grad_mode = torch.is_grad_enabled()
     return _ETStack.apply(meta, x, f, C.contiguous(), u.contiguous(), r, *params)
