@@ -38,6 +38,10 @@ enum { TMDNET_ET_V_PLANAR = 4 };
 /* tmdnet_et_message_bwd2_ex flags: accumulate d_cut / d_unit (ACC_EDGE) and d_grad_vec (ACC_GVEC)
  * into the caller's buffers instead of overwriting them. */
 enum { TMDNET_BWD2_ACC_EDGE = 8, TMDNET_BWD2_ACC_GVEC = 16 };
+/* tmdnet_et_message_bwd accumulate bit: the dr-mode backward as the two passes (destination, then
+ * source) instead of the merged pass that serves both roles of a node from one read of each pair row
+ * (the default from 16384 nodes; same results up to summation order). */
+enum { TMDNET_ET_TWO_PASS = 64 };
 
 /* ------------------------------------------------------------------------------------------
  * Neighbour list.  Replaces torchmdnet_neighbors::get_neighbor_pairs

@@ -441,16 +441,19 @@ def test_et_edge_kernel_gradcheck():
 
 @pytest.mark.parametrize("planar", [False, True])
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
-def test_et_bwd_dr_mode_matches_projection_gradient(dtype, planar):
+@pytest.mark.parametrize("H,n_mol,two_pass", [(64, 4, False), (64, 4, True), (128, 4, True),
+                                              (128, 1000, False), (128, 1000, True), (32, 1000, False)])
+def test_et_bwd_dr_mode_matches_projection_gradient(dtype, planar, H, n_mol, two_pass):
     """dr mode of tmdnet_et_message_bwd (the force pass): g_r[e] = <g_pk[e], dpk[row(e)]> +
     <g_pv[e], dpv[row(e)]> of the plain backward over the pair-shared rows, every other output
-    unchanged."""
+    unchanged -- for the merged pass (both roles of a node from one read of each pair row; from 16384
+    nodes) and the two-pass form (TMDNET_ET_TWO_PASS, k_bwd_both below 16384 nodes)."""
     from torchmdnet import _native as nat
     from torchmdnet import kernels
     torch.manual_seed(0)
-    z, pos, batch = O.qm9_like(4)
+    z, pos, batch = O.qm9_like(n_mol)
     g = kernels.build_graph(pos.to(DEV).to(dtype), batch.to(DEV), 0.0, 5.0, 64 * pos.shape[0], loop=True)
-    N, H, heads, E = pos.shape[0], 64, 8, g.n_edges
+    N, heads, E = pos.shape[0], 8, g.n_edges
     pr, pe = kernels.pair_index(g)
     o = dict(dtype=dtype, device=DEV)
     P = pe.shape[0]
@@ -461,6 +464,7 @@ def test_et_bwd_dr_mode_matches_projection_gradient(dtype, planar):
     flags = nat.ACC_VEC_RESIDUAL | nat.ACC_EDGE | (nat.ET_V_PLANAR if planar else 0)
 
     def run(dr):
+        fl = flags | (nat.ET_TWO_PASS if (dr and two_pass) else 0)
         gq, gk, gv, gw = (torch.empty(N, H, **o), torch.empty(N, H, **o), torch.empty(N, 3 * H, **o),
                           torch.empty(N, 3, H, **o))
         gC, gu = torch.zeros(E, **o), torch.zeros(E, 3, **o)
@@ -468,7 +472,7 @@ def test_et_bwd_dr_mode_matches_projection_gradient(dtype, planar):
         gr = torch.zeros(E, **o) if dr else None
         kernels.et_message_bwd_launch(
             q, k, v, vec, pkv[:, :H], pkv[:, H:], C, u, g, heads, gx, gvec, gq, gk, gv, gw,
-            None if dr else gpkv[:, :H], None if dr else gpkv[:, H:], gC, gu, accumulate=flags, pk_rows=pr,
+            None if dr else gpkv[:, :H], None if dr else gpkv[:, H:], gC, gu, accumulate=fl, pk_rows=pr,
             dpk=dpkv[:, :H] if dr else None, dpv=dpkv[:, H:] if dr else None, g_r=gr)
         return [gq, gk, gv, gw, gC, gu], gpkv, gr
 

@@ -126,7 +126,7 @@ def main():
         return [gq_, gk_, gv_, torch.empty(n, 3, H, device=dev), torch.empty(E, device=dev),
                 torch.empty(E, 3, device=dev), torch.empty(E, device=dev)]
 
-    outs = [grads() for _ in range(2)]
+    outs = [grads() for _ in range(3)]
 
     def unfused_dproj():
         return kernels.proj(fdp, W, None, wp=wp)
@@ -139,6 +139,12 @@ def main():
                                       None, None, gC, gu, accumulate=1 | 4, pk_rows=pair_row, dpk=dpkv[:, :H],
                                       dpv=dpkv[:, H:], g_r=gr)
 
+    def unfused_bwd_2pass():  # the same call as the two passes (TMDNET_ET_TWO_PASS)
+        gq, gk, gv, gw, gC, gu, gr = outs[2]
+        kernels.et_message_bwd_launch(q, k, v, vec, pkv[:, :H], pkv[:, H:], C, u, g, 8, gx, gvec, gq, gk, gv, gw,
+                                      None, None, gC, gu, accumulate=1 | 4 | 64, pk_rows=pair_row,
+                                      dpk=dpkv[:, :H], dpv=dpkv[:, H:], g_r=gr)
+
     def fused_bwd():
         gq, gk, gv, gw, gC, gu, gr = outs[1]
         kernels.et_fused_bwd_launch(q, k, v, vec, r, C, u, fep, (mu, beta, cl, cu, 0), g, 8, gx, gvec, gq, gk, gv,
@@ -146,12 +152,16 @@ def main():
 
     unfused_bwd()
     fused_bwd()
+    unfused_bwd_2pass()
     torch.cuda.synchronize()
+    merged_err = {nm: float((b - a).abs().max() / a.abs().max()) for nm, a, b in
+                  zip("gq gk gv gvec gC gu gr".split(), outs[2], outs[0])}
     bwd_err = {nm: float((b - a).abs().max() / a.abs().max()) for nm, a, b in
                zip("gq gk gv gvec gC gu gr".split(), outs[0], outs[1])}
     t_dproj = timed(unfused_dproj, reps)
     t_ubwd = timed(unfused_bwd, reps)
     t_fbwd = timed(fused_bwd, reps)
+    t_u2 = timed(unfused_bwd_2pass, reps)
     flop = 2.0 * E * R * 4 * H
     out = {**rows_info, "n_atoms": n, "edges": E, "pairs": int(pair_edge.shape[0]), "R": R,
            "max_rel_err_x": err_x, "max_rel_err_vec": err_v,
@@ -160,7 +170,8 @@ def main():
            "fused_fp32_equiv_tflops": round(flop / t_fused / 1e9, 1),
            "fused_f16_mfma_tflops": round(3 * flop / t_fused / 1e9, 1),
            "bwd_max_rel_err": bwd_err, "unfused_dproj_ms": round(t_dproj, 4), "unfused_bwd_ms": round(t_ubwd, 4),
-           "unfused_bwd_total_ms": round(t_dproj + t_ubwd, 4), "fused_bwd_ms": round(t_fbwd, 4)}
+           "unfused_bwd_total_ms": round(t_dproj + t_ubwd, 4), "fused_bwd_ms": round(t_fbwd, 4),
+           "two_pass_bwd_ms": round(t_u2, 4), "merged_vs_two_pass_err": merged_err}
     print(json.dumps(out))
 
 

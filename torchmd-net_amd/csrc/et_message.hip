@@ -253,6 +253,37 @@ __device__ __forceinline__ void edge_chunks_pf(const Args<T>& A, int b, int e, i
   }
 }
 
+// The same traversal without the stream prefetch: body(k, s, C, u0, u1, u2, row) issues every load of
+// the edge itself (fewer live registers: the merged backward's occupancy is worth more than the
+// pipelining).
+template <typename T, int S, typename F>
+__device__ __forceinline__ void edge_chunks(const Args<T>& A, int b, int e, int EPW, const Geo& G, F&& body) {
+  const int lane = lane_id();
+  const int step = EPW * S;
+  for (int c = b; c < e; c += TMD_WAVE) {
+    const int n = min(TMD_WAVE, e - c);
+    int s_r = 0, p_r = c + lane;
+    T C_r = T(0), u0_r = T(0), u1_r = T(0), u2_r = T(0);
+    if (lane < n) {
+      const int k = c + lane;
+      s_r = A.src[k];
+      TMD_DCHECK(s_r >= 0 && s_r < A.n);
+      if (A.prow) p_r = A.prow[k];
+      C_r = A.C[k];
+      u0_r = A.u[3 * k];
+      u1_r = A.u[3 * k + 1];
+      u2_r = A.u[3 * k + 2];
+    }
+    for (int j0 = EPW * G.sub; j0 < n; j0 += step) {
+      const int j = j0 + G.es;
+      const int jj = j < n ? j : n - 1;
+      const int s = __shfl(s_r, jj), row = __shfl(p_r, jj);
+      const T Ce = __shfl(C_r, jj), u0 = __shfl(u0_r, jj), u1 = __shfl(u1_r, jj), u2 = __shfl(u2_r, jj);
+      if (j < n) body(c + j, s, Ce, u0, u1, u2, row);
+    }
+  }
+}
+
 // ------------------------------------------------------------------ forward
 // ORD: nodes visited in the caller's `order` (cell order for large periodic systems, so the waves in
 // flight gather from a compact spatial window of source rows).
@@ -680,6 +711,237 @@ __global__ __launch_bounds__(256, (bwd_min_waves<T, V, DR>())) void k_bwd_both(A
   const int split = (int)gridDim.x / 2;
   if ((int)blockIdx.x < split) bwd_dst_body<T, V, S, CS, DR, AG>(A, blockIdx.x, split);
   else bwd_src_body<T, V, S, CS>(A, blockIdx.x - split, split);
+}
+
+// ------------------------------------------------------------------ backward, merged pass (dr mode)
+// Both roles of a node in ONE pass over its CSR row: for the edge e = (t <- s) the destination role
+// (gq[t], and e's g_cut / g_unit / g_r) and, from the same pair row, the source role of its reverse
+// s <- t (gk[t], gv[t], gvec_in[t]) -- the pair row (dk / dv pre-activations) is fetched once per
+// edge instead of once per pass (the two-pass backward reads it twice per direction, four times per
+// pair: 3.4x its distinct bytes at C5), and the per-edge activations are formed once.  Each edge
+// gathers both of its source's row sets (k, v, vec for the destination role; q, gx, gvec for the
+// source role).  The node's own vectors (q, gx, gvec | k, v, vec) are staged in LDS once per node
+// and re-read per edge (48 fewer VGPRs than holding them in registers).
+template <typename T, int V, int S, int PD>
+__device__ __forceinline__ void bwd_merged_body(const Args<T>& A, int blk, int nwg) {
+  constexpr int NA = 8 * V;            // accumulators summed over a node's S waves
+  extern __shared__ __attribute__((aligned(16))) char dyn_lds[];  // max(4/S nodes x 12 H, reduction)
+  T* lds = reinterpret_cast<T*>(dyn_lds);
+  const int HM = A.H;
+  const Geo G = geo<S, 1, false>(A.n, A.L, nullptr, A.xcd, blk, nwg);
+  const int t = G.node;
+  const int EPW = TMD_WAVE / A.L;
+  const int c0 = G.el * V;
+  const int hh = c0 / A.d, cc = c0 % A.d;
+  const int vo = A.planar ? c0 : hh * 3 * A.d + cc;
+  const bool hk = A.pk != nullptr, hv = A.pv != nullptr, hw = A.vec != nullptr;
+  const int pvd = hv ? A.vst : 0, vcd = hw ? A.H : 0;
+  const bool head_leader = (G.el % A.lph) == 0;
+  // node vectors: [q | gx | g0 | g1 | g2 | k | vx | v1 | v2 | w0 | w1 | w2] x H of this wave's node
+  T* nv = lds + ((threadIdx.x >> 6) / S) * 12 * HM;
+  if (t >= 0 && G.sub == 0 && G.es == 0) {
+    T a[V];
+    const T* src[12];
+    const T* gvt = A.gvec + (size_t)t * 3 * A.H;
+    const T* vt = A.v + (size_t)t * A.ldv;
+    const T* wt = A.vec + (size_t)t * 3 * A.H;
+    src[0] = A.q + (size_t)t * A.ldq + c0; src[1] = A.gx + (size_t)t * A.H + c0;
+    src[2] = gvt + c0; src[3] = gvt + A.H + c0; src[4] = gvt + 2 * A.H + c0;
+    src[5] = A.k + (size_t)t * A.ldk + c0;
+    src[6] = vt + vo; src[7] = vt + vo + A.vst; src[8] = vt + vo + 2 * A.vst;
+    src[9] = hw ? wt + c0 : src[0]; src[10] = hw ? wt + A.H + c0 : src[0]; src[11] = hw ? wt + 2 * A.H + c0 : src[0];
+#pragma unroll
+    for (int r = 0; r < 12; ++r) {
+      ldv<T, V>(a, src[r]);
+      if (r >= 9 && !hw) zero(a);
+      stv<T, V>(nv + r * HM + c0, a);
+    }
+  }
+  __syncthreads();
+  T gq[V], gk[V], gvx[V], gv1[V], gv2[V], gw0[V], gw1[V], gw2[V];
+  zero(gq); zero(gk); zero(gvx); zero(gv1); zero(gv2); zero(gw0); zero(gw1); zero(gw2);
+  if (t >= 0) {
+    const int b = min(A.row_ptr[t], A.cap), e = min(A.row_ptr[t + 1], A.cap);
+    const T* dummy = A.q + (size_t)t * A.ldq;
+    const bool acc_edge = (A.acc & TMDNET_ACC_EDGE) && G.el == 0;
+    struct St { T k[V], x[V], a[V], b[V]; int row; };
+    auto ld = [&](int k, St& st) {
+      ldv<T, V>(st.k, opt(A.pk, (size_t)k * A.ldpk + c0, dummy + c0));
+      const T* pvs = opt(A.pv, (size_t)k * A.ldpv + vo, dummy);
+      ldv<T, V>(st.x, pvs);
+      ldv<T, V>(st.a, pvs + pvd);
+      ldv<T, V>(st.b, pvs + 2 * pvd);
+      st.row = k;
+    };
+    auto body = [&](int k, int s, T Ce, T u0, T u1, T u2, const St& st, auto&& pre) {
+      T oc = T(0), ou0 = T(0), ou1 = T(0), ou2 = T(0), orr = T(0);
+      if (acc_edge) {
+        oc = A.gC[k]; ou0 = A.gu[3 * k]; ou1 = A.gu[3 * k + 1]; ou2 = A.gu[3 * k + 2]; orr = A.gr[k];
+      }
+      // the source's rows: k, v, vec (destination role) and q, gx, gvec (source role of the reverse)
+      T kk[V], vx[V], v1[V], v2[V], w0[V], w1[V], w2[V], qs[V], gxs[V], h0[V], h1[V], h2[V];
+      ldv<T, V>(kk, A.k + (size_t)s * A.ldk + c0);
+      const T* vs = A.v + (size_t)s * A.ldv + vo;
+      ldv<T, V>(vx, vs);
+      ldv<T, V>(v1, vs + A.vst);
+      ldv<T, V>(v2, vs + 2 * A.vst);
+      const T* vecs = hw ? A.vec + (size_t)s * 3 * A.H + c0 : dummy + c0;
+      ldv<T, V>(w0, vecs);
+      ldv<T, V>(w1, vecs + vcd);
+      ldv<T, V>(w2, vecs + 2 * vcd);
+      ldv<T, V>(qs, A.q + (size_t)s * A.ldq + c0);
+      ldv<T, V>(gxs, A.gx + (size_t)s * A.H + c0);
+      const T* gvs = A.gvec + (size_t)s * 3 * A.H + c0;
+      ldv<T, V>(h0, gvs);
+      ldv<T, V>(h1, gvs + A.H);
+      ldv<T, V>(h2, gvs + 2 * A.H);
+      T dpk_[V], dpx_[V], dp1_[V], dp2_[V];
+      ldv<T, V>(dpk_, opt(A.dpk, (size_t)st.row * A.ldpk + c0, dummy + c0));
+      const T* dps = opt(A.dpv, (size_t)st.row * A.ldpv + vo, dummy);
+      ldv<T, V>(dpx_, dps);
+      ldv<T, V>(dp1_, dps + pvd);
+      ldv<T, V>(dp2_, dps + 2 * pvd);
+      pre();
+      if (!hw) { zero(w0); zero(w1); zero(w2); }
+      T dk[V], ddk[V], dvx[V], dv1[V], dv2[V], ddx[V], dd1[V], dd2[V];
+      act<T, V>(st.k, hk, dk, ddk);
+      act<T, V>(st.x, hv, dvx, ddx);
+      act<T, V>(st.a, hv, dv1, dd1);
+      act<T, V>(st.b, hv, dv2, dd2);
+      // ---- destination role: e = (t <- s), the node's q / gx / gvec from LDS
+      {
+        T q[V], gx[V], g0[V], g1[V], g2[V];
+        ldv<T, V>(q, nv + 0 * HM + c0);
+        ldv<T, V>(gx, nv + 1 * HM + c0);
+        ldv<T, V>(g0, nv + 2 * HM + c0);
+        ldv<T, V>(g1, nv + 3 * HM + c0);
+        ldv<T, V>(g2, nv + 4 * HM + c0);
+        T part = T(0), ga = T(0), gu0 = T(0), gu1 = T(0), gu2 = T(0);
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+          part += q[i] * kk[i] * dk[i];
+          ga += gx[i] * vx[i] * dvx[i];
+          const T v2e = v2[i] * dv2[i];
+          gu0 += g0[i] * v2e;
+          gu1 += g1[i] * v2e;
+          gu2 += g2[i] * v2e;
+        }
+        part = group_sum(part, A.lph);
+        ga = group_sum(ga, A.lph);
+        const Silu<T> sa(part);
+        const T a = sa.s * Ce;
+        const T gs = ga * Ce * sa.d(part);
+        T grr = T(0);
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+          gq[i] += gs * kk[i] * dk[i];
+          const T gpk = gs * q[i] * kk[i] * ddk[i];
+          const T gpx = gx[i] * a * vx[i] * ddx[i];
+          const T gp1 = (g0[i] * w0[i] + g1[i] * w1[i] + g2[i] * w2[i]) * v1[i] * dd1[i];
+          const T gp2 = (g0[i] * u0 + g1[i] * u1 + g2[i] * u2) * v2[i] * dd2[i];
+          grr += (hk ? gpk * dpk_[i] : T(0)) + (hv ? gpx * dpx_[i] + gp1 * dp1_[i] + gp2 * dp2_[i] : T(0));
+        }
+        const T gc = group_sum(head_leader ? ga * sa.s : T(0), A.L);
+        gu0 = group_sum(gu0, A.L);
+        gu1 = group_sum(gu1, A.L);
+        gu2 = group_sum(gu2, A.L);
+        grr = group_sum(grr, A.L);
+        if (G.el == 0) {
+          A.gC[k] = oc + gc;
+          A.gu[3 * k] = ou0 + gu0;
+          A.gu[3 * k + 1] = ou1 + gu1;
+          A.gu[3 * k + 2] = ou2 + gu2;
+          A.gr[k] = orr + grr;
+        }
+      }
+      // ---- source role: the reverse edge s <- t (unit vector negated), the node's k / v / vec from LDS
+      {
+        T kt[V], vxt[V], v1t[V], w0t[V], w1t[V], w2t[V];
+        ldv<T, V>(kt, nv + 5 * HM + c0);
+        ldv<T, V>(vxt, nv + 6 * HM + c0);
+        ldv<T, V>(v1t, nv + 7 * HM + c0);
+        ldv<T, V>(w0t, nv + 9 * HM + c0);
+        ldv<T, V>(w1t, nv + 10 * HM + c0);
+        ldv<T, V>(w2t, nv + 11 * HM + c0);
+        T part = T(0), ga = T(0);
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+          part += qs[i] * kt[i] * dk[i];
+          ga += gxs[i] * vxt[i] * dvx[i];
+        }
+        part = group_sum(part, A.lph);
+        ga = group_sum(ga, A.lph);
+        const Silu<T> sa(part);
+        const T a = sa.s * Ce;
+        const T gs = ga * Ce * sa.d(part);
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+          gk[i] += gs * qs[i] * dk[i];
+          gvx[i] += gxs[i] * a * dvx[i];
+          gv1[i] += (h0[i] * w0t[i] + h1[i] * w1t[i] + h2[i] * w2t[i]) * dv1[i];
+          gv2[i] -= (h0[i] * u0 + h1[i] * u1 + h2[i] * u2) * dv2[i];
+          const T v1e = v1t[i] * dv1[i];
+          gw0[i] += h0[i] * v1e;
+          gw1[i] += h1[i] * v1e;
+          gw2[i] += h2[i] * v1e;
+        }
+      }
+    };
+    if constexpr (PD == 1) {
+      edge_chunks_pf<T, S, 1, St>(A, b, e, EPW, G, ld, body);
+    } else {
+      edge_chunks<T, S>(A, b, e, EPW, G, [&](int k, int s, T Ce, T u0, T u1, T u2, int row) {
+        St st;
+        ld(row, st);
+        body(k, s, Ce, u0, u1, u2, st, [] {});
+      });
+    }
+  }
+  xor_slots(gq, A.L); xor_slots(gk, A.L); xor_slots(gvx, A.L); xor_slots(gv1, A.L);
+  xor_slots(gv2, A.L); xor_slots(gw0, A.L); xor_slots(gw1, A.L); xor_slots(gw2, A.L);
+  T all[NA];
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    all[i] = gq[i]; all[V + i] = gk[i]; all[2 * V + i] = gvx[i]; all[3 * V + i] = gv1[i];
+    all[4 * V + i] = gv2[i]; all[5 * V + i] = gw0[i]; all[6 * V + i] = gw1[i]; all[7 * V + i] = gw2[i];
+  }
+  __syncthreads();  // the node vectors are dead: their LDS is the reduction's
+  reduce_waves<T, S, NA>(all, G.sub, lds);
+  if (t >= 0 && G.sub == 0 && G.es == 0) {
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+      gq[i] = all[i]; gk[i] = all[V + i]; gvx[i] = all[2 * V + i]; gv1[i] = all[3 * V + i];
+      gv2[i] = all[4 * V + i]; gw0[i] = all[5 * V + i]; gw1[i] = all[6 * V + i]; gw2[i] = all[7 * V + i];
+    }
+    const bool ag = A.acc & TMDNET_ACC_GRADS;
+    stv_acc<T, V>(A.gq + (size_t)t * A.ldq + c0, gq, ag);
+    stv_acc<T, V>(A.gk + (size_t)t * A.ldk + c0, gk, ag);
+    T* gvj = A.gv + (size_t)t * A.ldv + vo;
+    stv_acc<T, V>(gvj, gvx, ag);
+    stv_acc<T, V>(gvj + A.vst, gv1, ag);
+    stv_acc<T, V>(gvj + 2 * A.vst, gv2, ag);
+    if (A.gveci != nullptr) {
+      if (A.acc & TMDNET_ACC_VEC_RESIDUAL) {
+        T r0[V], r1[V], r2[V];  // (the node's gvec: its LDS copy was overwritten by the reduction)
+        const T* gr = A.gvec + (size_t)t * 3 * A.H + c0;
+        ldv<T, V>(r0, gr);
+        ldv<T, V>(r1, gr + A.H);
+        ldv<T, V>(r2, gr + 2 * A.H);
+#pragma unroll
+        for (int i = 0; i < V; ++i) { gw0[i] += r0[i]; gw1[i] += r1[i]; gw2[i] += r2[i]; }
+      }
+      T* gwj = A.gveci + (size_t)t * 3 * A.H + c0;
+      stv_acc<T, V>(gwj, gw0, ag);
+      stv_acc<T, V>(gwj + A.H, gw1, ag);
+      stv_acc<T, V>(gwj + 2 * A.H, gw2, ag);
+    }
+  }
+  zero_pad_rows(A, blk, nwg);
+}
+
+template <typename T, int V, int S, int PD>
+__global__ __launch_bounds__(256, 2) void k_bwd_merged(Args<T> A) {
+  bwd_merged_body<T, V, S, PD>(A, blockIdx.x, gridDim.x);
 }
 
 // ------------------------------------------------------------------ second-order backward
@@ -1314,6 +1576,13 @@ static int et_launch_vs(Args<T> A, hipStream_t st) {
   else if (KIND == 4) hipLaunchKernelGGL((k_bwd_dst<T, V, S, 1, true>), g, b, 0, st, A);
   else if (KIND == 5) hipLaunchKernelGGL((k_bwd_both<T, V, S, 1, true>), dim3(2 * nbn), b, 0, st, A);
   else if (KIND == 6) hipLaunchKernelGGL((k_bwd_both<T, V, S, 1, false, true>), dim3(2 * nbn), b, 0, st, A);
+  else if (KIND == 8 || KIND == 9) {
+    // dynamic LDS: the node vectors of the block's 4 / S nodes, or the cross-wave reduction
+    const size_t node = (size_t)(4 / S) * 12 * A.H, red = S > 1 ? 4 * 64 * 8 * V : 1;
+    const size_t bytes = (node > red ? node : red) * sizeof(T);
+    if (KIND == 8) hipLaunchKernelGGL((k_bwd_merged<T, V, S, 1>), dim3(nbn), b, bytes, st, A);
+    else hipLaunchKernelGGL((k_bwd_merged<T, V, S, 0>), dim3(nbn), b, bytes, st, A);
+  }
   else hipLaunchKernelGGL((k_bwd_dst<T, V, S, 1, false, true>), g, b, 0, st, A);
   return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
 }
@@ -1426,6 +1695,14 @@ static int bwd(int n, int H, int heads, const int32_t* row_ptr, const int32_t* s
   if (!dr && ((A.pk && !gpk) || (A.pv && !gpv))) return kBadArgument;
   static const int fuse_nodes = getenv("TMDNET_ET_FUSE") ? atoi(getenv("TMDNET_ET_FUSE")) : kBwdFuseNodes;
   const bool ag = !dr && (acc & TMDNET_ACC_GRADS) && (A.pk || A.pv);  // injected projection cotangents
+  // dr mode: both roles in one pass over the rows (k_bwd_merged)
+  // (tuning: TMDNET_ET_MERGED=0 off, 1 stream-prefetching variant, 2 loads per edge in the body).
+  // Large graphs only: C5 2.97 vs 3.38 ms per layer (the two passes); at C2 the two passes in one
+  // grid (k_bwd_both, twice the waves at 167 vs 222 VGPRs) win, 51 vs 69 us.
+  static const int merged = getenv("TMDNET_ET_MERGED") ? atoi(getenv("TMDNET_ET_MERGED")) : 1;
+  static const int merged_min = getenv("TMDNET_ET_MERGED_MIN") ? atoi(getenv("TMDNET_ET_MERGED_MIN")) : kBwdFuseNodes;
+  if (dr && merged && n >= merged_min && !(acc & TMDNET_ET_TWO_PASS) && !A.gpk && !A.gpv)
+    return merged == 2 ? et_launch<T, 9, false>(V, A, st) : et_launch<T, 8, false>(V, A, st);
   if (n < fuse_nodes)
     return dr ? et_launch<T, 5, false>(V, A, st) : ag ? et_launch<T, 6, false>(V, A, st) : et_launch<T, 3, false>(V, A, st);
   rc = dr ? et_launch<T, 4, false>(V, A, st) : ag ? et_launch<T, 7, false>(V, A, st) : et_launch<T, 1, false>(V, A, st);

@@ -21,6 +21,7 @@ ACC_VEC_RESIDUAL, ACC_EDGE = 1, 2
 ACC_GRADS = 32
 ET_V_PLANAR = 4
 BWD2_ACC_EDGE, BWD2_ACC_GVEC = 8, 16
+ET_TWO_PASS = 64
 
 _STATUS = {1: "bad argument", 2: "unsupported configuration", 3: "kernel launch failed",
            4: "workspace too small"}
