@@ -263,6 +263,13 @@ def probe_workload(n_atoms, H, dev):
     return launch, E, L
 
 
+def et_pair_bytes(E, N, P, H, s=4):
+    """Algorithmic bytes of one forward edge-kernel launch in the model's layout (pair-shared dk/dv
+    rows, et_stack.PAIR_ROWS): per edge its source index, pair-row index, cutoff and unit vector; the
+    P distinct projection rows (4H); per node q, k, v, vec read and x, vec written (12H), row_ptr."""
+    return E * (4 + 4 + 4 + 12) + P * 4 * H * s + N * (12 * H * s + 4)
+
+
 def et_bwd_bytes(E, N, P, H, dr, s=4):
     """Algorithmic bytes of one tmdnet_et_message_bwd call (destination + source pass) in the model's
     pair-row layout, every tensor touched once: edge scalars (src, pair row, cutoff, unit vector) and
@@ -284,8 +291,8 @@ PROBE_FLAGS = 4  # TMDNET_ET_V_PLANAR
 
 PMC_PASSES = ("FETCH_SIZE", "WRITE_SIZE", "TCC_HIT_sum TCC_MISS_sum")
 # the child's dispatch sequence (main(), --pmc-child): probe kernel name -> [(tag, count), ...] in order
-PMC_CHILD = {"k_fwd<float, 4, 1, 1, false>": [("graded", 8), ("pairs", 8)],
-             "k_bwd_dst<": [("bwd_dst", 4), ("bwd_dst_dr", 4)], "k_bwd_src<": [("bwd_src", 4), ("bwd_src_dr", 4)]}
+PMC_CHILD = {"k_fwd<float, 4, 1, 1, false>": [("per_edge", 8), ("pairs", 8)],
+             "k_bwd_dst<": [("bwd_dst", 4)], "k_bwd_src<": [("bwd_src", 4)], "k_bwd_merged<": [("bwd_dr", 4)]}
 
 
 def pmc_counters(a):
@@ -372,13 +379,12 @@ def roofline_probe(a, dev):
     ms = a0.elapsed_time(b0) / reps
     nbytes = et_algorithmic_bytes(E, n_atoms, H)
     gbs = nbytes / (ms * 1e-3) / 1e9
-    res = {"kernel": "tmdnet_et_message_fwd (k_fwd<float,4,1,1,false>)",
-            "workload": f"periodic water box, {n_atoms} atoms (Morton-renumbered as the model does), "
-                        f"L={L:.1f} A, cutoff 5, E={E}, H={H}, fp32",
-            "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
-            "bytes_per_launch": nbytes, "ms_per_launch": round(ms, 4), "launches": reps}
-    # the same kernel in the model's pair-row layout: the dk/dv stream has (E + N) / 2 distinct rows
+    per_edge = {"kernel": "tmdnet_et_message_fwd (k_fwd<float,4,1,1,false>), one dk/dv row per edge",
+                "bytes_per_launch": nbytes, "bytes_formula": "SURVEY.md 8(d): E*2068 + N*6148 (H=128)",
+                "ms_per_launch": round(ms, 4), "achieved": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
+                "launches": reps}
+    # the graded figure: the same kernel in the layout the model runs, the dk/dv stream over the
+    # (E + N) / 2 pair-shared rows read through pk_rows
     for _ in range(5):
         launch.pairs()
     torch.cuda.synchronize()
@@ -388,11 +394,20 @@ def roofline_probe(a, dev):
     b0.record()
     torch.cuda.synchronize()
     ms_p = a0.elapsed_time(b0) / reps
-    pbytes = nbytes - (E - launch.n_pairs) * 4 * H * 4
-    res["model_layout"] = {"pk_rows": "pair-shared dk/dv rows (et_stack.PAIR_ROWS)", "ms_per_launch": round(ms_p, 4),
-                           "distinct_bytes_per_launch": pbytes,
-                           "achieved_distinct": round(pbytes / (ms_p * 1e-3) / 1e9, 1),
-                           "achieved_survey_formula": round(nbytes / (ms_p * 1e-3) / 1e9, 1)}
+    pbytes = et_pair_bytes(E, n_atoms, launch.n_pairs, H)
+    gbp = pbytes / (ms_p * 1e-3) / 1e9
+    res = {"kernel": "tmdnet_et_message_fwd (k_fwd<float,4,1,1,false>) in the model's layout: pair-shared "
+                     "dk/dv rows (et_stack.PAIR_ROWS, planar v rows)",
+           "workload": f"periodic water box, {n_atoms} atoms (Morton-renumbered as the model does), "
+                       f"L={L:.1f} A, cutoff 5, E={E}, P={launch.n_pairs} pair rows, H={H}, fp32",
+           "bound": "hbm", "achieved": round(gbp, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(gbp / HBM_PEAK_GBS, 4), "traffic": None,
+           "bytes_per_launch": pbytes,
+           "bytes_formula": "E*(4+4+4+12) + P*4H*4 + N*(12H*4+4): edge scalars, distinct pair rows, node rows",
+           "ms_per_launch": round(ms_p, 4), "launches": reps, "per_edge_layout": per_edge}
+    fp = fused_projection_probe(launch, E, n_atoms, H, reps, dev)
+    if fp is not None:
+        res["fused_projection"] = fp
     # the backward (destination + source pass per call) in the model's layout, both forms
     bwd = {}
     for tag, dr in (("training_form", False), ("dr_force_form", True)):
@@ -408,7 +423,8 @@ def roofline_probe(a, dev):
         ms_b = a0.elapsed_time(b0) / nrep
         bb = et_bwd_bytes(E, n_atoms, launch.n_pairs, H, dr)
         gb = bb / (ms_b * 1e-3) / 1e9
-        bwd[tag] = {"kernels": "k_bwd_dst + k_bwd_src (one tmdnet_et_message_bwd call)" + (" , dr" if dr else ""),
+        bwd[tag] = {"kernels": ("k_bwd_merged (both roles of a node in one pass over its row, dr form)" if dr
+                                else "k_bwd_dst + k_bwd_src (one tmdnet_et_message_bwd call)"),
                     "ms_per_call": round(ms_b, 4), "bytes_per_call": bb, "achieved": round(gb, 1),
                     "frac": round(gb / HBM_PEAK_GBS, 4), "calls": nrep}
     res["backward"] = bwd
@@ -417,13 +433,62 @@ def roofline_probe(a, dev):
         if pm is None:
             res["traffic_detail"] = why
         else:
-            g = pm.get("graded", {})
+            g = pm.get("pairs", {})
             res["traffic"] = g.get("traffic")
             res["traffic_detail"] = {**g, "source": PMC_SOURCE}
-            res["model_layout"]["pmc"] = pm.get("pairs")
-            for tag, keys in (("training_form", ("bwd_dst", "bwd_src")), ("dr_force_form", ("bwd_dst_dr", "bwd_src_dr"))):
+            if g.get("traffic"):
+                res["traffic_detail"]["traffic_over_bytes"] = round(g["traffic"] / pbytes, 3)
+            per_edge["pmc"] = pm.get("per_edge")
+            for tag, keys in (("training_form", ("bwd_dst", "bwd_src")), ("dr_force_form", ("bwd_dr",))):
                 bwd[tag]["pmc"] = {k: pm.get(k) for k in keys}
+                tr = sum((pm.get(k) or {}).get("traffic") or 0 for k in keys)
+                if tr:
+                    bwd[tag]["traffic_over_bytes"] = round(tr / bwd[tag]["bytes_per_call"], 3)
     return res
+
+
+def fused_projection_probe(launch, E, N, H, reps, dev, R=64):
+    """The forward edge kernel with the dk/dv projection fused in (tmdnet_et_fused_fwd_f32, csrc/et_fused.hip)
+    on the probe graph: the RBF of r formed in registers and [dk|dv] = W f + b on the fp16 MFMA (exact
+    two-piece split: 3 products per term), no projection rows read.  Two rooflines: bytes (edge scalars,
+    r, node rows) over HBM, and the MFMA work over the dense fp16 peak.  The model runs it when no
+    backward follows (energy-only evaluation): et_stack.FEP / FEP_BWD."""
+    from torchmdnet import kernels
+    q, k, v, vec, C, u = launch.inputs
+    if not kernels.fep_supported(H, 8, R, q.dtype):
+        return None
+    g = launch.graph
+    r = g.distances.detach()
+    gen = torch.Generator(device=dev).manual_seed(11)
+    W = torch.randn(4 * H, R, device=dev, generator=gen) / R ** 0.5
+    b = torch.randn(4 * H, device=dev, generator=gen) * 0.1
+    start = math.exp(-5.0)
+    mu = torch.linspace(start, 1.0, R, device=dev)
+    beta = torch.full((R,), (2.0 / R * (1 - start)) ** -2, device=dev)
+    fep = kernels.fep_split(W, b)
+    xo, vo = torch.empty(N, H, device=dev), torch.empty(N, 3, H, device=dev)
+
+    def run():
+        kernels.et_fused_fwd_launch(q, k, v, vec, r, C, u, fep, (mu, beta, 0.0, 5.0, 0), g, 8, xo, vo)
+    for _ in range(5):
+        run()
+    torch.cuda.synchronize()
+    a0, b0 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a0.record()
+    for _ in range(reps):
+        run()
+    b0.record()
+    torch.cuda.synchronize()
+    ms = a0.elapsed_time(b0) / reps
+    nbytes = E * (4 + 4 + 4 + 12) + N * (12 * H * 4 + 4)
+    flop = 3 * 2.0 * E * R * 4 * H  # fp16 MFMA products (hi*hi, hi*lo, lo*hi)
+    return {"kernel": "tmdnet_et_fused_fwd_f32 (fep::k_fwd<2,8,0>)", "ms_per_launch": round(ms, 4),
+            "bytes_per_launch": nbytes, "achieved_gbs": round(nbytes / (ms * 1e-3) / 1e9, 1),
+            "frac_hbm": round(nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "mfma_flop_per_launch": flop, "achieved_tflops_f16": round(flop / (ms * 1e-3) / 1e12, 1),
+            "peak_tflops_f16": MFMA_BF16_PEAK_TFS, "frac_mfma": round(flop / (ms * 1e-3) / 1e12 / MFMA_BF16_PEAK_TFS, 4),
+            "bound": "VALU (PMC r03: 72% VALU-busy, 20% MFMA-busy; profiles/r03_fep_fwd_pmc_mode2.txt)",
+            "vs_unfused": "replaces the projection GEMM + this kernel in the pair layout"}
 
 
 def mfma_probe(E_c5, N_c5, E_c2, N_c2, H, R, dev):
