@@ -144,8 +144,15 @@ def host_cpu_info():
         aff = os.cpu_count() or 1
     omp = os.environ.get("OMP_NUM_THREADS")
     threads = min(aff, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else aff
+    quota = None  # the container's CPU bandwidth limit (cgroup v2 cpu.max "quota period"), in CPUs
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
     return {"cpu_model": model, "physical_cores_machine": len(phys) or None, "logical_cpus": os.cpu_count(),
-            "affinity_cpus": aff, "omp_num_threads_env": omp, "threads_used": threads}
+            "affinity_cpus": aff, "cgroup_cpu_quota": quota, "omp_num_threads_env": omp, "threads_used": threads}
 
 
 def setup_dist():
@@ -697,6 +704,27 @@ def secondary_tensornet(a, ws, rank, dev):
             "ms_per_step": round(1000 * el / a.steps, 4), "atoms_per_gpu": int(z.shape[0])}
 
 
+def secondary_scripted(a, ws, rank, dev):
+    """The bench model (C2 ET-QM9, 32 molecules per GPU) as torch.jit.script(model) -- the form MD
+    engines load (reference README.md:6, tests/test_model.py:42-84) -- energy + forces, eager, beside
+    the same model unscripted and eager (the headline replays a HIP graph)."""
+    from torchmdnet.models.model import create_model
+    torch.manual_seed(0)
+    model = create_model(et_args(a.channels)).to(dev)
+    z, pos, batch = qm9_like(a.batch, gen_seed=1 + rank)
+    z, pos, batch = z.to(dev), pos.float().to(dev), batch.to(dev)
+    scripted = torch.jit.script(model)
+    steps = max(10, a.steps)
+    el_s = timed_loop(lambda: scripted(z, pos, batch), a.warmup, steps, ws, dev)
+    el_e = timed_loop(lambda: model(z, pos, batch), a.warmup, steps, ws, dev)
+    return {"workload": "ET-QM9 energy+forces (C2 batch) through torch.jit.script(model), eager",
+            "value": round(a.batch * ws * steps / el_s, 2), "unit": "molecules/s",
+            "ms_per_step": round(1000 * el_s / steps, 4),
+            "eager_unscripted_ms_per_step": round(1000 * el_e / steps, 4),
+            "path": "per-layer dispatcher ops (tmdnet::neighbor_graph, edge_geometry, nbr_embed, et_message) + "
+                    "ATen GEMMs / LayerNorm; the fused stack (et_stack.py) is eager-only"}
+
+
 def secondary_water_box(a, ws, rank, dev):
     """C5: ET (the bench model: 128 ch, 8 layers, cutoff 5) on a periodic ~50k-atom water box,
     energy + forces through TorchMD_Net (cell-list neighbour search in the box, Morton renumbering,
@@ -795,23 +823,30 @@ def cpu_baseline(model, args, z, pos, batch, seconds):
     sd = _cpu_sd(model)
     mols = int(batch.max()) + 1
     share = info["threads_used"]
+    run = lambda secs: _time_cpu(lambda: O.energy_forces(sd, dict(args), z, pos, batch, dtype=torch.float32,  # noqa: E731
+                                                         create_graph=True), secs)
+    torch.set_num_threads(cores)
+    n, el = run(seconds)
+    all_cores = {"value": round(mols * n / el, 2), "unit": "molecules/s", "cores": cores,
+                 "sample": f"{n} calls, {el:.1f} s"}
     share_line = None
     if share != cores:
         torch.set_num_threads(share)
-        n_s, el_s = _time_cpu(lambda: O.energy_forces(sd, dict(args), z, pos, batch, dtype=torch.float32,
-                                                         create_graph=True), seconds / 2)
+        n_s, el_s = run(seconds / 2)
         share_line = {"value": round(mols * n_s / el_s, 2), "unit": "molecules/s", "cores": share,
                       "sample": f"{n_s} calls, {el_s:.1f} s"}
-    torch.set_num_threads(cores)
-    n, el = _time_cpu(lambda: O.energy_forces(sd, dict(args), z, pos, batch, dtype=torch.float32,
-                                                 create_graph=True), seconds)
-    return {"value": round(mols * n / el, 2), "unit": "molecules/s", "cores": cores, "kind": "port",
-            "host": info, "omp_share": share_line,
+    # the headline CPU figure is the FASTER of the two thread counts (on a box whose CPU bandwidth is
+    # capped below its core count -- cgroup_cpu_quota -- threads on every physical core oversubscribe
+    # the share and run slower); both are reported
+    best = all_cores if share_line is None or all_cores["value"] >= share_line["value"] else share_line
+    torch.set_num_threads(best["cores"])
+    return {"value": best["value"], "unit": "molecules/s", "cores": best["cores"], "kind": "port",
+            "host": info, "all_physical_cores": all_cores, "omp_share": share_line,
             "calibration": "profiles/r02_cpu_calibration.json (restatement vs the shimmed reference, same "
                            "8 cores of the build container)",
-            "sample": f"oracle/model_oracle.py (PyTorch-CPU restatement of the reference ET path), "
-                      f"{n} energy+force calls on the same {mols} molecules / weights, float32, "
-                      f"{el:.1f} s, torch threads={cores}"}
+            "sample": f"oracle/model_oracle.py (PyTorch-CPU restatement of the reference ET path), energy+force "
+                      f"calls on the same {mols} molecules / weights, float32, timed at {cores} and {share} "
+                      f"threads; headline = the faster ({best['cores']} threads, {best['sample']})"}
 
 
 def cpu_baseline_extra(a, model, args, z, pos, batch):
@@ -1004,6 +1039,8 @@ def main():
         sec["et_train_step"] = secondary_train(a, ws, rank, dev)
         phase("secondary: ET-SPICE C4")
         sec["et_spice_c4"] = secondary_spice(a, ws, rank, dev)
+        phase("secondary: TorchScript C2")
+        sec["et_scripted_c2"] = secondary_scripted(a, ws, rank, dev)
         phase("secondary: ET C5 water box")
         sec["et_water_box_c5"] = secondary_water_box(a, ws, rank, dev)
         if rank == 0:
