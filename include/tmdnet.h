@@ -478,6 +478,14 @@ int tmdnet_pair_index(int n_nodes, const int32_t* row_ptr, const int32_t* src, c
  * Requirements: K % 64 == 0, lda % 4 == 0, A 16-byte aligned (and B when trans_b); else
  * TMDNET_UNSUPPORTED (callers use the library GEMM).  Exact fp32 arithmetic. */
 int tmdnet_gemm_f32(int n_problems, const int* dims, const void* const* ptrs, void* stream);
+/* tmdnet_gemm_f32 with a fused epilogue (a Linear + SiLU stack in one launch per layer, and its
+ * backward chain): dims 10 per problem = the 8 of tmdnet_gemm_f32 + (act, ld_x); ptrs 7 per problem =
+ * (A, B, bias, C, pre, rscale, dpre).  Per output element: v = A op(B) + bias (+ C if beta);
+ * pre != NULL: pre[r][c] = v (row stride ld_x); act = 1: v = silu(v); rscale != NULL: v *= rscale[r];
+ * dpre != NULL: v *= silu'(dpre[r][c]) (row stride ld_x); C[r][c] = v.  act in {0, 1}.  Replaces the
+ * separate activation launches of the reference's Linear -> act chains (TensorNet edge / embedding
+ * MLPs and output head, tensornet.py:233, 320-321, 381-385). */
+int tmdnet_gemm_ex_f32(int n_problems, const int* dims, const void* const* ptrs, void* stream);
 /* Grouped fp32 weight-gradient GEMM: for each of n_problems (<= 32) C (+)= A^T B + A2^T B2, the sum
  * running over the ROWS of A [K][M] (lda), B [K][N] (ldb) and the optional second segment A2 [K2][M],
  * B2 [K2][N]; C [M][N] (ldc).  ones1 / ones2: column N-1 of B / B2 is a column of ones (not read; with

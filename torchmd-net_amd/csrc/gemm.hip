@@ -31,6 +31,13 @@ struct Prob {
   const float* bias;
   float* C;
   int tiles_n, tile0;
+  // epilogue extensions (tmdnet_gemm_ex_f32; all off for tmdnet_gemm_f32): v = acc + bias (+ C) ->
+  // pre[r][c] = v (the pre-activation a backward needs) -> v = silu(v) (act) -> v *= rscale[r] ->
+  // v *= silu'(dpre[r][c]) (a backward chain: the next-lower layer's activation derivative) -> C
+  int act, ldx;  // ldx: row stride of pre / dpre
+  float* pre;
+  const float* rscale;
+  const float* dpre;
 };
 
 struct Group {
@@ -101,6 +108,13 @@ __device__ __forceinline__ void store(const Prob& P, int gr, int gc, float v) {
   if (P.bias) v += P.bias[gc];
   float* out = P.C + (size_t)gr * P.ldc + gc;
   if (P.beta) v += *out;
+  if (P.pre) P.pre[(size_t)gr * P.ldx + gc] = v;
+  if (P.act) v = Silu<float>(v).s;
+  if (P.rscale) v *= P.rscale[gr];
+  if (P.dpre) {
+    const float x = P.dpre[(size_t)gr * P.ldx + gc];
+    v *= Silu<float>(x).d(x);
+  }
   *out = v;
 }
 
@@ -651,11 +665,12 @@ __global__ __launch_bounds__(256) void k_embed_fwd(int n, int num_types, const i
 
 using namespace tmd;
 
+static int gemm_run(gemm::Group& G, void* stream);
+
 extern "C" int tmdnet_gemm_f32(int n_problems, const int* dims, const void* const* ptrs, void* stream) {
   if (n_problems < 1 || n_problems > 4 || !dims || !ptrs) return kBadArgument;
   gemm::Group G{};
   G.n = n_problems;
-  int tiles = 0;
   for (int i = 0; i < n_problems; ++i) {
     const int* d = dims + 8 * i;
     gemm::Prob& P = G.p[i];
@@ -665,6 +680,38 @@ extern "C" int tmdnet_gemm_f32(int n_problems, const int* dims, const void* cons
     P.B = (const float*)ptrs[4 * i + 1];
     P.bias = (const float*)ptrs[4 * i + 2];
     P.C = (float*)ptrs[4 * i + 3];
+  }
+  return gemm_run(G, stream);
+}
+
+extern "C" int tmdnet_gemm_ex_f32(int n_problems, const int* dims, const void* const* ptrs, void* stream) {
+  if (n_problems < 1 || n_problems > 4 || !dims || !ptrs) return kBadArgument;
+  gemm::Group G{};
+  G.n = n_problems;
+  for (int i = 0; i < n_problems; ++i) {
+    const int* d = dims + 10 * i;
+    gemm::Prob& P = G.p[i];
+    P.M = d[0]; P.N = d[1]; P.K = d[2]; P.lda = d[3]; P.ldb = d[4]; P.ldc = d[5];
+    P.trans_b = d[6]; P.beta = d[7]; P.act = d[8]; P.ldx = d[9];
+    const void* const* q = ptrs + 7 * i;
+    P.A = (const float*)q[0];
+    P.B = (const float*)q[1];
+    P.bias = (const float*)q[2];
+    P.C = (float*)q[3];
+    P.pre = (float*)q[4];
+    P.rscale = (const float*)q[5];
+    P.dpre = (const float*)q[6];
+    if (P.act != 0 && P.act != 1) return kUnsupported;
+    if ((P.pre || P.dpre) && P.ldx < P.N) return kBadArgument;
+  }
+  return gemm_run(G, stream);
+}
+
+static int gemm_run(gemm::Group& G, void* stream) {
+  const int n_problems = G.n;
+  int tiles = 0;
+  for (int i = 0; i < n_problems; ++i) {
+    gemm::Prob& P = G.p[i];
     if (P.M <= 0 || P.N <= 0 || P.K <= 0 || !P.A || !P.B || !P.C) return kBadArgument;
     // K in 16-wide blocks (a wave's K slice may be empty: K = 32 over 4 waves leaves two idle)
     if (P.K % 16 || P.lda % 4 || (P.trans_b && P.ldb % 4) || P.lda < P.K || P.ldc < P.N) return kUnsupported;

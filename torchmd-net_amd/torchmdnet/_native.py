@@ -80,6 +80,7 @@ SIGNATURES = {
     "tmdnet_atom_sum_fwd": (I, [I, I, I, P, P, P, P, P, P]),
     "tmdnet_atom_sum_bwd": (I, [I, I, I, P, P, P, P, P]),
     "tmdnet_gemm_f32": (I, [I, P, P, P]),
+    "tmdnet_gemm_ex_f32": (I, [I, P, P, P]),
     "tmdnet_gemm_tn_f32": (I, [I, P, P, P]),
     "tmdnet_gemm_tn_workspace_bytes": (ctypes.c_size_t, [I, P]),
     "tmdnet_gemm_tn_f32_ws": (I, [I, P, P, P, ctypes.c_size_t, P]),

@@ -1925,6 +1925,162 @@ def linear(x, w, b=None):
     return _Linear.apply(x, w, b)
 
 
+# ----------------------------------------------------------------------------- Linear + SiLU stacks
+def gemm_ex_launch(problems):
+    """``tmdnet_gemm_ex_f32``: up to 4 problems, dicts with A, B, C and optional trans_b (default True),
+    bias, beta, act (0/1), pre, rscale, dpre (pre / dpre share a row stride).  Returns False when
+    outside the kernel's envelope (nothing launched)."""
+    if not problems or len(problems) > 4:
+        return False
+    for p in problems:
+        A, C = p["A"], p["C"]
+        if (A.dtype != torch.float32 or not A.is_cuda or not 0 < A.shape[0] <= GEMM_MAX_ROWS or A.shape[1] == 0
+                or C.shape[1] == 0 or A.stride(1) != 1 or p["B"].stride(1) != 1 or C.stride(1) != 1):
+            return False
+    lib = nat.load()
+    n = len(problems)
+    dims = (ctypes.c_int * (10 * n))()
+    ptrs = (ctypes.c_void_p * (7 * n))()
+    for i, p in enumerate(problems):
+        A, B, C = p["A"], p["B"], p["C"]
+        x = p.get("pre") if p.get("pre") is not None else p.get("dpre")
+        if x is not None and (x.stride(1) != 1 or x.shape != C.shape):
+            return False
+        dims[10 * i:10 * i + 10] = [A.shape[0], C.shape[1], A.shape[1], A.stride(0), B.stride(0), C.stride(0),
+                                    int(p.get("trans_b", True)), int(bool(p.get("beta"))), int(p.get("act", 0)),
+                                    0 if x is None else x.stride(0)]
+        ptrs[7 * i:7 * i + 7] = [A.data_ptr(), B.data_ptr()] + [
+            None if p.get(k) is None else p[k].data_ptr() for k in ("bias", "C", "pre", "rscale", "dpre")]
+    rc = lib.tmdnet_gemm_ex_f32(n, dims, ptrs, nat.stream(problems[0]["A"].device))
+    if rc == GEMM_UNSUPPORTED:
+        return False
+    nat.check(rc, "tmdnet_gemm_ex_f32")
+    return True
+
+
+def _mlp_composite(x, scale, *wb):
+    """Differentiable restatement: silu(Linear) layers, the last one times scale[:, None]."""
+    L = len(wb) // 2
+    h = x
+    for i in range(L):
+        h = F.silu(F.linear(h, wb[i], wb[L + i]))
+    return h if scale is None else h * scale.view(-1, 1)
+
+
+class _MLPAct(Function):
+    """h_{i+1} = silu(h_i W_i^T + b_i), the last layer times a per-row scale (reference tensornet.py
+    edge MLP 381-385 with the cutoff, embedding MLP 320-321, output head 233): every layer ONE
+    tmdnet_gemm_ex_f32 launch with the activation (and the pre-activation a backward needs) in its
+    epilogue -- the separate activation launch per layer is gone.  The backward runs the chain with
+    each layer's silu' in the epilogue of the GEMM that produces the gradient feeding it, and all
+    weight / bias gradients in one grouped TN launch."""
+
+    @staticmethod
+    def forward(ctx, x, scale, *wb):
+        L = len(wb) // 2
+        ws, bs = wb[:L], wb[L:]
+        o = dict(dtype=x.dtype, device=x.device)
+        h, pres, hs = x, [], []
+        for i in range(L):
+            pre = torch.empty((x.shape[0], ws[i].shape[0]), **o)
+            y = torch.empty_like(pre)
+            ok = gemm_ex_launch([{"A": h, "B": ws[i], "bias": bs[i], "C": y, "pre": pre, "act": 1,
+                                  "rscale": scale if i == L - 1 else None}])
+            if not ok:
+                raise RuntimeError("mlp_act: shape outside tmdnet_gemm_ex_f32's envelope")
+            pres.append(pre)
+            hs.append(h)
+            h = y
+        ctx.L = L
+        ctx.save_for_backward(x, scale, *ws, *bs, *pres, *hs[1:])
+        return h
+
+    @staticmethod
+    def backward(ctx, gy):
+        L = ctx.L
+        sv = ctx.saved_tensors
+        x, scale = sv[0], sv[1]
+        ws, bs = sv[2:2 + L], sv[2 + L:2 + 2 * L]
+        pres, hmid = sv[2 + 2 * L:2 + 3 * L], sv[2 + 3 * L:]
+        nf = ctx.next_functions
+        need = [ctx.needs_input_grad[i] and _will_run(nf[i][0]) for i in range(2 + 2 * L)]
+        if not any(need):
+            return (None,) * (2 + 2 * L)
+        outs = _MLPActBwd.apply(tuple(need), gy.contiguous(), x, scale, *ws, *bs, *pres, *hmid)
+        return tuple(o if n else None for o, n in zip(outs, need))
+
+
+class _MLPActBwd(Function):
+    @staticmethod
+    def forward(ctx, need, gy, x, scale, *rest):
+        L = (len(rest) + 1) // 4
+        ws, bs, pres, hmid = rest[:L], rest[L:2 * L], rest[2 * L:3 * L], rest[3 * L:]
+        hs = (x,) + tuple(hmid)
+        o = dict(dtype=x.dtype, device=x.device)
+        # the last layer: g_pre = gy * scale * silu'(pre), g_scale = sum_c gy * silu(pre) (tmdnet_silu_bwd)
+        gpre = torch.empty_like(pres[-1])
+        gs = torch.empty(x.shape[0], **o) if (scale is not None and need[1]) else None
+        silu_bwd_launch(pres[-1], scale, gy, gpre, gs)
+        gpres = [None] * L
+        gpres[L - 1] = gpre
+        gx = None
+        for i in range(L - 1, -1, -1):
+            if i > 0:  # the lower layer's pre-activation gradient: (g_pre_i W_i) * silu'(pre_{i-1})
+                g = torch.empty_like(pres[i - 1])
+                gemm_ex_launch([{"A": gpres[i], "B": ws[i], "trans_b": False, "C": g, "dpre": pres[i - 1]}]) or \
+                    _raise("mlp_act backward: GEMM envelope")
+                gpres[i - 1] = g
+            elif need[0]:
+                gx = torch.empty_like(x)
+                gemm_ex_launch([{"A": gpres[0], "B": ws[0], "trans_b": False, "C": gx}]) or \
+                    _raise("mlp_act backward: GEMM envelope")
+        gw, gb = [None] * L, [None] * L
+        tn = []
+        for i in range(L):
+            wn, bn = need[2 + i], need[2 + L + i]
+            if wn or bn:
+                gw[i] = torch.empty_like(ws[i]) if wn else None
+                gb[i] = torch.empty_like(bs[i]) if bn else None
+                if wn:
+                    tn.append({"A": gpres[i], "B": hs[i], "C": gw[i], "Cb": gb[i], "ones": bool(bn)})
+                else:
+                    tn.append({"A": gpres[i], "B": None, "C": gb[i].view(-1, 1), "ones": True})
+        wgrad_tn(tn)
+        ctx.save_for_backward(gy, x, scale, *ws, *bs)
+        ctx.L = L
+        return (gx, gs, *gw, *gb)
+
+    @staticmethod
+    def backward(ctx, *ggs):
+        from .tn_node import _double_backward
+        L = ctx.L
+        sv = ctx.saved_tensors
+        gy, x, scale = sv[0], sv[1], sv[2]
+        wb = list(sv[3:3 + 2 * L])
+        d = _double_backward(_mlp_composite, [x, scale] + wb, [gy], list(ggs))
+        # (need, gy, x, scale, *ws, *bs, *pres, *hmid): pres / hmid are functions of the others
+        return (None, d[0], d[1], d[2], *d[3:3 + 2 * L]) + (None,) * (2 * L - 1)
+
+
+def _raise(msg):
+    raise RuntimeError(msg)
+
+
+def mlp_act(x, weights, biases, act, scale=None):
+    """``act(... act(x W_0^T + b_0) ...) * scale[:, None]`` for nn.Linear weights / biases: the hand
+    fused path for SiLU on fp32 CUDA rows within the GEMM envelope, else Linear + fused_act per layer."""
+    L = len(weights)
+    ok = (isinstance(act, torch.nn.SiLU) and x.is_cuda and x.dtype == torch.float32 and x.dim() == 2
+          and 0 < x.shape[0] <= GEMM_MAX_ROWS and all(b is not None for b in biases)
+          and all(w.shape[1] % 16 == 0 for w in weights) and all(w.shape[0] % 16 == 0 for w in weights))
+    if not ok:
+        for i in range(L):
+            x = fused_act(act, linear(x, weights[i], biases[i]), scale if i == L - 1 else None)
+        return x
+    x = x.contiguous()
+    return _MLPAct.apply(x, None if scale is None else scale.contiguous(), *weights, *biases)
+
+
 # ----------------------------------------------------------------------------- training loss
 class _MSE2(Function):
     """w1 * mse(a1, b1) + w2 * mse(a2, b2), mean reductions (reference LNNP.step's E + F loss,

@@ -187,7 +187,7 @@ class TensorNet(nn.Module):
             X = layer(X, graph, graph.distances, edge_attr)
         x = tn_node.norms(X)  # cat(|I|^2, |A|^2, |S|^2) of decompose_tensor(X), one fused pass
         x = self.out_norm(x)
-        return kernels.fused_act(self.act, kernels.linear(x, self.linear.weight, self.linear.bias))
+        return kernels.mlp_act(x, [self.linear.weight], [self.linear.bias], self.act)
 
 
 def _check_symmetric_graph(edge_index, n):
@@ -270,8 +270,8 @@ class TensorEmbedding(nn.Module):
         norm = self.init_norm(tn_node.enorm(Ec))
         lt = self.linears_tensor
         Ec = tn_node.mix3(Ec, lt[0].weight, lt[1].weight, lt[2].weight)
-        for linear_scalar in self.linears_scalar:
-            norm = kernels.fused_act(self.act, kernels.linear(norm, linear_scalar.weight, linear_scalar.bias))
+        ls = self.linears_scalar  # Linear + act stack, the activations in the GEMM epilogues
+        norm = kernels.mlp_act(norm, [m.weight for m in ls], [m.bias for m in ls], self.act)
         # new_radial_tensor(I, A, S, norm[..., 0], norm[..., 1], norm[..., 2]) and I + A + S
         return tn_node.eout(Ec, norm)
 
@@ -326,10 +326,8 @@ class Interaction(nn.Module):
         if perm is not None:
             edge_weight, edge_attr = edge_weight[perm], edge_attr[perm]
         C = graph.cutoff if (perm is None and graph.cutoff is not None) else self.cutoff(edge_weight)
-        ls = self.linears_scalar
-        for linear_scalar in ls[:-1]:
-            edge_attr = kernels.fused_act(self.act, kernels.linear(edge_attr, linear_scalar.weight, linear_scalar.bias))
-        edge_attr = kernels.fused_act(self.act, kernels.linear(edge_attr, ls[-1].weight, ls[-1].bias), C)  # act(.) * C
+        ls = self.linears_scalar  # act(Linear) x 3, the last times C (reference 381-385), one launch per layer
+        edge_attr = kernels.mlp_act(edge_attr, [m.weight for m in ls], [m.bias for m in ls], self.act, C)
         lt = self.linears_tensor
         # X / (|X|^2 + 1), decompose, three channel mixes -> Y as compact [9, N, H] (I | A | S rows)
         Yc = tn_node.mix3(tn_node.pre(X), lt[0].weight, lt[1].weight, lt[2].weight)
