@@ -42,6 +42,14 @@ enum { TMDNET_BWD2_ACC_EDGE = 8, TMDNET_BWD2_ACC_GVEC = 16 };
  * source) instead of the merged pass that serves both roles of a node from one read of each pair row
  * (the default from 16384 nodes; same results up to summation order). */
 enum { TMDNET_ET_TWO_PASS = 64 };
+/* Activations of the ET message entry points (tmdnet_et_message_fwd flags, _bwd accumulate, _bwd2 /
+ * _bwd2_ex flags): bits 8-11 = the dk / dv projections' activation (reference EquivariantMultiHeadAttention
+ * `activation`, torchmd_et.py:285-291), bits 12-15 = the attention activation (`attn_activation`,
+ * torchmd_et.py:316), coded as the reference act_class_mapping (models/utils.py:579-584): SiLU (0, the
+ * default), ShiftedSoftplus, Tanh, Sigmoid.  Other codes: TMDNET_BAD_ARGUMENT.  (The fused-projection
+ * entry points tmdnet_et_fused_* implement SiLU only.) */
+enum { TMDNET_ACT_SILU = 0, TMDNET_ACT_SSP = 1, TMDNET_ACT_TANH = 2, TMDNET_ACT_SIGMOID = 3 };
+#define TMDNET_ET_ACT(kv, attn) (((kv) << 8) | ((attn) << 12))
 
 /* ------------------------------------------------------------------------------------------
  * Neighbour list.  Replaces torchmdnet_neighbors::get_neighbor_pairs

@@ -141,6 +141,13 @@ def edge_geometry(pos, batch, cl, cu, max_pairs=None, loop=True, pad_static=Fals
 
 
 # ----------------------------------------------------------------------------- ET
+# the reference act_class_mapping (models/utils.py:579-584); ShiftedSoftplus subtracts log 2 rounded to
+# fp32 (utils.py:354-359: torch.log(torch.tensor(2.0)).item())
+SSP_SHIFT = 0.693147182464599609375
+ACTS = {"silu": F.silu, "tanh": torch.tanh, "sigmoid": torch.sigmoid,
+        "ssp": lambda x: F.softplus(x) - SSP_SHIFT}
+
+
 def et_representation(sd, cfg, z, pos, batch, prefix="representation_model.", hooks=None):
     p = lambda n: prefix + n
     H, heads = cfg["embedding_dimension"], cfg["num_heads"]
@@ -166,6 +173,7 @@ def et_representation(sd, cfg, z, pos, batch, prefix="representation_model.", ho
         x = linear(sd, p("neighbor_embedding.combine"), torch.cat([x, agg], dim=1))
     vec = torch.zeros(N, 3, H, dtype=x.dtype)
     di = cfg.get("distance_influence", "both")
+    act, attn_act = ACTS[cfg.get("activation", "silu")], ACTS[cfg.get("attn_activation", "silu")]
     for li in range(cfg["num_layers"]):
         lp = p(f"attention_layers.{li}.")
         xn_ = layer_norm(sd, lp + "layernorm", x)
@@ -176,11 +184,11 @@ def et_representation(sd, cfg, z, pos, batch, prefix="representation_model.", ho
         vec_dot = (vec1 * vec2).sum(dim=1)
         att = q.index_select(0, dst) * k.index_select(0, src)
         if di in ("keys", "both"):
-            att = att * F.silu(linear(sd, lp + "dk_proj", f)).view(-1, heads, d)
-        att = F.silu(att.sum(-1)) * C.unsqueeze(1)
+            att = att * act(linear(sd, lp + "dk_proj", f)).view(-1, heads, d)
+        att = attn_act(att.sum(-1)) * C.unsqueeze(1)
         vj = v.index_select(0, src)
         if di in ("values", "both"):
-            vj = vj * F.silu(linear(sd, lp + "dv_proj", f)).view(-1, heads, 3 * d)
+            vj = vj * act(linear(sd, lp + "dv_proj", f)).view(-1, heads, 3 * d)
         xm, v1, v2 = torch.split(vj, d, dim=2)
         xm = xm * att.unsqueeze(2)
         vm = vec.view(N, 3, heads, d).index_select(0, src) * v1.unsqueeze(1) + v2.unsqueeze(1) * u.view(-1, 3, 1, 1)
@@ -198,25 +206,26 @@ def et_representation(sd, cfg, z, pos, batch, prefix="representation_model.", ho
     return x, vec
 
 
-def gated_block(sd, name, x, v, out_channels, scalar_act):
+def gated_block(sd, name, x, v, out_channels, scalar_act, act=F.silu):
     vb = linear(sd, name + ".vec1_proj", v)
     nz = (vb != 0).flatten(1).any(dim=1, keepdim=True)
     sq = (vb * vb).sum(dim=-2)
     vec1 = torch.where(nz, torch.where(nz, sq, torch.ones_like(sq)).sqrt(), torch.zeros_like(sq))
     vec2 = linear(sd, name + ".vec2_proj", v)
     h = torch.cat([x, vec1], dim=-1)
-    h = linear(sd, name + ".update_net.2", F.silu(linear(sd, name + ".update_net.0", h)))
+    h = linear(sd, name + ".update_net.2", act(linear(sd, name + ".update_net.0", h)))
     x, v = torch.split(h, out_channels, dim=-1)
     v = v.unsqueeze(1) * vec2
     if scalar_act:
-        x = F.silu(x)
+        x = act(x)
     return x, v
 
 
 def equivariant_scalar(sd, cfg, x, v, prefix="output_model."):
     H = cfg["embedding_dimension"]
-    x, v = gated_block(sd, prefix + "output_network.0", x, v, H // 2, True)
-    x, v = gated_block(sd, prefix + "output_network.1", x, v, 1, False)
+    act = ACTS[cfg.get("activation", "silu")]  # the head's activation is the model's (reference model.py:63-68)
+    x, v = gated_block(sd, prefix + "output_network.0", x, v, H // 2, True, act)
+    x, v = gated_block(sd, prefix + "output_network.1", x, v, 1, False, act)
     return x + v.sum() * 0
 
 

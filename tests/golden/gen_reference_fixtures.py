@@ -306,6 +306,24 @@ def gen_edge_cases():
         save(name, res)
 
 
+# --------------------------------------------------------------------------- activations (round 3)
+def gen_activations():
+    """ET with non-SiLU `activation` / `attn_activation` (reference act_class_mapping,
+    models/utils.py:579-584; EquivariantMultiHeadAttention, torchmd_et.py:208-347): energies, forces and
+    the force-loss parameter gradients."""
+    for name, act, attn in (("et_tiny_act_tanh_ssp_f64.npz", "tanh", "ssp"),
+                            ("et_tiny_act_sigmoid_tanh_f64.npz", "sigmoid", "tanh")):
+        args = base_args("equivariant-transformer", embedding_dimension=32, num_layers=2, num_rbf=16,
+                         num_heads=4, max_num_neighbors=32, derivative=True, output_model="Scalar",
+                         precision=64, activation=act, attn_activation=attn)
+        seed_everything(1234)
+        model = create_model(args)
+        z, pos, batch = qm9_like(3)
+        res = run_model(model, z, pos, batch, torch.float64)
+        res.update(state_dict_arrays(model))
+        save(name, res)
+
+
 def gen_splits():
     """utils.make_splits / train_val_test_split index sets (reference torchmdnet/utils.py:54-139)."""
     from torchmdnet.utils import make_splits
@@ -327,7 +345,9 @@ def gen_splits():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["neighbors", "et", "tensornet", "seed", "edge", "splits"]
+    which = sys.argv[1:] or ["neighbors", "et", "tensornet", "seed", "edge", "splits", "acts"]
+    if "acts" in which:
+        gen_activations()
     if "edge" in which:
         gen_edge_cases()
     if "splits" in which:

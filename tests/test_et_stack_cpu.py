@@ -68,7 +68,7 @@ def _fake_fwd(q, k, v, vec, pk, pv, C, u, graph, heads, xo, vo, flags=0, pk_rows
     v, pv = _to_inter(v, H, heads, planar), _to_inter(pv, H, heads, planar)
     vec_ = torch.zeros((N, 3, H), dtype=q.dtype) if vec is None else vec
     a, b = kernels.et_message_composite(q, k, v, vec_, pk, pv, C, u, graph.src.long(), graph.dst.long(),
-                                        N, heads)
+                                        N, heads, flags & 0xFF00)
     xo.copy_(a)
     vo.copy_(b)
 
@@ -85,7 +85,7 @@ def _fake_bwd(q, k, v, vec, pk, pv, C, u, graph, heads, gx, gvec, gq, gk, gv, gw
                for t in (q, k, v, vec, pk, pv, C, u)]
         vec_ = torch.zeros((N, 3, H), dtype=q.dtype) if vec is None else ins[3]
         xo, vo = kernels.et_message_composite(ins[0], ins[1], ins[2], vec_, ins[4], ins[5], ins[6], ins[7],
-                                              graph.src.long(), graph.dst.long(), N, heads)
+                                              graph.src.long(), graph.dst.long(), N, heads, accumulate & 0xFF00)
         live = [t for t in ins if t is not None]
         g = torch.autograd.grad((xo, vo), live, (gx, gvec), allow_unused=True)
     it = iter(g)
@@ -212,7 +212,7 @@ def _fake_bwd2_launch(q, k, v, vec, pk, pv, C, u, graph, heads, gx, gvec, ggs, f
         idx = pk_rows.long()
         pk = pk.index_select(0, idx) if pk is not None else None
         pv = pv.index_select(0, idx) if pv is not None else None
-    res = _fake_bwd2_core(q, k, v, vec, pk, pv, C, u, graph, heads, gx, gvec, ggs)
+    res = _fake_bwd2_core(q, k, v, vec, pk, pv, C, u, graph, heads, gx, gvec, ggs, flags & 0xFF00)
     if not out:
         return res
     d_gx, d_gvec, d_q, d_k, d_v, d_vec, d_pk, d_pv, d_C, d_u = res
@@ -236,14 +236,14 @@ def _fake_bwd2_launch(q, k, v, vec, pk, pv, C, u, graph, heads, gx, gvec, ggs, f
     return d_gx, d_gvec, d_q, d_k, d_v, d_vec, d_pk, d_pv, d_C, d_u
 
 
-def _fake_bwd2_core(q, k, v, vec, pk, pv, C, u, graph, heads, gx, gvec, ggs):
+def _fake_bwd2_core(q, k, v, vec, pk, pv, C, u, graph, heads, gx, gvec, ggs, acts=0):
     N, H = q.shape
     vec_ = torch.zeros((N, 3, H), dtype=q.dtype) if vec is None else vec
     with torch.enable_grad():
         prim = [None if t is None else t.detach().clone().requires_grad_(True)
                 for t in (q, k, v, vec_, pk, pv, C, u)]
         seeds = [gx.detach().clone().requires_grad_(True), gvec.detach().clone().requires_grad_(True)]
-        xo, vo = kernels.et_message_composite(*prim, graph.src.long(), graph.dst.long(), N, heads)
+        xo, vo = kernels.et_message_composite(*prim, graph.src.long(), graph.dst.long(), N, heads, acts)
         live = [t for t in prim if t is not None]
         first = torch.autograd.grad((xo, vo), live, seeds, create_graph=True, allow_unused=True)
         it = iter(first)
@@ -573,3 +573,70 @@ def test_hand_second_order_matches_composite(emulated, monkeypatch, infl, batche
             continue
         assert a is not None, i
         assert torch.allclose(a, b, atol=1e-10, rtol=1e-8), (i, (a - b).abs().max())
+
+
+def _ref_stack(layers, x, f, C, u, src, dst, act_kv, act_at):
+    """Independent restatement of the reference layer loop (torchmd_et.py:177-184, 293-347) with the
+    activations given as plain functions."""
+    N, H = x.shape
+    vec = torch.zeros((N, 3, H), dtype=x.dtype)
+    for layer in layers:
+        heads, d = layer.num_heads, H // layer.num_heads
+        xn = torch.nn.functional.layer_norm(x, (H,), layer.layernorm.weight, layer.layernorm.bias, 1e-5)
+        q = layer.q_proj(xn).view(N, heads, d)
+        k = layer.k_proj(xn).view(N, heads, d)
+        v = layer.v_proj(xn).view(N, heads, 3 * d)
+        vec1, vec2, vec3 = torch.split(layer.vec_proj(vec), H, dim=-1)
+        att = q[dst] * k[src]
+        if layer.dk_proj is not None:
+            att = att * act_kv(layer.dk_proj(f)).view(-1, heads, d)
+        att = act_at(att.sum(-1)) * C.unsqueeze(1)
+        vj = v[src]
+        if layer.dv_proj is not None:
+            vj = vj * act_kv(layer.dv_proj(f)).view(-1, heads, 3 * d)
+        xm, v1, v2 = torch.split(vj, d, dim=2)
+        xm = xm * att.unsqueeze(2)
+        vm = vec.view(N, 3, heads, d)[src] * v1.unsqueeze(1) + v2.unsqueeze(1) * u.view(-1, 3, 1, 1)
+        xa = torch.zeros(N, heads, d, dtype=x.dtype).index_add(0, dst, xm).view(N, H)
+        va = torch.zeros(N, 3, heads, d, dtype=x.dtype).index_add(0, dst, vm).view(N, 3, H)
+        o1, o2, o3 = torch.split(layer.o_proj(xa), H, dim=1)
+        x = x + (vec1 * vec2).sum(dim=1) * o2 + o3
+        vec = vec + vec3 * o1.unsqueeze(1) + va
+    return x, vec
+
+
+@pytest.mark.parametrize("acts", [("tanh", "ssp"), ("sigmoid", "tanh"), ("ssp", "sigmoid")])
+def test_stack_activations_match_reference_loop(emulated, acts):
+    """Non-SiLU `activation` / `attn_activation` (reference act_class_mapping, utils.py:579-584): the
+    stack's launches carry the activation codes (TMDNET_ET_ACT flags) through the forward, the
+    first-order backward and the second order, against a plain restatement of the layer loop."""
+    from torchmdnet.models.utils import act_class_mapping
+    H, R, heads = 16, 8, 4
+    n, graph, r, vecs = _system()
+    x, f, C, u = _inputs(n, graph, r, vecs, H, R)
+    torch.manual_seed(2)
+    layers = torch.nn.ModuleList([
+        EquivariantMultiHeadAttention(H, R, "both", heads, act_class_mapping[acts[0]], acts[1], 0.0, 4.0, DT)
+        for _ in range(2)])
+    with torch.no_grad():
+        for p in layers.parameters():
+            p.add_(0.1 * torch.randn_like(p))
+    fns = {"tanh": torch.tanh, "sigmoid": torch.sigmoid,
+           "ssp": lambda t: torch.nn.functional.softplus(t) - 0.693147182464599609375}
+    src, dst = graph.src.long(), graph.dst.long()
+    leaves = [t.clone().requires_grad_(True) for t in (x, f, C, u)]
+    xo, vo = ES.et_stack(layers, leaves[0], graph, leaves[1], leaves[2], leaves[3])
+    ref_leaves = [t.clone().requires_grad_(True) for t in (x, f, C, u)]
+    xr, vr = _ref_stack(layers, *ref_leaves, src, dst, fns[acts[0]], fns[acts[1]])
+    assert torch.allclose(xo, xr, atol=1e-12) and torch.allclose(vo, vr, atol=1e-12)
+    params = list(layers.parameters())
+    gx, gv = torch.randn_like(xo), torch.randn_like(vo)
+    a = torch.autograd.grad((xo, vo), leaves + params, (gx, gv), create_graph=True)
+    b = torch.autograd.grad((xr, vr), ref_leaves + params, (gx, gv), create_graph=True)
+    for ga, gb in zip(a, b):
+        assert torch.allclose(ga, gb, atol=1e-11, rtol=1e-9)
+    # second order: a scalar of the first-order input gradients, differentiated w.r.t. the parameters
+    sa = sum((t * t).sum() for t in a[:4])
+    sb = sum((t * t).sum() for t in b[:4])
+    for ga, gb in zip(torch.autograd.grad(sa, params), torch.autograd.grad(sb, params)):
+        assert torch.allclose(ga, gb, atol=1e-10, rtol=1e-8)

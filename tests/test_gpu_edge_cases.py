@@ -99,7 +99,12 @@ def _model_from_fixture(d, **kw):
 
 @pytest.mark.parametrize("name,kw", [("et_tiny_cl2_f64", dict(cutoff_lower=2.0, cutoff_upper=5.0)),
                                      ("et_tiny_atomref_f64", dict(prior_model="Atomref",
-                                                                  prior_args={"max_z": 100}))])
+                                                                  prior_args={"max_z": 100})),
+                                     # non-SiLU activations: the kernels' TMDNET_ET_ACT codes, first and
+                                     # second order (the hand-written force-loss backward included)
+                                     ("et_tiny_act_tanh_ssp_f64", dict(activation="tanh", attn_activation="ssp")),
+                                     ("et_tiny_act_sigmoid_tanh_f64",
+                                      dict(activation="sigmoid", attn_activation="tanh"))])
 def test_et_edge_case_fixture(name, kw):
     _lib_loaded()
     d = golden(name + ".npz")

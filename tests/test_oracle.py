@@ -161,7 +161,10 @@ def test_tensornet_c3_padded_fixture():
 
 
 @pytest.mark.parametrize("name,extra", [("et_tiny_cl2_f64", dict(cutoff_lower=2.0)),
-                                        ("et_tiny_atomref_f64", {})])
+                                        ("et_tiny_atomref_f64", {}),
+                                        ("et_tiny_act_tanh_ssp_f64", dict(activation="tanh", attn_activation="ssp")),
+                                        ("et_tiny_act_sigmoid_tanh_f64",
+                                         dict(activation="sigmoid", attn_activation="tanh"))])
 def test_et_oracle_matches_reference_edge_cases(name, extra):
     """Lower cutoff 2 A (shifted CosineCutoff + the neighbour list's lower bound, reference
     models/utils.py:362-390, neighbors_cpu.cpp:82-86) and the Atomref prior with non-zero

@@ -209,16 +209,18 @@ def test_torchscript_force_matching_gradients():
     f_t = torch.randn_like(pos)
     grads = []
     for m in (model, scripted):
-        params = [p for p in m.parameters() if p.requires_grad]
+        named = [(n, p) for n, p in m.named_parameters() if p.requires_grad]
         y, neg_dy = m(z, pos.clone(), batch)
         loss = ((y - y_t) ** 2).mean() + ((neg_dy - f_t) ** 2).mean()
-        grads.append(torch.autograd.grad(loss, params, allow_unused=True))
+        grads.append(torch.autograd.grad(loss, [p for _, p in named], allow_unused=True))
+    names = [n for n, _ in named]
     n_checked = 0
-    for ge, gs in zip(*grads):
+    for name, ge, gs in zip(names, *grads):
         if ge is None:
-            assert gs is None or gs.abs().max() == 0
+            assert gs is None or gs.abs().max() == 0, name
             continue
-        assert _rel(gs, ge) < 2e-4
+        assert gs is not None, name
+        assert _rel(gs, ge) < 2e-4, name
         n_checked += 1
     assert n_checked > 20
 
@@ -297,3 +299,36 @@ def test_torchscript_tensornet_force_matching_gradients():
     for ge, gs in zip(*grads):
         if ge is not None:
             assert _rel(gs, ge) < 2e-4
+
+
+# ----------------------------------------------------------------------------- the fused scripted stack
+def test_torchscript_et_runs_fused_stack_operator():
+    """The scripted ET model runs its interaction layers as ONE tmdnet::et_stack operator (the eager
+    stack's fused launches), not the per-layer ATen loop."""
+    _torch_lib_loaded()
+    model, _ = _et_model(channels=64, layers=2)
+    scripted = torch.jit.script(model.to(DEV))
+    code = scripted.representation_model.code
+    assert "tmdnet.et_stack" in code
+
+
+@pytest.mark.parametrize("influence", ["keys", "values", "none"])
+def test_torchscript_fused_stack_distance_influence(influence):
+    """tmdnet::et_stack with dk only, dv only and no distance projection: energies, forces and the
+    second derivative equal the eager model's."""
+    _torch_lib_loaded()
+    from torchmdnet.models.model import create_model
+    args = yaml_args("equivariant-transformer")
+    args.update(embedding_dimension=64, num_layers=3, derivative=True, distance_influence=influence)
+    torch.manual_seed(0)
+    model = create_model(args).to(DEV)
+    scripted = torch.jit.script(model)
+    z, pos, batch = _batch(4)
+    outs = []
+    for m in (model, scripted):
+        p = pos.clone().requires_grad_(True)
+        y, neg_dy = m(z, p, batch)
+        ddy, = torch.autograd.grad([neg_dy], [p], grad_outputs=[torch.ones_like(neg_dy)])
+        outs.append((y.detach(), neg_dy.detach(), ddy))
+    for a, b in zip(outs[1], outs[0]):
+        assert _rel(a, b) < 1e-4

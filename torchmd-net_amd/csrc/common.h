@@ -77,4 +77,45 @@ template <typename T> struct Silu {
   __device__ __forceinline__ T dd(T x) const { return sig * (T(1) - sig) * (T(2) + x * (T(1) - T(2) * sig)); }
 };
 
+// The reference's act_class_mapping (models/utils.py:579-584) as a wave-uniform runtime code of the
+// ET message kernels (TMDNET_ET_ACT flags bits): value, first and second derivative.  Code 0 is SiLU,
+// evaluated exactly as Silu above (the default path adds one scalar branch per evaluation).
+enum ActCode : int { kActSilu = 0, kActSsp = 1, kActTanh = 2, kActSigmoid = 3 };
+
+template <typename T> __device__ __forceinline__ T softplus_(T x) {  // F.softplus (beta 1, threshold 20)
+  return x > T(20) ? x : log1p(exp(x));
+}
+
+template <typename T> struct ActF {
+  T s, sg;  // value; the sigmoid (SiLU, shifted softplus, sigmoid) the derivatives reuse
+  int c;
+  __device__ __forceinline__ ActF(T x, int code) : c(code) {
+    if (code == kActSilu) {
+      sg = sigmoid<T>(x);
+      s = x * sg;
+    } else if (code == kActSsp) {  // ShiftedSoftplus: softplus(x) - log 2 (rounded to fp32 as the
+      sg = sigmoid<T>(x);          // reference's shift, models/utils.py:354-359)
+      s = softplus_<T>(x) - T(0.693147182464599609375);
+    } else if (code == kActTanh) {
+      s = tanh(x);
+      sg = T(0);
+    } else {
+      sg = sigmoid<T>(x);
+      s = sg;
+    }
+  }
+  __device__ __forceinline__ T d(T x) const {
+    if (c == kActSilu) return sg * (T(1) + x * (T(1) - sg));
+    if (c == kActSsp) return sg;
+    if (c == kActTanh) return T(1) - s * s;
+    return sg * (T(1) - sg);
+  }
+  __device__ __forceinline__ T dd(T x) const {
+    if (c == kActSilu) return sg * (T(1) - sg) * (T(2) + x * (T(1) - T(2) * sg));
+    if (c == kActSsp) return sg * (T(1) - sg);
+    if (c == kActTanh) return T(-2) * s * (T(1) - s * s);
+    return sg * (T(1) - sg) * (T(1) - T(2) * sg);
+  }
+};
+
 }  // namespace tmd

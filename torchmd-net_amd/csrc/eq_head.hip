@@ -780,7 +780,8 @@ static int head_tile(int dtype, int H, int n, size_t* smem) {
   const size_t es = dtype == TMDNET_F64 ? 8 : 4;
   const size_t per = (size_t)head::Layout(H).P * es;
   int cap = n < 2048 ? 1 : 2;
-  if (const char* e = getenv("TMDNET_HEAD_NT")) cap = atoi(e) >= 4 ? 4 : atoi(e) >= 2 ? 2 : 1;  // tuning
+  static const int env_nt = [] { const char* e = getenv("TMDNET_HEAD_NT"); return e ? atoi(e) : 0; }();  // tuning, read once
+  if (env_nt > 0) cap = env_nt >= 4 ? 4 : env_nt >= 2 ? 2 : 1;
   for (int nt = cap; nt >= 1; nt /= 2)
     if (nt * per <= 64 * 1024) {
       *smem = nt * per;

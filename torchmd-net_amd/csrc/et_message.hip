@@ -113,17 +113,34 @@ template <typename T> struct Args {
   int acc;  // TMDNET_ACC_* flags of the backward
   int planar;  // TMDNET_ET_V_PLANAR: v / pv rows are [x | v1 | v2] H-blocks (else per-head [x|v1|v2] d-blocks)
   int vst;     // distance between the x, v1, v2 parts of a v / pv row: H (planar) or d
+  int act_kv;  // ActCode of the dk / dv projections (reference `activation`) and of the attention
+  int act_at;  // (`attn_activation`), torchmd_et.py:285-291, 316: TMDNET_ET_ACT bits of the flags
 };
 
 // SiLU of a pre-activation row segment already in registers (or 1 / 0 when the projection is
 // absent).  Loads and activations are kept apart on purpose: every per-edge load of an edge is
 // issued before the first activation, so an edge costs one memory round trip, not one per load.
+// `code`: the ActCode (SiLU: one branch for the whole segment, the math unchanged).
 template <typename T, int V>
-__device__ __forceinline__ void act(const T (&x)[V], bool has, T (&s)[V], T (&ds)[V]) {
+__device__ __forceinline__ void act(const T (&x)[V], bool has, T (&s)[V], T (&ds)[V], int code) {
+  if (code == kActSilu) {
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+      if (has) {
+        Silu<T> f(x[i]);
+        s[i] = f.s;
+        ds[i] = f.d(x[i]);
+      } else {
+        s[i] = T(1);
+        ds[i] = T(0);
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < V; ++i) {
     if (has) {
-      Silu<T> f(x[i]);
+      ActF<T> f(x[i], code);
       s[i] = f.s;
       ds[i] = f.d(x[i]);
     } else {
@@ -331,15 +348,15 @@ __global__ __launch_bounds__(256) void k_fwd(Args<T> A) {
       pre();
       if (!hw) { zero(w0); zero(w1); zero(w2); }
       T dk[V], dvx[V], dv1[V], dv2[V], dd[V];
-      act<T, V>(st.k, hk, dk, dd);
-      act<T, V>(st.x, hv, dvx, dd);
-      act<T, V>(st.a, hv, dv1, dd);
-      act<T, V>(st.b, hv, dv2, dd);
+      act<T, V>(st.k, hk, dk, dd, A.act_kv);
+      act<T, V>(st.x, hv, dvx, dd, A.act_kv);
+      act<T, V>(st.a, hv, dv1, dd, A.act_kv);
+      act<T, V>(st.b, hv, dv2, dd, A.act_kv);
       T part = T(0);
 #pragma unroll
       for (int i = 0; i < V; ++i) part += q[i] * kk[i] * dk[i];
       part = group_sum(part, A.lph);
-      const Silu<T> sa(part);
+      const ActF<T> sa(part, A.act_at);
       const T a = sa.s * Ce;
 #pragma unroll
       for (int i = 0; i < V; ++i) {
@@ -479,10 +496,10 @@ __device__ __forceinline__ void bwd_dst_body(const Args<T>& A, int blk, int nwg)
       const T (&p1)[V] = st.a;
       const T (&p2)[V] = st.b;
       T dk[V], ddk[V], dvx[V], dv1[V], dv2[V], ddx[V], dd1[V], dd2[V];
-      act<T, V>(pk, hk, dk, ddk);
-      act<T, V>(px, hv, dvx, ddx);
-      act<T, V>(p1, hv, dv1, dd1);
-      act<T, V>(p2, hv, dv2, dd2);
+      act<T, V>(pk, hk, dk, ddk, A.act_kv);
+      act<T, V>(px, hv, dvx, ddx, A.act_kv);
+      act<T, V>(p1, hv, dv1, dd1, A.act_kv);
+      act<T, V>(p2, hv, dv2, dd2, A.act_kv);
       T part = T(0), ga = T(0), gu0 = T(0), gu1 = T(0), gu2 = T(0);
 #pragma unroll
       for (int i = 0; i < V; ++i) {
@@ -495,7 +512,7 @@ __device__ __forceinline__ void bwd_dst_body(const Args<T>& A, int blk, int nwg)
       }
       part = group_sum(part, A.lph);
       ga = group_sum(ga, A.lph);
-      const Silu<T> sa(part);
+      const ActF<T> sa(part, A.act_at);
       const T a = sa.s * Ce;
       const T gs = ga * Ce * sa.d(part);
       T gpk[V], gpx[V], gp1[V], gp2[V];
@@ -621,10 +638,10 @@ __device__ __forceinline__ void bwd_src_body(const Args<T>& A, int blk, int nwg)
       const T (&p1)[V] = st.a;
       const T (&p2)[V] = st.b;
       T dk[V], ddk[V], dvx[V], dv1[V], dv2[V], dd[V];
-      act<T, V>(pk, hk, dk, ddk);
-      act<T, V>(px, hv, dvx, dd);
-      act<T, V>(p1, hv, dv1, dd);
-      act<T, V>(p2, hv, dv2, dd);
+      act<T, V>(pk, hk, dk, ddk, A.act_kv);
+      act<T, V>(px, hv, dvx, dd, A.act_kv);
+      act<T, V>(p1, hv, dv1, dd, A.act_kv);
+      act<T, V>(p2, hv, dv2, dd, A.act_kv);
       T part = T(0), ga = T(0);
 #pragma unroll
       for (int i = 0; i < V; ++i) {
@@ -633,7 +650,7 @@ __device__ __forceinline__ void bwd_src_body(const Args<T>& A, int blk, int nwg)
       }
       part = group_sum(part, A.lph);
       ga = group_sum(ga, A.lph);
-      const Silu<T> sa(part);
+      const ActF<T> sa(part, A.act_at);
       const T a = sa.s * Ce;
       const T gs = ga * Ce * sa.d(part);
 #pragma unroll
@@ -804,10 +821,10 @@ __device__ __forceinline__ void bwd_merged_body(const Args<T>& A, int blk, int n
       pre();
       if (!hw) { zero(w0); zero(w1); zero(w2); }
       T dk[V], ddk[V], dvx[V], dv1[V], dv2[V], ddx[V], dd1[V], dd2[V];
-      act<T, V>(st.k, hk, dk, ddk);
-      act<T, V>(st.x, hv, dvx, ddx);
-      act<T, V>(st.a, hv, dv1, dd1);
-      act<T, V>(st.b, hv, dv2, dd2);
+      act<T, V>(st.k, hk, dk, ddk, A.act_kv);
+      act<T, V>(st.x, hv, dvx, ddx, A.act_kv);
+      act<T, V>(st.a, hv, dv1, dd1, A.act_kv);
+      act<T, V>(st.b, hv, dv2, dd2, A.act_kv);
       // ---- destination role: e = (t <- s), the node's q / gx / gvec from LDS
       {
         T q[V], gx[V], g0[V], g1[V], g2[V];
@@ -828,7 +845,7 @@ __device__ __forceinline__ void bwd_merged_body(const Args<T>& A, int blk, int n
         }
         part = group_sum(part, A.lph);
         ga = group_sum(ga, A.lph);
-        const Silu<T> sa(part);
+        const ActF<T> sa(part, A.act_at);
         const T a = sa.s * Ce;
         const T gs = ga * Ce * sa.d(part);
         T grr = T(0);
@@ -871,7 +888,7 @@ __device__ __forceinline__ void bwd_merged_body(const Args<T>& A, int blk, int n
         }
         part = group_sum(part, A.lph);
         ga = group_sum(ga, A.lph);
-        const Silu<T> sa(part);
+        const ActF<T> sa(part, A.act_at);
         const T a = sa.s * Ce;
         const T gs = ga * Ce * sa.d(part);
 #pragma unroll
@@ -1101,12 +1118,13 @@ __global__ __launch_bounds__(S > 4 ? 64 * S : 256) void k_bwd2(Args2<T> B) {
     T dk[V], dk1[V], dk2[V], dx[V], dx1[V], dx2[V], d1[V], d11[V], d12[V], d2[V], d21[V], d22[V];
 #pragma unroll
     for (int i = 0; i < V; ++i) {
-      if (hk) { Silu<T> f(rk[i]); dk[i] = f.s; dk1[i] = f.d(rk[i]); dk2[i] = f.dd(rk[i]); }
+      const int ca = A.act_kv;
+      if (hk) { ActF<T> f(rk[i], ca); dk[i] = f.s; dk1[i] = f.d(rk[i]); dk2[i] = f.dd(rk[i]); }
       else { dk[i] = T(1); dk1[i] = T(0); dk2[i] = T(0); }
       if (hv) {
-        Silu<T> fx(rx[i]); dx[i] = fx.s; dx1[i] = fx.d(rx[i]); dx2[i] = fx.dd(rx[i]);
-        Silu<T> f1(r1[i]); d1[i] = f1.s; d11[i] = f1.d(r1[i]); d12[i] = f1.dd(r1[i]);
-        Silu<T> f2(r2[i]); d2[i] = f2.s; d21[i] = f2.d(r2[i]); d22[i] = f2.dd(r2[i]);
+        ActF<T> fx(rx[i], ca); dx[i] = fx.s; dx1[i] = fx.d(rx[i]); dx2[i] = fx.dd(rx[i]);
+        ActF<T> f1(r1[i], ca); d1[i] = f1.s; d11[i] = f1.d(r1[i]); d12[i] = f1.dd(r1[i]);
+        ActF<T> f2(r2[i], ca); d2[i] = f2.s; d21[i] = f2.d(r2[i]); d22[i] = f2.dd(r2[i]);
       } else {
         dx[i] = d1[i] = d2[i] = T(1); dx1[i] = d11[i] = d21[i] = T(0); dx2[i] = d12[i] = d22[i] = T(0);
       }
@@ -1123,7 +1141,7 @@ __global__ __launch_bounds__(S > 4 ? 64 * S : 256) void k_bwd2(Args2<T> B) {
     ga = group_sum(ga, A.lph);
     Sh = group_sum(Sh, A.lph);
     Xh = group_sum(Xh, A.lph);
-    const Silu<T> sa(part);
+    const ActF<T> sa(part, A.act_at);
     const T sil = sa.s, sd = sa.d(part), sdd = sa.dd(part);
     const T gs = ga * Ce * sd, a = sil * Ce;
     const T P = Ce * ga * sdd * Sh + Ce * sd * Xh + ggC * ga * sd;
@@ -1548,7 +1566,8 @@ static int launch_v(int V, int n, AT A, hipStream_t st) {
 // S = 4 so that e.g. a 678-atom QM9 batch still puts ~2.7k waves on the 256 CUs).
 static inline int et_waves_per_node(int n, int bytes_per_lane_vec) {
   if (bytes_per_lane_vec > 32) return 1;
-  if (const char* e = getenv("TMDNET_ET_S")) return atoi(e) >= 4 ? 4 : atoi(e) >= 2 ? 2 : 1;  // tuning
+  static const int env_s = [] { const char* e = getenv("TMDNET_ET_S"); return e ? atoi(e) : 0; }();  // tuning, read once
+  if (env_s > 0) return env_s >= 4 ? 4 : env_s >= 2 ? 2 : 1;
   if (n < 4096) return 4;
   if (n < 8192) return 2;
   return 1;
@@ -1649,6 +1668,14 @@ static int setup(Args<T>& A, int n, int H, int heads, const int32_t* row_ptr, co
   return kOk;
 }
 
+// the activation codes of a call's flags (TMDNET_ET_ACT bits 8-11 / 12-15)
+template <typename T>
+static int set_acts(Args<T>& A, int flags) {
+  A.act_kv = (flags >> 8) & 15;
+  A.act_at = (flags >> 12) & 15;
+  return (A.act_kv > kActSigmoid || A.act_at > kActSigmoid) ? kBadArgument : kOk;
+}
+
 template <typename T>
 static int fwd(int n, int H, int heads, const int32_t* row_ptr, const int32_t* src, int cap,
                const void* q, int ldq, const void* k, int ldk, const void* v, int ldv_,
@@ -1660,6 +1687,7 @@ static int fwd(int n, int H, int heads, const int32_t* row_ptr, const int32_t* s
   int rc = setup<T>(A, n, H, heads, row_ptr, src, cap, q, ldq, k, ldk, v, ldv_, vec, pk, ldpk, pv,
                     ldpv, C, u, order, V, prow);
   if (rc) return rc;
+  if ((rc = set_acts(A, flags))) return rc;
   if (flags & TMDNET_ET_V_PLANAR) { A.planar = 1; A.vst = H; }
   A.xo = (T*)xo;
   A.veco = (T*)veco;
@@ -1683,6 +1711,7 @@ static int bwd(int n, int H, int heads, const int32_t* row_ptr, const int32_t* s
   A.gpk = (T*)gpk; A.gpv = (T*)gpv; A.gC = (T*)gC; A.gu = (T*)gu;
   A.dpk = (const T*)dpk; A.dpv = (const T*)dpv; A.gr = (T*)gr;
   A.acc = acc;
+  if ((rc = set_acts(A, acc))) return rc;
   static const int bwd_v = getenv("TMDNET_ET_BWD_V") ? atoi(getenv("TMDNET_ET_BWD_V")) : 0;  // tuning
   if (bwd_v && bwd_v < V && H % (32 * bwd_v) == 0 && H / bwd_v <= 64 && (A.d / bwd_v) > 0 &&
       A.d % bwd_v == 0 && !((A.d / bwd_v) & (A.d / bwd_v - 1))) {
@@ -1741,6 +1770,7 @@ static int bwd2(int n, int H, int heads, const int32_t* row_ptr, const int32_t* 
   B.a.lph = d / V;
   if (B.a.L > 64 || (B.a.L & (B.a.L - 1))) return kUnsupported;
   if (!aligned<T>(ggpk, ldggpk, V) || !aligned<T>(ggpv, ldggpv, V)) return kBadArgument;
+  if ((rc = set_acts(B.a, flags))) return rc;
   if (flags & TMDNET_ET_V_PLANAR) { B.a.planar = 1; B.a.vst = H; }
   B.a.gx = (const T*)gx; B.a.gvec = (const T*)gvec;
   B.ggq = (const T*)ggq; B.ggk = (const T*)ggk; B.ggv = (const T*)ggv; B.ggw = (const T*)ggw;

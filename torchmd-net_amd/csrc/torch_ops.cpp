@@ -28,10 +28,14 @@
 #include <c10/core/DeviceGuard.h>
 #include <c10/hip/HIPStream.h>
 #include <torch/autograd.h>
+#include <torch/custom_class.h>
 #include <torch/library.h>
 
 #include <cmath>
+#include <memory>
+#include <mutex>
 #include <string>
+#include <vector>
 
 #include "tmdnet.h"
 
@@ -77,6 +81,12 @@ int ld(const Tensor& t) { return t.defined() ? static_cast<int>(t.stride(0)) : 0
 // rows may be strided (views into fused projections); elements must be contiguous
 Tensor rowmajor(const Tensor& t) { return (!t.defined() || t.stride(-1) == 1) ? t : t.contiguous(); }
 Tensor contig(const Tensor& t) { return t.defined() ? t.contiguous() : t; }
+
+// Optional tensor arguments of the autograd Functions: an absent input must be an EMPTY optional
+// (no autograd edge) -- an undefined Tensor argument would be recorded as an input without metadata.
+using OptT = c10::optional<Tensor>;
+OptT opt(const Tensor& t) { return t.defined() ? OptT(t) : OptT(); }
+Tensor val(const OptT& t) { return (t.has_value() && t->defined()) ? *t : Tensor(); }
 
 void require_gpu(const Tensor& t, const char* what) {
   TORCH_CHECK(t.is_cuda(), "torchmd-net_amd: ", what, " runs only on a ROCm GPU (got a ", t.device(),
@@ -645,10 +655,13 @@ struct NbrEmbed : public Function<NbrEmbed> {
 struct EtMsgBwd : public Function<EtMsgBwd> {
   // (gx, gvec, q, k, v, vec?, pk?, pv?, C, u) -> (gq, gk, gv, gvec_in, gpk, gpv, gC, gu): tmdnet_et_message_bwd;
   // its backward is tmdnet_et_message_bwd2 (the third order is not provided)
+  // (absent vec / pk / pv travel as empty optionals: no autograd edge, so the Function stays
+  // recordable under create_graph)
   static variable_list forward(AutogradContext* ctx, const Tensor& gx, const Tensor& gvec, const Tensor& q,
-                               const Tensor& k, const Tensor& v, const Tensor& vec, const Tensor& pk, const Tensor& pv,
-                               const Tensor& C, const Tensor& u, const Tensor& row_ptr, const Tensor& src,
-                               const Tensor& dst, int64_t heads) {
+                               const Tensor& k, const Tensor& v, const OptT& vec_o, const OptT& pk_o,
+                               const OptT& pv_o, const Tensor& C, const Tensor& u, const Tensor& row_ptr,
+                               const Tensor& src, const Tensor& dst, int64_t heads, int64_t acts) {
+    const Tensor vec = val(vec_o), pk = val(pk_o), pv = val(pv_o);
     G g{row_ptr, src, dst, Tensor()};
     const int N = static_cast<int>(q.size(0)), H = static_cast<int>(q.size(1)), E = g.E();
     Tensor gq = at::empty({N, H}, opts(q)), gk = at::empty({N, H}, opts(q)), gv = at::empty({N, 3 * H}, opts(q));
@@ -661,12 +674,13 @@ struct EtMsgBwd : public Function<EtMsgBwd> {
                                 ptr(q), ld(q), ptr(k), ld(k), ptr(v), ld(v), ptr(vec), ptr(pk), ld(pk), ptr(pv),
                                 ld(pv), ptr(C), ptr(u), ptr(gxc), ptr(gvc), ptr(gq), ptr(gk), ptr(gv),
                                 vec.defined() ? ptr(gw) : nullptr, pk.defined() ? ptr(gpk) : nullptr,
-                                pv.defined() ? ptr(gpv) : nullptr, ptr(gC), ptr(gu), nullptr, nullptr, nullptr, 0,
-                                nullptr, nullptr, stream_of(q)),
+                                pv.defined() ? ptr(gpv) : nullptr, ptr(gC), ptr(gu), nullptr, nullptr, nullptr,
+                                static_cast<int>(acts), nullptr, nullptr, stream_of(q)),
           "tmdnet_et_message_bwd");
     if (!vec.defined()) gw.zero_();
     keep_graph(ctx, g);
     ctx->saved_data["heads"] = heads;
+    ctx->saved_data["acts"] = acts;
     ctx->save_for_backward({gxc, gvc, q, k, v, vec, pk, pv, C, u});
     return {gq, gk, gv, gw, gpk, gpv, gC, gu};
   }
@@ -697,18 +711,19 @@ struct EtMsgBwd : public Function<EtMsgBwd> {
                                  ptr(u), ptr(gx), ptr(gvec), ptr(ggq), ptr(ggk), ptr(ggv), ptr(ggw), ptr(ggpk),
                                  ld(ggpk), ptr(ggpv), ld(ggpv), ptr(ggC), ptr(ggu), ptr(d_gx), ptr(d_gvec), ptr(d_q),
                                  ptr(d_k), ptr(d_v), vec.defined() ? ptr(d_vec) : nullptr, ptr(d_pk), ptr(d_pv),
-                                 ptr(d_C), ptr(d_u), 0, stream_of(q)),
+                                 ptr(d_C), ptr(d_u), static_cast<int>(ctx->saved_data["acts"].toInt()), stream_of(q)),
           "tmdnet_et_message_bwd2");
     return {d_gx, d_gvec, d_q, d_k, d_v, vec.defined() ? d_vec : Tensor(), d_pk, d_pv, d_C, d_u,
-            Tensor(), Tensor(), Tensor(), Tensor()};
+            Tensor(), Tensor(), Tensor(), Tensor(), Tensor()};
   }
 };
 
 struct EtMsg : public Function<EtMsg> {
   static variable_list forward(AutogradContext* ctx, const Tensor& q_in, const Tensor& k_in, const Tensor& v_in,
-                               const Tensor& vec_in, const Tensor& pk_in, const Tensor& pv_in, const Tensor& C_in,
+                               const OptT& vec_o, const OptT& pk_o, const OptT& pv_o, const Tensor& C_in,
                                const Tensor& u_in, const Tensor& row_ptr, const Tensor& src, const Tensor& dst,
-                               int64_t heads) {
+                               int64_t heads, int64_t acts) {
+    const Tensor vec_in = val(vec_o), pk_in = val(pk_o), pv_in = val(pv_o);
     require_gpu(q_in, "et_message");
     Tensor q = rowmajor(q_in), k = rowmajor(k_in), v = rowmajor(v_in), pk = rowmajor(pk_in), pv = rowmajor(pv_in);
     Tensor vec = contig(vec_in), C = C_in.contiguous(), u = u_in.contiguous();
@@ -723,10 +738,12 @@ struct EtMsg : public Function<EtMsg> {
     Tensor xo = at::empty({N, H}, opts(q)), vo = at::empty({N, 3, H}, opts(q));
     check(tmdnet_et_message_fwd(dcode(q), N, H, static_cast<int>(heads), ptr<int32_t>(row_ptr), ptr<int32_t>(src),
                                 g.E(), ptr(q), ld(q), ptr(k), ld(k), ptr(v), ld(v), ptr(vec), ptr(pk), ld(pk), ptr(pv),
-                                ld(pv), ptr(C), ptr(u), ptr(xo), ptr(vo), 0, nullptr, nullptr, stream_of(q)),
+                                ld(pv), ptr(C), ptr(u), ptr(xo), ptr(vo), static_cast<int>(acts), nullptr, nullptr,
+                                stream_of(q)),
           "tmdnet_et_message_fwd");
     keep_graph(ctx, g);
     ctx->saved_data["heads"] = heads;
+    ctx->saved_data["acts"] = acts;
     ctx->save_for_backward({q, k, v, vec, pk, pv, C, u});
     return {xo, vo};
   }
@@ -739,9 +756,10 @@ struct EtMsg : public Function<EtMsg> {
     const int64_t N = q.size(0), H = q.size(1);
     Tensor gx = go[0].defined() ? go[0] : at::zeros({N, H}, opts(q));
     Tensor gvec = go[1].defined() ? go[1] : at::zeros({N, 3, H}, opts(q));
-    auto o = EtMsgBwd::apply(gx, gvec, sv[0], sv[1], sv[2], sv[3], sv[4], sv[5], sv[6], sv[7], g.row_ptr, g.src, g.dst,
-                             heads);
-    variable_list res(12);
+    auto o = EtMsgBwd::apply(gx, gvec, sv[0], sv[1], sv[2], opt(sv[3]), opt(sv[4]), opt(sv[5]), sv[6], sv[7], g.row_ptr,
+                             g.src, g.dst,
+                             heads, ctx->saved_data["acts"].toInt());
+    variable_list res(13);
     res[0] = o[0];
     res[1] = o[1];
     res[2] = o[2];
@@ -1041,12 +1059,520 @@ Tensor nbr_embed(const Tensor& x, const Tensor& w, const Tensor& C, const Tensor
 std::tuple<Tensor, Tensor> et_message(const Tensor& q, const Tensor& k, const Tensor& v,
                                       const c10::optional<Tensor>& vec, const c10::optional<Tensor>& pk,
                                       const c10::optional<Tensor>& pv, const Tensor& C, const Tensor& u,
-                                      const Tensor& row_ptr, const Tensor& src, const Tensor& dst, int64_t heads) {
+                                      const Tensor& row_ptr, const Tensor& src, const Tensor& dst, int64_t heads,
+                                      int64_t acts) {
   // launches, allocations and the stream on the input's device whatever the caller's current device
   // (the autograd engine runs each backward on its device's thread with that device current)
   const c10::OptionalDeviceGuard guard(q.device());
-  auto r = EtMsg::apply(q, k, v, vec.has_value() ? *vec : Tensor(), pk.has_value() ? *pk : Tensor(),
-                        pv.has_value() ? *pv : Tensor(), C, u, row_ptr, src, dst, heads);
+  auto r = EtMsg::apply(q, k, v, opt(val(vec)), opt(val(pk)), opt(val(pv)), C, u, row_ptr, src, dst, heads, acts);
+  return {r[0], r[1]};
+}
+
+// ----------------------------------------------------------------------------- ET layer stack
+// tmdnet::et_stack: every EquivariantMultiHeadAttention layer of TorchMD_ET plus the model's out_norm
+// (reference torchmd_et.py:177-187, 272-347) as ONE operator, so a TorchScript'd model runs the same
+// fused launches as the eager stack (et_stack.py) instead of the per-layer ATen loop:
+//   forward:  all layers' dk/dv projections in one GEMM (tmdnet_proj_f32 over the edges), per layer one
+//             grouped GEMM ([q|k|v] + vec_proj, tmdnet_gemm_f32), tmdnet_et_message_fwd, the o_proj GEMM
+//             and the epilogue fused with the next layer's LayerNorm (tmdnet_et_epilogue_ln_fwd; the
+//             last one with out_norm);
+//   backward (a force evaluation: no parameter gradient requested): "dr mode" -- d(dk,dv)/dr formed
+//             once (tmdnet_rbf_deriv + one projection GEMM), contracted with the projection gradient
+//             inside tmdnet_et_message_bwd, accumulating d/d r per edge; per layer the epilogue / o_proj /
+//             message / grouped transposed GEMM / LayerNorm backward kernels;
+//   parameter gradients (training through TorchScript) and every higher order: autograd over the
+//             differentiable restatement (ATen Linears / LayerNorms + the tmdnet::et_message Function,
+//             itself HIP to second order).
+// f must be rbf(dist) with the fixed (non-trainable) basis given by (mu, beta, rbf_type): the
+// operator's gradient for f is delivered to dist (f gets none), as the eager stack's dr mode does.
+// fp32 only (the model falls back to the per-layer loop for fp64 or a trainable basis).
+struct StackCfg {
+  int64_t heads, rbf;
+  double cl, cu;
+  bool hk, hv, out_norm;
+  int64_t acts;  // TMDNET_ET_ACT bits of the layers' activations
+};
+
+void keep_cfg(AutogradContext* ctx, const StackCfg& c) {
+  ctx->saved_data["heads"] = c.heads;
+  ctx->saved_data["rbf"] = c.rbf;
+  ctx->saved_data["cl"] = c.cl;
+  ctx->saved_data["cu"] = c.cu;
+  ctx->saved_data["flags"] = int64_t(c.hk) | (int64_t(c.hv) << 1) | (int64_t(c.out_norm) << 2);
+  ctx->saved_data["acts"] = c.acts;
+}
+
+StackCfg cfg_of(AutogradContext* ctx) {
+  const int64_t fl = ctx->saved_data["flags"].toInt();
+  return {ctx->saved_data["heads"].toInt(), ctx->saved_data["rbf"].toInt(), ctx->saved_data["cl"].toDouble(),
+          ctx->saved_data["cu"].toDouble(), bool(fl & 1), bool(fl & 2), bool(fl & 4),
+          ctx->saved_data["acts"].toInt()};
+}
+
+constexpr double kLnEps = 1e-5;  // nn.LayerNorm default (reference torchmd_et.py:223, :117)
+
+int64_t stack_np(bool hk, bool hv) { return 11 + 2 * int64_t(hk) + 2 * int64_t(hv); }
+
+// C = A op(B) (+ bias) (+ C if beta) on the hand-written grouped GEMM, the library outside its envelope
+void gemm_into(const Tensor& A, const Tensor& B, bool trans_b, const Tensor& bias, const Tensor& C, bool beta) {
+  const int M = static_cast<int>(A.size(0)), N = static_cast<int>(C.size(1)), K = static_cast<int>(A.size(1));
+  if (A.scalar_type() == at::kFloat && M > 0 && M <= 16384 && A.stride(1) == 1 && B.stride(1) == 1 &&
+      C.stride(1) == 1) {
+    int dims[8] = {M, N, K, static_cast<int>(A.stride(0)), static_cast<int>(B.stride(0)),
+                   static_cast<int>(C.stride(0)), int(trans_b), int(beta)};
+    const void* ptrs[4] = {A.data_ptr(), B.data_ptr(), bias.defined() ? bias.data_ptr() : nullptr, C.data_ptr()};
+    const int rc = tmdnet_gemm_f32(1, dims, ptrs, stream_of(A));
+    if (rc != TMDNET_UNSUPPORTED) {
+      check(rc, "tmdnet_gemm_f32");
+      return;
+    }
+  }
+  Tensor Bop = trans_b ? B.t() : B;
+  if (beta) {
+    C.addmm_(A, Bop);
+    if (bias.defined()) C.add_(bias);
+  } else if (bias.defined()) {
+    at::addmm_out(const_cast<Tensor&>(C), bias, A, Bop);
+  } else {
+    at::mm_out(const_cast<Tensor&>(C), A, Bop);
+  }
+}
+
+// out = A W^T (+ bias) for the dk/dv projection (tmdnet_proj_f32 on the exact bf16 split; library otherwise)
+void proj_into(const Tensor& A, const Tensor& W, const Tensor& Wp, const Tensor& bias, const Tensor& out) {
+  const int M = static_cast<int>(A.size(0)), N = static_cast<int>(W.size(0)), K = static_cast<int>(W.size(1));
+  if (Wp.defined() && M > 0) {
+    const int rc = tmdnet_proj_f32(M, N, K, A.data_ptr(), static_cast<int>(A.stride(0)), Wp.data_ptr(),
+                                   static_cast<long long>(N) * K, bias.defined() ? bias.data_ptr() : nullptr,
+                                   out.data_ptr(), static_cast<int>(out.stride(0)), stream_of(A));
+    if (rc != TMDNET_UNSUPPORTED) {
+      check(rc, "tmdnet_proj_f32");
+      return;
+    }
+  }
+  if (bias.defined()) at::addmm_out(const_cast<Tensor&>(out), bias, A, W.t());
+  else at::mm_out(const_cast<Tensor&>(out), A, W.t());
+}
+
+// The stacked weights of one parameter set: per layer [q|k|v] (5H x H) and its bias, all layers' [dk; dv]
+// rows (L*D x R) + bias and their bf16 split.  Rebuilt only when a parameter's storage or version changes
+// (an MD engine evaluates one fixed model: one pack for the whole run).
+struct Packed {
+  std::vector<std::pair<const void*, uint32_t>> key;
+  std::vector<Tensor> qkv_w, qkv_b;
+  Tensor dkv_w, dkv_b, dkv_wp;
+};
+
+std::shared_ptr<Packed> pack_stack(const std::vector<Tensor>& P, int64_t L, int64_t np, bool hk, bool hv) {
+  static std::mutex mu;
+  static std::shared_ptr<Packed> last;
+  std::vector<std::pair<const void*, uint32_t>> key;
+  key.reserve(P.size());
+  for (const auto& t : P) key.emplace_back(t.data_ptr(), t._version());
+  std::lock_guard<std::mutex> lock(mu);
+  if (last && last->key == key) return last;
+  auto pk = std::make_shared<Packed>();
+  pk->key = std::move(key);
+  at::NoGradGuard ng;
+  std::vector<Tensor> dw, db;
+  for (int64_t l = 0; l < L; ++l) {
+    const Tensor* p = P.data() + l * np;
+    pk->qkv_w.push_back(at::cat({p[2], p[4], p[6]}, 0).contiguous());
+    pk->qkv_b.push_back(at::cat({p[3], p[5], p[7]}, 0).contiguous());
+    int64_t i = 11;
+    if (hk) { dw.push_back(p[i]); db.push_back(p[i + 1]); i += 2; }
+    if (hv) { dw.push_back(p[i]); db.push_back(p[i + 1]); }
+  }
+  if (!dw.empty()) {
+    pk->dkv_w = at::cat(dw, 0).contiguous();
+    pk->dkv_b = at::cat(db, 0).contiguous();
+    const int N = static_cast<int>(pk->dkv_w.size(0)), K = static_cast<int>(pk->dkv_w.size(1));
+    if (pk->dkv_w.scalar_type() == at::kFloat && (K == 32 || K == 64) && N % 16 == 0) {
+      Tensor wp = at::empty({3, N, K}, pk->dkv_w.options().dtype(at::kShort));
+      const int rc = tmdnet_proj_split_f32(N, K, pk->dkv_w.data_ptr(), K, wp.data_ptr(), stream_of(pk->dkv_w));
+      if (rc != TMDNET_UNSUPPORTED) {
+        check(rc, "tmdnet_proj_split_f32");
+        pk->dkv_wp = wp;
+      }
+    }
+  }
+  last = pk;
+  return pk;
+}
+
+// The forward's intermediates the first-order backward reads (per layer, as et_stack._forward_layers);
+// kept in the autograd context as an IValue capsule (freed with the graph).
+struct StackActs : torch::CustomClassHolder {
+  std::vector<Tensor> x, vec, xn, mean, rstd, qkv, vecp, xa, o;
+  Tensor pkv_all, x_pre, mean_o, rstd_o;
+  std::shared_ptr<Packed> pk;
+  bool batched = true;
+};
+
+// differentiable restatement: (x, dist, C, u, params) -> (x_out, vec_out), the reference layer loop
+std::pair<Tensor, Tensor> stack_composite(const Tensor& x_in, const Tensor& dist, const Tensor& C, const Tensor& u,
+                                          const Tensor& mu, const Tensor& beta, const std::vector<Tensor>& P,
+                                          const G& g, const StackCfg& c) {
+  const int64_t H = x_in.size(1), np = stack_np(c.hk, c.hv);
+  const int64_t L = (static_cast<int64_t>(P.size()) - (c.out_norm ? 2 : 0)) / np;
+  Tensor f = edge_geom_composite(Tensor(), dist, Tensor(), mu, beta, c.cl, c.cu, c.rbf, true, false, false)[0];
+  Tensor x = x_in, vec;
+  for (int64_t l = 0; l < L; ++l) {
+    const Tensor* p = P.data() + l * np;
+    Tensor xn = at::layer_norm(x, {H}, p[0], p[1], kLnEps);
+    Tensor q = at::linear(xn, p[2], p[3]), k = at::linear(xn, p[4], p[5]), v = at::linear(xn, p[6], p[7]);
+    int64_t i = 11;
+    Tensor pk, pv;
+    if (c.hk) { pk = at::linear(f, p[i], p[i + 1]); i += 2; }
+    if (c.hv) pv = at::linear(f, p[i], p[i + 1]);
+    auto m = EtMsg::apply(q, k, v, opt(vec), opt(pk), opt(pv), C, u, g.row_ptr, g.src, g.dst, c.heads, c.acts);
+    auto o = at::linear(m[0], p[9], p[10]).split(H, 1);
+    if (vec.defined()) {
+      auto vp = at::linear(vec, p[8]).split(H, -1);
+      Tensor vec_dot = (vp[0] * vp[1]).sum(1);
+      x = x + vec_dot * o[1] + o[2];
+      vec = vec + vp[2] * o[0].unsqueeze(1) + m[1];
+    } else {  // layer 0: vec = 0 (torchmd_et.py:176)
+      x = x + o[2];
+      vec = m[1];
+    }
+  }
+  if (c.out_norm) x = at::layer_norm(x, {H}, P[P.size() - 2], P[P.size() - 1], kLnEps);
+  return {x, vec};
+}
+
+// The fast first-order backward of a force evaluation (et_stack._backward_layers with dr=True):
+// returns (g_x, g_dist, g_C, g_u).
+variable_list stack_backward_dr(const StackActs& A, Tensor gX, Tensor gV, const Tensor& dist, const Tensor& C,
+                                const Tensor& u, const Tensor& mu, const Tensor& beta, const std::vector<Tensor>& P,
+                                const G& g, const StackCfg& c) {
+  const int64_t N = gX.size(0), H = gX.size(1), E = g.E(), np = stack_np(c.hk, c.hv);
+  const int64_t L = static_cast<int64_t>(A.x.size()), D = (int64_t(c.hk) + 3 * int64_t(c.hv)) * H;
+  const bool has_e = c.hk || c.hv;
+  auto o = opts(gX);
+  // the edge gradients are accumulated across layers by the kernels; the first layer of the backward
+  // overwrites them (separate tensors: they are outputs of the backward Function)
+  Tensor g_C = at::empty({E}, o), g_u = at::empty({E, 3}, o), g_r = at::empty({E}, o);
+  if (!has_e) g_r.zero_();
+  Tensor dpkv_all;
+  if (has_e) {  // d(dk,dv)/dr = (d f / d r) W^T, every layer in one GEMM (or per layer for large graphs)
+    const int R = static_cast<int>(mu.size(0));
+    Tensor fdp = at::empty({E, R}, o);
+    check(tmdnet_rbf_deriv(dcode(dist), R, static_cast<int>(c.rbf), ptr(dist), ptr(mu), ptr(beta), c.cl, c.cu,
+                           nullptr, static_cast<int>(E), ptr(fdp), stream_of(dist)),
+          "tmdnet_rbf_deriv");
+    if (A.batched) {
+      dpkv_all = at::empty({E, L * D}, o);
+      proj_into(fdp, A.pk->dkv_w, A.pk->dkv_wp, Tensor(), dpkv_all);
+    } else {
+      dpkv_all = fdp;  // per layer below
+    }
+  }
+  std::vector<Tensor> g_o(L), g_vecp(L);
+  for (int64_t l = 0; l < L; ++l) {
+    g_o[l] = at::empty({N, 3 * H}, o);
+    if (A.vec[l].defined()) g_vecp[l] = at::empty({N, 3, 3 * H}, o);
+  }
+  bool epi_done = false;
+  if (c.out_norm) {  // back through out_norm and the last layer's epilogue in one kernel
+    Tensor g = at::empty_like(gX);
+    const Tensor& on_w = P[P.size() - 2];
+    check(tmdnet_ln_bwd_epilogue_w(dcode(gX), static_cast<int>(N), static_cast<int>(H), ptr(gX), ptr(A.x_pre),
+                                   ptr(A.mean_o), ptr(A.rstd_o), ptr(on_w), nullptr, nullptr, ptr(g), ptr(gV),
+                                   ptr(A.vecp[L - 1]), ptr(A.o[L - 1]), ptr(g_vecp[L - 1]), ptr(g_o[L - 1]), nullptr, 0,
+                                   stream_of(gX)),
+          "tmdnet_ln_bwd_epilogue_w");
+    gX = g;
+    epi_done = true;
+  }
+  for (int64_t l = L - 1; l >= 0; --l) {
+    const Tensor* p = P.data() + l * np;
+    if (!epi_done)
+      check(tmdnet_et_epilogue_bwd_acc(dcode(gX), static_cast<int>(N), static_cast<int>(H), ptr(gX), ptr(gV),
+                                       ptr(A.vecp[l]), ptr(A.o[l]), ptr(g_vecp[l]), ptr(g_o[l]), 0, stream_of(gX)),
+            "tmdnet_et_epilogue_bwd_acc");
+    Tensor g_xa = at::empty({N, H}, o);
+    gemm_into(g_o[l], p[9], false, Tensor(), g_xa, false);
+    const bool hv = A.vec[l].defined();
+    Tensor g_vec_in = hv ? at::empty({N, 3, H}, o) : Tensor();
+    Tensor g_qkv = at::empty({N, 5 * H}, o);
+    Tensor dpk, dpv, pk, pv;
+    Tensor pkv = A.batched ? A.pkv_all.narrow(1, l * D, D) : A.pkv_all;
+    if (has_e) {
+      Tensor dpkv = A.batched ? dpkv_all.narrow(1, l * D, D) : Tensor();
+      if (!A.batched) {
+        dpkv = at::empty({E, D}, o);
+        proj_into(dpkv_all, A.pk->dkv_w.narrow(0, l * D, D), Tensor(), Tensor(), dpkv);
+        pkv = at::empty({E, D}, o);  // the forward's rows of this layer again (not kept for large graphs)
+        proj_into(A.pkv_all, A.pk->dkv_w.narrow(0, l * D, D), Tensor(), A.pk->dkv_b.narrow(0, l * D, D), pkv);
+      }
+      if (c.hk) { pk = pkv.narrow(1, 0, H); dpk = dpkv.narrow(1, 0, H); }
+      if (c.hv) { pv = pkv.narrow(1, H * int64_t(c.hk), 3 * H); dpv = dpkv.narrow(1, H * int64_t(c.hk), 3 * H); }
+    }
+    const Tensor& qkv = A.qkv[l];
+    const int flags = TMDNET_ACC_VEC_RESIDUAL | (l < L - 1 ? TMDNET_ACC_EDGE : 0) | static_cast<int>(c.acts);
+    Tensor gq = g_qkv.narrow(1, 0, H), gk = g_qkv.narrow(1, H, H), gv = g_qkv.narrow(1, 2 * H, 3 * H);
+    const float* qb = static_cast<const float*>(qkv.data_ptr());
+    check(tmdnet_et_message_bwd(dcode(gX), static_cast<int>(N), static_cast<int>(H), static_cast<int>(c.heads),
+                                ptr<int32_t>(g.row_ptr), ptr<int32_t>(g.src), static_cast<int>(E), qb, ld(qkv),
+                                qb + H, ld(qkv), qb + 2 * H, ld(qkv), ptr(A.vec[l]), ptr(pk), ld(pk),
+                                ptr(pv), ld(pv), ptr(C), ptr(u), ptr(g_xa), ptr(gV), ptr(gq), ptr(gk), ptr(gv),
+                                ptr(g_vec_in), nullptr, nullptr, ptr(g_C), ptr(g_u), has_e ? ptr(dpk) : nullptr,
+                                has_e ? ptr(dpv) : nullptr, has_e ? ptr(g_r) : nullptr, flags, nullptr, nullptr,
+                                stream_of(gX)),
+          "tmdnet_et_message_bwd");
+    Tensor g_xn = at::empty({N, H}, o);
+    gemm_into(g_qkv, A.pk->qkv_w[l], false, Tensor(), g_xn, false);
+    if (hv) gemm_into(g_vecp[l].view({3 * N, 3 * H}), p[8], false, Tensor(), g_vec_in.view({3 * N, H}), true);
+    const bool prev = l > 0;
+    Tensor g_x = at::empty_like(g_xn);
+    check(tmdnet_ln_bwd_epilogue_w(dcode(gX), static_cast<int>(N), static_cast<int>(H), ptr(g_xn), ptr(A.x[l]),
+                                   ptr(A.mean[l]), ptr(A.rstd[l]), ptr(p[0]), ptr(gX), nullptr, ptr(g_x),
+                                   ptr(g_vec_in), prev ? ptr(A.vecp[l - 1]) : nullptr, prev ? ptr(A.o[l - 1]) : nullptr,
+                                   prev ? ptr(g_vecp[l - 1]) : nullptr, prev ? ptr(g_o[l - 1]) : nullptr, nullptr, 0,
+                                   stream_of(gX)),
+          "tmdnet_ln_bwd_epilogue_w");
+    epi_done = prev;
+    gX = g_x;
+    gV = g_vec_in;
+  }
+  return {gX, g_r, g_C, g_u};
+}
+
+struct StackIn {  // the operator's non-parameter tensors
+  Tensor x, f, dist, C, u, mu, beta;
+  G g;
+};
+
+// gradients of <(gX, gV), (x_out, vec_out)> w.r.t. (x, dist, C, u, params) by recompute; ``create`` keeps
+// the graph (higher orders).  `want`: per leaf, whether its gradient is wanted.
+variable_list stack_vjp(const StackIn& in, const std::vector<Tensor>& P, const StackCfg& c, const Tensor& gX,
+                        const Tensor& gV, bool create) {
+  at::AutoGradMode enable(true);
+  variable_list leaves = {in.x.detach().requires_grad_(true), in.dist.detach().requires_grad_(true),
+                          in.C.detach().requires_grad_(true), in.u.detach().requires_grad_(true)};
+  std::vector<Tensor> Pl;
+  for (const auto& t : P) Pl.push_back(t.detach().requires_grad_(true));
+  auto out = stack_composite(leaves[0], leaves[1], leaves[2], leaves[3], in.mu, in.beta, Pl, in.g, c);
+  variable_list all = leaves;
+  all.insert(all.end(), Pl.begin(), Pl.end());
+  return torch::autograd::grad({out.first, out.second}, all, {gX, gV}, create, create, true);
+}
+
+struct EtStackBwd : public Function<EtStackBwd> {
+  // (gX, gV, x, dist, C, u, mu, beta, row_ptr, src, dst, params...) -> (g_x, g_dist, g_C, g_u, g_params...)
+  static variable_list forward(AutogradContext* ctx, const Tensor& gX, const Tensor& gV, const Tensor& x,
+                               const Tensor& dist, const Tensor& C, const Tensor& u, const Tensor& mu,
+                               const Tensor& beta, const Tensor& row_ptr, const Tensor& src, const Tensor& dst,
+                               c10::intrusive_ptr<StackActs> acts, StackCfg cfg, bool want_params,
+                               at::TensorList params) {
+    std::vector<Tensor> P(params.begin(), params.end());
+    StackIn in{x, Tensor(), dist, C, u, mu, beta, G{row_ptr, src, dst, Tensor()}};
+    variable_list res;
+    if (!want_params) {
+      res = stack_backward_dr(*acts, gX.contiguous(), gV.contiguous(), dist, C, u, mu, beta, P, in.g, cfg);
+      for (size_t i = 0; i < P.size(); ++i) res.push_back(at::zeros({0}, opts(x)));
+    } else {  // training through TorchScript: autograd over the restatement
+      at::NoGradGuard off;
+      res = stack_vjp(in, P, cfg, gX, gV, false);
+      // a parameter the restatement does not use (layer 0's vec_proj: vec = 0) gets a zero gradient,
+      // as autograd over the reference's layer loop gives it
+      for (size_t i = 0; i < P.size(); ++i)
+        if (!res[4 + i].defined()) res[4 + i] = at::zeros_like(P[i]);
+      for (auto& t : res)
+        if (!t.defined()) t = at::zeros({0}, opts(x));
+    }
+    keep_cfg(ctx, cfg);
+    keep_graph(ctx, in.g);
+    variable_list sv = {gX, gV, x, dist, C, u, mu, beta};
+    sv.insert(sv.end(), P.begin(), P.end());
+    ctx->save_for_backward(sv);
+    return res;
+  }
+
+  // the second order (force-matching training) and beyond: recompute the restatement, differentiate twice
+  static variable_list backward(AutogradContext* ctx, variable_list ggs) {
+    auto sv = ctx->get_saved_variables();
+    const StackCfg c = cfg_of(ctx);
+    G g = graph_of(ctx);
+    const bool create = at::GradMode::is_enabled();
+    at::AutoGradMode enable(true);
+    variable_list leaves;
+    for (size_t i = 0; i < sv.size(); ++i)
+      leaves.push_back((i == 6 || i == 7) ? sv[i] : sv[i].detach().requires_grad_(true));  // mu, beta fixed
+    std::vector<Tensor> P(leaves.begin() + 8, leaves.end());
+    auto out = stack_composite(leaves[2], leaves[3], leaves[4], leaves[5], sv[6], sv[7], P, g, c);
+    variable_list prim = {leaves[2], leaves[3], leaves[4], leaves[5]};
+    prim.insert(prim.end(), P.begin(), P.end());
+    auto first = torch::autograd::grad({out.first, out.second}, prim, {leaves[0], leaves[1]}, true, true, true);
+    variable_list fs, fg;
+    for (size_t i = 0; i < first.size() && i < ggs.size(); ++i)
+      if (ggs[i].defined() && ggs[i].numel() && first[i].defined() && first[i].requires_grad()) {
+        fs.push_back(first[i]);
+        fg.push_back(ggs[i]);
+      }
+    // (gX, gV, x, dist, C, u, mu, beta, row_ptr, src, dst, acts, cfg, want_params, params...)
+    variable_list res(14 + P.size());
+    if (fs.empty()) return res;
+    variable_list wrt = {leaves[0], leaves[1], leaves[2], leaves[3], leaves[4], leaves[5]};
+    wrt.insert(wrt.end(), P.begin(), P.end());
+    auto second = torch::autograd::grad(fs, wrt, fg, true, create, true);
+    for (int i = 0; i < 6; ++i) res[i] = second[i];
+    for (size_t i = 0; i < P.size(); ++i) res[14 + i] = second[6 + i];
+    return res;
+  }
+};
+
+struct EtStack : public Function<EtStack> {
+  static variable_list forward(AutogradContext* ctx, const Tensor& x_in, const Tensor& f_in, const Tensor& dist,
+                               const Tensor& C_in, const Tensor& u_in, const Tensor& mu, const Tensor& beta,
+                               const Tensor& row_ptr, const Tensor& src, const Tensor& dst, StackCfg c,
+                               at::TensorList params) {
+    require_gpu(x_in, "et_stack");
+    TORCH_CHECK(x_in.scalar_type() == at::kFloat, "et_stack: fp32 only (the model's per-layer loop serves fp64)");
+    std::vector<Tensor> P(params.begin(), params.end());
+    const int64_t np = stack_np(c.hk, c.hv);
+    const int64_t nP = static_cast<int64_t>(P.size()) - (c.out_norm ? 2 : 0);
+    TORCH_CHECK(nP > 0 && nP % np == 0, "et_stack: ", P.size(), " parameters for ", np, " per layer");
+    const int64_t L = nP / np;
+    Tensor x = x_in.contiguous(), f = f_in.contiguous(), C = C_in.contiguous(), u = u_in.contiguous();
+    G g{row_ptr, src, dst, Tensor()};
+    const int64_t N = x.size(0), H = x.size(1), E = g.E(), D = (int64_t(c.hk) + 3 * int64_t(c.hv)) * H;
+    TORCH_CHECK(dist.size(0) == E && C.size(0) == E && u.size(0) == E && (!(c.hk || c.hv) || f.size(0) == E),
+                "et_stack: per-edge shapes");
+    auto o = opts(x);
+    auto A = c10::make_intrusive<StackActs>();
+    A->pk = pack_stack(P, L, np, c.hk, c.hv);
+    const bool has_e = c.hk || c.hv;
+    // every layer's projection rows in one GEMM unless that buffer would exceed 2 GB (large graphs:
+    // per layer, recomputed by the backward)
+    A->batched = E * L * D * 4 <= (int64_t(2) << 30);
+    if (has_e) {
+      if (A->batched) {
+        A->pkv_all = at::empty({E, L * D}, o);
+        proj_into(f, A->pk->dkv_w, A->pk->dkv_wp, A->pk->dkv_b, A->pkv_all);
+      } else {
+        A->pkv_all = f;
+      }
+    }
+    auto epi_ln = [&](const Tensor& xx, const Tensor& vv, const Tensor& vp, const Tensor& oo, const Tensor& va,
+                      const Tensor& w, const Tensor& b, Tensor* xo, Tensor* vo, Tensor* xn, Tensor* mean, Tensor* rstd) {
+      *xn = at::empty({N, H}, o);
+      *mean = at::empty({N, 1}, o);
+      *rstd = at::empty({N, 1}, o);
+      if (oo.defined()) {
+        *xo = at::empty({N, H}, o);
+        *vo = at::empty({N, 3, H}, o);
+      }
+      check(tmdnet_et_epilogue_ln_fwd(dcode(xx), static_cast<int>(N), static_cast<int>(H), ptr(xx), ptr(vv), ptr(vp),
+                                      ptr(oo), ptr(va), ptr(w), ptr(b), kLnEps, oo.defined() ? ptr(*xo) : nullptr,
+                                      oo.defined() ? ptr(*vo) : nullptr, ptr(*xn), ptr(*mean), ptr(*rstd),
+                                      stream_of(xx)),
+            "tmdnet_et_epilogue_ln_fwd");
+    };
+    Tensor vec, xn, mean, rstd, unused0, unused1;
+    epi_ln(x, Tensor(), Tensor(), Tensor(), Tensor(), P[0], P[1], &unused0, &unused1, &xn, &mean, &rstd);
+    for (int64_t l = 0; l < L; ++l) {
+      const Tensor* p = P.data() + l * np;
+      Tensor qkv = at::empty({N, 5 * H}, o), vecp;
+      gemm_into(xn, A->pk->qkv_w[l], true, A->pk->qkv_b[l], qkv, false);
+      if (vec.defined()) {
+        vecp = at::empty({N, 3, 3 * H}, o);
+        gemm_into(vec.view({3 * N, H}), p[8], true, Tensor(), vecp.view({3 * N, 3 * H}), false);
+      }
+      Tensor pkv, pk, pv;
+      if (has_e) {
+        if (A->batched) {
+          pkv = A->pkv_all.narrow(1, l * D, D);
+        } else {
+          pkv = at::empty({E, D}, o);
+          proj_into(f, A->pk->dkv_w.narrow(0, l * D, D), Tensor(), A->pk->dkv_b.narrow(0, l * D, D), pkv);
+        }
+        if (c.hk) pk = pkv.narrow(1, 0, H);
+        if (c.hv) pv = pkv.narrow(1, H * int64_t(c.hk), 3 * H);
+      }
+      Tensor xa = at::empty({N, H}, o), veca = at::empty({N, 3, H}, o);
+      float* qb = static_cast<float*>(qkv.data_ptr());
+      check(tmdnet_et_message_fwd(dcode(x), static_cast<int>(N), static_cast<int>(H), static_cast<int>(c.heads),
+                                  ptr<int32_t>(row_ptr), ptr<int32_t>(src), static_cast<int>(E), qb, ld(qkv), qb + H,
+                                  ld(qkv), qb + 2 * H, ld(qkv), ptr(vec), ptr(pk), ld(pk), ptr(pv), ld(pv), ptr(C),
+                                  ptr(u), ptr(xa), ptr(veca), static_cast<int>(c.acts), nullptr, nullptr,
+                                  stream_of(x)),
+            "tmdnet_et_message_fwd");
+      Tensor oo = at::empty({N, 3 * H}, o);
+      gemm_into(xa, p[9], true, p[10], oo, false);
+      A->x.push_back(x); A->vec.push_back(vec); A->xn.push_back(xn); A->mean.push_back(mean);
+      A->rstd.push_back(rstd); A->qkv.push_back(qkv); A->vecp.push_back(vecp); A->xa.push_back(xa);
+      A->o.push_back(oo);
+      Tensor xo, vo;
+      if (l + 1 < L) {
+        epi_ln(x, vec, vecp, oo, veca, P[(l + 1) * np], P[(l + 1) * np + 1], &xo, &vo, &xn, &mean, &rstd);
+      } else if (c.out_norm) {  // the last epilogue + out_norm: x_out = LN(x_pre)
+        epi_ln(x, vec, vecp, oo, veca, P[P.size() - 2], P[P.size() - 1], &xo, &vo, &xn, &mean, &rstd);
+        A->x_pre = xo;
+        A->mean_o = mean;
+        A->rstd_o = rstd;
+        xo = xn;
+      } else {
+        xo = at::empty({N, H}, o);
+        vo = at::empty({N, 3, H}, o);
+        check(tmdnet_et_epilogue_fwd(dcode(x), static_cast<int>(N), static_cast<int>(H), ptr(x), ptr(vec), ptr(vecp),
+                                     ptr(oo), ptr(veca), ptr(xo), ptr(vo), stream_of(x)),
+              "tmdnet_et_epilogue_fwd");
+      }
+      x = xo;
+      vec = vo;
+    }
+    ctx->saved_data["fwd_state"] = c10::IValue::make_capsule(A);  // the forward intermediates (StackActs)
+    keep_cfg(ctx, c);
+    keep_graph(ctx, g);
+    variable_list sv = {x_in, dist, C_in, u_in, mu, beta};
+    sv.insert(sv.end(), P.begin(), P.end());
+    ctx->save_for_backward(sv);
+    return {x, vec};
+  }
+
+  static variable_list backward(AutogradContext* ctx, variable_list go) {
+    auto sv = ctx->get_saved_variables();
+    const StackCfg c = cfg_of(ctx);
+    G g = graph_of(ctx);
+    auto A = c10::static_intrusive_pointer_cast<StackActs>(ctx->saved_data["fwd_state"].toCapsule());
+    std::vector<Tensor> P(sv.begin() + 6, sv.end());
+    // gradients: one per argument (x, f, dist, C, u, mu, beta, row_ptr, src, dst, cfg, params...);
+    // needs_input_grad counts tensor arguments only (cfg has no edge): parameter i is edge 10 + i
+    variable_list res(11 + P.size());
+    bool want_params = false;
+    for (size_t i = 0; i < P.size(); ++i) want_params = want_params || ctx->needs_input_grad(10 + i);
+    const bool any = want_params || ctx->needs_input_grad(0) || ctx->needs_input_grad(2) ||
+                     ctx->needs_input_grad(3) || ctx->needs_input_grad(4);
+    if (!any) return res;
+    Tensor x = sv[0];
+    const int64_t N = x.size(0), H = x.size(1);
+    Tensor gX = go[0].defined() ? go[0] : at::zeros({N, H}, opts(x));
+    Tensor gV = go[1].defined() ? go[1] : at::zeros({N, 3, H}, opts(x));
+    auto o = EtStackBwd::apply(gX, gV, x, sv[1], sv[2], sv[3], sv[4], sv[5], g.row_ptr, g.src, g.dst, A, c,
+                               want_params, at::TensorList(P));  // (a TensorList: every parameter an input)
+    auto sized = [](const Tensor& t) { return t.numel() ? t : Tensor(); };  // zero-size: no gradient
+    res[0] = sized(o[0]);
+    res[2] = sized(o[1]);
+    res[3] = sized(o[2]);
+    res[4] = sized(o[3]);
+    if (want_params)
+      for (size_t i = 0; i < P.size(); ++i)
+        if (ctx->needs_input_grad(10 + i) && o[4 + i].numel()) res[11 + i] = o[4 + i];
+    return res;
+  }
+};
+
+std::tuple<Tensor, Tensor> et_stack(const Tensor& x, const Tensor& f, const Tensor& dist, const Tensor& cutoff,
+                                    const Tensor& unit, const Tensor& mu, const Tensor& beta, const Tensor& row_ptr,
+                                    const Tensor& src, const Tensor& dst, double cutoff_lower, double cutoff_upper,
+                                    int64_t rbf_type, int64_t heads, bool has_dk, bool has_dv, bool out_norm,
+                                    at::TensorList params, int64_t acts) {
+  const c10::OptionalDeviceGuard guard(x.device());
+  StackCfg c{heads, rbf_type, cutoff_lower, cutoff_upper, has_dk, has_dv, out_norm, acts};
+  auto r = EtStack::apply(x, f, dist, cutoff, unit, mu.detach().to(dist.scalar_type()).contiguous(),
+                          beta.detach().to(dist.scalar_type()).contiguous(), row_ptr, src, dst, c, params);
   return {r[0], r[1]};
 }
 
@@ -1078,11 +1604,14 @@ TORCH_LIBRARY(tmdnet, m) {
         "Tensor unit)");
   m.def("nbr_embed(Tensor x, Tensor w, Tensor cutoff, Tensor row_ptr, Tensor src, Tensor dst) -> Tensor");
   m.def("et_message(Tensor q, Tensor k, Tensor v, Tensor? vec, Tensor? pk, Tensor? pv, Tensor cutoff, Tensor unit, "
-        "Tensor row_ptr, Tensor src, Tensor dst, int heads) -> (Tensor x, Tensor vec)");
+        "Tensor row_ptr, Tensor src, Tensor dst, int heads, int acts=0) -> (Tensor x, Tensor vec)");
   m.def("tn_embed(Tensor P, Tensor Q, Tensor W, Tensor cutoff, Tensor unit, Tensor row_ptr, Tensor src, "
         "Tensor dst, float self0_mult) -> Tensor");
   m.def("tn_message(Tensor edge_attr, Tensor comp, Tensor row_ptr, Tensor src, Tensor dst, float self0_mult) -> "
         "Tensor");
+  m.def("et_stack(Tensor x, Tensor f, Tensor dist, Tensor cutoff, Tensor unit, Tensor mu, Tensor beta, "
+        "Tensor row_ptr, Tensor src, Tensor dst, float cutoff_lower, float cutoff_upper, int rbf_type, int heads, "
+        "bool has_dk, bool has_dv, bool out_norm, Tensor[] params, int acts=0) -> (Tensor x, Tensor vec)");
 }
 
 TORCH_LIBRARY_IMPL(tmdnet, CompositeImplicitAutograd, m) {
@@ -1092,4 +1621,5 @@ TORCH_LIBRARY_IMPL(tmdnet, CompositeImplicitAutograd, m) {
   m.impl("et_message", tmdt::et_message);
   m.impl("tn_embed", tmdt::tn_embed);
   m.impl("tn_message", tmdt::tn_message);
+  m.impl("et_stack", tmdt::et_stack);
 }

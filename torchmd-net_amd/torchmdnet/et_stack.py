@@ -233,6 +233,7 @@ class _Meta:
         self.batched = batched  # one GEMM for every layer's projection
         self.planar = False     # TMDNET_ET_V_PLANAR row layout for v / dv (set by et_stack)
         self.flags = 0
+        self.acts = 0           # kernels.et_act_flags of the layers' activations (0: SiLU / SiLU)
         self.qkv_eff = fused    # the weights the GEMMs use (row-permuted copies when planar)
         self.dkv_eff = (dkv_w, dkv_b)
         self.np = 11 + 2 * int(hk) + 2 * int(hv)  # parameters per layer
@@ -1004,7 +1005,7 @@ def _second_order(ctx, ggs, want):
         d_gxa, d_gvec, d_q, d_k, d_v, d_vec, d_pk, d_pv, d_C, d_u = kernels.et_message_bwd2_launch(
             qkv[:, :H], qkv[:, H:2 * H], qkv[:, 2 * H:], vec_l, pk, pv, C, u, graph, meta.heads,
             R["g_xa"], R["gV"] if R["gV"] is not None else torch.zeros((N, 3, H), **o), ggs_m, out=outs,
-            pk_rows=meta.pk_rows if has_e else None, gg_pkv_scale=gr_scale)
+            pk_rows=meta.pk_rows if has_e else None, gg_pkv_scale=gr_scale, flags=meta.acts)
         inj["qkv"][l] = outs["qkv"]
         if has_e:
             inj["pkv"][l] = outs["pkv"]
@@ -1125,7 +1126,7 @@ def composite_stack(meta, x, f, C, u, params, message=None):
             pk = pk if meta.hk else None
             pv = pv if meta.hv else None
         if message is None:
-            xa, veca = kernels.et_message_composite(q, k, v, vec, pk, pv, C, u, src, dst, N, meta.heads)
+            xa, veca = kernels.et_message_composite(q, k, v, vec, pk, pv, C, u, src, dst, N, meta.heads, meta.acts)
         else:
             xa, veca = message(q, k, v, vec, pk, pv, C, u)
         o1, o2, o3 = torch.split(F.linear(xa, o_w, o_b), H, dim=1)
@@ -1265,7 +1266,7 @@ class _ETStackBwd(Function):
         graph, heads = meta.graph, meta.heads
 
         def message(q, k, v, vec, pk, pv, C_, u_):
-            return kernels.et_message(q, k, v, vec, pk, pv, C_, u_, graph, heads)
+            return kernels.et_message(q, k, v, vec, pk, pv, C_, u_, graph, heads, meta.acts)
 
         _create = torch.is_grad_enabled()  # third order only if the caller builds a graph
         n_out = 7 + len(saved)
@@ -1333,8 +1334,12 @@ def et_stack(layers, x, graph, f, C, u, rbf=None, out_norm=None, f_pairs=None):
     D = (int(hk) + 3 * int(hv)) * H
     batched = D > 0 and graph.n_edges * len(layers) * D * x.element_size() <= BATCH_DKV_BYTES
     meta = _Meta(graph, heads, H, hk, hv, len(layers), fused, None, dkv_w, dkv_b, batched)
+    meta.acts = l0.act_flags  # the activations (every layer of a model shares them)
+    if any(layer.act_flags != meta.acts for layer in layers):
+        raise NotImplementedError("et_stack: layers with different activations")
+    meta.flags = meta.acts
     if graph.n_edges >= PLANAR_MIN_EDGES:
-        meta.planar, meta.flags = True, nat.ET_V_PLANAR
+        meta.planar, meta.flags = True, nat.ET_V_PLANAR | meta.acts
         meta.perms = _planar_perms(meta, x.device)
     if D and PAIR_ROWS and graph.symmetric and graph.transpose is not None:
         meta.pairs = kernels.pair_index(graph)
@@ -1350,7 +1355,7 @@ def et_stack(layers, x, graph, f, C, u, rbf=None, out_norm=None, f_pairs=None):
     if rbf is not None and D:
         r, mu, beta, cl, cu, rbf_type = rbf
         meta.rbf = (mu.detach(), beta.detach(), float(cl), float(cu), int(rbf_type))
-        meta.fep = (FEP not in ("0", "off") and meta.planar and hk and hv and x.is_cuda
+        meta.fep = (FEP not in ("0", "off") and meta.planar and hk and hv and x.is_cuda and meta.acts == 0
                     and kernels.fep_supported(H, heads, mu.shape[0], x.dtype) and r.dtype == x.dtype)
     x = x.contiguous()
     f = f.contiguous() if (hk or hv) else None

@@ -686,8 +686,36 @@ def _rowmajor(t):
     return t
 
 
-def et_message_composite(q, k, v, vec, pk, pv, C, u, src, dst, n_nodes, heads):
-    """PyTorch restatement of torchmd_et.py:314-347 (used for the second-order backward only)."""
+# ET message activations (include/tmdnet.h TMDNET_ET_ACT): the reference act_class_mapping
+# (models/utils.py:579-584) by module class, coded in bits 8-11 (dk / dv) and 12-15 (attention) of the
+# message entry points' flags
+ACT_CODES = {"SiLU": 0, "ShiftedSoftplus": 1, "Tanh": 2, "Sigmoid": 3}
+SSP_SHIFT = 0.693147182464599609375  # log 2 rounded to fp32, as the reference's ShiftedSoftplus.shift
+_ACT_FNS = {0: F.silu, 1: lambda x: F.softplus(x) - SSP_SHIFT, 2: torch.tanh, 3: torch.sigmoid}
+
+
+def act_code(module):
+    """The kernels' code of an activation module (SiLU / ShiftedSoftplus / Tanh / Sigmoid)."""
+    code = ACT_CODES.get(type(module).__name__)
+    if code is None:
+        raise NotImplementedError(f"torchmd-net_amd: no ET kernel activation for {type(module).__name__}")
+    return code
+
+
+def et_act_flags(act_kv, act_attn):
+    """Flags bits selecting the dk/dv projection activation and the attention activation."""
+    return (int(act_kv) << 8) | (int(act_attn) << 12)
+
+
+def et_act_fns(acts):
+    """(dk/dv activation, attention activation) functions of a flags word."""
+    return _ACT_FNS[(acts >> 8) & 15], _ACT_FNS[(acts >> 12) & 15]
+
+
+def et_message_composite(q, k, v, vec, pk, pv, C, u, src, dst, n_nodes, heads, acts=0):
+    """PyTorch restatement of torchmd_et.py:314-347 (used for the second-order backward only);
+    ``acts``: the activation bits of the kernels' flags (et_act_flags)."""
+    act_kv, act_at = et_act_fns(acts)
     H = q.shape[1]
     d = H // heads
     valid = (src >= 0).to(q.dtype)  # static-capacity padding slots (-1) carry no message
@@ -696,11 +724,11 @@ def et_message_composite(q, k, v, vec, pk, pv, C, u, src, dst, n_nodes, heads):
     kj = k.index_select(0, src).view(-1, heads, d)
     s = qi * kj
     if pk is not None:
-        s = s * F.silu(pk).view(-1, heads, d)
-    attn = F.silu(s.sum(-1)) * C.unsqueeze(1)
+        s = s * act_kv(pk).view(-1, heads, d)
+    attn = act_at(s.sum(-1)) * C.unsqueeze(1)
     vj = v.index_select(0, src).view(-1, heads, 3 * d)
     if pv is not None:
-        vj = vj * F.silu(pv).view(-1, heads, 3 * d)
+        vj = vj * act_kv(pv).view(-1, heads, 3 * d)
     x, v1, v2 = torch.split(vj, d, dim=2)
     xm = x * (attn * valid.unsqueeze(1)).unsqueeze(2)
     vecj = vec.index_select(0, src).view(-1, 3, heads, d)
@@ -712,13 +740,14 @@ def et_message_composite(q, k, v, vec, pk, pv, C, u, src, dst, n_nodes, heads):
 
 class _ETMessage(Function):
     @staticmethod
-    def forward(ctx, q, k, v, vec, pk, pv, C, u, graph, heads):
+    def forward(ctx, q, k, v, vec, pk, pv, C, u, graph, heads, acts=0):
         N, H = q.shape
         xo = torch.empty((N, H), dtype=q.dtype, device=q.device)
         vo = torch.empty((N, 3, H), dtype=q.dtype, device=q.device)
-        et_message_fwd_launch(q, k, v, vec, pk, pv, C, u, graph, heads, xo, vo)
+        et_message_fwd_launch(q, k, v, vec, pk, pv, C, u, graph, heads, xo, vo, flags=acts)
         ctx.graph = graph
         ctx.heads = heads
+        ctx.acts = acts
         ctx.save_for_backward(q, k, v, vec, pk, pv, C, u)
         return xo, vo
 
@@ -730,15 +759,15 @@ class _ETMessage(Function):
         if gvec is None:
             gvec = torch.zeros((q.shape[0], 3, q.shape[1]), dtype=q.dtype, device=q.device)
         outs = _ETMessageBwd.apply(gx.contiguous(), gvec.contiguous(), q, k, v, vec, pk, pv, C, u,
-                                   ctx.graph, ctx.heads)
+                                   ctx.graph, ctx.heads, ctx.acts)
         gq, gk, gv, gw, gpk, gpv, gC, gu = outs
         return gq, gk, gv, gw, (gpk if pk is not None else None), (gpv if pv is not None else None), \
-            gC, gu, None, None
+            gC, gu, None, None, None
 
 
 class _ETMessageBwd(Function):
     @staticmethod
-    def forward(ctx, gx, gvec, q, k, v, vec, pk, pv, C, u, graph, heads):
+    def forward(ctx, gx, gvec, q, k, v, vec, pk, pv, C, u, graph, heads, acts=0):
         if not graph.symmetric:
             raise RuntimeError("torchmd-net_amd: the ET backward source pass needs a symmetric edge "
                                "list (include_transpose=True, no capacity overflow)")
@@ -753,13 +782,14 @@ class _ETMessageBwd(Function):
         gC = torch.empty((E,), **o)
         gu = torch.empty((E, 3), **o)
         et_message_bwd_launch(q, k, v, vec, pk, pv, C, u, graph, heads, gx, gvec, gq, gk, gv, gw,
-                              gpk, gpv, gC, gu)
+                              gpk, gpv, gC, gu, accumulate=acts)
         if gpk is None:
             gpk = torch.zeros(0, **o)
         if gpv is None:
             gpv = torch.zeros(0, **o)
         ctx.graph = graph
         ctx.heads = heads
+        ctx.acts = acts
         ctx.save_for_backward(gx, gvec, q, k, v, vec, pk, pv, C, u)
         return gq, gk, gv, gw, gpk, gpv, gC, gu
 
@@ -777,7 +807,8 @@ class _ETMessageBwd(Function):
         with torch.enable_grad():
             leaves = [None if t is None else t.detach().requires_grad_(True) for t in saved]
             gx, gvec, q, k, v, vec, pk, pv, C, u = leaves
-            xo, vo = et_message_composite(q, k, v, vec, pk, pv, C, u, src, dst, graph.n_nodes, ctx.heads)
+            xo, vo = et_message_composite(q, k, v, vec, pk, pv, C, u, src, dst, graph.n_nodes, ctx.heads,
+                                          ctx.acts)
             wrt = [t for t in (q, k, v, vec, pk, pv, C, u)]
             live = [t for t in wrt if t is not None]
             first = torch.autograd.grad((xo, vo), live, (gx, gvec), create_graph=True, allow_unused=True)
@@ -786,12 +817,12 @@ class _ETMessageBwd(Function):
             sel = [(f, g) for f, g in zip(first_full, ggs) if f is not None and g is not None and g.numel()]
             ins = [t for t in leaves if t is not None]
             if not sel:
-                return (None,) * 12
+                return (None,) * 13
             second = torch.autograd.grad([f for f, _ in sel], ins, [g for _, g in sel],
                                          create_graph=_create, allow_unused=True)
         it = iter(second)
         res = [next(it) if t is not None else None for t in leaves]
-        return tuple(res) + (None, None)
+        return tuple(res) + (None, None, None)
 
 
 # the deterministic source pass of tmdnet_et_message_bwd2_ex stores 7H values per edge: used up to
@@ -887,13 +918,15 @@ def et_message_bwd2(ctx, ggs):
     """HIP second-order backward of the ET message (``tmdnet_et_message_bwd2``).  Its own backward
     (third order) is not implemented."""
     gx, gvec, q, k, v, vec, pk, pv, C, u = ctx.saved_tensors
-    out = et_message_bwd2_launch(q, k, v, vec, pk, pv, C, u, ctx.graph, ctx.heads, gx, gvec, ggs)
-    return tuple(out) + (None, None)
+    out = et_message_bwd2_launch(q, k, v, vec, pk, pv, C, u, ctx.graph, ctx.heads, gx, gvec, ggs,
+                                 flags=getattr(ctx, "acts", 0))
+    return tuple(out) + (None, None, None)
 
 
-def et_message(q, k, v, vec, pk, pv, C, u, graph, heads):
+def et_message(q, k, v, vec, pk, pv, C, u, graph, heads, acts=0):
+    """The ET message + aggregation (HIP, differentiable twice); ``acts`` = et_act_flags(...)."""
     q, k, v, pk, pv = (_rowmajor(t) for t in (q, k, v, pk, pv))
-    return _ETMessage.apply(q, k, v, vec.contiguous(), pk, pv, C.contiguous(), u.contiguous(), graph, heads)
+    return _ETMessage.apply(q, k, v, vec.contiguous(), pk, pv, C.contiguous(), u.contiguous(), graph, heads, acts)
 
 
 # ----------------------------------------------------------------------------- neighbour embedding
@@ -2002,8 +2035,10 @@ class _MLPAct(Function):
         x, scale = sv[0], sv[1]
         ws, bs = sv[2:2 + L], sv[2 + L:2 + 2 * L]
         pres, hmid = sv[2 + 2 * L:2 + 3 * L], sv[2 + 3 * L:]
+        # next_functions has no entry for a None input (scale may be None): index by tensor inputs
         nf = ctx.next_functions
-        need = [ctx.needs_input_grad[i] and _will_run(nf[i][0]) for i in range(2 + 2 * L)]
+        at = [i - (1 if (scale is None and i > 1) else 0) for i in range(2 + 2 * L)]
+        need = [ctx.needs_input_grad[i] and _will_run(nf[at[i]][0]) for i in range(2 + 2 * L)]
         if not any(need):
             return (None,) * (2 + 2 * L)
         outs = _MLPActBwd.apply(tuple(need), gy.contiguous(), x, scale, *ws, *bs, *pres, *hmid)

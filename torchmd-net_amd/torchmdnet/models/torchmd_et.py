@@ -10,7 +10,7 @@ reference checkpoints load.  The per-edge work runs in HIP kernels:
 The dense node/edge projections (LayerNorm, q/k/v/o/vec, dk/dv) are GEMMs (rocBLAS/hipBLASLt via
 torch, MFMA) whose outputs feed the kernels without reshuffling.
 """
-from typing import Optional, Tuple
+from typing import List, Optional, Tuple
 
 import torch
 from torch import Tensor, nn
@@ -109,11 +109,12 @@ class TorchMD_ET(nn.Module):
         return x, vec, z, pos, batch
 
     def _forward_script(self, z: Tensor, pos: Tensor, batch: Tensor) -> Tuple[Tensor, Tensor]:
-        """TorchScript path (torch.jit.script(model)): the reference layer loop
-        (torchmd_et.py:160-190) over the dispatcher operators of libtmdnet_torch.so -- neighbour
-        list, edge geometry, neighbour embedding and the ET message are the HIP kernels with C++
-        autograd (differentiable twice: forces and force-matching training); the node projections are
-        ATen GEMMs."""
+        """TorchScript path (torch.jit.script(model)) over the dispatcher operators of
+        libtmdnet_torch.so -- neighbour list, edge geometry and neighbour embedding are the HIP kernels
+        with C++ autograd; the interaction layers (fp32, fixed RBF basis) run as ONE ``tmdnet::et_stack``
+        operator with the eager stack's fused launches and dr-mode force backward (differentiable to any
+        order: parameter gradients and higher orders by recompute).  fp64 or a trainable basis: the
+        reference layer loop (torchmd_et.py:160-190) over ``tmdnet::et_message`` with ATen node GEMMs."""
         x = self.embedding(z)
         d = self.distance
         row_ptr, src, dst, tr, deltas, dist, num_pairs = torch.ops.tmdnet.neighbor_graph(
@@ -129,6 +130,28 @@ class TorchMD_ET(nn.Module):
         ne = self.neighbor_embedding
         if ne is not None:
             x = ne.script_forward(z, x, row_ptr, src, dst, f, C)
+        if self.fused_stack and not trainable and x.dtype == torch.float32 and len(self.attention_layers) > 0:
+            # every layer + out_norm as ONE operator (tmdnet::et_stack): the eager stack's fused launches
+            # and its dr-mode force backward (et_stack.py), f delivered as rbf(dist)
+            params: List[Tensor] = []
+            hk = False
+            hv = False
+            acts = 0
+            for attn in self.attention_layers:
+                params += attn.stack_params()
+                hk = attn.dk_proj is not None
+                hv = attn.dv_proj is not None
+                acts = attn.act_flags
+            on = self.out_norm
+            fuse_norm = on.elementwise_affine and on.eps == 1e-5
+            if fuse_norm:
+                params += [on.weight, on.bias]
+            x, vec = torch.ops.tmdnet.et_stack(x, f, dist, C, u, mu, beta, row_ptr, src, dst, float(self.cutoff_lower),
+                                               float(self.cutoff_upper), de.rbf_type, self.num_heads, hk, hv,
+                                               fuse_norm, params, acts)
+            if not fuse_norm:
+                x = on(x)
+            return x, vec
         vec = torch.zeros(x.size(0), 3, x.size(1), device=x.device, dtype=x.dtype)
         for attn in self.attention_layers:
             dx, dvec = attn.script_forward(x, vec, row_ptr, src, dst, f, C, u)
@@ -208,6 +231,8 @@ class EquivariantMultiHeadAttention(nn.Module):
         self.layernorm = nn.LayerNorm(hidden_channels, dtype=dtype)
         self.act = activation()
         self.attn_activation = act_class_mapping[attn_activation]()
+        # both activations as the edge kernels' codes (SiLU / ShiftedSoftplus / Tanh / Sigmoid)
+        self.act_flags = kernels.et_act_flags(kernels.act_code(self.act), kernels.act_code(self.attn_activation))
         self.cutoff = CosineCutoff(cutoff_lower, cutoff_upper)
 
         self.q_proj = nn.Linear(hidden_channels, hidden_channels, dtype=dtype)
@@ -246,9 +271,20 @@ class EquivariantMultiHeadAttention(nn.Module):
             self.dv_proj.bias.data.fill_(0)
 
     def _check_supported(self):
-        if not isinstance(self.act, nn.SiLU) or not isinstance(self.attn_activation, nn.SiLU):
-            raise NotImplementedError("torchmd-net_amd: the fused ET edge kernel implements SiLU for "
-                                      "activation and attn_activation (the reference default)")
+        """Re-derive the kernels' activation codes (the modules may have been replaced after
+        construction); raises NotImplementedError outside the reference's act_class_mapping."""
+        self.act_flags = kernels.et_act_flags(kernels.act_code(self.act), kernels.act_code(self.attn_activation))
+
+    def stack_params(self) -> List[Tensor]:
+        """This layer's parameters in tmdnet::et_stack's order (et_stack.layer_params)."""
+        ps = [self.layernorm.weight, self.layernorm.bias, self.q_proj.weight, self.q_proj.bias,
+              self.k_proj.weight, self.k_proj.bias, self.v_proj.weight, self.v_proj.bias,
+              self.vec_proj.weight, self.o_proj.weight, self.o_proj.bias]
+        if self.dk_proj is not None:
+            ps += [self.dk_proj.weight, self.dk_proj.bias]
+        if self.dv_proj is not None:
+            ps += [self.dv_proj.weight, self.dv_proj.bias]
+        return ps
 
     def script_forward(self, x: Tensor, vec: Tensor, row_ptr: Tensor, src: Tensor, dst: Tensor, f_ij: Tensor,
                        C: Tensor, d_ij: Tensor) -> Tuple[Tensor, Tensor]:
@@ -266,7 +302,8 @@ class EquivariantMultiHeadAttention(nn.Module):
             pk = self.dk_proj(f_ij)
         if self.dv_proj is not None:
             pv = self.dv_proj(f_ij)
-        xa, veca = torch.ops.tmdnet.et_message(q, k, v, vec, pk, pv, C, d_ij, row_ptr, src, dst, self.num_heads)
+        xa, veca = torch.ops.tmdnet.et_message(q, k, v, vec, pk, pv, C, d_ij, row_ptr, src, dst, self.num_heads,
+                                               self.act_flags)
         o1, o2, o3 = torch.split(self.o_proj(xa), self.hidden_channels, dim=1)
         return vec_dot * o2 + o3, vec3 * o1.unsqueeze(1) + veca
 
@@ -287,7 +324,7 @@ class EquivariantMultiHeadAttention(nn.Module):
         vec_dot = (vec1 * vec2).sum(dim=1)
         pk = self.dk_proj(f_ij) if self.dk_proj is not None else None
         pv = self.dv_proj(f_ij) if self.dv_proj is not None else None
-        xa, veca = kernels.et_message(q, k, v, vec, pk, pv, C, d_ij, graph, self.num_heads)
+        xa, veca = kernels.et_message(q, k, v, vec, pk, pv, C, d_ij, graph, self.num_heads, self.act_flags)
         o1, o2, o3 = torch.split(self.o_proj(xa), self.hidden_channels, dim=1)
         dx = vec_dot * o2 + o3
         dvec = vec3 * o1.unsqueeze(1) + veca
