@@ -46,6 +46,8 @@ def _compare(model, ref, what):
             continue
         got = torch.zeros_like(p) if p.grad is None else p.grad
         d = float((got.detach().cpu().double() - ref[n]).norm()) / max(float(ref[n].norm()), floor)
+        if d > TOL:
+            print(f"{what}: {n} off by {d:.3g} (|ref| {float(ref[n].norm()):.3g}, |got| {float(got.norm()):.3g})")
         worst = max(worst, (d, n))
     print(f"{what}: worst parameter-gradient norm-relative error {worst[0]:.3g} ({worst[1]})")
     assert worst[0] <= TOL, f"{what}: worst parameter {worst[1]} at {worst[0]:.3g}"

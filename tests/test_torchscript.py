@@ -308,8 +308,9 @@ def test_torchscript_et_runs_fused_stack_operator():
     _torch_lib_loaded()
     model, _ = _et_model(channels=64, layers=2)
     scripted = torch.jit.script(model.to(DEV))
-    code = scripted.representation_model.code
-    assert "tmdnet.et_stack" in code
+    # (forward calls _forward_script: the inlined graph holds every method it reaches)
+    graph = str(scripted.representation_model.forward.inlined_graph)
+    assert "tmdnet::et_stack" in graph
 
 
 @pytest.mark.parametrize("influence", ["keys", "values", "none"])

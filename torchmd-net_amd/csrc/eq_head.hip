@@ -212,6 +212,99 @@ __device__ __forceinline__ void cols2(const T* __restrict__ A, int lda, int I, c
   }
 }
 
+// cols2 with the I rows split over thread slices: at K = 64-128 output columns cols2 keeps only K/2
+// threads of the workgroup busy, each walking all I (+ I2) weight rows as a dependent chain of L2
+// round trips.  Here IS = blockDim / (K/2) slices each sum their share of the rows, the partial
+// sums meet in LDS (`red`: IS x NT x R x K values) and are added in slice order (deterministic).
+// Every thread of the workgroup must call it (one internal barrier).
+template <typename T, int NT, int R, bool VEC>
+__device__ __forceinline__ void cols_range(T (&acc)[2][NT][R], const T* __restrict__ A, int lda, int i0, int i1,
+                                           const T* g, int ldg, int k0, int P) {
+  using V2 = T __attribute__((ext_vector_type(2)));
+  using V4 = T __attribute__((ext_vector_type(4)));
+  if (VEC) {  // i0, i1 multiples of 4
+#pragma unroll 4
+    for (int i = i0; i < i1; i += 4) {
+      V2 wv[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) wv[q] = *reinterpret_cast<const V2*>(A + (size_t)(i + q) * lda + k0);
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const V4 gv = *reinterpret_cast<const V4*>(g + t * P + r * ldg + i);
+          acc[0][t][r] += wv[0].x * gv.x + wv[1].x * gv.y + wv[2].x * gv.z + wv[3].x * gv.w;
+          acc[1][t][r] += wv[0].y * gv.x + wv[1].y * gv.y + wv[2].y * gv.z + wv[3].y * gv.w;
+        }
+    }
+  } else {
+#pragma unroll 8
+    for (int i = i0; i < i1; ++i) {
+      const V2 wv = *reinterpret_cast<const V2*>(A + (size_t)i * lda + k0);
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const T gv = g[t * P + r * ldg + i];
+          acc[0][t][r] += wv.x * gv;
+          acc[1][t][r] += wv.y * gv;
+        }
+    }
+  }
+}
+
+template <typename T, int NT, int R, bool VEC>
+__device__ __forceinline__ void cols2s(const T* __restrict__ A, int lda, int I, const T* g, int ldg,
+                                       const T* __restrict__ B, int ldb, int I2, const T* g2, int ldg2,
+                                       int K, T* out, int ldo, int P, int nt, size_t gstride, bool global,
+                                       T* red) {
+  const int CP = K / 2;
+  if (CP > (int)blockDim.x) {  // wider than the workgroup: the unsplit form
+    cols2<T, NT, R, VEC>(A, lda, I, g, ldg, B, ldb, I2, g2, ldg2, K, out, ldo, P, nt, gstride, global);
+    return;
+  }
+  int IS = 1;
+  while (2 * IS * CP <= (int)blockDim.x && 2 * IS <= 8) IS *= 2;
+  const int s = threadIdx.x / CP, k0 = (threadIdx.x % CP) * 2;
+  if (s < IS) {
+    T acc[2][NT][R];
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < R; ++r) acc[q][t][r] = T(0);
+    const int gran = VEC ? 4 : 1;
+    const int pa = ((I + IS * gran - 1) / (IS * gran)) * gran;
+    cols_range<T, NT, R, VEC>(acc, A, lda, min(I, s * pa), min(I, (s + 1) * pa), g, ldg, k0, P);
+    if (I2 > 0) {
+      const int pb = ((I2 + IS * gran - 1) / (IS * gran)) * gran;
+      cols_range<T, NT, R, VEC>(acc, B, ldb, min(I2, s * pb), min(I2, (s + 1) * pb), g2, ldg2, k0, P);
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) red[((s * NT + t) * R + r) * K + k0 + q] = acc[q][t][r];
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < NT * R * K; e += blockDim.x) {
+    const int t = e / (R * K), r = (e / K) % R, k = e % K;
+    T v = T(0);
+    for (int s2 = 0; s2 < IS; ++s2) v += red[((s2 * NT + t) * R + r) * K + k];
+    if (global) {
+      if (t < nt) out[t * gstride + r * ldo + k] = v;
+    } else {
+      out[t * P + r * ldo + k] = v;
+    }
+  }
+  __syncthreads();  // `red` is reused by the next call
+}
+
+// LDS scratch of cols2s per atom: IS x R x K <= (2 x 256 threads / K) x 3 x K values
+constexpr int kColsRed = 2 * 256 * 3;
+
 // LDS layout of one atom (units of T); H = hidden, O = H/2 (block-1 output = block-2 input), Q = O.
 struct Layout {
   int v, h, vb, v2, u, s, o, v1, h2, vb2, v22, u2, s2, o2;      // forward
@@ -262,6 +355,7 @@ __global__ __launch_bounds__(256) void k_eq_head(int n, int H, const T* __restri
   const int n0 = blockIdx.x * NT;
   const int nt = min(NT, n - n0);
   const int tid = threadIdx.x, bs = blockDim.x;
+  T* red = sm + NT * P;  // cols2s scratch (launch adds NT x kColsRed values)
 
   // stage x -> h[0:H], vec -> v (rows of absent atoms are zero)
   for (int i = tid; i < NT * 4 * H; i += bs) {
@@ -333,8 +427,8 @@ __global__ __launch_bounds__(256) void k_eq_head(int n, int H, const T* __restri
 
   // ---------------- reverse pass for J = d y / d (x, vec), seed dy = 1 (vec'' enters y as 0 * sum)
   // block 2: g_h2 = P1^T g_u2
-  cols2<T, NT, 1, VEC>(W.p1w, 2 * Q, Q, sm + L.gu2, 0, nullptr, 0, 0, nullptr, 0, 2 * Q, sm + L.gh2, 0, P, nt, 0,
-                  false);
+  cols2s<T, NT, 1, VEC>(W.p1w, 2 * Q, Q, sm + L.gu2, 0, nullptr, 0, 0, nullptr, 0, 2 * Q, sm + L.gh2, 0, P, nt, 0,
+                  false, red);
   __syncthreads();
   for (int i = tid; i < NT * Q; i += bs) {
     const int t = i / Q, c = i - t * Q;
@@ -346,7 +440,7 @@ __global__ __launch_bounds__(256) void k_eq_head(int n, int H, const T* __restri
   }
   __syncthreads();
   // g_v1 = V1^T g_vb2 (the vec'' gate contributes nothing: its cotangent is 0)
-  cols2<T, NT, 3, VEC>(W.v1, O, Q, sm + L.gvb2, Q, nullptr, 0, 0, nullptr, 0, O, sm + L.gv1, O, P, nt, 0, false);
+  cols2s<T, NT, 3, VEC>(W.v1, O, Q, sm + L.gvb2, Q, nullptr, 0, 0, nullptr, 0, O, sm + L.gv1, O, P, nt, 0, false, red);
   __syncthreads();
   // block 1 gate: g_xo = g_x1 SiLU'(xo), g_vo = sum_a g_v1 v2, g_v2 = g_v1 vo
   for (int i = tid; i < NT * O; i += bs) {
@@ -366,7 +460,7 @@ __global__ __launch_bounds__(256) void k_eq_head(int n, int H, const T* __restri
   }
   __syncthreads();
   // g_s = U2^T g_o, g_u = g_s SiLU'(u)
-  cols2<T, NT, 1, VEC>(W.u2w, H, 2 * O, sm + L.go, 0, nullptr, 0, 0, nullptr, 0, H, sm + L.gu, 0, P, nt, 0, false);
+  cols2s<T, NT, 1, VEC>(W.u2w, H, 2 * O, sm + L.go, 0, nullptr, 0, 0, nullptr, 0, H, sm + L.gu, 0, P, nt, 0, false, red);
   __syncthreads();
   for (int i = tid; i < NT * H; i += bs) {
     const int t = i / H, c = i - t * H;
@@ -377,10 +471,10 @@ __global__ __launch_bounds__(256) void k_eq_head(int n, int H, const T* __restri
   }
   __syncthreads();
   // g_h = U1^T g_u (U1 is [H][2H]): the x half is J_x (global), the vec1 half stays in LDS
-  cols2<T, NT, 1, VEC>(W.u1w, 2 * H, H, sm + L.gu, 0, nullptr, 0, 0, nullptr, 0, H, jx + (size_t)n0 * H, 0, P, nt,
-                  (size_t)H, true);
-  cols2<T, NT, 1, VEC>(W.u1w + H, 2 * H, H, sm + L.gu, 0, nullptr, 0, 0, nullptr, 0, H, sm + L.gvec1, 0, P, nt, 0,
-                  false);
+  cols2s<T, NT, 1, VEC>(W.u1w, 2 * H, H, sm + L.gu, 0, nullptr, 0, 0, nullptr, 0, H, jx + (size_t)n0 * H, 0, P, nt,
+                  (size_t)H, true, red);
+  cols2s<T, NT, 1, VEC>(W.u1w + H, 2 * H, H, sm + L.gu, 0, nullptr, 0, 0, nullptr, 0, H, sm + L.gvec1, 0, P, nt, 0,
+                  false, red);
   __syncthreads();
   for (int i = tid; i < NT * H; i += bs) {
     const int t = i / H, c = i - t * H;
@@ -392,8 +486,8 @@ __global__ __launch_bounds__(256) void k_eq_head(int n, int H, const T* __restri
   }
   __syncthreads();
   // J_vec[a] = W1^T g_vb[a] + W2^T g_v2[a]
-  cols2<T, NT, 3, VEC>(W.w1, H, H, sm + L.gvb, H, W.w2, H, O, sm + L.gv2, O, H, jv + (size_t)n0 * 3 * H, H, P,
-                  nt, (size_t)3 * H, true);
+  cols2s<T, NT, 3, VEC>(W.w1, H, H, sm + L.gvb, H, W.w2, H, O, sm + L.gv2, O, H, jv + (size_t)n0 * 3 * H, H, P,
+                  nt, (size_t)3 * H, true, red);
   if (S.a1 == nullptr) return;
   // weights mode: every LDS buffer is still intact (no aliasing); dump the per-atom factors
   const int wa1 = H + O, wa2 = Q + 1;
@@ -778,7 +872,7 @@ using namespace tmd;
 // MI355X: 56 us at 580 atoms with 1, 41 ns/atom at 50k atoms with 2; 4 is slower at every size).
 static int head_tile(int dtype, int H, int n, size_t* smem) {
   const size_t es = dtype == TMDNET_F64 ? 8 : 4;
-  const size_t per = (size_t)head::Layout(H).P * es;
+  const size_t per = ((size_t)head::Layout(H).P + head::kColsRed) * es;  // + the cols2s scratch
   int cap = n < 2048 ? 1 : 2;
   static const int env_nt = [] { const char* e = getenv("TMDNET_HEAD_NT"); return e ? atoi(e) : 0; }();  // tuning, read once
   if (env_nt > 0) cap = env_nt >= 4 ? 4 : env_nt >= 2 ? 2 : 1;

@@ -239,6 +239,35 @@ __global__ __launch_bounds__(256) void k_ln_bwd_epi(int n, int H, const T* __res
   if (t >= n) return;
   const T mu = mean[t], rs = rstd[t];
   T gh[CPL], xh[CPL];
+  // the epilogue-backward operands are loaded with the LayerNorm's, before the two row sums: one
+  // memory round trip per node instead of two (C2: 9 -> see DESIGN 3b)
+  T gr[CPL], o1[CPL], o2[CPL], vq[CPL][9], gq[CPL][3];
+  const bool ev = o != nullptr && vecp != nullptr;
+#pragma unroll
+  for (int i = 0; i < CPL; ++i) {
+    const int c = lane + 64 * i;
+    gr[i] = o1[i] = o2[i] = T(0);
+#pragma unroll
+    for (int a = 0; a < 9; ++a) vq[i][a] = T(0);
+#pragma unroll
+    for (int a = 0; a < 3; ++a) gq[i][a] = T(0);
+    if (c >= H) continue;
+    if (gres) gr[i] += gres[(size_t)t * H + c];
+    if (gres2) gr[i] += gres2[(size_t)t * H + c];
+    if (ev) {
+      const T* ot = o + (size_t)t * 3 * H;
+      const T* vp = vecp + (size_t)t * 9 * H;
+      o1[i] = ot[c];
+      o2[i] = ot[H + c];
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        vq[i][3 * a] = vp[a * 3 * H + c];
+        vq[i][3 * a + 1] = vp[a * 3 * H + H + c];
+        vq[i][3 * a + 2] = vp[a * 3 * H + 2 * H + c];
+        gq[i][a] = gvec[((size_t)t * 3 + a) * H + c];
+      }
+    }
+  }
   T s1 = T(0), s2 = T(0);
 #pragma unroll
   for (int i = 0; i < CPL; ++i) {
@@ -257,11 +286,9 @@ __global__ __launch_bounds__(256) void k_ln_bwd_epi(int n, int H, const T* __res
   for (int i = 0; i < CPL; ++i) {
     const int c = lane + 64 * i;
     if (c >= H) continue;
-    const T g = (gres ? gres[(size_t)t * H + c] : T(0)) + (gres2 ? gres2[(size_t)t * H + c] : T(0)) +
-                rs * (gh[i] - m1 - xh[i] * m2);
+    const T g = gr[i] + rs * (gh[i] - m1 - xh[i] * m2);
     gx[(size_t)t * H + c] = g;
     if (!o) continue;
-    const T* ot = o + (size_t)t * 3 * H;
     T* gt = go + (size_t)t * 3 * H;
     if (!vecp) {
       put(gt + c, T(0), acc);
@@ -269,20 +296,18 @@ __global__ __launch_bounds__(256) void k_ln_bwd_epi(int n, int H, const T* __res
       put(gt + 2 * H + c, g, acc);
       continue;
     }
-    const T* vp = vecp + (size_t)t * 9 * H;
     T* gvp = gvecp + (size_t)t * 9 * H;
-    const T o1 = ot[c], o2 = ot[H + c];
     T dot = T(0), go1 = T(0);
-    const T gd = g * o2;
+    const T gd = g * o2[i];
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
-      const T v1 = vp[a * 3 * H + c], v2 = vp[a * 3 * H + H + c], v3 = vp[a * 3 * H + 2 * H + c];
-      const T gv = gvec[((size_t)t * 3 + a) * H + c];
+      const T v1 = vq[i][3 * a], v2 = vq[i][3 * a + 1], v3 = vq[i][3 * a + 2];
+      const T gv = gq[i][a];
       dot += v1 * v2;
       go1 += gv * v3;
       put(gvp + a * 3 * H + c, gd * v2, acc);
       put(gvp + a * 3 * H + H + c, gd * v1, acc);
-      put(gvp + a * 3 * H + 2 * H + c, gv * o1, acc);
+      put(gvp + a * 3 * H + 2 * H + c, gv * o1[i], acc);
     }
     put(gt + c, go1, acc);
     put(gt + H + c, g * dot, acc);

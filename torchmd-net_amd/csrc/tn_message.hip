@@ -60,6 +60,20 @@ template <typename T> __device__ __forceinline__ T mult0_of(const Args<T>& A) {
   return T(1 + (pad > 0 ? pad : 0));
 }
 
+// Static-capacity edge lists: rows [row_ptr[n], cap) of the per-edge gradient outputs belong to no
+// CSR row.  They are zeroed here, spread over the whole grid (every thread, before any early exit),
+// so the weight-gradient GEMMs over all `cap` rows (the edge / distance MLPs) see zeros, not stale
+// memory; the dynamic graph (cap == row_ptr[n]) skips it.
+template <typename T>
+__device__ __forceinline__ void zero_tail_rows(const Args<T>& A, T* p, int w) {
+  if (p == nullptr) return;
+  const int e0 = min(A.row_ptr[A.n], A.cap);
+  if (e0 >= A.cap) return;
+  const long long cnt = (long long)(A.cap - e0) * w;
+  const long long tid = (long long)blockIdx.x * blockDim.x + threadIdx.x, nth = (long long)gridDim.x * blockDim.x;
+  for (long long i = tid; i < cnt; i += nth) p[(size_t)e0 * w + i] = T(0);
+}
+
 __device__ __forceinline__ void wave_node(int nblk, int& node, int& ch0) {
   const int w = blockIdx.x * (blockDim.x / TMD_WAVE) + threadIdx.x / TMD_WAVE;
   node = w / nblk;
@@ -135,6 +149,9 @@ __global__ __launch_bounds__(256) void k_embed_fwd(Args<T> A) {
 // blocks, so the per-edge channel sums (gC, gu) finish inside the wave: plain stores, deterministic.
 template <typename T, int NB>
 __global__ __launch_bounds__(256) void k_embed_bwd_dst(Args<T> A) {
+  zero_tail_rows(A, A.gW, 3 * A.H);
+  zero_tail_rows(A, A.gC, 1);
+  zero_tail_rows(A, A.gu, 3);
   const int n = blockIdx.x * (blockDim.x / TMD_WAVE) + threadIdx.x / TMD_WAVE;
   if (n >= A.n) return;
   const int lane = lane_id();
@@ -266,6 +283,7 @@ __global__ __launch_bounds__(256) void k_msg_fwd(Args<T> A) {
 // destination pass: gea[e'] = <gmsg[n], {I,A,S}[m]>
 template <typename T>
 __global__ __launch_bounds__(256) void k_msg_bwd_dst(Args<T> A) {
+  zero_tail_rows(A, A.gea, 3 * A.H);
   int n, ch0;
   wave_node(A.nblk, n, ch0);
   if (n >= A.n) return;

@@ -2101,11 +2101,15 @@ def _raise(msg):
     raise RuntimeError(msg)
 
 
+# TMDNET_MLP_ACT=0: the Linear + fused_act composite per layer instead (A/B switch)
+MLP_ACT = os.environ.get("TMDNET_MLP_ACT", "1") not in ("0", "off")
+
+
 def mlp_act(x, weights, biases, act, scale=None):
     """``act(... act(x W_0^T + b_0) ...) * scale[:, None]`` for nn.Linear weights / biases: the hand
     fused path for SiLU on fp32 CUDA rows within the GEMM envelope, else Linear + fused_act per layer."""
     L = len(weights)
-    ok = (isinstance(act, torch.nn.SiLU) and x.is_cuda and x.dtype == torch.float32 and x.dim() == 2
+    ok = (MLP_ACT and isinstance(act, torch.nn.SiLU) and x.is_cuda and x.dtype == torch.float32 and x.dim() == 2
           and 0 < x.shape[0] <= GEMM_MAX_ROWS and all(b is not None for b in biases)
           and all(w.shape[1] % 16 == 0 for w in weights) and all(w.shape[0] % 16 == 0 for w in weights))
     if not ok:
