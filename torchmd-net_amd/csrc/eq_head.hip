@@ -305,6 +305,17 @@ __device__ __forceinline__ void cols2s(const T* __restrict__ A, int lda, int I, 
 // LDS scratch of cols2s per atom: IS x R x K <= (2 x 256 threads / K) x 3 x K values
 constexpr int kColsRed = 2 * 256 * 3;
 
+// the split form when the launch could give the workgroup its `red` scratch (LDS budget), else cols2
+template <bool SPLIT, typename T, int NT, int R, bool VEC>
+__device__ __forceinline__ void colsx(const T* __restrict__ A, int lda, int I, const T* g, int ldg,
+                                      const T* __restrict__ B, int ldb, int I2, const T* g2, int ldg2, int K,
+                                      T* out, int ldo, int P, int nt, size_t gstride, bool global, T* red) {
+  if constexpr (SPLIT)
+    cols2s<T, NT, R, VEC>(A, lda, I, g, ldg, B, ldb, I2, g2, ldg2, K, out, ldo, P, nt, gstride, global, red);
+  else
+    cols2<T, NT, R, VEC>(A, lda, I, g, ldg, B, ldb, I2, g2, ldg2, K, out, ldo, P, nt, gstride, global);
+}
+
 // LDS layout of one atom (units of T); H = hidden, O = H/2 (block-1 output = block-2 input), Q = O.
 struct Layout {
   int v, h, vb, v2, u, s, o, v1, h2, vb2, v22, u2, s2, o2;      // forward
@@ -342,7 +353,7 @@ struct Layout {
 
 // y may be NULL; jx / jv receive d(seed * y)/d(x, vec) with seed = gy[n] (gy NULL: 1, i.e. the
 // Jacobian).  S: weight-gradient factors (weights mode), all NULL otherwise.
-template <typename T, int NT, bool VEC>
+template <typename T, int NT, bool VEC, bool SPLIT>
 __global__ __launch_bounds__(256) void k_eq_head(int n, int H, const T* __restrict__ x,
                                                  const T* __restrict__ vec, Weights<T> W,
                                                  T* __restrict__ y, T* __restrict__ jx,
@@ -427,7 +438,7 @@ __global__ __launch_bounds__(256) void k_eq_head(int n, int H, const T* __restri
 
   // ---------------- reverse pass for J = d y / d (x, vec), seed dy = 1 (vec'' enters y as 0 * sum)
   // block 2: g_h2 = P1^T g_u2
-  cols2s<T, NT, 1, VEC>(W.p1w, 2 * Q, Q, sm + L.gu2, 0, nullptr, 0, 0, nullptr, 0, 2 * Q, sm + L.gh2, 0, P, nt, 0,
+  colsx<SPLIT, T, NT, 1, VEC>(W.p1w, 2 * Q, Q, sm + L.gu2, 0, nullptr, 0, 0, nullptr, 0, 2 * Q, sm + L.gh2, 0, P, nt, 0,
                   false, red);
   __syncthreads();
   for (int i = tid; i < NT * Q; i += bs) {
@@ -440,7 +451,7 @@ __global__ __launch_bounds__(256) void k_eq_head(int n, int H, const T* __restri
   }
   __syncthreads();
   // g_v1 = V1^T g_vb2 (the vec'' gate contributes nothing: its cotangent is 0)
-  cols2s<T, NT, 3, VEC>(W.v1, O, Q, sm + L.gvb2, Q, nullptr, 0, 0, nullptr, 0, O, sm + L.gv1, O, P, nt, 0, false, red);
+  colsx<SPLIT, T, NT, 3, VEC>(W.v1, O, Q, sm + L.gvb2, Q, nullptr, 0, 0, nullptr, 0, O, sm + L.gv1, O, P, nt, 0, false, red);
   __syncthreads();
   // block 1 gate: g_xo = g_x1 SiLU'(xo), g_vo = sum_a g_v1 v2, g_v2 = g_v1 vo
   for (int i = tid; i < NT * O; i += bs) {
@@ -460,7 +471,7 @@ __global__ __launch_bounds__(256) void k_eq_head(int n, int H, const T* __restri
   }
   __syncthreads();
   // g_s = U2^T g_o, g_u = g_s SiLU'(u)
-  cols2s<T, NT, 1, VEC>(W.u2w, H, 2 * O, sm + L.go, 0, nullptr, 0, 0, nullptr, 0, H, sm + L.gu, 0, P, nt, 0, false, red);
+  colsx<SPLIT, T, NT, 1, VEC>(W.u2w, H, 2 * O, sm + L.go, 0, nullptr, 0, 0, nullptr, 0, H, sm + L.gu, 0, P, nt, 0, false, red);
   __syncthreads();
   for (int i = tid; i < NT * H; i += bs) {
     const int t = i / H, c = i - t * H;
@@ -471,9 +482,9 @@ __global__ __launch_bounds__(256) void k_eq_head(int n, int H, const T* __restri
   }
   __syncthreads();
   // g_h = U1^T g_u (U1 is [H][2H]): the x half is J_x (global), the vec1 half stays in LDS
-  cols2s<T, NT, 1, VEC>(W.u1w, 2 * H, H, sm + L.gu, 0, nullptr, 0, 0, nullptr, 0, H, jx + (size_t)n0 * H, 0, P, nt,
+  colsx<SPLIT, T, NT, 1, VEC>(W.u1w, 2 * H, H, sm + L.gu, 0, nullptr, 0, 0, nullptr, 0, H, jx + (size_t)n0 * H, 0, P, nt,
                   (size_t)H, true, red);
-  cols2s<T, NT, 1, VEC>(W.u1w + H, 2 * H, H, sm + L.gu, 0, nullptr, 0, 0, nullptr, 0, H, sm + L.gvec1, 0, P, nt, 0,
+  colsx<SPLIT, T, NT, 1, VEC>(W.u1w + H, 2 * H, H, sm + L.gu, 0, nullptr, 0, 0, nullptr, 0, H, sm + L.gvec1, 0, P, nt, 0,
                   false, red);
   __syncthreads();
   for (int i = tid; i < NT * H; i += bs) {
@@ -486,7 +497,7 @@ __global__ __launch_bounds__(256) void k_eq_head(int n, int H, const T* __restri
   }
   __syncthreads();
   // J_vec[a] = W1^T g_vb[a] + W2^T g_v2[a]
-  cols2s<T, NT, 3, VEC>(W.w1, H, H, sm + L.gvb, H, W.w2, H, O, sm + L.gv2, O, H, jv + (size_t)n0 * 3 * H, H, P,
+  colsx<SPLIT, T, NT, 3, VEC>(W.w1, H, H, sm + L.gvb, H, W.w2, H, O, sm + L.gv2, O, H, jv + (size_t)n0 * 3 * H, H, P,
                   nt, (size_t)3 * H, true, red);
   if (S.a1 == nullptr) return;
   // weights mode: every LDS buffer is still intact (no aliasing); dump the per-atom factors
@@ -599,7 +610,7 @@ struct Saves2 {
   T* vv;
 };
 
-template <typename T, int NT, bool VEC>
+template <typename T, int NT, bool VEC, bool SPLIT>
 __global__ __launch_bounds__(256) void k_eq_head_hvp(int n, int H, const T* __restrict__ x,
                                                      const T* __restrict__ vec, Weights<T> W,
                                                      const T* __restrict__ gy, const T* __restrict__ tx,
@@ -612,6 +623,7 @@ __global__ __launch_bounds__(256) void k_eq_head_hvp(int n, int H, const T* __re
   const int n0 = blockIdx.x * NT;
   const int nt = min(NT, n - n0);
   const int tid = threadIdx.x, bs = blockDim.x;
+  T* red = sm + NT * P;  // colsx scratch (SPLIT launches add NT x kColsRed values)
 
   // stage x -> h[0:H], vec -> v, t_x -> th[0:H], t_vec -> tv (absent atoms / tangents: zero)
   for (int i = tid; i < NT * 8 * H; i += bs) {
@@ -696,10 +708,10 @@ __global__ __launch_bounds__(256) void k_eq_head_hvp(int n, int H, const T* __re
   __syncthreads();
 
   // ---------------- reverse and its tangent (the transposed products shared in pairs)
-  cols2<T, NT, 1, VEC>(W.p1w, 2 * Q, Q, sm + L.gu2, 0, nullptr, 0, 0, nullptr, 0, 2 * Q, sm + L.gh2, 0, P, nt, 0,
-                       false);
-  cols2<T, NT, 1, VEC>(W.p1w, 2 * Q, Q, sm + L.tgu2, 0, nullptr, 0, 0, nullptr, 0, 2 * Q, sm + L.tgh2, 0, P, nt, 0,
-                       false);
+  colsx<SPLIT, T, NT, 1, VEC>(W.p1w, 2 * Q, Q, sm + L.gu2, 0, nullptr, 0, 0, nullptr, 0, 2 * Q, sm + L.gh2, 0, P, nt, 0,
+                       false, red);
+  colsx<SPLIT, T, NT, 1, VEC>(W.p1w, 2 * Q, Q, sm + L.tgu2, 0, nullptr, 0, 0, nullptr, 0, 2 * Q, sm + L.tgh2, 0, P, nt, 0,
+                       false, red);
   __syncthreads();
   for (int i = tid; i < NT * Q; i += bs) {
     const int t = i / Q, c = i - t * Q;
@@ -715,8 +727,8 @@ __global__ __launch_bounds__(256) void k_eq_head_hvp(int n, int H, const T* __re
     }
   }
   __syncthreads();
-  cols2<T, NT, 3, VEC>(W.v1, O, Q, sm + L.gvb2, Q, nullptr, 0, 0, nullptr, 0, O, sm + L.gv1, O, P, nt, 0, false);
-  cols2<T, NT, 3, VEC>(W.v1, O, Q, sm + L.tgvb2, Q, nullptr, 0, 0, nullptr, 0, O, sm + L.tgv1, O, P, nt, 0, false);
+  colsx<SPLIT, T, NT, 3, VEC>(W.v1, O, Q, sm + L.gvb2, Q, nullptr, 0, 0, nullptr, 0, O, sm + L.gv1, O, P, nt, 0, false, red);
+  colsx<SPLIT, T, NT, 3, VEC>(W.v1, O, Q, sm + L.tgvb2, Q, nullptr, 0, 0, nullptr, 0, O, sm + L.tgv1, O, P, nt, 0, false, red);
   __syncthreads();
   for (int i = tid; i < NT * O; i += bs) {
     const int t = i / O, c = i - t * O;
@@ -740,8 +752,8 @@ __global__ __launch_bounds__(256) void k_eq_head_hvp(int n, int H, const T* __re
     a[L.tgo + O + c] = tgvo;
   }
   __syncthreads();
-  cols2<T, NT, 1, VEC>(W.u2w, H, 2 * O, sm + L.go, 0, nullptr, 0, 0, nullptr, 0, H, sm + L.gs, 0, P, nt, 0, false);
-  cols2<T, NT, 1, VEC>(W.u2w, H, 2 * O, sm + L.tgo, 0, nullptr, 0, 0, nullptr, 0, H, sm + L.tgs, 0, P, nt, 0, false);
+  colsx<SPLIT, T, NT, 1, VEC>(W.u2w, H, 2 * O, sm + L.go, 0, nullptr, 0, 0, nullptr, 0, H, sm + L.gs, 0, P, nt, 0, false, red);
+  colsx<SPLIT, T, NT, 1, VEC>(W.u2w, H, 2 * O, sm + L.tgo, 0, nullptr, 0, 0, nullptr, 0, H, sm + L.tgs, 0, P, nt, 0, false, red);
   __syncthreads();
   for (int i = tid; i < NT * H; i += bs) {
     const int t = i / H, c = i - t * H;
@@ -753,12 +765,12 @@ __global__ __launch_bounds__(256) void k_eq_head_hvp(int n, int H, const T* __re
   }
   __syncthreads();
   // U1^T: the x half of the tangent is d_x (global); the vec1 halves stay in LDS
-  cols2<T, NT, 1, VEC>(W.u1w, 2 * H, H, sm + L.tgu, 0, nullptr, 0, 0, nullptr, 0, H, dx + (size_t)n0 * H, 0, P, nt,
-                       (size_t)H, true);
-  cols2<T, NT, 1, VEC>(W.u1w + H, 2 * H, H, sm + L.gu, 0, nullptr, 0, 0, nullptr, 0, H, sm + L.gvec1, 0, P, nt, 0,
-                       false);
-  cols2<T, NT, 1, VEC>(W.u1w + H, 2 * H, H, sm + L.tgu, 0, nullptr, 0, 0, nullptr, 0, H, sm + L.tgvec1, 0, P, nt, 0,
-                       false);
+  colsx<SPLIT, T, NT, 1, VEC>(W.u1w, 2 * H, H, sm + L.tgu, 0, nullptr, 0, 0, nullptr, 0, H, dx + (size_t)n0 * H, 0, P, nt,
+                       (size_t)H, true, red);
+  colsx<SPLIT, T, NT, 1, VEC>(W.u1w + H, 2 * H, H, sm + L.gu, 0, nullptr, 0, 0, nullptr, 0, H, sm + L.gvec1, 0, P, nt, 0,
+                       false, red);
+  colsx<SPLIT, T, NT, 1, VEC>(W.u1w + H, 2 * H, H, sm + L.tgu, 0, nullptr, 0, 0, nullptr, 0, H, sm + L.tgvec1, 0, P, nt, 0,
+                       false, red);
   __syncthreads();
   for (int i = tid; i < NT * H; i += bs) {
     const int t = i / H, c = i - t * H;
@@ -775,8 +787,8 @@ __global__ __launch_bounds__(256) void k_eq_head_hvp(int n, int H, const T* __re
   }
   __syncthreads();
   // d_vec[a] = W1^T gdot_vb[a] + W2^T gdot_v2[a]
-  cols2<T, NT, 3, VEC>(W.w1, H, H, sm + L.tgvb, H, W.w2, H, O, sm + L.tgv2, O, H, dvec + (size_t)n0 * 3 * H, H, P,
-                       nt, (size_t)3 * H, true);
+  colsx<SPLIT, T, NT, 3, VEC>(W.w1, H, H, sm + L.tgvb, H, W.w2, H, O, sm + L.tgv2, O, H, dvec + (size_t)n0 * 3 * H, H, P,
+                       nt, (size_t)3 * H, true, red);
   // d_g_y = ydot = P2[0][:] . s2dot
   if (dgy && tid < nt) {
     const T* a = sm + tid * P;
@@ -870,15 +882,18 @@ using namespace tmd;
 // Atoms per workgroup: the kernel is latency-bound (~20 dependent product phases), so small systems
 // want many workgroups (1 atom each); from ~2k atoms 2 atoms share each weight load (measured on
 // MI355X: 56 us at 580 atoms with 1, 41 ns/atom at 50k atoms with 2; 4 is slower at every size).
-static int head_tile(int dtype, int H, int n, size_t* smem) {
+static int head_tile(int dtype, int H, int n, size_t* smem, bool* split) {
   const size_t es = dtype == TMDNET_F64 ? 8 : 4;
-  const size_t per = ((size_t)head::Layout(H).P + head::kColsRed) * es;  // + the cols2s scratch
+  const size_t per = (size_t)head::Layout(H).P * es;
   int cap = n < 2048 ? 1 : 2;
   static const int env_nt = [] { const char* e = getenv("TMDNET_HEAD_NT"); return e ? atoi(e) : 0; }();  // tuning, read once
   if (env_nt > 0) cap = env_nt >= 4 ? 4 : env_nt >= 2 ? 2 : 1;
   for (int nt = cap; nt >= 1; nt /= 2)
     if (nt * per <= 64 * 1024) {
-      *smem = nt * per;
+      // the split transposed products (cols2s) when their scratch fits the same 64 KB
+      const size_t with = nt * (per + (size_t)head::kColsRed * es);
+      *split = with <= 64 * 1024;
+      *smem = *split ? with : nt * per;
       return nt;
     }
   return 0;
@@ -886,7 +901,7 @@ static int head_tile(int dtype, int H, int n, size_t* smem) {
 
 template <typename T>
 static int launch_head(int n, int H, const void* x, const void* vec, const void* const* w, void* y,
-                       void* jx, void* jv, const void* gy, void* const* sv, int nt, size_t smem,
+                       void* jx, void* jv, const void* gy, void* const* sv, int nt, size_t smem, bool split,
                        hipStream_t st) {
   head::Saves<T> S{};
   if (sv)
@@ -897,9 +912,13 @@ static int launch_head(int n, int H, const void* x, const void* vec, const void*
                      (const T*)w[8], (const T*)w[9], (const T*)w[10], (const T*)w[11]};
   dim3 g((n + nt - 1) / nt), b(256);
   const bool vec4 = H % 8 == 0;  // every LDS offset / row length a multiple of 4
-#define TMD_HEAD_LAUNCH(NT_, V_)                                                                     \
-  hipLaunchKernelGGL((head::k_eq_head<T, NT_, V_>), g, b, smem, st, n, H, (const T*)x, (const T*)vec, W, \
-                     (T*)y, (T*)jx, (T*)jv, (const T*)gy, S)
+#define TMD_HEAD_LAUNCH(NT_, V_)                                                                          \
+  if (split)                                                                                             \
+    hipLaunchKernelGGL((head::k_eq_head<T, NT_, V_, true>), g, b, smem, st, n, H, (const T*)x, (const T*)vec, \
+                       W, (T*)y, (T*)jx, (T*)jv, (const T*)gy, S);                                         \
+  else                                                                                                   \
+    hipLaunchKernelGGL((head::k_eq_head<T, NT_, V_, false>), g, b, smem, st, n, H, (const T*)x, (const T*)vec, \
+                       W, (T*)y, (T*)jx, (T*)jv, (const T*)gy, S)
   if (vec4) {
     if (nt == 4) TMD_HEAD_LAUNCH(4, true);
     else if (nt == 2) TMD_HEAD_LAUNCH(2, true);
@@ -922,13 +941,14 @@ extern "C" int tmdnet_eq_head_fwd(int dtype, int n_atoms, int hidden, const void
     if (!weights[i]) return kBadArgument;
   if (n_atoms == 0) return kOk;
   size_t smem = 0;
-  const int nt = head_tile(dtype, hidden, n_atoms, &smem);
+  bool split = false;
+  const int nt = head_tile(dtype, hidden, n_atoms, &smem, &split);
   if (nt == 0) return kUnsupported;
   hipStream_t st = (hipStream_t)stream;
   if (dtype == TMDNET_F32)
-    return launch_head<float>(n_atoms, hidden, x, vec, weights, y, jac_x, jac_vec, nullptr, nullptr, nt, smem, st);
+    return launch_head<float>(n_atoms, hidden, x, vec, weights, y, jac_x, jac_vec, nullptr, nullptr, nt, smem, split, st);
   if (dtype == TMDNET_F64)
-    return launch_head<double>(n_atoms, hidden, x, vec, weights, y, jac_x, jac_vec, nullptr, nullptr, nt, smem, st);
+    return launch_head<double>(n_atoms, hidden, x, vec, weights, y, jac_x, jac_vec, nullptr, nullptr, nt, smem, split, st);
   return kUnsupported;
 }
 
@@ -945,15 +965,16 @@ extern "C" int tmdnet_eq_head_bwd_weights(int dtype, int n_atoms, int hidden, co
     if (!saves[i]) return kBadArgument;
   if (n_atoms == 0) return kOk;
   size_t smem = 0;
-  const int nt = head_tile(dtype, hidden, n_atoms, &smem);
+  bool split = false;
+  const int nt = head_tile(dtype, hidden, n_atoms, &smem, &split);
   if (nt == 0) return kUnsupported;
   hipStream_t st = (hipStream_t)stream;
   if (dtype == TMDNET_F32)
     return launch_head<float>(n_atoms, hidden, x, vec, weights, nullptr, grad_x, grad_vec, grad_y, saves, nt,
-                              smem, st);
+                              smem, split, st);
   if (dtype == TMDNET_F64)
     return launch_head<double>(n_atoms, hidden, x, vec, weights, nullptr, grad_x, grad_vec, grad_y, saves, nt,
-                               smem, st);
+                               smem, split, st);
   return kUnsupported;
 }
 
@@ -973,12 +994,18 @@ static int launch_head_hvp(int n, int H, const void* x, const void* vec, const v
   // one atom per workgroup below 2048 atoms (latency-bound chain), two above when they fit 64 KB
   const int nt = (n >= 2048 && 2 * per <= 64 * 1024) ? 2 : 1;
   if (per > 64 * 1024) return kUnsupported;
-  const size_t smem = nt * per;
+  const size_t with = nt * (per + (size_t)head::kColsRed * sizeof(T));  // + the split products' scratch
+  const bool split = with <= 64 * 1024;
+  const size_t smem = split ? with : nt * per;
   dim3 g((n + nt - 1) / nt), b(256);
   const bool vec4 = H % 8 == 0;
-#define TMD_HVP_LAUNCH(NT_, V_)                                                                            \
-  hipLaunchKernelGGL((head::k_eq_head_hvp<T, NT_, V_>), g, b, smem, st, n, H, (const T*)x, (const T*)vec, W, \
-                     (const T*)gy, (const T*)tx, (const T*)tvec, (T*)dx, (T*)dvec, (T*)dgy, S)
+#define TMD_HVP_LAUNCH(NT_, V_)                                                                              \
+  if (split)                                                                                                \
+    hipLaunchKernelGGL((head::k_eq_head_hvp<T, NT_, V_, true>), g, b, smem, st, n, H, (const T*)x, (const T*)vec, \
+                       W, (const T*)gy, (const T*)tx, (const T*)tvec, (T*)dx, (T*)dvec, (T*)dgy, S);            \
+  else                                                                                                      \
+    hipLaunchKernelGGL((head::k_eq_head_hvp<T, NT_, V_, false>), g, b, smem, st, n, H, (const T*)x,           \
+                       (const T*)vec, W, (const T*)gy, (const T*)tx, (const T*)tvec, (T*)dx, (T*)dvec, (T*)dgy, S)
   if (vec4) {
     if (nt == 2) TMD_HVP_LAUNCH(2, true);
     else TMD_HVP_LAUNCH(1, true);

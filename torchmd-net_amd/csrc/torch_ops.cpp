@@ -1297,8 +1297,8 @@ variable_list stack_backward_dr(const StackActs& A, Tensor gX, Tensor gV, const 
     Tensor g_vec_in = hv ? at::empty({N, 3, H}, o) : Tensor();
     Tensor g_qkv = at::empty({N, 5 * H}, o);
     Tensor dpk, dpv, pk, pv;
-    Tensor pkv = A.batched ? A.pkv_all.narrow(1, l * D, D) : A.pkv_all;
-    if (has_e) {
+    if (has_e) {  // (distance_influence "none": no projection rows at all)
+      Tensor pkv = A.batched ? A.pkv_all.narrow(1, l * D, D) : A.pkv_all;
       Tensor dpkv = A.batched ? dpkv_all.narrow(1, l * D, D) : Tensor();
       if (!A.batched) {
         dpkv = at::empty({E, D}, o);
