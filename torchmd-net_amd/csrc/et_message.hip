@@ -812,20 +812,12 @@ __device__ __forceinline__ void bwd_merged_body(const Args<T>& A, int blk, int n
       ldv<T, V>(h0, gvs);
       ldv<T, V>(h1, gvs + A.H);
       ldv<T, V>(h2, gvs + 2 * A.H);
-      // d(dk,dv)/dr of the pair row: read by ONE endpoint of the pair (the larger index, s <= t),
-      // which contracts it with the projection gradients of BOTH directions (it holds both roles'
-      // operands); g_r of the pair lands on that endpoint's edge (the position gradient only sees
-      // g_r[e] + g_r[rev(e)]: r is one function of the pair).  Half the d(dk,dv)/dr stream.
-      const bool own = s <= t;
       T dpk_[V], dpx_[V], dp1_[V], dp2_[V];
-      zero(dpk_); zero(dpx_); zero(dp1_); zero(dp2_);
-      if (own) {
-        ldv<T, V>(dpk_, opt(A.dpk, (size_t)st.row * A.ldpk + c0, dummy + c0));
-        const T* dps = opt(A.dpv, (size_t)st.row * A.ldpv + vo, dummy);
-        ldv<T, V>(dpx_, dps);
-        ldv<T, V>(dp1_, dps + pvd);
-        ldv<T, V>(dp2_, dps + 2 * pvd);
-      }
+      ldv<T, V>(dpk_, opt(A.dpk, (size_t)st.row * A.ldpk + c0, dummy + c0));
+      const T* dps = opt(A.dpv, (size_t)st.row * A.ldpv + vo, dummy);
+      ldv<T, V>(dpx_, dps);
+      ldv<T, V>(dp1_, dps + pvd);
+      ldv<T, V>(dp2_, dps + 2 * pvd);
       pre();
       if (!hw) { zero(w0); zero(w1); zero(w2); }
       T dk[V], ddk[V], dvx[V], dv1[V], dv2[V], ddx[V], dd1[V], dd2[V];
@@ -833,7 +825,6 @@ __device__ __forceinline__ void bwd_merged_body(const Args<T>& A, int blk, int n
       act<T, V>(st.x, hv, dvx, ddx, A.act_kv);
       act<T, V>(st.a, hv, dv1, dd1, A.act_kv);
       act<T, V>(st.b, hv, dv2, dd2, A.act_kv);
-      T grr = T(0);  // <g_pre, d pre/dr> of this edge (own) and of its reverse (own, s != t)
       // ---- destination role: e = (t <- s), the node's q / gx / gvec from LDS
       {
         T q[V], gx[V], g0[V], g1[V], g2[V];
@@ -857,6 +848,7 @@ __device__ __forceinline__ void bwd_merged_body(const Args<T>& A, int blk, int n
         const ActF<T> sa(part, A.act_at);
         const T a = sa.s * Ce;
         const T gs = ga * Ce * sa.d(part);
+        T grr = T(0);
 #pragma unroll
         for (int i = 0; i < V; ++i) {
           gq[i] += gs * kk[i] * dk[i];
@@ -870,20 +862,21 @@ __device__ __forceinline__ void bwd_merged_body(const Args<T>& A, int blk, int n
         gu0 = group_sum(gu0, A.L);
         gu1 = group_sum(gu1, A.L);
         gu2 = group_sum(gu2, A.L);
+        grr = group_sum(grr, A.L);
         if (G.el == 0) {
           A.gC[k] = oc + gc;
           A.gu[3 * k] = ou0 + gu0;
           A.gu[3 * k + 1] = ou1 + gu1;
           A.gu[3 * k + 2] = ou2 + gu2;
+          A.gr[k] = orr + grr;
         }
       }
       // ---- source role: the reverse edge s <- t (unit vector negated), the node's k / v / vec from LDS
       {
-        T kt[V], vxt[V], v1t[V], v2t[V], w0t[V], w1t[V], w2t[V];
+        T kt[V], vxt[V], v1t[V], w0t[V], w1t[V], w2t[V];
         ldv<T, V>(kt, nv + 5 * HM + c0);
         ldv<T, V>(vxt, nv + 6 * HM + c0);
         ldv<T, V>(v1t, nv + 7 * HM + c0);
-        ldv<T, V>(v2t, nv + 8 * HM + c0);
         ldv<T, V>(w0t, nv + 9 * HM + c0);
         ldv<T, V>(w1t, nv + 10 * HM + c0);
         ldv<T, V>(w2t, nv + 11 * HM + c0);
@@ -898,28 +891,18 @@ __device__ __forceinline__ void bwd_merged_body(const Args<T>& A, int blk, int n
         const ActF<T> sa(part, A.act_at);
         const T a = sa.s * Ce;
         const T gs = ga * Ce * sa.d(part);
-        const bool rev = s < t;  // the reverse edge's d/dr term is this wave's (see `own`)
 #pragma unroll
         for (int i = 0; i < V; ++i) {
           gk[i] += gs * qs[i] * dk[i];
           gvx[i] += gxs[i] * a * dvx[i];
-          const T g1e = h0[i] * w0t[i] + h1[i] * w1t[i] + h2[i] * w2t[i];
-          const T g2e = h0[i] * u0 + h1[i] * u1 + h2[i] * u2;  // (unit vector of s <- t is -u)
-          gv1[i] += g1e * dv1[i];
-          gv2[i] -= g2e * dv2[i];
+          gv1[i] += (h0[i] * w0t[i] + h1[i] * w1t[i] + h2[i] * w2t[i]) * dv1[i];
+          gv2[i] -= (h0[i] * u0 + h1[i] * u1 + h2[i] * u2) * dv2[i];
           const T v1e = v1t[i] * dv1[i];
           gw0[i] += h0[i] * v1e;
           gw1[i] += h1[i] * v1e;
           gw2[i] += h2[i] * v1e;
-          if (rev)  // projection gradient of the reverse edge s <- t, contracted with the pair's d pre/dr
-            grr += (hk ? gs * qs[i] * kt[i] * ddk[i] * dpk_[i] : T(0)) +
-                   (hv ? gxs[i] * a * vxt[i] * ddx[i] * dpx_[i] + g1e * v1t[i] * dd1[i] * dp1_[i] -
-                             g2e * v2t[i] * dd2[i] * dp2_[i]
-                       : T(0));
         }
       }
-      grr = group_sum(grr, A.L);
-      if (G.el == 0) A.gr[k] = orr + grr;
     };
     if constexpr (PD == 1) {
       edge_chunks_pf<T, S, 1, St>(A, b, e, EPW, G, ld, body);
