@@ -8,4 +8,4 @@ bash tools/prof_train.sh r03 > /dev/null
 head -3 gpurun_out/r03_train_step_kernels.txt
 TMDNET_BENCH_REHEARSAL=1 timeout -k 10 400 python -u bench.py --gpus 2 --steps 20 --warmup 5 --no-cpu-baseline \
   --no-pmc > gpurun_out/r03_bench_rehearsal_2ranks.json 2> gpurun_out/r03_bench_rehearsal.err
-python -c "import json;d=json.load(open('gpurun_out/r03_bench_rehearsal_2ranks.json'));print(d['n_gpus'],d['value'],d['ms_per_step'],d.get('ddp_train',{}).get('ms_per_step'))"
+python -c "import json;d=json.loads(open('gpurun_out/r03_bench_rehearsal_2ranks.json').read().strip().splitlines()[-1]);print(d['n_gpus'],d['value'],d['ms_per_step'],d.get('ddp_train',{}).get('ms_per_step'))"
