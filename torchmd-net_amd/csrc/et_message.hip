@@ -304,8 +304,9 @@ __device__ __forceinline__ void edge_chunks(const Args<T>& A, int b, int e, int 
 // ------------------------------------------------------------------ forward
 // ORD: nodes visited in the caller's `order` (cell order for large periodic systems, so the waves in
 // flight gather from a compact spatial window of source rows).
-template <typename T, int V, int S, int CS, bool ORD>
+template <typename T, int V, int S, int CS, bool ORD, bool GA = true>
 __global__ __launch_bounds__(256) void k_fwd(Args<T> A) {
+  const int AKV = GA ? A.act_kv : kActSilu, AAT = GA ? A.act_at : kActSilu;  // GA: runtime codes
   __shared__ T lds[S > 1 ? 4 * 64 * 4 * V : 1];
   const Geo G = geo<S, CS, ORD>(A.n, A.L, A.order, A.xcd, blockIdx.x, gridDim.x);
   const int t = G.node;
@@ -348,15 +349,15 @@ __global__ __launch_bounds__(256) void k_fwd(Args<T> A) {
       pre();
       if (!hw) { zero(w0); zero(w1); zero(w2); }
       T dk[V], dvx[V], dv1[V], dv2[V], dd[V];
-      act<T, V>(st.k, hk, dk, dd, A.act_kv);
-      act<T, V>(st.x, hv, dvx, dd, A.act_kv);
-      act<T, V>(st.a, hv, dv1, dd, A.act_kv);
-      act<T, V>(st.b, hv, dv2, dd, A.act_kv);
+      act<T, V>(st.k, hk, dk, dd, AKV);
+      act<T, V>(st.x, hv, dvx, dd, AKV);
+      act<T, V>(st.a, hv, dv1, dd, AKV);
+      act<T, V>(st.b, hv, dv2, dd, AKV);
       T part = T(0);
 #pragma unroll
       for (int i = 0; i < V; ++i) part += q[i] * kk[i] * dk[i];
       part = group_sum(part, A.lph);
-      const ActF<T> sa(part, A.act_at);
+      const ActF<T> sa(part, AAT);
       const T a = sa.s * Ce;
 #pragma unroll
       for (int i = 0; i < V; ++i) {
@@ -414,8 +415,9 @@ __device__ __forceinline__ void zero_pad_rows(const Args<T>& A, int blk, int nwg
 
 // AG: TMDNET_ACC_GRADS in the training form -- the injected per-edge projection cotangents are loaded
 // with the edge's other loads (not read back after the math: one memory round trip per edge fewer)
-template <typename T, int V, int S, int CS, bool DR, bool AG = false>
+template <typename T, int V, int S, int CS, bool DR, bool AG = false, bool GA = true>
 __device__ __forceinline__ void bwd_dst_body(const Args<T>& A, int blk, int nwg) {
+  const int AKV = GA ? A.act_kv : kActSilu, AAT = GA ? A.act_at : kActSilu;  // GA: runtime codes
   __shared__ T lds[S > 1 ? 4 * 64 * V : 1];
   const Geo G = geo<S, CS, false>(A.n, A.L, nullptr, A.xcd, blk, nwg);
   const int t = G.node;
@@ -496,10 +498,10 @@ __device__ __forceinline__ void bwd_dst_body(const Args<T>& A, int blk, int nwg)
       const T (&p1)[V] = st.a;
       const T (&p2)[V] = st.b;
       T dk[V], ddk[V], dvx[V], dv1[V], dv2[V], ddx[V], dd1[V], dd2[V];
-      act<T, V>(pk, hk, dk, ddk, A.act_kv);
-      act<T, V>(px, hv, dvx, ddx, A.act_kv);
-      act<T, V>(p1, hv, dv1, dd1, A.act_kv);
-      act<T, V>(p2, hv, dv2, dd2, A.act_kv);
+      act<T, V>(pk, hk, dk, ddk, AKV);
+      act<T, V>(px, hv, dvx, ddx, AKV);
+      act<T, V>(p1, hv, dv1, dd1, AKV);
+      act<T, V>(p2, hv, dv2, dd2, AKV);
       T part = T(0), ga = T(0), gu0 = T(0), gu1 = T(0), gu2 = T(0);
 #pragma unroll
       for (int i = 0; i < V; ++i) {
@@ -512,7 +514,7 @@ __device__ __forceinline__ void bwd_dst_body(const Args<T>& A, int blk, int nwg)
       }
       part = group_sum(part, A.lph);
       ga = group_sum(ga, A.lph);
-      const ActF<T> sa(part, A.act_at);
+      const ActF<T> sa(part, AAT);
       const T a = sa.s * Ce;
       const T gs = ga * Ce * sa.d(part);
       T gpk[V], gpx[V], gp1[V], gp2[V];
@@ -582,8 +584,9 @@ __device__ __forceinline__ void bwd_dst_body(const Args<T>& A, int blk, int nwg)
 // ------------------------------------------------------------------ backward, source pass
 // A wave group owns node j as SOURCE.  Row j lists edges m->j; each is read as its reverse j->m
 // (same dk/dv/cutoff, unit vector negated), m being the destination whose q/gx/gvec are gathered.
-template <typename T, int V, int S, int CS>
+template <typename T, int V, int S, int CS, bool GA = true>
 __device__ __forceinline__ void bwd_src_body(const Args<T>& A, int blk, int nwg) {
+  const int AKV = GA ? A.act_kv : kActSilu, AAT = GA ? A.act_at : kActSilu;  // GA: runtime codes
   __shared__ T lds[S > 1 ? 4 * 64 * 7 * V : 1];
   const Geo G = geo<S, CS, false>(A.n, A.L, nullptr, A.xcd, blk, nwg);
   const int j = G.node;
@@ -638,10 +641,10 @@ __device__ __forceinline__ void bwd_src_body(const Args<T>& A, int blk, int nwg)
       const T (&p1)[V] = st.a;
       const T (&p2)[V] = st.b;
       T dk[V], ddk[V], dvx[V], dv1[V], dv2[V], dd[V];
-      act<T, V>(pk, hk, dk, ddk, A.act_kv);
-      act<T, V>(px, hv, dvx, dd, A.act_kv);
-      act<T, V>(p1, hv, dv1, dd, A.act_kv);
-      act<T, V>(p2, hv, dv2, dd, A.act_kv);
+      act<T, V>(pk, hk, dk, ddk, AKV);
+      act<T, V>(px, hv, dvx, dd, AKV);
+      act<T, V>(p1, hv, dv1, dd, AKV);
+      act<T, V>(p2, hv, dv2, dd, AKV);
       T part = T(0), ga = T(0);
 #pragma unroll
       for (int i = 0; i < V; ++i) {
@@ -650,7 +653,7 @@ __device__ __forceinline__ void bwd_src_body(const Args<T>& A, int blk, int nwg)
       }
       part = group_sum(part, A.lph);
       ga = group_sum(ga, A.lph);
-      const ActF<T> sa(part, A.act_at);
+      const ActF<T> sa(part, AAT);
       const T a = sa.s * Ce;
       const T gs = ga * Ce * sa.d(part);
 #pragma unroll
@@ -712,22 +715,22 @@ __device__ __forceinline__ void bwd_src_body(const Args<T>& A, int blk, int nwg)
 template <typename T, int V, bool DR>
 constexpr int bwd_min_waves() { return (DR && sizeof(T) == 4 && V <= 4) ? 3 : 1; }
 
-template <typename T, int V, int S, int CS, bool DR, bool AG = false>
+template <typename T, int V, int S, int CS, bool DR, bool AG = false, bool GA = true>
 __global__ __launch_bounds__(256, (bwd_min_waves<T, V, DR>())) void k_bwd_dst(Args<T> A) {
-  bwd_dst_body<T, V, S, CS, DR, AG>(A, blockIdx.x, gridDim.x);
+  bwd_dst_body<T, V, S, CS, DR, AG, GA>(A, blockIdx.x, gridDim.x);
 }
-template <typename T, int V, int S, int CS>
+template <typename T, int V, int S, int CS, bool GA = true>
 __global__ __launch_bounds__(256) void k_bwd_src(Args<T> A) {
-  bwd_src_body<T, V, S, CS>(A, blockIdx.x, gridDim.x);
+  bwd_src_body<T, V, S, CS, GA>(A, blockIdx.x, gridDim.x);
 }
 // Both passes in ONE grid (they only read the same inputs): blocks [0, split) run the destination
 // pass, [split, 2 split) the source pass.  Used for small systems, where one pass alone leaves most
 // of the chip idle and the launch gap between the two passes is a visible share of the layer.
-template <typename T, int V, int S, int CS, bool DR, bool AG = false>
+template <typename T, int V, int S, int CS, bool DR, bool AG = false, bool GA = true>
 __global__ __launch_bounds__(256, (bwd_min_waves<T, V, DR>())) void k_bwd_both(Args<T> A) {
   const int split = (int)gridDim.x / 2;
-  if ((int)blockIdx.x < split) bwd_dst_body<T, V, S, CS, DR, AG>(A, blockIdx.x, split);
-  else bwd_src_body<T, V, S, CS>(A, blockIdx.x - split, split);
+  if ((int)blockIdx.x < split) bwd_dst_body<T, V, S, CS, DR, AG, GA>(A, blockIdx.x, split);
+  else bwd_src_body<T, V, S, CS, GA>(A, blockIdx.x - split, split);
 }
 
 // ------------------------------------------------------------------ backward, merged pass (dr mode)
@@ -739,8 +742,9 @@ __global__ __launch_bounds__(256, (bwd_min_waves<T, V, DR>())) void k_bwd_both(A
 // gathers both of its source's row sets (k, v, vec for the destination role; q, gx, gvec for the
 // source role).  The node's own vectors (q, gx, gvec | k, v, vec) are staged in LDS once per node
 // and re-read per edge (48 fewer VGPRs than holding them in registers).
-template <typename T, int V, int S, int PD>
+template <typename T, int V, int S, int PD, bool GA = true>
 __device__ __forceinline__ void bwd_merged_body(const Args<T>& A, int blk, int nwg) {
+  const int AKV = GA ? A.act_kv : kActSilu, AAT = GA ? A.act_at : kActSilu;  // GA: runtime codes
   constexpr int NA = 8 * V;            // accumulators summed over a node's S waves
   extern __shared__ __attribute__((aligned(16))) char dyn_lds[];  // max(4/S nodes x 12 H, reduction)
   T* lds = reinterpret_cast<T*>(dyn_lds);
@@ -821,10 +825,10 @@ __device__ __forceinline__ void bwd_merged_body(const Args<T>& A, int blk, int n
       pre();
       if (!hw) { zero(w0); zero(w1); zero(w2); }
       T dk[V], ddk[V], dvx[V], dv1[V], dv2[V], ddx[V], dd1[V], dd2[V];
-      act<T, V>(st.k, hk, dk, ddk, A.act_kv);
-      act<T, V>(st.x, hv, dvx, ddx, A.act_kv);
-      act<T, V>(st.a, hv, dv1, dd1, A.act_kv);
-      act<T, V>(st.b, hv, dv2, dd2, A.act_kv);
+      act<T, V>(st.k, hk, dk, ddk, AKV);
+      act<T, V>(st.x, hv, dvx, ddx, AKV);
+      act<T, V>(st.a, hv, dv1, dd1, AKV);
+      act<T, V>(st.b, hv, dv2, dd2, AKV);
       // ---- destination role: e = (t <- s), the node's q / gx / gvec from LDS
       {
         T q[V], gx[V], g0[V], g1[V], g2[V];
@@ -845,7 +849,7 @@ __device__ __forceinline__ void bwd_merged_body(const Args<T>& A, int blk, int n
         }
         part = group_sum(part, A.lph);
         ga = group_sum(ga, A.lph);
-        const ActF<T> sa(part, A.act_at);
+        const ActF<T> sa(part, AAT);
         const T a = sa.s * Ce;
         const T gs = ga * Ce * sa.d(part);
         T grr = T(0);
@@ -888,7 +892,7 @@ __device__ __forceinline__ void bwd_merged_body(const Args<T>& A, int blk, int n
         }
         part = group_sum(part, A.lph);
         ga = group_sum(ga, A.lph);
-        const ActF<T> sa(part, A.act_at);
+        const ActF<T> sa(part, AAT);
         const T a = sa.s * Ce;
         const T gs = ga * Ce * sa.d(part);
 #pragma unroll
@@ -956,9 +960,9 @@ __device__ __forceinline__ void bwd_merged_body(const Args<T>& A, int blk, int n
   zero_pad_rows(A, blk, nwg);
 }
 
-template <typename T, int V, int S, int PD>
+template <typename T, int V, int S, int PD, bool GA = true>
 __global__ __launch_bounds__(256, 2) void k_bwd_merged(Args<T> A) {
-  bwd_merged_body<T, V, S, PD>(A, blockIdx.x, gridDim.x);
+  bwd_merged_body<T, V, S, PD, GA>(A, blockIdx.x, gridDim.x);
 }
 
 // ------------------------------------------------------------------ second-order backward
@@ -1573,6 +1577,9 @@ static inline int et_waves_per_node(int n, int bytes_per_lane_vec) {
   return 1;
 }
 
+template <typename T, int V, int S, int KIND, bool ORD, bool GA>
+static int et_launch_k(const Args<T>& A, dim3 g, dim3 b, int nbn, hipStream_t st);
+
 template <typename T, int V, int S, int KIND, bool ORD>
 static int et_launch_vs(Args<T> A, hipStream_t st) {
   // channel groups: split heads across XCDs for large systems (L2 working-set), not for the
@@ -1588,21 +1595,31 @@ static int et_launch_vs(Args<T> A, hipStream_t st) {
   if (A.L > 64 || (A.L & (A.L - 1))) return kUnsupported;
   const int nbn = (A.n + (4 / S) - 1) / (4 / S);
   const dim3 g(nbn * cs), b(256);
-  if (KIND == 0) hipLaunchKernelGGL((k_fwd<T, V, S, 1, ORD>), g, b, 0, st, A);
-  else if (KIND == 1) hipLaunchKernelGGL((k_bwd_dst<T, V, S, 1, false>), g, b, 0, st, A);
-  else if (KIND == 2) hipLaunchKernelGGL((k_bwd_src<T, V, S, 1>), g, b, 0, st, A);
-  else if (KIND == 3) hipLaunchKernelGGL((k_bwd_both<T, V, S, 1, false>), dim3(2 * nbn), b, 0, st, A);
-  else if (KIND == 4) hipLaunchKernelGGL((k_bwd_dst<T, V, S, 1, true>), g, b, 0, st, A);
-  else if (KIND == 5) hipLaunchKernelGGL((k_bwd_both<T, V, S, 1, true>), dim3(2 * nbn), b, 0, st, A);
-  else if (KIND == 6) hipLaunchKernelGGL((k_bwd_both<T, V, S, 1, false, true>), dim3(2 * nbn), b, 0, st, A);
+  // SiLU / SiLU (the configs' activations) runs kernels with the codes as compile-time constants: the
+  // runtime-code form splits every per-edge activation into its own basic block (C2: k_bwd_both
+  // 226 -> 264 us, k_fwd 83 -> 90 us per step when it was the only form)
+  if (A.act_kv == kActSilu && A.act_at == kActSilu)
+    return et_launch_k<T, V, S, KIND, ORD, false>(A, g, b, nbn, st);
+  return et_launch_k<T, V, S, KIND, ORD, true>(A, g, b, nbn, st);
+}
+
+template <typename T, int V, int S, int KIND, bool ORD, bool GA>
+static int et_launch_k(const Args<T>& A, dim3 g, dim3 b, int nbn, hipStream_t st) {
+  if (KIND == 0) hipLaunchKernelGGL((k_fwd<T, V, S, 1, ORD, GA>), g, b, 0, st, A);
+  else if (KIND == 1) hipLaunchKernelGGL((k_bwd_dst<T, V, S, 1, false, false, GA>), g, b, 0, st, A);
+  else if (KIND == 2) hipLaunchKernelGGL((k_bwd_src<T, V, S, 1, GA>), g, b, 0, st, A);
+  else if (KIND == 3) hipLaunchKernelGGL((k_bwd_both<T, V, S, 1, false, false, GA>), dim3(2 * nbn), b, 0, st, A);
+  else if (KIND == 4) hipLaunchKernelGGL((k_bwd_dst<T, V, S, 1, true, false, GA>), g, b, 0, st, A);
+  else if (KIND == 5) hipLaunchKernelGGL((k_bwd_both<T, V, S, 1, true, false, GA>), dim3(2 * nbn), b, 0, st, A);
+  else if (KIND == 6) hipLaunchKernelGGL((k_bwd_both<T, V, S, 1, false, true, GA>), dim3(2 * nbn), b, 0, st, A);
   else if (KIND == 8 || KIND == 9) {
     // dynamic LDS: the node vectors of the block's 4 / S nodes, or the cross-wave reduction
     const size_t node = (size_t)(4 / S) * 12 * A.H, red = S > 1 ? 4 * 64 * 8 * V : 1;
     const size_t bytes = (node > red ? node : red) * sizeof(T);
-    if (KIND == 8) hipLaunchKernelGGL((k_bwd_merged<T, V, S, 1>), dim3(nbn), b, bytes, st, A);
-    else hipLaunchKernelGGL((k_bwd_merged<T, V, S, 0>), dim3(nbn), b, bytes, st, A);
+    if (KIND == 8) hipLaunchKernelGGL((k_bwd_merged<T, V, S, 1, GA>), dim3(nbn), b, bytes, st, A);
+    else hipLaunchKernelGGL((k_bwd_merged<T, V, S, 0, GA>), dim3(nbn), b, bytes, st, A);
   }
-  else hipLaunchKernelGGL((k_bwd_dst<T, V, S, 1, false, true>), g, b, 0, st, A);
+  else hipLaunchKernelGGL((k_bwd_dst<T, V, S, 1, false, true, GA>), g, b, 0, st, A);
   return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
 }
 
