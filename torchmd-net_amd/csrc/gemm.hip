@@ -103,17 +103,22 @@ __device__ __forceinline__ void slice(const Prob& P, int r0, int c0, int kb0, in
   }
 }
 
+// EX: the tmdnet_gemm_ex_f32 epilogue switches; plain tmdnet_gemm_f32 launches compile them out
+// (they cost the latency-bound node mixes ~5 % per launch when tested per element)
+template <bool EX>
 __device__ __forceinline__ void store(const Prob& P, int gr, int gc, float v) {
   if (gr >= P.M || gc >= P.N) return;
   if (P.bias) v += P.bias[gc];
   float* out = P.C + (size_t)gr * P.ldc + gc;
   if (P.beta) v += *out;
-  if (P.pre) P.pre[(size_t)gr * P.ldx + gc] = v;
-  if (P.act) v = Silu<float>(v).s;
-  if (P.rscale) v *= P.rscale[gr];
-  if (P.dpre) {
-    const float x = P.dpre[(size_t)gr * P.ldx + gc];
-    v *= Silu<float>(x).d(x);
+  if constexpr (EX) {
+    if (P.pre) P.pre[(size_t)gr * P.ldx + gc] = v;
+    if (P.act) v = Silu<float>(v).s;
+    if (P.rscale) v *= P.rscale[gr];
+    if (P.dpre) {
+      const float x = P.dpre[(size_t)gr * P.ldx + gc];
+      v *= Silu<float>(x).d(x);
+    }
   }
   *out = v;
 }
@@ -121,7 +126,7 @@ __device__ __forceinline__ void store(const Prob& P, int gr, int gc, float v) {
 // NW waves per 32 x 32 tile, K split NW ways; KMAX = the load batch (K blocks) the launch's longest
 // per-wave slice needs: the register file is sized for the largest batch the kernel can issue, so a
 // K = 128 mix (2 blocks per wave) compiled with an 8-block batch ran at 160 VGPRs = 2 waves per SIMD
-template <int NW, int KMAX>
+template <int NW, int KMAX, bool EX = true>
 __global__ __launch_bounds__(NW * 64) void k_gemm(Group G) {
   __shared__ float part[NW][32][33];
   int pi = 0;
@@ -154,7 +159,7 @@ __global__ __launch_bounds__(NW * 64) void k_gemm(Group G) {
     float v = 0.f;
 #pragma unroll
     for (int i = 0; i < NW; ++i) v += part[i][r][c];
-    store(P, r0 + r, c0 + c, v);
+    store<EX>(P, r0 + r, c0 + c, v);
   }
 }
 
@@ -740,7 +745,12 @@ static int gemm_run(gemm::Group& G, void* stream) {
   // (a longer slice loops over batches, so any KMAX is correct; the choice only sizes registers)
   const int per = (kmax / 16 + nw - 1) / nw;
   hipStream_t st = (hipStream_t)stream;
-#define TMD_GEMM_LAUNCH(NW_, KB_) hipLaunchKernelGGL((gemm::k_gemm<NW_, KB_>), dim3(tiles), dim3(NW_ * 64), 0, st, G)
+  bool ex = false;  // any epilogue extension (tmdnet_gemm_ex_f32) in this launch
+  for (int i = 0; i < n_problems; ++i)
+    ex = ex || G.p[i].pre || G.p[i].act || G.p[i].rscale || G.p[i].dpre;
+#define TMD_GEMM_LAUNCH(NW_, KB_)                                                                   \
+  if (ex) hipLaunchKernelGGL((gemm::k_gemm<NW_, KB_, true>), dim3(tiles), dim3(NW_ * 64), 0, st, G); \
+  else hipLaunchKernelGGL((gemm::k_gemm<NW_, KB_, false>), dim3(tiles), dim3(NW_ * 64), 0, st, G)
   if (nw <= 2) TMD_GEMM_LAUNCH(2, 8);
   else if (nw >= 16) {
     // (the 16-wave launches measured equal with 1-, 2- and 3-block batches: one 1024-thread block per
