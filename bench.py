@@ -291,14 +291,14 @@ def et_bwd_bytes(E, N, P, H, dr, s=4):
     return b
 
 
-PROBE_KERNEL = "k_fwd<float, 4, 1, 1, false>"
+PROBE_KERNEL = "k_fwd<float, 4, 1, 1, false, false>"
 # the model runs large graphs with planar v / dv rows (et_stack.PLANAR_MIN_EDGES): probe that layout
 PROBE_FLAGS = 4  # TMDNET_ET_V_PLANAR
 
 
 PMC_PASSES = ("FETCH_SIZE", "WRITE_SIZE", "TCC_HIT_sum TCC_MISS_sum")
 # the child's dispatch sequence (main(), --pmc-child): probe kernel name -> [(tag, count), ...] in order
-PMC_CHILD = {"k_fwd<float, 4, 1, 1, false>": [("per_edge", 8), ("pairs", 8)],
+PMC_CHILD = {"k_fwd<float, 4, 1, 1, false, false>": [("per_edge", 8), ("pairs", 8)],
              "k_bwd_dst<": [("bwd_dst", 4)], "k_bwd_src<": [("bwd_src", 4)], "k_bwd_merged<": [("bwd_dr", 4)]}
 
 
