@@ -186,8 +186,25 @@ int tmdnet_et_message_fwd(int dtype, int n_nodes, int hidden, int heads, const i
                           int ld_pk, const void* pv, int ld_pv, const void* cutoff, const void* unit,
                           void* x_out, void* vec_out, int flags, const int32_t* pk_rows,
                           const int32_t* order, void* stream);
+/* Size switches of the message backward's launch forms (run-time tuning; tests force the large-graph
+ * forms onto small graphs).  BOTH_MAX_NODES: below it the destination and source passes share one grid
+ * (default 16384, env TMDNET_ET_FUSE); MERGED_MIN_NODES: from it the dr-mode force pass runs both roles in
+ * one pass over the rows (default 16384, env TMDNET_ET_MERGED_MIN).  Returns the previous value (-1:
+ * unknown key).  Not thread-safe against concurrent launches. */
+#define TMDNET_TUNE_ET_BOTH_MAX_NODES 1
+#define TMDNET_TUNE_ET_MERGED_MIN_NODES 2
+int tmdnet_set_tuning(int key, int value);
+
 /* Backward (two CSR passes, no atomics): destination pass -> gq, gpk, gpv, gcut, gunit; source
- * pass (requires a symmetric edge list, dk/dv/cutoff functions of |r| only) -> gk, gv, gvec_in.
+ * pass -> gk, gv, gvec_in.
+ * PRECONDITION (source pass, and the merged dr-mode pass used for >= 16384 nodes): the edge list is
+ * symmetric and pair-symmetric in its per-edge inputs -- for every edge e = (t <- s) the list holds
+ * rev(e) = (s <- t) with cutoff[rev(e)] == cutoff[e], unit[rev(e)] == -unit[e] and the same projection
+ * (pk / pv row, or pk_rows[rev(e)] == pk_rows[e]).  The source role of node s reads those values from
+ * s's OWN row (edge e' = (s <- m)) as the reversed edge m <- s, so a list violating this gives wrong
+ * gk / gv / gvec_in silently.  Every list the model builds satisfies it (dk, dv, cutoff depend on |r|
+ * only; minimum-image deltas flip sign).  Checked on the device by the Python launcher when
+ * TMDNET_LIB=debug or TMDNET_CHECK_SYMMETRY=1 (kernels.check_pair_symmetry).
  * Gradients are written with the leading dimension of the matching input (gq: ld_q, gk: ld_k,
  * gv: ld_v, gpk: ld_pk, gpv: ld_pv), so they can land directly in fused [q|k|v] / [dk|dv]
  * gradient buffers; gpk/gpv are gradients of the PRE-activation projections.

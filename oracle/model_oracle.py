@@ -269,7 +269,7 @@ def tensornet_representation(sd, cfg, z, pos, batch, static_shapes=True, prefix=
     cl, cu = cfg["cutoff_lower"], cfg["cutoff_upper"]
     N = z.shape[0]
     src, dst, dl, r, _ = edge_geometry(pos, batch, cl, cu, max_pairs=cfg["max_num_neighbors"] * N,
-                                       pad_static=static_shapes)
+                                       pad_static=static_shapes, box=cfg.get("box"))
     f = expnorm(r, sd[p("distance_expansion.means")], sd[p("distance_expansion.betas")], cl, cu)
     self_edge = src == dst
     u = dl / torch.where(self_edge, torch.ones_like(r), r).unsqueeze(1)

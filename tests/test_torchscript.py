@@ -333,3 +333,36 @@ def test_torchscript_fused_stack_distance_influence(influence):
         outs.append((y.detach(), neg_dy.detach(), ddy))
     for a, b in zip(outs[1], outs[0]):
         assert _rel(a, b) < 1e-4
+
+
+def test_torchscript_fused_stack_no_stale_pack_across_models():
+    """et_stack caches its packed weights per parameter set.  Two models built and loaded the same way
+    (identical version counters) must not share a pack even when the second model's parameters land at
+    the first one's freed addresses (the key holds weak references to the storages)."""
+    _torch_lib_loaded()
+    import gc
+    from torchmdnet.models.model import create_model
+    args = yaml_args("equivariant-transformer")
+    args.update(embedding_dimension=64, num_layers=2, derivative=True)
+    z, pos, batch = _batch(4)
+    for seed in (0, 1, 2):
+        torch.manual_seed(seed)
+        model = create_model(args).to(DEV)
+        scripted = torch.jit.script(model)
+        y_s, f_s = scripted(z, pos.clone(), batch)
+        y_e, f_e = model(z, pos.clone(), batch)
+        assert _rel(y_s, y_e) < 1e-4 and _rel(f_s, f_e) < 1e-4, seed
+        del model, scripted, y_s, f_s, y_e, f_e
+        gc.collect()
+    # in-place writes that bypass the version counter need the explicit invalidation
+    torch.manual_seed(3)
+    model = create_model(args).to(DEV)
+    scripted = torch.jit.script(model)
+    scripted(z, pos.clone(), batch)
+    with torch.no_grad():
+        for p in model.parameters():
+            p.data.mul_(0.5)
+    torch.ops.tmdnet.et_stack_invalidate()
+    y_s, f_s = scripted(z, pos.clone(), batch)
+    y_e, f_e = model(z, pos.clone(), batch)
+    assert _rel(y_s, y_e) < 1e-4 and _rel(f_s, f_e) < 1e-4

@@ -1626,6 +1626,18 @@ static int et_launch_k(const Args<T>& A, dim3 g, dim3 b, int nbn, hipStream_t st
 // below this many nodes the two backward passes share one grid (k_bwd_both)
 static constexpr int kBwdFuseNodes = 16384;
 
+// size switches of the backward's launch forms, settable at run time (tmdnet_set_tuning: tests force the
+// large-system forms on small graphs); first read from TMDNET_ET_FUSE / TMDNET_ET_MERGED_MIN
+static int g_tune[3] = {-1, -1, -1};
+static int tune_get(int key) {
+  int& v = g_tune[key];
+  if (v < 0) {
+    const char* e = getenv(key == TMDNET_TUNE_ET_BOTH_MAX_NODES ? "TMDNET_ET_FUSE" : "TMDNET_ET_MERGED_MIN");
+    v = e ? atoi(e) : kBwdFuseNodes;
+  }
+  return v;
+}
+
 template <typename T, int V, int KIND, bool ORD>
 static int et_launch_v(const Args<T>& A, hipStream_t st) {
   int S = et_waves_per_node(A.n, (int)sizeof(T) * V);
@@ -1739,14 +1751,14 @@ static int bwd(int n, int H, int heads, const int32_t* row_ptr, const int32_t* s
   const bool dr = gr != nullptr;
   if (dr && ((A.pk && !dpk) || (A.pv && !dpv))) return kBadArgument;
   if (!dr && ((A.pk && !gpk) || (A.pv && !gpv))) return kBadArgument;
-  static const int fuse_nodes = getenv("TMDNET_ET_FUSE") ? atoi(getenv("TMDNET_ET_FUSE")) : kBwdFuseNodes;
+  const int fuse_nodes = tune_get(TMDNET_TUNE_ET_BOTH_MAX_NODES);
   const bool ag = !dr && (acc & TMDNET_ACC_GRADS) && (A.pk || A.pv);  // injected projection cotangents
   // dr mode: both roles in one pass over the rows (k_bwd_merged)
   // (tuning: TMDNET_ET_MERGED=0 off, 1 stream-prefetching variant, 2 loads per edge in the body).
   // Large graphs only: C5 2.97 vs 3.38 ms per layer (the two passes); at C2 the two passes in one
   // grid (k_bwd_both, twice the waves at 167 vs 222 VGPRs) win, 51 vs 69 us.
   static const int merged = getenv("TMDNET_ET_MERGED") ? atoi(getenv("TMDNET_ET_MERGED")) : 1;
-  static const int merged_min = getenv("TMDNET_ET_MERGED_MIN") ? atoi(getenv("TMDNET_ET_MERGED_MIN")) : kBwdFuseNodes;
+  const int merged_min = tune_get(TMDNET_TUNE_ET_MERGED_MIN_NODES);
   if (dr && merged && n >= merged_min && !(acc & TMDNET_ET_TWO_PASS) && !A.gpk && !A.gpv)
     return merged == 2 ? et_launch<T, 9, false>(V, A, st) : et_launch<T, 8, false>(V, A, st);
   if (n < fuse_nodes)
@@ -2049,4 +2061,11 @@ extern "C" int tmdnet_nbr_embed_bwd2(int dtype, int n_nodes, int hidden, const i
 
 extern "C" const char* tmdnet_build_info(void) {
   return "torchmd-net_amd libtmdnet_hip (gfx950, wave64 CSR edge kernels)";
+}
+
+extern "C" int tmdnet_set_tuning(int key, int value) {
+  if (key != TMDNET_TUNE_ET_BOTH_MAX_NODES && key != TMDNET_TUNE_ET_MERGED_MIN_NODES) return -1;
+  const int prev = et::tune_get(key);
+  et::g_tune[key] = value < 0 ? 0 : value;
+  return prev;
 }

@@ -1157,22 +1157,50 @@ void proj_into(const Tensor& A, const Tensor& W, const Tensor& Wp, const Tensor&
 // The stacked weights of one parameter set: per layer [q|k|v] (5H x H) and its bias, all layers' [dk; dv]
 // rows (L*D x R) + bias and their bf16 split.  Rebuilt only when a parameter's storage or version changes
 // (an MD engine evaluates one fixed model: one pack for the whole run).
+//
+// The key holds a WEAK reference to every parameter's StorageImpl besides its data pointer and version: a
+// weak reference keeps the StorageImpl object itself allocated (not its bytes), so once a model is freed
+// its entries expire and no later storage -- even one the caching allocator places at the same address
+// with the same version counts -- can match them.  In-place writes that bypass the version counter
+// (`p.data.copy_(...)`) are invisible here: call `torch.ops.tmdnet.et_stack_invalidate()` after them.
+struct PackKey {
+  c10::weak_intrusive_ptr<c10::StorageImpl> st;
+  const void* ptr;
+  int64_t ver;
+};
 struct Packed {
-  std::vector<std::pair<const void*, uint32_t>> key;
+  std::vector<PackKey> key;
   std::vector<Tensor> qkv_w, qkv_b;
   Tensor dkv_w, dkv_b, dkv_wp;
 };
 
+static std::mutex g_pack_mu;
+static std::shared_ptr<Packed> g_pack_last;
+
+static bool pack_matches(const Packed& pk, const std::vector<Tensor>& P) {
+  if (pk.key.size() != P.size()) return false;
+  for (size_t i = 0; i < P.size(); ++i) {
+    const PackKey& k = pk.key[i];
+    if (k.ptr != P[i].data_ptr() || k.ver != P[i]._version()) return false;
+    auto live = k.st.lock();  // null once the storage was freed
+    if (!live || live.get() != P[i].storage().unsafeGetStorageImpl()) return false;
+  }
+  return true;
+}
+
+void et_stack_invalidate() {
+  std::lock_guard<std::mutex> lock(g_pack_mu);
+  g_pack_last.reset();
+}
+
 std::shared_ptr<Packed> pack_stack(const std::vector<Tensor>& P, int64_t L, int64_t np, bool hk, bool hv) {
-  static std::mutex mu;
-  static std::shared_ptr<Packed> last;
-  std::vector<std::pair<const void*, uint32_t>> key;
-  key.reserve(P.size());
-  for (const auto& t : P) key.emplace_back(t.data_ptr(), t._version());
-  std::lock_guard<std::mutex> lock(mu);
-  if (last && last->key == key) return last;
+  std::lock_guard<std::mutex> lock(g_pack_mu);
+  if (g_pack_last && pack_matches(*g_pack_last, P)) return g_pack_last;
   auto pk = std::make_shared<Packed>();
-  pk->key = std::move(key);
+  pk->key.reserve(P.size());
+  for (const auto& t : P)
+    pk->key.push_back(PackKey{c10::weak_intrusive_ptr<c10::StorageImpl>(t.storage().getWeakStorageImpl()),
+                              t.data_ptr(), t._version()});
   at::NoGradGuard ng;
   std::vector<Tensor> dw, db;
   for (int64_t l = 0; l < L; ++l) {
@@ -1196,7 +1224,7 @@ std::shared_ptr<Packed> pack_stack(const std::vector<Tensor>& P, int64_t L, int6
       }
     }
   }
-  last = pk;
+  g_pack_last = pk;
   return pk;
 }
 
@@ -1612,6 +1640,8 @@ TORCH_LIBRARY(tmdnet, m) {
   m.def("et_stack(Tensor x, Tensor f, Tensor dist, Tensor cutoff, Tensor unit, Tensor mu, Tensor beta, "
         "Tensor row_ptr, Tensor src, Tensor dst, float cutoff_lower, float cutoff_upper, int rbf_type, int heads, "
         "bool has_dk, bool has_dv, bool out_norm, Tensor[] params, int acts=0) -> (Tensor x, Tensor vec)");
+  // drops the packed-weight cache of et_stack (after in-place writes that bypass the version counter)
+  m.def("et_stack_invalidate() -> ()", tmdt::et_stack_invalidate);
 }
 
 TORCH_LIBRARY_IMPL(tmdnet, CompositeImplicitAutograd, m) {

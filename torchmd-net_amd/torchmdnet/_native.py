@@ -97,6 +97,7 @@ SIGNATURES = {
     "tmdnet_mse2_fwd": (I, [I, I, P, P, D, I, P, P, D, P, P]),
     "tmdnet_mse2_bwd": (I, [I, I, P, P, D, I, P, P, D, P, P, P, P]),
     "tmdnet_build_info": (ctypes.c_char_p, []),
+    "tmdnet_set_tuning": (I, [I, I]),
 }
 
 _lib = None

@@ -1035,6 +1035,8 @@ def _second_order(ctx, ggs, want):
     if node is not None and _will_run(node):
         inj["x_top"] = seed_x
         meta.pending = {"inj": inj, "W_bar": W_bar, "on_bar": on_bar, "C_bar": C_bar, "u_bar": u_bar}
+        # prune entries that are gone or already consumed (custom loops never call check_pending_consumed)
+        _HANDED_OFF[:] = [r for r in _HANDED_OFF if (m := r()) is not None and getattr(m, "pending", None) is not None]
         _HANDED_OFF.append(weakref.ref(meta))
         res = [gbar_x, gbar_v, None, None, None, None, r_bar] + [None] * len(params)
         return [t if w else None for t, w in zip(res, want)]

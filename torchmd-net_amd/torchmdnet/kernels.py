@@ -627,6 +627,44 @@ def et_fused_bwd_launch(q, k, v, vec, r, C, u, fep, rbf, graph, heads, gx, gvec,
     nat.check(rc, "tmdnet_et_fused_bwd_f32")
 
 
+# The message backward's source pass (and the merged dr-mode pass, k_bwd_merged) reads an edge's
+# cutoff, unit vector and projection row for its REVERSED edge: valid only for symmetric lists with
+# C[rev(e)] == C[e], unit[rev(e)] == -unit[e] and one projection row per pair (include/tmdnet.h,
+# tmdnet_et_message_bwd).  The debug library (TMDNET_LIB=debug) or TMDNET_CHECK_SYMMETRY=1 verifies
+# that on the device before every launch (a host sync: diagnostics only).
+CHECK_SYMMETRY = os.environ.get("TMDNET_LIB") == "debug" or os.environ.get("TMDNET_CHECK_SYMMETRY") == "1"
+
+
+# run-time size switches of the message backward's launch forms (include/tmdnet.h tmdnet_set_tuning)
+TUNE_ET_BOTH_MAX_NODES, TUNE_ET_MERGED_MIN_NODES = 1, 2
+
+
+def set_tuning(key, value):
+    """Set a launch-form size switch of the HIP library; returns the previous value."""
+    prev = int(nat.load().tmdnet_set_tuning(int(key), int(value)))
+    if prev < 0:
+        raise ValueError(f"tmdnet_set_tuning: unknown key {key}")
+    return prev
+
+
+def check_pair_symmetry(graph, C, u, pk_rows=None):
+    """Raise unless the per-edge inputs of the message backward are pair-symmetric over the graph's
+    valid edges (see CHECK_SYMMETRY)."""
+    tr = graph.transpose
+    if tr is None:
+        raise RuntimeError("et_message_bwd: the source pass needs a symmetric edge list (transpose map)")
+    n = int(graph.row_ptr[graph.n_nodes].item())
+    t = tr[:n].long()
+    if n and bool((t < 0).any()):
+        raise RuntimeError("et_message_bwd: edge without a reverse edge (asymmetric list)")
+    if not torch.equal(C[:n][t], C[:n]):
+        raise RuntimeError("et_message_bwd: cutoff not pair-symmetric (C[rev(e)] != C[e])")
+    if not torch.equal(u[:n][t], -u[:n]):
+        raise RuntimeError("et_message_bwd: unit vectors not antisymmetric (u[rev(e)] != -u[e])")
+    if pk_rows is not None and not torch.equal(pk_rows[:n][t], pk_rows[:n]):
+        raise RuntimeError("et_message_bwd: the two edges of a pair read different projection rows")
+
+
 def et_message_bwd_launch(q, k, v, vec, pk, pv, C, u, graph, heads, gx, gvec, gq, gk, gv, gw, gpk,
                           gpv, gC, gu, accumulate=0, pk_rows=None, dpk=None, dpv=None, g_r=None):
     """dr mode (g_r given): gpk / gpv stay None and <g_pk, dpk> + <g_pv, dpv> accumulates into g_r
@@ -638,6 +676,8 @@ def et_message_bwd_launch(q, k, v, vec, pk, pv, C, u, graph, heads, gx, gvec, gq
     for gt, t in ((gq, q), (gk, k), (gv, v), (gpk, pk), (gpv, pv)):
         if gt is not None and t is not None and gt.stride(0) != t.stride(0):
             raise ValueError("et_message_bwd: gradient buffers must have the row strides of their inputs")
+    if CHECK_SYMMETRY:
+        check_pair_symmetry(graph, C, u, pk_rows)
     lib = nat.load()
     N, H = q.shape
     rc = lib.tmdnet_et_message_bwd(
@@ -2112,11 +2152,18 @@ def mlp_act(x, weights, biases, act, scale=None):
     ok = (MLP_ACT and isinstance(act, torch.nn.SiLU) and x.is_cuda and x.dtype == torch.float32 and x.dim() == 2
           and 0 < x.shape[0] <= GEMM_MAX_ROWS and all(b is not None for b in biases)
           and all(w.shape[1] % 16 == 0 for w in weights) and all(w.shape[0] % 16 == 0 for w in weights))
+    if ok:
+        # tmdnet_gemm_ex_f32 also needs 16-byte aligned operands (a contiguous view with a storage offset
+        # may not be): realign x by a copy, take the composite for misaligned weights
+        x = x.contiguous()
+        if x.data_ptr() % 16:
+            x = x.clone()
+        ok = all(w.is_contiguous() and w.data_ptr() % 16 == 0 for w in weights) and \
+            all(b.data_ptr() % 16 == 0 for b in biases) and (scale is None or scale.contiguous().data_ptr() % 16 == 0)
     if not ok:
         for i in range(L):
             x = fused_act(act, linear(x, weights[i], biases[i]), scale if i == L - 1 else None)
         return x
-    x = x.contiguous()
     return _MLPAct.apply(x, None if scale is None else scale.contiguous(), *weights, *biases)
 
 
