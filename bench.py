@@ -476,7 +476,7 @@ def fused_projection_probe(launch, E, N, H, reps, dev, R=64):
     xo, vo = torch.empty(N, H, device=dev), torch.empty(N, 3, H, device=dev)
 
     def run():
-        kernels.et_fused_fwd_launch(q, k, v, vec, r, C, u, fep, (mu, beta, 0.0, 5.0, 0), g, 8, xo, vo)
+        kernels.et_fused_fwd_launch(q, k, v, vec, r, C, u, fep, (mu, beta, 0.0, 5.0, 0), g, 8, xo, vo, flags=4)
     for _ in range(5):
         run()
     torch.cuda.synchronize()

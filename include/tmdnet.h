@@ -559,22 +559,21 @@ int tmdnet_proj_split_f32(int N, int K, const void* W, int ldw, void* Wp, void* 
 int tmdnet_proj_f32(int M, int N, int K, const void* A, int lda, const void* Wp, long long piece_stride,
                     const void* bias, void* C, int ldc, void* stream);
 
-/* The ET message with the dk/dv projection FUSED in (large graphs; reference torchmd_et.py:282-291 +
- * :314-347, the RBF of models/utils.py:272-344 evaluated in-kernel): tmdnet_et_message_fwd's outputs
- * without the projection rows.  Per 16-edge tile the RBF values of the distances r[e] are formed in
- * registers and multiplied on the fp16 MFMA by the layer's weight, held in LDS for the whole launch as
- * the image made by tmdnet_fep_split_f32 (two fp16 pieces per value after exact power-of-two scaling:
- * fp32-GEMM accuracy).
+/* The ET message with the dk/dv projection FUSED in (reference torchmd_et.py:282-291 + :314-347, the
+ * RBF of models/utils.py:272-344 evaluated in-kernel): tmdnet_et_message_fwd's outputs without the
+ * projection rows.  Per 16-edge tile the RBF values of the distances r[e] are formed in registers and
+ * multiplied on the fp16 MFMA by the layer's weight, held in LDS for the whole launch as the image made
+ * by tmdnet_fep_split_f32 (two fp16 pieces per value after exact power-of-two scaling: fp32-GEMM
+ * accuracy).
  *   tmdnet_fep_split_f32: W [D][R] (ldw) = the layer's [dk | dv] rows in the planar order (dk, then the
  *     x, v1, v2 H-blocks of dv), bias [D] (nullable) -> img (tmdnet_fep_image_bytes(D, R), 16-byte
  *     aligned), wsc [D] (accumulator scale per row), bias_out [D].
- *   tmdnet_et_fused_fwd_f32: fp32 only; H = 128, heads = 8 (d = 16), R = 32 or 64, v in the planar
- *     layout (TMDNET_ET_V_PLANAR), both projections present (distance_influence "both"); vec_in
- *     nullable (layer 0); mu / beta: the RBF means / betas (gauss: offsets / coeff[0]).  Else
- *     TMDNET_UNSUPPORTED.  One workgroup per CU (its LDS), deterministic, no atomics on outputs.
- *     pkv_out (nullable): the pre-activation [dk | dv] rows are also written, for the canonical edge
- *     (src >= dst) of every pair, to row pk_rows[e] of pkv_out [n_pair_rows][ld_pkv] -- the rows an
- *     unfused backward reads (tmdnet_et_message_bwd with pk_rows). */
+ *   tmdnet_et_fused_fwd_f32: fp32 only; H = 128, heads = 8 (d = 16), R = 32 or 64, both projections
+ *     present (distance_influence "both"), SiLU activations; v in the planar layout when flags carries
+ *     TMDNET_ET_V_PLANAR, else the reference's per-head [x|v1|v2] interleave; q / k / v / vec_in / x_out /
+ *     vec_out 16-byte aligned with leading dimensions % 4 == 0; vec_in nullable (layer 0); mu / beta: the
+ *     RBF means / betas (gauss: offsets / coeff[0]).  Else TMDNET_UNSUPPORTED.  One workgroup per CU
+ *     (its LDS), deterministic, no atomics on outputs. */
 size_t tmdnet_fep_image_bytes(int D, int R);
 int tmdnet_fep_split_f32(int D, int R, const void* W, int ldw, const void* bias, void* img, void* wsc,
                          void* bias_out, void* stream);
@@ -583,16 +582,16 @@ int tmdnet_et_fused_fwd_f32(int n_nodes, int hidden, int heads, int num_rbf, con
                             const void* v, int ld_v, const void* vec_in, const void* dist, const void* cutoff,
                             const void* unit, const void* img, const void* wsc, const void* bias, const void* mu,
                             const void* beta, double cutoff_lower, double cutoff_upper, int rbf_type,
-                            void* x_out, void* vec_out, void* pkv_out, int ld_pkv, const int32_t* pk_rows,
-                            long long n_pair_rows, void* stream);
+                            void* x_out, void* vec_out, int flags, void* stream);
 
 /* The fused message's first-order backward for the force pass ("dr mode", reference: the autograd of
  * torchmd_et.py:282-291, :314-347 through f = rbf(r)): d pre / d r = W f'(r) is formed on the MFMA per
  * tile beside the projection (both from the tmdnet_fep_split_f32 image), and the projection gradient is
  * contracted with it in registers: gdist[e] = <g_pre, d pre / d r>.  Outputs as tmdnet_et_message_bwd in
- * dr mode (destination pass: gq, gcut, gunit, gdist; source pass over the reversed edges: gk, gv
- * (planar), gvec_in), with its accumulate bits (TMDNET_ACC_VEC_RESIDUAL / _EDGE / _GRADS).  Same
- * envelope as tmdnet_et_fused_fwd_f32; requires a symmetric edge list. */
+ * dr mode (destination pass: gq, gcut, gunit, gdist; source pass over the reversed edges: gk, gv (v's
+ * layout), gvec_in), with its accumulate bits (TMDNET_ACC_VEC_RESIDUAL / _EDGE / _GRADS, and
+ * TMDNET_ET_V_PLANAR for the layout).  Same envelope as tmdnet_et_fused_fwd_f32; the gradient buffers
+ * 16-byte aligned; requires a pair-symmetric edge list (tmdnet_et_message_bwd's precondition). */
 int tmdnet_et_fused_bwd_f32(int n_nodes, int hidden, int heads, int num_rbf, const int32_t* row_ptr,
                             const int32_t* src, int max_pairs, const void* q, int ld_q, const void* k, int ld_k,
                             const void* v, int ld_v, const void* vec_in, const void* dist, const void* cutoff,

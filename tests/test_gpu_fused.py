@@ -75,16 +75,14 @@ def test_fused_forward_matches_fp64_and_unfused(R, rbf_type, cl, monkeypatch):
     y64, f64 = _run(m64, z, pos, L, torch.float64)
     assert _rel(y, y64) < 1e-5
     assert _rel(f, f64) < 1e-4
-    # the fused forward with the unfused force-pass backward: over the pair rows the fused forward wrote
-    # ("rows"), or formed by the GEMM in the backward ("lazy")
+    # the fused forward with the unfused force-pass backward over rows formed by the GEMM ("lazy")
     monkeypatch.setattr(et_stack, "FUSED_BWD", False)
-    for mode in ("rows", "lazy"):
-        monkeypatch.setattr(et_stack, "FEP_BWD", mode)
-        y1, f1 = _run(m, z, pos, L, torch.float32)
-        assert len(bcalls) == 3
-        assert _rel(y, y1) < 1e-5
-        assert _rel(f, f1) < 1e-4
-    # default ("off"): with a backward to follow the forward is the unfused one; energy only -> fused
+    monkeypatch.setattr(et_stack, "FEP_BWD", "lazy")
+    y1, f1 = _run(m, z, pos, L, torch.float32)
+    assert len(bcalls) == 3 and len(calls) == 6
+    assert _rel(y, y1) < 1e-5
+    assert _rel(f, f1) < 1e-4
+    # "off": with a backward to follow the forward is the unfused one; energy only -> fused
     monkeypatch.setattr(et_stack, "FEP_BWD", "off")
     n0 = len(calls)
     y2, f2 = _run(m, z, pos, L, torch.float32)
@@ -102,4 +100,35 @@ def test_fused_forward_matches_fp64_and_unfused(R, rbf_type, cl, monkeypatch):
     assert len(calls) == n0
     assert _rel(y, y0) < 1e-5
     assert _rel(f, f0) < 1e-4
-    assert torch.isfinite(f).all()
+
+
+@pytest.mark.parametrize("planar", [False, True])
+def test_fused_c2_molecules_vs_oracle_and_unfused(planar, monkeypatch):
+    """The fused kernels on the C2 workload (32 QM9-like molecules, 128 ch, 8 layers, 64 RBF): the
+    reference per-head [x|v1|v2] v layout (default below the planar threshold) and the planar one,
+    against the fp64 oracle and the unfused path (TMDNET_FEP=0), energies and forces."""
+    from oracle import model_oracle as O
+    from torchmdnet import et_stack, kernels
+    from torchmdnet.models.model import create_model
+    calls = []
+    orig, origb = kernels.et_fused_fwd_launch, kernels.et_fused_bwd_launch
+    monkeypatch.setattr(kernels, "et_fused_fwd_launch", lambda *a, **k: (calls.append("f"), orig(*a, **k))[1])
+    monkeypatch.setattr(kernels, "et_fused_bwd_launch", lambda *a, **k: (calls.append("b"), origb(*a, **k))[1])
+    if planar:
+        monkeypatch.setattr(et_stack, "PLANAR_MIN_EDGES", 0)
+    args = yaml_args("equivariant-transformer", embedding_dimension=128, num_layers=8, num_rbf=64, num_heads=8,
+                     derivative=True)
+    torch.manual_seed(0)
+    m = create_model(args)
+    z, pos, batch = O.qm9_like(32)
+    y_ref, f_ref = O.energy_forces(m.state_dict(), dict(args), z, pos, batch)
+    m = m.to(DEV)
+    y, f = m(z.to(DEV), pos.float().to(DEV), batch.to(DEV))
+    assert calls.count("f") == 8 and calls.count("b") == 8, calls
+    assert _rel(y.detach().cpu(), y_ref.detach()) < 1e-4
+    assert _rel(f.detach().cpu(), f_ref) < 1e-4
+    monkeypatch.setattr(et_stack, "FEP", "0")
+    y0, f0 = m(z.to(DEV), pos.float().to(DEV), batch.to(DEV))
+    assert calls.count("f") == 8
+    assert _rel(y.detach(), y0.detach()) < 1e-5
+    assert _rel(f.detach(), f0.detach()) < 1e-4

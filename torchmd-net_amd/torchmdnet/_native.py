@@ -92,7 +92,7 @@ SIGNATURES = {
     "tmdnet_et_fused_bwd_f32": (I, [I, I, I, I, P, P, I, P, I, P, I, P, I, P, P, P, P, P, P, P, P, P, D, D, I,
                                     P, P, P, P, P, P, P, P, P, I, P]),
     "tmdnet_et_fused_fwd_f32": (I, [I, I, I, I, P, P, I, P, I, P, I, P, I, P, P, P, P, P, P, P, P, P, D, D, I,
-                                    P, P, P, I, P, ctypes.c_longlong, P]),
+                                    P, P, I, P]),
     "tmdnet_proj_f32": (I, [I, I, I, P, I, P, ctypes.c_longlong, P, P, I, P]),
     "tmdnet_mse2_fwd": (I, [I, I, P, P, D, I, P, P, D, P, P]),
     "tmdnet_mse2_bwd": (I, [I, I, P, P, D, I, P, P, D, P, P, P, P]),

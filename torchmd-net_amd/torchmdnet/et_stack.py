@@ -122,19 +122,18 @@ BATCH_DKV_BYTES = 2 << 30
 PLANAR_MIN_EDGES = 131072
 # dk/dv projection rows shared by the two directions of an edge pair (halves the projection GEMM)
 PAIR_ROWS = True
-# dk/dv projection FUSED into the forward edge kernel (tmdnet_et_fused_fwd_f32) on planar-layout graphs
-# (>= PLANAR_MIN_EDGES edges) with a fixed RBF basis of r: the projection rows are never written (C5:
-# 2.8 GB per layer, read back once per direction by the unfused kernel).  A backward that needs them
-# forms them then (_act_pkv).  TMDNET_FEP=0 turns it off.
+# dk/dv projection FUSED into the edge kernels (et_fused.hip: tmdnet_et_fused_fwd_f32 / _bwd_f32) for a
+# fixed RBF basis of r (H = 128, 8 heads, SiLU, both projections): the projection rows are never written
+# (C5: 2.8 GB per layer, read back once per direction by the unfused kernels; the force pass's
+# d(dk,dv)/dr rows likewise).  TMDNET_FEP=0 turns it off.
 FEP = os.environ.get("TMDNET_FEP", "auto")
-# When a backward can follow (grad enabled), how it gets the projection: "off" (default) = the
-# forward is the unfused one (projection GEMM + message kernel); "rows" = the fused forward also
-# writes the canonical edges' pre-activation pair rows and the unfused backward reads them; "fused" =
-# the force-pass (dr mode) backward is fused the same way (tmdnet_et_fused_bwd_f32, no rows at all:
-# 20 vs 67 GB peak at C5); "lazy" = the backward forms the rows by the GEMM.  Measured C5 energy +
-# forces (tools/c5_modes.sh, r03): off 69.2, rows 69.6, fused 71.8, lazy 72.4 ms -- the fused
-# forward (1.45 vs 0.91 + 1.17 ms per layer) pays only when no rows are needed (energy only).
-FEP_BWD = os.environ.get("TMDNET_FEP_BWD", "off")
+# When a backward can follow (grad enabled), how it gets the projection: "fused" (default) = the
+# force-pass (dr mode) backward is fused the same way (d pre / d r formed on the MFMA in-kernel); a
+# backward that needs the projection rows (parameter gradients, the recorded force pass of force-matching
+# training) forms them by the GEMM then ("lazy" for every backward); "off" = with a backward to follow,
+# the forward is the unfused one (projection GEMM + message kernel).  Force-matching training steps
+# (second_order_expected) always run the unfused forward: their backward reads the rows.
+FEP_BWD = os.environ.get("TMDNET_FEP_BWD", "fused")
 FUSED_BWD = FEP_BWD == "fused"
 # "dr mode" force pass (see _backward_layers): on whenever the force pass needs no weight gradient
 # and the features are a fixed basis of r (also under create_graph, which the reference force pass
@@ -371,16 +370,11 @@ def _forward_layers(meta, x, f, C, u, params, r=None, want_bwd=False):
     meta.refresh_effective()
     # the projections depend on |r| only: one row per edge PAIR ((E + N) / 2 rows), read by both
     # directions through pk_rows (bit-identical to the per-edge projection)
-    fep = meta.fep and r is not None and (FEP_BWD != "off" or not want_bwd)
+    fep = meta.fep and r is not None and (not want_bwd or (FEP_BWD != "off" and not _EXPECT_SECOND_ORDER[0]))
     if not fep:
         meta.fep_imgs = None  # (the backward's fused path keys on them: none from an earlier forward)
     fp = _pair_f(meta, f) if (D and not fep) else f
     pkv_all = meta.dkv_proj(fp) if (meta.batched and D and not fep) else None
-    # the fused forward writes the pair rows itself when the unfused backward will want them
-    fep_rows = (fep and FEP_BWD == "rows" and want_bwd and meta.pk_rows is not None
-                and meta.pairs is not None)
-    if fep_rows and meta.batched:
-        pkv_all = torch.empty((meta.pairs[1].shape[0], meta.n_layers * D), dtype=x.dtype, device=x.device)
     layers = meta.split(params)
     L = len(layers)
     od = dict(dtype=x.dtype, device=x.device)
@@ -405,17 +399,14 @@ def _forward_layers(meta, x, f, C, u, params, r=None, want_bwd=False):
         kernels.gemm_group(probs)
         xa = xa_all[l]
         veca = torch.empty((N, 3, H), dtype=x.dtype, device=x.device)
-        if fep:  # projection fused into the edge kernel (its rows written only for an unfused backward)
+        if fep:  # projection fused into the edge kernel (no rows: a backward that needs them forms them)
             pkv = None
-            if fep_rows:
-                pkv = pkv_all[:, l * D:(l + 1) * D] if pkv_all is not None else \
-                    torch.empty((meta.pairs[1].shape[0], D), dtype=x.dtype, device=x.device)
             if l == 0:
                 meta.fep_imgs = []
             meta.fep_imgs.append(kernels.fep_split(dkv_w, dkv_b))
             kernels.et_fused_fwd_launch(qkv[:, :H], qkv[:, H:2 * H], qkv[:, 2 * H:], vec, r, C, u,
                                         meta.fep_imgs[l], meta.rbf, meta.graph, meta.heads, xa, veca,
-                                        pkv_out=pkv, pk_rows=meta.pk_rows if fep_rows else None)
+                                        flags=meta.flags)
         else:
             if pkv_all is not None:
                 pkv = pkv_all[:, l * D:(l + 1) * D]
@@ -1357,7 +1348,7 @@ def et_stack(layers, x, graph, f, C, u, rbf=None, out_norm=None, f_pairs=None):
     if rbf is not None and D:
         r, mu, beta, cl, cu, rbf_type = rbf
         meta.rbf = (mu.detach(), beta.detach(), float(cl), float(cu), int(rbf_type))
-        meta.fep = (FEP not in ("0", "off") and meta.planar and hk and hv and x.is_cuda and meta.acts == 0
+        meta.fep = (FEP not in ("0", "off") and hk and hv and x.is_cuda and meta.acts == 0
                     and kernels.fep_supported(H, heads, mu.shape[0], x.dtype) and r.dtype == x.dtype)
     x = x.contiguous()
     f = f.contiguous() if (hk or hv) else None

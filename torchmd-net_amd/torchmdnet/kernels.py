@@ -583,11 +583,10 @@ def fep_supported(H, heads, R, dtype):
     return H == 128 and heads == 8 and R in (32, 64) and dtype == torch.float32
 
 
-def et_fused_fwd_launch(q, k, v, vec, r, C, u, fep, rbf, graph, heads, xo, vo, pkv_out=None, pk_rows=None):
+def et_fused_fwd_launch(q, k, v, vec, r, C, u, fep, rbf, graph, heads, xo, vo, flags=0):
     """One ``tmdnet_et_fused_fwd_f32`` launch: the ET message with the dk/dv projection fused in
     (``fep`` = fep_split(W, b) of the layer; ``rbf`` = (mu, beta, cutoff_lower, cutoff_upper, type));
-    v in the planar layout.  ``pkv_out`` [P, >= 4H] (with ``pk_rows``): also write the canonical edges'
-    pre-activation rows there (the pair rows an unfused backward reads)."""
+    ``flags``: nat.ET_V_PLANAR when v is in the planar layout."""
     lib = nat.load()
     N, H = q.shape
     mu, beta, cl, cu, rt = rbf
@@ -600,8 +599,7 @@ def et_fused_fwd_launch(q, k, v, vec, r, C, u, fep, rbf, graph, heads, xo, vo, p
                                      graph.n_edges, nat.ptr(q), _ld(q), nat.ptr(k), _ld(k), nat.ptr(v), _ld(v),
                                      nat.ptr(vec), nat.ptr(r), nat.ptr(C), nat.ptr(u), nat.ptr(img), nat.ptr(wsc),
                                      nat.ptr(bo), nat.ptr(mu), nat.ptr(beta), float(cl), float(cu), int(rt),
-                                     nat.ptr(xo), nat.ptr(vo), nat.ptr(pkv_out), _ld(pkv_out), nat.ptr(pk_rows),
-                                     0 if pkv_out is None else pkv_out.shape[0], nat.stream(q.device))
+                                     nat.ptr(xo), nat.ptr(vo), int(flags) & nat.ET_V_PLANAR, nat.stream(q.device))
     nat.check(rc, "tmdnet_et_fused_fwd_f32")
     if probe is not None:
         ev1.record()
