@@ -240,3 +240,45 @@ def test_fit_data_parallel_gloo():
     assert not set(s0) & set(s1) and len(set(s0) | set(s1)) == 12  # disjoint shards covering the split
     assert abs(w0 - w1).max() <= 1e-6  # averaged gradients keep the replicas identical
     assert abs(v0 - v1) < 1e-9  # epoch metrics are rank-averaged
+
+
+# ----------------------------------------------------------------------------- padded batches (captured fit)
+def test_padded_batches_layout_and_weights():
+    """training.PaddedBatches: real atoms first in molecule order, ghost atoms on the dummy molecule
+    spaced beyond the cutoff, weights that turn the weighted sums into the reference's mean losses."""
+    import torch
+    from torchmdnet.data import Data, collate
+    from torchmdnet.training import PaddedBatches, padded_losses
+    g = torch.Generator().manual_seed(0)
+    samples = []
+    for n in (5, 9, 3):
+        samples.append(Data(z=torch.randint(1, 10, (n,), generator=g), pos=torch.randn(n, 3, generator=g),
+                            y=torch.randn(1, generator=g), neg_dy=torch.randn(n, 3, generator=g)))
+    pb = PaddedBatches([16, 24, 32], max_molecules=4, cutoff=5.0)
+    b = pb.collate(samples)
+    ref = collate(samples)
+    assert b.capacity == 24 and b.n_atoms == 17 and b.n_mol == 3  # 17 atoms + >= 1 ghost
+    assert torch.equal(b.z[:17], ref.z) and torch.equal(b.pos[:17], ref.pos) and torch.equal(b.batch[:17], ref.batch)
+    assert (b.batch[17:] == 4).all() and (b.z[17:] == 1).all()
+    gp = b.pos[17:]
+    d = torch.cdist(gp.double(), torch.cat([ref.pos, gp]).double())
+    d[:, 17:].fill_diagonal_(1e9)
+    assert float(d.min()) > 5.0  # every ghost is alone within the cutoff
+    assert b.y.shape == (5, 1) and b.neg_dy.shape == (24, 3)
+    # weighted losses = the reference means over the real entries
+    pred = torch.randn(5, 1, generator=g)
+    nd = torch.randn(24, 3, generator=g)
+    ly, lf = padded_losses(pred, nd, b)
+    assert torch.allclose(ly, ((pred[:3] - ref.y.view(3, 1)) ** 2).mean())
+    assert torch.allclose(lf, ((nd[:17] - ref.neg_dy) ** 2).mean())
+    with pytest.raises(ValueError):
+        pb.collate(samples * 2)  # 6 molecules > 4
+
+
+def test_default_atom_buckets_cover_the_largest_batch():
+    import torch
+    from torchmdnet.data import Data
+    from torchmdnet.module import default_atom_buckets
+    ds = [Data(z=torch.ones(n, dtype=torch.long)) for n in (9, 12, 29, 17, 20) * 20]
+    b = default_atom_buckets(ds, 32)
+    assert b == sorted(set(b)) and b[-1] >= 29 * 32 + 1 and all(x % 32 == 0 for x in b)

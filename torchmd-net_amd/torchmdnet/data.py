@@ -159,18 +159,21 @@ class DataModule:
     def atomref(self):
         return self.dataset.get_atomref() if hasattr(self.dataset, "get_atomref") else None
 
-    def loader(self, stage):
-        if stage in self._loaders:
-            return self._loaders[stage]
+    def loader(self, stage, collate_fn=None):
+        """The stage's loader (cached); ``collate_fn`` replaces ``collate`` (e.g. the fixed-shape
+        ``training.PaddedBatches.collate`` of the captured training step)."""
+        key = (stage, collate_fn)
+        if key in self._loaders:
+            return self._loaders[key]
         ds = {"train": self.train_dataset, "val": self.val_dataset, "test": self.test_dataset}[stage]
         train = stage == "train"
         bs = self.hparams["batch_size"] if train else self.hparams.get("inference_batch_size",
                                                                        self.hparams["batch_size"])
         sampler = ShardSampler(len(ds), self.rank, self.world_size, shuffle=train, seed=self.hparams.get("seed", 0))
-        dl = torch.utils.data.DataLoader(ds, batch_size=bs, sampler=sampler, collate_fn=collate,
+        dl = torch.utils.data.DataLoader(ds, batch_size=bs, sampler=sampler, collate_fn=collate_fn or collate,
                                          num_workers=self.hparams.get("num_workers", 0),
                                          pin_memory=torch.cuda.is_available())
-        self._loaders[stage] = dl
+        self._loaders[key] = dl
         return dl
 
     def _standardize(self):

@@ -154,20 +154,69 @@ def _val_loss(metrics):
     return metrics.get("val_total_mse_loss", metrics.get("val_total_l1_loss"))
 
 
-def fit(lnnp, datamodule, epochs, device, group=None, test_interval=0, log=None, checkpoint=None):
+def default_atom_buckets(dataset, batch_size, n_probe=512, growth=1.125):
+    """Atom capacities of the padded training batches: geometric steps (``growth``) from a little
+    below the mean batch size to ``batch_size`` x the largest molecule seen in a probe of the dataset."""
+    import math
+    n = len(dataset)
+    step = max(1, n // n_probe)
+    sizes = [int(dataset[i].z.shape[0]) for i in range(0, n, step)]
+    mean, big = sum(sizes) / len(sizes), max(sizes)
+    lo, hi = int(0.85 * mean * batch_size), big * batch_size + 1
+    out, a = [], max(32, lo)
+    while True:
+        c = int(math.ceil(a / 32.0) * 32)
+        if not out or c > out[-1]:
+            out.append(c)
+        if c >= hi:
+            return out
+        a *= growth
+
+
+def fit(lnnp, datamodule, epochs, device, group=None, test_interval=0, log=None, checkpoint=None, graphed=False,
+        atom_buckets=None):
     """Epoch loop replacing Lightning's Trainer + DDPStrategy (scripts/train.py:126-202): per-rank
     shards, one fused gradient all-reduce per step, LR warm-up and ReduceLROnPlateau on val_loss,
     epoch metrics averaged over ranks; rank 0 writes a Lightning-layout checkpoint
-    (``{"state_dict": {"model.*": ...}, "hyper_parameters": ...}``, what ``load_model`` reads)."""
-    opt, sched = lnnp.configure_optimizers()
-    reduce = GradAllReduce(lnnp.model.parameters(), group)
+    (``{"state_dict": {"model.*": ...}, "hyper_parameters": ...}``, what ``load_model`` reads).
+
+    ``graphed``: every training step is ONE HIP-graph replay of the force-matching step on a padded batch
+    (training.PaddedGraphedTrainer; one capture per atom capacity of ``atom_buckets``, default
+    ``default_atom_buckets``); the same objective, EMA, warm-up and optimiser (fused AdamW)."""
+    hp = lnnp.hparams
+    if graphed:
+        from .training import PaddedBatches, PaddedGraphedTrainer
+        bs = datamodule.hparams["batch_size"]
+        if atom_buckets is None:
+            atom_buckets = default_atom_buckets(datamodule.train_dataset, bs)
+        rep = lnnp.model.representation_model
+        batches = PaddedBatches(atom_buckets, bs, float(rep.cutoff_upper))
+        trainer = PaddedGraphedTrainer(lnnp.model, batches, lr=hp.lr, weight_decay=hp.weight_decay,
+                                       y_weight=hp.y_weight, neg_dy_weight=hp.neg_dy_weight if hp.derivative else 0.0,
+                                       ema_alpha_y=hp.ema_alpha_y, ema_alpha_neg_dy=hp.ema_alpha_neg_dy,
+                                       lr_warmup_steps=hp.lr_warmup_steps, group=group)
+        opt = trainer.opt
+        sched = torch.optim.lr_scheduler.ReduceLROnPlateau(opt, "min", factor=hp.lr_factor, patience=hp.lr_patience,
+                                                           min_lr=hp.lr_min)
+        lnnp.graphed_trainer = trainer
+    else:
+        opt, sched = lnnp.configure_optimizers()
+        reduce = GradAllReduce(lnnp.model.parameters(), group)
     history = []
     for epoch in range(epochs):
         lnnp.current_epoch = epoch
-        train = datamodule.loader("train")
+        train = datamodule.loader("train", batches.collate if graphed else None)
         train.sampler.set_epoch(epoch)
         lnnp.model.train()
         for i, b in enumerate(train):
+            if graphed:
+                ly, lf, total = trainer.step(b)
+                for kind, v in (("y", ly), ("neg_dy", lf)):
+                    if getattr(hp, f"{kind}_weight") > 0:
+                        lnnp.losses["train"][kind]["mse_loss"].append(v.detach())
+                lnnp.losses["train"]["total"]["mse_loss"].append(total.detach())
+                lnnp.global_step = trainer.global_step
+                continue
             b = b.to(device, non_blocking=True)
             loss = lnnp.training_step(b, i)
             params = reduce.params
@@ -175,6 +224,8 @@ def fit(lnnp, datamodule, epochs, device, group=None, test_interval=0, log=None,
             check_pending_consumed()
             reduce()
             lnnp.optimizer_step(opt)
+        if graphed:
+            trainer.finish()
         lnnp.model.eval()
         for i, b in enumerate(datamodule.loader("val")):
             lnnp.validation_step(b.to(device, non_blocking=True), i, 0)
