@@ -46,12 +46,29 @@ class Custom(torch.utils.data.Dataset):
     def __len__(self):
         return len(self.index)
 
+    def _file(self, f):
+        """The memory maps / atom types of file group f, opened once per process (the loader's worker
+        processes each open their own on first use): a sample costs a few array copies, not four file
+        opens."""
+        mm = self.__dict__.setdefault("_mm", {})
+        if f not in mm:
+            mm[f] = (np.load(self.coordfiles[f], mmap_mode="r"),
+                     torch.from_numpy(np.load(self.embedfiles[f]).astype(np.int64)),
+                     np.load(self.energyfiles[f], mmap_mode="r") if self.has_energies else None,
+                     np.load(self.forcefiles[f], mmap_mode="r") if self.has_forces else None)
+        return mm[f]
+
+    def __getstate__(self):  # memory maps are per process
+        st = dict(self.__dict__)
+        st.pop("_mm", None)
+        return st
+
     def __getitem__(self, idx):
         f, k = self.index[idx]
-        d = Data(pos=torch.from_numpy(np.array(np.load(self.coordfiles[f], mmap_mode="r")[k])),
-                 z=torch.from_numpy(np.load(self.embedfiles[f]).astype(np.int64)))
+        coords, z, en, fo = self._file(f)
+        d = Data(pos=torch.from_numpy(np.array(coords[k])), z=z.clone())
         if self.has_energies:
-            d.y = torch.from_numpy(np.array(np.load(self.energyfiles[f], mmap_mode="r")[k]))
+            d.y = torch.from_numpy(np.array(en[k]))
         if self.has_forces:
-            d.neg_dy = torch.from_numpy(np.array(np.load(self.forcefiles[f], mmap_mode="r")[k]))
+            d.neg_dy = torch.from_numpy(np.array(fo[k]))
         return d
