@@ -721,8 +721,8 @@ def secondary_scripted(a, ws, rank, dev):
             "value": round(a.batch * ws * steps / el_s, 2), "unit": "molecules/s",
             "ms_per_step": round(1000 * el_s / steps, 4),
             "eager_unscripted_ms_per_step": round(1000 * el_e / steps, 4),
-            "path": "per-layer dispatcher ops (tmdnet::neighbor_graph, edge_geometry, nbr_embed, et_message) + "
-                    "ATen GEMMs / LayerNorm; the fused stack (et_stack.py) is eager-only"}
+            "path": "dispatcher ops (tmdnet::neighbor_graph, edge_geometry, nbr_embed) + the interaction layers as "
+                    "ONE tmdnet::et_stack operator (the eager stack's launches, dr-mode force backward)"}
 
 
 def secondary_water_box(a, ws, rank, dev):

@@ -76,6 +76,16 @@ def main():
             fused()
         torch.cuda.synchronize()
         return
+    if len(sys.argv) > 3 and sys.argv[3] == "fused_bwd_only":  # profiling: the fused backward alone
+        gx_, gv_ = torch.randn(n, H, device=dev), torch.randn(n, 3, H, device=dev)
+        bufs = [torch.empty(n, H, device=dev), torch.empty(n, H, device=dev), torch.empty(n, 3 * H, device=dev),
+                torch.empty(n, 3, H, device=dev), torch.empty(E, device=dev), torch.empty(E, 3, device=dev),
+                torch.empty(E, device=dev)]
+        for _ in range(6):
+            kernels.et_fused_bwd_launch(q, k, v, vec, r, C, u, fep, (mu, beta, cl, cu, 0), g, 8, gx_, gv_, *bufs,
+                                        accumulate=1 | 4)
+        torch.cuda.synchronize()
+        return
     unfused_msg()
     fused()
     torch.cuda.synchronize()

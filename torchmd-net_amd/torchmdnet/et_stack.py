@@ -403,6 +403,9 @@ def _forward_layers(meta, x, f, C, u, params, r=None, want_bwd=False):
             pkv = None
             if l == 0:
                 meta.fep_imgs = []
+            if not meta.planar:  # the image's rows are always in the planar [dk | dv_x | dv_1 | dv_2] order
+                one = _planar_perms(meta, x.device)[4]
+                dkv_w, dkv_b = dkv_w.index_select(0, one), dkv_b.index_select(0, one)
             meta.fep_imgs.append(kernels.fep_split(dkv_w, dkv_b))
             kernels.et_fused_fwd_launch(qkv[:, :H], qkv[:, H:2 * H], qkv[:, 2 * H:], vec, r, C, u,
                                         meta.fep_imgs[l], meta.rbf, meta.graph, meta.heads, xa, veca,
