@@ -142,38 +142,48 @@ template <int N, int I = 0, typename F> __device__ __forceinline__ void static_f
 // not bounded by 1): `dsc` = 2^(14 - sd) turns the weight's accumulator scale (which assumes the 2^14
 // of f) into the derivative's.  The edge-geometry kernel's formulas (edge_geom.hip basis()).
 template <int KS, bool DER>
-__device__ __forceinline__ void rbf_frags(int rbf, float rf, bool vf, float cl, float cu, float alpha,
-                                          const float* s_mu, const float* s_beta, int g, h8 (&A0)[KS],
-                                          h8 (&A1)[KS], h8 (&D0)[KS], h8 (&D1)[KS], float& dsc) {
+__device__ __forceinline__ void rbf_frags(int rbf, float rf, float cl, float cu, float alpha, const float* s_mu,
+                                          const float* s_beta, int g, h8 (&A0)[KS], h8 (&A1)[KS], h8 (&D0)[KS],
+                                          h8 (&D1)[KS], float& dsc) {
+  // hardware exp / cos / sin (v_exp_f32, v_cos_f32, v_sin_f32: ~1 ulp / ~2^-20 absolute): the library
+  // forms' range reduction and overflow branches were 40 % of the forward's VALU instructions.  An edge
+  // past the row needs no mask: its node gathers and cutoff are 0, so its terms vanish whatever f is.
   constexpr float kPi = 3.14159265358979323846f;
   const bool in = rf < cu;
-  const float cut0 = in ? 0.5f * (cosf(rf * kPi / cu) + 1.f) : 0.f;
-  const float dcut0 = (DER && in) ? -0.5f * sinf(rf * kPi / cu) * kPi / cu : 0.f;
-  const float ue = expf(alpha * (cl - rf));
+  const float th = rf * (kPi / cu);
+  const float cut0 = in ? 0.5f * (__cosf(th) + 1.f) : 0.f;
+  const float dcut0 = (DER && in) ? -0.5f * (kPi / cu) * __sinf(th) : 0.f;
+  const float ue = __expf(alpha * (cl - rf));
   float df[KS][8];
+  auto put = [&](int ks, int j, float f) {
+    const float x = f * kFScale;
+    const _Float16 hi = (_Float16)x;
+    A0[ks][j] = hi;
+    A1[ks][j] = (_Float16)(x - (float)hi);
+  };
+  if (rbf == TMDNET_RBF_EXPNORM) {  // (wave-uniform branch: one loop or the other)
 #pragma unroll
-  for (int ks = 0; ks < KS; ++ks)
+    for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int kk = 32 * ks + 8 * g + j;
-      float f, d = 0.f;
-      if (rbf == TMDNET_RBF_EXPNORM) {
+      for (int j = 0; j < 8; ++j) {
+        const int kk = 32 * ks + 8 * g + j;
         const float z = ue - s_mu[kk], b = s_beta[kk];
-        const float gg = expf(-b * z * z);
-        f = cut0 * gg;
-        if (DER) d = dcut0 * gg + cut0 * gg * (2.f * b * z * alpha * ue);  // d/dr: du = -alpha ue
-      } else {
-        const float z = rf - s_mu[kk], co = s_beta[kk];
-        f = expf(co * z * z);
-        if (DER) d = f * 2.f * co * z;
+        const float gg = __expf(-b * z * z);
+        put(ks, j, cut0 * gg);
+        if (DER) df[ks][j] = gg * (dcut0 + cut0 * (2.f * b * alpha) * z * ue);  // d/dr: du = -alpha ue
       }
-      f = vf ? f : 0.f;
-      if (DER) df[ks][j] = vf ? d : 0.f;
-      const float x = f * kFScale;
-      const _Float16 hi = (_Float16)x;
-      A0[ks][j] = hi;
-      A1[ks][j] = (_Float16)(x - (float)hi);
-    }
+  } else {
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int kk = 32 * ks + 8 * g + j;
+        const float z = rf - s_mu[kk], co = s_beta[kk];
+        const float f = __expf(co * z * z);
+        put(ks, j, f);
+        if (DER) df[ks][j] = f * (2.f * co) * z;
+      }
+  }
   if constexpr (DER) {
     float mx = 0.f;
 #pragma unroll
@@ -185,11 +195,12 @@ __device__ __forceinline__ void rbf_frags(int rbf, float rf, bool vf, float cl, 
     if (mx > 0.f) frexpf(mx, &ex);
     const int sd = mx > 0.f ? 14 - ex : 0;
     dsc = ldexpf(1.f, 14 - sd);
+    const float sc = ldexpf(1.f, sd);
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const float x = ldexpf(df[ks][j], sd);
+        const float x = df[ks][j] * sc;
         const _Float16 hi = (_Float16)x;
         D0[ks][j] = hi;
         D1[ks][j] = (_Float16)(x - (float)hi);
@@ -365,25 +376,29 @@ __global__ __launch_bounds__(NW * 64, 1) void k_fwd(Fwd P) {
   __shared__ __attribute__((aligned(16))) float s_sc[kD];
   __shared__ __attribute__((aligned(16))) float s_b[kD];
   __shared__ float s_mu[R], s_beta[R];
+  __shared__ __attribute__((aligned(16))) float s_q[NW][16 * HPW];  // the item's q channels (per wave)
   __shared__ int s_next;
   load_image<KS, NW * 64>(w, s_sc, s_b, s_mu, s_beta, P.img, P.wsc, P.bias, P.mu, P.beta, P.rbf);
   if (threadIdx.x == 0) s_next = 0;
   __syncthreads();
   const Work W = work_range<G>(P.n);
-  const int lane = lane_id(), c = lane & 15, g = lane >> 4;
+  const int lane = lane_id(), c = lane & 15, g = lane >> 4, wid = threadIdx.x >> 6;
   const rsrc_t Rk = make_rsrc(P.k, (unsigned)P.n * P.ldk * 4u), Rv = make_rsrc(P.v, (unsigned)P.n * P.ldv * 4u);
   const rsrc_t Rw = make_rsrc(P.vec, P.vec ? (unsigned)P.n * 3u * H * 4u : 0u);
+  float* sq = s_q[wid];
   for (;;) {
     const int it = next_item(&s_next);
     if (it >= W.items) break;
     const int t = W.n0 + it / G, h0 = (it % G) * HPW;
     const int rb = min(P.row_ptr[t], P.cap), re = min(P.row_ptr[t + 1], P.cap);
-    f4 qv[HPW], ax[HPW], a0[HPW], a1[HPW], a2[HPW];
+    __builtin_amdgcn_wave_barrier();  // the previous item's reads of sq are done (in-order LDS)
+    if (lane < 4 * HPW)
+      *reinterpret_cast<f4*>(sq + 4 * lane) = *reinterpret_cast<const f4*>(P.q + (size_t)t * P.ldq + 16 * h0 + 4 * lane);
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    f4 ax[HPW], a0[HPW], a1[HPW], a2[HPW];
 #pragma unroll
-    for (int hh = 0; hh < HPW; ++hh) {
-      qv[hh] = *reinterpret_cast<const f4*>(P.q + (size_t)t * P.ldq + 16 * (h0 + hh) + 4 * g);
-      ax[hh] = a0[hh] = a1[hh] = a2[hh] = f4{0.f, 0.f, 0.f, 0.f};
-    }
+    for (int hh = 0; hh < HPW; ++hh) ax[hh] = a0[hh] = a1[hh] = a2[hh] = f4{0.f, 0.f, 0.f, 0.f};
     for (int base = rb; base < re; base += 16) {
       const int e = base + c;
       const bool ok = e < re;
@@ -400,7 +415,7 @@ __global__ __launch_bounds__(NW * 64, 1) void k_fwd(Fwd P) {
       TMD_DCHECK(s >= 0 && s < P.n);
       h8 B0[KS], B1[KS], D0[KS], D1[KS];
       float dsc = 1.f;
-      rbf_frags<KS, false>(P.rbf, rf, ok, P.cl, P.cu, P.alpha, s_mu, s_beta, g, B0, B1, D0, D1, dsc);
+      rbf_frags<KS, false>(P.rbf, rf, P.cl, P.cu, P.alpha, s_mu, s_beta, g, B0, B1, D0, D1, dsc);
       // an edge past the row gathers from beyond the resources' ranges: its k, v and vec are 0, so its
       // terms vanish without masks (C = 0 as well)
       const int ok_ = ok ? (s * P.ldk + 4 * g) * 4 : kOOB;
@@ -411,18 +426,22 @@ __global__ __launch_bounds__(NW * 64, 1) void k_fwd(Fwd P) {
       const char* wt = reinterpret_cast<const char*>(w);
       // head hh + 1's gathers are in flight during head hh's MFMAs and math (two register sets); the
       // scheduler may not mix heads otherwise (one head's temporaries live at a time)
+      // head hh + 1's gathers are in flight during head hh's MFMAs and math (two register sets)
+      Gat X[2];
+      gather_kvw<PL>(X[0], Rk, Rv, Rw, ok_, ov_, ow_, h0);
       static_for<HPW>([&](auto hc) {
         constexpr int hh = decltype(hc)::value;
         const int h = h0 + hh;
-        Gat G;
-        gather_kvw<PL>(G, Rk, Rv, Rw, ok_, ov_, ow_, h);
+        if constexpr (hh + 1 < HPW) gather_kvw<PL>(X[(hh + 1) & 1], Rk, Rv, Rw, ok_, ov_, ow_, h + 1);
+        const Gat& G = X[hh & 1];
         const f4 pk = block_pre<KS>(wt, wb, s_sc, s_b, h, B0, B1, g);
         const f4 px = block_pre<KS>(wt, wb, s_sc, s_b, 8 + h, B0, B1, g);
         const f4 p1 = block_pre<KS>(wt, wb, s_sc, s_b, 16 + h, B0, B1, g);
         const f4 p2 = block_pre<KS>(wt, wb, s_sc, s_b, 24 + h, B0, B1, g);
+        const f4 qv = *reinterpret_cast<const f4*>(sq + 16 * hh + 4 * g);
         float part = 0.f;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) part += qv[hh][i] * G.kk[i] * Silu<float>(pk[i]).s;
+        for (int i = 0; i < 4; ++i) part += qv[i] * G.kk[i] * Silu<float>(pk[i]).s;
         const float att = gsum(part);
         const float a = Silu<float>(att).s * Ce;
 #pragma unroll
@@ -553,7 +572,7 @@ __global__ __launch_bounds__(NW * 64, 1) void k_bwd_dst(Bwd P) {
       TMD_DCHECK(s >= 0 && s < P.n);
       h8 B0[KS], B1[KS], D0[KS], D1[KS];
       float dsc = 1.f;
-      rbf_frags<KS, true>(P.rbf, rf, ok, P.cl, P.cu, P.alpha, s_mu, s_beta, g, B0, B1, D0, D1, dsc);
+      rbf_frags<KS, true>(P.rbf, rf, P.cl, P.cu, P.alpha, s_mu, s_beta, g, B0, B1, D0, D1, dsc);
       const int ok_ = ok ? (s * P.ldk + 4 * g) * 4 : kOOB;
       const int ov_ = ok ? (s * P.ldv + 4 * g) * 4 : kOOB;
       const int ow_ = ok ? (s * 3 * H + 4 * g) * 4 : kOOB;
@@ -706,7 +725,7 @@ __global__ __launch_bounds__(NW * 64, 1) void k_bwd_src(Bwd P) {
       TMD_DCHECK(m >= 0 && m < P.n);
       h8 B0[KS], B1[KS], D0[KS], D1[KS];
       float dsc = 1.f;
-      rbf_frags<KS, false>(P.rbf, rf, ok, P.cl, P.cu, P.alpha, s_mu, s_beta, g, B0, B1, D0, D1, dsc);
+      rbf_frags<KS, false>(P.rbf, rf, P.cl, P.cu, P.alpha, s_mu, s_beta, g, B0, B1, D0, D1, dsc);
       const int oq = ok ? (m * P.ldq + 4 * g) * 4 : kOOB;
       const int ox = ok ? (m * H + 4 * g) * 4 : kOOB;
       const int og = ok ? (m * 3 * H + 4 * g) * 4 : kOOB;
