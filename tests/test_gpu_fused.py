@@ -114,6 +114,7 @@ def test_fused_c2_molecules_vs_oracle_and_unfused(planar, monkeypatch):
     orig, origb = kernels.et_fused_fwd_launch, kernels.et_fused_bwd_launch
     monkeypatch.setattr(kernels, "et_fused_fwd_launch", lambda *a, **k: (calls.append("f"), orig(*a, **k))[1])
     monkeypatch.setattr(kernels, "et_fused_bwd_launch", lambda *a, **k: (calls.append("b"), origb(*a, **k))[1])
+    monkeypatch.setattr(et_stack, "FEP_MIN_EDGES", 0)
     if planar:
         monkeypatch.setattr(et_stack, "PLANAR_MIN_EDGES", 0)
     args = yaml_args("equivariant-transformer", embedding_dimension=128, num_layers=8, num_rbf=64, num_heads=8,

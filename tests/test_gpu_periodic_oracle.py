@@ -87,17 +87,29 @@ def _cfg(args, L):
     return cfg
 
 
-def test_et_periodic_box_vs_oracle(large_switches, monkeypatch):
+@pytest.mark.parametrize("path", ["rows", "fused"])
+def test_et_periodic_box_vs_oracle(path, large_switches, monkeypatch):
     """ET (128 ch, 8 layers, 64 RBF, 8 heads, cutoff 5) on a 2000-atom periodic water box with every
-    large-system switch forced: energy and forces vs the fp64 oracle; the energy-only call runs the
-    fused-projection forward and matches too."""
-    from torchmdnet import kernels
+    large-system switch forced: energy and forces vs the fp64 oracle, through the pair-row path (merged
+    dr-mode backward ``k_bwd_merged``) and through the fused-projection kernels (et_fused.hip, the C5
+    default); the energy-only call runs the fused forward and matches too."""
+    from torchmdnet import et_stack, kernels
+    fused_b = []
+    if path == "fused":
+        monkeypatch.setattr(et_stack, "FEP_MIN_EDGES", 0)
+        orig_b = kernels.et_fused_bwd_launch
+        monkeypatch.setattr(kernels, "et_fused_bwd_launch", lambda *a, **k: (fused_b.append(1), orig_b(*a, **k))[1])
+    else:
+        monkeypatch.setattr(et_stack, "FEP", "0")
     z, pos, batch, L = _water_box(2000)
     m = _et()
     y_ref, f_ref = O.energy_forces(m.state_dict(), _cfg(_args(), L), z, pos, batch)
     m = _periodic(m.to(DEV), L)
     y, f = m(z.to(DEV), pos.float().to(DEV), batch.to(DEV))
-    assert len(large_switches) == 8, "the dr-mode force backward did not run per layer"
+    if path == "rows":
+        assert len(large_switches) == 8, "the dr-mode force backward did not run per layer"
+    else:
+        assert len(fused_b) == 8, "the fused force backward did not run per layer"
     assert _rel(y, y_ref) < TOL, _rel(y, y_ref)
     assert _rel(f, f_ref) < TOL, _rel(f, f_ref)
     # energy only (no backward follows): the fused dk/dv projection forward
@@ -109,6 +121,8 @@ def test_et_periodic_box_vs_oracle(large_switches, monkeypatch):
         return orig(*a, **k)
 
     monkeypatch.setattr(kernels, "et_fused_fwd_launch", counting)
+    monkeypatch.setattr(et_stack, "FEP", "auto")
+    monkeypatch.setattr(et_stack, "FEP_MIN_EDGES", 0)
     m.derivative = False
     with torch.no_grad():
         y0, _ = m(z.to(DEV), pos.float().to(DEV), batch.to(DEV))

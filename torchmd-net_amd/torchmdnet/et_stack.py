@@ -127,6 +127,9 @@ PAIR_ROWS = True
 # (C5: 2.8 GB per layer, read back once per direction by the unfused kernels; the force pass's
 # d(dk,dv)/dr rows likewise).  TMDNET_FEP=0 turns it off.
 FEP = os.environ.get("TMDNET_FEP", "auto")
+# ... on graphs from this many edges (below it -- the QM9 batches -- the per-layer kernels are latency-bound:
+# C2 measured 1.39 ms fused vs 0.90 ms unfused per energy + force step, r04)
+FEP_MIN_EDGES = int(os.environ.get("TMDNET_FEP_MIN_EDGES", "131072"))
 # When a backward can follow (grad enabled), how it gets the projection: "fused" (default) = the
 # force-pass (dr mode) backward is fused the same way (d pre / d r formed on the MFMA in-kernel); a
 # backward that needs the projection rows (parameter gradients, the recorded force pass of force-matching
@@ -1351,7 +1354,8 @@ def et_stack(layers, x, graph, f, C, u, rbf=None, out_norm=None, f_pairs=None):
     if rbf is not None and D:
         r, mu, beta, cl, cu, rbf_type = rbf
         meta.rbf = (mu.detach(), beta.detach(), float(cl), float(cu), int(rbf_type))
-        meta.fep = (FEP not in ("0", "off") and hk and hv and x.is_cuda and meta.acts == 0
+        meta.fep = (FEP not in ("0", "off") and graph.n_edges >= FEP_MIN_EDGES and hk and hv and x.is_cuda
+                    and meta.acts == 0
                     and kernels.fep_supported(H, heads, mu.shape[0], x.dtype) and r.dtype == x.dtype)
     x = x.contiguous()
     f = f.contiguous() if (hk or hv) else None
