@@ -473,10 +473,11 @@ def fused_projection_probe(launch, E, N, H, reps, dev, R=64):
     mu = torch.linspace(start, 1.0, R, device=dev)
     beta = torch.full((R,), (2.0 / R * (1 - start)) ** -2, device=dev)
     fep = kernels.fep_split(W, b)
+    frag = kernels.fep_frag_set(g, r, (mu, beta, 0.0, 5.0, 0), (launch.pair_row, launch.pair_edge))
     xo, vo = torch.empty(N, H, device=dev), torch.empty(N, 3, H, device=dev)
 
     def run():
-        kernels.et_fused_fwd_launch(q, k, v, vec, r, C, u, fep, (mu, beta, 0.0, 5.0, 0), g, 8, xo, vo, flags=4)
+        kernels.et_fused_fwd_launch(q, k, v, vec, C, u, fep, frag, g, 8, xo, vo, flags=4)
     for _ in range(5):
         run()
     torch.cuda.synchronize()

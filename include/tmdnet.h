@@ -560,45 +560,56 @@ int tmdnet_proj_f32(int M, int N, int K, const void* A, int lda, const void* Wp,
                     const void* bias, void* C, int ldc, void* stream);
 
 /* The ET message with the dk/dv projection FUSED in (reference torchmd_et.py:282-291 + :314-347, the
- * RBF of models/utils.py:272-344 evaluated in-kernel): tmdnet_et_message_fwd's outputs without the
- * projection rows.  Per 16-edge tile the RBF values of the distances r[e] are formed in registers and
- * multiplied on the fp16 MFMA by the layer's weight, held in LDS for the whole launch as the image made
- * by tmdnet_fep_split_f32 (two fp16 pieces per value after exact power-of-two scaling: fp32-GEMM
- * accuracy).
+ * RBF of models/utils.py:272-344): tmdnet_et_message_fwd's outputs without the projection rows.  Per
+ * 16-edge tile the fragments of the RBF values of the edges are multiplied on the fp16 MFMA by the
+ * layer's weight, held in LDS for the whole launch as the image made by tmdnet_fep_split_f32 (two fp16
+ * pieces per value after exact power-of-two scaling: fp32-GEMM accuracy).
  *   tmdnet_fep_split_f32: W [D][R] (ldw) = the layer's [dk | dv] rows in the planar order (dk, then the
  *     x, v1, v2 H-blocks of dv), bias [D] (nullable) -> img (tmdnet_fep_image_bytes(D, R), 16-byte
  *     aligned), wsc [D] (accumulator scale per row), bias_out [D].
+ *   tmdnet_fep_frags_f32: the RBF (and d RBF / d r) MFMA fragments of `rows` projection rows (pair rows)
+ *     at distances r_rows [rows]: frags [rows][4][R] fp16 (tmdnet_fep_frags_bytes; f and f' in two pieces
+ *     each), dscale [rows] (the derivative's power-of-two scale).  mu / beta: the RBF means / betas
+ *     (gauss: offsets / coeff[0]).  Once per evaluation: every layer reads the same fragments.
  *   tmdnet_et_fused_fwd_f32: fp32 only; H = 128, heads = 8 (d = 16), R = 32 or 64, both projections
- *     present (distance_influence "both"), SiLU activations; v in the planar layout when flags carries
- *     TMDNET_ET_V_PLANAR, else the reference's per-head [x|v1|v2] interleave; q / k / v / vec_in / x_out /
- *     vec_out 16-byte aligned with leading dimensions % 4 == 0; vec_in nullable (layer 0); mu / beta: the
- *     RBF means / betas (gauss: offsets / coeff[0]).  Else TMDNET_UNSUPPORTED.  One workgroup per CU
- *     (its LDS), deterministic, no atomics on outputs. */
+ *     present (distance_influence "both"), SiLU activations; edge e reads fragment row frag_rows[e] (its
+ *     pair row; n_frag_rows rows); v in the planar layout when flags carries TMDNET_ET_V_PLANAR, else the
+ *     reference's per-head [x|v1|v2] interleave; q / k / v / vec_in / x_out / vec_out / frags 16-byte
+ *     aligned with leading dimensions % 4 == 0; vec_in nullable (layer 0).  Else TMDNET_UNSUPPORTED.  One
+ *     workgroup per CU (its LDS), deterministic, no atomics on outputs. */
 size_t tmdnet_fep_image_bytes(int D, int R);
 int tmdnet_fep_split_f32(int D, int R, const void* W, int ldw, const void* bias, void* img, void* wsc,
                          void* bias_out, void* stream);
+size_t tmdnet_fep_frags_bytes(long long rows, int R);
+int tmdnet_fep_frags_f32(long long rows, int R, const void* r_rows, const void* mu, const void* beta,
+                         double cutoff_lower, double cutoff_upper, int rbf_type, void* frags, void* dscale,
+                         void* stream);
 int tmdnet_et_fused_fwd_f32(int n_nodes, int hidden, int heads, int num_rbf, const int32_t* row_ptr,
                             const int32_t* src, int max_pairs, const void* q, int ld_q, const void* k, int ld_k,
-                            const void* v, int ld_v, const void* vec_in, const void* dist, const void* cutoff,
-                            const void* unit, const void* img, const void* wsc, const void* bias, const void* mu,
-                            const void* beta, double cutoff_lower, double cutoff_upper, int rbf_type,
-                            void* x_out, void* vec_out, int flags, void* stream);
+                            const void* v, int ld_v, const void* vec_in, const void* cutoff, const void* unit,
+                            const int32_t* frag_rows, const void* frags, long long n_frag_rows, const void* img,
+                            const void* wsc, const void* bias, void* x_out, void* vec_out, int flags, void* stream);
 
 /* The fused message's first-order backward for the force pass ("dr mode", reference: the autograd of
  * torchmd_et.py:282-291, :314-347 through f = rbf(r)): d pre / d r = W f'(r) is formed on the MFMA per
- * tile beside the projection (both from the tmdnet_fep_split_f32 image), and the projection gradient is
- * contracted with it in registers: gdist[e] = <g_pre, d pre / d r>.  Outputs as tmdnet_et_message_bwd in
- * dr mode (destination pass: gq, gcut, gunit, gdist; source pass over the reversed edges: gk, gv (v's
- * layout), gvec_in), with its accumulate bits (TMDNET_ACC_VEC_RESIDUAL / _EDGE / _GRADS, and
- * TMDNET_ET_V_PLANAR for the layout).  Same envelope as tmdnet_et_fused_fwd_f32; the gradient buffers
- * 16-byte aligned; requires a pair-symmetric edge list (tmdnet_et_message_bwd's precondition). */
+ * tile beside the projection (both from the tmdnet_fep_split_f32 image and the tmdnet_fep_frags_f32
+ * fragments), and the projection gradient is contracted with it in registers: gdist[e] = <g_pre,
+ * d pre / d r>.  Outputs as tmdnet_et_message_bwd in dr mode (destination pass: gq, gcut, gunit, gdist;
+ * source pass over the reversed edges: gk, gv (v's layout), gvec_in), with its accumulate bits
+ * (TMDNET_ACC_VEC_RESIDUAL / _EDGE / _GRADS, and TMDNET_ET_V_PLANAR for the layout); rows
+ * [row_ptr[n], max_pairs) of gcut / gunit / gdist are set to 0.  workspace: tmdnet_et_fused_bwd_workspace_bytes
+ * (max_pairs) bytes (the per-head-slice edge sums; 0 = none needed).  Same envelope as
+ * tmdnet_et_fused_fwd_f32; the gradient buffers 16-byte aligned; requires a pair-symmetric edge list
+ * (tmdnet_et_message_bwd's precondition). */
+size_t tmdnet_et_fused_bwd_workspace_bytes(int max_pairs);
 int tmdnet_et_fused_bwd_f32(int n_nodes, int hidden, int heads, int num_rbf, const int32_t* row_ptr,
                             const int32_t* src, int max_pairs, const void* q, int ld_q, const void* k, int ld_k,
-                            const void* v, int ld_v, const void* vec_in, const void* dist, const void* cutoff,
-                            const void* unit, const void* img, const void* wsc, const void* bias, const void* mu,
-                            const void* beta, double cutoff_lower, double cutoff_upper, int rbf_type,
-                            const void* grad_x, const void* grad_vec, void* gq, void* gk, void* gv, void* gvec_in,
-                            void* gcut, void* gunit, void* gdist, int accumulate, void* stream);
+                            const void* v, int ld_v, const void* vec_in, const void* cutoff, const void* unit,
+                            const int32_t* frag_rows, const void* frags, const void* dscale, long long n_frag_rows,
+                            const void* img, const void* wsc, const void* bias, const void* grad_x,
+                            const void* grad_vec, void* gq, void* gk, void* gv, void* gvec_in, void* gcut,
+                            void* gunit, void* gdist, int accumulate, void* workspace, size_t workspace_bytes,
+                            void* stream);
 
 /* Energy + force MSE training loss (reference LNNP.step, module.py:130-179, mean reductions):
  *   out[0] = w1 * mean((a1 - b1)^2) + w2 * mean((a2 - b2)^2)   over n1 / n2 elements (one launch),

@@ -258,3 +258,47 @@ def test_graphed_train_step_skips_overflowing_step():
     gtr.step(pos=pos)  # back in range: updates again
     assert any(not torch.equal(a, p.detach()) for a, p in zip(before, m.parameters()))
     gtr.release()
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_graph_capture_of_the_large_system_path(fused, monkeypatch):
+    """the renumbered large-system path (Morton renumbering, cell list in a periodic box,
+    planar rows, and -- fused -- the fused-projection kernels, or the pair-row path with the merged dr
+    backward) captured in one HIP graph: replays on fresh coordinates equal eager evaluations."""
+    from conftest import yaml_args
+    from torchmdnet import et_stack, kernels
+    from torchmdnet.graphs import GraphedEnergyForces
+    from torchmdnet.models.model import create_model
+    monkeypatch.setattr(kernels, "REORDER_MIN_ATOMS", 0)
+    monkeypatch.setattr(et_stack, "PLANAR_MIN_EDGES", 0)
+    if fused:
+        monkeypatch.setattr(et_stack, "FEP_MIN_EDGES", 0)
+    else:
+        monkeypatch.setattr(et_stack, "FEP", "0")
+    prev = kernels.set_tuning(kernels.TUNE_ET_MERGED_MIN_NODES, 0)
+    try:
+        torch.manual_seed(0)
+        m = create_model(yaml_args("equivariant-transformer", embedding_dimension=128, num_layers=3, num_rbf=64,
+                                   num_heads=8, max_num_neighbors=128, derivative=True)).to(DEV)
+        n = 3000
+        g = torch.Generator().manual_seed(5)
+        L = (n / 0.1003) ** (1.0 / 3.0)
+        pos = (torch.rand(n, 3, generator=g, dtype=torch.float64) * L).float().to(DEV)
+        z = torch.tensor([8, 1, 1], dtype=torch.long).repeat(n // 3 + 1)[:n].to(DEV)
+        batch = torch.zeros(n, dtype=torch.long, device=DEV)
+        d = m.representation_model.distance
+        d.box = torch.eye(3, dtype=torch.float32) * L
+        d.use_periodic = True
+        d.strategy = "cell"
+        gm = GraphedEnergyForces(m, z, pos, batch)
+        for step in range(3):
+            p = pos + 0.05 * torch.randn(pos.shape, generator=torch.Generator().manual_seed(step)).to(DEV)
+            y, f = gm(p)
+            y, f = y.clone(), f.clone()
+            ye, fe = m(z, p.clone(), batch)
+            assert float((y - ye).abs().max() / ye.abs().max()) < 1e-5
+            assert float((f - fe).abs().max() / fe.abs().max()) < 1e-5
+        gm.check_capacity()
+        gm.release()
+    finally:
+        kernels.set_tuning(kernels.TUNE_ET_MERGED_MIN_NODES, prev)

@@ -67,9 +67,10 @@ def main():
                                       flags=4, pk_rows=pair_row)
 
     fep = kernels.fep_split(W, b)
+    frag = kernels.fep_frag_set(g, r, (mu, beta, cl, cu, 0), (pair_row, pair_edge))
 
     def fused():
-        kernels.et_fused_fwd_launch(q, k, v, vec, r, C, u, fep, (mu, beta, cl, cu, 0), g, 8, xo1, vo1, flags=4)
+        kernels.et_fused_fwd_launch(q, k, v, vec, C, u, fep, frag, g, 8, xo1, vo1, flags=4)
 
     if len(sys.argv) > 3 and sys.argv[3] == "fused_only":  # profiling: the fused launches alone
         for _ in range(10):
@@ -82,7 +83,7 @@ def main():
                 torch.empty(n, 3, H, device=dev), torch.empty(E, device=dev), torch.empty(E, 3, device=dev),
                 torch.empty(E, device=dev)]
         for _ in range(6):
-            kernels.et_fused_bwd_launch(q, k, v, vec, r, C, u, fep, (mu, beta, cl, cu, 0), g, 8, gx_, gv_, *bufs,
+            kernels.et_fused_bwd_launch(q, k, v, vec, C, u, fep, frag, g, 8, gx_, gv_, *bufs,
                                         accumulate=1 | 4)
         torch.cuda.synchronize()
         return
@@ -132,7 +133,7 @@ def main():
 
     def fused_bwd():
         gq, gk, gv, gw, gC, gu, gr = outs[1]
-        kernels.et_fused_bwd_launch(q, k, v, vec, r, C, u, fep, (mu, beta, cl, cu, 0), g, 8, gx, gvec, gq, gk, gv,
+        kernels.et_fused_bwd_launch(q, k, v, vec, C, u, fep, frag, g, 8, gx, gvec, gq, gk, gv,
                                     gw, gC, gu, gr, accumulate=1 | 4)
 
     unfused_bwd()

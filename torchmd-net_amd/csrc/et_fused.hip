@@ -137,74 +137,68 @@ template <int N, int I = 0, typename F> __device__ __forceinline__ void static_f
   }
 }
 
-// The RBF tile as the MFMA's B operand: lane (c, g) holds edge c's values k = 32 ks + 8 g + j (two fp16
-// pieces of f * 2^14) and, DER, those of d f / d r with the edge's own power-of-two scale 2^sd (|f'| is
-// not bounded by 1): `dsc` = 2^(14 - sd) turns the weight's accumulator scale (which assumes the 2^14
-// of f) into the derivative's.  The edge-geometry kernel's formulas (edge_geom.hip basis()).
-template <int KS, bool DER>
-__device__ __forceinline__ void rbf_frags(int rbf, float rf, float cl, float cu, float alpha, const float* s_mu,
-                                          const float* s_beta, int g, h8 (&A0)[KS], h8 (&A1)[KS], h8 (&D0)[KS],
-                                          h8 (&D1)[KS], float& dsc) {
-  // hardware exp / cos / sin (v_exp_f32, v_cos_f32, v_sin_f32: ~1 ulp / ~2^-20 absolute): the library
-  // forms' range reduction and overflow branches were 40 % of the forward's VALU instructions.  An edge
-  // past the row needs no mask: its node gathers and cutoff are 0, so its terms vanish whatever f is.
+// The RBF tile as the MFMA's B operand, PRECOMPUTED once per projection row (pair row) and evaluation
+// (every layer shares it): row p of the fragment buffer holds [B0 | B1 | D0 | D1], R fp16 each -- the
+// two pieces of f(r_p) * 2^14 and of f'(r_p) * 2^sd_p with the row's own power-of-two scale
+// (|f'| is not bounded by 1; dscale[p] = 2^(14 - sd_p) turns the weight's accumulator scale, which
+// assumes the 2^14 of f, into the derivative's).  A lane of the edge kernels loads its edge's
+// 8-value chunk k = 32 ks + 8 g .. + 7 of each piece: one 16-byte load.  The edge-geometry kernel's
+// formulas (edge_geom.hip basis()).
+template <int KS>
+__global__ __launch_bounds__(256) void k_frags(long long rows, const float* __restrict__ r,
+                                               const float* __restrict__ mu, const float* __restrict__ beta,
+                                               int rbf, float cl, float cu, float alpha, _Float16* __restrict__ fr,
+                                               float* __restrict__ dscale) {
+  // R lanes per row (lane = k): coalesced 2-byte stores, the derivative's max a lane-group reduction
+  constexpr int R = 32 * KS;
   constexpr float kPi = 3.14159265358979323846f;
+  const long long p = (long long)blockIdx.x * (256 / R) + threadIdx.x / R;
+  const int k = threadIdx.x % R;
+  const bool live = p < rows;
+  const float rf = live ? r[p] : 0.f;
   const bool in = rf < cu;
-  const float th = rf * (kPi / cu);
-  const float cut0 = in ? 0.5f * (__cosf(th) + 1.f) : 0.f;
-  const float dcut0 = (DER && in) ? -0.5f * (kPi / cu) * __sinf(th) : 0.f;
-  const float ue = __expf(alpha * (cl - rf));
-  float df[KS][8];
-  auto put = [&](int ks, int j, float f) {
-    const float x = f * kFScale;
-    const _Float16 hi = (_Float16)x;
-    A0[ks][j] = hi;
-    A1[ks][j] = (_Float16)(x - (float)hi);
-  };
-  if (rbf == TMDNET_RBF_EXPNORM) {  // (wave-uniform branch: one loop or the other)
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int kk = 32 * ks + 8 * g + j;
-        const float z = ue - s_mu[kk], b = s_beta[kk];
-        const float gg = __expf(-b * z * z);
-        put(ks, j, cut0 * gg);
-        if (DER) df[ks][j] = gg * (dcut0 + cut0 * (2.f * b * alpha) * z * ue);  // d/dr: du = -alpha ue
-      }
+  const float cut0 = in ? 0.5f * (cosf(rf * kPi / cu) + 1.f) : 0.f;
+  const float dcut0 = in ? -0.5f * sinf(rf * kPi / cu) * kPi / cu : 0.f;
+  const float ue = expf(alpha * (cl - rf));
+  float f, d;
+  if (rbf == TMDNET_RBF_EXPNORM) {
+    const float z = ue - mu[k], b = beta[k];
+    const float gg = expf(-b * z * z);
+    f = cut0 * gg;
+    d = dcut0 * gg + cut0 * gg * (2.f * b * z * alpha * ue);  // d/dr: du = -alpha ue
   } else {
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int kk = 32 * ks + 8 * g + j;
-        const float z = rf - s_mu[kk], co = s_beta[kk];
-        const float f = __expf(co * z * z);
-        put(ks, j, f);
-        if (DER) df[ks][j] = f * (2.f * co) * z;
-      }
+    const float z = rf - mu[k], co = beta[0];
+    f = expf(co * z * z);
+    d = f * 2.f * co * z;
   }
-  if constexpr (DER) {
-    float mx = 0.f;
+  float mx = fabsf(d);
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks)
+  for (int o = R / 2; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+  if (!live) return;
+  int ex = 0;
+  if (mx > 0.f) frexpf(mx, &ex);
+  const int sd = mx > 0.f ? 14 - ex : 0;
+  if (k == 0) dscale[p] = ldexpf(1.f, 14 - sd);
+  _Float16* o = fr + p * 4 * R;
+  const float x = f * kFScale;
+  const _Float16 hi = (_Float16)x;
+  o[k] = hi;
+  o[R + k] = (_Float16)(x - (float)hi);
+  const float y = ldexpf(d, sd);
+  const _Float16 yh = (_Float16)y;
+  o[2 * R + k] = yh;
+  o[3 * R + k] = (_Float16)(y - (float)yh);
+}
+
+// the lane's B fragments (piece 0 / 1 at byte offsets 0 / 2R of section `sec`) of its edge's frag row
+template <int KS>
+__device__ __forceinline__ void load_frags(rsrc_t Rf, int fo, int g, int sec, h8 (&b0)[KS], h8 (&b1)[KS]) {
+  constexpr int R = 32 * KS;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) mx = fmaxf(mx, fabsf(df[ks][j]));
-    mx = gmax(mx);  // over the edge's 4 lane groups (its 64 k)
-    int ex = 0;
-    if (mx > 0.f) frexpf(mx, &ex);
-    const int sd = mx > 0.f ? 14 - ex : 0;
-    dsc = ldexpf(1.f, 14 - sd);
-    const float sc = ldexpf(1.f, sd);
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float x = df[ks][j] * sc;
-        const _Float16 hi = (_Float16)x;
-        D0[ks][j] = hi;
-        D1[ks][j] = (_Float16)(x - (float)hi);
-      }
+  for (int ks = 0; ks < KS; ++ks) {
+    const int o = fo + sec * 4 * R + (32 * ks + 8 * g) * 2;
+    b0[ks] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(Rf, o, 0, 0));
+    b1[ks] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(Rf, o + 2 * R, 0, 0));
   }
 }
 
@@ -297,29 +291,26 @@ __device__ __forceinline__ void gather_kvw(Gat& X, rsrc_t Rk, rsrc_t Rv, rsrc_t 
   X.w2 = bld4<8 * kH>(Rw, ow_, sk);
 }
 
-// the weight image, row scales / biases and RBF parameters into LDS (every thread of the workgroup)
+// the weight image and the row scales / biases into LDS (every thread of the workgroup)
 template <int KS, int NT>
-__device__ __forceinline__ void load_image(_Float16* w, float* s_sc, float* s_b, float* s_mu, float* s_beta,
-                                           const _Float16* img, const float* wsc, const float* bias, const float* mu,
-                                           const float* beta, int rbf) {
+__device__ __forceinline__ void load_image(_Float16* w, float* s_sc, float* s_b, const _Float16* img, const float* wsc,
+                                           const float* bias) {
   constexpr int R = 32 * KS;
   const u4* g = reinterpret_cast<const u4*>(img);
   u4* l = reinterpret_cast<u4*>(w);
   for (int i = threadIdx.x; i < 2 * kD * R / 8; i += NT) l[i] = g[i];
   for (int i = threadIdx.x; i < kD; i += NT) { s_sc[i] = wsc[i]; s_b[i] = bias[i]; }
-  for (int i = threadIdx.x; i < R; i += NT) {
-    s_mu[i] = mu[i];
-    s_beta[i] = rbf == TMDNET_RBF_EXPNORM ? beta[i] : beta[0];
-  }
 }
 
-// per-lane A-fragment offsets, opaque to the optimiser: the weight fragments are the same for every tile,
-// and without it the compiler hoists all blocks' fragments out of the tile loop (hundreds of VGPRs)
+// per-lane A-fragment offsets of the item's head slice (block h0 of every part), opaque to the optimiser:
+// the weight fragments are the same for every tile, and without it the compiler hoists all blocks'
+// fragments out of the tile loop (hundreds of VGPRs)
 template <int KS>
-__device__ __forceinline__ void frag_offsets(int lane, int (&wb)[KS]) {
+__device__ __forceinline__ void frag_offsets(int lane, int h0, int (&wb)[KS]) {
+  constexpr int R = 32 * KS;
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks) {
-    wb[ks] = wfrag_base<KS>(lane, ks);
+    wb[ks] = wfrag_base<KS>(lane, ks) + h0 * 16 * R * (int)sizeof(_Float16);
     asm volatile("" : "+v"(wb[ks]));
   }
 }
@@ -330,7 +321,7 @@ template <bool PL> struct VL {
   static constexpr int part = PL ? kH : 16;  // floats from part p to part p + 1
 };
 
-struct Work {  // the workgroup's node range and its work-item counter
+struct Work {  // the workgroup's node range and its work-item count
   int n0, items;
 };
 template <int G>
@@ -346,24 +337,47 @@ __device__ __forceinline__ int next_item(int* counter) {
   return __builtin_amdgcn_readfirstlane(__shfl(it, 0));
 }
 
+// one edge slot's per-tile inputs: source, cutoff, unit vector, fragment row offset
+struct Edge {
+  int s, fo;
+  float C, ux, uy, uz;
+  bool ok;
+};
+__device__ __forceinline__ Edge load_edge(int e, int re, const int32_t* src, const float* C, const float* u,
+                                          const int32_t* frow, int frow_bytes, float usign) {
+  Edge E;
+  E.ok = e < re;
+  E.s = 0;
+  E.fo = kOOB;
+  E.C = E.ux = E.uy = E.uz = 0.f;
+  if (E.ok) {
+    E.s = src[e];
+    E.fo = frow[e] * frow_bytes;
+    E.C = C[e];
+    E.ux = usign * u[3 * (size_t)e];
+    E.uy = usign * u[3 * (size_t)e + 1];
+    E.uz = usign * u[3 * (size_t)e + 2];
+  }
+  return E;
+}
+
 // ------------------------------------------------------------------ forward
 struct Fwd {
-  int n, cap, rbf;
+  int n, cap;
   const int32_t* row_ptr;
   const int32_t* src;
   const float* q; int ldq;
   const float* k; int ldk;
   const float* v; int ldv;
   const float* vec;  // [N][3][H] or NULL (layer 0)
-  const float* r;
   const float* C;
   const float* u;
+  const int32_t* frow;  // fragment row of every edge (its pair row)
+  const _Float16* fr;
+  unsigned fr_bytes;
   const _Float16* img;
   const float* wsc;
   const float* bias;
-  const float* mu;
-  const float* beta;
-  float cl, cu, alpha;
   float* xo;
   float* veco;
 };
@@ -371,20 +385,20 @@ struct Fwd {
 // HPW heads per work item (G = 8 / HPW items per node); NW waves per workgroup
 template <int KS, int HPW, int NW, bool PL>
 __global__ __launch_bounds__(NW * 64, 1) void k_fwd(Fwd P) {
-  constexpr int R = 32 * KS, H = kH, G = kHeads / HPW;
+  constexpr int R = 32 * KS, H = kH, G = kHeads / HPW, BS = 16 * R * (int)sizeof(_Float16);
   __shared__ __attribute__((aligned(16))) _Float16 w[2 * kD * R];
   __shared__ __attribute__((aligned(16))) float s_sc[kD];
   __shared__ __attribute__((aligned(16))) float s_b[kD];
-  __shared__ float s_mu[R], s_beta[R];
   __shared__ __attribute__((aligned(16))) float s_q[NW][16 * HPW];  // the item's q channels (per wave)
   __shared__ int s_next;
-  load_image<KS, NW * 64>(w, s_sc, s_b, s_mu, s_beta, P.img, P.wsc, P.bias, P.mu, P.beta, P.rbf);
+  load_image<KS, NW * 64>(w, s_sc, s_b, P.img, P.wsc, P.bias);
   if (threadIdx.x == 0) s_next = 0;
   __syncthreads();
   const Work W = work_range<G>(P.n);
   const int lane = lane_id(), c = lane & 15, g = lane >> 4, wid = threadIdx.x >> 6;
   const rsrc_t Rk = make_rsrc(P.k, (unsigned)P.n * P.ldk * 4u), Rv = make_rsrc(P.v, (unsigned)P.n * P.ldv * 4u);
   const rsrc_t Rw = make_rsrc(P.vec, P.vec ? (unsigned)P.n * 3u * H * 4u : 0u);
+  const rsrc_t Rf = make_rsrc(P.fr, P.fr_bytes);
   float* sq = s_q[wid];
   for (;;) {
     const int it = next_item(&s_next);
@@ -399,62 +413,47 @@ __global__ __launch_bounds__(NW * 64, 1) void k_fwd(Fwd P) {
     f4 ax[HPW], a0[HPW], a1[HPW], a2[HPW];
 #pragma unroll
     for (int hh = 0; hh < HPW; ++hh) ax[hh] = a0[hh] = a1[hh] = a2[hh] = f4{0.f, 0.f, 0.f, 0.f};
+    const float* sct = s_sc + 16 * h0;
+    const float* sbt = s_b + 16 * h0;
     for (int base = rb; base < re; base += 16) {
-      const int e = base + c;
-      const bool ok = e < re;
-      float rf = 0.f, Ce = 0.f, ux = 0.f, uy = 0.f, uz = 0.f;
-      int s = 0;
-      if (ok) {
-        rf = P.r[e];
-        s = P.src[e];
-        Ce = P.C[e];
-        ux = P.u[3 * (size_t)e];
-        uy = P.u[3 * (size_t)e + 1];
-        uz = P.u[3 * (size_t)e + 2];
-      }
-      TMD_DCHECK(s >= 0 && s < P.n);
-      h8 B0[KS], B1[KS], D0[KS], D1[KS];
-      float dsc = 1.f;
-      rbf_frags<KS, false>(P.rbf, rf, P.cl, P.cu, P.alpha, s_mu, s_beta, g, B0, B1, D0, D1, dsc);
+      const Edge E = load_edge(base + c, re, P.src, P.C, P.u, P.frow, 8 * R, 1.f);
+      TMD_DCHECK(E.s >= 0 && E.s < P.n);
+      h8 B0[KS], B1[KS];
+      load_frags<KS>(Rf, E.fo, g, 0, B0, B1);
       // an edge past the row gathers from beyond the resources' ranges: its k, v and vec are 0, so its
       // terms vanish without masks (C = 0 as well)
-      const int ok_ = ok ? (s * P.ldk + 4 * g) * 4 : kOOB;
-      const int ov_ = ok ? (s * P.ldv + 4 * g) * 4 : kOOB;
-      const int ow_ = ok ? (s * 3 * H + 4 * g) * 4 : kOOB;
+      const int ok_ = E.ok ? (E.s * P.ldk + 4 * g) * 4 : kOOB;
+      const int ov_ = E.ok ? (E.s * P.ldv + 4 * g) * 4 : kOOB;
+      const int ow_ = E.ok ? (E.s * 3 * H + 4 * g) * 4 : kOOB;
       int wb[KS];
-      frag_offsets<KS>(lane, wb);
+      frag_offsets<KS>(lane, h0, wb);
       const char* wt = reinterpret_cast<const char*>(w);
-      // head hh + 1's gathers are in flight during head hh's MFMAs and math (two register sets); the
-      // scheduler may not mix heads otherwise (one head's temporaries live at a time)
-      // head hh + 1's gathers are in flight during head hh's MFMAs and math (two register sets)
-      Gat X[2];
-      gather_kvw<PL>(X[0], Rk, Rv, Rw, ok_, ov_, ow_, h0);
       static_for<HPW>([&](auto hc) {
         constexpr int hh = decltype(hc)::value;
-        const int h = h0 + hh;
-        if constexpr (hh + 1 < HPW) gather_kvw<PL>(X[(hh + 1) & 1], Rk, Rv, Rw, ok_, ov_, ow_, h + 1);
-        const Gat& G = X[hh & 1];
-        const f4 pk = block_pre<KS>(wt, wb, s_sc, s_b, h, B0, B1, g);
-        const f4 px = block_pre<KS>(wt, wb, s_sc, s_b, 8 + h, B0, B1, g);
-        const f4 p1 = block_pre<KS>(wt, wb, s_sc, s_b, 16 + h, B0, B1, g);
-        const f4 p2 = block_pre<KS>(wt, wb, s_sc, s_b, 24 + h, B0, B1, g);
+        Gat X;
+        gather_kvw<PL>(X, Rk, Rv, Rw, ok_, ov_, ow_, h0 + hh);
+        const f4 pk = block_pre<KS>(wt, wb, sct, sbt, hh, B0, B1, g);
+        const f4 px = block_pre<KS>(wt, wb, sct, sbt, 8 + hh, B0, B1, g);
+        const f4 p1 = block_pre<KS>(wt, wb, sct, sbt, 16 + hh, B0, B1, g);
+        const f4 p2 = block_pre<KS>(wt, wb, sct, sbt, 24 + hh, B0, B1, g);
         const f4 qv = *reinterpret_cast<const f4*>(sq + 16 * hh + 4 * g);
         float part = 0.f;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) part += qv[i] * G.kk[i] * Silu<float>(pk[i]).s;
+        for (int i = 0; i < 4; ++i) part += qv[i] * X.kk[i] * Silu<float>(pk[i]).s;
         const float att = gsum(part);
-        const float a = Silu<float>(att).s * Ce;
+        const float a = Silu<float>(att).s * E.C;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          ax[hh][i] += G.vx[i] * Silu<float>(px[i]).s * a;
-          const float v1e = G.v1[i] * Silu<float>(p1[i]).s;
-          const float v2e = G.v2[i] * Silu<float>(p2[i]).s;
-          a0[hh][i] += G.w0[i] * v1e + v2e * ux;
-          a1[hh][i] += G.w1[i] * v1e + v2e * uy;
-          a2[hh][i] += G.w2[i] * v1e + v2e * uz;
+          ax[hh][i] += X.vx[i] * Silu<float>(px[i]).s * a;
+          const float v1e = X.v1[i] * Silu<float>(p1[i]).s;
+          const float v2e = X.v2[i] * Silu<float>(p2[i]).s;
+          a0[hh][i] += X.w0[i] * v1e + v2e * E.ux;
+          a1[hh][i] += X.w1[i] * v1e + v2e * E.uy;
+          a2[hh][i] += X.w2[i] * v1e + v2e * E.uz;
         }
         __builtin_amdgcn_sched_barrier(0);
       });
+      (void)BS;
     }
     // sum the 16 edge slots (lanes of a row); lane (g, c < HPW) stores head h0 + c's four channels 4 g + i
     f4 X{}, V0{}, V1{}, V2{};
@@ -483,22 +482,22 @@ __global__ __launch_bounds__(NW * 64, 1) void k_fwd(Fwd P) {
 
 // ------------------------------------------------------------------ backward (force pass, "dr mode")
 struct Bwd {
-  int n, cap, rbf, acc;
+  int n, cap, acc;
   const int32_t* row_ptr;
   const int32_t* src;
   const float* q; int ldq;
   const float* k; int ldk;
   const float* v; int ldv;
   const float* vec;
-  const float* r;
   const float* C;
   const float* u;
+  const int32_t* frow;
+  const _Float16* fr;
+  const float* dscale;
+  unsigned fr_bytes;
   const _Float16* img;
   const float* wsc;
   const float* bias;
-  const float* mu;
-  const float* beta;
-  float cl, cu, alpha;
   const float* gx;    // [N][H]   dL/d x_agg
   const float* gvec;  // [N][3][H] dL/d vec_agg (and the layer's residual cotangent)
   float* gq;          // ld ldq
@@ -508,24 +507,24 @@ struct Bwd {
   float* gC;
   float* gu;
   float* gr;
+  float* part;        // [S][5][cap] per-slice edge sums (S = 8 / HPW > 1), summed by k_edge_combine
 };
 
 // Destination pass: for edge e = (t <- s) of t's row: gq[t] and the per-edge g_cut, g_unit, g_r (the
-// projection gradient contracted with d pre / d r in registers).  All 8 heads per work item (the per-edge
-// sums run over every channel); t's q, gx, gvec rows are staged in the wave's LDS slot.
-template <int KS, int NW, bool PL>
+// projection gradient contracted with d pre / d r in registers).  HPW heads per work item; t's q, gx,
+// gvec channels of the slice staged in the wave's LDS slot.  The per-edge sums run over every channel:
+// with one slice (HPW = 8) they are written directly, else each slice writes its part for k_edge_combine.
+template <int KS, int HPW, int NW, bool PL>
 __global__ __launch_bounds__(NW * 64, 1) void k_bwd_dst(Bwd P) {
-  constexpr int R = 32 * KS, H = kH;
+  constexpr int R = 32 * KS, H = kH, G = kHeads / HPW, CH = 16 * HPW;
   __shared__ __attribute__((aligned(16))) _Float16 w[2 * kD * R];
   __shared__ __attribute__((aligned(16))) float s_sc[kD];
   __shared__ __attribute__((aligned(16))) float s_b[kD];
-  __shared__ float s_mu[R], s_beta[R];
-  __shared__ __attribute__((aligned(16))) float s_node[NW][5 * kH];  // q | gx | gvec (3 H)
+  __shared__ __attribute__((aligned(16))) float s_node[NW][5 * CH];  // q | gx | gvec (3) of the slice
   __shared__ int s_next;
-  load_image<KS, NW * 64>(w, s_sc, s_b, s_mu, s_beta, P.img, P.wsc, P.bias, P.mu, P.beta, P.rbf);
+  load_image<KS, NW * 64>(w, s_sc, s_b, P.img, P.wsc, P.bias);
   if (threadIdx.x == 0) s_next = 0;
-  // static-capacity lists: edge slots past the last row belong to no row -- zeroed (spread over the grid)
-  {
+  if (G == 1) {  // static-capacity lists: edge slots past the last row belong to no row -- zeroed here
     const int e0 = min(P.row_ptr[P.n], P.cap);
     for (int e = e0 + blockIdx.x * NW * 64 + threadIdx.x; e < P.cap; e += gridDim.x * NW * 64) {
       P.gC[e] = 0.f;
@@ -534,98 +533,94 @@ __global__ __launch_bounds__(NW * 64, 1) void k_bwd_dst(Bwd P) {
     }
   }
   __syncthreads();
-  const Work W = work_range<1>(P.n);
+  const Work W = work_range<G>(P.n);
   const int lane = lane_id(), c = lane & 15, g = lane >> 4, wid = threadIdx.x >> 6;
   const bool acc_edge = P.acc & TMDNET_ACC_EDGE, ag = P.acc & TMDNET_ACC_GRADS;
   const rsrc_t Rk = make_rsrc(P.k, (unsigned)P.n * P.ldk * 4u), Rv = make_rsrc(P.v, (unsigned)P.n * P.ldv * 4u);
   const rsrc_t Rw = make_rsrc(P.vec, P.vec ? (unsigned)P.n * 3u * H * 4u : 0u);
+  const rsrc_t Rf = make_rsrc(P.fr, P.fr_bytes);
   float* nd = s_node[wid];
   for (;;) {
     const int it = next_item(&s_next);
     if (it >= W.items) break;
-    const int t = W.n0 + it;
+    const int t = W.n0 + it / G, sl = it % G, h0 = sl * HPW;
     const int rb = min(P.row_ptr[t], P.cap), re = min(P.row_ptr[t + 1], P.cap);
-    // stage q[t] | gx[t] | gvec[t] (640 floats = 160 float4: 2.5 per lane)
-    for (int i = lane; i < 160; i += 64) {
-      const float* sp = i < 32 ? P.q + (size_t)t * P.ldq + 4 * i
-                                : i < 64 ? P.gx + (size_t)t * H + 4 * (i - 32) : P.gvec + (size_t)t * 3 * H + 4 * (i - 64);
-      *reinterpret_cast<f4*>(nd + 4 * i) = *reinterpret_cast<const f4*>(sp);
+    // stage the slice's q[t] | gx[t] | gvec[t] channels (5 CH floats)
+    __builtin_amdgcn_wave_barrier();
+    for (int i = lane; i < 5 * CH / 4; i += 64) {
+      const int part = i / (CH / 4), j = i % (CH / 4);
+      const float* sp = part == 0 ? P.q + (size_t)t * P.ldq : part == 1 ? P.gx + (size_t)t * H
+                                                             : P.gvec + ((size_t)t * 3 + (part - 2)) * H;
+      *reinterpret_cast<f4*>(nd + 4 * i) = *reinterpret_cast<const f4*>(sp + 16 * h0 + 4 * j);
     }
     __builtin_amdgcn_wave_barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    f4 gq[kHeads];
+    const float* sct = s_sc + 16 * h0;
+    const float* sbt = s_b + 16 * h0;
+    f4 gq[HPW];
 #pragma unroll
-    for (int h = 0; h < kHeads; ++h) gq[h] = f4{0.f, 0.f, 0.f, 0.f};
+    for (int hh = 0; hh < HPW; ++hh) gq[hh] = f4{0.f, 0.f, 0.f, 0.f};
     for (int base = rb; base < re; base += 16) {
       const int e = base + c;
-      const bool ok = e < re;
-      float rf = 0.f, Ce = 0.f, ux = 0.f, uy = 0.f, uz = 0.f;
-      int s = 0;
-      if (ok) {
-        rf = P.r[e];
-        s = P.src[e];
-        Ce = P.C[e];
-        ux = P.u[3 * (size_t)e];
-        uy = P.u[3 * (size_t)e + 1];
-        uz = P.u[3 * (size_t)e + 2];
-      }
-      TMD_DCHECK(s >= 0 && s < P.n);
+      const Edge E = load_edge(e, re, P.src, P.C, P.u, P.frow, 8 * R, 1.f);
+      TMD_DCHECK(E.s >= 0 && E.s < P.n);
       h8 B0[KS], B1[KS], D0[KS], D1[KS];
-      float dsc = 1.f;
-      rbf_frags<KS, true>(P.rbf, rf, P.cl, P.cu, P.alpha, s_mu, s_beta, g, B0, B1, D0, D1, dsc);
-      const int ok_ = ok ? (s * P.ldk + 4 * g) * 4 : kOOB;
-      const int ov_ = ok ? (s * P.ldv + 4 * g) * 4 : kOOB;
-      const int ow_ = ok ? (s * 3 * H + 4 * g) * 4 : kOOB;
+      load_frags<KS>(Rf, E.fo, g, 0, B0, B1);
+      load_frags<KS>(Rf, E.fo, g, 1, D0, D1);
+      const float dsc = E.ok ? P.dscale[E.fo / (8 * R)] : 1.f;
+      const int ok_ = E.ok ? (E.s * P.ldk + 4 * g) * 4 : kOOB;
+      const int ov_ = E.ok ? (E.s * P.ldv + 4 * g) * 4 : kOOB;
+      const int ow_ = E.ok ? (E.s * 3 * H + 4 * g) * 4 : kOOB;
       int wb[KS];
-      frag_offsets<KS>(lane, wb);
+      frag_offsets<KS>(lane, h0, wb);
       const char* wt = reinterpret_cast<const char*>(w);
       float eC = 0.f, er = 0.f, eu0 = 0.f, eu1 = 0.f, eu2 = 0.f;
-      static_for<kHeads>([&](auto hc) {
-        constexpr int h = decltype(hc)::value;
-        Gat G;
-        gather_kvw<PL>(G, Rk, Rv, Rw, ok_, ov_, ow_, h);
-        const f4 qd = *reinterpret_cast<const f4*>(nd + 16 * h + 4 * g);
-        const f4 gxd = *reinterpret_cast<const f4*>(nd + kH + 16 * h + 4 * g);
+      static_for<HPW>([&](auto hc) {
+        constexpr int hh = decltype(hc)::value;
+        Gat X;
+        gather_kvw<PL>(X, Rk, Rv, Rw, ok_, ov_, ow_, h0 + hh);
+        const f4 qd = *reinterpret_cast<const f4*>(nd + 16 * hh + 4 * g);
+        const f4 gxd = *reinterpret_cast<const f4*>(nd + CH + 16 * hh + 4 * g);
         // the attention part (dk, dv_x blocks) first: its head sums gate every other term
         f4 pk, rk, px, rx;
-        block_pre_dpre<KS>(wt, wb, s_sc, s_b, dsc, h, B0, B1, D0, D1, g, pk, rk);
-        block_pre_dpre<KS>(wt, wb, s_sc, s_b, dsc, 8 + h, B0, B1, D0, D1, g, px, rx);
+        block_pre_dpre<KS>(wt, wb, sct, sbt, dsc, hh, B0, B1, D0, D1, g, pk, rk);
+        block_pre_dpre<KS>(wt, wb, sct, sbt, dsc, 8 + hh, B0, B1, D0, D1, g, px, rx);
         f4 kdk, gpk, gpx;
         float pa = 0.f, pg = 0.f;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const Silu<float> fk(pk[i]);
-          kdk[i] = G.kk[i] * fk.s;
-          gpk[i] = qd[i] * G.kk[i] * fk.d(pk[i]);  // x gs below
+          kdk[i] = X.kk[i] * fk.s;
+          gpk[i] = qd[i] * X.kk[i] * fk.d(pk[i]);  // x gs below
           pa += qd[i] * kdk[i];
           const Silu<float> fx(px[i]);
-          pg += gxd[i] * G.vx[i] * fx.s;
-          gpx[i] = gxd[i] * G.vx[i] * fx.d(px[i]);  // x a below
+          pg += gxd[i] * X.vx[i] * fx.s;
+          gpx[i] = gxd[i] * X.vx[i] * fx.d(px[i]);  // x a below
         }
         const float att = gsum(pa), ga = gsum(pg);
         const Silu<float> sa(att);
-        const float a = sa.s * Ce;
-        const float gs = ga * Ce * sa.d(att);
+        const float a = sa.s * E.C;
+        const float gs = ga * E.C * sa.d(att);
         eC += ga * sa.s;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          gq[h][i] += gs * kdk[i];
+          gq[hh][i] += gs * kdk[i];
           er += gs * gpk[i] * rk[i] + a * gpx[i] * rx[i];
         }
         // the vector parts (dv_1, dv_2 blocks)
-        const f4 g0 = *reinterpret_cast<const f4*>(nd + 2 * kH + 16 * h + 4 * g);
-        const f4 g1 = *reinterpret_cast<const f4*>(nd + 3 * kH + 16 * h + 4 * g);
-        const f4 g2 = *reinterpret_cast<const f4*>(nd + 4 * kH + 16 * h + 4 * g);
+        const f4 g0 = *reinterpret_cast<const f4*>(nd + 2 * CH + 16 * hh + 4 * g);
+        const f4 g1 = *reinterpret_cast<const f4*>(nd + 3 * CH + 16 * hh + 4 * g);
+        const f4 g2 = *reinterpret_cast<const f4*>(nd + 4 * CH + 16 * hh + 4 * g);
         f4 p1, r1, p2, r2;
-        block_pre_dpre<KS>(wt, wb, s_sc, s_b, dsc, 16 + h, B0, B1, D0, D1, g, p1, r1);
-        block_pre_dpre<KS>(wt, wb, s_sc, s_b, dsc, 24 + h, B0, B1, D0, D1, g, p2, r2);
+        block_pre_dpre<KS>(wt, wb, sct, sbt, dsc, 16 + hh, B0, B1, D0, D1, g, p1, r1);
+        block_pre_dpre<KS>(wt, wb, sct, sbt, dsc, 24 + hh, B0, B1, D0, D1, g, p2, r2);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const Silu<float> f1(p1[i]), f2(p2[i]);
-          const float gv1e = g0[i] * G.w0[i] + g1[i] * G.w1[i] + g2[i] * G.w2[i];
-          const float gv2e = g0[i] * ux + g1[i] * uy + g2[i] * uz;
-          er += gv1e * G.v1[i] * f1.d(p1[i]) * r1[i] + gv2e * G.v2[i] * f2.d(p2[i]) * r2[i];
-          const float v2e = G.v2[i] * f2.s;
+          const float gv1e = g0[i] * X.w0[i] + g1[i] * X.w1[i] + g2[i] * X.w2[i];
+          const float gv2e = g0[i] * E.ux + g1[i] * E.uy + g2[i] * E.uz;
+          er += gv1e * X.v1[i] * f1.d(p1[i]) * r1[i] + gv2e * X.v2[i] * f2.d(p2[i]) * r2[i];
+          const float v2e = X.v2[i] * f2.s;
           eu0 += g0[i] * v2e;
           eu1 += g1[i] * v2e;
           eu2 += g2[i] * v2e;
@@ -637,34 +632,66 @@ __global__ __launch_bounds__(NW * 64, 1) void k_bwd_dst(Bwd P) {
       eu0 = gsum(eu0);
       eu1 = gsum(eu1);
       eu2 = gsum(eu2);
-      if (g == 0 && ok) {
-        float* gu = P.gu + 3 * (size_t)e;
-        if (acc_edge) {
-          P.gC[e] += eC;
-          gu[0] += eu0; gu[1] += eu1; gu[2] += eu2;
-          P.gr[e] += er;
+      if (g == 0 && E.ok) {
+        if (G == 1) {
+          float* gu = P.gu + 3 * (size_t)e;
+          if (acc_edge) {
+            P.gC[e] += eC;
+            gu[0] += eu0; gu[1] += eu1; gu[2] += eu2;
+            P.gr[e] += er;
+          } else {
+            P.gC[e] = eC;
+            gu[0] = eu0; gu[1] = eu1; gu[2] = eu2;
+            P.gr[e] = er;
+          }
         } else {
-          P.gC[e] = eC;
-          gu[0] = eu0; gu[1] = eu1; gu[2] = eu2;
-          P.gr[e] = er;
+          float* pp = P.part + (size_t)sl * 5 * P.cap + e;
+          pp[0] = eC;
+          pp[P.cap] = eu0;
+          pp[2 * (size_t)P.cap] = eu1;
+          pp[3 * (size_t)P.cap] = eu2;
+          pp[4 * (size_t)P.cap] = er;
         }
       }
     }
-    // gq: sum the 16 edge slots; lane (g, c < 8) stores head c's channels 4 g + i
+    // gq: sum the 16 edge slots; lane (g, c < HPW) stores head h0 + c's channels 4 g + i
     f4 Q{};
 #pragma unroll
-    for (int h = 0; h < kHeads; ++h) {
+    for (int hh = 0; hh < HPW; ++hh) {
       f4 sq;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) sq[i] = row_sum16(gq[h][i]);
-      if (c == h) Q = sq;
+      for (int i = 0; i < 4; ++i) sq[i] = row_sum16(gq[hh][i]);
+      if (c == hh) Q = sq;
     }
-    if (c < kHeads) {
-      float* d = P.gq + (size_t)t * P.ldq + 16 * c + 4 * g;
+    if (c < HPW) {
+      float* d = P.gq + (size_t)t * P.ldq + 16 * (h0 + c) + 4 * g;
       if (ag) Q += *reinterpret_cast<const f4*>(d);
       *reinterpret_cast<f4*>(d) = Q;
     }
-    __builtin_amdgcn_wave_barrier();  // the next item's staging overwrites this item's LDS slot
+  }
+}
+
+// the per-slice edge sums of the destination pass -> g_cut, g_unit, g_r (in slice order: deterministic);
+// also zeroes the static-capacity padding slots [row_ptr[n], cap)
+__global__ __launch_bounds__(256) void k_edge_combine(Bwd P, int S) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= P.cap) return;
+  const int e0 = min(P.row_ptr[P.n], P.cap);
+  float v[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+  if (e < e0) {
+    for (int s = 0; s < S; ++s)
+#pragma unroll
+      for (int j = 0; j < 5; ++j) v[j] += P.part[((size_t)s * 5 + j) * P.cap + e];
+  }
+  float* gu = P.gu + 3 * (size_t)e;
+  if ((P.acc & TMDNET_ACC_EDGE) && e < e0) {
+    P.gC[e] += v[0];
+    gu[0] += v[1]; gu[1] += v[2]; gu[2] += v[3];
+    P.gr[e] += v[4];
+  } else {
+    P.gC[e] = v[0];
+    gu[0] = v[1]; gu[1] = v[2]; gu[2] = v[3];
+    P.gr[e] = v[4];
   }
 }
 
@@ -673,114 +700,100 @@ __global__ __launch_bounds__(NW * 64, 1) void k_bwd_dst(Bwd P) {
 // TMDNET_ACC_VEC_RESIDUAL).  HPW heads per work item; j's k / v / vec channels in registers.
 template <int KS, int HPW, int NW, bool PL>
 __global__ __launch_bounds__(NW * 64, 1) void k_bwd_src(Bwd P) {
-  constexpr int R = 32 * KS, H = kH, G = kHeads / HPW;
+  constexpr int R = 32 * KS, H = kH, G = kHeads / HPW, CH = 16 * HPW;
   __shared__ __attribute__((aligned(16))) _Float16 w[2 * kD * R];
   __shared__ __attribute__((aligned(16))) float s_sc[kD];
   __shared__ __attribute__((aligned(16))) float s_b[kD];
-  __shared__ float s_mu[R], s_beta[R];
+  __shared__ __attribute__((aligned(16))) float s_node[NW][6 * CH];  // k | v_x | v_1 | vec (3) of the slice
   __shared__ int s_next;
-  load_image<KS, NW * 64>(w, s_sc, s_b, s_mu, s_beta, P.img, P.wsc, P.bias, P.mu, P.beta, P.rbf);
+  load_image<KS, NW * 64>(w, s_sc, s_b, P.img, P.wsc, P.bias);
   if (threadIdx.x == 0) s_next = 0;
   __syncthreads();
   const Work W = work_range<G>(P.n);
-  const int lane = lane_id(), c = lane & 15, g = lane >> 4;
+  const int lane = lane_id(), c = lane & 15, g = lane >> 4, wid = threadIdx.x >> 6;
   const bool ag = P.acc & TMDNET_ACC_GRADS, resid = P.acc & TMDNET_ACC_VEC_RESIDUAL;
+  float* nd = s_node[wid];
   const rsrc_t Rq = make_rsrc(P.q, (unsigned)P.n * P.ldq * 4u), Rgx = make_rsrc(P.gx, (unsigned)P.n * H * 4u);
   const rsrc_t Rgv = make_rsrc(P.gvec, (unsigned)P.n * 3u * H * 4u);
+  const rsrc_t Rf = make_rsrc(P.fr, P.fr_bytes);
   constexpr int PV = VL<PL>::part;
   for (;;) {
     const int it = next_item(&s_next);
     if (it >= W.items) break;
     const int j = W.n0 + it / G, h0 = (it % G) * HPW;
     const int rb = min(P.row_ptr[j], P.cap), re = min(P.row_ptr[j + 1], P.cap);
-    f4 kj[HPW], vxj[HPW], v1j[HPW], w0j[HPW], w1j[HPW], w2j[HPW];
+    // stage j's k, v_x, v_1, vec channels of the slice (6 CH floats; vec absent: zeros)
+    __builtin_amdgcn_wave_barrier();
+    for (int i = lane; i < 6 * CH / 4; i += 64) {
+      const int part = i / (CH / 4), jj = i % (CH / 4), hh = jj / 4, o = 4 * (jj % 4);
+      const int h = h0 + hh;
+      f4 val{0.f, 0.f, 0.f, 0.f};
+      if (part == 0) val = *reinterpret_cast<const f4*>(P.k + (size_t)j * P.ldk + 16 * h + o);
+      else if (part <= 2)
+        val = *reinterpret_cast<const f4*>(P.v + (size_t)j * P.ldv + VL<PL>::head * h + (part - 1) * PV + o);
+      else if (P.vec) val = *reinterpret_cast<const f4*>(P.vec + ((size_t)j * 3 + (part - 3)) * H + 16 * h + o);
+      *reinterpret_cast<f4*>(nd + 4 * i) = val;
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     f4 gk[HPW], gvx[HPW], gv1[HPW], gv2[HPW], gw0[HPW], gw1[HPW], gw2[HPW];
     const f4 z4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int hh = 0; hh < HPW; ++hh) {
-      const int h = h0 + hh;
-      kj[hh] = *reinterpret_cast<const f4*>(P.k + (size_t)j * P.ldk + 16 * h + 4 * g);
-      const float* vr = P.v + (size_t)j * P.ldv + VL<PL>::head * h + 4 * g;
-      vxj[hh] = *reinterpret_cast<const f4*>(vr);
-      v1j[hh] = *reinterpret_cast<const f4*>(vr + PV);
-      const float* wr = P.vec + (size_t)j * 3 * H + 16 * h + 4 * g;
-      w0j[hh] = P.vec ? *reinterpret_cast<const f4*>(wr) : z4;
-      w1j[hh] = P.vec ? *reinterpret_cast<const f4*>(wr + H) : z4;
-      w2j[hh] = P.vec ? *reinterpret_cast<const f4*>(wr + 2 * H) : z4;
-      gk[hh] = gvx[hh] = gv1[hh] = gv2[hh] = gw0[hh] = gw1[hh] = gw2[hh] = z4;
-    }
+    for (int hh = 0; hh < HPW; ++hh) gk[hh] = gvx[hh] = gv1[hh] = gv2[hh] = gw0[hh] = gw1[hh] = gw2[hh] = z4;
+    auto own = [&](int part, int hh) { return *reinterpret_cast<const f4*>(nd + part * CH + 16 * hh + 4 * g); };
+    const float* sct = s_sc + 16 * h0;
+    const float* sbt = s_b + 16 * h0;
     for (int base = rb; base < re; base += 16) {
-      const int e = base + c;
-      const bool ok = e < re;
-      float rf = 0.f, Ce = 0.f, ux = 0.f, uy = 0.f, uz = 0.f;
-      int m = 0;
-      if (ok) {
-        rf = P.r[e];
-        m = P.src[e];
-        Ce = P.C[e];
-        ux = -P.u[3 * (size_t)e];  // the reversed edge j -> m
-        uy = -P.u[3 * (size_t)e + 1];
-        uz = -P.u[3 * (size_t)e + 2];
-      }
-      TMD_DCHECK(m >= 0 && m < P.n);
-      h8 B0[KS], B1[KS], D0[KS], D1[KS];
-      float dsc = 1.f;
-      rbf_frags<KS, false>(P.rbf, rf, P.cl, P.cu, P.alpha, s_mu, s_beta, g, B0, B1, D0, D1, dsc);
-      const int oq = ok ? (m * P.ldq + 4 * g) * 4 : kOOB;
-      const int ox = ok ? (m * H + 4 * g) * 4 : kOOB;
-      const int og = ok ? (m * 3 * H + 4 * g) * 4 : kOOB;
+      const Edge E = load_edge(base + c, re, P.src, P.C, P.u, P.frow, 8 * R, -1.f);  // the reversed edge j -> m
+      TMD_DCHECK(E.s >= 0 && E.s < P.n);
+      h8 B0[KS], B1[KS];
+      load_frags<KS>(Rf, E.fo, g, 0, B0, B1);
+      const int oq = E.ok ? (E.s * P.ldq + 4 * g) * 4 : kOOB;
+      const int ox = E.ok ? (E.s * H + 4 * g) * 4 : kOOB;
+      const int og = E.ok ? (E.s * 3 * H + 4 * g) * 4 : kOOB;
       int wb[KS];
-      frag_offsets<KS>(lane, wb);
+      frag_offsets<KS>(lane, h0, wb);
       const char* wt = reinterpret_cast<const char*>(w);
-      struct GatD {  // the other end's q, gx, gvec of one head
-        f4 q, gx, g0, g1, g2;
-      };
-      auto gather_d = [&](GatD& Y, int h) {
-        const int sh = __builtin_amdgcn_readfirstlane(64 * h);
-        Y.q = bld4<0>(Rq, oq, sh);
-        Y.gx = bld4<0>(Rgx, ox, sh);
-        Y.g0 = bld4<0>(Rgv, og, sh);
-        Y.g1 = bld4<4 * kH>(Rgv, og, sh);
-        Y.g2 = bld4<8 * kH>(Rgv, og, sh);
-      };
       static_for<HPW>([&](auto hc) {
         constexpr int hh = decltype(hc)::value;
-        const int h = h0 + hh;
-        GatD Z;
-        gather_d(Z, h);
-        const f4 pk = block_pre<KS>(wt, wb, s_sc, s_b, h, B0, B1, g);
-        const f4 px = block_pre<KS>(wt, wb, s_sc, s_b, 8 + h, B0, B1, g);
+        const int sh = __builtin_amdgcn_readfirstlane(64 * (h0 + hh));
+        const f4 qm = bld4<0>(Rq, oq, sh), gxm = bld4<0>(Rgx, ox, sh);
+        const f4 g0 = bld4<0>(Rgv, og, sh), g1 = bld4<4 * kH>(Rgv, og, sh), g2 = bld4<8 * kH>(Rgv, og, sh);
+        const f4 pk = block_pre<KS>(wt, wb, sct, sbt, hh, B0, B1, g);
+        const f4 px = block_pre<KS>(wt, wb, sct, sbt, 8 + hh, B0, B1, g);
         f4 dk, dvx;
         float pa = 0.f, pg = 0.f;
+        const f4 kj = own(0, hh), vxj = own(1, hh);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           dk[i] = Silu<float>(pk[i]).s;
           dvx[i] = Silu<float>(px[i]).s;
-          pa += Z.q[i] * kj[hh][i] * dk[i];
-          pg += Z.gx[i] * vxj[hh][i] * dvx[i];
+          pa += qm[i] * kj[i] * dk[i];
+          pg += gxm[i] * vxj[i] * dvx[i];
         }
         const float att = gsum(pa), ga = gsum(pg);
         const Silu<float> sa(att);
-        const float a = sa.s * Ce;
-        const float gs = ga * Ce * sa.d(att);
+        const float a = sa.s * E.C;
+        const float gs = ga * E.C * sa.d(att);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          gk[hh][i] += gs * Z.q[i] * dk[i];
-          gvx[hh][i] += Z.gx[i] * a * dvx[i];
+          gk[hh][i] += gs * qm[i] * dk[i];
+          gvx[hh][i] += gxm[i] * a * dvx[i];
         }
-        const f4 p1 = block_pre<KS>(wt, wb, s_sc, s_b, 16 + h, B0, B1, g);
-        const f4 p2 = block_pre<KS>(wt, wb, s_sc, s_b, 24 + h, B0, B1, g);
+        const f4 p1 = block_pre<KS>(wt, wb, sct, sbt, 16 + hh, B0, B1, g);
+        const f4 p2 = block_pre<KS>(wt, wb, sct, sbt, 24 + hh, B0, B1, g);
+        const f4 v1j = own(2, hh), w0j = own(3, hh), w1j = own(4, hh), w2j = own(5, hh);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const float dv1 = Silu<float>(p1[i]).s, dv2 = Silu<float>(p2[i]).s;
-          const float gv1e = Z.g0[i] * w0j[hh][i] + Z.g1[i] * w1j[hh][i] + Z.g2[i] * w2j[hh][i];
+          const float gv1e = g0[i] * w0j[i] + g1[i] * w1j[i] + g2[i] * w2j[i];
           gv1[hh][i] += gv1e * dv1;
-          const float gv2e = Z.g0[i] * ux + Z.g1[i] * uy + Z.g2[i] * uz;
+          const float gv2e = g0[i] * E.ux + g1[i] * E.uy + g2[i] * E.uz;
           gv2[hh][i] += gv2e * dv2;
-          const float v1e = v1j[hh][i] * dv1;
-          gw0[hh][i] += Z.g0[i] * v1e;
-          gw1[hh][i] += Z.g1[i] * v1e;
-          gw2[hh][i] += Z.g2[i] * v1e;
+          const float v1e = v1j[i] * dv1;
+          gw0[hh][i] += g0[i] * v1e;
+          gw1[hh][i] += g1[i] * v1e;
+          gw2[hh][i] += g2[i] * v1e;
         }
         __builtin_amdgcn_sched_barrier(0);
       });
@@ -839,6 +852,12 @@ static int num_cus() {
   return n;
 }
 
+// launch shapes (heads per work item, waves per workgroup; one workgroup per CU): chosen so that no
+// variant spills (tools/regs.py) -- see the launchers
+constexpr int kFwdHPW = 2, kFwdNW = 12;
+constexpr int kDstHPW = 2, kDstNW = 8;  // 12 waves: 6-14 spilled VGPRs
+constexpr int kSrcHPW = 2, kSrcNW = 12;
+
 }  // namespace fep
 }  // namespace tmd
 
@@ -861,15 +880,39 @@ extern "C" int tmdnet_fep_split_f32(int D, int R, const void* W, int ldw, const 
   return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
 }
 
+extern "C" size_t tmdnet_fep_frags_bytes(long long rows, int R) {
+  return rows < 0 ? 0 : (size_t)rows * 4 * R * sizeof(_Float16);
+}
+
+extern "C" int tmdnet_fep_frags_f32(long long rows, int R, const void* r_rows, const void* mu, const void* beta,
+                                    double cutoff_lower, double cutoff_upper, int rbf_type, void* frags, void* dscale,
+                                    void* stream) {
+  if (rows < 0 || (rows && (!r_rows || !mu || !beta || !frags || !dscale))) return kBadArgument;
+  if (R != 32 && R != 64) return kUnsupported;
+  if (rows == 0) return kOk;
+  const float cl = (float)cutoff_lower, cu = (float)cutoff_upper, alpha = (float)(5.0 / (cutoff_upper - cutoff_lower));
+  const long long per = 256 / R;
+  const dim3 g((unsigned)((rows + per - 1) / per)), b(256);
+  hipStream_t st = (hipStream_t)stream;
+  if (R == 64)
+    hipLaunchKernelGGL(fep::k_frags<2>, g, b, 0, st, rows, (const float*)r_rows, (const float*)mu, (const float*)beta,
+                       rbf_type, cl, cu, alpha, (_Float16*)frags, (float*)dscale);
+  else
+    hipLaunchKernelGGL(fep::k_frags<1>, g, b, 0, st, rows, (const float*)r_rows, (const float*)mu, (const float*)beta,
+                       rbf_type, cl, cu, alpha, (_Float16*)frags, (float*)dscale);
+  return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
+}
+
 namespace {
 // the shape / layout checks shared by the fused entry points
 int fused_check(int n, int H, int heads, int R, int ldq, int ldk, int ldv, const void* q, const void* k, const void* v,
-                const void* vec, const void* img) {
+                const void* vec, const void* img, long long frag_rows) {
   if (H != fep::kH || heads != fep::kHeads || (R != 32 && R != 64)) return kUnsupported;
   if (ldq < H || ldk < H || ldv < 3 * H || ldq % 4 || ldk % 4 || ldv % 4) return kBadArgument;
   if ((((uintptr_t)q) | ((uintptr_t)k) | ((uintptr_t)v) | ((uintptr_t)vec) | ((uintptr_t)img)) & 15) return kUnsupported;
   // the gathers address rows through 32-bit byte offsets
-  if ((long long)n * (ldq > ldv ? ldq : ldv) * 4 >= fep::kOOB || (long long)n * 3 * H * 4 >= fep::kOOB)
+  if ((long long)n * (ldq > ldv ? ldq : ldv) * 4 >= fep::kOOB || (long long)n * 3 * H * 4 >= fep::kOOB ||
+      frag_rows * 8 * R >= fep::kOOB)
     return kUnsupported;
   return kOk;
 }
@@ -877,31 +920,28 @@ int fused_check(int n, int H, int heads, int R, int ldq, int ldk, int ldv, const
 
 extern "C" int tmdnet_et_fused_fwd_f32(int n, int H, int heads, int R, const int32_t* row_ptr, const int32_t* src,
                                        int cap, const void* q, int ldq, const void* k, int ldk, const void* v, int ldv,
-                                       const void* vec, const void* r, const void* C, const void* u, const void* img,
-                                       const void* wsc, const void* bias, const void* mu, const void* beta,
-                                       double cutoff_lower, double cutoff_upper, int rbf_type, void* x_out,
-                                       void* vec_out, int flags, void* stream) {
-  if (n < 0 || !row_ptr || !src || !q || !k || !v || !r || !C || !u || !img || !wsc || !bias || !mu || !beta ||
+                                       const void* vec, const void* C, const void* u, const int32_t* frag_rows,
+                                       const void* frags, long long n_frag_rows, const void* img, const void* wsc,
+                                       const void* bias, void* x_out, void* vec_out, int flags, void* stream) {
+  if (n < 0 || !row_ptr || !src || !q || !k || !v || !C || !u || !frag_rows || !frags || !img || !wsc || !bias ||
       !x_out || !vec_out)
     return kBadArgument;
   if (n == 0) return kOk;
-  int rc = fused_check(n, H, heads, R, ldq, ldk, ldv, q, k, v, vec, img);
+  int rc = fused_check(n, H, heads, R, ldq, ldk, ldv, q, k, v, vec, img, n_frag_rows);
   if (rc) return rc;
-  if ((((uintptr_t)x_out) | ((uintptr_t)vec_out)) & 15) return kUnsupported;
+  if ((((uintptr_t)x_out) | ((uintptr_t)vec_out) | ((uintptr_t)frags)) & 15) return kUnsupported;
   fep::Fwd P{};
-  P.n = n; P.cap = cap; P.rbf = rbf_type;
+  P.n = n; P.cap = cap;
   P.row_ptr = row_ptr; P.src = src;
   P.q = (const float*)q; P.ldq = ldq; P.k = (const float*)k; P.ldk = ldk; P.v = (const float*)v; P.ldv = ldv;
-  P.vec = (const float*)vec; P.r = (const float*)r; P.C = (const float*)C; P.u = (const float*)u;
+  P.vec = (const float*)vec; P.C = (const float*)C; P.u = (const float*)u;
+  P.frow = frag_rows; P.fr = (const _Float16*)frags; P.fr_bytes = (unsigned)(n_frag_rows * 8 * R);
   P.img = (const _Float16*)img; P.wsc = (const float*)wsc; P.bias = (const float*)bias;
-  P.mu = (const float*)mu; P.beta = (const float*)beta;
-  P.cl = (float)cutoff_lower; P.cu = (float)cutoff_upper;
-  P.alpha = (float)(5.0 / (cutoff_upper - cutoff_lower));
   P.xo = (float*)x_out; P.veco = (float*)vec_out;
   const int nwg = fep::num_cus();
   const bool pl = flags & TMDNET_ET_V_PLANAR;
   hipStream_t st = (hipStream_t)stream;
-  constexpr int NW = 8, HPW = 4;  // HPW 8: 128 accumulators per lane -> spills
+  constexpr int NW = fep::kFwdNW, HPW = fep::kFwdHPW;
 #define TMD_FEP(KS_, PL_) hipLaunchKernelGGL((fep::k_fwd<KS_, HPW, NW, PL_>), dim3(nwg), dim3(NW * 64), 0, st, P)
   if (R == 64) {
     if (pl) TMD_FEP(2, true); else TMD_FEP(2, false);
@@ -912,42 +952,52 @@ extern "C" int tmdnet_et_fused_fwd_f32(int n, int H, int heads, int R, const int
   return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
 }
 
+extern "C" size_t tmdnet_et_fused_bwd_workspace_bytes(int cap) {
+  constexpr int S = fep::kHeads / fep::kDstHPW;
+  return S > 1 && cap > 0 ? (size_t)S * 5 * cap * sizeof(float) : 0;
+}
+
 extern "C" int tmdnet_et_fused_bwd_f32(int n, int H, int heads, int R, const int32_t* row_ptr, const int32_t* src,
                                        int cap, const void* q, int ldq, const void* k, int ldk, const void* v, int ldv,
-                                       const void* vec, const void* r, const void* C, const void* u, const void* img,
-                                       const void* wsc, const void* bias, const void* mu, const void* beta,
-                                       double cutoff_lower, double cutoff_upper, int rbf_type, const void* gx,
-                                       const void* gvec, void* gq, void* gk, void* gv, void* gvec_in, void* gC,
-                                       void* gu, void* gdist, int accumulate, void* stream) {
-  if (n < 0 || !row_ptr || !src || !q || !k || !v || !r || !C || !u || !img || !wsc || !bias || !mu || !beta || !gx ||
-      !gvec || !gq || !gk || !gv || !gC || !gu || !gdist)
+                                       const void* vec, const void* C, const void* u, const int32_t* frag_rows,
+                                       const void* frags, const void* dscale, long long n_frag_rows, const void* img,
+                                       const void* wsc, const void* bias, const void* gx, const void* gvec, void* gq,
+                                       void* gk, void* gv, void* gvec_in, void* gC, void* gu, void* gdist,
+                                       int accumulate, void* workspace, size_t workspace_bytes, void* stream) {
+  if (n < 0 || !row_ptr || !src || !q || !k || !v || !C || !u || !frag_rows || !frags || !dscale || !img || !wsc ||
+      !bias || !gx || !gvec || !gq || !gk || !gv || !gC || !gu || !gdist)
     return kBadArgument;
   if (n == 0) return kOk;
-  int rc = fused_check(n, H, heads, R, ldq, ldk, ldv, q, k, v, vec, img);
+  int rc = fused_check(n, H, heads, R, ldq, ldk, ldv, q, k, v, vec, img, n_frag_rows);
   if (rc) return rc;
   if ((((uintptr_t)gx) | ((uintptr_t)gvec) | ((uintptr_t)gq) | ((uintptr_t)gk) | ((uintptr_t)gv) |
-       ((uintptr_t)gvec_in)) & 15)
+       ((uintptr_t)gvec_in) | ((uintptr_t)frags)) & 15)
     return kUnsupported;
+  const size_t need = tmdnet_et_fused_bwd_workspace_bytes(cap);
+  if (need && (!workspace || workspace_bytes < need)) return kWorkspaceTooSmall;
   fep::Bwd P{};
-  P.n = n; P.cap = cap; P.rbf = rbf_type; P.acc = accumulate;
+  P.n = n; P.cap = cap; P.acc = accumulate;
   P.row_ptr = row_ptr; P.src = src;
   P.q = (const float*)q; P.ldq = ldq; P.k = (const float*)k; P.ldk = ldk; P.v = (const float*)v; P.ldv = ldv;
-  P.vec = (const float*)vec; P.r = (const float*)r; P.C = (const float*)C; P.u = (const float*)u;
+  P.vec = (const float*)vec; P.C = (const float*)C; P.u = (const float*)u;
+  P.frow = frag_rows; P.fr = (const _Float16*)frags; P.dscale = (const float*)dscale;
+  P.fr_bytes = (unsigned)(n_frag_rows * 8 * R);
   P.img = (const _Float16*)img; P.wsc = (const float*)wsc; P.bias = (const float*)bias;
-  P.mu = (const float*)mu; P.beta = (const float*)beta;
-  P.cl = (float)cutoff_lower; P.cu = (float)cutoff_upper;
-  P.alpha = (float)(5.0 / (cutoff_upper - cutoff_lower));
   P.gx = (const float*)gx; P.gvec = (const float*)gvec;
   P.gq = (float*)gq; P.gk = (float*)gk; P.gv = (float*)gv; P.gveci = (float*)gvec_in;
   P.gC = (float*)gC; P.gu = (float*)gu; P.gr = (float*)gdist;
+  P.part = (float*)workspace;
   const int nwg = fep::num_cus();
-  constexpr int NW = 8, HPW = 2;  // source pass: HPW 4 -> 112 accumulators per lane, spills
+  constexpr int S = fep::kHeads / fep::kDstHPW;
   const bool pl = accumulate & TMDNET_ET_V_PLANAR;
   hipStream_t st = (hipStream_t)stream;
-#define TMD_BWD(KS_, PL_)                                                                                  \
-  do {                                                                                                     \
-    hipLaunchKernelGGL((fep::k_bwd_dst<KS_, NW, PL_>), dim3(nwg), dim3(NW * 64), 0, st, P);               \
-    hipLaunchKernelGGL((fep::k_bwd_src<KS_, HPW, NW, PL_>), dim3(nwg), dim3(NW * 64), 0, st, P);          \
+#define TMD_BWD(KS_, PL_)                                                                                          \
+  do {                                                                                                             \
+    hipLaunchKernelGGL((fep::k_bwd_dst<KS_, fep::kDstHPW, fep::kDstNW, PL_>), dim3(nwg), dim3(fep::kDstNW * 64), 0, \
+                       st, P);                                                                                     \
+    if (S > 1) hipLaunchKernelGGL(fep::k_edge_combine, dim3((cap + 255) / 256), dim3(256), 0, st, P, S);           \
+    hipLaunchKernelGGL((fep::k_bwd_src<KS_, fep::kSrcHPW, fep::kSrcNW, PL_>), dim3(nwg), dim3(fep::kSrcNW * 64), 0, \
+                       st, P);                                                                                     \
   } while (0)
   if (R == 64) {
     if (pl) TMD_BWD(2, true); else TMD_BWD(2, false);

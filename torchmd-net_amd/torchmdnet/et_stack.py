@@ -406,12 +406,14 @@ def _forward_layers(meta, x, f, C, u, params, r=None, want_bwd=False):
             pkv = None
             if l == 0:
                 meta.fep_imgs = []
+                # the RBF fragments of the evaluation (pair rows), shared by every layer's fused kernels
+                meta.fep_frag = kernels.fep_frag_set(meta.graph, r, meta.rbf, meta.pairs)
             if not meta.planar:  # the image's rows are always in the planar [dk | dv_x | dv_1 | dv_2] order
                 one = _planar_perms(meta, x.device)[4]
                 dkv_w, dkv_b = dkv_w.index_select(0, one), dkv_b.index_select(0, one)
             meta.fep_imgs.append(kernels.fep_split(dkv_w, dkv_b))
-            kernels.et_fused_fwd_launch(qkv[:, :H], qkv[:, H:2 * H], qkv[:, 2 * H:], vec, r, C, u,
-                                        meta.fep_imgs[l], meta.rbf, meta.graph, meta.heads, xa, veca,
+            kernels.et_fused_fwd_launch(qkv[:, :H], qkv[:, H:2 * H], qkv[:, 2 * H:], vec, C, u,
+                                        meta.fep_imgs[l], meta.fep_frag, meta.graph, meta.heads, xa, veca,
                                         flags=meta.flags)
         else:
             if pkv_all is not None:
@@ -567,8 +569,8 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws, r=None, dr=Fa
         flags = (nat.ACC_VEC_RESIDUAL | (nat.ACC_EDGE if l < L - 1 else 0) | meta.flags
                  | (nat.ACC_GRADS if acc else 0))
         if fused:
-            kernels.et_fused_bwd_launch(qkv[:, :H], qkv[:, H:2 * H], qkv[:, 2 * H:], vec, r, C, u, meta.fep_imgs[l],
-                                        meta.rbf, graph, meta.heads, g_xa, gV, g_qkv[:, :H], g_qkv[:, H:2 * H],
+            kernels.et_fused_bwd_launch(qkv[:, :H], qkv[:, H:2 * H], qkv[:, 2 * H:], vec, C, u, meta.fep_imgs[l],
+                                        meta.fep_frag, graph, meta.heads, g_xa, gV, g_qkv[:, :H], g_qkv[:, H:2 * H],
                                         g_qkv[:, 2 * H:], g_vec_in, g_C, g_u, g_r, accumulate=flags)
         else:
             pk = pkv[:, :H] if meta.hk else None

@@ -23,7 +23,6 @@ def _distance_modules(model):
 
 class GraphedEnergyForces:
     def __init__(self, model, z, pos, batch, edge_capacity=None, margin=1.25, warmup=3):
-        from . import kernels
         if not model.derivative:
             raise ValueError("GraphedEnergyForces captures TorchMD_Net(derivative=True)")
         rep = model.representation_model
@@ -32,8 +31,6 @@ class GraphedEnergyForces:
         self.z = z.clone()
         self.batch = batch.clone()
         self.pos = pos.detach().clone()
-        if getattr(rep, "reorder_atoms", False) and z.shape[0] >= kernels.REORDER_MIN_ATOMS:
-            raise NotImplementedError("capture of the spatially renumbered large-system path")
         # eager warm-up: sizes the edge capacity and the molecule count
         y, f = model(self.z, self.pos.clone(), self.batch)
         dists = _distance_modules(model)

@@ -583,30 +583,58 @@ def fep_supported(H, heads, R, dtype):
     return H == 128 and heads == 8 and R in (32, 64) and dtype == torch.float32
 
 
-def et_fused_fwd_launch(q, k, v, vec, r, C, u, fep, rbf, graph, heads, xo, vo, flags=0):
+def fep_frags(r_rows, mu, beta, cl, cu, rbf_type):
+    """The RBF / d RBF / d r MFMA fragments of the fused kernels for projection rows at distances r_rows
+    (``tmdnet_fep_frags_f32``; once per evaluation, every layer reads them).  Returns (frags, dscale)."""
+    lib = nat.load()
+    rows, R = int(r_rows.shape[0]), int(mu.shape[0])
+    fr = torch.empty(max(1, int(lib.tmdnet_fep_frags_bytes(rows, R)) // 2), dtype=torch.float16,
+                     device=r_rows.device)
+    dsc = torch.empty(max(1, rows), dtype=torch.float32, device=r_rows.device)
+    rc = lib.tmdnet_fep_frags_f32(rows, R, nat.ptr(r_rows.contiguous()), nat.ptr(mu.contiguous()),
+                                  nat.ptr(beta.contiguous()), float(cl), float(cu), int(rbf_type), nat.ptr(fr),
+                                  nat.ptr(dsc), nat.stream(r_rows.device))
+    nat.check(rc, "tmdnet_fep_frags_f32")
+    return fr, dsc
+
+
+def fep_frag_set(graph, r, rbf, pairs=None):
+    """(frag_rows [E] int32, frags, dscale, rows): the fragment set of one evaluation -- per pair row when
+    the graph has pair numbers (both directions of a pair read one row), else per edge."""
+    mu, beta, cl, cu, rt = rbf
+    if pairs is not None:
+        frag_rows, r_rows = pairs[0], r.detach().index_select(0, pairs[1].long())
+    else:
+        frag_rows = torch.arange(graph.n_edges, dtype=torch.int32, device=r.device)
+        r_rows = r.detach()
+    fr, dsc = fep_frags(r_rows, mu, beta, cl, cu, rt)
+    return frag_rows, fr, dsc, int(r_rows.shape[0])
+
+
+def et_fused_fwd_launch(q, k, v, vec, C, u, fep, frag, graph, heads, xo, vo, flags=0):
     """One ``tmdnet_et_fused_fwd_f32`` launch: the ET message with the dk/dv projection fused in
-    (``fep`` = fep_split(W, b) of the layer; ``rbf`` = (mu, beta, cutoff_lower, cutoff_upper, type));
+    (``fep`` = fep_split(W, b) of the layer; ``frag`` = fep_frag_set(...) of the evaluation);
     ``flags``: nat.ET_V_PLANAR when v is in the planar layout."""
     lib = nat.load()
     N, H = q.shape
-    mu, beta, cl, cu, rt = rbf
     img, wsc, bo = fep
+    frag_rows, fr, _, rows = frag
     probe = EVENT_PROBE
     if probe is not None:
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ev0.record()
-    rc = lib.tmdnet_et_fused_fwd_f32(N, H, heads, mu.shape[0], nat.ptr(graph.row_ptr), nat.ptr(graph.src),
-                                     graph.n_edges, nat.ptr(q), _ld(q), nat.ptr(k), _ld(k), nat.ptr(v), _ld(v),
-                                     nat.ptr(vec), nat.ptr(r), nat.ptr(C), nat.ptr(u), nat.ptr(img), nat.ptr(wsc),
-                                     nat.ptr(bo), nat.ptr(mu), nat.ptr(beta), float(cl), float(cu), int(rt),
-                                     nat.ptr(xo), nat.ptr(vo), int(flags) & nat.ET_V_PLANAR, nat.stream(q.device))
+    rc = lib.tmdnet_et_fused_fwd_f32(N, H, heads, img.numel() // (2 * 4 * H), nat.ptr(graph.row_ptr),
+                                     nat.ptr(graph.src), graph.n_edges, nat.ptr(q), _ld(q), nat.ptr(k), _ld(k),
+                                     nat.ptr(v), _ld(v), nat.ptr(vec), nat.ptr(C), nat.ptr(u), nat.ptr(frag_rows),
+                                     nat.ptr(fr), rows, nat.ptr(img), nat.ptr(wsc), nat.ptr(bo), nat.ptr(xo),
+                                     nat.ptr(vo), int(flags) & nat.ET_V_PLANAR, nat.stream(q.device))
     nat.check(rc, "tmdnet_et_fused_fwd_f32")
     if probe is not None:
         ev1.record()
         probe.append((ev0, ev1, graph.n_edges, N, H))
 
 
-def et_fused_bwd_launch(q, k, v, vec, r, C, u, fep, rbf, graph, heads, gx, gvec, gq, gk, gv, gw, gC, gu, g_r,
+def et_fused_bwd_launch(q, k, v, vec, C, u, fep, frag, graph, heads, gx, gvec, gq, gk, gv, gw, gC, gu, g_r,
                         accumulate=0):
     """``tmdnet_et_fused_bwd_f32``: the fused message's force-pass backward (dr mode: g_r accumulated,
     no projection rows); gradients land in the given buffers with their inputs' row strides."""
@@ -614,14 +642,18 @@ def et_fused_bwd_launch(q, k, v, vec, r, C, u, fep, rbf, graph, heads, gx, gvec,
         raise ValueError("et_fused_bwd: gradients must have the row strides of q / k / v")
     lib = nat.load()
     N, H = q.shape
-    mu, beta, cl, cu, rt = rbf
     img, wsc, bo = fep
-    rc = lib.tmdnet_et_fused_bwd_f32(N, H, heads, mu.shape[0], nat.ptr(graph.row_ptr), nat.ptr(graph.src),
-                                     graph.n_edges, nat.ptr(q), _ld(q), nat.ptr(k), _ld(k), nat.ptr(v), _ld(v),
-                                     nat.ptr(vec), nat.ptr(r), nat.ptr(C), nat.ptr(u), nat.ptr(img), nat.ptr(wsc),
-                                     nat.ptr(bo), nat.ptr(mu), nat.ptr(beta), float(cl), float(cu), int(rt),
-                                     nat.ptr(gx), nat.ptr(gvec), nat.ptr(gq), nat.ptr(gk), nat.ptr(gv), nat.ptr(gw),
-                                     nat.ptr(gC), nat.ptr(gu), nat.ptr(g_r), int(accumulate), nat.stream(q.device))
+    frag_rows, fr, dsc, rows = frag
+    cap = graph.n_edges
+    wsb = int(lib.tmdnet_et_fused_bwd_workspace_bytes(cap))
+    ws = torch.empty(max(1, wsb // 4), dtype=torch.float32, device=q.device) if wsb else None
+    rc = lib.tmdnet_et_fused_bwd_f32(N, H, heads, img.numel() // (2 * 4 * H), nat.ptr(graph.row_ptr),
+                                     nat.ptr(graph.src), cap, nat.ptr(q), _ld(q), nat.ptr(k), _ld(k), nat.ptr(v),
+                                     _ld(v), nat.ptr(vec), nat.ptr(C), nat.ptr(u), nat.ptr(frag_rows), nat.ptr(fr),
+                                     nat.ptr(dsc), rows, nat.ptr(img), nat.ptr(wsc), nat.ptr(bo), nat.ptr(gx),
+                                     nat.ptr(gvec), nat.ptr(gq), nat.ptr(gk), nat.ptr(gv), nat.ptr(gw), nat.ptr(gC),
+                                     nat.ptr(gu), nat.ptr(g_r), int(accumulate), nat.ptr(ws), wsb,
+                                     nat.stream(q.device))
     nat.check(rc, "tmdnet_et_fused_bwd_f32")
 
 
