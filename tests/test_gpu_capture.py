@@ -162,6 +162,9 @@ def test_static_capacity_build_replay_padding_contract(strategy):
         # poison every output slot: a replay must rewrite all of them
         for t in (g.src, g.dst, g.transpose, g.row_ptr):
             t.fill_(0x7ABCDEF)
+        if getattr(g, "_pairs", None) is not None:
+            for t in g._pairs:
+                t.fill_(0x7ABCDEF)
         g.deltas.detach().fill_(7.0)
         g.distances.detach().fill_(7.0)
         cg.replay()
@@ -190,6 +193,14 @@ def test_static_capacity_build_replay_padding_contract(strategy):
             seen_overflow = True
             assert bool(g.overflow.item())
             assert np.all((tr[:K] >= -1) & (tr[:K] < cap))
+        if getattr(g, "_pairs", None) is not None:
+            # every pair row index and every pair's canonical edge stays in range, also when the list
+            # overflowed (consumers gather r / f through pair_edge: an unwritten slot would be a wild index)
+            pr, pe = g._pairs[0].cpu().numpy(), g._pairs[1].cpu().numpy()
+            assert np.all((pr >= 0) & (pr < pe.shape[0])) and np.all((pe >= 0) & (pe < cap))
+            if P <= cap:
+                canon = src[:P] >= dst[:P]
+                assert np.array_equal(pe[pr[:P][canon]], np.nonzero(canon)[0])
     assert seen_overflow and seen_under
 
 

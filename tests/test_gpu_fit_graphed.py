@@ -88,7 +88,7 @@ def test_fit_graphed_matches_eager_fit(tmp_path):
     hp = dict(yaml_args("equivariant-transformer", embedding_dimension=64, num_layers=2, num_rbf=32, num_heads=8,
                         derivative=True), batch_size=16, inference_batch_size=16, train_size=64, val_size=16,
                      test_size=0, seed=1, lr=5e-4, lr_warmup_steps=3, y_weight=0.3, neg_dy_weight=0.7,
-                     ema_alpha_y=0.9, ema_alpha_neg_dy=1.0)
+                     ema_alpha_y=0.9, ema_alpha_neg_dy=1.0, log_dir=str(tmp_path))
     hist = []
     for graphed in (False, True):
         torch.manual_seed(0)

@@ -166,6 +166,10 @@ def test_tensornet_periodic_box_vs_oracle(static_shapes, large_switches):
                      max_num_neighbors=64, derivative=True, static_shapes=static_shapes)
     torch.manual_seed(0)
     m = create_model(args)
+    # create_model does not forward static_shapes (neither does the reference's, models/model.py:81-84: TensorNet
+    # keeps its default True); set it on the module as a user would
+    m.representation_model.static_shapes = static_shapes
+    m.representation_model.distance.resize_to_fit = not static_shapes
     z, pos, batch, L = _water_box(1500, seed=3)
     y_ref, f_ref = O.energy_forces(m.state_dict(), _cfg(args, L), z, pos, batch, static_shapes=static_shapes)
     m = _periodic(m.to(DEV), L)

@@ -232,7 +232,23 @@ __global__ void k_transpose(int32_t* __restrict__ nb, const int* __restrict__ ro
                             const int* __restrict__ num_pairs, int32_t* __restrict__ tr, int pad,
                             T* __restrict__ dlt, T* __restrict__ dist, Pairs PR) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (PR.prow && e < PR.slots && e >= PR.pair_ptr[PR.n]) PR.pedge[e] = 0;
+  if (SORTED_ROWS && PR.prow && e < PR.slots) {
+    // canonical edge of pair e, as a gather (every slot written once, always an edge index in [0, cap)):
+    // its row r is the last with pair_ptr[r] <= e, its position the (e - pair_ptr[r])-th of the row's
+    // canonical suffix.  A pair whose canonical edge fell past a capacity-truncated list gets edge 0 (the
+    // build reports the overflow; the scatter form left such slots unwritten -- garbage indices)
+    int edge = 0;
+    if (e < PR.pair_ptr[PR.n]) {
+      int lo = 0, hi = PR.n - 1;
+      while (lo < hi) {
+        const int m = (lo + hi + 1) >> 1;
+        if (PR.pair_ptr[m] <= e) lo = m; else hi = m - 1;
+      }
+      const int k = e - PR.pair_ptr[lo] + min(row_ptr[lo + 1], cap) - PR.cc[lo];
+      edge = (k >= 0 && k < cap) ? k : 0;
+    }
+    PR.pedge[e] = edge;
+  }
   if (e >= cap) return;
   if (e >= num_pairs[0]) {  // unwritten slot
     if (pad) {
@@ -274,7 +290,6 @@ __global__ void k_transpose(int32_t* __restrict__ nb, const int* __restrict__ ro
     if (s >= 0 && k >= 0) {
       pid = PR.pair_ptr[r] + k - (min(row_ptr[r + 1], cap) - PR.cc[r]);
       if (pid < 0 || pid >= PR.slots) pid = 0;
-      else if (canon) PR.pedge[pid] = e;
     }
     PR.prow[e] = pid;
   }

@@ -137,6 +137,8 @@ class DataModule:
                 self.dataset = getattr(datasets, hp["dataset"])(hp["dataset_root"], **(hp.get("dataset_arg") or {}))
         self.dataset = FloatCast(self.dataset, dtype_mapping[hp.get("precision", 32)])
         log_dir = hp.get("log_dir")
+        if log_dir:  # (the reference's Lightning logger creates it before the data module saves the splits)
+            os.makedirs(log_dir, exist_ok=True)
         self.idx_train, self.idx_val, self.idx_test = make_splits(
             len(self.dataset), hp["train_size"], hp["val_size"], hp["test_size"], hp["seed"],
             os.path.join(log_dir, "splits.npz") if log_dir else None, hp.get("splits"))

@@ -1628,8 +1628,10 @@ def spatial_permutation(pos, batch, cell_size, box=None):
     C5 water box vs random numbering (tools/kbench.py).  Sync-free (device argsort)."""
     p = pos.detach()
     if box is not None and box.numel() == 9:
-        L = torch.diagonal(box.to(p.device, p.dtype))
-        p = p - torch.floor(p / L) * L
+        # the box lives in host memory (reference OptimizedDistance keeps it on the CPU): its diagonal as
+        # Python scalars, so no host-to-device copy is issued (not allowed inside a graph capture)
+        L = torch.diagonal(box.detach().cpu()).tolist()
+        p = torch.stack([torch.remainder(p[:, i], float(L[i])) for i in range(3)], dim=1)
     lo = p.min(dim=0).values
     c = torch.clamp(((p - lo) / float(cell_size)).long(), 0, 1023)
     key = _spread10(c[:, 0]) | (_spread10(c[:, 1]) << 1) | (_spread10(c[:, 2]) << 2)

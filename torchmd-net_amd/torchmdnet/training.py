@@ -452,7 +452,9 @@ class PaddedGraphedTrainer:
         self.steps[int(b.capacity)] = st
         return st
 
-    def _run(self, b):
+    def _run(self, b, gs):
+        """Replay (capturing first if needed) the step of batch ``b`` as global step ``gs`` (the warm-up
+        schedule's index), all-reduce, AdamW (skipped on the device on overflow)."""
         st = self.steps.get(int(b.capacity))
         if st is None:
             st = self._capture(b)
@@ -460,21 +462,34 @@ class PaddedGraphedTrainer:
         st.graph.replay()
         self.reduce()
         self.found_inf.copy_(self.reduce.flag[0].sign())
-        if self.lr_warmup_steps and self.global_step < self.lr_warmup_steps:
-            scale = min(1.0, float(self.global_step + 1) / float(self.lr_warmup_steps))
+        if self.lr_warmup_steps and gs < self.lr_warmup_steps:
+            scale = min(1.0, float(gs + 1) / float(self.lr_warmup_steps))
             for g in self.opt.param_groups:
                 g["lr"] = scale * self.lr
         self.opt.step()
         self._flag_host.copy_(self.reduce.flag, non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
-        self._pending = (b, ev)
-        return st
+        return st, ev
+
+    def _loss_terms(self, st):
+        """(L_y, L_f, total) of the replayed step with the reference's EMA (updates ``self.ema``)."""
+        ly, lf = st.ly.detach().clone(), st.lf.detach().clone()
+        out = []
+        for kind, raw, alpha in (("y", ly, self.alpha_y), ("neg_dy", lf, self.alpha_f)):
+            if alpha < 1:
+                prev = self.ema.get(kind, raw)
+                raw = alpha * raw + (1 - alpha) * prev
+                self.ema[kind] = raw.detach()
+            out.append(raw)
+        return [out[0], out[1], out[0] * self.y_weight + out[1] * self.neg_dy_weight]
 
     def _settle(self):
-        """Check the previous step's overflow flag; recapture + redo it if it was skipped."""
+        """Check the previous step's overflow flag; recapture + redo it if it was skipped.  The redo runs
+        as the same global step from the same EMA state and writes its losses INTO the device scalars the
+        skipped step returned."""
         while self._pending is not None:
-            b, ev = self._pending
+            b, ev, gs, ema0, outs = self._pending
             ev.synchronize()
             if float(self._flag_host[0]) <= 0:
                 self._pending = None
@@ -485,23 +500,25 @@ class PaddedGraphedTrainer:
             del old
             self.recaptures += 1
             self._capture(b, need)
-            self._run(b)
+            self.ema = dict(ema0)
+            st, ev = self._run(b, gs)
+            for o, n in zip(outs, self._loss_terms(st)):
+                o.copy_(n)
+            self._pending = (b, ev, gs, ema0, outs)
 
     def step(self, b):
         """One training step on a padded device batch; returns (L_y, L_f, total) device scalars (the
-        reported loss applies the reference's EMA)."""
+        reported loss applies the reference's EMA).  They are final once the NEXT ``step`` (or
+        ``finish``) has returned: a step found to have overflowed the edge capacity is redone then, and
+        its losses are rewritten in place."""
         self._settle()
-        st = self._run(b)
-        ly, lf = st.ly.detach().clone(), st.lf.detach().clone()
-        out = []
-        for kind, raw, alpha in (("y", ly, self.alpha_y), ("neg_dy", lf, self.alpha_f)):
-            if alpha < 1:
-                prev = self.ema.get(kind, raw)
-                raw = alpha * raw + (1 - alpha) * prev
-                self.ema[kind] = raw.detach()
-            out.append(raw)
+        gs = self.global_step
+        ema0 = dict(self.ema)
+        st, ev = self._run(b, gs)
+        outs = self._loss_terms(st)
+        self._pending = (b, ev, gs, ema0, outs)
         self.global_step += 1
-        return out[0], out[1], out[0] * self.y_weight + out[1] * self.neg_dy_weight
+        return tuple(outs)
 
     def finish(self):
         self._settle()
