@@ -38,6 +38,8 @@
 // per-edge sums g_cut, g_unit, g_r over every channel stay in one wave; d pre / d r = W f'(r) formed on
 // the MFMA beside the projection) and a SOURCE pass over the same rows read as reversed edges (gk, gv,
 // gvec_in; no per-edge outputs, so HPW heads per item).  Deterministic, no atomics on outputs.
+#include <cstdlib>
+
 #include "common.h"
 #include "tmdnet.h"
 
@@ -321,15 +323,43 @@ template <bool PL> struct VL {
   static constexpr int part = PL ? kH : 16;  // floats from part p to part p + 1
 };
 
-struct Work {  // the workgroup's node range and its work-item count
-  int n0, items;
+// The workgroup's nodes.  Hardware deals workgroups round-robin over the 8 XCDs; each XCD takes one
+// contiguous node range, cut into chunks of `chk` nodes dealt round-robin to the XCD's m workgroups (the
+// j-th takes chunks j, j + m, ...).  At any moment the XCD's CUs then work on ONE window of about m * chk
+// consecutive -- Morton-ordered, so spatially close -- nodes whose source rows they share in that XCD's
+// L2 (a contiguous range per workgroup spread an XCD's in-flight nodes over m separate windows).
+struct Work {
+  int x0, x1, j, m, chk, items;
 };
 template <int G>
-__device__ __forceinline__ Work work_range(int n) {
-  const int nwg = gridDim.x, lb = xcd_remap(blockIdx.x, nwg);
-  const int per = (n + nwg - 1) / nwg;
-  const int n0 = lb * per, n1 = min(n, n0 + per);
-  return Work{n0, max(0, n1 - n0) * G};
+__device__ __forceinline__ Work work_range(int n, int chk) {
+  const int nwg = gridDim.x;
+  Work W;
+  W.chk = chk;
+  if (nwg >= 16 && nwg % 8 == 0) {
+    const int per = (n + 7) / 8, x = blockIdx.x % 8;
+    W.x0 = min(n, x * per);
+    W.x1 = min(n, W.x0 + per);
+    W.j = blockIdx.x / 8;
+    W.m = nwg / 8;
+  } else {
+    W.x0 = 0;
+    W.x1 = n;
+    W.j = blockIdx.x;
+    W.m = nwg;
+  }
+  const int nch = (W.x1 - W.x0 + chk - 1) / chk;
+  const int mine = W.j < nch ? (nch - W.j + W.m - 1) / W.m : 0;
+  W.items = mine * chk * G;
+  return W;
+}
+// item -> (node, slice); false past the end of the XCD's range (a partial last chunk)
+template <int G>
+__device__ __forceinline__ bool work_item(const Work& W, int it, int& t, int& sl) {
+  const int per = W.chk * G, k = it / per, rem = it - k * per;
+  t = W.x0 + (W.j + k * W.m) * W.chk + rem / G;
+  sl = rem % G;
+  return t < W.x1;
 }
 __device__ __forceinline__ int next_item(int* counter) {
   int it = 0;
@@ -363,7 +393,7 @@ __device__ __forceinline__ Edge load_edge(int e, int re, const int32_t* src, con
 
 // ------------------------------------------------------------------ forward
 struct Fwd {
-  int n, cap;
+  int n, cap, chunk;
   const int32_t* row_ptr;
   const int32_t* src;
   const float* q; int ldq;
@@ -394,7 +424,7 @@ __global__ __launch_bounds__(NW * 64, 1) void k_fwd(Fwd P) {
   load_image<KS, NW * 64>(w, s_sc, s_b, P.img, P.wsc, P.bias);
   if (threadIdx.x == 0) s_next = 0;
   __syncthreads();
-  const Work W = work_range<G>(P.n);
+  const Work W = work_range<G>(P.n, P.chunk);
   const int lane = lane_id(), c = lane & 15, g = lane >> 4, wid = threadIdx.x >> 6;
   const rsrc_t Rk = make_rsrc(P.k, (unsigned)P.n * P.ldk * 4u), Rv = make_rsrc(P.v, (unsigned)P.n * P.ldv * 4u);
   const rsrc_t Rw = make_rsrc(P.vec, P.vec ? (unsigned)P.n * 3u * H * 4u : 0u);
@@ -403,7 +433,9 @@ __global__ __launch_bounds__(NW * 64, 1) void k_fwd(Fwd P) {
   for (;;) {
     const int it = next_item(&s_next);
     if (it >= W.items) break;
-    const int t = W.n0 + it / G, h0 = (it % G) * HPW;
+    int t, sl;
+    if (!work_item<G>(W, it, t, sl)) continue;
+    const int h0 = sl * HPW;
     const int rb = min(P.row_ptr[t], P.cap), re = min(P.row_ptr[t + 1], P.cap);
     __builtin_amdgcn_wave_barrier();  // the previous item's reads of sq are done (in-order LDS)
     if (lane < 4 * HPW)
@@ -482,7 +514,7 @@ __global__ __launch_bounds__(NW * 64, 1) void k_fwd(Fwd P) {
 
 // ------------------------------------------------------------------ backward (force pass, "dr mode")
 struct Bwd {
-  int n, cap, acc;
+  int n, cap, acc, chunk;
   const int32_t* row_ptr;
   const int32_t* src;
   const float* q; int ldq;
@@ -533,7 +565,7 @@ __global__ __launch_bounds__(NW * 64, 1) void k_bwd_dst(Bwd P) {
     }
   }
   __syncthreads();
-  const Work W = work_range<G>(P.n);
+  const Work W = work_range<G>(P.n, P.chunk);
   const int lane = lane_id(), c = lane & 15, g = lane >> 4, wid = threadIdx.x >> 6;
   const bool acc_edge = P.acc & TMDNET_ACC_EDGE, ag = P.acc & TMDNET_ACC_GRADS;
   const rsrc_t Rk = make_rsrc(P.k, (unsigned)P.n * P.ldk * 4u), Rv = make_rsrc(P.v, (unsigned)P.n * P.ldv * 4u);
@@ -543,7 +575,9 @@ __global__ __launch_bounds__(NW * 64, 1) void k_bwd_dst(Bwd P) {
   for (;;) {
     const int it = next_item(&s_next);
     if (it >= W.items) break;
-    const int t = W.n0 + it / G, sl = it % G, h0 = sl * HPW;
+    int t, sl;
+    if (!work_item<G>(W, it, t, sl)) continue;
+    const int h0 = sl * HPW;
     const int rb = min(P.row_ptr[t], P.cap), re = min(P.row_ptr[t + 1], P.cap);
     // stage the slice's q[t] | gx[t] | gvec[t] channels (5 CH floats)
     __builtin_amdgcn_wave_barrier();
@@ -709,7 +743,7 @@ __global__ __launch_bounds__(NW * 64, 1) void k_bwd_src(Bwd P) {
   load_image<KS, NW * 64>(w, s_sc, s_b, P.img, P.wsc, P.bias);
   if (threadIdx.x == 0) s_next = 0;
   __syncthreads();
-  const Work W = work_range<G>(P.n);
+  const Work W = work_range<G>(P.n, P.chunk);
   const int lane = lane_id(), c = lane & 15, g = lane >> 4, wid = threadIdx.x >> 6;
   const bool ag = P.acc & TMDNET_ACC_GRADS, resid = P.acc & TMDNET_ACC_VEC_RESIDUAL;
   float* nd = s_node[wid];
@@ -720,7 +754,9 @@ __global__ __launch_bounds__(NW * 64, 1) void k_bwd_src(Bwd P) {
   for (;;) {
     const int it = next_item(&s_next);
     if (it >= W.items) break;
-    const int j = W.n0 + it / G, h0 = (it % G) * HPW;
+    int j, sl;
+    if (!work_item<G>(W, it, j, sl)) continue;
+    const int h0 = sl * HPW;
     const int rb = min(P.row_ptr[j], P.cap), re = min(P.row_ptr[j + 1], P.cap);
     // stage j's k, v_x, v_1, vec channels of the slice (6 CH floats; vec absent: zeros)
     __builtin_amdgcn_wave_barrier();
@@ -852,11 +888,53 @@ static int num_cus() {
   return n;
 }
 
+// nodes per scheduling chunk (work_range); TMDNET_FEP_CHUNK overrides (A/B)
+static int chunk_nodes() {
+  static int c = [] {
+    const char* e = getenv("TMDNET_FEP_CHUNK");
+    const int v = e ? atoi(e) : 0;
+    return v > 0 ? v : 2;
+  }();
+  return c;
+}
+
+// launch-form A/B switches (measured on C5, tools/fep_time.py; one workgroup per CU, no variant spills):
+// TMDNET_FEP_FWD_FORM 1 = the round-4 first form, 2 heads per item on 12 waves (1.46 ms vs 1.34 ms for the
+// default 4 heads on 8 waves); TMDNET_FEP_DST_FORM 1 = 4 heads on 4 waves (3.78 vs 3.42 ms per backward);
+// TMDNET_FEP_SRC_FORM 1 = 2 heads on 12 waves (3.43 vs 3.38).  Measured and dropped: 1 head on 16 waves
+// (fwd 1.78, src 3.64), 8 heads on 4 waves (fwd 1.65, dst 3.67, src 4.16), the one-tile-ahead edge
+// prefetch with both heads' gathers issued first on 8 waves (fwd 1.51 vs 1.46 at 2 heads)
+static int fwd_form() {
+  static int f = [] {
+    const char* e = getenv("TMDNET_FEP_FWD_FORM");
+    return e ? atoi(e) : 0;
+  }();
+  return f;
+}
+
+
+static int bwd_form(int which) {
+  static int f[2] = {[] {
+                       const char* e = getenv("TMDNET_FEP_DST_FORM");
+                       return e ? atoi(e) : 0;
+                     }(),
+                     [] {
+                       const char* e = getenv("TMDNET_FEP_SRC_FORM");
+                       return e ? atoi(e) : 0;
+                     }()};
+  return f[which];
+}
+static int dst_hpw();
+
 // launch shapes (heads per work item, waves per workgroup; one workgroup per CU): chosen so that no
 // variant spills (tools/regs.py) -- see the launchers
-constexpr int kFwdHPW = 2, kFwdNW = 12;
+constexpr int kFwdHPW = 4, kFwdNW = 8;
 constexpr int kDstHPW = 2, kDstNW = 8;  // 12 waves: 6-14 spilled VGPRs
-constexpr int kSrcHPW = 2, kSrcNW = 12;
+constexpr int kSrcHPW = 4, kSrcNW = 8;
+static int dst_hpw() {
+  const int f = bwd_form(0);
+  return f == 1 ? 4 : kDstHPW;
+}
 
 }  // namespace fep
 }  // namespace tmd
@@ -931,7 +1009,7 @@ extern "C" int tmdnet_et_fused_fwd_f32(int n, int H, int heads, int R, const int
   if (rc) return rc;
   if ((((uintptr_t)x_out) | ((uintptr_t)vec_out) | ((uintptr_t)frags)) & 15) return kUnsupported;
   fep::Fwd P{};
-  P.n = n; P.cap = cap;
+  P.n = n; P.cap = cap; P.chunk = fep::chunk_nodes();
   P.row_ptr = row_ptr; P.src = src;
   P.q = (const float*)q; P.ldq = ldq; P.k = (const float*)k; P.ldk = ldk; P.v = (const float*)v; P.ldv = ldv;
   P.vec = (const float*)vec; P.C = (const float*)C; P.u = (const float*)u;
@@ -942,7 +1020,13 @@ extern "C" int tmdnet_et_fused_fwd_f32(int n, int H, int heads, int R, const int
   const bool pl = flags & TMDNET_ET_V_PLANAR;
   hipStream_t st = (hipStream_t)stream;
   constexpr int NW = fep::kFwdNW, HPW = fep::kFwdHPW;
-#define TMD_FEP(KS_, PL_) hipLaunchKernelGGL((fep::k_fwd<KS_, HPW, NW, PL_>), dim3(nwg), dim3(NW * 64), 0, st, P)
+#define TMD_FEP(KS_, PL_)                                                                                  \
+  do {                                                                                                     \
+    if (fep::fwd_form() == 1)                                                                              \
+      hipLaunchKernelGGL((fep::k_fwd<KS_, 2, 12, PL_>), dim3(nwg), dim3(12 * 64), 0, st, P);                \
+    else                                                                                                   \
+      hipLaunchKernelGGL((fep::k_fwd<KS_, HPW, NW, PL_>), dim3(nwg), dim3(NW * 64), 0, st, P);              \
+  } while (0)
   if (R == 64) {
     if (pl) TMD_FEP(2, true); else TMD_FEP(2, false);
   } else {
@@ -953,7 +1037,7 @@ extern "C" int tmdnet_et_fused_fwd_f32(int n, int H, int heads, int R, const int
 }
 
 extern "C" size_t tmdnet_et_fused_bwd_workspace_bytes(int cap) {
-  constexpr int S = fep::kHeads / fep::kDstHPW;
+  const int S = fep::kHeads / fep::dst_hpw();
   return S > 1 && cap > 0 ? (size_t)S * 5 * cap * sizeof(float) : 0;
 }
 
@@ -976,7 +1060,7 @@ extern "C" int tmdnet_et_fused_bwd_f32(int n, int H, int heads, int R, const int
   const size_t need = tmdnet_et_fused_bwd_workspace_bytes(cap);
   if (need && (!workspace || workspace_bytes < need)) return kWorkspaceTooSmall;
   fep::Bwd P{};
-  P.n = n; P.cap = cap; P.acc = accumulate;
+  P.n = n; P.cap = cap; P.acc = accumulate; P.chunk = fep::chunk_nodes();
   P.row_ptr = row_ptr; P.src = src;
   P.q = (const float*)q; P.ldq = ldq; P.k = (const float*)k; P.ldk = ldk; P.v = (const float*)v; P.ldv = ldv;
   P.vec = (const float*)vec; P.C = (const float*)C; P.u = (const float*)u;
@@ -988,16 +1072,21 @@ extern "C" int tmdnet_et_fused_bwd_f32(int n, int H, int heads, int R, const int
   P.gC = (float*)gC; P.gu = (float*)gu; P.gr = (float*)gdist;
   P.part = (float*)workspace;
   const int nwg = fep::num_cus();
-  constexpr int S = fep::kHeads / fep::kDstHPW;
+  const int S = fep::kHeads / fep::dst_hpw();
   const bool pl = accumulate & TMDNET_ET_V_PLANAR;
   hipStream_t st = (hipStream_t)stream;
+  const int dform = fep::bwd_form(0), sform = fep::bwd_form(1);
+#define TMD_DST(KS_, PL_, HPW_, NW_) \
+  hipLaunchKernelGGL((fep::k_bwd_dst<KS_, HPW_, NW_, PL_>), dim3(nwg), dim3(NW_ * 64), 0, st, P)
+#define TMD_SRC(KS_, PL_, HPW_, NW_) \
+  hipLaunchKernelGGL((fep::k_bwd_src<KS_, HPW_, NW_, PL_>), dim3(nwg), dim3(NW_ * 64), 0, st, P)
 #define TMD_BWD(KS_, PL_)                                                                                          \
   do {                                                                                                             \
-    hipLaunchKernelGGL((fep::k_bwd_dst<KS_, fep::kDstHPW, fep::kDstNW, PL_>), dim3(nwg), dim3(fep::kDstNW * 64), 0, \
-                       st, P);                                                                                     \
+    if (dform == 1) TMD_DST(KS_, PL_, 4, 4);                                                                        \
+    else TMD_DST(KS_, PL_, fep::kDstHPW, fep::kDstNW);                                                              \
     if (S > 1) hipLaunchKernelGGL(fep::k_edge_combine, dim3((cap + 255) / 256), dim3(256), 0, st, P, S);           \
-    hipLaunchKernelGGL((fep::k_bwd_src<KS_, fep::kSrcHPW, fep::kSrcNW, PL_>), dim3(nwg), dim3(fep::kSrcNW * 64), 0, \
-                       st, P);                                                                                     \
+    if (sform == 1) TMD_SRC(KS_, PL_, 2, 12);                                                                       \
+    else TMD_SRC(KS_, PL_, fep::kSrcHPW, fep::kSrcNW);                                                              \
   } while (0)
   if (R == 64) {
     if (pl) TMD_BWD(2, true); else TMD_BWD(2, false);
@@ -1005,5 +1094,7 @@ extern "C" int tmdnet_et_fused_bwd_f32(int n, int H, int heads, int R, const int
     if (pl) TMD_BWD(1, true); else TMD_BWD(1, false);
   }
 #undef TMD_BWD
+#undef TMD_DST
+#undef TMD_SRC
   return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
 }
