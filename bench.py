@@ -298,8 +298,10 @@ PROBE_FLAGS = 4  # TMDNET_ET_V_PLANAR
 
 PMC_PASSES = ("FETCH_SIZE", "WRITE_SIZE", "TCC_HIT_sum TCC_MISS_sum")
 # the child's dispatch sequence (main(), --pmc-child): probe kernel name -> [(tag, count), ...] in order
-PMC_CHILD = {"k_fwd<float, 4, 1, 1, false, false>": [("per_edge", 8), ("pairs", 8)],
-             "k_bwd_dst<": [("bwd_dst", 4)], "k_bwd_src<": [("bwd_src", 4)], "k_bwd_merged<": [("bwd_dr", 4)]}
+PMC_CHILD = {"et::k_fwd<float, 4, 1, 1, false, false>": [("per_edge", 8), ("pairs", 8)],
+             "et::k_bwd_dst<": [("bwd_dst", 4)], "et::k_bwd_src<": [("bwd_src", 4)], "et::k_bwd_merged<": [("bwd_dr", 4)],
+             "fep::k_fwd<": [("fused_fwd", 8)], "fep::k_bwd_dst<": [("fused_bwd_dst", 4)],
+             "fep::k_bwd_src<": [("fused_bwd_src", 4)], "fep::k_edge_combine": [("fused_edge_combine", 4)]}
 
 
 def pmc_counters(a):
@@ -412,9 +414,6 @@ def roofline_probe(a, dev):
            "bytes_per_launch": pbytes,
            "bytes_formula": "E*(4+4+4+12) + P*4H*4 + N*(12H*4+4): edge scalars, distinct pair rows, node rows",
            "ms_per_launch": round(ms_p, 4), "launches": reps, "per_edge_layout": per_edge}
-    fp = fused_projection_probe(launch, E, n_atoms, H, reps, dev)
-    if fp is not None:
-        res["fused_projection"] = fp
     # the backward (destination + source pass per call) in the model's layout, both forms
     bwd = {}
     for tag, dr in (("training_form", False), ("dr_force_form", True)):
@@ -435,6 +434,10 @@ def roofline_probe(a, dev):
                     "ms_per_call": round(ms_b, 4), "bytes_per_call": bb, "achieved": round(gb, 1),
                     "frac": round(gb / HBM_PEAK_GBS, 4), "calls": nrep}
     res["backward"] = bwd
+    fp = fused_projection_probe(launch, E, n_atoms, H, reps, dev,
+                                {"message_forward_ms": ms_p, "merged_backward_ms": bwd["dr_force_form"]["ms_per_call"]})
+    if fp is not None:
+        res["fused_projection"] = fp
     if not a.no_pmc:
         pm, why = pmc_counters(a)
         if pm is None:
@@ -446,6 +449,9 @@ def roofline_probe(a, dev):
             if g.get("traffic"):
                 res["traffic_detail"]["traffic_over_bytes"] = round(g["traffic"] / pbytes, 3)
             per_edge["pmc"] = pm.get("per_edge")
+            if fp is not None:
+                fp["forward"]["pmc"] = pm.get("fused_fwd")
+                fp["backward_dr"]["pmc"] = {k: pm.get(k) for k in ("fused_bwd_dst", "fused_edge_combine", "fused_bwd_src")}
             for tag, keys in (("training_form", ("bwd_dst", "bwd_src")), ("dr_force_form", ("bwd_dr",))):
                 bwd[tag]["pmc"] = {k: pm.get(k) for k in keys}
                 tr = sum((pm.get(k) or {}).get("traffic") or 0 for k in keys)
@@ -454,17 +460,16 @@ def roofline_probe(a, dev):
     return res
 
 
-def fused_projection_probe(launch, E, N, H, reps, dev, R=64):
-    """The forward edge kernel with the dk/dv projection fused in (tmdnet_et_fused_fwd_f32, csrc/et_fused.hip)
-    on the probe graph: the RBF of r formed in registers and [dk|dv] = W f + b on the fp16 MFMA (exact
-    two-piece split: 3 products per term), no projection rows read.  Two rooflines: bytes (edge scalars,
-    r, node rows) over HBM, and the MFMA work over the dense fp16 peak.  The model runs it when no
-    backward follows (energy-only evaluation): et_stack.FEP / FEP_BWD."""
+def fused_setup(launch, H, dev, R=64):
+    """The probe graph's inputs for the fused dk/dv-projection kernels (csrc/et_fused.hip), the path the
+    model takes on C5-size graphs (et_stack.FEP_MIN_EDGES): one layer's split weight image, the
+    evaluation's RBF fragments per pair row, and launchers of the forward and the force-pass backward."""
     from torchmdnet import kernels
     q, k, v, vec, C, u = launch.inputs
     if not kernels.fep_supported(H, 8, R, q.dtype):
         return None
     g = launch.graph
+    N = q.shape[0]
     r = g.distances.detach()
     gen = torch.Generator(device=dev).manual_seed(11)
     W = torch.randn(4 * H, R, device=dev, generator=gen) / R ** 0.5
@@ -475,28 +480,95 @@ def fused_projection_probe(launch, E, N, H, reps, dev, R=64):
     fep = kernels.fep_split(W, b)
     frag = kernels.fep_frag_set(g, r, (mu, beta, 0.0, 5.0, 0), (launch.pair_row, launch.pair_edge))
     xo, vo = torch.empty(N, H, device=dev), torch.empty(N, 3, H, device=dev)
+    gx, gvec = torch.randn(N, H, device=dev, generator=gen), torch.randn(N, 3, H, device=dev, generator=gen)
+    E = g.n_edges
+    bufs = [torch.empty(N, H, device=dev), torch.empty(N, H, device=dev), torch.empty(N, 3 * H, device=dev),
+            torch.empty(N, 3, H, device=dev), torch.zeros(E, device=dev), torch.zeros(E, 3, device=dev),
+            torch.zeros(E, device=dev)]
 
-    def run():
-        kernels.et_fused_fwd_launch(q, k, v, vec, C, u, fep, frag, g, 8, xo, vo, flags=4)
-    for _ in range(5):
-        run()
+    class F:
+        pass
+    f = F()
+    f.R = R
+    # the unfused counterparts' projection GEMMs over the P pair rows (tmdnet_proj_f32, as the model issues them)
+    f_pairs = kernels.rbf_composite(r.index_select(0, launch.pair_edge.long()), mu, beta, 0.0, 5.0, 0).contiguous()
+    wp = kernels.proj_split(W)
+    f.proj = lambda: kernels.proj(f_pairs, W, b, wp=wp)
+    f.dproj = lambda: kernels.proj(kernels.rbf_deriv(r, mu, beta, 0.0, 5.0, 0, rows=launch.pair_edge), W, None, wp=wp)
+    f.fwd = lambda: kernels.et_fused_fwd_launch(q, k, v, vec, C, u, fep, frag, g, 8, xo, vo, flags=4)
+    f.bwd = lambda: kernels.et_fused_bwd_launch(q, k, v, vec, C, u, fep, frag, g, 8, gx, gvec, *bufs,
+                                                accumulate=1 | 2 | 4)
+    f.frags = lambda: kernels.fep_frag_set(g, r, (mu, beta, 0.0, 5.0, 0), (launch.pair_row, launch.pair_edge))
+    return f
+
+
+def _event_ms(fn, reps):
+    for _ in range(3):
+        fn()
     torch.cuda.synchronize()
     a0, b0 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a0.record()
     for _ in range(reps):
-        run()
+        fn()
     b0.record()
     torch.cuda.synchronize()
-    ms = a0.elapsed_time(b0) / reps
-    nbytes = E * (4 + 4 + 4 + 12) + N * (12 * H * 4 + 4)
+    return a0.elapsed_time(b0) / reps
+
+
+def fused_projection_probe(launch, E, N, H, reps, dev, unfused):
+    """The ET message with the dk/dv projection FUSED into the edge kernels (tmdnet_et_fused_fwd_f32 /
+    _bwd_f32, csrc/et_fused.hip) on the probe graph -- what the model runs per layer at C5 (E >= 131072,
+    et_stack.FEP_MIN_EDGES): the RBF of r as fp16 MFMA fragments (formed once per evaluation, shared by the
+    layers), [dk|dv] = W f + b (and d/dr = W f' in the backward) on the fp16 MFMA from an exact two-piece
+    split (3 products per term), no projection rows written or read.  Against the unfused pair-row layout:
+    forward = projection GEMM + message kernel, force-pass backward = d(dk,dv)/dr GEMM + merged dr pass.
+    Rooflines: algorithmic bytes over HBM and the MFMA work over the dense fp16 peak."""
+    f = fused_setup(launch, H, dev)
+    if f is None:
+        return None
+    R = f.R
+    ms = _event_ms(f.fwd, reps)
+    ms_b = _event_ms(f.bwd, max(4, reps // 2))
+    ms_fr = _event_ms(f.frags, 10)
+    P = launch.n_pairs
+    # edge scalars (src, fragment row, cutoff, unit vector), the P distinct fragment rows (two fp16 pieces of
+    # R values), node rows q, k, v, vec read and x, vec written, row_ptr
+    nbytes = E * (4 + 4 + 4 + 12) + P * 4 * R + N * (12 * H * 4 + 4)
     flop = 3 * 2.0 * E * R * 4 * H  # fp16 MFMA products (hi*hi, hi*lo, lo*hi)
-    return {"kernel": "tmdnet_et_fused_fwd_f32 (fep::k_fwd<2,8,0>)", "ms_per_launch": round(ms, 4),
-            "bytes_per_launch": nbytes, "achieved_gbs": round(nbytes / (ms * 1e-3) / 1e9, 1),
-            "frac_hbm": round(nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-            "mfma_flop_per_launch": flop, "achieved_tflops_f16": round(flop / (ms * 1e-3) / 1e12, 1),
-            "peak_tflops_f16": MFMA_BF16_PEAK_TFS, "frac_mfma": round(flop / (ms * 1e-3) / 1e12 / MFMA_BF16_PEAK_TFS, 4),
-            "bound": "VALU (PMC r03: 72% VALU-busy, 20% MFMA-busy; profiles/r03_fep_fwd_pmc_mode2.txt)",
-            "vs_unfused": "replaces the projection GEMM + this kernel in the pair layout"}
+    bbytes = E * (4 + 4 + 4 + 12) + N * 4 + P * (8 * R + 4)  # edge scalars, B and D fragment rows + scale
+    bbytes += N * (H + H + 3 * H + 3 * H + H + 3 * H) * 4 + N * (H + H + 3 * H + 3 * H) * 4  # node rows in / out
+    bbytes += 2 * E * (4 + 12) + 2 * E * 4                                              # g_cut, g_unit, g_r
+    bflop = 3 * 2.0 * E * R * 4 * H * 3  # pre + d pre/dr (destination pass), pre again (source pass)
+    res = {"kernels": "tmdnet_et_fused_fwd_f32 (fep::k_fwd, 4 heads per work item, 8 waves, one workgroup per CU, "
+                      "XCD-interleaved node chunks) and tmdnet_et_fused_bwd_f32 (fep::k_bwd_dst + k_edge_combine + "
+                      "k_bwd_src)",
+           "model_path": "C5 energy+forces per layer (et_stack.FEP / FEP_BWD, E >= 131072)",
+           "forward": {"ms_per_launch": round(ms, 4), "bytes_per_launch": nbytes,
+                       "achieved_gbs": round(nbytes / (ms * 1e-3) / 1e9, 1),
+                       "frac_hbm": round(nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                       "mfma_flop_per_launch": flop, "achieved_tflops_f16": round(flop / (ms * 1e-3) / 1e12, 1),
+                       "peak_tflops_f16": MFMA_BF16_PEAK_TFS,
+                       "frac_mfma": round(flop / (ms * 1e-3) / 1e12 / MFMA_BF16_PEAK_TFS, 4)},
+           "backward_dr": {"ms_per_call": round(ms_b, 4), "bytes_per_call": bbytes,
+                           "achieved_gbs": round(bbytes / (ms_b * 1e-3) / 1e9, 1),
+                           "frac_hbm": round(bbytes / (ms_b * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                           "mfma_flop_per_call": bflop,
+                           "achieved_tflops_f16": round(bflop / (ms_b * 1e-3) / 1e12, 1),
+                           "frac_mfma": round(bflop / (ms_b * 1e-3) / 1e12 / MFMA_BF16_PEAK_TFS, 4)},
+           "fragments_per_evaluation_ms": round(ms_fr, 4),
+           "bound": "latency of the dependent per-tile gathers (r04 PMC, profiles/r04_fep_pmc.txt: most wave "
+                    "cycles parked on memory waits, VALU and MFMA well below their issue rates)"}
+    if unfused:
+        t_proj, t_dproj = _event_ms(f.proj, 10), _event_ms(f.dproj, 10)
+        uf = round(unfused["message_forward_ms"] + t_proj, 4)
+        ub = round(unfused["merged_backward_ms"] + t_dproj, 4)
+        res["vs_unfused"] = {"unfused_forward_ms": uf, "unfused_backward_dr_ms": ub,
+                             "forward_speedup": round(uf / ms, 3) if uf else None,
+                             "backward_speedup": round(ub / ms_b, 3) if ub else None,
+                             "projection_gemm_ms": round(t_proj, 4), "dr_projection_ms": round(t_dproj, 4),
+                             "unfused": "forward = tmdnet_proj_f32 over the P pair rows + k_fwd (pair layout); backward = "
+                                        "d RBF/dr + the d(dk,dv)/dr GEMM over the pair rows + k_bwd_merged"}
+    return res
 
 
 def mfma_probe(E_c5, N_c5, E_c2, N_c2, H, R, dev):
@@ -1020,6 +1092,12 @@ def main():
             launch.bwd(False)
         for _ in range(4):
             launch.bwd(True)
+        fp = fused_setup(launch, a.channels, dev)
+        if fp is not None:
+            for _ in range(8):
+                fp.fwd()
+            for _ in range(4):
+                fp.bwd()
         torch.cuda.synchronize()
         return
     maybe_spawn(a)

@@ -438,6 +438,14 @@ int tmdnet_tn_message_bwd(int dtype, int n_nodes, int hidden, const int32_t* row
                           const int32_t* pad_pairs, int pad_capacity, const void* edge_attr,
                           int ld_ea, const void* comp, const void* grad_msg, void* g_edge_attr,
                           void* g_comp, void* stream);
+/* The same with g_comp_add ([9][N][H], or NULL) added to g_comp: the gradient the component tensor's
+ * other consumer (TensorNet's decompose(msg Y + Y msg), tensornet.py:398-401) contributes, so the
+ * autograd engine does not sum the two in a separate launch. */
+int tmdnet_tn_message_bwd_add(int dtype, int n_nodes, int hidden, const int32_t* row_ptr,
+                              const int32_t* src, int max_pairs, double self0_mult,
+                              const int32_t* pad_pairs, int pad_capacity, const void* edge_attr,
+                              int ld_ea, const void* comp, const void* grad_msg, const void* g_comp_add,
+                              void* g_edge_attr, void* g_comp, void* stream);
 
 /* TensorNet per-channel node algebra, one fused pass each (replaces the reference's elementwise
  * PyTorch chains).  X / "full" tensors are [N][H][3][3]; compact ones [9][N][H] as above.
@@ -481,6 +489,29 @@ int tmdnet_atom_sum_fwd(int dtype, int n_atoms, int n_mol, const void* x, const 
                         const void* std_, const void* mean, void* y, void* stream);
 int tmdnet_atom_sum_bwd(int dtype, int n_atoms, int n_mol, const void* grad_y, const int64_t* batch,
                         const void* std_, void* grad_x, void* stream);
+
+/* Scalar head tail fused with the reduction (output_modules.py:83-105, model.py:263-283):
+ *   y[b] = *mean + *std * sum_{n: batch[n] = b} (h[n] . w + *b0),  h [n_atoms][K] (ld_h), n_mol <= 8192
+ *   (std / mean / b0: device scalars, NULL = 1 / 0 / 0).  Backward: grad_h[n][k] = *std * grad_y[batch[n]] * w[k]. */
+int tmdnet_dot_sum_fwd(int dtype, int n_atoms, int K, const void* h, int ld_h, const void* w, const void* b0,
+                       int n_mol, const int64_t* batch, const void* std_, const void* mean, void* y, void* stream);
+int tmdnet_dot_sum_bwd(int dtype, int n_atoms, int K, const void* grad_y, const int64_t* batch, int n_mol,
+                       const void* std_, const void* w, void* grad_h, void* stream);
+
+/* LayerNorm over the last dimension, fp32, C <= 1024 (reference nn.LayerNorm; TensorNet's init_norm /
+ * out_norm, models/tensornet.py:232, 322): y = (x - mean) * rstd * w + b, mean / rstd [rows] saved.
+ * Backward: grad_x = rstd * (g w - mean(g w) - xhat * mean(g w xhat)) (accumulate: +=, grad_x contiguous);
+ * weight / bias gradients as deterministic column sums over the rows (workspace from
+ * tmdnet_layernorm_wgrad_workspace_bytes; grad_w or grad_b may be NULL). */
+int tmdnet_layernorm_fwd_f32(int rows, int C, const void* x, int ldx, const void* w, const void* b, double eps,
+                             void* y, int ldy, void* mean, void* rstd, void* stream);
+int tmdnet_layernorm_bwd_f32(int rows, int C, const void* x, int ldx, const void* w, const void* mean,
+                             const void* rstd, const void* grad_y, int ldg, void* grad_x, int accumulate,
+                             void* stream);
+size_t tmdnet_layernorm_wgrad_workspace_bytes(int rows, int C);
+int tmdnet_layernorm_wgrad_f32(int rows, int C, const void* x, int ldx, const void* mean, const void* rstd,
+                               const void* grad_y, int ldg, void* grad_w, void* grad_b, void* workspace,
+                               size_t workspace_bytes, void* stream);
 
 /* Pair numbering of a symmetric CSR edge list (for pk_rows above).  Canonical edges are those
  * with src >= dst (self loops and one direction of every pair), numbered row by row in CSR order;

@@ -131,10 +131,10 @@ def _fake_msg_fwd(ea, Tc, graph, out):
     out.copy_(kernels.tn_message_composite(ea, Tc, graph))
 
 
-def _fake_msg_bwd(ea, Tc, graph, gmsg, gea, gT):
+def _fake_msg_bwd(ea, Tc, graph, gmsg, gea, gT, gadd=None):
     g = _vjp(lambda e, t: kernels.tn_message_composite(e, t, graph), [ea, Tc], gmsg)
     gea.copy_(g[0])
-    gT.copy_(g[1])
+    gT.copy_(g[1] + (0 if gadd is None else gadd))
 
 
 @pytest.fixture

@@ -1641,6 +1641,11 @@ static int tune_get(int key) {
 template <typename T, int V, int KIND, bool ORD>
 static int et_launch_v(const Args<T>& A, hipStream_t st) {
   int S = et_waves_per_node(A.n, (int)sizeof(T) * V);
+  // the forward keeps 4 waves per node at every size: on the C5 probe (pair rows) 1.158 vs 1.196 ms at 1
+  // wave (r04, tools/pair_probe.py; fewer nodes in flight per XCD, so more of each pair row's second read
+  // hits L2); the backward passes are faster at 1 there (3.25 vs 3.52 ms)
+  static const bool env_s_set = getenv("TMDNET_ET_S") != nullptr;
+  if (KIND == 0 && !env_s_set && (int)sizeof(T) * V <= 32) S = 4;
   static const int bwd_s = getenv("TMDNET_ET_BWD_S") ? atoi(getenv("TMDNET_ET_BWD_S")) : 0;  // tuning
   if (KIND != 0 && bwd_s && (int)sizeof(T) * V <= 32) S = bwd_s >= 4 ? 4 : bwd_s >= 2 ? 2 : 1;
   if (S == 4) return et_launch_vs<T, V, (sizeof(T) * V <= 32 ? 4 : 1), KIND, ORD>(A, st);

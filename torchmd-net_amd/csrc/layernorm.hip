@@ -1,0 +1,182 @@
+// LayerNorm over the last dimension (reference nn.LayerNorm, eps 1e-5): TensorNet's init_norm
+// (models/tensornet.py:322, C = H) and out_norm (:232, C = 3H), the rows being atoms.
+//
+// Forward: one wave per row, the row in registers (CPL = C / 64 values per lane), mean and variance by
+// two wave reductions (the exact two-pass form), y = (x - mean) * rstd * w + b; mean / rstd saved.
+// Backward (input): gx = rstd * (g w - mean(g w) - xhat * mean(g w xhat)), one wave per row.
+// Weight / bias gradients (training only): column sums of g * xhat and g over the rows, in two
+// deterministic passes (row-chunk partials in chunk order, then their sum).
+#include "common.h"
+#include "tmdnet.h"
+
+namespace tmd {
+namespace ln {
+
+template <int CPL>
+__global__ __launch_bounds__(256) void k_fwd(int rows, int C, const float* __restrict__ x, int ldx,
+                                             const float* __restrict__ w, const float* __restrict__ b, float eps,
+                                             float* __restrict__ y, int ldy, float* __restrict__ mean,
+                                             float* __restrict__ rstd) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = lane_id();
+  if (row >= rows) return;
+  const float* xr = x + (size_t)row * ldx;
+  float v[CPL];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) {
+    const int c = lane + 64 * j;
+    v[j] = c < C ? xr[c] : 0.f;
+    s += v[j];
+  }
+  const float mu = wave_sum(s) / (float)C;
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) {
+    const int c = lane + 64 * j;
+    const float d = c < C ? v[j] - mu : 0.f;
+    q += d * d;
+  }
+  const float rs = rsqrtf(wave_sum(q) / (float)C + eps);
+  float* yr = y + (size_t)row * ldy;
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) {
+    const int c = lane + 64 * j;
+    if (c < C) yr[c] = (v[j] - mu) * rs * w[c] + b[c];
+  }
+  if (lane == 0) {
+    mean[row] = mu;
+    rstd[row] = rs;
+  }
+}
+
+template <int CPL>
+__global__ __launch_bounds__(256) void k_bwd(int rows, int C, const float* __restrict__ x, int ldx,
+                                             const float* __restrict__ w, const float* __restrict__ mean,
+                                             const float* __restrict__ rstd, const float* __restrict__ gy,
+                                             int ldg, float* __restrict__ gx, int acc) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = lane_id();
+  if (row >= rows) return;
+  const float mu = mean[row], rs = rstd[row];
+  const float* xr = x + (size_t)row * ldx;
+  const float* gr = gy + (size_t)row * ldg;
+  float h[CPL], gw[CPL];
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) {
+    const int c = lane + 64 * j;
+    h[j] = c < C ? (xr[c] - mu) * rs : 0.f;
+    gw[j] = c < C ? gr[c] * w[c] : 0.f;
+    s1 += gw[j];
+    s2 += gw[j] * h[j];
+  }
+  const float m1 = wave_sum(s1) / (float)C, m2 = wave_sum(s2) / (float)C;
+  float* o = gx + (size_t)row * C;
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) {
+    const int c = lane + 64 * j;
+    if (c < C) {
+      const float v = rs * (gw[j] - m1 - h[j] * m2);
+      o[c] = acc ? o[c] + v : v;
+    }
+  }
+}
+
+// weight / bias gradient partials: block k sums rows [k * kChunk, (k + 1) * kChunk) for every column
+constexpr int kChunk = 128;
+__global__ __launch_bounds__(256) void k_wgrad_part(int rows, int C, const float* __restrict__ x, int ldx,
+                                                    const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                    const float* __restrict__ gy, int ldg, float* __restrict__ part) {
+  const int r0 = blockIdx.y * kChunk, r1 = min(rows, r0 + kChunk);
+  for (int c = blockIdx.x * 256 + threadIdx.x; c < C; c += gridDim.x * 256) {
+    float sw = 0.f, sb = 0.f;
+    for (int r = r0; r < r1; ++r) {
+      const float g = gy[(size_t)r * ldg + c];
+      sw += g * (x[(size_t)r * ldx + c] - mean[r]) * rstd[r];
+      sb += g;
+    }
+    part[((size_t)blockIdx.y * 2) * C + c] = sw;
+    part[((size_t)blockIdx.y * 2 + 1) * C + c] = sb;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_wgrad_sum(int C, int chunks, const float* __restrict__ part,
+                                                   float* __restrict__ gw, float* __restrict__ gb) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  float sw = 0.f, sb = 0.f;
+  for (int k = 0; k < chunks; ++k) {
+    sw += part[((size_t)k * 2) * C + c];
+    sb += part[((size_t)k * 2 + 1) * C + c];
+  }
+  if (gw) gw[c] = sw;
+  if (gb) gb[c] = sb;
+}
+
+}  // namespace ln
+}  // namespace tmd
+
+using namespace tmd;
+
+#define TMD_LN_CPL(C_, F)                                 \
+  do {                                                    \
+    if ((C_) <= 128) F(2);                                \
+    else if ((C_) <= 256) F(4);                           \
+    else if ((C_) <= 384) F(6);                           \
+    else if ((C_) <= 512) F(8);                           \
+    else F(16);                                           \
+  } while (0)
+
+extern "C" int tmdnet_layernorm_fwd_f32(int rows, int C, const void* x, int ldx, const void* w, const void* b,
+                                        double eps, void* y, int ldy, void* mean, void* rstd, void* stream) {
+  if (rows < 0 || C <= 0 || C > 1024 || ldx < C || ldy < C || !x || !w || !b || !y || !mean || !rstd)
+    return kBadArgument;
+  if (rows == 0) return kOk;
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 g((rows + 3) / 4), t(256);
+#define TMD_F(K) hipLaunchKernelGGL(ln::k_fwd<K>, g, t, 0, st, rows, C, (const float*)x, ldx, (const float*)w, \
+                                    (const float*)b, (float)eps, (float*)y, ldy, (float*)mean, (float*)rstd)
+  TMD_LN_CPL(C, TMD_F);
+#undef TMD_F
+  return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
+}
+
+extern "C" int tmdnet_layernorm_bwd_f32(int rows, int C, const void* x, int ldx, const void* w, const void* mean,
+                                        const void* rstd, const void* grad_y, int ldg, void* grad_x, int accumulate,
+                                        void* stream) {
+  if (rows < 0 || C <= 0 || C > 1024 || ldx < C || ldg < C || !x || !w || !mean || !rstd || !grad_y || !grad_x)
+    return kBadArgument;
+  if (rows == 0) return kOk;
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 g((rows + 3) / 4), t(256);
+#define TMD_F(K)                                                                                                \
+  hipLaunchKernelGGL(ln::k_bwd<K>, g, t, 0, st, rows, C, (const float*)x, ldx, (const float*)w, (const float*)mean, \
+                     (const float*)rstd, (const float*)grad_y, ldg, (float*)grad_x, accumulate)
+  TMD_LN_CPL(C, TMD_F);
+#undef TMD_F
+  return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
+}
+
+extern "C" size_t tmdnet_layernorm_wgrad_workspace_bytes(int rows, int C) {
+  if (rows <= 0 || C <= 0) return 0;
+  return (size_t)((rows + ln::kChunk - 1) / ln::kChunk) * 2 * C * sizeof(float);
+}
+
+extern "C" int tmdnet_layernorm_wgrad_f32(int rows, int C, const void* x, int ldx, const void* mean, const void* rstd,
+                                          const void* grad_y, int ldg, void* grad_w, void* grad_b, void* workspace,
+                                          size_t workspace_bytes, void* stream) {
+  if (rows < 0 || C <= 0 || ldx < C || ldg < C || !x || !mean || !rstd || !grad_y || (!grad_w && !grad_b))
+    return kBadArgument;
+  hipStream_t st = (hipStream_t)stream;
+  if (rows == 0) {  // empty sums: zeros
+    hipLaunchKernelGGL(ln::k_wgrad_sum, dim3((C + 255) / 256), dim3(256), 0, st, C, 0, (const float*)nullptr,
+                       (float*)grad_w, (float*)grad_b);
+    return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
+  }
+  if (!workspace || workspace_bytes < tmdnet_layernorm_wgrad_workspace_bytes(rows, C)) return kWorkspaceTooSmall;
+  const int chunks = (rows + ln::kChunk - 1) / ln::kChunk;
+  hipLaunchKernelGGL(ln::k_wgrad_part, dim3((C + 255) / 256, chunks), dim3(256), 0, st, rows, C, (const float*)x, ldx,
+                     (const float*)mean, (const float*)rstd, (const float*)grad_y, ldg, (float*)workspace);
+  hipLaunchKernelGGL(ln::k_wgrad_sum, dim3((C + 255) / 256), dim3(256), 0, st, C, chunks, (const float*)workspace,
+                     (float*)grad_w, (float*)grad_b);
+  return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
+}

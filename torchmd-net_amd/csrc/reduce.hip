@@ -39,6 +39,45 @@ __global__ void k_atom_sum_bwd(int n, int n_mol, const T* __restrict__ gy, const
   gx[i] = (b >= 0 && b < n_mol) ? s * gy[b] : T(0);
 }
 
+// Scalar head tail + reduction (reference output_modules.py:83-105 Scalar: Linear(H/2 -> 1) after the
+// SiLU, then TorchMD_Net's `x * std`, per-molecule sum and `+ mean`): y[b] = mean + std * sum_n (h[n].w + b0).
+// One wave per atom row (K values, lane-strided), the molecule sums in LDS bins.
+template <typename T>
+__global__ __launch_bounds__(1024) void k_dot_sum(int n, int K, const T* __restrict__ h, int ldh,
+                                                  const T* __restrict__ w, const T* __restrict__ b0,
+                                                  int n_mol, const int64_t* __restrict__ batch,
+                                                  const T* __restrict__ std_, const T* __restrict__ mean,
+                                                  T* __restrict__ y) {
+  __shared__ T bins[kMaxBins];
+  for (int b = threadIdx.x; b < n_mol; b += blockDim.x) bins[b] = T(0);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const T bias = b0 ? *b0 : T(0);
+  for (int i = wid; i < n; i += nw) {
+    const T* hr = h + (size_t)i * ldh;
+    T s = T(0);
+    for (int k = lane; k < K; k += 64) s += hr[k] * w[k];
+    s = wave_sum(s);
+    const int64_t b = batch[i];
+    if (lane == 0 && b >= 0 && b < n_mol) atomicAdd(&bins[b], s + bias);
+  }
+  __syncthreads();
+  const T sc = std_ ? *std_ : T(1), m = mean ? *mean : T(0);
+  for (int b = threadIdx.x; b < n_mol; b += blockDim.x) y[b] = m + sc * bins[b];
+}
+
+// its input gradient: gh[n][k] = std * gy[batch[n]] * w[k]
+template <typename T>
+__global__ void k_dot_sum_bwd(int n, int K, const T* __restrict__ gy, const int64_t* __restrict__ batch, int n_mol,
+                              const T* __restrict__ std_, const T* __restrict__ w, T* __restrict__ gh) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)n * K) return;
+  const int a = (int)(i / K), k = (int)(i % K);
+  const int64_t b = batch[a];
+  const T sc = std_ ? *std_ : T(1);
+  gh[i] = (b >= 0 && b < n_mol) ? sc * gy[b] * w[k] : T(0);
+}
+
 }  // namespace red
 }  // namespace tmd
 
@@ -71,6 +110,43 @@ extern "C" int tmdnet_atom_sum_bwd(int dtype, int n_atoms, int n_mol, const void
   else if (dtype == TMDNET_F64)
     hipLaunchKernelGGL(red::k_atom_sum_bwd<double>, g, dim3(256), 0, st, n_atoms, n_mol, (const double*)grad_y,
                        batch, (const double*)std_, (double*)grad_x);
+  else
+    return kUnsupported;
+  return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
+}
+
+extern "C" int tmdnet_dot_sum_fwd(int dtype, int n_atoms, int K, const void* h, int ld_h, const void* w,
+                                  const void* b0, int n_mol, const int64_t* batch, const void* std_,
+                                  const void* mean, void* y, void* stream) {
+  if (n_atoms < 0 || K <= 0 || ld_h < K || n_mol <= 0 || n_mol > red::kMaxBins || !h || !w || !batch || !y)
+    return kBadArgument;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == TMDNET_F32)
+    hipLaunchKernelGGL(red::k_dot_sum<float>, dim3(1), dim3(1024), 0, st, n_atoms, K, (const float*)h, ld_h,
+                       (const float*)w, (const float*)b0, n_mol, batch, (const float*)std_, (const float*)mean,
+                       (float*)y);
+  else if (dtype == TMDNET_F64)
+    hipLaunchKernelGGL(red::k_dot_sum<double>, dim3(1), dim3(1024), 0, st, n_atoms, K, (const double*)h, ld_h,
+                       (const double*)w, (const double*)b0, n_mol, batch, (const double*)std_,
+                       (const double*)mean, (double*)y);
+  else
+    return kUnsupported;
+  return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
+}
+
+extern "C" int tmdnet_dot_sum_bwd(int dtype, int n_atoms, int K, const void* grad_y, const int64_t* batch, int n_mol,
+                                  const void* std_, const void* w, void* grad_h, void* stream) {
+  if (n_atoms < 0 || K <= 0 || n_mol <= 0 || !grad_y || !batch || !w || !grad_h) return kBadArgument;
+  if (n_atoms == 0) return kOk;
+  hipStream_t st = (hipStream_t)stream;
+  const long long tot = (long long)n_atoms * K;
+  const dim3 g((unsigned)((tot + 255) / 256));
+  if (dtype == TMDNET_F32)
+    hipLaunchKernelGGL(red::k_dot_sum_bwd<float>, g, dim3(256), 0, st, n_atoms, K, (const float*)grad_y, batch, n_mol,
+                       (const float*)std_, (const float*)w, (float*)grad_h);
+  else if (dtype == TMDNET_F64)
+    hipLaunchKernelGGL(red::k_dot_sum_bwd<double>, g, dim3(256), 0, st, n_atoms, K, (const double*)grad_y, batch,
+                       n_mol, (const double*)std_, (const double*)w, (double*)grad_h);
   else
     return kUnsupported;
   return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;

@@ -50,6 +50,7 @@ template <typename T> struct Args {
   T* msg;                   // [9][N][H]
   const T* gmsg;
   T* gea; T* gT;
+  const T* gTadd;           // [9][N][H] or NULL: added to gT (the component tensor's other consumer)
 };
 
 // Multiplicity of atom 0's self loop.  With a device pair count (static_shapes under HIP-graph
@@ -332,6 +333,12 @@ __global__ __launch_bounds__(256) void k_msg_bwd_src(Args<T> A) {
 #pragma unroll
     for (int i = 0; i < 9; ++i) acc[i] += node::ctype_scale(i, f0, f1, f2) * g[i];
   }
+  if (A.gTadd && on) {
+    T ad[9];
+    ldc(ad, A.gTadd + (size_t)m * A.H + h, A.nh);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) acc[i] += ad[i];
+  }
   if (on) stc(A.gT + (size_t)m * A.H + h, A.nh, acc);
 }
 
@@ -430,12 +437,12 @@ extern "C" int tmdnet_tn_message_fwd(int dtype, int n_nodes, int hidden, const i
   })
 }
 
-extern "C" int tmdnet_tn_message_bwd(int dtype, int n_nodes, int hidden, const int32_t* row_ptr,
-                                     const int32_t* src, int max_pairs, double self0_mult,
-                                     const int32_t* pad_pairs, int pad_capacity,
-                                     const void* edge_attr, int ld_ea, const void* comp,
-                                     const void* grad_msg, void* g_edge_attr, void* g_comp,
-                                     void* stream) {
+extern "C" int tmdnet_tn_message_bwd_add(int dtype, int n_nodes, int hidden, const int32_t* row_ptr,
+                                         const int32_t* src, int max_pairs, double self0_mult,
+                                         const int32_t* pad_pairs, int pad_capacity,
+                                         const void* edge_attr, int ld_ea, const void* comp,
+                                         const void* grad_msg, const void* g_comp_add, void* g_edge_attr,
+                                         void* g_comp, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   TN_DISPATCH(dtype, {
     auto a = tn::base<T>(n_nodes, hidden, row_ptr, src, max_pairs, self0_mult, pad_pairs,
@@ -443,8 +450,20 @@ extern "C" int tmdnet_tn_message_bwd(int dtype, int n_nodes, int hidden, const i
     a.ea = (const T*)edge_attr; a.ldea = ld_ea;
     a.Tc = (const T*)comp;
     a.gmsg = (const T*)grad_msg; a.gea = (T*)g_edge_attr; a.gT = (T*)g_comp;
+    a.gTadd = (const T*)g_comp_add;
     int rc = tn::launch<T>(tn::k_msg_bwd_dst<T>, a, st);
     if (rc) return rc;
     return tn::launch<T>(tn::k_msg_bwd_src<T>, a, st);
   })
+}
+
+extern "C" int tmdnet_tn_message_bwd(int dtype, int n_nodes, int hidden, const int32_t* row_ptr,
+                                     const int32_t* src, int max_pairs, double self0_mult,
+                                     const int32_t* pad_pairs, int pad_capacity,
+                                     const void* edge_attr, int ld_ea, const void* comp,
+                                     const void* grad_msg, void* g_edge_attr, void* g_comp,
+                                     void* stream) {
+  return tmdnet_tn_message_bwd_add(dtype, n_nodes, hidden, row_ptr, src, max_pairs, self0_mult, pad_pairs,
+                                   pad_capacity, edge_attr, ld_ea, comp, grad_msg, nullptr, g_edge_attr, g_comp,
+                                   stream);
 }

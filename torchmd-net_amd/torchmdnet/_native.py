@@ -73,12 +73,19 @@ SIGNATURES = {
     "tmdnet_tn_embed_bwd": (I, [I, I, I, P, P, I, D, P, I, P, P, P, I, P, P, P, P, P, P, P, P, P]),
     "tmdnet_tn_message_fwd": (I, [I, I, I, P, P, I, D, P, I, P, I, P, P, P]),
     "tmdnet_tn_message_bwd": (I, [I, I, I, P, P, I, D, P, I, P, I, P, P, P, P, P]),
+    "tmdnet_tn_message_bwd_add": (I, [I, I, I, P, P, I, D, P, I, P, I, P, P, P, P, P, P]),
     "tmdnet_tn_node_fwd": (I, [I, I, I, I, P, P, P, P]),
     "tmdnet_tn_node_bwd": (I, [I, I, I, I, P, P, P, P, P, P, P]),
     "tmdnet_silu_fwd": (I, [I, I, I, P, I, P, P, P]),
     "tmdnet_silu_bwd": (I, [I, I, I, P, I, P, P, I, P, P, P]),
     "tmdnet_atom_sum_fwd": (I, [I, I, I, P, P, P, P, P, P]),
     "tmdnet_atom_sum_bwd": (I, [I, I, I, P, P, P, P, P]),
+    "tmdnet_dot_sum_fwd": (I, [I, I, I, P, I, P, P, I, P, P, P, P, P]),
+    "tmdnet_dot_sum_bwd": (I, [I, I, I, P, P, I, P, P, P, P]),
+    "tmdnet_layernorm_fwd_f32": (I, [I, I, P, I, P, P, D, P, I, P, P, P]),
+    "tmdnet_layernorm_bwd_f32": (I, [I, I, P, I, P, P, P, P, I, P, I, P]),
+    "tmdnet_layernorm_wgrad_workspace_bytes": (SZ, [I, I]),
+    "tmdnet_layernorm_wgrad_f32": (I, [I, I, P, I, P, P, P, I, P, P, P, SZ, P]),
     "tmdnet_gemm_f32": (I, [I, P, P, P]),
     "tmdnet_gemm_ex_f32": (I, [I, P, P, P]),
     "tmdnet_gemm_tn_f32": (I, [I, P, P, P]),

@@ -1389,6 +1389,73 @@ def atom_sum(x, batch, n_mol, std, mean):
     return _AtomSum.apply(x.contiguous(), batch, int(n_mol), std, mean)
 
 
+def _dot_sum_composite(h, w, b0, batch, n_mol, std, mean):
+    x = h @ w.view(-1, 1) + b0.view(1, 1)
+    return _atom_sum_composite(x, batch, n_mol, std, mean)
+
+
+class _DotSum(Function):
+    """y[b] = mean + std * sum_{batch[n] = b} (h[n] . w + b0): the Scalar head's last Linear (H/2 -> 1)
+    fused with TorchMD_Net's `x * std`, per-molecule sum and `+ mean` (tmdnet_dot_sum_fwd)."""
+
+    @staticmethod
+    def forward(ctx, h, w, b0, batch, n_mol, std, mean):
+        lib = nat.load()
+        y = torch.empty((n_mol, 1), dtype=h.dtype, device=h.device)
+        rc = lib.tmdnet_dot_sum_fwd(nat.dtype_code(h.dtype), h.shape[0], h.shape[1], nat.ptr(h), h.stride(0),
+                                    nat.ptr(w), nat.ptr(b0), n_mol, nat.ptr(batch), nat.ptr(std), nat.ptr(mean),
+                                    nat.ptr(y), nat.stream(h.device))
+        nat.check(rc, "tmdnet_dot_sum_fwd")
+        ctx.n_mol = n_mol
+        ctx.save_for_backward(h, w, b0, batch, std)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        h, w, b0, batch, std = ctx.saved_tensors
+        nf = ctx.next_functions
+        need = (ctx.needs_input_grad[0] and _will_run(nf[0][0]), ctx.needs_input_grad[1] and _will_run(nf[1][0]),
+                ctx.needs_input_grad[2] and _will_run(nf[2][0]))
+        if not any(need):
+            return None, None, None, None, None, None, None
+        gh, gw, gb = _DotSumBwd.apply(gy.contiguous(), h, w, b0, batch, std, ctx.n_mol, need)
+        return gh, gw, gb, None, None, None, None
+
+
+class _DotSumBwd(Function):
+    @staticmethod
+    def forward(ctx, gy, h, w, b0, batch, std, n_mol, need):
+        gh = gw = gb = None
+        if need[0]:
+            gh = torch.empty_like(h)
+            rc = nat.load().tmdnet_dot_sum_bwd(nat.dtype_code(h.dtype), h.shape[0], h.shape[1], nat.ptr(gy),
+                                               nat.ptr(batch), n_mol, nat.ptr(std), nat.ptr(w), nat.ptr(gh),
+                                               nat.stream(h.device))
+            nat.check(rc, "tmdnet_dot_sum_bwd")
+        if need[1] or need[2]:  # training: the per-atom seed std * gy[batch], then its sums
+            ga = std * gy.index_select(0, batch).view(-1)
+            gw = (ga.view(1, -1) @ h).view(-1) if need[1] else None
+            gb = ga.sum().view(1) if need[2] else None
+        ctx.n_mol = n_mol
+        ctx.save_for_backward(gy, h, w, b0, batch, std)
+        return gh, gw, gb
+
+    @staticmethod
+    def backward(ctx, ggh, ggw, ggb):  # second order: the composite differentiated twice
+        gy, h, w, b0, batch, std = ctx.saved_tensors
+        n_mol = ctx.n_mol
+        zero = torch.zeros_like(std)
+        d = _tn_double_backward(lambda h_, w_, b_: _dot_sum_composite(h_, w_, b_, batch, n_mol, std, zero),
+                                [h, w, b0], [gy], [ggh, ggw, ggb])
+        return d[0], d[1], d[2], d[3], None, None, None, None
+
+
+def dot_sum(h, w, b0, batch, n_mol, std, mean):
+    """Fused ``reduce((h w + b0) * std) + mean`` (Scalar head's last Linear + TorchMD_Net's reduction)."""
+    nat.require_gpu(h, "dot_sum")
+    return _DotSum.apply(h.contiguous(), w.reshape(-1), b0.reshape(-1), batch, int(n_mol), std, mean)
+
+
 # ----------------------------------------------------------------------------- TensorNet
 def _self0_args(graph):
     """(host multiplicity, device pair count, padding capacity) for the TN kernels' atom-0 self loop
@@ -1490,13 +1557,13 @@ def tn_message_fwd_launch(ea, Tc, graph, out):
     nat.check(rc, "tmdnet_tn_message_fwd")
 
 
-def tn_message_bwd_launch(ea, Tc, graph, gmsg, gea, gT):
+def tn_message_bwd_launch(ea, Tc, graph, gmsg, gea, gT, gadd=None):
     lib = nat.load()
     N, H = Tc.shape[1], Tc.shape[2]
-    rc = lib.tmdnet_tn_message_bwd(nat.dtype_code(Tc.dtype), N, H, nat.ptr(graph.row_ptr), nat.ptr(graph.src),
-                                   graph.n_edges, *_self0_args(graph), nat.ptr(ea), _ld(ea), nat.ptr(Tc),
-                                   nat.ptr(gmsg), nat.ptr(gea), nat.ptr(gT), nat.stream(Tc.device))
-    nat.check(rc, "tmdnet_tn_message_bwd")
+    rc = lib.tmdnet_tn_message_bwd_add(nat.dtype_code(Tc.dtype), N, H, nat.ptr(graph.row_ptr), nat.ptr(graph.src),
+                                       graph.n_edges, *_self0_args(graph), nat.ptr(ea), _ld(ea), nat.ptr(Tc),
+                                       nat.ptr(gmsg), nat.ptr(gadd), nat.ptr(gea), nat.ptr(gT), nat.stream(Tc.device))
+    nat.check(rc, "tmdnet_tn_message_bwd_add")
 
 
 class _TNEmbed(Function):
@@ -1550,32 +1617,41 @@ class _TNEmbedBwd(Function):
 
 
 class _TNMessage(Function):
+    """The message.  ``fanout``: also returns an alias of Tc for its second consumer (the POST pass); that
+    consumer's gradient is added by the message backward kernel (no separate add launch)."""
+
     @staticmethod
-    def forward(ctx, ea, Tc, graph):
+    def forward(ctx, ea, Tc, graph, fanout):
         msg = torch.empty_like(Tc)
         tn_message_fwd_launch(ea, Tc, graph, msg)
         ctx.graph = graph
         ctx.save_for_backward(ea, Tc)
+        if fanout:
+            return msg, Tc.view_as(Tc)
         return msg
 
     @staticmethod
-    def backward(ctx, gmsg):
+    def backward(ctx, gmsg, galias=None):
         ea, Tc = ctx.saved_tensors
-        outs = _TNMessageBwd.apply(gmsg.contiguous(), ea, Tc, ctx.graph)
-        return tuple(outs) + (None,)
+        if gmsg is None:
+            gmsg = torch.zeros_like(Tc)
+        gadd = None if galias is None else galias.contiguous()
+        outs = _TNMessageBwd.apply(gmsg.contiguous(), ea, Tc, ctx.graph, gadd)
+        return tuple(outs) + (None, None)
 
 
 class _TNMessageBwd(Function):
     @staticmethod
-    def forward(ctx, gmsg, ea, Tc, graph):
+    def forward(ctx, gmsg, ea, Tc, graph, gadd):
         if not graph.symmetric:
             raise RuntimeError("torchmd-net_amd: TensorNet backward needs a symmetric edge list")
         E = graph.n_edges
         H = Tc.shape[2]
         gea = torch.empty((E, 3 * H), dtype=Tc.dtype, device=Tc.device)
         gT = torch.empty_like(Tc)
-        tn_message_bwd_launch(ea, Tc, graph, gmsg, gea, gT)
+        tn_message_bwd_launch(ea, Tc, graph, gmsg, gea, gT, gadd)
         ctx.graph = graph
+        ctx.has_add = gadd is not None
         ctx.save_for_backward(gmsg, ea, Tc)
         return gea, gT
 
@@ -1583,6 +1659,7 @@ class _TNMessageBwd(Function):
     def backward(ctx, *ggs):
         saved = ctx.saved_tensors
         _create = torch.is_grad_enabled()  # third order only if the caller builds a graph
+        g_add = ggs[1] if ctx.has_add else None  # gT = VJP(gmsg) + gadd: identity in gadd
         with torch.enable_grad():
             leaves = [t.detach().requires_grad_(True) for t in saved]
             gmsg, ea, Tc = leaves
@@ -1590,10 +1667,10 @@ class _TNMessageBwd(Function):
             first = torch.autograd.grad(msg, (ea, Tc), gmsg, create_graph=True)
             sel = [(f, g) for f, g in zip(first, ggs) if g is not None]
             if not sel:
-                return (None,) * 4
+                return (None,) * 4 + (g_add,)
             second = torch.autograd.grad([f for f, _ in sel], leaves, [g for _, g in sel],
                                          create_graph=_create, allow_unused=True)
-        return tuple(second) + (None,)
+        return tuple(second) + (None, g_add)
 
 
 def tn_embed(P, Q, W, C, u, graph):
@@ -1602,10 +1679,11 @@ def tn_embed(P, Q, W, C, u, graph):
     return _TNEmbed.apply(P.contiguous(), Q.contiguous(), _rowmajor(W), C.contiguous(), u.contiguous(), graph)
 
 
-def tn_message(ea, Tc, graph):
-    """Tensor message passing on a compact [9, N, H] tensor -> compact message."""
+def tn_message(ea, Tc, graph, fanout=False):
+    """Tensor message passing on a compact [9, N, H] tensor -> compact message (``fanout``: and an alias
+    of Tc for its second consumer, whose gradient the message backward adds)."""
     nat.require_gpu(Tc, "tn_message")
-    return _TNMessage.apply(_rowmajor(ea), Tc.contiguous(), graph)
+    return _TNMessage.apply(_rowmajor(ea), Tc.contiguous(), graph, fanout)
 
 
 # ----------------------------------------------------------------------------- spatial order
@@ -2197,6 +2275,112 @@ def mlp_act(x, weights, biases, act, scale=None):
             x = fused_act(act, linear(x, weights[i], biases[i]), scale if i == L - 1 else None)
         return x
     return _MLPAct.apply(x, None if scale is None else scale.contiguous(), *weights, *biases)
+
+
+# ----------------------------------------------------------------------------- LayerNorm
+def _ln_composite(x, w, b, eps):
+    return F.layer_norm(x, (x.shape[-1],), w, b, eps)
+
+
+class _LayerNorm(Function):
+    """nn.LayerNorm over the last dimension (TensorNet init_norm / out_norm, reference tensornet.py:232,
+    322) on tmdnet_layernorm_fwd_f32; its backward is _LayerNormBwd (HIP first order)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, eps):
+        rows, C = x.shape
+        y = torch.empty_like(x)
+        mean = torch.empty(rows, dtype=x.dtype, device=x.device)
+        rstd = torch.empty(rows, dtype=x.dtype, device=x.device)
+        rc = nat.load().tmdnet_layernorm_fwd_f32(rows, C, nat.ptr(x), x.stride(0), nat.ptr(w), nat.ptr(b), float(eps),
+                                                 nat.ptr(y), C, nat.ptr(mean), nat.ptr(rstd), nat.stream(x.device))
+        nat.check(rc, "tmdnet_layernorm_fwd_f32")
+        ctx.save_for_backward(x, w, b, mean, rstd)
+        ctx.eps = eps
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w, b, mean, rstd = ctx.saved_tensors
+        nf = ctx.next_functions
+        need = (ctx.needs_input_grad[0] and _will_run(nf[0][0]), ctx.needs_input_grad[1] and _will_run(nf[1][0]),
+                ctx.needs_input_grad[2] and _will_run(nf[2][0]))
+        if not any(need):
+            return None, None, None, None
+        gx, gw, gb = _LayerNormBwd.apply(gy.contiguous(), x, w, b, mean, rstd, ctx.eps, need)
+        return gx, gw, gb, None
+
+
+class _LayerNormBwd(Function):
+    @staticmethod
+    def forward(ctx, gy, x, w, b, mean, rstd, eps, need):
+        lib = nat.load()
+        rows, C = x.shape
+        st = nat.stream(x.device)
+        gx = gw = gb = None
+        if need[0]:
+            gx = torch.empty_like(x)
+            rc = lib.tmdnet_layernorm_bwd_f32(rows, C, nat.ptr(x), x.stride(0), nat.ptr(w), nat.ptr(mean),
+                                              nat.ptr(rstd), nat.ptr(gy), gy.stride(0), nat.ptr(gx), 0, st)
+            nat.check(rc, "tmdnet_layernorm_bwd_f32")
+        if need[1] or need[2]:
+            gw = torch.empty_like(w) if need[1] else None
+            gb = torch.empty_like(w) if need[2] else None
+            wsb = int(lib.tmdnet_layernorm_wgrad_workspace_bytes(rows, C))
+            ws = torch.empty(max(1, wsb // 4), dtype=torch.float32, device=x.device)
+            rc = lib.tmdnet_layernorm_wgrad_f32(rows, C, nat.ptr(x), x.stride(0), nat.ptr(mean), nat.ptr(rstd),
+                                                nat.ptr(gy), gy.stride(0), nat.ptr(gw), nat.ptr(gb), nat.ptr(ws), wsb, st)
+            nat.check(rc, "tmdnet_layernorm_wgrad_f32")
+        ctx.save_for_backward(gy, x, w, b)
+        ctx.eps = eps
+        return gx, gw, gb
+
+    @staticmethod
+    def backward(ctx, ggx, ggw, ggb):
+        # second order (force-matching training): differentiate the composite LayerNorm twice
+        gy, x, w, b = ctx.saved_tensors
+        eps = ctx.eps
+        d = _tn_double_backward(lambda x_, w_, b_: _ln_composite(x_, w_, b_, eps), [x, w, b], [gy], [ggx, ggw, ggb])
+        return d[0], d[1], d[2], d[3], None, None, None, None
+
+
+def _tn_double_backward(fwd, primals, gouts, ggs):
+    from .tn_node import _double_backward
+    return _double_backward(fwd, primals, gouts, ggs)
+
+
+def layer_norm(x, weight, bias, eps=1e-5):
+    """nn.LayerNorm(C) over [rows, C]: the HIP kernels for fp32 CUDA rows of C <= 1024, else ATen."""
+    if (x.is_cuda and x.dtype == torch.float32 and x.dim() == 2 and x.shape[1] <= 1024 and x.stride(1) == 1
+            and weight is not None and bias is not None and weight.dtype == torch.float32):
+        return _LayerNorm.apply(x, weight, bias, float(eps))
+    return _ln_composite(x, weight, bias, eps)
+
+
+class _StackedRows(Function):
+    """torch.cat(params, 0) when the parameters already are consecutive row blocks of ``buf``
+    (et_stack._stack_views): the buffer itself, no copy kernel; the gradient splits into views."""
+
+    @staticmethod
+    def forward(ctx, buf, *params):
+        ctx.rows = [p.shape[0] for p in params]
+        return buf.view_as(buf)
+
+    @staticmethod
+    def backward(ctx, g):
+        return (None, *torch.split(g, ctx.rows, 0))
+
+
+def stacked_rows(holder, name, params):
+    """cat(params, 0) without a copy: the parameters are made row blocks of one buffer once (their
+    ``.data`` re-pointed, as the ET stack does) and re-stacked only if that aliasing was broken
+    (``.to()``, a replaced tensor).  ``holder`` keeps the buffers (a dict)."""
+    from .et_stack import _is_stacked, _stack_views
+    buf = holder.get(name)
+    if not _is_stacked(buf, params):
+        buf = _stack_views(params)
+        holder[name] = buf
+    return _StackedRows.apply(buf, *params)
 
 
 # ----------------------------------------------------------------------------- training loss

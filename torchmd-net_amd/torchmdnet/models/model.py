@@ -184,9 +184,12 @@ class TorchMD_Net(nn.Module):
         if torch.jit.is_scripting():
             return self._forward_script(z, pos, batch, q, s, extra_args)
         x, v, z, pos, batch = self.representation_model(z, pos, batch, q=q, s=s)
-        x = self.output_model.pre_reduce(x, v, z, pos, batch)
         fused = None
-        if self.prior_model is None:  # x * std, reduce and + mean in one pass (one more for the backward)
+        if self.prior_model is None:  # the head's tail, x * std, reduce and + mean fused (Scalar)
+            fused = self.output_model.fused_head_reduce(x, v, z, pos, batch, self.std, self.mean)
+        if fused is None:
+            x = self.output_model.pre_reduce(x, v, z, pos, batch)
+        if fused is None and self.prior_model is None:  # x * std, reduce and + mean in one pass
             fused = self.output_model.fused_reduce(x, batch, self.std, self.mean)
         if fused is not None:
             x = fused

@@ -79,6 +79,11 @@ class OutputModel(nn.Module, metaclass=ABCMeta):
     def post_reduce(self, x):
         return x
 
+    def fused_head_reduce(self, x, v, z, pos, batch, std, mean):
+        """``reduce(pre_reduce(x, ...) * std) + mean`` with the head's tail fused into the reduction, or
+        None when this head has no such form (TorchMD_Net.forward then runs pre_reduce + fused_reduce)."""
+        return None
+
 
 class Scalar(OutputModel):
     def __init__(self, hidden_channels, activation="silu", allow_prior_model=True, reduce_op="sum",
@@ -103,6 +108,23 @@ class Scalar(OutputModel):
             return self.output_network(x)
         net = self.output_network
         return net[2](kernels.fused_act(net[1], net[0](x)))
+
+    @torch.jit.unused
+    def fused_head_reduce(self, x, v, z, pos, batch, std, mean):
+        """Linear + SiLU as one hand GEMM launch (kernels.mlp_act), then the last Linear (H/2 -> 1) fused
+        with `x * std`, the per-molecule sum and `+ mean` (kernels.dot_sum): 2 launches (their backward 2)
+        instead of two library GEMMs, the activation, the reduction and their backward passes."""
+        net = self.output_network
+        if not (x.is_cuda and x.dtype == torch.float32 and x.dim() == 2 and isinstance(net[1], nn.SiLU)
+                and self.reduce_op in ("sum", "add") and batch.dtype == torch.int64 and std is not None
+                and mean is not None and std.numel() == 1 and mean.numel() == 1
+                and net[0].out_features % 16 == 0 and net[0].in_features % 16 == 0):
+            return None
+        n_mol = self._dim_size(x, batch)
+        if n_mol > kernels.ATOM_SUM_MAX_MOLECULES:
+            return None
+        h = kernels.mlp_act(x, [net[0].weight], [net[0].bias], net[1])
+        return kernels.dot_sum(h, net[2].weight, net[2].bias, batch, n_mol, std.to(x.dtype), mean.to(x.dtype))
 
 
 class EquivariantScalar(OutputModel):

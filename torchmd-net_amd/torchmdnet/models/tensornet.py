@@ -186,7 +186,7 @@ class TensorNet(nn.Module):
         for layer in self.layers:
             X = layer(X, graph, graph.distances, edge_attr)
         x = tn_node.norms(X)  # cat(|I|^2, |A|^2, |S|^2) of decompose_tensor(X), one fused pass
-        x = self.out_norm(x)
+        x = kernels.layer_norm(x, self.out_norm.weight, self.out_norm.bias, self.out_norm.eps)
         return kernels.mlp_act(x, [self.linear.weight], [self.linear.bias], self.act)
 
 
@@ -260,14 +260,18 @@ class TensorEmbedding(nn.Module):
         H = self.hidden_channels
         # the Linears as kernels.linear: the hand-written MFMA GEMMs (tmdnet_gemm_f32 forward and input
         # gradient, the grouped TN kernel for weight gradients) instead of the library's small-GEMM tiles
-        W = kernels.linear(
-            edge_attr, torch.cat([self.distance_proj1.weight, self.distance_proj2.weight, self.distance_proj3.weight]),
-            torch.cat([self.distance_proj1.bias, self.distance_proj2.bias, self.distance_proj3.bias]))
-        Z = self.emb(z)
+        # the three distance projections as row blocks of one weight / bias (no per-step concatenation)
+        stacks = self.__dict__.setdefault("_stacks", {})
+        dp = (self.distance_proj1, self.distance_proj2, self.distance_proj3)
+        W = kernels.linear(edge_attr, kernels.stacked_rows(stacks, "w", [m.weight for m in dp]),
+                           kernels.stacked_rows(stacks, "b", [m.bias for m in dp]))
+        Z, = kernels.embedding(z, self.emb.weight)
         P = kernels.linear(Z, self.emb2.weight[:, :H], self.emb2.bias)
         Q = kernels.linear(Z, self.emb2.weight[:, H:])
         Ec = kernels.tn_embed(P, Q, W, C, edge_vec_norm, graph)  # compact [9, N, H]: I | A | S rows
-        norm = self.init_norm(tn_node.enorm(Ec))
+        ln = self.init_norm
+        en, Ec = tn_node.enorm(Ec, fanout=True)  # (Ec's second consumer's gradient joins in the ENORM bwd)
+        norm = kernels.layer_norm(en, ln.weight, ln.bias, ln.eps)
         lt = self.linears_tensor
         Ec = tn_node.mix3(Ec, lt[0].weight, lt[1].weight, lt[2].weight)
         ls = self.linears_scalar  # Linear + act stack, the activations in the GEMM epilogues
@@ -330,8 +334,11 @@ class Interaction(nn.Module):
         edge_attr = kernels.mlp_act(edge_attr, [m.weight for m in ls], [m.bias for m in ls], self.act, C)
         lt = self.linears_tensor
         # X / (|X|^2 + 1), decompose, three channel mixes -> Y as compact [9, N, H] (I | A | S rows)
-        Yc = tn_node.mix3(tn_node.pre(X), lt[0].weight, lt[1].weight, lt[2].weight)
-        msg = kernels.tn_message(edge_attr, Yc, graph)
+        # (the fan-out aliases let X's and Y's second consumers' gradients join inside the PRE / message
+        # backward kernels instead of separate autograd add launches)
+        Xp, X = tn_node.pre(X, fanout=True)
+        Yc = tn_node.mix3(Xp, lt[0].weight, lt[1].weight, lt[2].weight)
+        msg, Yc = kernels.tn_message(edge_attr, Yc, graph, fanout=True)
         # decompose(msg Y + Y msg) (O(3)) or decompose(2 Y msg) (SO(3)), / (|.|^2 + 1), three mixes
         Dc = tn_node.mix3(tn_node.post(Yc, msg, self.equivariance_invariance_group),
                           lt[3].weight, lt[4].weight, lt[5].weight)

@@ -143,30 +143,40 @@ def _double_backward(fwd, primals, gouts, ggs):
 
 # ----------------------------------------------------------------------------- Functions
 class _NodeOp(Function):
+    """One node pass.  ``fanout``: also returns an alias of the input ``a`` for a second consumer; that
+    consumer's gradient arrives here and the backward kernel adds it (``gadd``), instead of the
+    autograd engine summing the two gradients of ``a`` in a separate launch."""
+
     @staticmethod
-    def forward(ctx, op, a, b):
+    def forward(ctx, op, a, b, fanout):
         a = a.contiguous()
         b = None if b is None else b.contiguous()
         out = torch.empty(_out_shape(op, a), dtype=a.dtype, device=a.device)
         node_fwd_launch(op, a, b, out)
         ctx.op = op
         ctx.save_for_backward(a, b)
+        if fanout:
+            return out, a.view_as(a)
         return out
 
     @staticmethod
-    def backward(ctx, gout):
+    def backward(ctx, gout, galias=None):
         a, b = ctx.saved_tensors
-        ga, gb = _NodeOpBwd.apply(ctx.op, gout.contiguous(), a, b)
-        return None, ga, gb
+        if gout is None:
+            gout = torch.zeros(_out_shape(ctx.op, a), dtype=a.dtype, device=a.device)
+        gadd = None if galias is None else galias.contiguous()
+        ga, gb = _NodeOpBwd.apply(ctx.op, gout.contiguous(), a, b, gadd)
+        return None, ga, gb, None
 
 
 class _NodeOpBwd(Function):
     @staticmethod
-    def forward(ctx, op, gout, a, b):
+    def forward(ctx, op, gout, a, b, gadd):
         ga = torch.empty_like(a)
         gb = None if b is None else torch.empty_like(b)
-        node_bwd_launch(op, a, b, gout, None, ga, gb)
+        node_bwd_launch(op, a, b, gout, gadd, ga, gb)
         ctx.op = op
+        ctx.has_add = gadd is not None
         ctx.save_for_backward(gout, a, b)
         return ga, gb
 
@@ -174,21 +184,23 @@ class _NodeOpBwd(Function):
     def backward(ctx, gga, ggb):
         gout, a, b = ctx.saved_tensors
         op = ctx.op
+        g_add = gga if ctx.has_add else None  # ga = VJP(gout) + gadd: identity in gadd
         if b is None:
             d = _double_backward(lambda x: op_composite(op, x), [a], [gout], [gga])
-            return None, d[0], d[1], None
+            return None, d[0], d[1], None, g_add
         d = _double_backward(lambda x, y: op_composite(op, x, y), [a, b], [gout], [gga, ggb])
-        return None, d[0], d[1], d[2]
+        return None, d[0], d[1], d[2], g_add
 
 
-def _apply(op, a, b=None):
+def _apply(op, a, b=None, fanout=False):
     nat.require_gpu(a, "TensorNet node op")
-    return _NodeOp.apply(op, a, b)
+    return _NodeOp.apply(op, a, b, fanout)
 
 
-def pre(X):
-    """Interaction input: X / (|X|^2 + 1), decomposed -> compact (tensornet.py:391-392)."""
-    return _apply(PRE, X)
+def pre(X, fanout=False):
+    """Interaction input: X / (|X|^2 + 1), decomposed -> compact (tensornet.py:391-392).  ``fanout``:
+    returns (compact, X alias) -- the alias for the residual, whose X-gradient the PRE backward adds."""
+    return _apply(PRE, X, fanout=fanout)
 
 
 def post(Yc, Mc, group):
@@ -207,9 +219,10 @@ def norms(X):
     return _apply(NORMS, X)
 
 
-def enorm(c):
-    """tensor_norm(I + A + S) of a compact tensor (tensornet.py:317) -> [N, H]."""
-    return _apply(ENORM, c)
+def enorm(c, fanout=False):
+    """tensor_norm(I + A + S) of a compact tensor (tensornet.py:317) -> [N, H] (``fanout``: and an alias
+    of c for its second consumer, see pre)."""
+    return _apply(ENORM, c, fanout=fanout)
 
 
 def eout(c, f):
