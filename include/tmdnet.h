@@ -93,6 +93,12 @@ int tmdnet_nl_build_paired(int dtype, int strategy, const void* pos, const int64
 int tmdnet_nl_backward(int dtype, int n_atoms, const int32_t* row_ptr, const int32_t* transpose_map,
                        int max_pairs, const void* grad_deltas, const void* grad_distances,
                        const void* deltas, const void* distances, void* grad_pos, void* stream);
+/* The same with a second distance gradient (NULL allowed) summed in: the distances' second consumer
+ * (the ET layer stack's force-pass g_r beside the edge geometry's), no separate add launch. */
+int tmdnet_nl_backward_multi(int dtype, int n_atoms, const int32_t* row_ptr, const int32_t* transpose_map,
+                             int max_pairs, const void* grad_deltas, const void* grad_distances,
+                             const void* grad_distances2, const void* deltas, const void* distances,
+                             void* grad_pos, void* stream);
 
 /* The same backward for ANY list the op returns (half lists with include_transpose=0, capacity-
  * truncated lists, padding slots -1): one lane per slot of neighbors [2][max_pairs], g scattered to
@@ -162,6 +168,15 @@ int tmdnet_edge_geom_bwd(int dtype, int n_edges, int num_rbf, int rbf_type, cons
                          const void* beta, double cutoff_lower, double cutoff_upper,
                          const void* grad_rbf, const void* grad_cutoff, const void* grad_unit,
                          void* grad_dist, void* grad_deltas, void* stream);
+/* The same with up to three incoming gradients per rbf / cutoff output (one per consumer of that output,
+ * summed in slot order in the kernel; NULL slots skipped) -- replaces the autograd engine's add launches
+ * for outputs read by several modules (TensorNet's embedding and interaction layers, tensornet.py:222-230). */
+int tmdnet_edge_geom_bwd_multi(int dtype, int n_edges, int num_rbf, int rbf_type, const int32_t* src,
+                               const int32_t* dst, const void* deltas, const void* dist, const void* mu,
+                               const void* beta, double cutoff_lower, double cutoff_upper, const void* grad_rbf,
+                               const void* grad_rbf2, const void* grad_rbf3, const void* grad_cutoff,
+                               const void* grad_cutoff2, const void* grad_cutoff3, const void* grad_unit,
+                               void* grad_dist, void* grad_deltas, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Equivariant-Transformer edge message + aggregation (reference

@@ -332,9 +332,13 @@ def _cpu_graph(self, pos, batch=None):
     return graph
 
 
-def _cpu_edge_geometry(graph, mu, beta, cutoff_lower, cutoff_upper, rbf_type, want=(True, True, True)):
-    return kernels._edge_geom_composite(graph.deltas, graph.distances, graph.src == graph.dst, mu, beta,
-                                        float(cutoff_lower), float(cutoff_upper), rbf_type, want)
+def _cpu_edge_geometry(graph, mu, beta, cutoff_lower, cutoff_upper, rbf_type, want=(True, True, True), rows=None,
+                       fan=(1, 1)):
+    f, C, u = kernels._edge_geom_composite(graph.deltas, graph.distances, graph.src == graph.dst, mu, beta,
+                                           float(cutoff_lower), float(cutoff_upper), rbf_type, want)
+    if tuple(fan) != (1, 1):  # one alias per consumer, as the HIP path returns them
+        return [f] * fan[0], [C] * fan[1], u
+    return f, C, u
 
 
 @pytest.mark.parametrize("name", ["tn_tiny_o3_static_f64", "tn_tiny_so3_dyn_f64"])

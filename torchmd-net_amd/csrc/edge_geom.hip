@@ -134,29 +134,43 @@ __global__ void k_fwd(Cfg<T> P, T* __restrict__ f, T* __restrict__ C, T* __restr
   }
 }
 
+// The incoming gradients of the rbf and cutoff outputs: up to 3 each (one per consumer of the output;
+// summed here in slot order instead of by separate autograd add launches), NULL slots skipped.
+template <typename T> struct GIn {
+  const T* f[3];
+  const T* c[3];
+};
+
 // One wave per edge (grid-stride); lanes over the basis index.
 template <typename T>
-__global__ __launch_bounds__(256) void k_bwd(Cfg<T> P, const T* __restrict__ gf, const T* __restrict__ gC,
-                                             const T* __restrict__ gu, T* __restrict__ gr,
+__global__ __launch_bounds__(256) void k_bwd(Cfg<T> P, GIn<T> G, const T* __restrict__ gu, T* __restrict__ gr,
                                              T* __restrict__ gdl) {
   const int lane = lane_id();
   const int nw = gridDim.x * (blockDim.x / TMD_WAVE);
+  const bool anyf = G.f[0] || G.f[1] || G.f[2], anyc = G.c[0] || G.c[1] || G.c[2];
   for (int e = blockIdx.x * (blockDim.x / TMD_WAVE) + threadIdx.x / TMD_WAVE; e < P.E; e += nw) {
     const T r = P.r[e];
     T acc = T(0);
-    if (gf) {
+    if (anyf) {
       for (int k = lane; k < P.R; k += TMD_WAVE) {
         T v, dv;
         basis(P, r, k, v, dv);
-        acc += gf[(long long)e * P.R + k] * dv;
+        const long long o = (long long)e * P.R + k;
+        T g = G.f[0] ? G.f[0][o] : T(0);
+        if (G.f[1]) g += G.f[1][o];
+        if (G.f[2]) g += G.f[2][o];
+        acc += g * dv;
       }
       acc = wave_sum(acc);
     }
     if (lane == 0) {
-      if (gC) {
+      if (anyc) {
         T c, dc;
         cosine_cutoff<T>(r, P.cl, P.cu, c, dc);
-        acc += gC[e] * dc;
+        T g = G.c[0] ? G.c[0][e] : T(0);
+        if (G.c[1]) g += G.c[1][e];
+        if (G.c[2]) g += G.c[2][e];
+        acc += g * dc;
       }
       gr[e] = acc;
       T gx = T(0), gy = T(0), gz = T(0);
@@ -313,28 +327,44 @@ extern "C" int tmdnet_edge_geom_fwd_rows(int dtype, int n_edges, int num_rbf, in
                   rbf, cutoff, unit, rows, n_rows, rbf_rows, stream);
 }
 
-extern "C" int tmdnet_edge_geom_bwd(int dtype, int n_edges, int num_rbf, int rbf_type,
-                                    const int32_t* src, const int32_t* dst, const void* deltas,
-                                    const void* dist, const void* mu, const void* beta,
-                                    double cutoff_lower, double cutoff_upper, const void* grad_rbf,
-                                    const void* grad_cutoff, const void* grad_unit, void* grad_dist,
-                                    void* grad_deltas, void* stream) {
+extern "C" int tmdnet_edge_geom_bwd_multi(int dtype, int n_edges, int num_rbf, int rbf_type,
+                                          const int32_t* src, const int32_t* dst, const void* deltas,
+                                          const void* dist, const void* mu, const void* beta,
+                                          double cutoff_lower, double cutoff_upper, const void* grad_rbf,
+                                          const void* grad_rbf2, const void* grad_rbf3, const void* grad_cutoff,
+                                          const void* grad_cutoff2, const void* grad_cutoff3, const void* grad_unit,
+                                          void* grad_dist, void* grad_deltas, void* stream) {
   if (n_edges <= 0) return kOk;
   hipStream_t st = (hipStream_t)stream;
   const int tb = 256;
   const int blocks = (int)std::min<long long>(((long long)n_edges + 3) / 4, 256LL * 64);
   if (dtype == TMDNET_F32) {
     auto P = geom::make<float>(n_edges, num_rbf, rbf_type, src, dst, deltas, dist, mu, beta, cutoff_lower, cutoff_upper);
-    hipLaunchKernelGGL(geom::k_bwd<float>, dim3(blocks), dim3(tb), 0, st, P, (const float*)grad_rbf,
-                       (const float*)grad_cutoff, (const float*)grad_unit, (float*)grad_dist, (float*)grad_deltas);
+    geom::GIn<float> G{{(const float*)grad_rbf, (const float*)grad_rbf2, (const float*)grad_rbf3},
+                       {(const float*)grad_cutoff, (const float*)grad_cutoff2, (const float*)grad_cutoff3}};
+    hipLaunchKernelGGL(geom::k_bwd<float>, dim3(blocks), dim3(tb), 0, st, P, G, (const float*)grad_unit,
+                       (float*)grad_dist, (float*)grad_deltas);
   } else if (dtype == TMDNET_F64) {
     auto P = geom::make<double>(n_edges, num_rbf, rbf_type, src, dst, deltas, dist, mu, beta, cutoff_lower, cutoff_upper);
-    hipLaunchKernelGGL(geom::k_bwd<double>, dim3(blocks), dim3(tb), 0, st, P, (const double*)grad_rbf,
-                       (const double*)grad_cutoff, (const double*)grad_unit, (double*)grad_dist, (double*)grad_deltas);
+    geom::GIn<double> G{{(const double*)grad_rbf, (const double*)grad_rbf2, (const double*)grad_rbf3},
+                        {(const double*)grad_cutoff, (const double*)grad_cutoff2, (const double*)grad_cutoff3}};
+    hipLaunchKernelGGL(geom::k_bwd<double>, dim3(blocks), dim3(tb), 0, st, P, G, (const double*)grad_unit,
+                       (double*)grad_dist, (double*)grad_deltas);
   } else {
     return kUnsupported;
   }
   return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
+}
+
+extern "C" int tmdnet_edge_geom_bwd(int dtype, int n_edges, int num_rbf, int rbf_type,
+                                    const int32_t* src, const int32_t* dst, const void* deltas,
+                                    const void* dist, const void* mu, const void* beta,
+                                    double cutoff_lower, double cutoff_upper, const void* grad_rbf,
+                                    const void* grad_cutoff, const void* grad_unit, void* grad_dist,
+                                    void* grad_deltas, void* stream) {
+  return tmdnet_edge_geom_bwd_multi(dtype, n_edges, num_rbf, rbf_type, src, dst, deltas, dist, mu, beta,
+                                    cutoff_lower, cutoff_upper, grad_rbf, nullptr, nullptr, grad_cutoff, nullptr,
+                                    nullptr, grad_unit, grad_dist, grad_deltas, stream);
 }
 
 extern "C" int tmdnet_rbf_deriv(int dtype, int num_rbf, int rbf_type, const void* dist, const void* mu,

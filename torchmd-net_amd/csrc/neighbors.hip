@@ -391,10 +391,12 @@ __global__ __launch_bounds__(256) void k_cell_pairs(Params<T> P, CellGeom<T> G,
 //   g[e] = (r[e]==0) ? 0 : gdelta[e] + delta[e]/r[e] * gr[e];  dpos[src] += g, dpos[dst] -= g.
 // With a symmetric list and T:  dpos[n] = sum_{e in row n} g[T(e)] - g[e].
 template <typename T>
-__device__ __forceinline__ V3<T> edge_grad(int e, const T* gd, const T* gr, const T* dl, const T* r) {
+__device__ __forceinline__ V3<T> edge_grad(int e, const T* gd, const T* gr, const T* gr2, const T* dl, const T* r) {
   const T re = r[e];
   if (re == T(0)) return {T(0), T(0), T(0)};
-  const T gre = gr ? gr[e] / re : T(0);
+  T gsum = gr ? gr[e] : T(0);
+  if (gr2) gsum += gr2[e];  // the distances' second consumer (the ET stack's dr-mode g_r)
+  const T gre = gsum / re;
   V3<T> g{T(0), T(0), T(0)};
   if (gd) g = {gd[3 * e + 0], gd[3 * e + 1], gd[3 * e + 2]};
   g.x += dl[3 * e + 0] * gre;
@@ -417,18 +419,19 @@ __device__ __forceinline__ T group_sum16(T v) {
 template <typename T>
 __global__ void k_nl_backward(int n, const int* __restrict__ row_ptr, const int32_t* __restrict__ tr,
                               int cap, const T* __restrict__ gd, const T* __restrict__ gr,
-                              const T* __restrict__ dl, const T* __restrict__ r, T* __restrict__ gpos) {
+                              const T* __restrict__ gr2, const T* __restrict__ dl, const T* __restrict__ r,
+                              T* __restrict__ gpos) {
   const int gt = blockIdx.x * blockDim.x + threadIdx.x;
   const int t = gt / kNlLanes, lane = gt % kNlLanes;
   V3<T> acc{T(0), T(0), T(0)};
   if (t < n) {
     const int b = min(row_ptr[t], cap), e = min(row_ptr[t + 1], cap);
     for (int k = b + lane; k < e; k += kNlLanes) {
-      const V3<T> gm = edge_grad(k, gd, gr, dl, r);
+      const V3<T> gm = edge_grad(k, gd, gr, gr2, dl, r);
       acc.x -= gm.x; acc.y -= gm.y; acc.z -= gm.z;
       const int k2 = tr[k];
       if (k2 >= 0) {
-        const V3<T> gp = edge_grad(k2, gd, gr, dl, r);
+        const V3<T> gp = edge_grad(k2, gd, gr, gr2, dl, r);
         acc.x += gp.x; acc.y += gp.y; acc.z += gp.z;
       }
     }
@@ -710,25 +713,35 @@ extern "C" int tmdnet_nl_build_paired(int dtype, int strategy, const void* pos, 
                       stream);
 }
 
-extern "C" int tmdnet_nl_backward(int dtype, int n_atoms, const int32_t* row_ptr,
-                                  const int32_t* transpose_map, int max_pairs,
-                                  const void* grad_deltas, const void* grad_distances,
-                                  const void* deltas, const void* distances, void* grad_pos,
-                                  void* stream) {
+extern "C" int tmdnet_nl_backward_multi(int dtype, int n_atoms, const int32_t* row_ptr,
+                                        const int32_t* transpose_map, int max_pairs, const void* grad_deltas,
+                                        const void* grad_distances, const void* grad_distances2, const void* deltas,
+                                        const void* distances, void* grad_pos, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   const int tb = 256;
   dim3 g((unsigned)(((size_t)n_atoms * nl::kNlLanes + tb - 1) / tb));
   if (dtype == TMDNET_F32)
     hipLaunchKernelGGL(nl::k_nl_backward<float>, g, dim3(tb), 0, st, n_atoms, row_ptr, transpose_map,
                        max_pairs, (const float*)grad_deltas, (const float*)grad_distances,
-                       (const float*)deltas, (const float*)distances, (float*)grad_pos);
+                       (const float*)grad_distances2, (const float*)deltas, (const float*)distances,
+                       (float*)grad_pos);
   else if (dtype == TMDNET_F64)
     hipLaunchKernelGGL(nl::k_nl_backward<double>, g, dim3(tb), 0, st, n_atoms, row_ptr, transpose_map,
                        max_pairs, (const double*)grad_deltas, (const double*)grad_distances,
-                       (const double*)deltas, (const double*)distances, (double*)grad_pos);
+                       (const double*)grad_distances2, (const double*)deltas, (const double*)distances,
+                       (double*)grad_pos);
   else
     return kUnsupported;
   return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
+}
+
+extern "C" int tmdnet_nl_backward(int dtype, int n_atoms, const int32_t* row_ptr,
+                                  const int32_t* transpose_map, int max_pairs,
+                                  const void* grad_deltas, const void* grad_distances,
+                                  const void* deltas, const void* distances, void* grad_pos,
+                                  void* stream) {
+  return tmdnet_nl_backward_multi(dtype, n_atoms, row_ptr, transpose_map, max_pairs, grad_deltas, grad_distances,
+                                  nullptr, deltas, distances, grad_pos, stream);
 }
 
 extern "C" int tmdnet_nl_backward2(int dtype, int n_atoms, const int32_t* row_ptr, const int32_t* src,
@@ -775,7 +788,7 @@ __global__ void k_nl_backward_edges(int n, const int32_t* __restrict__ nb, int c
   if (e >= cap) return;
   const int s = nb[e], t = nb[cap + e];
   if (s < 0 || t < 0 || s >= n || t >= n) return;
-  const V3<T> g = edge_grad(e, gd, gr, dl, r);
+  const V3<T> g = edge_grad(e, gd, gr, (const T*)nullptr, dl, r);
   if (g.x == T(0) && g.y == T(0) && g.z == T(0)) return;
   atomicAdd(gpos + 3 * s + 0, g.x);
   atomicAdd(gpos + 3 * s + 1, g.y);

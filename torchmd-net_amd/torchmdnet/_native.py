@@ -37,11 +37,13 @@ SIGNATURES = {
     "tmdnet_nl_build": (I, [I, I, P, P, I, P, I, D, D, I, I, I, P, P, P, P, P, P, I, P, SZ, P]),
     "tmdnet_nl_build_paired": (I, [I, I, P, P, I, P, I, D, D, I, I, I, P, P, P, P, P, P, I, P, SZ, P, P, I, P]),
     "tmdnet_nl_backward": (I, [I, I, P, P, I, P, P, P, P, P, P]),
+    "tmdnet_nl_backward_multi": (I, [I, I, P, P, I, P, P, P, P, P, P, P]),
     "tmdnet_nl_backward2": (I, [I, I, P, P, P, I, P, P, P, P, P, P, P, P]),
     "tmdnet_nl_backward_edges": (I, [I, I, P, I, P, P, P, P, P, P]),
     "tmdnet_edge_geom_fwd": (I, [I, I, I, I, P, P, P, P, P, P, D, D, P, P, P, P]),
     "tmdnet_edge_geom_fwd_rows": (I, [I, I, I, I, P, P, P, P, P, P, D, D, P, P, P, P, I, P, P]),
     "tmdnet_edge_geom_bwd": (I, [I, I, I, I, P, P, P, P, P, P, D, D, P, P, P, P, P, P]),
+    "tmdnet_edge_geom_bwd_multi": (I, [I, I, I, I, P, P, P, P, P, P, D, D, P, P, P, P, P, P, P, P, P, P]),
     "tmdnet_edge_geom_bwd2": (I, [I, I, I, I, P, P, P, P, P, P, D, D, P, P, P, P, P, P, P, P, P, P, P]),
     "tmdnet_et_message_fwd": (I, [I, I, I, I, P, P, I, P, I, P, I, P, I, P, P, I, P, I, P, P, P, P, I, P, P,
                                   P]),

@@ -177,44 +177,51 @@ def validate_box(box, cutoff_upper):
 
 
 class _NeighborGeom(Function):
-    """(pos) -> (deltas, distances) of a prebuilt graph; backward = tmdnet_nl_backward."""
+    """(pos) -> (deltas, distances, distances alias) of a prebuilt graph; backward = tmdnet_nl_backward.
+    The alias is the distances for a second consumer (the ET stack's force pass reads r besides the edge
+    geometry): its gradient is summed by the backward kernel, not by an autograd add launch."""
 
     @staticmethod
     def forward(ctx, pos, graph, deltas, distances):
         ctx.graph = graph
         ctx.save_for_backward(pos, deltas, distances)
-        return deltas, distances
+        return deltas, distances, distances.view_as(distances)
 
     @staticmethod
-    def backward(ctx, g_deltas, g_dist):
+    def backward(ctx, g_deltas, g_dist, g_dist2):
         pos, deltas, distances = ctx.saved_tensors
-        gpos = _NeighborGeomBwd.apply(pos, g_deltas, g_dist, deltas, distances, ctx.graph)
+        if g_dist is None and g_dist2 is not None:
+            g_dist, g_dist2 = g_dist2, None
+        gpos = _NeighborGeomBwd.apply(pos, g_deltas, g_dist, deltas, distances, ctx.graph, g_dist2)
         return gpos, None, None, None
 
 
 class _NeighborGeomBwd(Function):
     @staticmethod
-    def forward(ctx, pos, g_deltas, g_dist, deltas, distances, graph):
+    def forward(ctx, pos, g_deltas, g_dist, deltas, distances, graph, g_dist2=None):
         lib = nat.load()
         n = pos.shape[0]
         gpos = torch.empty_like(pos)
         gd = None if g_deltas is None else g_deltas.contiguous()
         gr = None if g_dist is None else g_dist.contiguous()
-        rc = lib.tmdnet_nl_backward(nat.dtype_code(pos.dtype), n, nat.ptr(graph.row_ptr),
-                                    nat.ptr(graph.transpose), graph.n_edges, nat.ptr(gd), nat.ptr(gr),
-                                    nat.ptr(deltas), nat.ptr(distances), nat.ptr(gpos),
-                                    nat.stream(pos.device))
-        nat.check(rc, "tmdnet_nl_backward")
+        gr2 = None if g_dist2 is None else g_dist2.contiguous()
+        rc = lib.tmdnet_nl_backward_multi(nat.dtype_code(pos.dtype), n, nat.ptr(graph.row_ptr),
+                                          nat.ptr(graph.transpose), graph.n_edges, nat.ptr(gd), nat.ptr(gr),
+                                          nat.ptr(gr2), nat.ptr(deltas), nat.ptr(distances), nat.ptr(gpos),
+                                          nat.stream(pos.device))
+        nat.check(rc, "tmdnet_nl_backward_multi")
         ctx.graph = graph
-        ctx.save_for_backward(pos, gd, gr, deltas, distances)
+        ctx.two = gr2 is not None
+        # the second order sees the summed distance gradient (both slots get its gradient)
+        ctx.save_for_backward(pos, gd, gr if gr2 is None else gr + gr2, deltas, distances)
         return gpos
 
     @staticmethod
     def backward(ctx, ggpos):
         pos, gd, gr, deltas, distances = ctx.saved_tensors
         d_pos, d_gd, d_gr = _NeighborGeomBwd2.apply(pos, ggpos, gd, gr, deltas, distances, ctx.graph)
-        return d_pos, (d_gd if gd is not None else None), (d_gr if gr is not None else None), \
-            None, None, None
+        d_gr = d_gr if gr is not None else None
+        return d_pos, (d_gd if gd is not None else None), d_gr, None, None, None, (d_gr if ctx.two else None)
 
 
 def nl_backward_composite(pos, gd, gr, deltas, distances, src, dst):
@@ -341,9 +348,10 @@ def build_graph(pos, batch, cutoff_lower, cutoff_upper, max_num_pairs, loop=True
         graph.sorted_rows = strategy != "cell"  # brute / shared rows list sources ascending
         if fused_pairs is not None:
             graph._pairs = fused_pairs
-        deltas, distances = _NeighborGeom.apply(pos, graph, dl, dist)
+        deltas, distances, distances2 = _NeighborGeom.apply(pos, graph, dl, dist)
         graph.deltas = deltas
         graph.distances = distances
+        graph.distances_alias = distances2  # for a second consumer of r (no autograd add of the two)
         return graph
     nb, dl, dist, num, row_ptr, tr = neighbor_pairs_raw(
         strategy, pos, batch, box, use_periodic, cutoff_lower, cutoff_upper, max_num_pairs, loop,
@@ -358,9 +366,10 @@ def build_graph(pos, batch, cutoff_lower, cutoff_upper, max_num_pairs, loop=True
     graph.sorted_rows = strategy != "cell"  # brute / shared rows list sources ascending
     if fused_pairs is not None and graph.symmetric:  # the numbering of the kept prefix of rows
         graph._pairs = (fused_pairs[0][:E], fused_pairs[1][:(E + n) // 2])
-    deltas, distances = _NeighborGeom.apply(pos, graph, dl[:E], dist[:E])
+    deltas, distances, distances2 = _NeighborGeom.apply(pos, graph, dl[:E], dist[:E])
     graph.deltas = deltas
     graph.distances = distances
+    graph.distances_alias = distances2
     return graph
 
 
@@ -395,8 +404,12 @@ def _edge_geom_composite(deltas, dist, selfmask, mu, beta, cl, cu, rbf_type, wan
 
 
 class _EdgeGeom(Function):
+    """(rbf, cutoff, unit vectors) of the graph's edges.  ``fan`` = (k_f, k_c): k_f - 1 more aliases of the
+    rbf output and k_c - 1 of the cutoff, one per further consumer; their gradients are summed by the
+    backward kernel (tmdnet_edge_geom_bwd_multi) instead of by autograd add launches."""
+
     @staticmethod
-    def forward(ctx, deltas, dist, graph, mu, beta, cl, cu, rbf_type, want, rows_out=None):
+    def forward(ctx, deltas, dist, graph, mu, beta, cl, cu, rbf_type, want, rows_out=None, fan=(1, 1)):
         lib = nat.load()
         E = dist.shape[0]
         R = mu.shape[0]
@@ -414,35 +427,66 @@ class _EdgeGeom(Function):
         nat.check(rc, "tmdnet_edge_geom_fwd")
         ctx.graph = graph
         ctx.cfg = (cl, cu, rbf_type, want)
+        ctx.fan = fan
         ctx.save_for_backward(deltas, dist, mu, beta)
-        return f, C, u
+        extra = [f.view_as(f) for _ in range(fan[0] - 1)] + [C.view_as(C) for _ in range(fan[1] - 1)]
+        return (f, C, u, *extra)
 
     @staticmethod
-    def backward(ctx, gf, gC, gu):
+    def backward(ctx, gf, gC, gu, *galias):
         deltas, dist, mu, beta = ctx.saved_tensors
         cl, cu, rbf_type, want = ctx.cfg
-        g_dl, g_r = _EdgeGeomBwd.apply(deltas, dist, gf, gC, gu, ctx.graph, mu, beta, cl, cu, rbf_type)
-        return g_dl, g_r, None, None, None, None, None, None, None, None
+        kf = ctx.fan[0] - 1
+        gfs = [gf] + list(galias[:kf])
+        gCs = [gC] + list(galias[kf:])
+        gfs += [None] * (3 - len(gfs))
+        gCs += [None] * (3 - len(gCs))
+        g_dl, g_r = _EdgeGeomBwd.apply(deltas, dist, gfs[0], gCs[0], gu, ctx.graph, mu, beta, cl, cu, rbf_type,
+                                       gfs[1], gfs[2], gCs[1], gCs[2])
+        return g_dl, g_r, None, None, None, None, None, None, None, None, None
+
+
+def _sum_opt(ts):
+    live = [t for t in ts if t is not None]
+    if not live:
+        return None
+    out = live[0]
+    for t in live[1:]:
+        out = out + t
+    return out
+
+
+def _slot_grads(ctx, d_gf, d_gC):
+    """Gradients of _EdgeGeomBwd's extra gradient slots (gf2, gf3, gC2, gC3): the same as slot 1's."""
+    fs, cs = ctx.slots
+    return (d_gf if fs[1] else None, d_gf if fs[2] else None, d_gC if cs[1] else None, d_gC if cs[2] else None)
 
 
 class _EdgeGeomBwd(Function):
     @staticmethod
-    def forward(ctx, deltas, dist, gf, gC, gu, graph, mu, beta, cl, cu, rbf_type):
+    def forward(ctx, deltas, dist, gf, gC, gu, graph, mu, beta, cl, cu, rbf_type, gf2=None, gf3=None, gC2=None,
+                gC3=None):
         lib = nat.load()
         E = dist.shape[0]
         R = mu.shape[0]
         g_r = torch.empty_like(dist)
         g_dl = torch.empty_like(deltas)
-        gf_ = None if gf is None else gf.contiguous()
-        gC_ = None if gC is None else gC.contiguous()
-        gu_ = None if gu is None else gu.contiguous()
-        rc = lib.tmdnet_edge_geom_bwd(nat.dtype_code(dist.dtype), E, R, rbf_type, nat.ptr(graph.src),
-                                      nat.ptr(graph.dst), nat.ptr(deltas), nat.ptr(dist), nat.ptr(mu),
-                                      nat.ptr(beta), float(cl), float(cu), nat.ptr(gf_), nat.ptr(gC_),
-                                      nat.ptr(gu_), nat.ptr(g_r), nat.ptr(g_dl), nat.stream(dist.device))
-        nat.check(rc, "tmdnet_edge_geom_bwd")
+        c = lambda t: None if t is None else t.contiguous()  # noqa: E731
+        gfl = [c(gf), c(gf2), c(gf3)]
+        gCl = [c(gC), c(gC2), c(gC3)]
+        gu_ = c(gu)
+        rc = lib.tmdnet_edge_geom_bwd_multi(nat.dtype_code(dist.dtype), E, R, rbf_type, nat.ptr(graph.src),
+                                            nat.ptr(graph.dst), nat.ptr(deltas), nat.ptr(dist), nat.ptr(mu),
+                                            nat.ptr(beta), float(cl), float(cu), *[nat.ptr(t) for t in gfl],
+                                            *[nat.ptr(t) for t in gCl], nat.ptr(gu_), nat.ptr(g_r), nat.ptr(g_dl),
+                                            nat.stream(dist.device))
+        nat.check(rc, "tmdnet_edge_geom_bwd_multi")
         ctx.graph = graph
         ctx.cfg = (cl, cu, rbf_type)
+        # the second order sees the summed incoming gradients (each slot's gradient is the same)
+        ctx.slots = ([t is not None for t in gfl], [t is not None for t in gCl])
+        gf_ = _sum_opt(gfl)
+        gC_ = _sum_opt(gCl)
         ctx.save_for_backward(deltas, dist, gf_, gC_, gu_, mu, beta)
         return g_dl, g_r
 
@@ -460,8 +504,11 @@ class _EdgeGeomBwd(Function):
             for i, t in enumerate((deltas, dist, gf, gC, gu)):
                 node = next(nf)[0] if i < 2 or t is not None else None
                 want.append(t is not None and ctx.needs_input_grad[i] and _will_run(node))
+            fs, cs = ctx.slots  # extra gradient slots (fan-out) take slot 1's gradient
+            want[2] = want[2] or (gf is not None and any(fs[1:]))
+            want[3] = want[3] or (gC is not None and any(cs[1:]))
             if not any(want):
-                return (None,) * 11
+                return (None,) * 15
             o = [torch.empty_like(t) if w else None for t, w in zip((deltas, dist, gf, gC, gu), want)]
             lib = nat.load()
             rc = lib.tmdnet_edge_geom_bwd2(
@@ -471,7 +518,7 @@ class _EdgeGeomBwd(Function):
                 nat.ptr(None if gg_r is None else gg_r.contiguous()), nat.ptr(o[2]), nat.ptr(o[3]), nat.ptr(o[4]),
                 nat.ptr(o[1]), nat.ptr(o[0]), nat.stream(dist.device))
             nat.check(rc, "tmdnet_edge_geom_bwd2")
-            return (o[0], o[1], o[2], o[3], o[4], None, None, None, None, None, None)
+            return (o[0], o[1], o[2], o[3], o[4], None, None, None, None, None, None) + _slot_grads(ctx, o[2], o[3])
         selfmask = graph.src == graph.dst
         with torch.enable_grad():
             dl = deltas.detach().requires_grad_(True)
@@ -485,12 +532,13 @@ class _EdgeGeomBwd(Function):
             inputs = [dl, r] + [u for u in ups if u is not None]
             sel = [(f, g) for f, g in zip(first, (gg_dl, gg_r)) if f is not None and g is not None]
             if not sel:
-                return (None,) * 11
+                return (None,) * 15
             second = torch.autograd.grad([f for f, _ in sel], inputs, [g for _, g in sel],
                                          create_graph=_create, allow_unused=True)
         it = iter(second[2:])
         gups = [next(it) if u is not None else None for u in ups]
-        return (second[0], second[1], gups[0], gups[1], gups[2], None, None, None, None, None, None)
+        return (second[0], second[1], gups[0], gups[1], gups[2], None, None, None, None, None, None) + \
+            _slot_grads(ctx, gups[0], gups[1])
 
 
 def rbf_deriv_launch(r, mu, beta, cl, cu, rbf_type, rows, out):
@@ -516,17 +564,30 @@ def rbf_composite(r, mu, beta, cl, cu, rbf_type):
     return _edge_geom_composite(None, r, None, mu, beta, cl, cu, rbf_type, (True, False, False))[0]
 
 
-def edge_geometry(graph, mu, beta, cutoff_lower, cutoff_upper, rbf_type, want=(True, True, True), rows=None):
+def edge_geometry(graph, mu, beta, cutoff_lower, cutoff_upper, rbf_type, want=(True, True, True), rows=None,
+                  fan=(1, 1)):
     """(rbf [E,R], cutoff [E], unit vectors [E,3]) of the graph's edges, fused (one HIP kernel).
     ``rows`` (int32 [P]): also returns the rbf rows of those edges [P,R] from the same launch (a
-    forward-only tensor: gradients flow through the per-edge rbf), as a fourth value."""
+    forward-only tensor: gradients flow through the per-edge rbf), as a fourth value.
+    ``fan`` = (k_f, k_c), each <= 3: returns ([rbf aliases] * k_f, [cutoff aliases] * k_c, unit) instead --
+    one alias per consumer, whose gradients the backward kernel sums (no autograd add launches)."""
     rows_out = None
     if rows is not None:
         rows_out = (rows, torch.empty((rows.shape[0], mu.shape[0]), dtype=graph.distances.dtype,
                                       device=graph.distances.device))
+    fan = (max(1, min(3, int(fan[0]))), max(1, min(3, int(fan[1]))))
+    if fan != (1, 1) and not (want[0] and want[1]):
+        raise ValueError("edge_geometry: fan-out needs the rbf and cutoff outputs")
     out = _EdgeGeom.apply(graph.deltas, graph.distances, graph, mu.detach(), beta.detach(),
-                          float(cutoff_lower), float(cutoff_upper), rbf_type, tuple(want), rows_out)
-    return out if rows is None else tuple(out) + (rows_out[1],)
+                          float(cutoff_lower), float(cutoff_upper), rbf_type, tuple(want), rows_out, fan)
+    if fan != (1, 1):
+        f, C, u = out[0], out[1], out[2]
+        extra = out[3:]
+        fs = [f] + list(extra[:fan[0] - 1])
+        Cs = [C] + list(extra[fan[0] - 1:])
+        return (fs, Cs, u) if rows is None else (fs, Cs, u, rows_out[1])
+    out = tuple(out[:3])
+    return out if rows is None else out + (rows_out[1],)
 
 
 # ----------------------------------------------------------------------------- ET message

@@ -174,17 +174,22 @@ class TensorNet(nn.Module):
         else:
             graph.self0_mult = float(1 + max(0, cap - graph.num_pairs)) if self.static_shapes else 1.0
         de = self.distance_expansion
+        k = 1 + len(self.layers)  # consumers of the rbf / cutoff rows: the embedding and every layer
         if self.trainable_rbf and torch.is_grad_enabled():
             edge_attr = de(graph.distances)
             _, C, edge_vec = kernels.edge_geometry(graph, *de.kernel_params(), self.cutoff_lower,
                                                    self.cutoff_upper, de.rbf_type, want=(False, True, True))
+            fs, Cs = [edge_attr], [C]
         else:
-            edge_attr, C, edge_vec = kernels.edge_geometry(graph, *de.kernel_params(), self.cutoff_lower,
-                                                           self.cutoff_upper, de.rbf_type)
-        graph.cutoff = C
-        X = self.tensor_embedding(z, graph, graph.distances, edge_vec, edge_attr)
-        for layer in self.layers:
-            X = layer(X, graph, graph.distances, edge_attr)
+            # one alias per consumer (up to 3): their gradients are summed in the geometry backward kernel
+            fs, Cs, edge_vec = kernels.edge_geometry(graph, *de.kernel_params(), self.cutoff_lower, self.cutoff_upper,
+                                                     de.rbf_type, fan=(min(k, 3), min(k, 3)))
+        pick = lambda t, i: t[min(i, len(t) - 1)]  # noqa: E731
+        graph.cutoff = pick(Cs, 0)
+        X = self.tensor_embedding(z, graph, graph.distances, edge_vec, pick(fs, 0))
+        for i, layer in enumerate(self.layers):
+            graph.cutoff = pick(Cs, i + 1)
+            X = layer(X, graph, graph.distances, pick(fs, i + 1))
         x = tn_node.norms(X)  # cat(|I|^2, |A|^2, |S|^2) of decompose_tensor(X), one fused pass
         x = kernels.layer_norm(x, self.out_norm.weight, self.out_norm.bias, self.out_norm.eps)
         return kernels.mlp_act(x, [self.linear.weight], [self.linear.bias], self.act)

@@ -171,6 +171,7 @@ class TorchMD_ET(nn.Module):
             x = self.embedding(z)
         graph = self.distance.graph(pos, batch)
         f_pairs = None
+        edge_attr_s = C_s = None  # the layer stack's aliases of the rbf / cutoff rows
         de = self.distance_expansion
         if self.trainable_rbf and torch.is_grad_enabled():
             # trainable basis: parameters need gradients -> differentiable torch basis on the GPU
@@ -179,12 +180,20 @@ class TorchMD_ET(nn.Module):
                                                self.cutoff_upper, de.rbf_type, want=(False, True, True))
         else:
             pairs = getattr(graph, "_pairs", None)  # numbered by the neighbour build (sorted rows)
-            rows = pairs[1] if (pairs is not None and self.fused_stack and len(self.attention_layers)) else None
+            stack = self.fused_stack and len(self.attention_layers) > 0
+            rows = pairs[1] if (pairs is not None and stack) else None
+            # rbf and cutoff rows read by the neighbour embedding AND the layer stack: one alias each, their
+            # gradients summed in the geometry backward kernel (no autograd add launch)
+            fan = (2, 2) if (stack and self.neighbor_embedding is not None) else (1, 1)
             geo = kernels.edge_geometry(graph, *de.kernel_params(), self.cutoff_lower, self.cutoff_upper,
-                                        de.rbf_type, rows=rows)
+                                        de.rbf_type, rows=rows, fan=fan)
             edge_attr, C, d_ij = geo[:3]
             f_pairs = geo[3] if rows is not None else None
-        graph.cutoff = C
+            if fan != (1, 1):
+                (edge_attr, edge_attr_s), (C, C_s) = edge_attr, C
+        if edge_attr_s is None:
+            edge_attr_s, C_s = edge_attr, C
+        graph.cutoff = C_s
         if self.neighbor_embedding is not None:
             x = self.neighbor_embedding(z, x, graph, graph.distances, edge_attr, cutoff=C, x_emb=x_ne)
         if self.fused_stack and len(self.attention_layers) > 0:
@@ -192,10 +201,13 @@ class TorchMD_ET(nn.Module):
             # backward; same math as the loop below
             rbf = None
             if not (self.trainable_rbf and torch.is_grad_enabled()):  # fixed basis: f = rbf(r)
-                rbf = (graph.distances, *de.kernel_params(), self.cutoff_lower, self.cutoff_upper, de.rbf_type)
+                # (r's alias: the stack's g_r joins the geometry's in the neighbour backward kernel)
+                r_s = getattr(graph, "distances_alias", None)
+                rbf = (graph.distances if r_s is None else r_s, *de.kernel_params(), self.cutoff_lower,
+                       self.cutoff_upper, de.rbf_type)
             on = self.out_norm
             fuse_norm = on.elementwise_affine and on.eps == 1e-5
-            x, vec = et_stack(self.attention_layers, x, graph, edge_attr, C, d_ij, rbf=rbf,
+            x, vec = et_stack(self.attention_layers, x, graph, edge_attr_s, C_s, d_ij, rbf=rbf,
                               out_norm=on if fuse_norm else None, f_pairs=f_pairs)
             return (x if fuse_norm else on(x)), vec
         vec = torch.zeros(x.size(0), 3, x.size(1), device=x.device, dtype=x.dtype)
