@@ -9,6 +9,8 @@ reference math.  The kernels themselves are checked on the GPU (test_gpu_parity.
 """
 import math
 
+import os
+
 import pytest
 import torch
 
@@ -522,10 +524,16 @@ def test_stack_fused_out_norm(emulated, monkeypatch, batched):
         assert torch.allclose(a, b, atol=1e-10, rtol=1e-8), i
 
 
-@pytest.mark.parametrize("out_norm", [False, True])
-@pytest.mark.parametrize("dr", ["1", "0"])
-@pytest.mark.parametrize("batched", [True, False])
-@pytest.mark.parametrize("infl", ["both", "keys", "values", "none"])
+# every distance_influence mode against both values of each switch (pairwise cover of the 32-case grid:
+# each case takes ~20 s of emulated double backward on the CPU); TMDNET_FULL_GRID=1 runs all 32
+_SO_GRID = ([(i, b, d, o) for i in ("both", "keys", "values", "none") for b in (True, False) for d in ("1", "0")
+             for o in (False, True)] if os.environ.get("TMDNET_FULL_GRID") == "1" else
+            [("both", True, "1", True), ("both", False, "0", False), ("keys", True, "0", False),
+             ("keys", False, "1", True), ("values", True, "1", False), ("values", False, "0", True),
+             ("none", True, "0", True), ("none", False, "1", False)])
+
+
+@pytest.mark.parametrize("infl,batched,dr,out_norm", _SO_GRID)
 def test_hand_second_order_matches_composite(emulated, monkeypatch, infl, batched, dr, out_norm):
     """The hand-scheduled second order (et_stack._second_order: recorded first-order pass, its adjoint
     in forward layer order, a backward with injected cotangents) against autograd's double

@@ -366,3 +366,55 @@ def test_torchscript_fused_stack_no_stale_pack_across_models():
     y_s, f_s = scripted(z, pos.clone(), batch)
     y_e, f_e = model(z, pos.clone(), batch)
     assert _rel(y_s, y_e) < 1e-4 and _rel(f_s, f_e) < 1e-4
+
+
+@pytest.mark.parametrize("neighbor_embedding", [True, False])
+def test_torchscript_fused_eval_matches_eager_and_oracle(neighbor_embedding):
+    """Eval-mode TorchScript (the MD-engine form, reference README.md:6) runs the whole energy + force
+    evaluation as ONE operator, tmdnet::et_energy_forces: equal to the eager model and to the fp64 oracle
+    (fp32 bar 1e-4); in train mode the scripted model keeps the differentiable operator path."""
+    from torchmdnet.models.model import create_model
+    _torch_lib_loaded()
+    args = yaml_args("equivariant-transformer")
+    args.update(prior_model=None, embedding_dimension=128, num_layers=8, derivative=True,
+                neighbor_embedding=neighbor_embedding)
+    torch.manual_seed(0)
+    model = create_model(args).to(DEV).eval()
+    assert model.fused_eval
+    scripted = torch.jit.script(model)
+    assert "et_energy_forces" in str(scripted.inlined_graph)
+    z, pos, batch = _batch(8)
+    y_e, f_e = model(z, pos.clone(), batch)
+    y_s, f_s = scripted(z, pos.clone(), batch)
+    assert _rel(y_s, y_e) < 1e-4 and _rel(f_s, f_e) < 1e-4
+    y_ref, f_ref = O.energy_forces(model.state_dict(), dict(args), z.cpu(), pos.cpu().double(), batch.cpu())
+    assert _rel(y_s, y_ref) < 1e-4 and _rel(f_s, f_ref) < 1e-4
+    scripted.train()
+    p = pos.clone().requires_grad_(True)
+    y_t, f_t = scripted(z, p, batch)
+    assert f_t.requires_grad and _rel(f_t, f_e) < 1e-4
+
+
+def test_torchscript_fused_eval_periodic_cell_list():
+    """The fused evaluation on a periodic box with the cell list (its neighbour build and minimum-image
+    geometry inside the operator) against the eager model."""
+    from torchmdnet.models.model import create_model
+    _torch_lib_loaded()
+    args = yaml_args("equivariant-transformer")
+    args.update(prior_model=None, embedding_dimension=128, num_layers=3, derivative=True, max_num_neighbors=128)
+    torch.manual_seed(0)
+    model = create_model(args).to(DEV).eval()
+    n = 600
+    g = torch.Generator().manual_seed(2)
+    L = (n / 0.1003) ** (1.0 / 3.0)
+    pos = (torch.rand(n, 3, generator=g, dtype=torch.float64) * L).float().to(DEV)
+    z = torch.tensor([8, 1, 1], dtype=torch.long).repeat(n // 3 + 1)[:n].to(DEV)
+    batch = torch.zeros(n, dtype=torch.long, device=DEV)
+    d = model.representation_model.distance
+    d.box = torch.eye(3) * L
+    d.use_periodic = True
+    d.strategy = "cell"
+    scripted = torch.jit.script(model)
+    y_e, f_e = model(z, pos.clone(), batch)
+    y_s, f_s = scripted(z, pos.clone(), batch)
+    assert _rel(y_s, y_e) < 1e-4 and _rel(f_s, f_e) < 1e-4

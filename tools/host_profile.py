@@ -27,6 +27,16 @@ def main():
         forms.append(("eager", model))
     if which in ("script", "both"):
         forms.append(("script", torch.jit.script(model)))
+    if which in ("variants", "both"):  # the scripted model under other executor settings
+        m_eval = create_model(bench.et_args(128)).to(dev).eval()
+        try:
+            forms.append(("script_frozen_eval", torch.jit.freeze(torch.jit.script(m_eval))))
+        except Exception as e:  # noqa: BLE001
+            print("freeze failed:", type(e).__name__, str(e)[:200])
+        forms.append(("script_eval", torch.jit.script(m_eval)))
+    if which == "noprof":  # the legacy (non-profiling) graph executor
+        torch._C._jit_set_profiling_executor(False)
+        forms.append(("script_legacy_executor", torch.jit.script(model)))
     for name, m in forms:
         for _ in range(5):
             m(z, pos, batch)

@@ -1451,14 +1451,14 @@ struct EtStackBwd : public Function<EtStackBwd> {
   }
 };
 
-struct EtStack : public Function<EtStack> {
-  static variable_list forward(AutogradContext* ctx, const Tensor& x_in, const Tensor& f_in, const Tensor& dist,
-                               const Tensor& C_in, const Tensor& u_in, const Tensor& mu, const Tensor& beta,
-                               const Tensor& row_ptr, const Tensor& src, const Tensor& dst, StackCfg c,
-                               at::TensorList params) {
+// The stack's forward launches (EtStack::forward; also the fused inference operator et_energy_forces):
+// returns (x_out, vec_out) and fills the intermediates A the dr-mode backward reads.
+std::pair<Tensor, Tensor> stack_forward(const Tensor& x_in, const Tensor& f_in, const Tensor& dist, const Tensor& C_in,
+                                        const Tensor& u_in, const Tensor& row_ptr, const Tensor& src,
+                                        const Tensor& dst, const StackCfg& c, const std::vector<Tensor>& P,
+                                        StackActs* A) {
     require_gpu(x_in, "et_stack");
     TORCH_CHECK(x_in.scalar_type() == at::kFloat, "et_stack: fp32 only (the model's per-layer loop serves fp64)");
-    std::vector<Tensor> P(params.begin(), params.end());
     const int64_t np = stack_np(c.hk, c.hv);
     const int64_t nP = static_cast<int64_t>(P.size()) - (c.out_norm ? 2 : 0);
     TORCH_CHECK(nP > 0 && nP % np == 0, "et_stack: ", P.size(), " parameters for ", np, " per layer");
@@ -1469,7 +1469,6 @@ struct EtStack : public Function<EtStack> {
     TORCH_CHECK(dist.size(0) == E && C.size(0) == E && u.size(0) == E && (!(c.hk || c.hv) || f.size(0) == E),
                 "et_stack: per-edge shapes");
     auto o = opts(x);
-    auto A = c10::make_intrusive<StackActs>();
     A->pk = pack_stack(P, L, np, c.hk, c.hv);
     const bool has_e = c.hk || c.hv;
     // every layer's projection rows in one GEMM unless that buffer would exceed 2 GB (large graphs:
@@ -1551,6 +1550,19 @@ struct EtStack : public Function<EtStack> {
       x = xo;
       vec = vo;
     }
+  return {x, vec};
+}
+
+struct EtStack : public Function<EtStack> {
+  static variable_list forward(AutogradContext* ctx, const Tensor& x_in, const Tensor& f_in, const Tensor& dist,
+                               const Tensor& C_in, const Tensor& u_in, const Tensor& mu, const Tensor& beta,
+                               const Tensor& row_ptr, const Tensor& src, const Tensor& dst, StackCfg c,
+                               at::TensorList params) {
+    std::vector<Tensor> P(params.begin(), params.end());
+    auto A = c10::make_intrusive<StackActs>();
+    auto xv = stack_forward(x_in, f_in, dist, C_in, u_in, row_ptr, src, dst, c, P, A.get());
+    Tensor x = xv.first, vec = xv.second;
+    G g{row_ptr, src, dst, Tensor()};
     ctx->saved_data["fwd_state"] = c10::IValue::make_capsule(A);  // the forward intermediates (StackActs)
     keep_cfg(ctx, c);
     keep_graph(ctx, g);
@@ -1604,6 +1616,143 @@ std::tuple<Tensor, Tensor> et_stack(const Tensor& x, const Tensor& f, const Tens
   return {r[0], r[1]};
 }
 
+
+// ----------------------------------------------------------------------------- fused inference
+// A whole ET energy + force evaluation (TorchMD_Net.forward with derivative=True, reference
+// models/model.py:232-300, torchmd_et.py:154-187, output_modules.py:80-115) as ONE operator with no autograd
+// graph: the launches of the eager graph-replayed path issued from C++ -- embeddings, neighbour list, edge
+// geometry, neighbour embedding, the fused layer stack, the EquivariantScalar head with its per-atom
+// Jacobian, the per-molecule sum, then the force pass (the head's Jacobian scaled by -std, the stack's dr-mode
+// backward, the neighbour-embedding / geometry / neighbour backward passes, every second consumer's
+// gradient summed in-kernel).  For TorchScript inference (MD engines, reference README.md:6): the
+// scripted model takes it in eval mode; its outputs carry no autograd graph.
+std::tuple<Tensor, Tensor> et_energy_forces(
+    const Tensor& z, const Tensor& pos_in, const Tensor& batch, const Tensor& box, bool use_periodic, double cl,
+    double cu, int64_t max_pairs, bool loop, const std::string& strategy, bool check_errors, const Tensor& emb_w,
+    const c10::optional<Tensor>& nb_emb_w_, const c10::optional<Tensor>& nb_dist_w_,
+    const c10::optional<Tensor>& nb_dist_b_, const c10::optional<Tensor>& nb_comb_w_,
+    const c10::optional<Tensor>& nb_comb_b_, const Tensor& mu_in, const Tensor& beta_in, int64_t rbf_type,
+    int64_t heads, bool has_dk, bool has_dv, bool out_norm, at::TensorList stack_params, int64_t acts,
+    at::TensorList head_params, const Tensor& std_in, const Tensor& mean_in) {
+  const c10::OptionalDeviceGuard guard(pos_in.device());
+  require_gpu(pos_in, "et_energy_forces");
+  TORCH_CHECK(pos_in.scalar_type() == at::kFloat && emb_w.scalar_type() == at::kFloat,
+              "et_energy_forces: fp32 models only");
+  TORCH_CHECK(head_params.size() == 12, "et_energy_forces: the EquivariantScalar head's 12 tensors");
+  at::NoGradGuard ng;
+  const Tensor pos = pos_in.detach().contiguous();
+  const int64_t N = z.size(0), H = emb_w.size(1), R = mu_in.size(0);
+  auto o = opts(pos);
+  void* st = stream_of(pos);
+  const int dt = TMDNET_F32;
+  const Tensor mu = mu_in.detach().to(at::kFloat).contiguous(), beta = beta_in.detach().to(at::kFloat).contiguous();
+  const Tensor zl = z.to(at::kLong).contiguous();
+  // embeddings: both tables in one launch
+  const Tensor nb_emb_w = val(nb_emb_w_);
+  const bool nb = nb_emb_w.defined();
+  Tensor x = at::empty({N, H}, o), xe = nb ? at::empty({N, H}, o) : Tensor();
+  {
+    const void* tabs[2] = {emb_w.data_ptr(), nb ? nb_emb_w.data_ptr() : nullptr};
+    const int lts[2] = {static_cast<int>(emb_w.stride(0)), nb ? static_cast<int>(nb_emb_w.stride(0)) : 0};
+    void* outs[2] = {x.data_ptr(), nb ? xe.data_ptr() : nullptr};
+    const int lds[2] = {static_cast<int>(H), static_cast<int>(H)};
+    check(tmdnet_embedding_fwd_f32(static_cast<int>(N), static_cast<int>(H), static_cast<int>(emb_w.size(0)),
+                                   zl.data_ptr<int64_t>(), nb ? 2 : 1, tabs, lts, outs, lds, st),
+          "tmdnet_embedding_fwd_f32");
+  }
+  // neighbour list (reference OptimizedDistance: resize_to_fit, check_errors)
+  Tensor bx = box;
+  if (strategy == "cell" && !use_periodic) {
+    bx = at::zeros({3, 3}, at::TensorOptions().dtype(at::kDouble));
+    bx[0][0] = 3.0 * cu;
+    bx[1][1] = 3.0 * cu;
+    bx[2][2] = 3.0 * cu;
+  }
+  Built B = nl_build(strategy, pos, batch, bx, use_periodic, cl, cu, max_pairs, loop, true, true, true);
+  const int64_t found = B.num.item<int>();
+  TORCH_CHECK(!check_errors || found <= max_pairs, "Found num_pairs(", found, ") > max_num_pairs(", max_pairs, ")");
+  TORCH_CHECK(found <= max_pairs, "et_energy_forces: the force pass needs the full symmetric neighbour list");
+  const int64_t E = found;
+  const Tensor src = B.nb[0].narrow(0, 0, E), dst = B.nb[1].narrow(0, 0, E), tr = B.tr.narrow(0, 0, E);
+  const Tensor dl = B.dl.narrow(0, 0, E), dist = B.dist.narrow(0, 0, E);
+  const Tensor& row_ptr = B.row_ptr;
+  // edge geometry
+  Tensor f = at::empty({E, R}, o), C = at::empty({E}, o), u = at::empty({E, 3}, o);
+  check(tmdnet_edge_geom_fwd(dt, static_cast<int>(E), static_cast<int>(R), static_cast<int>(rbf_type),
+                             ptr<int32_t>(src), ptr<int32_t>(dst), ptr(dl), ptr(dist), ptr(mu), ptr(beta), cl, cu,
+                             ptr(f), ptr(C), ptr(u), st),
+        "tmdnet_edge_geom_fwd");
+  // neighbour embedding: W = distance_proj(f); [x | x_nb] by the aggregation kernel; combine
+  Tensor W, cat, x1 = x;
+  if (nb) {
+    W = at::empty({E, H}, o);
+    gemm_into(f, val(nb_dist_w_), true, val(nb_dist_b_), W, false);
+    cat = at::empty({N, 2 * H}, o);
+    float* cb = static_cast<float*>(cat.data_ptr());
+    check(tmdnet_nbr_embed_fwd(dt, static_cast<int>(N), static_cast<int>(H), ptr<int32_t>(row_ptr),
+                               ptr<int32_t>(src), static_cast<int>(E), ptr(xe), static_cast<int>(H), ptr(W),
+                               static_cast<int>(H), ptr(C), cb + H, static_cast<int>(2 * H), ptr(x), cb, st),
+          "tmdnet_nbr_embed_fwd");
+    x1 = at::empty({N, H}, o);
+    gemm_into(cat, val(nb_comb_w_), true, val(nb_comb_b_), x1, false);
+  }
+  // the layer stack
+  StackCfg c{heads, rbf_type, cl, cu, has_dk, has_dv, out_norm, acts};
+  std::vector<Tensor> P(stack_params.begin(), stack_params.end());
+  StackActs A;
+  auto xv = stack_forward(x1, f, dist, C, u, row_ptr, src, dst, c, P, &A);
+  const Tensor xo = xv.first.contiguous(), vo = xv.second.contiguous();
+  // the head (+ per-atom Jacobian) and the per-molecule sum
+  Tensor y_atom = at::empty({N, 1}, o), jx = at::empty({N, H}, o), jv = at::empty({N, 3, H}, o);
+  const void* hw[12];
+  for (int i = 0; i < 12; ++i) hw[i] = head_params[i].data_ptr();
+  check(tmdnet_eq_head_fwd(dt, static_cast<int>(N), static_cast<int>(H), ptr(xo), ptr(vo), hw, ptr(y_atom), ptr(jx),
+                           ptr(jv), st),
+        "tmdnet_eq_head_fwd");
+  const int64_t n_mol = batch.max().item<int64_t>() + 1;  // (the reference reduce's dim_size, a host read)
+  const Tensor sd = std_in.to(at::kFloat).contiguous(), mn = mean_in.to(at::kFloat).contiguous();
+  Tensor y = at::empty({n_mol, 1}, o);
+  check(tmdnet_atom_sum_fwd(dt, static_cast<int>(N), static_cast<int>(n_mol), ptr(y_atom), batch.data_ptr<int64_t>(),
+                            ptr(sd), ptr(mn), ptr(y), st),
+        "tmdnet_atom_sum_fwd");
+  // force pass, seeded with -1 (neg_dy directly)
+  Tensor seed = at::full({n_mol, 1}, -1.0, o), g_atom = at::empty({N, 1}, o);
+  check(tmdnet_atom_sum_bwd(dt, static_cast<int>(N), static_cast<int>(n_mol), ptr(seed), batch.data_ptr<int64_t>(),
+                            ptr(sd), ptr(g_atom), st),
+        "tmdnet_atom_sum_bwd");
+  Tensor gX = at::empty({N, H}, o), gV = at::empty({N, 3, H}, o);
+  check(tmdnet_eq_head_bwd(dt, static_cast<int>(N), static_cast<int>(H), ptr(g_atom), ptr(jx), ptr(jv), ptr(gX),
+                           ptr(gV), st),
+        "tmdnet_eq_head_bwd");
+  G g{row_ptr, src, dst, tr};
+  auto gs = stack_backward_dr(A, gX, gV, dist, C, u, mu, beta, P, g, c);  // (g_x1, g_r, g_C, g_u)
+  Tensor gf, gC_nb;
+  if (nb) {
+    Tensor g_cat = at::empty({N, 2 * H}, o);
+    gemm_into(gs[0], val(nb_comb_w_), false, Tensor(), g_cat, false);
+    Tensor gW = at::empty({E, H}, o);
+    gC_nb = at::empty({E}, o);
+    const float* gcb = static_cast<const float*>(g_cat.data_ptr());
+    check(tmdnet_nbr_embed_bwd(dt, static_cast<int>(N), static_cast<int>(H), ptr<int32_t>(row_ptr), ptr<int32_t>(src),
+                               static_cast<int>(E), ptr(xe), static_cast<int>(H), ptr(W), static_cast<int>(H), ptr(C),
+                               gcb + H, static_cast<int>(2 * H), nullptr, ptr(gW), ptr(gC_nb), st),
+          "tmdnet_nbr_embed_bwd");
+    gf = at::empty({E, R}, o);
+    gemm_into(gW, val(nb_dist_w_), false, Tensor(), gf, false);
+  }
+  Tensor g_r = at::empty({E}, o), g_dl = at::empty({E, 3}, o);
+  check(tmdnet_edge_geom_bwd_multi(dt, static_cast<int>(E), static_cast<int>(R), static_cast<int>(rbf_type),
+                                   ptr<int32_t>(src), ptr<int32_t>(dst), ptr(dl), ptr(dist), ptr(mu), ptr(beta), cl, cu,
+                                   ptr(gf), nullptr, nullptr, ptr(gs[2]), ptr(gC_nb), nullptr, ptr(gs[3]), ptr(g_r),
+                                   ptr(g_dl), st),
+        "tmdnet_edge_geom_bwd_multi");
+  Tensor neg_dy = at::empty({N, 3}, o);
+  check(tmdnet_nl_backward_multi(dt, static_cast<int>(N), ptr<int32_t>(row_ptr), ptr<int32_t>(tr), static_cast<int>(E),
+                                 ptr(g_dl), ptr(g_r), ptr(gs[1]), ptr(dl), ptr(dist), ptr(neg_dy), st),
+        "tmdnet_nl_backward_multi");
+  return {y, neg_dy};
+}
+
 }  // namespace tmdt
 
 // The reference schema, verbatim (torchmdnet/neighbors/neighbors.cpp:3-5).
@@ -1642,6 +1791,11 @@ TORCH_LIBRARY(tmdnet, m) {
         "bool has_dk, bool has_dv, bool out_norm, Tensor[] params, int acts=0) -> (Tensor x, Tensor vec)");
   // drops the packed-weight cache of et_stack (after in-place writes that bypass the version counter)
   m.def("et_stack_invalidate() -> ()", tmdt::et_stack_invalidate);
+  m.def("et_energy_forces(Tensor z, Tensor pos, Tensor batch, Tensor box, bool use_periodic, float cutoff_lower, "
+        "float cutoff_upper, int max_pairs, bool loop, str strategy, bool check_errors, Tensor emb_w, "
+        "Tensor? nb_emb_w, Tensor? nb_dist_w, Tensor? nb_dist_b, Tensor? nb_comb_w, Tensor? nb_comb_b, Tensor mu, "
+        "Tensor beta, int rbf_type, int heads, bool has_dk, bool has_dv, bool out_norm, Tensor[] stack_params, "
+        "int acts, Tensor[] head_params, Tensor std, Tensor mean) -> (Tensor, Tensor)");
 }
 
 TORCH_LIBRARY_IMPL(tmdnet, CompositeImplicitAutograd, m) {
@@ -1652,4 +1806,5 @@ TORCH_LIBRARY_IMPL(tmdnet, CompositeImplicitAutograd, m) {
   m.impl("tn_embed", tmdt::tn_embed);
   m.impl("tn_message", tmdt::tn_message);
   m.impl("et_stack", tmdt::et_stack);
+  m.impl("et_energy_forces", tmdt::et_energy_forces);
 }

@@ -142,6 +142,27 @@ class TorchMD_Net(nn.Module):
         std = torch.scalar_tensor(1) if std is None else std
         self.register_buffer("std", std.to(dtype=dtype))
         self.reset_parameters()
+        # TorchScript in eval mode: the whole energy + force evaluation as one operator
+        # (tmdnet::et_energy_forces) when the configuration is the one it implements
+        self.fused_eval = self._fused_eval_capable()
+
+    @torch.jit.unused
+    def _fused_eval_capable(self) -> bool:
+        """ET (fp32, fixed RBF basis, the fused stack with a fused out_norm) + EquivariantScalar (the fused head
+        kernel's configuration) + plain sum reduction, no priors, forces requested: what tmdnet::et_energy_forces
+        evaluates."""
+        from .. import kernels
+        from .output_modules import EquivariantScalar
+        from .torchmd_et import TorchMD_ET
+        rep, out = self.representation_model, self.output_model
+        if not (self.derivative and self.prior_model is None and type(rep) is TorchMD_ET
+                and type(out) is EquivariantScalar):
+            return False
+        on = rep.out_norm
+        return bool(rep.fused_stack and not rep.trainable_rbf and rep.embedding.weight.dtype == torch.float32
+                    and len(rep.attention_layers) > 0 and on.elementwise_affine and on.eps == 1e-5
+                    and out.reduce_op in ("sum", "add") and kernels.eq_head_fusable(out.output_network)
+                    and self.std.numel() == 1 and self.mean.numel() == 1)
 
     def reset_parameters(self):
         self.representation_model.reset_parameters()
@@ -219,7 +240,13 @@ class TorchMD_Net(nn.Module):
     def _forward_script(self, z: Tensor, pos: Tensor, batch: Tensor, q: Optional[Tensor], s: Optional[Tensor],
                         extra_args: Optional[Dict[str, Tensor]]) -> Tuple[Tensor, Optional[Tensor]]:
         """TorchScript body: reference model.py:252-300 line for line (the representation model's
-        scripted path runs the HIP operators of libtmdnet_torch.so)."""
+        scripted path runs the HIP operators of libtmdnet_torch.so).  In eval mode a supported ET model runs
+        the whole evaluation as ONE operator (tmdnet::et_energy_forces: the eager path's launches issued from
+        C++, no autograd graph -- its outputs are not differentiable; script the model in train mode, or set
+        ``fused_eval = False`` before scripting, to differentiate the forces)."""
+        if self.fused_eval and not self.training and pos.is_cuda and pos.dtype == torch.float32:
+            return self.representation_model.fused_energy_forces(z, pos, batch, self.output_model.head_params(),
+                                                                 self.std, self.mean)
         x, v, z, pos, batch = self.representation_model(z, pos, batch, q=q, s=s)
         x = self.output_model.pre_reduce(x, v, z, pos, batch)
         if self.std is not None:

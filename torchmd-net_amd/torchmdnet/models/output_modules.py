@@ -4,7 +4,7 @@ Node-level and tiny (H -> H/2 -> 1 per atom); they run as PyTorch GPU ops.  ``re
 into molecules with ``index_add`` (the reference uses torch_scatter, output_modules.py:27-43).
 """
 from abc import ABCMeta, abstractmethod
-from typing import Optional
+from typing import List, Optional
 
 import torch
 from torch import nn
@@ -84,6 +84,10 @@ class OutputModel(nn.Module, metaclass=ABCMeta):
         None when this head has no such form (TorchMD_Net.forward then runs pre_reduce + fused_reduce)."""
         return None
 
+    def head_params(self) -> List[torch.Tensor]:
+        """The fused head kernel's tensors (EquivariantScalar; empty for other heads)."""
+        return []
+
 
 class Scalar(OutputModel):
     def __init__(self, hidden_channels, activation="silu", allow_prior_model=True, reduce_op="sum",
@@ -141,6 +145,14 @@ class EquivariantScalar(OutputModel):
     def reset_parameters(self):
         for layer in self.output_network:
             layer.reset_parameters()
+
+    def head_params(self) -> List[torch.Tensor]:
+        """The 12 tensors of tmdnet_eq_head_fwd in its order (kernels.eq_head_params)."""
+        ps: List[torch.Tensor] = []
+        for b in self.output_network:
+            ps += [b.vec1_proj.weight, b.vec2_proj.weight, b.update_net[0].weight, b.update_net[0].bias,
+                   b.update_net[2].weight, b.update_net[2].bias]
+        return ps
 
     def pre_reduce(self, x, v, z, pos, batch):
         if torch.jit.is_scripting():  # reference output_modules.py:98-103

@@ -8,7 +8,7 @@ scatter over ``edge_index[0]`` becomes a CSR walk of the reversed rows (no atomi
 neighbour slots become extra (0, 0) edges with r = 0 (tensornet.py:215-221), applied here as a
 multiplicity on atom 0's self loop.
 """
-from typing import Optional, Tuple
+from typing import List, Optional, Tuple
 
 import torch
 from torch import Tensor, nn
@@ -137,6 +137,11 @@ class TensorNet(nn.Module):
             x = self._forward(z[perm], pos.index_select(0, perm), batch[perm])
             return x[inv], None, z, pos, batch
         return self._forward(z, pos, batch), None, z, pos, batch
+
+    def fused_energy_forces(self, z: Tensor, pos: Tensor, batch: Tensor, head: List[Tensor], std: Tensor,
+                            mean: Tensor) -> Tuple[Tensor, Tensor]:
+        """(TorchMD_Net.fused_eval is ET-only; the same signature keeps the scripted TorchMD_Net uniform)"""
+        raise RuntimeError("fused_energy_forces: TorchMD_ET only")
 
     def _forward_script(self, z: Tensor, pos: Tensor, batch: Tensor) -> Tensor:
         """TorchScript path: reference tensornet.py:200-232 over the libtmdnet_torch.so operators."""

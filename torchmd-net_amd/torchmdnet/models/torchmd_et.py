@@ -160,6 +160,40 @@ class TorchMD_ET(nn.Module):
         x = self.out_norm(x)
         return x, vec
 
+    def fused_energy_forces(self, z: Tensor, pos: Tensor, batch: Tensor, head: List[Tensor], std: Tensor,
+                            mean: Tensor) -> Tuple[Tensor, Tensor]:
+        """(y, neg_dy) of TorchMD_Net(this model, EquivariantScalar head) as ONE operator,
+        tmdnet::et_energy_forces (TorchMD_Net.fused_eval: TorchScript inference in eval mode)."""
+        d = self.distance
+        de = self.distance_expansion
+        mu, beta = de.kernel_params()
+        params: List[Tensor] = []
+        hk = False
+        hv = False
+        acts = 0
+        for attn in self.attention_layers:
+            params += attn.stack_params()
+            hk = attn.dk_proj is not None
+            hv = attn.dv_proj is not None
+            acts = attn.act_flags
+        params += [self.out_norm.weight, self.out_norm.bias]
+        nb_emb: Optional[Tensor] = None
+        nb_dw: Optional[Tensor] = None
+        nb_db: Optional[Tensor] = None
+        nb_cw: Optional[Tensor] = None
+        nb_cb: Optional[Tensor] = None
+        ne = self.neighbor_embedding
+        if ne is not None:
+            nb_emb = ne.embedding.weight
+            nb_dw = ne.distance_proj.weight
+            nb_db = ne.distance_proj.bias
+            nb_cw = ne.combine.weight
+            nb_cb = ne.combine.bias
+        return torch.ops.tmdnet.et_energy_forces(
+            z, pos, batch, d.box, d.use_periodic, float(d.cutoff_lower), float(d.cutoff_upper),
+            d._max_pairs(pos.shape[0]), d.loop, d.strategy, d.check_errors, self.embedding.weight, nb_emb, nb_dw,
+            nb_db, nb_cw, nb_cb, mu, beta, de.rbf_type, self.num_heads, hk, hv, True, params, acts, head, std, mean)
+
     def _forward(self, z: Tensor, pos: Tensor, batch: Tensor):
         ne = self.neighbor_embedding
         x_ne = None
