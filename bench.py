@@ -556,7 +556,7 @@ def fused_projection_probe(launch, E, N, H, reps, dev, unfused):
                            "achieved_tflops_f16": round(bflop / (ms_b * 1e-3) / 1e12, 1),
                            "frac_mfma": round(bflop / (ms_b * 1e-3) / 1e12 / MFMA_BF16_PEAK_TFS, 4)},
            "fragments_per_evaluation_ms": round(ms_fr, 4),
-           "bound": "latency of the dependent per-tile gathers (r04 PMC, profiles/r04_fep_pmc.txt: most wave "
+           "bound": "latency of the dependent per-tile gathers (r04 PMC, profiles/r04_fep_{fwd,bwd}_pmc.txt: most wave "
                     "cycles parked on memory waits, VALU and MFMA well below their issue rates)"}
     if unfused:
         t_proj, t_dproj = _event_ms(f.proj, 10), _event_ms(f.dproj, 10)
