@@ -270,6 +270,20 @@ def test_torchscript_tensornet_matches_eager(group):
         assert _rel(a, b) < 1e-4
 
 
+@pytest.mark.parametrize("family", ["et", "tensornet"])
+def test_torchscript_after_eager_runs(family):
+    """A model that already ran eagerly (host-side scratch: force seeds, stacked projection rows) still
+    scripts, in train and eval mode, and matches the eager outputs (the order the bench uses)."""
+    _torch_lib_loaded()
+    model = (_et_model()[0] if family == "et" else _tn_model("O(3)")[0]).to(DEV)
+    z, pos, batch = _batch()
+    y_e, f_e = model(z, pos.clone(), batch)
+    for train in (True, False):
+        model.train(train)
+        y_s, f_s = torch.jit.script(model)(z, pos.clone(), batch)
+        assert _rel(y_s, y_e) < 1e-4 and _rel(f_s, f_e) < 1e-4
+
+
 @pytest.mark.parametrize("static_shapes", [True, False])
 def test_torchscript_tensornet_fp64_matches_oracle(static_shapes):
     _torch_lib_loaded()

@@ -124,6 +124,9 @@ def create_prior_models(args, dataset=None):
 class TorchMD_Net(nn.Module):
     """Representation model + output head + priors; forces = -d(sum y)/d pos (reference model.py:180-300)."""
 
+    # host-side scratch, not model state: a model that already ran eagerly still scripts
+    __jit_ignored_attributes__ = ["_seed_cache"]
+
     def __init__(self, representation_model, output_model, prior_model=None, mean=None, std=None,
                  derivative=False, dtype=torch.float32):
         super().__init__()

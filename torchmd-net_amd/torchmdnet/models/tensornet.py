@@ -206,6 +206,8 @@ def _check_symmetric_graph(edge_index, n):
 
 
 class TensorEmbedding(nn.Module):
+    __jit_ignored_attributes__ = ["_stacks"]  # the stacked distance-projection rows (host-side scratch)
+
     def __init__(self, hidden_channels, num_rbf, activation, cutoff_lower, cutoff_upper, trainable_rbf=False,
                  max_z=128, dtype=torch.float32):
         super().__init__()
