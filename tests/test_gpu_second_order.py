@@ -163,16 +163,25 @@ def test_neighbor_embedding_second_order_hand_matches_composite(monkeypatch):
         assert _rel(p_, q_) < 1e-11, (i, _rel(p_, q_))
 
 
+_TN_WIDE = [(678, 640, 128, True, 678), (2034, 384, 128, False, 2034), (678, 128, 0, True, 678),
+            (12548, 128, 64, True, 0), (5000, 96, 64, True, 1200), (37, 100, 36, False, 5),
+            (12548, 4096, 64, True, 12548), (3, 4, 8, True, 0)]
+# every problem reads <= 32 columns of B: the 32-column tile form (the dk/dv weight gradient's shape)
+_TN_NARROW = [(5210, 4096, 32, True, 10420), (5000, 70, 20, True, 900), (678, 128, 0, True, 678),
+              (37, 100, 31, False, 5), (12548, 96, 32, False, 0), (3, 4, 8, True, 0)]
+
+
+@pytest.mark.parametrize("form", ["1", "2"])  # TMDNET_TN_V: the unpipelined kernel / the pipelined one
+@pytest.mark.parametrize("shapes", ["wide", "narrow"])
 @pytest.mark.parametrize("use_cb", [False, True])
-def test_weight_gradient_tn_gemm_16byte_kernel(use_cb):
+def test_weight_gradient_tn_gemm_16byte_kernel(monkeypatch, use_cb, shapes, form):
     """The 64 x 64-tile, 16-byte-load TN kernel (every row 16-byte aligned): ragged M / N / K, long K
     (split over the rows), two segments with the ones column on one of them, bias-only problems, beta,
     and the bias written to its own vector (Cb) -- against fp64."""
     from torchmdnet import kernels
+    monkeypatch.setenv("TMDNET_TN_V", form)
     torch.manual_seed(4)
-    shapes = [(678, 640, 128, True, 678), (2034, 384, 128, False, 2034), (678, 128, 0, True, 678),
-              (12548, 128, 64, True, 0), (5000, 96, 64, True, 1200), (37, 100, 36, False, 5),
-              (12548, 4096, 64, True, 12548), (3, 4, 8, True, 0)]
+    shapes = _TN_WIDE if shapes == "wide" else _TN_NARROW
     probs, refs = [], []
     for K, M, Nb, ones, K2 in shapes:
         A, B = torch.randn(K, M, device=DEV), (torch.randn(K, Nb, device=DEV) if Nb else None)

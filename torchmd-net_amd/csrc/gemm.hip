@@ -491,6 +491,179 @@ __global__ __launch_bounds__(256) void k_tn_reduce_v(GroupTN G, int tiles) {
   *out = v;
 }
 
+// The "v" kernel with the row loop software-pipelined and a small reduction buffer (A/B switch
+// TMDNET_TN_V=1 keeps k_gemm_tn_v).  k_gemm_tn_v issues a 16-row block's loads and then its MFMAs, so every
+// block waits out a full memory latency, and its per-wave reduction tiles (NW x 64 x 65 floats, 66 KB)
+// hold a CU to two workgroups.  Here the next block's A / B rows are in flight while the MFMAs consume the
+// current ones (two register sets, the loop unrolled by two), and the waves fold their tiles into ONE
+// 64 x (16 NB + 1) buffer in wave order (deterministic: the same order every run).  NB = 16-column blocks
+// per tile: 2 when every problem reads <= 32 columns of B (the dk/dv weight gradient: 4096 x 32 over the
+// edge pairs), so no MFMA runs on the zero half of a 64-wide tile.  The tile numbering and the partial
+// layout are k_gemm_tn_v's (64 x 64 + 64; with NB = 2 the one column tile is n0 = 0 and the reduction
+// never reads columns >= Nr), so k_tn_reduce_v and the workspace size serve both.
+template <int NW, int NB, bool PIPE>
+__global__ __launch_bounds__(NW * 64) void k_gemm_tn_v2(GroupTN G) {
+  constexpr int TN = 16 * NB;
+  __shared__ float red[TV][TN + 1];
+  __shared__ float redb[TV];
+  const int tg = blockIdx.x / G.S, sk = blockIdx.x % G.S;
+  int pi = 0;
+  for (int i = 1; i < G.n; ++i)
+    if (tg >= G.p[i].tile0) pi = i;
+  const ProbTN& P = G.p[pi];
+  const int t = tg - P.tile0;
+  const int w = threadIdx.x / TMD_WAVE, lane = lane_id();
+  const int c = lane & 15, kq = lane >> 4;
+  const int m0 = (t / P.tiles_n) * TV, n0 = (t % P.tiles_n) * TV;
+  const bool anyones = P.ones1 || P.ones2;
+  const int Nr = anyones ? P.N - 1 : P.N;
+  const bool do_bias = anyones && (t % P.tiles_n) == 0;
+  const int KT = P.K + P.K2;
+  const int nkt = (KT + 15) / 16, cper = (nkt + G.S - 1) / G.S;
+  const int c_lo = min(KT, sk * cper * 16), c_hi = min(KT, (sk + 1) * cper * 16);
+  const int nkb = (c_hi - c_lo + 15) / 16, per = (nkb + NW - 1) / NW;
+  const int k_lo = min(c_hi, c_lo + w * per * 16), k_hi = min(c_hi, c_lo + (w + 1) * per * 16);
+  f4 acc[4][NB];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < NB; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  f4 rs = f4{0.f, 0.f, 0.f, 0.f};
+  // MFMA labels: lane c feeds A row m0 + 4c + mb into block mb and B column n0 + NB c + nb into block nb
+  const int ma = m0 + 4 * c, na = n0 + NB * c;
+  const bool mfull = ma + 3 < P.M, nfull = na + NB - 1 < Nr;
+  const bool gemm = n0 < Nr;
+  for (int seg = 0; seg < 2; ++seg) {
+    const int s0 = seg ? P.K : 0, s1 = seg ? KT : P.K;
+    const int lo = max(k_lo, s0), hi = min(k_hi, s1);
+    if (lo >= hi) continue;
+    const float* A = seg ? P.A2 : P.A;
+    const float* B = seg ? P.B2 : P.B;
+    const int lda = seg ? P.lda2 : P.lda, ldb = seg ? P.ldb2 : P.ldb;
+    const bool bias_seg = do_bias && (seg ? P.ones2 : P.ones1);
+    const int64_t* zi = P.onehot ? reinterpret_cast<const int64_t*>(A) : nullptr;
+    auto load = [&](int kb, f4 (&a)[4], f4 (&b)[4]) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int k = kb + 4 * u + kq;
+        const bool kv = k < hi;
+        const size_t ro = (size_t)(kv ? k - s0 : 0);
+        if (zi) {
+          const int64_t zk = kv ? zi[ro] : -1;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) a[u][i] = (zk == ma + i && ma + i < P.M) ? 1.f : 0.f;
+        } else if (kv && mfull) {
+          a[u] = *reinterpret_cast<const f4*>(A + ro * lda + ma);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) a[u][i] = (kv && ma + i < P.M) ? A[ro * lda + ma + i] : 0.f;
+        }
+        b[u] = f4{0.f, 0.f, 0.f, 0.f};
+        if (!gemm || !B) {
+        } else if (kv && nfull) {
+          if constexpr (NB == 4) {
+            b[u] = *reinterpret_cast<const f4*>(B + ro * ldb + na);
+          } else {
+            const float2 v = *reinterpret_cast<const float2*>(B + ro * ldb + na);
+            b[u][0] = v.x;
+            b[u][1] = v.y;
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < NB; ++i) b[u][i] = (kv && na + i < Nr) ? B[ro * ldb + na + i] : 0.f;
+        }
+      }
+    };
+    auto mma = [&](const f4 (&a)[4], const f4 (&b)[4]) {
+      if (bias_seg) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) rs += a[u];
+      }
+      if (gemm) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+            for (int nb = 0; nb < NB; ++nb)
+              acc[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][mb], b[u][nb], acc[mb][nb], 0, 0, 0);
+      }
+    };
+    f4 a0[4], b0[4], a1[4], b1[4];
+    if constexpr (!PIPE) {
+      for (int kb = lo; kb < hi; kb += 16) {
+        load(kb, a0, b0);
+        mma(a0, b0);
+      }
+      continue;
+    }
+    load(lo, a0, b0);
+    for (int kb = lo; kb < hi; kb += 32) {
+      const bool more = kb + 16 < hi;
+      if (more) load(kb + 16, a1, b1);
+      mma(a0, b0);
+      if (!more) break;
+      if (kb + 32 < hi) load(kb + 32, a0, b0);
+      mma(a1, b1);
+    }
+  }
+  // fold the waves' tiles in wave order (C layout of a 16x16 block: lane holds rows 4 (lane >> 4) + i,
+  // column lane & 15 in the MFMA labels)
+  if (do_bias) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float v = rs[i];
+      v += __shfl_xor(v, 16);
+      v += __shfl_xor(v, 32);
+      rs[i] = v;
+    }
+  }
+  for (int i = 0; i < NW; ++i) {
+    if (w == i) {
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            float& r = red[4 * (4 * kq + j) + mb][NB * c + nb];
+            r = i ? r + acc[mb][nb][j] : acc[mb][nb][j];
+          }
+      if (do_bias && kq == 0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) redb[4 * c + j] = i ? redb[4 * c + j] + rs[j] : rs[j];
+      }
+    }
+    __syncthreads();
+  }
+  float* part = G.S > 1 ? G.part + ((size_t)tg * G.S + sk) * TV_PART : nullptr;
+  for (int e = threadIdx.x; e < TV * TN; e += blockDim.x) {
+    const int r = e / TN, cc = e - r * TN;
+    const float v = red[r][cc];
+    if (part) {
+      part[r * TV + cc] = v;
+      continue;
+    }
+    const int m = m0 + r, n = n0 + cc;
+    if (m >= P.M || n >= Nr) continue;
+    float* out = P.C + (size_t)m * P.ldc + n;
+    *out = P.beta ? *out + v : v;
+  }
+  if (do_bias) {
+    for (int r = threadIdx.x; r < TV; r += blockDim.x) {
+      const float v = redb[r];
+      if (part) {
+        part[TV * TV + r] = v;
+        continue;
+      }
+      const int m = m0 + r;
+      if (m >= P.M) continue;
+      float* out = P.Cb ? P.Cb + m : P.C + (size_t)m * P.ldc + (P.N - 1);
+      *out = P.beta ? *out + v : v;
+    }
+  }
+}
+
 }  // namespace gemm
 
 // ---------------------------------------------------------------------------------------------------
@@ -780,7 +953,12 @@ static int gemm_run(gemm::Group& G, void* stream) {
 
 // split-K factor: few tiles over many rows (e.g. a 128 x 64 weight over 12.5k edges is 8 tiles)
 // leave most CUs idle; S 4-wave workgroups per tile (~1024 workgroups in all), each wave >= 64 rows
-static int tn_split(int tiles, int kmax, int target = 1024) {
+static int tn_target() {  // A/B switch TMDNET_TN_TARGET: workgroups aimed at by the split (default 1024)
+  const char* te = getenv("TMDNET_TN_TARGET");
+  return te ? max(64, atoi(te)) : 1024;
+}
+
+static int tn_split(int tiles, int kmax, int target = tn_target()) {
   int S = (target + tiles - 1) / tiles;
   S = min(S, max(1, kmax / (4 * 64)));
   return max(1, min(S, 64));
@@ -817,8 +995,33 @@ static void launch_tn(gemm::GroupTN& G, int tiles, int kmax, float* ws, hipStrea
     const int tv = tn_tiles(G, gemm::TV);
     G.S = ws ? tn_split(tv, kmax) : 1;  // (512 workgroups measured slower than 1024: 259 vs 227 us per step)
     G.part = ws;
-    if (kmax >= 8192 && G.S == 1) hipLaunchKernelGGL(gemm::k_gemm_tn_v<8>, dim3(tv), dim3(512), 0, st, G);
-    else hipLaunchKernelGGL(gemm::k_gemm_tn_v<4>, dim3(tv * G.S), dim3(256), 0, st, G);
+    bool narrow = true;  // every problem reads <= 32 columns of B
+    for (int i = 0; i < G.n; ++i) {
+      const gemm::ProbTN& P = G.p[i];
+      narrow = narrow && ((P.ones1 || P.ones2) ? P.N - 1 : P.N) <= 32;
+    }
+    // (read per launch: tests compare the forms in one process).  Default: the pipelined 32-column form
+    // for narrow groups (4096 x 32 over 6.6k + 6.6k rows: 80 vs 96 us), k_gemm_tn_v for 64-wide tiles
+    // (the pipelined form at 2 waves per SIMD: 289 vs 210 us on the dk/dv weight gradient, 4096 x 64)
+    const char* fe = getenv("TMDNET_TN_V");
+    const int form = fe ? atoi(fe) : (narrow ? 2 : 1);
+    if (form == 2 || form == 3) {
+      const bool pipe = form == 2;
+      if (kmax >= 8192 && G.S == 1) {
+        if (narrow) hipLaunchKernelGGL((gemm::k_gemm_tn_v2<8, 2, true>), dim3(tv), dim3(512), 0, st, G);
+        else hipLaunchKernelGGL((gemm::k_gemm_tn_v2<8, 4, true>), dim3(tv), dim3(512), 0, st, G);
+      } else if (narrow) {
+        if (pipe) hipLaunchKernelGGL((gemm::k_gemm_tn_v2<4, 2, true>), dim3(tv * G.S), dim3(256), 0, st, G);
+        else hipLaunchKernelGGL((gemm::k_gemm_tn_v2<4, 2, false>), dim3(tv * G.S), dim3(256), 0, st, G);
+      } else {
+        if (pipe) hipLaunchKernelGGL((gemm::k_gemm_tn_v2<4, 4, true>), dim3(tv * G.S), dim3(256), 0, st, G);
+        else hipLaunchKernelGGL((gemm::k_gemm_tn_v2<4, 4, false>), dim3(tv * G.S), dim3(256), 0, st, G);
+      }
+    } else if (kmax >= 8192 && G.S == 1) {
+      hipLaunchKernelGGL(gemm::k_gemm_tn_v<8>, dim3(tv), dim3(512), 0, st, G);
+    } else {
+      hipLaunchKernelGGL(gemm::k_gemm_tn_v<4>, dim3(tv * G.S), dim3(256), 0, st, G);
+    }
     if (G.S > 1)
       hipLaunchKernelGGL(gemm::k_tn_reduce_v, dim3((tv * gemm::TV_PART + 255) / 256), dim3(256), 0, st, G, tv);
     return;

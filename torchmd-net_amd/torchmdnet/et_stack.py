@@ -520,12 +520,10 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws, r=None, dr=Fa
     if meta.out_norm and not seed_pre_norm:  # gX is the gradient of LN(x_out): back through out_norm first
         x_pre, mean_o, rstd_o = acts[meta.n_layers]
         last = acts[meta.n_layers - 1]
-        if need_ws[meta.n_layers]:
-            gX, g_onw, g_onb = torch.ops.aten.native_layer_norm_backward(
-                gX, x_pre, [H], mean_o, rstd_o, params[-2], params[-1], [True, True, True])
-            g_params[-2:] = [g_onw, g_onb]
-            if x_top is not None:
-                gX = gX + x_top
+        if need_ws[meta.n_layers]:  # LayerNorm backward (+ the injected cotangent) and its weight gradients
+            g_y = gX
+            gX = _ln_bwd_epi(g_y, x_pre, mean_o, rstd_o, params[-2], x_top, None, None, None, None, None)
+            g_params[-2:] = list(kernels.layer_norm_wgrad(g_y, x_pre, mean_o, rstd_o))
         elif x_top is not None:  # LayerNorm backward + the injected cotangent (epilogue in the loop)
             gX = _ln_bwd_epi(gX, x_pre, mean_o, rstd_o, params[-2], x_top, None, None, None, None, None)
         else:  # LayerNorm backward + the last layer's epilogue backward, one kernel
@@ -810,8 +808,10 @@ def adjoint_epi_ln_launch(epi, gbar_x_in, gbar_vec_in, ln, outs=None):
     nat.check(rc, "tmdnet_et_adjoint_epi_ln")
     if epi is None:
         gbx_out, gbv_out = gbar_x_in, gbar_vec_in
+    # (the column sums as a split-K TN launch: ATen's dim-0 reduction of [N, H] took 20 us at C2)
     return gbx_out, gbv_out, vpbar, obar, gbgy, xbar, \
-        (wrows.sum(0) if (wrows is not None and outs.get("wrows") is None) else None)
+        (kernels._linear_wgrad(wrows, wrows, False, True)[1] if (wrows is not None and outs.get("wrows") is None)
+         else None)
 
 
 def adjoint_epi_ln_composite(epi, gbar_x_in, gbar_vec_in, ln, outs=None):
@@ -1150,6 +1150,9 @@ def check_pending_consumed():
     _HANDED_OFF.clear()
     for m in left:
         m.pending = None
+    if kernels.head_pending_left():
+        raise RuntimeError("torchmd-net_amd: the output head's second-order weight terms were not consumed by "
+                           "the head's backward (engine order); the parameter gradients are incomplete")
     if left:
         raise RuntimeError("torchmd-net_amd: the ET stack's second-order cotangents were not consumed by the "
                            "forward node's backward (engine order); the parameter gradients are incomplete")

@@ -9,6 +9,7 @@ force-loss training; that second-order step is expressed with composite PyTorch 
 import ctypes
 import math
 import os
+import weakref
 
 import torch
 import torch.nn.functional as F
@@ -19,6 +20,47 @@ from . import _native as nat
 # second orders written out by hand ("hand", default) or autograd over the composites ("composite":
 # the reference's double differentiation, kept for A/B checks)
 HEAD_SECOND_ORDER = os.environ.get("TMDNET_HEAD_SECOND_ORDER", "hand")
+# the head's HVP hands its weight-gradient factor rows to the forward node's backward (A/B switch)
+HEAD_HANDOFF = os.environ.get("TMDNET_HEAD_HANDOFF", "1") == "1"
+_HEAD_HANDED = []  # weakrefs of head links holding handed-off factor rows (check: head_pending_left)
+
+
+class _HeadLink:
+    """Ties a head's forward node to its force-pass node (the HVP).  In a force-matching loss backward both
+    compute weight gradients of the same 12 tensors: whichever runs first leaves its factor rows here
+    (``pending`` = (side, (rows, factors))) and returns none; the second runs ONE grouped GEMM over both
+    row sets (no engine-side sums of two gradients)."""
+    __slots__ = ("fwd", "hvp", "pending", "__weakref__")
+
+    def __init__(self, fwd, hvp):
+        self.fwd, self.hvp, self.pending = fwd, hvp, None
+
+    def other_will_run(self, side):
+        node = (self.hvp if side == "fwd" else self.fwd)()
+        return node is not None and _will_run(node)
+
+    def take(self, side):
+        """The other side's pending factor rows (and clear them), or None."""
+        p = self.pending
+        if p is None or p[0] == side:
+            return None
+        self.pending = None
+        return p[1]
+
+    def leave(self, side, factors):
+        self.pending = (side, factors)
+        _HEAD_HANDED[:] = [r for r in _HEAD_HANDED if (m := r()) is not None and m.pending is not None]
+        _HEAD_HANDED.append(weakref.ref(self))
+
+
+def head_pending_left():
+    """Number of head links whose handed-off factor rows were never consumed (and drop them)."""
+    left = [m for m in (r() for r in _HEAD_HANDED) if m is not None and m.pending is not None]
+    _HEAD_HANDED.clear()
+    for m in left:
+        m.pending = None
+    return len(left)
+
 
 # Optional live kernel timing (bench.py): when a list is installed here, the ET message forward
 # launches are bracketed by HIP events recorded on the launching stream.
@@ -184,6 +226,7 @@ class _NeighborGeom(Function):
     @staticmethod
     def forward(ctx, pos, graph, deltas, distances):
         ctx.graph = graph
+        ctx.set_materialize_grads(False)  # an unused alias stays None (no zero fill + add)
         ctx.save_for_backward(pos, deltas, distances)
         return deltas, distances, distances.view_as(distances)
 
@@ -192,6 +235,8 @@ class _NeighborGeom(Function):
         pos, deltas, distances = ctx.saved_tensors
         if g_dist is None and g_dist2 is not None:
             g_dist, g_dist2 = g_dist2, None
+        if g_deltas is None and g_dist is None:
+            return None, None, None, None
         gpos = _NeighborGeomBwd.apply(pos, g_deltas, g_dist, deltas, distances, ctx.graph, g_dist2)
         return gpos, None, None, None
 
@@ -212,13 +257,15 @@ class _NeighborGeomBwd(Function):
         nat.check(rc, "tmdnet_nl_backward_multi")
         ctx.graph = graph
         ctx.two = gr2 is not None
-        # the second order sees the summed distance gradient (both slots get its gradient)
-        ctx.save_for_backward(pos, gd, gr if gr2 is None else gr + gr2, deltas, distances)
+        # the second order sees the summed distance gradient (both slots get its gradient); summed there,
+        # so a first-order-only pass (inference forces) launches no add
+        ctx.save_for_backward(pos, gd, gr, gr2, deltas, distances)
         return gpos
 
     @staticmethod
     def backward(ctx, ggpos):
-        pos, gd, gr, deltas, distances = ctx.saved_tensors
+        pos, gd, gr, gr2, deltas, distances = ctx.saved_tensors
+        gr = _sum_opt([gr, gr2])
         d_pos, d_gd, d_gr = _NeighborGeomBwd2.apply(pos, ggpos, gd, gr, deltas, distances, ctx.graph)
         d_gr = d_gr if gr is not None else None
         return d_pos, (d_gd if gd is not None else None), d_gr, None, None, None, (d_gr if ctx.two else None)
@@ -428,6 +475,7 @@ class _EdgeGeom(Function):
         ctx.graph = graph
         ctx.cfg = (cl, cu, rbf_type, want)
         ctx.fan = fan
+        ctx.set_materialize_grads(False)  # an alias whose consumer sends no gradient stays None (no zero fill)
         ctx.save_for_backward(deltas, dist, mu, beta)
         extra = [f.view_as(f) for _ in range(fan[0] - 1)] + [C.view_as(C) for _ in range(fan[1] - 1)]
         return (f, C, u, *extra)
@@ -441,6 +489,8 @@ class _EdgeGeom(Function):
         gCs = [gC] + list(galias[kf:])
         gfs += [None] * (3 - len(gfs))
         gCs += [None] * (3 - len(gCs))
+        if all(t is None for t in gfs + gCs) and gu is None:
+            return (None,) * 11
         g_dl, g_r = _EdgeGeomBwd.apply(deltas, dist, gfs[0], gCs[0], gu, ctx.graph, mu, beta, cl, cu, rbf_type,
                                        gfs[1], gfs[2], gCs[1], gCs[2])
         return g_dl, g_r, None, None, None, None, None, None, None, None, None
@@ -485,28 +535,28 @@ class _EdgeGeomBwd(Function):
         ctx.cfg = (cl, cu, rbf_type)
         # the second order sees the summed incoming gradients (each slot's gradient is the same)
         ctx.slots = ([t is not None for t in gfl], [t is not None for t in gCl])
-        gf_ = _sum_opt(gfl)
-        gC_ = _sum_opt(gCl)
-        ctx.save_for_backward(deltas, dist, gf_, gC_, gu_, mu, beta)
+        # (summed in backward: a first-order-only pass launches no adds)
+        ctx.save_for_backward(deltas, dist, gu_, mu, beta, *gfl, *gCl)
         return g_dl, g_r
 
     @staticmethod
     def backward(ctx, gg_dl, gg_r):
-        deltas, dist, gf, gC, gu, mu, beta = ctx.saved_tensors
+        deltas, dist, gu, mu, beta, *gs = ctx.saved_tensors
+        gf, gC = _sum_opt(gs[:3]), _sum_opt(gs[3:])
         cl, cu, rbf_type = ctx.cfg
         graph = ctx.graph
         _create = torch.is_grad_enabled()  # third order only if the caller builds a graph
         if not _create and HEAD_SECOND_ORDER != "composite":
             # tmdnet_edge_geom_bwd2: only the gradients the engine will consume (a training step's
             # loss.backward(inputs=params) never reaches the positions: no d_dist / d_deltas)
+            fs, cs = ctx.slots  # every gradient slot (fan-out) takes the summed slots' gradient
             nf = iter(ctx.next_functions)
             want = []
-            for i, t in enumerate((deltas, dist, gf, gC, gu)):
-                node = next(nf)[0] if i < 2 or t is not None else None
-                want.append(t is not None and ctx.needs_input_grad[i] and _will_run(node))
-            fs, cs = ctx.slots  # extra gradient slots (fan-out) take slot 1's gradient
-            want[2] = want[2] or (gf is not None and any(fs[1:]))
-            want[3] = want[3] or (gC is not None and any(cs[1:]))
+            for i, present in enumerate((True, True, fs[0], cs[0], gu is not None)):
+                node = next(nf)[0] if present else None
+                want.append(present and ctx.needs_input_grad[i] and _will_run(node))
+            want[2] = gf is not None and (want[2] or any(fs[1:]))
+            want[3] = gC is not None and (want[3] or any(cs[1:]))
             if not any(want):
                 return (None,) * 15
             o = [torch.empty_like(t) if w else None for t, w in zip((deltas, dist, gf, gC, gu), want)]
@@ -518,7 +568,8 @@ class _EdgeGeomBwd(Function):
                 nat.ptr(None if gg_r is None else gg_r.contiguous()), nat.ptr(o[2]), nat.ptr(o[3]), nat.ptr(o[4]),
                 nat.ptr(o[1]), nat.ptr(o[0]), nat.stream(dist.device))
             nat.check(rc, "tmdnet_edge_geom_bwd2")
-            return (o[0], o[1], o[2], o[3], o[4], None, None, None, None, None, None) + _slot_grads(ctx, o[2], o[3])
+            return (o[0], o[1], o[2] if fs[0] else None, o[3] if cs[0] else None, o[4], None, None, None, None, None,
+                    None) + _slot_grads(ctx, o[2], o[3])
         selfmask = graph.src == graph.dst
         with torch.enable_grad():
             dl = deltas.detach().requires_grad_(True)
@@ -537,8 +588,9 @@ class _EdgeGeomBwd(Function):
                                          create_graph=_create, allow_unused=True)
         it = iter(second[2:])
         gups = [next(it) if u is not None else None for u in ups]
-        return (second[0], second[1], gups[0], gups[1], gups[2], None, None, None, None, None, None) + \
-            _slot_grads(ctx, gups[0], gups[1])
+        fs, cs = ctx.slots
+        return (second[0], second[1], gups[0] if fs[0] else None, gups[1] if cs[0] else None, gups[2], None, None,
+                None, None, None, None) + _slot_grads(ctx, gups[0], gups[1])
 
 
 def rbf_deriv_launch(r, mu, beta, cl, cu, rbf_type, rows, out):
@@ -1859,24 +1911,47 @@ class _EqHead(Function):
         nf = ctx.next_functions
         off = len(nf) - len(params)
         need_w = any(_will_run(nf[off + i][0]) for i in range(len(params)))
-        outs = _EqHeadBwd.apply(need_w, gy.contiguous(), jx, jv, x, vec, *params)
+        # a force-matching loss backward reaches the head twice (here and its force pass's HVP): see _HeadLink
+        # (the HVP takes part only in its hand-written form: no third order, not the composite switch)
+        hand_ok = need_w and HEAD_HANDOFF and not torch.is_grad_enabled() and HEAD_SECOND_ORDER != "composite"
+        link = getattr(ctx, "link", None) if hand_ok else None
+        seg2 = link.take("fwd") if link is not None else None
+        stash = link if (link is not None and seg2 is None and link.other_will_run("fwd")) else None
+        outs = _EqHeadBwd.apply((need_w, seg2, stash), gy.contiguous(), jx, jv, x, vec, *params)
+        if outs[0].grad_fn is not None:  # (create_graph: the force pass)
+            link = _HeadLink(weakref.ref(ctx), weakref.ref(outs[0].grad_fn))
+            ctx.link = link
+            outs[0].grad_fn.link = link
         return outs
 
 
-def _head_wgrads(n, H, a1, vv, gu, hext, go, sext, a2, v1, gu2, h2ext, go2, s2ext):
-    """The head's six weight-gradient GEMMs over the n per-atom factor rows, in one grouped launch."""
+def _head_factor_ops(n, H, a1, vv, gu, hext, go, sext, a2, v1, gu2, h2ext, go2, s2ext):
     O = Q = H // 2
+    return [(a1.view(3 * n, H + O), vv.reshape(3 * n, H)), (gu, hext), (go, sext),
+            (a2.view(3 * n, Q + 1), v1.view(3 * n, O)), (gu2, h2ext), (go2, s2ext)]
+
+
+def _head_wgrads(n, H, *factors, seg2=None):
+    """The head's six weight-gradient GEMMs over the n per-atom factor rows, in one grouped launch;
+    ``seg2`` = (n2, factors2): a second set of factor rows summed by the same GEMMs (the other pass's)."""
+    O = Q = H // 2
+    a1 = factors[0]
     o = dict(dtype=a1.dtype, device=a1.device)
     outs = [torch.empty((H + O, H), **o), torch.empty((H, 2 * H + 1), **o), torch.empty((2 * O, H + 1), **o),
             torch.empty((Q + 1, O), **o), torch.empty((Q, 2 * Q + 1), **o), torch.empty((2, Q + 1), **o)]
-    ops = [(a1.view(3 * n, H + O), vv.reshape(3 * n, H)), (gu, hext), (go, sext),
-           (a2.view(3 * n, Q + 1), v1.view(3 * n, O)), (gu2, h2ext), (go2, s2ext)]
-    wgrad_tn([{"A": A, "B": B, "C": C} for (A, B), C in zip(ops, outs)])
+    ops = _head_factor_ops(n, H, *factors)
+    probs = [{"A": A, "B": B, "C": C} for (A, B), C in zip(ops, outs)]
+    if seg2 is not None:
+        for p, (A2, B2) in zip(probs, _head_factor_ops(seg2[0], H, *seg2[1])):
+            p.update(A2=A2, B2=B2)
+    wgrad_tn(probs)
     return outs
 
 
-def _eq_head_weight_grads(lib, x, vec, params, gy, gx, gv):
-    """tmdnet_eq_head_bwd_weights (g_x, g_vec and the per-atom factors) + one GEMM per weight pair."""
+def _eq_head_weight_grads(lib, x, vec, params, gy, gx, gv, seg2=None, stash=None):
+    """tmdnet_eq_head_bwd_weights (g_x, g_vec and the per-atom factors) + one GEMM per weight pair
+    (``seg2``: the HVP's factor rows, summed by the same GEMMs; ``stash``: a _HeadLink to leave this
+    pass's factor rows at instead -- returns None)."""
     N, H = x.shape
     O = Q = H // 2
     o = dict(dtype=x.dtype, device=x.device)
@@ -1897,8 +1972,11 @@ def _eq_head_weight_grads(lib, x, vec, params, gy, gx, gv):
     rc = lib.tmdnet_eq_head_bwd_weights(nat.dtype_code(x.dtype), N, H, nat.ptr(x), nat.ptr(vec), ws,
                                         nat.ptr(gy), nat.ptr(gx), nat.ptr(gv), sv, nat.stream(x.device))
     nat.check(rc, "tmdnet_eq_head_bwd_weights")
+    if stash is not None:
+        stash.leave("fwd", (N, (a1, vec, gu, hext, go, sext, a2, v1, gu2, h2ext, go2, s2ext)))
+        return None
     dw12, du1, du2, dv12, dp1, dp2 = _head_wgrads(N, H, a1, vec, gu, hext, go, sext, a2, v1, gu2, h2ext, go2,
-                                                  s2ext)
+                                                  s2ext, seg2=seg2)
     return [dw12[:H], dw12[H:], du1[:, :2 * H], du1[:, 2 * H], du2[:, :H], du2[:, H],
             dv12[:Q], dv12[Q:], dp1[:, :2 * Q], dp1[:, 2 * Q], dp2[:, :Q], dp2[:, Q]]
 
@@ -1908,14 +1986,16 @@ class _EqHeadBwd(Function):
     (training only) and every second-order term come from the composite."""
 
     @staticmethod
-    def forward(ctx, need_w, gy, jx, jv, x, vec, *params):
+    def forward(ctx, opts, gy, jx, jv, x, vec, *params):
+        need_w, seg2, stash = opts
         lib = nat.load()
         N, H = x.shape
         gx = torch.empty_like(x)
         gv = torch.empty_like(vec)
         g_params = [None] * len(params)
         if need_w:
-            g_params = _eq_head_weight_grads(lib, x, vec, params, gy, gx, gv)
+            g_params = _eq_head_weight_grads(lib, x, vec, params, gy, gx, gv, seg2=seg2, stash=stash)
+            g_params = [None] * len(params) if g_params is None else g_params
         else:
             if jx is None:
                 raise RuntimeError("torchmd-net_amd: head Jacobian was not computed in the forward")
@@ -1933,7 +2013,16 @@ class _EqHeadBwd(Function):
         if not _create and all(g is None for g in ggp) and HEAD_SECOND_ORDER != "composite":
             gy, x, vec, *params = saved
             need_p = [ctx.needs_input_grad[6 + i] for i in range(len(params))]
-            d_gy, d_x, d_vec, d_p = eq_head_hvp(x, vec, params, gy, ggx, ggv, ctx.needs_input_grad[1], any(need_p))
+            # the head's forward node also computes weight gradients in this pass (the energy loss): one
+            # grouped GEMM for both (_HeadLink)
+            link = getattr(ctx, "link", None) if (any(need_p) and HEAD_HANDOFF) else None
+            seg2 = link.take("hvp") if link is not None else None
+            hand = link is not None and seg2 is None and link.other_will_run("hvp")
+            d_gy, d_x, d_vec, d_p = eq_head_hvp(x, vec, params, gy, ggx, ggv, ctx.needs_input_grad[1], any(need_p),
+                                                factors_only=hand, seg2=seg2)
+            if hand:
+                link.leave("hvp", d_p)
+                d_p = None
             d_p = [g if w else None for g, w in zip(d_p, need_p)] if d_p is not None else [None] * len(params)
             return (None, d_gy, None, None, d_x, d_vec) + tuple(d_p)
         with torch.enable_grad():
@@ -1951,11 +2040,13 @@ class _EqHeadBwd(Function):
         return (None, d_gy, None, None, d_x, d_vec) + tuple(second[3:])
 
 
-def eq_head_hvp(x, vec, params, gy, tx, tv, want_gy=True, want_w=True):
+def eq_head_hvp(x, vec, params, gy, tx, tv, want_gy=True, want_w=True, factors_only=False, seg2=None):
     """Second order of the head's backward (tmdnet_eq_head_hvp, forward-over-reverse in one kernel):
     returns (d_gy [N,1] or None, d_x, d_vec, [12 weight terms] or None) for the cotangents (tx, tv)
     of (g_x, g_vec) = gy * J(x, vec); each weight term is one GEMM over the kernel's per-atom
-    factors ([tangent rows ; plain rows], the layouts of _eq_head_weight_grads)."""
+    factors ([tangent rows ; plain rows], the layouts of _eq_head_weight_grads).  ``factors_only``:
+    the fourth item is (2N, factor rows) for _head_wgrads' seg2 instead of the weight terms; ``seg2``:
+    the first-order pass's factor rows, summed by the same GEMMs."""
     lib = nat.load()
     N, H = x.shape
     O = Q = H // 2
@@ -1982,8 +2073,10 @@ def eq_head_hvp(x, vec, params, gy, tx, tv, want_gy=True, want_w=True):
     if saves is None:
         return d_gy, d_x, d_vec, None
     a1, gu, hext, go, sext, a2, v1, gu2, h2ext, go2, s2ext, vv = saves
+    if factors_only:
+        return d_gy, d_x, d_vec, (2 * N, (a1, vv, gu, hext, go, sext, a2, v1, gu2, h2ext, go2, s2ext))
     dw12, du1, du2, dv12, dp1, dp2 = _head_wgrads(2 * N, H, a1, vv, gu, hext, go, sext, a2, v1, gu2, h2ext, go2,
-                                                  s2ext)
+                                                  s2ext, seg2=seg2)
     d_p = [dw12[:H], dw12[H:], du1[:, :2 * H], du1[:, 2 * H], du2[:, :H], du2[:, H],
            dv12[:Q], dv12[Q:], dp1[:, :2 * Q], dp1[:, 2 * Q], dp2[:, :Q], dp2[:, Q]]
     return d_gy, d_x, d_vec, d_p
@@ -2370,6 +2463,24 @@ class _LayerNorm(Function):
             return None, None, None, None
         gx, gw, gb = _LayerNormBwd.apply(gy.contiguous(), x, w, b, mean, rstd, ctx.eps, need)
         return gx, gw, gb, None
+
+
+def layer_norm_wgrad(gy, x, mean, rstd):
+    """(g_weight, g_bias) = (sum_rows gy * xhat, sum_rows gy) of a LayerNorm over x's rows (xhat =
+    (x - mean) rstd): tmdnet_layernorm_wgrad_f32 (deterministic two-pass column sums) for fp32 CUDA rows."""
+    rows, C = x.shape
+    if x.is_cuda and x.dtype == torch.float32 and C <= 1024 and x.stride(1) == 1 and gy.stride(1) == 1:
+        lib = nat.load()
+        gw, gb = torch.empty(C, dtype=x.dtype, device=x.device), torch.empty(C, dtype=x.dtype, device=x.device)
+        wsb = int(lib.tmdnet_layernorm_wgrad_workspace_bytes(rows, C))
+        ws = torch.empty(max(1, wsb // 4), dtype=torch.float32, device=x.device)
+        rc = lib.tmdnet_layernorm_wgrad_f32(rows, C, nat.ptr(x), x.stride(0), nat.ptr(mean.contiguous()),
+                                            nat.ptr(rstd.contiguous()), nat.ptr(gy), gy.stride(0), nat.ptr(gw),
+                                            nat.ptr(gb), nat.ptr(ws), wsb, nat.stream(x.device))
+        nat.check(rc, "tmdnet_layernorm_wgrad_f32")
+        return gw, gb
+    xhat = (x - mean.reshape(rows, 1)) * rstd.reshape(rows, 1)
+    return (gy * xhat).sum(0), gy.sum(0)
 
 
 class _LayerNormBwd(Function):

@@ -97,6 +97,18 @@ def _adamw(params, lr, weight_decay):
     return torch.optim.AdamW(params, lr=lr, weight_decay=weight_decay, fused=dev.type == "cuda")
 
 
+def _copy_grads(pairs):
+    """Copy (flat-buffer view, gradient) pairs: ONE multi-tensor launch for the contiguous gradients (a
+    single strided one, e.g. a column block of a weight-gradient GEMM's output, would send the whole
+    list down the per-tensor path: one copy launch each), the strided ones one by one."""
+    fast = [(v, g) for v, g in pairs if g.is_contiguous()]
+    if fast:
+        torch._foreach_copy_([v for v, _ in fast], [g for _, g in fast])
+    for v, g in pairs:
+        if not g.is_contiguous():
+            v.copy_(g)
+
+
 class LNNPStep:
     """One optimisation step of the reference training objective on a batch of molecules."""
 
@@ -208,12 +220,15 @@ class GraphedTrainStep(LNNPStep):
         self.opt.zero_grad(set_to_none=True)
         params = self.reduce.params
         self.reduce.flat.zero_()
+        # the backward's seed: allocated outside the graph and kept alive with it (its replays read it)
+        self._seed = seed = torch.ones((), dtype=params[0].dtype, device=dev)
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
             self.static_loss = self.loss(self.z, self.pos, self.batch, self.y, self.neg_dy)
-            grads = torch.autograd.grad(self.static_loss, params, allow_unused=True)
+            grads = torch.autograd.grad(self.static_loss, params, grad_outputs=seed.expand_as(self.static_loss),
+                                        allow_unused=True)
             pairs = [(v, g) for v, g in zip(self.reduce.views, grads) if g is not None]
-            torch._foreach_copy_([v for v, _ in pairs], [g for _, g in pairs])
+            _copy_grads(pairs)
             ov = rep.distance.last_overflow
             self.reduce.flag.copy_(ov.num.reshape(1) > ov.capacity)
         torch.cuda.synchronize(dev)
@@ -374,13 +389,15 @@ class _BucketStep:
                 torch.autograd.grad(loss_fn()[2], params, allow_unused=True)
         torch.cuda.current_stream(dev).wait_stream(s)
         torch.cuda.synchronize(dev)
+        # the backward's seed: allocated outside the graph and kept alive with it (its replays read it)
+        self._seed = seed = torch.ones((), dtype=params[0].dtype, device=dev)
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
             self.ly, self.lf, total = loss_fn()
-            grads = torch.autograd.grad(total, params, allow_unused=True)
+            grads = torch.autograd.grad(total, params, grad_outputs=seed.expand_as(total), allow_unused=True)
             pairs = [(v, gr) for v, gr in zip(views, grads) if gr is not None]
             zero = [v for v, gr in zip(views, grads) if gr is None]
-            torch._foreach_copy_([v for v, _ in pairs], [gr for _, gr in pairs])
+            _copy_grads(pairs)
             if zero:
                 torch._foreach_zero_(zero)
             ov = rep.distance.last_overflow
