@@ -971,6 +971,7 @@ static bool tn_vec_ok(const gemm::GroupTN& G) {
   auto al = [](const void* p, int ld) { return !p || ((((uintptr_t)p) & 15) == 0 && ld % 4 == 0); };
   for (int i = 0; i < G.n; ++i) {
     const gemm::ProbTN& P = G.p[i];
+    if (P.Cb && !(P.ones1 || P.ones2)) return false;  // a read column N-1 redirected to Cb: the 32-tile kernel
     if (!(P.onehot || al(P.A, P.lda)) || !al(P.B, P.ldb)) return false;
     if (P.K2 > 0 && (!al(P.A2, P.lda2) || !al(P.B2, P.ldb2))) return false;
   }
@@ -1109,7 +1110,6 @@ static int tn_group(int n_problems, const int* dims, const void* const* ptrs, in
     P.A = (const float*)q[0]; P.B = (const float*)q[1];
     P.A2 = (const float*)q[2]; P.B2 = (const float*)q[3]; P.C = (float*)q[4];
     P.Cb = np > 5 ? (float*)q[5] : nullptr;
-    if (P.Cb && !(P.ones1 || P.ones2)) return kBadArgument;
     if (P.M <= 0 || P.N <= 0 || P.K < 0 || P.K2 < 0 || !P.C || P.ldc < P.N - (P.Cb ? 1 : 0)) return kBadArgument;
     if ((P.K > 0 && (!P.A || (!P.B && !(P.ones1 && P.N == 1)) || P.lda < P.M)) ||
         (P.K2 > 0 && (!P.A2 || (!P.B2 && !(P.ones2 && P.N == 1)) || P.lda2 < P.M)))

@@ -1933,19 +1933,25 @@ def _head_factor_ops(n, H, a1, vv, gu, hext, go, sext, a2, v1, gu2, h2ext, go2, 
 
 def _head_wgrads(n, H, *factors, seg2=None):
     """The head's six weight-gradient GEMMs over the n per-atom factor rows, in one grouped launch;
-    ``seg2`` = (n2, factors2): a second set of factor rows summed by the same GEMMs (the other pass's)."""
+    ``seg2`` = (n2, factors2): a second set of factor rows summed by the same GEMMs (the other pass's).
+    Returns the 12 parameter gradients, each contiguous (a bias is its factor's last column, written to
+    its own vector: no strided column blocks for the training step's gradient copy)."""
     O = Q = H // 2
     a1 = factors[0]
     o = dict(dtype=a1.dtype, device=a1.device)
-    outs = [torch.empty((H + O, H), **o), torch.empty((H, 2 * H + 1), **o), torch.empty((2 * O, H + 1), **o),
-            torch.empty((Q + 1, O), **o), torch.empty((Q, 2 * Q + 1), **o), torch.empty((2, Q + 1), **o)]
+    e = lambda *shape: torch.empty(shape, **o)  # noqa: E731
+    w12, v12 = e(H + O, H), e(Q + 1, O)
+    u1, u1b, u2, u2b = e(H, 2 * H), e(H), e(2 * O, H), e(2 * O)
+    p1, p1b, p2, p2b = e(Q, 2 * Q), e(Q), e(2, Q), e(2)
+    outs = [(w12, None), (u1, u1b), (u2, u2b), (v12, None), (p1, p1b), (p2, p2b)]
     ops = _head_factor_ops(n, H, *factors)
-    probs = [{"A": A, "B": B, "C": C} for (A, B), C in zip(ops, outs)]
+    probs = [{"A": A, "B": B, "C": C} if Cb is None else {"A": A, "B": B, "C": C, "Cb": Cb}
+             for (A, B), (C, Cb) in zip(ops, outs)]
     if seg2 is not None:
         for p, (A2, B2) in zip(probs, _head_factor_ops(seg2[0], H, *seg2[1])):
             p.update(A2=A2, B2=B2)
     wgrad_tn(probs)
-    return outs
+    return [w12[:H], w12[H:], u1, u1b, u2, u2b, v12[:Q], v12[Q:], p1, p1b, p2, p2b]
 
 
 def _eq_head_weight_grads(lib, x, vec, params, gy, gx, gv, seg2=None, stash=None):
@@ -1975,10 +1981,7 @@ def _eq_head_weight_grads(lib, x, vec, params, gy, gx, gv, seg2=None, stash=None
     if stash is not None:
         stash.leave("fwd", (N, (a1, vec, gu, hext, go, sext, a2, v1, gu2, h2ext, go2, s2ext)))
         return None
-    dw12, du1, du2, dv12, dp1, dp2 = _head_wgrads(N, H, a1, vec, gu, hext, go, sext, a2, v1, gu2, h2ext, go2,
-                                                  s2ext, seg2=seg2)
-    return [dw12[:H], dw12[H:], du1[:, :2 * H], du1[:, 2 * H], du2[:, :H], du2[:, H],
-            dv12[:Q], dv12[Q:], dp1[:, :2 * Q], dp1[:, 2 * Q], dp2[:, :Q], dp2[:, Q]]
+    return _head_wgrads(N, H, a1, vec, gu, hext, go, sext, a2, v1, gu2, h2ext, go2, s2ext, seg2=seg2)
 
 
 class _EqHeadBwd(Function):
@@ -2075,10 +2078,7 @@ def eq_head_hvp(x, vec, params, gy, tx, tv, want_gy=True, want_w=True, factors_o
     a1, gu, hext, go, sext, a2, v1, gu2, h2ext, go2, s2ext, vv = saves
     if factors_only:
         return d_gy, d_x, d_vec, (2 * N, (a1, vv, gu, hext, go, sext, a2, v1, gu2, h2ext, go2, s2ext))
-    dw12, du1, du2, dv12, dp1, dp2 = _head_wgrads(2 * N, H, a1, vv, gu, hext, go, sext, a2, v1, gu2, h2ext, go2,
-                                                  s2ext, seg2=seg2)
-    d_p = [dw12[:H], dw12[H:], du1[:, :2 * H], du1[:, 2 * H], du2[:, :H], du2[:, H],
-           dv12[:Q], dv12[Q:], dp1[:, :2 * Q], dp1[:, 2 * Q], dp2[:, :Q], dp2[:, Q]]
+    d_p = _head_wgrads(2 * N, H, a1, vv, gu, hext, go, sext, a2, v1, gu2, h2ext, go2, s2ext, seg2=seg2)
     return d_gy, d_x, d_vec, d_p
 
 
