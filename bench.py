@@ -291,14 +291,14 @@ def et_bwd_bytes(E, N, P, H, dr, s=4):
     return b
 
 
-PROBE_KERNEL = "k_fwd<float, 4, 1, 1, false, false>"
+PROBE_KERNEL = "k_fwd<float, 4, 4, 1, false, false>"  # (4 waves per node at every size since r04)
 # the model runs large graphs with planar v / dv rows (et_stack.PLANAR_MIN_EDGES): probe that layout
 PROBE_FLAGS = 4  # TMDNET_ET_V_PLANAR
 
 
 PMC_PASSES = ("FETCH_SIZE", "WRITE_SIZE", "TCC_HIT_sum TCC_MISS_sum")
 # the child's dispatch sequence (main(), --pmc-child): probe kernel name -> [(tag, count), ...] in order
-PMC_CHILD = {"et::k_fwd<float, 4, 1, 1, false, false>": [("per_edge", 8), ("pairs", 8)],
+PMC_CHILD = {"et::k_fwd<float, 4, 4, 1, false, false>": [("per_edge", 8), ("pairs", 8)],
              "et::k_bwd_dst<": [("bwd_dst", 4)], "et::k_bwd_src<": [("bwd_src", 4)], "et::k_bwd_merged<": [("bwd_dr", 4)],
              "fep::k_fwd<": [("fused_fwd", 8)], "fep::k_bwd_dst<": [("fused_bwd_dst", 4)],
              "fep::k_bwd_src<": [("fused_bwd_src", 4)], "fep::k_edge_combine": [("fused_edge_combine", 4)]}
@@ -388,7 +388,7 @@ def roofline_probe(a, dev):
     ms = a0.elapsed_time(b0) / reps
     nbytes = et_algorithmic_bytes(E, n_atoms, H)
     gbs = nbytes / (ms * 1e-3) / 1e9
-    per_edge = {"kernel": "tmdnet_et_message_fwd (k_fwd<float,4,1,1,false>), one dk/dv row per edge",
+    per_edge = {"kernel": "tmdnet_et_message_fwd (k_fwd<float,4,4,1,false,false>), one dk/dv row per edge",
                 "bytes_per_launch": nbytes, "bytes_formula": "SURVEY.md 8(d): E*2068 + N*6148 (H=128)",
                 "ms_per_launch": round(ms, 4), "achieved": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
                 "launches": reps}
@@ -405,7 +405,7 @@ def roofline_probe(a, dev):
     ms_p = a0.elapsed_time(b0) / reps
     pbytes = et_pair_bytes(E, n_atoms, launch.n_pairs, H)
     gbp = pbytes / (ms_p * 1e-3) / 1e9
-    res = {"kernel": "tmdnet_et_message_fwd (k_fwd<float,4,1,1,false>) in the model's layout: pair-shared "
+    res = {"kernel": "tmdnet_et_message_fwd (k_fwd<float,4,4,1,false,false>) in the model's layout: pair-shared "
                      "dk/dv rows (et_stack.PAIR_ROWS, planar v rows)",
            "workload": f"periodic water box, {n_atoms} atoms (Morton-renumbered as the model does), "
                        f"L={L:.1f} A, cutoff 5, E={E}, P={launch.n_pairs} pair rows, H={H}, fp32",

@@ -171,7 +171,7 @@ _TN_NARROW = [(5210, 4096, 32, True, 10420), (5000, 70, 20, True, 900), (678, 12
               (37, 100, 31, False, 5), (12548, 96, 32, False, 0), (3, 4, 8, True, 0)]
 
 
-@pytest.mark.parametrize("form", ["1", "2"])  # TMDNET_TN_V: the unpipelined kernel / the pipelined one
+@pytest.mark.parametrize("form", ["1", "2", "4"])  # TMDNET_TN_V: 64-tile, pipelined, bf16x3-split kernels
 @pytest.mark.parametrize("shapes", ["wide", "narrow"])
 @pytest.mark.parametrize("use_cb", [False, True])
 def test_weight_gradient_tn_gemm_16byte_kernel(monkeypatch, use_cb, shapes, form):

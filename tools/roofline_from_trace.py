@@ -13,7 +13,7 @@ import sys
 path = sys.argv[1]
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 50
 warm = int(sys.argv[3]) if len(sys.argv) > 3 else 5
-name = sys.argv[4] if len(sys.argv) > 4 else "k_fwd<float, 4, 1, 1, false, false>"
+name = sys.argv[4] if len(sys.argv) > 4 else "k_fwd<float, 4, 4, 1, false, false>"
 rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
 runs, cur = [], []
 for r in rows:

@@ -815,6 +815,178 @@ __global__ __launch_bounds__(256) void k_proj_x3(Args P) {
 
 }  // namespace proj
 
+// ---------------------------------------------------------------------------------------------------
+// The grouped TN GEMM (C (+)= A^T B [+ A2^T B2], bias = column sums of A) on the bf16 MFMA at fp32
+// accuracy (A/B switch TMDNET_TN_V=4): every operand value is split EXACTLY into three bf16 pieces
+// (proj::split3) and the six products with i + j <= 2 are accumulated in fp32, as tmdnet_proj_f32 does
+// -- 6 bf16 MFMAs per 16 x 16 x 32 block = 2.7x the fp32 MFMA's rate.  Both operands arrive k-major
+// (row k holds every m / n) while an MFMA fragment is 8 consecutive k of one m / n, so each 32-row step
+// goes through LDS: coalesced float4 loads, split in registers, written transposed into three bf16
+// planes per operand; the four waves (2 x 2 over the 64 x 64 tile) read 16-byte fragments.  The next
+// step's rows are loaded before the current step's MFMAs.  Tile numbering, split-K partial layout and
+// epilogue are k_gemm_tn_v's (k_tn_reduce_v sums the partials).  Not for one-hot A (the v kernel).
+namespace tnx3 {
+
+using gemm::GroupTN;
+using gemm::ProbTN;
+using gemm::TV;
+using gemm::TV_PART;
+using bf8 = __bf16 __attribute__((ext_vector_type(8)));
+using f4 = float __attribute__((ext_vector_type(4)));
+constexpr int KB = 32, LDK = KB + 8;  // rows per step; LDS pitch (bf16) of a transposed row
+
+__global__ __launch_bounds__(256) void k_gemm_tn_x3(GroupTN G) {
+  __shared__ __attribute__((aligned(16))) unsigned short la[3][TV][LDK];
+  __shared__ __attribute__((aligned(16))) unsigned short lb[3][TV][LDK];
+  __shared__ float rsum[16][TV];
+  const int tg = blockIdx.x / G.S, sk = blockIdx.x % G.S;
+  int pi = 0;
+  for (int i = 1; i < G.n; ++i)
+    if (tg >= G.p[i].tile0) pi = i;
+  const ProbTN& P = G.p[pi];
+  const int t = tg - P.tile0;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int m0 = (t / P.tiles_n) * TV, n0 = (t % P.tiles_n) * TV;
+  const bool anyones = P.ones1 || P.ones2;
+  const int Nr = anyones ? P.N - 1 : P.N;
+  const bool do_bias = anyones && (t % P.tiles_n) == 0;
+  const bool gemm = n0 < Nr;
+  const int KT = P.K + P.K2;
+  const int nks = (KT + KB - 1) / KB, cper = (nks + G.S - 1) / G.S;
+  const int c_lo = min(KT, sk * cper * KB), c_hi = min(KT, (sk + 1) * cper * KB);
+  // this thread's two float4 of each 32 x 64 operand tile: row kr[j], columns q4 .. q4 + 3
+  const int q4 = (tid & 15) * 4, kr0 = tid >> 4;  // rows kr0 and kr0 + 16
+  const int ma = m0 + q4, na = n0 + q4;
+  const bool mfull = ma + 3 < P.M, nfull = na + 3 < Nr;
+  f4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  f4 rs = f4{0.f, 0.f, 0.f, 0.f};
+  for (int seg = 0; seg < 2; ++seg) {
+    const int s0 = seg ? P.K : 0, s1 = seg ? KT : P.K;
+    const int lo = max(c_lo, s0), hi = min(c_hi, s1);
+    if (lo >= hi) continue;
+    const float* A = seg ? P.A2 : P.A;
+    const float* B = seg ? P.B2 : P.B;
+    const int lda = seg ? P.lda2 : P.lda, ldb = seg ? P.ldb2 : P.ldb;
+    const bool bias_seg = do_bias && (seg ? P.ones2 : P.ones1);
+    auto load = [&](int kb, f4 (&a)[2], f4 (&b)[2]) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int k = kb + kr0 + 16 * j;
+        const bool kv = k < hi;
+        const size_t ro = (size_t)(kv ? k - s0 : 0);
+        if (kv && mfull) {
+          a[j] = *reinterpret_cast<const f4*>(A + ro * lda + ma);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) a[j][i] = (kv && ma + i < P.M) ? A[ro * lda + ma + i] : 0.f;
+        }
+        if (!gemm || !B) {
+          b[j] = f4{0.f, 0.f, 0.f, 0.f};
+        } else if (kv && nfull) {
+          b[j] = *reinterpret_cast<const f4*>(B + ro * ldb + na);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) b[j][i] = (kv && na + i < Nr) ? B[ro * ldb + na + i] : 0.f;
+        }
+      }
+    };
+    // split into the three pieces and store transposed: plane[p][column][row]
+    auto stage = [&](const f4 (&a)[2], const f4 (&b)[2]) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int kr = kr0 + 16 * j;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          unsigned h, m, l;
+          proj::split3(a[j][i], h, m, l);
+          la[0][q4 + i][kr] = (unsigned short)(h >> 16);
+          la[1][q4 + i][kr] = (unsigned short)(m >> 16);
+          la[2][q4 + i][kr] = (unsigned short)(l >> 16);
+          proj::split3(b[j][i], h, m, l);
+          lb[0][q4 + i][kr] = (unsigned short)(h >> 16);
+          lb[1][q4 + i][kr] = (unsigned short)(m >> 16);
+          lb[2][q4 + i][kr] = (unsigned short)(l >> 16);
+        }
+      }
+    };
+    f4 a[2], b[2];
+    load(lo, a, b);
+    for (int kb = lo; kb < hi; kb += KB) {
+      if (bias_seg) rs += a[0] + a[1];
+      __syncthreads();  // the previous step's fragments are read
+      stage(a, b);
+      __syncthreads();
+      if (kb + KB < hi) load(kb + KB, a, b);  // next rows in flight during the MFMAs
+      if (gemm) {
+        bf8 fa[2][3], fb[2][3];
+        const int ko = 8 * (lane >> 4);
+#pragma unroll
+        for (int x = 0; x < 2; ++x)
+#pragma unroll
+          for (int p = 0; p < 3; ++p) {
+            fa[x][p] = *reinterpret_cast<const bf8*>(&la[p][32 * wm + 16 * x + (lane & 15)][ko]);
+            fb[x][p] = *reinterpret_cast<const bf8*>(&lb[p][32 * wn + 16 * x + (lane & 15)][ko]);
+          }
+        constexpr int TA[6] = {2, 1, 0, 1, 0, 0}, TB[6] = {0, 1, 2, 0, 1, 0};  // small terms first
+#pragma unroll
+        for (int q = 0; q < 6; ++q)
+#pragma unroll
+          for (int x = 0; x < 2; ++x)
+#pragma unroll
+            for (int y = 0; y < 2; ++y)
+              acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[x][TA[q]], fb[y][TB[q]], acc[x][y], 0, 0, 0);
+      }
+    }
+  }
+  float* part = G.S > 1 ? G.part + ((size_t)tg * G.S + sk) * TV_PART : nullptr;
+  if (gemm) {  // lane holds C[m = 4 (lane >> 4) + i][n = lane & 15] of each 16 x 16 block
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int y = 0; y < 2; ++y)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = 32 * wm + 16 * x + 4 * (lane >> 4) + i, c = 32 * wn + 16 * y + (lane & 15);
+          const float v = acc[x][y][i];
+          if (part) {
+            part[r * TV + c] = v;
+            continue;
+          }
+          const int m = m0 + r, n = n0 + c;
+          if (m >= P.M || n >= Nr) continue;
+          float* out = P.C + (size_t)m * P.ldc + n;
+          *out = P.beta ? *out + v : v;
+        }
+  } else if (part) {  // a bias-only tile: its partial's GEMM block is zero
+    for (int e = tid; e < TV * TV; e += 256) part[e] = 0.f;
+  }
+  if (do_bias) {  // column sums of A: the 16 row lanes of each column quad, in order
+    *reinterpret_cast<f4*>(&rsum[kr0][q4]) = rs;
+    __syncthreads();
+    if (tid < TV) {
+      float v = 0.f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) v += rsum[i][tid];
+      if (part) {
+        part[TV * TV + tid] = v;
+      } else {
+        const int m = m0 + tid;
+        if (m < P.M) {
+          float* out = P.Cb ? P.Cb + m : P.C + (size_t)m * P.ldc + (P.N - 1);
+          *out = P.beta ? *out + v : v;
+        }
+      }
+    }
+  }
+}
+
+}  // namespace tnx3
+
 namespace emb {
 constexpr int MAX_TABLES = 4;
 struct Tables {
@@ -1006,7 +1178,11 @@ static void launch_tn(gemm::GroupTN& G, int tiles, int kmax, float* ws, hipStrea
     // (the pipelined form at 2 waves per SIMD: 289 vs 210 us on the dk/dv weight gradient, 4096 x 64)
     const char* fe = getenv("TMDNET_TN_V");
     const int form = fe ? atoi(fe) : (narrow ? 2 : 1);
-    if (form == 2 || form == 3) {
+    bool onehot = false;
+    for (int i = 0; i < G.n; ++i) onehot = onehot || G.p[i].onehot;
+    if (form == 4 && !onehot) {
+      hipLaunchKernelGGL(tnx3::k_gemm_tn_x3, dim3(tv * G.S), dim3(256), 0, st, G);
+    } else if (form == 2 || form == 3) {
       const bool pipe = form == 2;
       if (kmax >= 8192 && G.S == 1) {
         if (narrow) hipLaunchKernelGGL((gemm::k_gemm_tn_v2<8, 2, true>), dim3(tv), dim3(512), 0, st, G);
