@@ -825,6 +825,10 @@ __global__ __launch_bounds__(256) void k_proj_x3(Args P) {
 // planes per operand; the four waves (2 x 2 over the 64 x 64 tile) read 16-byte fragments.  The next
 // step's rows are loaded before the current step's MFMAs.  Tile numbering, split-K partial layout and
 // epilogue are k_gemm_tn_v's (k_tn_reduce_v sums the partials).  Not for one-hot A (the v kernel).
+// Measured (tools/tn_time.py, C2 training shapes): SLOWER than the fp32-MFMA k_gemm_tn_v -- dk/dv 4096 x 64
+// over 6.6k + 13.2k rows 264 vs 142 us, node weights 259 vs 147 us: the transposed 2-byte LDS stores, the
+// in-register splits and two barriers per 32-row step cost more than the MFMA time they save at these
+// 64-wide outputs.  Kept as the A/B form; the default stays k_gemm_tn_v.
 namespace tnx3 {
 
 using gemm::GroupTN;
