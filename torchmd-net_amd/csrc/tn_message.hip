@@ -21,6 +21,8 @@
 // turns every (-1,-1) padding slot of the CUDA neighbour list into an extra (0,0) edge with r = 0
 // (tensornet.py:215-221), i.e. (max_num_pairs - num_pairs) more copies of that self loop.
 // Backward = destination pass (own outputs + per-edge grads) + source pass (gathered inputs' grads).
+#include <cstdlib>
+
 #include "common.h"
 #include "tmdnet.h"
 #include "tn_node.h"
@@ -75,10 +77,35 @@ __device__ __forceinline__ void zero_tail_rows(const Args<T>& A, T* p, int w) {
   for (long long i = tid; i < cnt; i += nth) p[(size_t)e0 * w + i] = T(0);
 }
 
-__device__ __forceinline__ void wave_node(int nblk, int& node, int& ch0) {
-  const int w = blockIdx.x * (blockDim.x / TMD_WAVE) + threadIdx.x / TMD_WAVE;
-  node = w / nblk;
-  ch0 = (w % nblk) * TMD_WAVE;
+// One workgroup of S waves per (node, 64-channel block): the node's edges are dealt round-robin to the
+// S waves (edge b + w, b + w + S, ...), whose partial sums are then folded in wave order through LDS
+// (deterministic).  With one wave walking a node's ~20 edges serially, each edge costing a dependent
+// src -> row gather, these kernels were latency chains: 11-36 us per launch at C3 (168 atoms).
+template <int S> __device__ __forceinline__ void slot_node(int nblk, int& node, int& ch0, int& w) {
+  node = blockIdx.x / nblk;
+  ch0 = (blockIdx.x % nblk) * TMD_WAVE;
+  w = threadIdx.x / TMD_WAVE;
+}
+
+// acc (K values per lane) summed over the block's S waves, wave 0 last-to-hold the total; red: S-1 x K x 64
+template <typename T, int K, int S>
+__device__ __forceinline__ bool fold_waves(T (&acc)[K], T* red) {
+  if constexpr (S == 1) {
+    return true;
+  } else {
+    const int w = threadIdx.x / TMD_WAVE, lane = lane_id();
+    if (w > 0) {
+#pragma unroll
+      for (int i = 0; i < K; ++i) red[((w - 1) * K + i) * TMD_WAVE + lane] = acc[i];
+    }
+    __syncthreads();
+    if (w != 0) return false;
+#pragma unroll
+    for (int s = 1; s < S; ++s)
+#pragma unroll
+      for (int i = 0; i < K; ++i) acc[i] += red[((s - 1) * K + i) * TMD_WAVE + lane];
+    return true;
+  }
 }
 
 template <typename T> __device__ __forceinline__ void ldc(T (&o)[9], const T* p, size_t nh) {
@@ -113,11 +140,11 @@ __device__ __forceinline__ void dsym_c(const T* g, T x, T y, T z, T& dx, T& dy, 
 }
 
 // ---------------------------------------------------------------- embedding forward
-template <typename T>
-__global__ __launch_bounds__(256) void k_embed_fwd(Args<T> A) {
-  int n, ch0;
-  wave_node(A.nblk, n, ch0);
-  if (n >= A.n) return;
+template <typename T, int S>
+__global__ __launch_bounds__(64 * S) void k_embed_fwd(Args<T> A) {
+  __shared__ T red[S > 1 ? (S - 1) * 9 * TMD_WAVE : 1];
+  int n, ch0, w;
+  slot_node<S>(A.nblk, n, ch0, w);
   const int h = ch0 + lane_id();
   const bool on = h < A.H;
   const int hc = on ? h : 0;
@@ -126,7 +153,7 @@ __global__ __launch_bounds__(256) void k_embed_fwd(Args<T> A) {
 #pragma unroll
   for (int k = 0; k < 9; ++k) acc[k] = T(0);
   const int b = min(A.row_ptr[n], A.cap), e = min(A.row_ptr[n + 1], A.cap);
-  for (int k = b; k < e; ++k) {
+  for (int k = b + w; k < e; k += S) {
     const int m = A.src[k];
     TMD_DCHECK(m >= 0 && m < A.n);
     const T mult = (m == n && n == 0) ? mult0_of(A) : T(1);
@@ -142,19 +169,19 @@ __global__ __launch_bounds__(256) void k_embed_fwd(Args<T> A) {
 #pragma unroll
     for (int i = 0; i < 5; ++i) acc[4 + i] += w3 * sy[i];
   }
-  if (on) stc(A.E + (size_t)n * A.H + h, A.nh, acc);
+  if (fold_waves<T, 9, S>(acc, red) && on) stc(A.E + (size_t)n * A.H + h, A.nh, acc);
 }
 
 // ---------------------------------------------------------------- embedding backward
 // destination pass: gP[n], gW[e'], gC[e'], gu[e'].  One wave per node covering all NB channel
 // blocks, so the per-edge channel sums (gC, gu) finish inside the wave: plain stores, deterministic.
-template <typename T, int NB>
-__global__ __launch_bounds__(256) void k_embed_bwd_dst(Args<T> A) {
+template <typename T, int NB, int S>
+__global__ __launch_bounds__(64 * S) void k_embed_bwd_dst(Args<T> A) {
+  __shared__ T red[S > 1 ? (S - 1) * NB * TMD_WAVE : 1];
   zero_tail_rows(A, A.gW, 3 * A.H);
   zero_tail_rows(A, A.gC, 1);
   zero_tail_rows(A, A.gu, 3);
-  const int n = blockIdx.x * (blockDim.x / TMD_WAVE) + threadIdx.x / TMD_WAVE;
-  if (n >= A.n) return;
+  const int n = blockIdx.x, w = threadIdx.x / TMD_WAVE;  // (the grid is one block per node)
   const int lane = lane_id();
   T g[NB][9], gPn[NB], Pn[NB];
 #pragma unroll
@@ -166,7 +193,7 @@ __global__ __launch_bounds__(256) void k_embed_bwd_dst(Args<T> A) {
     gPn[c] = T(0);
   }
   const int b = min(A.row_ptr[n], A.cap), e = min(A.row_ptr[n + 1], A.cap);
-  for (int k = b; k < e; ++k) {
+  for (int k = b + w; k < e; k += S) {
     const int m = A.src[k];
     TMD_DCHECK(m >= 0 && m < A.n);
     const T mult = (m == n && n == 0) ? mult0_of(A) : T(1);
@@ -216,6 +243,7 @@ __global__ __launch_bounds__(256) void k_embed_bwd_dst(Args<T> A) {
       A.gu[3 * k + 2] = guz;
     }
   }
+  if (!fold_waves<T, NB, S>(gPn, red)) return;
 #pragma unroll
   for (int c = 0; c < NB; ++c) {
     const int h = c * TMD_WAVE + lane;
@@ -224,17 +252,17 @@ __global__ __launch_bounds__(256) void k_embed_bwd_dst(Args<T> A) {
 }
 
 // source pass: gQ[m] = sum over reversed edges of the same g_z
-template <typename T>
-__global__ __launch_bounds__(256) void k_embed_bwd_src(Args<T> A) {
-  int m, ch0;
-  wave_node(A.nblk, m, ch0);
-  if (m >= A.n) return;
+template <typename T, int S>
+__global__ __launch_bounds__(64 * S) void k_embed_bwd_src(Args<T> A) {
+  __shared__ T red[S > 1 ? (S - 1) * TMD_WAVE : 1];
+  int m, ch0, w;
+  slot_node<S>(A.nblk, m, ch0, w);
   const int h = ch0 + lane_id();
   const bool on = h < A.H;
   const int hc = on ? h : 0;
-  T gQm = T(0);
+  T gQm[1] = {T(0)};
   const int b = min(A.row_ptr[m], A.cap), e = min(A.row_ptr[m + 1], A.cap);
-  for (int k = b; k < e; ++k) {
+  for (int k = b + w; k < e; k += S) {
     const int n = A.src[k];  // row edge n->m; its reverse m->n contributed Q[m] to E[n]
     TMD_DCHECK(n >= 0 && n < A.n);
     const T mult = (m == n && n == 0) ? mult0_of(A) : T(1);
@@ -249,17 +277,17 @@ __global__ __launch_bounds__(256) void k_embed_bwd_src(Args<T> A) {
     const T w1 = wr[hc], w2 = wr[A.H + hc], w3 = wr[2 * A.H + hc];
     const T gg = g[0] * w1 + (g[1] * sk[0] + g[2] * sk[1] + g[3] * sk[2]) * w2 +
                  (g[4] * sy[0] + g[5] * sy[1] + g[6] * sy[2] + g[7] * sy[3] + g[8] * sy[4]) * w3;
-    gQm += gg * A.C[k] * mult;
+    gQm[0] += gg * A.C[k] * mult;
   }
-  if (on) A.gQ[(size_t)m * A.H + h] = gQm;
+  if (fold_waves<T, 1, S>(gQm, red) && on) A.gQ[(size_t)m * A.H + h] = gQm[0];
 }
 
 // ---------------------------------------------------------------- message passing
-template <typename T>
-__global__ __launch_bounds__(256) void k_msg_fwd(Args<T> A) {
-  int n, ch0;
-  wave_node(A.nblk, n, ch0);
-  if (n >= A.n) return;
+template <typename T, int S>
+__global__ __launch_bounds__(64 * S) void k_msg_fwd(Args<T> A) {
+  __shared__ T red[S > 1 ? (S - 1) * 9 * TMD_WAVE : 1];
+  int n, ch0, w;
+  slot_node<S>(A.nblk, n, ch0, w);
   const int h = ch0 + lane_id();
   const bool on = h < A.H;
   const int hc = on ? h : 0;
@@ -267,7 +295,7 @@ __global__ __launch_bounds__(256) void k_msg_fwd(Args<T> A) {
 #pragma unroll
   for (int k = 0; k < 9; ++k) acc[k] = T(0);
   const int b = min(A.row_ptr[n], A.cap), e = min(A.row_ptr[n + 1], A.cap);
-  for (int k = b; k < e; ++k) {
+  for (int k = b + w; k < e; k += S) {
     const int m = A.src[k];
     TMD_DCHECK(m >= 0 && m < A.n);
     const T mult = (m == n && n == 0) ? mult0_of(A) : T(1);
@@ -278,23 +306,22 @@ __global__ __launch_bounds__(256) void k_msg_fwd(Args<T> A) {
 #pragma unroll
     for (int i = 0; i < 9; ++i) acc[i] += node::ctype_scale(i, f0, f1, f2) * t[i];
   }
-  if (on) stc(A.msg + (size_t)n * A.H + h, A.nh, acc);
+  if (fold_waves<T, 9, S>(acc, red) && on) stc(A.msg + (size_t)n * A.H + h, A.nh, acc);
 }
 
 // destination pass: gea[e'] = <gmsg[n], {I,A,S}[m]>
-template <typename T>
-__global__ __launch_bounds__(256) void k_msg_bwd_dst(Args<T> A) {
+template <typename T, int S>
+__global__ __launch_bounds__(64 * S) void k_msg_bwd_dst(Args<T> A) {
   zero_tail_rows(A, A.gea, 3 * A.H);
-  int n, ch0;
-  wave_node(A.nblk, n, ch0);
-  if (n >= A.n) return;
+  int n, ch0, w;
+  slot_node<S>(A.nblk, n, ch0, w);
   const int h = ch0 + lane_id();
   const bool on = h < A.H;
   const int hc = on ? h : 0;
   T g[9];
   ldc(g, A.gmsg + (size_t)n * A.H + hc, A.nh);
   const int b = min(A.row_ptr[n], A.cap), e = min(A.row_ptr[n + 1], A.cap);
-  for (int k = b; k < e; ++k) {
+  for (int k = b + w; k < e; k += S) {
     const int m = A.src[k];
     TMD_DCHECK(m >= 0 && m < A.n);
     const T mult = (m == n && n == 0) ? mult0_of(A) : T(1);
@@ -310,11 +337,11 @@ __global__ __launch_bounds__(256) void k_msg_bwd_dst(Args<T> A) {
 }
 
 // source pass: gT[m] = sum over reversed edges ea * gmsg[n]
-template <typename T>
-__global__ __launch_bounds__(256) void k_msg_bwd_src(Args<T> A) {
-  int m, ch0;
-  wave_node(A.nblk, m, ch0);
-  if (m >= A.n) return;
+template <typename T, int S>
+__global__ __launch_bounds__(64 * S) void k_msg_bwd_src(Args<T> A) {
+  __shared__ T red[S > 1 ? (S - 1) * 9 * TMD_WAVE : 1];
+  int m, ch0, w;
+  slot_node<S>(A.nblk, m, ch0, w);
   const int h = ch0 + lane_id();
   const bool on = h < A.H;
   const int hc = on ? h : 0;
@@ -322,7 +349,7 @@ __global__ __launch_bounds__(256) void k_msg_bwd_src(Args<T> A) {
 #pragma unroll
   for (int k = 0; k < 9; ++k) acc[k] = T(0);
   const int b = min(A.row_ptr[m], A.cap), e = min(A.row_ptr[m + 1], A.cap);
-  for (int k = b; k < e; ++k) {
+  for (int k = b + w; k < e; k += S) {
     const int n = A.src[k];
     TMD_DCHECK(n >= 0 && n < A.n);
     const T mult = (m == n && n == 0) ? mult0_of(A) : T(1);
@@ -333,6 +360,7 @@ __global__ __launch_bounds__(256) void k_msg_bwd_src(Args<T> A) {
 #pragma unroll
     for (int i = 0; i < 9; ++i) acc[i] += node::ctype_scale(i, f0, f1, f2) * g[i];
   }
+  if (!fold_waves<T, 9, S>(acc, red)) return;
   if (A.gTadd && on) {
     T ad[9];
     ldc(ad, A.gTadd + (size_t)m * A.H + h, A.nh);
@@ -342,12 +370,67 @@ __global__ __launch_bounds__(256) void k_msg_bwd_src(Args<T> A) {
   if (on) stc(A.gT + (size_t)m * A.H + h, A.nh, acc);
 }
 
-template <typename T>
-static int launch(void (*k)(Args<T>), const Args<T>& A, hipStream_t st) {
+// waves per (node, channel block): TMDNET_TN_S (A/B switch; 1, 2 or 4, default 4)
+static int slots() {
+  const char* e = getenv("TMDNET_TN_S");
+  const int s = e ? atoi(e) : 4;
+  return s >= 4 ? 4 : s >= 2 ? 2 : 1;
+}
+
+// one S-wave block per (node, channel block) of A.nblk
+template <typename T, template <typename, int> class K>
+static int launch_s(const Args<T>& A, hipStream_t st) {
   if (A.n <= 0) return kOk;
-  const long long waves = (long long)A.n * A.nblk;
-  const int tb = 256, wpb = tb / TMD_WAVE;
-  hipLaunchKernelGGL(k, dim3((unsigned)((waves + wpb - 1) / wpb)), dim3(tb), 0, st, A);
+  const dim3 g((unsigned)((long long)A.n * A.nblk));
+  switch (slots()) {
+    case 1: hipLaunchKernelGGL((K<T, 1>::fn), g, dim3(64), 0, st, A); break;
+    case 2: hipLaunchKernelGGL((K<T, 2>::fn), g, dim3(128), 0, st, A); break;
+    default: hipLaunchKernelGGL((K<T, 4>::fn), g, dim3(256), 0, st, A); break;
+  }
+  return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
+}
+#define TMD_TN_KERNEL(NAME)                                          \
+  template <typename T, int S> struct NAME##_k {                     \
+    static constexpr void (*fn)(Args<T>) = NAME<T, S>;               \
+  };
+TMD_TN_KERNEL(k_embed_fwd)
+TMD_TN_KERNEL(k_embed_bwd_src)
+TMD_TN_KERNEL(k_msg_fwd)
+TMD_TN_KERNEL(k_msg_bwd_dst)
+TMD_TN_KERNEL(k_msg_bwd_src)
+#undef TMD_TN_KERNEL
+
+template <typename T> static int launch_embed_fwd(const Args<T>& A, hipStream_t st) {
+  return launch_s<T, k_embed_fwd_k>(A, st);
+}
+template <typename T> static int launch_embed_bwd_src(const Args<T>& A, hipStream_t st) {
+  return launch_s<T, k_embed_bwd_src_k>(A, st);
+}
+template <typename T> static int launch_msg_fwd(const Args<T>& A, hipStream_t st) {
+  return launch_s<T, k_msg_fwd_k>(A, st);
+}
+template <typename T> static int launch_msg_bwd_dst(const Args<T>& A, hipStream_t st) {
+  return launch_s<T, k_msg_bwd_dst_k>(A, st);
+}
+template <typename T> static int launch_msg_bwd_src(const Args<T>& A, hipStream_t st) {
+  return launch_s<T, k_msg_bwd_src_k>(A, st);
+}
+
+// the embedding destination pass: one S-wave block per node (each wave covers every channel block)
+template <typename T>
+static int launch_embed_bwd_dst(const Args<T>& A, hipStream_t st) {
+  if (A.n <= 0) return kOk;
+  const dim3 g((unsigned)A.n);
+  const int s = slots();
+#define TMD_EBD(NB)                                                                                   \
+  if (s == 1) hipLaunchKernelGGL((k_embed_bwd_dst<T, NB, 1>), g, dim3(64), 0, st, A);                 \
+  else if (s == 2) hipLaunchKernelGGL((k_embed_bwd_dst<T, NB, 2>), g, dim3(128), 0, st, A);           \
+  else hipLaunchKernelGGL((k_embed_bwd_dst<T, NB, 4>), g, dim3(256), 0, st, A);
+  if (A.nblk == 1) { TMD_EBD(1) }
+  else if (A.nblk == 2) { TMD_EBD(2) }
+  else if (A.nblk <= 4) { TMD_EBD(4) }
+  else return kUnsupported;
+#undef TMD_EBD
   return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
 }
 
@@ -389,7 +472,7 @@ extern "C" int tmdnet_tn_embed_fwd(int dtype, int n_nodes, int hidden, const int
                          pad_capacity);
     a.P = (const T*)P; a.Q = (const T*)Q; a.W = (const T*)W; a.ldw = ld_w;
     a.C = (const T*)cutoff; a.u = (const T*)unit; a.E = (T*)out;
-    return tn::launch<T>(tn::k_embed_fwd<T>, a, st);
+    return tn::launch_embed_fwd<T>(a, st);
   })
 }
 
@@ -408,17 +491,9 @@ extern "C" int tmdnet_tn_embed_bwd(int dtype, int n_nodes, int hidden, const int
     a.C = (const T*)cutoff; a.u = (const T*)unit;
     a.gE = (const T*)grad_out;
     a.gP = (T*)gP; a.gQ = (T*)gQ; a.gW = (T*)gW; a.gC = (T*)gcut; a.gu = (T*)gunit;
-    int rc;
-    {
-      auto a1 = a;
-      a1.nblk = 1;  // wave per node, all channel blocks inside the wave
-      if (a.nblk == 1) rc = tn::launch<T>(tn::k_embed_bwd_dst<T, 1>, a1, st);
-      else if (a.nblk == 2) rc = tn::launch<T>(tn::k_embed_bwd_dst<T, 2>, a1, st);
-      else if (a.nblk <= 4) rc = tn::launch<T>(tn::k_embed_bwd_dst<T, 4>, a1, st);
-      else return kUnsupported;
-    }
+    const int rc = tn::launch_embed_bwd_dst<T>(a, st);  // (each wave covers every channel block)
     if (rc) return rc;
-    return tn::launch<T>(tn::k_embed_bwd_src<T>, a, st);
+    return tn::launch_embed_bwd_src<T>(a, st);
   })
 }
 
@@ -433,7 +508,7 @@ extern "C" int tmdnet_tn_message_fwd(int dtype, int n_nodes, int hidden, const i
                          pad_capacity);
     a.ea = (const T*)edge_attr; a.ldea = ld_ea;
     a.Tc = (const T*)comp; a.msg = (T*)msg;
-    return tn::launch<T>(tn::k_msg_fwd<T>, a, st);
+    return tn::launch_msg_fwd<T>(a, st);
   })
 }
 
@@ -451,9 +526,9 @@ extern "C" int tmdnet_tn_message_bwd_add(int dtype, int n_nodes, int hidden, con
     a.Tc = (const T*)comp;
     a.gmsg = (const T*)grad_msg; a.gea = (T*)g_edge_attr; a.gT = (T*)g_comp;
     a.gTadd = (const T*)g_comp_add;
-    int rc = tn::launch<T>(tn::k_msg_bwd_dst<T>, a, st);
+    int rc = tn::launch_msg_bwd_dst<T>(a, st);
     if (rc) return rc;
-    return tn::launch<T>(tn::k_msg_bwd_src<T>, a, st);
+    return tn::launch_msg_bwd_src<T>(a, st);
   })
 }
 
