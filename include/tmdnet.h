@@ -344,6 +344,15 @@ int tmdnet_et_adjoint_epi_ln(int dtype, int n_nodes, int hidden, const void* gb_
                              void* gbar_vec_out, void* vecp_bar, void* o_bar, const void* x, const void* mean,
                              const void* rstd, const void* ln_w, const void* grad_xn, void* gbar_grad_xn,
                              void* x_bar, void* w_bar_rows, void* stream);
+/* The same with the incoming vec cotangent as the sum of two buffers (gbar_vec_in + gbar_vec_in2, either
+ * NULL = 0): the force-loss adjoint passes the message VJP's d_gvec beside the running vec cotangent, so no
+ * separate add launch forms their sum. */
+int tmdnet_et_adjoint_epi_ln2(int dtype, int n_nodes, int hidden, const void* gb_o, const void* gb_vecp,
+                              const void* grad_x, const void* grad_vec, const void* vecp, const void* o,
+                              const void* gbar_x_in, const void* gbar_vec_in, const void* gbar_vec_in2,
+                              void* gbar_x_out, void* gbar_vec_out, void* vecp_bar, void* o_bar, const void* x,
+                              const void* mean, const void* rstd, const void* ln_w, const void* grad_xn,
+                              void* gbar_grad_xn, void* x_bar, void* w_bar_rows, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * EquivariantScalar output head (reference models/output_modules.py:80-115 with two

@@ -25,7 +25,8 @@ def _rel(a, b):
 @pytest.mark.parametrize("dtype,tol", [(torch.float64, 1e-12), (torch.float32, 2e-5)])
 @pytest.mark.parametrize("with_vec", [True, False])
 @pytest.mark.parametrize("with_epi,with_ln", [(True, True), (True, False), (False, True)])
-def test_adjoint_epi_ln_kernel(dtype, tol, with_vec, with_epi, with_ln):
+@pytest.mark.parametrize("split_vec", [False, True])  # the vec cotangent as two addends (..._ln2)
+def test_adjoint_epi_ln_kernel(dtype, tol, with_vec, with_epi, with_ln, split_vec):
     from torchmdnet import et_stack as ES
     torch.manual_seed(0)
     N, H = 77, 128
@@ -40,6 +41,8 @@ def test_adjoint_epi_ln_kernel(dtype, tol, with_vec, with_epi, with_ln):
         _, mean, rstd = torch.native_layer_norm(x, [H], None, None, 1e-5)
         ln = (x, mean, rstd, r(H), r(N, H))
     gbx, gbv = r(N, H), (r(N, 3, H) if with_vec else None)
+    if split_vec and gbv is not None:
+        gbv = (gbv, r(N, 3, H))
     a = ES.adjoint_epi_ln_launch(epi, gbx, gbv, ln)
     b = ES.adjoint_epi_ln_composite(epi, gbx, gbv, ln)
     for i, (ta, tb) in enumerate(zip(a, b)):

@@ -335,10 +335,10 @@ template <typename T, int CPL>
 __global__ __launch_bounds__(256) void k_adj_epi_ln(
     int n, int H, const T* __restrict__ gbo, const T* __restrict__ gbvp, const T* __restrict__ gX,
     const T* __restrict__ gV, const T* __restrict__ vecp, const T* __restrict__ o, const T* __restrict__ gbx_in,
-    const T* __restrict__ gbv_in, T* __restrict__ gbx_out, T* __restrict__ gbv_out, T* __restrict__ vpbar,
-    T* __restrict__ obar, const T* __restrict__ x, const T* __restrict__ mean, const T* __restrict__ rstd,
-    const T* __restrict__ lw, const T* __restrict__ gy, T* __restrict__ gbgy, T* __restrict__ xbar,
-    T* __restrict__ wrows) {
+    const T* __restrict__ gbv_in, const T* __restrict__ gbv_in2, T* __restrict__ gbx_out, T* __restrict__ gbv_out,
+    T* __restrict__ vpbar, T* __restrict__ obar, const T* __restrict__ x, const T* __restrict__ mean,
+    const T* __restrict__ rstd, const T* __restrict__ lw, const T* __restrict__ gy, T* __restrict__ gbgy,
+    T* __restrict__ xbar, T* __restrict__ wrows) {
   const int t = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
   const int lane = threadIdx.x & 63;
   if (t >= n) return;
@@ -365,7 +365,7 @@ __global__ __launch_bounds__(256) void k_adj_epi_ln(
 #pragma unroll
           for (int a = 0; a < 3; ++a) {
             const size_t iv = ((size_t)t * 3 + a) * H + c;
-            gbv_out[iv] = gbv_in ? gbv_in[iv] : T(0);
+            gbv_out[iv] = (gbv_in ? gbv_in[iv] : T(0)) + (gbv_in2 ? gbv_in2[iv] : T(0));
           }
         }
       } else {
@@ -383,7 +383,7 @@ __global__ __launch_bounds__(256) void k_adj_epi_ln(
           dot += v1 * v2;
           cross += c1 * v2 + c2 * v1;
           o1b += c3 * gv;
-          gbv_out[iv] = (gbv_in ? gbv_in[iv] : T(0)) + b1 * v3 + c3 * o1;
+          gbv_out[iv] = (gbv_in ? gbv_in[iv] : T(0)) + (gbv_in2 ? gbv_in2[iv] : T(0)) + b1 * v3 + c3 * o1;
           vb[a * 3 * H + c] = b2 * gx * v2 + c2 * gx * o2;
           vb[a * 3 * H + H + c] = b2 * gx * v1 + c1 * gx * o2;
           vb[a * 3 * H + 2 * H + c] = b1 * gv;
@@ -516,12 +516,13 @@ extern "C" int tmdnet_ln_bwd_epilogue_w(int dtype, int n_nodes, int hidden, cons
   return kUnsupported;
 }
 
-extern "C" int tmdnet_et_adjoint_epi_ln(int dtype, int n_nodes, int hidden, const void* gb_o, const void* gb_vecp,
-                                        const void* grad_x, const void* grad_vec, const void* vecp, const void* o,
-                                        const void* gbar_x_in, const void* gbar_vec_in, void* gbar_x_out,
-                                        void* gbar_vec_out, void* vecp_bar, void* o_bar, const void* x,
-                                        const void* mean, const void* rstd, const void* ln_w, const void* grad_xn,
-                                        void* gbar_grad_xn, void* x_bar, void* w_bar_rows, void* stream) {
+extern "C" int tmdnet_et_adjoint_epi_ln2(int dtype, int n_nodes, int hidden, const void* gb_o, const void* gb_vecp,
+                                         const void* grad_x, const void* grad_vec, const void* vecp, const void* o,
+                                         const void* gbar_x_in, const void* gbar_vec_in, const void* gbar_vec_in2,
+                                         void* gbar_x_out, void* gbar_vec_out, void* vecp_bar, void* o_bar,
+                                         const void* x, const void* mean, const void* rstd, const void* ln_w,
+                                         const void* grad_xn, void* gbar_grad_xn, void* x_bar, void* w_bar_rows,
+                                         void* stream) {
   if (n_nodes < 0 || hidden <= 0 || !gbar_x_in) return kBadArgument;
   if (o && (!gb_o || !gbar_x_out || !o_bar || (vecp && (!gb_vecp || !grad_x || !grad_vec || !gbar_vec_out ||
                                                         !vecp_bar))))
@@ -533,11 +534,23 @@ extern "C" int tmdnet_et_adjoint_epi_ln(int dtype, int n_nodes, int hidden, cons
 #define TMD_ADJ(T)                                                                                            \
   return launch_cpl<T, KAdj>(n_nodes, hidden, st, (const T*)gb_o, (const T*)gb_vecp, (const T*)grad_x,       \
                              (const T*)grad_vec, (const T*)vecp, (const T*)o, (const T*)gbar_x_in,            \
-                             (const T*)gbar_vec_in, (T*)gbar_x_out, (T*)gbar_vec_out, (T*)vecp_bar, (T*)o_bar, \
+                             (const T*)gbar_vec_in, (const T*)gbar_vec_in2, (T*)gbar_x_out, (T*)gbar_vec_out,    \
+                             (T*)vecp_bar, (T*)o_bar,                                                          \
                              (const T*)x, (const T*)mean, (const T*)rstd, (const T*)ln_w, (const T*)grad_xn,  \
                              (T*)gbar_grad_xn, (T*)x_bar, (T*)w_bar_rows)
   if (dtype == TMDNET_F32) TMD_ADJ(float);
   if (dtype == TMDNET_F64) TMD_ADJ(double);
 #undef TMD_ADJ
   return kUnsupported;
+}
+
+extern "C" int tmdnet_et_adjoint_epi_ln(int dtype, int n_nodes, int hidden, const void* gb_o, const void* gb_vecp,
+                                        const void* grad_x, const void* grad_vec, const void* vecp, const void* o,
+                                        const void* gbar_x_in, const void* gbar_vec_in, void* gbar_x_out,
+                                        void* gbar_vec_out, void* vecp_bar, void* o_bar, const void* x,
+                                        const void* mean, const void* rstd, const void* ln_w, const void* grad_xn,
+                                        void* gbar_grad_xn, void* x_bar, void* w_bar_rows, void* stream) {
+  return tmdnet_et_adjoint_epi_ln2(dtype, n_nodes, hidden, gb_o, gb_vecp, grad_x, grad_vec, vecp, o, gbar_x_in,
+                                   gbar_vec_in, nullptr, gbar_x_out, gbar_vec_out, vecp_bar, o_bar, x, mean, rstd,
+                                   ln_w, grad_xn, gbar_grad_xn, x_bar, w_bar_rows, stream);
 }

@@ -64,6 +64,7 @@ SIGNATURES = {
     "tmdnet_ln_bwd_epilogue": (I, [I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P]),
     "tmdnet_ln_bwd_epilogue_w": (I, [I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, P]),
     "tmdnet_et_adjoint_epi_ln": (I, [I, I, I] + [P] * 21),
+    "tmdnet_et_adjoint_epi_ln2": (I, [I, I, I] + [P] * 22),
     "tmdnet_eq_head_fwd": (I, [I, I, I, P, P, P, P, P, P, P]),
     "tmdnet_eq_head_bwd": (I, [I, I, I, P, P, P, P, P, P]),
     "tmdnet_eq_head_bwd_weights": (I, [I, I, I, P, P, P, P, P, P, P, P]),

@@ -778,10 +778,14 @@ def adjoint_epi_ln_launch(epi, gbar_x_in, gbar_vec_in, ln, outs=None):
     w_bar) with w_bar the weight cotangent (column sum of the kernel's per-row products).  The Python
     ``epi_adjoint`` / ``ln_adjoint`` restate it (CPU tests).  ``outs`` (optional dict): caller buffers
     "gbgy" (gbar_gy), "gbv" (gbar_vec_out), "wrows" (the per-row weight terms: w_bar is then None and
-    the caller sums the rows)."""
+    the caller sums the rows).  ``gbar_vec_in`` may be a pair (a, b): the cotangent a + b, summed by the
+    kernel (tmdnet_et_adjoint_epi_ln2)."""
     lib = nat.load()
     outs = outs or {}
     N, H = gbar_x_in.shape
+    gbar_vec_in2 = None
+    if isinstance(gbar_vec_in, tuple):
+        gbar_vec_in, gbar_vec_in2 = gbar_vec_in
     o_ = dict(dtype=gbar_x_in.dtype, device=gbar_x_in.device)
     gb_o = gb_vecp = gX = gV = vecp = o = None
     gbx_out = gbv_out = vpbar = obar = None
@@ -789,7 +793,7 @@ def adjoint_epi_ln_launch(epi, gbar_x_in, gbar_vec_in, ln, outs=None):
         gb_o, gb_vecp, gX, gV, vecp, o = epi
         gbx_out = torch.empty((N, H), **o_)
         obar = outs["obar"] if outs.get("obar") is not None else torch.empty((N, 3 * H), **o_)
-        if vecp is not None or gbar_vec_in is not None:
+        if vecp is not None or gbar_vec_in is not None or gbar_vec_in2 is not None:
             gbv_out = outs["gbv"] if outs.get("gbv") is not None else torch.empty((N, 3, H), **o_)
         if vecp is not None:
             vpbar = outs["vpbar"] if outs.get("vpbar") is not None else torch.empty((N, 3, 3 * H), **o_)
@@ -800,14 +804,16 @@ def adjoint_epi_ln_launch(epi, gbar_x_in, gbar_vec_in, ln, outs=None):
         wrows = outs["wrows"] if outs.get("wrows") is not None else torch.empty((N, H), **o_)
         xbar = torch.empty((N, H), **o_)
     c = lambda t: None if t is None else t.contiguous()  # noqa: E731
-    args = [c(t) for t in (gb_o, gb_vecp, gX, gV, vecp, o, gbar_x_in, gbar_vec_in)]
-    rc = lib.tmdnet_et_adjoint_epi_ln(nat.dtype_code(gbar_x_in.dtype), N, H, *[nat.ptr(t) for t in args],
-                                      nat.ptr(gbx_out), nat.ptr(gbv_out), nat.ptr(vpbar), nat.ptr(obar),
-                                      *[nat.ptr(c(t)) for t in (x, mean, rstd, w, gy)], nat.ptr(gbgy),
-                                      nat.ptr(xbar), nat.ptr(wrows), nat.stream(gbar_x_in.device))
-    nat.check(rc, "tmdnet_et_adjoint_epi_ln")
+    args = [c(t) for t in (gb_o, gb_vecp, gX, gV, vecp, o, gbar_x_in, gbar_vec_in, gbar_vec_in2)]
+    rc = lib.tmdnet_et_adjoint_epi_ln2(nat.dtype_code(gbar_x_in.dtype), N, H, *[nat.ptr(t) for t in args],
+                                       nat.ptr(gbx_out), nat.ptr(gbv_out), nat.ptr(vpbar), nat.ptr(obar),
+                                       *[nat.ptr(c(t)) for t in (x, mean, rstd, w, gy)], nat.ptr(gbgy),
+                                       nat.ptr(xbar), nat.ptr(wrows), nat.stream(gbar_x_in.device))
+    nat.check(rc, "tmdnet_et_adjoint_epi_ln2")
     if epi is None:
-        gbx_out, gbv_out = gbar_x_in, gbar_vec_in
+        gbx_out = gbar_x_in
+        gbv_out = gbar_vec_in if gbar_vec_in2 is None else \
+            (gbar_vec_in2 if gbar_vec_in is None else gbar_vec_in + gbar_vec_in2)
     # (the column sums as a split-K TN launch: ATen's dim-0 reduction of [N, H] took 20 us at C2)
     return gbx_out, gbv_out, vpbar, obar, gbgy, xbar, \
         (kernels._linear_wgrad(wrows, wrows, False, True)[1] if (wrows is not None and outs.get("wrows") is None)
@@ -816,6 +822,9 @@ def adjoint_epi_ln_launch(epi, gbar_x_in, gbar_vec_in, ln, outs=None):
 
 def adjoint_epi_ln_composite(epi, gbar_x_in, gbar_vec_in, ln, outs=None):
     """``adjoint_epi_ln_launch`` restated with ``epi_adjoint`` / ``ln_adjoint`` (CPU tests)."""
+    if isinstance(gbar_vec_in, tuple):  # (a, b): the cotangent a + b
+        a, b = gbar_vec_in
+        gbar_vec_in = b if a is None else (a if b is None else a + b)
     if outs:
         res = list(adjoint_epi_ln_composite(epi, gbar_x_in, gbar_vec_in, ln))
         if outs.get("gbv") is not None and res[1] is not None:
@@ -1009,7 +1018,8 @@ def _second_order(ctx, ggs, want):
         if has_e:
             inj["pkv"][l] = outs["pkv"]
         inj["vec"][l] = d_vec
-        gb_gV = d_gvec if gbar_v is None else gbar_v + d_gvec  # the vec residual g_vec = gV + ...
+        # the vec residual g_vec = gV + ...: the two addends go to the adjoint kernel, which sums them on load
+        gb_gV = d_gvec if gbar_v is None else (gbar_v, d_gvec)
         gb_go = torch.empty((N, o_w.shape[0]), **o)
         kernels.gemm_group([(d_gxa, o_w, True, None, gb_go, False)])
         if gb_gvecp is None and vecp is not None:
