@@ -242,16 +242,29 @@ __global__ __launch_bounds__(256) void k_ln_bwd_epi(int n, int H, const T* __res
   // the epilogue-backward operands are loaded with the LayerNorm's, before the two row sums: one
   // memory round trip per node instead of two (C2: 9 -> see DESIGN 3b)
   T gr[CPL], o1[CPL], o2[CPL], vq[CPL][9], gq[CPL][3];
+  // accumulate mode: the outputs' current values, loaded here too (a read-modify-write after the row sums
+  // was a second dependent memory round trip: 13-17 us per launch in the training step vs 5-6 us)
+  T pv[CPL][9], po[CPL][3];
   const bool ev = o != nullptr && vecp != nullptr;
 #pragma unroll
   for (int i = 0; i < CPL; ++i) {
     const int c = lane + 64 * i;
     gr[i] = o1[i] = o2[i] = T(0);
 #pragma unroll
-    for (int a = 0; a < 9; ++a) vq[i][a] = T(0);
+    for (int a = 0; a < 9; ++a) vq[i][a] = pv[i][a] = T(0);
 #pragma unroll
-    for (int a = 0; a < 3; ++a) gq[i][a] = T(0);
+    for (int a = 0; a < 3; ++a) gq[i][a] = po[i][a] = T(0);
     if (c >= H) continue;
+    if (acc && o) {
+      const T* gt = go + (size_t)t * 3 * H;
+#pragma unroll
+      for (int a = 0; a < 3; ++a) po[i][a] = gt[a * H + c];
+      if (vecp) {
+        const T* gvp = gvecp + (size_t)t * 9 * H;
+#pragma unroll
+        for (int a = 0; a < 9; ++a) pv[i][a] = gvp[a * H + c];
+      }
+    }
     if (gres) gr[i] += gres[(size_t)t * H + c];
     if (gres2) gr[i] += gres2[(size_t)t * H + c];
     if (ev) {
@@ -291,9 +304,9 @@ __global__ __launch_bounds__(256) void k_ln_bwd_epi(int n, int H, const T* __res
     if (!o) continue;
     T* gt = go + (size_t)t * 3 * H;
     if (!vecp) {
-      put(gt + c, T(0), acc);
-      put(gt + H + c, T(0), acc);
-      put(gt + 2 * H + c, g, acc);
+      gt[c] = po[i][0];
+      gt[H + c] = po[i][1];
+      gt[2 * H + c] = po[i][2] + g;
       continue;
     }
     T* gvp = gvecp + (size_t)t * 9 * H;
@@ -305,13 +318,13 @@ __global__ __launch_bounds__(256) void k_ln_bwd_epi(int n, int H, const T* __res
       const T gv = gq[i][a];
       dot += v1 * v2;
       go1 += gv * v3;
-      put(gvp + a * 3 * H + c, gd * v2, acc);
-      put(gvp + a * 3 * H + H + c, gd * v1, acc);
-      put(gvp + a * 3 * H + 2 * H + c, gv * o1[i], acc);
+      gvp[a * 3 * H + c] = pv[i][3 * a] + gd * v2;
+      gvp[a * 3 * H + H + c] = pv[i][3 * a + 1] + gd * v1;
+      gvp[a * 3 * H + 2 * H + c] = pv[i][3 * a + 2] + gv * o1[i];
     }
-    put(gt + c, go1, acc);
-    put(gt + H + c, g * dot, acc);
-    put(gt + 2 * H + c, g, acc);
+    gt[c] = po[i][0] + go1;
+    gt[H + c] = po[i][1] + g * dot;
+    gt[2 * H + c] = po[i][2] + g;
   }
 }
 
