@@ -282,3 +282,18 @@ def test_default_atom_buckets_cover_the_largest_batch():
     ds = [Data(z=torch.ones(n, dtype=torch.long)) for n in (9, 12, 29, 17, 20) * 20]
     b = default_atom_buckets(ds, 32)
     assert b == sorted(set(b)) and b[-1] >= 29 * 32 + 1 and all(x % 32 == 0 for x in b)
+
+
+def test_gradient_copy_keeps_strided_gradients():
+    """training._copy_grads: contiguous gradients in one multi-tensor copy, strided ones (column blocks of
+    a weight-gradient GEMM's output) one by one -- every view receives its gradient."""
+    from torchmdnet.training import _copy_grads
+    torch.manual_seed(0)
+    flat = torch.zeros(64 + 10 + 12)
+    views = [flat[:64].view(8, 8), flat[64:74], flat[74:].view(3, 4)]
+    block = torch.randn(3, 5)
+    grads = [torch.randn(8, 8), torch.randn(20)[::2], block[:, :4]]
+    assert not grads[1].is_contiguous() and not grads[2].is_contiguous()
+    _copy_grads(list(zip(views, grads)))
+    for v, g in zip(views, grads):
+        assert torch.equal(v, g)
