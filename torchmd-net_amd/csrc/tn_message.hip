@@ -421,11 +421,15 @@ template <typename T>
 static int launch_embed_bwd_dst(const Args<T>& A, hipStream_t st) {
   if (A.n <= 0) return kOk;
   const dim3 g((unsigned)A.n);
-  const int s = slots();
+  // (its per-edge channel sums make each edge a longer chain than the other kernels': TMDNET_TN_EBD_S=8
+  // gives it 8 waves per node)
+  const char* e8 = getenv("TMDNET_TN_EBD_S");
+  const int s = (e8 && atoi(e8) >= 8) ? 8 : slots();
 #define TMD_EBD(NB)                                                                                   \
   if (s == 1) hipLaunchKernelGGL((k_embed_bwd_dst<T, NB, 1>), g, dim3(64), 0, st, A);                 \
   else if (s == 2) hipLaunchKernelGGL((k_embed_bwd_dst<T, NB, 2>), g, dim3(128), 0, st, A);           \
-  else hipLaunchKernelGGL((k_embed_bwd_dst<T, NB, 4>), g, dim3(256), 0, st, A);
+  else if (s == 4) hipLaunchKernelGGL((k_embed_bwd_dst<T, NB, 4>), g, dim3(256), 0, st, A);           \
+  else hipLaunchKernelGGL((k_embed_bwd_dst<T, NB, 8>), g, dim3(512), 0, st, A);
   if (A.nblk == 1) { TMD_EBD(1) }
   else if (A.nblk == 2) { TMD_EBD(2) }
   else if (A.nblk <= 4) { TMD_EBD(4) }
