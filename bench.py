@@ -173,6 +173,33 @@ def setup_dist():
     return ws, rank, torch.device("cuda", local if ws > 1 else 0)
 
 
+def dist_info(ws, rank, dev):
+    """What the process group actually is: backend, world size, and per rank its
+    device index, PCI location and host -- so a multi-GPU record shows N ranks on N distinct devices."""
+    props = torch.cuda.get_device_properties(dev)
+    mine = [rank, dev.index if dev.index is not None else 0, int(getattr(props, "pci_domain_id", -1)),
+            int(getattr(props, "pci_bus_id", -1)), int(getattr(props, "pci_device_id", -1)),
+            int(os.environ.get("LOCAL_RANK", "0"))]
+    rows = [mine]
+    if ws > 1:
+        t = torch.tensor(mine, dtype=torch.int64, device=dev)
+        out = [torch.empty_like(t) for _ in range(ws)]
+        dist.all_gather(out, t)
+        rows = [[int(v) for v in x.cpu()] for x in out]
+    info = {"world_size": ws, "backend": dist.get_backend() if ws > 1 else None,
+            "device_name": props.name, "gcn_arch": getattr(props, "gcnArchName", None),
+            "ranks": [{"rank": r[0], "local_rank": r[5], "device": r[1], "pci": f"{r[2]:04x}:{r[3]:02x}:{r[4]:02x}"}
+                      for r in rows]}
+    if ws > 1:
+        info["distinct_devices"] = len({x["pci"] for x in info["ranks"]})
+        try:
+            v = torch.cuda.nccl.version()
+            info["rccl_version"] = ".".join(str(x) for x in v) if isinstance(v, tuple) else str(v)
+        except Exception:  # noqa: BLE001 -- informational only
+            pass
+    return info
+
+
 def barrier(ws):
     if ws > 1:
         dist.barrier()
@@ -1195,6 +1222,7 @@ def main():
                    "atoms_per_gpu": n_atoms, "global_batch": a.batch * ws, "parallelism": f"dp{ws}",
                    "execution": "eager" if (a.eager or a.mode == "train") else "hip-graph replay"},
     }
+    out["distributed"] = dist_info(ws, rank, dev)
     if rank == 0 and probe:
         H = a.channels
         ms = sum(e0.elapsed_time(e1) for e0, e1, *_ in probe) / len(probe)

@@ -343,9 +343,64 @@ def gen_splits():
     res["ncases"] = np.array([len(cases)])
     save("splits_ref.npz", res)
 
+# --------------------------------------------------------------------------- periodic models (round 5)
+def water_box(n, gen_seed=11):
+    """SURVEY.md §8(d) water box at small n: z = (O, H, H) repeated, uniform positions in a cube of
+    the water number density 0.1003 / A^3 (the exact tensors are stored in each fixture)."""
+    g = torch.Generator().manual_seed(gen_seed)
+    L = (n / 0.1003) ** (1.0 / 3.0)
+    z = torch.tensor([8, 1, 1], dtype=torch.long).repeat(n // 3 + 1)[:n]
+    pos = torch.rand(n, 3, generator=g, dtype=torch.float64) * L
+    return z, pos, torch.zeros(n, dtype=torch.long), L
+
+
+def gen_periodic():
+    """ET-tiny and TensorNet-tiny (static padded and dynamic shapes) on a rectangular periodic box: the
+    reference CPU neighbour op's minimum image (neighbors_cpu.cpp:63-70) through the whole model,
+    energies, forces and the force-loss parameter gradients."""
+    orig = ref_utils.get_neighbor_pairs_kernel
+    n = 120
+    z, pos, batch, L = water_box(n)
+    box = torch.eye(3, dtype=torch.float64) * L
+
+    def set_box(model, dtype):
+        d = model.representation_model.distance
+        d.box = box.to(dtype)
+        d.use_periodic = True
+
+    args = base_args("equivariant-transformer", embedding_dimension=32, num_layers=2, num_rbf=16, num_heads=4,
+                     max_num_neighbors=64, derivative=True, output_model="Scalar", precision=64)
+    seed_everything(1234)
+    model = create_model(args)
+    set_box(model, torch.float64)
+    res = run_model(model, z, pos, batch, torch.float64)
+    res.update(state_dict_arrays(model))
+    res["box"] = box.numpy()
+    save("et_tiny_periodic_f64.npz", res)
+    for static in (True, False):
+        ref_utils.get_neighbor_pairs_kernel = padded_kernel(orig) if static else orig
+        import torchmdnet.models.utils as u
+        u.get_neighbor_pairs_kernel = ref_utils.get_neighbor_pairs_kernel
+        args = base_args("tensornet", embedding_dimension=32, num_layers=2, num_rbf=16, max_num_neighbors=64,
+                         cutoff_upper=4.5, derivative=True, output_model="Scalar", precision=64)
+        seed_everything(1234)
+        model = create_model(args)
+        model.representation_model.static_shapes = static
+        model.representation_model.distance.resize_to_fit = not static
+        set_box(model, torch.float64)
+        res = run_model(model, z, pos, batch, torch.float64)
+        res.update(state_dict_arrays(model))
+        res["box"] = box.numpy()
+        save(f"tn_tiny_periodic_{'static' if static else 'dyn'}_f64.npz", res)
+    ref_utils.get_neighbor_pairs_kernel = orig
+    import torchmdnet.models.utils as u
+    u.get_neighbor_pairs_kernel = orig
+
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["neighbors", "et", "tensornet", "seed", "edge", "splits", "acts"]
+    which = sys.argv[1:] or ["neighbors", "et", "tensornet", "seed", "edge", "splits", "acts", "periodic"]
+    if "periodic" in which:
+        gen_periodic()
     if "acts" in which:
         gen_activations()
     if "edge" in which:

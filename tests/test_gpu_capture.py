@@ -122,14 +122,15 @@ def test_cuda_graph_compatible_backward(strategy, box_type, include_transpose):
     assert g_graph.abs().sum() > 0
 
 
-@pytest.mark.parametrize("strategy", ["brute", "cell"])
-def test_static_capacity_build_replay_padding_contract(strategy):
+@pytest.mark.parametrize("strategy,pairs", [("brute", True), ("cell", False), ("cell", True)])
+def test_static_capacity_build_replay_padding_contract(strategy, pairs):
     """One captured static-capacity build (the model's HIP-graph mode, kernels.build_graph with
     ``static_capacity``), replayed with positions that give FEWER, MORE and TOO MANY pairs than at
     capture: after every replay slots [num_pairs, cap) hold (-1, -1) / 0 (reference common.cuh:70-76),
     the transpose map -1 and the pair rows 0 there; every written index is a valid atom; the found
     pairs equal the oracle's; an overflowing replay reports num_pairs > cap and keeps every index
-    in range (the list is the truncated prefix)."""
+    in range (the list is the truncated prefix).  ``pairs``: the pair numbering (brute: inside the build;
+    cell: the separate pairs.hip kernels, the large-system path's form) on the same replays."""
     from torchmdnet import kernels
     _lib_loaded()
     torch.manual_seed(11)
@@ -148,13 +149,13 @@ def test_static_capacity_build_replay_padding_contract(strategy):
     s.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(s):
         kernels.build_graph(pos, batch, 0.0, cutoff, 512 * n, loop=True, strategy=strategy, box=box,
-                            static_capacity=cap, pairs=strategy != "cell")
+                            static_capacity=cap, pairs=pairs)
     torch.cuda.current_stream().wait_stream(s)
     torch.cuda.synchronize()
     cg = torch.cuda.CUDAGraph()
     with torch.cuda.graph(cg):
         g = kernels.build_graph(pos, batch, 0.0, cutoff, 512 * n, loop=True, strategy=strategy, box=box,
-                                static_capacity=cap, pairs=strategy != "cell")
+                                static_capacity=cap, pairs=pairs)
     torch.cuda.synchronize()
     seen_overflow = seen_under = False
     for scale in (0.8, 1.0, 0.75, 0.9, 0.6, 1.0, 0.8):

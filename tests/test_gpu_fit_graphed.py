@@ -29,11 +29,14 @@ def _dataset(n, seed=3):
     return out
 
 
-def _model(seed=0):
+def _model(seed=0, kind="et", derivative=True):
     from torchmdnet.models.model import create_model
     torch.manual_seed(seed)
+    if kind == "tn":  # static_shapes (the reference default): atom 0 takes the padding slots
+        return create_model(yaml_args("tensornet", embedding_dimension=64, num_layers=2, num_rbf=32,
+                                      max_num_neighbors=32, static_shapes=True, derivative=derivative)).to(DEV)
     return create_model(yaml_args("equivariant-transformer", embedding_dimension=128, num_layers=4, num_rbf=64,
-                                  num_heads=8, derivative=True)).to(DEV)
+                                  num_heads=8, derivative=derivative)).to(DEV)
 
 
 def _eager_steps(model, batches, lr, y_w, f_w, warmup):
@@ -45,6 +48,64 @@ def _eager_steps(model, batches, lr, y_w, f_w, warmup):
         b = collate(samples).to(DEV)
         losses.append(float(tr.step(b.z, b.pos.float(), b.batch, b.y.float(), b.neg_dy.float())))
     return losses
+
+
+def _padded_run(model, batches, pb, **kw):
+    from torchmdnet.training import PaddedGraphedTrainer
+    tr = PaddedGraphedTrainer(model, pb, **kw)
+    losses = []
+    for samples in batches:
+        losses.append(tr.step(pb.collate(samples).pin_memory())[2])
+    tr.finish()
+    return tr, [float(x) for x in losses]
+
+
+def _worst_param(model, ref_model):
+    worst = 0.0
+    for (n, p), (_, q) in zip(model.named_parameters(), ref_model.named_parameters()):
+        worst = max(worst, float((p - q).norm() / q.norm().clamp_min(1e-12)))
+    return worst
+
+
+def test_padded_graphed_trainer_tensornet_static_shapes():
+    """TensorNet with static_shapes=True: the padding slots of the reference's capacity
+    max_num_neighbors x N go to atom 0; in a padded batch N is the capacity and the ghosts' self loops
+    count as pairs, so without the pair-count correction atom 0 got (max_nb - 1) x n_ghosts extra self
+    loops.  The padded captured steps must equal the eager steps on the unpadded batches."""
+    from torchmdnet.training import PaddedBatches
+    data = _dataset(48, seed=5)
+    batches = [data[i:i + 8] for i in range(0, 48, 8)]
+    lr, y_w, f_w, warm = 1e-3, 0.3, 0.7, 2
+    ref_model = _model(kind="tn")
+    ref_losses = _eager_steps(ref_model, batches, lr, y_w, f_w, warm)
+    model = _model(kind="tn")
+    pb = PaddedBatches([160, 224, 288], max_molecules=8, cutoff=4.5)
+    tr, losses = _padded_run(model, batches, pb, lr=lr, y_weight=y_w, neg_dy_weight=f_w, lr_warmup_steps=warm)
+    for a, e in zip(losses, ref_losses):
+        assert abs(a - e) <= 1e-5 * abs(e), (losses, ref_losses)
+    assert _worst_param(model, ref_model) < 1e-4
+    assert model.representation_model._pad_shift is None  # eager calls after training see no correction
+
+
+def test_padded_graphed_trainer_energy_only():
+    """derivative=False: no forces, the force term is zero; energy-only captured steps
+    equal the eager ones."""
+    from torchmdnet.data import collate
+    from torchmdnet.training import LNNPStep, PaddedBatches
+    data = _dataset(32, seed=9)
+    batches = [data[i:i + 8] for i in range(0, 32, 8)]
+    ref_model = _model(derivative=False)
+    tr_e = LNNPStep(ref_model, lr=1e-3, y_weight=1.0, neg_dy_weight=0.0)
+    ref_losses = []
+    for samples in batches:
+        b = collate(samples).to(DEV)
+        ref_losses.append(float(tr_e.step(b.z, b.pos.float(), b.batch, b.y.float(), b.neg_dy.float())))
+    model = _model(derivative=False)
+    pb = PaddedBatches([192, 256, 320], max_molecules=8, cutoff=5.0)
+    tr, losses = _padded_run(model, batches, pb, lr=1e-3, y_weight=1.0, neg_dy_weight=0.0)
+    for a, e in zip(losses, ref_losses):
+        assert abs(a - e) <= 1e-5 * abs(e), (losses, ref_losses)
+    assert _worst_param(model, ref_model) < 1e-4
 
 
 @pytest.mark.parametrize("margin", [1.3, 0.6])

@@ -370,11 +370,15 @@ __global__ __launch_bounds__(64 * S) void k_msg_bwd_src(Args<T> A) {
   if (on) stc(A.gT + (size_t)m * A.H + h, A.nh, acc);
 }
 
-// waves per (node, channel block): TMDNET_TN_S (A/B switch; 1, 2 or 4, default 4)
+// waves per (node, channel block): TMDNET_TN_S (A/B switch; 1, 2 or 4, default 4), read once per process
+// (not per launch: the launch-bound C3 step, and a captured graph must not change form behind its back)
 static int slots() {
-  const char* e = getenv("TMDNET_TN_S");
-  const int s = e ? atoi(e) : 4;
-  return s >= 4 ? 4 : s >= 2 ? 2 : 1;
+  static const int s = [] {
+    const char* e = getenv("TMDNET_TN_S");
+    const int v = e ? atoi(e) : 4;
+    return v >= 4 ? 4 : v >= 2 ? 2 : 1;
+  }();
+  return s;
 }
 
 // one S-wave block per (node, channel block) of A.nblk
@@ -423,8 +427,11 @@ static int launch_embed_bwd_dst(const Args<T>& A, hipStream_t st) {
   const dim3 g((unsigned)A.n);
   // its per-edge channel sums make each edge a longer chain than in the other kernels: 8 waves per node
   // (C3: 9.4 vs 13.3 us at 4); TMDNET_TN_EBD_S = 1 / 2 / 4 for A/B
-  const char* e8 = getenv("TMDNET_TN_EBD_S");
-  const int s = e8 ? (atoi(e8) >= 8 ? 8 : atoi(e8) >= 4 ? 4 : atoi(e8) >= 2 ? 2 : 1) : 8;
+  static const int s = [] {  // read once per process (as slots())
+    const char* e8 = getenv("TMDNET_TN_EBD_S");
+    const int v = e8 ? atoi(e8) : 8;
+    return v >= 8 ? 8 : v >= 4 ? 4 : v >= 2 ? 2 : 1;
+  }();
 #define TMD_EBD(NB)                                                                                   \
   if (s == 1) hipLaunchKernelGGL((k_embed_bwd_dst<T, NB, 1>), g, dim3(64), 0, st, A);                 \
   else if (s == 2) hipLaunchKernelGGL((k_embed_bwd_dst<T, NB, 2>), g, dim3(128), 0, st, A);           \

@@ -25,6 +25,7 @@ class Custom(torch.utils.data.Dataset):
                 raise AssertionError(f"Number of coordinate files {n} does not match number of {name} files "
                                      f"{len(files)}.")
         self.index = []
+        self._n_atoms = []  # atoms per file group (every frame of a group has the same atoms)
         for i in range(n):
             coords = np.load(self.coordfiles[i], mmap_mode="r")
             embed = np.load(self.embedfiles[i])
@@ -42,20 +43,36 @@ class Custom(torch.utils.data.Dataset):
                     raise AssertionError(f"Data shape of coordinate file {i} {coords.shape} does not match the "
                                          f"shape of force file {i} {fo.shape}.")
             self.index.extend((i, k) for k in range(coords.shape[0]))
+            self._n_atoms.append(int(embed.shape[0]))
 
     def __len__(self):
         return len(self.index)
 
+    # open file groups kept per process (memory maps duplicate their file descriptor: a dataset of
+    # thousands of groups must not hold them all open)
+    MAX_OPEN_GROUPS = 64
+
+    def atom_counts(self):
+        """Atoms of every sample, without opening any sample (default_atom_buckets)."""
+        return [self._n_atoms[f] for f, _ in self.index]
+
     def _file(self, f):
         """The memory maps / atom types of file group f, opened once per process (the loader's worker
-        processes each open their own on first use): a sample costs a few array copies, not four file
-        opens."""
-        mm = self.__dict__.setdefault("_mm", {})
-        if f not in mm:
-            mm[f] = (np.load(self.coordfiles[f], mmap_mode="r"),
-                     torch.from_numpy(np.load(self.embedfiles[f]).astype(np.int64)),
-                     np.load(self.energyfiles[f], mmap_mode="r") if self.has_energies else None,
-                     np.load(self.forcefiles[f], mmap_mode="r") if self.has_forces else None)
+        processes each open their own on first use) and kept in a small LRU: a sample costs a few array
+        copies, not four file opens."""
+        from collections import OrderedDict
+        mm = self.__dict__.get("_mm")
+        if mm is None:
+            mm = self.__dict__["_mm"] = OrderedDict()
+        if f in mm:
+            mm.move_to_end(f)
+            return mm[f]
+        while len(mm) >= self.MAX_OPEN_GROUPS:
+            mm.popitem(last=False)
+        mm[f] = (np.load(self.coordfiles[f], mmap_mode="r"),
+                 torch.from_numpy(np.load(self.embedfiles[f]).astype(np.int64)),
+                 np.load(self.energyfiles[f], mmap_mode="r") if self.has_energies else None,
+                 np.load(self.forcefiles[f], mmap_mode="r") if self.has_forces else None)
         return mm[f]
 
     def __getstate__(self):  # memory maps are per process

@@ -154,6 +154,12 @@ class EquivariantScalar(OutputModel):
                    b.update_net[2].weight, b.update_net[2].bias]
         return ps
 
+    def _gated(self, x, v):
+        """(scalar, vector) outputs of the two gated blocks."""
+        for block in self.output_network:
+            x, v = block(x, v)
+        return x, v
+
     def pre_reduce(self, x, v, z, pos, batch):
         if torch.jit.is_scripting():  # reference output_modules.py:98-103
             for layer in self.output_network:
@@ -168,72 +174,89 @@ class EquivariantScalar(OutputModel):
         return x + v.sum() * 0
 
 
-class DipoleMoment(Scalar):
+# ----------------------------------------------------------------------------- secondary heads
+# Dipole / spatial-extent / vector heads (interface of reference output_modules.py:117-207: class names and
+# the state_dict layout of their networks).  Not on the hot path (SURVEY §8 names only the energy heads); they
+# run as plain tensor code.  Shared pieces: the mass-weighted centre of each molecule, and the gated blocks'
+# (scalar, vector) output of EquivariantScalar.
+
+
+def _offsets_from_centre(masses, z, pos, batch):
+    """pos minus its molecule's centre of mass, one row per atom."""
+    m = masses.index_select(0, z).unsqueeze(1)
+    n_mol = int(batch.max()) + 1 if batch.numel() else 0
+    acc = pos.new_zeros(n_mol, 4).index_add_(0, batch, torch.cat([pos * m, m], dim=1))
+    centre = acc[:, :3] / acc[:, 3:]
+    return pos - centre.index_select(0, batch)
+
+
+class _MassTable(nn.Module):
+    """Holds the ``atomic_mass`` buffer (a state_dict key of the reference heads)."""
+
+    def _add_masses(self, dtype):
+        self.register_buffer("atomic_mass", torch.as_tensor(atomic_masses, dtype=dtype))
+
+
+class DipoleMoment(Scalar, _MassTable):
+    """Per-atom partial charges q_i from the scalar network; reduces sum_i q_i (r_i - r_com) and returns its norm."""
+
     def __init__(self, hidden_channels, activation="silu", reduce_op="sum", dtype=torch.float):
         super().__init__(hidden_channels, activation, allow_prior_model=False, reduce_op=reduce_op, dtype=dtype)
-        self.register_buffer("atomic_mass", torch.from_numpy(atomic_masses).to(dtype))
+        self._add_masses(dtype)
 
     def pre_reduce(self, x, v: Optional[torch.Tensor], z, pos, batch):
-        x = self.output_network(x)
-        mass = self.atomic_mass[z].view(-1, 1)
-        c = scatter(mass * pos, batch, dim=0) / scatter(mass, batch, dim=0)
-        return x * (pos - c[batch])
+        charges = self.output_network(x)
+        return charges * _offsets_from_centre(self.atomic_mass, z, pos, batch)
 
     def post_reduce(self, x):
-        return torch.norm(x, dim=-1, keepdim=True)
+        return x.norm(dim=-1, keepdim=True)
 
 
-class EquivariantDipoleMoment(EquivariantScalar):
+class EquivariantDipoleMoment(EquivariantScalar, _MassTable):
+    """Charges plus a per-atom dipole vector from the gated blocks: q_i (r_i - r_com) + mu_i, then the norm."""
+
     def __init__(self, hidden_channels, activation="silu", reduce_op="sum", dtype=torch.float):
         super().__init__(hidden_channels, activation, allow_prior_model=False, reduce_op=reduce_op, dtype=dtype)
-        self.register_buffer("atomic_mass", torch.from_numpy(atomic_masses).to(dtype))
+        self._add_masses(dtype)
 
     def pre_reduce(self, x, v, z, pos, batch):
-        for layer in self.output_network:
-            x, v = layer(x, v)
-        mass = self.atomic_mass[z].view(-1, 1)
-        c = scatter(mass * pos, batch, dim=0) / scatter(mass, batch, dim=0)
-        x = x * (pos - c[batch])
-        return x + v.squeeze()
+        charges, mu = self._gated(x, v)
+        return charges * _offsets_from_centre(self.atomic_mass, z, pos, batch) + mu.squeeze()
 
     def post_reduce(self, x):
-        return torch.norm(x, dim=-1, keepdim=True)
+        return x.norm(dim=-1, keepdim=True)
 
 
-class ElectronicSpatialExtent(OutputModel):
+class ElectronicSpatialExtent(OutputModel, _MassTable):
+    """<R^2> = sum_i q_i |r_i - r_com|^2 with per-atom q_i from a two-layer scalar network."""
+
     def __init__(self, hidden_channels, activation="silu", reduce_op="sum", dtype=torch.float):
         super().__init__(allow_prior_model=False, reduce_op=reduce_op)
-        act_class = act_class_mapping[activation]
-        self.output_network = nn.Sequential(
-            nn.Linear(hidden_channels, hidden_channels // 2, dtype=dtype),
-            act_class(),
-            nn.Linear(hidden_channels // 2, 1, dtype=dtype),
-        )
-        self.register_buffer("atomic_mass", torch.from_numpy(atomic_masses).to(dtype))
+        half = hidden_channels // 2
+        self.output_network = nn.Sequential(nn.Linear(hidden_channels, half, dtype=dtype),
+                                            act_class_mapping[activation](), nn.Linear(half, 1, dtype=dtype))
+        self._add_masses(dtype)
         self.reset_parameters()
 
     def reset_parameters(self):
-        nn.init.xavier_uniform_(self.output_network[0].weight)
-        self.output_network[0].bias.data.fill_(0)
-        nn.init.xavier_uniform_(self.output_network[2].weight)
-        self.output_network[2].bias.data.fill_(0)
+        for lin in (self.output_network[0], self.output_network[2]):
+            nn.init.xavier_uniform_(lin.weight)
+            nn.init.zeros_(lin.bias)
 
     def pre_reduce(self, x, v: Optional[torch.Tensor], z, pos, batch):
-        x = self.output_network(x)
-        mass = self.atomic_mass[z].view(-1, 1)
-        c = scatter(mass * pos, batch, dim=0) / scatter(mass, batch, dim=0)
-        return torch.norm(pos - c[batch], dim=1, keepdim=True) ** 2 * x
+        r2 = _offsets_from_centre(self.atomic_mass, z, pos, batch).pow(2).sum(dim=1, keepdim=True)
+        return self.output_network(x) * r2
 
 
 class EquivariantElectronicSpatialExtent(ElectronicSpatialExtent):
-    pass
+    """Same head for equivariant models (the vector features are not used)."""
 
 
 class EquivariantVectorOutput(EquivariantScalar):
+    """One vector per atom: the vector output of the gated blocks."""
+
     def __init__(self, hidden_channels, activation="silu", reduce_op="sum", dtype=torch.float):
         super().__init__(hidden_channels, activation, allow_prior_model=False, reduce_op="sum", dtype=dtype)
 
     def pre_reduce(self, x, v, z, pos, batch):
-        for layer in self.output_network:
-            x, v = layer(x, v)
-        return v.squeeze()
+        return self._gated(x, v)[1].squeeze()

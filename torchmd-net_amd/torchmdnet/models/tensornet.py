@@ -78,6 +78,8 @@ def _s_mix3(c: Tensor, w0: Tensor, w1: Tensor, w2: Tensor) -> Tensor:
 
 
 class TensorNet(nn.Module):
+    __jit_ignored_attributes__ = ["_pad_shift"]  # host-side padded-training state (eager path only)
+
     def __init__(self, hidden_channels=128, num_layers=2, num_rbf=32, rbf_type="expnorm",
                  trainable_rbf=False, activation="silu", cutoff_lower=0, cutoff_upper=4.5,
                  max_num_neighbors=64, max_z=128, equivariance_invariance_group="O(3)",
@@ -112,6 +114,9 @@ class TensorNet(nn.Module):
         self.act = act_class()
         self.static_shapes = static_shapes
         self.reorder_atoms = True
+        # padded batches (training.PaddedBatches): (device int32 [1], host int) correction of the pair count
+        # that keeps atom 0's static_shapes padding multiplicity that of the REAL atoms (ghosts excluded)
+        self._pad_shift: Optional[Tuple[Tensor, int]] = None
         self.distance = OptimizedDistance(cutoff_lower, cutoff_upper, max_num_pairs=-max_num_neighbors,
                                           return_vecs=True, loop=True, check_errors=False,
                                           resize_to_fit=not self.static_shapes, long_edge_index=True)
@@ -173,11 +178,14 @@ class TensorNet(nn.Module):
     def _forward(self, z: Tensor, pos: Tensor, batch: Tensor) -> Tensor:
         graph = self.distance.graph(pos, batch)
         cap = self.distance._max_pairs(pos.shape[0])
+        shift = self._pad_shift
         if self.static_shapes and graph.static:
             # capture mode: the padding count stays on the device (no host sync)
-            graph.self0_dev = (graph.num_pairs_dev, cap)
+            npd = graph.num_pairs_dev if shift is None else graph.num_pairs_dev + shift[0]
+            graph.self0_dev = (npd, cap)
         else:
-            graph.self0_mult = float(1 + max(0, cap - graph.num_pairs)) if self.static_shapes else 1.0
+            n_eff = graph.num_pairs + (0 if shift is None else shift[1])
+            graph.self0_mult = float(1 + max(0, cap - n_eff)) if self.static_shapes else 1.0
         de = self.distance_expansion
         k = 1 + len(self.layers)  # consumers of the rbf / cutoff rows: the embedding and every layer
         if self.trainable_rbf and torch.is_grad_enabled():

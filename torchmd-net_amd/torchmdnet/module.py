@@ -154,13 +154,32 @@ def _val_loss(metrics):
     return metrics.get("val_total_mse_loss", metrics.get("val_total_l1_loss"))
 
 
-def default_atom_buckets(dataset, batch_size, n_probe=512, growth=1.125):
+def _atom_counts(dataset):
+    """Atoms of every sample: the dataset's own ``atom_counts()`` when it has one (through Subset /
+    FloatCast wrappers), else one pass over the samples."""
+    idx = None
+    ds = dataset
+    while True:
+        if isinstance(ds, torch.utils.data.Subset):
+            idx = [ds.indices[i] for i in idx] if idx is not None else list(ds.indices)
+            ds = ds.dataset
+        elif hasattr(ds, "dataset") and not hasattr(ds, "atom_counts"):
+            ds = ds.dataset
+        else:
+            break
+    counts = getattr(ds, "atom_counts", None)
+    if counts is not None:
+        c = counts()
+        return [c[i] for i in idx] if idx is not None else list(c)
+    return [int(dataset[i].z.shape[0]) for i in range(len(dataset))]
+
+
+def default_atom_buckets(dataset, batch_size, growth=1.125):
     """Atom capacities of the padded training batches: geometric steps (``growth``) from a little
-    below the mean batch size to ``batch_size`` x the largest molecule seen in a probe of the dataset."""
+    below the mean batch size to ``batch_size`` x the largest molecule of the dataset (every sample is
+    counted: a capacity below the largest possible batch would fail mid-epoch)."""
     import math
-    n = len(dataset)
-    step = max(1, n // n_probe)
-    sizes = [int(dataset[i].z.shape[0]) for i in range(0, n, step)]
+    sizes = _atom_counts(dataset)
     mean, big = sum(sizes) / len(sizes), max(sizes)
     lo, hi = int(0.85 * mean * batch_size), big * batch_size + 1
     out, a = [], max(32, lo)

@@ -346,8 +346,21 @@ def padded_losses(pred, neg_dy, b):
     """(L_y, L_f): the reference's mean-squared energy / force losses of a padded batch (weights 0 on
     the padding, so the sums are means over the real entries)."""
     ly = (b.wy * (pred - b.y) ** 2).sum() if "y" in b else pred.sum() * 0
-    lf = (b.wf * (neg_dy - b.neg_dy) ** 2).sum() if "neg_dy" in b else neg_dy.sum() * 0
+    # an energy-only model (derivative=False) returns no forces: the force term is a zero scalar
+    lf = (b.wf * (neg_dy - b.neg_dy) ** 2).sum() if ("neg_dy" in b and neg_dy is not None) else pred.sum() * 0
     return ly, lf
+
+
+def pad_shift(model, n_atoms, capacity):
+    """Host value of TensorNet's padded-batch pair-count correction (``TensorNet._pad_shift``).
+
+    The reference's static_shapes mode sends every unused slot of the ``max_num_pairs(N)`` capacity to
+    atom 0 as a (0, 0) edge (tensornet.py:215-221).  For the real molecules alone that is
+    ``max_pairs(n_real) - pairs_real`` slots; a padded batch of ``capacity`` atoms has
+    ``max_pairs(capacity) - (pairs_real + n_ghosts)`` (each ghost has its self loop).  Adding
+    ``max_pairs(capacity) - max_pairs(n_real) - n_ghosts`` to the pair count restores the real count."""
+    d = model.representation_model.distance
+    return d._max_pairs(int(capacity)) - d._max_pairs(int(n_atoms)) - (int(capacity) - int(n_atoms))
 
 
 class _BucketStep:
@@ -360,6 +373,12 @@ class _BucketStep:
         self.inputs = {k: getattr(b, k).to(dev).clone() for k in ("z", "pos", "batch", "wy", "wf", "y", "neg_dy")
                        if k in b}
         rep = model.representation_model
+        self.model = model
+        # TensorNet static_shapes: its atom-0 padding multiplicity must count the real atoms only
+        self.pad_shift = None
+        if getattr(rep, "static_shapes", False) and hasattr(rep, "_pad_shift"):
+            self.pad_shift = torch.zeros(1, dtype=torch.int32, device=dev)
+            self._set_shift(b)
         dists = _distance_modules(model)
         bs = _Static(self.inputs)
 
@@ -405,12 +424,21 @@ class _BucketStep:
         torch.cuda.synchronize(dev)
         for d in dists:
             d.static_capacity = None
+        if self.pad_shift is not None:
+            rep._pad_shift = None  # the graph keeps reading self.pad_shift; eager calls see no shift
         del grads, pairs
+
+    def _set_shift(self, b):
+        v = pad_shift(self.model, b.n_atoms, b.capacity)
+        self.pad_shift.fill_(v)
+        self.model.representation_model._pad_shift = (self.pad_shift, v)
 
     def load(self, b):
         with torch.no_grad():
             for k, dst in self.inputs.items():
                 dst.copy_(getattr(b, k), non_blocking=True)
+            if self.pad_shift is not None:
+                self.pad_shift.fill_(pad_shift(self.model, b.n_atoms, b.capacity))
 
 
 class _Static:
