@@ -137,3 +137,54 @@ def test_gated_eq_gradients_isolated_atom():
     assert not deriv.isnan().any()  # (sum F = 0 by translation invariance: this gradient is 0)
     (deriv2,) = torch.autograd.grad(forces.pow(2).sum(), emb)  # a force loss that does depend on it
     assert torch.isfinite(deriv2).all() and deriv2.abs().sum() > 0
+
+
+@pytest.mark.parametrize("R", [16, 32, 50, 64])
+@pytest.mark.parametrize("rbf", ["expnorm", "gauss"])
+@pytest.mark.parametrize("dtype,tol", [(torch.float64, 1e-11), (torch.float32, 2e-5)])
+@pytest.mark.parametrize("slots", [1, 3])
+def test_edge_geometry_backward_matches_autograd(R, rbf, dtype, tol, slots):
+    """tmdnet_edge_geom_bwd_multi (the lane-parallel k_bwd_v: R = 16 / 32 / 64; R = 50 takes the
+    wave-per-edge form) against autograd of the formulas (reference models/utils.py:272-390, the unit
+    vectors torchmd_et.py:173-174): g_r and g_deltas for 1 or 3 gradient slots of rbf and cutoff, with
+    self loops and a lower cutoff."""
+    from torchmdnet import kernels
+    from oracle import model_oracle as O
+    cl, cu = 0.5, 5.0
+    g = torch.Generator().manual_seed(R + slots)
+    pos = torch.randn(300, 3, generator=g, dtype=torch.float64) * 2.0
+    batch = torch.arange(6).repeat_interleave(50)
+    gr = kernels.build_graph(pos.to(dtype).to(DEV), batch.to(DEV), cl, cu, 300 * 300, loop=True)
+    E = gr.num_pairs
+    if rbf == "expnorm":
+        start = np.exp(-cu + cl)
+        mu = torch.linspace(start, 1.0, R, dtype=torch.float64)
+        beta = torch.full((R,), (2.0 / R * (1 - start)) ** -2, dtype=torch.float64)
+        code = kernels.nat.RBF_EXPNORM
+    else:
+        mu = torch.linspace(cl, cu, R, dtype=torch.float64)
+        beta = torch.full((1,), -0.5 / float(mu[1] - mu[0]) ** 2, dtype=torch.float64)
+        code = kernels.nat.RBF_GAUSS
+    dl = gr.deltas.detach().clone().requires_grad_(True)
+    r = gr.distances.detach().clone().requires_grad_(True)
+    outs = kernels._EdgeGeom.apply(dl, r, gr, mu.to(dtype).to(DEV), beta.to(dtype).to(DEV), cl, cu, code,
+                                   (True, True, True), None, (slots, slots))
+    f, C, u = outs[:3]
+    gens = [torch.randn(t.shape, generator=g, dtype=torch.float64) for t in outs]
+    loss = sum((t * w.to(dtype).to(DEV)).sum() for t, w in zip(outs, gens))
+    g_dl, g_r = torch.autograd.grad(loss, [dl, r])
+    # composite in fp64 on the CPU
+    dl64 = gr.deltas.detach().double().cpu().requires_grad_(True)
+    r64 = gr.distances.detach().double().cpu().requires_grad_(True)
+    f64 = O.expnorm(r64, mu, beta, cl, cu) if rbf == "expnorm" else O.gauss(r64, mu, beta[0])
+    C64 = O.cosine_cutoff(r64, cl, cu)
+    self_e = (gr.src == gr.dst).cpu().unsqueeze(1)
+    nrm = torch.where(self_e, torch.ones_like(r64).unsqueeze(1), dl64.norm(dim=1, keepdim=True))
+    u64 = torch.where(self_e, dl64, dl64 / nrm)
+    outs64 = [f64, C64, u64] + [f64] * (slots - 1) + [C64] * (slots - 1)
+    loss64 = sum((t * w).sum() for t, w in zip(outs64, gens))
+    e_dl, e_r = torch.autograd.grad(loss64, [dl64, r64])
+    assert E > 1000
+    rel = lambda a, b: float((a.double().cpu() - b).abs().max() / b.abs().max().clamp_min(1e-30))  # noqa: E731
+    assert rel(g_r, e_r) < tol, rel(g_r, e_r)
+    assert rel(g_dl, e_dl) < tol, rel(g_dl, e_dl)

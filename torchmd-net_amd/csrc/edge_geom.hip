@@ -195,6 +195,93 @@ __global__ __launch_bounds__(256) void k_bwd(Cfg<T> P, GIn<T> G, const T* __rest
   }
 }
 
+// Lane-parallel form of k_bwd (the default): LPE = R / KPL lanes per edge, each lane owning KPL = 16 /
+// sizeof(T) consecutive basis indices (one 16-byte load per gradient slot), 64 / LPE edges per wave, so
+// a wave reads 64 / LPE whole gradient rows as one coalesced stream.  The per-edge terms of the basis
+// (exp(alpha (cl - r)), the cosine cutoff and its derivative) are formed once per lane instead of once
+// per basis index; the lane group's partial sums meet in an xor butterfly (identical in every lane),
+// and the group's lanes 0 / 1..3 write g_r and the three unit-vector Jacobian components.
+template <typename T, int LPE>
+__global__ __launch_bounds__(256) void k_bwd_v(Cfg<T> P, GIn<T> G, const T* __restrict__ gu, T* __restrict__ gr,
+                                               T* __restrict__ gdl) {
+  constexpr int KPL = 16 / (int)sizeof(T), EPW = TMD_WAVE / LPE;
+  using V = T __attribute__((ext_vector_type(KPL)));
+  const int lane = lane_id(), sub = lane % LPE, slot = lane / LPE;
+  const long long nw = (long long)gridDim.x * (blockDim.x / TMD_WAVE);
+  const bool anyf = G.f[0] || G.f[1] || G.f[2], anyc = G.c[0] || G.c[1] || G.c[2];
+  const bool expnorm = P.type == TMDNET_RBF_EXPNORM;
+  for (long long w = (long long)blockIdx.x * (blockDim.x / TMD_WAVE) + threadIdx.x / TMD_WAVE;
+       w * EPW < P.E; w += nw) {
+    const long long e = w * EPW + slot;
+    const bool live = e < P.E;
+    const T r = live ? P.r[e] : T(0);
+    T acc = T(0);
+    if (anyf) {
+      const long long o = e * P.R + (long long)sub * KPL;
+      V g{};
+      if (live) {
+        if (G.f[0]) g = *reinterpret_cast<const V*>(G.f[0] + o);
+        if (G.f[1]) g += *reinterpret_cast<const V*>(G.f[1] + o);
+        if (G.f[2]) g += *reinterpret_cast<const V*>(G.f[2] + o);
+      }
+      if (expnorm) {
+        T c0, dc0;
+        cosine_cutoff<T>(r, T(0), P.cu, c0, dc0);
+        const T u = exp(P.alpha * (P.cl - r));
+        const T du = -P.alpha * u;
+#pragma unroll
+        for (int i = 0; i < KPL; ++i) {
+          const int k = sub * KPL + i;
+          const T b = P.beta[k];
+          const T z = u - P.mu[k];
+          const T gk = exp(-b * z * z);
+          acc += g[i] * gk * (dc0 + c0 * (T(-2) * b * z * du));
+        }
+      } else {
+        const T coeff = P.beta[0];
+#pragma unroll
+        for (int i = 0; i < KPL; ++i) {
+          const T z = r - P.mu[sub * KPL + i];
+          acc += g[i] * exp(coeff * z * z) * T(2) * coeff * z;
+        }
+      }
+#pragma unroll
+      for (int m = LPE / 2; m > 0; m >>= 1) acc += __shfl_xor(acc, m);
+    }
+    if (!live) continue;
+    if (sub == 0) {
+      if (anyc) {
+        T c, dc;
+        cosine_cutoff<T>(r, P.cl, P.cu, c, dc);
+        T g = G.c[0] ? G.c[0][e] : T(0);
+        if (G.c[1]) g += G.c[1][e];
+        if (G.c[2]) g += G.c[2][e];
+        acc += g * dc;
+      }
+      gr[e] = acc;
+    }
+    // the unit vector's Jacobian: component j = sub - 1 by lanes 1..3 of the group (LPE >= 4)
+    const int j = sub - 1;
+    if (j >= 0 && j < 3) {
+      T out = T(0);
+      if (gu) {
+        const T x = P.dl[3 * e], y = P.dl[3 * e + 1], zz = P.dl[3 * e + 2];
+        const T a = gu[3 * e], b = gu[3 * e + 1], c = gu[3 * e + 2];
+        const T gj = j == 0 ? a : j == 1 ? b : c;
+        if (P.src[e] == P.dst[e]) {
+          out = gj;
+        } else {
+          const T n = sqrt(x * x + y * y + zz * zz);
+          const T dot = (x * a + y * b + zz * c) / n;
+          const T uj = (j == 0 ? x : j == 1 ? y : zz) / n;
+          out = (gj - uj * dot) / n;
+        }
+      }
+      gdl[3 * e + j] = out;
+    }
+  }
+}
+
 // Second order of k_bwd (force-loss training): the VJP of (g_dl, g_r) = bwd(dl, r, gf, gC, gu) for
 // cotangents (gg_dl, gg_r).  With u = dl/n (n = |dl|, non-self edges), P = I - u u^T, g_dl = P gu / n:
 //   d_gf[k] = gg_r f_k'(r)      d_gC = gg_r C'(r)      d_r = gg_r (sum_k gf_k f_k''(r) + gC C''(r))
@@ -337,22 +424,35 @@ extern "C" int tmdnet_edge_geom_bwd_multi(int dtype, int n_edges, int num_rbf, i
   if (n_edges <= 0) return kOk;
   hipStream_t st = (hipStream_t)stream;
   const int tb = 256;
-  const int blocks = (int)std::min<long long>(((long long)n_edges + 3) / 4, 256LL * 64);
-  if (dtype == TMDNET_F32) {
-    auto P = geom::make<float>(n_edges, num_rbf, rbf_type, src, dst, deltas, dist, mu, beta, cutoff_lower, cutoff_upper);
-    geom::GIn<float> G{{(const float*)grad_rbf, (const float*)grad_rbf2, (const float*)grad_rbf3},
-                       {(const float*)grad_cutoff, (const float*)grad_cutoff2, (const float*)grad_cutoff3}};
-    hipLaunchKernelGGL(geom::k_bwd<float>, dim3(blocks), dim3(tb), 0, st, P, G, (const float*)grad_unit,
-                       (float*)grad_dist, (float*)grad_deltas);
-  } else if (dtype == TMDNET_F64) {
-    auto P = geom::make<double>(n_edges, num_rbf, rbf_type, src, dst, deltas, dist, mu, beta, cutoff_lower, cutoff_upper);
-    geom::GIn<double> G{{(const double*)grad_rbf, (const double*)grad_rbf2, (const double*)grad_rbf3},
-                        {(const double*)grad_cutoff, (const double*)grad_cutoff2, (const double*)grad_cutoff3}};
-    hipLaunchKernelGGL(geom::k_bwd<double>, dim3(blocks), dim3(tb), 0, st, P, G, (const double*)grad_unit,
-                       (double*)grad_dist, (double*)grad_deltas);
-  } else {
-    return kUnsupported;
+  // lane-parallel form when R splits into 16-byte lane chunks of 4..64 lanes per edge (every config: R = 16,
+  // 32, 64); the wave-per-edge form otherwise.  Gradient rows must be 16-byte aligned (contiguous [E][R]).
+  const int kpl = dtype == TMDNET_F32 ? 4 : 2, lpe = num_rbf / kpl;
+  const bool aligned = !((((uintptr_t)grad_rbf) | ((uintptr_t)grad_rbf2) | ((uintptr_t)grad_rbf3)) & 15);
+  const bool vec = num_rbf % kpl == 0 && (lpe == 4 || lpe == 8 || lpe == 16 || lpe == 32 || lpe == 64) && aligned;
+  const long long waves = vec ? ((long long)n_edges * lpe + TMD_WAVE - 1) / TMD_WAVE : n_edges;
+  const int blocks = (int)std::min<long long>((waves + 3) / 4, 256LL * 64);
+#define TMD_GEOM_BWD(T_)                                                                                           \
+  {                                                                                                                \
+    auto P = geom::make<T_>(n_edges, num_rbf, rbf_type, src, dst, deltas, dist, mu, beta, cutoff_lower, cutoff_upper); \
+    geom::GIn<T_> G{{(const T_*)grad_rbf, (const T_*)grad_rbf2, (const T_*)grad_rbf3},                               \
+                    {(const T_*)grad_cutoff, (const T_*)grad_cutoff2, (const T_*)grad_cutoff3}};                     \
+    const T_* gu_ = (const T_*)grad_unit;                                                                          \
+    T_* gr_ = (T_*)grad_dist;                                                                                      \
+    T_* gd_ = (T_*)grad_deltas;                                                                                    \
+    if (!vec) hipLaunchKernelGGL(geom::k_bwd<T_>, dim3(blocks), dim3(tb), 0, st, P, G, gu_, gr_, gd_);            \
+    else if (lpe == 4) hipLaunchKernelGGL((geom::k_bwd_v<T_, 4>), dim3(blocks), dim3(tb), 0, st, P, G, gu_, gr_, gd_);   \
+    else if (lpe == 8) hipLaunchKernelGGL((geom::k_bwd_v<T_, 8>), dim3(blocks), dim3(tb), 0, st, P, G, gu_, gr_, gd_);   \
+    else if (lpe == 16) hipLaunchKernelGGL((geom::k_bwd_v<T_, 16>), dim3(blocks), dim3(tb), 0, st, P, G, gu_, gr_, gd_); \
+    else if (lpe == 32) hipLaunchKernelGGL((geom::k_bwd_v<T_, 32>), dim3(blocks), dim3(tb), 0, st, P, G, gu_, gr_, gd_); \
+    else hipLaunchKernelGGL((geom::k_bwd_v<T_, 64>), dim3(blocks), dim3(tb), 0, st, P, G, gu_, gr_, gd_);                \
   }
+  if (dtype == TMDNET_F32)
+    TMD_GEOM_BWD(float)
+  else if (dtype == TMDNET_F64)
+    TMD_GEOM_BWD(double)
+  else
+    return kUnsupported;
+#undef TMD_GEOM_BWD
   return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
 }
 
