@@ -610,6 +610,16 @@ int tmdnet_embedding_bwd_f32(int n, int H, int num_types, const int64_t* z, int 
  * K = 32 or 64 (split: K % 4 == 0), N % 16 == 0, lda / ldc multiples of 4, 16-byte aligned A / Wp / C /
  * bias; else TMDNET_UNSUPPORTED (callers use the library GEMM).  Replaces the nn.Linear of
  * torchmd_et.py:287-288 over the edges. */
+/* Large-row fp32 GEMMs at fp32 accuracy on the bf16 MFMA (the node feature mixes of C5-size systems:
+ * EquivariantMultiHeadAttention q/k/v, vec_proj, o_proj Linears and their input gradients,
+ * reference torchmd_et.py:273-278, 309; the NeighborEmbedding distance_proj, models/utils.py:98-103):
+ *   tmdnet_split_t_f32: Bp [3][N][K] = the exact bf16 pieces of B^T for a [K][N] right operand (ldb);
+ *     (a [N][K] Linear weight is split by tmdnet_proj_split_f32);
+ *   tmdnet_gemm_x3_f32: C [M][N] = beta C + A [M][K] Bp^T + bias (nullable) -- K % 32 == 0, N % 16 == 0,
+ *     16-byte aligned rows / pointers, otherwise TMDNET_UNSUPPORTED (nothing launched). */
+int tmdnet_split_t_f32(int N, int K, const void* B, int ldb, void* Bp, void* stream);
+int tmdnet_gemm_x3_f32(int M, int N, int K, const void* A, int lda, const void* Bp, const void* bias, void* C,
+                       int ldc, int beta, void* stream);
 int tmdnet_proj_split_f32(int N, int K, const void* W, int ldw, void* Wp, void* stream);
 int tmdnet_proj_f32(int M, int N, int K, const void* A, int lda, const void* Wp, long long piece_stride,
                     const void* bias, void* C, int ldc, void* stream);

@@ -102,3 +102,52 @@ def test_proj_outside_envelope_falls_back():
     assert torch.equal(kernels.proj(A, W), A @ W.t())
     Ad, Wd = A.double(), torch.randn(32, 64, device=DEV, dtype=torch.float64)
     assert torch.equal(kernels.proj(Ad, Wd), Ad @ Wd.t())
+
+
+# ----------------------------------------------------------------------------- large-row node-mix GEMM
+@pytest.mark.parametrize("M", [16385, 50001])
+@pytest.mark.parametrize("N,K,tb", [(640, 128, True), (384, 128, True), (64, 128, True), (128, 640, False),
+                                    (128, 384, False), (64, 128, False), (144, 96, True)])
+@pytest.mark.parametrize("bias,beta", [(True, False), (False, True)])
+def test_gemm_x3_large_rows_match_fp64_like_library(M, N, K, tb, bias, beta):
+    """tmdnet_gemm_x3_f32 (the node feature mixes above GEMM_MAX_ROWS: the forward Linears with a [N][K]
+    weight and the input gradients g W with an untransposed [K][N] right operand, K chunked by 128 / 64,
+    ragged M) against fp64: no worse than 2x the library fp32 GEMM's error plus a few output ulps;
+    beta accumulates into C."""
+    from torchmdnet import kernels
+    torch.manual_seed(M + N + K)
+    A = torch.randn(M, K, device=DEV)
+    B = torch.randn(N, K, device=DEV) / K ** 0.5 if tb else torch.randn(K, N, device=DEV) / K ** 0.5
+    b = torch.randn(N, device=DEV) if bias else None
+    C0 = torch.randn(M, N, device=DEV)
+    C = C0.clone()
+    assert kernels.gemm_x3(A, B, tb, b, C, beta)
+    Bop = B.t() if tb else B
+    ref = A.double() @ Bop.double()
+    lib = A @ Bop
+    if b is not None:
+        ref = ref + b.double()
+        lib = lib + b
+    if beta:
+        ref = ref + C0.double()
+        lib = lib + C0
+    e_lib = float((lib.double() - ref).abs().max())
+    e_got = float((C.double() - ref).abs().max())
+    scale = float(ref.abs().max())
+    assert e_got <= 2 * e_lib + 4 * 2.0 ** -24 * scale, (e_got, e_lib, scale)
+
+
+def test_gemm_group_large_rows_takes_the_x3_kernel(monkeypatch):
+    """gemm_group above GEMM_MAX_ROWS: every fp32 problem on tmdnet_gemm_x3_f32 (no library GEMM)."""
+    from torchmdnet import kernels
+    seen = []
+    orig = kernels.gemm_x3
+    monkeypatch.setattr(kernels, "gemm_x3", lambda *a: seen.append(1) or orig(*a))
+    monkeypatch.setattr(torch, "mm", lambda *a, **k: (_ for _ in ()).throw(AssertionError("library GEMM")))
+    monkeypatch.setattr(torch, "addmm", lambda *a, **k: (_ for _ in ()).throw(AssertionError("library GEMM")))
+    M = kernels.GEMM_MAX_ROWS + 100
+    A = torch.randn(M, 128, device=DEV)
+    W1, W2 = torch.randn(640, 128, device=DEV), torch.randn(384, 128, device=DEV)
+    C1, C2 = torch.empty(M, 640, device=DEV), torch.empty(M, 384, device=DEV)
+    kernels.gemm_group([(A, W1, True, None, C1, False), (A, W2, True, None, C2, False)])
+    assert len(seen) == 2

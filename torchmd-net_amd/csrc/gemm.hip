@@ -813,6 +813,120 @@ __global__ __launch_bounds__(256) void k_proj_x3(Args P) {
   }
 }
 
+// B [K][N] (row-major, ldb) -> the three exact bf16 pieces of B^T, Bp [3][N][K]: the split of a weight that
+// multiplies from the right untransposed (an input gradient g_y W of a Linear y = x W^T), so that
+// k_gemm_x3 reads it as the k-contiguous [N][K] operand.  One thread per 4 consecutive k of one n.
+__global__ __launch_bounds__(256) void k_split_t(int N, int K, const float* B, int ldb, unsigned short* Bp) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= N * (K / 4)) return;
+  const int k = (i / N) * 4, n = i % N;  // consecutive threads: consecutive n (coalesced reads of B rows)
+  const float x[4] = {B[(size_t)k * ldb + n], B[(size_t)(k + 1) * ldb + n], B[(size_t)(k + 2) * ldb + n],
+                      B[(size_t)(k + 3) * ldb + n]};
+  unsigned h[4], m[4], l[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) split3(x[j], h[j], m[j], l[j]);
+  const size_t o = (size_t)n * K + k, ps = (size_t)N * K;
+  *reinterpret_cast<uint2*>(Bp + o) = make_uint2((h[0] >> 16) | h[1], (h[2] >> 16) | h[3]);
+  *reinterpret_cast<uint2*>(Bp + ps + o) = make_uint2((m[0] >> 16) | m[1], (m[2] >> 16) | m[3]);
+  *reinterpret_cast<uint2*>(Bp + 2 * ps + o) = make_uint2((l[0] >> 16) | l[1], (l[2] >> 16) | l[3]);
+}
+
+// Large-M fp32 GEMM on the bf16 MFMA at fp32 accuracy (the node feature mixes of C5-size systems, where
+// the grouped split-K k_gemm runs out of its envelope): C [M][N] = beta C + A [M][K] Bp^T + bias, Bp the
+// pre-split [3][N][K] pieces (k_proj_split of a Linear weight, or k_split_t of an untransposed right
+// operand).  k_proj_x3's scheme -- A split into three bf16 pieces in registers, the six products with
+// i + j <= 2 summed small first, W as the MFMA's A operand so a lane's four accumulator rows are four
+// consecutive output columns (one 16-byte store) -- with K walked in 128- (or 64-) wide chunks (any K % 32 == 0:
+// the input gradients have K = 3H / 5H): per chunk the workgroup stages its BN columns' pieces of the
+// chunk in LDS (two barriers) and each wave splits its MB 16-row blocks of the chunk; the accumulators of
+// all BN columns stay in registers across chunks.
+struct XArgs {
+  int M, N, K, lda, ldc, beta;
+  const float* A;
+  const unsigned short* Bp;
+  const float* bias;
+  float* C;
+};
+template <int MB, int BN>
+__global__ __launch_bounds__(256) void k_gemm_x3(XArgs P) {
+  // K chunk staged per barrier pair: 128 (64 at BN = 128) -> ~52 KB of LDS, 3 workgroups per CU
+  constexpr int KC = BN >= 128 ? 64 : 128, LD = KC + 8, NB = BN / 16;
+  __shared__ __attribute__((aligned(16))) unsigned short w[3][BN][LD];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int n0 = blockIdx.x * BN;
+  const int m0 = (blockIdx.y * 4 + wave) * (16 * MB);
+  const int kq = 8 * (lane >> 4);
+  const size_t ps = (size_t)P.N * P.K;
+  f4 acc[NB][MB];
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) acc[nb][mb] = f4{0.f, 0.f, 0.f, 0.f};
+  // A rows of this wave: row m0 + 16 mb + (lane & 15), k = 32 ks + kq .. + 7 (two 16-byte loads per
+  // k-step and row block), the next k-step's loads in flight while this one's MFMAs run
+  const float* arow[MB];
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb) arow[mb] = P.A + (size_t)min(m0 + 16 * mb + (lane & 15), P.M - 1) * P.lda + kq;
+  float4 an[MB][2];
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb) {
+    an[mb][0] = *reinterpret_cast<const float4*>(arow[mb]);
+    an[mb][1] = *reinterpret_cast<const float4*>(arow[mb] + 4);
+  }
+  constexpr int TW[6] = {2, 1, 0, 1, 0, 0}, TA[6] = {0, 1, 2, 0, 1, 0};
+  const int nks_all = P.K / 32;
+  for (int kc = 0; kc < P.K; kc += KC) {
+    const int nks = min(KC, P.K - kc) / 32;
+    __syncthreads();  // the previous chunk's LDS reads are done
+    const int ch = nks * 4;  // 16-byte chunks per row of this K chunk
+    for (int c = threadIdx.x; c < 3 * BN * ch; c += 256) {
+      const int p = c / (BN * ch), rc = c % (BN * ch), n = rc / ch, k = (rc % ch) * 8;
+      *reinterpret_cast<u4*>(&w[p][n][k]) =
+          *reinterpret_cast<const u4*>(P.Bp + p * ps + (size_t)min(n0 + n, P.N - 1) * P.K + kc + k);
+    }
+    __syncthreads();
+    for (int ks = 0; ks < nks; ++ks) {
+      bf8 a[MB][3];
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb) split8(an[mb][0], an[mb][1], a[mb]);
+      const int kn = kc / 32 + ks + 1;  // next k-step (clamped: the last one reloads itself)
+      const int ko = 32 * min(kn, nks_all - 1);
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb) {
+        an[mb][0] = *reinterpret_cast<const float4*>(arow[mb] + ko);
+        an[mb][1] = *reinterpret_cast<const float4*>(arow[mb] + ko + 4);
+      }
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) {
+        bf8 b[3];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) b[q] = *reinterpret_cast<const bf8*>(&w[q][16 * nb + (lane & 15)][32 * ks + kq]);
+#pragma unroll
+        for (int t = 0; t < 6; ++t)
+#pragma unroll
+          for (int mb = 0; mb < MB; ++mb)
+            acc[nb][mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[TW[t]], a[mb][TA[t]], acc[nb][mb], 0, 0, 0);
+      }
+    }
+  }
+  if (m0 >= P.M) return;
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) {
+    const int n = n0 + 16 * nb + 4 * (lane >> 4);
+    if (n >= P.N) continue;
+    const f4 bv = P.bias ? *reinterpret_cast<const f4*>(P.bias + n) : f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) {
+      const int m = m0 + 16 * mb + (lane & 15);
+      if (m >= P.M) continue;
+      f4* out = reinterpret_cast<f4*>(P.C + (size_t)m * P.ldc + n);
+      f4 v = acc[nb][mb] + bv;
+      if (P.beta) v += *out;
+      *out = v;
+    }
+  }
+}
+
 }  // namespace proj
 
 // ---------------------------------------------------------------------------------------------------
@@ -1388,5 +1502,38 @@ extern "C" int tmdnet_proj_f32(int M, int N, int K, const void* A, int lda, cons
     if (mb == 4) TMD_PROJ(1, 4, 64); else TMD_PROJ(1, 2, 64);
   }
 #undef TMD_PROJ
+  return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
+}
+
+extern "C" int tmdnet_split_t_f32(int N, int K, const void* B, int ldb, void* Bp, void* stream) {
+  if (N <= 0 || K <= 0 || !B || !Bp) return kBadArgument;
+  if (K % 4 || ldb < N || (((uintptr_t)Bp) & 7)) return kUnsupported;
+  const int n = N * (K / 4);
+  hipLaunchKernelGGL(proj::k_split_t, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, N, K,
+                     (const float*)B, ldb, (unsigned short*)Bp);
+  return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
+}
+
+// C [M][N] = beta C + A [M][K] Bp^T + bias (Bp: tmdnet_proj_split_f32 of a [N][K] weight, or
+// tmdnet_split_t_f32 of a [K][N] right operand); fp32 in / out at fp32 accuracy on the bf16 MFMA.
+// K % 32 == 0, N % 16 == 0, 16-byte aligned rows and pointers.
+extern "C" int tmdnet_gemm_x3_f32(int M, int N, int K, const void* A, int lda, const void* Bp, const void* bias,
+                                  void* C, int ldc, int beta, void* stream) {
+  if (M < 0 || N <= 0 || K <= 0 || !A || !Bp || !C) return kBadArgument;
+  if (M == 0) return kOk;
+  if (K % 32 || N % 16 || lda < K || ldc < N || lda % 4 || ldc % 4) return kUnsupported;
+  if ((((uintptr_t)A) | ((uintptr_t)Bp) | ((uintptr_t)C) | ((uintptr_t)bias)) & 15) return kUnsupported;
+  proj::XArgs P{M, N, K, lda, ldc, beta ? 1 : 0, (const float*)A, (const unsigned short*)Bp, (const float*)bias,
+                (float*)C};
+  hipStream_t st = (hipStream_t)stream;
+  // 64-column tiles for wide outputs (the forward mixes, N = 3H..5H), 128 for the narrow input gradients
+  // (N = H: one column tile, A read once); 2 row blocks per wave (128 rows per workgroup)
+  if (N >= 256 || N <= 64) {
+    const dim3 g((N + 63) / 64, (M + 127) / 128);
+    hipLaunchKernelGGL((proj::k_gemm_x3<2, 64>), g, dim3(256), 0, st, P);
+  } else {
+    const dim3 g((N + 127) / 128, (M + 127) / 128);
+    hipLaunchKernelGGL((proj::k_gemm_x3<2, 128>), g, dim3(256), 0, st, P);
+  }
   return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
 }

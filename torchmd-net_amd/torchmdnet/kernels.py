@@ -1322,12 +1322,55 @@ def gemm_launch(problems):
     return True
 
 
+# above GEMM_MAX_ROWS (C5-size systems) fp32 GEMMs run on tmdnet_gemm_x3_f32 (bf16 MFMA, exact three-piece
+# split, fp32 accuracy); TMDNET_GEMM_BIG=lib keeps the library GEMM there (A/B switch)
+GEMM_BIG = os.environ.get("TMDNET_GEMM_BIG", "x3")
+
+
+def _al16(*ts):
+    return all(t is None or (t.data_ptr() % 16 == 0) for t in ts)
+
+
+def gemm_x3(A, B, tb, bias, C, beta):
+    """``C = beta C + A op(B) + bias`` on ``tmdnet_gemm_x3_f32`` for large row counts: op(B) = B^T for a
+    [N][K] Linear weight (split once per call, tmdnet_proj_split_f32), B for a [K][N] right operand
+    (tmdnet_split_t_f32).  Returns False (nothing launched) outside its envelope (non-fp32, K % 32,
+    N % 16, strides / alignment); the caller then uses the library GEMM."""
+    M, K = A.shape
+    N = C.shape[1]
+    if not (GEMM_BIG == "x3" and A.is_cuda and A.dtype == torch.float32 and B.dtype == torch.float32
+            and C.dtype == torch.float32 and M > 0 and K % 32 == 0 and N % 16 == 0 and A.stride(1) == 1
+            and B.stride(1) == 1 and C.stride(1) == 1 and A.stride(0) % 4 == 0 and C.stride(0) % 4 == 0
+            and B.stride(0) % 4 == 0 and (bias is None or bias.is_contiguous()) and _al16(A, B, C, bias)):
+        return False
+    lib = nat.load()
+    st = nat.stream(A.device)
+    bp = torch.empty((3, N, K), dtype=torch.int16, device=A.device)
+    if tb:
+        rc = lib.tmdnet_proj_split_f32(N, K, B.data_ptr(), B.stride(0), bp.data_ptr(), st)
+    else:
+        rc = lib.tmdnet_split_t_f32(N, K, B.data_ptr(), B.stride(0), bp.data_ptr(), st)
+    if rc == GEMM_UNSUPPORTED:
+        return False
+    nat.check(rc, "tmdnet_split")
+    rc = lib.tmdnet_gemm_x3_f32(M, N, K, A.data_ptr(), A.stride(0), bp.data_ptr(),
+                                None if bias is None else bias.data_ptr(), C.data_ptr(), C.stride(0), int(bool(beta)),
+                                st)
+    if rc == GEMM_UNSUPPORTED:
+        return False
+    nat.check(rc, "tmdnet_gemm_x3_f32")
+    return True
+
+
 def gemm_group(problems):
     """The node feature-mix GEMMs of one step, grouped into one launch when the kernel supports
-    them (fp32); otherwise each through the library GEMM (fp64 parity runs)."""
+    them (fp32, up to GEMM_MAX_ROWS rows); large systems one tmdnet_gemm_x3_f32 launch each; otherwise
+    the library GEMM (fp64 parity runs)."""
     if gemm_launch(problems):
         return
     for A, B, tb, bias, C, beta in problems:
+        if A.shape[0] > GEMM_MAX_ROWS and gemm_x3(A, B, tb, bias, C, beta):
+            continue
         Bop = B.t() if tb else B
         if beta:
             C.addmm_(A, Bop)
@@ -2179,6 +2222,8 @@ class _Linear(Function):
             y = torch.empty((x.shape[0], w.shape[0]), dtype=x.dtype, device=x.device)
             if gemm_launch([(x, w, True, b, y, False)]):
                 return y
+            if x.shape[0] > GEMM_MAX_ROWS and gemm_x3(x, w, True, b, y, False):
+                return y
         return F.linear(x, w, b)
 
     @staticmethod
@@ -2224,7 +2269,8 @@ class _LinearBwd(Function):
         if need[0]:
             gy = gy.contiguous()
             gx = torch.empty((gy.shape[0], w.shape[1]), dtype=gy.dtype, device=gy.device)
-            if not (gy.is_cuda and gemm_launch([(gy, w, False, None, gx, False)])):
+            if not (gy.is_cuda and (gemm_launch([(gy, w, False, None, gx, False)])
+                                    or (gy.shape[0] > GEMM_MAX_ROWS and gemm_x3(gy, w, False, None, gx, False)))):
                 torch.mm(gy, w, out=gx)
         gw, gb = _linear_wgrad(gy, x, need[1], need[2]) if (need[1] or need[2]) else (None, None)
         ctx.save_for_backward(gy, x, w)
