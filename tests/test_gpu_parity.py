@@ -298,9 +298,13 @@ def test_et_c5_timed_configuration_fp32_fused_vs_fp64(monkeypatch):
     8 layers, 64 RBF, 8 heads, cutoff 5, fp32, on a 50,001-atom periodic water box (~2.7 M edges) --
     cell list, Morton renumbering, planar rows and the fused-projection forward / dr-mode backward
     kernels (et_fused.hip, counted below: every layer must have run them), against the SAME weights in
-    fp64 (pair-row path: no fused kernels in fp64).  Bars: energy and forces within 1e-4 relative
-    (forces: max |dF| / max |F|), and the fp32 forces sum to ~0 (translation invariance; fp32 rounding of
-    2.7 M edge terms)."""
+    fp64 (pair-row path: no fused kernels in fp64) on the SAME fp32-rounded positions.  Bars: energy and
+    forces within 1e-4 relative (forces: max |dF| / max |F|; RMS 2e-5), and the fp32 forces sum to ~0
+    (translation invariance).  Measured (tools/c5_precision.py): rounding the positions alone moves the fp64
+    forces by 1.3e-4 (0.1 A pairs in a 79 A box: ~5e-6 A of input quantisation), so the fp64 reference
+    gets the rounded positions; the fp32 path is then at 7.8e-5 max / 8.3e-6 RMS -- the same for the
+    fused and the pair-row kernels and for either node-mix GEMM: fp32 periodic-delta geometry, not a
+    kernel."""
     from torchmdnet import et_stack, kernels
     from torchmdnet.models.model import create_model
     calls = {"fwd": 0, "bwd": 0}
@@ -345,12 +349,13 @@ def test_et_c5_timed_configuration_fp32_fused_vs_fp64(monkeypatch):
     periodic(m64, torch.float64)
     del m32
     torch.cuda.empty_cache()
-    y64, f64 = m64(z, pos64, batch)
+    y64, f64 = m64(z, pos64.float().double(), batch)
     assert calls["fwd"] == layers  # fp64 took the pair-row path
     y64, f64 = y64.detach().cpu(), f64.detach().cpu()
     assert torch.isfinite(f32).all()
     assert abs(float(y32.sum() - y64.sum())) <= 1e-4 * abs(float(y64.sum()))
     assert _rel(f32, f64) < 1e-4, _rel(f32, f64)
+    assert float((f32 - f64).pow(2).mean().sqrt() / f64.pow(2).mean().sqrt()) < 2e-5
     assert f32.sum(0).abs().max().item() < 1e-5 * f32.abs().sum().item()
 
 

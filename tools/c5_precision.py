@@ -39,8 +39,16 @@ def main():
         d.box = torch.eye(3, dtype=dt) * L
         d.use_periodic = True
         d.strategy = "cell"
+    y64x, f64x = m64(z, pos, batch)  # exact positions
+    y64x, f64x = y64x.detach(), f64x.detach()
+    # the reference on the fp32-rounded positions the fp32 model sees (input quantisation: ~5e-6 A at
+    # L = 79 A, i.e. ~5e-5 relative on the delta of a 0.1 A pair)
+    pos = pos.float().double()
     y64, f64 = m64(z, pos, batch)
     y64, f64 = y64.detach(), f64.detach()
+    print(json.dumps({"rounding_only": {"energy_rel": float((y64 - y64x).abs().sum() / y64x.abs().sum()),
+                                        "force_maxabs_rel": float((f64 - f64x).abs().max() / f64x.abs().max())}}),
+          flush=True)
     del m64
     torch.cuda.empty_cache()
     fmax = f64.abs().max()

@@ -75,7 +75,9 @@ __global__ void k_split(int D, const float* __restrict__ W, int ldw, const float
   for (int k = 0; k < R; ++k) m = fmaxf(m, fabsf(w[k]));
   int ex = 0;
   if (m > 0.f) frexpf(m, &ex);  // m < 2^ex
-  const int s = m > 0.f ? 14 - ex : 0;
+  // (capped at 2^30: the t-domain forward divides the bias by the accumulator scale, which must stay
+  // finite; a row below 2^-16 carries a negligible share of its pre-activation anyway)
+  const int s = m > 0.f ? min(14 - ex, 30) : 0;
   for (int k = 0; k < R; ++k) {
     const float x = ldexpf(w[k], s);
     const _Float16 h = (_Float16)x;
@@ -241,6 +243,35 @@ __device__ __forceinline__ f4 block_pre(const char* wl, const int (&wb)[KS], con
   const f4 b = *reinterpret_cast<const f4*>(sb + 16 * blk + 4 * g);
   return acc * s + b;
 }
+// ---- "t-domain" SiLU (forward and source pass).  With t = -log2(e) pre, SiLU(pre) = pre / (1 + 2^t) =
+// -ln2 * u(t), u(t) = t / (1 + 2^t): the exponent is v_exp_f32 of t itself (no multiply), and the bias add
+// and the -log2(e) factor fold into the MFMA chain -- it starts from the row's bias divided by the
+// accumulator scale (exact: the scale is a power of two) and one multiply by scale * -log2(e) gives t.
+// The -ln2 of every SiLU value is folded into a staged node operand or applied once to the sums (callers).
+// Per head and 16-edge tile this removes 16 adds and 16 multiplies of ~180 VALU instructions.
+constexpr float kNegLog2e = -1.44269504088896340736f;
+constexpr float kNegLn2 = -0.693147180559945309417f;
+__device__ __forceinline__ float silu_u(float t) {
+  return t * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(t));
+}
+// t of the lane's four channels of block blk (sct = scale * -log2(e), sbt = bias / scale, both in LDS)
+template <int KS>
+__device__ __forceinline__ f4 block_t(const char* wl, const int (&wb)[KS], const float* sct, const float* sbt, int blk,
+                                      const h8 (&b0)[KS], const h8 (&b1)[KS], int g) {
+  constexpr int R = 32 * KS, PB = kD * R * (int)sizeof(_Float16);
+  f4 acc = *reinterpret_cast<const f4*>(sbt + 16 * blk + 4 * g);
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    const char* f0 = wl + wb[ks] + blk * 16 * R * (int)sizeof(_Float16);
+    const h8 w0 = *reinterpret_cast<const h8*>(f0);
+    const h8 w1 = *reinterpret_cast<const h8*>(f0 + PB);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(w0, b1[ks], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1, b0[ks], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(w0, b0[ks], acc, 0, 0, 0);
+  }
+  return acc * *reinterpret_cast<const f4*>(sct + 16 * blk + 4 * g);
+}
+
 // d pre / d r: W f' (no bias), scaled back by the row scale and the edge's derivative scale
 template <int KS>
 __device__ __forceinline__ f4 block_dpre(const char* wl, const int (&wb)[KS], const float* sc, float dsc, int blk,
@@ -302,6 +333,21 @@ __device__ __forceinline__ void load_image(_Float16* w, float* s_sc, float* s_b,
   u4* l = reinterpret_cast<u4*>(w);
   for (int i = threadIdx.x; i < 2 * kD * R / 8; i += NT) l[i] = g[i];
   for (int i = threadIdx.x; i < kD; i += NT) { s_sc[i] = wsc[i]; s_b[i] = bias[i]; }
+}
+
+// the same with the t-domain constants: scale * -log2(e) and bias / scale (the scale is 2^-k: exact)
+template <int KS, int NT>
+__device__ __forceinline__ void load_image_t(_Float16* w, float* s_sc, float* s_b, const _Float16* img,
+                                             const float* wsc, const float* bias) {
+  constexpr int R = 32 * KS;
+  const u4* g = reinterpret_cast<const u4*>(img);
+  u4* l = reinterpret_cast<u4*>(w);
+  for (int i = threadIdx.x; i < 2 * kD * R / 8; i += NT) l[i] = g[i];
+  for (int i = threadIdx.x; i < kD; i += NT) {
+    const float sc = wsc[i];
+    s_sc[i] = sc * kNegLog2e;
+    s_b[i] = bias[i] / sc;  // sc = 2^-k: exact
+  }
 }
 
 // per-lane A-fragment offsets of the item's head slice (block h0 of every part), opaque to the optimiser:
@@ -421,7 +467,7 @@ __global__ __launch_bounds__(NW * 64, 1) void k_fwd(Fwd P) {
   __shared__ __attribute__((aligned(16))) float s_b[kD];
   __shared__ __attribute__((aligned(16))) float s_q[NW][16 * HPW];  // the item's q channels (per wave)
   __shared__ int s_next;
-  load_image<KS, NW * 64>(w, s_sc, s_b, P.img, P.wsc, P.bias);
+  load_image_t<KS, NW * 64>(w, s_sc, s_b, P.img, P.wsc, P.bias);
   if (threadIdx.x == 0) s_next = 0;
   __syncthreads();
   const Work W = work_range<G>(P.n, P.chunk);
@@ -438,8 +484,9 @@ __global__ __launch_bounds__(NW * 64, 1) void k_fwd(Fwd P) {
     const int h0 = sl * HPW;
     const int rb = min(P.row_ptr[t], P.cap), re = min(P.row_ptr[t + 1], P.cap);
     __builtin_amdgcn_wave_barrier();  // the previous item's reads of sq are done (in-order LDS)
-    if (lane < 4 * HPW)
-      *reinterpret_cast<f4*>(sq + 4 * lane) = *reinterpret_cast<const f4*>(P.q + (size_t)t * P.ldq + 16 * h0 + 4 * lane);
+    if (lane < 4 * HPW)  // q * -ln2: the dk SiLU's t-domain factor (silu_u)
+      *reinterpret_cast<f4*>(sq + 4 * lane) =
+          kNegLn2 * *reinterpret_cast<const f4*>(P.q + (size_t)t * P.ldq + 16 * h0 + 4 * lane);
     __builtin_amdgcn_wave_barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     f4 ax[HPW], a0[HPW], a1[HPW], a2[HPW];
@@ -464,21 +511,22 @@ __global__ __launch_bounds__(NW * 64, 1) void k_fwd(Fwd P) {
         constexpr int hh = decltype(hc)::value;
         Gat X;
         gather_kvw<PL>(X, Rk, Rv, Rw, ok_, ov_, ow_, h0 + hh);
-        const f4 pk = block_pre<KS>(wt, wb, sct, sbt, hh, B0, B1, g);
-        const f4 px = block_pre<KS>(wt, wb, sct, sbt, 8 + hh, B0, B1, g);
-        const f4 p1 = block_pre<KS>(wt, wb, sct, sbt, 16 + hh, B0, B1, g);
-        const f4 p2 = block_pre<KS>(wt, wb, sct, sbt, 24 + hh, B0, B1, g);
+        // t-domain: silu(pre) = -ln2 u(t); the -ln2 is in the staged q (dk) and applied to the sums (dv)
+        const f4 pk = block_t<KS>(wt, wb, sct, sbt, hh, B0, B1, g);
+        const f4 px = block_t<KS>(wt, wb, sct, sbt, 8 + hh, B0, B1, g);
+        const f4 p1 = block_t<KS>(wt, wb, sct, sbt, 16 + hh, B0, B1, g);
+        const f4 p2 = block_t<KS>(wt, wb, sct, sbt, 24 + hh, B0, B1, g);
         const f4 qv = *reinterpret_cast<const f4*>(sq + 16 * hh + 4 * g);
         float part = 0.f;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) part += qv[i] * X.kk[i] * Silu<float>(pk[i]).s;
+        for (int i = 0; i < 4; ++i) part += qv[i] * X.kk[i] * silu_u(pk[i]);
         const float att = gsum(part);
         const float a = Silu<float>(att).s * E.C;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          ax[hh][i] += X.vx[i] * Silu<float>(px[i]).s * a;
-          const float v1e = X.v1[i] * Silu<float>(p1[i]).s;
-          const float v2e = X.v2[i] * Silu<float>(p2[i]).s;
+          ax[hh][i] += X.vx[i] * silu_u(px[i]) * a;
+          const float v1e = X.v1[i] * silu_u(p1[i]);
+          const float v2e = X.v2[i] * silu_u(p2[i]);
           a0[hh][i] += X.w0[i] * v1e + v2e * E.ux;
           a1[hh][i] += X.w1[i] * v1e + v2e * E.uy;
           a2[hh][i] += X.w2[i] * v1e + v2e * E.uz;
@@ -503,6 +551,10 @@ __global__ __launch_bounds__(NW * 64, 1) void k_fwd(Fwd P) {
     }
     if (c < HPW) {
       const int ch = 16 * (h0 + c) + 4 * g;
+      X *= kNegLn2;  // the dv SiLUs' t-domain factor
+      V0 *= kNegLn2;
+      V1 *= kNegLn2;
+      V2 *= kNegLn2;
       *reinterpret_cast<f4*>(P.xo + (size_t)t * H + ch) = X;
       float* vo = P.veco + (size_t)t * 3 * H + ch;
       *reinterpret_cast<f4*>(vo) = V0;
@@ -740,7 +792,7 @@ __global__ __launch_bounds__(NW * 64, 1) void k_bwd_src(Bwd P) {
   __shared__ __attribute__((aligned(16))) float s_b[kD];
   __shared__ __attribute__((aligned(16))) float s_node[NW][6 * CH];  // k | v_x | v_1 | vec (3) of the slice
   __shared__ int s_next;
-  load_image<KS, NW * 64>(w, s_sc, s_b, P.img, P.wsc, P.bias);
+  load_image_t<KS, NW * 64>(w, s_sc, s_b, P.img, P.wsc, P.bias);
   if (threadIdx.x == 0) s_next = 0;
   __syncthreads();
   const Work W = work_range<G>(P.n, P.chunk);
@@ -768,7 +820,8 @@ __global__ __launch_bounds__(NW * 64, 1) void k_bwd_src(Bwd P) {
       else if (part <= 2)
         val = *reinterpret_cast<const f4*>(P.v + (size_t)j * P.ldv + VL<PL>::head * h + (part - 1) * PV + o);
       else if (P.vec) val = *reinterpret_cast<const f4*>(P.vec + ((size_t)j * 3 + (part - 3)) * H + 16 * h + o);
-      *reinterpret_cast<f4*>(nd + 4 * i) = val;
+      // k, v_x, v_1 times -ln2: the t-domain factor of the SiLU values they multiply (silu_u)
+      *reinterpret_cast<f4*>(nd + 4 * i) = part <= 2 ? kNegLn2 * val : val;
     }
     __builtin_amdgcn_wave_barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -795,15 +848,16 @@ __global__ __launch_bounds__(NW * 64, 1) void k_bwd_src(Bwd P) {
         const int sh = __builtin_amdgcn_readfirstlane(64 * (h0 + hh));
         const f4 qm = bld4<0>(Rq, oq, sh), gxm = bld4<0>(Rgx, ox, sh);
         const f4 g0 = bld4<0>(Rgv, og, sh), g1 = bld4<4 * kH>(Rgv, og, sh), g2 = bld4<8 * kH>(Rgv, og, sh);
-        const f4 pk = block_pre<KS>(wt, wb, sct, sbt, hh, B0, B1, g);
-        const f4 px = block_pre<KS>(wt, wb, sct, sbt, 8 + hh, B0, B1, g);
+        // t-domain SiLU values (silu = -ln2 u): the -ln2 is in the staged k, v_x, v_1 and on the final sums
+        const f4 pk = block_t<KS>(wt, wb, sct, sbt, hh, B0, B1, g);
+        const f4 px = block_t<KS>(wt, wb, sct, sbt, 8 + hh, B0, B1, g);
         f4 dk, dvx;
         float pa = 0.f, pg = 0.f;
         const f4 kj = own(0, hh), vxj = own(1, hh);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          dk[i] = Silu<float>(pk[i]).s;
-          dvx[i] = Silu<float>(px[i]).s;
+          dk[i] = silu_u(pk[i]);
+          dvx[i] = silu_u(px[i]);
           pa += qm[i] * kj[i] * dk[i];
           pg += gxm[i] * vxj[i] * dvx[i];
         }
@@ -816,12 +870,12 @@ __global__ __launch_bounds__(NW * 64, 1) void k_bwd_src(Bwd P) {
           gk[hh][i] += gs * qm[i] * dk[i];
           gvx[hh][i] += gxm[i] * a * dvx[i];
         }
-        const f4 p1 = block_pre<KS>(wt, wb, sct, sbt, 16 + hh, B0, B1, g);
-        const f4 p2 = block_pre<KS>(wt, wb, sct, sbt, 24 + hh, B0, B1, g);
+        const f4 p1 = block_t<KS>(wt, wb, sct, sbt, 16 + hh, B0, B1, g);
+        const f4 p2 = block_t<KS>(wt, wb, sct, sbt, 24 + hh, B0, B1, g);
         const f4 v1j = own(2, hh), w0j = own(3, hh), w1j = own(4, hh), w2j = own(5, hh);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const float dv1 = Silu<float>(p1[i]).s, dv2 = Silu<float>(p2[i]).s;
+          const float dv1 = silu_u(p1[i]), dv2 = silu_u(p2[i]);
           const float gv1e = g0[i] * w0j[i] + g1[i] * w1j[i] + g2[i] * w2j[i];
           gv1[hh][i] += gv1e * dv1;
           const float gv2e = g0[i] * E.ux + g1[i] * E.uy + g2[i] * E.uz;
@@ -853,6 +907,10 @@ __global__ __launch_bounds__(NW * 64, 1) void k_bwd_src(Bwd P) {
     }
     if (c < HPW) {
       const int h = h0 + c;
+      K *= kNegLn2;  // the t-domain factor of dk, dv_x, dv_1, dv_2 (gw's is in the staged v_1)
+      VX *= kNegLn2;
+      V1 *= kNegLn2;
+      V2 *= kNegLn2;
       auto put = [&](float* d, f4 val) {
         if (ag) val += *reinterpret_cast<const f4*>(d);
         *reinterpret_cast<f4*>(d) = val;
