@@ -494,11 +494,15 @@ __global__ __launch_bounds__(NW * 64, 1) void k_fwd(Fwd P) {
     for (int hh = 0; hh < HPW; ++hh) ax[hh] = a0[hh] = a1[hh] = a2[hh] = f4{0.f, 0.f, 0.f, 0.f};
     const float* sct = s_sc + 16 * h0;
     const float* sbt = s_b + 16 * h0;
+    // the next tile's edge scalars are loaded while this tile computes: a tile waits on one memory round
+    // trip (its fragments and gathers), not two
+    Edge En = load_edge(rb + c, re, P.src, P.C, P.u, P.frow, 8 * R, 1.f);
     for (int base = rb; base < re; base += 16) {
-      const Edge E = load_edge(base + c, re, P.src, P.C, P.u, P.frow, 8 * R, 1.f);
+      const Edge E = En;
       TMD_DCHECK(E.s >= 0 && E.s < P.n);
       h8 B0[KS], B1[KS];
       load_frags<KS>(Rf, E.fo, g, 0, B0, B1);
+      if (base + 16 < re) En = load_edge(base + 16 + c, re, P.src, P.C, P.u, P.frow, 8 * R, 1.f);
       // an edge past the row gathers from beyond the resources' ranges: its k, v and vec are 0, so its
       // terms vanish without masks (C = 0 as well)
       const int ok_ = E.ok ? (E.s * P.ldk + 4 * g) * 4 : kOOB;
@@ -646,9 +650,11 @@ __global__ __launch_bounds__(NW * 64, 1) void k_bwd_dst(Bwd P) {
     f4 gq[HPW];
 #pragma unroll
     for (int hh = 0; hh < HPW; ++hh) gq[hh] = f4{0.f, 0.f, 0.f, 0.f};
+    Edge En = load_edge(rb + c, re, P.src, P.C, P.u, P.frow, 8 * R, 1.f);  // (next tile's scalars: as k_fwd)
     for (int base = rb; base < re; base += 16) {
       const int e = base + c;
-      const Edge E = load_edge(e, re, P.src, P.C, P.u, P.frow, 8 * R, 1.f);
+      const Edge E = En;
+      if (base + 16 < re) En = load_edge(base + 16 + c, re, P.src, P.C, P.u, P.frow, 8 * R, 1.f);
       TMD_DCHECK(E.s >= 0 && E.s < P.n);
       h8 B0[KS], B1[KS], D0[KS], D1[KS];
       load_frags<KS>(Rf, E.fo, g, 0, B0, B1);
@@ -832,8 +838,11 @@ __global__ __launch_bounds__(NW * 64, 1) void k_bwd_src(Bwd P) {
     auto own = [&](int part, int hh) { return *reinterpret_cast<const f4*>(nd + part * CH + 16 * hh + 4 * g); };
     const float* sct = s_sc + 16 * h0;
     const float* sbt = s_b + 16 * h0;
+    // the reversed edges j -> m; the next tile's scalars load while this one computes (as k_fwd)
+    Edge En = load_edge(rb + c, re, P.src, P.C, P.u, P.frow, 8 * R, -1.f);
     for (int base = rb; base < re; base += 16) {
-      const Edge E = load_edge(base + c, re, P.src, P.C, P.u, P.frow, 8 * R, -1.f);  // the reversed edge j -> m
+      const Edge E = En;
+      if (base + 16 < re) En = load_edge(base + 16 + c, re, P.src, P.C, P.u, P.frow, 8 * R, -1.f);
       TMD_DCHECK(E.s >= 0 && E.s < P.n);
       h8 B0[KS], B1[KS];
       load_frags<KS>(Rf, E.fo, g, 0, B0, B1);

@@ -769,12 +769,23 @@ __global__ __launch_bounds__(256) void k_proj_x3(Args P) {
       ar[mb][ks][1] = *reinterpret_cast<const float4*>(r + 32 * ks + 4);
     }
   }
-  // W tile (3 pieces x BN rows x K bf16, 16-byte chunks; rows past N clamp) and bias -> LDS
+  // W tile (3 pieces x BN rows x K bf16, 16-byte chunks; rows past N clamp) and bias -> LDS: all of the
+  // thread's loads first, then the stores (one memory round trip, not one per chunk)
   constexpr int CH = K / 8;  // 16-byte chunks per row
-  for (int c = threadIdx.x; c < 3 * BN * CH; c += 256) {
+  constexpr int NL = (3 * BN * CH + 255) / 256;
+  u4 stg[NL];
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {
+    const int c = threadIdx.x + 256 * i;
     const int p = c / (BN * CH), rc = c % (BN * CH), n = rc / CH, k = (rc % CH) * 8;
-    *reinterpret_cast<u4*>(&w[p][n][k]) =
-        *reinterpret_cast<const u4*>(P.Wp + p * P.pstride + (size_t)min(n0 + n, P.N - 1) * K + k);
+    if (c < 3 * BN * CH)
+      stg[i] = *reinterpret_cast<const u4*>(P.Wp + p * P.pstride + (size_t)min(n0 + n, P.N - 1) * K + k);
+  }
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {
+    const int c = threadIdx.x + 256 * i;
+    const int p = c / (BN * CH), rc = c % (BN * CH), n = rc / CH, k = (rc % CH) * 8;
+    if (c < 3 * BN * CH) *reinterpret_cast<u4*>(&w[p][n][k]) = stg[i];
   }
   if (threadIdx.x < BN) sb[threadIdx.x] = P.bias ? P.bias[min(n0 + (int)threadIdx.x, P.N - 1)] : 0.f;
   bf8 a[MB][KS][3];
@@ -877,12 +888,24 @@ __global__ __launch_bounds__(256) void k_gemm_x3(XArgs P) {
   const int nks_all = P.K / 32;
   for (int kc = 0; kc < P.K; kc += KC) {
     const int nks = min(KC, P.K - kc) / 32;
-    __syncthreads();  // the previous chunk's LDS reads are done
+    // the chunk's pieces: every 16-byte load of the thread issued before the first LDS store (one memory
+    // round trip per chunk; a load -> store loop serialises ~12 of them)
+    constexpr int CH = KC / 8, NL = 3 * BN * CH / 256;
     const int ch = nks * 4;  // 16-byte chunks per row of this K chunk
-    for (int c = threadIdx.x; c < 3 * BN * ch; c += 256) {
-      const int p = c / (BN * ch), rc = c % (BN * ch), n = rc / ch, k = (rc % ch) * 8;
-      *reinterpret_cast<u4*>(&w[p][n][k]) =
-          *reinterpret_cast<const u4*>(P.Bp + p * ps + (size_t)min(n0 + n, P.N - 1) * P.K + kc + k);
+    u4 st[NL];
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      const int c = threadIdx.x + 256 * i;
+      const int p = c / (BN * CH), rc = c % (BN * CH), n = rc / CH, k = (rc % CH) * 8;
+      st[i] = k < 8 * ch ? *reinterpret_cast<const u4*>(P.Bp + p * ps + (size_t)min(n0 + n, P.N - 1) * P.K + kc + k)
+                         : u4{0u, 0u, 0u, 0u};
+    }
+    __syncthreads();  // the previous chunk's LDS reads are done
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      const int c = threadIdx.x + 256 * i;
+      const int p = c / (BN * CH), rc = c % (BN * CH), n = rc / CH, k = (rc % CH) * 8;
+      *reinterpret_cast<u4*>(&w[p][n][k]) = st[i];
     }
     __syncthreads();
     for (int ks = 0; ks < nks; ++ks) {
