@@ -133,3 +133,58 @@ def test_lnnp_step_broadcasts_and_keeps_replicas_identical():
     assert v0 and v1
     assert l0 != l1  # on different data
     assert lr0 == lr1 == pytest.approx(1e-2)  # warm-up over 3 steps reached the base LR
+
+
+def _split_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from torchmdnet.training import GradAllReduce, SplitAdamW, _adamw, step_reduce
+    torch.manual_seed(0)
+    model = torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.SiLU(), torch.nn.Linear(16, 4),
+                                torch.nn.Linear(4, 1))
+    ref = torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.SiLU(), torch.nn.Linear(16, 4),
+                              torch.nn.Linear(4, 1))
+    ref.load_state_dict(model.state_dict())
+    red = GradAllReduce(model.parameters())
+    tail, head = red.split_params()
+    opt = SplitAdamW(tail, head, 1e-2, 0.01)
+    red_ref = GradAllReduce(ref.parameters())
+    opt_ref = _adamw(red_ref.params, 1e-2, 0.01)
+    seen = []
+    g = torch.Generator().manual_seed(100 + rank)
+    for _ in range(3):
+        x = torch.randn(32, 8, generator=g)
+        for m in (model, ref):
+            m.zero_grad(set_to_none=False)
+            m(x).pow(2).sum().backward()
+        # the tail bucket (last parameters + the skip flag) is averaged before the first part steps
+        step_reduce(red, opt, lambda: seen.append(float(red.flag[0])))
+        red_ref()
+        opt_ref.step()
+    same = all(torch.equal(p, q) for p, q in zip(model.parameters(), ref.parameters()))
+    out.put((rank, same, len(tail) > 0 and len(head) > 0, seen, [p.detach().numpy() for p in model.parameters()]))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_two_bucket_allreduce_overlapped_step_equals_fused():
+    """The two-bucket all-reduce with the tail bucket's AdamW update issued before the head bucket is
+    reduced (training.step_reduce / SplitAdamW, world > 1) gives the SAME parameters as one fused
+    all-reduce + one AdamW, on every rank (replicas identical)."""
+    import sys
+    from conftest import PKG
+    sys.path.insert(0, PKG)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_split_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {r: rest for r, *rest in (q.get(timeout=100) for _ in procs)}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in (0, 1):
+        same, both, seen, _ = res[r]
+        assert same and both and seen == [0.0, 0.0, 0.0]
+    assert all((a == b).all() for a, b in zip(res[0][3], res[1][3]))

@@ -90,6 +90,131 @@ class GradAllReduce:
         dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=self.group)
         self.flat.div_(_world(self.group))
 
+    # --- two buckets, the optimizer overlapped with the second all-reduce (world > 1)
+    def split_params(self, frac=0.5):
+        """(tail, head) parameter lists of a two-bucket split: the TAIL bucket is the flat buffer's end
+        (the last parameters and the skip flag) and is reduced first, so the optimizer over its
+        parameters -- which needs the reduced flag -- can run while the HEAD bucket is reduced."""
+        n = sum(p.numel() for p in self.params)
+        cut, off, k = int(n * frac), 0, 0
+        for i, p in enumerate(self.params):
+            if off >= cut:
+                k = i
+                break
+            off += p.numel()
+        else:
+            k = len(self.params)
+        self._cut = off  # flat[:off] = head bucket, flat[off:] = tail bucket (incl. the flag)
+        return self.params[k:], self.params[:k]
+
+    def reduce_overlapped(self, first, second):
+        """All-reduce the tail bucket, then the head bucket, on a side stream (RCCL over xGMI); ``first()``
+        (the optimizer step of the tail's parameters) runs on the current stream as soon as the tail is
+        averaged, overlapped with the head's all-reduce, then ``second()``.  World 1: both steps, no
+        collective.  CPU (gloo): the same order without streams."""
+        ws = _world(self.group)
+        if ws == 1:
+            first()
+            second()
+            return
+        self.bind()
+        tail, head = self.flat[self._cut:], self.flat[:self._cut]
+        if not self.flat.is_cuda:
+            dist.all_reduce(tail, op=dist.ReduceOp.SUM, group=self.group)
+            tail.div_(ws)
+            first()
+            if head.numel():
+                dist.all_reduce(head, op=dist.ReduceOp.SUM, group=self.group)
+                head.div_(ws)
+            second()
+            return
+        cur = torch.cuda.current_stream(self.flat.device)
+        side = getattr(self, "_side", None)
+        if side is None:
+            side = self._side = torch.cuda.Stream(device=self.flat.device)
+        side.wait_stream(cur)  # the gradients are complete
+        with torch.cuda.stream(side):
+            dist.all_reduce(tail, op=dist.ReduceOp.SUM, group=self.group)
+            ev_tail = torch.cuda.Event()
+            ev_tail.record(side)
+            if head.numel():
+                dist.all_reduce(head, op=dist.ReduceOp.SUM, group=self.group)
+            ev_head = torch.cuda.Event()
+            ev_head.record(side)
+        cur.wait_event(ev_tail)
+        tail.div_(ws)
+        first()
+        cur.wait_event(ev_head)
+        head.div_(ws)
+        second()
+        # the buffer is rewritten by the next backward on `cur`: the side stream's use of it must end first
+        tail.record_stream(side)
+        head.record_stream(side)
+
+
+class SplitAdamW(torch.optim.Optimizer):
+    """Two fused AdamW instances over the tail / head buckets of ``GradAllReduce.split_params`` (the
+    same per-parameter update as one AdamW: it is elementwise), so the tail's update can overlap the
+    head bucket's all-reduce.  A torch Optimizer (schedulers such as ReduceLROnPlateau accept it) whose
+    param_groups ARE the parts' groups (an LR change reaches them)."""
+
+    def __init__(self, tail, head, lr, weight_decay):
+        parts = [_adamw(ps, lr, weight_decay) for ps in (tail, head) if ps]
+        super().__init__([g for o in parts for g in o.param_groups], dict(lr=lr, weight_decay=weight_decay))
+        self.parts = parts
+        self.param_groups = [g for o in parts for g in o.param_groups]  # the same dict objects
+
+    def __setattr__(self, k, v):
+        if k in ("found_inf", "grad_scale"):
+            for o in self.__dict__.get("parts", []):
+                setattr(o, k, v)
+        super().__setattr__(k, v)
+
+    def zero_grad(self, set_to_none=True):
+        for o in self.parts:
+            o.zero_grad(set_to_none=set_to_none)
+
+    def step(self, closure=None):
+        for o in self.parts:
+            o.step()
+
+    def step_part(self, i):
+        if i < len(self.parts):
+            self.parts[i].step()
+
+    def state_dict(self):
+        return {"parts": [o.state_dict() for o in self.parts]}
+
+    def load_state_dict(self, sd):
+        for o, d in zip(self.parts, sd["parts"]):
+            o.load_state_dict(d)
+
+
+def _make_optimizer(reduce, lr, weight_decay):
+    """One fused AdamW at world 1; at world > 1 the two-bucket SplitAdamW whose tail update overlaps
+    the head bucket's all-reduce (``step_reduce``)."""
+    if _world(reduce.group) > 1:
+        tail, head = reduce.split_params()
+        return SplitAdamW(tail, head, lr, weight_decay)
+    return _adamw(reduce.params, lr, weight_decay)
+
+
+def step_reduce(reduce, opt, before_first=None):
+    """All-reduce the gradients and step the optimizer: with a SplitAdamW the tail bucket's update runs
+    while the head bucket is still being reduced (world > 1); ``before_first()`` runs once the tail
+    (which holds the skip flag) is averaged."""
+    if isinstance(opt, SplitAdamW):
+        def first():
+            if before_first is not None:
+                before_first()
+            opt.step_part(0)
+        reduce.reduce_overlapped(first, lambda: opt.step_part(1))
+        return
+    reduce()
+    if before_first is not None:
+        before_first()
+    opt.step()
+
 
 def _adamw(params, lr, weight_decay):
     dev = params[0].device
@@ -121,7 +246,7 @@ class LNNPStep:
         self.lr_warmup_steps = lr_warmup_steps
         broadcast_parameters(model, 0, group)
         self.reduce = GradAllReduce(model.parameters(), group)
-        self.opt = _adamw(self.reduce.params, lr, weight_decay)
+        self.opt = _make_optimizer(self.reduce, lr, weight_decay)
         self.global_step = 0
 
     def loss(self, z, pos, batch, y, neg_dy):
@@ -159,9 +284,8 @@ class LNNPStep:
         self.opt.zero_grad(set_to_none=False)  # zeroes the flat buffer's views in place
         loss = self.loss(z, pos, batch, y, neg_dy)
         self.backward(loss)
-        self.reduce()
         self._warmup_lr()
-        self.opt.step()
+        step_reduce(self.reduce, self.opt)
         self.global_step += 1
         return loss.detach()
 
@@ -253,12 +377,13 @@ class GraphedTrainStep(LNNPStep):
                                      f"layout is {tuple(dst.shape)}")
                 dst.copy_(src)
         self.graph.replay()
-        self.reduce()
-        # skip flag (> 0 on any rank) -> AdamW's found_inf (exactly 1.0 or 0.0)
-        self.found_inf.copy_(self.reduce.flag[0].sign())
-        self.skip_count.add_(self.found_inf)
         self._warmup_lr()
-        self.opt.step()
+
+        def flag():  # skip flag (> 0 on any rank) -> AdamW's found_inf (exactly 1.0 or 0.0)
+            self.found_inf.copy_(self.reduce.flag[0].sign())
+            self.skip_count.add_(self.found_inf)
+
+        step_reduce(self.reduce, self.opt, flag)
         self.global_step += 1
         return self.static_loss.detach()
 
@@ -469,7 +594,7 @@ class PaddedGraphedTrainer:
         self.margin, self.warmup = margin, warmup
         broadcast_parameters(model, 0, group)
         self.reduce = GradAllReduce(model.parameters(), group)
-        self.opt = _adamw(self.reduce.params, lr, weight_decay)
+        self.opt = _make_optimizer(self.reduce, lr, weight_decay)
         dev = self.reduce.flat.device
         self.found_inf = torch.zeros((), dtype=torch.float32, device=dev)
         self.opt.found_inf = self.found_inf
@@ -505,13 +630,11 @@ class PaddedGraphedTrainer:
             st = self._capture(b)
         st.load(b)
         st.graph.replay()
-        self.reduce()
-        self.found_inf.copy_(self.reduce.flag[0].sign())
         if self.lr_warmup_steps and gs < self.lr_warmup_steps:
             scale = min(1.0, float(gs + 1) / float(self.lr_warmup_steps))
             for g in self.opt.param_groups:
                 g["lr"] = scale * self.lr
-        self.opt.step()
+        step_reduce(self.reduce, self.opt, lambda: self.found_inf.copy_(self.reduce.flag[0].sign()))
         self._flag_host.copy_(self.reduce.flag, non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
