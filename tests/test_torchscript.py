@@ -432,3 +432,47 @@ def test_torchscript_fused_eval_periodic_cell_list():
     y_e, f_e = model(z, pos.clone(), batch)
     y_s, f_s = scripted(z, pos.clone(), batch)
     assert _rel(y_s, y_e) < 1e-4 and _rel(f_s, f_e) < 1e-4
+
+
+@pytest.mark.parametrize("strategy", ["cell", "brute"])
+def test_torchscript_fused_eval_large_system_forms(monkeypatch, strategy):
+    """The MD-engine form at C5 layout: tmdnet::et_energy_forces with its large-system
+    switches forced on a 3000-atom periodic water box -- Morton renumbering, pair-shared rows
+    (tmdnet_pair_index), planar v rows and the fused-projection layer kernels, node mixes above 16k rows
+    on tmdnet_gemm_x3_f32 -- against the eager model with the same switches forced (1e-4), and against
+    the eager model on its default small-system path; forces come back in the caller's atom order."""
+    from torchmdnet import et_stack, kernels
+    from torchmdnet.models.model import create_model
+    _torch_lib_loaded()
+    args = yaml_args("equivariant-transformer")
+    args.update(prior_model=None, embedding_dimension=128, num_layers=4, derivative=True, max_num_neighbors=128)
+    torch.manual_seed(0)
+    model = create_model(args).to(DEV).eval()
+    n = 3000
+    g = torch.Generator().manual_seed(5)
+    L = (n / 0.1003) ** (1.0 / 3.0)
+    pos = (torch.rand(n, 3, generator=g, dtype=torch.float64) * L).float().to(DEV)
+    z = torch.tensor([8, 1, 1], dtype=torch.long).repeat(n // 3 + 1)[:n].to(DEV)
+    batch = torch.zeros(n, dtype=torch.long, device=DEV)
+    d = model.representation_model.distance
+    d.box = torch.eye(3) * L
+    d.use_periodic = True
+    d.strategy = strategy
+    y_plain, f_plain = model(z, pos.clone(), batch)  # eager, small-system forms
+    monkeypatch.setattr(kernels, "REORDER_MIN_ATOMS", 0)
+    monkeypatch.setattr(et_stack, "PLANAR_MIN_EDGES", 0)
+    monkeypatch.setattr(et_stack, "FEP_MIN_EDGES", 0)
+    fused_calls = []
+    orig = kernels.et_fused_fwd_launch
+    monkeypatch.setattr(kernels, "et_fused_fwd_launch", lambda *a, **k: fused_calls.append(1) or orig(*a, **k))
+    y_e, f_e = model(z, pos.clone(), batch)
+    assert len(fused_calls) == 4
+    scripted = torch.jit.script(model)
+    prev = torch.ops.tmdnet.set_large_system_thresholds(0, 0)
+    try:
+        y_s, f_s = scripted(z, pos.clone(), batch)
+    finally:
+        torch.ops.tmdnet.set_large_system_thresholds(prev[0], prev[1])
+    assert not f_s.requires_grad
+    assert _rel(y_s, y_e) < 1e-4 and _rel(f_s, f_e) < 1e-4
+    assert _rel(y_s, y_plain) < 1e-4 and _rel(f_s, f_plain) < 1e-4

@@ -1113,9 +1113,35 @@ constexpr double kLnEps = 1e-5;  // nn.LayerNorm default (reference torchmd_et.p
 
 int64_t stack_np(bool hk, bool hv) { return 11 + 2 * int64_t(hk) + 2 * int64_t(hv); }
 
-// C = A op(B) (+ bias) (+ C if beta) on the hand-written grouped GEMM, the library outside its envelope
+// Large-row fp32 GEMM on tmdnet_gemm_x3_f32 (kernels.gemm_x3): B split per call (a [N][K] weight with
+// trans_b, a [K][N] right operand without); false when outside its envelope
+bool gemm_x3_into(const Tensor& A, const Tensor& B, bool trans_b, const Tensor& bias, const Tensor& C, bool beta) {
+  const int M = static_cast<int>(A.size(0)), N = static_cast<int>(C.size(1)), K = static_cast<int>(A.size(1));
+  auto al = [](const Tensor& t) { return !t.defined() || reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0; };
+  if (!(A.scalar_type() == at::kFloat && B.scalar_type() == at::kFloat && C.scalar_type() == at::kFloat && M > 0 &&
+        K % 32 == 0 && N % 16 == 0 && A.stride(1) == 1 && B.stride(1) == 1 && C.stride(1) == 1 &&
+        A.stride(0) % 4 == 0 && B.stride(0) % 4 == 0 && C.stride(0) % 4 == 0 && al(A) && al(B) && al(C) &&
+        (!bias.defined() || (bias.is_contiguous() && al(bias)))))
+    return false;
+  Tensor bp = at::empty({3, N, K}, A.options().dtype(at::kShort));
+  void* st = stream_of(A);
+  int rc = trans_b ? tmdnet_proj_split_f32(N, K, B.data_ptr(), static_cast<int>(B.stride(0)), bp.data_ptr(), st)
+                   : tmdnet_split_t_f32(N, K, B.data_ptr(), static_cast<int>(B.stride(0)), bp.data_ptr(), st);
+  if (rc == TMDNET_UNSUPPORTED) return false;
+  check(rc, "tmdnet_split");
+  rc = tmdnet_gemm_x3_f32(M, N, K, A.data_ptr(), static_cast<int>(A.stride(0)), bp.data_ptr(),
+                          bias.defined() ? bias.data_ptr() : nullptr, C.data_ptr(), static_cast<int>(C.stride(0)),
+                          beta ? 1 : 0, st);
+  if (rc == TMDNET_UNSUPPORTED) return false;
+  check(rc, "tmdnet_gemm_x3_f32");
+  return true;
+}
+
+// C = A op(B) (+ bias) (+ C if beta) on the hand-written grouped GEMM (up to 16384 rows) or the x3 GEMM
+// (more rows), the library outside both envelopes
 void gemm_into(const Tensor& A, const Tensor& B, bool trans_b, const Tensor& bias, const Tensor& C, bool beta) {
   const int M = static_cast<int>(A.size(0)), N = static_cast<int>(C.size(1)), K = static_cast<int>(A.size(1));
+  if (M > 16384 && gemm_x3_into(A, B, trans_b, bias, C, beta)) return;
   if (A.scalar_type() == at::kFloat && M > 0 && M <= 16384 && A.stride(1) == 1 && B.stride(1) == 1 &&
       C.stride(1) == 1) {
     int dims[8] = {M, N, K, static_cast<int>(A.stride(0)), static_cast<int>(B.stride(0)),
@@ -1617,6 +1643,209 @@ std::tuple<Tensor, Tensor> et_stack(const Tensor& x, const Tensor& f, const Tens
 }
 
 
+// ----------------------------------------------------------------------------- large systems (C5 size)
+// The eager path's large-system forms, for the fused inference operator: Morton renumbering of the atoms
+// (kernels.spatial_permutation), pair-shared projection rows (tmdnet_pair_index), the planar v layout and
+// the fused-projection layer kernels (et_fused.hip; et_stack FEP) -- no projection row of any layer is
+// written: per layer only the split weight image (128 KB) and per evaluation the pair rows' RBF fragments.
+// size switches (kernels.REORDER_MIN_ATOMS, et_stack.FEP_MIN_EDGES); tests force them on small systems
+// through tmdnet::set_large_system_thresholds
+static int64_t g_reorder_min_atoms = 16384, g_fep_min_edges = 131072;
+
+std::vector<int64_t> set_large_system_thresholds(int64_t min_atoms, int64_t min_edges) {
+  std::vector<int64_t> prev{g_reorder_min_atoms, g_fep_min_edges};
+  if (min_atoms >= 0) g_reorder_min_atoms = min_atoms;
+  if (min_edges >= 0) g_fep_min_edges = min_edges;
+  return prev;
+}
+
+Tensor spread10(Tensor x) {
+  x = at::bitwise_and(x, 0x3FF);
+  x = at::bitwise_and(at::bitwise_or(x, at::bitwise_left_shift(x, 16)), 0x030000FF);
+  x = at::bitwise_and(at::bitwise_or(x, at::bitwise_left_shift(x, 8)), 0x0300F00F);
+  x = at::bitwise_and(at::bitwise_or(x, at::bitwise_left_shift(x, 4)), 0x030C30C3);
+  return at::bitwise_and(at::bitwise_or(x, at::bitwise_left_shift(x, 2)), 0x09249249);
+}
+
+// molecule-major, then Morton order of cutoff-sized cells (kernels.spatial_permutation)
+Tensor spatial_permutation(const Tensor& pos, const Tensor& batch, double cell, const Tensor& box, bool periodic) {
+  Tensor p = pos.detach();
+  if (periodic && box.defined() && box.numel() == 9) {
+    Tensor b = box.detach().to(at::kCPU).to(at::kDouble).contiguous();
+    const double* bd = b.data_ptr<double>();
+    p = at::stack({at::remainder(p.select(1, 0), bd[0]), at::remainder(p.select(1, 1), bd[4]),
+                   at::remainder(p.select(1, 2), bd[8])},
+                  1);
+  }
+  Tensor lo = std::get<0>(p.min(0));
+  Tensor c = at::clamp(((p - lo) / cell).to(at::kLong), 0, 1023);
+  Tensor key = at::bitwise_or(at::bitwise_or(spread10(c.select(1, 0)), at::bitwise_left_shift(spread10(c.select(1, 1)), 1)),
+                              at::bitwise_left_shift(spread10(c.select(1, 2)), 2));
+  key = key + batch.to(at::kLong) * (int64_t(1) << 31);
+  return at::argsort(key, /*stable=*/true);
+}
+
+// planar [x | v1 | v2] row j of v = row vperm[j] of the reference per-head interleave (et_stack._v_perm)
+Tensor v_perm(int64_t H, int64_t heads, const Tensor& like) {
+  const int64_t d = H / heads;
+  Tensor j = at::arange(3 * H, like.options().dtype(at::kLong));
+  Tensor part = at::floor_divide(j, H), rem = at::remainder(j, H);
+  return at::floor_divide(rem, d) * (3 * d) + part * d + at::remainder(rem, d);
+}
+
+struct FusedAux {  // per evaluation: pair numbering + RBF fragments; per layer: planar weights + images
+  Tensor pair_row, pair_edge, frags, dscale, qkv_perm;
+  int64_t n_rows = 0;
+  std::vector<Tensor> qkv_w, qkv_b, img, wsc, bias;
+};
+
+// the fused-projection stack forward (et_stack._forward_layers with meta.fep): returns (x_out, vec_out)
+std::pair<Tensor, Tensor> stack_forward_fused(const Tensor& x_in, const Tensor& dist, const Tensor& C, const Tensor& u,
+                                              const Tensor& row_ptr, const Tensor& src, const Tensor& mu,
+                                              const Tensor& beta, const StackCfg& c, const std::vector<Tensor>& P,
+                                              StackActs* A, FusedAux* F) {
+  const int64_t np = stack_np(c.hk, c.hv);
+  const int64_t L = (static_cast<int64_t>(P.size()) - 2) / np;
+  Tensor x = x_in.contiguous();
+  const int64_t N = x.size(0), H = x.size(1), E = src.size(0), R = mu.size(0), D = 4 * H;
+  auto o = opts(x);
+  void* st = stream_of(x);
+  A->pk = pack_stack(P, L, np, c.hk, c.hv);
+  // RBF fragments of the pair rows, once for every layer
+  Tensor r_rows = dist.index_select(0, F->pair_edge.to(at::kLong)).contiguous();
+  F->n_rows = r_rows.size(0);
+  F->frags = at::empty({std::max<int64_t>(1, static_cast<int64_t>(tmdnet_fep_frags_bytes(F->n_rows, R) / 2))},
+                       o.dtype(at::kHalf));
+  F->dscale = at::empty({std::max<int64_t>(1, F->n_rows)}, o);
+  check(tmdnet_fep_frags_f32(F->n_rows, static_cast<int>(R), ptr(r_rows), ptr(mu), ptr(beta), c.cl, c.cu,
+                             static_cast<int>(c.rbf), ptr(F->frags), ptr(F->dscale), st),
+        "tmdnet_fep_frags_f32");
+  Tensor vp = v_perm(H, c.heads, x);
+  F->qkv_perm = at::cat({at::arange(2 * H, vp.options()), 2 * H + vp});
+  Tensor one = at::cat({at::arange(H, vp.options()), H + vp});  // [dk | dv] rows in the planar order
+  auto epi_ln = [&](const Tensor& xx, const Tensor& vv, const Tensor& vpp, const Tensor& oo, const Tensor& va,
+                    const Tensor& w, const Tensor& b, Tensor* xo, Tensor* vo, Tensor* xn, Tensor* mean, Tensor* rstd) {
+    *xn = at::empty({N, H}, o);
+    *mean = at::empty({N, 1}, o);
+    *rstd = at::empty({N, 1}, o);
+    if (oo.defined()) {
+      *xo = at::empty({N, H}, o);
+      *vo = at::empty({N, 3, H}, o);
+    }
+    check(tmdnet_et_epilogue_ln_fwd(TMDNET_F32, static_cast<int>(N), static_cast<int>(H), ptr(xx), ptr(vv), ptr(vpp),
+                                    ptr(oo), ptr(va), ptr(w), ptr(b), kLnEps, oo.defined() ? ptr(*xo) : nullptr,
+                                    oo.defined() ? ptr(*vo) : nullptr, ptr(*xn), ptr(*mean), ptr(*rstd), st),
+          "tmdnet_et_epilogue_ln_fwd");
+  };
+  Tensor vec, xn, mean, rstd, unused0, unused1;
+  epi_ln(x, Tensor(), Tensor(), Tensor(), Tensor(), P[0], P[1], &unused0, &unused1, &xn, &mean, &rstd);
+  for (int64_t l = 0; l < L; ++l) {
+    const Tensor* p = P.data() + l * np;
+    F->qkv_w.push_back(A->pk->qkv_w[l].index_select(0, F->qkv_perm).contiguous());
+    F->qkv_b.push_back(A->pk->qkv_b[l].index_select(0, F->qkv_perm).contiguous());
+    const Tensor W = A->pk->dkv_w.narrow(0, l * D, D).index_select(0, one).contiguous();
+    const Tensor Wb = A->pk->dkv_b.narrow(0, l * D, D).index_select(0, one).contiguous();
+    F->img.push_back(at::empty({static_cast<int64_t>(tmdnet_fep_image_bytes(static_cast<int>(D), static_cast<int>(R)) / 2)},
+                               o.dtype(at::kHalf)));
+    F->wsc.push_back(at::empty({D}, o));
+    F->bias.push_back(at::empty({D}, o));
+    check(tmdnet_fep_split_f32(static_cast<int>(D), static_cast<int>(R), ptr(W), static_cast<int>(R), ptr(Wb),
+                               ptr(F->img[l]), ptr(F->wsc[l]), ptr(F->bias[l]), st),
+          "tmdnet_fep_split_f32");
+    Tensor qkv = at::empty({N, 5 * H}, o), vecp;
+    gemm_into(xn, F->qkv_w[l], true, F->qkv_b[l], qkv, false);
+    if (vec.defined()) {
+      vecp = at::empty({N, 3, 3 * H}, o);
+      gemm_into(vec.view({3 * N, H}), p[8], true, Tensor(), vecp.view({3 * N, 3 * H}), false);
+    }
+    Tensor xa = at::empty({N, H}, o), veca = at::empty({N, 3, H}, o);
+    const float* qb = static_cast<const float*>(qkv.data_ptr());
+    check(tmdnet_et_fused_fwd_f32(static_cast<int>(N), static_cast<int>(H), static_cast<int>(c.heads), static_cast<int>(R),
+                                  ptr<int32_t>(row_ptr), ptr<int32_t>(src), static_cast<int>(E), qb, ld(qkv), qb + H,
+                                  ld(qkv), qb + 2 * H, ld(qkv), ptr(vec), ptr(C), ptr(u), ptr<int32_t>(F->pair_row),
+                                  ptr(F->frags), F->n_rows, ptr(F->img[l]), ptr(F->wsc[l]), ptr(F->bias[l]), ptr(xa),
+                                  ptr(veca), TMDNET_ET_V_PLANAR, st),
+          "tmdnet_et_fused_fwd_f32");
+    Tensor oo = at::empty({N, 3 * H}, o);
+    gemm_into(xa, p[9], true, p[10], oo, false);
+    A->x.push_back(x); A->vec.push_back(vec); A->xn.push_back(xn); A->mean.push_back(mean);
+    A->rstd.push_back(rstd); A->qkv.push_back(qkv); A->vecp.push_back(vecp); A->xa.push_back(xa);
+    A->o.push_back(oo);
+    Tensor xo, vo;
+    if (l + 1 < L) {
+      epi_ln(x, vec, vecp, oo, veca, P[(l + 1) * np], P[(l + 1) * np + 1], &xo, &vo, &xn, &mean, &rstd);
+    } else {  // the last epilogue + out_norm
+      epi_ln(x, vec, vecp, oo, veca, P[P.size() - 2], P[P.size() - 1], &xo, &vo, &xn, &mean, &rstd);
+      A->x_pre = xo;
+      A->mean_o = mean;
+      A->rstd_o = rstd;
+      xo = xn;
+    }
+    x = xo;
+    vec = vo;
+  }
+  return {x, vec};
+}
+
+// its force-pass backward (et_stack._backward_layers, dr mode, fused): (g_x, g_r, g_C, g_u)
+variable_list stack_backward_fused(const StackActs& A, const FusedAux& F, Tensor gX, Tensor gV, const Tensor& C,
+                                   const Tensor& u, const Tensor& row_ptr, const Tensor& src, const std::vector<Tensor>& P,
+                                   const StackCfg& c, int64_t R) {
+  const int64_t N = gX.size(0), H = gX.size(1), E = src.size(0), np = stack_np(c.hk, c.hv);
+  const int64_t L = static_cast<int64_t>(A.x.size());
+  auto o = opts(gX);
+  void* st = stream_of(gX);
+  Tensor g_C = at::empty({E}, o), g_u = at::empty({E, 3}, o), g_r = at::empty({E}, o);
+  const size_t wsb = tmdnet_et_fused_bwd_workspace_bytes(static_cast<int>(E));
+  Tensor ws = wsb ? at::empty({static_cast<int64_t>(wsb / 4)}, o) : Tensor();
+  std::vector<Tensor> g_o(L), g_vecp(L);
+  for (int64_t l = 0; l < L; ++l) {
+    g_o[l] = at::empty({N, 3 * H}, o);
+    if (A.vec[l].defined()) g_vecp[l] = at::empty({N, 3, 3 * H}, o);
+  }
+  {  // back through out_norm and the last layer's epilogue in one kernel
+    Tensor g = at::empty_like(gX);
+    check(tmdnet_ln_bwd_epilogue_w(TMDNET_F32, static_cast<int>(N), static_cast<int>(H), ptr(gX), ptr(A.x_pre),
+                                   ptr(A.mean_o), ptr(A.rstd_o), ptr(P[P.size() - 2]), nullptr, nullptr, ptr(g), ptr(gV),
+                                   ptr(A.vecp[L - 1]), ptr(A.o[L - 1]), ptr(g_vecp[L - 1]), ptr(g_o[L - 1]), nullptr, 0,
+                                   st),
+          "tmdnet_ln_bwd_epilogue_w");
+    gX = g;
+  }
+  for (int64_t l = L - 1; l >= 0; --l) {
+    const Tensor* p = P.data() + l * np;
+    Tensor g_xa = at::empty({N, H}, o);
+    gemm_into(g_o[l], p[9], false, Tensor(), g_xa, false);
+    const bool hv = A.vec[l].defined();
+    Tensor g_vec_in = hv ? at::empty({N, 3, H}, o) : Tensor();
+    Tensor g_qkv = at::empty({N, 5 * H}, o);
+    const Tensor& qkv = A.qkv[l];
+    const float* qb = static_cast<const float*>(qkv.data_ptr());
+    float* gb = static_cast<float*>(g_qkv.data_ptr());
+    const int flags = TMDNET_ACC_VEC_RESIDUAL | (l < L - 1 ? TMDNET_ACC_EDGE : 0) | TMDNET_ET_V_PLANAR;
+    check(tmdnet_et_fused_bwd_f32(static_cast<int>(N), static_cast<int>(H), static_cast<int>(c.heads), static_cast<int>(R),
+                                  ptr<int32_t>(row_ptr), ptr<int32_t>(src), static_cast<int>(E), qb, ld(qkv), qb + H,
+                                  ld(qkv), qb + 2 * H, ld(qkv), ptr(A.vec[l]), ptr(C), ptr(u), ptr<int32_t>(F.pair_row),
+                                  ptr(F.frags), ptr(F.dscale), F.n_rows, ptr(F.img[l]), ptr(F.wsc[l]), ptr(F.bias[l]),
+                                  ptr(g_xa), ptr(gV), gb, gb + H, gb + 2 * H, ptr(g_vec_in), ptr(g_C), ptr(g_u), ptr(g_r),
+                                  flags, ptr(ws), wsb, st),
+          "tmdnet_et_fused_bwd_f32");
+    Tensor g_xn = at::empty({N, H}, o);
+    gemm_into(g_qkv, F.qkv_w[l], false, Tensor(), g_xn, false);
+    if (hv) gemm_into(g_vecp[l].view({3 * N, 3 * H}), p[8], false, Tensor(), g_vec_in.view({3 * N, H}), true);
+    const bool prev = l > 0;
+    Tensor g_x = at::empty_like(g_xn);
+    check(tmdnet_ln_bwd_epilogue_w(TMDNET_F32, static_cast<int>(N), static_cast<int>(H), ptr(g_xn), ptr(A.x[l]),
+                                   ptr(A.mean[l]), ptr(A.rstd[l]), ptr(p[0]), ptr(gX), nullptr, ptr(g_x), ptr(g_vec_in),
+                                   prev ? ptr(A.vecp[l - 1]) : nullptr, prev ? ptr(A.o[l - 1]) : nullptr,
+                                   prev ? ptr(g_vecp[l - 1]) : nullptr, prev ? ptr(g_o[l - 1]) : nullptr, nullptr, 0, st),
+          "tmdnet_ln_bwd_epilogue_w");
+    gX = g_x;
+    gV = g_vec_in;
+  }
+  return {gX, g_r, g_C, g_u};
+}
+
 // ----------------------------------------------------------------------------- fused inference
 // A whole ET energy + force evaluation (TorchMD_Net.forward with derivative=True, reference
 // models/model.py:232-300, torchmd_et.py:154-187, output_modules.py:80-115) as ONE operator with no autograd
@@ -1627,7 +1856,7 @@ std::tuple<Tensor, Tensor> et_stack(const Tensor& x, const Tensor& f, const Tens
 // gradient summed in-kernel).  For TorchScript inference (MD engines, reference README.md:6): the
 // scripted model takes it in eval mode; its outputs carry no autograd graph.
 std::tuple<Tensor, Tensor> et_energy_forces(
-    const Tensor& z, const Tensor& pos_in, const Tensor& batch, const Tensor& box, bool use_periodic, double cl,
+    const Tensor& z_arg, const Tensor& pos_in, const Tensor& batch_arg, const Tensor& box, bool use_periodic, double cl,
     double cu, int64_t max_pairs, bool loop, const std::string& strategy, bool check_errors, const Tensor& emb_w,
     const c10::optional<Tensor>& nb_emb_w_, const c10::optional<Tensor>& nb_dist_w_,
     const c10::optional<Tensor>& nb_dist_b_, const c10::optional<Tensor>& nb_comb_w_,
@@ -1640,8 +1869,17 @@ std::tuple<Tensor, Tensor> et_energy_forces(
               "et_energy_forces: fp32 models only");
   TORCH_CHECK(head_params.size() == 12, "et_energy_forces: the EquivariantScalar head's 12 tensors");
   at::NoGradGuard ng;
-  const Tensor pos = pos_in.detach().contiguous();
+  Tensor pos = pos_in.detach().contiguous(), z = z_arg, batch = batch_arg.contiguous();
   const int64_t N = z.size(0), H = emb_w.size(1), R = mu_in.size(0);
+  // large systems: the spatially coherent atom numbering of the eager path (TorchMD_ET.forward); the
+  // forces are returned in the caller's order
+  Tensor perm;
+  if (N >= g_reorder_min_atoms) {
+    perm = spatial_permutation(pos, batch, cu, box, use_periodic);
+    z = z.index_select(0, perm);
+    pos = pos.index_select(0, perm).contiguous();
+    batch = batch.index_select(0, perm).contiguous();
+  }
   auto o = opts(pos);
   void* st = stream_of(pos);
   const int dt = TMDNET_F32;
@@ -1676,6 +1914,22 @@ std::tuple<Tensor, Tensor> et_energy_forces(
   const Tensor src = B.nb[0].narrow(0, 0, E), dst = B.nb[1].narrow(0, 0, E), tr = B.tr.narrow(0, 0, E);
   const Tensor dl = B.dl.narrow(0, 0, E), dist = B.dist.narrow(0, 0, E);
   const Tensor& row_ptr = B.row_ptr;
+  // the fused-projection layer kernels (et_stack FEP: C5-size graphs, the configuration they implement)
+  const bool fused = E >= g_fep_min_edges && H == 128 && heads == 8 && (R == 32 || R == 64) && has_dk && has_dv &&
+                     acts == 0 && out_norm;
+  FusedAux F;
+  if (fused) {  // pair numbering: both directions of a pair read one fragment row
+    F.pair_row = at::empty({E}, iopts(pos));
+    F.pair_edge = at::empty({(E + N) / 2}, iopts(pos));
+    Tensor pws = at::empty({static_cast<int64_t>(std::max<size_t>(16, tmdnet_pair_index_workspace_bytes(static_cast<int>(N))))},
+                           pos.options().dtype(at::kByte));
+    const bool sorted_rows = strategy != "cell";  // brute / shared rows list sources ascending
+    check(tmdnet_pair_index(static_cast<int>(N), ptr<int32_t>(row_ptr), ptr<int32_t>(src), ptr<int32_t>(dst),
+                            ptr<int32_t>(tr), static_cast<int>(E), ptr<int32_t>(B.num), sorted_rows ? 1 : 0,
+                            ptr<int32_t>(F.pair_row), ptr<int32_t>(F.pair_edge), static_cast<int>(F.pair_edge.size(0)),
+                            pws.data_ptr(), static_cast<size_t>(pws.numel()), st),
+          "tmdnet_pair_index");
+  }
   // edge geometry
   Tensor f = at::empty({E, R}, o), C = at::empty({E}, o), u = at::empty({E, 3}, o);
   check(tmdnet_edge_geom_fwd(dt, static_cast<int>(E), static_cast<int>(R), static_cast<int>(rbf_type),
@@ -1700,7 +1954,8 @@ std::tuple<Tensor, Tensor> et_energy_forces(
   StackCfg c{heads, rbf_type, cl, cu, has_dk, has_dv, out_norm, acts};
   std::vector<Tensor> P(stack_params.begin(), stack_params.end());
   StackActs A;
-  auto xv = stack_forward(x1, f, dist, C, u, row_ptr, src, dst, c, P, &A);
+  auto xv = fused ? stack_forward_fused(x1, dist, C, u, row_ptr, src, mu, beta, c, P, &A, &F)
+                  : stack_forward(x1, f, dist, C, u, row_ptr, src, dst, c, P, &A);
   const Tensor xo = xv.first.contiguous(), vo = xv.second.contiguous();
   // the head (+ per-atom Jacobian) and the per-molecule sum
   Tensor y_atom = at::empty({N, 1}, o), jx = at::empty({N, H}, o), jv = at::empty({N, 3, H}, o);
@@ -1725,7 +1980,8 @@ std::tuple<Tensor, Tensor> et_energy_forces(
                            ptr(gV), st),
         "tmdnet_eq_head_bwd");
   G g{row_ptr, src, dst, tr};
-  auto gs = stack_backward_dr(A, gX, gV, dist, C, u, mu, beta, P, g, c);  // (g_x1, g_r, g_C, g_u)
+  auto gs = fused ? stack_backward_fused(A, F, gX, gV, C, u, row_ptr, src, P, c, R)
+                  : stack_backward_dr(A, gX, gV, dist, C, u, mu, beta, P, g, c);  // (g_x1, g_r, g_C, g_u)
   Tensor gf, gC_nb;
   if (nb) {
     Tensor g_cat = at::empty({N, 2 * H}, o);
@@ -1750,6 +2006,11 @@ std::tuple<Tensor, Tensor> et_energy_forces(
   check(tmdnet_nl_backward_multi(dt, static_cast<int>(N), ptr<int32_t>(row_ptr), ptr<int32_t>(tr), static_cast<int>(E),
                                  ptr(g_dl), ptr(g_r), ptr(gs[1]), ptr(dl), ptr(dist), ptr(neg_dy), st),
         "tmdnet_nl_backward_multi");
+  if (perm.defined()) {  // back to the caller's atom order
+    Tensor out = at::empty_like(neg_dy);
+    out.index_copy_(0, perm, neg_dy);
+    neg_dy = out;
+  }
   return {y, neg_dy};
 }
 
@@ -1791,6 +2052,9 @@ TORCH_LIBRARY(tmdnet, m) {
         "bool has_dk, bool has_dv, bool out_norm, Tensor[] params, int acts=0) -> (Tensor x, Tensor vec)");
   // drops the packed-weight cache of et_stack (after in-place writes that bypass the version counter)
   m.def("et_stack_invalidate() -> ()", tmdt::et_stack_invalidate);
+  // the large-system switches of et_energy_forces (Morton renumbering from min_atoms atoms, the fused
+  // projection kernels from min_edges edges; < 0 keeps a value); returns the previous values
+  m.def("set_large_system_thresholds(int min_atoms, int min_edges) -> int[]", tmdt::set_large_system_thresholds);
   m.def("et_energy_forces(Tensor z, Tensor pos, Tensor batch, Tensor box, bool use_periodic, float cutoff_lower, "
         "float cutoff_upper, int max_pairs, bool loop, str strategy, bool check_errors, Tensor emb_w, "
         "Tensor? nb_emb_w, Tensor? nb_dist_w, Tensor? nb_dist_b, Tensor? nb_comb_w, Tensor? nb_comb_b, Tensor mu, "
