@@ -1,6 +1,6 @@
 """C5 water box (50,001 atoms, ET 128 ch x 8 layers, cutoff 5, periodic, cell list) energy + forces,
 timed eagerly as bench.py's secondary_water_box does; the edge-kernel variant comes from the
-environment (TMDNET_FEP, TMDNET_FEP_BWD).  usage: python tools/c5_time.py [n_atoms] [steps]"""
+environment (TMDNET_FEP, TMDNET_FEP_BWD).  usage: python tools/c5_time.py [n_atoms] [steps] [script]"""
 import json
 import os
 import sys
@@ -33,6 +33,8 @@ def main():
     d.box = torch.eye(3, dtype=torch.float32) * L
     d.use_periodic = True
     d.strategy = "cell"
+    if len(sys.argv) > 3 and sys.argv[3] == "script":  # the MD-engine form: one tmdnet::et_energy_forces
+        model = torch.jit.script(model.eval())
     for _ in range(2):
         y, f = model(z, pos, batch)
     torch.cuda.synchronize()
