@@ -304,13 +304,11 @@ __device__ __forceinline__ void edge_chunks(const Args<T>& A, int b, int e, int 
 // ------------------------------------------------------------------ forward
 // ORD: nodes visited in the caller's `order` (cell order for large periodic systems, so the waves in
 // flight gather from a compact spatial window of source rows).
-// WPB: waves per block (4; or S = WPB = 8 / 16: one node per 512- / 1024-thread block -- the large-system
-// form, fewer nodes in flight per XCD so more second reads of a pair row hit that XCD's L2)
-template <typename T, int V, int S, int CS, bool ORD, bool GA = true, int WPB = 4>
-__global__ __launch_bounds__(WPB * 64) void k_fwd(Args<T> A) {
+template <typename T, int V, int S, int CS, bool ORD, bool GA = true>
+__global__ __launch_bounds__(256) void k_fwd(Args<T> A) {
   const int AKV = GA ? A.act_kv : kActSilu, AAT = GA ? A.act_at : kActSilu;  // GA: runtime codes
-  __shared__ T lds[S > 1 ? WPB * 64 * 4 * V : 1];
-  const Geo G = geo<S, CS, ORD, WPB>(A.n, A.L, A.order, A.xcd, blockIdx.x, gridDim.x);
+  __shared__ T lds[S > 1 ? 4 * 64 * 4 * V : 1];
+  const Geo G = geo<S, CS, ORD>(A.n, A.L, A.order, A.xcd, blockIdx.x, gridDim.x);
   const int t = G.node;
   const bool on = true;
   const int EPW = TMD_WAVE / A.L;  // edges per wave instruction
@@ -1605,24 +1603,8 @@ static int et_launch_vs(Args<T> A, hipStream_t st) {
   return et_launch_k<T, V, S, KIND, ORD, true>(A, g, b, nbn, st);
 }
 
-// TMDNET_ET_FWD_S = 8 / 16: the forward at S = WPB waves per node (one node per block; A/B switch, fp32
-// V = 4 only), read once
-static int fwd_wide() {
-  static const int w = [] { const char* e = getenv("TMDNET_ET_FWD_S"); return e ? atoi(e) : 0; }();
-  return w;
-}
-
 template <typename T, int V, int S, int KIND, bool ORD, bool GA>
 static int et_launch_k(const Args<T>& A, dim3 g, dim3 b, int nbn, hipStream_t st) {
-  if constexpr (KIND == 0 && sizeof(T) == 4 && V == 4) {
-    const int w = fwd_wide();
-    if (w == 8 || w == 16) {
-      const dim3 gw((unsigned)A.n), bw((unsigned)(64 * w));
-      if (w == 8) hipLaunchKernelGGL((k_fwd<T, V, 8, 1, ORD, GA, 8>), gw, bw, 0, st, A);
-      else hipLaunchKernelGGL((k_fwd<T, V, 16, 1, ORD, GA, 16>), gw, bw, 0, st, A);
-      return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
-    }
-  }
   if (KIND == 0) hipLaunchKernelGGL((k_fwd<T, V, S, 1, ORD, GA>), g, b, 0, st, A);
   else if (KIND == 1) hipLaunchKernelGGL((k_bwd_dst<T, V, S, 1, false, false, GA>), g, b, 0, st, A);
   else if (KIND == 2) hipLaunchKernelGGL((k_bwd_src<T, V, S, 1, GA>), g, b, 0, st, A);
