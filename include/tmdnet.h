@@ -676,6 +676,28 @@ int tmdnet_et_fused_bwd_f32(int n_nodes, int hidden, int heads, int num_rbf, con
                             void* gunit, void* gdist, int accumulate, void* workspace, size_t workspace_bytes,
                             void* stream);
 
+/* The neighbour embedding with distance_proj FUSED in (reference NeighborEmbedding, models/utils.py:90-108):
+ * tmdnet_nbr_embed_fwd's output with W = distance_proj(rbf) formed per 16-edge tile on the fp16 MFMA from
+ * the tmdnet_fep_frags_f32 fragments and the tmdnet_fep_split_f32 image of distance_proj (D = hidden
+ * rows, its bias) -- no E x hidden rows:
+ *   out[t] = sum_{e in row t, src[e] != t} x[src[e]] * (W f(r_e) + b) * cutoff[e]   (row stride ld_out),
+ * and with x_self / out_self (both or neither) the [x_self | x_nb] concatenation as tmdnet_nbr_embed_fwd.
+ * The force pass's backward ("dr mode", first order, no parameter or x gradients) -- per edge
+ *   gcut[e] = sum_h grad_out[t][h] x[s][h] (W f + b)[h],  gdist[e] = cutoff[e] sum_h grad_out[t][h] x[s][h] (W f')[h]
+ * (0 for self edges), written (or added with TMDNET_ACC_EDGE; written: rows [row_ptr[n], max_pairs) set to 0).
+ * fp32; hidden = 128, num_rbf 32 or 64; x / img / frags / out / grad_out 16-byte aligned, strides % 4 == 0;
+ * else TMDNET_UNSUPPORTED. */
+int tmdnet_nbr_fused_fwd_f32(int n_nodes, int hidden, int num_rbf, const int32_t* row_ptr, const int32_t* src,
+                             int max_pairs, const void* x, int ld_x, const void* cutoff, const int32_t* frag_rows,
+                             const void* frags, long long n_frag_rows, const void* img, const void* wsc,
+                             const void* bias, void* out, int ld_out, const void* x_self, void* out_self,
+                             void* stream);
+int tmdnet_nbr_fused_bwd_f32(int n_nodes, int hidden, int num_rbf, const int32_t* row_ptr, const int32_t* src,
+                             int max_pairs, const void* x, int ld_x, const void* cutoff, const int32_t* frag_rows,
+                             const void* frags, const void* dscale, long long n_frag_rows, const void* img,
+                             const void* wsc, const void* bias, const void* grad_out, int ld_grad_out, void* gcut,
+                             void* gdist, int accumulate, void* stream);
+
 /* Energy + force MSE training loss (reference LNNP.step, module.py:130-179, mean reductions):
  *   out[0] = w1 * mean((a1 - b1)^2) + w2 * mean((a2 - b2)^2)   over n1 / n2 elements (one launch),
  * and its backward d1 = g w1 2 (a1 - b1) / n1, d2 = g w2 2 (a2 - b2) / n2 with g = grad_out[0] read

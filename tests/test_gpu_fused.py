@@ -133,3 +133,78 @@ def test_fused_c2_molecules_vs_oracle_and_unfused(planar, monkeypatch):
     assert calls.count("f") == 8
     assert _rel(y.detach(), y0.detach()) < 1e-5
     assert _rel(f.detach(), f0.detach()) < 1e-4
+
+
+def test_fused_neighbor_embedding_force_pass_and_parameter_gradients(monkeypatch):
+    """The neighbour embedding with distance_proj fused into its aggregation kernel
+    (kernels.nbr_embed_fused: tmdnet_nbr_fused_fwd_f32, dr-mode tmdnet_nbr_fused_bwd_f32; reference
+    utils.py:90-108) on a 3000-atom periodic water box: energy and forces against the row path
+    (TMDNET_NE_FUSED=0: W = distance_proj(rbf) rows, the unfused kernels) and against fp64; then the
+    composite backward (parameter gradients of an energy loss, distance_proj / embedding / combine)
+    against the row path's."""
+    from torchmdnet import kernels
+    from torchmdnet.models import torchmd_et
+    calls = []
+    orig = kernels.nbr_embed_fused
+    monkeypatch.setattr(kernels, "nbr_embed_fused", lambda *a, **k: (calls.append(1), orig(*a, **k))[1])
+    z, pos, L = _water_box(3000)
+    m = _model(64, "expnorm")
+    sd = m.state_dict()
+    y, f = _run(m, z, pos, L, torch.float32)
+    assert len(calls) == 1, "the fused neighbour embedding did not run"
+    monkeypatch.setattr(torchmd_et, "NE_FUSED", False)
+    y0, f0 = _run(m, z, pos, L, torch.float32)
+    assert len(calls) == 1
+    assert _rel(y, y0) < 1e-5 and _rel(f, f0) < 1e-4
+    m64 = _model(64, "expnorm", precision=64)
+    m64.load_state_dict({k: v.double() if v.is_floating_point() else v for k, v in sd.items()})
+    y64, f64 = _run(m64, z, pos, L, torch.float64)
+    assert _rel(y, y64) < 1e-5 and _rel(f, f64) < 1e-4
+
+    monkeypatch.setattr(torchmd_et, "NE_FUSED", True)
+    m.derivative = False
+    m.zero_grad(set_to_none=True)
+    m = m.to(DEV)
+    dd = m.representation_model.distance
+    dd.box = torch.eye(3) * L
+    dd.use_periodic = True
+    dd.strategy = "cell"
+    n0 = len(calls)
+    m(z.to(DEV), pos.float().to(DEV), torch.zeros_like(z).to(DEV))[0].sum().backward()
+    assert len(calls) == n0 + 1
+    ne = m.representation_model.neighbor_embedding
+    g1 = [p.grad.detach().clone() for p in (ne.distance_proj.weight, ne.distance_proj.bias, ne.embedding.weight,
+                                             ne.combine.weight)]
+    monkeypatch.setattr(torchmd_et, "NE_FUSED", False)
+    m.zero_grad(set_to_none=True)
+    m(z.to(DEV), pos.float().to(DEV), torch.zeros_like(z).to(DEV))[0].sum().backward()
+    g0 = [p.grad for p in (ne.distance_proj.weight, ne.distance_proj.bias, ne.embedding.weight, ne.combine.weight)]
+    m.derivative = True
+    for a, b in zip(g1, g0):
+        assert _rel(a, b) < 1e-4
+
+
+def test_fused_neighbor_embedding_force_loss_second_order(monkeypatch):
+    """Force-matching training through the fused neighbour embedding: the dr-mode backward
+    (_NbrEmbedFusedBwd) differentiated again (its composite second order) gives the same parameter
+    gradients of a force loss as the row path (TMDNET_NE_FUSED=0)."""
+    from torchmdnet.models import torchmd_et
+    z, pos, L = _water_box(3000)
+    m = _model(64, "expnorm").to(DEV)
+    d = m.representation_model.distance
+    d.box = torch.eye(3) * L
+    d.use_periodic = True
+    d.strategy = "cell"
+    ne = m.representation_model.neighbor_embedding
+    ps = [ne.distance_proj.weight, ne.distance_proj.bias, ne.embedding.weight, ne.combine.weight]
+
+    def grads(fused):
+        monkeypatch.setattr(torchmd_et, "NE_FUSED", fused)
+        m.zero_grad(set_to_none=True)
+        y, f = m(z.to(DEV), pos.float().to(DEV), torch.zeros_like(z).to(DEV))
+        (f.pow(2).sum() + y.sum()).backward()
+        return [p.grad.detach().clone() for p in ps]
+
+    g1, g0 = grads(True), grads(False)
+    for a, b in zip(g1, g0):
+        assert _rel(a, b) < 1e-4

@@ -218,10 +218,10 @@ __device__ __forceinline__ int wfrag_base(int lane, int ks) {
 
 // One 16-channel block of the tile's projection: acc[i] = sum_k W[16 blk + 4 g + i][k] B[k][c] -- the
 // weight block is the A operand, the RBF (or its derivative) tile B.  Pieces: small terms first.
-template <int KS>
+template <int KS, int D = kD>
 __device__ __forceinline__ f4 block_acc(const char* wl, const int (&wb)[KS], int blk, const h8 (&b0)[KS],
                                         const h8 (&b1)[KS]) {
-  constexpr int R = 32 * KS, PB = kD * R * (int)sizeof(_Float16);
+  constexpr int R = 32 * KS, PB = D * R * (int)sizeof(_Float16);
   f4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks) {
@@ -235,10 +235,10 @@ __device__ __forceinline__ f4 block_acc(const char* wl, const int (&wb)[KS], int
   return acc;
 }
 // pre-activation: acc * scale + bias of the lane's four channels
-template <int KS>
+template <int KS, int D = kD>
 __device__ __forceinline__ f4 block_pre(const char* wl, const int (&wb)[KS], const float* sc, const float* sb,
                                         int blk, const h8 (&b0)[KS], const h8 (&b1)[KS], int g) {
-  const f4 acc = block_acc<KS>(wl, wb, blk, b0, b1);
+  const f4 acc = block_acc<KS, D>(wl, wb, blk, b0, b1);
   const f4 s = *reinterpret_cast<const f4*>(sc + 16 * blk + 4 * g);
   const f4 b = *reinterpret_cast<const f4*>(sb + 16 * blk + 4 * g);
   return acc * s + b;
@@ -282,11 +282,11 @@ __device__ __forceinline__ f4 block_dpre(const char* wl, const int (&wb)[KS], co
 }
 
 // pre and d pre / d r of one block from ONE read of its weight fragments (the destination pass)
-template <int KS>
+template <int KS, int D = kD>
 __device__ __forceinline__ void block_pre_dpre(const char* wl, const int (&wb)[KS], const float* sc, const float* sb,
                                                float dsc, int blk, const h8 (&b0)[KS], const h8 (&b1)[KS],
                                                const h8 (&d0)[KS], const h8 (&d1)[KS], int g, f4& pre, f4& dpre) {
-  constexpr int R = 32 * KS, PB = kD * R * (int)sizeof(_Float16);
+  constexpr int R = 32 * KS, PB = D * R * (int)sizeof(_Float16);
   f4 a = {0.f, 0.f, 0.f, 0.f}, d = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks) {
@@ -305,6 +305,41 @@ __device__ __forceinline__ void block_pre_dpre(const char* wl, const int (&wb)[K
   pre = a * s + b;
   dpre = d * (s * dsc);
 }
+
+// t (as block_t) and d pre / d r up to the edge's derivative scale (W f' times the row scale; the caller
+// multiplies its r-sums by dsc once per edge) from ONE read of the block's weight fragments (the
+// destination pass); sct / sbt the t-domain constants, sc the raw row scales
+template <int KS>
+__device__ __forceinline__ void block_t_dr(const char* wl, const int (&wb)[KS], const float* sct, const float* sbt,
+                                           const float* sc, int blk, const h8 (&b0)[KS], const h8 (&b1)[KS],
+                                           const h8 (&d0)[KS], const h8 (&d1)[KS], int g, f4& t, f4& dr) {
+  constexpr int R = 32 * KS, PB = kD * R * (int)sizeof(_Float16);
+  f4 a = *reinterpret_cast<const f4*>(sbt + 16 * blk + 4 * g), d = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    const char* f0 = wl + wb[ks] + blk * 16 * R * (int)sizeof(_Float16);
+    const h8 w0 = *reinterpret_cast<const h8*>(f0);
+    const h8 w1 = *reinterpret_cast<const h8*>(f0 + PB);
+    a = __builtin_amdgcn_mfma_f32_16x16x32_f16(w0, b1[ks], a, 0, 0, 0);
+    d = __builtin_amdgcn_mfma_f32_16x16x32_f16(w0, d1[ks], d, 0, 0, 0);
+    a = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1, b0[ks], a, 0, 0, 0);
+    d = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1, d0[ks], d, 0, 0, 0);
+    a = __builtin_amdgcn_mfma_f32_16x16x32_f16(w0, b0[ks], a, 0, 0, 0);
+    d = __builtin_amdgcn_mfma_f32_16x16x32_f16(w0, d0[ks], d, 0, 0, 0);
+  }
+  t = a * *reinterpret_cast<const f4*>(sct + 16 * blk + 4 * g);
+  dr = d * *reinterpret_cast<const f4*>(sc + 16 * blk + 4 * g);
+}
+// t-domain SiLU with its derivative: sig = 1 / (1 + 2^t), u = t sig (SiLU = -ln2 u) and
+// SiLU'(pre) = sig + SiLU (1 - sig) = sig - ln2 (u - u sig)
+struct SiluT {
+  float sig, u, d;
+  __device__ __forceinline__ explicit SiluT(float t) {
+    sig = __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(t));
+    u = t * sig;
+    d = fmaf(kNegLn2, fmaf(-u, sig, u), sig);
+  }
+};
 
 // the seven 16-byte node-row gathers of one head for the lane's edge: k, v (x | v1 | v2), vec (3 axes)
 struct Gat {
@@ -459,7 +494,10 @@ struct Fwd {
 };
 
 // HPW heads per work item (G = 8 / HPW items per node); NW waves per workgroup
-template <int KS, int HPW, int NW, bool PL>
+// HP: head-pipelined gathers -- head hh + 1's seven gathers are issued before head hh computes, so they
+// have a whole head's MFMA and SiLU work to land (one extra set of gather registers); HP = 2 also issues
+// the next tile's first head during the last head (the set then lives across the tile loop)
+template <int KS, int HPW, int NW, bool PL, int HP = 0>
 __global__ __launch_bounds__(NW * 64, 1) void k_fwd(Fwd P) {
   constexpr int R = 32 * KS, H = kH, G = kHeads / HPW, BS = 16 * R * (int)sizeof(_Float16);
   __shared__ __attribute__((aligned(16))) _Float16 w[2 * kD * R];
@@ -497,6 +535,7 @@ __global__ __launch_bounds__(NW * 64, 1) void k_fwd(Fwd P) {
     // the next tile's edge scalars are loaded while this tile computes: a tile waits on one memory round
     // trip (its fragments and gathers), not two
     Edge En = load_edge(rb + c, re, P.src, P.C, P.u, P.frow, 8 * R, 1.f);
+    Gat Xc;  // HP: the gathers of the head about to compute (issued one head ahead, across tiles too)
     for (int base = rb; base < re; base += 16) {
       const Edge E = En;
       TMD_DCHECK(E.s >= 0 && E.s < P.n);
@@ -511,10 +550,21 @@ __global__ __launch_bounds__(NW * 64, 1) void k_fwd(Fwd P) {
       int wb[KS];
       frag_offsets<KS>(lane, h0, wb);
       const char* wt = reinterpret_cast<const char*>(w);
+      if (HP == 1 || (HP == 2 && base == rb)) gather_kvw<PL>(Xc, Rk, Rv, Rw, ok_, ov_, ow_, h0);
       static_for<HPW>([&](auto hc) {
         constexpr int hh = decltype(hc)::value;
-        Gat X;
-        gather_kvw<PL>(X, Rk, Rv, Rw, ok_, ov_, ow_, h0 + hh);
+        Gat X, Xn;
+        if (HP) {
+          if (hh + 1 < HPW) {
+            gather_kvw<PL>(Xn, Rk, Rv, Rw, ok_, ov_, ow_, h0 + hh + 1);
+          } else if (HP == 2 && base + 16 < re) {  // the next tile's first head (its edge scalars are in En)
+            gather_kvw<PL>(Xn, Rk, Rv, Rw, En.ok ? (En.s * P.ldk + 4 * g) * 4 : kOOB,
+                           En.ok ? (En.s * P.ldv + 4 * g) * 4 : kOOB, En.ok ? (En.s * 3 * H + 4 * g) * 4 : kOOB, h0);
+          }
+          X = Xc;
+        } else {
+          gather_kvw<PL>(X, Rk, Rv, Rw, ok_, ov_, ow_, h0 + hh);
+        }
         // t-domain: silu(pre) = -ln2 u(t); the -ln2 is in the staged q (dk) and applied to the sums (dv)
         const f4 pk = block_t<KS>(wt, wb, sct, sbt, hh, B0, B1, g);
         const f4 px = block_t<KS>(wt, wb, sct, sbt, 8 + hh, B0, B1, g);
@@ -535,6 +585,7 @@ __global__ __launch_bounds__(NW * 64, 1) void k_fwd(Fwd P) {
           a1[hh][i] += X.w1[i] * v1e + v2e * E.uy;
           a2[hh][i] += X.w2[i] * v1e + v2e * E.uz;
         }
+        if (HP) Xc = Xn;
         __builtin_amdgcn_sched_barrier(0);
       });
       (void)BS;
@@ -602,15 +653,17 @@ struct Bwd {
 // projection gradient contracted with d pre / d r in registers).  HPW heads per work item; t's q, gx,
 // gvec channels of the slice staged in the wave's LDS slot.  The per-edge sums run over every channel:
 // with one slice (HPW = 8) they are written directly, else each slice writes its part for k_edge_combine.
-template <int KS, int HPW, int NW, bool PL>
+template <int KS, int HPW, int NW, bool PL, int HP = 0>
 __global__ __launch_bounds__(NW * 64, 1) void k_bwd_dst(Bwd P) {
   constexpr int R = 32 * KS, H = kH, G = kHeads / HPW, CH = 16 * HPW;
   __shared__ __attribute__((aligned(16))) _Float16 w[2 * kD * R];
   __shared__ __attribute__((aligned(16))) float s_sc[kD];
   __shared__ __attribute__((aligned(16))) float s_b[kD];
+  __shared__ __attribute__((aligned(16))) float s_raw[kD];  // the raw row scales (d pre / d r)
   __shared__ __attribute__((aligned(16))) float s_node[NW][5 * CH];  // q | gx | gvec (3) of the slice
   __shared__ int s_next;
-  load_image<KS, NW * 64>(w, s_sc, s_b, P.img, P.wsc, P.bias);
+  load_image_t<KS, NW * 64>(w, s_sc, s_b, P.img, P.wsc, P.bias);
+  for (int i = threadIdx.x; i < kD; i += NW * 64) s_raw[i] = P.wsc[i];
   if (threadIdx.x == 0) s_next = 0;
   if (G == 1) {  // static-capacity lists: edge slots past the last row belong to no row -- zeroed here
     const int e0 = min(P.row_ptr[P.n], P.cap);
@@ -647,10 +700,12 @@ __global__ __launch_bounds__(NW * 64, 1) void k_bwd_dst(Bwd P) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     const float* sct = s_sc + 16 * h0;
     const float* sbt = s_b + 16 * h0;
+    const float* scr = s_raw + 16 * h0;
     f4 gq[HPW];
 #pragma unroll
     for (int hh = 0; hh < HPW; ++hh) gq[hh] = f4{0.f, 0.f, 0.f, 0.f};
     Edge En = load_edge(rb + c, re, P.src, P.C, P.u, P.frow, 8 * R, 1.f);  // (next tile's scalars: as k_fwd)
+    Gat Xc;
     for (int base = rb; base < re; base += 16) {
       const int e = base + c;
       const Edge E = En;
@@ -667,63 +722,76 @@ __global__ __launch_bounds__(NW * 64, 1) void k_bwd_dst(Bwd P) {
       frag_offsets<KS>(lane, h0, wb);
       const char* wt = reinterpret_cast<const char*>(w);
       float eC = 0.f, er = 0.f, eu0 = 0.f, eu1 = 0.f, eu2 = 0.f;
+      if (HP == 1 || (HP == 2 && base == rb)) gather_kvw<PL>(Xc, Rk, Rv, Rw, ok_, ov_, ow_, h0);
       static_for<HPW>([&](auto hc) {
         constexpr int hh = decltype(hc)::value;
-        Gat X;
-        gather_kvw<PL>(X, Rk, Rv, Rw, ok_, ov_, ow_, h0 + hh);
+        Gat X, Xn;
+        if (HP) {  // head-pipelined gathers, as k_fwd
+          if (hh + 1 < HPW) {
+            gather_kvw<PL>(Xn, Rk, Rv, Rw, ok_, ov_, ow_, h0 + hh + 1);
+          } else if (HP == 2 && base + 16 < re) {
+            gather_kvw<PL>(Xn, Rk, Rv, Rw, En.ok ? (En.s * P.ldk + 4 * g) * 4 : kOOB,
+                           En.ok ? (En.s * P.ldv + 4 * g) * 4 : kOOB, En.ok ? (En.s * 3 * H + 4 * g) * 4 : kOOB, h0);
+          }
+          X = Xc;
+        } else {
+          gather_kvw<PL>(X, Rk, Rv, Rw, ok_, ov_, ow_, h0 + hh);
+        }
         const f4 qd = *reinterpret_cast<const f4*>(nd + 16 * hh + 4 * g);
         const f4 gxd = *reinterpret_cast<const f4*>(nd + CH + 16 * hh + 4 * g);
-        // the attention part (dk, dv_x blocks) first: its head sums gate every other term
-        f4 pk, rk, px, rx;
-        block_pre_dpre<KS>(wt, wb, sct, sbt, dsc, hh, B0, B1, D0, D1, g, pk, rk);
-        block_pre_dpre<KS>(wt, wb, sct, sbt, dsc, 8 + hh, B0, B1, D0, D1, g, px, rx);
-        f4 kdk, gpk, gpx;
-        float pa = 0.f, pg = 0.f;
+        // the attention part (dk, dv_x blocks) first: its head sums gate every other term.  t-domain
+        // (SiluT): the SiLU values enter as u = SiLU / -ln2 -- the head sums, gq and g_unit take the -ln2
+        // once -- and the r-sums as (d pre / d r) / dsc, multiplied by dsc once per edge
+        f4 tk, rk, tx, rx;
+        block_t_dr<KS>(wt, wb, sct, sbt, scr, hh, B0, B1, D0, D1, g, tk, rk);
+        block_t_dr<KS>(wt, wb, sct, sbt, scr, 8 + hh, B0, B1, D0, D1, g, tx, rx);
+        f4 kdu;
+        float pa = 0.f, pg = 0.f, sk = 0.f, sx = 0.f;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const Silu<float> fk(pk[i]);
-          kdk[i] = X.kk[i] * fk.s;
-          gpk[i] = qd[i] * X.kk[i] * fk.d(pk[i]);  // x gs below
-          pa += qd[i] * kdk[i];
-          const Silu<float> fx(px[i]);
-          pg += gxd[i] * X.vx[i] * fx.s;
-          gpx[i] = gxd[i] * X.vx[i] * fx.d(px[i]);  // x a below
+          const SiluT fk(tk[i]), fx(tx[i]);
+          const float qk = qd[i] * X.kk[i], gv = gxd[i] * X.vx[i];
+          kdu[i] = X.kk[i] * fk.u;
+          pa = fmaf(qk, fk.u, pa);
+          sk = fmaf(qk, fk.d * rk[i], sk);
+          pg = fmaf(gv, fx.u, pg);
+          sx = fmaf(gv, fx.d * rx[i], sx);
         }
-        const float att = gsum(pa), ga = gsum(pg);
+        const float att = kNegLn2 * gsum(pa), ga = kNegLn2 * gsum(pg);
         const Silu<float> sa(att);
         const float a = sa.s * E.C;
         const float gs = ga * E.C * sa.d(att);
         eC += ga * sa.s;
+        er = fmaf(gs, sk, fmaf(a, sx, er));
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          gq[hh][i] += gs * kdk[i];
-          er += gs * gpk[i] * rk[i] + a * gpx[i] * rx[i];
-        }
+        for (int i = 0; i < 4; ++i) gq[hh][i] = fmaf(gs, kdu[i], gq[hh][i]);
         // the vector parts (dv_1, dv_2 blocks)
         const f4 g0 = *reinterpret_cast<const f4*>(nd + 2 * CH + 16 * hh + 4 * g);
         const f4 g1 = *reinterpret_cast<const f4*>(nd + 3 * CH + 16 * hh + 4 * g);
         const f4 g2 = *reinterpret_cast<const f4*>(nd + 4 * CH + 16 * hh + 4 * g);
-        f4 p1, r1, p2, r2;
-        block_pre_dpre<KS>(wt, wb, sct, sbt, dsc, 16 + hh, B0, B1, D0, D1, g, p1, r1);
-        block_pre_dpre<KS>(wt, wb, sct, sbt, dsc, 24 + hh, B0, B1, D0, D1, g, p2, r2);
+        f4 t1, r1, t2, r2;
+        block_t_dr<KS>(wt, wb, sct, sbt, scr, 16 + hh, B0, B1, D0, D1, g, t1, r1);
+        block_t_dr<KS>(wt, wb, sct, sbt, scr, 24 + hh, B0, B1, D0, D1, g, t2, r2);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const Silu<float> f1(p1[i]), f2(p2[i]);
+          const SiluT f1(t1[i]), f2(t2[i]);
           const float gv1e = g0[i] * X.w0[i] + g1[i] * X.w1[i] + g2[i] * X.w2[i];
           const float gv2e = g0[i] * E.ux + g1[i] * E.uy + g2[i] * E.uz;
-          er += gv1e * X.v1[i] * f1.d(p1[i]) * r1[i] + gv2e * X.v2[i] * f2.d(p2[i]) * r2[i];
-          const float v2e = X.v2[i] * f2.s;
-          eu0 += g0[i] * v2e;
-          eu1 += g1[i] * v2e;
-          eu2 += g2[i] * v2e;
+          er = fmaf(gv1e * X.v1[i], f1.d * r1[i], er);
+          er = fmaf(gv2e * X.v2[i], f2.d * r2[i], er);
+          const float v2u = X.v2[i] * f2.u;
+          eu0 = fmaf(g0[i], v2u, eu0);
+          eu1 = fmaf(g1[i], v2u, eu1);
+          eu2 = fmaf(g2[i], v2u, eu2);
         }
+        if (HP) Xc = Xn;
         __builtin_amdgcn_sched_barrier(0);
       });
       // the edge sums over the 4 lane groups (eC is already a head total in every lane)
-      er = gsum(er);
-      eu0 = gsum(eu0);
-      eu1 = gsum(eu1);
-      eu2 = gsum(eu2);
+      er = dsc * gsum(er);
+      eu0 = kNegLn2 * gsum(eu0);
+      eu1 = kNegLn2 * gsum(eu1);
+      eu2 = kNegLn2 * gsum(eu2);
       if (g == 0 && E.ok) {
         if (G == 1) {
           float* gu = P.gu + 3 * (size_t)e;
@@ -752,7 +820,7 @@ __global__ __launch_bounds__(NW * 64, 1) void k_bwd_dst(Bwd P) {
     for (int hh = 0; hh < HPW; ++hh) {
       f4 sq;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) sq[i] = row_sum16(gq[hh][i]);
+      for (int i = 0; i < 4; ++i) sq[i] = kNegLn2 * row_sum16(gq[hh][i]);
       if (c == hh) Q = sq;
     }
     if (c < HPW) {
@@ -945,6 +1013,429 @@ __global__ __launch_bounds__(NW * 64, 1) void k_bwd_src(Bwd P) {
   }
 }
 
+// Merged backward (round 5): ONE pass over node t's row does both passes above.  Edge e = (t <- s) is the
+// destination pass's edge and, read reversed (t -> s, unit vector negated), the source pass's edge of t's
+// row -- both with the same pair's dk / dv pre-activations, which are now formed (with their r-derivatives)
+// once per edge and head instead of once in each pass.  Every output is t's (gq | gk, gv, gvec_in) or e's
+// (the per-edge sums), so it stays deterministic without atomics.  Per (edge, head) the lane gathers s's
+// k, v, vec (destination terms) and q, gx, gvec (source terms): 12 16-byte loads.
+template <int KS, int HPW, int NW, bool PL>
+__global__ __launch_bounds__(NW * 64, 1) void k_bwd_row(Bwd P) {
+  constexpr int R = 32 * KS, H = kH, G = kHeads / HPW, CH = 16 * HPW;
+  // t's staged channels of the slice: q | gx | gvec (3) | k | v_x | v_1 | vec (3)
+  constexpr int NQ = 0, NGX = 1, NGV = 2, NK = 5, NVX = 6, NV1 = 7, NW0 = 8, NP = 11;
+  __shared__ __attribute__((aligned(16))) _Float16 w[2 * kD * R];
+  __shared__ __attribute__((aligned(16))) float s_sc[kD];
+  __shared__ __attribute__((aligned(16))) float s_b[kD];
+  __shared__ __attribute__((aligned(16))) float s_node[NW][NP * CH];
+  __shared__ int s_next;
+  load_image<KS, NW * 64>(w, s_sc, s_b, P.img, P.wsc, P.bias);
+  if (threadIdx.x == 0) s_next = 0;
+  if (G == 1) {  // static-capacity lists: edge slots past the last row belong to no row -- zeroed here
+    const int e0 = min(P.row_ptr[P.n], P.cap);
+    for (int e = e0 + blockIdx.x * NW * 64 + threadIdx.x; e < P.cap; e += gridDim.x * NW * 64) {
+      P.gC[e] = 0.f;
+      P.gu[3 * (size_t)e] = P.gu[3 * (size_t)e + 1] = P.gu[3 * (size_t)e + 2] = 0.f;
+      P.gr[e] = 0.f;
+    }
+  }
+  __syncthreads();
+  const Work W = work_range<G>(P.n, P.chunk);
+  const int lane = lane_id(), c = lane & 15, g = lane >> 4, wid = threadIdx.x >> 6;
+  const bool acc_edge = P.acc & TMDNET_ACC_EDGE, ag = P.acc & TMDNET_ACC_GRADS;
+  const bool resid = P.acc & TMDNET_ACC_VEC_RESIDUAL;
+  const rsrc_t Rk = make_rsrc(P.k, (unsigned)P.n * P.ldk * 4u), Rv = make_rsrc(P.v, (unsigned)P.n * P.ldv * 4u);
+  const rsrc_t Rw = make_rsrc(P.vec, P.vec ? (unsigned)P.n * 3u * H * 4u : 0u);
+  const rsrc_t Rq = make_rsrc(P.q, (unsigned)P.n * P.ldq * 4u), Rgx = make_rsrc(P.gx, (unsigned)P.n * H * 4u);
+  const rsrc_t Rgv = make_rsrc(P.gvec, (unsigned)P.n * 3u * H * 4u);
+  const rsrc_t Rf = make_rsrc(P.fr, P.fr_bytes);
+  constexpr int PV = VL<PL>::part;
+  float* nd = s_node[wid];
+  auto own = [&](int part, int hh) { return *reinterpret_cast<const f4*>(nd + part * CH + 16 * hh + 4 * g); };
+  for (;;) {
+    const int it = next_item(&s_next);
+    if (it >= W.items) break;
+    int t, sl;
+    if (!work_item<G>(W, it, t, sl)) continue;
+    const int h0 = sl * HPW;
+    const int rb = min(P.row_ptr[t], P.cap), re = min(P.row_ptr[t + 1], P.cap);
+    __builtin_amdgcn_wave_barrier();
+    for (int i = lane; i < NP * CH / 4; i += 64) {
+      const int part = i / (CH / 4), jj = i % (CH / 4), hh = jj / 4, o = 4 * (jj % 4);
+      const int h = h0 + hh;
+      f4 val{0.f, 0.f, 0.f, 0.f};
+      if (part == NQ) val = *reinterpret_cast<const f4*>(P.q + (size_t)t * P.ldq + 16 * h + o);
+      else if (part == NGX) val = *reinterpret_cast<const f4*>(P.gx + (size_t)t * H + 16 * h + o);
+      else if (part < NK) val = *reinterpret_cast<const f4*>(P.gvec + ((size_t)t * 3 + (part - NGV)) * H + 16 * h + o);
+      else if (part == NK) val = *reinterpret_cast<const f4*>(P.k + (size_t)t * P.ldk + 16 * h + o);
+      else if (part < NW0)
+        val = *reinterpret_cast<const f4*>(P.v + (size_t)t * P.ldv + VL<PL>::head * h + (part - NVX) * PV + o);
+      else if (P.vec) val = *reinterpret_cast<const f4*>(P.vec + ((size_t)t * 3 + (part - NW0)) * H + 16 * h + o);
+      *reinterpret_cast<f4*>(nd + 4 * i) = val;
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const float* sct = s_sc + 16 * h0;
+    const float* sbt = s_b + 16 * h0;
+    const f4 z4{0.f, 0.f, 0.f, 0.f};
+    // source-term sums: gk, gv_x, gv_2 and A_a = sum_s gvec[s]_a silu(p1) (a = axis); gvec_in[t]_a =
+    // v_1[t] A_a and gv_1[t] = sum_a vec[t]_a A_a are formed from A once per node, not per edge
+    f4 gq[HPW], gk[HPW], gvx[HPW], gv2[HPW], A0[HPW], A1[HPW], A2[HPW];
+#pragma unroll
+    for (int hh = 0; hh < HPW; ++hh) gq[hh] = gk[hh] = gvx[hh] = gv2[hh] = A0[hh] = A1[hh] = A2[hh] = z4;
+    Edge En = load_edge(rb + c, re, P.src, P.C, P.u, P.frow, 8 * R, 1.f);
+    for (int base = rb; base < re; base += 16) {
+      const int e = base + c;
+      const Edge E = En;
+      if (base + 16 < re) En = load_edge(base + 16 + c, re, P.src, P.C, P.u, P.frow, 8 * R, 1.f);
+      TMD_DCHECK(E.s >= 0 && E.s < P.n);
+      h8 B0[KS], B1[KS], D0[KS], D1[KS];
+      load_frags<KS>(Rf, E.fo, g, 0, B0, B1);
+      load_frags<KS>(Rf, E.fo, g, 1, D0, D1);
+      const float dsc = E.ok ? P.dscale[E.fo / (8 * R)] : 1.f;
+      const int ok_ = E.ok ? (E.s * P.ldk + 4 * g) * 4 : kOOB;
+      const int ov_ = E.ok ? (E.s * P.ldv + 4 * g) * 4 : kOOB;
+      const int ow_ = E.ok ? (E.s * 3 * H + 4 * g) * 4 : kOOB;
+      const int oq = E.ok ? (E.s * P.ldq + 4 * g) * 4 : kOOB;
+      const int ox = E.ok ? (E.s * H + 4 * g) * 4 : kOOB;
+      int wb[KS];
+      frag_offsets<KS>(lane, h0, wb);
+      const char* wt = reinterpret_cast<const char*>(w);
+      float eC = 0.f, er = 0.f, eu0 = 0.f, eu1 = 0.f, eu2 = 0.f;
+      static_for<HPW>([&](auto hc) {
+        constexpr int hh = decltype(hc)::value;
+        // the attention phase's gathers: s's k, v_x (destination terms), q, gx (source terms)
+        const int sh = __builtin_amdgcn_readfirstlane(64 * (h0 + hh));
+        const int sv = __builtin_amdgcn_readfirstlane(4 * VL<PL>::head * (h0 + hh));
+        const f4 kk = bld4<0>(Rk, ok_, sh), vx = bld4<0>(Rv, ov_, sv);
+        const f4 qm = bld4<0>(Rq, oq, sh), gxm = bld4<0>(Rgx, ox, sh);
+        const f4 qd = own(NQ, hh), gxd = own(NGX, hh), kt = own(NK, hh), vxt = own(NVX, hh);
+        // the attention blocks (dk, dv_x) of both directions
+        f4 pk, rk, px, rx;
+        block_pre_dpre<KS>(wt, wb, sct, sbt, dsc, hh, B0, B1, D0, D1, g, pk, rk);
+        block_pre_dpre<KS>(wt, wb, sct, sbt, dsc, 8 + hh, B0, B1, D0, D1, g, px, rx);
+        f4 kdk, gpk, gpx, dk, dvx;
+        float pa = 0.f, pg = 0.f, qa = 0.f, qg = 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const Silu<float> fk(pk[i]);
+          dk[i] = fk.s;
+          kdk[i] = kk[i] * fk.s;
+          gpk[i] = qd[i] * kk[i] * fk.d(pk[i]);  // x gs below
+          pa += qd[i] * kdk[i];
+          qa += qm[i] * kt[i] * fk.s;
+          const Silu<float> fx(px[i]);
+          dvx[i] = fx.s;
+          pg += gxd[i] * vx[i] * fx.s;
+          gpx[i] = gxd[i] * vx[i] * fx.d(px[i]);  // x a below
+          qg += gxm[i] * vxt[i] * fx.s;
+        }
+        const float att = gsum(pa), ga = gsum(pg), att2 = gsum(qa), ga2 = gsum(qg);
+        const Silu<float> sa(att), sa2(att2);
+        const float a = sa.s * E.C, a2 = sa2.s * E.C;
+        const float gs = ga * E.C * sa.d(att), gs2 = ga2 * E.C * sa2.d(att2);
+        eC += ga * sa.s;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          gq[hh][i] += gs * kdk[i];
+          er += gs * gpk[i] * rk[i] + a * gpx[i] * rx[i];
+          gk[hh][i] += gs2 * qm[i] * dk[i];
+          gvx[hh][i] += gxm[i] * a2 * dvx[i];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        // the vector phase: s's v_1, v_2, vec (destination) and gvec (source terms)
+        constexpr int PVB = 4 * VL<PL>::part;
+        const f4 v1 = bld4<PVB>(Rv, ov_, sv), v2 = bld4<2 * PVB>(Rv, ov_, sv);
+        const f4 w0 = bld4<0>(Rw, ow_, sh), w1 = bld4<4 * kH>(Rw, ow_, sh), w2 = bld4<8 * kH>(Rw, ow_, sh);
+        const f4 m0 = bld4<0>(Rgv, ow_, sh), m1 = bld4<4 * kH>(Rgv, ow_, sh), m2 = bld4<8 * kH>(Rgv, ow_, sh);
+        const f4 g0 = own(NGV, hh), g1 = own(NGV + 1, hh), g2 = own(NGV + 2, hh);
+        f4 p1, r1, p2, r2;
+        block_pre_dpre<KS>(wt, wb, sct, sbt, dsc, 16 + hh, B0, B1, D0, D1, g, p1, r1);
+        block_pre_dpre<KS>(wt, wb, sct, sbt, dsc, 24 + hh, B0, B1, D0, D1, g, p2, r2);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const Silu<float> f1(p1[i]), f2(p2[i]);
+          const float gv1e = g0[i] * w0[i] + g1[i] * w1[i] + g2[i] * w2[i];
+          const float gv2e = g0[i] * E.ux + g1[i] * E.uy + g2[i] * E.uz;
+          er += gv1e * v1[i] * f1.d(p1[i]) * r1[i] + gv2e * v2[i] * f2.d(p2[i]) * r2[i];
+          const float v2e = v2[i] * f2.s;
+          eu0 += g0[i] * v2e;
+          eu1 += g1[i] * v2e;
+          eu2 += g2[i] * v2e;
+          // source terms of t -> s (unit vector -u)
+          gv2[hh][i] -= (m0[i] * E.ux + m1[i] * E.uy + m2[i] * E.uz) * f2.s;
+          A0[hh][i] += m0[i] * f1.s;
+          A1[hh][i] += m1[i] * f1.s;
+          A2[hh][i] += m2[i] * f1.s;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      });
+      er = gsum(er);
+      eu0 = gsum(eu0);
+      eu1 = gsum(eu1);
+      eu2 = gsum(eu2);
+      if (g == 0 && E.ok) {
+        if (G == 1) {
+          float* gu = P.gu + 3 * (size_t)e;
+          if (acc_edge) {
+            P.gC[e] += eC;
+            gu[0] += eu0; gu[1] += eu1; gu[2] += eu2;
+            P.gr[e] += er;
+          } else {
+            P.gC[e] = eC;
+            gu[0] = eu0; gu[1] = eu1; gu[2] = eu2;
+            P.gr[e] = er;
+          }
+        } else {
+          float* pp = P.part + (size_t)sl * 5 * P.cap + e;
+          pp[0] = eC;
+          pp[P.cap] = eu0;
+          pp[2 * (size_t)P.cap] = eu1;
+          pp[3 * (size_t)P.cap] = eu2;
+          pp[4 * (size_t)P.cap] = er;
+        }
+      }
+    }
+    // sum the 16 edge slots; lane (g, c < HPW) stores head h0 + c
+    f4 Q{}, K{}, VX{}, V2{}, S0{}, S1{}, S2{};
+#pragma unroll
+    for (int hh = 0; hh < HPW; ++hh) {
+      f4 a[7];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        a[0][i] = row_sum16(gq[hh][i]);
+        a[1][i] = row_sum16(gk[hh][i]);
+        a[2][i] = row_sum16(gvx[hh][i]);
+        a[3][i] = row_sum16(gv2[hh][i]);
+        a[4][i] = row_sum16(A0[hh][i]);
+        a[5][i] = row_sum16(A1[hh][i]);
+        a[6][i] = row_sum16(A2[hh][i]);
+      }
+      if (c == hh) { Q = a[0]; K = a[1]; VX = a[2]; V2 = a[3]; S0 = a[4]; S1 = a[5]; S2 = a[6]; }
+    }
+    if (c < HPW) {
+      const int h = h0 + c;
+      const f4 v1t = own(NV1, c);
+      const f4 V1 = own(NW0, c) * S0 + own(NW0 + 1, c) * S1 + own(NW0 + 2, c) * S2;
+      f4 W0 = v1t * S0, W1 = v1t * S1, W2 = v1t * S2;
+      auto put = [&](float* d, f4 val) {
+        if (ag) val += *reinterpret_cast<const f4*>(d);
+        *reinterpret_cast<f4*>(d) = val;
+      };
+      put(P.gq + (size_t)t * P.ldq + 16 * h + 4 * g, Q);
+      put(P.gk + (size_t)t * P.ldk + 16 * h + 4 * g, K);
+      float* gvt = P.gv + (size_t)t * P.ldv + VL<PL>::head * h + 4 * g;
+      put(gvt, VX);
+      put(gvt + PV, V1);
+      put(gvt + 2 * PV, V2);
+      if (P.gveci) {
+        if (resid) {
+          W0 += own(NGV, c);
+          W1 += own(NGV + 1, c);
+          W2 += own(NGV + 2, c);
+        }
+        float* gw = P.gveci + (size_t)t * 3 * H + 16 * h + 4 * g;
+        put(gw, W0);
+        put(gw + H, W1);
+        put(gw + 2 * H, W2);
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------ neighbour embedding, distance_proj fused
+// Reference NeighborEmbedding (models/utils.py:90-108): x_nb[t] = sum_{e in row t, s != t} x[s] *
+// (W f(r_e) + b) * C_e, W = distance_proj [H][R].  As the message kernels above: the projection of the
+// per-pair RBF fragments on the fp16 MFMA (W the A operand from an LDS image of D = H rows), so neither
+// the E x H rows W f + b nor, in the force pass, their gradient (E x H) and its E x R contraction with
+// d f / d r exist in memory.  The force pass ("dr mode") needs only the edge gradients:
+//   g_C[e] = sum_h gout[t][h] x[s][h] (W f + b)[h],  g_r[e] = C_e sum_h gout[t][h] x[s][h] (W f')[h].
+// One work item = one node, all H = 128 channels (8 blocks of 16); a lane holds its edge's channels
+// 16 blk + 4 g + i.  Self edges (s == t) contribute nothing (the reference's remove_self_loops).
+constexpr int kNbD = kH;  // the image's rows: H output channels
+struct NbF {
+  int n, cap, chunk, acc;
+  const int32_t* row_ptr;
+  const int32_t* src;
+  const float* x; int ldx;  // [N][H] the embedding rows
+  const float* C;
+  const int32_t* frow;
+  const _Float16* fr;
+  const float* dscale;
+  unsigned fr_bytes;
+  const _Float16* img;
+  const float* wsc;
+  const float* bias;
+  float* out; int ldo;       // forward: x_nb rows (stride ldo)
+  const float* xself;        // forward: optional [N][H] rows copied to oself (stride ldo)
+  float* oself;
+  const float* gout; int ldg;  // backward: dL / d x_nb rows
+  float* gC;                   // backward: [cap] dL / d C
+  float* gr;                   // backward: [cap] dL / d r
+};
+
+template <int KS, int NT>
+__device__ __forceinline__ void load_image_nb(_Float16* w, float* s_sc, float* s_b, const NbF& P) {
+  constexpr int R = 32 * KS;
+  const u4* gi = reinterpret_cast<const u4*>(P.img);
+  u4* l = reinterpret_cast<u4*>(w);
+  for (int i = threadIdx.x; i < 2 * kNbD * R / 8; i += NT) l[i] = gi[i];
+  for (int i = threadIdx.x; i < kNbD; i += NT) { s_sc[i] = P.wsc[i]; s_b[i] = P.bias[i]; }
+}
+
+// one 16-edge tile slot: source, cutoff (0 for self / past-the-row edges), fragment row offset
+struct NbEdge {
+  int s, fo;
+  float C;
+  bool ok, live;
+};
+__device__ __forceinline__ NbEdge nb_edge(int e, int re, int t, const NbF& P, int frow_bytes) {
+  NbEdge E;
+  E.ok = e < re;
+  E.s = E.ok ? P.src[e] : 0;
+  E.live = E.ok && E.s != t;
+  E.fo = E.ok ? P.frow[e] * frow_bytes : kOOB;
+  E.C = E.live ? P.C[e] : 0.f;
+  return E;
+}
+
+template <int KS, int NW>
+__global__ __launch_bounds__(NW * 64, 4) void k_nb_fwd(NbF P) {
+  constexpr int R = 32 * KS, NB = kNbD / 16;
+  __shared__ __attribute__((aligned(16))) _Float16 w[2 * kNbD * R];
+  __shared__ __attribute__((aligned(16))) float s_sc[kNbD];
+  __shared__ __attribute__((aligned(16))) float s_b[kNbD];
+  __shared__ int s_next;
+  load_image_nb<KS, NW * 64>(w, s_sc, s_b, P);
+  if (threadIdx.x == 0) s_next = 0;
+  __syncthreads();
+  const Work W = work_range<1>(P.n, P.chunk);
+  const int lane = lane_id(), c = lane & 15, g = lane >> 4;
+  const rsrc_t Rx = make_rsrc(P.x, (unsigned)P.n * P.ldx * 4u), Rf = make_rsrc(P.fr, P.fr_bytes);
+  const char* wt = reinterpret_cast<const char*>(w);
+  for (;;) {
+    const int it = next_item(&s_next);
+    if (it >= W.items) break;
+    int t, sl;
+    if (!work_item<1>(W, it, t, sl)) continue;
+    const int rb = min(P.row_ptr[t], P.cap), re = min(P.row_ptr[t + 1], P.cap);
+    f4 acc[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) acc[b] = f4{0.f, 0.f, 0.f, 0.f};
+    NbEdge En = nb_edge(rb + c, re, t, P, 8 * R);
+    for (int base = rb; base < re; base += 16) {
+      const NbEdge E = En;
+      if (base + 16 < re) En = nb_edge(base + 16 + c, re, t, P, 8 * R);
+      h8 B0[KS], B1[KS];
+      load_frags<KS>(Rf, E.fo, g, 0, B0, B1);
+      const int ox = E.live ? (E.s * P.ldx + 4 * g) * 4 : kOOB;
+      f4 xs[NB];
+#pragma unroll
+      for (int b = 0; b < NB; ++b) xs[b] = bld4<0>(Rx, ox, __builtin_amdgcn_readfirstlane(64 * b));
+      int wb[KS];
+      frag_offsets<KS>(lane, 0, wb);
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        const f4 pre = block_pre<KS, kNbD>(wt, wb, s_sc, s_b, b, B0, B1, g);
+        acc[b] += xs[b] * pre * E.C;
+      }
+    }
+    // the 16 edge slots; lane (g, c < NB) stores block c's channels 16 c + 4 g + i
+    f4 o{};
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      f4 sb;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sb[i] = row_sum16(acc[b][i]);
+      if (c == b) o = sb;
+    }
+    if (c < NB) {
+      const int ch = 16 * c + 4 * g;
+      *reinterpret_cast<f4*>(P.out + (size_t)t * P.ldo + ch) = o;
+      if (P.xself)
+        *reinterpret_cast<f4*>(P.oself + (size_t)t * P.ldo + ch) =
+            *reinterpret_cast<const f4*>(P.xself + (size_t)t * kNbD + ch);
+    }
+  }
+}
+
+// the force pass's backward (dr mode): g_C and g_r per edge (written, or added with TMDNET_ACC_EDGE);
+// static-capacity padding slots [row_ptr[n], cap) zeroed
+template <int KS, int NW>
+__global__ __launch_bounds__(NW * 64, 4) void k_nb_bwd(NbF P) {
+  constexpr int R = 32 * KS, NB = kNbD / 16;
+  __shared__ __attribute__((aligned(16))) _Float16 w[2 * kNbD * R];
+  __shared__ __attribute__((aligned(16))) float s_sc[kNbD];
+  __shared__ __attribute__((aligned(16))) float s_b[kNbD];
+  __shared__ __attribute__((aligned(16))) float s_go[NW][kNbD];  // gout[t] of the wave's node
+  __shared__ int s_next;
+  load_image_nb<KS, NW * 64>(w, s_sc, s_b, P);
+  if (threadIdx.x == 0) s_next = 0;
+  const bool acc_edge = P.acc & TMDNET_ACC_EDGE;
+  if (!acc_edge) {
+    const int e0 = min(P.row_ptr[P.n], P.cap);
+    for (int e = e0 + blockIdx.x * NW * 64 + threadIdx.x; e < P.cap; e += gridDim.x * NW * 64) P.gC[e] = P.gr[e] = 0.f;
+  }
+  __syncthreads();
+  const Work W = work_range<1>(P.n, P.chunk);
+  const int lane = lane_id(), c = lane & 15, g = lane >> 4;
+  const rsrc_t Rx = make_rsrc(P.x, (unsigned)P.n * P.ldx * 4u), Rf = make_rsrc(P.fr, P.fr_bytes);
+  const char* wt = reinterpret_cast<const char*>(w);
+  for (;;) {
+    const int it = next_item(&s_next);
+    if (it >= W.items) break;
+    int t, sl;
+    if (!work_item<1>(W, it, t, sl)) continue;
+    const int rb = min(P.row_ptr[t], P.cap), re = min(P.row_ptr[t + 1], P.cap);
+    float* go = s_go[threadIdx.x >> 6];
+    __builtin_amdgcn_wave_barrier();  // the previous node's reads are done (in-order LDS)
+    if (lane < kNbD / 4)
+      *reinterpret_cast<f4*>(go + 4 * lane) = *reinterpret_cast<const f4*>(P.gout + (size_t)t * P.ldg + 4 * lane);
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    NbEdge En = nb_edge(rb + c, re, t, P, 8 * R);
+    for (int base = rb; base < re; base += 16) {
+      const int e = base + c;
+      const NbEdge E = En;
+      if (base + 16 < re) En = nb_edge(base + 16 + c, re, t, P, 8 * R);
+      h8 B0[KS], B1[KS], D0[KS], D1[KS];
+      load_frags<KS>(Rf, E.fo, g, 0, B0, B1);
+      load_frags<KS>(Rf, E.fo, g, 1, D0, D1);
+      const float dsc = E.ok ? P.dscale[E.fo / (8 * R)] : 1.f;
+      const int ox = E.live ? (E.s * P.ldx + 4 * g) * 4 : kOOB;
+      f4 xs[NB];
+#pragma unroll
+      for (int b = 0; b < NB; ++b) xs[b] = bld4<0>(Rx, ox, __builtin_amdgcn_readfirstlane(64 * b));
+      int wb[KS];
+      frag_offsets<KS>(lane, 0, wb);
+      float gc = 0.f, gd = 0.f;
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        f4 pre, dpre;
+        block_pre_dpre<KS, kNbD>(wt, wb, s_sc, s_b, dsc, b, B0, B1, D0, D1, g, pre, dpre);
+        const f4 gx = *reinterpret_cast<const f4*>(go + 16 * b + 4 * g) * xs[b];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          gc = fmaf(gx[i], pre[i], gc);
+          gd = fmaf(gx[i], dpre[i], gd);
+        }
+      }
+      gc = gsum(gc);
+      gd = gsum(gd) * E.C;
+      if (g == 0 && E.ok) {
+        if (!E.live) gc = gd = 0.f;
+        if (acc_edge) {
+          P.gC[e] += gc;
+          P.gr[e] += gd;
+        } else {
+          P.gC[e] = gc;
+          P.gr[e] = gd;
+        }
+      }
+    }
+  }
+}
+
 static int num_cus() {
   static int n = [] {
     int dev = 0, v = 0;
@@ -970,11 +1461,14 @@ static int chunk_nodes() {
 // default 4 heads on 8 waves); TMDNET_FEP_DST_FORM 1 = 4 heads on 4 waves (3.78 vs 3.42 ms per backward);
 // TMDNET_FEP_SRC_FORM 1 = 2 heads on 12 waves (3.43 vs 3.38).  Measured and dropped: 1 head on 16 waves
 // (fwd 1.78, src 3.64), 8 heads on 4 waves (fwd 1.65, dst 3.67, src 4.16), the one-tile-ahead edge
-// prefetch with both heads' gathers issued first on 8 waves (fwd 1.51 vs 1.46 at 2 heads)
+// prefetch with both heads' gathers issued first on 8 waves (fwd 1.51 vs 1.46 at 2 heads).
+// Round 5 (default 2 for both): head-pipelined gathers (HP = 1: head hh + 1's issued before head hh
+// computes) fwd 1.340 -> 1.313 ms, backward 3.346 -> 3.329; across tiles too (HP = 2, form 3) fwd 2.74
+// (79 spilled VGPRs) / 2 heads per item (form 4) 1.51; dst form 3 (HP = 2, 2 spills) 3.367.
 static int fwd_form() {
   static int f = [] {
     const char* e = getenv("TMDNET_FEP_FWD_FORM");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : 2;
   }();
   return f;
 }
@@ -983,7 +1477,7 @@ static int fwd_form() {
 static int bwd_form(int which) {
   static int f[2] = {[] {
                        const char* e = getenv("TMDNET_FEP_DST_FORM");
-                       return e ? atoi(e) : 0;
+                       return e ? atoi(e) : 2;
                      }(),
                      [] {
                        const char* e = getenv("TMDNET_FEP_SRC_FORM");
@@ -992,6 +1486,19 @@ static int bwd_form(int which) {
   return f[which];
 }
 static int dst_hpw();
+// TMDNET_FEP_ROW=1: the merged row pass (k_bwd_row, one head per item on 8 waves) instead of the two
+// passes.  Measured at C5 (tools/fep_time.py, ms per backward): two passes 3.38; merged, 1 head on 8
+// waves 3.83 (no spills), 2 heads on 4 waves 4.08, 2 heads on 8 waves 4.33 (45 spilled VGPRs).  The
+// merged pass forms the projection once instead of twice but issues 12 gathers per (edge, head) back to
+// back: both passes are bound by the per-wave latency chain at 2 waves per SIMD, not by the MFMA work
+// the merge removes.
+static bool row_pass() {
+  static bool r = [] {
+    const char* e = getenv("TMDNET_FEP_ROW");
+    return e && atoi(e) == 1;
+  }();
+  return r;
+}
 
 // launch shapes (heads per work item, waves per workgroup; one workgroup per CU): chosen so that no
 // variant spills (tools/regs.py) -- see the launchers
@@ -999,6 +1506,7 @@ constexpr int kFwdHPW = 4, kFwdNW = 8;
 constexpr int kDstHPW = 2, kDstNW = 8;  // 12 waves: 6-14 spilled VGPRs
 constexpr int kSrcHPW = 4, kSrcNW = 8;
 static int dst_hpw() {
+  if (row_pass()) return 1;
   const int f = bwd_form(0);
   return f == 1 ? 4 : kDstHPW;
 }
@@ -1091,6 +1599,12 @@ extern "C" int tmdnet_et_fused_fwd_f32(int n, int H, int heads, int R, const int
   do {                                                                                                     \
     if (fep::fwd_form() == 1)                                                                              \
       hipLaunchKernelGGL((fep::k_fwd<KS_, 2, 12, PL_>), dim3(nwg), dim3(12 * 64), 0, st, P);                \
+    else if (fep::fwd_form() == 2)                                                                         \
+      hipLaunchKernelGGL((fep::k_fwd<KS_, HPW, NW, PL_, 1>), dim3(nwg), dim3(NW * 64), 0, st, P);           \
+    else if (fep::fwd_form() == 3)                                                                         \
+      hipLaunchKernelGGL((fep::k_fwd<KS_, HPW, NW, PL_, 2>), dim3(nwg), dim3(NW * 64), 0, st, P);           \
+    else if (fep::fwd_form() == 4)                                                                         \
+      hipLaunchKernelGGL((fep::k_fwd<KS_, 2, NW, PL_, 2>), dim3(nwg), dim3(NW * 64), 0, st, P);             \
     else                                                                                                   \
       hipLaunchKernelGGL((fep::k_fwd<KS_, HPW, NW, PL_>), dim3(nwg), dim3(NW * 64), 0, st, P);              \
   } while (0)
@@ -1147,9 +1661,24 @@ extern "C" int tmdnet_et_fused_bwd_f32(int n, int H, int heads, int R, const int
   hipLaunchKernelGGL((fep::k_bwd_dst<KS_, HPW_, NW_, PL_>), dim3(nwg), dim3(NW_ * 64), 0, st, P)
 #define TMD_SRC(KS_, PL_, HPW_, NW_) \
   hipLaunchKernelGGL((fep::k_bwd_src<KS_, HPW_, NW_, PL_>), dim3(nwg), dim3(NW_ * 64), 0, st, P)
+#define TMD_ROW(KS_, PL_, HPW_, NW_) \
+  hipLaunchKernelGGL((fep::k_bwd_row<KS_, HPW_, NW_, PL_>), dim3(nwg), dim3(NW_ * 64), 0, st, P)
 #define TMD_BWD(KS_, PL_)                                                                                          \
   do {                                                                                                             \
+    if (fep::row_pass()) {                                                                                         \
+      TMD_ROW(KS_, PL_, 1, 8);                                                                                     \
+      if (S > 1) hipLaunchKernelGGL(fep::k_edge_combine, dim3((cap + 255) / 256), dim3(256), 0, st, P, S);         \
+      break;                                                                                                       \
+    }                                                                                                              \
     if (dform == 1) TMD_DST(KS_, PL_, 4, 4);                                                                        \
+    else if (dform == 2 || dform == 3) {                                                                           \
+      if (dform == 2)                                                                                              \
+        hipLaunchKernelGGL((fep::k_bwd_dst<KS_, fep::kDstHPW, fep::kDstNW, PL_, 1>), dim3(nwg),                    \
+                           dim3(fep::kDstNW * 64), 0, st, P);                                                      \
+      else                                                                                                         \
+        hipLaunchKernelGGL((fep::k_bwd_dst<KS_, fep::kDstHPW, fep::kDstNW, PL_, 2>), dim3(nwg),                    \
+                           dim3(fep::kDstNW * 64), 0, st, P);                                                      \
+    }                                                                                                              \
     else TMD_DST(KS_, PL_, fep::kDstHPW, fep::kDstNW);                                                              \
     if (S > 1) hipLaunchKernelGGL(fep::k_edge_combine, dim3((cap + 255) / 256), dim3(256), 0, st, P, S);           \
     if (sform == 1) TMD_SRC(KS_, PL_, 2, 12);                                                                       \
@@ -1161,7 +1690,73 @@ extern "C" int tmdnet_et_fused_bwd_f32(int n, int H, int heads, int R, const int
     if (pl) TMD_BWD(1, true); else TMD_BWD(1, false);
   }
 #undef TMD_BWD
+#undef TMD_ROW
 #undef TMD_DST
 #undef TMD_SRC
+  return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
+}
+
+// ---- the fused neighbour embedding (reference NeighborEmbedding, models/utils.py:90-108)
+namespace {
+constexpr int kNbNW = 8;  // waves per workgroup; two workgroups per CU (32 KB image, <= 128 VGPRs)
+int nb_check(int n, int H, int R, const void* x, int ld_x, const void* img, long long frag_rows) {
+  if (H != fep::kNbD || (R != 32 && R != 64)) return kUnsupported;
+  if (ld_x < H || ld_x % 4) return kBadArgument;
+  if ((((uintptr_t)x) | ((uintptr_t)img)) & 15) return kUnsupported;
+  if ((long long)n * ld_x * 4 >= fep::kOOB || frag_rows * 8 * R >= fep::kOOB) return kUnsupported;
+  return kOk;
+}
+}  // namespace
+
+extern "C" int tmdnet_nbr_fused_fwd_f32(int n, int H, int R, const int32_t* row_ptr, const int32_t* src, int cap,
+                                        const void* x, int ld_x, const void* C, const int32_t* frag_rows,
+                                        const void* frags, long long n_frag_rows, const void* img, const void* wsc,
+                                        const void* bias, void* out, int ld_out, const void* x_self, void* out_self,
+                                        void* stream) {
+  if (n < 0 || !row_ptr || !src || !x || !C || !frag_rows || !frags || !img || !wsc || !bias || !out)
+    return kBadArgument;
+  if ((x_self == nullptr) != (out_self == nullptr)) return kBadArgument;
+  if (n == 0) return kOk;
+  int rc = nb_check(n, H, R, x, ld_x, img, n_frag_rows);
+  if (rc) return rc;
+  if (ld_out < H || ld_out % 4 || ((((uintptr_t)out) | ((uintptr_t)out_self) | ((uintptr_t)x_self) |
+                                    ((uintptr_t)frags)) & 15))
+    return kUnsupported;
+  fep::NbF P{};
+  P.n = n; P.cap = cap; P.chunk = fep::chunk_nodes();
+  P.row_ptr = row_ptr; P.src = src; P.x = (const float*)x; P.ldx = ld_x; P.C = (const float*)C;
+  P.frow = frag_rows; P.fr = (const _Float16*)frags; P.fr_bytes = (unsigned)(n_frag_rows * 8 * R);
+  P.img = (const _Float16*)img; P.wsc = (const float*)wsc; P.bias = (const float*)bias;
+  P.out = (float*)out; P.ldo = ld_out; P.xself = (const float*)x_self; P.oself = (float*)out_self;
+  const dim3 g(2 * fep::num_cus()), b(kNbNW * 64);
+  hipStream_t st = (hipStream_t)stream;
+  if (R == 64) hipLaunchKernelGGL((fep::k_nb_fwd<2, kNbNW>), g, b, 0, st, P);
+  else hipLaunchKernelGGL((fep::k_nb_fwd<1, kNbNW>), g, b, 0, st, P);
+  return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
+}
+
+extern "C" int tmdnet_nbr_fused_bwd_f32(int n, int H, int R, const int32_t* row_ptr, const int32_t* src, int cap,
+                                        const void* x, int ld_x, const void* C, const int32_t* frag_rows,
+                                        const void* frags, const void* dscale, long long n_frag_rows,
+                                        const void* img, const void* wsc, const void* bias, const void* grad_out,
+                                        int ld_grad_out, void* gcut, void* gdist, int accumulate, void* stream) {
+  if (n < 0 || !row_ptr || !src || !x || !C || !frag_rows || !frags || !dscale || !img || !wsc || !bias ||
+      !grad_out || !gcut || !gdist)
+    return kBadArgument;
+  if (n == 0) return kOk;
+  int rc = nb_check(n, H, R, x, ld_x, img, n_frag_rows);
+  if (rc) return rc;
+  if (ld_grad_out < H || ld_grad_out % 4 || ((((uintptr_t)grad_out) | ((uintptr_t)frags)) & 15)) return kUnsupported;
+  fep::NbF P{};
+  P.n = n; P.cap = cap; P.chunk = fep::chunk_nodes(); P.acc = accumulate;
+  P.row_ptr = row_ptr; P.src = src; P.x = (const float*)x; P.ldx = ld_x; P.C = (const float*)C;
+  P.frow = frag_rows; P.fr = (const _Float16*)frags; P.dscale = (const float*)dscale;
+  P.fr_bytes = (unsigned)(n_frag_rows * 8 * R);
+  P.img = (const _Float16*)img; P.wsc = (const float*)wsc; P.bias = (const float*)bias;
+  P.gout = (const float*)grad_out; P.ldg = ld_grad_out; P.gC = (float*)gcut; P.gr = (float*)gdist;
+  const dim3 g(2 * fep::num_cus()), b(kNbNW * 64);
+  hipStream_t st = (hipStream_t)stream;
+  if (R == 64) hipLaunchKernelGGL((fep::k_nb_bwd<2, kNbNW>), g, b, 0, st, P);
+  else hipLaunchKernelGGL((fep::k_nb_bwd<1, kNbNW>), g, b, 0, st, P);
   return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
 }

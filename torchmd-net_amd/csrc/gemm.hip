@@ -853,19 +853,36 @@ __global__ __launch_bounds__(256) void k_split_t(int N, int K, const float* B, i
 // all BN columns stay in registers across chunks.
 struct XArgs {
   int M, N, K, lda, ldc, beta;
+  int nx, ny, remap;  // column / row tiles; remap: 1-D grid dealt XCD-major (see k_gemm_x3)
   const float* A;
   const unsigned short* Bp;
   const float* bias;
   float* C;
 };
-template <int MB, int BN>
+template <int MB, int BN, int PD>
 __global__ __launch_bounds__(256) void k_gemm_x3(XArgs P) {
   // K chunk staged per barrier pair: 128 (64 at BN = 128) -> ~52 KB of LDS, 3 workgroups per CU
-  constexpr int KC = BN >= 128 ? 64 : 128, LD = KC + 8, NB = BN / 16;
+  constexpr int KC = BN >= 128 ? 64 : 128, LD = KC + 8, NB = BN / 16, SPC = KC / 32;
+  // A prefetch depth in k-steps: the loads of step s + PD are issued when step s is split, so ~PD steps of
+  // MFMA work (PD x 6 x NB x MB MFMAs) cover the HBM latency of a row block.  Measured (tools/x3_time.py,
+  // C5 shapes): the narrow input-gradient form (BN = 128, K = 3H / 5H) gains from PD = 4 (vec_bwd 132 ->
+  // 114 us), the wide forward form (BN = 64, K = H) loses (the ring's registers cost it a wave per SIMD:
+  // 75 -> 100 us), so it keeps PD = 1
   __shared__ __attribute__((aligned(16))) unsigned short w[3][BN][LD];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int n0 = blockIdx.x * BN;
-  const int m0 = (blockIdx.y * 4 + wave) * (16 * MB);
+  int bx = blockIdx.x, by = blockIdx.y;
+  if (P.remap) {
+    // The hardware deals consecutive workgroups round-robin to the 8 XCDs, so the nx column tiles of one
+    // row block -- which all read the same A rows -- would land on nx different XCDs (nx fetches of A from
+    // HBM / MALL, one per XCD L2).  Dealt XCD-major instead: XCD x (= b % 8) walks the contiguous tile range
+    // [start(x), start(x) + count(x)) in order, so a row block's column tiles run on one XCD, together.
+    const int T = P.nx * P.ny, b = blockIdx.x, x = b & 7, q = T >> 3, r = T & 7;
+    const int t = x * q + min(x, r) + (b >> 3);
+    bx = t % P.nx;
+    by = t / P.nx;
+  }
+  const int n0 = bx * BN;
+  const int m0 = (by * 4 + wave) * (16 * MB);
   const int kq = 8 * (lane >> 4);
   const size_t ps = (size_t)P.N * P.K;
   f4 acc[NB][MB];
@@ -873,62 +890,73 @@ __global__ __launch_bounds__(256) void k_gemm_x3(XArgs P) {
   for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb) acc[nb][mb] = f4{0.f, 0.f, 0.f, 0.f};
-  // A rows of this wave: row m0 + 16 mb + (lane & 15), k = 32 ks + kq .. + 7 (two 16-byte loads per
-  // k-step and row block), the next k-step's loads in flight while this one's MFMAs run
+  // A rows of this wave: row m0 + 16 mb + (lane & 15), k = 32 s + kq .. + 7 (two 16-byte loads per k-step
+  // and row block), in a ring of PD k-steps
   const float* arow[MB];
 #pragma unroll
   for (int mb = 0; mb < MB; ++mb) arow[mb] = P.A + (size_t)min(m0 + 16 * mb + (lane & 15), P.M - 1) * P.lda + kq;
-  float4 an[MB][2];
-#pragma unroll
-  for (int mb = 0; mb < MB; ++mb) {
-    an[mb][0] = *reinterpret_cast<const float4*>(arow[mb]);
-    an[mb][1] = *reinterpret_cast<const float4*>(arow[mb] + 4);
-  }
-  constexpr int TW[6] = {2, 1, 0, 1, 0, 0}, TA[6] = {0, 1, 2, 0, 1, 0};
   const int nks_all = P.K / 32;
-  for (int kc = 0; kc < P.K; kc += KC) {
-    const int nks = min(KC, P.K - kc) / 32;
-    // the chunk's pieces: every 16-byte load of the thread issued before the first LDS store (one memory
-    // round trip per chunk; a load -> store loop serialises ~12 of them)
-    constexpr int CH = KC / 8, NL = 3 * BN * CH / 256;
-    const int ch = nks * 4;  // 16-byte chunks per row of this K chunk
-    u4 st[NL];
+  float4 an[PD][MB][2];
 #pragma unroll
-    for (int i = 0; i < NL; ++i) {
-      const int c = threadIdx.x + 256 * i;
-      const int p = c / (BN * CH), rc = c % (BN * CH), n = rc / CH, k = (rc % CH) * 8;
-      st[i] = k < 8 * ch ? *reinterpret_cast<const u4*>(P.Bp + p * ps + (size_t)min(n0 + n, P.N - 1) * P.K + kc + k)
+  for (int d = 0; d < PD; ++d)
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) {
+      const int ko = 32 * min(d, nks_all - 1);
+      an[d][mb][0] = *reinterpret_cast<const float4*>(arow[mb] + ko);
+      an[d][mb][1] = *reinterpret_cast<const float4*>(arow[mb] + ko + 4);
+    }
+  constexpr int TW[6] = {2, 1, 0, 1, 0, 0}, TA[6] = {0, 1, 2, 0, 1, 0};
+  for (int s0 = 0; s0 < nks_all; s0 += PD) {
+#pragma unroll
+    for (int d = 0; d < PD; ++d) {
+      const int st_ = s0 + d;
+      if (st_ < nks_all) {
+        if (st_ % SPC == 0) {
+          // the chunk's pieces: every 16-byte load of the thread issued before the first LDS store (one
+          // memory round trip per chunk; a load -> store loop serialises ~12 of them)
+          const int kc = 32 * st_;
+          const int nks = min(KC, P.K - kc) / 32;
+          constexpr int CH = KC / 8, NL = 3 * BN * CH / 256;
+          const int ch = nks * 4;  // 16-byte chunks per row of this K chunk
+          u4 stg[NL];
+#pragma unroll
+          for (int i = 0; i < NL; ++i) {
+            const int c = threadIdx.x + 256 * i;
+            const int p = c / (BN * CH), rc = c % (BN * CH), n = rc / CH, k = (rc % CH) * 8;
+            stg[i] = k < 8 * ch
+                         ? *reinterpret_cast<const u4*>(P.Bp + p * ps + (size_t)min(n0 + n, P.N - 1) * P.K + kc + k)
                          : u4{0u, 0u, 0u, 0u};
-    }
-    __syncthreads();  // the previous chunk's LDS reads are done
+          }
+          __syncthreads();  // the previous chunk's LDS reads are done
 #pragma unroll
-    for (int i = 0; i < NL; ++i) {
-      const int c = threadIdx.x + 256 * i;
-      const int p = c / (BN * CH), rc = c % (BN * CH), n = rc / CH, k = (rc % CH) * 8;
-      *reinterpret_cast<u4*>(&w[p][n][k]) = st[i];
-    }
-    __syncthreads();
-    for (int ks = 0; ks < nks; ++ks) {
-      bf8 a[MB][3];
+          for (int i = 0; i < NL; ++i) {
+            const int c = threadIdx.x + 256 * i;
+            const int p = c / (BN * CH), rc = c % (BN * CH), n = rc / CH, k = (rc % CH) * 8;
+            *reinterpret_cast<u4*>(&w[p][n][k]) = stg[i];
+          }
+          __syncthreads();
+        }
+        bf8 a[MB][3];
 #pragma unroll
-      for (int mb = 0; mb < MB; ++mb) split8(an[mb][0], an[mb][1], a[mb]);
-      const int kn = kc / 32 + ks + 1;  // next k-step (clamped: the last one reloads itself)
-      const int ko = 32 * min(kn, nks_all - 1);
+        for (int mb = 0; mb < MB; ++mb) split8(an[d][mb][0], an[d][mb][1], a[mb]);
+        const int ko = 32 * min(st_ + PD, nks_all - 1);  // (clamped: the tail reloads the last step)
 #pragma unroll
-      for (int mb = 0; mb < MB; ++mb) {
-        an[mb][0] = *reinterpret_cast<const float4*>(arow[mb] + ko);
-        an[mb][1] = *reinterpret_cast<const float4*>(arow[mb] + ko + 4);
-      }
+        for (int mb = 0; mb < MB; ++mb) {
+          an[d][mb][0] = *reinterpret_cast<const float4*>(arow[mb] + ko);
+          an[d][mb][1] = *reinterpret_cast<const float4*>(arow[mb] + ko + 4);
+        }
+        const int kl = 32 * (st_ % SPC);
 #pragma unroll
-      for (int nb = 0; nb < NB; ++nb) {
-        bf8 b[3];
+        for (int nb = 0; nb < NB; ++nb) {
+          bf8 b[3];
 #pragma unroll
-        for (int q = 0; q < 3; ++q) b[q] = *reinterpret_cast<const bf8*>(&w[q][16 * nb + (lane & 15)][32 * ks + kq]);
+          for (int q = 0; q < 3; ++q) b[q] = *reinterpret_cast<const bf8*>(&w[q][16 * nb + (lane & 15)][kl + kq]);
 #pragma unroll
-        for (int t = 0; t < 6; ++t)
+          for (int t = 0; t < 6; ++t)
 #pragma unroll
-          for (int mb = 0; mb < MB; ++mb)
-            acc[nb][mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[TW[t]], a[mb][TA[t]], acc[nb][mb], 0, 0, 0);
+            for (int mb = 0; mb < MB; ++mb)
+              acc[nb][mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[TW[t]], a[mb][TA[t]], acc[nb][mb], 0, 0, 0);
+        }
       }
     }
   }
@@ -1546,17 +1574,23 @@ extern "C" int tmdnet_gemm_x3_f32(int M, int N, int K, const void* A, int lda, c
   if (M == 0) return kOk;
   if (K % 32 || N % 16 || lda < K || ldc < N || lda % 4 || ldc % 4) return kUnsupported;
   if ((((uintptr_t)A) | ((uintptr_t)Bp) | ((uintptr_t)C) | ((uintptr_t)bias)) & 15) return kUnsupported;
-  proj::XArgs P{M, N, K, lda, ldc, beta ? 1 : 0, (const float*)A, (const unsigned short*)Bp, (const float*)bias,
-                (float*)C};
+  static const int remap_env = [] {
+    const char* e = getenv("TMDNET_X3_REMAP");
+    return e ? atoi(e) : 1;
+  }();
+  proj::XArgs P{M, N, K, lda, ldc, beta ? 1 : 0, 0, 0, 0, (const float*)A, (const unsigned short*)Bp,
+                (const float*)bias, (float*)C};
   hipStream_t st = (hipStream_t)stream;
   // 64-column tiles for wide outputs (the forward mixes, N = 3H..5H), 128 for the narrow input gradients
   // (N = H: one column tile, A read once); 2 row blocks per wave (128 rows per workgroup)
-  if (N >= 256 || N <= 64) {
-    const dim3 g((N + 63) / 64, (M + 127) / 128);
-    hipLaunchKernelGGL((proj::k_gemm_x3<2, 64>), g, dim3(256), 0, st, P);
-  } else {
-    const dim3 g((N + 127) / 128, (M + 127) / 128);
-    hipLaunchKernelGGL((proj::k_gemm_x3<2, 128>), g, dim3(256), 0, st, P);
-  }
+  const int bn = (N >= 256 || N <= 64) ? 64 : 128;
+  P.nx = (N + bn - 1) / bn;
+  P.ny = (M + 127) / 128;
+  P.remap = remap_env && P.nx > 1 && (long long)P.nx * P.ny < (1ll << 31);
+  const dim3 g = P.remap ? dim3(P.nx * P.ny) : dim3(P.nx, P.ny);
+  if (bn == 64)
+    hipLaunchKernelGGL((proj::k_gemm_x3<2, 64, 1>), g, dim3(256), 0, st, P);
+  else
+    hipLaunchKernelGGL((proj::k_gemm_x3<2, 128, 4>), g, dim3(256), 0, st, P);
   return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
 }

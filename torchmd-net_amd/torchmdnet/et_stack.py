@@ -407,7 +407,8 @@ def _forward_layers(meta, x, f, C, u, params, r=None, want_bwd=False):
             if l == 0:
                 meta.fep_imgs = []
                 # the RBF fragments of the evaluation (pair rows), shared by every layer's fused kernels
-                meta.fep_frag = kernels.fep_frag_set(meta.graph, r, meta.rbf, meta.pairs)
+                # (the fused neighbour embedding's, when it made them already: kernels.fep_frag_shared)
+                meta.fep_frag = kernels.fep_frag_shared(meta.graph, r, meta.rbf)
             if not meta.planar:  # the image's rows are always in the planar [dk | dv_x | dv_1 | dv_2] order
                 one = _planar_perms(meta, x.device)[4]
                 dkv_w, dkv_b = dkv_w.index_select(0, one), dkv_b.index_select(0, one)

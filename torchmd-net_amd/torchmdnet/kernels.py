@@ -724,6 +724,20 @@ def fep_frag_set(graph, r, rbf, pairs=None):
     return frag_rows, fr, dsc, int(r_rows.shape[0])
 
 
+def fep_frag_shared(graph, r, rbf):
+    """fep_frag_set(graph, r, rbf) cached on the graph: the fused neighbour embedding and the fused layer
+    stack of one evaluation read the same fragments (keyed on r's storage and the basis)."""
+    mu, beta, cl, cu, rt = rbf
+    key = (r.data_ptr(), int(r.shape[0]), mu.data_ptr(), beta.data_ptr(), float(cl), float(cu), int(rt))
+    cached = getattr(graph, "_fep_frag", None)
+    if cached is not None and cached[0] == key:
+        return cached[1]
+    pairs = pair_index(graph) if (graph.symmetric and graph.transpose is not None) else None
+    frag = fep_frag_set(graph, r, rbf, pairs)
+    graph._fep_frag = (key, frag)
+    return frag
+
+
 def et_fused_fwd_launch(q, k, v, vec, C, u, fep, frag, graph, heads, xo, vo, flags=0):
     """One ``tmdnet_et_fused_fwd_f32`` launch: the ET message with the dk/dv projection fused in
     (``fep`` = fep_split(W, b) of the layer; ``frag`` = fep_frag_set(...) of the evaluation);
@@ -1218,6 +1232,125 @@ class _NbrEmbedBwd(Function):
             second = torch.autograd.grad([f for f, _ in sel], leaves, [g for _, g in sel],
                                          create_graph=_create, allow_unused=True)
         return tuple(second) + (None, None)
+
+
+def nbr_fused_supported(graph, H, R, dtype):
+    """Shapes the fused neighbour embedding takes (tmdnet_nbr_fused_fwd_f32): fp32, H = 128, R = 32 / 64,
+    a symmetric list (its force-pass backward reads the edges of each node's own row only)."""
+    return H == 128 and R in (32, 64) and dtype == torch.float32 and graph.symmetric
+
+
+class _NbrEmbedFused(Function):
+    """[x_self | x_nb] of the neighbour embedding (reference utils.py:90-108) with distance_proj FUSED in:
+    x_nb[t] = sum_{e in row t, s != t} x[s] (W rbf(r_e) + b) C_e, the projection formed per tile on the MFMA
+    (tmdnet_nbr_fused_fwd_f32) -- no E x H rows.  Backward: the force pass (only r / C gradients wanted,
+    no graph) runs tmdnet_nbr_fused_bwd_f32 (dr mode: g_r and g_C per edge); anything else (parameter or
+    embedding gradients, create_graph) differentiates the composite restatement through ``rbf_fn``."""
+
+    @staticmethod
+    def forward(ctx, x, r, C, W, b, graph, rbf, x_self, rbf_fn):
+        lib = nat.load()
+        N, H = x.shape
+        R = W.shape[1]
+        frag = fep_frag_shared(graph, r, rbf)
+        img = fep_split(W.detach().contiguous(), b.detach().contiguous())
+        if x_self is None:
+            buf = out = torch.empty((N, H), dtype=x.dtype, device=x.device)
+        else:
+            buf = torch.empty((N, 2 * H), dtype=x.dtype, device=x.device)
+            out = buf[:, H:]
+        frag_rows, fr, _, rows = frag
+        rc = lib.tmdnet_nbr_fused_fwd_f32(N, H, R, nat.ptr(graph.row_ptr), nat.ptr(graph.src), graph.n_edges,
+                                          nat.ptr(x), _ld(x), nat.ptr(C), nat.ptr(frag_rows), nat.ptr(fr), rows,
+                                          nat.ptr(img[0]), nat.ptr(img[1]), nat.ptr(img[2]), nat.ptr(out),
+                                          out.stride(0), nat.ptr(x_self), None if x_self is None else nat.ptr(buf),
+                                          nat.stream(x.device))
+        nat.check(rc, "tmdnet_nbr_fused_fwd_f32")
+        ctx.graph, ctx.frag, ctx.img, ctx.rbf_fn = graph, frag, img, rbf_fn
+        ctx.has_self = x_self is not None
+        ctx.save_for_backward(x, r, C, W, b)
+        return buf
+
+    @staticmethod
+    def backward(ctx, gout):
+        x, r, C, W, b = ctx.saved_tensors
+        graph = ctx.graph
+        N, H = x.shape
+        g_self = None
+        if gout.stride(-1) != 1:
+            gout = gout.contiguous()
+        if ctx.has_self:
+            g_self, gout = gout[:, :H], gout[:, H:]
+        nodes = [e[0] for e in ctx.next_functions]
+        want = [bool(ctx.needs_input_grad[i]) and _will_run(nodes[i]) for i in range(5)]
+        tail = (None, None, g_self, None)
+        if not (want[0] or want[3] or want[4]):  # the force pass: r / C gradients only (dr mode)
+            if not (want[1] or want[2]):
+                return (None,) * 5 + tail
+            g_r, g_C = _NbrEmbedFusedBwd.apply(gout, x, r, C, W, b, graph, ctx.frag, ctx.img, ctx.rbf_fn)
+            return (None, g_r if want[1] else None, g_C if want[2] else None, None, None) + tail
+        # parameter / embedding gradients: the composite restatement
+        with torch.enable_grad():
+            leaves = [t.detach().requires_grad_(w) for t, w in zip((x, r, C, W, b), want)]
+            out = _nbr_fused_composite(leaves, graph, ctx.rbf_fn)
+            req = [t for t, w_ in zip(leaves, want) if w_]
+            gs = torch.autograd.grad(out, req, gout, create_graph=torch.is_grad_enabled(), allow_unused=True)
+        it = iter(gs)
+        return tuple(next(it) if w_ else None for w_ in want) + tail
+
+
+def _nbr_fused_composite(leaves, graph, rbf_fn):
+    """Differentiable restatement of the fused neighbour embedding's x_nb (reference utils.py:90-107)."""
+    x, r, C, W, b = leaves
+    w = torch.nn.functional.linear(rbf_fn(r), W, b)
+    return nbr_embed_composite(x, w, C, graph.src.long(), graph.dst.long(), graph.n_nodes)
+
+
+class _NbrEmbedFusedBwd(Function):
+    """(g_r, g_C) of the fused neighbour embedding in the force pass (tmdnet_nbr_fused_bwd_f32, dr mode);
+    differentiable for force-matching training: its backward differentiates the composite restatement
+    twice (the second order at large sizes is not a timed configuration)."""
+
+    @staticmethod
+    def forward(ctx, gout, x, r, C, W, b, graph, frag, img, rbf_fn):
+        lib = nat.load()
+        N, H = x.shape
+        E = graph.n_edges
+        eb = torch.empty((2 * E,), dtype=x.dtype, device=x.device)
+        g_C, g_r = eb[:E], eb[E:]
+        frag_rows, fr, dsc, rows = frag
+        rc = lib.tmdnet_nbr_fused_bwd_f32(N, H, W.shape[1], nat.ptr(graph.row_ptr), nat.ptr(graph.src), E,
+                                          nat.ptr(x), _ld(x), nat.ptr(C), nat.ptr(frag_rows), nat.ptr(fr),
+                                          nat.ptr(dsc), rows, nat.ptr(img[0]), nat.ptr(img[1]), nat.ptr(img[2]),
+                                          nat.ptr(gout), gout.stride(0), nat.ptr(g_C), nat.ptr(g_r), 0,
+                                          nat.stream(x.device))
+        nat.check(rc, "tmdnet_nbr_fused_bwd_f32")
+        ctx.graph, ctx.rbf_fn = graph, rbf_fn
+        ctx.save_for_backward(gout, x, r, C, W, b)
+        return g_r, g_C
+
+    @staticmethod
+    def backward(ctx, gg_r, gg_C):
+        saved = ctx.saved_tensors
+        sel = [(i, g) for i, g in ((2, gg_r), (3, gg_C)) if g is not None]
+        if not sel:
+            return (None,) * 10
+        with torch.enable_grad():
+            leaves = [t.detach().requires_grad_(True) for t in saved]
+            out = _nbr_fused_composite(leaves[1:], ctx.graph, ctx.rbf_fn)
+            first = torch.autograd.grad(out, [leaves[i] for i, _ in sel], leaves[0], create_graph=True)
+            second = torch.autograd.grad(first, leaves, [g for _, g in sel], create_graph=torch.is_grad_enabled(),
+                                         allow_unused=True)
+        return tuple(g if ctx.needs_input_grad[i] else None for i, g in enumerate(second)) + (None,) * 4
+
+
+def nbr_embed_fused(x, r, C, W, b, graph, rbf, rbf_fn, x_self=None):
+    """The neighbour-embedding aggregation with distance_proj fused (reference utils.py:90-108):
+    ``cat([x_self, x_nb], 1)`` (or x_nb) from r directly -- no rbf or projection rows.  ``rbf`` = (mu, beta,
+    cutoff_lower, cutoff_upper, rbf_type) of the basis, ``rbf_fn`` its differentiable module (the composite
+    backward)."""
+    return _NbrEmbedFused.apply(_rowmajor(x), r, C.contiguous(), W, b, graph, rbf,
+                                None if x_self is None else x_self.contiguous(), rbf_fn)
 
 
 def nbr_embed(x, w, C, graph, x_self=None):

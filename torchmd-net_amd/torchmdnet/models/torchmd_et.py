@@ -10,15 +10,21 @@ reference checkpoints load.  The per-edge work runs in HIP kernels:
 The dense node/edge projections (LayerNorm, q/k/v/o/vec, dk/dv) are GEMMs (rocBLAS/hipBLASLt via
 torch, MFMA) whose outputs feed the kernels without reshuffling.
 """
+import os
 from typing import List, Optional, Tuple
 
 import torch
 from torch import Tensor, nn
 
+from .. import et_stack as et_stack_mod
 from .. import kernels
 from ..et_stack import et_stack
 from .utils import (CosineCutoff, NeighborEmbedding, OptimizedDistance, act_class_mapping, as_graph,
                     rbf_class_mapping)
+
+# large systems: the neighbour embedding's distance_proj formed inside its aggregation kernel
+# (kernels.nbr_embed_fused; same size threshold as the fused layer stack).  TMDNET_NE_FUSED=0: rows (A/B)
+NE_FUSED = os.environ.get("TMDNET_NE_FUSED", "1") != "0"
 
 
 class TorchMD_ET(nn.Module):
@@ -205,6 +211,7 @@ class TorchMD_ET(nn.Module):
             x = self.embedding(z)
         graph = self.distance.graph(pos, batch)
         f_pairs = None
+        ne_fused = None
         edge_attr_s = C_s = None  # the layer stack's aliases of the rbf / cutoff rows
         de = self.distance_expansion
         if self.trainable_rbf and torch.is_grad_enabled():
@@ -216,20 +223,34 @@ class TorchMD_ET(nn.Module):
             pairs = getattr(graph, "_pairs", None)  # numbered by the neighbour build (sorted rows)
             stack = self.fused_stack and len(self.attention_layers) > 0
             rows = pairs[1] if (pairs is not None and stack) else None
+            ne = self.neighbor_embedding
+            if (ne is not None and z.is_cuda and NE_FUSED and graph.n_edges >= et_stack_mod.FEP_MIN_EDGES
+                    and et_stack_mod.FEP not in ("0", "off")
+                    and kernels.nbr_fused_supported(graph, self.hidden_channels, self.num_rbf, pos.dtype)):
+                # large systems: distance_proj formed inside the aggregation kernel from r (no rbf or
+                # projection rows for the neighbour embedding; dr-mode force backward)
+                mu, beta = de.kernel_params()
+                ne_fused = ((mu.detach(), beta.detach(), float(self.cutoff_lower), float(self.cutoff_upper),
+                             int(de.rbf_type)), de)
             # rbf and cutoff rows read by the neighbour embedding AND the layer stack: one alias each, their
             # gradients summed in the geometry backward kernel (no autograd add launch)
-            fan = (2, 2) if (stack and self.neighbor_embedding is not None) else (1, 1)
+            fan = (1, 1)
+            if stack and ne is not None:
+                fan = (1, 2) if ne_fused is not None else (2, 2)
             geo = kernels.edge_geometry(graph, *de.kernel_params(), self.cutoff_lower, self.cutoff_upper,
                                         de.rbf_type, rows=rows, fan=fan)
             edge_attr, C, d_ij = geo[:3]
             f_pairs = geo[3] if rows is not None else None
-            if fan != (1, 1):
+            if fan == (2, 2):
                 (edge_attr, edge_attr_s), (C, C_s) = edge_attr, C
+            elif fan == (1, 2):
+                (edge_attr_s,), (C, C_s) = edge_attr, C
+                edge_attr = None
         if edge_attr_s is None:
             edge_attr_s, C_s = edge_attr, C
         graph.cutoff = C_s
         if self.neighbor_embedding is not None:
-            x = self.neighbor_embedding(z, x, graph, graph.distances, edge_attr, cutoff=C, x_emb=x_ne)
+            x = self.neighbor_embedding(z, x, graph, graph.distances, edge_attr, cutoff=C, x_emb=x_ne, fused=ne_fused)
         if self.fused_stack and len(self.attention_layers) > 0:
             # all layers as one autograd node (et_stack.py): fused GEMMs, HIP epilogue, hand-scheduled
             # backward; same math as the loop below

@@ -296,12 +296,20 @@ class NeighborEmbedding(nn.Module):
         x_nb = torch.ops.tmdnet.nbr_embed(self.embedding(z), W, C, row_ptr, src, dst)
         return self.combine(torch.cat([x, x_nb], dim=1))
 
-    def forward(self, z: Tensor, x: Tensor, edge_index: Tensor, edge_weight: Tensor, edge_attr: Tensor,
-                cutoff: Optional[Tensor] = None, x_emb: Optional[Tensor] = None) -> Tensor:
+    def forward(self, z: Tensor, x: Tensor, edge_index: Tensor, edge_weight: Tensor, edge_attr: Optional[Tensor],
+                cutoff: Optional[Tensor] = None, x_emb: Optional[Tensor] = None, fused=None) -> Tensor:
         """``x_emb``: this module's embedding of ``z`` when the caller looked it up already (TorchMD_ET
-        does both tables' lookups in one node)."""
+        does both tables' lookups in one node).  ``fused`` = (rbf params, rbf module): distance_proj is
+        formed inside the aggregation kernel from ``edge_weight`` (large systems, kernels.nbr_embed_fused;
+        ``edge_attr`` unused, the caller's CSR graph and cutoff required)."""
         if torch.jit.is_scripting():
             raise RuntimeError("scripted NeighborEmbedding: use script_forward (CSR graph)")
+        if fused is not None:
+            if x_emb is None:
+                x_emb = self.embedding(z)
+            x_cat = kernels.nbr_embed_fused(x_emb, edge_weight, cutoff, self.distance_proj.weight,
+                                            self.distance_proj.bias, edge_index, fused[0], fused[1], x_self=x)
+            return kernels.linear(x_cat, self.combine.weight, self.combine.bias)
         graph, perm = as_graph(edge_index, x.shape[0])
         if perm is not None:
             edge_weight, edge_attr = edge_weight[perm], edge_attr[perm]
