@@ -930,6 +930,45 @@ def secondary_train(a, ws, rank, dev):
     return res
 
 
+def secondary_tn_train(a, ws, rank, dev):
+    """C3 training: TensorNet-rMD17 (8 x aspirin, O(3), static_shapes) E + F MSE step -- forces by
+    create_graph, the double backward through the hand-written second order (tmdnet_tn_node_bwd2, the
+    GEMM / message second orders) -- eager and as one HIP-graph replay (GraphedTrainStep) + AdamW."""
+    import yaml
+    from torchmdnet.models.model import create_model
+    from torchmdnet.training import GraphedTrainStep, LNNPStep
+    with open(os.path.join(ROOT, "tests", "golden", "configs", "tensornet_rmd17.yaml")) as f:
+        args = yaml.safe_load(f)
+    args.update(prior_model=None, precision=32, derivative=True)
+    torch.manual_seed(0)
+    model = create_model(args).to(dev)
+    n_mol = 8
+    z, pos, batch = rmd17_like(n_mol, 1 + rank)
+    gy = torch.Generator().manual_seed(300 + rank)
+    y_lab = torch.randn(n_mol, 1, generator=gy).to(dev)
+    f_lab = torch.randn(z.shape[0], 3, generator=gy).to(dev)
+    z, pos, batch = z.to(dev), pos.float().to(dev), batch.to(dev)
+    steps = max(10, a.steps // 2)
+    trainer = LNNPStep(model, lr=4e-4)
+    el = timed_loop(lambda: trainer.step(z, pos, batch, y_lab, f_lab), max(3, a.warmup // 2), steps, ws, dev)
+    res = {"workload": "TensorNet-rMD17 training step (C3: 8 x aspirin, E+F MSE, double backward, AdamW), eager",
+           "value": round(n_mol * ws * steps / el, 2), "unit": "molecules/s",
+           "ms_per_step": round(1000 * el / steps, 4), "steps": steps, "parallelism": f"dp{ws}"}
+    if a.graphed_train:
+        del trainer
+        try:
+            gtr = GraphedTrainStep(model, z, pos, batch, y_lab, f_lab, lr=4e-4)
+            el = timed_loop(lambda: gtr.step(), max(3, a.warmup // 2), steps, ws, dev)
+            gtr.check_capacity()
+            gtr.release()
+            res["graphed"] = {"value": round(n_mol * ws * steps / el, 2), "unit": "molecules/s",
+                              "ms_per_step": round(1000 * el / steps, 4),
+                              "execution": "fwd + force pass + double backward in one HIP graph; fused AdamW eager"}
+        except RuntimeError as exc:
+            res["graphed"] = {"error": str(exc)[:300]}
+    return res
+
+
 def write_custom_dataset(root, n_mol, gen_seed):
     """SURVEY.md 8(d) QM9-like molecules in the reference's Custom npy format (datasets/custom.py:
     one coordinate / embedding / energy / force file per molecule size, frames of that size), with
@@ -1272,6 +1311,8 @@ def main():
         sec = {"tensornet_c3": secondary_tensornet(a, ws, rank, dev)}
         phase("secondary: ET training step")
         sec["et_train_step"] = secondary_train(a, ws, rank, dev)
+        phase("secondary: TensorNet C3 training step")
+        sec["tn_train_step_c3"] = secondary_tn_train(a, ws, rank, dev)
         phase("secondary: fit() on the data path")
         sec["et_fit_data_path"] = secondary_fit(a, ws, rank, dev)
         phase("secondary: ET-SPICE C4")

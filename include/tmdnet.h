@@ -495,6 +495,15 @@ int tmdnet_tn_node_fwd(int dtype, int op, int n_nodes, int hidden, const void* a
 int tmdnet_tn_node_bwd(int dtype, int op, int n_nodes, int hidden, const void* a, const void* b,
                        const void* grad_out, const void* grad_add, void* ga, void* gb,
                        void* stream);
+/* Second order of a node pass (force-matching training; replaces autograd's double differentiation of
+ * the pass): the VJP of (ga, gb) = tmdnet_tn_node_bwd(a, b, grad_out) for cotangents t_a / t_b (layouts
+ * of a / b; NULL = 0) -- d_grad_out = J (t_a, t_b) (layout of out) and (d_a, d_b) = the Hessian of
+ * <grad_out, f(a, b)> applied to (t_a, t_b); every output NULL = not computed, written otherwise.
+ * (grad_add's derivative is the identity: the caller passes t_a through.)  b / t_b / d_b only for the
+ * two-input passes. */
+int tmdnet_tn_node_bwd2(int dtype, int op, int n_nodes, int hidden, const void* a, const void* b,
+                        const void* grad_out, const void* t_a, const void* t_b, void* d_grad_out, void* d_a,
+                        void* d_b, void* stream);
 
 /* SiLU with an optional per-row scale (TensorNet edge MLP `act(linear(.)) * C`,
  * tensornet.py:385-389; the scalar MLPs of the embedding, output and Scalar head).

@@ -1,0 +1,152 @@
+"""TensorNet's hand-written second order (force-matching training; replaces autograd's double
+differentiation of the PyTorch restatements, reference tensornet.py:287-410 under module.py:130-179):
+
+* every node pass (tn_node.py, reference decompose_tensor / tensor_norm and the interaction's
+  normalisation, product and residual, tensornet.py:47-67, 391-410) through
+  ``tmdnet_tn_node_bwd2`` -- the same kernel code evaluated on dual numbers (forward-over-reverse);
+* the channel mixes (``mix3``, tensornet.py:318-320, 354-356, 372-374) through GEMMs;
+* the message (tensornet.py:329-332), bilinear in (edge factors, tensor), through its own forward and
+  first-backward kernels;
+
+each against ``tn_node._double_backward`` of the composite restatement in fp64 (1e-10), and the padded
+C3 model's force-loss parameter gradients hip vs composite in fp32.
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _rel(a, b):
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-300))
+
+
+def _node_inputs(op, N, H, g):
+    from torchmdnet import tn_node as T
+    full = lambda: torch.randn(N, H, 3, 3, generator=g, dtype=torch.float64)  # noqa: E731
+    comp = lambda: torch.randn(9, N, H, generator=g, dtype=torch.float64)  # noqa: E731
+    if op == T.PRE or op == T.NORMS:
+        return full(), None
+    if op in (T.POST_O3, T.POST_SO3):
+        return comp(), comp()
+    if op == T.RESID:
+        return full(), comp()
+    if op == T.ENORM:
+        return comp(), None
+    return comp(), torch.randn(N, 3 * H, generator=g, dtype=torch.float64)  # EOUT
+
+
+@pytest.mark.parametrize("op", list(range(7)), ids=["pre", "post_o3", "post_so3", "resid", "norms", "enorm", "eout"])
+def test_node_pass_second_order_matches_composite(op):
+    from torchmdnet import tn_node as T
+    g = torch.Generator().manual_seed(op)
+    N, H = 37, 24
+    a, b = _node_inputs(op, N, H, g)
+    out = T.op_composite(op, a, b)
+    gout = torch.randn(out.shape, generator=g, dtype=torch.float64)
+    ta = torch.randn(a.shape, generator=g, dtype=torch.float64)
+    tb = None if b is None else torch.randn(b.shape, generator=g, dtype=torch.float64)
+    prim = [a] if b is None else [a, b]
+    fwd = (lambda x: T.op_composite(op, x)) if b is None else (lambda x, y: T.op_composite(op, x, y))
+    ref = T._double_backward(fwd, prim, [gout], [ta] if b is None else [ta, tb])
+    dv = lambda t: None if t is None else t.to(DEV)  # noqa: E731
+    d_g = torch.empty(gout.shape, dtype=torch.float64, device=DEV)
+    d_a = torch.empty(a.shape, dtype=torch.float64, device=DEV)
+    d_b = None if b is None else torch.empty(b.shape, dtype=torch.float64, device=DEV)
+    T.node_bwd2_launch(op, dv(a), dv(b), dv(gout), dv(ta), dv(tb), d_g, d_a, d_b)
+    torch.cuda.synchronize()
+    assert _rel(d_g.cpu(), ref[0]) < 1e-10
+    assert _rel(d_a.cpu(), ref[1]) < 1e-10
+    if b is not None:
+        assert _rel(d_b.cpu(), ref[2]) < 1e-10
+
+
+def test_mix3_second_order_matches_composite():
+    from torchmdnet import tn_node as T
+    g = torch.Generator().manual_seed(5)
+    N, I, O = 53, 32, 48
+    o = dict(dtype=torch.float64, device=DEV)
+    c = torch.randn(9, N, I, generator=g, dtype=torch.float64).to(DEV)
+    ws = [torch.randn(O, I, generator=g, dtype=torch.float64).to(DEV) for _ in range(3)]
+    gout = torch.randn(9, N, O, generator=g, dtype=torch.float64).to(DEV)
+    ggc = torch.randn(9, N, I, generator=g, dtype=torch.float64).to(DEV)
+    for drop in (None, 1):  # a None weight cotangent too
+        ggw = [None if i == drop else torch.randn(O, I, generator=g, dtype=torch.float64).to(DEV) for i in range(3)]
+        got = T._mix3_second_order((False, True, True, True, True, True), gout, c, ws, ggc, ggw)
+        ref = T._double_backward(T.mix3_composite, [c] + ws, [gout], [ggc] + ggw)
+        for x, y in zip(got, ref):
+            assert _rel(x, y) < 1e-10
+    del o
+
+
+def _tn_graph(n_mol=3):
+    from torchmdnet.models.utils import OptimizedDistance
+    g = torch.Generator().manual_seed(2)
+    pos = (torch.randn(n_mol * 12, 3, generator=g, dtype=torch.float64) * 1.4).to(DEV)
+    batch = torch.arange(n_mol).repeat_interleave(12).to(DEV)
+    d = OptimizedDistance(0.0, 4.5, max_num_pairs=-64, return_vecs=True, loop=True)
+    return d.graph(pos, batch)
+
+
+def test_message_second_order_matches_composite(monkeypatch):
+    from torchmdnet import kernels, tn_node
+    graph = _tn_graph()
+    g = torch.Generator().manual_seed(3)
+    N, H, E = graph.n_nodes, 16, graph.n_edges
+    ea = torch.randn(E, 3 * H, generator=g, dtype=torch.float64).to(DEV)
+    Tc = torch.randn(9, N, H, generator=g, dtype=torch.float64).to(DEV)
+    gmsg = torch.randn(9, N, H, generator=g, dtype=torch.float64).to(DEV)
+    t_ea = torch.randn(E, 3 * H, generator=g, dtype=torch.float64).to(DEV)
+    t_T = torch.randn(9, N, H, generator=g, dtype=torch.float64).to(DEV)
+    # the kernels' precondition: edge factors -- and so their cotangents, functions of the pair distance
+    # through the edge MLP -- are equal on the two directions of a pair (include/tmdnet.h)
+    tr = graph.transpose.long()
+    ea = 0.5 * (ea + ea[tr])
+    t_ea = 0.5 * (t_ea + t_ea[tr])
+
+    def second(mode):
+        monkeypatch.setattr(tn_node, "SECOND_ORDER", mode)
+        e, t, gm = (x.clone().requires_grad_(True) for x in (ea, Tc, gmsg))
+        msg = kernels.tn_message(e, t, graph)
+        first = torch.autograd.grad(msg, (e, t), gm, create_graph=True)
+        return torch.autograd.grad(first, (gm, e, t), (t_ea, t_T))
+
+    (g1, e1, t1), (g0, e0, t0) = second("hip"), second("composite")
+    assert _rel(g1, g0) < 1e-10 and _rel(t1, t0) < 1e-10
+    # the kernels number an edge factor's gradient by the row that reads it (the reverse of the
+    # reference's scatter orientation); the two directions of a pair share one factor, so the per-pair
+    # sums are what any consumer sees
+    assert _rel(e1 + e1[tr], e0 + e0[tr]) < 1e-10
+
+
+@pytest.mark.parametrize("static_shapes", [True, False])
+def test_tensornet_force_loss_gradients_hip_vs_composite(static_shapes, monkeypatch):
+    """C3-shaped TensorNet (O(3)) force-matching loss: parameter gradients through the hand second order
+    equal those through the composite restatements (fp32)."""
+    import os
+    import yaml
+    from conftest import GOLDEN
+    from torchmdnet import tn_node
+    from torchmdnet.models.model import create_model
+    with open(os.path.join(GOLDEN, "configs", "tensornet_rmd17.yaml")) as fh:
+        args = yaml.safe_load(fh)
+    args.update(prior_model=None, precision=32, derivative=True, static_shapes=static_shapes)
+    torch.manual_seed(0)
+    m = create_model(args).to(DEV)
+    g = torch.Generator().manual_seed(1)
+    z = torch.tensor([6] * 9 + [1] * 8 + [8] * 4, dtype=torch.long).repeat(4).to(DEV)
+    pos = (torch.randn(z.shape[0], 3, generator=g) * 1.6).to(DEV)
+    batch = torch.arange(4).repeat_interleave(21).to(DEV)
+
+    def grads(mode):
+        monkeypatch.setattr(tn_node, "SECOND_ORDER", mode)
+        m.zero_grad(set_to_none=True)
+        y, f = m(z, pos, batch)
+        (y.pow(2).sum() + f.pow(2).sum()).backward()
+        return {n: p.grad.detach().clone() for n, p in m.named_parameters() if p.grad is not None}
+
+    a, b = grads("hip"), grads("composite")
+    assert a.keys() == b.keys()
+    for n in a:
+        assert _rel(a[n], b[n]) < 2e-5, n

@@ -20,32 +20,80 @@
 namespace tmd {
 namespace node {
 
-template <typename T> struct NodeArgs {
+// CP / OP: the input / output "pointer" types -- const T* / T* for the first-order passes, DIn / DOut
+// (value and tangent arrays) for the second order's dual-number evaluation below
+template <typename T, typename CP = const T*, typename OP = T*> struct NodeArgs {
   int n, H;
   size_t nh;
-  const T* a; const T* b; T* out;           // forward
-  const T* gout; T* ga; T* gb; const T* gadd;  // backward
+  CP a; CP b; OP out;           // forward
+  CP gout; OP ga; OP gb; CP gadd;  // backward
 };
 
-template <typename T> __device__ __forceinline__ void ldc(T (&o)[9], const T* p, size_t nh) {
+// ---- second order by forward-over-reverse on dual numbers (value, tangent).  The first backward maps
+// (a, b, g) to (ga, gb) = J_f(a, b)^T g; its VJP for cotangents (t_a, t_b) of (ga, gb) is
+//   d_g      = J_f (t_a, t_b)                         -- the forward pass with tangents (t_a, t_b)
+//   (d_a, d_b) = H_<g, f> (t_a, t_b)                   -- the first backward with tangents (t_a, t_b), g fixed
+// (the Hessian of <g, f(a, b)> is symmetric).  Every pass above only adds, subtracts, multiplies and
+// divides, so the SAME code evaluated on Dual<T> gives both (the derivative of a quotient included).
+template <typename T> struct Dual {
+  T v, d;
+  __device__ __forceinline__ Dual() : v(0), d(0) {}
+  __device__ __forceinline__ Dual(double x) : v(T(x)), d(0) {}  // constants
+  __device__ __forceinline__ Dual(T v_, T d_) : v(v_), d(d_) {}
+};
+template <typename T> __device__ __forceinline__ Dual<T> operator+(Dual<T> x, Dual<T> y) { return {x.v + y.v, x.d + y.d}; }
+template <typename T> __device__ __forceinline__ Dual<T> operator-(Dual<T> x, Dual<T> y) { return {x.v - y.v, x.d - y.d}; }
+template <typename T> __device__ __forceinline__ Dual<T> operator-(Dual<T> x) { return {-x.v, -x.d}; }
+template <typename T> __device__ __forceinline__ Dual<T> operator*(Dual<T> x, Dual<T> y) {
+  return {x.v * y.v, x.d * y.v + x.v * y.d};
+}
+template <typename T> __device__ __forceinline__ Dual<T> operator/(Dual<T> x, Dual<T> y) {
+  const T q = x.v / y.v;
+  return {q, (x.d - q * y.d) / y.v};
+}
+template <typename T> __device__ __forceinline__ Dual<T>& operator+=(Dual<T>& x, Dual<T> y) { return x = x + y; }
+template <typename T> __device__ __forceinline__ Dual<T>& operator-=(Dual<T>& x, Dual<T> y) { return x = x - y; }
+template <typename T> __device__ __forceinline__ Dual<T>& operator*=(Dual<T>& x, Dual<T> y) { return x = x * y; }
+// input: value and tangent arrays (tangent NULL: 0)
+template <typename T> struct DIn {
+  const T* v; const T* d;
+  __device__ __forceinline__ DIn operator+(size_t o) const { return {v + o, d ? d + o : nullptr}; }
+  __device__ __forceinline__ Dual<T> operator[](size_t i) const { return {v[i], d ? d[i] : T(0)}; }
+  __device__ __forceinline__ explicit operator bool() const { return v != nullptr; }
+};
+// output: value and tangent arrays (either NULL: not stored)
+template <typename T> struct DRef {
+  T* v; T* d;
+  __device__ __forceinline__ void operator=(Dual<T> x) const {
+    if (v) *v = x.v;
+    if (d) *d = x.d;
+  }
+};
+template <typename T> struct DOut {
+  T* v; T* d;
+  __device__ __forceinline__ DOut operator+(size_t o) const { return {v ? v + o : nullptr, d ? d + o : nullptr}; }
+  __device__ __forceinline__ DRef<T> operator[](size_t i) const { return {v ? v + i : nullptr, d ? d + i : nullptr}; }
+};
+
+template <typename T, typename P> __device__ __forceinline__ void ldc(T (&o)[9], P p, size_t nh) {
 #pragma unroll
   for (int k = 0; k < 9; ++k) o[k] = p[k * nh];
 }
-template <typename T> __device__ __forceinline__ void stc(T* p, size_t nh, const T (&o)[9]) {
+template <typename T, typename P> __device__ __forceinline__ void stc(P p, size_t nh, const T (&o)[9]) {
 #pragma unroll
   for (int k = 0; k < 9; ++k) p[k * nh] = o[k];
 }
-template <typename T> __device__ __forceinline__ void ld9(T (&o)[9], const T* p) {
+template <typename T, typename P> __device__ __forceinline__ void ld9(T (&o)[9], P p) {
 #pragma unroll
   for (int k = 0; k < 9; ++k) o[k] = p[k];
 }
-template <typename T> __device__ __forceinline__ void st9(T* p, const T (&o)[9]) {
+template <typename T, typename P> __device__ __forceinline__ void st9(P p, const T (&o)[9]) {
 #pragma unroll
   for (int k = 0; k < 9; ++k) p[k] = o[k];
 }
 
-template <typename T, int OP>
-__global__ __launch_bounds__(256) void k_node_fwd(NodeArgs<T> A) {
+template <typename T, int OP, typename AR = NodeArgs<T>>
+__global__ __launch_bounds__(256) void k_node_fwd(AR A) {
   const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= A.nh) return;
   const int n = (int)(t / A.H), h = (int)(t % A.H);
@@ -95,7 +143,7 @@ __global__ __launch_bounds__(256) void k_node_fwd(NodeArgs<T> A) {
     ld9(X, A.a + 9 * t);
     decomp(c, X);
     const T ss = c[4] + c[5];
-    T* o = A.out + (size_t)n * 3 * A.H + h;
+    auto o = A.out + (size_t)n * 3 * A.H + h;
     o[0] = T(3) * c[0] * c[0];
     o[A.H] = T(2) * (c[1] * c[1] + c[2] * c[2] + c[3] * c[3]);
     o[2 * A.H] = c[4] * c[4] + c[5] * c[5] + ss * ss + T(2) * (c[6] * c[6] + c[7] * c[7] + c[8] * c[8]);
@@ -107,7 +155,7 @@ __global__ __launch_bounds__(256) void k_node_fwd(NodeArgs<T> A) {
   } else if constexpr (OP == TMDNET_TN_EOUT) {
     T c[9], F[9];
     ldc(c, A.a + t, A.nh);
-    const T* f = A.b + 3 * t;  // norm.reshape(N, H, 3)
+    auto f = A.b + 3 * t;  // norm.reshape(N, H, 3)
     const T fI = f[0], fA = f[1], fS = f[2];
 #pragma unroll
     for (int k = 0; k < 9; ++k) c[k] *= ctype_scale(k, fI, fA, fS);
@@ -116,8 +164,8 @@ __global__ __launch_bounds__(256) void k_node_fwd(NodeArgs<T> A) {
   }
 }
 
-template <typename T, int OP>
-__global__ __launch_bounds__(256) void k_node_bwd(NodeArgs<T> A) {
+template <typename T, int OP, typename AR = NodeArgs<T>>
+__global__ __launch_bounds__(256) void k_node_bwd(AR A) {
   const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= A.nh) return;
   const int n = (int)(t / A.H), h = (int)(t % A.H);
@@ -222,7 +270,7 @@ __global__ __launch_bounds__(256) void k_node_bwd(NodeArgs<T> A) {
     T X[9], c[9], gc[9], gX[9];
     ld9(X, A.a + 9 * t);
     decomp(c, X);
-    const T* go = A.gout + (size_t)n * 3 * A.H + h;
+    auto go = A.gout + (size_t)n * 3 * A.H + h;
     const T g0 = go[0], g1 = go[A.H], g2 = go[2 * A.H];
     const T ss = c[4] + c[5];
     gc[0] = T(6) * g0 * c[0];
@@ -258,7 +306,7 @@ __global__ __launch_bounds__(256) void k_node_bwd(NodeArgs<T> A) {
     ldc(c, A.a + t, A.nh);
     ld9(g, A.gout + 9 * t);
     fullT(gc, g);
-    const T* f = A.b + 3 * t;
+    auto f = A.b + 3 * t;
     const T fI = f[0], fA = f[1], fS = f[2];
     T gI = gc[0] * c[0];
     T gA = gc[1] * c[1] + gc[2] * c[2] + gc[3] * c[3];
@@ -266,7 +314,7 @@ __global__ __launch_bounds__(256) void k_node_bwd(NodeArgs<T> A) {
 #pragma unroll
     for (int k = 0; k < 9; ++k) gc[k] *= ctype_scale(k, fI, fA, fS);
     stc(A.ga + t, A.nh, gc);
-    T* gf = A.gb + 3 * t;
+    auto gf = A.gb + 3 * t;
     gf[0] = gI;
     gf[1] = gA;
     gf[2] = gS;
@@ -297,10 +345,68 @@ static int run(int op, bool bwd, const NodeArgs<T>& A, hipStream_t st) {
   }
 }
 
+// second order (see Dual above): d_g = J_f (t_a, t_b) by the forward on duals (tangent output only) and
+// (d_a, d_b) = H (t_a, t_b) by the first backward on duals (g with a zero tangent; tangent outputs only)
+template <typename T, int OP>
+static int launch_op2(const NodeArgs<T>& A, const T* ta, const T* tb, T* d_g, T* d_a, T* d_b, hipStream_t st) {
+  using DA = NodeArgs<Dual<T>, DIn<T>, DOut<T>>;
+  const int tb_ = 256;
+  const unsigned grid = (unsigned)((A.nh + tb_ - 1) / tb_);
+  const DIn<T> a{A.a, ta}, b{A.b, tb};
+  if (d_g) {
+    DA F{A.n, A.H, A.nh, a, b, DOut<T>{nullptr, d_g}, DIn<T>{nullptr, nullptr}, DOut<T>{nullptr, nullptr},
+         DOut<T>{nullptr, nullptr}, DIn<T>{nullptr, nullptr}};
+    hipLaunchKernelGGL((k_node_fwd<Dual<T>, OP, DA>), dim3(grid), dim3(tb_), 0, st, F);
+  }
+  if (d_a || d_b) {
+    DA B{A.n, A.H, A.nh, a, b, DOut<T>{nullptr, nullptr}, DIn<T>{A.gout, nullptr}, DOut<T>{nullptr, d_a},
+         DOut<T>{nullptr, d_b}, DIn<T>{nullptr, nullptr}};
+    hipLaunchKernelGGL((k_node_bwd<Dual<T>, OP, DA>), dim3(grid), dim3(tb_), 0, st, B);
+  }
+  return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
+}
+
+template <typename T>
+static int run2(int op, const NodeArgs<T>& A, const T* ta, const T* tb, T* d_g, T* d_a, T* d_b, hipStream_t st) {
+  if (A.nh == 0) return kOk;
+  switch (op) {
+    case TMDNET_TN_PRE: return launch_op2<T, TMDNET_TN_PRE>(A, ta, tb, d_g, d_a, d_b, st);
+    case TMDNET_TN_POST_O3: return launch_op2<T, TMDNET_TN_POST_O3>(A, ta, tb, d_g, d_a, d_b, st);
+    case TMDNET_TN_POST_SO3: return launch_op2<T, TMDNET_TN_POST_SO3>(A, ta, tb, d_g, d_a, d_b, st);
+    case TMDNET_TN_RESID: return launch_op2<T, TMDNET_TN_RESID>(A, ta, tb, d_g, d_a, d_b, st);
+    case TMDNET_TN_NORMS: return launch_op2<T, TMDNET_TN_NORMS>(A, ta, tb, d_g, d_a, d_b, st);
+    case TMDNET_TN_ENORM: return launch_op2<T, TMDNET_TN_ENORM>(A, ta, tb, d_g, d_a, d_b, st);
+    case TMDNET_TN_EOUT: return launch_op2<T, TMDNET_TN_EOUT>(A, ta, tb, d_g, d_a, d_b, st);
+    default: return kBadArgument;
+  }
+}
+
 }  // namespace node
 }  // namespace tmd
 
 using namespace tmd;
+
+extern "C" int tmdnet_tn_node_bwd2(int dtype, int op, int n_nodes, int hidden, const void* a, const void* b,
+                                   const void* grad_out, const void* t_a, const void* t_b, void* d_grad_out,
+                                   void* d_a, void* d_b, void* stream) {
+  if (n_nodes < 0 || hidden <= 0 || !a || !grad_out) return kBadArgument;
+  const bool two = op == TMDNET_TN_POST_O3 || op == TMDNET_TN_POST_SO3 || op == TMDNET_TN_RESID || op == TMDNET_TN_EOUT;
+  if (two && !b) return kBadArgument;
+  if (!two && (t_b || d_b)) return kBadArgument;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == TMDNET_F32) {
+    node::NodeArgs<float> A{n_nodes, hidden, (size_t)n_nodes * hidden, (const float*)a, (const float*)b, nullptr,
+                            (const float*)grad_out, nullptr, nullptr, nullptr};
+    return node::run2<float>(op, A, (const float*)t_a, (const float*)t_b, (float*)d_grad_out, (float*)d_a,
+                             (float*)d_b, st);
+  } else if (dtype == TMDNET_F64) {
+    node::NodeArgs<double> A{n_nodes, hidden, (size_t)n_nodes * hidden, (const double*)a, (const double*)b, nullptr,
+                             (const double*)grad_out, nullptr, nullptr, nullptr};
+    return node::run2<double>(op, A, (const double*)t_a, (const double*)t_b, (double*)d_grad_out, (double*)d_a,
+                              (double*)d_b, st);
+  }
+  return kUnsupported;
+}
 
 extern "C" int tmdnet_tn_node_fwd(int dtype, int op, int n_nodes, int hidden, const void* a,
                                   const void* b, void* out, void* stream) {

@@ -79,6 +79,7 @@ SIGNATURES = {
     "tmdnet_tn_message_bwd_add": (I, [I, I, I, P, P, I, D, P, I, P, I, P, P, P, P, P, P]),
     "tmdnet_tn_node_fwd": (I, [I, I, I, I, P, P, P, P]),
     "tmdnet_tn_node_bwd": (I, [I, I, I, I, P, P, P, P, P, P, P]),
+    "tmdnet_tn_node_bwd2": (I, [I, I, I, I, P, P, P, P, P, P, P, P, P]),
     "tmdnet_silu_fwd": (I, [I, I, I, P, I, P, P, P]),
     "tmdnet_silu_bwd": (I, [I, I, I, P, I, P, P, I, P, P, P]),
     "tmdnet_atom_sum_fwd": (I, [I, I, I, P, P, P, P, P, P]),

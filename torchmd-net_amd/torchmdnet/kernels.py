@@ -1949,6 +1949,9 @@ class _TNMessageBwd(Function):
         saved = ctx.saved_tensors
         _create = torch.is_grad_enabled()  # third order only if the caller builds a graph
         g_add = ggs[1] if ctx.has_add else None  # gT = VJP(gmsg) + gadd: identity in gadd
+        from . import tn_node
+        if tn_node.SECOND_ORDER != "composite" and not _create:
+            return _tn_message_second_order(ctx, saved, ggs) + (None, g_add)
         with torch.enable_grad():
             leaves = [t.detach().requires_grad_(True) for t in saved]
             gmsg, ea, Tc = leaves
@@ -1960,6 +1963,36 @@ class _TNMessageBwd(Function):
             second = torch.autograd.grad([f for f, _ in sel], leaves, [g for _, g in sel],
                                          create_graph=_create, allow_unused=True)
         return tuple(second) + (None, g_add)
+
+
+def _tn_message_second_order(ctx, saved, ggs):
+    """The message is bilinear in (ea, Tc): with (gea, gT) = (G(gmsg, Tc), M^T(ea, gmsg)) its second-order
+    VJP for cotangents (t_ea, t_T) is d_gmsg = M(t_ea, Tc) + M(ea, t_T) (two forward launches) and
+    (d_ea, d_T) = (G(gmsg, t_T), M^T(t_ea, gmsg)) -- ONE first-backward launch with (t_ea, t_T) in place of
+    (ea, Tc).  The first backward's pair-symmetry precondition then applies to t_ea: the edge factors'
+    cotangent is, like the factors, a function of the pair distance (edge MLP -> rbf -> r, whose
+    cotangent <t_pos[src] - t_pos[dst], u> is the same for both directions of a pair)."""
+    gmsg, ea, Tc = saved
+    t_ea, t_T = ggs
+    graph = ctx.graph
+    need = ctx.needs_input_grad  # gmsg, ea, Tc, graph, gadd
+    if t_ea is None and t_T is None:
+        return None, None, None
+    t_ea = torch.zeros_like(ea) if t_ea is None else _rowmajor(t_ea)
+    t_T = torch.zeros_like(Tc) if t_T is None else t_T.contiguous()
+    d_g = None
+    if need[0]:
+        d_g = torch.empty_like(Tc)
+        tn_message_fwd_launch(t_ea, Tc, graph, d_g)
+        tmp = torch.empty_like(Tc)
+        tn_message_fwd_launch(ea, t_T, graph, tmp)
+        d_g.add_(tmp)
+    d_ea = d_T = None
+    if need[1] or need[2]:
+        d_ea = torch.empty((graph.n_edges, 3 * Tc.shape[2]), dtype=Tc.dtype, device=Tc.device)
+        d_T = torch.empty_like(Tc)
+        tn_message_bwd_launch(t_ea, t_T, graph, gmsg, d_ea, d_T)
+    return d_g, (d_ea if need[1] else None), (d_T if need[2] else None)
 
 
 def tn_embed(P, Q, W, C, u, graph):

@@ -183,9 +183,11 @@ class TensorNet(nn.Module):
             # capture mode: the padding count stays on the device (no host sync)
             npd = graph.num_pairs_dev if shift is None else graph.num_pairs_dev + shift[0]
             graph.self0_dev = (npd, cap)
-        else:
+        elif self.static_shapes:
             n_eff = graph.num_pairs + (0 if shift is None else shift[1])
-            graph.self0_mult = float(1 + max(0, cap - n_eff)) if self.static_shapes else 1.0
+            graph.self0_mult = float(1 + max(0, cap - n_eff))
+        else:  # (no padding multiplicity: the host pair count is not needed, e.g. under capture)
+            graph.self0_mult = 1.0
         de = self.distance_expansion
         k = 1 + len(self.layers)  # consumers of the rbf / cutoff rows: the embedding and every layer
         if self.trainable_rbf and torch.is_grad_enabled():

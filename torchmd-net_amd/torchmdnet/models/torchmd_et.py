@@ -250,7 +250,10 @@ class TorchMD_ET(nn.Module):
             edge_attr_s, C_s = edge_attr, C
         graph.cutoff = C_s
         if self.neighbor_embedding is not None:
-            x = self.neighbor_embedding(z, x, graph, graph.distances, edge_attr, cutoff=C, x_emb=x_ne, fused=ne_fused)
+            if ne_fused is not None:
+                x = self.neighbor_embedding.fused_forward(z, x, graph, graph.distances, C, x_ne, *ne_fused)
+            else:
+                x = self.neighbor_embedding(z, x, graph, graph.distances, edge_attr, cutoff=C, x_emb=x_ne)
         if self.fused_stack and len(self.attention_layers) > 0:
             # all layers as one autograd node (et_stack.py): fused GEMMs, HIP epilogue, hand-scheduled
             # backward; same math as the loop below

@@ -296,20 +296,24 @@ class NeighborEmbedding(nn.Module):
         x_nb = torch.ops.tmdnet.nbr_embed(self.embedding(z), W, C, row_ptr, src, dst)
         return self.combine(torch.cat([x, x_nb], dim=1))
 
-    def forward(self, z: Tensor, x: Tensor, edge_index: Tensor, edge_weight: Tensor, edge_attr: Optional[Tensor],
-                cutoff: Optional[Tensor] = None, x_emb: Optional[Tensor] = None, fused=None) -> Tensor:
+    @torch.jit.unused
+    def fused_forward(self, z: Tensor, x: Tensor, graph, r: Tensor, cutoff: Tensor, x_emb: Optional[Tensor],
+                      rbf, rbf_fn) -> Tensor:
+        """Large systems (TorchMD_ET): distance_proj formed inside the aggregation kernel from the distances
+        ``r`` (kernels.nbr_embed_fused; ``rbf`` = (mu, beta, cutoff_lower, cutoff_upper, rbf_type), ``rbf_fn``
+        the basis module) -- no rbf or projection rows; the model's CSR graph and cutoff."""
+        if x_emb is None:
+            x_emb = self.embedding(z)
+        x_cat = kernels.nbr_embed_fused(x_emb, r, cutoff, self.distance_proj.weight, self.distance_proj.bias,
+                                        graph, rbf, rbf_fn, x_self=x)
+        return kernels.linear(x_cat, self.combine.weight, self.combine.bias)
+
+    def forward(self, z: Tensor, x: Tensor, edge_index: Tensor, edge_weight: Tensor, edge_attr: Tensor,
+                cutoff: Optional[Tensor] = None, x_emb: Optional[Tensor] = None) -> Tensor:
         """``x_emb``: this module's embedding of ``z`` when the caller looked it up already (TorchMD_ET
-        does both tables' lookups in one node).  ``fused`` = (rbf params, rbf module): distance_proj is
-        formed inside the aggregation kernel from ``edge_weight`` (large systems, kernels.nbr_embed_fused;
-        ``edge_attr`` unused, the caller's CSR graph and cutoff required)."""
+        does both tables' lookups in one node)."""
         if torch.jit.is_scripting():
             raise RuntimeError("scripted NeighborEmbedding: use script_forward (CSR graph)")
-        if fused is not None:
-            if x_emb is None:
-                x_emb = self.embedding(z)
-            x_cat = kernels.nbr_embed_fused(x_emb, edge_weight, cutoff, self.distance_proj.weight,
-                                            self.distance_proj.bias, edge_index, fused[0], fused[1], x_self=x)
-            return kernels.linear(x_cat, self.combine.weight, self.combine.bias)
         graph, perm = as_graph(edge_index, x.shape[0])
         if perm is not None:
             edge_weight, edge_attr = edge_weight[perm], edge_attr[perm]

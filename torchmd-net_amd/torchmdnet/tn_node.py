@@ -16,6 +16,8 @@ Every op is an autograd Function with HIP forward and HIP first backward; the ba
 Function whose backward (second order, force-loss training only) differentiates the PyTorch
 composite below twice -- the same scheme as the other hot-path ops (``kernels.py``).
 """
+import os
+
 import torch
 from torch.autograd import Function
 
@@ -116,6 +118,20 @@ def node_bwd_launch(op, a, b, gout, gadd, ga, gb):
     nat.check(rc, f"tmdnet_tn_node_bwd(op={op})")
 
 
+def node_bwd2_launch(op, a, b, gout, ta, tb, d_g, d_a, d_b):
+    lib = nat.load()
+    n, h = _nh(op, a)
+    rc = lib.tmdnet_tn_node_bwd2(nat.dtype_code(a.dtype), op, n, h, nat.ptr(a), nat.ptr(b), nat.ptr(gout),
+                                 nat.ptr(ta), nat.ptr(tb), nat.ptr(d_g), nat.ptr(d_a), nat.ptr(d_b),
+                                 nat.stream(a.device))
+    nat.check(rc, f"tmdnet_tn_node_bwd2(op={op})")
+
+
+# the hand-written second orders (tmdnet_tn_node_bwd2, the channel mixes' GEMMs); "composite": autograd's
+# double differentiation of the PyTorch restatements (A/B switch, and always for a third order)
+SECOND_ORDER = os.environ.get("TMDNET_TN_SECOND_ORDER", "hip")
+
+
 def _double_backward(fwd, primals, gouts, ggs):
     """Second order of a first backward ``g -> VJP(fwd, primals, g)``: returns the gradients w.r.t.
     (gouts..., primals...) for the incoming ``ggs`` (one per primal), differentiating the composite
@@ -185,6 +201,20 @@ class _NodeOpBwd(Function):
         gout, a, b = ctx.saved_tensors
         op = ctx.op
         g_add = gga if ctx.has_add else None  # ga = VJP(gout) + gadd: identity in gadd
+        if SECOND_ORDER != "composite" and not torch.is_grad_enabled() and a.is_cuda:
+            # forward-over-reverse on dual numbers (tmdnet_tn_node_bwd2): d_gout = J (t_a, t_b),
+            # (d_a, d_b) = H (t_a, t_b)
+            need = ctx.needs_input_grad
+            ta = None if gga is None else gga.contiguous()
+            tb = None if (ggb is None or b is None) else ggb.contiguous()
+            if ta is None and tb is None:
+                return None, None, None, None, g_add
+            d_g = torch.empty_like(gout) if need[1] else None
+            d_a = torch.empty_like(a) if need[2] else None
+            d_b = torch.empty_like(b) if (b is not None and need[3]) else None
+            if d_g is not None or d_a is not None or d_b is not None:
+                node_bwd2_launch(op, a, b, gout, ta, tb, d_g, d_a, d_b)
+            return None, d_g, d_a, d_b, g_add
         if b is None:
             d = _double_backward(lambda x: op_composite(op, x), [a], [gout], [gga])
             return None, d[0], d[1], None, g_add
@@ -293,8 +323,50 @@ class _Mix3Bwd(Function):
     @staticmethod
     def backward(ctx, ggc, *ggw):
         gout, c, w0, w1, w2 = ctx.saved_tensors
+        if SECOND_ORDER != "composite" and not torch.is_grad_enabled() and c.is_cuda:
+            return (None,) + _mix3_second_order(ctx.needs_input_grad, gout, c, (w0, w1, w2), ggc, ggw)
         d = _double_backward(mix3_composite, [c, w0, w1, w2], [gout], [ggc] + list(ggw))
         return (None,) + tuple(d)
+
+
+def _mix3_second_order(need, gout, c, ws, ggc, ggw):
+    """VJP of (gc, gW_p) = (gout W_p, gout_p^T c_p) per row block p for cotangents (ggc, ggW_p) -- all GEMMs:
+    d_gout_p = ggc_p W_p^T + c_p ggW_p^T,  d_c_p = gout_p ggW_p,  d_W_p = gout_p^T ggc_p."""
+    ggw = [None if g is None else g.contiguous() for g in ggw]
+    ggc = None if ggc is None else ggc.contiguous()
+    gb, cb = _blocks(gout), _blocks(c)
+    d_gout = d_c = None
+    d_w = [None, None, None]
+    if need[1] and (ggc is not None or any(g is not None for g in ggw)):
+        d_gout = torch.empty_like(gout)
+        probs = []
+        for p, dst in enumerate(_blocks(d_gout)):
+            first = True
+            if ggc is not None:
+                probs.append((_blocks(ggc)[p], ws[p], True, None, dst, False))
+                first = False
+            if ggw[p] is not None:
+                probs.append((cb[p], ggw[p], True, None, dst, not first))
+                first = False
+            if first:
+                dst.zero_()
+        # the accumulating problems after the ones they add to (problems of one launch run in any order)
+        kernels.gemm_group([q for q in probs if not q[5]])
+        acc = [q for q in probs if q[5]]
+        if acc:
+            kernels.gemm_group(acc)
+    if need[2] and any(g is not None for g in ggw):
+        d_c = torch.zeros_like(c) if any(g is None for g in ggw) else torch.empty_like(c)
+        kernels.gemm_group([(gb[p], ggw[p], False, None, dst, False)
+                            for p, dst in enumerate(_blocks(d_c)) if ggw[p] is not None])
+    if ggc is not None:
+        tn = []
+        for p in range(3):
+            if need[3 + p]:
+                d_w[p] = torch.empty_like(ws[p])
+                tn.append({"A": gb[p], "B": _blocks(ggc)[p], "C": d_w[p]})
+        kernels.wgrad_tn(tn)
+    return (d_gout, d_c) + tuple(d_w)
 
 
 def mix3(c, w0, w1, w2):
