@@ -390,6 +390,19 @@ int tmdnet_eq_head_hvp(int dtype, int n_atoms, int hidden, const void* x, const 
                        const void* const* weights, const void* grad_y, const void* tan_x,
                        const void* tan_vec, void* d_x, void* d_vec, void* d_grad_y,
                        void* const* saves, void* stream);
+/* The same forward + Jacobian (seeded with grad_y, NULL = 1) on the bf16 MFMA at fp32 accuracy over 16-atom
+ * tiles (eq_head_x3.hip): fp32, hidden = 128 only (else TMDNET_UNSUPPORTED).  pieces[10]: the exact
+ * three-piece bf16 splits (tmdnet_proj_split_f32 layout [3][N][K]) of [W1; W2] (192 x 128), U1 (128 x 256),
+ * U2 (128 x 128), V1 (64 x 64), P1 (64 x 128) and of their transposes P1^T, V1^T, U2^T, U1^T, [W1; W2]^T;
+ * vectors[5] = u1b, u2b, p1b, p2w (2 x 64), p2b (block 1 = vec1_proj W1, vec2_proj W2, update_net U1 / U2;
+ * block 2 = V1, P1 / P2).  jac_x / jac_vec both or neither; 16-byte aligned rows. */
+int tmdnet_eq_head_x3_f32(int n_atoms, int hidden, const void* x, const void* vec, const void* const* pieces,
+                          const void* const* vectors, void* y, void* jac_x, void* jac_vec, const void* grad_y,
+                          void* stream);
+/* The ten piece matrices of tmdnet_eq_head_x3_f32 from the head's 12 weights (tmdnet_eq_head_fwd's order),
+ * in ONE launch, packed back to back in that order into pieces_buf (tmdnet_eq_head_x3_pieces_bytes). */
+size_t tmdnet_eq_head_x3_pieces_bytes(int hidden);
+int tmdnet_eq_head_x3_split_f32(int hidden, const void* const* weights, void* pieces_buf, void* stream);
 /* grad_x = grad_y[n] * jac_x[n], grad_vec = grad_y[n] * jac_vec[n] (the head's backward). */
 int tmdnet_eq_head_bwd(int dtype, int n_atoms, int hidden, const void* grad_y, const void* jac_x,
                        const void* jac_vec, void* grad_x, void* grad_vec, void* stream);

@@ -167,3 +167,34 @@ def test_head_second_order_hand_matches_composite(dtype, H, N, tol, monkeypatch)
         assert a is not None and torch.isfinite(a).all(), i
         assert _rel(a, b) < tol, (i, _rel(a, b))
     assert torch.all(hand[1][2] == 0)  # the isolated atom's masked rows get nothing of any order
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N", [37, 576, 5003])
+def test_mfma_head_matches_valu_kernel_and_fp64(N, monkeypatch):
+    """tmdnet_eq_head_x3_f32 (16-atom tiles on the bf16 MFMA, exact three-piece splits; the default fp32
+    H = 128 path) against the per-atom VALU kernel (TMDNET_HEAD_X3 off) and the fp64 composite: energies,
+    the per-atom Jacobian through the force pass (g_x, g_vec with a random seed), a zero-vector atom
+    (the masked norm) and a partial last tile."""
+    head = _head(128, torch.float32).to(DEV)
+    ps = kernels.eq_head_params(head.output_network)
+    x, vec = _inputs(N, 128, torch.float32, DEV)
+    gy = torch.randn(N, 1, device=DEV)
+
+    def run(x3):
+        monkeypatch.setattr(kernels, "HEAD_X3", x3)
+        xx, vv = x.clone().requires_grad_(True), vec.clone().requires_grad_(True)
+        y = kernels.eq_scalar_head(xx, vv, head.output_network)
+        gx, gv = torch.autograd.grad(y, (xx, vv), gy)
+        return y.detach(), gx, gv
+
+    y1, gx1, gv1 = run(True)
+    y0, gx0, gv0 = run(False)
+    ps64 = [p.detach().double() for p in ps]
+    x64, v64 = x.double().requires_grad_(True), vec.double().requires_grad_(True)
+    y64 = kernels.eq_head_composite(x64, v64, ps64)
+    gx64, gv64 = torch.autograd.grad(y64, (x64, v64), gy.double())
+    for a, b, r in ((y1, y0, y64), (gx1, gx0, gx64), (gv1, gv0, gv64)):
+        assert _rel(a.double(), r.detach()) < 2e-6
+        assert _rel(b.double(), r.detach()) < 2e-6
+    assert torch.all(gv1[2] == 0)

@@ -746,8 +746,9 @@ __global__ __launch_bounds__(256) void k_proj_split(int N, int K, const float* W
 // Grid: x = column tiles (fast: the tiles of one row block run together and re-read its A rows from
 // L2), y = row tiles.
 // (Output stores staged per wave through LDS as whole 128-byte lines were measured and dropped: the
-// L2 already merges the half-line pieces of adjacent column blocks)
-template <int KS, int MB, int BN, bool NT = false>
+// L2 already merges the half-line pieces of adjacent column blocks; nontemporal stores too:
+// C2 step 0.885 -> 0.913 ms.)
+template <int KS, int MB, int BN>
 __global__ __launch_bounds__(256) void k_proj_x3(Args P) {
   constexpr int K = 32 * KS, LD = K + 8;  // LDS row pitch in bf16 (16-byte pad: rows shift banks)
   __shared__ __attribute__((aligned(16))) unsigned short w[3][BN][LD];
@@ -819,11 +820,7 @@ __global__ __launch_bounds__(256) void k_proj_x3(Args P) {
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb) {
       const int m = m0 + 16 * mb + (lane & 15);
-      if (m < P.M) {
-        f4* out = reinterpret_cast<f4*>(P.C + (size_t)m * P.ldc + n0 + nl);
-        if (NT) __builtin_nontemporal_store(acc[mb] + bv, out);
-        else *out = acc[mb] + bv;
-      }
+      if (m < P.M) *reinterpret_cast<f4*>(P.C + (size_t)m * P.ldc + n0 + nl) = acc[mb] + bv;
     }
   }
 }
@@ -1534,7 +1531,6 @@ extern "C" int tmdnet_proj_f32(int M, int N, int K, const void* A, int lda, cons
   if ((((uintptr_t)A) | ((uintptr_t)Wp) | ((uintptr_t)C) | ((uintptr_t)bias)) & 15) return kUnsupported;
   static const int mb_env = getenv("TMDNET_PROJ_MB") ? atoi(getenv("TMDNET_PROJ_MB")) : 0;  // tuning
   static const int bn_env = getenv("TMDNET_PROJ_BN") ? atoi(getenv("TMDNET_PROJ_BN")) : 0;
-  static const bool nt_env = getenv("TMDNET_PROJ_NT") && atoi(getenv("TMDNET_PROJ_NT"));  // A/B: streaming stores
   // measured (tools/proj_time.py): C2 [6613 x 64] x [64 x 4096] 38 us at 128 x 64 tiles (library 48);
   // C5 [1.36M x 64] x [64 x 512] 0.90 ms at 256 x 128 (library 1.07)
   const bool big = M >= 65536;
@@ -1552,10 +1548,7 @@ extern "C" int tmdnet_proj_f32(int M, int N, int K, const void* A, int lda, cons
     if (bn == 128) {
       if (mb == 4) TMD_PROJ(2, 4, 128); else TMD_PROJ(2, 2, 128);
     } else {
-      if (mb == 4) TMD_PROJ(2, 4, 64);
-      else if (mb == 2 && nt_env) hipLaunchKernelGGL((proj::k_proj_x3<2, 2, 64, true>), g, dim3(256), 0, st, P);
-      else if (mb == 2) TMD_PROJ(2, 2, 64);
-      else TMD_PROJ(2, 1, 64);
+      if (mb == 4) TMD_PROJ(2, 4, 64); else if (mb == 2) TMD_PROJ(2, 2, 64); else TMD_PROJ(2, 1, 64);
     }
   } else {
     if (mb == 4) TMD_PROJ(1, 4, 64); else TMD_PROJ(1, 2, 64);

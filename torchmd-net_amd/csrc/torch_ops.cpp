@@ -1699,6 +1699,21 @@ struct FusedAux {  // per evaluation: pair numbering + RBF fragments; per layer:
   std::vector<Tensor> qkv_w, qkv_b, img, wsc, bias;
 };
 
+// the RBF fragments of the pair rows (tmdnet_fep_frags_f32), once per evaluation
+void fused_frags(FusedAux* F, const Tensor& dist, const Tensor& mu, const Tensor& beta, double cl, double cu,
+                 int64_t rbf, void* st) {
+  if (F->frags.defined()) return;
+  const int64_t R = mu.size(0);
+  Tensor r_rows = dist.index_select(0, F->pair_edge.to(at::kLong)).contiguous();
+  F->n_rows = r_rows.size(0);
+  F->frags = at::empty({std::max<int64_t>(1, static_cast<int64_t>(tmdnet_fep_frags_bytes(F->n_rows, R) / 2))},
+                       opts(dist).dtype(at::kHalf));
+  F->dscale = at::empty({std::max<int64_t>(1, F->n_rows)}, opts(dist));
+  check(tmdnet_fep_frags_f32(F->n_rows, static_cast<int>(R), ptr(r_rows), ptr(mu), ptr(beta), cl, cu,
+                             static_cast<int>(rbf), ptr(F->frags), ptr(F->dscale), st),
+        "tmdnet_fep_frags_f32");
+}
+
 // the fused-projection stack forward (et_stack._forward_layers with meta.fep): returns (x_out, vec_out)
 std::pair<Tensor, Tensor> stack_forward_fused(const Tensor& x_in, const Tensor& dist, const Tensor& C, const Tensor& u,
                                               const Tensor& row_ptr, const Tensor& src, const Tensor& mu,
@@ -1711,15 +1726,8 @@ std::pair<Tensor, Tensor> stack_forward_fused(const Tensor& x_in, const Tensor& 
   auto o = opts(x);
   void* st = stream_of(x);
   A->pk = pack_stack(P, L, np, c.hk, c.hv);
-  // RBF fragments of the pair rows, once for every layer
-  Tensor r_rows = dist.index_select(0, F->pair_edge.to(at::kLong)).contiguous();
-  F->n_rows = r_rows.size(0);
-  F->frags = at::empty({std::max<int64_t>(1, static_cast<int64_t>(tmdnet_fep_frags_bytes(F->n_rows, R) / 2))},
-                       o.dtype(at::kHalf));
-  F->dscale = at::empty({std::max<int64_t>(1, F->n_rows)}, o);
-  check(tmdnet_fep_frags_f32(F->n_rows, static_cast<int>(R), ptr(r_rows), ptr(mu), ptr(beta), c.cl, c.cu,
-                             static_cast<int>(c.rbf), ptr(F->frags), ptr(F->dscale), st),
-        "tmdnet_fep_frags_f32");
+  // RBF fragments of the pair rows, once for every layer (the fused neighbour embedding may have made them)
+  fused_frags(F, dist, mu, beta, c.cl, c.cu, c.rbf, st);
   Tensor vp = v_perm(H, c.heads, x);
   F->qkv_perm = at::cat({at::arange(2 * H, vp.options()), 2 * H + vp});
   Tensor one = at::cat({at::arange(H, vp.options()), H + vp});  // [dk | dv] rows in the planar order
@@ -1936,17 +1944,37 @@ std::tuple<Tensor, Tensor> et_energy_forces(
                              ptr<int32_t>(src), ptr<int32_t>(dst), ptr(dl), ptr(dist), ptr(mu), ptr(beta), cl, cu,
                              ptr(f), ptr(C), ptr(u), st),
         "tmdnet_edge_geom_fwd");
-  // neighbour embedding: W = distance_proj(f); [x | x_nb] by the aggregation kernel; combine
-  Tensor W, cat, x1 = x;
+  // neighbour embedding: W = distance_proj(f); [x | x_nb] by the aggregation kernel; combine.  Large systems
+  // (the fused stack's envelope): distance_proj formed inside the aggregation kernel from the pair rows'
+  // fragments (tmdnet_nbr_fused_fwd_f32, eager kernels.nbr_embed_fused) -- no E x H rows
+  Tensor W, cat, x1 = x, nimg, nwsc, nbias;
+  const bool nb_fused = nb && fused;
   if (nb) {
-    W = at::empty({E, H}, o);
-    gemm_into(f, val(nb_dist_w_), true, val(nb_dist_b_), W, false);
     cat = at::empty({N, 2 * H}, o);
     float* cb = static_cast<float*>(cat.data_ptr());
-    check(tmdnet_nbr_embed_fwd(dt, static_cast<int>(N), static_cast<int>(H), ptr<int32_t>(row_ptr),
-                               ptr<int32_t>(src), static_cast<int>(E), ptr(xe), static_cast<int>(H), ptr(W),
-                               static_cast<int>(H), ptr(C), cb + H, static_cast<int>(2 * H), ptr(x), cb, st),
-          "tmdnet_nbr_embed_fwd");
+    if (nb_fused) {
+      fused_frags(&F, dist, mu, beta, cl, cu, rbf_type, st);
+      const Tensor dw = val(nb_dist_w_).contiguous(), db = val(nb_dist_b_).contiguous();
+      nimg = at::empty({static_cast<int64_t>(tmdnet_fep_image_bytes(static_cast<int>(H), static_cast<int>(R)) / 2)},
+                       o.dtype(at::kHalf));
+      nwsc = at::empty({H}, o);
+      nbias = at::empty({H}, o);
+      check(tmdnet_fep_split_f32(static_cast<int>(H), static_cast<int>(R), ptr(dw), static_cast<int>(dw.stride(0)),
+                                 ptr(db), ptr(nimg), ptr(nwsc), ptr(nbias), st),
+            "tmdnet_fep_split_f32");
+      check(tmdnet_nbr_fused_fwd_f32(static_cast<int>(N), static_cast<int>(H), static_cast<int>(R),
+                                     ptr<int32_t>(row_ptr), ptr<int32_t>(src), static_cast<int>(E), ptr(xe),
+                                     static_cast<int>(H), ptr(C), ptr<int32_t>(F.pair_row), ptr(F.frags), F.n_rows,
+                                     ptr(nimg), ptr(nwsc), ptr(nbias), cb + H, static_cast<int>(2 * H), ptr(x), cb, st),
+            "tmdnet_nbr_fused_fwd_f32");
+    } else {
+      W = at::empty({E, H}, o);
+      gemm_into(f, val(nb_dist_w_), true, val(nb_dist_b_), W, false);
+      check(tmdnet_nbr_embed_fwd(dt, static_cast<int>(N), static_cast<int>(H), ptr<int32_t>(row_ptr),
+                                 ptr<int32_t>(src), static_cast<int>(E), ptr(xe), static_cast<int>(H), ptr(W),
+                                 static_cast<int>(H), ptr(C), cb + H, static_cast<int>(2 * H), ptr(x), cb, st),
+            "tmdnet_nbr_embed_fwd");
+    }
     x1 = at::empty({N, H}, o);
     gemm_into(cat, val(nb_comb_w_), true, val(nb_comb_b_), x1, false);
   }
@@ -1961,9 +1989,33 @@ std::tuple<Tensor, Tensor> et_energy_forces(
   Tensor y_atom = at::empty({N, 1}, o), jx = at::empty({N, H}, o), jv = at::empty({N, 3, H}, o);
   const void* hw[12];
   for (int i = 0; i < 12; ++i) hw[i] = head_params[i].data_ptr();
-  check(tmdnet_eq_head_fwd(dt, static_cast<int>(N), static_cast<int>(H), ptr(xo), ptr(vo), hw, ptr(y_atom), ptr(jx),
-                           ptr(jv), st),
-        "tmdnet_eq_head_fwd");
+  // the MFMA head over 16-atom tiles (eager kernels._eq_head_x3) when its envelope holds, else per atom
+  bool head_x3 = dt == TMDNET_F32 && tmdnet_eq_head_x3_pieces_bytes(static_cast<int>(H)) > 0;
+  for (int i : {3, 5, 9}) head_x3 = head_x3 && (reinterpret_cast<uintptr_t>(hw[i]) & 15) == 0;
+  for (int i = 0; i < 12; ++i) head_x3 = head_x3 && head_params[i].is_contiguous();
+  if (head_x3) {
+    const size_t pb = tmdnet_eq_head_x3_pieces_bytes(static_cast<int>(H));
+    Tensor pieces = at::empty({static_cast<int64_t>(pb / 2)}, o.dtype(at::kShort));
+    check(tmdnet_eq_head_x3_split_f32(static_cast<int>(H), hw, pieces.data_ptr(), st), "tmdnet_eq_head_x3_split_f32");
+    const int64_t O = H / 2;
+    const int64_t nk[10][2] = {{H + O, H}, {H, 2 * H}, {H, H}, {O, O}, {O, 2 * O},
+                               {2 * O, O}, {O, O},     {H, H}, {2 * H, H}, {H, H + O}};
+    const void* pc[10];
+    const int16_t* base = static_cast<const int16_t*>(pieces.data_ptr());
+    int64_t off = 0;
+    for (int i = 0; i < 10; ++i) {
+      pc[i] = base + off;
+      off += 3 * nk[i][0] * nk[i][1];
+    }
+    const void* hv[5] = {hw[3], hw[5], hw[9], hw[10], hw[11]};
+    check(tmdnet_eq_head_x3_f32(static_cast<int>(N), static_cast<int>(H), ptr(xo), ptr(vo), pc, hv, ptr(y_atom),
+                                ptr(jx), ptr(jv), nullptr, st),
+          "tmdnet_eq_head_x3_f32");
+  } else {
+    check(tmdnet_eq_head_fwd(dt, static_cast<int>(N), static_cast<int>(H), ptr(xo), ptr(vo), hw, ptr(y_atom), ptr(jx),
+                             ptr(jv), st),
+          "tmdnet_eq_head_fwd");
+  }
   const int64_t n_mol = batch.max().item<int64_t>() + 1;  // (the reference reduce's dim_size, a host read)
   const Tensor sd = std_in.to(at::kFloat).contiguous(), mn = mean_in.to(at::kFloat).contiguous();
   Tensor y = at::empty({n_mol, 1}, o);
@@ -1983,7 +2035,17 @@ std::tuple<Tensor, Tensor> et_energy_forces(
   auto gs = fused ? stack_backward_fused(A, F, gX, gV, C, u, row_ptr, src, P, c, R)
                   : stack_backward_dr(A, gX, gV, dist, C, u, mu, beta, P, g, c);  // (g_x1, g_r, g_C, g_u)
   Tensor gf, gC_nb;
-  if (nb) {
+  if (nb_fused) {  // dr mode: g_C and g_r per edge, added to the stack's (no E x H / E x R gradient rows)
+    Tensor g_cat = at::empty({N, 2 * H}, o);
+    gemm_into(gs[0], val(nb_comb_w_), false, Tensor(), g_cat, false);
+    const float* gcb = static_cast<const float*>(g_cat.data_ptr());
+    check(tmdnet_nbr_fused_bwd_f32(static_cast<int>(N), static_cast<int>(H), static_cast<int>(R), ptr<int32_t>(row_ptr),
+                                   ptr<int32_t>(src), static_cast<int>(E), ptr(xe), static_cast<int>(H), ptr(C),
+                                   ptr<int32_t>(F.pair_row), ptr(F.frags), ptr(F.dscale), F.n_rows, ptr(nimg),
+                                   ptr(nwsc), ptr(nbias), gcb + H, static_cast<int>(2 * H), ptr(gs[2]), ptr(gs[1]),
+                                   TMDNET_ACC_EDGE, st),
+          "tmdnet_nbr_fused_bwd_f32");
+  } else if (nb) {
     Tensor g_cat = at::empty({N, 2 * H}, o);
     gemm_into(gs[0], val(nb_comb_w_), false, Tensor(), g_cat, false);
     Tensor gW = at::empty({E, H}, o);

@@ -110,6 +110,9 @@ SIGNATURES = {
     "tmdnet_nbr_fused_fwd_f32": (I, [I, I, I, P, P, I, P, I, P, P, P, ctypes.c_longlong, P, P, P, P, I, P, P, P]),
     "tmdnet_nbr_fused_bwd_f32": (I, [I, I, I, P, P, I, P, I, P, P, P, P, ctypes.c_longlong, P, P, P, P, I, P, P, I,
                                      P]),
+    "tmdnet_eq_head_x3_f32": (I, [I, I, P, P, P, P, P, P, P, P, P]),
+    "tmdnet_eq_head_x3_pieces_bytes": (SZ, [I]),
+    "tmdnet_eq_head_x3_split_f32": (I, [I, P, P, P]),
     "tmdnet_fep_frags_bytes": (SZ, [ctypes.c_longlong, I]),
     "tmdnet_fep_frags_f32": (I, [ctypes.c_longlong, I, P, P, P, D, D, I, P, P, P]),
     "tmdnet_proj_f32": (I, [I, I, I, P, I, P, ctypes.c_longlong, P, P, I, P]),

@@ -2095,6 +2095,40 @@ def _will_run(node):
         return True
 
 
+# the head's forward + Jacobian on the bf16 MFMA over 16-atom tiles (tmdnet_eq_head_x3_f32; fp32, H = 128);
+# TMDNET_HEAD_X3=0: the per-atom VALU kernel (A/B)
+HEAD_X3 = os.environ.get("TMDNET_HEAD_X3", "1") != "0"
+
+
+def _eq_head_x3(lib, x, vec, params, y, jx, jv):
+    """tmdnet_eq_head_x3_split_f32 (the weights' pieces, one launch: they always match the current weights,
+    also inside a captured step) + tmdnet_eq_head_x3_f32.  Returns False outside its envelope."""
+    N, H = x.shape
+    nbytes = int(lib.tmdnet_eq_head_x3_pieces_bytes(H))
+    if not (HEAD_X3 and nbytes and x.dtype == torch.float32 and all(p.is_contiguous() for p in params)
+            and all(p.data_ptr() % 16 == 0 for p in (params[3], params[5], params[9]))):
+        return False
+    st = nat.stream(x.device)
+    buf = torch.empty((nbytes // 2,), dtype=torch.int16, device=x.device)
+    ws = (ctypes.c_void_p * 12)(*[p.data_ptr() for p in params])
+    rc = lib.tmdnet_eq_head_x3_split_f32(H, ws, buf.data_ptr(), st)
+    if rc == GEMM_UNSUPPORTED:
+        return False
+    nat.check(rc, "tmdnet_eq_head_x3_split_f32")
+    O = H // 2
+    nk = [(H + O, H), (H, 2 * H), (H, H), (O, O), (O, 2 * O), (2 * O, O), (O, O), (H, H), (2 * H, H), (H, H + O)]
+    offs, o = [], 0
+    for n, k in nk:
+        offs.append(buf.data_ptr() + 2 * o)
+        o += 3 * n * k
+    pieces = (ctypes.c_void_p * 10)(*offs)
+    vecs = (ctypes.c_void_p * 5)(*[params[i].data_ptr() for i in (3, 5, 9, 10, 11)])
+    rc = lib.tmdnet_eq_head_x3_f32(N, H, nat.ptr(x), nat.ptr(vec), pieces, vecs, nat.ptr(y), nat.ptr(jx),
+                                   nat.ptr(jv), None, st)
+    nat.check(rc, "tmdnet_eq_head_x3_f32")
+    return True
+
+
 class _EqHead(Function):
     """(x, vec, *head params) -> y [N, 1]; the HIP kernel also returns dy/dx, dy/dvec per atom."""
 
@@ -2107,10 +2141,11 @@ class _EqHead(Function):
         want_j = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
         jx = torch.empty_like(x) if want_j else None
         jv = torch.empty_like(vec) if want_j else None
-        ws = (ctypes.c_void_p * 12)(*[p.data_ptr() for p in params])
-        rc = lib.tmdnet_eq_head_fwd(nat.dtype_code(x.dtype), N, H, nat.ptr(x), nat.ptr(vec), ws, nat.ptr(y),
-                                    nat.ptr(jx), nat.ptr(jv), nat.stream(x.device))
-        nat.check(rc, "tmdnet_eq_head_fwd")
+        if not (N and _eq_head_x3(lib, x, vec, params, y, jx, jv)):
+            ws = (ctypes.c_void_p * 12)(*[p.data_ptr() for p in params])
+            rc = lib.tmdnet_eq_head_fwd(nat.dtype_code(x.dtype), N, H, nat.ptr(x), nat.ptr(vec), ws, nat.ptr(y),
+                                        nat.ptr(jx), nat.ptr(jv), nat.stream(x.device))
+            nat.check(rc, "tmdnet_eq_head_fwd")
         ctx.save_for_backward(x, vec, jx, jv, *params)
         return y
 
