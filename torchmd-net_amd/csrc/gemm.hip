@@ -1583,7 +1583,9 @@ extern "C" int tmdnet_gemm_x3_f32(int M, int N, int K, const void* A, int lda, c
                 (const float*)bias, (float*)C};
   hipStream_t st = (hipStream_t)stream;
   // 64-column tiles for wide outputs (the forward mixes, N = 3H..5H), 128 for the narrow input gradients
-  // (N = H: one column tile, A read once); 2 row blocks per wave (128 rows per workgroup)
+  // (N = H: one column tile, A read once); 2 row blocks per wave (128 rows per workgroup).  Wide-form
+  // alternatives measured slower at C5 (us for qkv / o / vec_proj): <2,64,1> 75.6 / 50.0 / 150.7,
+  // <2,64,2> 93.8 / 58.3 / 167.3, <1,64,4> 106.1 / 65.2 / 192.0, <1,64,2> 96.6 / 59.2 / 181.9
   const int bn = (N >= 256 || N <= 64) ? 64 : 128;
   P.nx = (N + bn - 1) / bn;
   P.ny = (M + 127) / 128;
