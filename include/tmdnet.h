@@ -142,6 +142,13 @@ int tmdnet_edge_geom_fwd_rows(int dtype, int n_edges, int num_rbf, int rbf_type,
                               const void* beta, double cutoff_lower, double cutoff_upper, void* rbf,
                               void* cutoff, void* unit, const int32_t* rows, int n_rows, void* rbf_rows,
                               void* stream);
+/* tmdnet_edge_geom_fwd_rows plus d rbf / d r of the same rows into drbf_rows [n_rows][num_rbf] (the ET
+ * force pass's dr-mode operand, formed with the features; replaces a tmdnet_rbf_deriv launch). */
+int tmdnet_edge_geom_fwd_rows2(int dtype, int n_edges, int num_rbf, int rbf_type, const int32_t* src,
+                               const int32_t* dst, const void* deltas, const void* dist, const void* mu,
+                               const void* beta, double cutoff_lower, double cutoff_upper, void* rbf,
+                               void* cutoff, void* unit, const int32_t* rows, int n_rows, void* rbf_rows,
+                               void* drbf_rows, void* stream);
 /* Backward: given grad_rbf [E][R], grad_cutoff [E], grad_unit [E][3] (each nullable) produce
  * grad_dist [E] and grad_deltas [E][3] (both overwritten). */
 /* Second order of tmdnet_edge_geom_bwd (force-matching training; replaces autograd's double
@@ -327,6 +334,32 @@ int tmdnet_ln_bwd_epilogue_w(int dtype, int n_nodes, int hidden, const void* gra
                              const void* o, void* grad_vecp, void* grad_o, void* w_rows, int accumulate,
                              void* stream);
 /* (grad_res2: a second residual term, NULL = none; accumulate != 0: grad_vecp / grad_o are ADDED to.) */
+
+/* The ET layer's node mixes with the epilogue / LayerNorm pass folded in (et_nodemix.hip; fp32, hidden %
+ * 64 == 0, hidden <= 256, 16-byte aligned x_agg / o_w).  Replaces tmdnet_gemm_f32(o_proj) +
+ * tmdnet_et_epilogue_ln_fwd (reference torchmd_et.py:181-184, 278-280, 309-311): o [N][3H] = x_agg o_w^T +
+ * o_b, then x_out, vec_out as tmdnet_et_epilogue_fwd (vecp NULL: first layer, vec unused).  o, x_out and
+ * vec_out are bit-identical to the two-launch form. */
+int tmdnet_et_oproj_epilogue_f32(int n_nodes, int hidden, const void* x_agg, const void* o_w, const void* o_b,
+                                 const void* x, const void* vec, const void* vecp, const void* vec_agg, void* o,
+                                 void* x_out, void* vec_out, void* stream);
+/* LayerNorm(x) (affine, biased variance, rstd = 1/sqrt(var + eps); torchmd_et.py:262) -> xn [N][H], mean
+ * [N], rstd [N], and out [N][n_out] = xn w^T + b (the [q|k|v] Linear, torchmd_et.py:264-266) -- with, when
+ * vec != NULL, vec_out [3N][n_vec_out] = vec [3N][H] vec_w^T (vec_proj, torchmd_et.py:268) in the same
+ * launch.  Replaces the LayerNorm half of tmdnet_et_epilogue_ln_fwd + tmdnet_gemm_f32([q|k|v], vec_proj).
+ * fp32, hidden % 64 == 0, hidden <= 256, 16-byte aligned operands. */
+int tmdnet_et_ln_mix_f32(int n_nodes, int hidden, const void* x, const void* ln_w, const void* ln_b, double eps,
+                         const void* w, const void* b, int n_out, void* out, void* xn, void* mean, void* rstd,
+                         const void* vec, const void* vec_w, int n_vec_out, void* vec_out, void* stream);
+/* The force pass's mirror (et_nodemix.hip; fp32, hidden == 128): the LayerNorm backward of layer l
+ * (tmdnet_ln_bwd_epilogue with grad_res, no weight rows) -> grad_x, the epilogue backward of layer l-1 ->
+ * grad_vecp, grad_o (vecp NULL: layer l-1 is the first, grad_vecp unused), and grad_xa [N][H] = grad_o o_w
+ * (o_w = layer l-1's o_proj weight [3H][H], torchmd_et.py:311) in one launch.  Replaces
+ * tmdnet_ln_bwd_epilogue + tmdnet_gemm_f32(o_proj^T). */
+int tmdnet_et_lnbwd_oproj_f32(int n_nodes, int hidden, const void* grad_xn, const void* x, const void* mean,
+                              const void* rstd, const void* ln_w, const void* grad_res, const void* grad_vec,
+                              const void* vecp, const void* o, const void* o_w, void* grad_x, void* grad_vecp,
+                              void* grad_o, void* grad_xa, void* stream);
 
 /* Second order of the layer tail (force-matching training, et_stack._second_order): layer l's
  * epilogue-backward VJP fused with layer l+1's LayerNorm-backward VJP, one wave per node.

@@ -1139,26 +1139,3 @@ def test_grouped_gemm_matches_torch():
     # outside the envelope (K % 16): not launched
     assert not kernels.gemm_launch([(torch.randn(5, 72, **f), torch.randn(7, 72, **f), True, None,
                                      torch.empty(5, 7, **f), False)])
-
-
-def test_eager_eval_mode_takes_the_one_operator_evaluation():
-    """Eval mode, eager (TorchMD_Net.fused_eval): the whole energy + force evaluation as
-    tmdnet::et_energy_forces (the scripted eval path), equal to the train-mode Python path; fused_eval =
-    False keeps the differentiable Python path in eval mode."""
-    from oracle import model_oracle as O
-    from torchmdnet.models.model import create_model
-    torch.manual_seed(0)
-    m = create_model(yaml_args("equivariant-transformer", embedding_dimension=128, derivative=True)).to(DEV)
-    assert m.fused_eval
-    z, pos, batch = O.qm9_like(32)
-    z, pos, batch = z.to(DEV), pos.float().to(DEV), batch.to(DEV)
-    y0, f0 = m(z, pos.clone(), batch)
-    m.eval()
-    y1, f1 = m(z, pos.clone(), batch)
-    assert y1.grad_fn is None and f1.grad_fn is None  # the operator's outputs (documented)
-    assert float((y1 - y0).abs().max() / y0.abs().max()) < 1e-5
-    assert float((f1 - f0).abs().max() / f0.abs().max()) < 1e-4
-    m.fused_eval = False
-    y2, f2 = m(z, pos.clone(), batch)
-    assert f2.grad_fn is not None
-    assert float((f2 - f0).abs().max() / f0.abs().max()) < 1e-5

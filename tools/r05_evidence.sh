@@ -4,13 +4,15 @@
 # per-probe trace average of the graded kernel, the kernel lists of one C2 / C3 graph replay and of one
 # captured ET training step, the C5 per-kernel breakdown, the C2 PMC passes.
 # Output: gpurun_out/prof_r05/ (copy into profiles/ as r05_*).
-#   bash tools/r05_evidence.sh [skip-tests]
+#   bash tools/r05_evidence.sh part1 [skip-tests]   (tests, bench, bench under rocprof)
+#   bash tools/r05_evidence.sh part2                (graph-step traces, C5 breakdown, training check, C2 PMC)
 set -o pipefail
 root=$(pwd)
 out=$root/gpurun_out/prof_r05
 mkdir -p "$out"
 export TMPDIR=/tmp
-if [ "$1" != "skip-tests" ]; then
+if [ "$1" = "part1" ]; then
+if [ "$2" != "skip-tests" ]; then
   timeout -k 10 1000 python -u -m pytest tests -m gpu --maxfail=10 -q --timeout 300 --timeout-method thread > "$out/gputest.log" 2>&1 || { tail -30 "$out/gputest.log"; exit 1; }
   tail -1 "$out/gputest.log"
 fi
@@ -22,6 +24,9 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/p
 cp "$(find /tmp/prof_stats -name '*kernel_stats.csv' | head -1)" "$out/bench_kernel_stats.csv"
 python3 "$root/tools/roofline_from_trace.py" "$(find /tmp/prof_stats -name '*kernel_trace.csv' | head -1)" > "$out/roofline_from_trace.txt"
 head -5 "$out/roofline_from_trace.txt"
+exit 0
+fi
+cd /tmp && rm -rf /tmp/prof_et /tmp/prof_tn /tmp/prof_train
 timeout -k 10 180 rocprofv3 --kernel-trace --output-format csv -d /tmp/prof_et -o run -- python3 "$root/tools/graph_trace.py" et > /dev/null 2>&1
 python3 "$root/tools/trace_summary.py" "$(find /tmp/prof_et -name '*kernel_trace.csv' | head -1)" > "$out/et_c2_graph_step_kernels.txt"
 timeout -k 10 180 rocprofv3 --kernel-trace --output-format csv -d /tmp/prof_tn -o run -- python3 "$root/tools/graph_trace.py" tn > /dev/null 2>&1

@@ -97,10 +97,11 @@ __device__ __forceinline__ void basis(const Cfg<T>& P, T r, int k, T& f, T& df) 
 }
 
 // rows != NULL: also the features of the edges rows[p] into frows [n_rows][R] (the pair rows the ET
-// projection GEMM reads; replaces a gather of f)
+// projection GEMM reads; replaces a gather of f), and with drows != NULL their r-derivatives into drows
+// (the dr-mode force pass's operand; replaces a tmdnet_rbf_deriv launch after the forward)
 template <typename T>
 __global__ void k_fwd(Cfg<T> P, T* __restrict__ f, T* __restrict__ C, T* __restrict__ u,
-                      const int32_t* __restrict__ rows, int n_rows, T* __restrict__ frows) {
+                      const int32_t* __restrict__ rows, int n_rows, T* __restrict__ frows, T* __restrict__ drows) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long nf = f ? (long long)P.E * P.R : 0;
   if (i < nf) {
@@ -114,6 +115,7 @@ __global__ void k_fwd(Cfg<T> P, T* __restrict__ f, T* __restrict__ C, T* __restr
     T v, dv;
     basis(P, P.r[rows[p]], k, v, dv);
     frows[i] = v;
+    if (drows) drows[i] = dv;
   }
   if (i < P.E) {
     const int e = (int)i;
@@ -373,7 +375,7 @@ using namespace tmd;
 static int geom_fwd(int dtype, int n_edges, int num_rbf, int rbf_type, const int32_t* src, const int32_t* dst,
                     const void* deltas, const void* dist, const void* mu, const void* beta, double cutoff_lower,
                     double cutoff_upper, void* rbf, void* cutoff, void* unit, const int32_t* rows, int n_rows,
-                    void* rbf_rows, void* stream) {
+                    void* rbf_rows, void* drbf_rows, void* stream) {
   if (n_edges <= 0) return kOk;
   hipStream_t st = (hipStream_t)stream;
   long long work = rbf ? (long long)n_edges * num_rbf : n_edges;
@@ -383,11 +385,11 @@ static int geom_fwd(int dtype, int n_edges, int num_rbf, int rbf_type, const int
   if (dtype == TMDNET_F32) {
     auto P = geom::make<float>(n_edges, num_rbf, rbf_type, src, dst, deltas, dist, mu, beta, cutoff_lower, cutoff_upper);
     hipLaunchKernelGGL(geom::k_fwd<float>, g, dim3(tb), 0, st, P, (float*)rbf, (float*)cutoff, (float*)unit, rows,
-                       n_rows, (float*)rbf_rows);
+                       n_rows, (float*)rbf_rows, (float*)drbf_rows);
   } else if (dtype == TMDNET_F64) {
     auto P = geom::make<double>(n_edges, num_rbf, rbf_type, src, dst, deltas, dist, mu, beta, cutoff_lower, cutoff_upper);
     hipLaunchKernelGGL(geom::k_fwd<double>, g, dim3(tb), 0, st, P, (double*)rbf, (double*)cutoff, (double*)unit, rows,
-                       n_rows, (double*)rbf_rows);
+                       n_rows, (double*)rbf_rows, (double*)drbf_rows);
   } else {
     return kUnsupported;
   }
@@ -400,7 +402,7 @@ extern "C" int tmdnet_edge_geom_fwd(int dtype, int n_edges, int num_rbf, int rbf
                                     double cutoff_lower, double cutoff_upper, void* rbf, void* cutoff,
                                     void* unit, void* stream) {
   return geom_fwd(dtype, n_edges, num_rbf, rbf_type, src, dst, deltas, dist, mu, beta, cutoff_lower, cutoff_upper,
-                  rbf, cutoff, unit, nullptr, 0, nullptr, stream);
+                  rbf, cutoff, unit, nullptr, 0, nullptr, nullptr, stream);
 }
 
 extern "C" int tmdnet_edge_geom_fwd_rows(int dtype, int n_edges, int num_rbf, int rbf_type,
@@ -411,7 +413,18 @@ extern "C" int tmdnet_edge_geom_fwd_rows(int dtype, int n_edges, int num_rbf, in
                                          void* stream) {
   if (!rows || n_rows < 0 || (n_rows > 0 && !rbf_rows)) return kBadArgument;
   return geom_fwd(dtype, n_edges, num_rbf, rbf_type, src, dst, deltas, dist, mu, beta, cutoff_lower, cutoff_upper,
-                  rbf, cutoff, unit, rows, n_rows, rbf_rows, stream);
+                  rbf, cutoff, unit, rows, n_rows, rbf_rows, nullptr, stream);
+}
+
+extern "C" int tmdnet_edge_geom_fwd_rows2(int dtype, int n_edges, int num_rbf, int rbf_type,
+                                          const int32_t* src, const int32_t* dst, const void* deltas,
+                                          const void* dist, const void* mu, const void* beta,
+                                          double cutoff_lower, double cutoff_upper, void* rbf, void* cutoff,
+                                          void* unit, const int32_t* rows, int n_rows, void* rbf_rows,
+                                          void* drbf_rows, void* stream) {
+  if (!rows || n_rows < 0 || (n_rows > 0 && (!rbf_rows || !drbf_rows))) return kBadArgument;
+  return geom_fwd(dtype, n_edges, num_rbf, rbf_type, src, dst, deltas, dist, mu, beta, cutoff_lower, cutoff_upper,
+                  rbf, cutoff, unit, rows, n_rows, rbf_rows, drbf_rows, stream);
 }
 
 extern "C" int tmdnet_edge_geom_bwd_multi(int dtype, int n_edges, int num_rbf, int rbf_type,

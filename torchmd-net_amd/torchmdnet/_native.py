@@ -42,6 +42,7 @@ SIGNATURES = {
     "tmdnet_nl_backward_edges": (I, [I, I, P, I, P, P, P, P, P, P]),
     "tmdnet_edge_geom_fwd": (I, [I, I, I, I, P, P, P, P, P, P, D, D, P, P, P, P]),
     "tmdnet_edge_geom_fwd_rows": (I, [I, I, I, I, P, P, P, P, P, P, D, D, P, P, P, P, I, P, P]),
+    "tmdnet_edge_geom_fwd_rows2": (I, [I, I, I, I, P, P, P, P, P, P, D, D, P, P, P, P, I, P, P, P]),
     "tmdnet_edge_geom_bwd": (I, [I, I, I, I, P, P, P, P, P, P, D, D, P, P, P, P, P, P]),
     "tmdnet_edge_geom_bwd_multi": (I, [I, I, I, I, P, P, P, P, P, P, D, D, P, P, P, P, P, P, P, P, P, P]),
     "tmdnet_edge_geom_bwd2": (I, [I, I, I, I, P, P, P, P, P, P, D, D, P, P, P, P, P, P, P, P, P, P, P]),
@@ -63,6 +64,9 @@ SIGNATURES = {
     "tmdnet_et_epilogue_ln_fwd": (I, [I, I, I, P, P, P, P, P, P, P, D, P, P, P, P, P, P]),
     "tmdnet_ln_bwd_epilogue": (I, [I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P]),
     "tmdnet_ln_bwd_epilogue_w": (I, [I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, P]),
+    "tmdnet_et_oproj_epilogue_f32": (I, [I, I] + [P] * 11),
+    "tmdnet_et_ln_mix_f32": (I, [I, I, P, P, P, D, P, P, I, P, P, P, P, P, P, I, P, P]),
+    "tmdnet_et_lnbwd_oproj_f32": (I, [I, I] + [P] * 15),
     "tmdnet_et_adjoint_epi_ln": (I, [I, I, I] + [P] * 21),
     "tmdnet_et_adjoint_epi_ln2": (I, [I, I, I] + [P] * 22),
     "tmdnet_eq_head_fwd": (I, [I, I, I, P, P, P, P, P, P, P]),

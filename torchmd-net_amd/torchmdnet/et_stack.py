@@ -244,6 +244,7 @@ class _Meta:
         self.rbf = None         # (mu, beta, cutoff_lower, cutoff_upper, rbf_type): f = rbf(r) ("dr mode")
         self.out_norm = False   # the model's final LayerNorm fused into the last epilogue (2 trailing params)
         self.f_pairs = None     # f at the pair rows, when the caller produced it with the features
+        self.fdp_pairs = None   # ... and d f / d r there (the dr-mode force pass's operand)
         self.dkv_wp = None      # the bf16 split of dkv_eff[0] (dkv_split), once per forward
         self.fep = False        # the forward runs the fused-projection edge kernel (FEP)
         self.fep_imgs = None    # per layer: its weight image (kernels.fep_split), made by the forward
@@ -325,6 +326,64 @@ def _epi_ln(x, vec, vecp, o, veca, ln_w, ln_b, xn_out=None, vo_out=None):
     return xo, vo, xn, mean, rstd
 
 
+# The forward's node mixes with the epilogue / LayerNorm pass folded in (et_nodemix.hip): per layer
+# tmdnet_et_ln_mix_f32 (LayerNorm + [q|k|v] + vec_proj) and tmdnet_et_oproj_epilogue_f32 (o_proj + the
+# epilogue) instead of [q|k|v]/vec_proj GEMM + o_proj GEMM + epilogue-LayerNorm pass: one launch per layer
+# fewer.  fp32, H % 64 == 0, H <= 256.  TMDNET_ET_NODE_FUSE=0 keeps the three-launch form.
+NODE_FUSE = os.environ.get("TMDNET_ET_NODE_FUSE", "1") != "0"
+
+
+def _node_fuse_ok(x):
+    H = x.shape[1]
+    return NODE_FUSE and x.is_cuda and x.dtype == torch.float32 and H % 64 == 0 and H <= 256
+
+
+def _ln_mix(x, ln_w, ln_b, w, b, vec, vec_w, xn_out):
+    """tmdnet_et_ln_mix_f32: (qkv, vecp, xn, mean, rstd) with xn written into ``xn_out``."""
+    lib = nat.load()
+    N, H = x.shape
+    qkv = torch.empty((N, w.shape[0]), dtype=x.dtype, device=x.device)
+    mean = torch.empty((N, 1), dtype=x.dtype, device=x.device)
+    rstd = torch.empty((N, 1), dtype=x.dtype, device=x.device)
+    vecp = torch.empty((N, 3, vec_w.shape[0]), dtype=x.dtype, device=x.device) if vec is not None else None
+    w, ln_w, ln_b = w.contiguous(), ln_w.contiguous(), ln_b.contiguous()
+    vec_w = vec_w.contiguous() if vec is not None else None
+    rc = lib.tmdnet_et_ln_mix_f32(N, H, nat.ptr(x), nat.ptr(ln_w), nat.ptr(ln_b), _EPS, nat.ptr(w), nat.ptr(b),
+                                  w.shape[0], nat.ptr(qkv), nat.ptr(xn_out), nat.ptr(mean), nat.ptr(rstd),
+                                  nat.ptr(vec), nat.ptr(vec_w), vec_w.shape[0] if vec is not None else 0,
+                                  nat.ptr(vecp), nat.stream(x.device))
+    nat.check(rc, "tmdnet_et_ln_mix_f32")
+    return qkv, vecp, xn_out, mean, rstd
+
+
+def _oproj_epi(xa, o_w, o_b, x, vec, vecp, veca, vo_out):
+    """tmdnet_et_oproj_epilogue_f32: (o, x_out, vec_out) with vec_out written into ``vo_out``."""
+    lib = nat.load()
+    N, H = x.shape
+    o = torch.empty((N, o_w.shape[0]), dtype=x.dtype, device=x.device)
+    xo = torch.empty_like(x)
+    o_w = o_w.contiguous()
+    rc = lib.tmdnet_et_oproj_epilogue_f32(N, H, nat.ptr(xa), nat.ptr(o_w), nat.ptr(o_b), nat.ptr(x), nat.ptr(vec),
+                                          nat.ptr(vecp), nat.ptr(veca), nat.ptr(o), nat.ptr(xo), nat.ptr(vo_out),
+                                          nat.stream(x.device))
+    nat.check(rc, "tmdnet_et_oproj_epilogue_f32")
+    return o, xo, vo_out
+
+
+def _ln_bwd_oproj(g_xn, x, mean, rstd, ln_w, g_res, g_vec, vecp, o, o_w, g_vecp, g_o):
+    """tmdnet_et_lnbwd_oproj_f32: (g_x, g_xa) -- the LayerNorm backward of a layer (+ residual g_res), the
+    previous layer's epilogue backward into g_vecp / g_o, and that layer's g_xa = g_o W_o (H = 128)."""
+    lib = nat.load()
+    N, H = x.shape
+    gx = torch.empty_like(x)
+    gxa = torch.empty_like(x)
+    rc = lib.tmdnet_et_lnbwd_oproj_f32(N, H, nat.ptr(g_xn), nat.ptr(x), nat.ptr(mean), nat.ptr(rstd), nat.ptr(ln_w),
+                                       nat.ptr(g_res), nat.ptr(g_vec), nat.ptr(vecp), nat.ptr(o), nat.ptr(o_w),
+                                       nat.ptr(gx), nat.ptr(g_vecp), nat.ptr(g_o), nat.ptr(gxa), nat.stream(x.device))
+    nat.check(rc, "tmdnet_et_lnbwd_oproj_f32")
+    return gx, gxa
+
+
 def _ln_bwd_epi(g_xn, x, mean, rstd, ln_w, g_res, g_vec, vecp, o, g_vecp, g_o, wrows=None, g_res2=None, acc=False):
     """tmdnet_ln_bwd_epilogue_w: g_x = g_res + LayerNorm backward (g_res None: no residual), then the
     previous layer's epilogue backward into g_vecp / g_o (o None: skipped); ``wrows`` (optional
@@ -386,20 +445,26 @@ def _forward_layers(meta, x, f, C, u, params, r=None, want_bwd=False):
     xn_all, xa_all = torch.empty((L, N, H), **od), torch.empty((L, N, H), **od)
     vec_all = torch.empty((L, N, 3, H), **od)
     meta.stk = (xn_all, xa_all, vec_all)
-    # layer l's LayerNorm is computed by layer l-1's epilogue kernel (layer 0: LayerNorm alone)
-    _, _, xn, mean, rstd = _epi_ln(x, None, None, None, None, layers[0][0], layers[0][1], xn_out=xn_all[0])
+    # layer l's LayerNorm is computed by layer l-1's epilogue kernel (layer 0: LayerNorm alone) -- or, in the
+    # node-fused form, by layer l's [q|k|v] mix (tmdnet_et_ln_mix_f32)
+    nf = _node_fuse_ok(x)
+    if not nf:
+        _, _, xn, mean, rstd = _epi_ln(x, None, None, None, None, layers[0][0], layers[0][1], xn_out=xn_all[0])
     for l, p in enumerate(layers):
         vec_w, o_w, o_b = p[8], p[9], p[10]
         qkv_w, qkv_b = meta.qkv_eff[l]
         dkv_w, dkv_b = meta.dkv_layer(l)
-        # [q|k|v] and vec_proj in ONE launch (tmdnet_gemm_f32; library GEMMs outside its envelope)
-        qkv = torch.empty((N, qkv_w.shape[0]), dtype=x.dtype, device=x.device)
-        probs = [(xn, qkv_w, True, qkv_b, qkv, False)]
-        vecp = None
-        if vec is not None:
-            vecp = torch.empty((N, 3, 3 * H), dtype=x.dtype, device=x.device)
-            probs.append((vec.view(3 * N, H), vec_w, True, None, vecp.view(3 * N, 3 * H), False))
-        kernels.gemm_group(probs)
+        if nf:  # LayerNorm + [q|k|v] + vec_proj, one launch
+            qkv, vecp, xn, mean, rstd = _ln_mix(x, p[0], p[1], qkv_w, qkv_b, vec, vec_w, xn_all[l])
+        else:
+            # [q|k|v] and vec_proj in ONE launch (tmdnet_gemm_f32; library GEMMs outside its envelope)
+            qkv = torch.empty((N, qkv_w.shape[0]), dtype=x.dtype, device=x.device)
+            probs = [(xn, qkv_w, True, qkv_b, qkv, False)]
+            vecp = None
+            if vec is not None:
+                vecp = torch.empty((N, 3, 3 * H), dtype=x.dtype, device=x.device)
+                probs.append((vec.view(3 * N, H), vec_w, True, None, vecp.view(3 * N, 3 * H), False))
+            kernels.gemm_group(probs)
         xa = xa_all[l]
         veca = torch.empty((N, 3, H), dtype=x.dtype, device=x.device)
         if fep:  # projection fused into the edge kernel (no rows: a backward that needs them forms them)
@@ -425,6 +490,11 @@ def _forward_layers(meta, x, f, C, u, params, r=None, want_bwd=False):
             pv = pkv[:, H * int(meta.hk):] if meta.hv else None
             kernels.et_message_fwd_launch(qkv[:, :H], qkv[:, H:2 * H], qkv[:, 2 * H:], vec, pk, pv, C, u,
                                           meta.graph, meta.heads, xa, veca, meta.flags, meta.pk_rows)
+        if nf and l + 1 < len(layers):  # o_proj + the epilogue, one launch (the next LayerNorm: its mix)
+            o, x_next, vec_next = _oproj_epi(xa, o_w, o_b, x, vec, vecp, veca, vec_all[l + 1])
+            acts.append((x, vec, xn, mean, rstd, qkv, vecp, pkv, xa, o))
+            x, vec = x_next, vec_next
+            continue
         o = torch.empty((N, o_w.shape[0]), dtype=x.dtype, device=x.device)
         kernels.gemm_group([(xa, o_w, True, o_b, o, False)])
         acts.append((x, vec, xn, mean, rstd, qkv, vecp, pkv, xa, o))
@@ -489,7 +559,10 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws, r=None, dr=Fa
         assert has_e and not any(need_ws) and meta.rbf is not None
         g_r = zbuf[4 * E:]
         if not fused:
-            fdp = kernels.rbf_deriv(r, *meta.rbf, rows=meta.pairs[1] if meta.pairs is not None else None)
+            if meta.fdp_pairs is not None and meta.pairs is not None:
+                fdp = meta.fdp_pairs
+            else:
+                fdp = kernels.rbf_deriv(r, *meta.rbf, rows=meta.pairs[1] if meta.pairs is not None else None)
             dpkv_all = meta.dkv_proj(fdp, bias=False) if meta.batched else None
     # dr mode recorded (the create_graph force pass): g_r in-kernel AND the projection gradient kept
     # padding rows of a static-capacity list are zeroed by the kernel: no memset needed
@@ -517,6 +590,11 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws, r=None, dr=Fa
     layers = meta.split(params)
     g_params = [None] * len(params)
     epi_done = False  # this layer's epilogue backward already ran (fused into the next layer's LN bwd)
+    # the node-fused backward (tmdnet_et_lnbwd_oproj_f32): each LayerNorm backward also runs the layer
+    # below's epilogue backward and its o_proj input gradient g_xa (no injections, no weight rows)
+    bwd_nf = (NODE_FUSE and not acc and not inj and not any(need_ws[:meta.n_layers + 1]) and gX is not None
+              and gX.is_cuda and gX.dtype == torch.float32 and H == 128)
+    g_xa_pre = None  # the next (lower) layer's g_xa, formed by the fused kernel
     x_top = inj.get("x_top")  # a cotangent of the last epilogue's output (the out_norm input)
     if meta.out_norm and not seed_pre_norm:  # gX is the gradient of LN(x_out): back through out_norm first
         x_pre, mean_o, rstd_o = acts[meta.n_layers]
@@ -527,6 +605,10 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws, r=None, dr=Fa
             g_params[-2:] = list(kernels.layer_norm_wgrad(g_y, x_pre, mean_o, rstd_o))
         elif x_top is not None:  # LayerNorm backward + the injected cotangent (epilogue in the loop)
             gX = _ln_bwd_epi(gX, x_pre, mean_o, rstd_o, params[-2], x_top, None, None, None, None, None)
+        elif bwd_nf and gV is not None:  # ... and the last layer's o_proj input gradient, one kernel
+            gX, g_xa_pre = _ln_bwd_oproj(gX, x_pre, mean_o, rstd_o, params[-2], None, gV, last[6], last[9],
+                                         layers[L - 1][9], g_vecp_all[L - 1], g_o_all[L - 1])
+            epi_done = True
         else:  # LayerNorm backward + the last layer's epilogue backward, one kernel
             gX = _ln_bwd_epi(gX, x_pre, mean_o, rstd_o, params[-2], None, gV, last[6], last[9], g_vecp_all[L - 1],
                              g_o_all[L - 1])
@@ -560,8 +642,11 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws, r=None, dr=Fa
             g_o.add_(injected("o", l))
             if vecp is not None:
                 g_vecp.add_(injected("vecp", l))
-        g_xa = torch.empty((N, H), **o)
-        kernels.gemm_group([(g_o, o_w, False, None, g_xa, False)])
+        if g_xa_pre is not None:
+            g_xa, g_xa_pre = g_xa_pre, None
+        else:
+            g_xa = torch.empty((N, H), **o)
+            kernels.gemm_group([(g_o, o_w, False, None, g_xa, False)])
         g_vec_in = gvec_bufs[l % 2] if vec is not None else None
         if acc and vec is not None:  # the injected vec cotangent's buffer takes the gradient
             g_vec_in = injected("vec", l) if injected("vec", l) is not None else torch.zeros((N, 3, H), **o)
@@ -606,10 +691,14 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws, r=None, dr=Fa
         # LayerNorm backward + residual (+ the injected x cotangent) + the previous layer's epilogue
         # backward, one kernel (with the row terms of the LayerNorm weight gradient when weights are wanted)
         prev = acts[l - 1] if l > 0 else None
-        g_x = _ln_bwd_epi(g_xn, x, mean, rstd, ln_w, gX, g_vec_in,
-                          prev[6] if prev else None, prev[9] if prev else None,
-                          g_vecp_all[l - 1] if prev else None, g_o_all[l - 1] if prev else None,
-                          wrows=ln_rows[l] if any_w else None, g_res2=injected("x", l), acc=acc)
+        if bwd_nf and prev is not None:
+            g_x, g_xa_pre = _ln_bwd_oproj(g_xn, x, mean, rstd, ln_w, gX, g_vec_in, prev[6], prev[9], layers[l - 1][9],
+                                          g_vecp_all[l - 1], g_o_all[l - 1])
+        else:
+            g_x = _ln_bwd_epi(g_xn, x, mean, rstd, ln_w, gX, g_vec_in,
+                              prev[6] if prev else None, prev[9] if prev else None,
+                              g_vecp_all[l - 1] if prev else None, g_o_all[l - 1] if prev else None,
+                              wrows=ln_rows[l] if any_w else None, g_res2=injected("x", l), acc=acc)
         epi_done = prev is not None
         if need_w and has_e and not (meta.batched or rec):
             base = l * meta.np
@@ -1322,7 +1411,7 @@ class _ETStackBwd(Function):
         return (None,) * 7 + tuple(res)
 
 
-def et_stack(layers, x, graph, f, C, u, rbf=None, out_norm=None, f_pairs=None):
+def et_stack(layers, x, graph, f, C, u, rbf=None, out_norm=None, f_pairs=None, fdp_pairs=None):
     """Run ``layers`` (EquivariantMultiHeadAttention modules) as one node.  Returns (x, vec) after
     the last residual update (reference torchmd_et.py:180-184).
 
@@ -1361,6 +1450,8 @@ def et_stack(layers, x, graph, f, C, u, rbf=None, out_norm=None, f_pairs=None):
         meta.pk_rows = meta.pairs[0]
         if f_pairs is not None and f_pairs.shape[0] == meta.pairs[1].shape[0]:
             meta.f_pairs = f_pairs.detach()
+            if fdp_pairs is not None and fdp_pairs.shape == f_pairs.shape:
+                meta.fdp_pairs = fdp_pairs.detach()
     if out_norm is not None:
         if not (out_norm.elementwise_affine and tuple(out_norm.normalized_shape) == (H,) and out_norm.eps == _EPS):
             raise ValueError("et_stack: out_norm must be an affine nn.LayerNorm(H) with eps 1e-5")

@@ -465,10 +465,14 @@ class _EdgeGeom(Function):
         u = torch.empty((E, 3), dtype=dist.dtype, device=dist.device) if want[2] else None
         args = (nat.dtype_code(dist.dtype), E, R, rbf_type, nat.ptr(graph.src), nat.ptr(graph.dst), nat.ptr(deltas),
                 nat.ptr(dist), nat.ptr(mu), nat.ptr(beta), float(cl), float(cu), nat.ptr(f), nat.ptr(C), nat.ptr(u))
-        if rows_out is not None:  # also f at rows (written in place, no autograd: a forward-only copy)
-            rows, frows = rows_out
-            rc = lib.tmdnet_edge_geom_fwd_rows(*args, nat.ptr(rows), rows.shape[0], nat.ptr(frows),
-                                               nat.stream(dist.device))
+        if rows_out is not None:  # also f (and df/dr) at rows (written in place, no autograd: forward-only)
+            rows, frows, drows = rows_out
+            if drows is not None:
+                rc = lib.tmdnet_edge_geom_fwd_rows2(*args, nat.ptr(rows), rows.shape[0], nat.ptr(frows),
+                                                    nat.ptr(drows), nat.stream(dist.device))
+            else:
+                rc = lib.tmdnet_edge_geom_fwd_rows(*args, nat.ptr(rows), rows.shape[0], nat.ptr(frows),
+                                                   nat.stream(dist.device))
         else:
             rc = lib.tmdnet_edge_geom_fwd(*args, nat.stream(dist.device))
         nat.check(rc, "tmdnet_edge_geom_fwd")
@@ -617,16 +621,18 @@ def rbf_composite(r, mu, beta, cl, cu, rbf_type):
 
 
 def edge_geometry(graph, mu, beta, cutoff_lower, cutoff_upper, rbf_type, want=(True, True, True), rows=None,
-                  fan=(1, 1)):
+                  fan=(1, 1), drows=False):
     """(rbf [E,R], cutoff [E], unit vectors [E,3]) of the graph's edges, fused (one HIP kernel).
     ``rows`` (int32 [P]): also returns the rbf rows of those edges [P,R] from the same launch (a
-    forward-only tensor: gradients flow through the per-edge rbf), as a fourth value.
+    forward-only tensor: gradients flow through the per-edge rbf), as a fourth value -- and with
+    ``drows``, their r-derivatives [P,R] as a fifth (the dr-mode force pass's operand).
     ``fan`` = (k_f, k_c), each <= 3: returns ([rbf aliases] * k_f, [cutoff aliases] * k_c, unit) instead --
     one alias per consumer, whose gradients the backward kernel sums (no autograd add launches)."""
     rows_out = None
     if rows is not None:
-        rows_out = (rows, torch.empty((rows.shape[0], mu.shape[0]), dtype=graph.distances.dtype,
-                                      device=graph.distances.device))
+        mk = lambda: torch.empty((rows.shape[0], mu.shape[0]), dtype=graph.distances.dtype,  # noqa: E731
+                                 device=graph.distances.device)
+        rows_out = (rows, mk(), mk() if drows else None)
     fan = (max(1, min(3, int(fan[0]))), max(1, min(3, int(fan[1]))))
     if fan != (1, 1) and not (want[0] and want[1]):
         raise ValueError("edge_geometry: fan-out needs the rbf and cutoff outputs")
@@ -637,9 +643,12 @@ def edge_geometry(graph, mu, beta, cutoff_lower, cutoff_upper, rbf_type, want=(T
         extra = out[3:]
         fs = [f] + list(extra[:fan[0] - 1])
         Cs = [C] + list(extra[fan[0] - 1:])
-        return (fs, Cs, u) if rows is None else (fs, Cs, u, rows_out[1])
-    out = tuple(out[:3])
-    return out if rows is None else out + (rows_out[1],)
+        res = (fs, Cs, u)
+    else:
+        res = tuple(out[:3])
+    if rows is None:
+        return res
+    return res + (rows_out[1],) + ((rows_out[2],) if drows else ())
 
 
 # ----------------------------------------------------------------------------- ET message

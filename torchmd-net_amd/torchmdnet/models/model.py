@@ -207,16 +207,6 @@ class TorchMD_Net(nn.Module):
             pos.requires_grad_(True)
         if torch.jit.is_scripting():
             return self._forward_script(z, pos, batch, q, s, extra_args)
-        if (self.fused_eval and not self.training and pos.is_cuda and pos.dtype == torch.float32
-                and not torch.cuda.is_current_stream_capturing()):
-            # eval mode, eager: the scripted path's one-operator evaluation (tmdnet::et_energy_forces: the
-            # launches issued from C++, ~2 ms of Python orchestration per C2 evaluation gone); as there, the
-            # outputs are not differentiable -- set ``fused_eval = False`` (or stay in train mode) to
-            # differentiate the forces.  Not under HIP-graph capture (the operator reads two counts back)
-            from .. import _native
-            _native.load_torch_ops()
-            return self.representation_model.fused_energy_forces(z, pos, batch, self.output_model.head_params(),
-                                                                 self.std, self.mean)
         x, v, z, pos, batch = self.representation_model(z, pos, batch, q=q, s=s)
         fused = None
         if self.prior_model is None:  # the head's tail, x * std, reduce and + mean fused (Scalar)

@@ -210,7 +210,7 @@ class TorchMD_ET(nn.Module):
         else:
             x = self.embedding(z)
         graph = self.distance.graph(pos, batch)
-        f_pairs = None
+        f_pairs = fdp_pairs = None
         ne_fused = None
         edge_attr_s = C_s = None  # the layer stack's aliases of the rbf / cutoff rows
         de = self.distance_expansion
@@ -222,7 +222,9 @@ class TorchMD_ET(nn.Module):
         else:
             pairs = getattr(graph, "_pairs", None)  # numbered by the neighbour build (sorted rows)
             stack = self.fused_stack and len(self.attention_layers) > 0
-            rows = pairs[1] if (pairs is not None and stack) else None
+            # (no pair rows where the stack forms the projection in-kernel: at C5 they are 350 MB unread)
+            fep_scale = graph.n_edges >= et_stack_mod.FEP_MIN_EDGES and et_stack_mod.FEP not in ("0", "off")
+            rows = pairs[1] if (pairs is not None and stack and not fep_scale) else None
             ne = self.neighbor_embedding
             if (ne is not None and z.is_cuda and NE_FUSED and graph.n_edges >= et_stack_mod.FEP_MIN_EDGES
                     and et_stack_mod.FEP not in ("0", "off")
@@ -237,10 +239,13 @@ class TorchMD_ET(nn.Module):
             fan = (1, 1)
             if stack and ne is not None:
                 fan = (1, 2) if ne_fused is not None else (2, 2)
+            # a force pass to follow (pos differentiated): the pair rows' d rbf / d r from the same launch
+            drows = rows is not None and pos.requires_grad and torch.is_grad_enabled()
             geo = kernels.edge_geometry(graph, *de.kernel_params(), self.cutoff_lower, self.cutoff_upper,
-                                        de.rbf_type, rows=rows, fan=fan)
+                                        de.rbf_type, rows=rows, fan=fan, drows=drows)
             edge_attr, C, d_ij = geo[:3]
             f_pairs = geo[3] if rows is not None else None
+            fdp_pairs = geo[4] if drows else None
             if fan == (2, 2):
                 (edge_attr, edge_attr_s), (C, C_s) = edge_attr, C
             elif fan == (1, 2):
@@ -266,7 +271,7 @@ class TorchMD_ET(nn.Module):
             on = self.out_norm
             fuse_norm = on.elementwise_affine and on.eps == 1e-5
             x, vec = et_stack(self.attention_layers, x, graph, edge_attr_s, C_s, d_ij, rbf=rbf,
-                              out_norm=on if fuse_norm else None, f_pairs=f_pairs)
+                              out_norm=on if fuse_norm else None, f_pairs=f_pairs, fdp_pairs=fdp_pairs)
             return (x if fuse_norm else on(x)), vec
         vec = torch.zeros(x.size(0), 3, x.size(1), device=x.device, dtype=x.dtype)
         for attn in self.attention_layers:
