@@ -20,7 +20,7 @@ timeout -k 10 900 python3 bench.py > "$out/bench.json" 2> "$out/bench.err" || { 
 python3 -c "import json;d=json.load(open('$out/bench.json'));s=d['secondary'];r=d['roofline'];print('C2',d['ms_per_step'],d['value'],'roof',r['frac'],r.get('traffic'),'train',s['et_train_step']['graphed']['ms_per_step'],'tn_train',s['tn_train_step_c3'],'C5',s['et_water_box_c5']['ms_per_step'],'C5scr',s['et_scripted_c5'].get('ms_per_step'),'C3',s['tensornet_c3']['ms_per_step'],'scr',s['et_scripted_c2']['ms_per_step'],'cpu',d['cpu_baseline']['value'])"
 cd /tmp && rm -rf /tmp/prof_stats /tmp/prof_et /tmp/prof_tn /tmp/prof_train
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/prof_stats -o run -- \
-  python3 "$root/bench.py" --no-cpu-baseline --no-pmc > "$out/bench_under_rocprof.json" 2> "$out/rocprof.err" || { echo "rocprof bench failed"; tail -5 "$out/rocprof.err"; exit 1; }
+  python3 "$root/bench.py" --no-cpu-baseline --no-pmc --no-secondary > "$out/bench_under_rocprof.json" 2> "$out/rocprof.err" || { echo "rocprof bench failed"; tail -5 "$out/rocprof.err"; exit 1; }
 cp "$(find /tmp/prof_stats -name '*kernel_stats.csv' | head -1)" "$out/bench_kernel_stats.csv"
 python3 "$root/tools/roofline_from_trace.py" "$(find /tmp/prof_stats -name '*kernel_trace.csv' | head -1)" > "$out/roofline_from_trace.txt"
 head -5 "$out/roofline_from_trace.txt"

@@ -1295,6 +1295,50 @@ std::pair<Tensor, Tensor> stack_composite(const Tensor& x_in, const Tensor& dist
   return {x, vec};
 }
 
+// The node-fused layer mixes (et_nodemix.hip; et_stack.NODE_FUSE): LayerNorm + [q|k|v] + vec_proj, o_proj +
+// the epilogue, and in the force pass the LayerNorm / epilogue backward + the o_proj input gradient, each one
+// launch.  Used in the regime of the small grouped GEMM (3N <= 16384 rows; the x3 GEMMs above) at H = 128.
+bool node_fuse_ok(int64_t N, int64_t H) { return H == 128 && N > 0 && 3 * N <= 16384; }
+
+void ln_mix(const Tensor& x, const Tensor& ln_w, const Tensor& ln_b, const Tensor& w, const Tensor& b,
+            const Tensor& vec, const Tensor& vec_w, const Tensor& qkv, Tensor* vecp, Tensor* xn, Tensor* mean,
+            Tensor* rstd) {
+  const int64_t N = x.size(0), H = x.size(1);
+  auto o = opts(x);
+  *xn = at::empty({N, H}, o);
+  *mean = at::empty({N, 1}, o);
+  *rstd = at::empty({N, 1}, o);
+  *vecp = vec.defined() ? at::empty({N, 3, vec_w.size(0)}, o) : Tensor();
+  check(tmdnet_et_ln_mix_f32(static_cast<int>(N), static_cast<int>(H), ptr(x), ptr(ln_w), ptr(ln_b), kLnEps, ptr(w),
+                             ptr(b), static_cast<int>(w.size(0)), ptr(qkv), ptr(*xn), ptr(*mean), ptr(*rstd), ptr(vec),
+                             vec.defined() ? ptr(vec_w) : nullptr, vec.defined() ? static_cast<int>(vec_w.size(0)) : 0,
+                             ptr(*vecp), stream_of(x)),
+        "tmdnet_et_ln_mix_f32");
+}
+
+void oproj_epi(const Tensor& xa, const Tensor& o_w, const Tensor& o_b, const Tensor& x, const Tensor& vec,
+               const Tensor& vecp, const Tensor& veca, const Tensor& oo, Tensor* xo, Tensor* vo) {
+  const int64_t N = x.size(0), H = x.size(1);
+  *xo = at::empty({N, H}, opts(x));
+  *vo = at::empty({N, 3, H}, opts(x));
+  check(tmdnet_et_oproj_epilogue_f32(static_cast<int>(N), static_cast<int>(H), ptr(xa), ptr(o_w), ptr(o_b), ptr(x),
+                                     ptr(vec), ptr(vecp), ptr(veca), ptr(oo), ptr(*xo), ptr(*vo), stream_of(x)),
+        "tmdnet_et_oproj_epilogue_f32");
+}
+
+// returns g_x; g_xa (layer l-1's o_proj input gradient) into *g_xa
+Tensor lnbwd_oproj(const Tensor& g_xn, const Tensor& x, const Tensor& mean, const Tensor& rstd, const Tensor& ln_w,
+                   const Tensor& g_res, const Tensor& g_vec, const Tensor& vecp, const Tensor& oo, const Tensor& o_w,
+                   const Tensor& g_vecp, const Tensor& g_o, Tensor* g_xa) {
+  Tensor gx = at::empty_like(x);
+  *g_xa = at::empty_like(x);
+  check(tmdnet_et_lnbwd_oproj_f32(static_cast<int>(x.size(0)), static_cast<int>(x.size(1)), ptr(g_xn), ptr(x),
+                                  ptr(mean), ptr(rstd), ptr(ln_w), ptr(g_res), ptr(g_vec), ptr(vecp), ptr(oo), ptr(o_w),
+                                  ptr(gx), ptr(g_vecp), ptr(g_o), ptr(*g_xa), stream_of(x)),
+        "tmdnet_et_lnbwd_oproj_f32");
+  return gx;
+}
+
 // The fast first-order backward of a force evaluation (et_stack._backward_layers with dr=True):
 // returns (g_x, g_dist, g_C, g_u).
 variable_list stack_backward_dr(const StackActs& A, Tensor gX, Tensor gV, const Tensor& dist, const Tensor& C,
@@ -1328,7 +1372,13 @@ variable_list stack_backward_dr(const StackActs& A, Tensor gX, Tensor gV, const 
     if (A.vec[l].defined()) g_vecp[l] = at::empty({N, 3, 3 * H}, o);
   }
   bool epi_done = false;
-  if (c.out_norm) {  // back through out_norm and the last layer's epilogue in one kernel
+  const bool nf = node_fuse_ok(N, H);
+  Tensor g_xa_pre;  // the next (lower) layer's g_xa, formed by the node-fused LayerNorm backward
+  if (c.out_norm && nf) {  // back through out_norm, the last layer's epilogue and its o_proj^T in one kernel
+    gX = lnbwd_oproj(gX, A.x_pre, A.mean_o, A.rstd_o, P[P.size() - 2], Tensor(), gV, A.vecp[L - 1], A.o[L - 1],
+                     P[(L - 1) * np + 9], g_vecp[L - 1], g_o[L - 1], &g_xa_pre);
+    epi_done = true;
+  } else if (c.out_norm) {  // back through out_norm and the last layer's epilogue in one kernel
     Tensor g = at::empty_like(gX);
     const Tensor& on_w = P[P.size() - 2];
     check(tmdnet_ln_bwd_epilogue_w(dcode(gX), static_cast<int>(N), static_cast<int>(H), ptr(gX), ptr(A.x_pre),
@@ -1345,8 +1395,12 @@ variable_list stack_backward_dr(const StackActs& A, Tensor gX, Tensor gV, const 
       check(tmdnet_et_epilogue_bwd_acc(dcode(gX), static_cast<int>(N), static_cast<int>(H), ptr(gX), ptr(gV),
                                        ptr(A.vecp[l]), ptr(A.o[l]), ptr(g_vecp[l]), ptr(g_o[l]), 0, stream_of(gX)),
             "tmdnet_et_epilogue_bwd_acc");
-    Tensor g_xa = at::empty({N, H}, o);
-    gemm_into(g_o[l], p[9], false, Tensor(), g_xa, false);
+    Tensor g_xa = g_xa_pre;
+    g_xa_pre = Tensor();
+    if (!g_xa.defined()) {
+      g_xa = at::empty({N, H}, o);
+      gemm_into(g_o[l], p[9], false, Tensor(), g_xa, false);
+    }
     const bool hv = A.vec[l].defined();
     Tensor g_vec_in = hv ? at::empty({N, 3, H}, o) : Tensor();
     Tensor g_qkv = at::empty({N, 5 * H}, o);
@@ -1379,13 +1433,19 @@ variable_list stack_backward_dr(const StackActs& A, Tensor gX, Tensor gV, const 
     gemm_into(g_qkv, A.pk->qkv_w[l], false, Tensor(), g_xn, false);
     if (hv) gemm_into(g_vecp[l].view({3 * N, 3 * H}), p[8], false, Tensor(), g_vec_in.view({3 * N, H}), true);
     const bool prev = l > 0;
-    Tensor g_x = at::empty_like(g_xn);
-    check(tmdnet_ln_bwd_epilogue_w(dcode(gX), static_cast<int>(N), static_cast<int>(H), ptr(g_xn), ptr(A.x[l]),
-                                   ptr(A.mean[l]), ptr(A.rstd[l]), ptr(p[0]), ptr(gX), nullptr, ptr(g_x),
-                                   ptr(g_vec_in), prev ? ptr(A.vecp[l - 1]) : nullptr, prev ? ptr(A.o[l - 1]) : nullptr,
-                                   prev ? ptr(g_vecp[l - 1]) : nullptr, prev ? ptr(g_o[l - 1]) : nullptr, nullptr, 0,
-                                   stream_of(gX)),
-          "tmdnet_ln_bwd_epilogue_w");
+    Tensor g_x;
+    if (nf && prev) {
+      g_x = lnbwd_oproj(g_xn, A.x[l], A.mean[l], A.rstd[l], p[0], gX, g_vec_in, A.vecp[l - 1], A.o[l - 1],
+                        P[(l - 1) * np + 9], g_vecp[l - 1], g_o[l - 1], &g_xa_pre);
+    } else {
+      g_x = at::empty_like(g_xn);
+      check(tmdnet_ln_bwd_epilogue_w(dcode(gX), static_cast<int>(N), static_cast<int>(H), ptr(g_xn), ptr(A.x[l]),
+                                     ptr(A.mean[l]), ptr(A.rstd[l]), ptr(p[0]), ptr(gX), nullptr, ptr(g_x),
+                                     ptr(g_vec_in), prev ? ptr(A.vecp[l - 1]) : nullptr,
+                                     prev ? ptr(A.o[l - 1]) : nullptr, prev ? ptr(g_vecp[l - 1]) : nullptr,
+                                     prev ? ptr(g_o[l - 1]) : nullptr, nullptr, 0, stream_of(gX)),
+            "tmdnet_ln_bwd_epilogue_w");
+    }
     epi_done = prev;
     gX = g_x;
     gV = g_vec_in;
@@ -1524,14 +1584,19 @@ std::pair<Tensor, Tensor> stack_forward(const Tensor& x_in, const Tensor& f_in, 
             "tmdnet_et_epilogue_ln_fwd");
     };
     Tensor vec, xn, mean, rstd, unused0, unused1;
-    epi_ln(x, Tensor(), Tensor(), Tensor(), Tensor(), P[0], P[1], &unused0, &unused1, &xn, &mean, &rstd);
+    const bool nf = node_fuse_ok(N, H);
+    if (!nf) epi_ln(x, Tensor(), Tensor(), Tensor(), Tensor(), P[0], P[1], &unused0, &unused1, &xn, &mean, &rstd);
     for (int64_t l = 0; l < L; ++l) {
       const Tensor* p = P.data() + l * np;
       Tensor qkv = at::empty({N, 5 * H}, o), vecp;
-      gemm_into(xn, A->pk->qkv_w[l], true, A->pk->qkv_b[l], qkv, false);
-      if (vec.defined()) {
-        vecp = at::empty({N, 3, 3 * H}, o);
-        gemm_into(vec.view({3 * N, H}), p[8], true, Tensor(), vecp.view({3 * N, 3 * H}), false);
+      if (nf) {  // LayerNorm + [q|k|v] + vec_proj in one launch
+        ln_mix(x, p[0], p[1], A->pk->qkv_w[l], A->pk->qkv_b[l], vec, p[8], qkv, &vecp, &xn, &mean, &rstd);
+      } else {
+        gemm_into(xn, A->pk->qkv_w[l], true, A->pk->qkv_b[l], qkv, false);
+        if (vec.defined()) {
+          vecp = at::empty({N, 3, 3 * H}, o);
+          gemm_into(vec.view({3 * N, H}), p[8], true, Tensor(), vecp.view({3 * N, 3 * H}), false);
+        }
       }
       Tensor pkv, pk, pv;
       if (has_e) {
@@ -1553,12 +1618,18 @@ std::pair<Tensor, Tensor> stack_forward(const Tensor& x_in, const Tensor& f_in, 
                                   stream_of(x)),
             "tmdnet_et_message_fwd");
       Tensor oo = at::empty({N, 3 * H}, o);
-      gemm_into(xa, p[9], true, p[10], oo, false);
+      Tensor xo, vo;
+      if (nf && l + 1 < L) {  // o_proj + the epilogue in one launch (the next LayerNorm: its mix)
+        oproj_epi(xa, p[9], p[10], x, vec, vecp, veca, oo, &xo, &vo);
+      } else {
+        gemm_into(xa, p[9], true, p[10], oo, false);
+      }
       A->x.push_back(x); A->vec.push_back(vec); A->xn.push_back(xn); A->mean.push_back(mean);
       A->rstd.push_back(rstd); A->qkv.push_back(qkv); A->vecp.push_back(vecp); A->xa.push_back(xa);
       A->o.push_back(oo);
-      Tensor xo, vo;
-      if (l + 1 < L) {
+      if (nf && l + 1 < L) {
+        // (x_out, vec_out came with o; the next LayerNorm runs in the next layer's mix)
+      } else if (l + 1 < L) {
         epi_ln(x, vec, vecp, oo, veca, P[(l + 1) * np], P[(l + 1) * np + 1], &xo, &vo, &xn, &mean, &rstd);
       } else if (c.out_norm) {  // the last epilogue + out_norm: x_out = LN(x_pre)
         epi_ln(x, vec, vecp, oo, veca, P[P.size() - 2], P[P.size() - 1], &xo, &vo, &xn, &mean, &rstd);
@@ -1746,7 +1817,8 @@ std::pair<Tensor, Tensor> stack_forward_fused(const Tensor& x_in, const Tensor& 
           "tmdnet_et_epilogue_ln_fwd");
   };
   Tensor vec, xn, mean, rstd, unused0, unused1;
-  epi_ln(x, Tensor(), Tensor(), Tensor(), Tensor(), P[0], P[1], &unused0, &unused1, &xn, &mean, &rstd);
+  const bool nf = node_fuse_ok(N, H);
+  if (!nf) epi_ln(x, Tensor(), Tensor(), Tensor(), Tensor(), P[0], P[1], &unused0, &unused1, &xn, &mean, &rstd);
   for (int64_t l = 0; l < L; ++l) {
     const Tensor* p = P.data() + l * np;
     F->qkv_w.push_back(A->pk->qkv_w[l].index_select(0, F->qkv_perm).contiguous());
@@ -1761,10 +1833,14 @@ std::pair<Tensor, Tensor> stack_forward_fused(const Tensor& x_in, const Tensor& 
                                ptr(F->img[l]), ptr(F->wsc[l]), ptr(F->bias[l]), st),
           "tmdnet_fep_split_f32");
     Tensor qkv = at::empty({N, 5 * H}, o), vecp;
-    gemm_into(xn, F->qkv_w[l], true, F->qkv_b[l], qkv, false);
-    if (vec.defined()) {
-      vecp = at::empty({N, 3, 3 * H}, o);
-      gemm_into(vec.view({3 * N, H}), p[8], true, Tensor(), vecp.view({3 * N, 3 * H}), false);
+    if (nf) {
+      ln_mix(x, p[0], p[1], F->qkv_w[l], F->qkv_b[l], vec, p[8], qkv, &vecp, &xn, &mean, &rstd);
+    } else {
+      gemm_into(xn, F->qkv_w[l], true, F->qkv_b[l], qkv, false);
+      if (vec.defined()) {
+        vecp = at::empty({N, 3, 3 * H}, o);
+        gemm_into(vec.view({3 * N, H}), p[8], true, Tensor(), vecp.view({3 * N, 3 * H}), false);
+      }
     }
     Tensor xa = at::empty({N, H}, o), veca = at::empty({N, 3, H}, o);
     const float* qb = static_cast<const float*>(qkv.data_ptr());
@@ -1775,12 +1851,17 @@ std::pair<Tensor, Tensor> stack_forward_fused(const Tensor& x_in, const Tensor& 
                                   ptr(veca), TMDNET_ET_V_PLANAR, st),
           "tmdnet_et_fused_fwd_f32");
     Tensor oo = at::empty({N, 3 * H}, o);
-    gemm_into(xa, p[9], true, p[10], oo, false);
+    Tensor xo, vo;
+    if (nf && l + 1 < L)
+      oproj_epi(xa, p[9], p[10], x, vec, vecp, veca, oo, &xo, &vo);
+    else
+      gemm_into(xa, p[9], true, p[10], oo, false);
     A->x.push_back(x); A->vec.push_back(vec); A->xn.push_back(xn); A->mean.push_back(mean);
     A->rstd.push_back(rstd); A->qkv.push_back(qkv); A->vecp.push_back(vecp); A->xa.push_back(xa);
     A->o.push_back(oo);
-    Tensor xo, vo;
-    if (l + 1 < L) {
+    if (nf && l + 1 < L) {
+      // (x_out, vec_out came with o; the next LayerNorm runs in the next layer's mix)
+    } else if (l + 1 < L) {
       epi_ln(x, vec, vecp, oo, veca, P[(l + 1) * np], P[(l + 1) * np + 1], &xo, &vo, &xn, &mean, &rstd);
     } else {  // the last epilogue + out_norm
       epi_ln(x, vec, vecp, oo, veca, P[P.size() - 2], P[P.size() - 1], &xo, &vo, &xn, &mean, &rstd);
@@ -1811,7 +1892,12 @@ variable_list stack_backward_fused(const StackActs& A, const FusedAux& F, Tensor
     g_o[l] = at::empty({N, 3 * H}, o);
     if (A.vec[l].defined()) g_vecp[l] = at::empty({N, 3, 3 * H}, o);
   }
-  {  // back through out_norm and the last layer's epilogue in one kernel
+  const bool nf = node_fuse_ok(N, H);
+  Tensor g_xa_pre;
+  if (nf) {
+    gX = lnbwd_oproj(gX, A.x_pre, A.mean_o, A.rstd_o, P[P.size() - 2], Tensor(), gV, A.vecp[L - 1], A.o[L - 1],
+                     P[(L - 1) * np + 9], g_vecp[L - 1], g_o[L - 1], &g_xa_pre);
+  } else {  // back through out_norm and the last layer's epilogue in one kernel
     Tensor g = at::empty_like(gX);
     check(tmdnet_ln_bwd_epilogue_w(TMDNET_F32, static_cast<int>(N), static_cast<int>(H), ptr(gX), ptr(A.x_pre),
                                    ptr(A.mean_o), ptr(A.rstd_o), ptr(P[P.size() - 2]), nullptr, nullptr, ptr(g), ptr(gV),
@@ -1822,8 +1908,12 @@ variable_list stack_backward_fused(const StackActs& A, const FusedAux& F, Tensor
   }
   for (int64_t l = L - 1; l >= 0; --l) {
     const Tensor* p = P.data() + l * np;
-    Tensor g_xa = at::empty({N, H}, o);
-    gemm_into(g_o[l], p[9], false, Tensor(), g_xa, false);
+    Tensor g_xa = g_xa_pre;
+    g_xa_pre = Tensor();
+    if (!g_xa.defined()) {
+      g_xa = at::empty({N, H}, o);
+      gemm_into(g_o[l], p[9], false, Tensor(), g_xa, false);
+    }
     const bool hv = A.vec[l].defined();
     Tensor g_vec_in = hv ? at::empty({N, 3, H}, o) : Tensor();
     Tensor g_qkv = at::empty({N, 5 * H}, o);
@@ -1842,12 +1932,19 @@ variable_list stack_backward_fused(const StackActs& A, const FusedAux& F, Tensor
     gemm_into(g_qkv, F.qkv_w[l], false, Tensor(), g_xn, false);
     if (hv) gemm_into(g_vecp[l].view({3 * N, 3 * H}), p[8], false, Tensor(), g_vec_in.view({3 * N, H}), true);
     const bool prev = l > 0;
-    Tensor g_x = at::empty_like(g_xn);
-    check(tmdnet_ln_bwd_epilogue_w(TMDNET_F32, static_cast<int>(N), static_cast<int>(H), ptr(g_xn), ptr(A.x[l]),
-                                   ptr(A.mean[l]), ptr(A.rstd[l]), ptr(p[0]), ptr(gX), nullptr, ptr(g_x), ptr(g_vec_in),
-                                   prev ? ptr(A.vecp[l - 1]) : nullptr, prev ? ptr(A.o[l - 1]) : nullptr,
-                                   prev ? ptr(g_vecp[l - 1]) : nullptr, prev ? ptr(g_o[l - 1]) : nullptr, nullptr, 0, st),
-          "tmdnet_ln_bwd_epilogue_w");
+    Tensor g_x;
+    if (nf && prev) {
+      g_x = lnbwd_oproj(g_xn, A.x[l], A.mean[l], A.rstd[l], p[0], gX, g_vec_in, A.vecp[l - 1], A.o[l - 1],
+                        P[(l - 1) * np + 9], g_vecp[l - 1], g_o[l - 1], &g_xa_pre);
+    } else {
+      g_x = at::empty_like(g_xn);
+      check(tmdnet_ln_bwd_epilogue_w(TMDNET_F32, static_cast<int>(N), static_cast<int>(H), ptr(g_xn), ptr(A.x[l]),
+                                     ptr(A.mean[l]), ptr(A.rstd[l]), ptr(p[0]), ptr(gX), nullptr, ptr(g_x), ptr(g_vec_in),
+                                     prev ? ptr(A.vecp[l - 1]) : nullptr, prev ? ptr(A.o[l - 1]) : nullptr,
+                                     prev ? ptr(g_vecp[l - 1]) : nullptr, prev ? ptr(g_o[l - 1]) : nullptr, nullptr, 0,
+                                     st),
+            "tmdnet_ln_bwd_epilogue_w");
+    }
     gX = g_x;
     gV = g_vec_in;
   }

@@ -329,13 +329,15 @@ def _epi_ln(x, vec, vecp, o, veca, ln_w, ln_b, xn_out=None, vo_out=None):
 # The forward's node mixes with the epilogue / LayerNorm pass folded in (et_nodemix.hip): per layer
 # tmdnet_et_ln_mix_f32 (LayerNorm + [q|k|v] + vec_proj) and tmdnet_et_oproj_epilogue_f32 (o_proj + the
 # epilogue) instead of [q|k|v]/vec_proj GEMM + o_proj GEMM + epilogue-LayerNorm pass: one launch per layer
-# fewer.  fp32, H % 64 == 0, H <= 256.  TMDNET_ET_NODE_FUSE=0 keeps the three-launch form.
+# fewer.  fp32, H % 64 == 0, H <= 256, in the small grouped GEMM's regime (3N rows <= GEMM_MAX_ROWS; larger
+# systems keep the x3 GEMMs).  TMDNET_ET_NODE_FUSE=0 keeps the three-launch form.
 NODE_FUSE = os.environ.get("TMDNET_ET_NODE_FUSE", "1") != "0"
 
 
 def _node_fuse_ok(x):
-    H = x.shape[1]
-    return NODE_FUSE and x.is_cuda and x.dtype == torch.float32 and H % 64 == 0 and H <= 256
+    N, H = x.shape
+    return (NODE_FUSE and x.is_cuda and x.dtype == torch.float32 and H % 64 == 0 and H <= 256
+            and 3 * N <= kernels.GEMM_MAX_ROWS)
 
 
 def _ln_mix(x, ln_w, ln_b, w, b, vec, vec_w, xn_out):
@@ -592,8 +594,8 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws, r=None, dr=Fa
     epi_done = False  # this layer's epilogue backward already ran (fused into the next layer's LN bwd)
     # the node-fused backward (tmdnet_et_lnbwd_oproj_f32): each LayerNorm backward also runs the layer
     # below's epilogue backward and its o_proj input gradient g_xa (no injections, no weight rows)
-    bwd_nf = (NODE_FUSE and not acc and not inj and not any(need_ws[:meta.n_layers + 1]) and gX is not None
-              and gX.is_cuda and gX.dtype == torch.float32 and H == 128)
+    bwd_nf = (not acc and not inj and not any(need_ws[:meta.n_layers + 1]) and gX is not None and H == 128
+              and _node_fuse_ok(gX))
     g_xa_pre = None  # the next (lower) layer's g_xa, formed by the fused kernel
     x_top = inj.get("x_top")  # a cotangent of the last epilogue's output (the out_norm input)
     if meta.out_norm and not seed_pre_norm:  # gX is the gradient of LN(x_out): back through out_norm first

@@ -54,7 +54,7 @@ class GraphedEnergyForces:
         torch.cuda.current_stream(dev).wait_stream(s)
         torch.cuda.synchronize(dev)
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
+        with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
             self.y, self.neg_dy = model(self.z, self.pos, self.batch)
         torch.cuda.synchronize(dev)
         # device flag written by every replay (lives in the graph's memory pool)

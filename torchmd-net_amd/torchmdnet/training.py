@@ -347,7 +347,7 @@ class GraphedTrainStep(LNNPStep):
         # the backward's seed: allocated outside the graph and kept alive with it (its replays read it)
         self._seed = seed = torch.ones((), dtype=params[0].dtype, device=dev)
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
+        with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
             self.static_loss = self.loss(self.z, self.pos, self.batch, self.y, self.neg_dy)
             grads = torch.autograd.grad(self.static_loss, params, grad_outputs=seed.expand_as(self.static_loss),
                                         allow_unused=True)
@@ -536,7 +536,9 @@ class _BucketStep:
         # the backward's seed: allocated outside the graph and kept alive with it (its replays read it)
         self._seed = seed = torch.ones((), dtype=params[0].dtype, device=dev)
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
+        # thread-local capture: the data loader's pin-memory thread keeps issuing host-allocation and copy calls
+        # while a new bucket is captured mid-epoch (global mode invalidated such a capture under a profiler)
+        with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
             self.ly, self.lf, total = loss_fn()
             grads = torch.autograd.grad(total, params, grad_outputs=seed.expand_as(total), allow_unused=True)
             pairs = [(v, gr) for v, gr in zip(views, grads) if gr is not None]
