@@ -188,3 +188,41 @@ def test_edge_geometry_backward_matches_autograd(R, rbf, dtype, tol, slots):
     rel = lambda a, b: float((a.double().cpu() - b).abs().max() / b.abs().max().clamp_min(1e-30))  # noqa: E731
     assert rel(g_r, e_r) < tol, rel(g_r, e_r)
     assert rel(g_dl, e_dl) < tol, rel(g_dl, e_dl)
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float64, 1e-11), (torch.float32, 2e-5)])
+@pytest.mark.parametrize("slots", [1, 2])
+def test_edge_geometry_backward_without_rbf_gradient(dtype, tol, slots):
+    """No consumer sends an rbf-row gradient (the fused C5 stack and neighbour embedding return g_r
+    themselves): the thread-per-edge k_bwd_e form -- cutoff and unit-vector terms only -- against autograd of
+    the formulas, with self loops and a lower cutoff."""
+    from torchmdnet import kernels
+    cl, cu, R = 0.5, 5.0, 64
+    g = torch.Generator().manual_seed(11 + slots)
+    pos = torch.randn(300, 3, generator=g, dtype=torch.float64) * 2.0
+    batch = torch.arange(6).repeat_interleave(50)
+    gr = kernels.build_graph(pos.to(dtype).to(DEV), batch.to(DEV), cl, cu, 300 * 300, loop=True)
+    start = np.exp(-cu + cl)
+    mu = torch.linspace(start, 1.0, R, dtype=torch.float64)
+    beta = torch.full((R,), (2.0 / R * (1 - start)) ** -2, dtype=torch.float64)
+    dl = gr.deltas.detach().clone().requires_grad_(True)
+    r = gr.distances.detach().clone().requires_grad_(True)
+    outs = kernels._EdgeGeom.apply(dl, r, gr, mu.to(dtype).to(DEV), beta.to(dtype).to(DEV), cl, cu,
+                                   kernels.nat.RBF_EXPNORM, (True, True, True), None, (1, slots))
+    C_all = [outs[1]] + list(outs[3:])
+    u = outs[2]
+    gens = [torch.randn(t.shape, generator=g, dtype=torch.float64) for t in C_all + [u]]
+    loss = sum((t * w.to(dtype).to(DEV)).sum() for t, w in zip(C_all + [u], gens))  # f unused: no gradient
+    g_dl, g_r = torch.autograd.grad(loss, [dl, r])
+    from oracle import model_oracle as O
+    dl64 = gr.deltas.detach().double().cpu().requires_grad_(True)
+    r64 = gr.distances.detach().double().cpu().requires_grad_(True)
+    C64 = O.cosine_cutoff(r64, cl, cu)
+    self_e = (gr.src == gr.dst).cpu().unsqueeze(1)
+    nrm = torch.where(self_e, torch.ones_like(r64).unsqueeze(1), dl64.norm(dim=1, keepdim=True))
+    u64 = torch.where(self_e, dl64, dl64 / nrm)
+    loss64 = sum((t * w).sum() for t, w in zip([C64] * slots + [u64], gens))
+    e_dl, e_r = torch.autograd.grad(loss64, [dl64, r64])
+    rel = lambda a, b: float((a.double().cpu() - b).abs().max() / b.abs().max().clamp_min(1e-30))  # noqa: E731
+    assert rel(g_r, e_r) < tol, rel(g_r, e_r)
+    assert rel(g_dl, e_dl) < tol, rel(g_dl, e_dl)

@@ -1,14 +1,16 @@
 #!/bin/bash
-# Round-5 judged evidence in one GPU call (GPU box, repo root): the -m gpu suite, the full bench line (CPU
+# The judged evidence of a round (GPU box, repo root), in two GPU calls: the -m gpu suite, the full bench line (CPU
 # baseline, PMC traffic), a rocprofv3 --kernel-trace --stats run of the bench (no PMC / CPU legs) with the
 # per-probe trace average of the graded kernel, the kernel lists of one C2 / C3 graph replay and of one
 # captured ET training step, the C5 per-kernel breakdown, the C2 PMC passes.
-# Output: gpurun_out/prof_r05/ (copy into profiles/ as r05_*).
-#   bash tools/r05_evidence.sh part1 [skip-tests]   (tests, bench, bench under rocprof)
-#   bash tools/r05_evidence.sh part2                (graph-step traces, C5 breakdown, training check, C2 PMC)
+# Output: gpurun_out/prof_<tag>/ (copy into profiles/ as <tag>_*).
+#   bash tools/evidence.sh <tag> part1 [skip-tests]   (tests, bench, bench under rocprof)
+#   bash tools/evidence.sh <tag> part2                (graph-step traces, C5 breakdown, training check, C2 PMC)
 set -o pipefail
 root=$(pwd)
-out=$root/gpurun_out/prof_r05
+tag=${1:?round tag}
+shift
+out=$root/gpurun_out/prof_$tag
 mkdir -p "$out"
 export TMPDIR=/tmp
 if [ "$1" = "part1" ]; then
@@ -36,7 +38,7 @@ csv=$(find /tmp/prof_train -name '*kernel_trace.csv' | head -1)
 python3 "$root/tools/trace_summary.py" "$csv" summary > "$out/train_step_kernels.txt"
 grep -h "kernels per step\|busy" "$out/et_c2_graph_step_kernels.txt" "$out/tn_c3_graph_step_kernels.txt" "$out/train_step_kernels.txt"
 cd "$root"
-timeout -k 10 360 bash tools/c5_profile.sh r05ev > /dev/null 2>&1 && cp gpurun_out/r05ev_c5_kernel_stats.csv "$out/c5_kernel_stats.csv" && cp gpurun_out/r05ev_c5time.json "$out/c5_time.json"
+timeout -k 10 360 bash tools/c5_profile.sh ${tag}ev > /dev/null 2>&1 && cp gpurun_out/${tag}ev_c5_kernel_stats.csv "$out/c5_kernel_stats.csv" && cp gpurun_out/${tag}ev_c5time.json "$out/c5_time.json"
 timeout -k 10 240 python3 tools/graphed_train_check.py 30 > "$out/graphed_train_check.json" 2> "$out/gtr.err" || echo "graphed train check failed"
-timeout -k 10 420 bash tools/c2_pmc.sh r05ev > /dev/null 2>&1 && cp gpurun_out/r05ev_pmc/summary.txt "$out/c2_pmc.txt"
+timeout -k 10 420 bash tools/c2_pmc.sh ${tag}ev > /dev/null 2>&1 && cp gpurun_out/${tag}ev_pmc/summary.txt "$out/c2_pmc.txt"
 echo done

@@ -197,6 +197,46 @@ __global__ __launch_bounds__(256) void k_bwd(Cfg<T> P, GIn<T> G, const T* __rest
   }
 }
 
+// No basis-row gradient at all (every consumer of the rbf rows took the dr route: the fused C5 stack and
+// neighbour embedding hand back g_r themselves): one thread per edge -- the cutoff and unit-vector terms
+// only, every load and store coalesced (the lane-parallel form below leaves 13 of an edge's 16 lanes
+// idle then: C5 0.33 ms).
+template <typename T>
+__global__ __launch_bounds__(256) void k_bwd_e(Cfg<T> P, GIn<T> G, const T* __restrict__ gu, T* __restrict__ gr,
+                                               T* __restrict__ gdl) {
+  const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= P.E) return;
+  const T r = P.r[e];
+  T acc = T(0);
+  if (G.c[0] || G.c[1] || G.c[2]) {
+    T c, dc;
+    cosine_cutoff<T>(r, P.cl, P.cu, c, dc);
+    T g = G.c[0] ? G.c[0][e] : T(0);
+    if (G.c[1]) g += G.c[1][e];
+    if (G.c[2]) g += G.c[2][e];
+    acc = g * dc;
+  }
+  gr[e] = acc;
+  T gx = T(0), gy = T(0), gz = T(0);
+  if (gu) {
+    const T x = P.dl[3 * e], y = P.dl[3 * e + 1], z = P.dl[3 * e + 2];
+    const T a = gu[3 * e], b = gu[3 * e + 1], c = gu[3 * e + 2];
+    if (P.src[e] == P.dst[e]) {
+      gx = a; gy = b; gz = c;
+    } else {
+      const T n = sqrt(x * x + y * y + z * z);
+      const T ux = x / n, uy = y / n, uz = z / n;
+      const T dot = ux * a + uy * b + uz * c;
+      gx = (a - ux * dot) / n;
+      gy = (b - uy * dot) / n;
+      gz = (c - uz * dot) / n;
+    }
+  }
+  gdl[3 * e] = gx;
+  gdl[3 * e + 1] = gy;
+  gdl[3 * e + 2] = gz;
+}
+
 // Lane-parallel form of k_bwd (the default): LPE = R / KPL lanes per edge, each lane owning KPL = 16 /
 // sizeof(T) consecutive basis indices (one 16-byte load per gradient slot), 64 / LPE edges per wave, so
 // a wave reads 64 / LPE whole gradient rows as one coalesced stream.  The per-edge terms of the basis
@@ -452,7 +492,10 @@ extern "C" int tmdnet_edge_geom_bwd_multi(int dtype, int n_edges, int num_rbf, i
     const T_* gu_ = (const T_*)grad_unit;                                                                          \
     T_* gr_ = (T_*)grad_dist;                                                                                      \
     T_* gd_ = (T_*)grad_deltas;                                                                                    \
-    if (!vec) hipLaunchKernelGGL(geom::k_bwd<T_>, dim3(blocks), dim3(tb), 0, st, P, G, gu_, gr_, gd_);            \
+    if (!grad_rbf && !grad_rbf2 && !grad_rbf3)                                                                    \
+      hipLaunchKernelGGL(geom::k_bwd_e<T_>, dim3((unsigned)((n_edges + 255) / 256)), dim3(256), 0, st, P, G, gu_,     \
+                         gr_, gd_);                                                                                \
+    else if (!vec) hipLaunchKernelGGL(geom::k_bwd<T_>, dim3(blocks), dim3(tb), 0, st, P, G, gu_, gr_, gd_);       \
     else if (lpe == 4) hipLaunchKernelGGL((geom::k_bwd_v<T_, 4>), dim3(blocks), dim3(tb), 0, st, P, G, gu_, gr_, gd_);   \
     else if (lpe == 8) hipLaunchKernelGGL((geom::k_bwd_v<T_, 8>), dim3(blocks), dim3(tb), 0, st, P, G, gu_, gr_, gd_);   \
     else if (lpe == 16) hipLaunchKernelGGL((geom::k_bwd_v<T_, 16>), dim3(blocks), dim3(tb), 0, st, P, G, gu_, gr_, gd_); \

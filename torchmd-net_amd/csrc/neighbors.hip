@@ -67,7 +67,8 @@ template <typename T> struct Params {
   V3<T> L;
   T cl2, cu2;
   int loop, transpose;
-  const int* unsorted;  // brute/shared: set by k_segments when `batch` descends somewhere
+  const int* unsorted;  // brute/shared: k_segments' per-block descent flags (nonzero somewhere: unsorted)
+  int n_unsorted;       // ... their count
 };
 
 // Directed edge s -> t (neighbors[0]=s, neighbors[1]=t): delta = pos[s] - pos[t] (minimum image).
@@ -98,15 +99,17 @@ __device__ __forceinline__ bool accept(const Params<T>& P, int s, int t, int64_t
 
 // ---------------------------------------------------------------- batch segments (no host sync)
 // seg[2t], seg[2t+1] = candidate range of destination t, by binary search as if `batch` were sorted;
-// in the same pass every thread checks its neighbour pair and raises `flag` on a descent.  The
-// pair kernels read the flag and fall back to all candidates [0, n) when it is set (the reference
-// accepts unsorted batches), so the searched ranges are only used when they are valid.
-__global__ void k_segments(const int64_t* __restrict__ batch, int n, int* __restrict__ flag,
-                           int* __restrict__ seg) {
+// in the same pass every thread checks its neighbour pair and each block stores whether it saw a descent
+// in flag[block] (written unconditionally: no zero fill before the launch).  The pair kernels OR the block
+// flags and fall back to all candidates [0, n) when any is set (the reference accepts unsorted batches),
+// so the searched ranges are only used when they are valid.
+__global__ __launch_bounds__(256) void k_segments(const int64_t* __restrict__ batch, int n, int* __restrict__ flag,
+                                                  int* __restrict__ seg) {
   int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t b = t < n ? batch[t] : 0;
+  const int desc = __syncthreads_or(t + 1 < n && b > batch[t + 1]);
+  if (threadIdx.x == 0) flag[blockIdx.x] = desc;
   if (t >= n) return;
-  const int64_t b = batch[t];
-  if (t + 1 < n && b > batch[t + 1]) atomicOr(flag, 1);
   int lo = 0, hi = t;  // first index with batch == b
   while (lo < hi) {
     int m = (lo + hi) >> 1;
@@ -135,7 +138,9 @@ __global__ __launch_bounds__(256) void k_pairs(Params<T> P, const int* __restric
   const int t = blockIdx.x * (blockDim.x / TMD_WAVE) + threadIdx.x / TMD_WAVE;
   if (t >= P.n) return;
   const int lane = lane_id();
-  const bool all = *P.unsorted != 0;  // unsorted batch: every atom is a candidate
+  int uf = 0;  // unsorted batch (a descent flagged by any k_segments block): every atom is a candidate
+  for (int i = lane; i < P.n_unsorted; i += TMD_WAVE) uf |= P.unsorted[i];
+  const bool all = __any(uf);
   const int lo = all ? 0 : seg[2 * t], hi = all ? P.n : seg[2 * t + 1];
   const V3<T> pt = load3(P.pos, t);
   const int64_t bt = P.batch[t];
@@ -549,7 +554,7 @@ struct Layout {
 static Layout layout(int n, int strategy, const double* box, double cut) {
   Layout L{};
   size_t o = 0;
-  L.flag = o; o += 16;
+  L.flag = o; o += align16(sizeof(int) * (size_t)(n > 256 ? (n + 255) / 256 : 1));  // k_segments block flags
   L.seg = o; o += align16(sizeof(int) * 2 * (size_t)n);
   L.counts = o; o += align16(sizeof(int) * ((size_t)n + 1));
   L.rowp = o; o += align16(sizeof(int) * ((size_t)n + 1));
@@ -636,8 +641,8 @@ static int build(int strategy, const T* pos, const int64_t* batch, int n, const 
   } else {
     // (a single-workgroup fusion of the segment search and the count pass measured slower: 25 us
     // against 14 us at 678 atoms -- its binary searches become dependent-load chains on one CU)
-    TMD_CHECK(hipMemsetAsync(flag, 0, sizeof(int), st));
     P.unsorted = flag;
+    P.n_unsorted = (n + tb - 1) / tb;
     hipLaunchKernelGGL(k_segments, dim3((n + tb - 1) / tb), dim3(tb), 0, st, batch, n, flag, seg);
     const int wpb = tb / TMD_WAVE;
     const dim3 g((n + wpb - 1) / wpb);
