@@ -72,3 +72,28 @@ def test_eval_eager_stack_operator_parameter_gradients(monkeypatch):
     assert a.keys() == b.keys() and len(a) > 0
     for n in a:
         assert _rel(a[n], b[n]) < 1e-4, n
+
+
+def test_cpp_route_after_fused_optimizer_step(monkeypatch):
+    """A fused AdamW step rewrites the parameters without bumping their version counters, which the C++
+    operator's packed-weight cache keys on: after the package's invalidation (every optimizer step of
+    training.step_reduce / LNNP.optimizer_step calls it) the operator sees the new weights."""
+    from oracle import model_oracle as O
+    from torchmdnet import _native
+    from torchmdnet.models import torchmd_et
+    m = _model(64, 2, 32).eval()
+    z, pos, batch = O.qm9_like(8)
+    z, pos, batch = z.to(DEV), pos.float().to(DEV), batch.to(DEV)
+    monkeypatch.setattr(torchmd_et, "CPP_EAGER", True)
+    m(z, pos, batch)  # packs the weights
+    params = [p for p in m.parameters() if p.requires_grad]
+    vers = [p._version for p in params]
+    for p in params:
+        p.grad = torch.randn_like(p) * 0.1
+    torch.optim.AdamW(params, lr=1e-2, fused=True).step()
+    assert [p._version for p in params] == vers  # (the premise: no version bump)
+    _native.invalidate_stack_cache()
+    y1, f1 = m(z, pos, batch)
+    monkeypatch.setattr(torchmd_et, "CPP_EAGER", False)
+    y0, f0 = m(z, pos, batch)
+    assert _rel(y1.detach(), y0.detach()) < 1e-6 and _rel(f1.detach(), f0.detach()) < 1e-6

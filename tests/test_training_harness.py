@@ -297,3 +297,21 @@ def test_gradient_copy_keeps_strided_gradients():
     _copy_grads(list(zip(views, grads)))
     for v, g in zip(views, grads):
         assert torch.equal(v, g)
+
+
+def test_optimizer_steps_invalidate_the_packed_weight_cache(monkeypatch):
+    """Every optimizer step of the package (training.step_reduce, LNNP.optimizer_step) drops the C++
+    et_stack operator's packed-weight cache: a fused AdamW rewrites parameters without bumping the version
+    counters that cache keys on."""
+    from torchmdnet import _native, training
+    calls = []
+    monkeypatch.setattr(_native, "invalidate_stack_cache", lambda: calls.append(1))
+    p = torch.nn.Parameter(torch.zeros(4))
+    p.grad = torch.ones(4)
+    opt = torch.optim.SGD([p], lr=0.1)
+    training.step_reduce(lambda: None, opt)
+    assert len(calls) == 1 and float(p[0]) == pytest.approx(-0.1)
+    monkeypatch.setattr(M, "create_model", lambda args, prior=None, mean=None, std=None: TinyPotential())
+    lnnp = M.LNNP(dict(lr=0.1, lr_warmup_steps=0))
+    lnnp.optimizer_step(opt)
+    assert len(calls) == 2

@@ -144,6 +144,15 @@ def load_torch_ops():
     _torch_ops_loaded = True
 
 
+def invalidate_stack_cache():
+    """Drop the C++ ``tmdnet::et_stack`` operator's packed-weight cache (torch_ops.cpp ``pack_stack``: keyed on
+    each parameter's storage, data pointer and version counter).  Fused optimizers (``AdamW(fused=True)``)
+    update parameters in place WITHOUT bumping their version counters, so every optimizer step of this
+    package calls this.  No-op while the operator library is not loaded."""
+    if _torch_ops_loaded:
+        torch.ops.tmdnet.et_stack_invalidate()
+
+
 def library_path():
     return _LIB_PATH
 

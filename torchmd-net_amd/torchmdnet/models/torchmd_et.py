@@ -29,10 +29,11 @@ NE_FUSED = os.environ.get("TMDNET_NE_FUSED", "1") != "0"
 # operator (the scripted path's; same kernels, differentiable to any order) instead of the Python
 # _ETStack / _ETStackBwd, whose launch orchestration costs ~2 ms of host time per C2 evaluation.  Training
 # (train mode: the force-loss second order is hand-written on the Python side) and HIP-graph capture keep
-# the Python stack.  Opt-in (TMDNET_ET_CPP_EAGER=1): C2 eval 2.84 -> 2.17 ms eager, energies / forces equal
-# to the Python stack's to 1e-7 on the QM9 batches, but an L1 validation loss of tests/test_gpu_fit_graphed.py
-# moved by 1.1e-4 relative.
-CPP_EAGER = os.environ.get("TMDNET_ET_CPP_EAGER", "0") == "1"
+# the Python stack.  C2 eval 2.84 -> 2.17 ms eager; energies / forces equal to the Python stack's to 1e-7.
+# The operator caches its packed weights by parameter version: the package's optimizer steps invalidate it
+# (fused AdamW does not bump versions; _native.invalidate_stack_cache).  TMDNET_ET_CPP_EAGER=0 keeps the Python
+# stack everywhere.
+CPP_EAGER = os.environ.get("TMDNET_ET_CPP_EAGER", "1") != "0"
 
 
 class TorchMD_ET(nn.Module):

@@ -20,6 +20,7 @@ import torch
 import torch.distributed as dist
 from torch.nn.functional import l1_loss, mse_loss
 
+from . import _native
 from .models.model import create_model, load_model
 from .et_stack import check_pending_consumed, second_order_expected
 from .training import GradAllReduce
@@ -59,6 +60,7 @@ class LNNP(torch.nn.Module):
             for pg in optimizer.param_groups:
                 pg["lr"] = scale * self.hparams.lr
         optimizer.step()
+        _native.invalidate_stack_cache()  # (a fused optimizer leaves the parameter versions unchanged)
         optimizer.zero_grad()
         self.global_step += 1
 

@@ -16,7 +16,7 @@ import torch
 import torch.distributed as dist
 import torch.nn.functional as F
 
-from . import kernels
+from . import _native, kernels
 from . import et_stack
 from .et_stack import second_order_expected
 
@@ -209,11 +209,14 @@ def step_reduce(reduce, opt, before_first=None):
                 before_first()
             opt.step_part(0)
         reduce.reduce_overlapped(first, lambda: opt.step_part(1))
-        return
-    reduce()
-    if before_first is not None:
-        before_first()
-    opt.step()
+    else:
+        reduce()
+        if before_first is not None:
+            before_first()
+        opt.step()
+    # fused AdamW writes the parameters without bumping their version counters: the C++ et_stack
+    # operator's packed weights (TorchScript / eval-mode eager) must not outlive this step
+    _native.invalidate_stack_cache()
 
 
 def _adamw(params, lr, weight_decay):
