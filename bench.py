@@ -820,6 +820,8 @@ def secondary_scripted(a, ws, rank, dev):
     el_t = timed_loop(lambda: scripted(z, pos, batch), a.warmup, steps, ws, dev)
     el_e = timed_loop(lambda: model(z, pos, batch), a.warmup, steps, ws, dev)
     model.eval()
+    # eval mode, unscripted: the layers through the C++ et_stack operator (torchmd_et.CPP_EAGER)
+    el_ev = timed_loop(lambda: model(z, pos, batch), a.warmup, steps, ws, dev)
     scripted_eval = torch.jit.script(model)
     el_s = timed_loop(lambda: scripted_eval(z, pos, batch), a.warmup, steps, ws, dev)
     return {"workload": "ET-QM9 energy+forces (C2 batch) through torch.jit.script(model.eval()), eager",
@@ -830,7 +832,10 @@ def secondary_scripted(a, ws, rank, dev):
             "train_mode_ms_per_step": round(1000 * el_t / steps, 4),
             "train_mode_path": "dispatcher ops (tmdnet::neighbor_graph, edge_geometry, nbr_embed) + the interaction "
                                "layers as ONE differentiable tmdnet::et_stack operator",
-            "eager_unscripted_ms_per_step": round(1000 * el_e / steps, 4)}
+            "eager_unscripted_ms_per_step": round(1000 * el_e / steps, 4),
+            "eager_unscripted_eval_ms_per_step": round(1000 * el_ev / steps, 4),
+            "eager_unscripted_eval_path": "model.eval(), unscripted: the interaction layers as the C++ "
+                                          "tmdnet::et_stack operator (differentiable), the rest Python autograd"}
 
 
 def secondary_water_box(a, ws, rank, dev):
