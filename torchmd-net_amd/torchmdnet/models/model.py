@@ -198,6 +198,13 @@ class TorchMD_Net(nn.Module):
         state.pop("_seed_cache", None)
         return state
 
+    @torch.jit.unused
+    def _early_dim_size(self, batch: Tensor) -> None:
+        """The molecule count read back now, while the queue is short: at the reduction the read-back would
+        wait out the whole enqueued forward before the force pass could be enqueued (eager evaluation)."""
+        if batch.is_cuda and batch.numel() and not torch.cuda.is_current_stream_capturing():
+            self.output_model.dim_size_hint = int(batch.max()) + 1
+
     def forward(self, z: Tensor, pos: Tensor, batch: Optional[Tensor] = None, q: Optional[Tensor] = None,
                 s: Optional[Tensor] = None, extra_args: Optional[Dict[str, Tensor]] = None
                 ) -> Tuple[Tensor, Optional[Tensor]]:
@@ -207,6 +214,7 @@ class TorchMD_Net(nn.Module):
             pos.requires_grad_(True)
         if torch.jit.is_scripting():
             return self._forward_script(z, pos, batch, q, s, extra_args)
+        self._early_dim_size(batch)
         x, v, z, pos, batch = self.representation_model(z, pos, batch, q=q, s=s)
         fused = None
         if self.prior_model is None:  # the head's tail, x * std, reduce and + mean fused (Scalar)

@@ -37,6 +37,7 @@ class OutputModel(nn.Module, metaclass=ABCMeta):
         self.allow_prior_model = allow_prior_model
         self.reduce_op = reduce_op
         self.dim_size = 0
+        self.dim_size_hint = -1  # the molecule count, read back early by TorchMD_Net.forward (-1: none)
 
     def reset_parameters(self):
         pass
@@ -48,7 +49,10 @@ class OutputModel(nn.Module, metaclass=ABCMeta):
     def _dim_size(self, x, batch):
         is_capturing = x.is_cuda and check_stream_capturing()
         if not x.is_cuda or not is_capturing:
-            self.dim_size = int(batch.max().item() + 1)
+            if self.dim_size_hint >= 0:  # (read back before the forward was enqueued: no wait here)
+                self.dim_size, self.dim_size_hint = self.dim_size_hint, -1
+            else:
+                self.dim_size = int(batch.max().item() + 1)
         if is_capturing:
             assert self.dim_size > 0, "Warming up is needed before capturing the model into a CUDA graph"
         return self.dim_size
