@@ -1,7 +1,7 @@
 """Host-side cost of an eager C2 energy+force evaluation (bench model, 32 QM9-like molecules), scripted
 and unscripted: torch.profiler CPU self time per op, the launch count, and wall time per evaluation
 with the GPU idle-waiting (host-bound when wall ~= host enqueue time).
-usage (GPU box): python tools/host_profile.py [script|eager|both] [rows]"""
+usage (GPU box): python tools/host_profile.py [script|eager|eager_eval|both] [rows]"""
 import os
 import sys
 import time
@@ -25,6 +25,8 @@ def main():
     forms = []
     if which in ("eager", "both"):
         forms.append(("eager", model))
+    if which in ("eager_eval", "both"):  # eval mode: the C++ et_stack route (torchmd_et.CPP_EAGER)
+        forms.append(("eager_eval", create_model(bench.et_args(128)).to(dev).eval()))
     if which in ("script", "both"):
         forms.append(("script", torch.jit.script(model)))
     if which in ("variants", "both"):  # the scripted model under other executor settings
