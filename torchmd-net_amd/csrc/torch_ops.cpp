@@ -1164,6 +1164,42 @@ void gemm_into(const Tensor& A, const Tensor& B, bool trans_b, const Tensor& bia
   }
 }
 
+// Two independent products in ONE tmdnet_gemm_f32 launch when both fit the grouped kernel (the layer's
+// [q|k|v]^T and vec_proj^T input gradients: 8 launches fewer per C2 force pass); else two gemm_into
+void gemm2_into(const Tensor& A1, const Tensor& B1, bool tb1, const Tensor& C1, bool beta1, const Tensor& A2,
+                const Tensor& B2, bool tb2, const Tensor& C2, bool beta2) {
+  auto ok = [](const Tensor& A, const Tensor& B, const Tensor& C) {
+    return A.scalar_type() == at::kFloat && A.size(0) > 0 && A.size(0) <= 16384 && A.stride(1) == 1 &&
+           B.stride(1) == 1 && C.stride(1) == 1;
+  };
+  if (ok(A1, B1, C1) && ok(A2, B2, C2)) {
+    int dims[16];
+    const void* ptrs[8];
+    const Tensor* As[2] = {&A1, &A2};
+    const Tensor* Bs[2] = {&B1, &B2};
+    const Tensor* Cs[2] = {&C1, &C2};
+    const bool tb[2] = {tb1, tb2}, be[2] = {beta1, beta2};
+    for (int i = 0; i < 2; ++i) {
+      const Tensor &A = *As[i], &B = *Bs[i], &C = *Cs[i];
+      const int d[8] = {static_cast<int>(A.size(0)), static_cast<int>(C.size(1)), static_cast<int>(A.size(1)),
+                        static_cast<int>(A.stride(0)), static_cast<int>(B.stride(0)), static_cast<int>(C.stride(0)),
+                        int(tb[i]), int(be[i])};
+      for (int j = 0; j < 8; ++j) dims[8 * i + j] = d[j];
+      ptrs[4 * i] = A.data_ptr();
+      ptrs[4 * i + 1] = B.data_ptr();
+      ptrs[4 * i + 2] = nullptr;
+      ptrs[4 * i + 3] = C.data_ptr();
+    }
+    const int rc = tmdnet_gemm_f32(2, dims, ptrs, stream_of(A1));
+    if (rc != TMDNET_UNSUPPORTED) {
+      check(rc, "tmdnet_gemm_f32");
+      return;
+    }
+  }
+  gemm_into(A1, B1, tb1, Tensor(), C1, beta1);
+  gemm_into(A2, B2, tb2, Tensor(), C2, beta2);
+}
+
 // out = A W^T (+ bias) for the dk/dv projection (tmdnet_proj_f32 on the exact bf16 split; library otherwise)
 void proj_into(const Tensor& A, const Tensor& W, const Tensor& Wp, const Tensor& bias, const Tensor& out) {
   const int M = static_cast<int>(A.size(0)), N = static_cast<int>(W.size(0)), K = static_cast<int>(W.size(1));
@@ -1430,8 +1466,11 @@ variable_list stack_backward_dr(const StackActs& A, Tensor gX, Tensor gV, const 
                                 stream_of(gX)),
           "tmdnet_et_message_bwd");
     Tensor g_xn = at::empty({N, H}, o);
-    gemm_into(g_qkv, A.pk->qkv_w[l], false, Tensor(), g_xn, false);
-    if (hv) gemm_into(g_vecp[l].view({3 * N, 3 * H}), p[8], false, Tensor(), g_vec_in.view({3 * N, H}), true);
+    if (hv)
+      gemm2_into(g_qkv, A.pk->qkv_w[l], false, g_xn, false, g_vecp[l].view({3 * N, 3 * H}), p[8], false,
+                 g_vec_in.view({3 * N, H}), true);
+    else
+      gemm_into(g_qkv, A.pk->qkv_w[l], false, Tensor(), g_xn, false);
     const bool prev = l > 0;
     Tensor g_x;
     if (nf && prev) {
@@ -1932,8 +1971,11 @@ variable_list stack_backward_fused(const StackActs& A, const FusedAux& F, Tensor
                                   flags, ptr(ws), wsb, st),
           "tmdnet_et_fused_bwd_f32");
     Tensor g_xn = at::empty({N, H}, o);
-    gemm_into(g_qkv, F.qkv_w[l], false, Tensor(), g_xn, false);
-    if (hv) gemm_into(g_vecp[l].view({3 * N, 3 * H}), p[8], false, Tensor(), g_vec_in.view({3 * N, H}), true);
+    if (hv)
+      gemm2_into(g_qkv, F.qkv_w[l], false, g_xn, false, g_vecp[l].view({3 * N, 3 * H}), p[8], false,
+                 g_vec_in.view({3 * N, H}), true);
+    else
+      gemm_into(g_qkv, F.qkv_w[l], false, Tensor(), g_xn, false);
     const bool prev = l > 0;
     Tensor g_x;
     if (nf && prev) {
