@@ -183,6 +183,7 @@ def test_mfma_head_matches_valu_kernel_and_fp64(N, monkeypatch):
 
     def run(x3):
         monkeypatch.setattr(kernels, "HEAD_X3", x3)
+        monkeypatch.setattr(kernels, "HEAD_X3_MIN_ATOMS", 0)
         xx, vv = x.clone().requires_grad_(True), vec.clone().requires_grad_(True)
         y = kernels.eq_scalar_head(xx, vv, head.output_network)
         gx, gv = torch.autograd.grad(y, (xx, vv), gy)

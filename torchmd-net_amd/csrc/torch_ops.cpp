@@ -2131,8 +2131,9 @@ std::tuple<Tensor, Tensor> et_energy_forces(
   Tensor y_atom = at::empty({N, 1}, o), jx = at::empty({N, H}, o), jv = at::empty({N, 3, H}, o);
   const void* hw[12];
   for (int i = 0; i < 12; ++i) hw[i] = head_params[i].data_ptr();
-  // the MFMA head over 16-atom tiles (eager kernels._eq_head_x3) when its envelope holds, else per atom
-  bool head_x3 = dt == TMDNET_F32 && tmdnet_eq_head_x3_pieces_bytes(static_cast<int>(H)) > 0;
+  // the MFMA head over 16-atom tiles (eager kernels._eq_head_x3) when its envelope holds and the system is
+  // past the per-atom kernel's crossover (kernels.HEAD_X3_MIN_ATOMS), else per atom
+  bool head_x3 = dt == TMDNET_F32 && N >= 768 && tmdnet_eq_head_x3_pieces_bytes(static_cast<int>(H)) > 0;
   for (int i : {3, 5, 9}) head_x3 = head_x3 && (reinterpret_cast<uintptr_t>(hw[i]) & 15) == 0;
   for (int i = 0; i < 12; ++i) head_x3 = head_x3 && head_params[i].is_contiguous();
   if (head_x3) {

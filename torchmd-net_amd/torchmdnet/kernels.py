@@ -2105,8 +2105,11 @@ def _will_run(node):
 
 
 # the head's forward + Jacobian on the bf16 MFMA over 16-atom tiles (tmdnet_eq_head_x3_f32; fp32, H = 128);
-# TMDNET_HEAD_X3=0: the per-atom VALU kernel (A/B)
+# TMDNET_HEAD_X3=0: the per-atom VALU kernel (A/B).  Below HEAD_X3_MIN_ATOMS the per-atom kernel is the
+# faster one (tools/head_ab.py, graph-replayed fwd + Jacobian: 678 atoms 40.2 µs VALU vs 47.4 MFMA;
+# 1024 atoms 59.1 vs 47.5; 50000 atoms 1255 vs 549)
 HEAD_X3 = os.environ.get("TMDNET_HEAD_X3", "1") != "0"
+HEAD_X3_MIN_ATOMS = int(os.environ.get("TMDNET_HEAD_X3_MIN_ATOMS", "768"))
 
 
 def _eq_head_x3(lib, x, vec, params, y, jx, jv):
@@ -2114,7 +2117,7 @@ def _eq_head_x3(lib, x, vec, params, y, jx, jv):
     also inside a captured step) + tmdnet_eq_head_x3_f32.  Returns False outside its envelope."""
     N, H = x.shape
     nbytes = int(lib.tmdnet_eq_head_x3_pieces_bytes(H))
-    if not (HEAD_X3 and nbytes and x.dtype == torch.float32 and all(p.is_contiguous() for p in params)
+    if not (HEAD_X3 and N >= HEAD_X3_MIN_ATOMS and nbytes and x.dtype == torch.float32 and all(p.is_contiguous() for p in params)
             and all(p.data_ptr() % 16 == 0 for p in (params[3], params[5], params[9]))):
         return False
     st = nat.stream(x.device)
