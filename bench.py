@@ -865,6 +865,61 @@ def secondary_water_box(a, ws, rank, dev):
             "edges": int(d.last_num_pairs.item()) if torch.is_tensor(d.last_num_pairs) else d.last_num_pairs}
 
 
+def tn_args():
+    import yaml
+    with open(os.path.join(ROOT, "tests", "golden", "configs", "tensornet_rmd17.yaml")) as f:
+        args = yaml.safe_load(f)
+    args.update(prior_model=None, precision=32, derivative=True)
+    return args
+
+
+def tn_water_box_model(n, static_shapes, seed, dev, precision=32):
+    """C5's TensorNet arm: the TensorNet-rMD17 architecture (128 ch, 2 layers, 32 RBF, cutoff 4.5, O(3);
+    the model reference benchmarks/inference.py:63-71 times) on a periodic n-atom water box (SURVEY §8(d):
+    z = (8,1,1) repeated, pos = rand * L, L = (n/0.1003)^(1/3)), cell list, max_num_neighbors 64 (the 32 of
+    inference.py would overflow at water density).  Returns (model, z, pos, batch, L) on dev."""
+    from torchmdnet.models.model import create_model
+    args = tn_args()
+    args.update(max_num_neighbors=64, precision=precision)
+    torch.manual_seed(0)
+    model = create_model(args).to(dev)
+    rep_ = model.representation_model
+    rep_.static_shapes = static_shapes  # (create_model keeps TensorNet's default True, as the reference's)
+    rep_.distance.resize_to_fit = not static_shapes
+    g = torch.Generator().manual_seed(7 + seed)
+    L = (n / 0.1003) ** (1.0 / 3.0)
+    dt = torch.float64 if precision == 64 else torch.float32
+    pos = (torch.rand(n, 3, generator=g, dtype=torch.float64) * L).to(dt).to(dev)
+    z = torch.tensor([8, 1, 1], dtype=torch.long).repeat(n // 3 + 1)[:n].to(dev)
+    batch = torch.zeros(n, dtype=torch.long, device=dev)
+    d = rep_.distance
+    d.box = torch.eye(3, dtype=dt) * L
+    d.use_periodic = True
+    d.strategy = "cell"
+    return model, z, pos, batch, L
+
+
+def secondary_tn_water_box(a, ws, rank, dev):
+    """C5, TensorNet arm: TensorNet-rMD17 architecture on the ~50k-atom periodic water
+    box, energy + forces through TorchMD_Net, eager, static_shapes (reference default) and dynamic shapes;
+    one system per GPU (replicas)."""
+    n = a.roofline_atoms
+    steps = max(3, a.steps // 10)
+    out = {}
+    for static in (True, False):
+        model, z, pos, batch, L = tn_water_box_model(n, static, rank, dev)
+        el = timed_loop(lambda: model(z, pos, batch), 2, steps, ws, dev)
+        d = model.representation_model.distance
+        out["static_shapes" if static else "dynamic_shapes"] = {
+            "value": round(n * ws * steps / el, 1), "unit": "atoms/s", "ms_per_step": round(1000 * el / steps, 3),
+            "edges": int(d.last_num_pairs.item()) if torch.is_tensor(d.last_num_pairs) else d.last_num_pairs}
+        del model
+    res = out["static_shapes"]
+    return {"workload": f"TensorNet (rMD17 arch: 128 ch, 2 layers, 32 RBF, cutoff 4.5, O(3)) water box, {n} atoms, "
+                        f"periodic L={L:.1f} A, cell list, energy+forces, eager (C5, benchmarks/inference.py model)",
+            "value": res["value"], "unit": "atoms/s", "ms_per_step": res["ms_per_step"], **out}
+
+
 def secondary_scripted_water_box(a, ws, rank, dev, eager_ms=None):
     """C5 as the MD-engine form: torch.jit.script(model) in eval mode on the same water box -- the whole
     energy + force evaluation as ONE tmdnet::et_energy_forces operator with the large-system forms (Morton
@@ -1328,6 +1383,8 @@ def main():
         sec["et_water_box_c5"] = secondary_water_box(a, ws, rank, dev)
         phase("secondary: ET C5 water box, TorchScript")
         sec["et_scripted_c5"] = secondary_scripted_water_box(a, ws, rank, dev, sec["et_water_box_c5"]["ms_per_step"])
+        phase("secondary: TensorNet C5 water box")
+        sec["tn_water_box_c5"] = secondary_tn_water_box(a, ws, rank, dev)
         if rank == 0:
             out["secondary"] = sec
     if a.mode == "infer" and a.ddp_train:

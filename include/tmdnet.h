@@ -516,6 +516,22 @@ int tmdnet_tn_message_bwd_add(int dtype, int n_nodes, int hidden, const int32_t*
                               const int32_t* pad_pairs, int pad_capacity, const void* edge_attr,
                               int ld_ea, const void* comp, const void* grad_msg, const void* g_comp_add,
                               void* g_edge_attr, void* g_comp, void* stream);
+/* Pair-row forms (large systems): the edge factors are functions of |r| only, so the two directions of a
+ * pair share one row.  edge_attr / g_edge_attr are [n_pair_slots][3H] in tmdnet_pair_index's numbering
+ * (pair_row [E] -> slot, pair_edge [n_pair_slots] -> the slot's canonical edge, src >= dst); edge e reads
+ * row pair_row[e].  The backward's destination pass runs per pair (its canonical edge forms the sum over
+ * both directions, one write per pair, no atomics; inert slots zeroed); g_edge_attr or g_comp may be NULL
+ * (that pass skipped). */
+int tmdnet_tn_message_fwd_pairs(int dtype, int n_nodes, int hidden, const int32_t* row_ptr,
+                                const int32_t* src, int max_pairs, double self0_mult,
+                                const int32_t* pad_pairs, int pad_capacity, const int32_t* pair_row,
+                                const void* edge_attr, int ld_ea, const void* comp, void* msg, void* stream);
+int tmdnet_tn_message_bwd_pairs(int dtype, int n_nodes, int hidden, const int32_t* row_ptr,
+                                const int32_t* src, int max_pairs, double self0_mult,
+                                const int32_t* pad_pairs, int pad_capacity, const int32_t* pair_row,
+                                const int32_t* pair_edge, int n_pair_slots, const void* edge_attr, int ld_ea,
+                                const void* comp, const void* grad_msg, const void* g_comp_add,
+                                void* g_edge_attr, void* g_comp, void* stream);
 
 /* TensorNet per-channel node algebra, one fused pass each (replaces the reference's elementwise
  * PyTorch chains).  X / "full" tensors are [N][H][3][3]; compact ones [9][N][H] as above.
@@ -576,6 +592,11 @@ int tmdnet_dot_sum_fwd(int dtype, int n_atoms, int K, const void* h, int ld_h, c
                        int n_mol, const int64_t* batch, const void* std_, const void* mean, void* y, void* stream);
 int tmdnet_dot_sum_bwd(int dtype, int n_atoms, int K, const void* grad_y, const int64_t* batch, int n_mol,
                        const void* std_, const void* w, void* grad_h, void* stream);
+/* The same for large systems: the row products over the whole grid into atom_buf [n_atoms] (per-atom
+ * h[n].w + b0), then the per-molecule sums (atom_buf NULL: tmdnet_dot_sum_fwd). */
+int tmdnet_dot_sum_fwd_atoms(int dtype, int n_atoms, int K, const void* h, int ld_h, const void* w, const void* b0,
+                             int n_mol, const int64_t* batch, const void* std_, const void* mean, void* atom_buf,
+                             void* y, void* stream);
 
 /* LayerNorm over the last dimension, fp32, C <= 1024 (reference nn.LayerNorm; TensorNet's init_norm /
  * out_norm, models/tensornet.py:232, 322): y = (x - mean) * rstd * w + b, mean / rstd [rows] saved.
@@ -675,6 +696,14 @@ int tmdnet_embedding_bwd_f32(int n, int H, int num_types, const int64_t* z, int 
 int tmdnet_split_t_f32(int N, int K, const void* B, int ldb, void* Bp, void* stream);
 int tmdnet_gemm_x3_f32(int M, int N, int K, const void* A, int lda, const void* Bp, const void* bias, void* C,
                        int ldc, int beta, void* stream);
+/* tmdnet_gemm_x3_f32 with tmdnet_gemm_ex_f32's epilogue, for the Linear + SiLU stacks of large systems
+ * (TensorNet's edge MLP, reference tensornet.py:381-385, over ~1M pair rows at C5; the embedding's scalar
+ * MLP tensornet.py:320-321): v = acc + bias (+ C if beta) -> pre[r][c] = v (nullable) -> v = silu(v) if act
+ * -> v *= rscale[r] (nullable) -> v *= silu'(dpre[r][c]) (nullable) -> C.  pre / dpre: row stride ldx
+ * (>= N, % 4), 16-byte aligned. */
+int tmdnet_gemm_x3_ex_f32(int M, int N, int K, const void* A, int lda, const void* Bp, const void* bias, void* C,
+                          int ldc, int beta, int act, void* pre, const void* rscale, const void* dpre, int ldx,
+                          void* stream);
 int tmdnet_proj_split_f32(int N, int K, const void* W, int ldw, void* Wp, void* stream);
 int tmdnet_proj_f32(int M, int N, int K, const void* A, int lda, const void* Wp, long long piece_stride,
                     const void* bias, void* C, int ldc, void* stream);

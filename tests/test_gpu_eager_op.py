@@ -74,26 +74,50 @@ def test_eval_eager_stack_operator_parameter_gradients(monkeypatch):
         assert _rel(a[n], b[n]) < 1e-4, n
 
 
-def test_cpp_route_after_fused_optimizer_step(monkeypatch):
-    """A fused AdamW step rewrites the parameters without bumping their version counters, which the C++
-    operator's packed-weight cache keys on: after the package's invalidation (every optimizer step of
-    training.step_reduce / LNNP.optimizer_step calls it) the operator sees the new weights."""
+def _stale_check(monkeypatch, mutate, scripted=False):
+    """Evaluate through the C++ operator, rewrite the weights with ``mutate`` (no invalidation call of any
+    kind), evaluate again: the result must be the Python stack's on the NEW weights."""
     from oracle import model_oracle as O
-    from torchmdnet import _native
     from torchmdnet.models import torchmd_et
     m = _model(64, 2, 32).eval()
     z, pos, batch = O.qm9_like(8)
     z, pos, batch = z.to(DEV), pos.float().to(DEV), batch.to(DEV)
     monkeypatch.setattr(torchmd_et, "CPP_EAGER", True)
-    m(z, pos, batch)  # packs the weights
+    run = torch.jit.script(m) if scripted else m
+    y_old, _ = run(z, pos, batch)
+    mutate(m)
+    y1, f1 = run(z, pos, batch)
+    monkeypatch.setattr(torchmd_et, "CPP_EAGER", False)
+    y0, f0 = m(z, pos, batch)
+    assert _rel(y_old.detach(), y0.detach()) > 1e-4  # (the premise: the weights did change the energy)
+    assert _rel(y1.detach(), y0.detach()) < 1e-6 and _rel(f1.detach(), f0.detach()) < 1e-6
+
+
+def _fused_adamw(m):
     params = [p for p in m.parameters() if p.requires_grad]
     vers = [p._version for p in params]
     for p in params:
         p.grad = torch.randn_like(p) * 0.1
     torch.optim.AdamW(params, lr=1e-2, fused=True).step()
-    assert [p._version for p in params] == vers  # (the premise: no version bump)
-    _native.invalidate_stack_cache()
-    y1, f1 = m(z, pos, batch)
-    monkeypatch.setattr(torchmd_et, "CPP_EAGER", False)
-    y0, f0 = m(z, pos, batch)
-    assert _rel(y1.detach(), y0.detach()) < 1e-6 and _rel(f1.detach(), f0.detach()) < 1e-6
+    assert [p._version for p in params] == vers  # (the premise: a fused step bumps no version counter)
+
+
+def _data_copy(m):
+    g = torch.Generator(device=DEV).manual_seed(3)
+    for name, p in m.named_parameters():
+        if "attention_layers" in name:  # an EMA-style swap: p.data written, version counter untouched
+            p.data.copy_(p.data + 0.05 * torch.randn(p.shape, device=DEV, generator=g))
+
+
+@pytest.mark.parametrize("mutate", [_fused_adamw, _data_copy], ids=["fused_adamw", "data_copy"])
+def test_cpp_route_sees_weight_updates_without_invalidation(mutate, monkeypatch):
+    """a plain ``torch.optim.AdamW(fused=True)`` step, or ``p.data.copy_``, then an eval-mode
+    evaluation through the C++ operator -- WITHOUT any cache invalidation call -- matches the Python stack on
+    the new weights (the operator holds no packed copy: pack_stack takes views of the parameters)."""
+    _stale_check(monkeypatch, mutate)
+
+
+@pytest.mark.parametrize("mutate", [_fused_adamw, _data_copy], ids=["fused_adamw", "data_copy"])
+def test_scripted_fused_eval_sees_weight_updates(mutate, monkeypatch):
+    """The same through torch.jit.script(model.eval()) (one tmdnet::et_energy_forces operator)."""
+    _stale_check(monkeypatch, mutate, scripted=True)

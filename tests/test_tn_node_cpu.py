@@ -127,12 +127,12 @@ def _fake_embed_bwd(P, Q, W, C, u, graph, gE, gP, gQ, gW, gC, gu):
         dst.copy_(src)
 
 
-def _fake_msg_fwd(ea, Tc, graph, out):
-    out.copy_(kernels.tn_message_composite(ea, Tc, graph))
+def _fake_msg_fwd(ea, Tc, graph, out, pairs=None):
+    out.copy_(kernels.tn_message_composite(kernels._ea_edges(ea, pairs), Tc, graph))
 
 
-def _fake_msg_bwd(ea, Tc, graph, gmsg, gea, gT, gadd=None):
-    g = _vjp(lambda e, t: kernels.tn_message_composite(e, t, graph), [ea, Tc], gmsg)
+def _fake_msg_bwd(ea, Tc, graph, gmsg, gea, gT, gadd=None, pairs=None):
+    g = _vjp(lambda e, t: kernels.tn_message_composite(kernels._ea_edges(e, pairs), t, graph), [ea, Tc], gmsg)
     gea.copy_(g[0])
     gT.copy_(g[1] + (0 if gadd is None else gadd))
 

@@ -859,6 +859,12 @@ struct XArgs {
   const unsigned short* Bp;
   const float* bias;
   float* C;
+  // epilogue extensions (tmdnet_gemm_x3_ex_f32, k_gemm's tmdnet_gemm_ex_f32 semantics): v = acc + bias (+ C)
+  // -> pre[r][c] = v -> v = silu(v) (act) -> v *= rscale[r] -> v *= silu'(dpre[r][c]) -> C
+  int act, ldx;
+  float* pre;
+  const float* rscale;
+  const float* dpre;
 };
 template <int MB, int BN, int PD>
 __global__ __launch_bounds__(256) void k_gemm_x3(XArgs P) {
@@ -974,6 +980,17 @@ __global__ __launch_bounds__(256) void k_gemm_x3(XArgs P) {
       f4* out = reinterpret_cast<f4*>(P.C + (size_t)m * P.ldc + n);
       f4 v = acc[nb][mb] + bv;
       if (P.beta) v += *out;
+      if (P.pre) *reinterpret_cast<f4*>(P.pre + (size_t)m * P.ldx + n) = v;
+      if (P.act) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = Silu<float>(v[j]).s;
+      }
+      if (P.rscale) v *= P.rscale[m];
+      if (P.dpre) {
+        const f4 x = *reinterpret_cast<const f4*>(P.dpre + (size_t)m * P.ldx + n);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] *= Silu<float>(x[j]).d(x[j]);
+      }
       *out = v;
     }
   }
@@ -1571,16 +1588,27 @@ extern "C" int tmdnet_split_t_f32(int N, int K, const void* B, int ldb, void* Bp
 // K % 32 == 0, N % 16 == 0, 16-byte aligned rows and pointers.
 extern "C" int tmdnet_gemm_x3_f32(int M, int N, int K, const void* A, int lda, const void* Bp, const void* bias,
                                   void* C, int ldc, int beta, void* stream) {
+  return tmdnet_gemm_x3_ex_f32(M, N, K, A, lda, Bp, bias, C, ldc, beta, 0, nullptr, nullptr, nullptr, 0, stream);
+}
+
+// tmdnet_gemm_x3_f32 with tmdnet_gemm_ex_f32's epilogue: pre (the pre-activation, row stride ldx), act (SiLU),
+// rscale (per-row scale), dpre (times silu'(dpre), row stride ldx) -- the Linear + SiLU stacks of large
+// systems (TensorNet's edge MLP over ~1M pair rows at C5) without separate activation passes.
+extern "C" int tmdnet_gemm_x3_ex_f32(int M, int N, int K, const void* A, int lda, const void* Bp, const void* bias,
+                                     void* C, int ldc, int beta, int act, void* pre, const void* rscale,
+                                     const void* dpre, int ldx, void* stream) {
   if (M < 0 || N <= 0 || K <= 0 || !A || !Bp || !C) return kBadArgument;
   if (M == 0) return kOk;
   if (K % 32 || N % 16 || lda < K || ldc < N || lda % 4 || ldc % 4) return kUnsupported;
   if ((((uintptr_t)A) | ((uintptr_t)Bp) | ((uintptr_t)C) | ((uintptr_t)bias)) & 15) return kUnsupported;
+  if ((pre || dpre) && (ldx < N || ldx % 4 || ((((uintptr_t)pre) | ((uintptr_t)dpre)) & 15))) return kUnsupported;
   static const int remap_env = [] {
     const char* e = getenv("TMDNET_X3_REMAP");
     return e ? atoi(e) : 1;
   }();
   proj::XArgs P{M, N, K, lda, ldc, beta ? 1 : 0, 0, 0, 0, (const float*)A, (const unsigned short*)Bp,
-                (const float*)bias, (float*)C};
+                (const float*)bias, (float*)C, act ? 1 : 0, ldx, (float*)pre, (const float*)rscale,
+                (const float*)dpre};
   hipStream_t st = (hipStream_t)stream;
   // 64-column tiles for wide outputs (the forward mixes, N = 3H..5H), 128 for the narrow input gradients
   // (N = H: one column tile, A read once); 2 row blocks per wave (128 rows per workgroup).  Wide-form

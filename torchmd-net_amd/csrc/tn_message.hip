@@ -53,7 +53,16 @@ template <typename T> struct Args {
   const T* gmsg;
   T* gea; T* gT;
   const T* gTadd;           // [9][N][H] or NULL: added to gT (the component tensor's other consumer)
+  // pair rows (large systems): ea / gea hold one row per edge PAIR (the two directions of a pair have the
+  // same factors, functions of |r| only), edge k reads row prow[k] (tmdnet_pair_index numbering)
+  const int32_t* prow;      // [E] or NULL (per-edge rows)
+  const int32_t* pedge;     // [np] the canonical edge of each pair slot
+  int np;                   // pair slots
 };
+
+template <typename T> __device__ __forceinline__ int ea_row(const Args<T>& A, int k) {
+  return A.prow ? A.prow[k] : k;
+}
 
 // Multiplicity of atom 0's self loop.  With a device pair count (static_shapes under HIP-graph
 // capture) it is computed here: 1 + (reference padding capacity - pairs found), a uniform scalar load.
@@ -299,7 +308,7 @@ __global__ __launch_bounds__(64 * S) void k_msg_fwd(Args<T> A) {
     const int m = A.src[k];
     TMD_DCHECK(m >= 0 && m < A.n);
     const T mult = (m == n && n == 0) ? mult0_of(A) : T(1);
-    const T* er = A.ea + (size_t)k * A.ldea + 3 * hc;
+    const T* er = A.ea + (size_t)ea_row(A, k) * A.ldea + 3 * hc;
     const T f0 = er[0] * mult, f1 = er[1] * mult, f2 = er[2] * mult;
     T t[9];
     ldc(t, A.Tc + (size_t)m * A.H + hc, A.nh);
@@ -336,6 +345,56 @@ __global__ __launch_bounds__(64 * S) void k_msg_bwd_dst(Args<T> A) {
   }
 }
 
+// pair-row destination pass: gea[p] = sum over the pair's two directions of <gmsg[dst], {I,A,S}[src]>, formed
+// by the pair's canonical edge (row n, src m >= n; tmdnet_pair_index) from both endpoints' rows -- one write
+// per pair instead of one per edge, no atomics.  Inert pair slots (static capacity) are zeroed.
+template <typename T, int S>
+__global__ __launch_bounds__(64 * S) void k_msg_bwd_pair(Args<T> A) {
+  {
+    const long long tid = (long long)blockIdx.x * blockDim.x + threadIdx.x, nth = (long long)gridDim.x * blockDim.x;
+    const int w3 = 3 * A.H;
+    for (long long i = tid; i < (long long)A.np * w3; i += nth) {
+      const int p = (int)(i / w3);
+      if (A.prow[A.pedge[p]] != p) A.gea[i] = T(0);
+    }
+  }
+  int n, ch0, w;
+  slot_node<S>(A.nblk, n, ch0, w);
+  const int h = ch0 + lane_id();
+  const bool on = h < A.H;
+  const int hc = on ? h : 0;
+  T gn[9], tn_[9];
+  ldc(gn, A.gmsg + (size_t)n * A.H + hc, A.nh);
+  ldc(tn_, A.Tc + (size_t)n * A.H + hc, A.nh);
+  const int b = min(A.row_ptr[n], A.cap), e = min(A.row_ptr[n + 1], A.cap);
+  for (int k = b + w; k < e; k += S) {
+    const int m = A.src[k];
+    TMD_DCHECK(m >= 0 && m < A.n);
+    if (m < n) continue;  // the pair's other direction: formed by row m
+    const T mult = (m == n && n == 0) ? mult0_of(A) : T(1);
+    T g0, g1, g2;
+    if (m == n) {  // self loop: one direction
+      g0 = gn[0] * tn_[0];
+      g1 = gn[1] * tn_[1] + gn[2] * tn_[2] + gn[3] * tn_[3];
+      g2 = gn[4] * tn_[4] + gn[5] * tn_[5] + gn[6] * tn_[6] + gn[7] * tn_[7] + gn[8] * tn_[8];
+    } else {
+      T t[9], g[9];
+      ldc(t, A.Tc + (size_t)m * A.H + hc, A.nh);
+      ldc(g, A.gmsg + (size_t)m * A.H + hc, A.nh);
+      g0 = gn[0] * t[0] + g[0] * tn_[0];
+      g1 = gn[1] * t[1] + gn[2] * t[2] + gn[3] * t[3] + g[1] * tn_[1] + g[2] * tn_[2] + g[3] * tn_[3];
+      g2 = gn[4] * t[4] + gn[5] * t[5] + gn[6] * t[6] + gn[7] * t[7] + gn[8] * t[8] +
+           g[4] * tn_[4] + g[5] * tn_[5] + g[6] * tn_[6] + g[7] * tn_[7] + g[8] * tn_[8];
+    }
+    if (on) {
+      T* gr = A.gea + (size_t)A.prow[k] * 3 * A.H + 3 * h;
+      gr[0] = g0 * mult;
+      gr[1] = g1 * mult;
+      gr[2] = g2 * mult;
+    }
+  }
+}
+
 // source pass: gT[m] = sum over reversed edges ea * gmsg[n]
 template <typename T, int S>
 __global__ __launch_bounds__(64 * S) void k_msg_bwd_src(Args<T> A) {
@@ -353,7 +412,7 @@ __global__ __launch_bounds__(64 * S) void k_msg_bwd_src(Args<T> A) {
     const int n = A.src[k];
     TMD_DCHECK(n >= 0 && n < A.n);
     const T mult = (m == n && n == 0) ? mult0_of(A) : T(1);
-    const T* er = A.ea + (size_t)k * A.ldea + 3 * hc;
+    const T* er = A.ea + (size_t)ea_row(A, k) * A.ldea + 3 * hc;
     const T f0 = er[0] * mult, f1 = er[1] * mult, f2 = er[2] * mult;
     T g[9];
     ldc(g, A.gmsg + (size_t)n * A.H + hc, A.nh);
@@ -402,6 +461,7 @@ TMD_TN_KERNEL(k_embed_bwd_src)
 TMD_TN_KERNEL(k_msg_fwd)
 TMD_TN_KERNEL(k_msg_bwd_dst)
 TMD_TN_KERNEL(k_msg_bwd_src)
+TMD_TN_KERNEL(k_msg_bwd_pair)
 #undef TMD_TN_KERNEL
 
 template <typename T> static int launch_embed_fwd(const Args<T>& A, hipStream_t st) {
@@ -418,6 +478,9 @@ template <typename T> static int launch_msg_bwd_dst(const Args<T>& A, hipStream_
 }
 template <typename T> static int launch_msg_bwd_src(const Args<T>& A, hipStream_t st) {
   return launch_s<T, k_msg_bwd_src_k>(A, st);
+}
+template <typename T> static int launch_msg_bwd_pair(const Args<T>& A, hipStream_t st) {
+  return launch_s<T, k_msg_bwd_pair_k>(A, st);
 }
 
 // the embedding destination pass: one S-wave block per node (each wave covers every channel block)
@@ -552,4 +615,43 @@ extern "C" int tmdnet_tn_message_bwd(int dtype, int n_nodes, int hidden, const i
   return tmdnet_tn_message_bwd_add(dtype, n_nodes, hidden, row_ptr, src, max_pairs, self0_mult, pad_pairs,
                                    pad_capacity, edge_attr, ld_ea, comp, grad_msg, nullptr, g_edge_attr, g_comp,
                                    stream);
+}
+
+// Pair-row forms of the message (large systems): edge_attr / g_edge_attr hold one row per pair slot of
+// tmdnet_pair_index (pair_row [E] -> slot, pair_edge [n_pair_slots] -> canonical edge).
+extern "C" int tmdnet_tn_message_fwd_pairs(int dtype, int n_nodes, int hidden, const int32_t* row_ptr,
+                                           const int32_t* src, int max_pairs, double self0_mult,
+                                           const int32_t* pad_pairs, int pad_capacity, const int32_t* pair_row,
+                                           const void* edge_attr, int ld_ea, const void* comp, void* msg,
+                                           void* stream) {
+  if (!pair_row) return kBadArgument;
+  hipStream_t st = (hipStream_t)stream;
+  TN_DISPATCH(dtype, {
+    auto a = tn::base<T>(n_nodes, hidden, row_ptr, src, max_pairs, self0_mult, pad_pairs, pad_capacity);
+    a.prow = pair_row;
+    a.ea = (const T*)edge_attr; a.ldea = ld_ea;
+    a.Tc = (const T*)comp; a.msg = (T*)msg;
+    return tn::launch_msg_fwd<T>(a, st);
+  })
+}
+
+extern "C" int tmdnet_tn_message_bwd_pairs(int dtype, int n_nodes, int hidden, const int32_t* row_ptr,
+                                           const int32_t* src, int max_pairs, double self0_mult,
+                                           const int32_t* pad_pairs, int pad_capacity, const int32_t* pair_row,
+                                           const int32_t* pair_edge, int n_pair_slots, const void* edge_attr,
+                                           int ld_ea, const void* comp, const void* grad_msg,
+                                           const void* g_comp_add, void* g_edge_attr, void* g_comp, void* stream) {
+  if (!pair_row || !pair_edge || n_pair_slots < 0) return kBadArgument;
+  hipStream_t st = (hipStream_t)stream;
+  TN_DISPATCH(dtype, {
+    auto a = tn::base<T>(n_nodes, hidden, row_ptr, src, max_pairs, self0_mult, pad_pairs, pad_capacity);
+    a.prow = pair_row; a.pedge = pair_edge; a.np = n_pair_slots;
+    a.ea = (const T*)edge_attr; a.ldea = ld_ea;
+    a.Tc = (const T*)comp;
+    a.gmsg = (const T*)grad_msg; a.gea = (T*)g_edge_attr; a.gT = (T*)g_comp;
+    a.gTadd = (const T*)g_comp_add;
+    int rc = g_edge_attr ? tn::launch_msg_bwd_pair<T>(a, st) : kOk;
+    if (rc) return rc;
+    return g_comp ? tn::launch_msg_bwd_src<T>(a, st) : kOk;
+  })
 }

@@ -1217,65 +1217,56 @@ void proj_into(const Tensor& A, const Tensor& W, const Tensor& Wp, const Tensor&
 }
 
 // The stacked weights of one parameter set: per layer [q|k|v] (5H x H) and its bias, all layers' [dk; dv]
-// rows (L*D x R) + bias and their bf16 split.  Rebuilt only when a parameter's storage or version changes
-// (an MD engine evaluates one fixed model: one pack for the whole run).
-//
-// The key holds a WEAK reference to every parameter's StorageImpl besides its data pointer and version: a
-// weak reference keeps the StorageImpl object itself allocated (not its bytes), so once a model is freed
-// its entries expire and no later storage -- even one the caching allocator places at the same address
-// with the same version counts -- can match them.  In-place writes that bypass the version counter
-// (`p.data.copy_(...)`) are invisible here: call `torch.ops.tmdnet.et_stack_invalidate()` after them.
-struct PackKey {
-  c10::weak_intrusive_ptr<c10::StorageImpl> st;
-  const void* ptr;
-  int64_t ver;
-};
+// rows (L*D x R) + bias and their bf16 split.  Formed on EVERY call -- there is no cache that an in-place
+// write could leave stale (a fused optimizer step, `p.data.copy_`, an EMA swap: none bumps a version
+// counter that a cache could key on).  The Python stack (et_stack.py _stack_views) makes the parameters
+// row blocks of one buffer in exactly this layout, and TorchMD_ET stacks them before it calls this operator
+// (eager eval and __prepare_scriptable__), so the stacked weights are VIEWS of the parameters' own storage:
+// no copy, always current.  Parameters stored separately (e.g. after `.to()` of a scripted module) are
+// concatenated per call.  The dk/dv weights' bf16 split is one launch per call.
 struct Packed {
-  std::vector<PackKey> key;
   std::vector<Tensor> qkv_w, qkv_b;
   Tensor dkv_w, dkv_b, dkv_wp;
 };
 
-static std::mutex g_pack_mu;
-static std::shared_ptr<Packed> g_pack_last;
-
-static bool pack_matches(const Packed& pk, const std::vector<Tensor>& P) {
-  if (pk.key.size() != P.size()) return false;
-  for (size_t i = 0; i < P.size(); ++i) {
-    const PackKey& k = pk.key[i];
-    if (k.ptr != P[i].data_ptr() || k.ver != P[i]._version()) return false;
-    auto live = k.st.lock();  // null once the storage was freed
-    if (!live || live.get() != P[i].storage().unsafeGetStorageImpl()) return false;
+// ts as consecutive row blocks of one storage (same dtype / device / trailing shape, contiguous, adjacent):
+// that span as one tensor (a view); otherwise their concatenation (a copy)
+static Tensor stacked_or_cat(const std::vector<Tensor>& ts) {
+  const Tensor& a = ts[0];
+  const int64_t row = a.dim() > 1 ? a.numel() / std::max<int64_t>(a.size(0), 1) : 1;
+  bool ok = a.is_contiguous();
+  int64_t rows = 0;
+  for (const auto& t : ts) {
+    ok = ok && t.is_contiguous() && t.dim() == a.dim() && t.scalar_type() == a.scalar_type() &&
+         t.device() == a.device() && t.storage().unsafeGetStorageImpl() == a.storage().unsafeGetStorageImpl() &&
+         t.storage_offset() == a.storage_offset() + rows * row;
+    for (int64_t d = 1; ok && d < a.dim(); ++d) ok = t.size(d) == a.size(d);
+    if (!ok) break;
+    rows += t.size(0);
   }
-  return true;
+  if (!ok) return at::cat(ts, 0).contiguous();
+  std::vector<int64_t> sz(a.sizes().begin(), a.sizes().end());
+  sz[0] = rows;
+  return a.as_strided(sz, a.strides(), a.storage_offset());
 }
 
-void et_stack_invalidate() {
-  std::lock_guard<std::mutex> lock(g_pack_mu);
-  g_pack_last.reset();
-}
+void et_stack_invalidate() {}  // (kept for callers of the old cached form: nothing is cached any more)
 
 std::shared_ptr<Packed> pack_stack(const std::vector<Tensor>& P, int64_t L, int64_t np, bool hk, bool hv) {
-  std::lock_guard<std::mutex> lock(g_pack_mu);
-  if (g_pack_last && pack_matches(*g_pack_last, P)) return g_pack_last;
   auto pk = std::make_shared<Packed>();
-  pk->key.reserve(P.size());
-  for (const auto& t : P)
-    pk->key.push_back(PackKey{c10::weak_intrusive_ptr<c10::StorageImpl>(t.storage().getWeakStorageImpl()),
-                              t.data_ptr(), t._version()});
   at::NoGradGuard ng;
   std::vector<Tensor> dw, db;
   for (int64_t l = 0; l < L; ++l) {
     const Tensor* p = P.data() + l * np;
-    pk->qkv_w.push_back(at::cat({p[2], p[4], p[6]}, 0).contiguous());
-    pk->qkv_b.push_back(at::cat({p[3], p[5], p[7]}, 0).contiguous());
+    pk->qkv_w.push_back(stacked_or_cat({p[2], p[4], p[6]}));
+    pk->qkv_b.push_back(stacked_or_cat({p[3], p[5], p[7]}));
     int64_t i = 11;
     if (hk) { dw.push_back(p[i]); db.push_back(p[i + 1]); i += 2; }
     if (hv) { dw.push_back(p[i]); db.push_back(p[i + 1]); }
   }
   if (!dw.empty()) {
-    pk->dkv_w = at::cat(dw, 0).contiguous();
-    pk->dkv_b = at::cat(db, 0).contiguous();
+    pk->dkv_w = stacked_or_cat(dw);
+    pk->dkv_b = stacked_or_cat(db);
     const int N = static_cast<int>(pk->dkv_w.size(0)), K = static_cast<int>(pk->dkv_w.size(1));
     if (pk->dkv_w.scalar_type() == at::kFloat && (K == 32 || K == 64) && N % 16 == 0) {
       Tensor wp = at::empty({3, N, K}, pk->dkv_w.options().dtype(at::kShort));
@@ -1286,7 +1277,6 @@ std::shared_ptr<Packed> pack_stack(const std::vector<Tensor>& P, int64_t L, int6
       }
     }
   }
-  g_pack_last = pk;
   return pk;
 }
 
@@ -2255,7 +2245,7 @@ TORCH_LIBRARY(tmdnet, m) {
   m.def("et_stack(Tensor x, Tensor f, Tensor dist, Tensor cutoff, Tensor unit, Tensor mu, Tensor beta, "
         "Tensor row_ptr, Tensor src, Tensor dst, float cutoff_lower, float cutoff_upper, int rbf_type, int heads, "
         "bool has_dk, bool has_dv, bool out_norm, Tensor[] params, int acts=0) -> (Tensor x, Tensor vec)");
-  // drops the packed-weight cache of et_stack (after in-place writes that bypass the version counter)
+  // (no-op: et_stack forms its stacked weights on every call; kept for callers of the cached form)
   m.def("et_stack_invalidate() -> ()", tmdt::et_stack_invalidate);
   // the large-system switches of et_energy_forces (Morton renumbering from min_atoms atoms, the fused
   // projection kernels from min_edges edges; < 0 keeps a value); returns the previous values

@@ -81,6 +81,8 @@ SIGNATURES = {
     "tmdnet_tn_message_fwd": (I, [I, I, I, P, P, I, D, P, I, P, I, P, P, P]),
     "tmdnet_tn_message_bwd": (I, [I, I, I, P, P, I, D, P, I, P, I, P, P, P, P, P]),
     "tmdnet_tn_message_bwd_add": (I, [I, I, I, P, P, I, D, P, I, P, I, P, P, P, P, P, P]),
+    "tmdnet_tn_message_fwd_pairs": (I, [I, I, I, P, P, I, D, P, I, P, P, I, P, P, P]),
+    "tmdnet_tn_message_bwd_pairs": (I, [I, I, I, P, P, I, D, P, I, P, P, I, P, I, P, P, P, P, P, P]),
     "tmdnet_tn_node_fwd": (I, [I, I, I, I, P, P, P, P]),
     "tmdnet_tn_node_bwd": (I, [I, I, I, I, P, P, P, P, P, P, P]),
     "tmdnet_tn_node_bwd2": (I, [I, I, I, I, P, P, P, P, P, P, P, P, P]),
@@ -90,6 +92,7 @@ SIGNATURES = {
     "tmdnet_atom_sum_bwd": (I, [I, I, I, P, P, P, P, P]),
     "tmdnet_dot_sum_fwd": (I, [I, I, I, P, I, P, P, I, P, P, P, P, P]),
     "tmdnet_dot_sum_bwd": (I, [I, I, I, P, P, I, P, P, P, P]),
+    "tmdnet_dot_sum_fwd_atoms": (I, [I, I, I, P, I, P, P, I, P, P, P, P, P, P]),
     "tmdnet_layernorm_fwd_f32": (I, [I, I, P, I, P, P, D, P, I, P, P, P]),
     "tmdnet_layernorm_bwd_f32": (I, [I, I, P, I, P, P, P, P, I, P, I, P]),
     "tmdnet_layernorm_wgrad_workspace_bytes": (SZ, [I, I]),
@@ -104,6 +107,7 @@ SIGNATURES = {
     "tmdnet_proj_split_f32": (I, [I, I, P, I, P, P]),
     "tmdnet_split_t_f32": (I, [I, I, P, I, P, P]),
     "tmdnet_gemm_x3_f32": (I, [I, I, I, P, I, P, P, P, I, I, P]),
+    "tmdnet_gemm_x3_ex_f32": (I, [I, I, I, P, I, P, P, P, I, I, I, P, P, P, I, P]),
     "tmdnet_fep_image_bytes": (SZ, [I, I]),
     "tmdnet_fep_split_f32": (I, [I, I, P, I, P, P, P, P, P]),
     "tmdnet_et_fused_bwd_f32": (I, [I, I, I, I, P, P, I, P, I, P, I, P, I, P, P, P, P, P, P, ctypes.c_longlong, P, P, P,
@@ -145,10 +149,10 @@ def load_torch_ops():
 
 
 def invalidate_stack_cache():
-    """Drop the C++ ``tmdnet::et_stack`` operator's packed-weight cache (torch_ops.cpp ``pack_stack``: keyed on
-    each parameter's storage, data pointer and version counter).  Fused optimizers (``AdamW(fused=True)``)
-    update parameters in place WITHOUT bumping their version counters, so every optimizer step of this
-    package calls this.  No-op while the operator library is not loaded."""
+    """No-op kept for compatibility: the C++ ``tmdnet::et_stack`` operator used to cache packed weights keyed
+    on parameter versions (which fused optimizers and ``p.data`` writes do not bump); it now takes them as
+    views of the parameters' own storage on every call (torch_ops.cpp ``pack_stack``), so nothing can go
+    stale."""
     if _torch_ops_loaded:
         torch.ops.tmdnet.et_stack_invalidate()
 

@@ -1413,6 +1413,25 @@ class _ETStackBwd(Function):
         return (None,) * 7 + tuple(res)
 
 
+def stack_parameters(layers):
+    """Make every layer's [q|k|v] weights / biases and all layers' [dk; dv] weights / biases row blocks of
+    shared buffers (``_stack_views``; no-op when they already are).  Returns (dkv_w, dkv_b, [(qkv_w, qkv_b)]).
+    The C++ ``tmdnet::et_stack`` / ``et_energy_forces`` operators then take these blocks as views of the
+    parameters' own storage (torch_ops.cpp ``pack_stack``): nothing is packed or cached, so optimizer steps
+    and ``p.data`` writes are seen on the next call."""
+    sw = getattr(layers, "_tmd_stack", None)
+    if sw is None or sw.layers is not layers:
+        sw = StackWeights(layers)
+        layers._tmd_stack = sw
+    dkv_w, dkv_b = sw.dkv()
+    fused = []
+    for layer in layers:
+        if layer._stacked is None:
+            layer._stacked = LayerWeights(layer)
+        fused.append(layer._stacked.fused())
+    return dkv_w, dkv_b, fused
+
+
 def et_stack(layers, x, graph, f, C, u, rbf=None, out_norm=None, f_pairs=None, fdp_pairs=None):
     """Run ``layers`` (EquivariantMultiHeadAttention modules) as one node.  Returns (x, vec) after
     the last residual update (reference torchmd_et.py:180-184).
@@ -1425,17 +1444,10 @@ def et_stack(layers, x, graph, f, C, u, rbf=None, out_norm=None, f_pairs=None, f
     l0 = layers[0]
     H, heads = l0.hidden_channels, l0.num_heads
     hk, hv = l0.dk_proj is not None, l0.dv_proj is not None
-    fused, params = [], []
-    sw = getattr(layers, "_tmd_stack", None)
-    if sw is None or sw.layers is not layers:
-        sw = StackWeights(layers)
-        layers._tmd_stack = sw
-    dkv_w, dkv_b = sw.dkv()
+    params = []
+    dkv_w, dkv_b, fused = stack_parameters(layers)
     for layer in layers:
         layer._check_supported()
-        if layer._stacked is None:
-            layer._stacked = LayerWeights(layer)
-        fused.append(layer._stacked.fused())
         params += layer_params(layer)
     D = (int(hk) + 3 * int(hv)) * H
     batched = D > 0 and graph.n_edges * len(layers) * D * x.element_size() <= BATCH_DKV_BYTES

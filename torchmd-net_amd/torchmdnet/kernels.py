@@ -1473,17 +1473,22 @@ def _al16(*ts):
     return all(t is None or (t.data_ptr() % 16 == 0) for t in ts)
 
 
-def gemm_x3(A, B, tb, bias, C, beta):
+def gemm_x3(A, B, tb, bias, C, beta, act=0, pre=None, rscale=None, dpre=None):
     """``C = beta C + A op(B) + bias`` on ``tmdnet_gemm_x3_f32`` for large row counts: op(B) = B^T for a
     [N][K] Linear weight (split once per call, tmdnet_proj_split_f32), B for a [K][N] right operand
-    (tmdnet_split_t_f32).  Returns False (nothing launched) outside its envelope (non-fp32, K % 32,
+    (tmdnet_split_t_f32).  ``act`` / ``pre`` / ``rscale`` / ``dpre``: tmdnet_gemm_ex_f32's epilogue
+    (tmdnet_gemm_x3_ex_f32).  Returns False (nothing launched) outside its envelope (non-fp32, K % 32,
     N % 16, strides / alignment); the caller then uses the library GEMM."""
     M, K = A.shape
     N = C.shape[1]
+    x = pre if pre is not None else dpre
     if not (GEMM_BIG == "x3" and A.is_cuda and A.dtype == torch.float32 and B.dtype == torch.float32
             and C.dtype == torch.float32 and M > 0 and K % 32 == 0 and N % 16 == 0 and A.stride(1) == 1
             and B.stride(1) == 1 and C.stride(1) == 1 and A.stride(0) % 4 == 0 and C.stride(0) % 4 == 0
-            and B.stride(0) % 4 == 0 and (bias is None or bias.is_contiguous()) and _al16(A, B, C, bias)):
+            and B.stride(0) % 4 == 0 and (bias is None or bias.is_contiguous()) and _al16(A, B, C, bias, pre, dpre)
+            and (x is None or (x.stride(1) == 1 and x.stride(0) % 4 == 0 and x.shape == C.shape))
+            and (pre is None or dpre is None or pre.stride(0) == dpre.stride(0))
+            and (rscale is None or (rscale.is_contiguous() and rscale.dtype == torch.float32))):
         return False
     lib = nat.load()
     st = nat.stream(A.device)
@@ -1495,12 +1500,13 @@ def gemm_x3(A, B, tb, bias, C, beta):
     if rc == GEMM_UNSUPPORTED:
         return False
     nat.check(rc, "tmdnet_split")
-    rc = lib.tmdnet_gemm_x3_f32(M, N, K, A.data_ptr(), A.stride(0), bp.data_ptr(),
-                                None if bias is None else bias.data_ptr(), C.data_ptr(), C.stride(0), int(bool(beta)),
-                                st)
+    rc = lib.tmdnet_gemm_x3_ex_f32(M, N, K, A.data_ptr(), A.stride(0), bp.data_ptr(),
+                                   None if bias is None else bias.data_ptr(), C.data_ptr(), C.stride(0),
+                                   int(bool(beta)), int(act), nat.ptr(pre), nat.ptr(rscale), nat.ptr(dpre),
+                                   0 if x is None else x.stride(0), st)
     if rc == GEMM_UNSUPPORTED:
         return False
-    nat.check(rc, "tmdnet_gemm_x3_f32")
+    nat.check(rc, "tmdnet_gemm_x3_ex_f32")
     return True
 
 
@@ -1700,9 +1706,11 @@ class _DotSum(Function):
     def forward(ctx, h, w, b0, batch, n_mol, std, mean):
         lib = nat.load()
         y = torch.empty((n_mol, 1), dtype=h.dtype, device=h.device)
-        rc = lib.tmdnet_dot_sum_fwd(nat.dtype_code(h.dtype), h.shape[0], h.shape[1], nat.ptr(h), h.stride(0),
-                                    nat.ptr(w), nat.ptr(b0), n_mol, nat.ptr(batch), nat.ptr(std), nat.ptr(mean),
-                                    nat.ptr(y), nat.stream(h.device))
+        # large systems: the row products over the whole grid first (per-atom buffer)
+        buf = torch.empty(h.shape[0], dtype=h.dtype, device=h.device) if h.shape[0] > 4096 else None
+        rc = lib.tmdnet_dot_sum_fwd_atoms(nat.dtype_code(h.dtype), h.shape[0], h.shape[1], nat.ptr(h), h.stride(0),
+                                          nat.ptr(w), nat.ptr(b0), n_mol, nat.ptr(batch), nat.ptr(std),
+                                          nat.ptr(mean), nat.ptr(buf), nat.ptr(y), nat.stream(h.device))
         nat.check(rc, "tmdnet_dot_sum_fwd")
         ctx.n_mol = n_mol
         ctx.save_for_backward(h, w, b0, batch, std)
@@ -1846,22 +1854,43 @@ def tn_embed_bwd_launch(P, Q, W, C, u, graph, gE, gP, gQ, gW, gC, gu):
     nat.check(rc, "tmdnet_tn_embed_bwd")
 
 
-def tn_message_fwd_launch(ea, Tc, graph, out):
+def tn_message_fwd_launch(ea, Tc, graph, out, pairs=None):
+    """``pairs`` = (pair_row [E], pair_edge [P]) of ``pair_index``: ea holds one row per pair slot."""
     lib = nat.load()
     N, H = Tc.shape[1], Tc.shape[2]
+    if pairs is not None:
+        rc = lib.tmdnet_tn_message_fwd_pairs(nat.dtype_code(Tc.dtype), N, H, nat.ptr(graph.row_ptr),
+                                             nat.ptr(graph.src), graph.n_edges, *_self0_args(graph),
+                                             nat.ptr(pairs[0]), nat.ptr(ea), _ld(ea), nat.ptr(Tc), nat.ptr(out),
+                                             nat.stream(Tc.device))
+        nat.check(rc, "tmdnet_tn_message_fwd_pairs")
+        return
     rc = lib.tmdnet_tn_message_fwd(nat.dtype_code(Tc.dtype), N, H, nat.ptr(graph.row_ptr), nat.ptr(graph.src),
                                    graph.n_edges, *_self0_args(graph), nat.ptr(ea), _ld(ea), nat.ptr(Tc),
                                    nat.ptr(out), nat.stream(Tc.device))
     nat.check(rc, "tmdnet_tn_message_fwd")
 
 
-def tn_message_bwd_launch(ea, Tc, graph, gmsg, gea, gT, gadd=None):
+def tn_message_bwd_launch(ea, Tc, graph, gmsg, gea, gT, gadd=None, pairs=None):
     lib = nat.load()
     N, H = Tc.shape[1], Tc.shape[2]
+    if pairs is not None:
+        rc = lib.tmdnet_tn_message_bwd_pairs(nat.dtype_code(Tc.dtype), N, H, nat.ptr(graph.row_ptr),
+                                             nat.ptr(graph.src), graph.n_edges, *_self0_args(graph),
+                                             nat.ptr(pairs[0]), nat.ptr(pairs[1]), pairs[1].shape[0], nat.ptr(ea),
+                                             _ld(ea), nat.ptr(Tc), nat.ptr(gmsg), nat.ptr(gadd), nat.ptr(gea),
+                                             nat.ptr(gT), nat.stream(Tc.device))
+        nat.check(rc, "tmdnet_tn_message_bwd_pairs")
+        return
     rc = lib.tmdnet_tn_message_bwd_add(nat.dtype_code(Tc.dtype), N, H, nat.ptr(graph.row_ptr), nat.ptr(graph.src),
                                        graph.n_edges, *_self0_args(graph), nat.ptr(ea), _ld(ea), nat.ptr(Tc),
                                        nat.ptr(gmsg), nat.ptr(gadd), nat.ptr(gea), nat.ptr(gT), nat.stream(Tc.device))
     nat.check(rc, "tmdnet_tn_message_bwd_add")
+
+
+def _ea_edges(ea, pairs):
+    """Per-edge factor rows from pair rows (differentiable gather; the composite restatements)."""
+    return ea if pairs is None else ea.index_select(0, pairs[0].long())
 
 
 class _TNEmbed(Function):
@@ -1916,13 +1945,15 @@ class _TNEmbedBwd(Function):
 
 class _TNMessage(Function):
     """The message.  ``fanout``: also returns an alias of Tc for its second consumer (the POST pass); that
-    consumer's gradient is added by the message backward kernel (no separate add launch)."""
+    consumer's gradient is added by the message backward kernel (no separate add launch).  ``pairs``: ea is
+    given per pair slot (``pair_index``), its gradient likewise."""
 
     @staticmethod
-    def forward(ctx, ea, Tc, graph, fanout):
+    def forward(ctx, ea, Tc, graph, fanout, pairs=None):
         msg = torch.empty_like(Tc)
-        tn_message_fwd_launch(ea, Tc, graph, msg)
+        tn_message_fwd_launch(ea, Tc, graph, msg, pairs)
         ctx.graph = graph
+        ctx.pairs = pairs
         ctx.save_for_backward(ea, Tc)
         if fanout:
             return msg, Tc.view_as(Tc)
@@ -1934,21 +1965,21 @@ class _TNMessage(Function):
         if gmsg is None:
             gmsg = torch.zeros_like(Tc)
         gadd = None if galias is None else galias.contiguous()
-        outs = _TNMessageBwd.apply(gmsg.contiguous(), ea, Tc, ctx.graph, gadd)
-        return tuple(outs) + (None, None)
+        outs = _TNMessageBwd.apply(gmsg.contiguous(), ea, Tc, ctx.graph, gadd, ctx.pairs)
+        return tuple(outs) + (None, None, None)
 
 
 class _TNMessageBwd(Function):
     @staticmethod
-    def forward(ctx, gmsg, ea, Tc, graph, gadd):
+    def forward(ctx, gmsg, ea, Tc, graph, gadd, pairs=None):
         if not graph.symmetric:
             raise RuntimeError("torchmd-net_amd: TensorNet backward needs a symmetric edge list")
-        E = graph.n_edges
         H = Tc.shape[2]
-        gea = torch.empty((E, 3 * H), dtype=Tc.dtype, device=Tc.device)
+        gea = torch.empty((ea.shape[0], 3 * H), dtype=Tc.dtype, device=Tc.device)
         gT = torch.empty_like(Tc)
-        tn_message_bwd_launch(ea, Tc, graph, gmsg, gea, gT, gadd)
+        tn_message_bwd_launch(ea, Tc, graph, gmsg, gea, gT, gadd, pairs)
         ctx.graph = graph
+        ctx.pairs = pairs
         ctx.has_add = gadd is not None
         ctx.save_for_backward(gmsg, ea, Tc)
         return gea, gT
@@ -1960,18 +1991,18 @@ class _TNMessageBwd(Function):
         g_add = ggs[1] if ctx.has_add else None  # gT = VJP(gmsg) + gadd: identity in gadd
         from . import tn_node
         if tn_node.SECOND_ORDER != "composite" and not _create:
-            return _tn_message_second_order(ctx, saved, ggs) + (None, g_add)
+            return _tn_message_second_order(ctx, saved, ggs) + (None, g_add, None)
         with torch.enable_grad():
             leaves = [t.detach().requires_grad_(True) for t in saved]
             gmsg, ea, Tc = leaves
-            msg = tn_message_composite(ea, Tc, ctx.graph)
+            msg = tn_message_composite(_ea_edges(ea, ctx.pairs), Tc, ctx.graph)
             first = torch.autograd.grad(msg, (ea, Tc), gmsg, create_graph=True)
             sel = [(f, g) for f, g in zip(first, ggs) if g is not None]
             if not sel:
-                return (None,) * 4 + (g_add,)
+                return (None,) * 4 + (g_add, None)
             second = torch.autograd.grad([f for f, _ in sel], leaves, [g for _, g in sel],
                                          create_graph=_create, allow_unused=True)
-        return tuple(second) + (None, g_add)
+        return tuple(second) + (None, g_add, None)
 
 
 def _tn_message_second_order(ctx, saved, ggs):
@@ -1980,10 +2011,12 @@ def _tn_message_second_order(ctx, saved, ggs):
     (d_ea, d_T) = (G(gmsg, t_T), M^T(t_ea, gmsg)) -- ONE first-backward launch with (t_ea, t_T) in place of
     (ea, Tc).  The first backward's pair-symmetry precondition then applies to t_ea: the edge factors'
     cotangent is, like the factors, a function of the pair distance (edge MLP -> rbf -> r, whose
-    cotangent <t_pos[src] - t_pos[dst], u> is the same for both directions of a pair)."""
+    cotangent <t_pos[src] - t_pos[dst], u> is the same for both directions of a pair).  (Pair rows: t_ea is
+    per pair slot, the same kernels with pair_row.)"""
     gmsg, ea, Tc = saved
     t_ea, t_T = ggs
     graph = ctx.graph
+    pairs = ctx.pairs
     need = ctx.needs_input_grad  # gmsg, ea, Tc, graph, gadd
     if t_ea is None and t_T is None:
         return None, None, None
@@ -1992,15 +2025,15 @@ def _tn_message_second_order(ctx, saved, ggs):
     d_g = None
     if need[0]:
         d_g = torch.empty_like(Tc)
-        tn_message_fwd_launch(t_ea, Tc, graph, d_g)
+        tn_message_fwd_launch(t_ea, Tc, graph, d_g, pairs)
         tmp = torch.empty_like(Tc)
-        tn_message_fwd_launch(ea, t_T, graph, tmp)
+        tn_message_fwd_launch(ea, t_T, graph, tmp, pairs)
         d_g.add_(tmp)
     d_ea = d_T = None
     if need[1] or need[2]:
-        d_ea = torch.empty((graph.n_edges, 3 * Tc.shape[2]), dtype=Tc.dtype, device=Tc.device)
+        d_ea = torch.empty((ea.shape[0], 3 * Tc.shape[2]), dtype=Tc.dtype, device=Tc.device)
         d_T = torch.empty_like(Tc)
-        tn_message_bwd_launch(t_ea, t_T, graph, gmsg, d_ea, d_T)
+        tn_message_bwd_launch(t_ea, t_T, graph, gmsg, d_ea, d_T, pairs=pairs)
     return d_g, (d_ea if need[1] else None), (d_T if need[2] else None)
 
 
@@ -2010,11 +2043,12 @@ def tn_embed(P, Q, W, C, u, graph):
     return _TNEmbed.apply(P.contiguous(), Q.contiguous(), _rowmajor(W), C.contiguous(), u.contiguous(), graph)
 
 
-def tn_message(ea, Tc, graph, fanout=False):
+def tn_message(ea, Tc, graph, fanout=False, pairs=None):
     """Tensor message passing on a compact [9, N, H] tensor -> compact message (``fanout``: and an alias
-    of Tc for its second consumer, whose gradient the message backward adds)."""
+    of Tc for its second consumer, whose gradient the message backward adds).  ``pairs`` = ``pair_index``'s
+    (pair_row, pair_edge): ea has one row per pair slot (large systems: the edge MLP runs per pair)."""
     nat.require_gpu(Tc, "tn_message")
-    return _TNMessage.apply(_rowmajor(ea), Tc.contiguous(), graph, fanout)
+    return _TNMessage.apply(_rowmajor(ea), Tc.contiguous(), graph, fanout, pairs)
 
 
 # ----------------------------------------------------------------------------- spatial order
@@ -2528,6 +2562,16 @@ def gemm_ex_launch(problems):
     outside the kernel's envelope (nothing launched)."""
     if not problems or len(problems) > 4:
         return False
+    if any(p["A"].shape[0] > GEMM_MAX_ROWS for p in problems):
+        # large systems: one tmdnet_gemm_x3_ex_f32 launch per problem (same epilogue), all or nothing
+        ok = [_x3_ex_ok(p) for p in problems]
+        if not all(ok):
+            return False
+        for p in problems:
+            if not gemm_x3(p["A"], p["B"], p.get("trans_b", True), p.get("bias"), p["C"], p.get("beta"),
+                           act=int(p.get("act", 0)), pre=p.get("pre"), rscale=p.get("rscale"), dpre=p.get("dpre")):
+                raise RuntimeError("gemm_ex_launch: tmdnet_gemm_x3_ex_f32 refused a checked problem")
+        return True
     for p in problems:
         A, C = p["A"], p["C"]
         if (A.dtype != torch.float32 or not A.is_cuda or not 0 < A.shape[0] <= GEMM_MAX_ROWS or A.shape[1] == 0
@@ -2552,6 +2596,18 @@ def gemm_ex_launch(problems):
         return False
     nat.check(rc, "tmdnet_gemm_ex_f32")
     return True
+
+
+def _x3_ex_ok(p):
+    """Whether gemm_x3 takes problem p (the x3 kernel's envelope, checked before anything launches)."""
+    A, B, C = p["A"], p["B"], p["C"]
+    bias, x = p.get("bias"), (p.get("pre") if p.get("pre") is not None else p.get("dpre"))
+    return (GEMM_BIG == "x3" and A.is_cuda and all(t.dtype == torch.float32 for t in (A, B, C))
+            and A.shape[0] > 0 and A.shape[1] % 32 == 0 and C.shape[1] % 16 == 0
+            and A.stride(1) == 1 and B.stride(1) == 1 and C.stride(1) == 1
+            and A.stride(0) % 4 == 0 and B.stride(0) % 4 == 0 and C.stride(0) % 4 == 0
+            and (bias is None or bias.is_contiguous()) and _al16(A, B, C, bias, p.get("pre"), p.get("dpre"))
+            and (x is None or (x.stride(1) == 1 and x.stride(0) % 4 == 0 and x.shape == C.shape)))
 
 
 def _mlp_composite(x, scale, *wb):
@@ -2672,9 +2728,12 @@ def mlp_act(x, weights, biases, act, scale=None):
     """``act(... act(x W_0^T + b_0) ...) * scale[:, None]`` for nn.Linear weights / biases: the hand
     fused path for SiLU on fp32 CUDA rows within the GEMM envelope, else Linear + fused_act per layer."""
     L = len(weights)
+    # (above GEMM_MAX_ROWS rows every GEMM runs on tmdnet_gemm_x3_ex_f32, which needs K % 32 in both directions)
+    big = x.dim() == 2 and x.shape[0] > GEMM_MAX_ROWS
+    mod = 32 if big else 16
     ok = (MLP_ACT and isinstance(act, torch.nn.SiLU) and x.is_cuda and x.dtype == torch.float32 and x.dim() == 2
-          and 0 < x.shape[0] <= GEMM_MAX_ROWS and all(b is not None for b in biases)
-          and all(w.shape[1] % 16 == 0 for w in weights) and all(w.shape[0] % 16 == 0 for w in weights))
+          and 0 < x.shape[0] and (not big or GEMM_BIG == "x3") and all(b is not None for b in biases)
+          and all(w.shape[1] % mod == 0 for w in weights) and all(w.shape[0] % mod == 0 for w in weights))
     if ok:
         # tmdnet_gemm_ex_f32 also needs 16-byte aligned operands (a contiguous view with a storage offset
         # may not be): realign x by a copy, take the composite for misaligned weights

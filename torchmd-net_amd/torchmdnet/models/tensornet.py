@@ -8,6 +8,7 @@ scatter over ``edge_index[0]`` becomes a CSR walk of the reversed rows (no atomi
 neighbour slots become extra (0, 0) edges with r = 0 (tensornet.py:215-221), applied here as a
 multiplicity on atom 0's self loop.
 """
+import os
 from typing import List, Optional, Tuple
 
 import torch
@@ -18,6 +19,13 @@ from .utils import CosineCutoff, OptimizedDistance, act_class_mapping, as_graph,
 
 # reference tensornet.py:13-14 sets TF32 matmul globally; gfx950 has no TF32/xf32 path, so fp32
 # GEMMs stay exact fp32 here.
+
+# Large systems (C5: the 50k-atom water box, ~2M edges): the Interaction's edge MLP (reference
+# tensornet.py:381-385, a function of |r| only) runs once per edge PAIR -- (E + N) / 2 rows instead of E --
+# on the x3 GEMM with SiLU / cutoff epilogues, and the message reads the pair rows (tmdnet_tn_message_*_pairs).
+# From this many edges on; TMDNET_TN_PAIRS=0 keeps per-edge rows (A/B).
+PAIR_MIN_EDGES = 131072
+PAIRS = os.environ.get("TMDNET_TN_PAIRS", "1") != "0"
 
 
 def vector_to_skewtensor(vector):
@@ -353,6 +361,15 @@ class Interaction(nn.Module):
             edge_weight, edge_attr = edge_weight[perm], edge_attr[perm]
         C = graph.cutoff if (perm is None and graph.cutoff is not None) else self.cutoff(edge_weight)
         ls = self.linears_scalar  # act(Linear) x 3, the last times C (reference 381-385), one launch per layer
+        pairs = None
+        if (PAIRS and perm is None and X.is_cuda and graph.n_edges >= PAIR_MIN_EDGES and graph.symmetric
+                and graph.transpose is not None):
+            # one MLP row per edge pair (the factors depend on |r| only): gather the pairs' rbf / cutoff rows
+            pairs = kernels.pair_index(graph)
+            pe = getattr(graph, "_pair_edge_long", None)
+            if pe is None:
+                pe = graph._pair_edge_long = pairs[1].long()
+            edge_attr, C = edge_attr.index_select(0, pe), C.index_select(0, pe)
         edge_attr = kernels.mlp_act(edge_attr, [m.weight for m in ls], [m.bias for m in ls], self.act, C)
         lt = self.linears_tensor
         # X / (|X|^2 + 1), decompose, three channel mixes -> Y as compact [9, N, H] (I | A | S rows)
@@ -360,7 +377,7 @@ class Interaction(nn.Module):
         # backward kernels instead of separate autograd add launches)
         Xp, X = tn_node.pre(X, fanout=True)
         Yc = tn_node.mix3(Xp, lt[0].weight, lt[1].weight, lt[2].weight)
-        msg, Yc = kernels.tn_message(edge_attr, Yc, graph, fanout=True)
+        msg, Yc = kernels.tn_message(edge_attr, Yc, graph, fanout=True, pairs=pairs)
         # decompose(msg Y + Y msg) (O(3)) or decompose(2 Y msg) (SO(3)), / (|.|^2 + 1), three mixes
         Dc = tn_node.mix3(tn_node.post(Yc, msg, self.equivariance_invariance_group),
                           lt[3].weight, lt[4].weight, lt[5].weight)

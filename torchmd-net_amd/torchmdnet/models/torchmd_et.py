@@ -30,9 +30,9 @@ NE_FUSED = os.environ.get("TMDNET_NE_FUSED", "1") != "0"
 # _ETStack / _ETStackBwd, whose launch orchestration costs ~2 ms of host time per C2 evaluation.  Training
 # (train mode: the force-loss second order is hand-written on the Python side) and HIP-graph capture keep
 # the Python stack.  C2 eval 2.84 -> 2.17 ms eager; energies / forces equal to the Python stack's to 1e-7.
-# The operator caches its packed weights by parameter version: the package's optimizer steps invalidate it
-# (fused AdamW does not bump versions; _native.invalidate_stack_cache).  TMDNET_ET_CPP_EAGER=0 keeps the Python
-# stack everywhere.
+# The operator caches nothing: its stacked weights are views of the parameters' own storage (stacked here
+# before every call, et_stack.stack_parameters), so optimizer steps of any kind and ``p.data`` writes are
+# seen by the next evaluation.  TMDNET_ET_CPP_EAGER=0 keeps the Python stack everywhere.
 CPP_EAGER = os.environ.get("TMDNET_ET_CPP_EAGER", "1") != "0"
 
 
@@ -103,6 +103,9 @@ class TorchMD_ET(nn.Module):
     def __prepare_scriptable__(self):
         for attn in self.attention_layers:
             attn._check_supported()
+        if len(self.attention_layers) > 0:
+            # the scripted operators take the stacked weights as views of the parameters (torch_ops.cpp pack_stack)
+            et_stack_mod.stack_parameters(self.attention_layers)
         return self
 
     def forward(self, z: Tensor, pos: Tensor, batch: Tensor, q: Optional[Tensor] = None,
@@ -300,6 +303,7 @@ class TorchMD_ET(nn.Module):
         """The interaction layers as ``tmdnet::et_stack`` (see CPP_EAGER)."""
         from .. import _native
         _native.load_torch_ops()
+        et_stack_mod.stack_parameters(self.attention_layers)  # (views, not copies: see CPP_EAGER)
         r, mu, beta, cl, cu, rbf_type = rbf
         params = []
         hk = hv = False
