@@ -297,6 +297,71 @@ def probe_workload(n_atoms, H, dev):
     return launch, E, L
 
 
+def tn_message_probe_setup(n_atoms, H, dev, static=False):
+    """The TensorNet message (tmdnet_tn_message_fwd_pairs / _bwd_pairs, csrc/tn_message.hip) on the C5 TensorNet
+    graph: a periodic n-atom water box, cutoff 4.5, cell list, Morton-renumbered as the model does, the edge
+    factors as the model's pair rows (one [3H] row per edge pair, kernels.pair_index).  Returns launchers of one
+    forward and one backward (pair destination pass + source pass) plus (E, N, P)."""
+    from torchmdnet import kernels
+    g = torch.Generator().manual_seed(7)
+    L = (n_atoms / 0.1003) ** (1.0 / 3.0)
+    pos = (torch.rand(n_atoms, 3, generator=g, dtype=torch.float64) * L).float().to(dev)
+    batch = torch.zeros(n_atoms, dtype=torch.long, device=dev)
+    box = torch.eye(3, dtype=torch.float32) * L
+    perm = kernels.spatial_permutation(pos, batch, 4.5, box)
+    pos = pos[perm].contiguous()
+    graph = kernels.build_graph(pos, batch, 0.0, 4.5, 64 * n_atoms, loop=True, strategy="cell", box=box)
+    pairs = kernels.pair_index(graph)
+    P = pairs[1].shape[0]
+    gen = torch.Generator(device=dev).manual_seed(3)
+    ea = torch.randn(P, 3 * H, device=dev, generator=gen)
+    Tc = torch.randn(9, n_atoms, H, device=dev, generator=gen)
+    msg = torch.empty_like(Tc)
+    bw = {}
+
+    def fwd():
+        kernels.tn_message_fwd_launch(ea, Tc, graph, msg, pairs)
+
+    def bwd():
+        if not bw:
+            bw["g"] = torch.randn(9, n_atoms, H, device=dev, generator=gen)
+            bw["gea"], bw["gT"] = torch.empty_like(ea), torch.empty_like(Tc)
+        kernels.tn_message_bwd_launch(ea, Tc, graph, bw["g"], bw["gea"], bw["gT"], pairs=pairs)
+
+    return fwd, bwd, graph.n_edges, n_atoms, P, L
+
+
+def tn_message_bytes(E, N, H, s=4):
+    """SURVEY.md 8(d) TensorNet message, per layer: E*(4 + 3H*s) + N*(9H*s + 9H*s + 4) -- src index and the
+    edge factor row per edge, the compact I/A/S tensor (9 per channel) read and the message written per node."""
+    return E * (4 + 3 * H * s) + N * (18 * H * s + 4)
+
+
+def tn_message_probe(a, dev):
+    H = a.channels
+    fwd, bwd, E, N, P, L = tn_message_probe_setup(a.roofline_atoms, H, dev)
+    ms = _event_ms(fwd, a.roofline_reps)
+    ms_b = _event_ms(bwd, max(4, a.roofline_reps // 2))
+    nb = tn_message_bytes(E, N, H)
+    pb = E * (4 + 4) + P * 3 * H * 4 + N * (18 * H * 4 + 4)  # distinct bytes in the pair layout
+    # backward: gmsg + Tc read per node, both endpoints' rows per pair, the pair gradient rows written; the
+    # source pass: factor rows per edge, gmsg rows, gT written
+    bb = E * 4 + N * (18 * H * 4) + P * 3 * H * 4 + (E * (4 + 3 * H * 4) + N * (18 * H * 4 + 4))
+    gbs = nb / (ms * 1e-3) / 1e9
+    return {"kernel": "tmdnet_tn_message_fwd_pairs (tn::k_msg_fwd<float,4>): TensorNet message passing, pair-row edge "
+                      "factors (the C5 TensorNet path, models/tensornet.py PAIR_MIN_EDGES)",
+            "workload": f"periodic water box, {N} atoms (Morton-renumbered), L={L:.1f} A, cutoff 4.5, E={E}, P={P} pair "
+                        f"rows, H={H}, fp32",
+            "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None, "bytes_per_launch": nb,
+            "bytes_formula": "SURVEY.md 8(d): E*(4 + 3H*4) + N*(18H*4 + 4)",
+            "pair_layout_distinct_bytes": pb, "ms_per_launch": round(ms, 4), "launches": a.roofline_reps,
+            "backward": {"kernels": "k_msg_bwd_pair (pair-owner destination pass) + k_msg_bwd_src",
+                         "ms_per_call": round(ms_b, 4), "bytes_per_call": bb,
+                         "achieved": round(bb / (ms_b * 1e-3) / 1e9, 1),
+                         "frac": round(bb / (ms_b * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}}
+
+
 def et_pair_bytes(E, N, P, H, s=4):
     """Algorithmic bytes of one forward edge-kernel launch in the model's layout (pair-shared dk/dv
     rows, et_stack.PAIR_ROWS): per edge its source index, pair-row index, cutoff and unit vector; the
@@ -328,7 +393,9 @@ PMC_PASSES = ("FETCH_SIZE", "WRITE_SIZE", "TCC_HIT_sum TCC_MISS_sum")
 PMC_CHILD = {"et::k_fwd<float, 4, 4, 1, false, false>": [("per_edge", 8), ("pairs", 8)],
              "et::k_bwd_dst<": [("bwd_dst", 4)], "et::k_bwd_src<": [("bwd_src", 4)], "et::k_bwd_merged<": [("bwd_dr", 4)],
              "fep::k_fwd<": [("fused_fwd", 8)], "fep::k_bwd_dst<": [("fused_bwd_dst", 4)],
-             "fep::k_bwd_src<": [("fused_bwd_src", 4)], "fep::k_edge_combine": [("fused_edge_combine", 4)]}
+             "fep::k_bwd_src<": [("fused_bwd_src", 4)], "fep::k_edge_combine": [("fused_edge_combine", 4)],
+             "tn::k_msg_fwd<": [("tn_msg_fwd", 8)], "tn::k_msg_bwd_pair<": [("tn_msg_bwd_pair", 4)],
+             "tn::k_msg_bwd_src<": [("tn_msg_bwd_src", 4)]}
 
 
 def pmc_counters(a):
@@ -484,6 +551,7 @@ def roofline_probe(a, dev):
                 tr = sum((pm.get(k) or {}).get("traffic") or 0 for k in keys)
                 if tr:
                     bwd[tag]["traffic_over_bytes"] = round(tr / bwd[tag]["bytes_per_call"], 3)
+            res["_tn_pmc"] = {k: pm.get(k) for k in ("tn_msg_fwd", "tn_msg_bwd_pair", "tn_msg_bwd_src")}
     return res
 
 
@@ -1264,6 +1332,13 @@ def main():
             for _ in range(4):
                 fp.bwd()
         torch.cuda.synchronize()
+        del launch, fp
+        tfwd, tbwd, *_ = tn_message_probe_setup(a.roofline_atoms, a.channels, dev)
+        for _ in range(8):
+            tfwd()
+        for _ in range(4):
+            tbwd()
+        torch.cuda.synchronize()
         return
     maybe_spawn(a)
     ws, rank, dev = setup_dist()
@@ -1400,6 +1475,19 @@ def main():
         gc.collect()
         torch.cuda.empty_cache()
         out["roofline"] = roofline_probe(a, dev)
+        tn_pmc = out["roofline"].pop("_tn_pmc", None)
+        gc.collect()
+        torch.cuda.empty_cache()
+        phase("roofline probe: TensorNet message (C5 TensorNet graph)")
+        tnr = tn_message_probe(a, dev)
+        if tn_pmc:
+            f = tn_pmc.get("tn_msg_fwd") or {}
+            tnr["traffic"] = f.get("traffic")
+            tnr["traffic_detail"] = {**f, "source": PMC_SOURCE}
+            if f.get("traffic"):
+                tnr["traffic_detail"]["traffic_over_bytes"] = round(f["traffic"] / tnr["bytes_per_launch"], 3)
+            tnr["backward"]["pmc"] = {k: tn_pmc.get(k) for k in ("tn_msg_bwd_pair", "tn_msg_bwd_src")}
+        out["roofline"]["tensornet_message"] = tnr
         phase("MFMA probe (dk/dv projection GEMM)")
         E_c5 = int(out["roofline"]["workload"].split("E=")[1].split(",")[0])
         E_c2, N_c2 = (int(probe[0][2]), int(probe[0][3])) if probe else (12548, 678)

@@ -704,6 +704,12 @@ int tmdnet_gemm_x3_f32(int M, int N, int K, const void* A, int lda, const void* 
 int tmdnet_gemm_x3_ex_f32(int M, int N, int K, const void* A, int lda, const void* Bp, const void* bias, void* C,
                           int ldc, int beta, int act, void* pre, const void* rscale, const void* dpre, int ldx,
                           void* stream);
+/* tmdnet_gemm_x3_ex_f32 with the right operand as fp32, split into its exact bf16 pieces inside the kernel
+ * while it is staged in LDS (no split launch, no cached pieces): trans_w = 1 -> W [N][K] (a Linear weight,
+ * C = A W^T), trans_w = 0 -> W [K][N] (C = A W); ldw % 4 == 0, W 16-byte aligned. */
+int tmdnet_gemm_x3w_f32(int M, int N, int K, const void* A, int lda, const void* W, int ldw, int trans_w,
+                        const void* bias, void* C, int ldc, int beta, int act, void* pre, const void* rscale,
+                        const void* dpre, int ldx, void* stream);
 int tmdnet_proj_split_f32(int N, int K, const void* W, int ldw, void* Wp, void* stream);
 int tmdnet_proj_f32(int M, int N, int K, const void* A, int lda, const void* Wp, long long piece_stride,
                     const void* bias, void* C, int ldc, void* stream);

@@ -135,15 +135,19 @@ def test_lnnp_step_broadcasts_and_keeps_replicas_identical():
     assert lr0 == lr1 == pytest.approx(1e-2)  # warm-up over 3 steps reached the base LR
 
 
-def _split_worker(rank, world, port, out):
+def _split_model(kind):
+    if kind == "last_largest":  # the last parameter holds most elements: the TAIL bucket is empty
+        return torch.nn.Sequential(torch.nn.Linear(8, 4), torch.nn.SiLU(), torch.nn.Linear(4, 300, bias=False))
+    return torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.SiLU(), torch.nn.Linear(16, 4), torch.nn.Linear(4, 1))
+
+
+def _split_worker(rank, world, port, out, kind="balanced"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from torchmdnet.training import GradAllReduce, SplitAdamW, _adamw, step_reduce
     torch.manual_seed(0)
-    model = torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.SiLU(), torch.nn.Linear(16, 4),
-                                torch.nn.Linear(4, 1))
-    ref = torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.SiLU(), torch.nn.Linear(16, 4),
-                              torch.nn.Linear(4, 1))
+    model = _split_model(kind)
+    ref = _split_model(kind)
     ref.load_state_dict(model.state_dict())
     red = GradAllReduce(model.parameters())
     tail, head = red.split_params()
@@ -162,22 +166,26 @@ def _split_worker(rank, world, port, out):
         red_ref()
         opt_ref.step()
     same = all(torch.equal(p, q) for p, q in zip(model.parameters(), ref.parameters()))
-    out.put((rank, same, len(tail) > 0 and len(head) > 0, seen, [p.detach().numpy() for p in model.parameters()]))
+    both = (len(tail) > 0 and len(head) > 0) if kind == "balanced" else (len(tail) == 0 and len(head) > 0)
+    out.put((rank, same, both, seen, [p.detach().numpy() for p in model.parameters()]))
     dist.destroy_process_group()
 
 
 @pytest.mark.timeout(120)
-def test_two_bucket_allreduce_overlapped_step_equals_fused():
+@pytest.mark.parametrize("kind", ["balanced", "last_largest"])
+def test_two_bucket_allreduce_overlapped_step_equals_fused(kind):
     """The two-bucket all-reduce with the tail bucket's AdamW update issued before the head bucket is
     reduced (training.step_reduce / SplitAdamW, world > 1) gives the SAME parameters as one fused
-    all-reduce + one AdamW, on every rank (replicas identical)."""
+    all-reduce + one AdamW, on every rank (replicas identical).  ``last_largest``: the last parameter holds
+    more than half of all elements, so the tail bucket is empty (the head optimizer must keep its
+    slot and step only after the head bucket is averaged)."""
     import sys
     from conftest import PKG
     sys.path.insert(0, PKG)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_split_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_split_worker, args=(r, 2, port, q, kind)) for r in range(2)]
     for p in procs:
         p.start()
     res = {r: rest for r, *rest in (q.get(timeout=100) for _ in procs)}

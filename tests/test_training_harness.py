@@ -127,6 +127,10 @@ def test_hdf5_format_with_stand_in_file():
     s = ds[3]
     assert s.z.tolist() == [1, 1] and s.y.shape == (1, 1) and s.neg_dy.shape == (2, 3)
     assert np.isclose(float(s.y), files["b.h5"]["g2"]["energy"][1], atol=1e-6)
+    # atom counts from the `types` shapes, in sample order, without reading arrays
+    assert ds.atom_counts() == [3, 3, 2, 2, 2] == [int(ds[i].z.shape[0]) for i in range(len(ds))]
+    from torchmdnet.module import _atom_counts
+    assert _atom_counts(torch.utils.data.Subset(ds, [4, 0])) == [2, 3]
 
 
 # ----------------------------------------------------------------------------- LNNP logic

@@ -865,8 +865,13 @@ struct XArgs {
   float* pre;
   const float* rscale;
   const float* dpre;
+  // WS != 0: the right operand as fp32, split into its three pieces while it is staged in LDS (no separate
+  // split launch, nothing cached that an in-place weight update could leave stale): WS = 1 a [N][K] Linear
+  // weight (C = A W^T), WS = 2 a [K][N] right operand (C = A W); row stride ldw
+  const float* W;
+  int ldw;
 };
-template <int MB, int BN, int PD>
+template <int MB, int BN, int PD, int WS = 0>
 __global__ __launch_bounds__(256) void k_gemm_x3(XArgs P) {
   // K chunk staged per barrier pair: 128 (64 at BN = 128) -> ~52 KB of LDS, 3 workgroups per CU
   constexpr int KC = BN >= 128 ? 64 : 128, LD = KC + 8, NB = BN / 16, SPC = KC / 32;
@@ -925,21 +930,76 @@ __global__ __launch_bounds__(256) void k_gemm_x3(XArgs P) {
           const int nks = min(KC, P.K - kc) / 32;
           constexpr int CH = KC / 8, NL = 3 * BN * CH / 256;
           const int ch = nks * 4;  // 16-byte chunks per row of this K chunk
-          u4 stg[NL];
+          if constexpr (WS == 0) {
+            u4 stg[NL];
 #pragma unroll
-          for (int i = 0; i < NL; ++i) {
-            const int c = threadIdx.x + 256 * i;
-            const int p = c / (BN * CH), rc = c % (BN * CH), n = rc / CH, k = (rc % CH) * 8;
-            stg[i] = k < 8 * ch
-                         ? *reinterpret_cast<const u4*>(P.Bp + p * ps + (size_t)min(n0 + n, P.N - 1) * P.K + kc + k)
-                         : u4{0u, 0u, 0u, 0u};
-          }
-          __syncthreads();  // the previous chunk's LDS reads are done
+            for (int i = 0; i < NL; ++i) {
+              const int c = threadIdx.x + 256 * i;
+              const int p = c / (BN * CH), rc = c % (BN * CH), n = rc / CH, k = (rc % CH) * 8;
+              stg[i] = k < 8 * ch
+                           ? *reinterpret_cast<const u4*>(P.Bp + p * ps + (size_t)min(n0 + n, P.N - 1) * P.K + kc + k)
+                           : u4{0u, 0u, 0u, 0u};
+            }
+            __syncthreads();  // the previous chunk's LDS reads are done
 #pragma unroll
-          for (int i = 0; i < NL; ++i) {
-            const int c = threadIdx.x + 256 * i;
-            const int p = c / (BN * CH), rc = c % (BN * CH), n = rc / CH, k = (rc % CH) * 8;
-            *reinterpret_cast<u4*>(&w[p][n][k]) = stg[i];
+            for (int i = 0; i < NL; ++i) {
+              const int c = threadIdx.x + 256 * i;
+              const int p = c / (BN * CH), rc = c % (BN * CH), n = rc / CH, k = (rc % CH) * 8;
+              *reinterpret_cast<u4*>(&w[p][n][k]) = stg[i];
+            }
+          } else if constexpr (WS == 1) {
+            // 8 consecutive k of one weight row per chunk: two 16-byte loads, split8 -> three 16-byte LDS stores
+            constexpr int NC = BN * CH / 256;
+            float4 lo[NC], hi[NC];
+#pragma unroll
+            for (int i = 0; i < NC; ++i) {
+              const int c = threadIdx.x + 256 * i;
+              const int n = c / CH, k = (c % CH) * 8;
+              if (k < 8 * ch) {
+                const float* r = P.W + (size_t)min(n0 + n, P.N - 1) * P.ldw + kc + k;
+                lo[i] = *reinterpret_cast<const float4*>(r);
+                hi[i] = *reinterpret_cast<const float4*>(r + 4);
+              } else {
+                lo[i] = hi[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+              }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < NC; ++i) {
+              const int c = threadIdx.x + 256 * i;
+              const int n = c / CH, k = (c % CH) * 8;
+              bf8 f[3];
+              split8(lo[i], hi[i], f);
+#pragma unroll
+              for (int p = 0; p < 3; ++p) *reinterpret_cast<bf8*>(&w[p][n][k]) = f[p];
+            }
+          } else {
+            // W [K][N]: 4 consecutive n of one k row per 16-byte load, written transposed (2-byte LDS stores)
+            constexpr int NC = KC * BN / 4 / 256, QN = BN / 4;
+            float4 v[NC];
+#pragma unroll
+            for (int i = 0; i < NC; ++i) {
+              const int c = threadIdx.x + 256 * i;
+              const int k = c / QN, n4 = (c % QN) * 4;
+              v[i] = (k < 32 * nks && n0 + n4 < P.N)
+                         ? *reinterpret_cast<const float4*>(P.W + (size_t)(kc + k) * P.ldw + n0 + n4)
+                         : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < NC; ++i) {
+              const int c = threadIdx.x + 256 * i;
+              const int k = c / QN, n4 = (c % QN) * 4;
+              const float x[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+#pragma unroll
+              for (int j = 0; j < 4; ++j) {
+                unsigned h, m, l;
+                split3(x[j], h, m, l);
+                w[0][n4 + j][k] = (unsigned short)(h >> 16);
+                w[1][n4 + j][k] = (unsigned short)(m >> 16);
+                w[2][n4 + j][k] = (unsigned short)(l >> 16);
+              }
+            }
           }
           __syncthreads();
         }
@@ -1594,10 +1654,33 @@ extern "C" int tmdnet_gemm_x3_f32(int M, int N, int K, const void* A, int lda, c
 // tmdnet_gemm_x3_f32 with tmdnet_gemm_ex_f32's epilogue: pre (the pre-activation, row stride ldx), act (SiLU),
 // rscale (per-row scale), dpre (times silu'(dpre), row stride ldx) -- the Linear + SiLU stacks of large
 // systems (TensorNet's edge MLP over ~1M pair rows at C5) without separate activation passes.
+static int gemm_x3_launch(int M, int N, int K, const void* A, int lda, const void* Bp, const void* W, int ldw, int ws,
+                          const void* bias, void* C, int ldc, int beta, int act, void* pre, const void* rscale,
+                          const void* dpre, int ldx, void* stream);
+
 extern "C" int tmdnet_gemm_x3_ex_f32(int M, int N, int K, const void* A, int lda, const void* Bp, const void* bias,
                                      void* C, int ldc, int beta, int act, void* pre, const void* rscale,
                                      const void* dpre, int ldx, void* stream) {
-  if (M < 0 || N <= 0 || K <= 0 || !A || !Bp || !C) return kBadArgument;
+  if (!Bp) return kBadArgument;
+  return gemm_x3_launch(M, N, K, A, lda, Bp, nullptr, 0, 0, bias, C, ldc, beta, act, pre, rscale, dpre, ldx, stream);
+}
+
+// The same with the right operand given as fp32 and split inside the kernel while it is staged in LDS:
+// trans_w = 1: W [N][K] (a Linear weight, C = A W^T); trans_w = 0: W [K][N] (C = A W).  ldw % 4 == 0,
+// W 16-byte aligned.
+extern "C" int tmdnet_gemm_x3w_f32(int M, int N, int K, const void* A, int lda, const void* W, int ldw, int trans_w,
+                                   const void* bias, void* C, int ldc, int beta, int act, void* pre,
+                                   const void* rscale, const void* dpre, int ldx, void* stream) {
+  if (!W) return kBadArgument;
+  if (ldw % 4 || (((uintptr_t)W) & 15) || ldw < (trans_w ? K : N)) return kUnsupported;
+  return gemm_x3_launch(M, N, K, A, lda, nullptr, W, ldw, trans_w ? 1 : 2, bias, C, ldc, beta, act, pre, rscale,
+                        dpre, ldx, stream);
+}
+
+static int gemm_x3_launch(int M, int N, int K, const void* A, int lda, const void* Bp, const void* W, int ldw, int ws,
+                          const void* bias, void* C, int ldc, int beta, int act, void* pre, const void* rscale,
+                          const void* dpre, int ldx, void* stream) {
+  if (M < 0 || N <= 0 || K <= 0 || !A || !C) return kBadArgument;
   if (M == 0) return kOk;
   if (K % 32 || N % 16 || lda < K || ldc < N || lda % 4 || ldc % 4) return kUnsupported;
   if ((((uintptr_t)A) | ((uintptr_t)Bp) | ((uintptr_t)C) | ((uintptr_t)bias)) & 15) return kUnsupported;
@@ -1608,7 +1691,7 @@ extern "C" int tmdnet_gemm_x3_ex_f32(int M, int N, int K, const void* A, int lda
   }();
   proj::XArgs P{M, N, K, lda, ldc, beta ? 1 : 0, 0, 0, 0, (const float*)A, (const unsigned short*)Bp,
                 (const float*)bias, (float*)C, act ? 1 : 0, ldx, (float*)pre, (const float*)rscale,
-                (const float*)dpre};
+                (const float*)dpre, (const float*)W, ldw};
   hipStream_t st = (hipStream_t)stream;
   // 64-column tiles for wide outputs (the forward mixes, N = 3H..5H), 128 for the narrow input gradients
   // (N = H: one column tile, A read once); 2 row blocks per wave (128 rows per workgroup).  Wide-form
@@ -1619,9 +1702,18 @@ extern "C" int tmdnet_gemm_x3_ex_f32(int M, int N, int K, const void* A, int lda
   P.ny = (M + 127) / 128;
   P.remap = remap_env && P.nx > 1 && (long long)P.nx * P.ny < (1ll << 31);
   const dim3 g = P.remap ? dim3(P.nx * P.ny) : dim3(P.nx, P.ny);
-  if (bn == 64)
-    hipLaunchKernelGGL((proj::k_gemm_x3<2, 64, 1>), g, dim3(256), 0, st, P);
-  else
-    hipLaunchKernelGGL((proj::k_gemm_x3<2, 128, 4>), g, dim3(256), 0, st, P);
+#define TMD_X3(WS_)                                                               \
+  if (bn == 64)                                                                   \
+    hipLaunchKernelGGL((proj::k_gemm_x3<2, 64, 1, WS_>), g, dim3(256), 0, st, P);  \
+  else                                                                            \
+    hipLaunchKernelGGL((proj::k_gemm_x3<2, 128, 4, WS_>), g, dim3(256), 0, st, P);
+  if (ws == 1) {
+    TMD_X3(1)
+  } else if (ws == 2) {
+    TMD_X3(2)
+  } else {
+    TMD_X3(0)
+  }
+#undef TMD_X3
   return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
 }

@@ -292,28 +292,49 @@ __global__ __launch_bounds__(64 * S) void k_embed_bwd_src(Args<T> A) {
 }
 
 // ---------------------------------------------------------------- message passing
+// The row's edges are taken in chunks of 64: lane i loads the chunk's i-th source index (and pair row) in
+// ONE coalesced load, and each edge's indices are then broadcast by v_readlane (wave-uniform: the gathers'
+// base addresses live in scalar registers).  Each wave takes two of its edges per iteration (j and j + S, the
+// same edges and summation order as one at a time), so their 2 x 12 row loads are in flight together instead
+// of a src -> row load chain per edge.
+__device__ __forceinline__ int bcast(int v, int j) { return __builtin_amdgcn_readlane(v, j); }
+
+template <typename T>
+__device__ __forceinline__ void msg_acc(T (&acc)[9], const Args<T>& A, int n, int m, int r, int hc) {
+  const T mult = (m == n && n == 0) ? mult0_of(A) : T(1);
+  const T* er = A.ea + (size_t)r * A.ldea + 3 * hc;
+  const T f0 = er[0] * mult, f1 = er[1] * mult, f2 = er[2] * mult;
+  T t[9];
+  ldc(t, A.Tc + (size_t)m * A.H + hc, A.nh);
+#pragma unroll
+  for (int i = 0; i < 9; ++i) acc[i] += node::ctype_scale(i, f0, f1, f2) * t[i];
+}
+
 template <typename T, int S>
 __global__ __launch_bounds__(64 * S) void k_msg_fwd(Args<T> A) {
   __shared__ T red[S > 1 ? (S - 1) * 9 * TMD_WAVE : 1];
   int n, ch0, w;
   slot_node<S>(A.nblk, n, ch0, w);
-  const int h = ch0 + lane_id();
+  const int lane = lane_id();
+  const int h = ch0 + lane;
   const bool on = h < A.H;
   const int hc = on ? h : 0;
   T acc[9];
 #pragma unroll
   for (int k = 0; k < 9; ++k) acc[k] = T(0);
   const int b = min(A.row_ptr[n], A.cap), e = min(A.row_ptr[n + 1], A.cap);
-  for (int k = b + w; k < e; k += S) {
-    const int m = A.src[k];
-    TMD_DCHECK(m >= 0 && m < A.n);
-    const T mult = (m == n && n == 0) ? mult0_of(A) : T(1);
-    const T* er = A.ea + (size_t)ea_row(A, k) * A.ldea + 3 * hc;
-    const T f0 = er[0] * mult, f1 = er[1] * mult, f2 = er[2] * mult;
-    T t[9];
-    ldc(t, A.Tc + (size_t)m * A.H + hc, A.nh);
-#pragma unroll
-    for (int i = 0; i < 9; ++i) acc[i] += node::ctype_scale(i, f0, f1, f2) * t[i];
+  for (int base = b; base < e; base += TMD_WAVE) {
+    const int cnt = min(TMD_WAVE, e - base);
+    const int sv = lane < cnt ? A.src[base + lane] : 0;
+    const int rv = lane < cnt ? ea_row(A, base + lane) : 0;
+    int j = w;
+    for (; j + S < cnt; j += 2 * S) {
+      const int ma = bcast(sv, j), mb = bcast(sv, j + S);
+      TMD_DCHECK(ma >= 0 && ma < A.n && mb >= 0 && mb < A.n);
+      msg_acc(acc, A, n, ma, bcast(rv, j), hc);
+      msg_acc(acc, A, n, mb, bcast(rv, j + S), hc);
+    }
+    if (j < cnt) msg_acc(acc, A, n, bcast(sv, j), bcast(rv, j), hc);
   }
   if (fold_waves<T, 9, S>(acc, red) && on) stc(A.msg + (size_t)n * A.H + h, A.nh, acc);
 }
@@ -347,9 +368,37 @@ __global__ __launch_bounds__(64 * S) void k_msg_bwd_dst(Args<T> A) {
 
 // pair-row destination pass: gea[p] = sum over the pair's two directions of <gmsg[dst], {I,A,S}[src]>, formed
 // by the pair's canonical edge (row n, src m >= n; tmdnet_pair_index) from both endpoints' rows -- one write
-// per pair instead of one per edge, no atomics.  Inert pair slots (static capacity) are zeroed.
+// per pair instead of one per edge, no atomics.  Inert pair slots (static capacity) are zeroed.  The chunk's
+// canonical edges are compacted per wave (ballot rank -> LDS), then taken two per iteration as above.
+template <typename T>
+__device__ __forceinline__ void pair_grad(const Args<T>& A, int n, int m, int r, int h, int hc, const T (&gn)[9],
+                                          const T (&tn_)[9], bool on) {
+  const T mult = (m == n && n == 0) ? mult0_of(A) : T(1);
+  T g0, g1, g2;
+  if (m == n) {  // self loop: one direction
+    g0 = gn[0] * tn_[0];
+    g1 = gn[1] * tn_[1] + gn[2] * tn_[2] + gn[3] * tn_[3];
+    g2 = gn[4] * tn_[4] + gn[5] * tn_[5] + gn[6] * tn_[6] + gn[7] * tn_[7] + gn[8] * tn_[8];
+  } else {
+    T t[9], g[9];
+    ldc(t, A.Tc + (size_t)m * A.H + hc, A.nh);
+    ldc(g, A.gmsg + (size_t)m * A.H + hc, A.nh);
+    g0 = gn[0] * t[0] + g[0] * tn_[0];
+    g1 = gn[1] * t[1] + gn[2] * t[2] + gn[3] * t[3] + g[1] * tn_[1] + g[2] * tn_[2] + g[3] * tn_[3];
+    g2 = gn[4] * t[4] + gn[5] * t[5] + gn[6] * t[6] + gn[7] * t[7] + gn[8] * t[8] +
+         g[4] * tn_[4] + g[5] * tn_[5] + g[6] * tn_[6] + g[7] * tn_[7] + g[8] * tn_[8];
+  }
+  if (on) {
+    T* gr = A.gea + (size_t)r * 3 * A.H + 3 * h;
+    gr[0] = g0 * mult;
+    gr[1] = g1 * mult;
+    gr[2] = g2 * mult;
+  }
+}
+
 template <typename T, int S>
 __global__ __launch_bounds__(64 * S) void k_msg_bwd_pair(Args<T> A) {
+  __shared__ int cs[S][TMD_WAVE], cr[S][TMD_WAVE];
   {
     const long long tid = (long long)blockIdx.x * blockDim.x + threadIdx.x, nth = (long long)gridDim.x * blockDim.x;
     const int w3 = 3 * A.H;
@@ -360,64 +409,78 @@ __global__ __launch_bounds__(64 * S) void k_msg_bwd_pair(Args<T> A) {
   }
   int n, ch0, w;
   slot_node<S>(A.nblk, n, ch0, w);
-  const int h = ch0 + lane_id();
+  const int lane = lane_id();
+  const int h = ch0 + lane;
   const bool on = h < A.H;
   const int hc = on ? h : 0;
   T gn[9], tn_[9];
   ldc(gn, A.gmsg + (size_t)n * A.H + hc, A.nh);
   ldc(tn_, A.Tc + (size_t)n * A.H + hc, A.nh);
   const int b = min(A.row_ptr[n], A.cap), e = min(A.row_ptr[n + 1], A.cap);
-  for (int k = b + w; k < e; k += S) {
-    const int m = A.src[k];
-    TMD_DCHECK(m >= 0 && m < A.n);
-    if (m < n) continue;  // the pair's other direction: formed by row m
-    const T mult = (m == n && n == 0) ? mult0_of(A) : T(1);
-    T g0, g1, g2;
-    if (m == n) {  // self loop: one direction
-      g0 = gn[0] * tn_[0];
-      g1 = gn[1] * tn_[1] + gn[2] * tn_[2] + gn[3] * tn_[3];
-      g2 = gn[4] * tn_[4] + gn[5] * tn_[5] + gn[6] * tn_[6] + gn[7] * tn_[7] + gn[8] * tn_[8];
-    } else {
-      T t[9], g[9];
-      ldc(t, A.Tc + (size_t)m * A.H + hc, A.nh);
-      ldc(g, A.gmsg + (size_t)m * A.H + hc, A.nh);
-      g0 = gn[0] * t[0] + g[0] * tn_[0];
-      g1 = gn[1] * t[1] + gn[2] * t[2] + gn[3] * t[3] + g[1] * tn_[1] + g[2] * tn_[2] + g[3] * tn_[3];
-      g2 = gn[4] * t[4] + gn[5] * t[5] + gn[6] * t[6] + gn[7] * t[7] + gn[8] * t[8] +
-           g[4] * tn_[4] + g[5] * tn_[5] + g[6] * tn_[6] + g[7] * tn_[7] + g[8] * tn_[8];
+  for (int base = b; base < e; base += TMD_WAVE) {
+    const int cnt = min(TMD_WAVE, e - base);
+    const int sv = lane < cnt ? A.src[base + lane] : -1;
+    const bool own = lane < cnt && sv >= n;  // the pair's other direction is formed by row sv
+    const unsigned long long mask = __ballot(own);
+    const int no = __popcll(mask);
+    if (own) {
+      const int rank = __popcll(mask & ((1ull << lane) - 1ull));
+      cs[w][rank] = sv;
+      cr[w][rank] = A.prow[base + lane];
     }
-    if (on) {
-      T* gr = A.gea + (size_t)A.prow[k] * 3 * A.H + 3 * h;
-      gr[0] = g0 * mult;
-      gr[1] = g1 * mult;
-      gr[2] = g2 * mult;
+    __builtin_amdgcn_wave_barrier();
+    int j = w;
+    for (; j + S < no; j += 2 * S) {
+      const int ma = __builtin_amdgcn_readfirstlane(cs[w][j]), mb = __builtin_amdgcn_readfirstlane(cs[w][j + S]);
+      const int ra = __builtin_amdgcn_readfirstlane(cr[w][j]), rb = __builtin_amdgcn_readfirstlane(cr[w][j + S]);
+      TMD_DCHECK(ma >= 0 && ma < A.n && mb >= 0 && mb < A.n);
+      pair_grad(A, n, ma, ra, h, hc, gn, tn_, on);
+      pair_grad(A, n, mb, rb, h, hc, gn, tn_, on);
     }
+    if (j < no)
+      pair_grad(A, n, __builtin_amdgcn_readfirstlane(cs[w][j]), __builtin_amdgcn_readfirstlane(cr[w][j]), h, hc, gn,
+                tn_, on);
+    __builtin_amdgcn_wave_barrier();  // (the next chunk's compaction rewrites cs / cr)
   }
 }
 
 // source pass: gT[m] = sum over reversed edges ea * gmsg[n]
+template <typename T>
+__device__ __forceinline__ void src_acc(T (&acc)[9], const Args<T>& A, int m, int n, int r, int hc) {
+  const T mult = (m == n && n == 0) ? mult0_of(A) : T(1);
+  const T* er = A.ea + (size_t)r * A.ldea + 3 * hc;
+  const T f0 = er[0] * mult, f1 = er[1] * mult, f2 = er[2] * mult;
+  T g[9];
+  ldc(g, A.gmsg + (size_t)n * A.H + hc, A.nh);
+#pragma unroll
+  for (int i = 0; i < 9; ++i) acc[i] += node::ctype_scale(i, f0, f1, f2) * g[i];
+}
+
 template <typename T, int S>
 __global__ __launch_bounds__(64 * S) void k_msg_bwd_src(Args<T> A) {
   __shared__ T red[S > 1 ? (S - 1) * 9 * TMD_WAVE : 1];
   int m, ch0, w;
   slot_node<S>(A.nblk, m, ch0, w);
-  const int h = ch0 + lane_id();
+  const int lane = lane_id();
+  const int h = ch0 + lane;
   const bool on = h < A.H;
   const int hc = on ? h : 0;
   T acc[9];
 #pragma unroll
   for (int k = 0; k < 9; ++k) acc[k] = T(0);
   const int b = min(A.row_ptr[m], A.cap), e = min(A.row_ptr[m + 1], A.cap);
-  for (int k = b + w; k < e; k += S) {
-    const int n = A.src[k];
-    TMD_DCHECK(n >= 0 && n < A.n);
-    const T mult = (m == n && n == 0) ? mult0_of(A) : T(1);
-    const T* er = A.ea + (size_t)ea_row(A, k) * A.ldea + 3 * hc;
-    const T f0 = er[0] * mult, f1 = er[1] * mult, f2 = er[2] * mult;
-    T g[9];
-    ldc(g, A.gmsg + (size_t)n * A.H + hc, A.nh);
-#pragma unroll
-    for (int i = 0; i < 9; ++i) acc[i] += node::ctype_scale(i, f0, f1, f2) * g[i];
+  for (int base = b; base < e; base += TMD_WAVE) {
+    const int cnt = min(TMD_WAVE, e - base);
+    const int sv = lane < cnt ? A.src[base + lane] : 0;
+    const int rv = lane < cnt ? ea_row(A, base + lane) : 0;
+    int j = w;
+    for (; j + S < cnt; j += 2 * S) {
+      const int na = bcast(sv, j), nb = bcast(sv, j + S);
+      TMD_DCHECK(na >= 0 && na < A.n && nb >= 0 && nb < A.n);
+      src_acc(acc, A, m, na, bcast(rv, j), hc);
+      src_acc(acc, A, m, nb, bcast(rv, j + S), hc);
+    }
+    if (j < cnt) src_acc(acc, A, m, bcast(sv, j), bcast(rv, j), hc);
   }
   if (!fold_waves<T, 9, S>(acc, red)) return;
   if (A.gTadd && on) {

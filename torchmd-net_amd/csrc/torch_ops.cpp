@@ -1113,8 +1113,9 @@ constexpr double kLnEps = 1e-5;  // nn.LayerNorm default (reference torchmd_et.p
 
 int64_t stack_np(bool hk, bool hv) { return 11 + 2 * int64_t(hk) + 2 * int64_t(hv); }
 
-// Large-row fp32 GEMM on tmdnet_gemm_x3_f32 (kernels.gemm_x3): B split per call (a [N][K] weight with
-// trans_b, a [K][N] right operand without); false when outside its envelope
+// Large-row fp32 GEMM on the x3 kernel (kernels.gemm_x3): B split inside the kernel (tmdnet_gemm_x3w_f32; a
+// [N][K] weight with trans_b, a [K][N] right operand without), else by a split launch; false when outside
+// its envelope
 bool gemm_x3_into(const Tensor& A, const Tensor& B, bool trans_b, const Tensor& bias, const Tensor& C, bool beta) {
   const int M = static_cast<int>(A.size(0)), N = static_cast<int>(C.size(1)), K = static_cast<int>(A.size(1));
   auto al = [](const Tensor& t) { return !t.defined() || reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0; };
@@ -1123,9 +1124,18 @@ bool gemm_x3_into(const Tensor& A, const Tensor& B, bool trans_b, const Tensor& 
         A.stride(0) % 4 == 0 && B.stride(0) % 4 == 0 && C.stride(0) % 4 == 0 && al(A) && al(B) && al(C) &&
         (!bias.defined() || (bias.is_contiguous() && al(bias)))))
     return false;
-  Tensor bp = at::empty({3, N, K}, A.options().dtype(at::kShort));
   void* st = stream_of(A);
-  int rc = trans_b ? tmdnet_proj_split_f32(N, K, B.data_ptr(), static_cast<int>(B.stride(0)), bp.data_ptr(), st)
+  // the weight split inside the GEMM while it is staged in LDS (no split launch; kernels.X3_WSPLIT)
+  int rc = tmdnet_gemm_x3w_f32(M, N, K, A.data_ptr(), static_cast<int>(A.stride(0)), B.data_ptr(),
+                               static_cast<int>(B.stride(0)), trans_b ? 1 : 0, bias.defined() ? bias.data_ptr() : nullptr,
+                               C.data_ptr(), static_cast<int>(C.stride(0)), beta ? 1 : 0, 0, nullptr, nullptr, nullptr, 0,
+                               st);
+  if (rc != TMDNET_UNSUPPORTED) {
+    check(rc, "tmdnet_gemm_x3w_f32");
+    return true;
+  }
+  Tensor bp = at::empty({3, N, K}, A.options().dtype(at::kShort));
+  rc = trans_b ? tmdnet_proj_split_f32(N, K, B.data_ptr(), static_cast<int>(B.stride(0)), bp.data_ptr(), st)
                    : tmdnet_split_t_f32(N, K, B.data_ptr(), static_cast<int>(B.stride(0)), bp.data_ptr(), st);
   if (rc == TMDNET_UNSUPPORTED) return false;
   check(rc, "tmdnet_split");

@@ -108,6 +108,7 @@ SIGNATURES = {
     "tmdnet_split_t_f32": (I, [I, I, P, I, P, P]),
     "tmdnet_gemm_x3_f32": (I, [I, I, I, P, I, P, P, P, I, I, P]),
     "tmdnet_gemm_x3_ex_f32": (I, [I, I, I, P, I, P, P, P, I, I, I, P, P, P, I, P]),
+    "tmdnet_gemm_x3w_f32": (I, [I, I, I, P, I, P, I, I, P, P, I, I, I, P, P, P, I, P]),
     "tmdnet_fep_image_bytes": (SZ, [I, I]),
     "tmdnet_fep_split_f32": (I, [I, I, P, I, P, P, P, P, P]),
     "tmdnet_et_fused_bwd_f32": (I, [I, I, I, I, P, P, I, P, I, P, I, P, I, P, P, P, P, P, P, ctypes.c_longlong, P, P, P,

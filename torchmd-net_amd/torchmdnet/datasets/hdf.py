@@ -61,6 +61,22 @@ class HDF5(torch.utils.data.Dataset):
     def __len__(self):
         return self.num_molecules
 
+    def atom_counts(self):
+        """Atoms of every sample from each group's ``types`` SHAPE (n_conf, n_atoms) -- no array is read
+        (module.default_atom_buckets would otherwise load every conformation at training start)."""
+        out = []
+        for path in self.filename.split(";"):
+            f = self._open(path)
+            for gname in f:
+                if gname == "_metadata":
+                    continue
+                g = f[gname]
+                shape = tuple(g["types"].shape) if hasattr(g["types"], "shape") else np.shape(g["types"])
+                out.extend([int(shape[-1])] * len(g["energy"]))
+            if hasattr(f, "close"):
+                f.close()
+        return out
+
     def __getitem__(self, idx):
         if self.index is None:
             self._setup_index()

@@ -1467,6 +1467,9 @@ def gemm_launch(problems):
 # above GEMM_MAX_ROWS (C5-size systems) fp32 GEMMs run on tmdnet_gemm_x3_f32 (bf16 MFMA, exact three-piece
 # split, fp32 accuracy); TMDNET_GEMM_BIG=lib keeps the library GEMM there (A/B switch)
 GEMM_BIG = os.environ.get("TMDNET_GEMM_BIG", "x3")
+# where the weight's bf16 pieces come from: "kernel" = split inside the GEMM while staged in LDS
+# (tmdnet_gemm_x3w_f32), "launch" = a split launch per call (tmdnet_proj_split_f32 / tmdnet_split_t_f32; A/B)
+X3_WSPLIT = os.environ.get("TMDNET_X3_WSPLIT", "kernel")
 
 
 def _al16(*ts):
@@ -1492,6 +1495,15 @@ def gemm_x3(A, B, tb, bias, C, beta, act=0, pre=None, rscale=None, dpre=None):
         return False
     lib = nat.load()
     st = nat.stream(A.device)
+    if X3_WSPLIT == "kernel" and B.data_ptr() % 16 == 0:
+        # the weight split inside the GEMM while it is staged in LDS (no split launch, nothing cached)
+        rc = lib.tmdnet_gemm_x3w_f32(M, N, K, A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), int(bool(tb)),
+                                     None if bias is None else bias.data_ptr(), C.data_ptr(), C.stride(0),
+                                     int(bool(beta)), int(act), nat.ptr(pre), nat.ptr(rscale), nat.ptr(dpre),
+                                     0 if x is None else x.stride(0), st)
+        if rc != GEMM_UNSUPPORTED:
+            nat.check(rc, "tmdnet_gemm_x3w_f32")
+            return True
     bp = torch.empty((3, N, K), dtype=torch.int16, device=A.device)
     if tb:
         rc = lib.tmdnet_proj_split_f32(N, K, B.data_ptr(), B.stride(0), bp.data_ptr(), st)

@@ -141,12 +141,21 @@ class TensorNet(nn.Module):
                 s: Optional[Tensor] = None) -> Tuple[Tensor, Optional[Tensor], Tensor, Tensor, Tensor]:
         if torch.jit.is_scripting():
             return self._forward_script(z, pos, batch), None, z, pos, batch
-        if self.reorder_atoms and z.shape[0] >= kernels.REORDER_MIN_ATOMS and not self.static_shapes:
-            # (static_shapes keeps the caller's numbering: its padding semantics single out atom 0)
+        if self.reorder_atoms and z.shape[0] >= kernels.REORDER_MIN_ATOMS:
             perm = kernels.spatial_permutation(pos, batch, self.cutoff_upper,
                                                self.distance.box if self.distance.use_periodic else None)
             inv = torch.empty_like(perm)
-            inv[perm] = torch.arange(perm.numel(), device=perm.device)
+            ar = torch.arange(perm.numel(), device=perm.device)
+            inv[perm] = ar
+            if self.static_shapes:
+                # the padding semantics single out the caller's atom 0 (padded slots become (0, 0) edges,
+                # tensornet.py:215-221): keep it at index 0 by swapping it with the Morton-first atom (same
+                # molecule: the batch stays sorted).  Device ops only (no sync; capturable).
+                j = inv[0:1]
+                perm = perm.clone()
+                perm.index_put_((j,), perm[0:1].clone())
+                perm[0] = 0
+                inv[perm] = ar
             x = self._forward(z[perm], pos.index_select(0, perm), batch[perm])
             return x[inv], None, z, pos, batch
         return self._forward(z, pos, batch), None, z, pos, batch

@@ -159,35 +159,43 @@ class SplitAdamW(torch.optim.Optimizer):
     param_groups ARE the parts' groups (an LR change reaches them)."""
 
     def __init__(self, tail, head, lr, weight_decay):
-        parts = [_adamw(ps, lr, weight_decay) for ps in (tail, head) if ps]
-        super().__init__([g for o in parts for g in o.param_groups], dict(lr=lr, weight_decay=weight_decay))
+        # fixed roles: parts[0] = TAIL (stepped by step_part(0) once the tail bucket is averaged), parts[1] =
+        # HEAD; an empty bucket keeps its slot as None -- dropping it would shift the head optimizer into
+        # slot 0 and step it before the head bucket's all-reduce finished (un-averaged gradients)
+        parts = [_adamw(ps, lr, weight_decay) if ps else None for ps in (tail, head)]
+        live = [o for o in parts if o is not None]
+        super().__init__([g for o in live for g in o.param_groups], dict(lr=lr, weight_decay=weight_decay))
         self.parts = parts
-        self.param_groups = [g for o in parts for g in o.param_groups]  # the same dict objects
+        self.param_groups = [g for o in live for g in o.param_groups]  # the same dict objects
 
     def __setattr__(self, k, v):
         if k in ("found_inf", "grad_scale"):
             for o in self.__dict__.get("parts", []):
-                setattr(o, k, v)
+                if o is not None:
+                    setattr(o, k, v)
         super().__setattr__(k, v)
 
     def zero_grad(self, set_to_none=True):
         for o in self.parts:
-            o.zero_grad(set_to_none=set_to_none)
+            if o is not None:
+                o.zero_grad(set_to_none=set_to_none)
 
     def step(self, closure=None):
         for o in self.parts:
-            o.step()
+            if o is not None:
+                o.step()
 
     def step_part(self, i):
-        if i < len(self.parts):
+        if self.parts[i] is not None:
             self.parts[i].step()
 
     def state_dict(self):
-        return {"parts": [o.state_dict() for o in self.parts]}
+        return {"parts": [None if o is None else o.state_dict() for o in self.parts]}
 
     def load_state_dict(self, sd):
         for o, d in zip(self.parts, sd["parts"]):
-            o.load_state_dict(d)
+            if o is not None and d is not None:
+                o.load_state_dict(d)
 
 
 def _make_optimizer(reduce, lr, weight_decay):
@@ -516,46 +524,51 @@ class _BucketStep:
             ly, lf = padded_losses(pred, nd, bs)
             return ly, lf, ly * scale_y + lf * scale_f
 
-        # eager warm-up on a clone of the positions (sizes the edge capacity, freezes the molecule count
-        # of reduce): the captured positions' autograd state must not start on the default stream
-        for d in dists:
-            d.static_capacity = None
-        g = rep.distance.graph(bs.pos.clone(), bs.batch)
-        self.edge_capacity = max(int(math.ceil(g.num_pairs * margin / 256.0) * 256), int(min_capacity))
-        del g
-        pos0 = bs.pos
-        bs.pos = pos0.clone()
-        torch.autograd.grad(loss_fn()[2], params, allow_unused=True)
-        bs.pos = pos0
-        for d in dists:
-            d.static_capacity = self.edge_capacity
-        s = torch.cuda.Stream(device=dev)
-        s.wait_stream(torch.cuda.current_stream(dev))
-        with torch.cuda.stream(s):
-            for _ in range(warmup):
-                torch.autograd.grad(loss_fn()[2], params, allow_unused=True)
-        torch.cuda.current_stream(dev).wait_stream(s)
-        torch.cuda.synchronize(dev)
-        # the backward's seed: allocated outside the graph and kept alive with it (its replays read it)
-        self._seed = seed = torch.ones((), dtype=params[0].dtype, device=dev)
-        self.graph = torch.cuda.CUDAGraph()
-        # thread-local capture: the data loader's pin-memory thread keeps issuing host-allocation and copy calls
-        # while a new bucket is captured mid-epoch (global mode invalidated such a capture under a profiler)
-        with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
-            self.ly, self.lf, total = loss_fn()
-            grads = torch.autograd.grad(total, params, grad_outputs=seed.expand_as(total), allow_unused=True)
-            pairs = [(v, gr) for v, gr in zip(views, grads) if gr is not None]
-            zero = [v for v, gr in zip(views, grads) if gr is None]
-            _copy_grads(pairs)
-            if zero:
-                torch._foreach_zero_(zero)
-            ov = rep.distance.last_overflow
-            flag.copy_(ov.num.reshape(1) > ov.capacity)
-        torch.cuda.synchronize(dev)
-        for d in dists:
-            d.static_capacity = None
-        if self.pad_shift is not None:
-            rep._pad_shift = None  # the graph keeps reading self.pad_shift; eager calls see no shift
+        # (try / finally: a warm-up or capture that raises must not leave the static capacity or TensorNet's
+        # padded-batch shift set for later eager calls, e.g. validation on unpadded batches)
+        grads = pairs = None
+        try:
+            # eager warm-up on a clone of the positions (sizes the edge capacity, freezes the molecule count
+            # of reduce): the captured positions' autograd state must not start on the default stream
+            for d in dists:
+                d.static_capacity = None
+            g = rep.distance.graph(bs.pos.clone(), bs.batch)
+            self.edge_capacity = max(int(math.ceil(g.num_pairs * margin / 256.0) * 256), int(min_capacity))
+            del g
+            pos0 = bs.pos
+            bs.pos = pos0.clone()
+            torch.autograd.grad(loss_fn()[2], params, allow_unused=True)
+            bs.pos = pos0
+            for d in dists:
+                d.static_capacity = self.edge_capacity
+            s = torch.cuda.Stream(device=dev)
+            s.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(s):
+                for _ in range(warmup):
+                    torch.autograd.grad(loss_fn()[2], params, allow_unused=True)
+            torch.cuda.current_stream(dev).wait_stream(s)
+            torch.cuda.synchronize(dev)
+            # the backward's seed: allocated outside the graph and kept alive with it (its replays read it)
+            self._seed = seed = torch.ones((), dtype=params[0].dtype, device=dev)
+            self.graph = torch.cuda.CUDAGraph()
+            # thread-local capture: the data loader's pin-memory thread keeps issuing host-allocation and copy calls
+            # while a new bucket is captured mid-epoch (global mode invalidated such a capture under a profiler)
+            with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
+                self.ly, self.lf, total = loss_fn()
+                grads = torch.autograd.grad(total, params, grad_outputs=seed.expand_as(total), allow_unused=True)
+                pairs = [(v, gr) for v, gr in zip(views, grads) if gr is not None]
+                zero = [v for v, gr in zip(views, grads) if gr is None]
+                _copy_grads(pairs)
+                if zero:
+                    torch._foreach_zero_(zero)
+                ov = rep.distance.last_overflow
+                flag.copy_(ov.num.reshape(1) > ov.capacity)
+            torch.cuda.synchronize(dev)
+        finally:
+            for d in dists:
+                d.static_capacity = None
+            if self.pad_shift is not None:
+                rep._pad_shift = None  # the graph keeps reading self.pad_shift; eager calls see no shift
         del grads, pairs
 
     def _set_shift(self, b):
