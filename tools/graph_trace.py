@@ -1,6 +1,7 @@
 """Graph-replayed ET-QM9 energy+force steps (the bench workload) bracketed by marker kernels, for
 rocprofv3 --kernel-trace (tools/trace_summary.py lists the kernels of the marked replay).
-usage: graph_trace.py [et|tn|train]   (train: the replay of the captured ET-QM9 training step)"""
+usage: graph_trace.py [et|tn|train|tn_train|tn_c5]   (train / tn_train: the replay of the captured ET-QM9 /
+TensorNet-rMD17 C3 training step; tn_c5: one EAGER TensorNet energy+force evaluation of the C5 water box)"""
 import os
 import sys
 
@@ -16,10 +17,21 @@ from torchmdnet.models.model import create_model  # noqa: E402
 dev = torch.device("cuda", 0)
 torch.manual_seed(0)
 which = sys.argv[1] if len(sys.argv) > 1 else "et"
+if which == "tn_c5":
+    import bench
+    model, z, pos, batch, _ = bench.tn_water_box_model(50001, True, 0, dev)
+    for _ in range(2):
+        model(z, pos, batch)
+    torch.cuda.synchronize()
+    torch.cuda._sleep(100)
+    model(z, pos, batch)
+    torch.cuda._sleep(100)
+    torch.cuda.synchronize()
+    sys.exit(0)
 if which in ("et", "train"):
     model = create_model(et_args(128)).to(dev)
     z, pos, batch = qm9_like(32, 1)
-else:
+else:  # tn, tn_train: TensorNet-rMD17 (C3)
     from bench import rmd17_like
     with open(os.path.join(ROOT, "tests", "golden", "configs", "tensornet_rmd17.yaml")) as f:
         args = yaml.safe_load(f)
@@ -27,10 +39,10 @@ else:
     model = create_model(args).to(dev)
     z, pos, batch = rmd17_like(8, 1)
 z, pos, batch = z.to(dev), pos.float().to(dev), batch.to(dev)
-if which == "train":
+if which in ("train", "tn_train"):
     from torchmdnet.training import GraphedTrainStep
     g = torch.Generator().manual_seed(200)
-    y_lab = torch.randn(32, 1, generator=g).to(dev)
+    y_lab = torch.randn(int(batch.max()) + 1, 1, generator=g).to(dev)
     f_lab = torch.randn(z.shape[0], 3, generator=g).to(dev)
     tr = GraphedTrainStep(model, z, pos, batch, y_lab, f_lab, lr=1e-4)
     for _ in range(3):

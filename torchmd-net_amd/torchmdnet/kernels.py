@@ -1436,7 +1436,7 @@ def fused_act(act, x, scale=None):
 
 # ----------------------------------------------------------------------------- small grouped GEMM
 GEMM_UNSUPPORTED = 2
-GEMM_MAX_ROWS = 16384  # above this the library GEMM's large tiles win (C5-size systems)
+GEMM_MAX_ROWS = 16384  # the grouped split-K kernel's envelope; above it the x3 GEMM (gemm_x3) takes the rows
 
 
 def gemm_launch(problems):
@@ -1528,8 +1528,12 @@ def gemm_group(problems):
     the library GEMM (fp64 parity runs)."""
     if gemm_launch(problems):
         return
+    mixed = len(problems) > 1
     for A, B, tb, bias, C, beta in problems:
-        if A.shape[0] > GEMM_MAX_ROWS and gemm_x3(A, B, tb, bias, C, beta):
+        if A.shape[0] > GEMM_MAX_ROWS:
+            if gemm_x3(A, B, tb, bias, C, beta):
+                continue
+        elif mixed and gemm_launch([(A, B, tb, bias, C, beta)]):  # (a group with rows on both sides)
             continue
         Bop = B.t() if tb else B
         if beta:

@@ -290,7 +290,9 @@ class _Mix3(Function):
         c = c.contiguous()
         out = torch.empty((9, c.shape[1], w0.shape[0]), dtype=c.dtype, device=c.device)
         probs = [(src, w, True, None, dst, False) for src, w, dst in zip(_blocks(c), (w0, w1, w2), _blocks(out))]
-        if not (c.is_cuda and kernels.gemm_launch(probs)):  # the three mixes in one hand-written launch
+        if c.is_cuda:  # one hand-written launch (x3 GEMMs above GEMM_MAX_ROWS rows; the library for fp64)
+            kernels.gemm_group(probs)
+        else:
             for src, w, _, _, dst, _ in probs:
                 torch.mm(src, w.t(), out=dst)
         ctx.save_for_backward(c, w0, w1, w2)
@@ -310,7 +312,9 @@ class _Mix3Bwd(Function):
         gc = torch.empty_like(c)
         ws = (w0, w1, w2)
         probs = [(g, w, False, None, dst, False) for g, w, dst in zip(_blocks(gout), ws, _blocks(gc))]
-        if not (c.is_cuda and kernels.gemm_launch(probs)):  # input gradients: one launch
+        if c.is_cuda:  # input gradients: one launch (x3 GEMMs above GEMM_MAX_ROWS rows)
+            kernels.gemm_group(probs)
+        else:
             for g, w, _, _, dst, _ in probs:
                 torch.mm(g, w, out=dst)
         # weight gradients: one grouped TN launch (sums over the rows)
