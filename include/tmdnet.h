@@ -494,6 +494,18 @@ int tmdnet_tn_embed_bwd(int dtype, int n_nodes, int hidden, const int32_t* row_p
                         const void* Q, const void* W, int ld_w, const void* cutoff, const void* unit,
                         const void* grad_out, void* gP, void* gQ, void* gW, void* gcut, void* gunit,
                         void* stream);
+/* Second order of the embedding (force-matching training through TensorEmbedding, tensornet.py:287-326 under
+ * module.py:130-179): for cotangents (tP, tQ, tW, tcut, tunit) of the first backward's outputs (gP, gQ, gW,
+ * gcut, gunit), d_grad_out [9][N][H] = J t (the forward's directional derivative) and (dP, dQ, dW [E][3H],
+ * dcut, dunit) = H_<grad_out, E> t (the first backward's directional derivative, grad_out fixed): the
+ * first-order kernels evaluated on dual numbers.  tW shares W's row stride ld_w; a NULL tangent is zero, a
+ * NULL output is not computed; outputs overwritten. */
+int tmdnet_tn_embed_bwd2(int dtype, int n_nodes, int hidden, const int32_t* row_ptr, const int32_t* src,
+                         int max_pairs, double self0_mult, const int32_t* pad_pairs, int pad_capacity,
+                         const void* P, const void* Q, const void* W, int ld_w, const void* cutoff,
+                         const void* unit, const void* grad_out, const void* tP, const void* tQ, const void* tW,
+                         const void* tcut, const void* tunit, void* d_grad_out, void* dP, void* dQ, void* dW,
+                         void* dcut, void* dunit, void* stream);
 /* Message (replaces tensor_message_passing, tensornet.py:329-332):
  *   msg[n] = sum_{edges e with edge_index[0]==n} ea[e,h,0] I[m] + ea[e,h,1] A[m] + ea[e,h,2] S[m],
  * m = edge_index[1][e]; edge_attr [E][3H] interleaved (h, component) as reshape(E, H, 3);

@@ -120,6 +120,40 @@ def test_message_second_order_matches_composite(monkeypatch):
     assert _rel(e1 + e1[tr], e0 + e0[tr]) < 1e-10
 
 
+def test_embedding_second_order_matches_composite(monkeypatch):
+    """TensorEmbedding's aggregation (tensornet.py:295-315) differentiated twice: the hand second order
+    (tmdnet_tn_embed_bwd2: the first-order kernels on dual numbers) vs autograd's double differentiation of
+    the composite, fp64.  Inputs and tangents obey the kernels' pair precondition: W, C (and their tangents)
+    equal on the two directions of a pair, u (and its tangent) opposite -- as in the model, where they are
+    functions of the pair distance / the displacement."""
+    from torchmdnet import kernels, tn_node
+    graph = _tn_graph()
+    g = torch.Generator().manual_seed(4)
+    N, H, E = graph.n_nodes, 16, graph.n_edges
+    rn = lambda *s: torch.randn(*s, generator=g, dtype=torch.float64).to(DEV)  # noqa: E731
+    tr = graph.transpose.long()
+    sym = lambda t: 0.5 * (t + t[tr])  # noqa: E731
+    asym = lambda t: 0.5 * (t - t[tr])  # noqa: E731
+    P, Q, W, C, u, gE = rn(N, H), rn(N, H), sym(rn(E, 3 * H)), sym(rn(E)), asym(rn(E, 3)), rn(9, N, H)
+    tP, tQ, tW, tC, tu = rn(N, H), rn(N, H), sym(rn(E, 3 * H)), sym(rn(E)), asym(rn(E, 3))
+
+    def second(mode):
+        monkeypatch.setattr(tn_node, "SECOND_ORDER", mode)
+        xs = [x.clone().requires_grad_(True) for x in (P, Q, W, C, u, gE)]
+        out = kernels.tn_embed(*xs[:5], graph)
+        first = torch.autograd.grad(out, xs[:5], xs[5], create_graph=True)
+        return torch.autograd.grad(first, xs, (tP, tQ, tW, tC, tu))
+
+    a, b = second("hip"), second("composite")
+    assert _rel(a[0], b[0]) < 1e-10 and _rel(a[1], b[1]) < 1e-10  # P, Q
+    assert _rel(a[5], b[5]) < 1e-10  # gE
+    # per-edge rows are numbered by the row that reads them: compare what any consumer sees, the pair sums
+    # (W, C: symmetric) and differences (u: antisymmetric)
+    assert _rel(a[2] + a[2][tr], b[2] + b[2][tr]) < 1e-10
+    assert _rel(a[3] + a[3][tr], b[3] + b[3][tr]) < 1e-10
+    assert _rel(a[4] - a[4][tr], b[4] - b[4][tr]) < 1e-10
+
+
 @pytest.mark.parametrize("static_shapes", [True, False])
 def test_tensornet_force_loss_gradients_hip_vs_composite(static_shapes, monkeypatch):
     """C3-shaped TensorNet (O(3)) force-matching loss: parameter gradients through the hand second order

@@ -30,7 +30,9 @@
 namespace tmd {
 namespace tn {
 
-template <typename T> struct Args {
+// CP / OP: input / output "pointer" types -- const T* / T* for the first-order kernels, node::DIn / DOut
+// (value and tangent arrays) for the embedding's second order on dual numbers (tmdnet_tn_embed_bwd2)
+template <typename T, typename CP = const T*, typename OP = T*> struct ArgsT {
   int n, H, nblk, cap;
   size_t nh;                // component stride of the compact layout (N * H)
   T mult0;
@@ -39,13 +41,13 @@ template <typename T> struct Args {
   const int32_t* row_ptr;
   const int32_t* src;
   // embedding
-  const T* P; const T* Q;   // [N][H]
-  const T* W; int ldw;      // [E][3H] (W1 | W2 | W3), pre-cutoff
-  const T* C;               // [E]
-  const T* u;               // [E][3]
-  T* E;                     // [9][N][H]
-  const T* gE;
-  T* gP; T* gQ; T* gW; T* gC; T* gu;
+  CP P; CP Q;               // [N][H]
+  CP W; int ldw;            // [E][3H] (W1 | W2 | W3), pre-cutoff
+  CP C;                     // [E]
+  CP u;                     // [E][3]
+  OP E;                     // [9][N][H]
+  CP gE;
+  OP gP; OP gQ; OP gW; OP gC; OP gu;
   // message
   const T* ea; int ldea;    // [E][3H] interleaved (h, c)
   const T* Tc;              // [9][N][H]
@@ -59,31 +61,33 @@ template <typename T> struct Args {
   const int32_t* pedge;     // [np] the canonical edge of each pair slot
   int np;                   // pair slots
 };
+template <typename T> using Args = ArgsT<T>;
 
-template <typename T> __device__ __forceinline__ int ea_row(const Args<T>& A, int k) {
+template <typename AT> __device__ __forceinline__ int ea_row(const AT& A, int k) {
   return A.prow ? A.prow[k] : k;
 }
 
 // Multiplicity of atom 0's self loop.  With a device pair count (static_shapes under HIP-graph
 // capture) it is computed here: 1 + (reference padding capacity - pairs found), a uniform scalar load.
-template <typename T> __device__ __forceinline__ T mult0_of(const Args<T>& A) {
+template <typename T, typename CP, typename OP>
+__device__ __forceinline__ T mult0_of(const ArgsT<T, CP, OP>& A) {
   if (A.npd == nullptr) return A.mult0;
   const int pad = A.padcap - __builtin_amdgcn_readfirstlane(A.npd[0]);
-  return T(1 + (pad > 0 ? pad : 0));
+  return T(double(1 + (pad > 0 ? pad : 0)));
 }
 
 // Static-capacity edge lists: rows [row_ptr[n], cap) of the per-edge gradient outputs belong to no
 // CSR row.  They are zeroed here, spread over the whole grid (every thread, before any early exit),
 // so the weight-gradient GEMMs over all `cap` rows (the edge / distance MLPs) see zeros, not stale
 // memory; the dynamic graph (cap == row_ptr[n]) skips it.
-template <typename T>
-__device__ __forceinline__ void zero_tail_rows(const Args<T>& A, T* p, int w) {
-  if (p == nullptr) return;
+template <typename AT, typename P>
+__device__ __forceinline__ void zero_tail_rows(const AT& A, P p, int w) {
+  if (!p) return;
   const int e0 = min(A.row_ptr[A.n], A.cap);
   if (e0 >= A.cap) return;
   const long long cnt = (long long)(A.cap - e0) * w;
   const long long tid = (long long)blockIdx.x * blockDim.x + threadIdx.x, nth = (long long)gridDim.x * blockDim.x;
-  for (long long i = tid; i < cnt; i += nth) p[(size_t)e0 * w + i] = T(0);
+  for (long long i = tid; i < cnt; i += nth) p[(size_t)e0 * w + i] = decltype(A.mult0)(0.0);
 }
 
 // One workgroup of S waves per (node, 64-channel block): the node's edges are dealt round-robin to the
@@ -117,11 +121,11 @@ __device__ __forceinline__ bool fold_waves(T (&acc)[K], T* red) {
   }
 }
 
-template <typename T> __device__ __forceinline__ void ldc(T (&o)[9], const T* p, size_t nh) {
+template <typename T, typename P> __device__ __forceinline__ void ldc(T (&o)[9], P p, size_t nh) {
 #pragma unroll
   for (int k = 0; k < 9; ++k) o[k] = p[k * nh];
 }
-template <typename T> __device__ __forceinline__ void stc(T* p, size_t nh, const T (&o)[9]) {
+template <typename T, typename P> __device__ __forceinline__ void stc(P p, size_t nh, const T (&o)[9]) {
 #pragma unroll
   for (int k = 0; k < 9; ++k) p[k * nh] = o[k];
 }
@@ -149,9 +153,15 @@ __device__ __forceinline__ void dsym_c(const T* g, T x, T y, T z, T& dx, T& dy, 
 }
 
 // ---------------------------------------------------------------- embedding forward
-template <typename T, int S>
-__global__ __launch_bounds__(64 * S) void k_embed_fwd(Args<T> A) {
-  __shared__ T red[S > 1 ? (S - 1) * 9 * TMD_WAVE : 1];
+// (T = node::Dual<float|double> with DIn / DOut pointers: the second order, tmdnet_tn_embed_bwd2; shared
+// arrays as raw bytes, the dual type having a constructor)
+#define TMD_RED(T, NV) \
+  __shared__ __attribute__((aligned(16))) unsigned char red_[(NV) * sizeof(T)]; \
+  T* red = reinterpret_cast<T*>(red_);
+
+template <typename T, int S, typename AT = Args<T>>
+__global__ __launch_bounds__(64 * S) void k_embed_fwd(AT A) {
+  TMD_RED(T, S > 1 ? (S - 1) * 9 * TMD_WAVE : 1)
   int n, ch0, w;
   slot_node<S>(A.nblk, n, ch0, w);
   const int h = ch0 + lane_id();
@@ -167,7 +177,7 @@ __global__ __launch_bounds__(64 * S) void k_embed_fwd(Args<T> A) {
     TMD_DCHECK(m >= 0 && m < A.n);
     const T mult = (m == n && n == 0) ? mult0_of(A) : T(1);
     const T zc = (Pn + A.Q[(size_t)m * A.H + hc]) * A.C[k] * mult;
-    const T* wr = A.W + (size_t)k * A.ldw;
+    const auto wr = A.W + (size_t)k * A.ldw;
     const T w1 = wr[hc] * zc, w2 = wr[A.H + hc] * zc, w3 = wr[2 * A.H + hc] * zc;
     T sk[3], sy[5];
     skew_c(sk, -A.u[3 * k], -A.u[3 * k + 1], -A.u[3 * k + 2]);
@@ -184,9 +194,9 @@ __global__ __launch_bounds__(64 * S) void k_embed_fwd(Args<T> A) {
 // ---------------------------------------------------------------- embedding backward
 // destination pass: gP[n], gW[e'], gC[e'], gu[e'].  One wave per node covering all NB channel
 // blocks, so the per-edge channel sums (gC, gu) finish inside the wave: plain stores, deterministic.
-template <typename T, int NB, int S>
-__global__ __launch_bounds__(64 * S) void k_embed_bwd_dst(Args<T> A) {
-  __shared__ T red[S > 1 ? (S - 1) * NB * TMD_WAVE : 1];
+template <typename T, int NB, int S, typename AT = Args<T>>
+__global__ __launch_bounds__(64 * S) void k_embed_bwd_dst(AT A) {
+  TMD_RED(T, S > 1 ? (S - 1) * NB * TMD_WAVE : 1)
   zero_tail_rows(A, A.gW, 3 * A.H);
   zero_tail_rows(A, A.gC, 1);
   zero_tail_rows(A, A.gu, 3);
@@ -211,8 +221,8 @@ __global__ __launch_bounds__(64 * S) void k_embed_bwd_dst(Args<T> A) {
     T sk[3], sy[5];
     skew_c(sk, ux, uy, uz);
     sym_c(sy, ux, uy, uz);
-    const T* wr = A.W + (size_t)k * A.ldw;
-    T* gw = A.gW + (size_t)k * 3 * A.H;
+    const auto wr = A.W + (size_t)k * A.ldw;
+    const auto gw = A.gW + (size_t)k * 3 * A.H;
     T gc = T(0), gux = T(0), guy = T(0), guz = T(0);
 #pragma unroll
     for (int c = 0; c < NB; ++c) {
@@ -261,9 +271,9 @@ __global__ __launch_bounds__(64 * S) void k_embed_bwd_dst(Args<T> A) {
 }
 
 // source pass: gQ[m] = sum over reversed edges of the same g_z
-template <typename T, int S>
-__global__ __launch_bounds__(64 * S) void k_embed_bwd_src(Args<T> A) {
-  __shared__ T red[S > 1 ? (S - 1) * TMD_WAVE : 1];
+template <typename T, int S, typename AT = Args<T>>
+__global__ __launch_bounds__(64 * S) void k_embed_bwd_src(AT A) {
+  TMD_RED(T, S > 1 ? (S - 1) * TMD_WAVE : 1)
   int m, ch0, w;
   slot_node<S>(A.nblk, m, ch0, w);
   const int h = ch0 + lane_id();
@@ -282,7 +292,7 @@ __global__ __launch_bounds__(64 * S) void k_embed_bwd_src(Args<T> A) {
     T sk[3], sy[5];
     skew_c(sk, A.u[3 * k], A.u[3 * k + 1], A.u[3 * k + 2]);
     sym_c(sy, A.u[3 * k], A.u[3 * k + 1], A.u[3 * k + 2]);
-    const T* wr = A.W + (size_t)k * A.ldw;
+    const auto wr = A.W + (size_t)k * A.ldw;
     const T w1 = wr[hc], w2 = wr[A.H + hc], w3 = wr[2 * A.H + hc];
     const T gg = g[0] * w1 + (g[1] * sk[0] + g[2] * sk[1] + g[3] * sk[2]) * w2 +
                  (g[4] * sy[0] + g[5] * sy[1] + g[6] * sy[2] + g[7] * sy[3] + g[8] * sy[4]) * w3;
@@ -717,4 +727,69 @@ extern "C" int tmdnet_tn_message_bwd_pairs(int dtype, int n_nodes, int hidden, c
     if (rc) return rc;
     return g_comp ? tn::launch_msg_bwd_src<T>(a, st) : kOk;
   })
+}
+
+// Second order of the embedding (forward-over-reverse on dual numbers, as tmdnet_tn_node_bwd2): with the
+// first backward (gP, gQ, gW, gcut, gunit) = J^T(theta) gE, theta = (P, Q, W, cut, unit), its VJP for the
+// cotangents t_theta of those outputs is
+//   d_gE      = J(theta) t_theta                   -- the forward kernel on theta + eps t_theta (eps part)
+//   d_theta   = H_<gE, E>(theta) t_theta           -- the first backward on theta + eps t_theta, gE fixed
+// (the Hessian of <gE, E(theta)> is symmetric).  The kernels are the first-order ones instantiated on
+// node::Dual<T> with value / tangent pointer pairs; a NULL tangent is 0, a NULL output is not written.
+namespace tmd {
+namespace tn {
+template <typename T>
+static int embed_bwd2(int n_nodes, int hidden, const int32_t* row_ptr, const int32_t* src, int max_pairs,
+                      double self0_mult, const int32_t* pad_pairs, int pad_capacity, const void* P, const void* Q,
+                      const void* W, int ld_w, const void* cutoff, const void* unit, const void* grad_out,
+                      const void* tP, const void* tQ, const void* tW, const void* tcut, const void* tunit,
+                      void* d_grad_out, void* dP, void* dQ, void* dW, void* dcut, void* dunit, hipStream_t st) {
+  using D = node::Dual<T>;
+  using DI = node::DIn<T>;
+  using DO = node::DOut<T>;
+  using DA = ArgsT<D, DI, DO>;
+  DA a{};
+  a.n = n_nodes; a.H = hidden; a.nblk = (hidden + TMD_WAVE - 1) / TMD_WAVE; a.cap = max_pairs;
+  a.mult0 = D(self0_mult); a.nh = (size_t)n_nodes * hidden; a.npd = pad_pairs; a.padcap = pad_capacity;
+  a.row_ptr = row_ptr; a.src = src;
+  a.P = DI{(const T*)P, (const T*)tP}; a.Q = DI{(const T*)Q, (const T*)tQ};
+  a.W = DI{(const T*)W, (const T*)tW}; a.ldw = ld_w;
+  a.C = DI{(const T*)cutoff, (const T*)tcut}; a.u = DI{(const T*)unit, (const T*)tunit};
+  a.gE = DI{(const T*)grad_out, nullptr};
+  a.E = DO{nullptr, (T*)d_grad_out};
+  a.gP = DO{nullptr, (T*)dP}; a.gQ = DO{nullptr, (T*)dQ}; a.gW = DO{nullptr, (T*)dW};
+  a.gC = DO{nullptr, (T*)dcut}; a.gu = DO{nullptr, (T*)dunit};
+  const dim3 gs((unsigned)((long long)n_nodes * a.nblk));
+  if (d_grad_out) hipLaunchKernelGGL((k_embed_fwd<D, 4, DA>), gs, dim3(256), 0, st, a);
+  if (dP || dW || dcut || dunit) {
+    const dim3 g((unsigned)n_nodes);
+    if (a.nblk == 1) hipLaunchKernelGGL((k_embed_bwd_dst<D, 1, 4, DA>), g, dim3(256), 0, st, a);
+    else if (a.nblk == 2) hipLaunchKernelGGL((k_embed_bwd_dst<D, 2, 4, DA>), g, dim3(256), 0, st, a);
+    else if (a.nblk <= 4) hipLaunchKernelGGL((k_embed_bwd_dst<D, 4, 4, DA>), g, dim3(256), 0, st, a);
+    else return kUnsupported;
+  }
+  if (dQ) hipLaunchKernelGGL((k_embed_bwd_src<D, 4, DA>), gs, dim3(256), 0, st, a);
+  return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
+}
+}  // namespace tn
+}  // namespace tmd
+
+extern "C" int tmdnet_tn_embed_bwd2(int dtype, int n_nodes, int hidden, const int32_t* row_ptr,
+                                    const int32_t* src, int max_pairs, double self0_mult,
+                                    const int32_t* pad_pairs, int pad_capacity, const void* P, const void* Q,
+                                    const void* W, int ld_w, const void* cutoff, const void* unit,
+                                    const void* grad_out, const void* tP, const void* tQ, const void* tW,
+                                    const void* tcut, const void* tunit, void* d_grad_out, void* dP, void* dQ,
+                                    void* dW, void* dcut, void* dunit, void* stream) {
+  if (n_nodes <= 0) return kOk;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == TMDNET_F32)
+    return tn::embed_bwd2<float>(n_nodes, hidden, row_ptr, src, max_pairs, self0_mult, pad_pairs, pad_capacity, P, Q,
+                                 W, ld_w, cutoff, unit, grad_out, tP, tQ, tW, tcut, tunit, d_grad_out, dP, dQ, dW,
+                                 dcut, dunit, st);
+  if (dtype == TMDNET_F64)
+    return tn::embed_bwd2<double>(n_nodes, hidden, row_ptr, src, max_pairs, self0_mult, pad_pairs, pad_capacity, P,
+                                  Q, W, ld_w, cutoff, unit, grad_out, tP, tQ, tW, tcut, tunit, d_grad_out, dP, dQ, dW,
+                                  dcut, dunit, st);
+  return kUnsupported;
 }

@@ -29,52 +29,7 @@ template <typename T, typename CP = const T*, typename OP = T*> struct NodeArgs 
   CP gout; OP ga; OP gb; CP gadd;  // backward
 };
 
-// ---- second order by forward-over-reverse on dual numbers (value, tangent).  The first backward maps
-// (a, b, g) to (ga, gb) = J_f(a, b)^T g; its VJP for cotangents (t_a, t_b) of (ga, gb) is
-//   d_g      = J_f (t_a, t_b)                         -- the forward pass with tangents (t_a, t_b)
-//   (d_a, d_b) = H_<g, f> (t_a, t_b)                   -- the first backward with tangents (t_a, t_b), g fixed
-// (the Hessian of <g, f(a, b)> is symmetric).  Every pass above only adds, subtracts, multiplies and
-// divides, so the SAME code evaluated on Dual<T> gives both (the derivative of a quotient included).
-template <typename T> struct Dual {
-  T v, d;
-  __device__ __forceinline__ Dual() : v(0), d(0) {}
-  __device__ __forceinline__ Dual(double x) : v(T(x)), d(0) {}  // constants
-  __device__ __forceinline__ Dual(T v_, T d_) : v(v_), d(d_) {}
-};
-template <typename T> __device__ __forceinline__ Dual<T> operator+(Dual<T> x, Dual<T> y) { return {x.v + y.v, x.d + y.d}; }
-template <typename T> __device__ __forceinline__ Dual<T> operator-(Dual<T> x, Dual<T> y) { return {x.v - y.v, x.d - y.d}; }
-template <typename T> __device__ __forceinline__ Dual<T> operator-(Dual<T> x) { return {-x.v, -x.d}; }
-template <typename T> __device__ __forceinline__ Dual<T> operator*(Dual<T> x, Dual<T> y) {
-  return {x.v * y.v, x.d * y.v + x.v * y.d};
-}
-template <typename T> __device__ __forceinline__ Dual<T> operator/(Dual<T> x, Dual<T> y) {
-  const T q = x.v / y.v;
-  return {q, (x.d - q * y.d) / y.v};
-}
-template <typename T> __device__ __forceinline__ Dual<T>& operator+=(Dual<T>& x, Dual<T> y) { return x = x + y; }
-template <typename T> __device__ __forceinline__ Dual<T>& operator-=(Dual<T>& x, Dual<T> y) { return x = x - y; }
-template <typename T> __device__ __forceinline__ Dual<T>& operator*=(Dual<T>& x, Dual<T> y) { return x = x * y; }
-// input: value and tangent arrays (tangent NULL: 0)
-template <typename T> struct DIn {
-  const T* v; const T* d;
-  __device__ __forceinline__ DIn operator+(size_t o) const { return {v + o, d ? d + o : nullptr}; }
-  __device__ __forceinline__ Dual<T> operator[](size_t i) const { return {v[i], d ? d[i] : T(0)}; }
-  __device__ __forceinline__ explicit operator bool() const { return v != nullptr; }
-};
-// output: value and tangent arrays (either NULL: not stored)
-template <typename T> struct DRef {
-  T* v; T* d;
-  __device__ __forceinline__ void operator=(Dual<T> x) const {
-    if (v) *v = x.v;
-    if (d) *d = x.d;
-  }
-};
-template <typename T> struct DOut {
-  T* v; T* d;
-  __device__ __forceinline__ DOut operator+(size_t o) const { return {v ? v + o : nullptr, d ? d + o : nullptr}; }
-  __device__ __forceinline__ DRef<T> operator[](size_t i) const { return {v ? v + i : nullptr, d ? d + i : nullptr}; }
-};
-
+// (Dual / DIn / DOut: tn_node.h, shared with the TensorNet edge kernels' second order)
 template <typename T, typename P> __device__ __forceinline__ void ldc(T (&o)[9], P p, size_t nh) {
 #pragma unroll
   for (int k = 0; k < 9; ++k) o[k] = p[k * nh];

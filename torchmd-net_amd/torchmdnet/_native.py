@@ -78,6 +78,8 @@ SIGNATURES = {
     "tmdnet_nbr_embed_bwd2": (I, [I, I, I, P, P, P, I, P, I, P, I, P, P, I, P, P, P, P, P, P, P, P]),
     "tmdnet_tn_embed_fwd": (I, [I, I, I, P, P, I, D, P, I, P, P, P, I, P, P, P, P]),
     "tmdnet_tn_embed_bwd": (I, [I, I, I, P, P, I, D, P, I, P, P, P, I, P, P, P, P, P, P, P, P, P]),
+    "tmdnet_tn_embed_bwd2": (I, [I, I, I, P, P, I, D, P, I, P, P, P, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P,
+                                 P]),
     "tmdnet_tn_message_fwd": (I, [I, I, I, P, P, I, D, P, I, P, I, P, P, P]),
     "tmdnet_tn_message_bwd": (I, [I, I, I, P, P, I, D, P, I, P, I, P, P, P, P, P]),
     "tmdnet_tn_message_bwd_add": (I, [I, I, I, P, P, I, D, P, I, P, I, P, P, P, P, P, P]),

@@ -1946,6 +1946,9 @@ class _TNEmbedBwd(Function):
     def backward(ctx, *ggs):
         saved = ctx.saved_tensors
         _create = torch.is_grad_enabled()  # third order only if the caller builds a graph
+        from . import tn_node
+        if tn_node.SECOND_ORDER != "composite" and not _create and saved[0].is_cuda:
+            return _tn_embed_second_order(ctx, saved, ggs)
         with torch.enable_grad():
             leaves = [t.detach().requires_grad_(True) for t in saved]
             gE, P, Q, W, C, u = leaves
@@ -1957,6 +1960,36 @@ class _TNEmbedBwd(Function):
             second = torch.autograd.grad([f for f, _ in sel], leaves, [g for _, g in sel],
                                          create_graph=_create, allow_unused=True)
         return tuple(second) + (None,)
+
+
+def _tn_embed_second_order(ctx, saved, ggs):
+    """VJP of the embedding's first backward (gP, gQ, gW, gC, gu) = J^T gE for cotangents t of those outputs:
+    d_gE = J t and d_(P, Q, W, C, u) = H_<gE, E> t -- ONE tmdnet_tn_embed_bwd2 call (the first-order kernels on
+    dual numbers) instead of autograd's double differentiation of the composite (~370 launches per C3 step)."""
+    gE, P, Q, W, C, u = saved
+    graph = ctx.graph
+    need = ctx.needs_input_grad  # gE, P, Q, W, C, u, graph
+    t = [None if g is None else g.contiguous() for g in ggs]
+    if all(x is None for x in t):
+        return (None,) * 7
+    tW = t[2]
+    if tW is not None and tW.stride(0) != W.stride(0):
+        W = W.contiguous()
+        tW = tW.contiguous()
+    o = dict(dtype=P.dtype, device=P.device)
+    N, H = P.shape
+    E = graph.n_edges
+    outs = [torch.empty((9, N, H), **o) if need[0] else None,
+            torch.empty((N, H), **o) if need[1] else None, torch.empty((N, H), **o) if need[2] else None,
+            torch.empty((E, 3 * H), **o) if need[3] else None, torch.empty((E,), **o) if need[4] else None,
+            torch.empty((E, 3), **o) if need[5] else None]
+    lib = nat.load()
+    rc = lib.tmdnet_tn_embed_bwd2(nat.dtype_code(P.dtype), N, H, nat.ptr(graph.row_ptr), nat.ptr(graph.src),
+                                  graph.n_edges, *_self0_args(graph), nat.ptr(P), nat.ptr(Q), nat.ptr(W), _ld(W),
+                                  nat.ptr(C), nat.ptr(u), nat.ptr(gE), *[nat.ptr(x) for x in (t[0], t[1], tW, t[3], t[4])],
+                                  *[nat.ptr(x) for x in outs], nat.stream(P.device))
+    nat.check(rc, "tmdnet_tn_embed_bwd2")
+    return tuple(outs) + (None,)
 
 
 class _TNMessage(Function):
