@@ -588,6 +588,18 @@ int tmdnet_silu_fwd(int dtype, int rows, int cols, const void* x, int ld_x, cons
                     void* out, void* stream);
 int tmdnet_silu_bwd(int dtype, int rows, int cols, const void* x, int ld_x, const void* row_scale,
                     const void* grad_out, int ld_g, void* grad_x, void* grad_scale, void* stream);
+/* Second order of a Linear + SiLU stack (TensorNet's MLPs, tensornet.py:320-323, 381-385, 233, under
+ * force-matching training), per layer of the reverse-mode VJP of the first backward (all [rows][cols]):
+ *   tmdnet_mlp2_up:   ahat = ghat silu'(pre);  dpre = ghat a silu''(pre), or for the LAST layer (gy non-NULL:
+ *     a = gy * scale[r], scale nullable) dpre = ghat gy scale silu''(pre) + sbar[r] gy silu'(pre),
+ *     dgy = ahat scale + sbar[r] silu(pre) (nullable), dscale[r] = sum_c ahat gy (nullable); sbar nullable.
+ *   tmdnet_mlp2_down: c = dp + dh silu'(pre) (c may alias dp).
+ * pre: row stride ld_pre; a: ld_a; the rest contiguous. */
+int tmdnet_mlp2_up(int dtype, int rows, int cols, const void* pre, int ld_pre, const void* ghat, const void* a,
+                   int ld_a, const void* gy, const void* scale, const void* sbar, void* ahat, void* dpre, void* dgy,
+                   void* dscale, void* stream);
+int tmdnet_mlp2_down(int dtype, int rows, int cols, const void* pre, int ld_pre, const void* dh, const void* dp,
+                     void* c, void* stream);
 
 /* Per-molecule energy (TorchMD_Net.forward, model.py:263-283 with output_modules.py:27-43):
  *   y[b] = *mean + *std * sum_{n: batch[n] = b} x[n],  b < n_mol <= 8192  (std / mean: device

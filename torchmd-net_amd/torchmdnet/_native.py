@@ -90,6 +90,8 @@ SIGNATURES = {
     "tmdnet_tn_node_bwd2": (I, [I, I, I, I, P, P, P, P, P, P, P, P, P]),
     "tmdnet_silu_fwd": (I, [I, I, I, P, I, P, P, P]),
     "tmdnet_silu_bwd": (I, [I, I, I, P, I, P, P, I, P, P, P]),
+    "tmdnet_mlp2_up": (I, [I, I, I, P, I, P, P, I, P, P, P, P, P, P, P, P]),
+    "tmdnet_mlp2_down": (I, [I, I, I, P, I, P, P, P, P]),
     "tmdnet_atom_sum_fwd": (I, [I, I, I, P, P, P, P, P, P]),
     "tmdnet_atom_sum_bwd": (I, [I, I, I, P, P, P, P, P]),
     "tmdnet_dot_sum_fwd": (I, [I, I, I, P, I, P, P, I, P, P, P, P, P]),

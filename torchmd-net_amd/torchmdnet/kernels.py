@@ -2726,12 +2726,14 @@ class _MLPActBwd(Function):
         silu_bwd_launch(pres[-1], scale, gy, gpre, gs)
         gpres = [None] * L
         gpres[L - 1] = gpre
+        ups = [None] * L  # a_{i-1} = g_pre_i W_i before the silu' factor (the hand second order reads them)
         gx = None
         for i in range(L - 1, -1, -1):
             if i > 0:  # the lower layer's pre-activation gradient: (g_pre_i W_i) * silu'(pre_{i-1})
                 g = torch.empty_like(pres[i - 1])
-                gemm_ex_launch([{"A": gpres[i], "B": ws[i], "trans_b": False, "C": g, "dpre": pres[i - 1]}]) or \
-                    _raise("mlp_act backward: GEMM envelope")
+                ups[i - 1] = torch.empty_like(pres[i - 1])
+                gemm_ex_launch([{"A": gpres[i], "B": ws[i], "trans_b": False, "C": g, "dpre": pres[i - 1],
+                                 "pre": ups[i - 1]}]) or _raise("mlp_act backward: GEMM envelope")
                 gpres[i - 1] = g
             elif need[0]:
                 gx = torch.empty_like(x)
@@ -2749,16 +2751,20 @@ class _MLPActBwd(Function):
                 else:
                     tn.append({"A": gpres[i], "B": None, "C": gb[i].view(-1, 1), "ones": True})
         wgrad_tn(tn)
-        ctx.save_for_backward(gy, x, scale, *ws, *bs)
+        ctx.save_for_backward(gy, x, scale, *ws, *bs, *pres, *hmid, *gpres, *ups[:L - 1])
         ctx.L = L
         return (gx, gs, *gw, *gb)
 
     @staticmethod
     def backward(ctx, *ggs):
+        from . import tn_node
         from .tn_node import _double_backward
         L = ctx.L
         sv = ctx.saved_tensors
         gy, x, scale = sv[0], sv[1], sv[2]
+        if tn_node.SECOND_ORDER != "composite" and not torch.is_grad_enabled() and x.is_cuda \
+                and x.dtype == torch.float32:
+            return _mlp_second_order(ctx, sv, ggs)
         wb = list(sv[3:3 + 2 * L])
         d = _double_backward(_mlp_composite, [x, scale] + wb, [gy], list(ggs))
         # (need, gy, x, scale, *ws, *bs, *pres, *hmid): pres / hmid are functions of the others
@@ -2767,6 +2773,94 @@ class _MLPActBwd(Function):
 
 def _raise(msg):
     raise RuntimeError(msg)
+
+
+def _mlp_second_order(ctx, sv, ggs):
+    """Hand-written VJP of _MLPActBwd (the Linear + SiLU stack's first backward: a_{L-1} = gy s, g_i = a_i
+    silu'(p_i), a_{i-1} = g_i W_i, gW_i = g_i^T h_i, gb_i = colsum g_i, gx = g_0 W_0, gs = rowsum gy silu(p_{L-1}))
+    for cotangents (X, S, Wbar_i, Bbar_i) of (gx, gs, gW_i, gb_i), instead of autograd's double differentiation
+    of the composite (~100 launches per TensorNet edge MLP).  Up the layers, the adjoint of g_i,
+        ghat_i = (i = 0: X W_0^T | else ahat_{i-1} W_i^T) + h_i Wbar_i^T + Bbar_i,
+    gives ahat_i = ghat_i silu'(p_i) and the adjoint of p_i, dp_i = ghat_i a_i silu''(p_i) (last layer: + the gs
+    terms, and the adjoints of gy and s) (tmdnet_mlp2_up); the h_i adjoints g_i Wbar_i and the W_i adjoints
+    g_i^T (X | ahat_{i-1}) are injected.  Down the layers the p / h adjoints go back through the forward:
+    c_i = dp_i + dh_{i+1} silu'(p_i) (tmdnet_mlp2_down), dW_i += c_i^T h_i, db_i = colsum c_i, dh_i = c_i W_i +
+    g_i Wbar_i, dx = dh_0.  GEMMs on the hand-written kernels (gemm_group, wgrad_tn)."""
+    L = ctx.L
+    gy, x, scale = sv[0], sv[1], sv[2]
+    ws, bs = sv[3:3 + L], sv[3 + L:3 + 2 * L]
+    pres, hmid = sv[3 + 2 * L:3 + 3 * L], sv[3 + 3 * L:2 + 4 * L]
+    gpres, ups = sv[2 + 4 * L:2 + 5 * L], sv[2 + 5 * L:]
+    hs = (x,) + tuple(hmid)
+    X, S = ggs[0], ggs[1]
+    Wb, Bb = ggs[2:2 + L], ggs[2 + L:2 + 2 * L]
+    need = ctx.needs_input_grad  # (need, gy, x, scale, *ws, *bs, *pres, *hmid)
+    M = x.shape[0]
+    o = dict(dtype=x.dtype, device=x.device)
+    lib = nat.load()
+    st = nat.stream(x.device)
+    dps, ahats, injs = [None] * L, [None] * L, [None] * L
+    dgy = torch.empty_like(gy) if need[1] else None
+    ds = torch.empty(M, **o) if (scale is not None and need[3]) else None
+    for i in range(L):
+        N = ws[i].shape[0]
+        ghat = torch.empty((M, N), **o)
+        up = X if i == 0 else ahats[i - 1]
+        probs = []
+        if up is not None:
+            probs.append((up.contiguous(), ws[i], True, None, ghat, False))
+        if Wb[i] is not None:
+            probs.append((hs[i], Wb[i].contiguous(), True, None, ghat, bool(probs)))
+        if not probs:
+            ghat.zero_()
+        for q in probs:  # (sequential: the second accumulates)
+            gemm_group([q])
+        if Bb[i] is not None:
+            ghat.add_(Bb[i])
+        ah, dp = torch.empty_like(ghat), torch.empty_like(ghat)
+        last = i == L - 1
+        rc = lib.tmdnet_mlp2_up(nat.dtype_code(x.dtype), M, N, nat.ptr(pres[i]), pres[i].stride(0), nat.ptr(ghat),
+                                None if last else nat.ptr(ups[i]), 0 if last else ups[i].stride(0),
+                                nat.ptr(gy) if last else None, nat.ptr(scale) if last else None,
+                                nat.ptr(S.contiguous()) if (last and S is not None) else None, nat.ptr(ah), nat.ptr(dp),
+                                nat.ptr(dgy) if last else None, nat.ptr(ds) if last else None, st)
+        nat.check(rc, "tmdnet_mlp2_up")
+        ahats[i], dps[i] = ah, dp
+        if Wb[i] is not None:  # gW_i = g_i^T h_i -> the adjoint of h_i gets g_i Wbar_i
+            injs[i] = torch.empty_like(hs[i])
+            gemm_group([(gpres[i], Wb[i].contiguous(), False, None, injs[i], False)])
+    if dgy is not None and not need[1]:
+        dgy = None
+    dW = [torch.empty_like(w) if need[4 + i] else None for i, w in enumerate(ws)]
+    dB = [torch.empty_like(b) if need[4 + L + i] else None for i, b in enumerate(bs)]
+    dx = None
+    c = dps[L - 1]
+    for i in range(L - 1, -1, -1):
+        up = X if i == 0 else ahats[i - 1]
+        if dW[i] is not None or dB[i] is not None:
+            prob = {"A": c, "B": hs[i] if dW[i] is not None else None,
+                    "C": dW[i] if dW[i] is not None else dB[i].view(-1, 1),
+                    "Cb": dB[i] if (dW[i] is not None and dB[i] is not None) else None,
+                    "ones": dB[i] is not None}
+            if dW[i] is not None and up is not None:  # + g_i^T (X | ahat_{i-1}) (from gx = g_0 W_0 / a_{i-1} = g_i W_i)
+                prob.update(A2=gpres[i], B2=up.contiguous())
+            wgrad_tn([prob])
+        if i == 0 and not need[2]:
+            break
+        dh = torch.empty_like(hs[i])
+        gemm_group([(c, ws[i], False, None, dh, False)])
+        if injs[i] is not None:
+            dh.add_(injs[i])
+        if i == 0:
+            dx = dh
+        else:
+            cn = torch.empty_like(dps[i - 1])
+            rc = lib.tmdnet_mlp2_down(nat.dtype_code(x.dtype), M, cn.shape[1], nat.ptr(pres[i - 1]),
+                                      pres[i - 1].stride(0), nat.ptr(dh), nat.ptr(dps[i - 1]), nat.ptr(cn), st)
+            nat.check(rc, "tmdnet_mlp2_down")
+            c = cn
+    n_rest = len(ctx.needs_input_grad) - 4 - 2 * L
+    return (None, dgy, dx, ds, *dW, *dB) + (None,) * n_rest
 
 
 # TMDNET_MLP_ACT=0: the Linear + fused_act composite per layer instead (A/B switch)
