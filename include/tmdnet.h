@@ -632,6 +632,13 @@ int tmdnet_layernorm_fwd_f32(int rows, int C, const void* x, int ldx, const void
 int tmdnet_layernorm_bwd_f32(int rows, int C, const void* x, int ldx, const void* w, const void* mean,
                              const void* rstd, const void* grad_y, int ldg, void* grad_x, int accumulate,
                              void* stream);
+/* Second order (force-matching training through TensorNet's LayerNorms): for cotangents t_gx [rows][C],
+ * t_gw [C], t_gb [C] (each nullable) of the first backward's (grad_x, grad_w, grad_b): d_grad_y, d_x [rows][C]
+ * (nullable) and t_row [rows][C] (nullable) = rstd (t_gx - mean t_gx - xhat mean(t_gx xhat)), from which the
+ * caller forms d_w = colsum(grad_y t_row) (d_b = 0). */
+int tmdnet_layernorm_bwd2_f32(int rows, int C, const void* x, int ldx, const void* w, const void* mean,
+                              const void* rstd, const void* grad_y, int ldg, const void* t_gx, const void* t_gw,
+                              const void* t_gb, void* d_grad_y, void* d_x, void* t_row, void* stream);
 size_t tmdnet_layernorm_wgrad_workspace_bytes(int rows, int C);
 int tmdnet_layernorm_wgrad_f32(int rows, int C, const void* x, int ldx, const void* mean, const void* rstd,
                                const void* grad_y, int ldg, void* grad_w, void* grad_b, void* workspace,

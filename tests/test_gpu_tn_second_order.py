@@ -162,6 +162,31 @@ def test_mlp_second_order_matches_composite(layers, scaled, monkeypatch):
         assert _rel(a, b) < 1e-4
 
 
+@pytest.mark.parametrize("C", [128, 384])
+def test_layer_norm_second_order_matches_composite(C, monkeypatch):
+    """TensorNet's LayerNorms (init_norm C = H, out_norm C = 3H) differentiated twice: the hand second order
+    (tmdnet_layernorm_bwd2_f32) vs autograd's double differentiation of the composite (fp32 and fp64)."""
+    from torchmdnet import kernels, tn_node
+    g = torch.Generator(device=DEV).manual_seed(C)
+    M = 300
+    rn = lambda *sh: torch.randn(*sh, device=DEV, generator=g)  # noqa: E731
+    x, w, b, gy = rn(M, C) * 2 + 0.5, rn(C), rn(C), rn(M, C)
+    tang = [rn(M, C), rn(C), rn(C)]
+
+    def second(mode, dtype):
+        monkeypatch.setattr(tn_node, "SECOND_ORDER", mode)
+        xs = [t.to(dtype).clone().requires_grad_(True) for t in (x, w, b)]
+        g0 = gy.to(dtype).clone().requires_grad_(True)
+        y = kernels._ln_composite(*xs, 1e-5) if dtype == torch.float64 else kernels.layer_norm(*xs, 1e-5)
+        first = torch.autograd.grad(y, xs, g0, create_graph=True)
+        return torch.autograd.grad(first, xs[:2] + [g0], [t.to(dtype) for t in tang], allow_unused=True)
+
+    hip, comp, ref = second("hip", torch.float32), second("composite", torch.float32), second("composite", torch.float64)
+    for a, bb, r in zip(hip, comp, ref):
+        assert _rel(a.double(), r) < 1e-4
+        assert _rel(a, bb) < 1e-4
+
+
 def test_embedding_second_order_matches_composite(monkeypatch):
     """TensorEmbedding's aggregation (tensornet.py:295-315) differentiated twice: the hand second order
     (tmdnet_tn_embed_bwd2: the first-order kernels on dual numbers) vs autograd's double differentiation of

@@ -81,6 +81,71 @@ __global__ __launch_bounds__(256) void k_bwd(int rows, int C, const float* __res
   }
 }
 
+// Second order (force-matching training through TensorNet's init_norm / out_norm): the VJP of the first
+// backward (gx = r (G - mean G - h mean(G h)), G = gy w, h = (x - mean) r; gw = colsum gy h; gb = colsum gy) for
+// cotangents (X, Wb, Bb) of (gx, gw, gb), per row (one wave):
+//   T     = r (X - mean X - h mean(X h))                      (dw = colsum gy T, formed by the caller)
+//   d_gy  = w T + Wb h + Bb
+//   u     = -r (G mean(X h) + mean(G h) X) + Wb gy            (the adjoint of h)
+//   v     = sum X (G - mean G - h mean(G h))                  (the adjoint of r, times r)
+//   d_x   = r (u - mean u - h mean(u h)) - v r^2 h / C
+template <int CPL>
+__global__ __launch_bounds__(256) void k_bwd2(int rows, int C, const float* __restrict__ x, int ldx,
+                                              const float* __restrict__ w, const float* __restrict__ mean,
+                                              const float* __restrict__ rstd, const float* __restrict__ gy, int ldg,
+                                              const float* __restrict__ X, const float* __restrict__ Wb,
+                                              const float* __restrict__ Bb, float* __restrict__ dgy,
+                                              float* __restrict__ dx, float* __restrict__ T) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = lane_id();
+  if (row >= rows) return;
+  const float mu = mean[row], rs = rstd[row];
+  const float* xr = x + (size_t)row * ldx;
+  const float* gr = gy + (size_t)row * ldg;
+  float h[CPL], G[CPL], Xv[CPL], g[CPL];
+  float sx = 0.f, sxh = 0.f, sg = 0.f, sgh = 0.f, sxg = 0.f;
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) {
+    const int c = lane + 64 * j;
+    const bool on = c < C;
+    h[j] = on ? (xr[c] - mu) * rs : 0.f;
+    g[j] = on ? gr[c] : 0.f;
+    G[j] = on ? g[j] * w[c] : 0.f;
+    Xv[j] = (on && X) ? X[(size_t)row * C + c] : 0.f;
+    sx += Xv[j];
+    sxh += Xv[j] * h[j];
+    sg += G[j];
+    sgh += G[j] * h[j];
+    sxg += Xv[j] * G[j];
+  }
+  const float invC = 1.f / (float)C;
+  const float mX = wave_sum(sx) * invC, mXh = wave_sum(sxh) * invC, mG = wave_sum(sg) * invC,
+              mGh = wave_sum(sgh) * invC, SXG = wave_sum(sxg);
+  const float v = SXG - (float)C * (mG * mX + mGh * mXh);
+  float u[CPL];
+  float su = 0.f, suh = 0.f;
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) {
+    const int c = lane + 64 * j;
+    const bool on = c < C;
+    const float wb = (on && Wb) ? Wb[c] : 0.f;
+    const float t = rs * (Xv[j] - mX - h[j] * mXh);
+    if (on) {
+      if (T) T[(size_t)row * C + c] = t;
+      if (dgy) dgy[(size_t)row * C + c] = w[c] * t + wb * h[j] + ((Bb) ? Bb[c] : 0.f);
+    }
+    u[j] = on ? -rs * (G[j] * mXh + mGh * Xv[j]) + wb * g[j] : 0.f;
+    su += u[j];
+    suh += u[j] * h[j];
+  }
+  if (!dx) return;
+  const float mu_ = wave_sum(su) * invC, muh = wave_sum(suh) * invC;
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) {
+    const int c = lane + 64 * j;
+    if (c < C) dx[(size_t)row * C + c] = rs * (u[j] - mu_ - h[j] * muh) - v * rs * rs * h[j] * invC;
+  }
+}
+
 // weight / bias gradient partials: block k sums rows [k * chunk, (k + 1) * chunk) for every column.  The
 // chunk is short (>= 16 rows, at most ~256 chunks): a C2 out_norm (678 x 128) at 128-row chunks was 6
 // blocks walking 128 dependent rows each, 34 us.
@@ -183,5 +248,23 @@ extern "C" int tmdnet_layernorm_wgrad_f32(int rows, int C, const void* x, int ld
                      (const float*)mean, (const float*)rstd, (const float*)grad_y, ldg, (float*)workspace);
   hipLaunchKernelGGL(ln::k_wgrad_sum, dim3((C + 255) / 256), dim3(256), 0, st, C, chunks, (const float*)workspace,
                      (float*)grad_w, (float*)grad_b);
+  return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
+}
+
+extern "C" int tmdnet_layernorm_bwd2_f32(int rows, int C, const void* x, int ldx, const void* w, const void* mean,
+                                         const void* rstd, const void* grad_y, int ldg, const void* t_gx,
+                                         const void* t_gw, const void* t_gb, void* d_grad_y, void* d_x, void* t_row,
+                                         void* stream) {
+  if (rows < 0 || C <= 0 || C > 1024 || ldx < C || ldg < C || !x || !w || !mean || !rstd || !grad_y)
+    return kBadArgument;
+  if (rows == 0) return kOk;
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 g((rows + 3) / 4), t(256);
+#define TMD_F(K)                                                                                                  \
+  hipLaunchKernelGGL(ln::k_bwd2<K>, g, t, 0, st, rows, C, (const float*)x, ldx, (const float*)w, (const float*)mean, \
+                     (const float*)rstd, (const float*)grad_y, ldg, (const float*)t_gx, (const float*)t_gw,          \
+                     (const float*)t_gb, (float*)d_grad_y, (float*)d_x, (float*)t_row)
+  TMD_LN_CPL(C, TMD_F);
+#undef TMD_F
   return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed;
 }

@@ -99,6 +99,7 @@ SIGNATURES = {
     "tmdnet_dot_sum_fwd_atoms": (I, [I, I, I, P, I, P, P, I, P, P, P, P, P, P]),
     "tmdnet_layernorm_fwd_f32": (I, [I, I, P, I, P, P, D, P, I, P, P, P]),
     "tmdnet_layernorm_bwd_f32": (I, [I, I, P, I, P, P, P, P, I, P, I, P]),
+    "tmdnet_layernorm_bwd2_f32": (I, [I, I, P, I, P, P, P, P, I, P, P, P, P, P, P, P]),
     "tmdnet_layernorm_wgrad_workspace_bytes": (SZ, [I, I]),
     "tmdnet_layernorm_wgrad_f32": (I, [I, I, P, I, P, P, P, I, P, P, P, SZ, P]),
     "tmdnet_gemm_f32": (I, [I, P, P, P]),

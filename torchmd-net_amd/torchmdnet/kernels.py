@@ -2964,15 +2964,34 @@ class _LayerNormBwd(Function):
             rc = lib.tmdnet_layernorm_wgrad_f32(rows, C, nat.ptr(x), x.stride(0), nat.ptr(mean), nat.ptr(rstd),
                                                 nat.ptr(gy), gy.stride(0), nat.ptr(gw), nat.ptr(gb), nat.ptr(ws), wsb, st)
             nat.check(rc, "tmdnet_layernorm_wgrad_f32")
-        ctx.save_for_backward(gy, x, w, b)
+        ctx.save_for_backward(gy, x, w, b, mean, rstd)
         ctx.eps = eps
         return gx, gw, gb
 
     @staticmethod
     def backward(ctx, ggx, ggw, ggb):
-        # second order (force-matching training): differentiate the composite LayerNorm twice
-        gy, x, w, b = ctx.saved_tensors
+        gy, x, w, b, mean, rstd = ctx.saved_tensors
         eps = ctx.eps
+        from . import tn_node
+        if tn_node.SECOND_ORDER != "composite" and not torch.is_grad_enabled() and x.is_cuda \
+                and x.dtype == torch.float32 and x.shape[1] <= 1024:
+            # hand second order (tmdnet_layernorm_bwd2_f32): one pass per row + the weight's column sum
+            need = ctx.needs_input_grad  # gy, x, w, b, mean, rstd, eps, need
+            rows, C = x.shape
+            d_gy = torch.empty_like(gy) if need[0] else None
+            d_x = torch.empty_like(x) if need[1] else None
+            t_row = torch.empty((rows, C), dtype=x.dtype, device=x.device) if (need[2] and ggx is not None) else None
+            cont = lambda t: None if t is None else t.contiguous()  # noqa: E731
+            rc = nat.load().tmdnet_layernorm_bwd2_f32(
+                rows, C, nat.ptr(x), x.stride(0), nat.ptr(w), nat.ptr(mean), nat.ptr(rstd), nat.ptr(gy), gy.stride(0),
+                nat.ptr(cont(ggx)), nat.ptr(cont(ggw)), nat.ptr(cont(ggb)), nat.ptr(d_gy), nat.ptr(d_x), nat.ptr(t_row),
+                nat.stream(x.device))
+            nat.check(rc, "tmdnet_layernorm_bwd2_f32")
+            d_w = None
+            if need[2]:
+                d_w = (gy * t_row).sum(0) if t_row is not None else torch.zeros_like(w)
+            return d_gy, d_x, d_w, None, None, None, None, None
+        # composite: differentiate the composite LayerNorm twice
         d = _tn_double_backward(lambda x_, w_, b_: _ln_composite(x_, w_, b_, eps), [x, w, b], [gy], [ggx, ggw, ggb])
         return d[0], d[1], d[2], d[3], None, None, None, None
 
