@@ -1125,17 +1125,10 @@ bool gemm_x3_into(const Tensor& A, const Tensor& B, bool trans_b, const Tensor& 
         (!bias.defined() || (bias.is_contiguous() && al(bias)))))
     return false;
   void* st = stream_of(A);
-  // the weight split inside the GEMM while it is staged in LDS (no split launch; kernels.X3_WSPLIT)
-  int rc = tmdnet_gemm_x3w_f32(M, N, K, A.data_ptr(), static_cast<int>(A.stride(0)), B.data_ptr(),
-                               static_cast<int>(B.stride(0)), trans_b ? 1 : 0, bias.defined() ? bias.data_ptr() : nullptr,
-                               C.data_ptr(), static_cast<int>(C.stride(0)), beta ? 1 : 0, 0, nullptr, nullptr, nullptr, 0,
-                               st);
-  if (rc != TMDNET_UNSUPPORTED) {
-    check(rc, "tmdnet_gemm_x3w_f32");
-    return true;
-  }
+  // (a split launch per call, as kernels.X3_WSPLIT = "launch": faster at C5 than the in-kernel split of
+  // tmdnet_gemm_x3w_f32, and nothing cached)
   Tensor bp = at::empty({3, N, K}, A.options().dtype(at::kShort));
-  rc = trans_b ? tmdnet_proj_split_f32(N, K, B.data_ptr(), static_cast<int>(B.stride(0)), bp.data_ptr(), st)
+  int rc = trans_b ? tmdnet_proj_split_f32(N, K, B.data_ptr(), static_cast<int>(B.stride(0)), bp.data_ptr(), st)
                    : tmdnet_split_t_f32(N, K, B.data_ptr(), static_cast<int>(B.stride(0)), bp.data_ptr(), st);
   if (rc == TMDNET_UNSUPPORTED) return false;
   check(rc, "tmdnet_split");

@@ -1467,9 +1467,12 @@ def gemm_launch(problems):
 # above GEMM_MAX_ROWS (C5-size systems) fp32 GEMMs run on tmdnet_gemm_x3_f32 (bf16 MFMA, exact three-piece
 # split, fp32 accuracy); TMDNET_GEMM_BIG=lib keeps the library GEMM there (A/B switch)
 GEMM_BIG = os.environ.get("TMDNET_GEMM_BIG", "x3")
-# where the weight's bf16 pieces come from: "kernel" = split inside the GEMM while staged in LDS
-# (tmdnet_gemm_x3w_f32), "launch" = a split launch per call (tmdnet_proj_split_f32 / tmdnet_split_t_f32; A/B)
-X3_WSPLIT = os.environ.get("TMDNET_X3_WSPLIT", "kernel")
+# where the weight's bf16 pieces come from: "launch" = a split launch per call (tmdnet_proj_split_f32 /
+# tmdnet_split_t_f32, ~5 us each; nothing cached, so in-place weight updates are always seen), "kernel" = split
+# inside the GEMM while staged in LDS (tmdnet_gemm_x3w_f32: no split launch, but every workgroup re-splits its
+# weight tile -- measured slower: C5 ET 50.8-51.1 vs 48.3-49.1 ms, C5 TensorNet 35.5 vs 34.2 ms per evaluation,
+# the transposed form's 2-byte LDS scatter and the split VALU work competing with the MFMA chain)
+X3_WSPLIT = os.environ.get("TMDNET_X3_WSPLIT", "launch")
 
 
 def _al16(*ts):
