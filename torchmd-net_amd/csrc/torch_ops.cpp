@@ -1113,9 +1113,8 @@ constexpr double kLnEps = 1e-5;  // nn.LayerNorm default (reference torchmd_et.p
 
 int64_t stack_np(bool hk, bool hv) { return 11 + 2 * int64_t(hk) + 2 * int64_t(hv); }
 
-// Large-row fp32 GEMM on the x3 kernel (kernels.gemm_x3): B split inside the kernel (tmdnet_gemm_x3w_f32; a
-// [N][K] weight with trans_b, a [K][N] right operand without), else by a split launch; false when outside
-// its envelope
+// Large-row fp32 GEMM on tmdnet_gemm_x3_f32 (kernels.gemm_x3): B split per call (a [N][K] weight with
+// trans_b, a [K][N] right operand without); false when outside its envelope
 bool gemm_x3_into(const Tensor& A, const Tensor& B, bool trans_b, const Tensor& bias, const Tensor& C, bool beta) {
   const int M = static_cast<int>(A.size(0)), N = static_cast<int>(C.size(1)), K = static_cast<int>(A.size(1));
   auto al = [](const Tensor& t) { return !t.defined() || reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0; };
