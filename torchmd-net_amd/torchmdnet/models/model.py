@@ -20,8 +20,14 @@ from .. import priors
 
 def create_model(args, prior_model=None, mean=None, std=None):
     dtype = dtype_mapping[args["precision"]]
+    # precision 16 (reference dtype_mapping[16] = float16, models/utils.py:586): parameters and buffers are
+    # STORED in float16 (the reference's state_dict dtype), the hot path computes in float32 on upcast copies
+    # of them (TorchMD_Net.half_storage_); its outputs are returned in float16
+    half = dtype == torch.float16
+    if half:
+        dtype = torch.float32
     if dtype not in (torch.float32, torch.float64):
-        raise NotImplementedError("torchmd-net_amd computes in float32 or float64 (precision 32/64)")
+        raise NotImplementedError("torchmd-net_amd computes in float32 or float64 (precision 16/32/64)")
     shared_args = dict(
         hidden_channels=args["embedding_dimension"],
         num_layers=args["num_layers"],
@@ -72,8 +78,9 @@ def create_model(args, prior_model=None, mean=None, std=None):
         reduce_op=args["reduce_op"],
         dtype=dtype,
     )
-    return TorchMD_Net(representation_model, output_model, prior_model=prior_model, mean=mean, std=std,
-                       derivative=args["derivative"], dtype=dtype)
+    model = TorchMD_Net(representation_model, output_model, prior_model=prior_model, mean=mean, std=std,
+                        derivative=args["derivative"], dtype=dtype)
+    return model.half_storage_() if half else model
 
 
 def load_model(filepath, args=None, device="cpu", **kwargs):
@@ -148,6 +155,36 @@ class TorchMD_Net(nn.Module):
         # TorchScript in eval mode: the whole energy + force evaluation as one operator
         # (tmdnet::et_energy_forces) when the configuration is the one it implements
         self.fused_eval = self._fused_eval_capable()
+        # precision 16: float16 storage, float32 arithmetic (half_storage_)
+        self._half_storage = False
+        self._half_inner = False
+
+    @torch.jit.unused
+    def half_storage_(self):
+        """The reference's precision=16 (``dtype_mapping[16]`` = float16, models/utils.py:586; scripts/train.py:43):
+        every floating parameter and buffer is STORED in float16 -- the state_dict a precision-16 reference
+        checkpoint holds -- while the HIP kernels (fp32 / fp64 only) compute on float32 upcasts of them, made per
+        call (differentiable: gradients reach the float16 parameters through the casts).  Energies and forces
+        come back in float16.  Arithmetic is therefore the fp32 path's on fp16-rounded weights; the gate is the
+        looser precision-16 one (tests/test_gpu_precision16.py)."""
+        self.to(torch.float16)
+        self._half_storage = True
+        self.fused_eval = False
+        return self
+
+    @torch.jit.unused
+    def _forward_half(self, z, pos, batch, q, s, extra_args):
+        import itertools
+        from torch.func import functional_call
+        state = {n: (t.float() if t.is_floating_point() else t)
+                 for n, t in itertools.chain(self.named_parameters(), self.named_buffers())}
+        self._half_inner = True
+        try:
+            y, neg_dy = functional_call(self, state, (z, pos.float() if pos.is_floating_point() else pos, batch),
+                                        {"q": q, "s": s, "extra_args": extra_args}, strict=False)
+        finally:
+            self._half_inner = False
+        return y.half(), (None if neg_dy is None else neg_dy.half())
 
     @torch.jit.unused
     def _fused_eval_capable(self) -> bool:
@@ -210,10 +247,17 @@ class TorchMD_Net(nn.Module):
                 ) -> Tuple[Tensor, Optional[Tensor]]:
         assert z.dim() == 1 and z.dtype == torch.long
         batch = torch.zeros_like(z) if batch is None else batch
+        if torch.jit.is_scripting():
+            if self._half_storage:
+                raise RuntimeError("torchmd-net_amd: precision-16 models run eagerly (float16 storage, float32 "
+                                   "arithmetic); script a precision-32 copy")
+            if self.derivative:
+                pos.requires_grad_(True)
+            return self._forward_script(z, pos, batch, q, s, extra_args)
+        if self._half_storage and not self._half_inner:
+            return self._forward_half(z, pos, batch, q, s, extra_args)
         if self.derivative:
             pos.requires_grad_(True)
-        if torch.jit.is_scripting():
-            return self._forward_script(z, pos, batch, q, s, extra_args)
         self._early_dim_size(batch)
         x, v, z, pos, batch = self.representation_model(z, pos, batch, q=q, s=s)
         fused = None
