@@ -1697,7 +1697,17 @@ static int gemm_x3_launch(int M, int N, int K, const void* A, int lda, const voi
   // (N = H: one column tile, A read once); 2 row blocks per wave (128 rows per workgroup).  Wide-form
   // alternatives measured slower at C5 (us for qkv / o / vec_proj): <2,64,1> 75.6 / 50.0 / 150.7,
   // <2,64,2> 93.8 / 58.3 / 167.3, <1,64,4> 106.1 / 65.2 / 192.0, <1,64,2> 96.6 / 59.2 / 181.9
-  const int bn = (N >= 256 || N <= 64) ? 64 : 128;
+  // TMDNET_X3_BN = 64 / 128 forces the tile width (A/B; read once per process)
+  static const int bn_env = [] {
+    const char* e = getenv("TMDNET_X3_BN");
+    return e ? atoi(e) : 0;
+  }();
+  // auto: 128-column tiles for the narrow outputs (N < 256) and, for wide ones, from 131072 rows on (measured,
+  // tools/x3_time.py / x3_tn_time.py: C5 ET vec_fwd 150k rows 155 -> 148 us, TensorNet's 1M-row edge MLP
+  // 2110 -> 1836 us (256 -> 384), 1001 -> 854 (128 -> 256); at 50k rows the 64-wide form stays ahead: qkv_fwd
+  // 79 vs 83, o_fwd 51 vs 56 us)
+  const int bn = bn_env == 64 || bn_env == 128 ? bn_env
+                                               : (N <= 64 ? 64 : (N < 256 || M >= 131072) ? 128 : 64);
   P.nx = (N + bn - 1) / bn;
   P.ny = (M + 127) / 128;
   P.remap = remap_env && P.nx > 1 && (long long)P.nx * P.ny < (1ll << 31);
