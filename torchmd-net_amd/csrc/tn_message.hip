@@ -172,21 +172,37 @@ __global__ __launch_bounds__(64 * S) void k_embed_fwd(AT A) {
 #pragma unroll
   for (int k = 0; k < 9; ++k) acc[k] = T(0);
   const int b = min(A.row_ptr[n], A.cap), e = min(A.row_ptr[n + 1], A.cap);
-  for (int k = b + w; k < e; k += S) {
-    const int m = A.src[k];
-    TMD_DCHECK(m >= 0 && m < A.n);
-    const T mult = (m == n && n == 0) ? mult0_of(A) : T(1);
-    const T zc = (Pn + A.Q[(size_t)m * A.H + hc]) * A.C[k] * mult;
-    const auto wr = A.W + (size_t)k * A.ldw;
-    const T w1 = wr[hc] * zc, w2 = wr[A.H + hc] * zc, w3 = wr[2 * A.H + hc] * zc;
-    T sk[3], sy[5];
-    skew_c(sk, -A.u[3 * k], -A.u[3 * k + 1], -A.u[3 * k + 2]);
-    sym_c(sy, -A.u[3 * k], -A.u[3 * k + 1], -A.u[3 * k + 2]);
-    acc[0] += w1;
+  // two edges per iteration (k, k + S: the one-at-a-time order), every load of both issued before the math
+  for (int k = b + w; k < e; k += 2 * S) {
+    const bool two = k + S < e;
+    const int kk[2] = {k, two ? k + S : k};
+    int m[2];
+    T q[2], cc[2], wv[2][3], ux[2], uy[2], uz[2];
 #pragma unroll
-    for (int i = 0; i < 3; ++i) acc[1 + i] += w2 * sk[i];
+    for (int j = 0; j < 2; ++j) {
+      m[j] = A.src[kk[j]];
+      TMD_DCHECK(m[j] >= 0 && m[j] < A.n);
+      q[j] = A.Q[(size_t)m[j] * A.H + hc];
+      cc[j] = A.C[kk[j]];
+      const auto wr = A.W + (size_t)kk[j] * A.ldw;
+      wv[j][0] = wr[hc]; wv[j][1] = wr[A.H + hc]; wv[j][2] = wr[2 * A.H + hc];
+      ux[j] = -A.u[3 * kk[j]]; uy[j] = -A.u[3 * kk[j] + 1]; uz[j] = -A.u[3 * kk[j] + 2];
+    }
 #pragma unroll
-    for (int i = 0; i < 5; ++i) acc[4 + i] += w3 * sy[i];
+    for (int j = 0; j < 2; ++j) {
+      if (j == 1 && !two) break;
+      const T mult = (m[j] == n && n == 0) ? mult0_of(A) : T(1);
+      const T zc = (Pn + q[j]) * cc[j] * mult;
+      const T w1 = wv[j][0] * zc, w2 = wv[j][1] * zc, w3 = wv[j][2] * zc;
+      T sk[3], sy[5];
+      skew_c(sk, ux[j], uy[j], uz[j]);
+      sym_c(sy, ux[j], uy[j], uz[j]);
+      acc[0] += w1;
+#pragma unroll
+      for (int i = 0; i < 3; ++i) acc[1 + i] += w2 * sk[i];
+#pragma unroll
+      for (int i = 0; i < 5; ++i) acc[4 + i] += w3 * sy[i];
+    }
   }
   if (fold_waves<T, 9, S>(acc, red) && on) stc(A.E + (size_t)n * A.H + h, A.nh, acc);
 }
@@ -212,54 +228,80 @@ __global__ __launch_bounds__(64 * S) void k_embed_bwd_dst(AT A) {
     gPn[c] = T(0);
   }
   const int b = min(A.row_ptr[n], A.cap), e = min(A.row_ptr[n + 1], A.cap);
-  for (int k = b + w; k < e; k += S) {
-    const int m = A.src[k];
-    TMD_DCHECK(m >= 0 && m < A.n);
-    const T mult = (m == n && n == 0) ? mult0_of(A) : T(1);
-    const T Ck = A.C[k];
-    const T ux = -A.u[3 * k], uy = -A.u[3 * k + 1], uz = -A.u[3 * k + 2];
-    T sk[3], sy[5];
-    skew_c(sk, ux, uy, uz);
-    sym_c(sy, ux, uy, uz);
-    const auto wr = A.W + (size_t)k * A.ldw;
-    const auto gw = A.gW + (size_t)k * 3 * A.H;
-    T gc = T(0), gux = T(0), guy = T(0), guz = T(0);
+  // two edges per iteration (k, k + S): both edges' loads issued first, their eight wave sums interleaved
+  for (int k = b + w; k < e; k += 2 * S) {
+    const bool two = k + S < e;
+    const int kk[2] = {k, two ? k + S : k};
+    int m[2];
+    T Ck[2], ux[2], uy[2], uz[2], qv[2][NB], wv[2][NB][3];
 #pragma unroll
-    for (int c = 0; c < NB; ++c) {
-      const int h = c * TMD_WAVE + lane;
-      const bool on = h < A.H;
-      const int hc = on ? h : 0;
-      const T z = Pn[c] + A.Q[(size_t)m * A.H + hc];
-      const T w1 = wr[hc], w2 = wr[A.H + hc], w3 = wr[2 * A.H + hc];
-      const T g1 = g[c][0] * mult;
-      const T g2 = (g[c][1] * sk[0] + g[c][2] * sk[1] + g[c][3] * sk[2]) * mult;
-      const T g3 = (g[c][4] * sy[0] + g[c][5] * sy[1] + g[c][6] * sy[2] + g[c][7] * sy[3] +
-                    g[c][8] * sy[4]) * mult;
-      gPn[c] += (g1 * w1 + g2 * w2 + g3 * w3) * Ck;
-      if (on) {
-        gw[h] = g1 * z * Ck;
-        gw[A.H + h] = g2 * z * Ck;
-        gw[2 * A.H + h] = g3 * z * Ck;
-        gc += (g1 * w1 + g2 * w2 + g3 * w3) * z;
-        // gradient w.r.t. the row edge's u (= -u(n->m)): chain through the sign flip
-        T dax, day, daz, dsx, dsy, dsz;
-        dskew_c(&g[c][1], dax, day, daz);
-        dsym_c(&g[c][4], ux, uy, uz, dsx, dsy, dsz);
-        const T a2 = z * w2 * Ck * mult, a3 = z * w3 * Ck * mult;
-        gux -= a2 * dax + a3 * dsx;
-        guy -= a2 * day + a3 * dsy;
-        guz -= a2 * daz + a3 * dsz;
+    for (int j = 0; j < 2; ++j) {
+      m[j] = A.src[kk[j]];
+      TMD_DCHECK(m[j] >= 0 && m[j] < A.n);
+      Ck[j] = A.C[kk[j]];
+      ux[j] = -A.u[3 * kk[j]]; uy[j] = -A.u[3 * kk[j] + 1]; uz[j] = -A.u[3 * kk[j] + 2];
+      const auto wr = A.W + (size_t)kk[j] * A.ldw;
+#pragma unroll
+      for (int c = 0; c < NB; ++c) {
+        const int h = c * TMD_WAVE + lane;
+        const int hc = h < A.H ? h : 0;
+        qv[j][c] = A.Q[(size_t)m[j] * A.H + hc];
+        wv[j][c][0] = wr[hc]; wv[j][c][1] = wr[A.H + hc]; wv[j][c][2] = wr[2 * A.H + hc];
       }
     }
-    gc = wave_sum(gc);
-    gux = wave_sum(gux);
-    guy = wave_sum(guy);
-    guz = wave_sum(guz);
+    T red4[2][4];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const T mult = (m[j] == n && n == 0) ? mult0_of(A) : T(1);
+      const bool live = j == 0 || two;
+      T sk[3], sy[5];
+      skew_c(sk, ux[j], uy[j], uz[j]);
+      sym_c(sy, ux[j], uy[j], uz[j]);
+      const auto gw = A.gW + (size_t)kk[j] * 3 * A.H;
+      T gc = T(0), gux = T(0), guy = T(0), guz = T(0);
+#pragma unroll
+      for (int c = 0; c < NB; ++c) {
+        const int h = c * TMD_WAVE + lane;
+        const bool on = h < A.H;
+        const T z = Pn[c] + qv[j][c];
+        const T w1 = wv[j][c][0], w2 = wv[j][c][1], w3 = wv[j][c][2];
+        const T g1 = g[c][0] * mult;
+        const T g2 = (g[c][1] * sk[0] + g[c][2] * sk[1] + g[c][3] * sk[2]) * mult;
+        const T g3 = (g[c][4] * sy[0] + g[c][5] * sy[1] + g[c][6] * sy[2] + g[c][7] * sy[3] +
+                      g[c][8] * sy[4]) * mult;
+        if (live) gPn[c] += (g1 * w1 + g2 * w2 + g3 * w3) * Ck[j];
+        if (on && live) {
+          gw[h] = g1 * z * Ck[j];
+          gw[A.H + h] = g2 * z * Ck[j];
+          gw[2 * A.H + h] = g3 * z * Ck[j];
+        }
+        if (on) {
+          gc += (g1 * w1 + g2 * w2 + g3 * w3) * z;
+          // gradient w.r.t. the row edge's u (= -u(n->m)): chain through the sign flip
+          T dax, day, daz, dsx, dsy, dsz;
+          dskew_c(&g[c][1], dax, day, daz);
+          dsym_c(&g[c][4], ux[j], uy[j], uz[j], dsx, dsy, dsz);
+          const T a2 = z * w2 * Ck[j] * mult, a3 = z * w3 * Ck[j] * mult;
+          gux -= a2 * dax + a3 * dsx;
+          guy -= a2 * day + a3 * dsy;
+          guz -= a2 * daz + a3 * dsz;
+        }
+      }
+      red4[j][0] = gc; red4[j][1] = gux; red4[j][2] = guy; red4[j][3] = guz;
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) red4[j][i] = wave_sum(red4[j][i]);
     if (lane == 0) {
-      A.gC[k] = gc;
-      A.gu[3 * k] = gux;
-      A.gu[3 * k + 1] = guy;
-      A.gu[3 * k + 2] = guz;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        if (j == 1 && !two) break;
+        A.gC[kk[j]] = red4[j][0];
+        A.gu[3 * kk[j]] = red4[j][1];
+        A.gu[3 * kk[j] + 1] = red4[j][2];
+        A.gu[3 * kk[j] + 2] = red4[j][3];
+      }
     }
   }
   if (!fold_waves<T, NB, S>(gPn, red)) return;
@@ -281,22 +323,36 @@ __global__ __launch_bounds__(64 * S) void k_embed_bwd_src(AT A) {
   const int hc = on ? h : 0;
   T gQm[1] = {T(0)};
   const int b = min(A.row_ptr[m], A.cap), e = min(A.row_ptr[m + 1], A.cap);
-  for (int k = b + w; k < e; k += S) {
-    const int n = A.src[k];  // row edge n->m; its reverse m->n contributed Q[m] to E[n]
-    TMD_DCHECK(n >= 0 && n < A.n);
-    const T mult = (m == n && n == 0) ? mult0_of(A) : T(1);
-    T g[9];
-    ldc(g, A.gE + (size_t)n * A.H + hc, A.nh);
-    // u of the reversed edge's own row edge (m->n as seen from row n) is -u(k); the embedding
-    // used skew/sym of -(that) = u(k)
-    T sk[3], sy[5];
-    skew_c(sk, A.u[3 * k], A.u[3 * k + 1], A.u[3 * k + 2]);
-    sym_c(sy, A.u[3 * k], A.u[3 * k + 1], A.u[3 * k + 2]);
-    const auto wr = A.W + (size_t)k * A.ldw;
-    const T w1 = wr[hc], w2 = wr[A.H + hc], w3 = wr[2 * A.H + hc];
-    const T gg = g[0] * w1 + (g[1] * sk[0] + g[2] * sk[1] + g[3] * sk[2]) * w2 +
-                 (g[4] * sy[0] + g[5] * sy[1] + g[6] * sy[2] + g[7] * sy[3] + g[8] * sy[4]) * w3;
-    gQm[0] += gg * A.C[k] * mult;
+  // two edges per iteration (k, k + S), loads first
+  for (int k = b + w; k < e; k += 2 * S) {
+    const bool two = k + S < e;
+    const int kk[2] = {k, two ? k + S : k};
+    int nn[2];
+    T g[2][9], wv[2][3], cc[2], u0[2], u1[2], u2[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      nn[j] = A.src[kk[j]];  // row edge n->m; its reverse m->n contributed Q[m] to E[n]
+      TMD_DCHECK(nn[j] >= 0 && nn[j] < A.n);
+      ldc(g[j], A.gE + (size_t)nn[j] * A.H + hc, A.nh);
+      const auto wr = A.W + (size_t)kk[j] * A.ldw;
+      wv[j][0] = wr[hc]; wv[j][1] = wr[A.H + hc]; wv[j][2] = wr[2 * A.H + hc];
+      cc[j] = A.C[kk[j]];
+      u0[j] = A.u[3 * kk[j]]; u1[j] = A.u[3 * kk[j] + 1]; u2[j] = A.u[3 * kk[j] + 2];
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      if (j == 1 && !two) break;
+      const T mult = (m == nn[j] && nn[j] == 0) ? mult0_of(A) : T(1);
+      // u of the reversed edge's own row edge (m->n as seen from row n) is -u(k); the embedding
+      // used skew/sym of -(that) = u(k)
+      T sk[3], sy[5];
+      skew_c(sk, u0[j], u1[j], u2[j]);
+      sym_c(sy, u0[j], u1[j], u2[j]);
+      const T gg = g[j][0] * wv[j][0] + (g[j][1] * sk[0] + g[j][2] * sk[1] + g[j][3] * sk[2]) * wv[j][1] +
+                   (g[j][4] * sy[0] + g[j][5] * sy[1] + g[j][6] * sy[2] + g[j][7] * sy[3] + g[j][8] * sy[4]) *
+                       wv[j][2];
+      gQm[0] += gg * cc[j] * mult;
+    }
   }
   if (fold_waves<T, 1, S>(gQm, red) && on) A.gQ[(size_t)m * A.H + h] = gQm[0];
 }
