@@ -510,6 +510,80 @@ __global__ __launch_bounds__(64 * S) void k_msg_bwd_pair(Args<T> A) {
   }
 }
 
+// Pair rows, both backward roles in ONE pass over each row (the neighbours of n are the same set in both):
+// per edge (n <- m) the wave gathers gmsg[m] and the pair's factor row once for the source role (gT[n] +=
+// ea * gmsg[m]) and, when it is the pair's canonical edge (m >= n, a wave-uniform branch), T[m] for the pair's
+// factor gradient (as k_msg_bwd_pair).  Replaces k_msg_bwd_pair + k_msg_bwd_src (gmsg rows gathered once).
+template <typename T, int S>
+__global__ __launch_bounds__(64 * S) void k_msg_bwd_fused(Args<T> A) {
+  __shared__ T red[S > 1 ? (S - 1) * 9 * TMD_WAVE : 1];
+  {
+    const long long tid = (long long)blockIdx.x * blockDim.x + threadIdx.x, nth = (long long)gridDim.x * blockDim.x;
+    const int w3 = 3 * A.H;
+    for (long long i = tid; i < (long long)A.np * w3; i += nth) {
+      const int p = (int)(i / w3);
+      if (A.prow[A.pedge[p]] != p) A.gea[i] = T(0);
+    }
+  }
+  int n, ch0, w;
+  slot_node<S>(A.nblk, n, ch0, w);
+  const int lane = lane_id();
+  const int h = ch0 + lane;
+  const bool on = h < A.H;
+  const int hc = on ? h : 0;
+  T gn[9], tn_[9], acc[9];
+  ldc(gn, A.gmsg + (size_t)n * A.H + hc, A.nh);
+  ldc(tn_, A.Tc + (size_t)n * A.H + hc, A.nh);
+#pragma unroll
+  for (int k = 0; k < 9; ++k) acc[k] = T(0);
+  const int b = min(A.row_ptr[n], A.cap), e = min(A.row_ptr[n + 1], A.cap);
+  for (int base = b; base < e; base += TMD_WAVE) {
+    const int cnt = min(TMD_WAVE, e - base);
+    const int sv = lane < cnt ? A.src[base + lane] : 0;
+    const int rv = lane < cnt ? A.prow[base + lane] : 0;
+    for (int j = w; j < cnt; j += S) {
+      const int m = bcast(sv, j), r = bcast(rv, j);
+      TMD_DCHECK(m >= 0 && m < A.n);
+      const T mult = (m == n && n == 0) ? mult0_of(A) : T(1);
+      const T* er = A.ea + (size_t)r * A.ldea + 3 * hc;
+      const T f0 = er[0] * mult, f1 = er[1] * mult, f2 = er[2] * mult;
+      T g[9];
+      ldc(g, A.gmsg + (size_t)m * A.H + hc, A.nh);
+      if (m >= n) {  // the pair's canonical edge: its factor gradient from both directions
+        T g0, g1, g2;
+        if (m == n) {
+          g0 = gn[0] * tn_[0];
+          g1 = gn[1] * tn_[1] + gn[2] * tn_[2] + gn[3] * tn_[3];
+          g2 = gn[4] * tn_[4] + gn[5] * tn_[5] + gn[6] * tn_[6] + gn[7] * tn_[7] + gn[8] * tn_[8];
+        } else {
+          T t[9];
+          ldc(t, A.Tc + (size_t)m * A.H + hc, A.nh);
+          g0 = gn[0] * t[0] + g[0] * tn_[0];
+          g1 = gn[1] * t[1] + gn[2] * t[2] + gn[3] * t[3] + g[1] * tn_[1] + g[2] * tn_[2] + g[3] * tn_[3];
+          g2 = gn[4] * t[4] + gn[5] * t[5] + gn[6] * t[6] + gn[7] * t[7] + gn[8] * t[8] +
+               g[4] * tn_[4] + g[5] * tn_[5] + g[6] * tn_[6] + g[7] * tn_[7] + g[8] * tn_[8];
+        }
+        if (on) {
+          T* gr = A.gea + (size_t)r * 3 * A.H + 3 * h;
+          gr[0] = g0 * mult;
+          gr[1] = g1 * mult;
+          gr[2] = g2 * mult;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 9; ++i) acc[i] += node::ctype_scale(i, f0, f1, f2) * g[i];
+    }
+  }
+  if (!fold_waves<T, 9, S>(acc, red)) return;
+  if (A.gTadd && on) {
+    T ad[9];
+    ldc(ad, A.gTadd + (size_t)n * A.H + h, A.nh);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) acc[i] += ad[i];
+  }
+  if (on) stc(A.gT + (size_t)n * A.H + h, A.nh, acc);
+}
+
 // source pass: gT[m] = sum over reversed edges ea * gmsg[n]
 template <typename T>
 __device__ __forceinline__ void src_acc(T (&acc)[9], const Args<T>& A, int m, int n, int r, int hc) {
@@ -591,6 +665,7 @@ TMD_TN_KERNEL(k_msg_fwd)
 TMD_TN_KERNEL(k_msg_bwd_dst)
 TMD_TN_KERNEL(k_msg_bwd_src)
 TMD_TN_KERNEL(k_msg_bwd_pair)
+TMD_TN_KERNEL(k_msg_bwd_fused)
 #undef TMD_TN_KERNEL
 
 template <typename T> static int launch_embed_fwd(const Args<T>& A, hipStream_t st) {
@@ -607,6 +682,9 @@ template <typename T> static int launch_msg_bwd_dst(const Args<T>& A, hipStream_
 }
 template <typename T> static int launch_msg_bwd_src(const Args<T>& A, hipStream_t st) {
   return launch_s<T, k_msg_bwd_src_k>(A, st);
+}
+template <typename T> static int launch_msg_bwd_fused(const Args<T>& A, hipStream_t st) {
+  return launch_s<T, k_msg_bwd_fused_k>(A, st);
 }
 template <typename T> static int launch_msg_bwd_pair(const Args<T>& A, hipStream_t st) {
   return launch_s<T, k_msg_bwd_pair_k>(A, st);
@@ -779,6 +857,13 @@ extern "C" int tmdnet_tn_message_bwd_pairs(int dtype, int n_nodes, int hidden, c
     a.Tc = (const T*)comp;
     a.gmsg = (const T*)grad_msg; a.gea = (T*)g_edge_attr; a.gT = (T*)g_comp;
     a.gTadd = (const T*)g_comp_add;
+    // TMDNET_TN_BWD_FUSED=1: both roles in one pass (k_msg_bwd_fused; measured equal at C5: 32.5-33.0 vs
+    // 32.7-32.8 ms per evaluation, so the two-kernel form stays the default)
+    static const bool fused = [] {
+      const char* e = getenv("TMDNET_TN_BWD_FUSED");
+      return e && atoi(e) == 1;
+    }();
+    if (fused && g_edge_attr && g_comp) return tn::launch_msg_bwd_fused<T>(a, st);
     int rc = g_edge_attr ? tn::launch_msg_bwd_pair<T>(a, st) : kOk;
     if (rc) return rc;
     return g_comp ? tn::launch_msg_bwd_src<T>(a, st) : kOk;
