@@ -2581,7 +2581,18 @@ class _LinearBwd(Function):
         nf = ctx.next_functions
         want = [ctx.needs_input_grad[i] and _will_run(nf[i][0]) for i in range(3)]
         d_gy = d_x = d_w = None
-        if want[0]:
+        hand = gy.is_cuda and gy.dtype == torch.float32 and not torch.is_grad_enabled()
+        if want[0] and hand and (ggx is not None or ggw is not None):
+            # d gy = ggx W + x ggW^T + ggb on the hand GEMMs (the bias on the first, the second accumulating)
+            d_gy = torch.empty_like(gy)
+            probs = []
+            if ggx is not None:
+                probs.append((ggx.contiguous(), w, True, ggb, d_gy, False))
+            if ggw is not None:
+                probs.append((x.contiguous(), ggw.contiguous(), True, ggb if not probs else None, d_gy, bool(probs)))
+            for q in probs:
+                gemm_group([q])
+        elif want[0]:
             parts = []
             if ggx is not None:
                 parts.append(ggx @ w.t())
@@ -2594,7 +2605,11 @@ class _LinearBwd(Function):
                 for t in parts[1:]:
                     d_gy = d_gy + t
         if want[1] and ggw is not None:
-            d_x = gy @ ggw
+            if hand:
+                d_x = torch.empty((gy.shape[0], ggw.shape[1]), dtype=gy.dtype, device=gy.device)
+                gemm_group([(gy.contiguous(), ggw.contiguous(), False, None, d_x, False)])
+            else:
+                d_x = gy @ ggw
         if want[2] and ggx is not None:
             if torch.is_grad_enabled():
                 d_w = gy.t() @ ggx
