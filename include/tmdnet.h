@@ -689,6 +689,12 @@ int tmdnet_gemm_tn_f32(int n_problems, const int* dims, const void* const* ptrs,
 size_t tmdnet_gemm_tn_workspace_bytes(int n_problems, const int* dims);
 int tmdnet_gemm_tn_f32_ws(int n_problems, const int* dims, const void* const* ptrs, void* workspace,
                           size_t workspace_bytes, void* stream);
+/* The same with a device row count per problem: ptrs 7 per problem {A, B, A2, B2, C, Cb, rows}, rows an
+ * int32 device scalar (NULL: none): only rows < *rows of each segment are summed.  For the per-edge sums
+ * of a static-capacity (HIP-graph) neighbour list, whose padding slots follow the *rows found pairs and
+ * contribute zero anyway: the launch's workgroups over padding exit without reading it. */
+int tmdnet_gemm_tn_rows_f32_ws(int n_problems, const int* dims, const void* const* ptrs, void* workspace,
+                               size_t workspace_bytes, void* stream);
 /* Embedding lookups (the forward of nn.Embedding(num_types, H) at z, TorchMD_ET.embedding and
  * NeighborEmbedding.embedding, reference torchmd_et.py:170, utils.py:92; replaces the two index_select
  * gathers): for each of n_tables (<= 4) tables sharing z[n] (int64), outs_t[k][:] = tables_t[z[k]][:]

@@ -174,7 +174,7 @@ _TN_NARROW = [(5210, 4096, 32, True, 10420), (5000, 70, 20, True, 900), (678, 12
               (37, 100, 31, False, 5), (12548, 96, 32, False, 0), (3, 4, 8, True, 0)]
 
 
-@pytest.mark.parametrize("form", ["1", "2", "4"])  # TMDNET_TN_V: 64-tile, pipelined, bf16x3-split kernels
+@pytest.mark.parametrize("form", ["1", "2", "4", "5"])  # TMDNET_TN_V: 64-tile, pipelined, bf16x3 LDS / register
 @pytest.mark.parametrize("shapes", ["wide", "narrow"])
 @pytest.mark.parametrize("use_cb", [False, True])
 def test_weight_gradient_tn_gemm_16byte_kernel(monkeypatch, use_cb, shapes, form):
@@ -215,6 +215,26 @@ def test_weight_gradient_tn_gemm_16byte_kernel(monkeypatch, use_cb, shapes, form
     for p, ref in zip(probs, refs):
         got = torch.cat((p["C"], p["Cb"][:, None]), 1) if p.get("Cb") is not None else p["C"]
         assert _rel(got, ref) < 2e-5, (tuple(p["A"].shape), _rel(got, ref))
+
+
+@pytest.mark.parametrize("form", ["1", "2", "5"])
+def test_weight_gradient_tn_gemm_device_row_count(monkeypatch, form):
+    """tmdnet_gemm_tn_rows_f32_ws: only rows < *rows of each segment are summed (the found pairs of a
+    static-capacity edge list), incl. a count of 0, a count inside a split chunk, and one above K."""
+    from torchmdnet import kernels
+    monkeypatch.setenv("TMDNET_TN_V", form)
+    torch.manual_seed(7)
+    K, M, Nb = 15872, 4096 if form != "2" else 512, 64 if form != "2" else 32
+    A, B = torch.randn(K, M, device=DEV), torch.randn(K, Nb, device=DEV)
+    A2, B2 = torch.randn(K, M, device=DEV), torch.randn(K, Nb, device=DEV)
+    for count in (12548, 0, 777, K + 100):
+        rows = torch.tensor([count], dtype=torch.int32, device=DEV)
+        C, Cb = torch.empty(M, Nb, device=DEV), torch.empty(M, device=DEV)
+        kernels.wgrad_tn([{"A": A, "B": B, "A2": A2, "B2": B2, "C": C, "Cb": Cb, "ones": True, "rows": rows}])
+        c = min(count, K)
+        ref = A[:c].double().t() @ B[:c].double() + A2[:c].double().t() @ B2[:c].double()
+        refb = A[:c].double().sum(0)
+        assert _rel(C, ref) < 2e-5 and _rel(Cb, refb) < 2e-5, (count, _rel(C, ref), _rel(Cb, refb))
 
 
 def test_weight_gradient_tn_gemm_matches_library():

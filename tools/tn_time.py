@@ -70,11 +70,11 @@ def timed(probs, reps=50):
 
 cases = [("dkv K2=Ep", dkv_probs(Ep)), ("dkv K2=2Ep", dkv_probs(2 * Ep)), ("node x8 layers", node_probs())]
 for name, probs in cases:
-    for target in ("1024",):
+    for target in ("1024", "2048"):
         os.environ["TMDNET_TN_TARGET"] = target
         row = []
-        for form in ("1", "2", "4"):
+        for form in ("1", "2", "3", "4", "5"):
             os.environ["TMDNET_TN_V"] = form
             row.append(timed(probs))
-        print(f"{name:16s} target {target:5s} form1 {row[0]:7.1f} us  form2 (pipelined) {row[1]:7.1f} us  "
-              f"form4 (bf16x3) {row[2]:7.1f} us", flush=True)
+        print(f"{name:16s} target {target:5s} form1 {row[0]:7.1f} us  form2 (pipelined) {row[1]:7.1f} us  form3 {row[2]:7.1f} us  "
+              f"form4 (bf16x3) {row[3]:7.1f} us  form5 (bf16x3 regs) {row[4]:7.1f} us", flush=True)

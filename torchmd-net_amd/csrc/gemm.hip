@@ -182,12 +182,16 @@ constexpr int TN_UB = 4;
 struct ProbTN {
   int M, N, K, K2, lda, ldb, lda2, ldb2, ldc, beta, ones1, ones2, tiles_n, tile0;
   int onehot;  // A is an int64 index vector: A[k][m] = (A[k] == m) (embedding-table gradients)
+  // 64-tile kernels: this problem's split-K factor, first workgroup, tile count, first partial tile
+  int S, wg0, ntiles;
+  long long part0;
   const float* A;
   const float* B;
   const float* A2;
   const float* B2;
   float* C;
   float* Cb;  // non-NULL: column N-1 (the ones / bias column) goes to Cb[m] instead of C[m][N-1]
+  const int* rows;  // non-NULL (64-tile kernels): only rows < *rows of each segment are summed (device count)
 };
 
 struct GroupTN {
@@ -209,7 +213,9 @@ __global__ __launch_bounds__(NW * 64) void k_gemm_tn(GroupTN G) {
   const int w = threadIdx.x / TMD_WAVE, lane = lane_id();
   const int lr = lane & 15, lk = lane >> 4;
   const int r0 = (t / P.tiles_n) * 32, c0 = (t % P.tiles_n) * 32;
-  const int KT = P.K + P.K2;
+  // (a device row count shortens both segments: the chunks split the rows actually summed)
+  const int cnt = P.rows ? max(0, *P.rows) : P.K + P.K2;
+  const int K1 = min(P.K, cnt), KT = K1 + min(P.K2, cnt);
   // this workgroup's rows (16-row blocks split evenly over the S chunks), then this wave's share
   const int nkt = (KT + 15) / 16, cper = (nkt + G.S - 1) / G.S;
   const int c_lo = min(KT, sk * cper * 16), c_hi = min(KT, (sk + 1) * cper * 16);
@@ -224,7 +230,7 @@ __global__ __launch_bounds__(NW * 64) void k_gemm_tn(GroupTN G) {
   const bool va = ma < P.M, vb = mb < P.M;
   const bool anyones = P.ones1 || P.ones2;
   for (int seg = 0; seg < 2; ++seg) {  // the two row segments (wave-uniform)
-    const int s0 = seg ? P.K : 0, s1 = seg ? KT : P.K;
+    const int s0 = seg ? K1 : 0, s1 = seg ? KT : K1;
     const int lo = max(k_lo, s0), hi = min(k_hi, s1);
     if (lo >= hi) continue;
     const float* A = seg ? P.A2 : P.A;
@@ -326,24 +332,44 @@ __global__ __launch_bounds__(256) void k_tn_reduce(GroupTN G, int tiles) {
 constexpr int TV = 64;
 constexpr int TV_PART = TV * TV + TV;  // partial tile + bias partials (split-K)
 
+// Workgroup -> (problem, tile, row chunk) of the 64-tile kernels.  Each problem has its own split-K factor
+// (every workgroup gets about the same number of rows: a 3N-row vec_proj problem is not split like an
+// N-row one), and within a problem the chunk is the slow index, so the workgroups resident together read
+// whole rows of A (every tile's column strip of the same row chunk) instead of long columns.
+struct TNLoc {
+  int pi, t, sk;
+};
+__device__ __forceinline__ TNLoc tn_locate(const GroupTN& G) {
+  const int b = blockIdx.x;
+  int pi = 0;
+  for (int i = 1; i < G.n; ++i)
+    if (b >= G.p[i].wg0) pi = i;
+  const ProbTN& P = G.p[pi];
+  const int l = b - P.wg0;
+  return TNLoc{pi, l % P.ntiles, l / P.ntiles};
+}
+// this chunk's partial tile (S > 1), summed in chunk order by k_tn_reduce_v
+__device__ __forceinline__ float* tn_part(const GroupTN& G, const ProbTN& P, int t, int sk) {
+  return P.S > 1 ? G.part + ((size_t)P.part0 + (size_t)t * P.S + sk) * TV_PART : nullptr;
+}
+
 template <int NW>
 __global__ __launch_bounds__(NW * 64) void k_gemm_tn_v(GroupTN G) {
   __shared__ float red[NW][TV][TV + 1];
   __shared__ float redb[NW][TV];
-  const int tg = blockIdx.x / G.S, sk = blockIdx.x % G.S;
-  int pi = 0;
-  for (int i = 1; i < G.n; ++i)
-    if (tg >= G.p[i].tile0) pi = i;
-  const ProbTN& P = G.p[pi];
-  const int t = tg - P.tile0;
+  const TNLoc L = tn_locate(G);
+  const ProbTN& P = G.p[L.pi];
+  const int t = L.t, sk = L.sk;
   const int w = threadIdx.x / TMD_WAVE, lane = lane_id();
   const int c = lane & 15, kq = lane >> 4;
   const int m0 = (t / P.tiles_n) * TV, n0 = (t % P.tiles_n) * TV;
   const bool anyones = P.ones1 || P.ones2;
   const int Nr = anyones ? P.N - 1 : P.N;  // columns of B that are read (the ones column is the row sum)
   const bool do_bias = anyones && (t % P.tiles_n) == 0;
-  const int KT = P.K + P.K2;
-  const int nkt = (KT + 15) / 16, cper = (nkt + G.S - 1) / G.S;
+  // (a device row count shortens both segments: the chunks split the rows actually summed)
+  const int cnt = P.rows ? max(0, *P.rows) : P.K + P.K2;
+  const int K1 = min(P.K, cnt), KT = K1 + min(P.K2, cnt);
+  const int nkt = (KT + 15) / 16, cper = (nkt + P.S - 1) / P.S;
   const int c_lo = min(KT, sk * cper * 16), c_hi = min(KT, (sk + 1) * cper * 16);
   const int nkb = (c_hi - c_lo + 15) / 16, per = (nkb + NW - 1) / NW;
   const int k_lo = min(c_hi, c_lo + w * per * 16), k_hi = min(c_hi, c_lo + (w + 1) * per * 16);
@@ -357,7 +383,7 @@ __global__ __launch_bounds__(NW * 64) void k_gemm_tn_v(GroupTN G) {
   const bool mfull = ma + 3 < P.M, nfull = na + 3 < Nr;
   const bool gemm = n0 < Nr;  // a bias-only tile (B = ones only) skips the MFMAs
   for (int seg = 0; seg < 2; ++seg) {
-    const int s0 = seg ? P.K : 0, s1 = seg ? KT : P.K;
+    const int s0 = seg ? K1 : 0, s1 = seg ? KT : K1;
     const int lo = max(k_lo, s0), hi = min(k_hi, s1);
     if (lo >= hi) continue;
     const float* A = seg ? P.A2 : P.A;
@@ -427,7 +453,7 @@ __global__ __launch_bounds__(NW * 64) void k_gemm_tn_v(GroupTN G) {
     }
   }
   __syncthreads();
-  float* part = G.S > 1 ? G.part + ((size_t)tg * G.S + sk) * TV_PART : nullptr;
+  float* part = tn_part(G, P, t, sk);
   for (int e = threadIdx.x; e < TV * TV; e += blockDim.x) {
     const int r = e >> 6, cc = e & 63;
     float v = 0.f;
@@ -469,6 +495,7 @@ __global__ __launch_bounds__(256) void k_tn_reduce_v(GroupTN G, int tiles) {
   for (int j = 1; j < G.n; ++j)
     if (tg >= G.p[j].tile0) pi = j;
   const ProbTN& P = G.p[pi];
+  if (P.S <= 1) return;  // written by the GEMM kernel itself
   const int t = tg - P.tile0;
   const int m0 = (t / P.tiles_n) * TV, n0 = (t % P.tiles_n) * TV;
   const bool anyones = P.ones1 || P.ones2;
@@ -483,10 +510,10 @@ __global__ __launch_bounds__(256) void k_tn_reduce_v(GroupTN G, int tiles) {
     if (!anyones || (t % P.tiles_n) != 0 || m >= P.M) return;
     out = P.Cb ? P.Cb + m : P.C + (size_t)m * P.ldc + (P.N - 1);
   }
-  const float* src = G.part + (size_t)tg * G.S * TV_PART + e;
+  const float* src = G.part + ((size_t)P.part0 + (size_t)t * P.S) * TV_PART + e;
   float v = 0.f;
 #pragma unroll 8
-  for (int s = 0; s < G.S; ++s) v += src[(size_t)s * TV_PART];
+  for (int s = 0; s < P.S; ++s) v += src[(size_t)s * TV_PART];
   if (P.beta) v += *out;
   *out = v;
 }
@@ -506,20 +533,19 @@ __global__ __launch_bounds__(NW * 64) void k_gemm_tn_v2(GroupTN G) {
   constexpr int TN = 16 * NB;
   __shared__ float red[TV][TN + 1];
   __shared__ float redb[TV];
-  const int tg = blockIdx.x / G.S, sk = blockIdx.x % G.S;
-  int pi = 0;
-  for (int i = 1; i < G.n; ++i)
-    if (tg >= G.p[i].tile0) pi = i;
-  const ProbTN& P = G.p[pi];
-  const int t = tg - P.tile0;
+  const TNLoc L = tn_locate(G);
+  const ProbTN& P = G.p[L.pi];
+  const int t = L.t, sk = L.sk;
   const int w = threadIdx.x / TMD_WAVE, lane = lane_id();
   const int c = lane & 15, kq = lane >> 4;
   const int m0 = (t / P.tiles_n) * TV, n0 = (t % P.tiles_n) * TV;
   const bool anyones = P.ones1 || P.ones2;
   const int Nr = anyones ? P.N - 1 : P.N;
   const bool do_bias = anyones && (t % P.tiles_n) == 0;
-  const int KT = P.K + P.K2;
-  const int nkt = (KT + 15) / 16, cper = (nkt + G.S - 1) / G.S;
+  // (a device row count shortens both segments: the chunks split the rows actually summed)
+  const int cnt = P.rows ? max(0, *P.rows) : P.K + P.K2;
+  const int K1 = min(P.K, cnt), KT = K1 + min(P.K2, cnt);
+  const int nkt = (KT + 15) / 16, cper = (nkt + P.S - 1) / P.S;
   const int c_lo = min(KT, sk * cper * 16), c_hi = min(KT, (sk + 1) * cper * 16);
   const int nkb = (c_hi - c_lo + 15) / 16, per = (nkb + NW - 1) / NW;
   const int k_lo = min(c_hi, c_lo + w * per * 16), k_hi = min(c_hi, c_lo + (w + 1) * per * 16);
@@ -534,7 +560,7 @@ __global__ __launch_bounds__(NW * 64) void k_gemm_tn_v2(GroupTN G) {
   const bool mfull = ma + 3 < P.M, nfull = na + NB - 1 < Nr;
   const bool gemm = n0 < Nr;
   for (int seg = 0; seg < 2; ++seg) {
-    const int s0 = seg ? P.K : 0, s1 = seg ? KT : P.K;
+    const int s0 = seg ? K1 : 0, s1 = seg ? KT : K1;
     const int lo = max(k_lo, s0), hi = min(k_hi, s1);
     if (lo >= hi) continue;
     const float* A = seg ? P.A2 : P.A;
@@ -636,7 +662,7 @@ __global__ __launch_bounds__(NW * 64) void k_gemm_tn_v2(GroupTN G) {
     }
     __syncthreads();
   }
-  float* part = G.S > 1 ? G.part + ((size_t)tg * G.S + sk) * TV_PART : nullptr;
+  float* part = tn_part(G, P, t, sk);
   for (int e = threadIdx.x; e < TV * TN; e += blockDim.x) {
     const int r = e / TN, cc = e - r * TN;
     const float v = red[r][cc];
@@ -1078,6 +1104,9 @@ using gemm::GroupTN;
 using gemm::ProbTN;
 using gemm::TV;
 using gemm::TV_PART;
+using gemm::TNLoc;
+using gemm::tn_locate;
+using gemm::tn_part;
 using bf8 = __bf16 __attribute__((ext_vector_type(8)));
 using f4 = float __attribute__((ext_vector_type(4)));
 constexpr int KB = 32, LDK = KB + 8;  // rows per step; LDS pitch (bf16) of a transposed row
@@ -1086,12 +1115,9 @@ __global__ __launch_bounds__(256) void k_gemm_tn_x3(GroupTN G) {
   __shared__ __attribute__((aligned(16))) unsigned short la[3][TV][LDK];
   __shared__ __attribute__((aligned(16))) unsigned short lb[3][TV][LDK];
   __shared__ float rsum[16][TV];
-  const int tg = blockIdx.x / G.S, sk = blockIdx.x % G.S;
-  int pi = 0;
-  for (int i = 1; i < G.n; ++i)
-    if (tg >= G.p[i].tile0) pi = i;
-  const ProbTN& P = G.p[pi];
-  const int t = tg - P.tile0;
+  const TNLoc L = tn_locate(G);
+  const ProbTN& P = G.p[L.pi];
+  const int t = L.t, sk = L.sk;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const int m0 = (t / P.tiles_n) * TV, n0 = (t % P.tiles_n) * TV;
@@ -1099,8 +1125,10 @@ __global__ __launch_bounds__(256) void k_gemm_tn_x3(GroupTN G) {
   const int Nr = anyones ? P.N - 1 : P.N;
   const bool do_bias = anyones && (t % P.tiles_n) == 0;
   const bool gemm = n0 < Nr;
-  const int KT = P.K + P.K2;
-  const int nks = (KT + KB - 1) / KB, cper = (nks + G.S - 1) / G.S;
+  // (a device row count shortens both segments: the chunks split the rows actually summed)
+  const int cnt = P.rows ? max(0, *P.rows) : P.K + P.K2;
+  const int K1 = min(P.K, cnt), KT = K1 + min(P.K2, cnt);
+  const int nks = (KT + KB - 1) / KB, cper = (nks + P.S - 1) / P.S;
   const int c_lo = min(KT, sk * cper * KB), c_hi = min(KT, (sk + 1) * cper * KB);
   // this thread's two float4 of each 32 x 64 operand tile: row kr[j], columns q4 .. q4 + 3
   const int q4 = (tid & 15) * 4, kr0 = tid >> 4;  // rows kr0 and kr0 + 16
@@ -1113,7 +1141,7 @@ __global__ __launch_bounds__(256) void k_gemm_tn_x3(GroupTN G) {
     for (int j = 0; j < 2; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
   f4 rs = f4{0.f, 0.f, 0.f, 0.f};
   for (int seg = 0; seg < 2; ++seg) {
-    const int s0 = seg ? P.K : 0, s1 = seg ? KT : P.K;
+    const int s0 = seg ? K1 : 0, s1 = seg ? KT : K1;
     const int lo = max(c_lo, s0), hi = min(c_hi, s1);
     if (lo >= hi) continue;
     const float* A = seg ? P.A2 : P.A;
@@ -1190,7 +1218,7 @@ __global__ __launch_bounds__(256) void k_gemm_tn_x3(GroupTN G) {
       }
     }
   }
-  float* part = G.S > 1 ? G.part + ((size_t)tg * G.S + sk) * TV_PART : nullptr;
+  float* part = tn_part(G, P, t, sk);
   if (gemm) {  // lane holds C[m = 4 (lane >> 4) + i][n = lane & 15] of each 16 x 16 block
 #pragma unroll
     for (int x = 0; x < 2; ++x)
@@ -1233,6 +1261,195 @@ __global__ __launch_bounds__(256) void k_gemm_tn_x3(GroupTN G) {
 }
 
 }  // namespace tnx3
+
+// ---------------------------------------------------------------------------------------------------
+// The grouped TN GEMM on the bf16 MFMA at fp32 accuracy with NO LDS staging (TMDNET_TN_V=5).  The k index
+// of an MFMA is a summation label, so a lane may feed ANY 8 rows as its k group as long as its A and B
+// fragments use the same rows: lane (c, g) loads rows kb + 8g + j (j < 8), A columns m0 + 4c .. + 3 and B
+// columns n0 + 4c .. + 3 as float4 (coalesced 256-byte row segments per 16 lanes), and the 8 values of
+// A column m0 + 4c + mb ARE the lane's fragment of 16 x 16 block mb (MFMA row label c) -- k_gemm_tn_v's
+// label permutation with 8 k per lane instead of one.  Each value is split in registers into its three
+// exact bf16 pieces (proj::split3) and the six piece products with i + j <= 2 run as 16x16x32 bf16 MFMAs:
+// 96 MFMAs of 16 cycles per 32-row step of a 64 x 64 tile against the f32 kernel's 128 of 32.  The split
+// of a step happens before the next step's loads are issued (the raw registers are then free), so the
+// loads fly during the MFMAs.  Tile numbering, split-K partial layout, bias (A's column sums from the raw
+// values) and the cross-wave reduction are k_gemm_tn_v's.  Not for one-hot A.
+namespace tnx3r {
+
+using gemm::GroupTN;
+using gemm::ProbTN;
+using gemm::TV;
+using gemm::TV_PART;
+using gemm::TNLoc;
+using gemm::tn_locate;
+using gemm::tn_part;
+using bf8 = __bf16 __attribute__((ext_vector_type(8)));
+using f4 = float __attribute__((ext_vector_type(4)));
+using u4 = unsigned __attribute__((ext_vector_type(4)));
+constexpr int KS = 32;  // rows per step (4 k groups x 8)
+
+// element i of 8 float4 (rows k .. k + 7 of the lane's group) -> the three bf16 fragments
+__device__ __forceinline__ void split_col(const f4 (&x)[8], int i, bf8 (&f)[3]) {
+  unsigned h[8], m[8], l[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) proj::split3(x[j][i], h[j], m[j], l[j]);
+  u4 H, M, L;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {  // element 2p in the low half of register p
+    H[p] = (h[2 * p] >> 16) | h[2 * p + 1];
+    M[p] = (m[2 * p] >> 16) | m[2 * p + 1];
+    L[p] = (l[2 * p] >> 16) | l[2 * p + 1];
+  }
+  f[0] = __builtin_bit_cast(bf8, H);
+  f[1] = __builtin_bit_cast(bf8, M);
+  f[2] = __builtin_bit_cast(bf8, L);
+}
+
+template <int NW>
+__global__ __launch_bounds__(NW * 64, 2) void k_gemm_tn_x3r(GroupTN G) {
+  __shared__ float red[NW][TV][TV + 1];
+  __shared__ float redb[NW][TV];
+  const TNLoc L = tn_locate(G);
+  const ProbTN& P = G.p[L.pi];
+  const int t = L.t, sk = L.sk;
+  const int w = threadIdx.x / TMD_WAVE, lane = lane_id();
+  const int c = lane & 15, kg = lane >> 4;
+  const int m0 = (t / P.tiles_n) * TV, n0 = (t % P.tiles_n) * TV;
+  const bool anyones = P.ones1 || P.ones2;
+  const int Nr = anyones ? P.N - 1 : P.N;
+  const bool do_bias = anyones && (t % P.tiles_n) == 0;
+  // (a device row count shortens both segments: the chunks split the rows actually summed)
+  const int cnt = P.rows ? max(0, *P.rows) : P.K + P.K2;
+  const int K1 = min(P.K, cnt), KT = K1 + min(P.K2, cnt);
+  const int nkt = (KT + KS - 1) / KS, cper = (nkt + P.S - 1) / P.S;
+  const int c_lo = min(KT, sk * cper * KS), c_hi = min(KT, (sk + 1) * cper * KS);
+  const int nkb = (c_hi - c_lo + KS - 1) / KS, per = (nkb + NW - 1) / NW;
+  const int k_lo = min(c_hi, c_lo + w * per * KS), k_hi = min(c_hi, c_lo + (w + 1) * per * KS);
+  f4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  f4 rs = f4{0.f, 0.f, 0.f, 0.f};
+  const int ma = m0 + 4 * c, na = n0 + 4 * c;
+  const bool mfull = ma + 3 < P.M, nfull = na + 3 < Nr;
+  const bool gemm = n0 < Nr;
+  for (int seg = 0; seg < 2; ++seg) {
+    const int s0 = seg ? K1 : 0, s1 = seg ? KT : K1;
+    const int lo = max(k_lo, s0), hi = min(k_hi, s1);
+    if (lo >= hi) continue;
+    const float* A = seg ? P.A2 : P.A;
+    const float* B = seg ? P.B2 : P.B;
+    const int lda = seg ? P.lda2 : P.lda, ldb = seg ? P.ldb2 : P.ldb;
+    const bool bias_seg = do_bias && (seg ? P.ones2 : P.ones1);
+    const bool rb = gemm && B;
+    auto load = [&](int kb, f4 (&a)[8], f4 (&b)[8]) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = kb + 8 * kg + j;
+        const bool kv = k < hi;
+        const size_t ro = (size_t)(kv ? k - s0 : 0);
+        if (kv && mfull) {
+          a[j] = *reinterpret_cast<const f4*>(A + ro * lda + ma);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) a[j][i] = (kv && ma + i < P.M) ? A[ro * lda + ma + i] : 0.f;
+        }
+        if (!rb) {
+          b[j] = f4{0.f, 0.f, 0.f, 0.f};
+        } else if (kv && nfull) {
+          b[j] = *reinterpret_cast<const f4*>(B + ro * ldb + na);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) b[j][i] = (kv && na + i < Nr) ? B[ro * ldb + na + i] : 0.f;
+        }
+      }
+    };
+    f4 a[8], b[8];
+    load(lo, a, b);
+    for (int kb = lo; kb < hi; kb += KS) {
+      if (bias_seg) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) rs += a[j];
+      }
+      bf8 fa[4][3], fb[4][3];
+      if (gemm) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          split_col(a, i, fa[i]);
+          split_col(b, i, fb[i]);
+        }
+      }
+      if (kb + KS < hi) load(kb + KS, a, b);  // in flight during this step's MFMAs
+      if (gemm) {
+        constexpr int TA[6] = {2, 1, 0, 1, 0, 0}, TB[6] = {0, 1, 2, 0, 1, 0};  // small terms first
+#pragma unroll
+        for (int q = 0; q < 6; ++q)
+#pragma unroll
+          for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+            for (int nb = 0; nb < 4; ++nb)
+              acc[mb][nb] =
+                  __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[mb][TA[q]], fb[nb][TB[q]], acc[mb][nb], 0, 0, 0);
+      }
+    }
+  }
+  // C layout of a 16x16 block: lane holds MFMA rows 4 (lane >> 4) + i, column lane & 15 (labels as above)
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) red[w][4 * (4 * kg + i) + mb][4 * c + nb] = acc[mb][nb][i];
+  if (do_bias) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float v = rs[i];
+      v += __shfl_xor(v, 16);
+      v += __shfl_xor(v, 32);
+      rs[i] = v;
+    }
+    if (kg == 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) redb[w][4 * c + i] = rs[i];
+    }
+  }
+  __syncthreads();
+  float* part = tn_part(G, P, t, sk);
+  for (int e = threadIdx.x; e < TV * TV; e += blockDim.x) {
+    const int r = e >> 6, cc = e & 63;
+    float v = 0.f;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) v += red[i][r][cc];
+    if (part) {
+      part[e] = v;
+      continue;
+    }
+    const int m = m0 + r, n = n0 + cc;
+    if (m >= P.M || n >= Nr) continue;
+    float* out = P.C + (size_t)m * P.ldc + n;
+    if (P.beta) v += *out;
+    *out = v;
+  }
+  if (do_bias) {
+    for (int r = threadIdx.x; r < TV; r += blockDim.x) {
+      float v = 0.f;
+#pragma unroll
+      for (int i = 0; i < NW; ++i) v += redb[i][r];
+      if (part) {
+        part[TV * TV + r] = v;
+        continue;
+      }
+      const int m = m0 + r;
+      if (m >= P.M) continue;
+      float* out = P.Cb ? P.Cb + m : P.C + (size_t)m * P.ldc + (P.N - 1);
+      if (P.beta) v += *out;
+      *out = v;
+    }
+  }
+}
+
+}  // namespace tnx3r
 
 namespace emb {
 constexpr int MAX_TABLES = 4;
@@ -1410,10 +1627,53 @@ static int tn_tiles(gemm::GroupTN& G, int T) {
   return tiles;
 }
 
+// The 64-tile kernels' split: rows per workgroup = the group's (tile x row) work over ~target workgroups, at
+// least 4 waves x 64 rows, and S = ceil(rows of the problem / that) per problem (<= 64), so the workgroups of
+// a 3N-row problem and of an N-row one take about equally long (one S for the group left the vec_proj
+// tiles of the node weight gradients three times longer than the others).  Shapes only (the workspace
+// query uses it too).  Returns the workgroup count; parts = partial tiles of the S > 1 problems.
+struct TNShape {
+  int M, Nr, KT;
+};
+static int tn_plan_v(int n, const TNShape* sh, bool split, int* S, int* ntiles, long long* part0, long long& parts) {
+  long long work = 0;
+  for (int i = 0; i < n; ++i) {
+    ntiles[i] = ((sh[i].M + gemm::TV - 1) / gemm::TV) * max(1, (sh[i].Nr + gemm::TV - 1) / gemm::TV);
+    work += (long long)ntiles[i] * sh[i].KT;
+  }
+  const long long target = tn_target(), rows = max(256LL, (work + target - 1) / target);
+  int wgs = 0;
+  parts = 0;
+  for (int i = 0; i < n; ++i) {
+    S[i] = split ? (int)max(1LL, min(64LL, (sh[i].KT + rows - 1) / rows)) : 1;
+    part0[i] = parts;
+    if (S[i] > 1) parts += (long long)ntiles[i] * S[i];
+    wgs += ntiles[i] * S[i];
+  }
+  return wgs;
+}
+
 static void launch_tn(gemm::GroupTN& G, int tiles, int kmax, float* ws, hipStream_t st) {
   if (tn_vec_ok(G)) {
     const int tv = tn_tiles(G, gemm::TV);
-    G.S = ws ? tn_split(tv, kmax) : 1;  // (512 workgroups measured slower than 1024: 259 vs 227 us per step)
+    TNShape sh[gemm::TN_MAX];
+    int S[gemm::TN_MAX], nt[gemm::TN_MAX];
+    long long p0[gemm::TN_MAX], parts = 0;
+    for (int i = 0; i < G.n; ++i) {
+      const gemm::ProbTN& P = G.p[i];
+      sh[i] = TNShape{P.M, (P.ones1 || P.ones2) ? P.N - 1 : P.N, P.K + P.K2};
+    }
+    const int wgs = tn_plan_v(G.n, sh, ws != nullptr, S, nt, p0, parts);
+    G.S = 1;
+    for (int i = 0, w0 = 0; i < G.n; ++i) {
+      gemm::ProbTN& P = G.p[i];
+      P.S = S[i];
+      P.ntiles = nt[i];
+      P.part0 = p0[i];
+      P.wg0 = w0;
+      w0 += nt[i] * S[i];
+      G.S = max(G.S, S[i]);  // (> 1: some problem writes partial tiles)
+    }
     G.part = ws;
     bool narrow = true;  // every problem reads <= 32 columns of B
     for (int i = 0; i < G.n; ++i) {
@@ -1428,23 +1688,25 @@ static void launch_tn(gemm::GroupTN& G, int tiles, int kmax, float* ws, hipStrea
     bool onehot = false;
     for (int i = 0; i < G.n; ++i) onehot = onehot || G.p[i].onehot;
     if (form == 4 && !onehot) {
-      hipLaunchKernelGGL(tnx3::k_gemm_tn_x3, dim3(tv * G.S), dim3(256), 0, st, G);
+      hipLaunchKernelGGL(tnx3::k_gemm_tn_x3, dim3(wgs), dim3(256), 0, st, G);
+    } else if (form == 5 && !onehot) {
+      hipLaunchKernelGGL(tnx3r::k_gemm_tn_x3r<4>, dim3(wgs), dim3(256), 0, st, G);
     } else if (form == 2 || form == 3) {
       const bool pipe = form == 2;
       if (kmax >= 8192 && G.S == 1) {
         if (narrow) hipLaunchKernelGGL((gemm::k_gemm_tn_v2<8, 2, true>), dim3(tv), dim3(512), 0, st, G);
         else hipLaunchKernelGGL((gemm::k_gemm_tn_v2<8, 4, true>), dim3(tv), dim3(512), 0, st, G);
       } else if (narrow) {
-        if (pipe) hipLaunchKernelGGL((gemm::k_gemm_tn_v2<4, 2, true>), dim3(tv * G.S), dim3(256), 0, st, G);
-        else hipLaunchKernelGGL((gemm::k_gemm_tn_v2<4, 2, false>), dim3(tv * G.S), dim3(256), 0, st, G);
+        if (pipe) hipLaunchKernelGGL((gemm::k_gemm_tn_v2<4, 2, true>), dim3(wgs), dim3(256), 0, st, G);
+        else hipLaunchKernelGGL((gemm::k_gemm_tn_v2<4, 2, false>), dim3(wgs), dim3(256), 0, st, G);
       } else {
-        if (pipe) hipLaunchKernelGGL((gemm::k_gemm_tn_v2<4, 4, true>), dim3(tv * G.S), dim3(256), 0, st, G);
-        else hipLaunchKernelGGL((gemm::k_gemm_tn_v2<4, 4, false>), dim3(tv * G.S), dim3(256), 0, st, G);
+        if (pipe) hipLaunchKernelGGL((gemm::k_gemm_tn_v2<4, 4, true>), dim3(wgs), dim3(256), 0, st, G);
+        else hipLaunchKernelGGL((gemm::k_gemm_tn_v2<4, 4, false>), dim3(wgs), dim3(256), 0, st, G);
       }
     } else if (kmax >= 8192 && G.S == 1) {
       hipLaunchKernelGGL(gemm::k_gemm_tn_v<8>, dim3(tv), dim3(512), 0, st, G);
     } else {
-      hipLaunchKernelGGL(gemm::k_gemm_tn_v<4>, dim3(tv * G.S), dim3(256), 0, st, G);
+      hipLaunchKernelGGL(gemm::k_gemm_tn_v<4>, dim3(wgs), dim3(256), 0, st, G);
     }
     if (G.S > 1)
       hipLaunchKernelGGL(gemm::k_tn_reduce_v, dim3((tv * gemm::TV_PART + 255) / 256), dim3(256), 0, st, G, tv);
@@ -1533,6 +1795,7 @@ static int tn_group(int n_problems, const int* dims, const void* const* ptrs, in
     P.A = (const float*)q[0]; P.B = (const float*)q[1];
     P.A2 = (const float*)q[2]; P.B2 = (const float*)q[3]; P.C = (float*)q[4];
     P.Cb = np > 5 ? (float*)q[5] : nullptr;
+    P.rows = np > 6 ? (const int*)q[6] : nullptr;
     if (P.M <= 0 || P.N <= 0 || P.K < 0 || P.K2 < 0 || !P.C || P.ldc < P.N - (P.Cb ? 1 : 0)) return kBadArgument;
     if ((P.K > 0 && (!P.A || (!P.B && !(P.ones1 && P.N == 1)) || P.lda < P.M)) ||
         (P.K2 > 0 && (!P.A2 || (!P.B2 && !(P.ones2 && P.N == 1)) || P.lda2 < P.M)))
@@ -1569,21 +1832,28 @@ extern "C" size_t tmdnet_gemm_tn_workspace_bytes(int n_problems, const int* dims
     tiles += ((d[0] + 31) / 32) * ((d[1] + 31) / 32);
     kmax = max(kmax, d[2] + d[3]);
   }
-  int tv = 0;  // the 64-tile kernel's tiling (bias rides in the first column tile)
+  TNShape sh[gemm::TN_MAX];  // the 64-tile kernels' plan (bias rides in the first column tile)
   for (int i = 0; i < n_problems; ++i) {
     const int* d = dims + 12 * i;
-    const int nr = (d[10] || d[11]) ? d[1] - 1 : d[1];
-    tv += ((d[0] + gemm::TV - 1) / gemm::TV) * max(1, (nr + gemm::TV - 1) / gemm::TV);
+    sh[i] = TNShape{d[0], (d[10] || d[11]) ? d[1] - 1 : d[1], d[2] + d[3]};
   }
-  const int S = tn_split(tiles, kmax), Sv = tn_split(tv, kmax);
+  int Sv[gemm::TN_MAX], nt[gemm::TN_MAX];
+  long long p0[gemm::TN_MAX], parts = 0;
+  tn_plan_v(n_problems, sh, true, Sv, nt, p0, parts);
+  const int S = tn_split(tiles, kmax);
   const size_t b32 = S > 1 ? sizeof(float) * 1024 * (size_t)tiles * S : 0;
-  const size_t bv = Sv > 1 ? sizeof(float) * gemm::TV_PART * (size_t)tv * Sv : 0;
+  const size_t bv = sizeof(float) * gemm::TV_PART * (size_t)parts;
   return max(b32, bv);
 }
 
 extern "C" int tmdnet_gemm_tn_f32_ws(int n_problems, const int* dims, const void* const* ptrs, void* workspace,
                                      size_t workspace_bytes, void* stream) {
   return gemm_tn(n_problems, dims, ptrs, 6, workspace, workspace_bytes, stream);
+}
+
+extern "C" int tmdnet_gemm_tn_rows_f32_ws(int n_problems, const int* dims, const void* const* ptrs, void* workspace,
+                                          size_t workspace_bytes, void* stream) {
+  return gemm_tn(n_problems, dims, ptrs, 7, workspace, workspace_bytes, stream);
 }
 
 // Wp [3][N][K] (bf16 bit patterns) = the exact three-piece split of W [N][K] (ldw), see tmd::proj.

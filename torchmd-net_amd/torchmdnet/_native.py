@@ -107,6 +107,7 @@ SIGNATURES = {
     "tmdnet_gemm_tn_f32": (I, [I, P, P, P]),
     "tmdnet_gemm_tn_workspace_bytes": (ctypes.c_size_t, [I, P]),
     "tmdnet_gemm_tn_f32_ws": (I, [I, P, P, P, ctypes.c_size_t, P]),
+    "tmdnet_gemm_tn_rows_f32_ws": (I, [I, P, P, P, ctypes.c_size_t, P]),
     "tmdnet_embedding_bwd_f32": (I, [I, I, I, P, I, P, P, P, I, P]),
     "tmdnet_embedding_fwd_f32": (I, [I, I, I, P, I, P, P, P, P, P]),
     "tmdnet_proj_split_f32": (I, [I, I, P, I, P, P]),

@@ -722,8 +722,10 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws, r=None, dr=Fa
         g_f = torch.mm(g_pkv_all, meta.dkv_eff[0]) if want_f else None
         if any(need_ws[:meta.n_layers]):
             if PROJ_WGRAD == "tn":  # weight + bias (+ the adjoint's g_pkv^T gb_f): one split-K TN launch
+                # (a static-capacity list: the sums stop at the device pair count, the padding rows are zero)
                 g_w_all, g_b_all = kernels._linear_wgrad(g_pkv_all, f, True, True,
-                                                         seg2=adj.get("dkv") if adj is not None else None)
+                                                         seg2=adj.get("dkv") if adj is not None else None,
+                                                         rows=_edge_rows(meta.graph, g_pkv_all))
             else:
                 g_w_all = torch.mm(g_pkv_all.t(), f)
                 if adj is not None and adj.get("dkv") is not None:  # + the adjoint's g_pkv^T gb_f
@@ -739,6 +741,16 @@ def _backward_layers(meta, gX, gV, f, C, u, params, acts, need_ws, r=None, dr=Fa
                     gl = _dkv_param_grads(meta, g_w_all[a:b], g_b_all[a:b])
                     g_params[base:base + len(gl)] = gl
     return gX, g_f, g_C, g_u, g_r, g_params
+
+
+def _edge_rows(graph, rows_tensor):
+    """The device pair count of a static-capacity graph whose per-edge rows ``rows_tensor`` holds (CUDA),
+    else None."""
+    npd = getattr(graph, "num_pairs_dev", None)
+    if npd is None or not getattr(graph, "static", False) or not rows_tensor.is_cuda \
+            or rows_tensor.shape[0] != graph.n_edges:
+        return None
+    return npd
 
 
 def _node_weight_grads(meta, g_params, need_ws, g_qkv_all, g_o_all, g_vecp_all, g_xn_all, ln_rows, adj):

@@ -1600,7 +1600,8 @@ def wgrad_tn(problems):
     ``tmdnet_gemm_tn_f32`` launch (fp32; the library per problem otherwise).  Each problem is a dict:
     A [K, M], B [K, Nb] (or None with ``ones`` and C of one column), C [M, N], optional "beta",
     "ones" (C's last column = the column sums of A: B is implicitly [B | 1], N = Nb + 1), "A2" / "B2" /
-    "ones2" (a second row segment of the same sum)."""
+    "ones2" (a second row segment of the same sum), "rows" (an int32 device scalar: only rows < rows of
+    each segment are summed -- a static-capacity edge list's found pairs; the padding rows are zero)."""
     if not problems:
         return
     fp32 = all(p["A"].dtype == torch.float32 and p["A"].is_cuda for p in problems)
@@ -1635,7 +1636,8 @@ def _wgrad_tn_launch(problems):
     lib = nat.load()
     n = len(problems)
     dims = (ctypes.c_int * (12 * n))()
-    ptrs = (ctypes.c_void_p * (6 * n))()
+    npp = 7 if any(p.get("rows") is not None for p in problems) else 6
+    ptrs = (ctypes.c_void_p * (npp * n))()
     keep = []
     for i, p in enumerate(problems):
         A, B, C, Cb = p["A"], p.get("B"), p["C"], p.get("Cb")
@@ -1651,11 +1653,16 @@ def _wgrad_tn_launch(problems):
                                     0 if B is None else B.stride(0), 0 if A2 is None else A2.stride(0),
                                     0 if B2 is None else B2.stride(0), C.stride(0) if C.dim() == 2 else 1,
                                     int(bool(p.get("beta"))), int(bool(p.get("ones"))), int(bool(p.get("ones2")))]
-        ptrs[6 * i:6 * i + 6] = [None if t is None else t.data_ptr() for t in (A, B, A2, B2, C, Cb)]
+        rows = p.get("rows")
+        if rows is not None and (rows.dtype != torch.int32 or rows.numel() != 1 or rows.device != A.device):
+            raise RuntimeError("wgrad_tn: rows must be an int32 device scalar")
+        ts = (A, B, A2, B2, C, Cb) + ((rows,) if npp == 7 else ())
+        ptrs[npp * i:npp * i + npp] = [None if t is None else t.data_ptr() for t in ts]
     dev = problems[0]["A"].device
     wsb = lib.tmdnet_gemm_tn_workspace_bytes(n, dims)  # split over the rows: partial tiles
     ws = torch.empty((max(wsb, 4) // 4,), dtype=torch.float32, device=dev) if wsb else None
-    rc = lib.tmdnet_gemm_tn_f32_ws(n, dims, ptrs, None if ws is None else ws.data_ptr(), wsb, nat.stream(dev))
+    fn = lib.tmdnet_gemm_tn_rows_f32_ws if npp == 7 else lib.tmdnet_gemm_tn_f32_ws
+    rc = fn(n, dims, ptrs, None if ws is None else ws.data_ptr(), wsb, nat.stream(dev))
     nat.check(rc, "tmdnet_gemm_tn_f32_ws")
 
 
@@ -2538,8 +2545,9 @@ class _Linear(Function):
         return gx, gw, gb
 
 
-def _linear_wgrad(gy, x, want_w, want_b, seg2=None):
-    """(g_W, g_b) = (gy^T x, sum gy) [+ seg2 = (gy2, x2): gy2^T x2] in one TN launch (fp32 CUDA)."""
+def _linear_wgrad(gy, x, want_w, want_b, seg2=None, rows=None):
+    """(g_W, g_b) = (gy^T x, sum gy) [+ seg2 = (gy2, x2): gy2^T x2] in one TN launch (fp32 CUDA); ``rows``
+    (int32 device scalar): only the first rows of each segment are non-zero (see wgrad_tn)."""
     out_f, in_f = gy.shape[1], x.shape[1]
     if not _tn_ok(gy, x) or gy.stride(1) != 1 or x.stride(1) != 1:
         gw = (gy.t() @ x + (seg2[0].t() @ seg2[1] if seg2 is not None else 0)) if want_w else None
@@ -2553,6 +2561,8 @@ def _linear_wgrad(gy, x, want_w, want_b, seg2=None):
             p.update(A2=seg2[0], B2=seg2[1], ones2=False)
     else:
         p = {"A": gy, "B": None, "C": gb.view(out_f, 1), "ones": True}
+    if rows is not None:
+        p["rows"] = rows
     wgrad_tn([p])
     return gw, gb
 
