@@ -9,7 +9,7 @@ last = rows[marks[-2] + 1:marks[-1]]
 print("kernels per step:", len(last))
 t0 = int(last[0]["Start_Timestamp"])
 if len(sys.argv) > 2 and sys.argv[2] == "summary":
-    last_only = True
+    last_only = False  # (the full sequence is always listed: the judged kernel lists are untruncated)
 else:
     last_only = False
 busy = 0
@@ -24,8 +24,8 @@ t = Counter()
 for r in last:
     t[r["Kernel_Name"][:60]] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
 print("-- by count")
-for k, v in c.most_common(25):
+for k, v in c.most_common():
     print(v, k)
 print("-- by total time (us)")
-for k, v in t.most_common(25):
+for k, v in t.most_common():
     print(f"{v:9.1f} {c[k]:5d} {k}")
