@@ -187,6 +187,38 @@ def test_layer_norm_second_order_matches_composite(C, monkeypatch):
         assert _rel(a, bb) < 1e-4
 
 
+@pytest.mark.parametrize("n_atoms", [168, 5000])
+def test_dot_sum_second_order_matches_composite(n_atoms):
+    """The Scalar head's last Linear fused with the molecule sum (kernels.dot_sum) differentiated twice: the hand
+    VJP of its first backward (dot-sum / TN launches, no library GEMM) vs the composite differentiated twice
+    in fp64, every input (h, w, b0) and the seed gy."""
+    from torchmdnet import kernels
+    g = torch.Generator(device=DEV).manual_seed(n_atoms)
+    H, n_mol = 64, 8
+    rn = lambda *sh: torch.randn(*sh, device=DEV, generator=g)  # noqa: E731
+    batch = torch.sort(torch.randint(0, n_mol, (n_atoms,), device=DEV, generator=g)).values
+    batch[:n_mol] = torch.arange(n_mol, device=DEV)
+    batch = torch.sort(batch).values
+    h, w, b0, gy = rn(n_atoms, H), rn(H), rn(1), rn(n_mol, 1)
+    std, mean = torch.scalar_tensor(1.7, device=DEV), torch.scalar_tensor(0.3, device=DEV)
+    tang = [rn(n_atoms, H), rn(H), rn(1)]
+
+    def second(dtype):
+        xs = [t.to(dtype).clone().requires_grad_(True) for t in (h, w, b0)]
+        g0 = gy.to(dtype).clone().requires_grad_(True)
+        s, m = std.to(dtype), mean.to(dtype)
+        if dtype == torch.float64:
+            y = kernels._dot_sum_composite(xs[0], xs[1], xs[2], batch, n_mol, s, m)
+        else:
+            y = kernels.dot_sum(xs[0], xs[1], xs[2], batch, n_mol, s, m)
+        first = torch.autograd.grad(y, xs, g0, create_graph=True)
+        return torch.autograd.grad(first, xs[:2] + [g0], [t.to(dtype) for t in tang], allow_unused=True)
+
+    hip, ref = second(torch.float32), second(torch.float64)
+    for a, r in zip(hip, ref):
+        assert _rel(a.double().reshape(r.shape), r) < 1e-5
+
+
 def test_embedding_second_order_matches_composite(monkeypatch):
     """TensorEmbedding's aggregation (tensornet.py:295-315) differentiated twice: the hand second order
     (tmdnet_tn_embed_bwd2: the first-order kernels on dual numbers) vs autograd's double differentiation of

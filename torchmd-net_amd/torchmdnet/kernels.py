@@ -1719,6 +1719,27 @@ def atom_sum(x, batch, n_mol, std, mean):
     return _AtomSum.apply(x.contiguous(), batch, int(n_mol), std, mean)
 
 
+def _dot_sum_launch(h, w, b0, batch, n_mol, std, mean):
+    """y[b] = mean + std * sum_{batch[n] = b} (h[n] . w + b0), one tmdnet_dot_sum_fwd_atoms launch."""
+    y = torch.empty((n_mol, 1), dtype=h.dtype, device=h.device)
+    # large systems: the row products over the whole grid first (per-atom buffer)
+    buf = torch.empty(h.shape[0], dtype=h.dtype, device=h.device) if h.shape[0] > 4096 else None
+    rc = nat.load().tmdnet_dot_sum_fwd_atoms(nat.dtype_code(h.dtype), h.shape[0], h.shape[1], nat.ptr(h), h.stride(0),
+                                             nat.ptr(w), nat.ptr(b0), n_mol, nat.ptr(batch), nat.ptr(std),
+                                             nat.ptr(mean), nat.ptr(buf), nat.ptr(y), nat.stream(h.device))
+    nat.check(rc, "tmdnet_dot_sum_fwd")
+    return y
+
+
+def _dot_sum_bwd_launch(gy, batch, n_mol, std, w, rows):
+    """gh[n] = std * gy[batch[n]] * w (tmdnet_dot_sum_bwd), [rows, len(w)]."""
+    gh = torch.empty((rows, w.shape[0]), dtype=gy.dtype, device=gy.device)
+    rc = nat.load().tmdnet_dot_sum_bwd(nat.dtype_code(gy.dtype), rows, w.shape[0], nat.ptr(gy), nat.ptr(batch), n_mol,
+                                       nat.ptr(std), nat.ptr(w), nat.ptr(gh), nat.stream(gy.device))
+    nat.check(rc, "tmdnet_dot_sum_bwd")
+    return gh
+
+
 def _dot_sum_composite(h, w, b0, batch, n_mol, std, mean):
     x = h @ w.view(-1, 1) + b0.view(1, 1)
     return _atom_sum_composite(x, batch, n_mol, std, mean)
@@ -1730,14 +1751,7 @@ class _DotSum(Function):
 
     @staticmethod
     def forward(ctx, h, w, b0, batch, n_mol, std, mean):
-        lib = nat.load()
-        y = torch.empty((n_mol, 1), dtype=h.dtype, device=h.device)
-        # large systems: the row products over the whole grid first (per-atom buffer)
-        buf = torch.empty(h.shape[0], dtype=h.dtype, device=h.device) if h.shape[0] > 4096 else None
-        rc = lib.tmdnet_dot_sum_fwd_atoms(nat.dtype_code(h.dtype), h.shape[0], h.shape[1], nat.ptr(h), h.stride(0),
-                                          nat.ptr(w), nat.ptr(b0), n_mol, nat.ptr(batch), nat.ptr(std),
-                                          nat.ptr(mean), nat.ptr(buf), nat.ptr(y), nat.stream(h.device))
-        nat.check(rc, "tmdnet_dot_sum_fwd")
+        y = _dot_sum_launch(h, w, b0, batch, n_mol, std, mean)
         ctx.n_mol = n_mol
         ctx.save_for_backward(h, w, b0, batch, std)
         return y
@@ -1759,24 +1773,38 @@ class _DotSumBwd(Function):
     def forward(ctx, gy, h, w, b0, batch, std, n_mol, need):
         gh = gw = gb = None
         if need[0]:
-            gh = torch.empty_like(h)
-            rc = nat.load().tmdnet_dot_sum_bwd(nat.dtype_code(h.dtype), h.shape[0], h.shape[1], nat.ptr(gy),
-                                               nat.ptr(batch), n_mol, nat.ptr(std), nat.ptr(w), nat.ptr(gh),
-                                               nat.stream(h.device))
-            nat.check(rc, "tmdnet_dot_sum_bwd")
-        if need[1] or need[2]:  # training: the per-atom seed std * gy[batch], then its sums
-            ga = std * gy.index_select(0, batch).view(-1)
-            gw = (ga.view(1, -1) @ h).view(-1) if need[1] else None
-            gb = ga.sum().view(1) if need[2] else None
+            gh = _dot_sum_bwd_launch(gy, batch, n_mol, std, w, h.shape[0])
+        if need[1] or need[2]:  # training: the per-atom seed a = std * gy[batch], then (a^T h, sum a): one TN launch
+            ga = (std * gy.index_select(0, batch).view(-1)).view(-1, 1)
+            gw, gb = _linear_wgrad(ga, h, need[1], need[2])
+            gw = gw.view(-1) if gw is not None else None
         ctx.n_mol = n_mol
         ctx.save_for_backward(gy, h, w, b0, batch, std)
         return gh, gw, gb
 
     @staticmethod
-    def backward(ctx, ggh, ggw, ggb):  # second order: the composite differentiated twice
+    def backward(ctx, ggh, ggw, ggb):
         gy, h, w, b0, batch, std = ctx.saved_tensors
         n_mol = ctx.n_mol
         zero = torch.zeros_like(std)
+        if h.is_cuda and h.dtype == torch.float32 and not torch.is_grad_enabled():
+            # hand VJP of (gh = a w, gw = a^T h, gb = sum a), a_n = std gy[batch[n]]:
+            #   d_gy[b] = std sum_{batch[n] = b} (ggh[n] . w + h[n] . ggw + ggb),
+            #   d_h = a ggw,  d_w = a^T ggh  (no library GEMM: dot-sum / TN launches)
+            d_gy = None
+            if ggh is not None or ggb is not None:
+                d_gy = _dot_sum_launch(ggh if ggh is not None else torch.zeros_like(h), w,
+                                       ggb.reshape(1) if ggb is not None else zero.reshape(1), batch, n_mol, std, zero)
+            if ggw is not None:
+                t = _dot_sum_launch(h, ggw.reshape(-1), zero.reshape(1), batch, n_mol, std, zero)
+                d_gy = t if d_gy is None else d_gy + t
+            d_h = _dot_sum_bwd_launch(gy, batch, n_mol, std, ggw.reshape(-1), h.shape[0]) if ggw is not None else None
+            d_w = None
+            if ggh is not None:
+                ga = (std * gy.index_select(0, batch).view(-1)).view(-1, 1)
+                d_w = _linear_wgrad(ga, ggh.contiguous(), True, False)[0].view(-1)
+            return d_gy, d_h, d_w, None, None, None, None, None
+        # (fp64 / a graph of the second order: the composite differentiated twice)
         d = _tn_double_backward(lambda h_, w_, b_: _dot_sum_composite(h_, w_, b_, batch, n_mol, std, zero),
                                 [h, w, b0], [gy], [ggh, ggw, ggb])
         return d[0], d[1], d[2], d[3], None, None, None, None
