@@ -695,13 +695,15 @@ template <typename T>
 static int launch_embed_bwd_dst(const Args<T>& A, hipStream_t st) {
   if (A.n <= 0) return kOk;
   const dim3 g((unsigned)A.n);
-  // its per-edge channel sums make each edge a longer chain than in the other kernels: 8 waves per node
-  // (C3: 9.4 vs 13.3 us at 4); TMDNET_TN_EBD_S = 1 / 2 / 4 for A/B
-  static const int s = [] {  // read once per process (as slots())
+  // its per-edge channel sums make each edge a longer chain than in the other kernels: 8 waves per node on
+  // small systems (C3: 9.4 vs 13.3 us at 4), 2 on large ones, where the nodes alone fill the chip (C5 TensorNet,
+  // 50k atoms: 31.5 vs 32.2-32.8 ms per evaluation, tools/tn_c5_time.py); TMDNET_TN_EBD_S = 1 / 2 / 4 / 8 for A/B
+  static const int env_s = [] {  // read once per process (as slots())
     const char* e8 = getenv("TMDNET_TN_EBD_S");
-    const int v = e8 ? atoi(e8) : 8;
-    return v >= 8 ? 8 : v >= 4 ? 4 : v >= 2 ? 2 : 1;
+    const int v = e8 ? atoi(e8) : 0;
+    return v <= 0 ? 0 : v >= 8 ? 8 : v >= 4 ? 4 : v >= 2 ? 2 : 1;
   }();
+  const int s = env_s ? env_s : (A.n < 8192 ? 8 : 2);
 #define TMD_EBD(NB)                                                                                   \
   if (s == 1) hipLaunchKernelGGL((k_embed_bwd_dst<T, NB, 1>), g, dim3(64), 0, st, A);                 \
   else if (s == 2) hipLaunchKernelGGL((k_embed_bwd_dst<T, NB, 2>), g, dim3(128), 0, st, A);           \
